@@ -1,0 +1,246 @@
+"""ctypes binding of ``libfslr_hip.so`` (C ABI: include/fslr_hip.h).
+
+The HIP library is the only compute path: there is no CPU fallback.  If the
+shared object is missing or no HIP device is present, every entry point raises
+``HipUnavailable`` — loudly, never silently.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libfslr_hip.so')
+
+FSLR_OK, FSLR_ERR_ZERO_DIVISION, FSLR_ERR_INVALID, FSLR_ERR_HIP, FSLR_ERR_NOMEM, FSLR_ERR_STATE = range(6)
+FSLR_MAX_L = 64
+FSLR_MAX_READS = 1 << 25
+FSLR_THR_ZERO_ALN = -(1 << 31)
+PASS_STRIDE = 2 * FSLR_MAX_L
+
+# every symbol include/fslr_hip.h declares (checked by tests/test_abi.py)
+EXPORTED = ['fslr_abi_version', 'fslr_last_error', 'fslr_ctx_create', 'fslr_ctx_destroy', 'fslr_set_profiling',
+            'fslr_set_reads', 'fslr_set_thresholds', 'fslr_reserve_edges', 'fslr_build_index', 'fslr_query',
+            'fslr_components', 'fslr_run', 'fslr_sync', 'fslr_read_stats', 'fslr_get_timings', 'fslr_get_labels',
+            'fslr_get_fwd_degree', 'fslr_get_edges', 'fslr_labels_device_ptr', 'fslr_copy_labels_device',
+            'fslr_copy_fwd_device', 'fslr_union_pairs', 'fslr_finalize_labels']
+
+
+class HipUnavailable(RuntimeError):
+    pass
+
+
+class FslrError(RuntimeError):
+    pass
+
+
+class Reads(ctypes.Structure):
+    _fields_ = [('n_reads', ctypes.c_int64), ('n_intervals', ctypes.c_int64), ('n_chroms', ctypes.c_int32)] + [
+        (f, ctypes.c_void_p) for f in ('read_off', 'read_qlen2', 'read_nal', 'iv_chrom', 'iv_start', 'iv_end',
+                                       'iv_thr')]
+
+
+class Params(ctypes.Structure):
+    _fields_ = [('qlen_cut', ctypes.c_double), ('nal_cut', ctypes.c_double), ('pass_table', ctypes.c_void_p),
+                ('edge_threshold', ctypes.c_int32), ('flags', ctypes.c_int32)]
+
+
+class QueryStats(ctypes.Structure):
+    _fields_ = [('evaluated_pairs', ctypes.c_int64), ('jaccard_evals', ctypes.c_int64),
+                ('candidates', ctypes.c_int64), ('n_edges', ctypes.c_int64), ('max_fwd', ctypes.c_int32),
+                ('error', ctypes.c_int32), ('err_a', ctypes.c_int32), ('err_b', ctypes.c_int32),
+                ('algo_bytes', ctypes.c_int64)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+class Timings(ctypes.Structure):
+    _fields_ = [('index_ms', ctypes.c_float), ('query_ms', ctypes.c_float), ('components_ms', ctypes.c_float),
+                ('total_ms', ctypes.c_float)]
+
+    def as_dict(self):
+        return {f: float(getattr(self, f)) for f, _ in self._fields_}
+
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load the shared library (no device access)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise HipUnavailable(f'{path} is not built: run `python -c "import __graft_entry__ as g; g.build()"` '
+                             '(or `make -C fslr_amd/csrc`).  There is no CPU fallback.')
+    L = ctypes.CDLL(path)
+    vp, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32
+    sig = {
+        'fslr_abi_version': (ctypes.c_int, []),
+        'fslr_last_error': (ctypes.c_char_p, [vp]),
+        'fslr_ctx_create': (ctypes.c_int, [ctypes.c_int, vp, ctypes.POINTER(vp)]),
+        'fslr_ctx_destroy': (None, [vp]),
+        'fslr_set_profiling': (ctypes.c_int, [vp, ctypes.c_int]),
+        'fslr_set_reads': (ctypes.c_int, [vp, ctypes.POINTER(Reads)]),
+        'fslr_set_thresholds': (ctypes.c_int, [vp, vp]),
+        'fslr_reserve_edges': (ctypes.c_int, [vp, i64]),
+        'fslr_build_index': (ctypes.c_int, [vp]),
+        'fslr_query': (ctypes.c_int, [vp, ctypes.POINTER(Params), i64, i64]),
+        'fslr_components': (ctypes.c_int, [vp]),
+        'fslr_run': (ctypes.c_int, [vp, ctypes.POINTER(Params)]),
+        'fslr_sync': (ctypes.c_int, [vp]),
+        'fslr_read_stats': (ctypes.c_int, [vp, ctypes.POINTER(QueryStats)]),
+        'fslr_get_timings': (ctypes.c_int, [vp, ctypes.POINTER(Timings)]),
+        'fslr_get_labels': (ctypes.c_int, [vp, vp]),
+        'fslr_get_fwd_degree': (ctypes.c_int, [vp, vp]),
+        'fslr_get_edges': (ctypes.c_int, [vp, vp, vp, vp, i64]),
+        'fslr_labels_device_ptr': (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
+        'fslr_copy_labels_device': (ctypes.c_int, [vp, vp]),
+        'fslr_copy_fwd_device': (ctypes.c_int, [vp, vp]),
+        'fslr_union_pairs': (ctypes.c_int, [vp, vp, vp, i64, ctypes.c_int]),
+        'fslr_finalize_labels': (ctypes.c_int, [vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class Context:
+    """One HIP device context (library-owned HBM buffers + a stream)."""
+
+    def __init__(self, device: int = 0, stream: int | None = None, profiling: bool = False):
+        """``stream``: a hipStream_t handle (e.g. ``torch.cuda.Stream().cuda_stream``); None or 0
+        (the null stream cannot be shared) = the library creates its own stream."""
+        self._L = load()
+        h = ctypes.c_void_p()
+        rc = self._L.fslr_ctx_create(int(device), ctypes.c_void_p(stream) if stream else None, ctypes.byref(h))
+        if rc != FSLR_OK:
+            raise HipUnavailable(f'fslr_ctx_create(device={device}) failed (rc={rc}): no usable HIP device')
+        self._h = h
+        self.device = device
+        self.n_reads = 0
+        self.edge_capacity = 0
+        self._keep = ()
+        if profiling:
+            self._check(self._L.fslr_set_profiling(self._h, 1))
+
+    def close(self):
+        if getattr(self, '_h', None):
+            self._L.fslr_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc == FSLR_OK:
+            return
+        msg = (self._L.fslr_last_error(self._h) or b'').decode()
+        if rc == FSLR_ERR_ZERO_DIVISION:
+            raise ZeroDivisionError('division by zero')
+        raise FslrError(f'fslr error {rc}: {msg}')
+
+    # -- data -------------------------------------------------------------------------
+    def set_reads(self, read_off, read_qlen2, read_nal, iv_chrom, iv_start, iv_end, iv_thr, n_chroms):
+        arrs = [np.ascontiguousarray(x, dtype=np.int32) for x in
+                (read_off, read_qlen2, read_nal, iv_chrom, iv_start, iv_end, iv_thr)]
+        r = Reads(len(arrs[1]), len(arrs[3]), int(n_chroms), *(_ptr(a) for a in arrs))
+        self._check(self._L.fslr_set_reads(self._h, ctypes.byref(r)))
+        self.n_reads = len(arrs[1])
+
+    def set_thresholds(self, iv_thr):
+        t = np.ascontiguousarray(iv_thr, dtype=np.int32)
+        self._check(self._L.fslr_set_thresholds(self._h, _ptr(t)))
+
+    def reserve_edges(self, cap):
+        self._check(self._L.fslr_reserve_edges(self._h, int(cap)))
+        self.edge_capacity = max(self.edge_capacity, int(cap))
+
+    # -- compute (async) ------------------------------------------------------------------
+    def _params(self, qlen_cut, nal_cut, pass_table, edge_threshold):
+        pt = np.ascontiguousarray(pass_table, dtype=np.uint8)
+        assert pt.size == FSLR_MAX_L * PASS_STRIDE
+        self._keep = (pt,)
+        return Params(float(qlen_cut), float(nal_cut), _ptr(pt), int(edge_threshold), 0)
+
+    def build_index(self):
+        self._check(self._L.fslr_build_index(self._h))
+
+    def query(self, qlen_cut, nal_cut, pass_table, edge_threshold=10, a_begin=0, a_end=None):
+        p = self._params(qlen_cut, nal_cut, pass_table, edge_threshold)
+        a_end = self.n_reads if a_end is None else a_end
+        self._check(self._L.fslr_query(self._h, ctypes.byref(p), int(a_begin), int(a_end)))
+
+    def components(self):
+        self._check(self._L.fslr_components(self._h))
+
+    def run(self, qlen_cut, nal_cut, pass_table, edge_threshold=10):
+        p = self._params(qlen_cut, nal_cut, pass_table, edge_threshold)
+        self._check(self._L.fslr_run(self._h, ctypes.byref(p)))
+
+    def sync(self):
+        self._check(self._L.fslr_sync(self._h))
+
+    # -- results ------------------------------------------------------------------------
+    def stats(self) -> dict:
+        s = QueryStats()
+        self._check(self._L.fslr_read_stats(self._h, ctypes.byref(s)))
+        return s.as_dict()
+
+    def timings(self) -> dict:
+        t = Timings()
+        self._check(self._L.fslr_get_timings(self._h, ctypes.byref(t)))
+        return t.as_dict()
+
+    def labels(self) -> np.ndarray:
+        out = np.empty(self.n_reads, np.int32)
+        self._check(self._L.fslr_get_labels(self._h, _ptr(out)))
+        return out
+
+    def fwd_degree(self) -> np.ndarray:
+        out = np.empty(self.n_reads, np.int32)
+        self._check(self._L.fslr_get_fwd_degree(self._h, _ptr(out)))
+        return out
+
+    def edges(self, n_edges: int):
+        a = np.empty(n_edges, np.int32)
+        b = np.empty(n_edges, np.int32)
+        iu = np.empty(n_edges, np.uint16)
+        self._check(self._L.fslr_get_edges(self._h, _ptr(a), _ptr(b), _ptr(iu), int(n_edges)))
+        return a, b, (iu & 0xff).astype(np.int32), (iu >> 8).astype(np.int32)
+
+    def labels_device_ptr(self) -> int:
+        p = ctypes.c_void_p()
+        self._check(self._L.fslr_labels_device_ptr(self._h, ctypes.byref(p)))
+        return p.value
+
+    def copy_labels_device(self, dptr: int):
+        self._check(self._L.fslr_copy_labels_device(self._h, ctypes.c_void_p(dptr)))
+
+    def copy_fwd_device(self, dptr: int):
+        self._check(self._L.fslr_copy_fwd_device(self._h, ctypes.c_void_p(dptr)))
+
+    def union_pairs(self, src, dst, n, on_device: bool):
+        """Union (src[k], dst[k]); ``src`` None means src[k] = k.  Pointers are ints when on_device."""
+        if on_device:
+            self._check(self._L.fslr_union_pairs(self._h, ctypes.c_void_p(src) if src else None,
+                                                 ctypes.c_void_p(dst), int(n), 1))
+        else:
+            s = None if src is None else np.ascontiguousarray(src, np.int32)
+            d = np.ascontiguousarray(dst, np.int32)
+            self._check(self._L.fslr_union_pairs(self._h, _ptr(s) if s is not None else None, _ptr(d), int(n), 0))
+
+    def finalize_labels(self):
+        self._check(self._L.fslr_finalize_labels(self._h))

@@ -1,0 +1,319 @@
+"""Drop-in replacement of ``fslr/cluster.py`` whose hot path runs on MI355X.
+
+Same function names, arguments and return shapes as the reference module
+(/root/reference/fslr/cluster.py); the per-pair work of ``query_interval_trees``
+and the connected components run in ``libfslr_hip.so`` (HIP, gfx950).  Host
+stages are vectorised numpy/pandas with the reference's exact semantics.
+
+Function map (reference file:line → here):
+  keep_fillings              cluster.py:14-31    vectorised first/last drop + group span
+  rename_chromosomes         cluster.py:34-43    chrN by N, others after (equality-only downstream)
+  chrom_to_str               cluster.py:46-49
+  calc_coverage              cluster.py:52-67
+  filter_high_coverage       cluster.py:70-77
+  delete_false               cluster.py:80-86
+  mask_sequences2            cluster.py:89-106   vectorised for IntervalData
+  prepare_data               cluster.py:109-121  → IntervalData (sequence of IntervalItem)
+  build_interval_trees       cluster.py:124-130  → DeviceIntervalIndex (HBM CSR + sorted index)
+  get_chromosome_lengths     cluster.py:173-175  own BGZF/BAM header reader (no pysam)
+  query_interval_trees       cluster.py:187-227  device pair kernel; returns (match_df, ClusterGraph)
+  get_subgraphs              cluster.py:230-234  components ordered by min read rank
+  choose_alignment           cluster.py:237-254  vectorised groupby/idxmax
+"""
+from __future__ import annotations
+
+import os
+import sys
+import warnings
+
+import numpy as np
+import pandas as pd
+
+from . import bam_header
+from ._lib import FSLR_THR_ZERO_ALN, Context
+from .prep import (IntervalData, IntervalItem, build_csr, data_order, first_last_masks, fold_overlap_threshold,
+                   group_span, mask_keep, pass_table)
+
+__all__ = ['IntervalItem', 'keep_fillings', 'rename_chromosomes', 'chrom_to_str', 'calc_coverage',
+           'filter_high_coverage', 'delete_false', 'mask_sequences2', 'prepare_data', 'build_interval_trees',
+           'get_chromosome_lengths', 'query_interval_trees', 'get_subgraphs', 'choose_alignment',
+           'ClusterGraph', 'DeviceIntervalIndex', 'EdgeCapWarning']
+
+
+class EdgeCapWarning(UserWarning):
+    """A read has more than ``edge_threshold`` forward partners: the reference's
+    result then depends on superintervals' result order (cluster.py:223-224)."""
+
+
+def _default_device() -> int:
+    return int(os.environ.get('FSLR_DEVICE', os.environ.get('LOCAL_RANK', '0')))
+
+
+# ------------------------------------------------------------------ host stages
+def keep_fillings(bed_file: pd.DataFrame) -> pd.DataFrame:
+    """cluster.py:14-31: drop the first and last row (file order) of every qname; add qlen2."""
+    codes, uniq = pd.factorize(bed_file['qname'], sort=False)
+    first, last = first_last_masks(codes)
+    keep = ~(first | last)
+    out = bed_file[keep]
+    kc = codes[keep]
+    span = group_span(kc, out['qstart'].to_numpy(), out['qend'].to_numpy(), len(uniq))
+    with warnings.catch_warnings():
+        warnings.simplefilter('ignore')
+        out['qlen2'] = span[kc]
+    return out
+
+
+def _chrom_key(name):
+    if isinstance(name, str) and name[:3] == 'chr' and name[3:].isdigit():
+        return (0, int(name[3:]))
+    return (1, 0)
+
+
+def rename_chromosomes(bed_file, chromosome_lengths, chromosome_mask):
+    """cluster.py:34-43.  chrN → N-order ids, other names after (first-appearance order).
+
+    Only equality of ids is used downstream, so this deterministic numbering is
+    interchangeable with the reference's set-iteration order for non-chrN names.
+    """
+    names = list(pd.unique(bed_file['chrom']))
+    order = sorted(range(len(names)), key=lambda i: (_chrom_key(names[i]), i))
+    cmap = {names[i]: k + 1 for k, i in enumerate(order)}
+    chr_lengths = {cmap.get(k): v for k, v in chromosome_lengths.items()}
+    bed_file['chrom'] = bed_file['chrom'].map(cmap)
+    mask = [cmap.get(x) if x != 'subtelomere' else x for x in chromosome_mask]
+    return bed_file, chr_lengths, mask, cmap
+
+
+def chrom_to_str(bed_df, chromosome_to_numeric_map):
+    """cluster.py:46-49."""
+    inv = {v: k for k, v in chromosome_to_numeric_map.items()}
+    bed_df['chrom'] = bed_df['chrom'].map(inv)
+    return bed_df
+
+
+def calc_coverage(bed_file, chromosome_lengths):
+    """cluster.py:52-67: per-chromosome +1/-1 coverage at rstart/rend, cumulative."""
+    cov = {}
+    for chrom, grp in bed_file.groupby('chrom'):
+        if chrom not in chromosome_lengths:
+            continue
+        c = np.zeros(chromosome_lengths[chrom] + 1)
+        np.add.at(c, grp['rstart'].to_numpy(), 1)
+        np.add.at(c, grp['rend'].to_numpy(), -1)
+        cov[chrom] = np.cumsum(c)
+    return cov
+
+
+def filter_high_coverage(data, bed_file, chromosome_lengths, threshold):
+    """cluster.py:70-77.  (main.py:235 passes a DataFrame here, which fails in the
+    reference exactly as it fails here: iterating a DataFrame yields column names.)"""
+    cov = calc_coverage(bed_file, chromosome_lengths)
+    if isinstance(data, IntervalData):
+        keep = np.array([cov[c][m] <= threshold for c, m in zip(data.chrom.tolist(), data.middle.tolist())],
+                        dtype=bool)
+        return data.select(keep)
+    return [aln for aln in data if not cov[aln.chrom][aln.middle] > threshold]
+
+
+def delete_false(bed_file):
+    """cluster.py:80-86."""
+    return bed_file[~bed_file['qname'].str.contains('False')]
+
+
+def mask_sequences2(read_alignments, mask, chromosome_lengths, threshold=500_000):
+    """cluster.py:89-106 (lines 104-105 can never fire: len==1 and >=4)."""
+    if not mask:
+        return read_alignments
+    if isinstance(read_alignments, IntervalData):
+        keep = mask_keep(read_alignments.chrom, read_alignments.start, read_alignments.end, mask,
+                         chromosome_lengths, threshold)
+        return read_alignments.select(keep)
+    long_ = {k: v for k, v in chromosome_lengths.items() if v > 1_000_000}
+    out = []
+    for a in read_alignments:
+        if a.chrom in mask:
+            continue
+        if 'subtelomere' in mask and a.chrom in long_ and (a.start < threshold or long_[a.chrom] - a.end < threshold):
+            continue
+        out.append(a)
+    return out
+
+
+def prepare_data(bed_df, cluster_mask, chromosome_lengths, threshold=500_000) -> IntervalData:
+    """cluster.py:109-121 → IntervalData in ``sort_values('start')`` order, masked."""
+    rs = bed_df['rstart'].to_numpy()
+    re_ = bed_df['rend'].to_numpy()
+    start = np.minimum(rs, re_)
+    end = np.maximum(rs, re_)
+    aln = bed_df['aln_size'].to_numpy()
+    with warnings.catch_warnings():
+        warnings.simplefilter('ignore')
+        bed_df['start'] = start
+        bed_df['end'] = end
+        bed_df['middle'] = aln // 2 + start
+    order = data_order(start)
+    codes, uniq = pd.factorize(bed_df['qname'], sort=False)
+    chrom = bed_df['chrom'].to_numpy()
+    if chrom.dtype.kind not in 'iu':                    # not renamed (rename_chromosomes not called)
+        chrom = pd.factorize(bed_df['chrom'], sort=False)[0]
+    data = IntervalData(
+        chrom=chrom.astype(np.int64)[order], start=start.astype(np.int64)[order],
+        end=end.astype(np.int64)[order], aln_size=aln.astype(np.int64)[order], qcode=codes.astype(np.int64)[order],
+        qnames=np.asarray(uniq, dtype=object), n_alignments=bed_df['n_alignments'].to_numpy().astype(np.int64)[order],
+        qlen2=bed_df['qlen2'].to_numpy().astype(np.int64)[order],
+        middle=(aln // 2 + start).astype(np.int64)[order], index=bed_df.index.to_numpy()[order])
+    if cluster_mask:
+        data = mask_sequences2(data, cluster_mask, chromosome_lengths, threshold)
+    return data
+
+
+def get_chromosome_lengths(bam_path):
+    """cluster.py:173-175 (BAM header reference dictionary)."""
+    return bam_header.get_chromosome_lengths(bam_path)
+
+
+# ------------------------------------------------------------------ device stages
+class DeviceIntervalIndex:
+    """What build_interval_trees returns: the CSR in HBM plus the sorted interval index."""
+
+    def __init__(self, data: IntervalData, device: int | None = None, ctx: Context | None = None):
+        if not isinstance(data, IntervalData):
+            raise TypeError('build_interval_trees expects the IntervalData returned by prepare_data')
+        self.data = data
+        self.csr = data.csr()
+        self.ctx = ctx or Context(_default_device() if device is None else device)
+        c = self.csr
+        thr0 = np.where(c.iv_aln == 0, FSLR_THR_ZERO_ALN, 0).astype(np.int32)
+        self.ctx.set_reads(c.read_off, c.read_qlen2, c.read_nal, c.iv_chrom, c.iv_start, c.iv_end, thr0, c.n_chroms)
+        self.ctx.build_index()
+
+
+def build_interval_trees(data, device: int | None = None) -> DeviceIntervalIndex:
+    """cluster.py:124-130: upload the prepared intervals and build the (chrom, start) index on the GPU."""
+    return DeviceIntervalIndex(data, device)
+
+
+class ClusterGraph:
+    """Graph of read pairs (the reference's ``nx.Graph``), held as device-computed labels.
+
+    ``labels[r]`` = minimum rank in read r's connected component (ranks are the
+    first-appearance order of reads in ``data``).  Nodes are the reads with at
+    least one edge, as in ``G.add_edge`` (cluster.py:221).
+    """
+
+    def __init__(self, qnames_by_rank, labels, edges_ab, fwd, stats):
+        self.qnames_by_rank = qnames_by_rank
+        self.labels = labels
+        self.edges_ab = edges_ab
+        self.fwd = fwd
+        self.stats = stats
+        n = labels.shape[0]
+        sizes = np.bincount(labels, minlength=n) if n else np.zeros(0, np.int64)
+        self.comp_size = sizes[labels] if n else np.zeros(0, np.int64)
+        self.node_mask = self.comp_size >= 2
+        roots = np.flatnonzero((sizes >= 2))          # component roots = min ranks, ascending
+        self.roots = roots
+        cid = np.full(n, -1, dtype=np.int64)
+        if n:
+            rid = np.full(n, -1, dtype=np.int64)
+            rid[roots] = np.arange(roots.size)
+            cid = np.where(self.node_mask, rid[labels], -1)
+        self.component_id = cid                        # per rank; -1 = not a node
+
+    def number_of_nodes(self):
+        return int(self.node_mask.sum())
+
+    def number_of_edges(self):
+        return int(self.edges_ab[0].shape[0])
+
+    @property
+    def nodes(self):
+        return [self.qnames_by_rank[r] for r in np.flatnonzero(self.node_mask)]
+
+    @property
+    def edges(self):
+        a, b = self.edges_ab
+        return [(self.qnames_by_rank[x], self.qnames_by_rank[y]) for x, y in zip(a.tolist(), b.tolist())]
+
+    def components(self):
+        order = np.flatnonzero(self.node_mask)
+        cid = self.component_id[order]
+        srt = np.argsort(cid, kind='stable')
+        out = [set() for _ in range(self.roots.size)]
+        for c, r in zip(cid[srt].tolist(), order[srt].tolist()):
+            out[c].add(self.qnames_by_rank[r])
+        return out
+
+    def to_networkx(self):
+        import networkx as nx
+        G = nx.Graph()
+        G.add_edges_from(self.edges)
+        return G
+
+
+def query_interval_trees(interval_trees, data, overlap_cutoff, jaccard_threshold, edge_threshold, qlen_diff, diff):
+    """cluster.py:187-227 on the GPU.
+
+    Returns ``(match_df, G)``.  ``match_df`` rows are the graph's edges
+    (query1 = lower-rank read, jaccard = I/U as a Python float) sorted by
+    (query1 rank, query2 rank); the reference's row order is set order
+    (arbitrary).  Every pair is evaluated without the per-read edge cap: the
+    result equals the reference whenever no read has more than
+    ``edge_threshold`` forward partners; otherwise an
+    ``EdgeCapWarning`` is issued.
+    """
+    min(jaccard_threshold)                              # cluster.py:188 raises on an empty list
+    if not isinstance(interval_trees, DeviceIntervalIndex) or interval_trees.data is not data:
+        interval_trees = DeviceIntervalIndex(data)
+    idx = interval_trees
+    csr = idx.csr
+    ctx = idx.ctx
+    qnames_by_rank = data.qnames[csr.read_qcode]
+    if csr.nal_varies:
+        warnings.warn('n_alignments differs between rows of one read; the reference then uses the row its '
+                      'search reaches first (order-dependent); the first row in data order is used', EdgeCapWarning)
+    ctx.set_thresholds(fold_overlap_threshold(csr.iv_aln, overlap_cutoff))
+    pt = pass_table(jaccard_threshold)
+    qcut = 1 - qlen_diff
+    ncut = 1 - diff
+    ctx.reserve_edges(max(1 << 16, 12 * csr.n_reads))
+    while True:
+        ctx.query(qcut, ncut, pt, int(edge_threshold))
+        st = ctx.stats()
+        if st['n_edges'] <= ctx.edge_capacity:
+            break
+        ctx.reserve_edges(int(st['n_edges'] * 1.25) + 1024)
+    ctx.components()
+    labels = ctx.labels()
+    ne = st['n_edges']
+    a, b, I, U = ctx.edges(ne)
+    fwd = ctx.fwd_degree()
+    if st['max_fwd'] > edge_threshold:
+        warnings.warn(f'a read has {st["max_fwd"]} forward partners > edge_threshold={edge_threshold}: the '
+                      'reference result depends on superintervals result order here (parity unpinned); '
+                      'all edges are kept', EdgeCapWarning)
+    order = np.lexsort((b, a))
+    a, b, I, U = a[order], b[order], I[order], U[order]
+    match_df = pd.DataFrame({'query1': qnames_by_rank[a] if ne else np.zeros(0, object),
+                             'query2': qnames_by_rank[b] if ne else np.zeros(0, object),
+                             'jaccard_similarity': I / U if ne else np.zeros(0)})
+    G = ClusterGraph(qnames_by_rank, labels, (a, b), fwd, st)
+    return match_df, G
+
+
+def get_subgraphs(G):
+    """cluster.py:230-234: connected components, in the reference's order (by min read rank)."""
+    if isinstance(G, ClusterGraph):
+        return G.components()
+    import networkx as nx
+    return list(nx.connected_components(G))
+
+
+def choose_alignment(bed_file):
+    """cluster.py:237-254: per cluster the read with the highest mean alignment_score (first on ties)."""
+    avg = bed_file.groupby('qname')['alignment_score'].mean()
+    bed_file['avg_alignment_score'] = bed_file['qname'].map(avg)
+    sel = bed_file.groupby('cluster')['avg_alignment_score'].idxmax()
+    chosen = bed_file.loc[sel.to_numpy(), 'qname']
+    return bed_file[bed_file['qname'].isin(chosen)]

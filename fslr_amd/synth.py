@@ -95,6 +95,63 @@ class SynthBed:
     def write_tsv(self, path: str) -> None:
         self.to_dataframe().to_csv(path, sep='\t', index=False)
 
+    def interval_data(self, cluster_mask=('subtelomere',), threshold: int = 500_000):
+        """The prepared ``data`` (fslr_amd.prep.IntervalData) straight from the columns.
+
+        Same host stages as the DataFrame path (rename → keep_fillings →
+        prepare_data → mask, main.py:227-237) on numeric columns; qname strings
+        are materialised lazily (``LazyNames``).  Checked against the DataFrame
+        path by tests/test_synth.py.
+        """
+        from .prep import IntervalData, data_order, first_last_masks, group_span, mask_keep
+        first, last = first_last_masks(self.read_id)
+        keep = ~(first | last)
+        qlen2 = group_span(self.read_id[keep], self.qstart[keep], self.qend[keep], self.n_reads)
+        rid = self.read_id[keep]
+        rs, re_ = self.rstart[keep], self.rend[keep]
+        start = np.minimum(rs, re_)
+        end = np.maximum(rs, re_)
+        aln = self.aln_size[keep]
+        # rename_chromosomes numbering: chrN by N (all synthetic names are chrN / chrX)
+        names = self.chrom_names
+        key = [(0, int(n[3:])) if n[3:].isdigit() else (1, i) for i, n in enumerate(names)]
+        order_names = sorted(range(len(names)), key=lambda i: key[i])
+        num = np.empty(len(names), dtype=np.int64)
+        num[order_names] = np.arange(1, len(names) + 1)
+        chrom = num[self.chrom[keep]]
+        order = data_order(start)
+        lens = {int(num[names.index(k)]): v for k, v in self.chrom_lengths.items() if k in names}
+        mask = [m if m == 'subtelomere' else int(num[names.index(m)]) for m in cluster_mask if
+                m == 'subtelomere' or m in names]
+        data = IntervalData(chrom=chrom[order], start=start[order].astype(np.int64), end=end[order].astype(np.int64),
+                            aln_size=aln[order].astype(np.int64), qcode=rid[order].astype(np.int64),
+                            qnames=LazyNames(self.name_prefix, self.name_suffix, self.n_reads),
+                            n_alignments=self.n_alignments[keep][order].astype(np.int64),
+                            qlen2=qlen2[rid][order].astype(np.int64),
+                            middle=(aln // 2 + start)[order].astype(np.int64),
+                            index=np.flatnonzero(keep)[order])
+        if mask:
+            data = data.select(mask_keep(data.chrom, data.start, data.end, mask, lens, threshold))
+        return data
+
+
+class LazyNames:
+    """code → qname, formatted on access (indexable like the object array of the DataFrame path)."""
+
+    def __init__(self, prefix, suffix, n):
+        self.prefix, self.suffix, self.n = prefix, suffix, n
+
+    def __len__(self):
+        return self.n
+
+    def _one(self, i):
+        return f"{self.prefix}{int(i):08d}{self.suffix}"
+
+    def __getitem__(self, k):
+        if isinstance(k, (int, np.integer)):
+            return self._one(k)
+        return np.array([self._one(i) for i in np.asarray(k).ravel()], dtype=object).reshape(np.shape(k))
+
 
 def _zipf_trunc(rng, a: float, lmax: int, size: int) -> np.ndarray:
     k = np.arange(1, lmax + 1, dtype=np.float64)

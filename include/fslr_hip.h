@@ -1,0 +1,161 @@
+/*
+ * fslr_hip.h — C ABI of the MI355X (gfx950) clustering hot path of fslr.
+ *
+ * The reference (kcleal/fslr, pure Python) has no native FFI for this path; its
+ * hot path is the Python driver in fslr/cluster.py calling the third-party
+ * native interval index `superintervals`.  Each entry point below replaces one
+ * reference interface (file:line into /root/reference/fslr/):
+ *
+ *   fslr_set_reads        cluster.py:189-191  the per-read interval lists
+ *                         (`query_intervals`) handed to the driver, packed CSR
+ *   fslr_build_index      cluster.py:124-130  build_interval_trees (per-chrom
+ *                         superintervals.IntervalMap add/build)
+ *   fslr_query            cluster.py:187-227  query_interval_trees: candidate
+ *                         search (:201), seen-set (:205-208),
+ *                         different_lengths_or_alignments (:178-183),
+ *                         overall_jaccard_similarity (:140-170),
+ *                         calculate_overlap (:133-136), cutoff lookup (:218-219)
+ *   fslr_components       cluster.py:230-234  get_subgraphs (networkx
+ *                         connected_components)
+ *   fslr_union_pairs      (multi-GPU merge of per-shard component labels; no
+ *                         reference counterpart — the reference is single-process)
+ *
+ * Conventions: plain C types, caller-owned host arrays, library-owned device
+ * memory behind an opaque context.  Every function returns FSLR_OK (0) or an
+ * error code; fslr_last_error() gives the message.  Calls on one context are
+ * not re-entrant; different contexts are independent.
+ *
+ * Semantics the caller folds in on the host (so the device does integer work
+ * only, bit-exact to the reference's IEEE-double comparisons):
+ *   iv_thr[k]   overlap threshold of interval k for `calculate_overlap >= overlap`
+ *               (cluster.py:133-136): with o = max(0, min(e1,e2) - max(s1,s2)),
+ *               interval k accepts o iff  thr >= 0 ? o >= thr : o <= ~thr.
+ *               FSLR_THR_ZERO_ALN marks aln_size == 0 (the reference raises
+ *               ZeroDivisionError when such an interval is compared).
+ *   pass_table  [FSLR_MAX_L][2*FSLR_MAX_L] bytes: pass_table[(I-1)*2*FSLR_MAX_L + (U-1)]
+ *               = (I/U >= cutoff(I)) evaluated in Python floats (cluster.py:218-219).
+ *   qlen_cut, nal_cut = 1 - qlen_diff, 1 - n_alignment_diff (Python floats);
+ *               the device compares min/max ratios in IEEE double, as Python does.
+ */
+#ifndef FSLR_HIP_H
+#define FSLR_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FSLR_ABI_VERSION 1
+#define FSLR_MAX_L 64                /* max intervals per read (bitmask width) */
+#define FSLR_MAX_READS (1 << 25)     /* read rank packs into bits 6..30 of the index record */
+#define FSLR_THR_ZERO_ALN INT32_MIN
+
+enum {
+    FSLR_OK = 0,
+    FSLR_ERR_ZERO_DIVISION = 1,   /* the reference would raise ZeroDivisionError */
+    FSLR_ERR_INVALID = 2,         /* bad arguments / unsupported input */
+    FSLR_ERR_HIP = 3,             /* HIP runtime failure */
+    FSLR_ERR_NOMEM = 4,
+    FSLR_ERR_STATE = 5            /* call order violated (e.g. query before index) */
+};
+
+typedef struct fslr_ctx fslr_ctx;
+
+/* Rank-ordered CSR of the prepared intervals.  Reads are in first-appearance
+ * order of the start-sorted `data` list; a read's intervals are in `data` order
+ * (cluster.py:189-191).  All coordinates must lie in [0, 2^30). */
+typedef struct {
+    int64_t n_reads;
+    int64_t n_intervals;
+    int32_t n_chroms;              /* iv_chrom values lie in [0, n_chroms) */
+    const int32_t *read_off;       /* [n_reads+1] */
+    const int32_t *read_qlen2;     /* [n_reads]  keep_fillings qlen2 (cluster.py:26-29) */
+    const int32_t *read_nal;       /* [n_reads]  n_alignments */
+    const int32_t *iv_chrom;       /* [n_intervals] */
+    const int32_t *iv_start;       /* min(rstart, rend)  (cluster.py:111) */
+    const int32_t *iv_end;         /* max(rstart, rend)  (cluster.py:112) */
+    const int32_t *iv_thr;         /* folded overlap threshold, see above */
+} fslr_reads;
+
+typedef struct {
+    double qlen_cut;               /* 1 - qlen_diff */
+    double nal_cut;                /* 1 - n_alignment_diff */
+    const uint8_t *pass_table;     /* host pointer, FSLR_MAX_L * 2*FSLR_MAX_L bytes */
+    int32_t edge_threshold;        /* main.py:221 (10); reported against, see max_fwd */
+    int32_t flags;                 /* reserved, 0 */
+} fslr_params;
+
+typedef struct {
+    int64_t evaluated_pairs;       /* unique candidate read pairs (the reference's seen-set size) */
+    int64_t jaccard_evals;         /* pairs that passed different_lengths_or_alignments */
+    int64_t candidates;            /* interval-level index hits (before pair dedupe) */
+    int64_t n_edges;               /* edges of E* (may exceed edge capacity, see fslr_reserve_edges) */
+    int32_t max_fwd;               /* max over reads of forward (higher-rank) edges */
+    int32_t error;                 /* FSLR_OK or FSLR_ERR_ZERO_DIVISION */
+    int32_t err_a, err_b;          /* read ranks of the pair that raised */
+    int64_t algo_bytes;            /* sum over evaluated pairs of 16*(L_A+L_B)+32 */
+} fslr_query_stats;
+
+typedef struct {
+    float index_ms;                /* fslr_build_index device time */
+    float query_ms;                /* fslr_query: pair kernel device time (events around the launch) */
+    float components_ms;           /* union-find device time */
+    float total_ms;                /* first to last event of the last fslr_run/individual calls */
+} fslr_timings;
+
+int  fslr_abi_version(void);
+const char *fslr_last_error(const fslr_ctx *ctx);
+
+/* device: HIP ordinal; stream: hipStream_t to launch on (NULL = the library creates one). */
+int  fslr_ctx_create(int device, void *stream, fslr_ctx **out);
+void fslr_ctx_destroy(fslr_ctx *ctx);
+int  fslr_set_profiling(fslr_ctx *ctx, int enable);     /* hipEvent timing per phase */
+
+/* Copy the CSR (host pointers) into context-owned HBM buffers (H2D). */
+int  fslr_set_reads(fslr_ctx *ctx, const fslr_reads *reads);
+/* Replace the folded overlap thresholds (iv_thr, CSR order) without re-uploading
+ * or re-indexing: the index does not depend on them (calculate_overlap's
+ * `percentage`, cluster.py:157, is a query-time parameter). */
+int  fslr_set_thresholds(fslr_ctx *ctx, const int32_t *iv_thr);
+/* Edge buffer capacity (edges of E*); grows only. */
+int  fslr_reserve_edges(fslr_ctx *ctx, int64_t capacity);
+
+/* cluster.py:124-130 — sort intervals by (chrom, start), prefix-max of end. Async. */
+int  fslr_build_index(fslr_ctx *ctx);
+/* cluster.py:187-227 — all candidate pairs of query reads with rank in
+ * [a_begin, a_end) against every read of higher rank.  Async; stats are read
+ * with fslr_read_stats. */
+int  fslr_query(fslr_ctx *ctx, const fslr_params *params, int64_t a_begin, int64_t a_end);
+/* cluster.py:230-234 — union-find over the edges: label = min rank in component.  Async. */
+int  fslr_components(fslr_ctx *ctx);
+/* build_index + query(all reads) + components, enqueued back to back.  Async. */
+int  fslr_run(fslr_ctx *ctx, const fslr_params *params);
+
+int  fslr_sync(fslr_ctx *ctx);
+int  fslr_read_stats(fslr_ctx *ctx, fslr_query_stats *out);     /* syncs; returns stats.error */
+int  fslr_get_timings(fslr_ctx *ctx, fslr_timings *out);        /* syncs */
+
+/* D2H copies (sync). */
+int  fslr_get_labels(fslr_ctx *ctx, int32_t *labels);          /* [n_reads] min-rank root */
+int  fslr_get_fwd_degree(fslr_ctx *ctx, int32_t *fwd);         /* [n_reads] */
+int  fslr_get_edges(fslr_ctx *ctx, int32_t *a, int32_t *b, uint16_t *iu, int64_t capacity);
+                                                                /* iu = I | (U << 8); returns count via stats */
+
+/* Device-side views for collectives (e.g. RCCL all_gather of labels). */
+int  fslr_labels_device_ptr(fslr_ctx *ctx, void **dptr);
+/* Copy the [n_reads] labels into a caller-owned device buffer on this device (async, ctx stream). */
+int  fslr_copy_labels_device(fslr_ctx *ctx, int32_t *dst);
+/* Copy the [n_reads] forward degrees into a caller-owned device buffer (async, ctx stream). */
+int  fslr_copy_fwd_device(fslr_ctx *ctx, int32_t *dst);
+/* Union (src[k], dst[k]) into the context's forest; pointers are device pointers
+ * on this context's device when on_device != 0, else host.  Follow with
+ * fslr_finalize_labels.  Async. */
+int  fslr_union_pairs(fslr_ctx *ctx, const int32_t *src, const int32_t *dst, int64_t n, int on_device);
+int  fslr_finalize_labels(fslr_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FSLR_HIP_H */

@@ -64,6 +64,7 @@ typedef struct {
     double nal_diff;
     int64_t edge_threshold;    /* main.py:221 hard-codes 10 */
     int64_t use_cap;           /* 1 = reference behaviour; 0 = E* (no cap) */
+    int64_t query_end;         /* evaluate query reads [0, query_end) only (-1 = all): bounded CPU samples */
 } oracle_params;
 
 typedef struct {
@@ -244,7 +245,8 @@ int oracle_query(const oracle_input *in, const oracle_params *p,
     if (!ins_order || !ins_pos || !uf) { rc = ORACLE_NOMEM; goto done; }
     for (int64_t r = 0; r < N; r++) { ins_pos[r] = -1; uf[r] = r; fwd_count[r] = 0; }
 
-    for (int64_t a = 0; a < N && rc == ORACLE_OK; a++) {
+    const int64_t qend = (p->query_end >= 0 && p->query_end < N) ? p->query_end : N;
+    for (int64_t a = 0; a < qend && rc == ORACLE_OK; a++) {
         int64_t edges = 0;
         const int64_t a0 = in->read_off[a], la = in->read_off[a + 1] - a0;
         for (int64_t i = 0; i < la && rc == ORACLE_OK; i++) {

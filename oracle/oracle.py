@@ -36,7 +36,7 @@ class _Input(ctypes.Structure):
 class _Params(ctypes.Structure):
     _fields_ = [('overlap', ctypes.c_double), ('cutoffs', ctypes.c_void_p), ('n_cutoffs', ctypes.c_int64),
                 ('qlen_diff', ctypes.c_double), ('nal_diff', ctypes.c_double),
-                ('edge_threshold', ctypes.c_int64), ('use_cap', ctypes.c_int64)]
+                ('edge_threshold', ctypes.c_int64), ('use_cap', ctypes.c_int64), ('query_end', ctypes.c_int64)]
 
 
 class _Stats(ctypes.Structure):
@@ -98,15 +98,19 @@ class OracleZeroDivision(ZeroDivisionError):
 
 
 def run_core(csr: OracleCSR, overlap=0.8, cutoffs=(1, 1, 0.66, 0.66, 0.66, 0.5), qlen_diff=0.04,
-             n_aln_diff=0.25, edge_threshold=10, use_cap=True):
-    """Run ``oracle_query``; returns dict with edges, fwd counts, component per read, stats."""
+             n_aln_diff=0.25, edge_threshold=10, use_cap=True, query_end=-1):
+    """Run ``oracle_query``; returns dict with edges, fwd counts, component per read, stats.
+
+    ``query_end`` >= 0 restricts the driver to query reads [0, query_end) (a bounded
+    sample for the CPU baseline; components are then those of the sampled edges).
+    """
     L = lib()
     N = csr.n_reads
     inp = _Input(N, *(_p(getattr(csr, f)) for f in ('read_off', 'chrom', 'start', 'end', 'aln', 'qlen2', 'nal',
                                                      'data_pos')))
     cut = np.ascontiguousarray(cutoffs, dtype=np.float64)
     prm = _Params(float(overlap), _p(cut), len(cut), float(qlen_diff), float(n_aln_diff), int(edge_threshold),
-                  1 if use_cap else 0)
+                  1 if use_cap else 0, int(query_end))
     cap = max(1024, 16 * N)
     while True:
         ea = np.empty(cap, np.int64)
