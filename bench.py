@@ -173,6 +173,8 @@ def main():
                 'n_reads': n, 'n_intervals': csr.n_intervals,
                 'evaluated_pairs_per_step': int(pairs), 'jaccard_evals_per_step': int(jacc),
                 'edges': int(n_edges), 'max_fwd_degree': int(st['max_fwd']),
+                'kernel_stats_rank0': {k: int(st[k]) for k in ('candidates', 'overflow_candidates', 'gather_pairs',
+                                                               'match_entries', 'matched_pairs')},
                 'dense_equivalent_pairs_per_s': (n * (n - 1) / 2) / (elapsed / args.steps),
                 'parallelism': f'pair-space row shards x{world} + RCCL label all_gather' if world > 1 else 'single GPU',
             },

@@ -50,7 +50,9 @@ class QueryStats(ctypes.Structure):
     _fields_ = [('evaluated_pairs', ctypes.c_int64), ('jaccard_evals', ctypes.c_int64),
                 ('candidates', ctypes.c_int64), ('n_edges', ctypes.c_int64), ('max_fwd', ctypes.c_int32),
                 ('error', ctypes.c_int32), ('err_a', ctypes.c_int32), ('err_b', ctypes.c_int32),
-                ('algo_bytes', ctypes.c_int64)]
+                ('algo_bytes', ctypes.c_int64), ('overflow_candidates', ctypes.c_int64),
+                ('gather_pairs', ctypes.c_int64), ('match_entries', ctypes.c_int64),
+                ('matched_pairs', ctypes.c_int64)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

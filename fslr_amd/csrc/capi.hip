@@ -1,0 +1,501 @@
+// capi.hip — the C ABI (include/fslr_hip.h): context, HBM buffers, launch sequencing, timing.
+#include <algorithm>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "fslr_hip.h"
+#include "kernels.hpp"
+
+using namespace fslr;
+
+struct fslr_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  std::string err;
+  int64_t n = 0, ni = 0;
+  int n_chroms = 0;
+  int thr_mode = 0;
+  bool reads_set = false, index_built = false;
+  // device buffers
+  int4* rmeta = nullptr;
+  int4* iv = nullptr;
+  int4* iv_rng = nullptr;
+  int4* idx4 = nullptr;
+  int4* idx_meta = nullptr;
+  int* iv_read = nullptr;
+  int* s_start = nullptr;
+  int2* crange = nullptr;
+  unsigned long long* keys = nullptr;
+  unsigned long long* keys2 = nullptr;
+  int* vals = nullptr;
+  int* vals2 = nullptr;
+  unsigned long long* endkey = nullptr;
+  unsigned long long* pmaxkey = nullptr;
+  void* temp = nullptr;
+  size_t temp_bytes = 0;
+  int* umax = nullptr;     // [FSLR_MAX_L] derived from the pass table
+  int2* edges = nullptr;
+  unsigned short* edge_iu = nullptr;
+  int64_t edge_cap = 0;
+  int* fwd = nullptr;
+  int* parent = nullptr;
+  unsigned long long* counters = nullptr;
+  int* errw = nullptr;     // [0..2] error, [3] max_fwd
+  int* thr_tmp = nullptr;
+  int64_t cap_n = 0, cap_ni = 0, cap_chroms = 0;
+  std::vector<int> umax_host;
+  std::vector<unsigned char> aln_zero_host;   // per CSR interval: FSLR_THR_ZERO_ALN at set_reads
+  int ablate = 0;
+  // profiling
+  bool profiling = false;
+  hipEvent_t ev[8] = {};
+  bool ev_ok = false;
+  bool t_index_rec = false, t_query_rec = false, t_comp_rec = false;
+};
+
+namespace {
+
+int fail(fslr_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+#define HIP_TRY(ctx, expr)                                                                       \
+  do {                                                                                           \
+    hipError_t e_ = (expr);                                                                      \
+    if (e_ != hipSuccess)                                                                        \
+      return fail((ctx), FSLR_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));       \
+  } while (0)
+
+template <typename T>
+int dalloc(fslr_ctx* c, T** p, size_t count) {
+  if (*p) {
+    (void)hipFree(*p);
+    *p = nullptr;
+  }
+  if (count == 0) count = 1;
+  hipError_t e = hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T));
+  if (e != hipSuccess) return fail(c, FSLR_ERR_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+  return FSLR_OK;
+}
+
+int ensure_capacity(fslr_ctx* c, int64_t n, int64_t ni, int n_chroms) {
+  int rc;
+  if (n > c->cap_n) {
+    if ((rc = dalloc(c, &c->rmeta, n)) || (rc = dalloc(c, &c->fwd, n)) || (rc = dalloc(c, &c->parent, n)))
+      return rc;
+    c->cap_n = n;
+  }
+  if (ni > c->cap_ni) {
+    if ((rc = dalloc(c, &c->iv, ni)) || (rc = dalloc(c, &c->iv_rng, ni)) || (rc = dalloc(c, &c->idx4, ni)) ||
+        (rc = dalloc(c, &c->idx_meta, ni)) || (rc = dalloc(c, &c->iv_read, ni)) || (rc = dalloc(c, &c->s_start, ni)) ||
+        (rc = dalloc(c, &c->keys, ni)) || (rc = dalloc(c, &c->keys2, ni)) || (rc = dalloc(c, &c->vals, ni)) ||
+        (rc = dalloc(c, &c->vals2, ni)) || (rc = dalloc(c, &c->endkey, ni)) || (rc = dalloc(c, &c->pmaxkey, ni)) ||
+        (rc = dalloc(c, &c->thr_tmp, ni)))
+      return rc;
+    c->cap_ni = ni;
+    size_t need = 0;
+    HIP_TRY(c, index_temp_bytes(static_cast<int>(ni), &need, c->stream));
+    if (need > c->temp_bytes) {
+      if (c->temp) (void)hipFree(c->temp);
+      c->temp = nullptr;
+      HIP_TRY(c, hipMalloc(&c->temp, need));
+      c->temp_bytes = need;
+    }
+  }
+  if (n_chroms > c->cap_chroms) {
+    if ((rc = dalloc(c, &c->crange, n_chroms))) return rc;
+    c->cap_chroms = n_chroms;
+  }
+  if (!c->umax) {
+    if ((rc = dalloc(c, &c->umax, FSLR_MAX_L))) return rc;
+    if ((rc = dalloc(c, &c->counters, kNumCounters))) return rc;
+    if ((rc = dalloc(c, &c->errw, 4))) return rc;
+  }
+  return FSLR_OK;
+}
+
+int thr_mode_of(const int32_t* thr, int64_t ni) {
+  for (int64_t k = 0; k < ni; ++k)
+    if (thr[k] != FSLR_THR_ZERO_ALN && thr[k] < 1) return 1;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fslr_abi_version(void) { return FSLR_ABI_VERSION; }
+
+const char* fslr_last_error(const fslr_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int fslr_ctx_create(int device, void* stream, fslr_ctx** out) {
+  if (!out) return FSLR_ERR_INVALID;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return FSLR_ERR_HIP;
+  if (device < 0 || device >= ndev) return FSLR_ERR_INVALID;
+  if (hipSetDevice(device) != hipSuccess) return FSLR_ERR_HIP;
+  fslr_ctx* c = new fslr_ctx();
+  c->device = device;
+  if (stream) {
+    c->stream = static_cast<hipStream_t>(stream);
+  } else {
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+      delete c;
+      return FSLR_ERR_HIP;
+    }
+    c->own_stream = true;
+  }
+  if (const char* m = std::getenv("FSLR_ABLATE")) c->ablate = std::atoi(m);   // profiling only
+  *out = c;
+  return FSLR_OK;
+}
+
+void fslr_ctx_destroy(fslr_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  void* bufs[] = {c->rmeta,  c->iv,     c->iv_rng,  c->idx4,    c->idx_meta, c->iv_read, c->s_start,
+                  c->crange, c->keys,   c->keys2,   c->vals,    c->vals2,   c->endkey,  c->pmaxkey,
+                  c->temp,   c->umax,   c->edges,   c->edge_iu, c->fwd,     c->parent,  c->counters,
+                  c->errw,   c->thr_tmp};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  if (c->ev_ok)
+    for (auto& e : c->ev) (void)hipEventDestroy(e);
+  if (c->own_stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int fslr_set_profiling(fslr_ctx* c, int enable) {
+  if (!c) return FSLR_ERR_INVALID;
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (enable && !c->ev_ok) {
+    for (auto& e : c->ev) HIP_TRY(c, hipEventCreate(&e));
+    c->ev_ok = true;
+  }
+  c->profiling = enable != 0;
+  return FSLR_OK;
+}
+
+int fslr_set_reads(fslr_ctx* c, const fslr_reads* r) {
+  if (!c || !r) return FSLR_ERR_INVALID;
+  HIP_TRY(c, hipSetDevice(c->device));
+  const int64_t n = r->n_reads, ni = r->n_intervals;
+  if (n < 0 || ni < 0 || n >= FSLR_MAX_READS || ni >= (int64_t(1) << 31) - 1)
+    return fail(c, FSLR_ERR_INVALID, "read / interval count out of range");
+  if (r->n_chroms < 1 || r->n_chroms >= (1 << 24)) return fail(c, FSLR_ERR_INVALID, "n_chroms out of range");
+  if (!r->read_off || !r->read_qlen2 || !r->read_nal || !r->iv_chrom || !r->iv_start || !r->iv_end || !r->iv_thr)
+    return fail(c, FSLR_ERR_INVALID, "null array");
+  if (r->read_off[0] != 0 || r->read_off[n] != ni)
+    return fail(c, FSLR_ERR_INVALID, "read_off does not span intervals");
+  std::vector<int4> rm(static_cast<size_t>(n));
+  std::vector<int4> iv(static_cast<size_t>(ni));
+  std::vector<unsigned char> zero(static_cast<size_t>(ni), 0);
+  for (int64_t k = 0; k < ni; ++k) {
+    const int ch = r->iv_chrom[k], s = r->iv_start[k], e = r->iv_end[k], t = r->iv_thr[k];
+    if (ch < 0 || ch >= r->n_chroms) return fail(c, FSLR_ERR_INVALID, "chrom id out of range");
+    if (s < 0 || e < s || e >= kMaxCoord)
+      return fail(c, FSLR_ERR_INVALID, "interval coordinates out of [0, 2^30)");
+    if (t == FSLR_THR_ZERO_ALN) zero[k] = 1;
+    iv[k] = make_int4(ch, s, e, t);
+  }
+  for (int64_t i = 0; i < n; ++i) {
+    const int o = r->read_off[i], len = r->read_off[i + 1] - o;
+    if (len < 1 || len > FSLR_MAX_L)
+      return fail(c, FSLR_ERR_INVALID, "every read needs 1.." + std::to_string(FSLR_MAX_L) + " intervals");
+    int flags = 0;
+    for (int k = o; k < o + len; ++k)
+      if (zero[k]) flags |= 1;
+    rm[i] = make_int4(o, len | (flags << 16), r->read_qlen2[i], r->read_nal[i]);
+  }
+  int rc = ensure_capacity(c, n, ni, r->n_chroms);
+  if (rc) return rc;
+  c->n = n;
+  c->ni = ni;
+  c->n_chroms = r->n_chroms;
+  c->thr_mode = thr_mode_of(r->iv_thr, ni);
+  c->aln_zero_host.swap(zero);
+  if (n) HIP_TRY(c, hipMemcpyAsync(c->rmeta, rm.data(), n * sizeof(int4), hipMemcpyHostToDevice, c->stream));
+  if (ni) HIP_TRY(c, hipMemcpyAsync(c->iv, iv.data(), ni * sizeof(int4), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->reads_set = true;
+  c->index_built = false;
+  return FSLR_OK;
+}
+
+int fslr_set_thresholds(fslr_ctx* c, const int32_t* thr) {
+  if (!c || (!thr && c->ni)) return FSLR_ERR_INVALID;
+  if (!c->reads_set) return fail(c, FSLR_ERR_STATE, "fslr_set_reads first");
+  HIP_TRY(c, hipSetDevice(c->device));
+  for (int64_t k = 0; k < c->ni; ++k)
+    if ((thr[k] == FSLR_THR_ZERO_ALN) != (c->aln_zero_host[k] != 0))
+      return fail(c, FSLR_ERR_INVALID, "FSLR_THR_ZERO_ALN must mark the same intervals as in fslr_set_reads");
+  if (c->ni) {
+    HIP_TRY(c, hipMemcpyAsync(c->thr_tmp, thr, c->ni * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, launch_set_thr(c->thr_tmp, c->iv, c->iv_rng, c->index_built ? c->idx4 : nullptr,
+                              static_cast<int>(c->ni), c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+  }
+  c->thr_mode = thr_mode_of(thr, c->ni);
+  return FSLR_OK;
+}
+
+int fslr_reserve_edges(fslr_ctx* c, int64_t capacity) {
+  if (!c || capacity < 0) return FSLR_ERR_INVALID;
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (capacity <= c->edge_cap) return FSLR_OK;
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  int rc;
+  if ((rc = dalloc(c, &c->edges, capacity)) || (rc = dalloc(c, &c->edge_iu, capacity))) return rc;
+  c->edge_cap = capacity;
+  return FSLR_OK;
+}
+
+int fslr_build_index(fslr_ctx* c) {
+  if (!c) return FSLR_ERR_INVALID;
+  if (!c->reads_set) return fail(c, FSLR_ERR_STATE, "fslr_set_reads first");
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (c->profiling) HIP_TRY(c, hipEventRecord(c->ev[0], c->stream));
+  IndexBufs b;
+  b.rmeta = c->rmeta;
+  b.iv = c->iv;
+  b.iv_read = c->iv_read;
+  b.keys = c->keys;
+  b.keys2 = c->keys2;
+  b.vals = c->vals;
+  b.vals2 = c->vals2;
+  b.s_start = c->s_start;
+  b.endkey = c->endkey;
+  b.pmaxkey = c->pmaxkey;
+  b.temp = c->temp;
+  b.temp_bytes = c->temp_bytes;
+  b.crange = c->crange;
+  b.iv_rng = c->iv_rng;
+  b.idx4 = c->idx4;
+  b.idx_meta = c->idx_meta;
+  HIP_TRY(c, launch_build_index(b, static_cast<int>(c->n), static_cast<int>(c->ni), c->n_chroms, c->stream));
+  if (c->profiling) HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));
+  c->t_index_rec = c->profiling;
+  c->index_built = true;
+  return FSLR_OK;
+}
+
+int fslr_query(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_t a_end) {
+  if (!c || !p || !p->pass_table) return FSLR_ERR_INVALID;
+  if (!c->index_built) return fail(c, FSLR_ERR_STATE, "fslr_build_index first");
+  if (a_begin < 0 || a_end > c->n || a_begin > a_end) return fail(c, FSLR_ERR_INVALID, "bad read range");
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (c->edge_cap == 0) {
+    int rc = fslr_reserve_edges(c, std::max<int64_t>(1 << 16, 12 * c->n));
+    if (rc) return rc;
+  }
+  // I/U >= cut(I) is monotone in U (fl(I/U) never increases with U): fold each row of the pass
+  // table into its largest passing U; reject tables that are not of that form
+  c->umax_host.assign(FSLR_MAX_L, 0);
+  for (int I = 1; I <= FSLR_MAX_L; ++I) {
+    const unsigned char* row = p->pass_table + (I - 1) * kPassStride;
+    int um = 0;
+    for (int U = I; U <= kPassStride; ++U)
+      if (row[U - 1]) um = U;
+    for (int U = I; U <= um; ++U)
+      if (!row[U - 1]) return fail(c, FSLR_ERR_INVALID, "pass_table row is not a prefix in U");
+    c->umax_host[I - 1] = um;
+  }
+  HIP_TRY(c, hipMemcpyAsync(c->umax, c->umax_host.data(), FSLR_MAX_L * sizeof(int), hipMemcpyHostToDevice,
+                            c->stream));
+  HIP_TRY(c, hipMemsetAsync(c->counters, 0, kNumCounters * sizeof(unsigned long long), c->stream));
+  HIP_TRY(c, hipMemsetAsync(c->errw, 0, 4 * sizeof(int), c->stream));
+  if (c->n) HIP_TRY(c, hipMemsetAsync(c->fwd, 0, c->n * sizeof(int), c->stream));
+  QueryArgs g;
+  g.rmeta = c->rmeta;
+  g.iv = c->iv;
+  g.iv_rng = c->iv_rng;
+  g.idx4 = c->idx4;
+  g.idx_meta = c->idx_meta;
+  g.umax = c->umax;
+  g.qlen_cut = p->qlen_cut;
+  g.nal_cut = p->nal_cut;
+  g.a_begin = static_cast<int>(a_begin);
+  g.a_end = static_cast<int>(a_end);
+  g.edges = c->edges;
+  g.edge_iu = c->edge_iu;
+  g.edge_cap = c->edge_cap;
+  g.fwd = c->fwd;
+  g.counters = c->counters;
+  g.err = c->errw;
+  g.mode = c->ablate;
+  if (c->profiling) HIP_TRY(c, hipEventRecord(c->ev[2], c->stream));
+  HIP_TRY(c, launch_query(g, c->thr_mode, c->stream));
+  if (c->profiling) HIP_TRY(c, hipEventRecord(c->ev[3], c->stream));
+  c->t_query_rec = c->profiling;
+  return FSLR_OK;
+}
+
+int fslr_components(fslr_ctx* c) {
+  if (!c) return FSLR_ERR_INVALID;
+  if (!c->reads_set) return fail(c, FSLR_ERR_STATE, "fslr_set_reads first");
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (c->profiling) HIP_TRY(c, hipEventRecord(c->ev[4], c->stream));
+  const int n = static_cast<int>(c->n);
+  HIP_TRY(c, launch_uf_init(c->parent, n, c->stream));
+  if (c->edge_cap) HIP_TRY(c, launch_uf_edges(c->parent, c->edges, c->counters, c->edge_cap, c->stream));
+  HIP_TRY(c, launch_uf_finalize(c->parent, n, c->stream));
+  if (c->profiling) HIP_TRY(c, hipEventRecord(c->ev[5], c->stream));
+  c->t_comp_rec = c->profiling;
+  return FSLR_OK;
+}
+
+int fslr_run(fslr_ctx* c, const fslr_params* p) {
+  int rc = fslr_build_index(c);
+  if (rc) return rc;
+  if ((rc = fslr_query(c, p, 0, c->n))) return rc;
+  return fslr_components(c);
+}
+
+int fslr_sync(fslr_ctx* c) {
+  if (!c) return FSLR_ERR_INVALID;
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FSLR_OK;
+}
+
+int fslr_read_stats(fslr_ctx* c, fslr_query_stats* out) {
+  if (!c || !out) return FSLR_ERR_INVALID;
+  HIP_TRY(c, hipSetDevice(c->device));
+  unsigned long long cnt[kNumCounters] = {};
+  int ew[4] = {};
+  if (c->counters) {
+    HIP_TRY(c, hipMemcpyAsync(cnt, c->counters, sizeof(cnt), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(ew, c->errw, sizeof(ew), hipMemcpyDeviceToHost, c->stream));
+  }
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  std::memset(out, 0, sizeof(*out));
+  out->n_edges = static_cast<int64_t>(cnt[kEdgeCount]);
+  out->evaluated_pairs = static_cast<int64_t>(cnt[kEval]);
+  out->jaccard_evals = static_cast<int64_t>(cnt[kJacc]);
+  out->candidates = static_cast<int64_t>(cnt[kCand]);
+  out->algo_bytes = static_cast<int64_t>(cnt[kAlgoBytes]);
+  out->overflow_candidates = static_cast<int64_t>(cnt[kOverflow]);
+  out->gather_pairs = static_cast<int64_t>(cnt[kGather]);
+  out->match_entries = static_cast<int64_t>(cnt[kMatchEntries]);
+  out->matched_pairs = static_cast<int64_t>(cnt[kMatchedPairs]);
+  out->error = ew[0];
+  out->err_a = ew[1];
+  out->err_b = ew[2];
+  out->max_fwd = ew[3];
+  if (ew[0] == FSLR_ERR_ZERO_DIVISION) {
+    c->err = "division by zero";
+    return FSLR_ERR_ZERO_DIVISION;
+  }
+  return FSLR_OK;
+}
+
+int fslr_get_timings(fslr_ctx* c, fslr_timings* out) {
+  if (!c || !out) return FSLR_ERR_INVALID;
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  std::memset(out, 0, sizeof(*out));
+  if (!c->ev_ok) return FSLR_OK;
+  if (c->t_index_rec) HIP_TRY(c, hipEventElapsedTime(&out->index_ms, c->ev[0], c->ev[1]));
+  if (c->t_query_rec) HIP_TRY(c, hipEventElapsedTime(&out->query_ms, c->ev[2], c->ev[3]));
+  if (c->t_comp_rec) HIP_TRY(c, hipEventElapsedTime(&out->components_ms, c->ev[4], c->ev[5]));
+  if (c->t_index_rec && c->t_comp_rec) HIP_TRY(c, hipEventElapsedTime(&out->total_ms, c->ev[0], c->ev[5]));
+  return FSLR_OK;
+}
+
+int fslr_get_labels(fslr_ctx* c, int32_t* labels) {
+  if (!c || (!labels && c->n)) return FSLR_ERR_INVALID;
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (c->n) HIP_TRY(c, hipMemcpyAsync(labels, c->parent, c->n * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FSLR_OK;
+}
+
+int fslr_get_fwd_degree(fslr_ctx* c, int32_t* fwd) {
+  if (!c || (!fwd && c->n)) return FSLR_ERR_INVALID;
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (c->n) HIP_TRY(c, hipMemcpyAsync(fwd, c->fwd, c->n * sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FSLR_OK;
+}
+
+int fslr_get_edges(fslr_ctx* c, int32_t* a, int32_t* b, uint16_t* iu, int64_t capacity) {
+  if (!c) return FSLR_ERR_INVALID;
+  HIP_TRY(c, hipSetDevice(c->device));
+  unsigned long long cnt = 0;
+  if (c->counters)
+    HIP_TRY(c, hipMemcpyAsync(&cnt, c->counters + kEdgeCount, sizeof(cnt), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  const int64_t ne = static_cast<int64_t>(cnt);
+  if (ne > c->edge_cap) return fail(c, FSLR_ERR_STATE, "edge buffer overflowed; reserve and rerun");
+  if (ne > capacity) return fail(c, FSLR_ERR_INVALID, "output capacity too small");
+  if (ne == 0) return FSLR_OK;
+  std::vector<int2> tmp(static_cast<size_t>(ne));
+  HIP_TRY(c, hipMemcpyAsync(tmp.data(), c->edges, ne * sizeof(int2), hipMemcpyDeviceToHost, c->stream));
+  if (iu) HIP_TRY(c, hipMemcpyAsync(iu, c->edge_iu, ne * sizeof(uint16_t), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  for (int64_t k = 0; k < ne; ++k) {
+    if (a) a[k] = tmp[k].x;
+    if (b) b[k] = tmp[k].y;
+  }
+  return FSLR_OK;
+}
+
+int fslr_labels_device_ptr(fslr_ctx* c, void** dptr) {
+  if (!c || !dptr) return FSLR_ERR_INVALID;
+  *dptr = c->parent;
+  return FSLR_OK;
+}
+
+int fslr_copy_labels_device(fslr_ctx* c, int32_t* dst) {
+  if (!c || (!dst && c->n)) return FSLR_ERR_INVALID;
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (c->n) HIP_TRY(c, hipMemcpyAsync(dst, c->parent, c->n * sizeof(int), hipMemcpyDeviceToDevice, c->stream));
+  return FSLR_OK;
+}
+
+int fslr_copy_fwd_device(fslr_ctx* c, int32_t* dst) {
+  if (!c || (!dst && c->n)) return FSLR_ERR_INVALID;
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (c->n) HIP_TRY(c, hipMemcpyAsync(dst, c->fwd, c->n * sizeof(int), hipMemcpyDeviceToDevice, c->stream));
+  return FSLR_OK;
+}
+
+int fslr_union_pairs(fslr_ctx* c, const int32_t* src, const int32_t* dst, int64_t n, int on_device) {
+  if (!c || !dst || n < 0) return FSLR_ERR_INVALID;
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (n == 0) return FSLR_OK;
+  const int* ds = src;
+  const int* dd = dst;
+  int* tmp = nullptr;
+  if (!on_device) {
+    HIP_TRY(c, hipMallocAsync(reinterpret_cast<void**>(&tmp), (src ? 2 : 1) * n * sizeof(int), c->stream));
+    HIP_TRY(c, hipMemcpyAsync(tmp, dst, n * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    dd = tmp;
+    if (src) {
+      HIP_TRY(c, hipMemcpyAsync(tmp + n, src, n * sizeof(int), hipMemcpyHostToDevice, c->stream));
+      ds = tmp + n;
+    }
+  }
+  HIP_TRY(c, launch_uf_pairs(c->parent, ds, dd, n, c->stream));
+  if (tmp) {
+    HIP_TRY(c, hipFreeAsync(tmp, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+  }
+  return FSLR_OK;
+}
+
+int fslr_finalize_labels(fslr_ctx* c) {
+  if (!c) return FSLR_ERR_INVALID;
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, launch_uf_finalize(c->parent, static_cast<int>(c->n), c->stream));
+  return FSLR_OK;
+}
+
+}  // extern "C"

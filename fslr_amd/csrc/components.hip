@@ -1,0 +1,94 @@
+// components.hip — connected components (replaces get_subgraphs, cluster.py:230-234, i.e.
+// networkx.connected_components over the graph built at cluster.py:221).
+//
+// Lock-free union-find: roots are hooked larger-under-smaller with a CAS, so the root of a
+// component is its minimum read rank — the order networkx yields components in (first inserted
+// node = minimum rank when every edge is added in its lower-rank read's loop).
+// Parent reads/writes are relaxed agent-scope atomics (L1-bypassing), so no CU reads a stale
+// parent from its own L1 (MI355X_MICROARCH.md, inter-workgroup visibility).  Parent values only
+// decrease, so path halving never breaks the forest.
+#include "kernels.hpp"
+
+namespace fslr {
+namespace {
+
+__device__ __forceinline__ int ld_rlx(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_rlx(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ int uf_find(int* p, int x) {
+  while (true) {
+    const int px = ld_rlx(p + x);
+    if (px == x) return x;
+    const int ppx = ld_rlx(p + px);
+    if (ppx != px) st_rlx(p + x, ppx);   // path halving; ppx is still an ancestor of x
+    x = ppx;
+  }
+}
+
+__device__ void uf_union(int* p, int a, int b) {
+  while (true) {
+    a = uf_find(p, a);
+    b = uf_find(p, b);
+    if (a == b) return;
+    if (a > b) { const int t = a; a = b; b = t; }
+    const int old = atomicCAS(p + b, b, a);   // hook the larger root under the smaller
+    if (old == b) return;
+    b = old;
+  }
+}
+
+__global__ void k_uf_init(int* p, int n) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = i;
+}
+
+__global__ void k_uf_edges(int* p, const int2* __restrict__ edges, const unsigned long long* __restrict__ count,
+                           long long cap) {
+  const long long ne = min(static_cast<long long>(*count), cap);
+  for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < ne;
+       k += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const int2 e = edges[k];
+    uf_union(p, e.x, e.y);
+  }
+}
+
+__global__ void k_uf_pairs(int* p, const int* __restrict__ src, const int* __restrict__ dst, long long n) {
+  for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < n;
+       k += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const int s = src ? src[k] : static_cast<int>(k);
+    uf_union(p, s, dst[k]);
+  }
+}
+
+__global__ void k_uf_finalize(int* p, int n) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    st_rlx(p + i, uf_find(p, i));
+}
+
+}  // namespace
+
+hipError_t launch_uf_init(int* parent, int n, hipStream_t s) {
+  if (n > 0) k_uf_init<<<grid_for(n), 256, 0, s>>>(parent, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_uf_edges(int* parent, const int2* edges, const unsigned long long* count, long long cap,
+                           hipStream_t s) {
+  if (cap > 0) k_uf_edges<<<grid_for(cap), 256, 0, s>>>(parent, edges, count, cap);
+  return hipGetLastError();
+}
+
+hipError_t launch_uf_pairs(int* parent, const int* src, const int* dst, long long n, hipStream_t s) {
+  if (n > 0) k_uf_pairs<<<grid_for(n), 256, 0, s>>>(parent, src, dst, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_uf_finalize(int* parent, int n, hipStream_t s) {
+  if (n > 0) k_uf_finalize<<<grid_for(n), 256, 0, s>>>(parent, n);
+  return hipGetLastError();
+}
+
+}  // namespace fslr

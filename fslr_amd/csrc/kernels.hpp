@@ -1,0 +1,87 @@
+// kernels.hpp — internal interface between the C API (capi.hip) and the gfx950 kernels.
+//
+// Device layout (all in HBM, see DESIGN.md "Data layout"):
+//   rmeta[N]    int4 {iv offset, len | flags<<16, qlen2, n_alignments}       rank order
+//   iv[NI]      int4 {chrom, start, end, thr}                                 CSR (rank, data order)
+//   iv_rng[NI]  int4 {q, n_fwd, bwd_begin, n_bwd}                             per CSR interval:
+//               q = its position in the (chrom,start)-sorted index; sorted positions
+//               q+1 .. q+n_fwd all overlap it (start <= end_q); bwd_begin .. q-1 are the
+//               earlier positions whose prefix-max end reaches start_q (hit iff end >= start_q)
+//   idx4[NI]    int4 {start, end, thr, read << 6 | j} of the interval at sorted position
+//   idx_meta[NI] int4 = rmeta[read] of the interval at sorted position (gate inputs at hit time)
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace fslr {
+
+constexpr int kWave = 64;
+constexpr int kPassStride = 128;      // 2 * FSLR_MAX_L
+constexpr int kMaxCoord = 1 << 30;
+
+enum Counter { kEdgeCount = 0, kEval = 1, kJacc = 2, kCand = 3, kAlgoBytes = 4, kOverflow = 5, kGather = 6,
+               kMatchEntries = 7, kMatchedPairs = 8, kNumCounters = 9 };
+
+// ---- index build (index.hip) -------------------------------------------------------------
+struct IndexBufs {
+  const int4* rmeta;
+  const int4* iv;
+  int* iv_read;                       // scratch [NI]
+  unsigned long long* keys;           // scratch [NI] x2 (double buffer for the sort)
+  unsigned long long* keys2;
+  int* vals;
+  int* vals2;
+  int* s_start;                       // scratch [NI] starts in sorted order
+  unsigned long long* endkey;         // scratch [NI]
+  unsigned long long* pmaxkey;        // scratch [NI]
+  void* temp;
+  size_t temp_bytes;
+  int2* crange;                       // [n_chroms] {begin, end} in sorted order
+  int4* iv_rng;                       // out [NI]
+  int4* idx4;                         // out [NI]
+  int4* idx_meta;                     // out [NI]
+};
+// bytes of hipcub temp storage the index build needs for ni intervals
+hipError_t index_temp_bytes(int ni, size_t* bytes, hipStream_t s);
+hipError_t launch_build_index(const IndexBufs& b, int n_reads, int ni, int n_chroms, hipStream_t s);
+// thresholds into iv[k].w and (when the index exists) idx4[iv_rng[k].x].z
+hipError_t launch_set_thr(const int* thr, int4* iv, const int4* iv_rng, int4* idx4, int ni, hipStream_t s);
+
+// ---- pair kernel (query.hip) -------------------------------------------------------------
+struct QueryArgs {
+  const int4* rmeta;
+  const int4* iv;
+  const int4* iv_rng;
+  const int4* idx4;
+  const int4* idx_meta;
+  const int* umax;                    // [64]: pair with I matches is an edge iff I + ... U <= umax[I-1]
+  double qlen_cut, nal_cut;
+  int a_begin, a_end;
+  int2* edges;
+  unsigned short* edge_iu;
+  long long edge_cap;
+  int* fwd;
+  unsigned long long* counters;
+  int* err;                           // [0] code, [1] a, [2] b, [3] max forward degree
+  int mode;                           // profiling ablation (FSLR_ABLATE): 0 full, 1 scan only, 2 no greedy
+};
+// thr_mode: 0 = every non-sentinel threshold >= 1 (fast match), 1 = general encoding
+hipError_t launch_query(const QueryArgs& a, int thr_mode, hipStream_t s);
+
+// ---- components (components.hip) ---------------------------------------------------------
+hipError_t launch_uf_init(int* parent, int n, hipStream_t s);
+hipError_t launch_uf_edges(int* parent, const int2* edges, const unsigned long long* count, long long cap,
+                           hipStream_t s);
+hipError_t launch_uf_pairs(int* parent, const int* src, const int* dst, long long n, hipStream_t s);
+hipError_t launch_uf_finalize(int* parent, int n, hipStream_t s);
+
+inline int grid_for(long long n, int block = 256, int cap = 256 * 16) {
+  long long g = (n + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return static_cast<int>(g);
+}
+
+}  // namespace fslr

@@ -96,6 +96,11 @@ typedef struct {
     int32_t error;                 /* FSLR_OK or FSLR_ERR_ZERO_DIVISION */
     int32_t err_a, err_b;          /* read ranks of the pair that raised */
     int64_t algo_bytes;            /* sum over evaluated pairs of 16*(L_A+L_B)+32 */
+    int64_t overflow_candidates;   /* candidates of reads past the per-wave partner-set limit (witness path) */
+    int64_t gather_pairs;          /* pairs evaluated by gathering B's intervals (general thresholds,
+                                      aln_size==0 replay, match-list overflow) */
+    int64_t match_entries;         /* matching interval pairs recorded in the per-read match lists */
+    int64_t matched_pairs;         /* read pairs with at least one matching interval pair */
 } fslr_query_stats;
 
 typedef struct {

@@ -1,0 +1,16 @@
+#!/bin/bash
+# PMC passes for the pair kernel (separate rocprofv3 runs, --pmc only with --kernel-trace-free collection).
+# Usage (GPU box, repo root): OUT=gpurun_out/pmc tools/pmc.sh [bench args]
+set -e
+OUT=${OUT:-gpurun_out/pmc}
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+mkdir -p $ROOT/$OUT
+cd /tmp && export TMPDIR=/tmp
+i=0
+for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
+           "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $set --kernel-include-regex "query_kernel" -d $ROOT/$OUT/p$i -o pmc \
+      --output-format csv -- python3 $ROOT/bench.py --steps 2 --warmup 1 --cpu-sample-reads 0 "$@" \
+      > $ROOT/$OUT/p$i.log 2>&1
+done
