@@ -78,8 +78,7 @@ def main():
     torch.cuda.set_stream(stream)
     ctx = _lib.Context(local_rank, stream=stream.cuda_stream, profiling=True)
     thr = fold_overlap_threshold(csr.iv_aln, 0.8)
-    ctx.set_reads(csr.read_off, csr.read_qlen2, csr.read_nal, csr.iv_chrom, csr.iv_start, csr.iv_end, thr,
-                  csr.n_chroms)
+    ctx.load_csr(csr, thr)
     ctx.reserve_edges(12 * csr.n_reads)
     pt = pass_table([1, 1, 0.66, 0.66, 0.66, 0.5])
     qcut, ncut = 1 - 0.04, 1 - 0.25

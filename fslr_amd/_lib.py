@@ -21,7 +21,8 @@ PASS_STRIDE = 2 * FSLR_MAX_L
 
 # every symbol include/fslr_hip.h declares (checked by tests/test_abi.py)
 EXPORTED = ['fslr_abi_version', 'fslr_last_error', 'fslr_ctx_create', 'fslr_ctx_destroy', 'fslr_set_profiling',
-            'fslr_set_reads', 'fslr_set_thresholds', 'fslr_reserve_edges', 'fslr_build_index', 'fslr_query',
+            'fslr_set_reads', 'fslr_set_thresholds', 'fslr_reserve_edges', 'fslr_reserve_deferred',
+            'fslr_build_index', 'fslr_query',
             'fslr_components', 'fslr_run', 'fslr_sync', 'fslr_read_stats', 'fslr_get_timings', 'fslr_get_labels',
             'fslr_get_fwd_degree', 'fslr_get_edges', 'fslr_labels_device_ptr', 'fslr_copy_labels_device',
             'fslr_copy_fwd_device', 'fslr_union_pairs', 'fslr_finalize_labels']
@@ -38,7 +39,7 @@ class FslrError(RuntimeError):
 class Reads(ctypes.Structure):
     _fields_ = [('n_reads', ctypes.c_int64), ('n_intervals', ctypes.c_int64), ('n_chroms', ctypes.c_int32)] + [
         (f, ctypes.c_void_p) for f in ('read_off', 'read_qlen2', 'read_nal', 'iv_chrom', 'iv_start', 'iv_end',
-                                       'iv_thr')]
+                                       'iv_thr', 'iv_data_pos')]
 
 
 class Params(ctypes.Structure):
@@ -52,7 +53,8 @@ class QueryStats(ctypes.Structure):
                 ('error', ctypes.c_int32), ('err_a', ctypes.c_int32), ('err_b', ctypes.c_int32),
                 ('algo_bytes', ctypes.c_int64), ('overflow_candidates', ctypes.c_int64),
                 ('gather_pairs', ctypes.c_int64), ('match_entries', ctypes.c_int64),
-                ('matched_pairs', ctypes.c_int64)]
+                ('matched_pairs', ctypes.c_int64), ('deferred', ctypes.c_int64),
+                ('deferred_capacity', ctypes.c_int64), ('edge_capacity', ctypes.c_int64)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
@@ -88,6 +90,7 @@ def load(path: str = LIB_PATH):
         'fslr_set_reads': (ctypes.c_int, [vp, ctypes.POINTER(Reads)]),
         'fslr_set_thresholds': (ctypes.c_int, [vp, vp]),
         'fslr_reserve_edges': (ctypes.c_int, [vp, i64]),
+        'fslr_reserve_deferred': (ctypes.c_int, [vp, i64]),
         'fslr_build_index': (ctypes.c_int, [vp]),
         'fslr_query': (ctypes.c_int, [vp, ctypes.POINTER(Params), i64, i64]),
         'fslr_components': (ctypes.c_int, [vp]),
@@ -155,12 +158,22 @@ class Context:
         raise FslrError(f'fslr error {rc}: {msg}')
 
     # -- data -------------------------------------------------------------------------
-    def set_reads(self, read_off, read_qlen2, read_nal, iv_chrom, iv_start, iv_end, iv_thr, n_chroms):
+    def set_reads(self, read_off, read_qlen2, read_nal, iv_chrom, iv_start, iv_end, iv_thr, n_chroms,
+                  iv_data_pos=None):
         arrs = [np.ascontiguousarray(x, dtype=np.int32) for x in
                 (read_off, read_qlen2, read_nal, iv_chrom, iv_start, iv_end, iv_thr)]
-        r = Reads(len(arrs[1]), len(arrs[3]), int(n_chroms), *(_ptr(a) for a in arrs))
+        dp = None if iv_data_pos is None else np.ascontiguousarray(iv_data_pos, dtype=np.int32)
+        r = Reads(len(arrs[1]), len(arrs[3]), int(n_chroms), *(_ptr(a) for a in arrs),
+                  _ptr(dp) if dp is not None else None)
         self._check(self._L.fslr_set_reads(self._h, ctypes.byref(r)))
+        if arrs[2].size and (arrs[2].min() < 0 or arrs[2].max() >= (1 << 24)):
+            raise ValueError('n_alignments must lie in [0, 2**24) for the device path')
         self.n_reads = len(arrs[1])
+
+    def load_csr(self, csr, iv_thr):
+        """Upload a ``fslr_amd.prep.CSR`` (with its start-sorted data order) and thresholds."""
+        self.set_reads(csr.read_off, csr.read_qlen2, csr.read_nal, csr.iv_chrom, csr.iv_start, csr.iv_end, iv_thr,
+                       csr.n_chroms, iv_data_pos=csr.data_pos)
 
     def set_thresholds(self, iv_thr):
         t = np.ascontiguousarray(iv_thr, dtype=np.int32)
@@ -196,10 +209,34 @@ class Context:
         self._check(self._L.fslr_sync(self._h))
 
     # -- results ------------------------------------------------------------------------
-    def stats(self) -> dict:
+    def reserve_deferred(self, cap):
+        self._check(self._L.fslr_reserve_deferred(self._h, int(cap)))
+
+    def stats(self, check: bool = True) -> dict:
+        """Counters of the last query.  With ``check`` a buffer overflow raises FslrError;
+        ``run_query`` grows the buffers and reruns instead."""
         s = QueryStats()
-        self._check(self._L.fslr_read_stats(self._h, ctypes.byref(s)))
+        rc = self._L.fslr_read_stats(self._h, ctypes.byref(s))
+        if rc == FSLR_ERR_STATE and not check:
+            return s.as_dict()
+        self._check(rc)
         return s.as_dict()
+
+    def run_query(self, qlen_cut, nal_cut, pass_table, edge_threshold=10, a_begin=0, a_end=None) -> dict:
+        """query + stats, growing the edge / deferred buffers and rerunning on overflow."""
+        while True:
+            self.query(qlen_cut, nal_cut, pass_table, edge_threshold, a_begin, a_end)
+            st = self.stats(check=False)
+            grow = False
+            if st['n_edges'] > st['edge_capacity']:
+                self.reserve_edges(int(st['n_edges'] * 1.25) + 4096)
+                grow = True
+            if st['deferred'] > st['deferred_capacity']:
+                self.reserve_deferred(int(st['deferred'] * 1.25) + 4096)
+                grow = True
+            if not grow:
+                self.stats()          # raises on a device-side error (ZeroDivisionError)
+                return st
 
     def timings(self) -> dict:
         t = Timings()

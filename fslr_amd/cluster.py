@@ -185,7 +185,7 @@ class DeviceIntervalIndex:
         self.ctx = ctx or Context(_default_device() if device is None else device)
         c = self.csr
         thr0 = np.where(c.iv_aln == 0, FSLR_THR_ZERO_ALN, 0).astype(np.int32)
-        self.ctx.set_reads(c.read_off, c.read_qlen2, c.read_nal, c.iv_chrom, c.iv_start, c.iv_end, thr0, c.n_chroms)
+        self.ctx.load_csr(c, thr0)
         self.ctx.build_index()
 
 
@@ -278,12 +278,7 @@ def query_interval_trees(interval_trees, data, overlap_cutoff, jaccard_threshold
     qcut = 1 - qlen_diff
     ncut = 1 - diff
     ctx.reserve_edges(max(1 << 16, 12 * csr.n_reads))
-    while True:
-        ctx.query(qcut, ncut, pt, int(edge_threshold))
-        st = ctx.stats()
-        if st['n_edges'] <= ctx.edge_capacity:
-            break
-        ctx.reserve_edges(int(st['n_edges'] * 1.25) + 1024)
+    st = ctx.run_query(qcut, ncut, pt, int(edge_threshold))
     ctx.components()
     labels = ctx.labels()
     ne = st['n_edges']

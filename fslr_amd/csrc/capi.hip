@@ -19,14 +19,16 @@ struct fslr_ctx {
   int64_t n = 0, ni = 0;
   int n_chroms = 0;
   int thr_mode = 0;
-  bool reads_set = false, index_built = false;
+  bool reads_set = false, index_built = false, have_data_pos = false;
   // device buffers
   int4* rmeta = nullptr;
   int4* iv = nullptr;
   int4* iv_rng = nullptr;
   int4* idx4 = nullptr;
-  int4* idx_meta = nullptr;
-  int* iv_read = nullptr;
+  int2* idx_gate = nullptr;
+  unsigned long long* defer = nullptr;
+  int64_t defer_cap = 0;
+  int* data_pos = nullptr;
   int* s_start = nullptr;
   int2* crange = nullptr;
   unsigned long long* keys = nullptr;
@@ -92,7 +94,7 @@ int ensure_capacity(fslr_ctx* c, int64_t n, int64_t ni, int n_chroms) {
   }
   if (ni > c->cap_ni) {
     if ((rc = dalloc(c, &c->iv, ni)) || (rc = dalloc(c, &c->iv_rng, ni)) || (rc = dalloc(c, &c->idx4, ni)) ||
-        (rc = dalloc(c, &c->idx_meta, ni)) || (rc = dalloc(c, &c->iv_read, ni)) || (rc = dalloc(c, &c->s_start, ni)) ||
+        (rc = dalloc(c, &c->idx_gate, ni)) || (rc = dalloc(c, &c->data_pos, ni)) || (rc = dalloc(c, &c->s_start, ni)) ||
         (rc = dalloc(c, &c->keys, ni)) || (rc = dalloc(c, &c->keys2, ni)) || (rc = dalloc(c, &c->vals, ni)) ||
         (rc = dalloc(c, &c->vals2, ni)) || (rc = dalloc(c, &c->endkey, ni)) || (rc = dalloc(c, &c->pmaxkey, ni)) ||
         (rc = dalloc(c, &c->thr_tmp, ni)))
@@ -160,10 +162,10 @@ void fslr_ctx_destroy(fslr_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* bufs[] = {c->rmeta,  c->iv,     c->iv_rng,  c->idx4,    c->idx_meta, c->iv_read, c->s_start,
+  void* bufs[] = {c->rmeta,  c->iv,     c->iv_rng,  c->idx4,    c->idx_gate, c->data_pos, c->s_start,
                   c->crange, c->keys,   c->keys2,   c->vals,    c->vals2,   c->endkey,  c->pmaxkey,
                   c->temp,   c->umax,   c->edges,   c->edge_iu, c->fwd,     c->parent,  c->counters,
-                  c->errw,   c->thr_tmp};
+                  c->errw,   c->thr_tmp, c->defer};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->ev_ok)
@@ -209,13 +211,44 @@ int fslr_set_reads(fslr_ctx* c, const fslr_reads* r) {
     const int o = r->read_off[i], len = r->read_off[i + 1] - o;
     if (len < 1 || len > FSLR_MAX_L)
       return fail(c, FSLR_ERR_INVALID, "every read needs 1.." + std::to_string(FSLR_MAX_L) + " intervals");
+    if (r->read_nal[i] < 0 || r->read_nal[i] >= (1 << 24))
+      return fail(c, FSLR_ERR_INVALID, "n_alignments outside [0, 2^24)");
     int flags = 0;
     for (int k = o; k < o + len; ++k)
       if (zero[k]) flags |= 1;
     rm[i] = make_int4(o, len | (flags << 16), r->read_qlen2[i], r->read_nal[i]);
   }
+  // chromosome ranges of the (chrom, start)-sorted index: chromosome ids ascending (host counts)
+  std::vector<int2> cr(static_cast<size_t>(r->n_chroms), make_int2(0, 0));
+  {
+    std::vector<int64_t> cnt(static_cast<size_t>(r->n_chroms), 0);
+    for (int64_t k = 0; k < ni; ++k) cnt[r->iv_chrom[k]]++;
+    int64_t acc = 0;
+    for (int ch = 0; ch < r->n_chroms; ++ch) {
+      cr[ch] = make_int2(static_cast<int>(acc), static_cast<int>(acc + cnt[ch]));
+      acc += cnt[ch];
+    }
+  }
+  // optional start-sorted data order: must be a permutation with non-decreasing start
+  bool use_dp = false;
+  if (r->iv_data_pos) {
+    std::vector<int> inv(static_cast<size_t>(ni), -1);
+    use_dp = true;
+    for (int64_t k = 0; k < ni && use_dp; ++k) {
+      const int d = r->iv_data_pos[k];
+      if (d < 0 || d >= ni || inv[d] >= 0) use_dp = false;
+      else inv[d] = static_cast<int>(k);
+    }
+    for (int64_t d = 1; d < ni && use_dp; ++d)
+      if (r->iv_start[inv[d]] < r->iv_start[inv[d - 1]]) use_dp = false;
+    if (!use_dp) return fail(c, FSLR_ERR_INVALID, "iv_data_pos is not a start-sorted permutation");
+  }
   int rc = ensure_capacity(c, n, ni, r->n_chroms);
   if (rc) return rc;
+  HIP_TRY(c, hipMemcpyAsync(c->crange, cr.data(), cr.size() * sizeof(int2), hipMemcpyHostToDevice, c->stream));
+  if (use_dp && ni)
+    HIP_TRY(c, hipMemcpyAsync(c->data_pos, r->iv_data_pos, ni * sizeof(int), hipMemcpyHostToDevice, c->stream));
+  c->have_data_pos = use_dp;
   c->n = n;
   c->ni = ni;
   c->n_chroms = r->n_chroms;
@@ -257,6 +290,17 @@ int fslr_reserve_edges(fslr_ctx* c, int64_t capacity) {
   return FSLR_OK;
 }
 
+int fslr_reserve_deferred(fslr_ctx* c, int64_t capacity) {
+  if (!c || capacity < 0) return FSLR_ERR_INVALID;
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (capacity <= c->defer_cap) return FSLR_OK;
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  int rc;
+  if ((rc = dalloc(c, &c->defer, capacity))) return rc;
+  c->defer_cap = capacity;
+  return FSLR_OK;
+}
+
 int fslr_build_index(fslr_ctx* c) {
   if (!c) return FSLR_ERR_INVALID;
   if (!c->reads_set) return fail(c, FSLR_ERR_STATE, "fslr_set_reads first");
@@ -265,7 +309,7 @@ int fslr_build_index(fslr_ctx* c) {
   IndexBufs b;
   b.rmeta = c->rmeta;
   b.iv = c->iv;
-  b.iv_read = c->iv_read;
+  b.data_pos = c->have_data_pos ? c->data_pos : nullptr;
   b.keys = c->keys;
   b.keys2 = c->keys2;
   b.vals = c->vals;
@@ -278,7 +322,7 @@ int fslr_build_index(fslr_ctx* c) {
   b.crange = c->crange;
   b.iv_rng = c->iv_rng;
   b.idx4 = c->idx4;
-  b.idx_meta = c->idx_meta;
+  b.idx_gate = c->idx_gate;
   HIP_TRY(c, launch_build_index(b, static_cast<int>(c->n), static_cast<int>(c->ni), c->n_chroms, c->stream));
   if (c->profiling) HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));
   c->t_index_rec = c->profiling;
@@ -293,6 +337,10 @@ int fslr_query(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_t a_end
   HIP_TRY(c, hipSetDevice(c->device));
   if (c->edge_cap == 0) {
     int rc = fslr_reserve_edges(c, std::max<int64_t>(1 << 16, 12 * c->n));
+    if (rc) return rc;
+  }
+  if (c->defer_cap == 0) {
+    int rc = fslr_reserve_deferred(c, std::max<int64_t>(1 << 20, c->n));
     if (rc) return rc;
   }
   // I/U >= cut(I) is monotone in U (fl(I/U) never increases with U): fold each row of the pass
@@ -317,7 +365,9 @@ int fslr_query(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_t a_end
   g.iv = c->iv;
   g.iv_rng = c->iv_rng;
   g.idx4 = c->idx4;
-  g.idx_meta = c->idx_meta;
+  g.idx_gate = c->idx_gate;
+  g.defer = c->defer;
+  g.defer_cap = c->defer_cap;
   g.umax = c->umax;
   g.qlen_cut = p->qlen_cut;
   g.nal_cut = p->nal_cut;
@@ -385,6 +435,9 @@ int fslr_read_stats(fslr_ctx* c, fslr_query_stats* out) {
   out->gather_pairs = static_cast<int64_t>(cnt[kGather]);
   out->match_entries = static_cast<int64_t>(cnt[kMatchEntries]);
   out->matched_pairs = static_cast<int64_t>(cnt[kMatchedPairs]);
+  out->deferred = static_cast<int64_t>(cnt[kDeferCount]);
+  out->deferred_capacity = c->defer_cap;
+  out->edge_capacity = c->edge_cap;
   out->error = ew[0];
   out->err_a = ew[1];
   out->err_b = ew[2];
@@ -393,6 +446,7 @@ int fslr_read_stats(fslr_ctx* c, fslr_query_stats* out) {
     c->err = "division by zero";
     return FSLR_ERR_ZERO_DIVISION;
   }
+  if (out->deferred > c->defer_cap) return fail(c, FSLR_ERR_STATE, "deferred list overflowed; reserve and rerun");
   return FSLR_OK;
 }
 

@@ -8,7 +8,8 @@
 //               q+1 .. q+n_fwd all overlap it (start <= end_q); bwd_begin .. q-1 are the
 //               earlier positions whose prefix-max end reaches start_q (hit iff end >= start_q)
 //   idx4[NI]    int4 {start, end, thr, read << 6 | j} of the interval at sorted position
-//   idx_meta[NI] int4 = rmeta[read] of the interval at sorted position (gate inputs at hit time)
+//   idx_gate[NI] int2 {qlen2, nal | LB << 24 | haz << 31} of the read at sorted position
+//               (the pair gate's inputs, read beside the hit; nal < 2^24 is validated)
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -22,13 +23,13 @@ constexpr int kPassStride = 128;      // 2 * FSLR_MAX_L
 constexpr int kMaxCoord = 1 << 30;
 
 enum Counter { kEdgeCount = 0, kEval = 1, kJacc = 2, kCand = 3, kAlgoBytes = 4, kOverflow = 5, kGather = 6,
-               kMatchEntries = 7, kMatchedPairs = 8, kNumCounters = 9 };
+               kMatchEntries = 7, kMatchedPairs = 8, kDeferCount = 9, kNumCounters = 10 };
 
 // ---- index build (index.hip) -------------------------------------------------------------
 struct IndexBufs {
   const int4* rmeta;
   const int4* iv;
-  int* iv_read;                       // scratch [NI]
+  const int* data_pos;                // [NI] or nullptr: start-sorted order is given (one chrom pass)
   unsigned long long* keys;           // scratch [NI] x2 (double buffer for the sort)
   unsigned long long* keys2;
   int* vals;
@@ -38,10 +39,10 @@ struct IndexBufs {
   unsigned long long* pmaxkey;        // scratch [NI]
   void* temp;
   size_t temp_bytes;
-  int2* crange;                       // [n_chroms] {begin, end} in sorted order
+  const int2* crange;                 // [n_chroms] {begin, end} in sorted order (host counts)
   int4* iv_rng;                       // out [NI]
   int4* idx4;                         // out [NI]
-  int4* idx_meta;                     // out [NI]
+  int2* idx_gate;                     // out [NI]
 };
 // bytes of hipcub temp storage the index build needs for ni intervals
 hipError_t index_temp_bytes(int ni, size_t* bytes, hipStream_t s);
@@ -55,7 +56,7 @@ struct QueryArgs {
   const int4* iv;
   const int4* iv_rng;
   const int4* idx4;
-  const int4* idx_meta;
+  const int2* idx_gate;
   const int* umax;                    // [64]: pair with I matches is an edge iff I + ... U <= umax[I-1]
   double qlen_cut, nal_cut;
   int a_begin, a_end;
@@ -63,6 +64,8 @@ struct QueryArgs {
   unsigned short* edge_iu;
   long long edge_cap;
   int* fwd;
+  unsigned long long* defer;          // deferred pairs (query_kernel → deferred_kernel)
+  long long defer_cap;
   unsigned long long* counters;
   int* err;                           // [0] code, [1] a, [2] b, [3] max forward degree
   int mode;                           // profiling ablation (FSLR_ABLATE): 0 full, 1 scan only, 2 no greedy

@@ -1,28 +1,28 @@
-// query.hip — the pair kernel: replaces the driver of query_interval_trees (cluster.py:187-227)
+// query.hip — the pair kernels: replace the driver of query_interval_trees (cluster.py:187-227)
 // with its predicates different_lengths_or_alignments (:178-183), overall_jaccard_similarity
 // (:140-170), calculate_overlap (:133-136) and the cutoff lookup (:216-219).
 //
-// One wavefront per query read A (grid-stride over ranks a in [a_begin, a_end)).  A's intervals
-// live in lanes 0..LA-1 and are read wave-uniformly with v_readlane.
-//
-//  1. candidate walk — A's scan ranges (kernels.hpp: iv_rng) are flattened with a wave prefix
-//     sum and walked 64 records per step, one record per lane (4-8 B loads, no wasted reads):
-//     forward records are all hits, backward records hit iff end >= start_i.
-//  2. dedupe — a hit on read B > A is inserted into a per-wave LDS hash set (epoch-tagged,
-//     1024 slots); the first insertion of B is the one evaluation of (A, B), exactly like the
-//     reference's seen-set (:205-208).  Reads with more than kHashLimit distinct partners
-//     continue in lookup-only mode; partners not in the set are evaluated once by the witness
-//     rule (the candidate whose (j, i) is the first overlapping interval pair in B-major order).
-//  3. gate queue (LDS) → 64 pairs at a time: read B's record, apply the length / alignment-count
-//     gate in IEEE double (bit-identical to Python's int/int true division).
-//  4. eval queue (LDS) → 64 pairs at a time: each lane walks B's intervals four rows per load
-//     group; per row j the 64-bit match mask M_j over A's intervals feeds the first-fit greedy
-//     (m = M_j & free; take lowest).  First-fit greedy is symmetric in (l1, l2) (SURVEY §8a A8,
-//     tests/test_oracle_golden.py::test_kat_jaccard_symmetric), so B-major = the reference's
-//     A-major count.  Pairs holding an aln_size==0 interval replay the reference loop exactly to
-//     raise ZeroDivisionError where the reference does.
-//  5. edges (A, B, I, U) are appended with one atomic per wave batch; A's forward degree is the
-//     wave's edge count.
+// query_kernel — one wavefront per query read A (grid-stride over ranks a in [a_begin, a_end));
+// A's intervals live in lanes 0..LA-1 and are read with v_readlane / ds_bpermute.
+//  1. candidate walk: A's scan ranges (kernels.hpp: iv_rng) are flattened with a wave prefix sum
+//     and walked 64 records per step, one record per lane; the next step's records (and the next
+//     read's header) are loaded while the current step is processed.  Forward records are hits,
+//     backward records hit iff end >= start_i.
+//  2. dedupe: a hit on read B > A goes into a per-wave LDS hash set (epoch-tagged): the first
+//     insertion is the one evaluation of (A, B), like the reference's seen-set (:205-208).
+//  3. gate at first sight: B's packed read record sits beside the hit record (idx_gate), so
+//     different_lengths_or_alignments is decided without a dependent gather (IEEE double ==
+//     Python int/int true division).
+//  4. match list: with every overlap threshold >= 1 (overlap > 0), a matching interval pair
+//     overlaps, so it IS one of the hits: hits whose reciprocal overlap passes are appended to a
+//     per-wave LDS list in A-major order (the walk never moves back in i).
+//  5. first-fit greedy per matched partner, one lane each, straight from the list in the
+//     reference's order (rows i of A ascending, lowest unused j of B) — no row of B is read.
+//  6. edges (A, B, I, U) are staged in LDS and flushed 64 at a time (one global atomic per 64).
+// Pairs that need B's rows — thresholds < 1 (overlap <= 0: matches need not overlap), an
+// aln_size == 0 interval (exact ZeroDivisionError replay), a full match list, or more distinct
+// partners than the hash holds (witness rule) — are appended to a deferred list for
+// deferred_kernel, one lane per pair, which gathers A's and B's intervals.
 #include "fslr_hip.h"
 #include "kernels.hpp"
 
@@ -31,18 +31,22 @@ namespace {
 
 constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = kWave * kWavesPerBlock;
-constexpr int kQueueCap = 2 * kWave;
+constexpr int kStageCap = kWave;          // LDS staging of edges / deferred entries (flush before overflow)
 constexpr int kHashBits = 9;
 constexpr int kHashSize = 1 << kHashBits;
 constexpr int kHashLimit = 320;           // insert while distinct partners < limit (load <= 75 %)
-constexpr int kMatchCap = 256;            // match-list entries per query read
+constexpr int kMatchCap = 192;            // match-list entries per query read
 constexpr unsigned kEpochShift = 25;      // key = epoch << 25 | B  (B < FSLR_MAX_READS = 2^25)
 constexpr unsigned kEpochMax = 127;
+constexpr unsigned kBMask = 0x1FFFFFFu;
 // per-partner state (one word per hash slot)
 constexpr unsigned kStLenOk = 1u;         // passed different_lengths_or_alignments
-constexpr unsigned kStHaz = 2u;           // holds an aln_size == 0 interval: exact replay
+constexpr unsigned kStDefer = 2u;         // evaluated by deferred_kernel
 constexpr unsigned kStMatch = 4u;         // has at least one matching interval pair
-constexpr unsigned kStSpill = 8u;         // a match did not fit the match list: gather evaluation
+constexpr unsigned kStSpill = 8u;         // a match did not fit the match list
+// deferred entries: a << 39 | B << 14 | ic << 8 | jc << 2 | kind
+constexpr unsigned kDefPair = 0u;         // unique lenOK pair: gather evaluation (replay if aln_size==0)
+constexpr unsigned kDefWitness = 1u;      // candidate past the hash limit: witness rule, then as above
 
 __device__ __forceinline__ int lane_id() { return static_cast<int>(__lane_id()); }
 
@@ -62,12 +66,9 @@ __device__ __forceinline__ void wave_lds_sync() {
 // interval accepts overlap o (fslr_hip.h: thr >= 0 ? o >= thr : o <= ~thr)
 __device__ __forceinline__ bool thr_ok(int o, int t) { return t >= 0 ? o >= t : o <= ~t; }
 
-// calculate_overlap(i1, i2) >= overlap (cluster.py:133-136), same chromosome already checked.
-template <int kThrMode>
-__device__ __forceinline__ bool iv_match(int sa, int ea, int ta, int sb, int eb, int tb) {
-  const int o_raw = min(ea, eb) - max(sa, sb);
-  if (kThrMode == 0) return o_raw >= max(ta, tb);   // every threshold >= 1: o_raw < 0 never passes
-  const int o = max(o_raw, 0);
+// calculate_overlap(i1, i2) >= overlap (cluster.py:133-136), same chromosome already checked
+__device__ __forceinline__ bool iv_match_general(int sa, int ea, int ta, int sb, int eb, int tb) {
+  const int o = max(min(ea, eb) - max(sa, sb), 0);
   return thr_ok(o, ta) && thr_ok(o, tb);
 }
 
@@ -83,70 +84,134 @@ __device__ __forceinline__ bool lengths_pass(int q1, int q2, int n1, int n2, dou
   return static_cast<double>(mn) / static_cast<double>(mx) >= ncut;
 }
 
+__device__ __forceinline__ void raise_zd(int* err, bool zd, int a, int b) {
+  if (zd && atomicCAS(err, 0, FSLR_ERR_ZERO_DIVISION) == 0) {
+    err[1] = a;
+    err[2] = b;
+  }
+}
+
+// Wave-level edge staging in LDS (64-edge flushes).  `ES` holds a << 39 | B << 14 | I << 7 | U.
+struct EdgeStage {
+  unsigned long long* ES;
+  int n;
+  __device__ void flush(const QueryArgs& g, int nb, int lane) {
+    wave_lds_sync();
+    const bool act = lane < nb;
+    const unsigned long long e = act ? ES[lane] : 0ull;
+    const int rem = n - nb;
+    const unsigned long long mv = lane < rem ? ES[nb + lane] : 0ull;
+    wave_lds_sync();
+    if (lane < rem) ES[lane] = mv;
+    n = rem;
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(&g.counters[kEdgeCount], static_cast<unsigned long long>(nb));
+    base = __shfl(base, 0);
+    const long long k = static_cast<long long>(base) + lane;
+    if (act && k < g.edge_cap) {
+      g.edges[k] = make_int2(static_cast<int>(e >> 39), static_cast<int>((e >> 14) & kBMask));
+      g.edge_iu[k] = static_cast<unsigned short>(((e >> 7) & 127u) | ((e & 127u) << 8));
+    }
+  }
+  // stage the lanes' edges; returns the number staged
+  __device__ int put(const QueryArgs& g, bool edge, int a, int B, int I, int U, int lane) {
+    const unsigned long long em = __ballot(edge);
+    const int ne = __popcll(em);
+    if (ne) {
+      if (n + ne > kStageCap) flush(g, n, lane);
+      if (edge)
+        ES[n + mbcnt(em)] = (static_cast<unsigned long long>(a) << 39) | (static_cast<unsigned long long>(B) << 14) |
+                            (static_cast<unsigned long long>(I) << 7) | static_cast<unsigned long long>(U);
+      n += ne;
+    }
+    return ne;
+  }
+};
+
+// Deferred-list appends, staged in LDS like the edges.
+struct DeferStage {
+  unsigned long long* DQ;
+  int n;
+  __device__ void flush(const QueryArgs& g, int nb, int lane) {
+    wave_lds_sync();
+    const bool act = lane < nb;
+    const unsigned long long e = act ? DQ[lane] : 0ull;
+    const int rem = n - nb;
+    const unsigned long long mv = lane < rem ? DQ[nb + lane] : 0ull;
+    wave_lds_sync();
+    if (lane < rem) DQ[lane] = mv;
+    n = rem;
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(&g.counters[kDeferCount], static_cast<unsigned long long>(nb));
+    base = __shfl(base, 0);
+    const long long k = static_cast<long long>(base) + lane;
+    if (act && k < g.defer_cap) g.defer[k] = e;
+  }
+  __device__ void put(const QueryArgs& g, bool p, int a, int B, int ic, int jc, unsigned kind, int lane) {
+    const unsigned long long m = __ballot(p);
+    if (!m) return;
+    const int np = __popcll(m);
+    if (n + np > kStageCap) flush(g, n, lane);
+    if (p)
+      DQ[n + mbcnt(m)] = (static_cast<unsigned long long>(a) << 39) | (static_cast<unsigned long long>(B) << 14) |
+                         (static_cast<unsigned long long>(ic) << 8) | (static_cast<unsigned long long>(jc) << 2) |
+                         kind;
+    n += np;
+  }
+};
+
 template <int kThrMode>
 __global__ __launch_bounds__(kBlock) void query_kernel(QueryArgs g) {
   __shared__ unsigned hash_all[kWavesPerBlock][kHashSize];
   __shared__ unsigned state_all[kWavesPerBlock][kHashSize];
   __shared__ unsigned ml_all[kWavesPerBlock][kMatchCap];
-  __shared__ unsigned long long eq_all[kWavesPerBlock][kQueueCap];
   __shared__ unsigned short mp_all[kWavesPerBlock][kHashLimit + kWave];
-  __shared__ unsigned long long es_all[kWavesPerBlock][kQueueCap];
+  __shared__ unsigned long long es_all[kWavesPerBlock][kStageCap];
+  __shared__ unsigned long long dq_all[kWavesPerBlock][kStageCap];
   const int lane = lane_id();
   const int wv = threadIdx.x >> 6;
   unsigned* H = hash_all[wv];
   unsigned* ST = state_all[wv];
   unsigned* ML = ml_all[wv];
   unsigned short* MP = mp_all[wv];     // partners (hash slots) with at least one match, first-match order
-  unsigned long long* ES = es_all[wv]; // staged edges: a << 39 | B << 14 | I << 7 | U
-  int esn = 0;
-  // edge iff U <= umax[I-1] (cluster.py:218-219 folded on the host); lane l holds umax[l]
-  const int umax_v = g.umax[lane];
-  // flush nb staged edges with one atomic (a single global counter per edge would serialise)
-  auto flush_edges = [&](int nb) {
-    wave_lds_sync();
-    const bool act = lane < nb;
-    const unsigned long long e = act ? ES[lane] : 0ull;
-    const int rem = esn - nb;
-    const unsigned long long mv = lane < rem ? ES[nb + lane] : 0ull;
-    wave_lds_sync();
-    if (lane < rem) ES[lane] = mv;
-    esn = rem;
-    unsigned long long base = 0;
-    if (lane == 0) base = atomicAdd(&g.counters[kEdgeCount], static_cast<unsigned long long>(nb));
-    base = __shfl(base, 0);
-    const long long k = static_cast<long long>(base) + lane;
-    if (act && k < g.edge_cap) {
-      g.edges[k] = make_int2(static_cast<int>(e >> 39), static_cast<int>((e >> 14) & 0x1FFFFFFull));
-      g.edge_iu[k] = static_cast<unsigned short>(((e >> 7) & 127u) | ((e & 127u) << 8));
-    }
-  };
-  unsigned long long* EQ = eq_all[wv];
+  EdgeStage es{es_all[wv], 0};
+  DeferStage ds{dq_all[wv], 0};
   for (int k = lane; k < kHashSize; k += kWave) H[k] = 0u;
   unsigned epoch = 0;
+  // edge iff U <= umax[I-1] (cluster.py:218-219 folded on the host); lane l holds umax[l]
+  const int umax_v = g.umax[lane];
   const int nwaves = gridDim.x * kWavesPerBlock;
-  unsigned long long w_eval = 0, w_jacc = 0, w_cand = 0, w_over = 0, w_gather = 0, w_ml = 0, w_mp = 0;
+  unsigned long long w_eval = 0, w_jacc = 0, w_cand = 0, w_over = 0, w_ml = 0, w_mp = 0;
   unsigned long long l_bytes = 0;       // per lane: algorithmic bytes of evaluated pairs
   int w_maxfwd = 0;
 
-  for (int a = g.a_begin + blockIdx.x * kWavesPerBlock + wv; a < g.a_end; a += nwaves) {
+  int a = g.a_begin + blockIdx.x * kWavesPerBlock + wv;
+  int4 am = make_int4(0, 0, 0, 0);
+  if (a < g.a_end) am = g.rmeta[a];
+  int4 my = make_int4(-1, 0, 0, 0), rg = make_int4(0, 0, 0, 0);
+  {
+    const int off = __builtin_amdgcn_readfirstlane(am.x), len = __builtin_amdgcn_readfirstlane(am.y) & 0xffff;
+    if (a < g.a_end && lane < len) {
+      my = g.iv[off + lane];
+      rg = g.iv_rng[off + lane];
+    }
+  }
+
+  for (; a < g.a_end; a += nwaves) {
     if (++epoch > kEpochMax) {
       wave_lds_sync();
       for (int k = lane; k < kHashSize; k += kWave) H[k] = 0u;
       epoch = 1;
     }
-    const int4 am = g.rmeta[a];
-    const int offA = __builtin_amdgcn_readfirstlane(am.x);
     const int amy = __builtin_amdgcn_readfirstlane(am.y);
     const int LA = amy & 0xffff;
     const bool hazA = (static_cast<unsigned>(amy) >> 16) & 1u;
     const int q1 = __builtin_amdgcn_readfirstlane(am.z), n1 = __builtin_amdgcn_readfirstlane(am.w);
-    int4 my = make_int4(-1, 0, 0, 0);
-    int4 rg = make_int4(0, 0, 0, 0);
-    if (lane < LA) {
-      my = g.iv[offA + lane];
-      rg = g.iv_rng[offA + lane];
-    }
-    const unsigned long long fullA = LA == 64 ? ~0ull : ((1ull << LA) - 1ull);
+    // prefetch the next read's header
+    const int a_next = a + nwaves;
+    int4 am_next = make_int4(0, 0, 0, 0);
+    if (a_next < g.a_end) am_next = g.rmeta[a_next];
+
     const int cnt = rg.y + rg.w;
     int pre = cnt;
 #pragma unroll
@@ -156,173 +221,56 @@ __global__ __launch_bounds__(kBlock) void query_kernel(QueryArgs g) {
     }
     const int ex = pre - cnt;
     const int R = rdl(pre, kWave - 1);
-    int en = 0, uniq = 0, mln = 0, mpn = 0, fwdA = 0;
+    int uniq = 0, mln = 0, mpn = 0, fwdA = 0;
 
-    auto raise_zd = [&](bool zd, int B) {
-      if (zd && atomicCAS(g.err, 0, FSLR_ERR_ZERO_DIVISION) == 0) {
-        g.err[1] = a;
-        g.err[2] = B;
-      }
-    };
-
-    auto emit = [&](bool edge, int B, int I, int U) {
-      const unsigned long long em = __ballot(edge);
-      const int ne = __popcll(em);
-      if (ne) {
-        if (edge)
-          ES[esn + mbcnt(em)] = (static_cast<unsigned long long>(a) << 39) |
-                                (static_cast<unsigned long long>(B) << 14) |
-                                (static_cast<unsigned long long>(I) << 7) | static_cast<unsigned long long>(U);
-        esn += ne;
-        fwdA += ne;
-        if (esn >= kWave) flush_edges(kWave);
-      }
-    };
-
-    // U <= umax[I-1]  (I in 1..64 → lane I-1)
-    auto passes = [&](int I, int U) { return U <= __shfl(umax_v, max(I, 1) - 1); };
-
-    // exact replay of the reference's i-major loop (cluster.py:152-161) for pairs holding an
-    // aln_size == 0 interval: ZeroDivisionError exactly when the reference divides by it
-    auto replay = [&](int offB, int LB, bool* zd) {
-      unsigned long long used = 0ull;
-      int I = 0;
-      for (int i = 0; i < LA && !*zd; ++i) {
-        const int4 ai = g.iv[offA + i];
-        for (int j = 0; j < LB; ++j) {
-          if ((used >> j) & 1ull) continue;
-          const int4 b = g.iv[offB + j];
-          if (b.x != ai.x) continue;
-          if (ai.w == FSLR_THR_ZERO_ALN || b.w == FSLR_THR_ZERO_ALN) { *zd = true; break; }
-          const int o = max(min(ai.z, b.z) - max(ai.y, b.y), 0);
-          if (thr_ok(o, ai.w) && thr_ok(o, b.w)) { used |= 1ull << j; ++I; break; }
-        }
-      }
-      return I;
-    };
-
-    // gather evaluation: B's intervals are read four rows per load group; B-major first-fit
-    // greedy on 64-bit match masks over A (symmetric to the reference's A-major count)
-    auto eval_batch = [&](int nb) {
-      wave_lds_sync();
-      const bool act = lane < nb;
-      const unsigned long long e = act ? EQ[lane] : 0ull;
-      const int rem = en - nb;
-      const unsigned long long mv = lane < rem ? EQ[nb + lane] : 0ull;
-      wave_lds_sync();
-      if (lane < rem) EQ[lane] = mv;
-      en = rem;
-      w_gather += nb;
-      const unsigned lo = static_cast<unsigned>(e);
-      const int B = static_cast<int>(lo & 0x1FFFFFFu);
-      const int LB = act ? static_cast<int>((lo >> 25) & 63u) + 1 : 0;
-      const bool haz = (lo >> 31) & 1u;
-      const int offB = static_cast<int>(e >> 32);
-      unsigned long long freeA = fullA;
-      int I = 0;
-      bool zd = false;
-      if (!haz) {
-        for (int j0 = 0; j0 < LB; j0 += 4) {
-          int4 b[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) b[u] = (j0 + u < LB) ? g.iv[offB + j0 + u] : make_int4(-1, 0, -1, 0);
-          unsigned long long M[4] = {0ull, 0ull, 0ull, 0ull};
-          for (int i = 0; i < LA; ++i) {
-            const int ci = rdl(my.x, i), si = rdl(my.y, i), ei = rdl(my.z, i), ti = rdl(my.w, i);
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const bool mt = b[u].x == ci && iv_match<kThrMode>(si, ei, ti, b[u].y, b[u].z, b[u].w);
-              M[u] |= static_cast<unsigned long long>(mt) << i;
-            }
-          }
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const unsigned long long m = M[u] & freeA;
-            if (m) { freeA ^= m & (~m + 1ull); ++I; }
-          }
-        }
-      } else if (act) {
-        I = replay(offB, LB, &zd);
-      }
-      raise_zd(act && zd, B);
-      const int U = LA + LB - I;
-      const bool edge = passes(I, U) && act && !zd && I > 0;
-      emit(edge, B, I, U);
-    };
-
-    auto push_eval = [&](bool push, int B, int offB, int LB, bool haz) {
-      const unsigned long long pm = __ballot(push);
-      if (push) {
-        const unsigned tag = static_cast<unsigned>(B) | (static_cast<unsigned>(LB - 1) << 25) |
-                             (static_cast<unsigned>(haz) << 31);
-        EQ[en + mbcnt(pm)] = (static_cast<unsigned long long>(static_cast<unsigned>(offB)) << 32) | tag;
-      }
-      en += __popcll(pm);
-      if (en >= kWave) eval_batch(kWave);
-    };
-
-    // partners past the hash limit: witness rule (first overlapping pair in B-major order), in place
-    auto witness_batch = [&](bool act, int B, int ic, int jc, int4 bm) {
-      const int offB = bm.x;
-      const int LB = act ? (bm.y & 0xffff) : 0;
-      const bool haz = hazA || ((bm.y >> 16) & 1);
-      bool zd = false;
-      const bool lenok = act && lengths_pass(q1, bm.z, n1, bm.w, g.qlen_cut, g.nal_cut, &zd);
-      const bool full = lenok && !haz && g.mode == 0;
-      unsigned long long freeA = fullA;
-      int I = 0;
-      int state = act ? 0 : 2;   // 0 witness unknown, 1 canonical, 2 duplicate / idle
-      for (int j = 0; j < LB; ++j) {
-        const int4 b = g.iv[offB + j];
-        unsigned long long O = 0ull, M = 0ull;
-        for (int i = 0; i < LA; ++i) {
-          const int ci = rdl(my.x, i), si = rdl(my.y, i), ei = rdl(my.z, i), ti = rdl(my.w, i);
-          const bool same = b.x == ci;
-          O |= static_cast<unsigned long long>(same && min(b.z, ei) >= max(b.y, si)) << i;
-          M |= static_cast<unsigned long long>(same && iv_match<kThrMode>(si, ei, ti, b.y, b.z, b.w)) << i;
-        }
-        if (state == 0 && O != 0ull) state = (j == jc && __builtin_ctzll(O) == ic) ? 1 : 2;
-        if (state == 2 || (state == 1 && !full)) break;
-        const unsigned long long m = M & freeA;
-        if (m) { freeA ^= m & (~m + 1ull); ++I; }
-      }
-      const bool canon = state == 1;
-      if (canon && lenok && haz && g.mode == 0) I = replay(offB, LB, &zd);
-      raise_zd(canon && zd, B);
-      const unsigned long long cm = __ballot(canon);
-      w_eval += __popcll(cm);
-      w_gather += __popcll(cm);
-      w_jacc += __popcll(__ballot(canon && lenok));
-      if (canon) l_bytes += 16ull * static_cast<unsigned long long>(LA + LB) + 32ull;
-      const int U = LA + LB - I;
-      const bool edge = passes(I, U) && canon && lenok && !zd && g.mode == 0 && I > 0;
-      emit(edge, B, I, U);
-    };
-
-    // ---- 1. candidate walk over A's flattened scan ranges -------------------------------
-    for (int base = 0; base < R; base += kWave) {
+    // record r of A's walk → (interval mi, sorted position p, forward?)
+    auto map_record = [&](int base, int& mi, int& p, bool& fwd) {
       const int r = base + lane;
-      const bool valid = r < R;
       const int i0 = __popcll(__ballot(lane < LA && pre <= base));
-      int mi = i0;
+      mi = i0;
       for (int k = i0 + 1; k < LA; ++k) {
         const int exk = rdl(ex, k);
         if (exk >= base + kWave) break;
         if (r >= exk) mi = k;
       }
       const int q_i = __shfl(rg.x, mi), nf_i = __shfl(rg.y, mi), bb_i = __shfl(rg.z, mi);
-      const int ex_i = __shfl(ex, mi);
+      const int loc = r - __shfl(ex, mi);
+      fwd = loc < nf_i;
+      p = fwd ? q_i + 1 + loc : bb_i + (loc - nf_i);
+    };
+
+    int mi_c = 0, p_c = 0;
+    bool fwd_c = false;
+    int4 rec_c = make_int4(0, -1, 0, 0);
+    int2 gt_c = make_int2(0, 0);
+    if (R > 0) {
+      map_record(0, mi_c, p_c, fwd_c);
+      if (lane < R) {
+        rec_c = g.idx4[p_c];
+        gt_c = g.idx_gate[p_c];
+      }
+    }
+    for (int base = 0; base < R; base += kWave) {
+      const bool valid = base + lane < R;
+      const int mi = mi_c;
+      const bool fwd = fwd_c;
+      const int4 rec = rec_c;
+      const int2 gt = gt_c;
+      // issue the next step's loads before working on this one
+      if (base + kWave < R) {
+        map_record(base + kWave, mi_c, p_c, fwd_c);
+        rec_c = make_int4(0, -1, 0, 0);
+        if (base + kWave + lane < R) {
+          rec_c = g.idx4[p_c];
+          gt_c = g.idx_gate[p_c];
+        }
+      }
       const int s_i = __shfl(my.y, mi), e_i = __shfl(my.z, mi), t_i = __shfl(my.w, mi);
-      const int loc = r - ex_i;
-      const bool fwd = loc < nf_i;
-      const int p = fwd ? q_i + 1 + loc : bb_i + (loc - nf_i);
-      int4 rec = make_int4(0, -1, 0, 0);
-      if (valid) rec = g.idx4[p];
       const bool hit = valid && (fwd || rec.y >= s_i);
       w_cand += __popcll(__ballot(hit));
       const int B = rec.w >> 6;
       const bool cand = hit && B > a;
-      // ---- 2. dedupe: per-wave LDS hash set of partners (the reference's seen-set) -------
+      // ---- dedupe: per-wave LDS hash set of partners (the reference's seen-set) ----------
       const bool ins_mode = uniq < kHashLimit;
       bool isnew = false, over = false;
       unsigned h = (static_cast<unsigned>(B) * 2654435761u) >> (32 - kHashBits);
@@ -344,25 +292,26 @@ __global__ __launch_bounds__(kBlock) void query_kernel(QueryArgs g) {
       const unsigned long long nm = __ballot(isnew);
       uniq += __popcll(nm);
       if (g.mode == 1) continue;
-      // ---- 3. gate at first sight: B's read record sits beside its interval record -------
-      int4 bm = make_int4(0, 0, 0, 0);
-      if (isnew || over) bm = g.idx_meta[p];
-      const int LB = bm.y & 0xffff;
-      const bool haz = hazA || ((bm.y >> 16) & 1);
+      // ---- gate at first sight (idx_gate: {qlen2, nal | LB << 24 | haz << 31}) -------------
+      const int LB = (gt.y >> 24) & 127;
+      const bool haz = hazA || (static_cast<unsigned>(gt.y) >> 31);
       bool zd = false;
-      const bool lenok = isnew && lengths_pass(q1, bm.z, n1, bm.w, g.qlen_cut, g.nal_cut, &zd);
-      raise_zd(isnew && zd, B);
+      const bool lenok = isnew && lengths_pass(q1, gt.x, n1, gt.y & 0xFFFFFF, g.qlen_cut, g.nal_cut, &zd);
+      raise_zd(g.err, isnew && zd, a, B);
+      const bool defer = lenok && (kThrMode == 1 || haz);
       if (isnew) {
-        ST[h] = (lenok ? kStLenOk : 0u) | (haz ? kStHaz : 0u) | (static_cast<unsigned>(LB) << 8);
+        ST[h] = (lenok ? kStLenOk : 0u) | (defer ? kStDefer : 0u) | (static_cast<unsigned>(LB) << 8);
         l_bytes += 16ull * static_cast<unsigned long long>(LA + LB) + 32ull;
       }
       w_eval += __popcll(nm);
       w_jacc += __popcll(__ballot(lenok));
+      if (g.mode == 0) {
+        ds.put(g, defer, a, B, 0, 0, kDefPair, lane);
+        ds.put(g, over, a, B, mi, rec.w & 63, kDefWitness, lane);
+      }
+      w_over += __popcll(__ballot(over));
       wave_lds_sync();
-      // pairs evaluated by gathering B's intervals: every pair under general thresholds,
-      // aln_size == 0 replays
-      push_eval(lenok && g.mode == 0 && (kThrMode == 1 || haz), B, bm.x, LB, haz);
-      // ---- 4. matching interval pairs → match list (A-major order: i never decreases) -----
+      // ---- matching interval pairs → match list (A-major: i never decreases) -----------------
       if (kThrMode == 0) {
         const bool mt = cand && !over && (min(e_i, rec.y) - max(s_i, rec.x) >= max(t_i, rec.z));
         const unsigned long long mm = __ballot(mt);
@@ -386,13 +335,18 @@ __global__ __launch_bounds__(kBlock) void query_kernel(QueryArgs g) {
           mln = min(mln + __popcll(mm), kMatchCap);
         }
       }
-      const unsigned long long om = __ballot(over);
-      if (om) {
-        w_over += __popcll(om);
-        witness_batch(over, B, mi, rec.w & 63, bm);
+    }
+    // prefetch the next read's intervals while this read's greedy runs from LDS
+    int4 my_next = make_int4(-1, 0, 0, 0), rg_next = make_int4(0, 0, 0, 0);
+    {
+      const int off = __builtin_amdgcn_readfirstlane(am_next.x);
+      const int len = __builtin_amdgcn_readfirstlane(am_next.y) & 0xffff;
+      if (a_next < g.a_end && lane < len) {
+        my_next = g.iv[off + lane];
+        rg_next = g.iv_rng[off + lane];
       }
     }
-    // ---- 5. first-fit greedy from the match list, one lane per matched partner ------------
+    // ---- first-fit greedy from the match list, one lane per matched partner ----------------
     if (kThrMode == 0 && g.mode == 0 && mpn > 0) {
       wave_lds_sync();
       for (int k0 = 0; k0 < mpn; k0 += kWave) {
@@ -400,10 +354,10 @@ __global__ __launch_bounds__(kBlock) void query_kernel(QueryArgs g) {
         const int h = act ? static_cast<int>(MP[k0 + lane]) : 0;
         const unsigned key = H[h];
         const unsigned st = act ? ST[h] : 0u;
-        const bool hasm = act && (st & kStLenOk) && !(st & kStHaz);
+        const bool hasm = act && (st & kStLenOk) && !(st & kStDefer);
         const bool spill = hasm && (st & kStSpill);
         const bool need = hasm && !spill;
-        const int B = static_cast<int>(key & 0x1FFFFFFu);
+        const int B = static_cast<int>(key & kBMask);
         const int LB = static_cast<int>((st >> 8) & 0xffu);
         int I = 0;
         if (__ballot(need)) {
@@ -428,20 +382,21 @@ __global__ __launch_bounds__(kBlock) void query_kernel(QueryArgs g) {
           if (m) { used |= m & (~m + 1ull); ++I; }
         }
         const int U = LA + LB - I;
-        const bool edge = passes(I, U) && need && I > 0;
-        emit(edge, B, I, U);
-        int4 bm = make_int4(0, 0, 0, 0);
-        if (spill) bm = g.rmeta[B];
-        push_eval(spill, B, bm.x, LB, false);
+        const bool pass = U <= __shfl(umax_v, max(I, 1) - 1);
+        fwdA += es.put(g, pass && need && I > 0, a, B, I, U, lane);
+        ds.put(g, spill, a, B, 0, 0, kDefPair, lane);
       }
     }
-    while (en > 0) eval_batch(min(en, kWave));
     w_ml += mln;
     w_mp += mpn;
     if (lane == 0) g.fwd[a] = fwdA;
     w_maxfwd = max(w_maxfwd, fwdA);
+    am = am_next;
+    my = my_next;
+    rg = rg_next;
   }
-  if (esn > 0) flush_edges(esn);
+  if (es.n > 0) es.flush(g, es.n, lane);
+  if (ds.n > 0) ds.flush(g, ds.n, lane);
   for (int o = 32; o > 0; o >>= 1) l_bytes += __shfl_xor(l_bytes, o);
   if (lane == 0) {
     if (l_bytes) atomicAdd(&g.counters[kAlgoBytes], l_bytes);
@@ -449,14 +404,119 @@ __global__ __launch_bounds__(kBlock) void query_kernel(QueryArgs g) {
     if (w_jacc) atomicAdd(&g.counters[kJacc], w_jacc);
     if (w_cand) atomicAdd(&g.counters[kCand], w_cand);
     if (w_over) atomicAdd(&g.counters[kOverflow], w_over);
-    if (w_gather) atomicAdd(&g.counters[kGather], w_gather);
     if (w_ml) atomicAdd(&g.counters[kMatchEntries], w_ml);
     if (w_mp) atomicAdd(&g.counters[kMatchedPairs], w_mp);
     if (w_maxfwd) atomicMax(g.err + 3, w_maxfwd);
   }
 }
 
-}  // namespace
+// ------------------------------------------------------------------------------------------
+// deferred_kernel: one lane per deferred entry; gathers A's and B's intervals.
+//   kDefPair     lenOK pair: B-major first-fit greedy on 64-bit match masks over A (symmetric
+//                to the reference's A-major count), or the exact replay of cluster.py:152-161
+//                when an aln_size == 0 interval is involved (ZeroDivisionError where the
+//                reference raises it).
+//   kDefWitness  candidate (A, B, ic, jc) of a read past the hash limit: evaluated only if
+//                (jc, ic) is the first overlapping interval pair in B-major order, which makes
+//                exactly one candidate of each such pair the evaluator; then gate + as above.
+// Forward degrees are added atomically on top of query_kernel's counts.
+__global__ __launch_bounds__(256) void deferred_kernel(QueryArgs g) {
+  __shared__ unsigned long long es_all[4][kStageCap];
+  const int lane = lane_id();
+  EdgeStage es{es_all[threadIdx.x >> 6], 0};
+  const long long n = min(static_cast<long long>(g.counters[kDeferCount]), g.defer_cap);
+  const int umax_v = g.umax[lane];
+  unsigned long long w_eval = 0, w_jacc = 0, w_gather = 0;
+  unsigned long long l_bytes = 0;
+  const long long stride = static_cast<long long>(gridDim.x) * blockDim.x;
+  // whole waves iterate together (ballots below need uniform trip counts)
+  const long long n_round = (n + kWave - 1) / kWave * kWave;
+  for (long long t = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; t - lane < n_round;
+       t += stride) {
+    const bool act = t < n;
+    const unsigned long long e = act ? g.defer[t] : 0ull;
+    const int a = static_cast<int>(e >> 39);
+    const int B = static_cast<int>((e >> 14) & kBMask);
+    const int ic = static_cast<int>((e >> 8) & 63u), jc = static_cast<int>((e >> 2) & 63u);
+    const unsigned kind = static_cast<unsigned>(e & 3u);
+    int4 am = make_int4(0, 0, 0, 0), bm = make_int4(0, 0, 0, 0);
+    if (act) {
+      am = g.rmeta[a];
+      bm = g.rmeta[B];
+    }
+    const int offA = am.x, LA = act ? (am.y & 0xffff) : 0;
+    const int offB = bm.x, LB = act ? (bm.y & 0xffff) : 0;
+    const bool haz = ((am.y | bm.y) >> 16) & 1;
+    bool zd = false;
+    bool lenok = act && kind == kDefPair;
+    bool canon = lenok;
+    if (act && kind == kDefWitness) {
+      // witness: first overlapping (j, i) in B-major order
+      int wj = -1, wi = -1;
+      for (int j = 0; j < LB && wj < 0; ++j) {
+        const int4 b = g.iv[offB + j];
+        for (int i = 0; i < LA; ++i) {
+          const int4 ai = g.iv[offA + i];
+          if (ai.x == b.x && min(ai.z, b.z) >= max(ai.y, b.y)) { wj = j; wi = i; break; }
+        }
+      }
+      canon = wj == jc && wi == ic;
+      if (canon) {
+        lenok = lengths_pass(am.z, bm.z, am.w, bm.w, g.qlen_cut, g.nal_cut, &zd);
+        raise_zd(g.err, zd, a, B);
+        l_bytes += 16ull * static_cast<unsigned long long>(LA + LB) + 32ull;
+      }
+    }
+    w_eval += __popcll(__ballot(act && kind == kDefWitness && canon));
+    w_jacc += __popcll(__ballot(act && kind == kDefWitness && canon && lenok));
+    const bool work = canon && lenok && !zd && g.mode == 0;
+    w_gather += __popcll(__ballot(work));
+    int I = 0;
+    if (work && haz) {
+      unsigned long long used = 0ull;
+      for (int i = 0; i < LA && !zd; ++i) {
+        const int4 ai = g.iv[offA + i];
+        for (int j = 0; j < LB; ++j) {
+          if ((used >> j) & 1ull) continue;
+          const int4 b = g.iv[offB + j];
+          if (b.x != ai.x) continue;
+          if (ai.w == FSLR_THR_ZERO_ALN || b.w == FSLR_THR_ZERO_ALN) { zd = true; break; }
+          if (iv_match_general(ai.y, ai.z, ai.w, b.y, b.z, b.w)) { used |= 1ull << j; ++I; break; }
+        }
+      }
+      raise_zd(g.err, zd, a, B);
+    } else if (work) {
+      const unsigned long long fullA = LA == 64 ? ~0ull : ((1ull << LA) - 1ull);
+      unsigned long long freeA = fullA;
+      for (int j = 0; j < LB; ++j) {
+        const int4 b = g.iv[offB + j];
+        unsigned long long M = 0ull;
+        for (int i = 0; i < LA; ++i) {
+          const int4 ai = g.iv[offA + i];
+          M |= static_cast<unsigned long long>(ai.x == b.x && iv_match_general(ai.y, ai.z, ai.w, b.y, b.z, b.w)) << i;
+        }
+        const unsigned long long m = M & freeA;
+        if (m) { freeA ^= m & (~m + 1ull); ++I; }
+      }
+    }
+    const int U = LA + LB - I;
+    const bool pass = U <= __shfl(umax_v, max(I, 1) - 1);
+    const bool edge = pass && work && !zd && I > 0;
+    es.put(g, edge, a, B, I, U, lane);
+    if (edge) {
+      const int old = atomicAdd(&g.fwd[a], 1);
+      atomicMax(g.err + 3, old + 1);
+    }
+  }
+  if (es.n > 0) es.flush(g, es.n, lane);
+  for (int o = 32; o > 0; o >>= 1) l_bytes += __shfl_xor(l_bytes, o);
+  if (lane == 0) {
+    if (l_bytes) atomicAdd(&g.counters[kAlgoBytes], l_bytes);
+    if (w_eval) atomicAdd(&g.counters[kEval], w_eval);
+    if (w_jacc) atomicAdd(&g.counters[kJacc], w_jacc);
+    if (w_gather) atomicAdd(&g.counters[kGather], w_gather);
+  }
+}
 
 // resident grid: waves walk the read ranks grid-stride, so launch exactly what fits on the chip
 template <int kThrMode>
@@ -472,17 +532,22 @@ int resident_blocks() {
   return cached;
 }
 
+}  // namespace
+
 hipError_t launch_query(const QueryArgs& a, int thr_mode, hipStream_t s) {
   const long long nq = static_cast<long long>(a.a_end) - a.a_begin;
-  if (nq <= 0) return hipSuccess;
-  const long long want = (nq + kWavesPerBlock - 1) / kWavesPerBlock;
-  if (thr_mode == 0) {
-    const int cap = resident_blocks<0>();
-    query_kernel<0><<<static_cast<int>(want < cap ? want : cap), kBlock, 0, s>>>(a);
-  } else {
-    const int cap = resident_blocks<1>();
-    query_kernel<1><<<static_cast<int>(want < cap ? want : cap), kBlock, 0, s>>>(a);
+  if (nq > 0) {
+    const long long want = (nq + kWavesPerBlock - 1) / kWavesPerBlock;
+    if (thr_mode == 0) {
+      const int cap = resident_blocks<0>();
+      query_kernel<0><<<static_cast<int>(want < cap ? want : cap), kBlock, 0, s>>>(a);
+    } else {
+      const int cap = resident_blocks<1>();
+      query_kernel<1><<<static_cast<int>(want < cap ? want : cap), kBlock, 0, s>>>(a);
+    }
   }
+  // the deferred list's length is only known on the device: a fixed grid walks it
+  deferred_kernel<<<1024, 256, 0, s>>>(a);
   return hipGetLastError();
 }
 

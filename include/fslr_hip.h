@@ -72,11 +72,14 @@ typedef struct {
     int32_t n_chroms;              /* iv_chrom values lie in [0, n_chroms) */
     const int32_t *read_off;       /* [n_reads+1] */
     const int32_t *read_qlen2;     /* [n_reads]  keep_fillings qlen2 (cluster.py:26-29) */
-    const int32_t *read_nal;       /* [n_reads]  n_alignments */
+    const int32_t *read_nal;       /* [n_reads]  n_alignments, in [0, 2^24) */
     const int32_t *iv_chrom;       /* [n_intervals] */
     const int32_t *iv_start;       /* min(rstart, rend)  (cluster.py:111) */
     const int32_t *iv_end;         /* max(rstart, rend)  (cluster.py:112) */
     const int32_t *iv_thr;         /* folded overlap threshold, see above */
+    const int32_t *iv_data_pos;    /* optional (NULL): position of each interval in the start-sorted
+                                      `data` list (cluster.py:114).  With it the index build is one
+                                      stable pass on chromosome instead of a (chrom, start) sort. */
 } fslr_reads;
 
 typedef struct {
@@ -101,6 +104,9 @@ typedef struct {
                                       aln_size==0 replay, match-list overflow) */
     int64_t match_entries;         /* matching interval pairs recorded in the per-read match lists */
     int64_t matched_pairs;         /* read pairs with at least one matching interval pair */
+    int64_t deferred;              /* entries on the deferred (gather-evaluated) list */
+    int64_t deferred_capacity;     /* its capacity; deferred > capacity ⇒ FSLR_ERR_STATE, reserve + rerun */
+    int64_t edge_capacity;         /* edge buffer capacity; n_edges > capacity ⇒ reserve + rerun */
 } fslr_query_stats;
 
 typedef struct {
@@ -126,6 +132,8 @@ int  fslr_set_reads(fslr_ctx *ctx, const fslr_reads *reads);
 int  fslr_set_thresholds(fslr_ctx *ctx, const int32_t *iv_thr);
 /* Edge buffer capacity (edges of E*); grows only. */
 int  fslr_reserve_edges(fslr_ctx *ctx, int64_t capacity);
+/* Deferred-pair list capacity (pairs evaluated by gathering intervals); grows only. */
+int  fslr_reserve_deferred(fslr_ctx *ctx, int64_t capacity);
 
 /* cluster.py:124-130 — sort intervals by (chrom, start), prefix-max of end. Async. */
 int  fslr_build_index(fslr_ctx *ctx);

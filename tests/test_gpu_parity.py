@@ -38,18 +38,17 @@ def oracle_from_csr(c):
                        np.repeat(c.read_nal, cnt), c.data_pos)
 
 
-def gpu_run(ctx, csr, overlap=0.8, cutoffs=(1, 1, 0.66, 0.66, 0.66, 0.5), qlen_diff=0.04, nal_diff=0.25):
+def gpu_run(ctx, csr, overlap=0.8, cutoffs=(1, 1, 0.66, 0.66, 0.66, 0.5), qlen_diff=0.04, nal_diff=0.25,
+            full_sort=False):
     thr = fold_overlap_threshold(csr.iv_aln, overlap)
-    ctx.set_reads(csr.read_off, csr.read_qlen2, csr.read_nal, csr.iv_chrom, csr.iv_start, csr.iv_end, thr,
-                  csr.n_chroms)
+    if full_sort:
+        ctx.set_reads(csr.read_off, csr.read_qlen2, csr.read_nal, csr.iv_chrom, csr.iv_start, csr.iv_end, thr,
+                      csr.n_chroms)
+    else:
+        ctx.load_csr(csr, thr)
     ctx.reserve_edges(max(1 << 16, 12 * csr.n_reads))
     ctx.build_index()
-    while True:
-        ctx.query(1 - qlen_diff, 1 - nal_diff, pass_table(cutoffs))
-        st = ctx.stats()
-        if st['n_edges'] <= ctx.edge_capacity:
-            break
-        ctx.reserve_edges(st['n_edges'] + 1024)
+    st = ctx.run_query(1 - qlen_diff, 1 - nal_diff, pass_table(cutoffs))
     ctx.components()
     a, b, I, U = ctx.edges(st['n_edges'])
     return dict(stats=st, labels=ctx.labels(), fwd=ctx.fwd_degree(), a=a, b=b, I=I, U=U)
@@ -224,6 +223,18 @@ def test_config3_1m_vs_oracle(ctx):
     g = gpu_run(ctx, csr)
     o = O.run_core(oracle_from_csr(csr), use_cap=False)
     compare_with_oracle(g, o, csr.n_reads)
+
+
+def test_full_sort_index_path_matches_data_order_path(ctx):
+    """Index built by the (chrom, start) radix sort == index built from the host's start order."""
+    s = synth.generate(40_000, 16, 4)
+    csr = s.interval_data().csr()
+    g1 = gpu_run(ctx, csr, full_sort=True)
+    g2 = gpu_run(ctx, csr)
+    np.testing.assert_array_equal(g1['labels'], g2['labels'])
+    np.testing.assert_array_equal(g1['fwd'], g2['fwd'])
+    assert sorted(zip(g1['a'], g1['b'], g1['I'])) == sorted(zip(g2['a'], g2['b'], g2['I']))
+    assert g1['stats']['evaluated_pairs'] == g2['stats']['evaluated_pairs']
 
 
 def test_rerun_is_deterministic(ctx):
