@@ -29,6 +29,8 @@ struct fslr_ctx {
   unsigned long long* defer = nullptr;
   int64_t defer_cap = 0;
   int* data_pos = nullptr;
+  unsigned* dchrom = nullptr;    // data order (start-sorted `data` list): chromosome
+  int4* drec = nullptr;          // data order: {start, end, thr, read << 6 | j}
   int* s_start = nullptr;
   int2* crange = nullptr;
   unsigned long long* keys = nullptr;
@@ -94,7 +96,8 @@ int ensure_capacity(fslr_ctx* c, int64_t n, int64_t ni, int n_chroms) {
   }
   if (ni > c->cap_ni) {
     if ((rc = dalloc(c, &c->iv, ni)) || (rc = dalloc(c, &c->iv_rng, ni)) || (rc = dalloc(c, &c->idx4, ni)) ||
-        (rc = dalloc(c, &c->idx_gate, ni)) || (rc = dalloc(c, &c->data_pos, ni)) || (rc = dalloc(c, &c->s_start, ni)) ||
+        (rc = dalloc(c, &c->idx_gate, ni)) || (rc = dalloc(c, &c->data_pos, ni)) ||
+        (rc = dalloc(c, &c->dchrom, ni)) || (rc = dalloc(c, &c->drec, ni)) || (rc = dalloc(c, &c->s_start, ni)) ||
         (rc = dalloc(c, &c->keys, ni)) || (rc = dalloc(c, &c->keys2, ni)) || (rc = dalloc(c, &c->vals, ni)) ||
         (rc = dalloc(c, &c->vals2, ni)) || (rc = dalloc(c, &c->endkey, ni)) || (rc = dalloc(c, &c->pmaxkey, ni)) ||
         (rc = dalloc(c, &c->thr_tmp, ni)))
@@ -165,7 +168,7 @@ void fslr_ctx_destroy(fslr_ctx* c) {
   void* bufs[] = {c->rmeta,  c->iv,     c->iv_rng,  c->idx4,    c->idx_gate, c->data_pos, c->s_start,
                   c->crange, c->keys,   c->keys2,   c->vals,    c->vals2,   c->endkey,  c->pmaxkey,
                   c->temp,   c->umax,   c->edges,   c->edge_iu, c->fwd,     c->parent,  c->counters,
-                  c->errw,   c->thr_tmp, c->defer};
+                  c->errw,   c->thr_tmp, c->defer,   c->dchrom,  c->drec};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->ev_ok)
@@ -246,8 +249,23 @@ int fslr_set_reads(fslr_ctx* c, const fslr_reads* r) {
   int rc = ensure_capacity(c, n, ni, r->n_chroms);
   if (rc) return rc;
   HIP_TRY(c, hipMemcpyAsync(c->crange, cr.data(), cr.size() * sizeof(int2), hipMemcpyHostToDevice, c->stream));
-  if (use_dp && ni)
+  std::vector<unsigned> dch;
+  std::vector<int4> drc;
+  if (use_dp && ni) {
+    // the `data` list itself (cluster.py:116-121) in its start-sorted order
+    dch.resize(static_cast<size_t>(ni));
+    drc.resize(static_cast<size_t>(ni));
+    for (int64_t i = 0; i < n; ++i)
+      for (int k = r->read_off[i]; k < r->read_off[i + 1]; ++k) {
+        const int d = r->iv_data_pos[k];
+        dch[d] = static_cast<unsigned>(r->iv_chrom[k]);
+        drc[d] = make_int4(r->iv_start[k], r->iv_end[k], r->iv_thr[k],
+                           static_cast<int>((i << 6) | (k - r->read_off[i])));
+      }
     HIP_TRY(c, hipMemcpyAsync(c->data_pos, r->iv_data_pos, ni * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->dchrom, dch.data(), ni * sizeof(unsigned), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->drec, drc.data(), ni * sizeof(int4), hipMemcpyHostToDevice, c->stream));
+  }
   c->have_data_pos = use_dp;
   c->n = n;
   c->ni = ni;
@@ -271,8 +289,8 @@ int fslr_set_thresholds(fslr_ctx* c, const int32_t* thr) {
       return fail(c, FSLR_ERR_INVALID, "FSLR_THR_ZERO_ALN must mark the same intervals as in fslr_set_reads");
   if (c->ni) {
     HIP_TRY(c, hipMemcpyAsync(c->thr_tmp, thr, c->ni * sizeof(int), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(c, launch_set_thr(c->thr_tmp, c->iv, c->iv_rng, c->index_built ? c->idx4 : nullptr,
-                              static_cast<int>(c->ni), c->stream));
+    HIP_TRY(c, launch_set_thr(c->thr_tmp, c->iv, c->iv_rng, c->index_built ? c->idx4 : nullptr, c->data_pos,
+                              c->have_data_pos ? c->drec : nullptr, static_cast<int>(c->ni), c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
   }
   c->thr_mode = thr_mode_of(thr, c->ni);
@@ -309,7 +327,8 @@ int fslr_build_index(fslr_ctx* c) {
   IndexBufs b;
   b.rmeta = c->rmeta;
   b.iv = c->iv;
-  b.data_pos = c->have_data_pos ? c->data_pos : nullptr;
+  b.dchrom = c->have_data_pos ? c->dchrom : nullptr;
+  b.drec = c->have_data_pos ? c->drec : nullptr;
   b.keys = c->keys;
   b.keys2 = c->keys2;
   b.vals = c->vals;

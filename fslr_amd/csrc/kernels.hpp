@@ -29,7 +29,8 @@ enum Counter { kEdgeCount = 0, kEval = 1, kJacc = 2, kCand = 3, kAlgoBytes = 4, 
 struct IndexBufs {
   const int4* rmeta;
   const int4* iv;
-  const int* data_pos;                // [NI] or nullptr: start-sorted order is given (one chrom pass)
+  const unsigned* dchrom;             // [NI] or nullptr: chromosome per data position (start-sorted
+  const int4* drec;                   //      order given) and {start, end, thr, tag} per data position
   unsigned long long* keys;           // scratch [NI] x2 (double buffer for the sort)
   unsigned long long* keys2;
   int* vals;
@@ -48,7 +49,8 @@ struct IndexBufs {
 hipError_t index_temp_bytes(int ni, size_t* bytes, hipStream_t s);
 hipError_t launch_build_index(const IndexBufs& b, int n_reads, int ni, int n_chroms, hipStream_t s);
 // thresholds into iv[k].w and (when the index exists) idx4[iv_rng[k].x].z
-hipError_t launch_set_thr(const int* thr, int4* iv, const int4* iv_rng, int4* idx4, int ni, hipStream_t s);
+hipError_t launch_set_thr(const int* thr, int4* iv, const int4* iv_rng, int4* idx4, const int* data_pos,
+                          int4* drec, int ni, hipStream_t s);
 
 // ---- pair kernel (query.hip) -------------------------------------------------------------
 struct QueryArgs {
