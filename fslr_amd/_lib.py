@@ -11,7 +11,7 @@ import os
 
 import numpy as np
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libfslr_hip.so')
+LIB_PATH = os.environ.get('FSLR_LIB') or os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libfslr_hip.so')
 
 FSLR_OK, FSLR_ERR_ZERO_DIVISION, FSLR_ERR_INVALID, FSLR_ERR_HIP, FSLR_ERR_NOMEM, FSLR_ERR_STATE = range(6)
 FSLR_MAX_L = 64
@@ -23,7 +23,8 @@ PASS_STRIDE = 2 * FSLR_MAX_L
 EXPORTED = ['fslr_abi_version', 'fslr_last_error', 'fslr_ctx_create', 'fslr_ctx_destroy', 'fslr_set_profiling',
             'fslr_set_reads', 'fslr_set_thresholds', 'fslr_reserve_edges', 'fslr_reserve_deferred',
             'fslr_build_index', 'fslr_query',
-            'fslr_components', 'fslr_run', 'fslr_sync', 'fslr_read_stats', 'fslr_get_timings', 'fslr_get_labels',
+            'fslr_components', 'fslr_run', 'fslr_sync', 'fslr_read_stats', 'fslr_get_timings', 'fslr_read_counters',
+            'fslr_get_labels',
             'fslr_get_fwd_degree', 'fslr_get_edges', 'fslr_labels_device_ptr', 'fslr_copy_labels_device',
             'fslr_copy_fwd_device', 'fslr_union_pairs', 'fslr_finalize_labels']
 
@@ -98,6 +99,7 @@ def load(path: str = LIB_PATH):
         'fslr_sync': (ctypes.c_int, [vp]),
         'fslr_read_stats': (ctypes.c_int, [vp, ctypes.POINTER(QueryStats)]),
         'fslr_get_timings': (ctypes.c_int, [vp, ctypes.POINTER(Timings)]),
+        'fslr_read_counters': (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
         'fslr_get_labels': (ctypes.c_int, [vp, vp]),
         'fslr_get_fwd_degree': (ctypes.c_int, [vp, vp]),
         'fslr_get_edges': (ctypes.c_int, [vp, vp, vp, vp, i64]),
@@ -242,6 +244,14 @@ class Context:
         t = Timings()
         self._check(self._L.fslr_get_timings(self._h, ctypes.byref(t)))
         return t.as_dict()
+
+    def counters(self, n: int = 32) -> np.ndarray:
+        """Raw device counters of the last query (kernels.hpp Counter; diagnostics)."""
+        out = np.zeros(n, np.uint64)
+        got = self._L.fslr_read_counters(self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), n)
+        if got < 0:
+            self._check(-got)
+        return out[:got]
 
     def labels(self) -> np.ndarray:
         out = np.empty(self.n_reads, np.int32)

@@ -42,6 +42,7 @@ struct fslr_ctx {
   void* temp = nullptr;
   size_t temp_bytes = 0;
   int* umax = nullptr;     // [FSLR_MAX_L] derived from the pass table
+  int4* lbounds = nullptr; // [N] per query read: exact integer ranges of the length gate
   int2* edges = nullptr;
   unsigned short* edge_iu = nullptr;
   int64_t edge_cap = 0;
@@ -51,7 +52,7 @@ struct fslr_ctx {
   int* errw = nullptr;     // [0..2] error, [3] max_fwd
   int* thr_tmp = nullptr;
   int64_t cap_n = 0, cap_ni = 0, cap_chroms = 0;
-  std::vector<int> umax_host;
+  std::vector<int> umax_host, umax_dev_copy;   // dev copy: what c->umax holds
   std::vector<unsigned char> aln_zero_host;   // per CSR interval: FSLR_THR_ZERO_ALN at set_reads
   int ablate = 0;
   // profiling
@@ -90,7 +91,8 @@ int dalloc(fslr_ctx* c, T** p, size_t count) {
 int ensure_capacity(fslr_ctx* c, int64_t n, int64_t ni, int n_chroms) {
   int rc;
   if (n > c->cap_n) {
-    if ((rc = dalloc(c, &c->rmeta, n)) || (rc = dalloc(c, &c->fwd, n)) || (rc = dalloc(c, &c->parent, n)))
+    if ((rc = dalloc(c, &c->rmeta, n)) || (rc = dalloc(c, &c->fwd, n)) || (rc = dalloc(c, &c->parent, n)) ||
+        (rc = dalloc(c, &c->lbounds, n)))
       return rc;
     c->cap_n = n;
   }
@@ -168,7 +170,7 @@ void fslr_ctx_destroy(fslr_ctx* c) {
   void* bufs[] = {c->rmeta,  c->iv,     c->iv_rng,  c->idx4,    c->idx_gate, c->data_pos, c->s_start,
                   c->crange, c->keys,   c->keys2,   c->vals,    c->vals2,   c->endkey,  c->pmaxkey,
                   c->temp,   c->umax,   c->edges,   c->edge_iu, c->fwd,     c->parent,  c->counters,
-                  c->errw,   c->thr_tmp, c->defer,   c->dchrom,  c->drec};
+                  c->errw,   c->thr_tmp, c->defer,   c->dchrom,  c->drec,    c->lbounds};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->ev_ok)
@@ -216,6 +218,8 @@ int fslr_set_reads(fslr_ctx* c, const fslr_reads* r) {
       return fail(c, FSLR_ERR_INVALID, "every read needs 1.." + std::to_string(FSLR_MAX_L) + " intervals");
     if (r->read_nal[i] < 0 || r->read_nal[i] >= (1 << 24))
       return fail(c, FSLR_ERR_INVALID, "n_alignments outside [0, 2^24)");
+    if (r->read_qlen2[i] < 0)   // max(qend) - min(qstart) over a read's fillings (cluster.py:26-29)
+      return fail(c, FSLR_ERR_INVALID, "qlen2 < 0");
     int flags = 0;
     for (int k = o; k < o + len; ++k)
       if (zero[k]) flags |= 1;
@@ -374,8 +378,11 @@ int fslr_query(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_t a_end
       if (!row[U - 1]) return fail(c, FSLR_ERR_INVALID, "pass_table row is not a prefix in U");
     c->umax_host[I - 1] = um;
   }
-  HIP_TRY(c, hipMemcpyAsync(c->umax, c->umax_host.data(), FSLR_MAX_L * sizeof(int), hipMemcpyHostToDevice,
-                            c->stream));
+  if (c->umax_host != c->umax_dev_copy) {
+    c->umax_dev_copy = c->umax_host;
+    HIP_TRY(c, hipMemcpyAsync(c->umax, c->umax_dev_copy.data(), FSLR_MAX_L * sizeof(int), hipMemcpyHostToDevice,
+                              c->stream));
+  }
   HIP_TRY(c, hipMemsetAsync(c->counters, 0, kNumCounters * sizeof(unsigned long long), c->stream));
   HIP_TRY(c, hipMemsetAsync(c->errw, 0, 4 * sizeof(int), c->stream));
   if (c->n) HIP_TRY(c, hipMemsetAsync(c->fwd, 0, c->n * sizeof(int), c->stream));
@@ -388,6 +395,7 @@ int fslr_query(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_t a_end
   g.defer = c->defer;
   g.defer_cap = c->defer_cap;
   g.umax = c->umax;
+  g.lb = c->lbounds;
   g.qlen_cut = p->qlen_cut;
   g.nal_cut = p->nal_cut;
   g.a_begin = static_cast<int>(a_begin);
@@ -432,6 +440,17 @@ int fslr_sync(fslr_ctx* c) {
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   return FSLR_OK;
+}
+
+int fslr_read_counters(fslr_ctx* c, uint64_t* out, int n) {
+  if (!c || !out || n < 0) return -FSLR_ERR_INVALID;
+  if (n > kNumCounters) n = kNumCounters;
+  if (!c->counters || n == 0) return 0;
+  if (hipSetDevice(c->device) != hipSuccess ||
+      hipMemcpyAsync(out, c->counters, n * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+      hipStreamSynchronize(c->stream) != hipSuccess)
+    return -fail(c, FSLR_ERR_HIP, "reading counters");
+  return n;
 }
 
 int fslr_read_stats(fslr_ctx* c, fslr_query_stats* out) {

@@ -23,7 +23,9 @@ constexpr int kPassStride = 128;      // 2 * FSLR_MAX_L
 constexpr int kMaxCoord = 1 << 30;
 
 enum Counter { kEdgeCount = 0, kEval = 1, kJacc = 2, kCand = 3, kAlgoBytes = 4, kOverflow = 5, kGather = 6,
-               kMatchEntries = 7, kMatchedPairs = 8, kDeferCount = 9, kNumCounters = 10 };
+               kMatchEntries = 7, kMatchedPairs = 8, kDeferCount = 9,
+               kSecBase = 16,           // FSLR_SECTION_PROF builds: per-section cycle sums of the pair kernel
+               kNumCounters = 32 };
 
 // ---- index build (index.hip) -------------------------------------------------------------
 struct IndexBufs {
@@ -59,7 +61,8 @@ struct QueryArgs {
   const int4* iv_rng;
   const int4* idx4;
   const int2* idx_gate;
-  const int* umax;                    // [64]: pair with I matches is an edge iff I + ... U <= umax[I-1]
+  const int* umax;                    // [64]: pair with I matches is an edge iff U <= umax[I-1]
+  int4* lb;                           // [N] scratch: per query read {qlo, qhi, nlo, nhi} (length gate)
   double qlen_cut, nal_cut;
   int a_begin, a_end;
   int2* edges;

@@ -44,15 +44,45 @@ constexpr unsigned kStLenOk = 1u;         // passed different_lengths_or_alignme
 constexpr unsigned kStDefer = 2u;         // evaluated by deferred_kernel
 constexpr unsigned kStMatch = 4u;         // has at least one matching interval pair
 constexpr unsigned kStSpill = 8u;         // a match did not fit the match list
+constexpr unsigned kStConflict = 16u;     // two matching pairs share a row or a column (ordered greedy)
 // deferred entries: a << 39 | B << 14 | ic << 8 | jc << 2 | kind
 constexpr unsigned kDefPair = 0u;         // unique lenOK pair: gather evaluation (replay if aln_size==0)
 constexpr unsigned kDefWitness = 1u;      // candidate past the hash limit: witness rule, then as above
+
+// FSLR_SECTION_PROF builds (make prof): per-wave cycle sums of the kernel's sections land in
+// counters[kSecBase + k] — 0 read setup, 1 next-chunk map + loads, 2 hit + dedupe (absorbs the
+// load wait), 3 gate + deferred puts, 4 match list, 5 next-read prefetch, 6 greedy + edges, 7 wave total
+#ifdef FSLR_SECTION_PROF
+#define SEC_NOW(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define SEC_ADD(k, t0) (sec[k] += __builtin_amdgcn_s_memtime() - (t0))
+constexpr int kSections = 8;
+#else
+#define SEC_NOW(v) (void)0
+#define SEC_ADD(k, t0) (void)0
+#endif
 
 __device__ __forceinline__ int lane_id() { return static_cast<int>(__lane_id()); }
 
 __device__ __forceinline__ int mbcnt(unsigned long long m) {
   return __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(m >> 32),
                                    __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(m), 0u));
+}
+
+// wave-uniform loads through the scalar cache (constant address space => s_load)
+typedef const __attribute__((address_space(4))) int* const_i32_ptr;
+__device__ __forceinline__ int2 sload2(const void* p, int i) {
+  const_i32_ptr q = (const_i32_ptr)(p) + 2 * i;
+  return make_int2(q[0], q[1]);
+}
+__device__ __forceinline__ int4 sload4(const void* p, int i) {
+  const_i32_ptr q = (const_i32_ptr)(p) + 4 * i;
+  return make_int4(q[0], q[1], q[2], q[3]);
+}
+
+// three consecutive dwords of a 16-B record, starting at dword `first`
+__device__ __forceinline__ int3 load3(const int4* p, int k, int first) {
+  const int* q = reinterpret_cast<const int*>(p + k) + first;
+  return make_int3(q[0], q[1], q[2]);
 }
 
 __device__ __forceinline__ int rdl(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
@@ -82,6 +112,37 @@ __device__ __forceinline__ bool lengths_pass(int q1, int q2, int n1, int n2, dou
   mx = max(n1, n2);
   if (mx == 0) { *zd = true; return false; }
   return static_cast<double>(mn) / static_cast<double>(mx) >= ncut;
+}
+
+// The gate of one query read as integer ranges (exact: IEEE division is monotone, so the
+// reference's double test fl(min/max) >= cut, cluster.py:178-183, holds on a contiguous range of
+// the partner's value).  {lo, hi}: partner values x in [lo, hi] pass; lo < 0 marks v == 0, where
+// x == 0 raises ZeroDivisionError and the passing range is [1, hi].
+__device__ int2 ratio_range(int v, double cut) {
+  constexpr int kTop = 0x7FFFFFFF;
+  if (v == 0) return make_int2(-1, 0.0 >= cut ? kTop : 0);
+  if (!(1.0 >= cut)) return make_int2(1, 0);
+  const double dv = static_cast<double>(v);
+  if (!(cut > 0.0)) return make_int2(0, kTop);      // every ratio >= 0 >= cut
+  // smallest x <= v with fl(x / v) >= cut: start at the estimate, then walk with the exact test
+  // (monotone, so the walks end at the true bound whatever the estimate; here they take 1-2 steps)
+  int lo = static_cast<int>(fmin(fmax(ceil(cut * dv), 0.0), dv));
+  while (lo > 0 && static_cast<double>(lo - 1) / dv >= cut) --lo;
+  while (!(static_cast<double>(lo) / dv >= cut)) ++lo;
+  // largest x >= v with fl(v / x) >= cut
+  int hi = static_cast<int>(fmin(fmax(floor(dv / cut), dv), static_cast<double>(kTop)));
+  while (hi < kTop && dv / static_cast<double>(hi + 1) >= cut) ++hi;
+  while (!(dv / static_cast<double>(hi) >= cut)) --hi;
+  return make_int2(lo, hi);
+}
+
+__global__ void k_len_bounds(const int4* __restrict__ rmeta, int a0, int a1, double qcut, double ncut,
+                             int4* __restrict__ lb) {
+  for (int a = a0 + blockIdx.x * blockDim.x + threadIdx.x; a < a1; a += gridDim.x * blockDim.x) {
+    const int4 m = rmeta[a];
+    const int2 q = ratio_range(m.z, qcut), n = ratio_range(m.w, ncut);
+    lb[a] = make_int4(q.x, q.y, n.x, n.y);
+  }
 }
 
 __device__ __forceinline__ void raise_zd(int* err, bool zd, int a, int b) {
@@ -161,7 +222,7 @@ struct DeferStage {
 };
 
 template <int kThrMode>
-__global__ __launch_bounds__(kBlock) void query_kernel(QueryArgs g) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) void query_kernel(QueryArgs g) {
   __shared__ unsigned hash_all[kWavesPerBlock][kHashSize];
   __shared__ unsigned state_all[kWavesPerBlock][kHashSize];
   __shared__ unsigned ml_all[kWavesPerBlock][kMatchCap];
@@ -182,37 +243,54 @@ __global__ __launch_bounds__(kBlock) void query_kernel(QueryArgs g) {
   const int umax_v = g.umax[lane];
   const int nwaves = gridDim.x * kWavesPerBlock;
   unsigned long long w_eval = 0, w_jacc = 0, w_cand = 0, w_over = 0, w_ml = 0, w_mp = 0;
-  unsigned long long l_bytes = 0;       // per lane: algorithmic bytes of evaluated pairs
+  // algorithmic bytes of evaluated pairs: 16 (LA + LB) + 32 each
+  unsigned long long w_la_pairs = 0;
+  unsigned l_lb = 0;
   int w_maxfwd = 0;
 
+#ifdef FSLR_SECTION_PROF
+  unsigned long long sec[kSections] = {};
+#endif
+  SEC_NOW(t_wave);
+  // read pipeline: headers (scalar loads) two reads ahead, intervals one read ahead — the next
+  // read's rows are requested when this read starts, so they land during its walk
   int a = g.a_begin + blockIdx.x * kWavesPerBlock + wv;
-  int4 am = make_int4(0, 0, 0, 0);
-  if (a < g.a_end) am = g.rmeta[a];
-  int4 my = make_int4(-1, 0, 0, 0), rg = make_int4(0, 0, 0, 0);
-  {
-    const int off = __builtin_amdgcn_readfirstlane(am.x), len = __builtin_amdgcn_readfirstlane(am.y) & 0xffff;
-    if (a < g.a_end && lane < len) {
-      my = g.iv[off + lane];
-      rg = g.iv_rng[off + lane];
-    }
+  const int2* rm2 = reinterpret_cast<const int2*>(g.rmeta);     // {iv offset, len | flags << 16}
+  int2 am = make_int2(0, 0), am_n = make_int2(0, 0);
+  if (a < g.a_end) am = sload2(rm2, 2 * a);
+  if (a + nwaves < g.a_end) am_n = sload2(rm2, 2 * (a + nwaves));
+  // lane i of A: my = {start, end, thr} of interval i, rg = {q, n_fwd, bwd_begin} (kernels.hpp)
+  int3 my = make_int3(0, 0, 0), rg = make_int3(0, 0, 0);
+  if (a < g.a_end && lane < (am.y & 0xffff)) {
+    my = load3(g.iv, am.x + lane, 1);
+    rg = load3(g.iv_rng, am.x + lane, 0);
   }
 
   for (; a < g.a_end; a += nwaves) {
+    SEC_NOW(t_s0);
+    const int a_next = a + nwaves;
+    int3 my_next = make_int3(0, 0, 0), rg_next = make_int3(0, 0, 0);
+    if (a_next < g.a_end && lane < (am_n.y & 0xffff)) {
+      my_next = load3(g.iv, am_n.x + lane, 1);
+      rg_next = load3(g.iv_rng, am_n.x + lane, 0);
+    }
+    int2 am_nn = make_int2(0, 0);
+    if (a_next + nwaves < g.a_end) am_nn = sload2(rm2, 2 * (a_next + nwaves));
+    const int4 alb = sload4(g.lb, a);
     if (++epoch > kEpochMax) {
       wave_lds_sync();
       for (int k = lane; k < kHashSize; k += kWave) H[k] = 0u;
       epoch = 1;
     }
-    const int amy = __builtin_amdgcn_readfirstlane(am.y);
+    const int amy = am.y;
     const int LA = amy & 0xffff;
     const bool hazA = (static_cast<unsigned>(amy) >> 16) & 1u;
-    const int q1 = __builtin_amdgcn_readfirstlane(am.z), n1 = __builtin_amdgcn_readfirstlane(am.w);
-    // prefetch the next read's header
-    const int a_next = a + nwaves;
-    int4 am_next = make_int4(0, 0, 0, 0);
-    if (a_next < g.a_end) am_next = g.rmeta[a_next];
+    // length gate of A as integer ranges (k_len_bounds)
+    const int qlo = alb.x, qhi = alb.y, nlo = alb.z, nhi = alb.w;
+    const bool qz = qlo < 0, nz = nlo < 0;
+    const int qlo_e = qz ? 1 : qlo, nlo_e = nz ? 1 : nlo;
 
-    const int cnt = rg.y + rg.w;
+    const int cnt = rg.y + (rg.x - rg.z);   // n_fwd + n_bwd
     int pre = cnt;
 #pragma unroll
     for (int o = 1; o < kWave; o <<= 1) {
@@ -250,7 +328,9 @@ __global__ __launch_bounds__(kBlock) void query_kernel(QueryArgs g) {
         gt_c = g.idx_gate[p_c];
       }
     }
+    SEC_ADD(0, t_s0);
     for (int base = 0; base < R; base += kWave) {
+      SEC_NOW(t_s1);
       const bool valid = base + lane < R;
       const int mi = mi_c;
       const bool fwd = fwd_c;
@@ -265,7 +345,9 @@ __global__ __launch_bounds__(kBlock) void query_kernel(QueryArgs g) {
           gt_c = g.idx_gate[p_c];
         }
       }
-      const int s_i = __shfl(my.y, mi), e_i = __shfl(my.z, mi), t_i = __shfl(my.w, mi);
+      SEC_ADD(1, t_s1);
+      SEC_NOW(t_s2);
+      const int s_i = __shfl(my.x, mi), e_i = __shfl(my.y, mi), t_i = __shfl(my.z, mi);
       const bool hit = valid && (fwd || rec.y >= s_i);
       w_cand += __popcll(__ballot(hit));
       const int B = rec.w >> 6;
@@ -291,19 +373,24 @@ __global__ __launch_bounds__(kBlock) void query_kernel(QueryArgs g) {
       }
       const unsigned long long nm = __ballot(isnew);
       uniq += __popcll(nm);
+      SEC_ADD(2, t_s2);
       if (g.mode == 1) continue;
+      SEC_NOW(t_s3);
       // ---- gate at first sight (idx_gate: {qlen2, nal | LB << 24 | haz << 31}) -------------
       const int LB = (gt.y >> 24) & 127;
       const bool haz = hazA || (static_cast<unsigned>(gt.y) >> 31);
-      bool zd = false;
-      const bool lenok = isnew && lengths_pass(q1, gt.x, n1, gt.y & 0xFFFFFF, g.qlen_cut, g.nal_cut, &zd);
-      raise_zd(g.err, isnew && zd, a, B);
+      const int q2 = gt.x, n2 = gt.y & 0xFFFFFF;
+      const bool pq = q2 >= qlo_e && q2 <= qhi;
+      const bool zd = isnew && ((qz && q2 == 0) || (!pq && nz && n2 == 0));
+      const bool lenok = isnew && !zd && (pq || (n2 >= nlo_e && n2 <= nhi));
+      raise_zd(g.err, zd, a, B);
       const bool defer = lenok && (kThrMode == 1 || haz);
       if (isnew) {
         ST[h] = (lenok ? kStLenOk : 0u) | (defer ? kStDefer : 0u) | (static_cast<unsigned>(LB) << 8);
-        l_bytes += 16ull * static_cast<unsigned long long>(LA + LB) + 32ull;
+        l_lb += static_cast<unsigned>(LB);
       }
       w_eval += __popcll(nm);
+      w_la_pairs += static_cast<unsigned long long>(LA) * __popcll(nm);
       w_jacc += __popcll(__ballot(lenok));
       if (g.mode == 0) {
         ds.put(g, defer, a, B, 0, 0, kDefPair, lane);
@@ -311,6 +398,8 @@ __global__ __launch_bounds__(kBlock) void query_kernel(QueryArgs g) {
       }
       w_over += __popcll(__ballot(over));
       wave_lds_sync();
+      SEC_ADD(3, t_s3);
+      SEC_NOW(t_s4);
       // ---- matching interval pairs → match list (A-major: i never decreases) -----------------
       if (kThrMode == 0) {
         const bool mt = cand && !over && (min(e_i, rec.y) - max(s_i, rec.x) >= max(t_i, rec.z));
@@ -335,20 +424,42 @@ __global__ __launch_bounds__(kBlock) void query_kernel(QueryArgs g) {
           mln = min(mln + __popcll(mm), kMatchCap);
         }
       }
+      SEC_ADD(4, t_s4);
     }
-    // prefetch the next read's intervals while this read's greedy runs from LDS
-    int4 my_next = make_int4(-1, 0, 0, 0), rg_next = make_int4(0, 0, 0, 0);
-    {
-      const int off = __builtin_amdgcn_readfirstlane(am_next.x);
-      const int len = __builtin_amdgcn_readfirstlane(am_next.y) & 0xffff;
-      if (a_next < g.a_end && lane < len) {
-        my_next = g.iv[off + lane];
-        rg_next = g.iv_rng[off + lane];
-      }
-    }
+    SEC_NOW(t_s5);
+    SEC_ADD(5, t_s5);
+    SEC_NOW(t_s6);
     // ---- first-fit greedy from the match list, one lane per matched partner ----------------
     if (kThrMode == 0 && g.mode == 0 && mpn > 0) {
       wave_lds_sync();
+      // Fast path: a partner none of whose matching interval pairs share a row i or a column j
+      // keeps every pair under first-fit (each row has one candidate, nobody else wants it), so
+      // I = its number of pairs.  One pass with lanes = list entries ORs each entry's i and j into
+      // the partner's masks (scratch words after the list; partner index in ST bits 16..21) and
+      // flags the partner when a bit was already set; only flagged partners run the ordered scan.
+      const bool fast = mpn <= kWave && mln + 4 * mpn <= kMatchCap;
+      unsigned* SM = ML + mln;
+      if (fast) {
+        if (lane < mpn) {
+          const int hp = MP[lane];
+          ST[hp] = (ST[hp] & 0xFFFFu) | (static_cast<unsigned>(lane) << 16);
+          SM[4 * lane] = SM[4 * lane + 1] = SM[4 * lane + 2] = SM[4 * lane + 3] = 0u;
+        }
+        wave_lds_sync();
+        for (int kb = 0; kb < mln; kb += kWave) {
+          if (kb + lane < mln) {
+            const unsigned e = ML[kb + lane];
+            const unsigned hh = e & (kHashSize - 1);
+            const unsigned i = (e >> kHashBits) & 63u, j = (e >> (kHashBits + 6)) & 63u;
+            const unsigned p = (ST[hh] >> 16) & 63u;
+            const unsigned bi = 1u << (i & 31u), bj = 1u << (j & 31u);
+            const unsigned oi = atomicOr(&SM[4 * p + (i >> 5)], bi);
+            const unsigned oj = atomicOr(&SM[4 * p + 2 + (j >> 5)], bj);
+            if ((oi & bi) | (oj & bj)) atomicOr(&ST[hh], kStConflict);
+          }
+        }
+        wave_lds_sync();
+      }
       for (int k0 = 0; k0 < mpn; k0 += kWave) {
         const bool act = k0 + lane < mpn;
         const int h = act ? static_cast<int>(MP[k0 + lane]) : 0;
@@ -360,26 +471,41 @@ __global__ __launch_bounds__(kBlock) void query_kernel(QueryArgs g) {
         const int B = static_cast<int>(key & kBMask);
         const int LB = static_cast<int>((st >> 8) & 0xffu);
         int I = 0;
-        if (__ballot(need)) {
-          // reference order (cluster.py:152-161): rows i of A ascending, lowest unused j of B
-          unsigned long long used = 0ull, rowm = 0ull;
-          int cur = -1;
-          for (int k = 0; k < mln; ++k) {
-            const unsigned e = ML[k];
-            if (need && static_cast<int>(e & (kHashSize - 1)) == h) {
+        bool ordered = need;
+        if (fast) {
+          ordered = need && (st & kStConflict);
+          if (act) I = __popc(SM[4 * lane]) + __popc(SM[4 * lane + 1]);
+        }
+        if (__ballot(ordered)) {
+          // reference order (cluster.py:152-161): rows i of A ascending, lowest unused j of B.  The
+          // list is A-major, so the row index is wave-uniform along it: entries are read 64 per
+          // LDS load and walked with readlane, each lane ORs the j of its own partner's entries
+          // into the current row, and a row change settles every lane's row at once.
+          unsigned used_lo = 0u, used_hi = 0u, row_lo = 0u, row_hi = 0u;
+          int cur = -1, Io = 0;
+          for (int kb = 0; kb < mln; kb += kWave) {
+            const unsigned ev = kb + lane < mln ? ML[kb + lane] : 0u;
+            const int ne = min(kWave, mln - kb);
+            for (int t = 0; t < ne; ++t) {
+              const unsigned e = static_cast<unsigned>(rdl(static_cast<int>(ev), t));
               const int i = static_cast<int>((e >> kHashBits) & 63u);
-              const int j = static_cast<int>((e >> (kHashBits + 6)) & 63u);
               if (i != cur) {
-                const unsigned long long m = rowm & ~used;
-                if (m) { used |= m & (~m + 1ull); ++I; }
-                rowm = 0ull;
+                const unsigned m_lo = row_lo & ~used_lo, m_hi = row_hi & ~used_hi;
+                used_lo |= m_lo & (0u - m_lo);
+                used_hi |= m_lo ? 0u : (m_hi & (0u - m_hi));
+                Io += (m_lo | m_hi) != 0u;
+                row_lo = row_hi = 0u;
                 cur = i;
               }
-              rowm |= 1ull << j;
+              const unsigned j = (e >> (kHashBits + 6)) & 63u;
+              const bool mine = static_cast<int>(e & (kHashSize - 1)) == h;
+              if (j < 32u) row_lo |= mine ? (1u << j) : 0u;
+              else row_hi |= mine ? (1u << (j - 32u)) : 0u;
             }
           }
-          const unsigned long long m = rowm & ~used;
-          if (m) { used |= m & (~m + 1ull); ++I; }
+          const unsigned m_lo = row_lo & ~used_lo, m_hi = row_hi & ~used_hi;
+          Io += (m_lo | m_hi) != 0u;
+          if (ordered) I = Io;
         }
         const int U = LA + LB - I;
         const bool pass = U <= __shfl(umax_v, max(I, 1) - 1);
@@ -387,18 +513,26 @@ __global__ __launch_bounds__(kBlock) void query_kernel(QueryArgs g) {
         ds.put(g, spill, a, B, 0, 0, kDefPair, lane);
       }
     }
+    SEC_ADD(6, t_s6);
     w_ml += mln;
     w_mp += mpn;
     if (lane == 0) g.fwd[a] = fwdA;
     w_maxfwd = max(w_maxfwd, fwdA);
-    am = am_next;
+    am = am_n;
+    am_n = am_nn;
     my = my_next;
     rg = rg_next;
   }
   if (es.n > 0) es.flush(g, es.n, lane);
   if (ds.n > 0) ds.flush(g, ds.n, lane);
+  SEC_ADD(7, t_wave);
+  unsigned long long l_bytes = l_lb;
   for (int o = 32; o > 0; o >>= 1) l_bytes += __shfl_xor(l_bytes, o);
+  l_bytes = 16ull * (l_bytes + w_la_pairs) + 32ull * w_eval;
   if (lane == 0) {
+#ifdef FSLR_SECTION_PROF
+    for (int k = 0; k < kSections; ++k) atomicAdd(&g.counters[kSecBase + k], sec[k]);
+#endif
     if (l_bytes) atomicAdd(&g.counters[kAlgoBytes], l_bytes);
     if (w_eval) atomicAdd(&g.counters[kEval], w_eval);
     if (w_jacc) atomicAdd(&g.counters[kJacc], w_jacc);
@@ -537,6 +671,7 @@ int resident_blocks() {
 hipError_t launch_query(const QueryArgs& a, int thr_mode, hipStream_t s) {
   const long long nq = static_cast<long long>(a.a_end) - a.a_begin;
   if (nq > 0) {
+    k_len_bounds<<<grid_for(nq), 256, 0, s>>>(a.rmeta, a.a_begin, a.a_end, a.qlen_cut, a.nal_cut, a.lb);
     const long long want = (nq + kWavesPerBlock - 1) / kWavesPerBlock;
     if (thr_mode == 0) {
       const int cap = resident_blocks<0>();

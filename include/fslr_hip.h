@@ -149,6 +149,9 @@ int  fslr_run(fslr_ctx *ctx, const fslr_params *params);
 int  fslr_sync(fslr_ctx *ctx);
 int  fslr_read_stats(fslr_ctx *ctx, fslr_query_stats *out);     /* syncs; returns stats.error */
 int  fslr_get_timings(fslr_ctx *ctx, fslr_timings *out);        /* syncs */
+/* Raw device counters of the last query (diagnostics; layout is internal, kernels.hpp:
+ * Counter).  Copies min(n, 32) words, syncs, returns the count or -error. */
+int  fslr_read_counters(fslr_ctx *ctx, uint64_t *out, int n);
 
 /* D2H copies (sync). */
 int  fslr_get_labels(fslr_ctx *ctx, int32_t *labels);          /* [n_reads] min-rank root */

@@ -268,3 +268,49 @@ def test_vectors_cluster_ids(ctx):
         fwd[csr.read_qcode] = g['fwd']
         np.testing.assert_array_equal(comp, z['comp'])
         np.testing.assert_array_equal(fwd, z['fwd'])
+
+
+# ------------------------------------------------------------------ length gate at ratio boundaries
+def _boundary_pool(cut, top, rng):
+    """Values v and partners just inside / outside fl(min/max) >= cut for several magnitudes."""
+    pool = {1, 2, 3, top}
+    for v in (1, 2, 7, 25, 100, 1000, 12345, 1 << 20, top):
+        pool.add(v)
+        if cut > 0:
+            for x in (int(np.floor(cut * v)), int(np.ceil(v / cut)) if cut <= 1 else v):
+                for d in (-1, 0, 1):
+                    if 1 <= x + d <= top:
+                        pool.add(x + d)
+    pool = np.array(sorted(pool), np.int64)
+    return pool[rng.integers(0, pool.size, 400)]
+
+
+@pytest.mark.parametrize('qlen_diff,nal_diff', [(0.04, 0.25), (0.0, 0.0), (1.0, 1.0), (1.5, -0.5), (-0.5, 1.5),
+                                                (0.34, 0.999999), (1e-12, 0.5)])
+def test_length_gate_boundaries_vs_oracle(ctx, qlen_diff, nal_diff):
+    """400 reads with one identical interval each (every pair overlaps, so every pair is evaluated
+    and the first reads overflow the per-read partner hash): qlen2 / n_alignments drawn around the
+    exact ratio boundaries of cluster.py:178-183; one read each with qlen2 == 0 and nal == 0."""
+    rng = np.random.default_rng(int(1000 * (qlen_diff + 2 * nal_diff)) & 0xFFFF)
+    n = 400
+    q = _boundary_pool(1 - qlen_diff, (1 << 31) - 1, rng)
+    m = _boundary_pool(1 - nal_diff, (1 << 24) - 1, rng)
+    q[17] = 0
+    m[211] = 0
+    off = np.arange(n + 1, dtype=np.int64)
+    chrom = np.zeros(n, np.int32)
+    start = np.full(n, 5000, np.int32)
+    end = np.full(n, 6000, np.int32)
+    aln = np.full(n, 1000, np.int64)
+    thr = fold_overlap_threshold(aln, 0.8)
+    ctx.set_reads(off, q.astype(np.int32), m.astype(np.int32), chrom, start, end, thr, 1)
+    ctx.reserve_edges(n * n)
+    ctx.build_index()
+    st = ctx.run_query(1 - qlen_diff, 1 - nal_diff, pass_table([1.0]))
+    ctx.components()
+    a, b, I, U = ctx.edges(st['n_edges'])
+    g = dict(stats=st, labels=ctx.labels(), fwd=ctx.fwd_degree(), a=a, b=b, I=I, U=U)
+    o = O.run_core(O.OracleCSR(off, chrom, start, end, aln, q, m, np.arange(n)), 0.8, (1.0,), qlen_diff, nal_diff,
+                   use_cap=False)
+    assert st['overflow_candidates'] > 0
+    compare_with_oracle(g, o, n)

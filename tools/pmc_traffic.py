@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc passes (tools/pmc.sh) into per-launch HBM traffic of the pair kernel.
+
+    python tools/pmc_traffic.py gpurun_out/pmc [-o profiles/r01/pmc_traffic.json]
+
+Reads every */pmc_counter_collection.csv under the directory, keeps the dispatches of the
+named kernel, and averages each counter per dispatch.  HBM bytes per launch follow
+/opt/skills/guides/MI355X_MICROARCH.md (HBM / rocprofv3 section):
+  FETCH_SIZE, WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports 1/2 of the bytes of wide
+  (16 B/lane) streaming reads, so the corrected read bytes are 2 x FETCH_SIZE.  The pair
+  kernel's loads are 16-B-per-lane records (idx4) and 8-B gate words, so the x2 correction is
+  applied to all of FETCH_SIZE; the uncorrected figure is kept beside it.
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import json
+import os
+from collections import defaultdict
+
+
+def collect(root, kernel):
+    vals = defaultdict(list)
+    dur = []
+    for path in sorted(glob.glob(os.path.join(root, '**', '*counter_collection.csv'), recursive=True)):
+        with open(path, newline='') as fh:
+            for row in csv.DictReader(fh):
+                if kernel not in row['Kernel_Name']:
+                    continue
+                vals[row['Counter_Name']].append(float(row['Counter_Value']))
+                if row['Counter_Name'] in ('FETCH_SIZE', 'SQ_WAVES'):
+                    dur.append((int(row['End_Timestamp']) - int(row['Start_Timestamp'])) * 1e-9)
+    return {k: sum(v) / len(v) for k, v in vals.items()}, dur
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('root')
+    ap.add_argument('--kernel', default='query_kernel<0>')
+    ap.add_argument('-o', '--out', default=None)
+    args = ap.parse_args()
+    c, dur = collect(args.root, args.kernel)
+    if 'FETCH_SIZE' not in c:
+        raise SystemExit(f'no FETCH_SIZE rows for {args.kernel} under {args.root}')
+    fetch = c['FETCH_SIZE'] * 1024.0
+    write = c.get('WRITE_SIZE', 0.0) * 1024.0
+    out = {
+        'kernel': args.kernel,
+        'query_kernel_hbm_bytes_per_launch': 2.0 * fetch + write,
+        'fetch_bytes_raw': fetch,
+        'fetch_bytes_corrected_x2': 2.0 * fetch,
+        'write_bytes': write,
+        'pmc_pass_launch_s_mean': (sum(dur) / len(dur)) if dur else None,
+        'counters_mean_per_dispatch': c,
+        'correction': 'MI355X_MICROARCH.md: FETCH_SIZE x2 on gfx950 for 16-B/lane reads; WRITE_SIZE as is',
+    }
+    if 'TCC_HIT_sum' in c and 'TCC_MISS_sum' in c:
+        out['l2_hit_rate'] = c['TCC_HIT_sum'] / max(1.0, c['TCC_HIT_sum'] + c['TCC_MISS_sum'])
+    if 'SQ_WAVE_CYCLES' in c:
+        wc = max(1.0, c['SQ_WAVE_CYCLES'])
+        out['wave_cycle_split'] = {k: c.get(k, 0.0) / wc for k in ('SQ_WAIT_ANY', 'SQ_WAIT_INST_ANY',
+                                                                  'SQ_ACTIVE_INST_ANY')}
+    text = json.dumps(out, indent=1)
+    if args.out:
+        with open(args.out, 'w') as fh:
+            fh.write(text + '\n')
+    print(text)
+
+
+if __name__ == '__main__':
+    main()
