@@ -35,7 +35,9 @@
  *   pass_table  [FSLR_MAX_L][2*FSLR_MAX_L] bytes: pass_table[(I-1)*2*FSLR_MAX_L + (U-1)]
  *               = (I/U >= cutoff(I)) evaluated in Python floats (cluster.py:218-219).
  *   qlen_cut, nal_cut = 1 - qlen_diff, 1 - n_alignment_diff (Python floats);
- *               the device compares min/max ratios in IEEE double, as Python does.
+ *               the device evaluates fl(min/max) >= cut in IEEE double, as Python does,
+ *               once per query read to get the exact integer range of partner values that
+ *               pass (the ratio test is monotone on each side of the read's own value).
  */
 #ifndef FSLR_HIP_H
 #define FSLR_HIP_H
