@@ -4,19 +4,23 @@
 // Lock-free union-find: roots are hooked larger-under-smaller with a CAS, so the root of a
 // component is its minimum read rank — the order networkx yields components in (first inserted
 // node = minimum rank when every edge is added in its lower-rank read's loop).
-// Parent reads/writes are relaxed agent-scope atomics (L1-bypassing), so no CU reads a stale
-// parent from its own L1 (MI355X_MICROARCH.md, inter-workgroup visibility).  Parent values only
-// decrease, so path halving never breaks the forest.
+// Every parent pointer goes to an ancestor with a smaller rank, and a node's ancestors stay its
+// ancestors, so any value a node's parent ever held is still a valid step towards its root.  The
+// find walk therefore uses ordinary (cached, possibly stale) loads: a stale value is just an
+// older ancestor.  Only the hook is a coherent agent-scope CAS; when it fails, its returned value
+// (the fresh parent of the would-be root) continues the walk, so every retry moves strictly up
+// the tree and the loop ends.  Kernel boundaries make the final forest visible to finalize.
 #include "kernels.hpp"
 
 namespace fslr {
 namespace {
 
+// plain (cached) single-copy-atomic accesses: wavefront scope adds no coherence bits
 __device__ __forceinline__ int ld_rlx(const int* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 __device__ __forceinline__ void st_rlx(int* p, int v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 
 __device__ int uf_find(int* p, int x) {
@@ -35,9 +39,9 @@ __device__ void uf_union(int* p, int a, int b) {
     b = uf_find(p, b);
     if (a == b) return;
     if (a > b) { const int t = a; a = b; b = t; }
-    const int old = atomicCAS(p + b, b, a);   // hook the larger root under the smaller
+    const int old = atomicCAS(p + b, b, a);   // hook the larger root under the smaller (coherent)
     if (old == b) return;
-    b = old;
+    b = old;                                  // fresh parent of b: continue strictly upwards
   }
 }
 

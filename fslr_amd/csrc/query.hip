@@ -545,11 +545,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
 }
 
 // ------------------------------------------------------------------------------------------
-// deferred_kernel: one lane per deferred entry; gathers A's and B's intervals.
-//   kDefPair     lenOK pair: B-major first-fit greedy on 64-bit match masks over A (symmetric
-//                to the reference's A-major count), or the exact replay of cluster.py:152-161
-//                when an aln_size == 0 interval is involved (ZeroDivisionError where the
-//                reference raises it).
+// deferred_kernel: one wavefront per deferred entry (grid-stride over the list); B's intervals sit
+// in lanes j, A's are broadcast a row at a time with readlane.
+//   kDefPair     lenOK pair: first-fit greedy in the reference's order (cluster.py:152-161): for
+//                each row i of A, the lowest unused j of B on the same chromosome that either
+//                matches or — when an aln_size == 0 interval is involved — raises
+//                ZeroDivisionError at the position the reference would (first such candidate).
 //   kDefWitness  candidate (A, B, ic, jc) of a read past the hash limit: evaluated only if
 //                (jc, ic) is the first overlapping interval pair in B-major order, which makes
 //                exactly one candidate of each such pair the evaluator; then gate + as above.
@@ -560,92 +561,72 @@ __global__ __launch_bounds__(256) void deferred_kernel(QueryArgs g) {
   EdgeStage es{es_all[threadIdx.x >> 6], 0};
   const long long n = min(static_cast<long long>(g.counters[kDeferCount]), g.defer_cap);
   const int umax_v = g.umax[lane];
-  unsigned long long w_eval = 0, w_jacc = 0, w_gather = 0;
-  unsigned long long l_bytes = 0;
-  const long long stride = static_cast<long long>(gridDim.x) * blockDim.x;
-  // whole waves iterate together (ballots below need uniform trip counts)
-  const long long n_round = (n + kWave - 1) / kWave * kWave;
-  for (long long t = static_cast<long long>(blockIdx.x) * blockDim.x + threadIdx.x; t - lane < n_round;
-       t += stride) {
-    const bool act = t < n;
-    const unsigned long long e = act ? g.defer[t] : 0ull;
+  unsigned long long w_eval = 0, w_jacc = 0, w_gather = 0, w_bytes = 0;
+  const long long nw = static_cast<long long>(gridDim.x) * (blockDim.x >> 6);
+  for (long long t = static_cast<long long>(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6); t < n; t += nw) {
+    const unsigned long long e = g.defer[t];
     const int a = static_cast<int>(e >> 39);
     const int B = static_cast<int>((e >> 14) & kBMask);
     const int ic = static_cast<int>((e >> 8) & 63u), jc = static_cast<int>((e >> 2) & 63u);
     const unsigned kind = static_cast<unsigned>(e & 3u);
-    int4 am = make_int4(0, 0, 0, 0), bm = make_int4(0, 0, 0, 0);
-    if (act) {
-      am = g.rmeta[a];
-      bm = g.rmeta[B];
-    }
-    const int offA = am.x, LA = act ? (am.y & 0xffff) : 0;
-    const int offB = bm.x, LB = act ? (bm.y & 0xffff) : 0;
+    const int4 am = sload4(g.rmeta, a), bm = sload4(g.rmeta, B);
+    const int LA = am.y & 0xffff, LB = bm.y & 0xffff;
     const bool haz = ((am.y | bm.y) >> 16) & 1;
-    bool zd = false;
-    bool lenok = act && kind == kDefPair;
-    bool canon = lenok;
-    if (act && kind == kDefWitness) {
-      // witness: first overlapping (j, i) in B-major order
-      int wj = -1, wi = -1;
-      for (int j = 0; j < LB && wj < 0; ++j) {
-        const int4 b = g.iv[offB + j];
-        for (int i = 0; i < LA; ++i) {
-          const int4 ai = g.iv[offA + i];
-          if (ai.x == b.x && min(ai.z, b.z) >= max(ai.y, b.y)) { wj = j; wi = i; break; }
-        }
+    int4 ai = make_int4(-1, 0, 0, 0), bj = make_int4(-2, 0, 0, 0);
+    if (lane < LA) ai = g.iv[am.x + lane];
+    if (lane < LB) bj = g.iv[bm.x + lane];
+    bool zd = false, lenok = kind == kDefPair, canon = lenok;
+    if (kind == kDefWitness) {
+      // lane j: does B's interval j overlap (end-inclusive, same chromosome) any of A's?
+      unsigned long long ov = 0ull;
+      for (int i = 0; i < LA; ++i) {
+        const int c = rdl(ai.x, i), si = rdl(ai.y, i), ei = rdl(ai.z, i);
+        ov |= static_cast<unsigned long long>(lane < LB && bj.x == c && min(ei, bj.z) >= max(si, bj.y)) << i;
       }
+      const unsigned long long jm = __ballot(ov != 0ull);
+      const int wj = jm ? __builtin_ctzll(jm) : -1;
+      const unsigned long long ovw = wj >= 0 ? __shfl(ov, wj) : 0ull;
+      const int wi = ovw ? __builtin_ctzll(ovw) : -1;
       canon = wj == jc && wi == ic;
       if (canon) {
         lenok = lengths_pass(am.z, bm.z, am.w, bm.w, g.qlen_cut, g.nal_cut, &zd);
-        raise_zd(g.err, zd, a, B);
-        l_bytes += 16ull * static_cast<unsigned long long>(LA + LB) + 32ull;
+        if (lane == 0) raise_zd(g.err, zd, a, B);
+        ++w_eval;
+        w_jacc += lenok;
+        w_bytes += 16ull * static_cast<unsigned long long>(LA + LB) + 32ull;
       }
     }
-    w_eval += __popcll(__ballot(act && kind == kDefWitness && canon));
-    w_jacc += __popcll(__ballot(act && kind == kDefWitness && canon && lenok));
     const bool work = canon && lenok && !zd && g.mode == 0;
-    w_gather += __popcll(__ballot(work));
     int I = 0;
-    if (work && haz) {
-      unsigned long long used = 0ull;
-      for (int i = 0; i < LA && !zd; ++i) {
-        const int4 ai = g.iv[offA + i];
-        for (int j = 0; j < LB; ++j) {
-          if ((used >> j) & 1ull) continue;
-          const int4 b = g.iv[offB + j];
-          if (b.x != ai.x) continue;
-          if (ai.w == FSLR_THR_ZERO_ALN || b.w == FSLR_THR_ZERO_ALN) { zd = true; break; }
-          if (iv_match_general(ai.y, ai.z, ai.w, b.y, b.z, b.w)) { used |= 1ull << j; ++I; break; }
-        }
+    if (work) {
+      ++w_gather;
+      bool used = false;
+      for (int i = 0; i < LA; ++i) {
+        const int c = rdl(ai.x, i), si = rdl(ai.y, i), ei = rdl(ai.z, i), ti = rdl(ai.w, i);
+        const bool cand = lane < LB && !used && bj.x == c;
+        const bool zero = haz && cand && (ti == FSLR_THR_ZERO_ALN || bj.w == FSLR_THR_ZERO_ALN);
+        const bool hit = cand && (zero || iv_match_general(si, ei, ti, bj.y, bj.z, bj.w));
+        const unsigned long long hm = __ballot(hit);
+        if (!hm) continue;
+        const int j = __builtin_ctzll(hm);
+        if (__shfl(static_cast<int>(zero), j)) { zd = true; break; }
+        if (lane == j) used = true;
+        ++I;
       }
-      raise_zd(g.err, zd, a, B);
-    } else if (work) {
-      const unsigned long long fullA = LA == 64 ? ~0ull : ((1ull << LA) - 1ull);
-      unsigned long long freeA = fullA;
-      for (int j = 0; j < LB; ++j) {
-        const int4 b = g.iv[offB + j];
-        unsigned long long M = 0ull;
-        for (int i = 0; i < LA; ++i) {
-          const int4 ai = g.iv[offA + i];
-          M |= static_cast<unsigned long long>(ai.x == b.x && iv_match_general(ai.y, ai.z, ai.w, b.y, b.z, b.w)) << i;
-        }
-        const unsigned long long m = M & freeA;
-        if (m) { freeA ^= m & (~m + 1ull); ++I; }
-      }
+      if (lane == 0) raise_zd(g.err, zd, a, B);
     }
     const int U = LA + LB - I;
     const bool pass = U <= __shfl(umax_v, max(I, 1) - 1);
     const bool edge = pass && work && !zd && I > 0;
-    es.put(g, edge, a, B, I, U, lane);
-    if (edge) {
+    es.put(g, edge && lane == 0, a, B, I, U, lane);
+    if (edge && lane == 0) {
       const int old = atomicAdd(&g.fwd[a], 1);
       atomicMax(g.err + 3, old + 1);
     }
   }
   if (es.n > 0) es.flush(g, es.n, lane);
-  for (int o = 32; o > 0; o >>= 1) l_bytes += __shfl_xor(l_bytes, o);
   if (lane == 0) {
-    if (l_bytes) atomicAdd(&g.counters[kAlgoBytes], l_bytes);
+    if (w_bytes) atomicAdd(&g.counters[kAlgoBytes], w_bytes);
     if (w_eval) atomicAdd(&g.counters[kEval], w_eval);
     if (w_jacc) atomicAdd(&g.counters[kJacc], w_jacc);
     if (w_gather) atomicAdd(&g.counters[kGather], w_gather);
@@ -682,7 +663,7 @@ hipError_t launch_query(const QueryArgs& a, int thr_mode, hipStream_t s) {
     }
   }
   // the deferred list's length is only known on the device: a fixed grid walks it
-  deferred_kernel<<<1024, 256, 0, s>>>(a);
+  deferred_kernel<<<2048, 256, 0, s>>>(a);
   return hipGetLastError();
 }
 
