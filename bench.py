@@ -40,6 +40,8 @@ def parse():
     ap.add_argument('--dist', default='uniform')
     ap.add_argument('--cpu-sample-reads', type=int, default=200_000,
                     help='query reads in the bounded CPU-oracle baseline sample (0 = skip)')
+    ap.add_argument('--verify', action='store_true',
+                    help='after timing, rank 0 checks its labels against a single-context run of all reads')
     ap.add_argument('--traffic-json', default=None,
                     help='rocprofv3 PMC summary (tools/pmc_traffic.py) giving HBM bytes per launch')
     return ap.parse_args()
@@ -54,13 +56,19 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    # FSLR_BENCH_DEVICE / FSLR_BENCH_BACKEND=gloo: rehearse N ranks on one GPU (tools/rehearse_multi.sh)
+    dev_index = int(os.environ.get('FSLR_BENCH_DEVICE', local_rank))
+    backend = os.environ.get('FSLR_BENCH_BACKEND', 'nccl')
     import torch
-    torch.cuda.set_device(local_rank)
-    dev = torch.device('cuda', local_rank)
+    torch.cuda.set_device(dev_index)
+    dev = torch.device('cuda', dev_index)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group('nccl', device_id=dev)
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=dev)      # RCCL over xGMI
+        else:
+            dist.init_process_group(backend)
 
     from fslr_amd import _lib, synth
     from fslr_amd.dist import DeviceShardMerge, shard_range
@@ -76,7 +84,7 @@ def main():
     # a dedicated (non-null) stream shared by the library, torch events and RCCL
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
-    ctx = _lib.Context(local_rank, stream=stream.cuda_stream, profiling=True)
+    ctx = _lib.Context(dev_index, stream=stream.cuda_stream, profiling=True)
     thr = fold_overlap_threshold(csr.iv_aln, 0.8)
     ctx.load_csr(csr, thr)
     ctx.reserve_edges(12 * csr.n_reads)
@@ -126,7 +134,8 @@ def main():
     st = ctx.stats()
 
     tot = torch.tensor([elapsed, float(st['evaluated_pairs']), float(st['algo_bytes']), float(st['n_edges']),
-                        float(st['jaccard_evals'])], dtype=torch.float64, device=dev)
+                        float(st['jaccard_evals'])], dtype=torch.float64,
+                       device=dev if backend == 'nccl' else 'cpu')
     if dist:
         t_max = tot[:1].clone()
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
@@ -146,6 +155,17 @@ def main():
     if args.traffic_json and os.path.exists(args.traffic_json):
         with open(args.traffic_json) as fh:
             traffic = json.load(fh).get('query_kernel_hbm_bytes_per_launch')
+
+    verified = None
+    if args.verify and rank == 0:
+        got = ctx.labels()
+        ref = _lib.Context(dev_index)
+        ref.load_csr(csr, thr)
+        ref.reserve_edges(12 * csr.n_reads)
+        ref.run(qcut, ncut, pt)
+        verified = bool(np.array_equal(got, ref.labels()))
+        ref.close()
+        log(f'[rank 0] labels identical to a single-context run: {verified}')
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample_reads > 0:
@@ -191,6 +211,8 @@ def main():
             },
             'cpu_baseline': cpu,
         }
+        if verified is not None:
+            out['verified_labels_vs_single_context'] = verified
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()

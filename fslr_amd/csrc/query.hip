@@ -85,6 +85,18 @@ __device__ __forceinline__ int3 load3(const int4* p, int k, int first) {
   return make_int3(q[0], q[1], q[2]);
 }
 
+// inclusive wave64 prefix sum on DPP: row_shr 1/2/4/8 inside each row of 16 lanes, then
+// row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3) — six VALU ops, no LDS round trips
+__device__ __forceinline__ int wave_incl_scan(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);
+  return x;
+}
+
 __device__ __forceinline__ int rdl(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
 
 __device__ __forceinline__ void wave_lds_sync() {
@@ -241,41 +253,44 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
   unsigned epoch = 0;
   // edge iff U <= umax[I-1] (cluster.py:218-219 folded on the host); lane l holds umax[l]
   const int umax_v = g.umax[lane];
+  // rank assignment: grid-stride, 4 consecutive ranks per workgroup.  (Slicing each stride of
+  // ranks by XCD for L2 sharing between reads of one event measured no gain.)
   const int nwaves = gridDim.x * kWavesPerBlock;
+  const int a_hi = g.a_end;
+  const int a_first = g.a_begin + blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
   unsigned long long w_eval = 0, w_jacc = 0, w_cand = 0, w_over = 0, w_ml = 0, w_mp = 0;
   // algorithmic bytes of evaluated pairs: 16 (LA + LB) + 32 each
   unsigned long long w_la_pairs = 0;
   unsigned l_lb = 0;
   int w_maxfwd = 0;
-
 #ifdef FSLR_SECTION_PROF
   unsigned long long sec[kSections] = {};
 #endif
   SEC_NOW(t_wave);
   // read pipeline: headers (scalar loads) two reads ahead, intervals one read ahead — the next
   // read's rows are requested when this read starts, so they land during its walk
-  int a = g.a_begin + blockIdx.x * kWavesPerBlock + wv;
+  int a = a_first;
   const int2* rm2 = reinterpret_cast<const int2*>(g.rmeta);     // {iv offset, len | flags << 16}
   int2 am = make_int2(0, 0), am_n = make_int2(0, 0);
-  if (a < g.a_end) am = sload2(rm2, 2 * a);
-  if (a + nwaves < g.a_end) am_n = sload2(rm2, 2 * (a + nwaves));
+  if (a < a_hi) am = sload2(rm2, 2 * a);
+  if (a + nwaves < a_hi) am_n = sload2(rm2, 2 * (a + nwaves));
   // lane i of A: my = {start, end, thr} of interval i, rg = {q, n_fwd, bwd_begin} (kernels.hpp)
   int3 my = make_int3(0, 0, 0), rg = make_int3(0, 0, 0);
-  if (a < g.a_end && lane < (am.y & 0xffff)) {
+  if (a < a_hi && lane < (am.y & 0xffff)) {
     my = load3(g.iv, am.x + lane, 1);
     rg = load3(g.iv_rng, am.x + lane, 0);
   }
 
-  for (; a < g.a_end; a += nwaves) {
+  for (; a < a_hi; a += nwaves) {
     SEC_NOW(t_s0);
     const int a_next = a + nwaves;
     int3 my_next = make_int3(0, 0, 0), rg_next = make_int3(0, 0, 0);
-    if (a_next < g.a_end && lane < (am_n.y & 0xffff)) {
+    if (a_next < a_hi && lane < (am_n.y & 0xffff)) {
       my_next = load3(g.iv, am_n.x + lane, 1);
       rg_next = load3(g.iv_rng, am_n.x + lane, 0);
     }
     int2 am_nn = make_int2(0, 0);
-    if (a_next + nwaves < g.a_end) am_nn = sload2(rm2, 2 * (a_next + nwaves));
+    if (a_next + nwaves < a_hi) am_nn = sload2(rm2, 2 * (a_next + nwaves));
     const int4 alb = sload4(g.lb, a);
     if (++epoch > kEpochMax) {
       wave_lds_sync();
@@ -291,14 +306,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
     const int qlo_e = qz ? 1 : qlo, nlo_e = nz ? 1 : nlo;
 
     const int cnt = rg.y + (rg.x - rg.z);   // n_fwd + n_bwd
-    int pre = cnt;
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-      const int t = __shfl_up(pre, o);
-      if (lane >= o) pre += t;
-    }
+    const int pre = wave_incl_scan(cnt);
     const int ex = pre - cnt;
     const int R = rdl(pre, kWave - 1);
+    // interval i's records r in [ex, ex + cnt) are two runs of sorted positions:
+    // forward r < bnd: p = r + off_f;  backward: p = r + off_b
+    const int bnd = ex + rg.y, off_f = rg.x + 1 - ex, off_b = rg.z - rg.y - ex;
     int uniq = 0, mln = 0, mpn = 0, fwdA = 0;
 
     // record r of A's walk → (interval mi, sorted position p, forward?)
@@ -311,10 +324,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
         if (exk >= base + kWave) break;
         if (r >= exk) mi = k;
       }
-      const int q_i = __shfl(rg.x, mi), nf_i = __shfl(rg.y, mi), bb_i = __shfl(rg.z, mi);
-      const int loc = r - __shfl(ex, mi);
-      fwd = loc < nf_i;
-      p = fwd ? q_i + 1 + loc : bb_i + (loc - nf_i);
+      const int bnd_i = __shfl(bnd, mi), of_i = __shfl(off_f, mi), ob_i = __shfl(off_b, mi);
+      fwd = r < bnd_i;
+      p = r + (fwd ? of_i : ob_i);
     };
 
     int mi_c = 0, p_c = 0;

@@ -74,7 +74,13 @@ class DeviceShardMerge:
     def __call__(self):
         import torch.distributed as dist
         self.ctx.copy_labels_device(self.local.data_ptr())
-        dist.all_gather_into_tensor(self.gathered, self.local)
+        if dist.get_backend() == 'gloo':
+            # CPU-transport rehearsal (several ranks on one GPU): stage the exchange through host memory
+            out = self.gathered.new_empty(self.gathered.shape, device='cpu')
+            dist.all_gather_into_tensor(out, self.local.cpu())
+            self.gathered.copy_(out)
+        else:
+            dist.all_gather_into_tensor(self.gathered, self.local)
         base = self.gathered.data_ptr()
         for g in range(self.world):
             if g != self.rank:
