@@ -71,7 +71,7 @@ def main():
             dist.init_process_group(backend)
 
     from fslr_amd import _lib, synth
-    from fslr_amd.dist import DeviceShardMerge, shard_range
+    from fslr_amd.dist import DeviceShardMerge
     from fslr_amd.prep import fold_overlap_threshold, pass_table
 
     t0 = time.perf_counter()
@@ -90,7 +90,6 @@ def main():
     ctx.reserve_edges(12 * csr.n_reads)
     pt = pass_table([1, 1, 0.66, 0.66, 0.66, 0.5])
     qcut, ncut = 1 - 0.04, 1 - 0.25
-    a0, a1 = shard_range(csr.n_reads, rank, world)
     merge = DeviceShardMerge(ctx, csr.n_reads, world, rank, dev) if world > 1 else None
 
     ev_q0 = torch.cuda.Event(enable_timing=True)
@@ -101,7 +100,10 @@ def main():
         ctx.build_index()
         if timed:
             ev_q0.record(stream)
-        ctx.query(qcut, ncut, pt, 10, a0, a1)
+        if world > 1:
+            ctx.query_shard(qcut, ncut, pt, rank, world)      # balanced rank blocks (fslr_query_shard)
+        else:
+            ctx.query(qcut, ncut, pt, 10)
         if timed:
             ev_q1.record(stream)
         ctx.components()
@@ -195,7 +197,8 @@ def main():
                 'kernel_stats_rank0': {k: int(st[k]) for k in ('candidates', 'overflow_candidates', 'gather_pairs',
                                                                'match_entries', 'matched_pairs')},
                 'dense_equivalent_pairs_per_s': (n * (n - 1) / 2) / (elapsed / args.steps),
-                'parallelism': f'pair-space row shards x{world} + RCCL label all_gather' if world > 1 else 'single GPU',
+                'parallelism': f'query-read shards x{world} (64-rank blocks round robin) + RCCL label all_gather'
+                if world > 1 else 'single GPU',
             },
             'roofline': {
                 'bound': 'hbm',

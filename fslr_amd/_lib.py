@@ -22,7 +22,7 @@ PASS_STRIDE = 2 * FSLR_MAX_L
 # every symbol include/fslr_hip.h declares (checked by tests/test_abi.py)
 EXPORTED = ['fslr_abi_version', 'fslr_last_error', 'fslr_ctx_create', 'fslr_ctx_destroy', 'fslr_set_profiling',
             'fslr_set_reads', 'fslr_set_thresholds', 'fslr_reserve_edges', 'fslr_reserve_deferred',
-            'fslr_build_index', 'fslr_query',
+            'fslr_build_index', 'fslr_query', 'fslr_query_shard',
             'fslr_components', 'fslr_run', 'fslr_sync', 'fslr_read_stats', 'fslr_get_timings', 'fslr_read_counters',
             'fslr_get_labels',
             'fslr_get_fwd_degree', 'fslr_get_edges', 'fslr_labels_device_ptr', 'fslr_copy_labels_device',
@@ -94,6 +94,7 @@ def load(path: str = LIB_PATH):
         'fslr_reserve_deferred': (ctypes.c_int, [vp, i64]),
         'fslr_build_index': (ctypes.c_int, [vp]),
         'fslr_query': (ctypes.c_int, [vp, ctypes.POINTER(Params), i64, i64]),
+        'fslr_query_shard': (ctypes.c_int, [vp, ctypes.POINTER(Params), i32, i32]),
         'fslr_components': (ctypes.c_int, [vp]),
         'fslr_run': (ctypes.c_int, [vp, ctypes.POINTER(Params)]),
         'fslr_sync': (ctypes.c_int, [vp]),
@@ -199,6 +200,11 @@ class Context:
         p = self._params(qlen_cut, nal_cut, pass_table, edge_threshold)
         a_end = self.n_reads if a_end is None else a_end
         self._check(self._L.fslr_query(self._h, ctypes.byref(p), int(a_begin), int(a_end)))
+
+    def query_shard(self, qlen_cut, nal_cut, pass_table, shard, n_shards, edge_threshold=10):
+        """Query shard `shard` of `n_shards` (rank blocks of 64 dealt round robin; fslr_query_shard)."""
+        p = self._params(qlen_cut, nal_cut, pass_table, edge_threshold)
+        self._check(self._L.fslr_query_shard(self._h, ctypes.byref(p), int(shard), int(n_shards)))
 
     def components(self):
         self._check(self._L.fslr_components(self._h))

@@ -353,10 +353,22 @@ int fslr_build_index(fslr_ctx* c) {
   return FSLR_OK;
 }
 
+static int query_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_t a_end, int shard, int n_shards);
+
 int fslr_query(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_t a_end) {
   if (!c || !p || !p->pass_table) return FSLR_ERR_INVALID;
-  if (!c->index_built) return fail(c, FSLR_ERR_STATE, "fslr_build_index first");
   if (a_begin < 0 || a_end > c->n || a_begin > a_end) return fail(c, FSLR_ERR_INVALID, "bad read range");
+  return query_impl(c, p, a_begin, a_end, 0, 1);
+}
+
+int fslr_query_shard(fslr_ctx* c, const fslr_params* p, int32_t shard, int32_t n_shards) {
+  if (!c || !p || !p->pass_table) return FSLR_ERR_INVALID;
+  if (n_shards < 1 || shard < 0 || shard >= n_shards) return fail(c, FSLR_ERR_INVALID, "bad shard");
+  return query_impl(c, p, 0, c->n, shard, n_shards);
+}
+
+static int query_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_t a_end, int shard, int n_shards) {
+  if (!c->index_built) return fail(c, FSLR_ERR_STATE, "fslr_build_index first");
   HIP_TRY(c, hipSetDevice(c->device));
   if (c->edge_cap == 0) {
     int rc = fslr_reserve_edges(c, std::max<int64_t>(1 << 16, 12 * c->n));
@@ -400,6 +412,8 @@ int fslr_query(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_t a_end
   g.nal_cut = p->nal_cut;
   g.a_begin = static_cast<int>(a_begin);
   g.a_end = static_cast<int>(a_end);
+  g.shard = shard;
+  g.n_shards = n_shards;
   g.edges = c->edges;
   g.edge_iu = c->edge_iu;
   g.edge_cap = c->edge_cap;

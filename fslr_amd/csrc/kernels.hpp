@@ -65,6 +65,7 @@ struct QueryArgs {
   int4* lb;                           // [N] scratch: per query read {qlo, qhi, nlo, nhi} (length gate)
   double qlen_cut, nal_cut;
   int a_begin, a_end;
+  int shard, n_shards;                // query reads: blocks of 64 ranks of [a_begin, a_end) dealt round robin
   int2* edges;
   unsigned short* edge_iu;
   long long edge_cap;

@@ -30,6 +30,8 @@ namespace fslr {
 namespace {
 
 constexpr int kWavesPerBlock = 4;
+constexpr int kShardShift = 6;            // query shards own blocks of 64 consecutive ranks
+constexpr int kShardMask = (1 << kShardShift) - 1;
 constexpr int kBlock = kWave * kWavesPerBlock;
 constexpr int kStageCap = kWave;          // LDS staging of edges / deferred entries (flush before overflow)
 constexpr int kHashBits = 9;
@@ -253,11 +255,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
   unsigned epoch = 0;
   // edge iff U <= umax[I-1] (cluster.py:218-219 folded on the host); lane l holds umax[l]
   const int umax_v = g.umax[lane];
-  // rank assignment: grid-stride, 4 consecutive ranks per workgroup.  (Slicing each stride of
-  // ranks by XCD for L2 sharing between reads of one event measured no gain.)
+  // rank assignment: grid-stride over a virtual index v, 4 consecutive v per workgroup.  A query
+  // shard (multi-GPU) owns blocks of 64 consecutive ranks dealt round robin, which balances the
+  // shards (low ranks have more higher-rank partners); one shard: rank = a_begin + v.
   const int nwaves = gridDim.x * kWavesPerBlock;
   const int a_hi = g.a_end;
-  const int a_first = g.a_begin + blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
+  auto rank_of = [&](int v) {
+    return g.a_begin + ((((v >> kShardShift) * g.n_shards + g.shard) << kShardShift) | (v & kShardMask));
+  };
+  int v = blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
   unsigned long long w_eval = 0, w_jacc = 0, w_cand = 0, w_over = 0, w_ml = 0, w_mp = 0;
   // algorithmic bytes of evaluated pairs: 16 (LA + LB) + 32 each
   unsigned long long w_la_pairs = 0;
@@ -269,11 +275,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
   SEC_NOW(t_wave);
   // read pipeline: headers (scalar loads) two reads ahead, intervals one read ahead — the next
   // read's rows are requested when this read starts, so they land during its walk
-  int a = a_first;
+  int a = rank_of(v);
   const int2* rm2 = reinterpret_cast<const int2*>(g.rmeta);     // {iv offset, len | flags << 16}
   int2 am = make_int2(0, 0), am_n = make_int2(0, 0);
   if (a < a_hi) am = sload2(rm2, 2 * a);
-  if (a + nwaves < a_hi) am_n = sload2(rm2, 2 * (a + nwaves));
+  if (rank_of(v + nwaves) < a_hi) am_n = sload2(rm2, 2 * rank_of(v + nwaves));
   // lane i of A: my = {start, end, thr} of interval i, rg = {q, n_fwd, bwd_begin} (kernels.hpp)
   int3 my = make_int3(0, 0, 0), rg = make_int3(0, 0, 0);
   if (a < a_hi && lane < (am.y & 0xffff)) {
@@ -281,16 +287,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
     rg = load3(g.iv_rng, am.x + lane, 0);
   }
 
-  for (; a < a_hi; a += nwaves) {
+  for (; a < a_hi; v += nwaves, a = rank_of(v)) {
     SEC_NOW(t_s0);
-    const int a_next = a + nwaves;
+    const int a_next = rank_of(v + nwaves), a_nn = rank_of(v + 2 * nwaves);
     int3 my_next = make_int3(0, 0, 0), rg_next = make_int3(0, 0, 0);
     if (a_next < a_hi && lane < (am_n.y & 0xffff)) {
       my_next = load3(g.iv, am_n.x + lane, 1);
       rg_next = load3(g.iv_rng, am_n.x + lane, 0);
     }
     int2 am_nn = make_int2(0, 0);
-    if (a_next + nwaves < a_hi) am_nn = sload2(rm2, 2 * (a_next + nwaves));
+    if (a_nn < a_hi) am_nn = sload2(rm2, 2 * a_nn);
     const int4 alb = sload4(g.lb, a);
     if (++epoch > kEpochMax) {
       wave_lds_sync();
@@ -662,9 +668,10 @@ int resident_blocks() {
 }  // namespace
 
 hipError_t launch_query(const QueryArgs& a, int thr_mode, hipStream_t s) {
-  const long long nq = static_cast<long long>(a.a_end) - a.a_begin;
-  if (nq > 0) {
-    k_len_bounds<<<grid_for(nq), 256, 0, s>>>(a.rmeta, a.a_begin, a.a_end, a.qlen_cut, a.nal_cut, a.lb);
+  const long long span = static_cast<long long>(a.a_end) - a.a_begin;
+  const long long nq = (span + a.n_shards - 1) / a.n_shards + kShardMask;   // reads of this shard (bound)
+  if (span > 0) {
+    k_len_bounds<<<grid_for(span), 256, 0, s>>>(a.rmeta, a.a_begin, a.a_end, a.qlen_cut, a.nal_cut, a.lb);
     const long long want = (nq + kWavesPerBlock - 1) / kWavesPerBlock;
     if (thr_mode == 0) {
       const int cap = resident_blocks<0>();

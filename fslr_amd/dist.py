@@ -1,8 +1,10 @@
 """Multi-GPU sharding of the pair space (one process per GPU, torch.distributed over RCCL).
 
-Partition: query reads are split into contiguous rank ranges,
-one per process; every process holds the full CSR and index in its HBM and
-evaluates the pairs (A, B) with A in its range and B > A.  Pair evaluation needs
+Partition: query reads are split into blocks of SHARD_BLOCK
+consecutive ranks dealt round robin to the processes (fslr_query_shard; low
+ranks have more higher-rank partners, so contiguous ranges would not balance);
+every process holds the full CSR and index in its HBM and evaluates the pairs
+(A, B) with A in its shard and B > A.  Pair evaluation needs
 no communication.  The one real exchange is connectivity: each process unions
 its own edges into a forest whose labels are min-rank roots, the label vectors
 (int32[N], 4 MB at 1M reads) are all-gathered over RCCL, and every process
@@ -16,6 +18,14 @@ all found by the shard that owns it); they are summed only for reporting.
 from __future__ import annotations
 
 import numpy as np
+
+
+SHARD_BLOCK = 64     # query.hip kShardShift
+
+
+def shard_of(reads, world: int):
+    """Shard owning each read rank under fslr_query_shard (blocks of 64 ranks, round robin)."""
+    return (np.asarray(reads) // SHARD_BLOCK) % world
 
 
 def shard_range(n_reads: int, rank: int, world: int):

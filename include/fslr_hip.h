@@ -15,6 +15,7 @@
  *                         different_lengths_or_alignments (:178-183),
  *                         overall_jaccard_similarity (:140-170),
  *                         calculate_overlap (:133-136), cutoff lookup (:218-219)
+ *   fslr_query_shard      the same over one multi-GPU shard of the query reads
  *   fslr_components       cluster.py:230-234  get_subgraphs (networkx
  *                         connected_components)
  *   fslr_union_pairs      (multi-GPU merge of per-shard component labels; no
@@ -143,6 +144,10 @@ int  fslr_build_index(fslr_ctx *ctx);
  * [a_begin, a_end) against every read of higher rank.  Async; stats are read
  * with fslr_read_stats. */
 int  fslr_query(fslr_ctx *ctx, const fslr_params *params, int64_t a_begin, int64_t a_end);
+/* Multi-GPU query shard: the reads of rank blocks [64 k, 64 k + 64) with k % n_shards == shard
+ * (balanced: low ranks have more higher-rank partners).  The shards of 0..n_shards-1 together
+ * evaluate exactly the pairs of fslr_query(ctx, params, 0, n_reads).  Async. */
+int  fslr_query_shard(fslr_ctx *ctx, const fslr_params *params, int32_t shard, int32_t n_shards);
 /* cluster.py:230-234 — union-find over the edges: label = min rank in component.  Async. */
 int  fslr_components(fslr_ctx *ctx);
 /* build_index + query(all reads) + components, enqueued back to back.  Async. */

@@ -15,7 +15,7 @@ import numpy as np
 import pytest
 
 from fslr_amd import synth
-from fslr_amd.dist import merge_label_sets, shard_range, union_find_labels
+from fslr_amd.dist import merge_label_sets, shard_of, shard_range, union_find_labels
 from oracle import oracle as O
 
 
@@ -54,6 +54,14 @@ def world_case():
     return csr, o
 
 
+def test_shard_of_balances_and_partitions():
+    n = 1_000_003
+    for world in (2, 3, 8):
+        sh = shard_of(np.arange(n), world)
+        counts = np.bincount(sh, minlength=world)
+        assert counts.sum() == n and counts.max() - counts.min() <= 64
+
+
 def test_shards_partition_evaluated_pairs(world_case):
     """Pairs are owned by their lower-rank read: per-shard oracle counts add up to the whole."""
     csr, o = world_case
@@ -80,8 +88,7 @@ def _gloo_worker(rank, world, port, n, ea, eb, out_dir):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
     dist.init_process_group('gloo', rank=rank, world_size=world)
-    a0, a1 = shard_range(n, rank, world)
-    mine = (ea >= a0) & (ea < a1)
+    mine = shard_of(ea, world) == rank
     local = union_find_labels(n, ea[mine], eb[mine])
     t = torch.from_numpy(local.astype(np.int64))
     gathered = [torch.empty_like(t) for _ in range(world)]
@@ -131,8 +138,7 @@ def test_device_shard_merge_two_contexts_one_gpu(monkeypatch):
         c.load_csr(csr, thr)
         c.reserve_edges(12 * n)
         c.build_index()
-        a0, a1 = shard_range(n, r, 2)
-        c.query(1 - 0.04, 1 - 0.25, pt, 10, a0, a1)
+        c.query_shard(1 - 0.04, 1 - 0.25, pt, r, 2)
         c.components()
         ctxs.append(c)
         merges.append(DeviceShardMerge(c, n, 2, r, dev))
@@ -162,5 +168,10 @@ def test_device_shard_merge_two_contexts_one_gpu(monkeypatch):
     st = [c.stats() for c in ctxs]
     assert sum(x['evaluated_pairs'] for x in st) == o['stats']['evaluated_pairs']
     assert sum(x['n_edges'] for x in st) == o['edge_a'].size
+    # each shard's edges are exactly the oracle edges whose lower-rank read it owns
+    for r, c in enumerate(ctxs):
+        a, b, I, U = c.edges(st[r]['n_edges'])
+        mine = shard_of(o['edge_a'], 2) == r
+        assert sorted(zip(a.tolist(), b.tolist())) == sorted(zip(o['edge_a'][mine].tolist(), o['edge_b'][mine].tolist()))
     for c in ctxs + [ref]:
         c.close()

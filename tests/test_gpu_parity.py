@@ -314,3 +314,32 @@ def test_length_gate_boundaries_vs_oracle(ctx, qlen_diff, nal_diff):
                    use_cap=False)
     assert st['overflow_candidates'] > 0
     compare_with_oracle(g, o, n)
+
+
+@pytest.mark.parametrize('n_shards', [2, 3, 8])
+def test_query_shards_partition_the_pairs(ctx, n_shards):
+    """fslr_query_shard over all shards evaluates exactly the pairs and edges of one full query."""
+    s = synth.generate(25_000, 16, 19)
+    csr = s.interval_data().csr()
+    o = O.run_core(oracle_from_csr(csr), use_cap=False)
+    thr = fold_overlap_threshold(csr.iv_aln, 0.8)
+    ctx.load_csr(csr, thr)
+    ctx.reserve_edges(12 * csr.n_reads)
+    ctx.build_index()
+    pt = pass_table([1, 1, 0.66, 0.66, 0.66, 0.5])
+    edges, pairs = [], 0
+    fwd = np.zeros(csr.n_reads, np.int64)
+    for r in range(n_shards):
+        ctx.query_shard(1 - 0.04, 1 - 0.25, pt, r, n_shards)
+        st = ctx.stats()
+        pairs += st['evaluated_pairs']
+        a, b, I, U = ctx.edges(st['n_edges'])
+        assert np.all((a // 64) % n_shards == r)
+        edges += list(zip(a.tolist(), b.tolist(), I.tolist(), U.tolist()))
+        f = ctx.fwd_degree()
+        own = (np.arange(csr.n_reads) // 64) % n_shards == r
+        fwd[own] = f[own]
+    assert pairs == o['stats']['evaluated_pairs']
+    oe = sorted(zip(o['edge_a'].tolist(), o['edge_b'].tolist(), o['edge_I'].tolist(), o['edge_U'].tolist()))
+    assert sorted(edges) == oe
+    np.testing.assert_array_equal(fwd, o['fwd'])
