@@ -38,7 +38,7 @@ struct fslr_ctx {
   int* vals = nullptr;
   int* vals2 = nullptr;
   unsigned long long* endkey = nullptr;
-  unsigned long long* pmaxkey = nullptr;
+  unsigned long long* pmaxkey = nullptr;   // per 256-position tile: max (chrom, end) key, then its scan
   void* temp = nullptr;
   size_t temp_bytes = 0;
   int* umax = nullptr;     // [FSLR_MAX_L] derived from the pass table
@@ -101,7 +101,7 @@ int ensure_capacity(fslr_ctx* c, int64_t n, int64_t ni, int n_chroms) {
         (rc = dalloc(c, &c->idx_gate, ni)) || (rc = dalloc(c, &c->data_pos, ni)) ||
         (rc = dalloc(c, &c->dchrom, ni)) || (rc = dalloc(c, &c->drec, ni)) || (rc = dalloc(c, &c->s_start, ni)) ||
         (rc = dalloc(c, &c->keys, ni)) || (rc = dalloc(c, &c->keys2, ni)) || (rc = dalloc(c, &c->vals, ni)) ||
-        (rc = dalloc(c, &c->vals2, ni)) || (rc = dalloc(c, &c->endkey, ni)) || (rc = dalloc(c, &c->pmaxkey, ni)) ||
+        (rc = dalloc(c, &c->vals2, ni)) || (rc = dalloc(c, &c->endkey, ni)) || (rc = dalloc(c, &c->pmaxkey, 2 * (ni / 256) + ni / (256 * 1024) + 8)) ||
         (rc = dalloc(c, &c->thr_tmp, ni)))
       return rc;
     c->cap_ni = ni;

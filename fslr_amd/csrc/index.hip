@@ -7,9 +7,12 @@
 //   2. per sorted position q (coalesced): the read's packed gate fields, start, (chrom, end) key
 // General path (CSR only): radix sort of (chrom << 32 | start) → gather the records.
 // Then, both paths:
-//   3. inclusive max-scan of (chrom << 32 | end): per-chromosome prefix max of end (pmax)
+//   3. per 256-position tile, the max of (chrom << 32 | end) (written by k_finish), and their
+//      inclusive max-scan (one small block): the per-chromosome prefix max of end (pmax) at tile
+//      granularity — pmax at any position is the previous tile's prefix and a scan inside the tile
 //   4. scan ranges per interval, searched in an LDS window of starts / pmax around the block
-//      (galloping out of the window in global memory when a range is longer):
+//      (pmax rebuilt in LDS from the tile prefix; galloping out of the window in global memory
+//      when a range is longer):
 //        n_fwd     = #{p > q : start_p <= end_q}        (all overlap: start_q <= start_p <= end_q)
 //        bwd_begin = first p with pmax_p >= start_q     (p < q with pmax < start_q cannot overlap)
 //      so a query interval's end-inclusive overlaps (superintervals search_values semantics,
@@ -22,6 +25,7 @@ namespace fslr {
 namespace {
 
 constexpr int kRangeBlock = 256;
+constexpr int kTile = kRangeBlock;      // pmax tiles == range blocks (window edges are tile-aligned)
 constexpr int kWin = 512;
 
 __global__ void k_keys_csr(const int4* __restrict__ rmeta, const int4* __restrict__ iv, int n,
@@ -48,52 +52,140 @@ __global__ void k_gather_records(const int* __restrict__ stags, const int4* __re
   }
 }
 
-// per sorted position: gate fields of the read, start, (chrom, end) key
+__device__ __forceinline__ unsigned long long max_u64(unsigned long long a, unsigned long long b) {
+  return a > b ? a : b;
+}
+
+// per sorted position: gate fields of the read, start, (chrom, end) key; per tile of kTile
+// positions (one block iteration): the max key
 template <bool kKey64>
-__global__ void k_finish(const int4* __restrict__ idx4, const void* __restrict__ skeys,
-                         const int4* __restrict__ rmeta, int ni, int2* __restrict__ idx_gate,
-                         int* __restrict__ s_start, unsigned long long* __restrict__ endkey) {
-  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < ni; q += gridDim.x * blockDim.x) {
-    const int4 rec = idx4[q];
-    const int4 m = rmeta[rec.w >> 6];
-    const unsigned c = kKey64 ? static_cast<unsigned>(static_cast<const unsigned long long*>(skeys)[q] >> 32)
-                              : static_cast<const unsigned*>(skeys)[q];
-    // {qlen2, nal | LB << 24 | haz << 31}
-    idx_gate[q] = make_int2(m.z, (m.w & 0xFFFFFF) | ((m.y & 0x7F) << 24) | (((m.y >> 16) & 1) << 31));
-    s_start[q] = rec.x;
-    endkey[q] = (static_cast<unsigned long long>(c) << 32) | static_cast<unsigned>(rec.y);
+__global__ __launch_bounds__(kTile) void k_finish(const int4* __restrict__ idx4, const void* __restrict__ skeys,
+                                                  const int4* __restrict__ rmeta, int ni, int2* __restrict__ idx_gate,
+                                                  int* __restrict__ s_start, unsigned long long* __restrict__ endkey,
+                                                  unsigned long long* __restrict__ tile_max) {
+  __shared__ unsigned long long wmax[kTile / 64];
+  const int n_tiles = (ni + kTile - 1) / kTile;
+  for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+    const int q = t * kTile + threadIdx.x;
+    unsigned long long key = 0ull;
+    if (q < ni) {
+      const int4 rec = idx4[q];
+      const int4 m = rmeta[rec.w >> 6];
+      const unsigned c = kKey64 ? static_cast<unsigned>(static_cast<const unsigned long long*>(skeys)[q] >> 32)
+                                : static_cast<const unsigned*>(skeys)[q];
+      // {qlen2, nal | LB << 24 | haz << 31}
+      idx_gate[q] = make_int2(m.z, (m.w & 0xFFFFFF) | ((m.y & 0x7F) << 24) | (((m.y >> 16) & 1) << 31));
+      s_start[q] = rec.x;
+      key = (static_cast<unsigned long long>(c) << 32) | static_cast<unsigned>(rec.y);
+      endkey[q] = key;
+    }
+    for (int o = 32; o > 0; o >>= 1) key = max_u64(key, __shfl_xor(key, o));
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = key;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long mx = wmax[0];
+      for (int w = 1; w < kTile / 64; ++w) mx = max_u64(mx, wmax[w]);
+      tile_max[t] = mx;
+    }
+    __syncthreads();
   }
 }
 
-struct MaxU64 {
-  __device__ __forceinline__ unsigned long long operator()(unsigned long long a, unsigned long long b) const {
-    return a > b ? a : b;
+// inclusive max-scan of the tile maxima in two levels: groups of 1024 tiles (one block each,
+// coalesced) hold local inclusive prefixes and a group total; one block scans the group totals.
+// The inclusive prefix of tile t is max(group_excl[t / 1024], tile_loc[t]).
+constexpr int kGroup = 1024;
+
+__global__ __launch_bounds__(kGroup) void k_tile_scan_local(const unsigned long long* __restrict__ tile_max, int nt,
+                                                            unsigned long long* __restrict__ tile_loc,
+                                                            unsigned long long* __restrict__ group_tot) {
+  __shared__ unsigned long long part[kGroup];
+  const int t = blockIdx.x * kGroup + threadIdx.x;
+  part[threadIdx.x] = t < nt ? tile_max[t] : 0ull;
+  __syncthreads();
+  for (int o = 1; o < kGroup; o <<= 1) {
+    const unsigned long long v = threadIdx.x >= o ? part[threadIdx.x - o] : 0ull;
+    __syncthreads();
+    part[threadIdx.x] = max_u64(part[threadIdx.x], v);
+    __syncthreads();
   }
+  if (t < nt) tile_loc[t] = part[threadIdx.x];
+  if (threadIdx.x == kGroup - 1) group_tot[blockIdx.x] = part[kGroup - 1];
+}
+
+__global__ __launch_bounds__(kGroup) void k_group_scan(unsigned long long* __restrict__ group, int ng) {
+  __shared__ unsigned long long part[kGroup];
+  const int per = (ng + kGroup - 1) / kGroup;
+  const int b = threadIdx.x * per, e = min(b + per, ng);
+  unsigned long long m = 0ull;
+  for (int i = b; i < e; ++i) m = max_u64(m, group[i]);
+  part[threadIdx.x] = m;
+  __syncthreads();
+  for (int o = 1; o < kGroup; o <<= 1) {
+    const unsigned long long v = threadIdx.x >= o ? part[threadIdx.x - o] : 0ull;
+    __syncthreads();
+    part[threadIdx.x] = max_u64(part[threadIdx.x], v);
+    __syncthreads();
+  }
+  m = threadIdx.x > 0 ? part[threadIdx.x - 1] : 0ull;     // exclusive prefix of this thread's groups
+  for (int i = b; i < e; ++i) {
+    const unsigned long long tot = group[i];
+    group[i] = m;                                           // in place: exclusive prefix per group
+    m = max_u64(m, tot);
+  }
+}
+
+struct TilePrefix {
+  const unsigned long long* loc;
+  const unsigned long long* group_excl;
+  __device__ __forceinline__ unsigned long long incl(int t) const { return max_u64(group_excl[t / kGroup], loc[t]); }
 };
-
-__device__ __forceinline__ int pmax_at(const unsigned long long* pmaxkey, int p) {
-  return static_cast<int>(static_cast<unsigned>(pmaxkey[p]));
-}
 
 __global__ __launch_bounds__(kRangeBlock) void k_ranges(const int4* __restrict__ idx4, const int4* __restrict__ rmeta,
                                                         const int* __restrict__ s_start,
                                                         const unsigned long long* __restrict__ endkey,
-                                                        const unsigned long long* __restrict__ pmaxkey,
+                                                        TilePrefix tile_incl,
                                                         const int2* __restrict__ crange, int ni,
                                                         int4* __restrict__ iv_rng) {
   __shared__ int w_st[kRangeBlock + 2 * kWin];   // starts of [w0, w1)
-  __shared__ int w_pm[kRangeBlock + kWin];       // pmax of [w0, q0 + kRangeBlock)
+  __shared__ int w_pm[kRangeBlock + kWin];       // pmax (end part) of [w0, q0 + kRangeBlock)
+  __shared__ unsigned long long t_part[kRangeBlock];
   const int q0 = blockIdx.x * kRangeBlock;
-  const int w0 = max(q0 - kWin, 0);
+  const int w0 = max(q0 - kWin, 0);              // tile-aligned
   const int w1 = min(q0 + kRangeBlock + kWin, ni);
   const int wp1 = min(q0 + kRangeBlock, ni);
   for (int t = threadIdx.x; t < w1 - w0; t += kRangeBlock) w_st[t] = s_start[w0 + t];
-  for (int t = threadIdx.x; t < wp1 - w0; t += kRangeBlock) w_pm[t] = pmax_at(pmaxkey, w0 + t);
+  // pmax over [w0, wp1): prefix of the tiles before w0, then a scan of the window's keys
+  {
+    constexpr int kPer = (kRangeBlock + kWin) / kRangeBlock;   // consecutive keys per thread
+    unsigned long long k[kPer];
+    unsigned long long m = 0ull;
+    for (int u = 0; u < kPer; ++u) {
+      const int p = w0 + threadIdx.x * kPer + u;
+      k[u] = p < wp1 ? endkey[p] : 0ull;
+      m = max_u64(m, k[u]);
+    }
+    t_part[threadIdx.x] = m;
+    __syncthreads();
+    for (int o = 1; o < kRangeBlock; o <<= 1) {
+      const unsigned long long v = threadIdx.x >= o ? t_part[threadIdx.x - o] : 0ull;
+      __syncthreads();
+      t_part[threadIdx.x] = max_u64(t_part[threadIdx.x], v);
+      __syncthreads();
+    }
+    m = w0 > 0 ? tile_incl.incl(w0 / kTile - 1) : 0ull;
+    if (threadIdx.x > 0) m = max_u64(m, t_part[threadIdx.x - 1]);
+    for (int u = 0; u < kPer; ++u) {
+      m = max_u64(m, k[u]);
+      w_pm[threadIdx.x * kPer + u] = static_cast<int>(static_cast<unsigned>(m));
+    }
+  }
   __syncthreads();
   const int q = q0 + threadIdx.x;
   if (q >= ni) return;
   const unsigned long long ek = endkey[q];
-  const int2 cr = crange[static_cast<int>(ek >> 32)];
+  const int c = static_cast<int>(ek >> 32);
+  const int2 cr = crange[c];
   const int s = w_st[q - w0], e = static_cast<int>(static_cast<unsigned>(ek));
   // forward: first p in (q, cr.y) with start_p > e
   int hi_lim = min(cr.y, w1);
@@ -125,19 +217,23 @@ __global__ __launch_bounds__(kRangeBlock) void k_ranges(const int4* __restrict__
     const int mid = (lo + hi) >> 1;
     if (w_pm[mid - w0] >= s) hi = mid; else lo = mid + 1;
   }
-  if (lo == lo_lim && lo_lim > cr.x && lo < q) {   // may extend below the window
-    hi = lo;
-    int step = 1;
-    int cand = lo - 1;
-    while (cand >= cr.x && pmax_at(pmaxkey, cand) >= s) {
-      hi = cand;
-      cand = hi - step;
-      step <<= 1;
+  if (lo == lo_lim && lo_lim > cr.x && lo < q) {
+    // the answer may lie below the window: first tile (from the chromosome's) whose inclusive
+    // prefix reaches (c, s), then the first position inside it
+    const unsigned long long key = (static_cast<unsigned long long>(c) << 32) | static_cast<unsigned>(s);
+    int tb = cr.x / kTile, te = w0 / kTile;
+    while (tb < te) {
+      const int mid = (tb + te) >> 1;
+      if (tile_incl.incl(mid) >= key) te = mid; else tb = mid + 1;
     }
-    lo = cand < cr.x ? cr.x : cand + 1;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (pmax_at(pmaxkey, mid) >= s) hi = mid; else lo = mid + 1;
+    if (tb < w0 / kTile) {
+      unsigned long long m = tb > 0 ? tile_incl.incl(tb - 1) : 0ull;
+      int p = tb * kTile;
+      for (; p < w0; ++p) {
+        m = max_u64(m, endkey[p]);
+        if (m >= key) break;
+      }
+      lo = max(p, cr.x);
     }
   }
   const int rj = idx4[q].w;
@@ -173,9 +269,6 @@ hipError_t index_temp_bytes(int ni, size_t* bytes, hipStream_t s) {
                                          static_cast<unsigned*>(nullptr), static_cast<int4*>(nullptr),
                                          static_cast<int4*>(nullptr), ni, 0, 32, s);
   if (e != hipSuccess) return e;
-  e = hipcub::DeviceScan::InclusiveScan(nullptr, b2, static_cast<unsigned long long*>(nullptr),
-                                        static_cast<unsigned long long*>(nullptr), MaxU64(), ni, s);
-  if (e != hipSuccess) return e;
   *bytes = b1 > b2 ? b1 : b2;
   if (b3 > *bytes) *bytes = b3;
   return hipSuccess;
@@ -189,20 +282,24 @@ hipError_t launch_build_index(const IndexBufs& b, int n, int ni, int n_chroms, h
     unsigned* k32 = reinterpret_cast<unsigned*>(b.keys2);
     e = hipcub::DeviceRadixSort::SortPairs(b.temp, tb, b.dchrom, k32, b.drec, b.idx4, ni, 0, bits_for(n_chroms), s);
     if (e != hipSuccess) return e;
-    k_finish<false><<<grid_for(ni), 256, 0, s>>>(b.idx4, k32, b.rmeta, ni, b.idx_gate, b.s_start, b.endkey);
+    k_finish<false><<<grid_for(ni, kTile), kTile, 0, s>>>(b.idx4, k32, b.rmeta, ni, b.idx_gate, b.s_start, b.endkey,
+                                                          b.pmaxkey);
   } else {
     k_keys_csr<<<grid_for(n), 256, 0, s>>>(b.rmeta, b.iv, n, b.keys, b.vals);
     e = hipcub::DeviceRadixSort::SortPairs(b.temp, tb, b.keys, b.keys2, b.vals, b.vals2, ni, 0,
                                            32 + bits_for(n_chroms), s);
     if (e != hipSuccess) return e;
     k_gather_records<<<grid_for(ni), 256, 0, s>>>(b.vals2, b.iv, b.rmeta, ni, b.idx4);
-    k_finish<true><<<grid_for(ni), 256, 0, s>>>(b.idx4, b.keys2, b.rmeta, ni, b.idx_gate, b.s_start, b.endkey);
+    k_finish<true><<<grid_for(ni, kTile), kTile, 0, s>>>(b.idx4, b.keys2, b.rmeta, ni, b.idx_gate, b.s_start, b.endkey,
+                                                         b.pmaxkey);
   }
-  tb = b.temp_bytes;
-  e = hipcub::DeviceScan::InclusiveScan(b.temp, tb, b.endkey, b.pmaxkey, MaxU64(), ni, s);
-  if (e != hipSuccess) return e;
-  k_ranges<<<(ni + kRangeBlock - 1) / kRangeBlock, kRangeBlock, 0, s>>>(b.idx4, b.rmeta, b.s_start, b.endkey,
-                                                                         b.pmaxkey, b.crange, ni, b.iv_rng);
+  // pmaxkey: tile maxima [0, nt), local group prefixes [nt, 2 nt), group prefixes [2 nt, 2 nt + ng)
+  const int nt = (ni + kTile - 1) / kTile, ng = (nt + kGroup - 1) / kGroup;
+  unsigned long long *tmax = b.pmaxkey, *tloc = b.pmaxkey + nt, *grp = b.pmaxkey + 2 * nt;
+  k_tile_scan_local<<<ng, kGroup, 0, s>>>(tmax, nt, tloc, grp);
+  k_group_scan<<<1, kGroup, 0, s>>>(grp, ng);
+  k_ranges<<<nt, kRangeBlock, 0, s>>>(b.idx4, b.rmeta, b.s_start, b.endkey, TilePrefix{tloc, grp}, b.crange, ni,
+                                      b.iv_rng);
   return hipGetLastError();
 }
 
