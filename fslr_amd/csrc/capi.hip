@@ -23,7 +23,8 @@ struct fslr_ctx {
   // device buffers
   int4* rmeta = nullptr;
   int4* iv = nullptr;
-  int4* iv_rng = nullptr;
+  int* qpos = nullptr;       // [NI] CSR interval -> its position in the sorted index
+  int2* rng_s = nullptr;     // [NI] sorted position -> {n_fwd, bwd_begin}
   int4* idx4 = nullptr;
   int2* idx_gate = nullptr;
   unsigned long long* defer = nullptr;
@@ -97,7 +98,7 @@ int ensure_capacity(fslr_ctx* c, int64_t n, int64_t ni, int n_chroms) {
     c->cap_n = n;
   }
   if (ni > c->cap_ni) {
-    if ((rc = dalloc(c, &c->iv, ni)) || (rc = dalloc(c, &c->iv_rng, ni)) || (rc = dalloc(c, &c->idx4, ni)) ||
+    if ((rc = dalloc(c, &c->iv, ni)) || (rc = dalloc(c, &c->qpos, ni)) || (rc = dalloc(c, &c->rng_s, ni)) || (rc = dalloc(c, &c->idx4, ni)) ||
         (rc = dalloc(c, &c->idx_gate, ni)) || (rc = dalloc(c, &c->data_pos, ni)) ||
         (rc = dalloc(c, &c->dchrom, ni)) || (rc = dalloc(c, &c->drec, ni)) || (rc = dalloc(c, &c->s_start, ni)) ||
         (rc = dalloc(c, &c->keys, ni)) || (rc = dalloc(c, &c->keys2, ni)) || (rc = dalloc(c, &c->vals, ni)) ||
@@ -167,7 +168,7 @@ void fslr_ctx_destroy(fslr_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* bufs[] = {c->rmeta,  c->iv,     c->iv_rng,  c->idx4,    c->idx_gate, c->data_pos, c->s_start,
+  void* bufs[] = {c->rmeta,  c->iv,     c->qpos,    c->rng_s,  c->idx4,    c->idx_gate, c->data_pos, c->s_start,
                   c->crange, c->keys,   c->keys2,   c->vals,    c->vals2,   c->endkey,  c->pmaxkey,
                   c->temp,   c->umax,   c->edges,   c->edge_iu, c->fwd,     c->parent,  c->counters,
                   c->errw,   c->thr_tmp, c->defer,   c->dchrom,  c->drec,    c->lbounds};
@@ -293,7 +294,7 @@ int fslr_set_thresholds(fslr_ctx* c, const int32_t* thr) {
       return fail(c, FSLR_ERR_INVALID, "FSLR_THR_ZERO_ALN must mark the same intervals as in fslr_set_reads");
   if (c->ni) {
     HIP_TRY(c, hipMemcpyAsync(c->thr_tmp, thr, c->ni * sizeof(int), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(c, launch_set_thr(c->thr_tmp, c->iv, c->iv_rng, c->index_built ? c->idx4 : nullptr, c->data_pos,
+    HIP_TRY(c, launch_set_thr(c->thr_tmp, c->iv, c->qpos, c->index_built ? c->idx4 : nullptr, c->data_pos,
                               c->have_data_pos ? c->drec : nullptr, static_cast<int>(c->ni), c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
   }
@@ -343,7 +344,8 @@ int fslr_build_index(fslr_ctx* c) {
   b.temp = c->temp;
   b.temp_bytes = c->temp_bytes;
   b.crange = c->crange;
-  b.iv_rng = c->iv_rng;
+  b.qpos = c->qpos;
+  b.rng_s = c->rng_s;
   b.idx4 = c->idx4;
   b.idx_gate = c->idx_gate;
   HIP_TRY(c, launch_build_index(b, static_cast<int>(c->n), static_cast<int>(c->ni), c->n_chroms, c->stream));
@@ -401,7 +403,8 @@ static int query_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_
   QueryArgs g;
   g.rmeta = c->rmeta;
   g.iv = c->iv;
-  g.iv_rng = c->iv_rng;
+  g.qpos = c->qpos;
+  g.rng_s = c->rng_s;
   g.idx4 = c->idx4;
   g.idx_gate = c->idx_gate;
   g.defer = c->defer;

@@ -62,7 +62,7 @@ template <bool kKey64>
 __global__ __launch_bounds__(kTile) void k_finish(const int4* __restrict__ idx4, const void* __restrict__ skeys,
                                                   const int4* __restrict__ rmeta, int ni, int2* __restrict__ idx_gate,
                                                   int* __restrict__ s_start, unsigned long long* __restrict__ endkey,
-                                                  unsigned long long* __restrict__ tile_max) {
+                                                  unsigned long long* __restrict__ tile_max, int* __restrict__ qpos) {
   __shared__ unsigned long long wmax[kTile / 64];
   const int n_tiles = (ni + kTile - 1) / kTile;
   for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
@@ -76,6 +76,7 @@ __global__ __launch_bounds__(kTile) void k_finish(const int4* __restrict__ idx4,
       // {qlen2, nal | LB << 24 | haz << 31}
       idx_gate[q] = make_int2(m.z, (m.w & 0xFFFFFF) | ((m.y & 0x7F) << 24) | (((m.y >> 16) & 1) << 31));
       s_start[q] = rec.x;
+      qpos[m.x + (rec.w & 63)] = q;     // CSR interval -> sorted position (the one scatter of the build)
       key = (static_cast<unsigned long long>(c) << 32) | static_cast<unsigned>(rec.y);
       endkey[q] = key;
     }
@@ -141,12 +142,11 @@ struct TilePrefix {
   __device__ __forceinline__ unsigned long long incl(int t) const { return max_u64(group_excl[t / kGroup], loc[t]); }
 };
 
-__global__ __launch_bounds__(kRangeBlock) void k_ranges(const int4* __restrict__ idx4, const int4* __restrict__ rmeta,
-                                                        const int* __restrict__ s_start,
+__global__ __launch_bounds__(kRangeBlock) void k_ranges(const int* __restrict__ s_start,
                                                         const unsigned long long* __restrict__ endkey,
                                                         TilePrefix tile_incl,
                                                         const int2* __restrict__ crange, int ni,
-                                                        int4* __restrict__ iv_rng) {
+                                                        int2* __restrict__ rng_s) {
   __shared__ int w_st[kRangeBlock + 2 * kWin];   // starts of [w0, w1)
   __shared__ int w_pm[kRangeBlock + kWin];       // pmax (end part) of [w0, q0 + kRangeBlock)
   __shared__ unsigned long long t_part[kRangeBlock];
@@ -236,16 +236,15 @@ __global__ __launch_bounds__(kRangeBlock) void k_ranges(const int4* __restrict__
       lo = max(p, cr.x);
     }
   }
-  const int rj = idx4[q].w;
-  iv_rng[rmeta[rj >> 6].x + (rj & 63)] = make_int4(q, n_fwd, lo, q - lo);
+  rng_s[q] = make_int2(n_fwd, lo);
 }
 
-__global__ void k_set_thr(const int* __restrict__ thr, int4* __restrict__ iv, const int4* __restrict__ iv_rng,
+__global__ void k_set_thr(const int* __restrict__ thr, int4* __restrict__ iv, const int* __restrict__ qpos,
                           int4* __restrict__ idx4, const int* __restrict__ data_pos, int4* __restrict__ drec,
                           int ni) {
   for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < ni; k += gridDim.x * blockDim.x) {
     iv[k].w = thr[k];
-    if (idx4) idx4[iv_rng[k].x].z = thr[k];
+    if (idx4) idx4[qpos[k]].z = thr[k];
     if (drec) drec[data_pos[k]].z = thr[k];
   }
 }
@@ -283,7 +282,7 @@ hipError_t launch_build_index(const IndexBufs& b, int n, int ni, int n_chroms, h
     e = hipcub::DeviceRadixSort::SortPairs(b.temp, tb, b.dchrom, k32, b.drec, b.idx4, ni, 0, bits_for(n_chroms), s);
     if (e != hipSuccess) return e;
     k_finish<false><<<grid_for(ni, kTile), kTile, 0, s>>>(b.idx4, k32, b.rmeta, ni, b.idx_gate, b.s_start, b.endkey,
-                                                          b.pmaxkey);
+                                                          b.pmaxkey, b.qpos);
   } else {
     k_keys_csr<<<grid_for(n), 256, 0, s>>>(b.rmeta, b.iv, n, b.keys, b.vals);
     e = hipcub::DeviceRadixSort::SortPairs(b.temp, tb, b.keys, b.keys2, b.vals, b.vals2, ni, 0,
@@ -291,22 +290,21 @@ hipError_t launch_build_index(const IndexBufs& b, int n, int ni, int n_chroms, h
     if (e != hipSuccess) return e;
     k_gather_records<<<grid_for(ni), 256, 0, s>>>(b.vals2, b.iv, b.rmeta, ni, b.idx4);
     k_finish<true><<<grid_for(ni, kTile), kTile, 0, s>>>(b.idx4, b.keys2, b.rmeta, ni, b.idx_gate, b.s_start, b.endkey,
-                                                         b.pmaxkey);
+                                                         b.pmaxkey, b.qpos);
   }
   // pmaxkey: tile maxima [0, nt), local group prefixes [nt, 2 nt), group prefixes [2 nt, 2 nt + ng)
   const int nt = (ni + kTile - 1) / kTile, ng = (nt + kGroup - 1) / kGroup;
   unsigned long long *tmax = b.pmaxkey, *tloc = b.pmaxkey + nt, *grp = b.pmaxkey + 2 * nt;
   k_tile_scan_local<<<ng, kGroup, 0, s>>>(tmax, nt, tloc, grp);
   k_group_scan<<<1, kGroup, 0, s>>>(grp, ng);
-  k_ranges<<<nt, kRangeBlock, 0, s>>>(b.idx4, b.rmeta, b.s_start, b.endkey, TilePrefix{tloc, grp}, b.crange, ni,
-                                      b.iv_rng);
+  k_ranges<<<nt, kRangeBlock, 0, s>>>(b.s_start, b.endkey, TilePrefix{tloc, grp}, b.crange, ni, b.rng_s);
   return hipGetLastError();
 }
 
-hipError_t launch_set_thr(const int* thr, int4* iv, const int4* iv_rng, int4* idx4, const int* data_pos,
+hipError_t launch_set_thr(const int* thr, int4* iv, const int* qpos, int4* idx4, const int* data_pos,
                           int4* drec, int ni, hipStream_t s) {
   if (ni <= 0) return hipSuccess;
-  k_set_thr<<<grid_for(ni), 256, 0, s>>>(thr, iv, iv_rng, idx4, data_pos, drec, ni);
+  k_set_thr<<<grid_for(ni), 256, 0, s>>>(thr, iv, qpos, idx4, data_pos, drec, ni);
   return hipGetLastError();
 }
 

@@ -3,10 +3,10 @@
 // Device layout (all in HBM, see DESIGN.md "Data layout"):
 //   rmeta[N]    int4 {iv offset, len | flags<<16, qlen2, n_alignments}       rank order
 //   iv[NI]      int4 {chrom, start, end, thr}                                 CSR (rank, data order)
-//   iv_rng[NI]  int4 {q, n_fwd, bwd_begin, n_bwd}                             per CSR interval:
-//               q = its position in the (chrom,start)-sorted index; sorted positions
-//               q+1 .. q+n_fwd all overlap it (start <= end_q); bwd_begin .. q-1 are the
-//               earlier positions whose prefix-max end reaches start_q (hit iff end >= start_q)
+//   qpos[NI]    int  q = position of CSR interval k in the (chrom,start)-sorted index
+//   rng_s[NI]   int2 {n_fwd, bwd_begin} per sorted position q: positions q+1 .. q+n_fwd all
+//               overlap it (start <= end_q); bwd_begin .. q-1 are the earlier positions whose
+//               prefix-max end reaches start_q (hit iff end >= start_q)
 //   idx4[NI]    int4 {start, end, thr, read << 6 | j} of the interval at sorted position
 //   idx_gate[NI] int2 {qlen2, nal | LB << 24 | haz << 31} of the read at sorted position
 //               (the pair gate's inputs, read beside the hit; nal < 2^24 is validated)
@@ -43,22 +43,24 @@ struct IndexBufs {
   void* temp;
   size_t temp_bytes;
   const int2* crange;                 // [n_chroms] {begin, end} in sorted order (host counts)
-  int4* iv_rng;                       // out [NI]
+  int* qpos;                          // out [NI] CSR order
+  int2* rng_s;                        // out [NI] sorted order
   int4* idx4;                         // out [NI]
   int2* idx_gate;                     // out [NI]
 };
 // bytes of hipcub temp storage the index build needs for ni intervals
 hipError_t index_temp_bytes(int ni, size_t* bytes, hipStream_t s);
 hipError_t launch_build_index(const IndexBufs& b, int n_reads, int ni, int n_chroms, hipStream_t s);
-// thresholds into iv[k].w and (when the index exists) idx4[iv_rng[k].x].z
-hipError_t launch_set_thr(const int* thr, int4* iv, const int4* iv_rng, int4* idx4, const int* data_pos,
+// thresholds into iv[k].w and (when the index exists) idx4[qpos[k]].z
+hipError_t launch_set_thr(const int* thr, int4* iv, const int* qpos, int4* idx4, const int* data_pos,
                           int4* drec, int ni, hipStream_t s);
 
 // ---- pair kernel (query.hip) -------------------------------------------------------------
 struct QueryArgs {
   const int4* rmeta;
   const int4* iv;
-  const int4* iv_rng;
+  const int* qpos;
+  const int2* rng_s;
   const int4* idx4;
   const int2* idx_gate;
   const int* umax;                    // [64]: pair with I matches is an edge iff U <= umax[I-1]

@@ -4,7 +4,7 @@
 //
 // query_kernel — one wavefront per query read A (grid-stride over ranks a in [a_begin, a_end));
 // A's intervals live in lanes 0..LA-1 and are read with v_readlane / ds_bpermute.
-//  1. candidate walk: A's scan ranges (kernels.hpp: iv_rng) are flattened with a wave prefix sum
+//  1. candidate walk: A's scan ranges (kernels.hpp: rng_s) are flattened with a wave prefix sum
 //     and walked 64 records per step, one record per lane; the next step's records (and the next
 //     read's header) are loaded while the current step is processed.  Forward records are hits,
 //     backward records hit iff end >= start_i.
@@ -273,30 +273,35 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
   unsigned long long sec[kSections] = {};
 #endif
   SEC_NOW(t_wave);
-  // read pipeline: headers (scalar loads) two reads ahead, intervals one read ahead — the next
-  // read's rows are requested when this read starts, so they land during its walk
+  // read pipeline: headers (scalar loads) three reads ahead, the sorted positions of a read's
+  // intervals (qpos, coalesced) two ahead, its rows in the index one ahead — so a read's rows are
+  // requested when the previous read starts, from positions that arrived one read earlier
   int a = rank_of(v);
   const int2* rm2 = reinterpret_cast<const int2*>(g.rmeta);     // {iv offset, len | flags << 16}
-  int2 am = make_int2(0, 0), am_n = make_int2(0, 0);
-  if (a < a_hi) am = sload2(rm2, 2 * a);
-  if (rank_of(v + nwaves) < a_hi) am_n = sload2(rm2, 2 * rank_of(v + nwaves));
+  auto hdr = [&](int r) { return r < a_hi ? sload2(rm2, 2 * r) : make_int2(0, 0); };
+  auto qpos_of = [&](int r, int2 h) { return r < a_hi && lane < (h.y & 0xffff) ? g.qpos[h.x + lane] : 0; };
   // lane i of A: my = {start, end, thr} of interval i, rg = {q, n_fwd, bwd_begin} (kernels.hpp)
-  int3 my = make_int3(0, 0, 0), rg = make_int3(0, 0, 0);
-  if (a < a_hi && lane < (am.y & 0xffff)) {
-    my = load3(g.iv, am.x + lane, 1);
-    rg = load3(g.iv_rng, am.x + lane, 0);
-  }
+  auto rows = [&](int r, int2 h, int q, int3& m, int3& rr) {
+    m = make_int3(0, 0, 0);
+    rr = make_int3(0, 0, 0);
+    if (r < a_hi && lane < (h.y & 0xffff)) {
+      m = load3(g.idx4, q, 0);
+      const int2 rs = g.rng_s[q];
+      rr = make_int3(q, rs.x, rs.y);
+    }
+  };
+  int2 am = hdr(a), am_n = hdr(rank_of(v + nwaves)), am_nn = hdr(rank_of(v + 2 * nwaves));
+  int3 my, rg;
+  rows(a, am, qpos_of(a, am), my, rg);
+  int qv_n = qpos_of(rank_of(v + nwaves), am_n);
 
   for (; a < a_hi; v += nwaves, a = rank_of(v)) {
     SEC_NOW(t_s0);
     const int a_next = rank_of(v + nwaves), a_nn = rank_of(v + 2 * nwaves);
-    int3 my_next = make_int3(0, 0, 0), rg_next = make_int3(0, 0, 0);
-    if (a_next < a_hi && lane < (am_n.y & 0xffff)) {
-      my_next = load3(g.iv, am_n.x + lane, 1);
-      rg_next = load3(g.iv_rng, am_n.x + lane, 0);
-    }
-    int2 am_nn = make_int2(0, 0);
-    if (a_nn < a_hi) am_nn = sload2(rm2, 2 * a_nn);
+    int3 my_next, rg_next;
+    rows(a_next, am_n, qv_n, my_next, rg_next);
+    const int qv_nn = qpos_of(a_nn, am_nn);
+    const int2 am_nnn = hdr(rank_of(v + 3 * nwaves));
     const int4 alb = sload4(g.lb, a);
     if (++epoch > kEpochMax) {
       wave_lds_sync();
@@ -538,6 +543,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
     w_maxfwd = max(w_maxfwd, fwdA);
     am = am_n;
     am_n = am_nn;
+    am_nn = am_nnn;
+    qv_n = qv_nn;
     my = my_next;
     rg = rg_next;
   }
