@@ -27,6 +27,17 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK = 8.0e12          # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
+TRAFFIC_JSON = os.path.join(REPO, 'profiles', 'pmc_traffic_latest.json')
+
+
+def kernel_source_hash():
+    """sha256 of the pair-kernel sources: ties a committed PMC summary to the code it measured."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in ('query.hip', 'kernels.hpp'):
+        with open(os.path.join(REPO, 'fslr_amd', 'csrc', f), 'rb') as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def parse():
@@ -42,8 +53,9 @@ def parse():
                     help='query reads in the bounded CPU-oracle baseline sample (0 = skip)')
     ap.add_argument('--verify', action='store_true',
                     help='after timing, rank 0 checks its labels against a single-context run of all reads')
-    ap.add_argument('--traffic-json', default=None,
-                    help='rocprofv3 PMC summary (tools/pmc_traffic.py) giving HBM bytes per launch')
+    ap.add_argument('--traffic-json', default=TRAFFIC_JSON,
+                    help='rocprofv3 PMC summary (tools/pmc_traffic.py) giving HBM bytes per launch; used only '
+                         'when it was measured on the current pair-kernel sources')
     return ap.parse_args()
 
 
@@ -154,9 +166,13 @@ def main():
     # per-launch algorithmic bytes of this rank's pair kernel (SURVEY §8d B_pair summed over its pairs)
     achieved = st['algo_bytes'] / (kernel_ms / 1000.0)
     traffic = None
+    traffic_src = None
     if args.traffic_json and os.path.exists(args.traffic_json):
         with open(args.traffic_json) as fh:
-            traffic = json.load(fh).get('query_kernel_hbm_bytes_per_launch')
+            tj = json.load(fh)
+        if tj.get('source_hash') == kernel_source_hash():
+            traffic = tj.get('query_kernel_hbm_bytes_per_launch')
+            traffic_src = os.path.relpath(args.traffic_json, REPO)
 
     verified = None
     if args.verify and rank == 0:
@@ -208,6 +224,7 @@ def main():
                 'unit': 'GB/s',
                 'frac': achieved / HBM_PEAK,
                 'traffic': traffic,
+                'traffic_source': traffic_src,
                 'kernel_ms': kernel_ms,
                 'algo_bytes_per_launch': int(st['algo_bytes']),
                 'phase_ms_last_step': lib_t,

@@ -14,3 +14,7 @@ for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_
       --output-format csv -- python3 $ROOT/bench.py --steps 2 --warmup 1 --cpu-sample-reads 0 "$@" \
       > $ROOT/$OUT/p$i.log 2>&1
 done
+cd $ROOT
+H=$(python3 -c "import bench; print(bench.kernel_source_hash())")
+python3 tools/pmc_traffic.py $ROOT/$OUT --source-hash $H -o $ROOT/$OUT/traffic.json > /dev/null
+echo "traffic summary: $OUT/traffic.json (source $H)"
