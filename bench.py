@@ -103,6 +103,8 @@ def main():
     pt = pass_table([1, 1, 0.66, 0.66, 0.66, 0.5])
     qcut, ncut = 1 - 0.04, 1 - 0.25
     merge = DeviceShardMerge(ctx, csr.n_reads, world, rank, dev) if world > 1 else None
+    if world > 1:
+        ctx.set_shard(rank, world)      # query-side index data (positions, ranges) for this shard's reads
 
     ev_q0 = torch.cuda.Event(enable_timing=True)
     ev_q1 = torch.cuda.Event(enable_timing=True)
@@ -177,7 +179,7 @@ def main():
     verified = None
     if args.verify and rank == 0:
         got = ctx.labels()
-        ref = _lib.Context(dev_index)
+        ref = _lib.Context(dev_index)      # full, unsharded
         ref.load_csr(csr, thr)
         ref.reserve_edges(12 * csr.n_reads)
         ref.run(qcut, ncut, pt)

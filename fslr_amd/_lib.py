@@ -22,7 +22,7 @@ PASS_STRIDE = 2 * FSLR_MAX_L
 # every symbol include/fslr_hip.h declares (checked by tests/test_abi.py)
 EXPORTED = ['fslr_abi_version', 'fslr_last_error', 'fslr_ctx_create', 'fslr_ctx_destroy', 'fslr_set_profiling',
             'fslr_set_reads', 'fslr_set_thresholds', 'fslr_reserve_edges', 'fslr_reserve_deferred',
-            'fslr_build_index', 'fslr_query', 'fslr_query_shard',
+            'fslr_set_shard', 'fslr_build_index', 'fslr_query', 'fslr_query_shard',
             'fslr_components', 'fslr_run', 'fslr_sync', 'fslr_read_stats', 'fslr_get_timings', 'fslr_read_counters',
             'fslr_get_labels',
             'fslr_get_fwd_degree', 'fslr_get_edges', 'fslr_labels_device_ptr', 'fslr_copy_labels_device',
@@ -92,6 +92,7 @@ def load(path: str = LIB_PATH):
         'fslr_set_thresholds': (ctypes.c_int, [vp, vp]),
         'fslr_reserve_edges': (ctypes.c_int, [vp, i64]),
         'fslr_reserve_deferred': (ctypes.c_int, [vp, i64]),
+        'fslr_set_shard': (ctypes.c_int, [vp, i32, i32]),
         'fslr_build_index': (ctypes.c_int, [vp]),
         'fslr_query': (ctypes.c_int, [vp, ctypes.POINTER(Params), i64, i64]),
         'fslr_query_shard': (ctypes.c_int, [vp, ctypes.POINTER(Params), i32, i32]),
@@ -200,6 +201,10 @@ class Context:
         p = self._params(qlen_cut, nal_cut, pass_table, edge_threshold)
         a_end = self.n_reads if a_end is None else a_end
         self._check(self._L.fslr_query(self._h, ctypes.byref(p), int(a_begin), int(a_end)))
+
+    def set_shard(self, shard: int, n_shards: int):
+        """Build the query-side index data only for shard `shard` of `n_shards` (fslr_set_shard)."""
+        self._check(self._L.fslr_set_shard(self._h, int(shard), int(n_shards)))
 
     def query_shard(self, qlen_cut, nal_cut, pass_table, shard, n_shards, edge_threshold=10):
         """Query shard `shard` of `n_shards` (rank blocks of 64 dealt round robin; fslr_query_shard)."""

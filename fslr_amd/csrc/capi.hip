@@ -20,6 +20,8 @@ struct fslr_ctx {
   int n_chroms = 0;
   int thr_mode = 0;
   bool reads_set = false, index_built = false, have_data_pos = false;
+  int shard = 0, n_shards = 1;             // fslr_set_shard: A-side index data for this shard only
+  int built_shard = 0, built_n_shards = 1;
   // device buffers
   int4* rmeta = nullptr;
   int4* iv = nullptr;
@@ -294,6 +296,7 @@ int fslr_set_thresholds(fslr_ctx* c, const int32_t* thr) {
       return fail(c, FSLR_ERR_INVALID, "FSLR_THR_ZERO_ALN must mark the same intervals as in fslr_set_reads");
   if (c->ni) {
     HIP_TRY(c, hipMemcpyAsync(c->thr_tmp, thr, c->ni * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    if (c->index_built && c->built_n_shards != 1) c->index_built = false;   // qpos is partial: rebuild
     HIP_TRY(c, launch_set_thr(c->thr_tmp, c->iv, c->qpos, c->index_built ? c->idx4 : nullptr, c->data_pos,
                               c->have_data_pos ? c->drec : nullptr, static_cast<int>(c->ni), c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -324,6 +327,14 @@ int fslr_reserve_deferred(fslr_ctx* c, int64_t capacity) {
   return FSLR_OK;
 }
 
+int fslr_set_shard(fslr_ctx* c, int32_t shard, int32_t n_shards) {
+  if (!c) return FSLR_ERR_INVALID;
+  if (n_shards < 1 || shard < 0 || shard >= n_shards) return fail(c, FSLR_ERR_INVALID, "bad shard");
+  c->shard = shard;
+  c->n_shards = n_shards;
+  return FSLR_OK;
+}
+
 int fslr_build_index(fslr_ctx* c) {
   if (!c) return FSLR_ERR_INVALID;
   if (!c->reads_set) return fail(c, FSLR_ERR_STATE, "fslr_set_reads first");
@@ -332,6 +343,8 @@ int fslr_build_index(fslr_ctx* c) {
   IndexBufs b;
   b.rmeta = c->rmeta;
   b.iv = c->iv;
+  b.shard = c->shard;
+  b.n_shards = c->n_shards;
   b.dchrom = c->have_data_pos ? c->dchrom : nullptr;
   b.drec = c->have_data_pos ? c->drec : nullptr;
   b.keys = c->keys;
@@ -352,6 +365,8 @@ int fslr_build_index(fslr_ctx* c) {
   if (c->profiling) HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));
   c->t_index_rec = c->profiling;
   c->index_built = true;
+  c->built_shard = c->shard;
+  c->built_n_shards = c->n_shards;
   return FSLR_OK;
 }
 
@@ -360,12 +375,16 @@ static int query_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_
 int fslr_query(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_t a_end) {
   if (!c || !p || !p->pass_table) return FSLR_ERR_INVALID;
   if (a_begin < 0 || a_end > c->n || a_begin > a_end) return fail(c, FSLR_ERR_INVALID, "bad read range");
+  if (c->index_built && c->built_n_shards != 1)
+    return fail(c, FSLR_ERR_STATE, "index built for one shard (fslr_set_shard): use fslr_query_shard");
   return query_impl(c, p, a_begin, a_end, 0, 1);
 }
 
 int fslr_query_shard(fslr_ctx* c, const fslr_params* p, int32_t shard, int32_t n_shards) {
   if (!c || !p || !p->pass_table) return FSLR_ERR_INVALID;
   if (n_shards < 1 || shard < 0 || shard >= n_shards) return fail(c, FSLR_ERR_INVALID, "bad shard");
+  if (c->index_built && c->built_n_shards != 1 && (c->built_shard != shard || c->built_n_shards != n_shards))
+    return fail(c, FSLR_ERR_STATE, "index built for another shard");
   return query_impl(c, p, 0, c->n, shard, n_shards);
 }
 

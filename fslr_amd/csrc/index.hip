@@ -62,7 +62,8 @@ template <bool kKey64>
 __global__ __launch_bounds__(kTile) void k_finish(const int4* __restrict__ idx4, const void* __restrict__ skeys,
                                                   const int4* __restrict__ rmeta, int ni, int2* __restrict__ idx_gate,
                                                   int* __restrict__ s_start, unsigned long long* __restrict__ endkey,
-                                                  unsigned long long* __restrict__ tile_max, int* __restrict__ qpos) {
+                                                  unsigned long long* __restrict__ tile_max, int* __restrict__ qpos,
+                                                  int shard, int n_shards) {
   __shared__ unsigned long long wmax[kTile / 64];
   const int n_tiles = (ni + kTile - 1) / kTile;
   for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
@@ -76,7 +77,8 @@ __global__ __launch_bounds__(kTile) void k_finish(const int4* __restrict__ idx4,
       // {qlen2, nal | LB << 24 | haz << 31}
       idx_gate[q] = make_int2(m.z, (m.w & 0xFFFFFF) | ((m.y & 0x7F) << 24) | (((m.y >> 16) & 1) << 31));
       s_start[q] = rec.x;
-      qpos[m.x + (rec.w & 63)] = q;     // CSR interval -> sorted position (the one scatter of the build)
+      // CSR interval -> sorted position (the one scatter of the build; this shard's reads only)
+      if (shard_owns(rec.w >> 6, shard, n_shards)) qpos[m.x + (rec.w & 63)] = q;
       key = (static_cast<unsigned long long>(c) << 32) | static_cast<unsigned>(rec.y);
       endkey[q] = key;
     }
@@ -142,7 +144,8 @@ struct TilePrefix {
   __device__ __forceinline__ unsigned long long incl(int t) const { return max_u64(group_excl[t / kGroup], loc[t]); }
 };
 
-__global__ __launch_bounds__(kRangeBlock) void k_ranges(const int* __restrict__ s_start,
+__global__ __launch_bounds__(kRangeBlock) void k_ranges(const int4* __restrict__ idx4, int shard, int n_shards,
+                                                        const int* __restrict__ s_start,
                                                         const unsigned long long* __restrict__ endkey,
                                                         TilePrefix tile_incl,
                                                         const int2* __restrict__ crange, int ni,
@@ -183,6 +186,7 @@ __global__ __launch_bounds__(kRangeBlock) void k_ranges(const int* __restrict__ 
   __syncthreads();
   const int q = q0 + threadIdx.x;
   if (q >= ni) return;
+  if (n_shards > 1 && !shard_owns(idx4[q].w >> 6, shard, n_shards)) return;   // another shard's A side
   const unsigned long long ek = endkey[q];
   const int c = static_cast<int>(ek >> 32);
   const int2 cr = crange[c];
@@ -282,7 +286,7 @@ hipError_t launch_build_index(const IndexBufs& b, int n, int ni, int n_chroms, h
     e = hipcub::DeviceRadixSort::SortPairs(b.temp, tb, b.dchrom, k32, b.drec, b.idx4, ni, 0, bits_for(n_chroms), s);
     if (e != hipSuccess) return e;
     k_finish<false><<<grid_for(ni, kTile), kTile, 0, s>>>(b.idx4, k32, b.rmeta, ni, b.idx_gate, b.s_start, b.endkey,
-                                                          b.pmaxkey, b.qpos);
+                                                          b.pmaxkey, b.qpos, b.shard, b.n_shards);
   } else {
     k_keys_csr<<<grid_for(n), 256, 0, s>>>(b.rmeta, b.iv, n, b.keys, b.vals);
     e = hipcub::DeviceRadixSort::SortPairs(b.temp, tb, b.keys, b.keys2, b.vals, b.vals2, ni, 0,
@@ -290,14 +294,15 @@ hipError_t launch_build_index(const IndexBufs& b, int n, int ni, int n_chroms, h
     if (e != hipSuccess) return e;
     k_gather_records<<<grid_for(ni), 256, 0, s>>>(b.vals2, b.iv, b.rmeta, ni, b.idx4);
     k_finish<true><<<grid_for(ni, kTile), kTile, 0, s>>>(b.idx4, b.keys2, b.rmeta, ni, b.idx_gate, b.s_start, b.endkey,
-                                                         b.pmaxkey, b.qpos);
+                                                         b.pmaxkey, b.qpos, b.shard, b.n_shards);
   }
   // pmaxkey: tile maxima [0, nt), local group prefixes [nt, 2 nt), group prefixes [2 nt, 2 nt + ng)
   const int nt = (ni + kTile - 1) / kTile, ng = (nt + kGroup - 1) / kGroup;
   unsigned long long *tmax = b.pmaxkey, *tloc = b.pmaxkey + nt, *grp = b.pmaxkey + 2 * nt;
   k_tile_scan_local<<<ng, kGroup, 0, s>>>(tmax, nt, tloc, grp);
   k_group_scan<<<1, kGroup, 0, s>>>(grp, ng);
-  k_ranges<<<nt, kRangeBlock, 0, s>>>(b.s_start, b.endkey, TilePrefix{tloc, grp}, b.crange, ni, b.rng_s);
+  k_ranges<<<nt, kRangeBlock, 0, s>>>(b.idx4, b.shard, b.n_shards, b.s_start, b.endkey, TilePrefix{tloc, grp},
+                                      b.crange, ni, b.rng_s);
   return hipGetLastError();
 }
 

@@ -21,6 +21,11 @@ namespace fslr {
 constexpr int kWave = 64;
 constexpr int kPassStride = 128;      // 2 * FSLR_MAX_L
 constexpr int kMaxCoord = 1 << 30;
+constexpr int kShardShift = 6;        // query shards own blocks of 64 consecutive ranks, round robin
+
+__host__ __device__ inline bool shard_owns(int read, int shard, int n_shards) {
+  return n_shards == 1 || ((read >> kShardShift) % n_shards) == shard;
+}
 
 enum Counter { kEdgeCount = 0, kEval = 1, kJacc = 2, kCand = 3, kAlgoBytes = 4, kOverflow = 5, kGather = 6,
                kMatchEntries = 7, kMatchedPairs = 8, kDeferCount = 9,
@@ -29,6 +34,7 @@ enum Counter { kEdgeCount = 0, kEval = 1, kJacc = 2, kCand = 3, kAlgoBytes = 4, 
 
 // ---- index build (index.hip) -------------------------------------------------------------
 struct IndexBufs {
+  int shard, n_shards;                // A-side outputs (qpos, rng_s) only for reads of this query shard
   const int4* rmeta;
   const int4* iv;
   const unsigned* dchrom;             // [NI] or nullptr: chromosome per data position (start-sorted

@@ -30,8 +30,7 @@ namespace fslr {
 namespace {
 
 constexpr int kWavesPerBlock = 4;
-constexpr int kShardShift = 6;            // query shards own blocks of 64 consecutive ranks
-constexpr int kShardMask = (1 << kShardShift) - 1;
+constexpr int kShardMask = (1 << kShardShift) - 1;   // kernels.hpp: kShardShift
 constexpr int kBlock = kWave * kWavesPerBlock;
 constexpr int kStageCap = kWave;          // LDS staging of edges / deferred entries (flush before overflow)
 constexpr int kHashBits = 9;

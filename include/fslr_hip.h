@@ -138,6 +138,10 @@ int  fslr_reserve_edges(fslr_ctx *ctx, int64_t capacity);
 /* Deferred-pair list capacity (pairs evaluated by gathering intervals); grows only. */
 int  fslr_reserve_deferred(fslr_ctx *ctx, int64_t capacity);
 
+/* Multi-GPU: build the query-side index data (positions, scan ranges) only for the reads of
+ * query shard `shard` of `n_shards` (see fslr_query_shard); the walked index stays complete.
+ * Takes effect at the next fslr_build_index; fslr_query then needs n_shards == 1. */
+int  fslr_set_shard(fslr_ctx *ctx, int32_t shard, int32_t n_shards);
 /* cluster.py:124-130 — sort intervals by (chrom, start), prefix-max of end. Async. */
 int  fslr_build_index(fslr_ctx *ctx);
 /* cluster.py:187-227 — all candidate pairs of query reads with rank in

@@ -137,6 +137,7 @@ def test_device_shard_merge_two_contexts_one_gpu(monkeypatch):
         c = _lib.Context(0, stream=stream.cuda_stream)
         c.load_csr(csr, thr)
         c.reserve_edges(12 * n)
+        c.set_shard(r, 2)                # shard-restricted query-side index data, as bench.py
         c.build_index()
         c.query_shard(1 - 0.04, 1 - 0.25, pt, r, 2)
         c.components()

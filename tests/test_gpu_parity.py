@@ -343,3 +343,33 @@ def test_query_shards_partition_the_pairs(ctx, n_shards):
     oe = sorted(zip(o['edge_a'].tolist(), o['edge_b'].tolist(), o['edge_I'].tolist(), o['edge_U'].tolist()))
     assert sorted(edges) == oe
     np.testing.assert_array_equal(fwd, o['fwd'])
+
+
+def test_shard_built_index_matches_full_index():
+    """fslr_set_shard: an index whose query-side data covers one shard gives that shard exactly
+    the edges of a fully built index; the full-range query is refused on it."""
+    s = synth.generate(25_000, 16, 29)
+    csr = s.interval_data().csr()
+    thr = fold_overlap_threshold(csr.iv_aln, 0.8)
+    pt = pass_table([1, 1, 0.66, 0.66, 0.66, 0.5])
+    full = _lib.Context(0)
+    full.load_csr(csr, thr)
+    full.reserve_edges(12 * csr.n_reads)
+    full.build_index()
+    for r in range(4):
+        c = _lib.Context(0)
+        c.load_csr(csr, thr)
+        c.reserve_edges(12 * csr.n_reads)
+        c.set_shard(r, 4)
+        c.build_index()
+        c.query_shard(1 - 0.04, 1 - 0.25, pt, r, 4)
+        st = c.stats()
+        full.query_shard(1 - 0.04, 1 - 0.25, pt, r, 4)
+        sf = full.stats()
+        assert st['evaluated_pairs'] == sf['evaluated_pairs']
+        assert sorted(zip(*[x.tolist() for x in c.edges(st['n_edges'])])) == \
+            sorted(zip(*[x.tolist() for x in full.edges(sf['n_edges'])]))
+        with pytest.raises(_lib.FslrError):
+            c.query(1 - 0.04, 1 - 0.25, pt)
+        c.close()
+    full.close()
