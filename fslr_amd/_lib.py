@@ -256,7 +256,7 @@ class Context:
         self._check(self._L.fslr_get_timings(self._h, ctypes.byref(t)))
         return t.as_dict()
 
-    def counters(self, n: int = 32) -> np.ndarray:
+    def counters(self, n: int = 80) -> np.ndarray:
         """Raw device counters of the last query (kernels.hpp Counter; diagnostics)."""
         out = np.zeros(n, np.uint64)
         got = self._L.fslr_read_counters(self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), n)

@@ -52,6 +52,9 @@ struct fslr_ctx {
   int* fwd = nullptr;
   int* parent = nullptr;
   unsigned long long* counters = nullptr;
+  unsigned long long* wstat = nullptr;       // [wstat_waves x kWStride] per-wave statistics of the pair kernel
+  int wstat_waves = 0;
+  unsigned long long* diag = nullptr;        // FSLR_SECTION_PROF builds: per-read timing of the pair kernel
   int* errw = nullptr;     // [0..2] error, [3] max_fwd
   int* thr_tmp = nullptr;
   int64_t cap_n = 0, cap_ni = 0, cap_chroms = 0;
@@ -97,6 +100,9 @@ int ensure_capacity(fslr_ctx* c, int64_t n, int64_t ni, int n_chroms) {
     if ((rc = dalloc(c, &c->rmeta, n)) || (rc = dalloc(c, &c->fwd, n)) || (rc = dalloc(c, &c->parent, n)) ||
         (rc = dalloc(c, &c->lbounds, n)))
       return rc;
+#ifdef FSLR_SECTION_PROF
+    if ((rc = dalloc(c, &c->diag, 2 * n))) return rc;
+#endif
     c->cap_n = n;
   }
   if (ni > c->cap_ni) {
@@ -173,7 +179,7 @@ void fslr_ctx_destroy(fslr_ctx* c) {
   void* bufs[] = {c->rmeta,  c->iv,     c->qpos,    c->rng_s,  c->idx4,    c->idx_gate, c->data_pos, c->s_start,
                   c->crange, c->keys,   c->keys2,   c->vals,    c->vals2,   c->endkey,  c->pmaxkey,
                   c->temp,   c->umax,   c->edges,   c->edge_iu, c->fwd,     c->parent,  c->counters,
-                  c->errw,   c->thr_tmp, c->defer,   c->dchrom,  c->drec,    c->lbounds};
+                  c->errw,   c->thr_tmp, c->defer,   c->dchrom,  c->drec,    c->lbounds, c->diag, c->wstat};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->ev_ok)
@@ -417,6 +423,12 @@ static int query_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_
                               c->stream));
   }
   HIP_TRY(c, hipMemsetAsync(c->counters, 0, kNumCounters * sizeof(unsigned long long), c->stream));
+  if (!c->wstat) {
+    const int w = query_max_waves();
+    int rc = dalloc(c, &c->wstat, static_cast<size_t>(w) * kWStride);
+    if (rc) return rc;
+    c->wstat_waves = w;
+  }
   HIP_TRY(c, hipMemsetAsync(c->errw, 0, 4 * sizeof(int), c->stream));
   if (c->n) HIP_TRY(c, hipMemsetAsync(c->fwd, 0, c->n * sizeof(int), c->stream));
   QueryArgs g;
@@ -443,6 +455,9 @@ static int query_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_
   g.counters = c->counters;
   g.err = c->errw;
   g.mode = c->ablate;
+  g.diag = c->diag;
+  g.wstat = c->wstat;
+  g.wstat_waves = c->wstat_waves;
   if (c->profiling) HIP_TRY(c, hipEventRecord(c->ev[2], c->stream));
   HIP_TRY(c, launch_query(g, c->thr_mode, c->stream));
   if (c->profiling) HIP_TRY(c, hipEventRecord(c->ev[3], c->stream));
@@ -477,6 +492,16 @@ int fslr_sync(fslr_ctx* c) {
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   return FSLR_OK;
 }
+
+#ifdef FSLR_SECTION_PROF
+// diagnostics of the section-timing build (not part of the C ABI): per-read timing of the last query
+extern "C" int fslr_prof_read_diag(fslr_ctx* c, uint64_t* out) {
+  if (!c || !out || !c->diag) return FSLR_ERR_INVALID;
+  HIP_TRY(c, hipMemcpyAsync(out, c->diag, 2 * c->n * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FSLR_OK;
+}
+#endif
 
 int fslr_read_counters(fslr_ctx* c, uint64_t* out, int n) {
   if (!c || !out || n < 0) return -FSLR_ERR_INVALID;

@@ -27,10 +27,20 @@ __host__ __device__ inline bool shard_owns(int read, int shard, int n_shards) {
   return n_shards == 1 || ((read >> kShardShift) % n_shards) == shard;
 }
 
-enum Counter { kEdgeCount = 0, kEval = 1, kJacc = 2, kCand = 3, kAlgoBytes = 4, kOverflow = 5, kGather = 6,
-               kMatchEntries = 7, kMatchedPairs = 8, kDeferCount = 9,
-               kSecBase = 16,           // FSLR_SECTION_PROF builds: per-section cycle sums of the pair kernel
-               kNumCounters = 32 };
+// Device counters.  The two hot atomics (edge / deferred appends) sit on cache lines of their own;
+// the pair kernel's per-wave statistics are plain stores into per-wave slots (`wstat`) summed by a
+// small reduction kernel, so no wave ever retires through a contended global atomic.
+enum Counter { kEdgeCount = 0,          // atomic (own 128-B line)
+               kDeferCount = 16,        // atomic (own 128-B line)
+               kEval = 32, kJacc = 33, kCand = 34, kAlgoBytes = 35, kOverflow = 36, kGather = 37,
+               kMatchEntries = 38, kMatchedPairs = 39, kMaxFwd = 40,
+               kSecBase = 48,           // FSLR_SECTION_PROF builds: per-section cycle sums of the pair kernel
+               kNumCounters = 80 };
+// per-wave statistics of query_kernel: fields 0..8 (sum, except kWsMaxFwd: max), then (section-
+// timing builds) 8 section sums, slowest read cycles (max), its rank, wave cycles max / min,
+// wave count, cycle sums of reads 0, 1 and >= 2 of the wave
+enum WaveStat { kWsEval = 0, kWsJacc, kWsCand, kWsAlgoBytes, kWsOverflow, kWsMatchEntries, kWsMatchedPairs,
+                kWsMaxFwd, kWsBase = 8, kWsProf = kWsBase + 16, kWStride = 32 };
 
 // ---- index build (index.hip) -------------------------------------------------------------
 struct IndexBufs {
@@ -83,9 +93,14 @@ struct QueryArgs {
   unsigned long long* counters;
   int* err;                           // [0] code, [1] a, [2] b, [3] max forward degree
   int mode;                           // profiling ablation (FSLR_ABLATE): 0 full, 1 scan only, 2 no greedy
+  unsigned long long* wstat;          // [wstat_waves x kWStride] per-wave statistics (plain stores)
+  int wstat_waves;
+  unsigned long long* diag;           // FSLR_SECTION_PROF: [N] per read (start cycle in its wave) << 32 | cycles
 };
 // thr_mode: 0 = every non-sentinel threshold >= 1 (fast match), 1 = general encoding
 hipError_t launch_query(const QueryArgs& a, int thr_mode, hipStream_t s);
+// waves of the largest query_kernel grid (the size of QueryArgs::wstat)
+int query_max_waves();
 
 // ---- components (components.hip) ---------------------------------------------------------
 hipError_t launch_uf_init(int* parent, int n, hipStream_t s);

@@ -24,6 +24,9 @@
 // partners than the hash holds (witness rule) — are appended to a deferred list for
 // deferred_kernel, one lane per pair, which gathers A's and B's intervals.
 #include "fslr_hip.h"
+#include <algorithm>
+#include <cstdlib>
+
 #include "kernels.hpp"
 
 namespace fslr {
@@ -270,6 +273,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
   int w_maxfwd = 0;
 #ifdef FSLR_SECTION_PROF
   unsigned long long sec[kSections] = {};
+  unsigned long long read_max = 0;
+  int read_max_a = -1;
+  unsigned long long it_sum[3] = {0, 0, 0};
+  int it_k = 0;
 #endif
   SEC_NOW(t_wave);
   // read pipeline: headers (scalar loads) three reads ahead, the sorted positions of a read's
@@ -296,6 +303,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
 
   for (; a < a_hi; v += nwaves, a = rank_of(v)) {
     SEC_NOW(t_s0);
+#ifdef FSLR_SECTION_PROF
+    const unsigned long long rt_s0 = __builtin_amdgcn_s_memrealtime();
+#endif
     const int a_next = rank_of(v + nwaves), a_nn = rank_of(v + 2 * nwaves);
     int3 my_next, rg_next;
     rows(a_next, am_n, qv_n, my_next, rg_next);
@@ -540,6 +550,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
     w_mp += mpn;
     if (lane == 0) g.fwd[a] = fwdA;
     w_maxfwd = max(w_maxfwd, fwdA);
+#ifdef FSLR_SECTION_PROF
+    {
+      const unsigned long long dt = __builtin_amdgcn_s_memtime() - t_s0;
+      if (dt > read_max) {
+        read_max = dt;
+        read_max_a = a;
+      }
+      it_sum[min(it_k, 2)] += dt;
+      ++it_k;
+      if (lane == 0 && g.diag) {
+        g.diag[2 * a] = rt_s0;
+        g.diag[2 * a + 1] = min(dt, 0xffffffffull) | (static_cast<unsigned long long>(__smid() & 0xffffu) << 32) |
+                            (static_cast<unsigned long long>(min(it_k, 4095)) << 48);
+      }
+    }
+#endif
     am = am_n;
     am_n = am_nn;
     am_nn = am_nnn;
@@ -553,18 +579,84 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
   unsigned long long l_bytes = l_lb;
   for (int o = 32; o > 0; o >>= 1) l_bytes += __shfl_xor(l_bytes, o);
   l_bytes = 16ull * (l_bytes + w_la_pairs) + 32ull * w_eval;
-  if (lane == 0) {
+  // per-wave statistics: one plain 8-B store per lane into this wave's slot (kernels.hpp WaveStat)
+  {
+    const int wid = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    unsigned long long f = 0;
+    f = lane == kWsEval ? w_eval : f;
+    f = lane == kWsJacc ? w_jacc : f;
+    f = lane == kWsCand ? w_cand : f;
+    f = lane == kWsAlgoBytes ? l_bytes : f;
+    f = lane == kWsOverflow ? w_over : f;
+    f = lane == kWsMatchEntries ? w_ml : f;
+    f = lane == kWsMatchedPairs ? w_mp : f;
+    f = lane == kWsMaxFwd ? static_cast<unsigned long long>(w_maxfwd) : f;
 #ifdef FSLR_SECTION_PROF
-    for (int k = 0; k < kSections; ++k) atomicAdd(&g.counters[kSecBase + k], sec[k]);
+    for (int k = 0; k < kSections; ++k) f = lane == kWsBase + k ? sec[k] : f;
+    f = lane == kWsBase + 8 ? read_max : f;
+    f = lane == kWsBase + 9 ? static_cast<unsigned long long>(read_max_a) : f;
+    f = lane == kWsBase + 10 ? sec[7] : f;
+    f = lane == kWsBase + 11 ? sec[7] : f;
+    f = lane == kWsBase + 12 ? 1ull : f;
+    for (int k = 0; k < 3; ++k) f = lane == kWsBase + 13 + k ? it_sum[k] : f;
 #endif
-    if (l_bytes) atomicAdd(&g.counters[kAlgoBytes], l_bytes);
-    if (w_eval) atomicAdd(&g.counters[kEval], w_eval);
-    if (w_jacc) atomicAdd(&g.counters[kJacc], w_jacc);
-    if (w_cand) atomicAdd(&g.counters[kCand], w_cand);
-    if (w_over) atomicAdd(&g.counters[kOverflow], w_over);
-    if (w_ml) atomicAdd(&g.counters[kMatchEntries], w_ml);
-    if (w_mp) atomicAdd(&g.counters[kMatchedPairs], w_mp);
-    if (w_maxfwd) atomicMax(g.err + 3, w_maxfwd);
+    if (lane < kWsProf) g.wstat[static_cast<long long>(wid) * kWStride + lane] = f;
+  }
+}
+
+// Sum of the per-wave statistics into the counters (one block, after query_kernel).  Thread t
+// reduces field t % 32 over the waves w = t / 32 (mod 32); then 24 threads combine the 32 partials.
+enum WsOp { kOpSum, kOpMax, kOpMin, kOpArg };
+__device__ __forceinline__ WsOp ws_op(int f) {
+  if (f == kWsMaxFwd) return kOpMax;
+#ifdef FSLR_SECTION_PROF
+  if (f == kWsBase + 8 || f == kWsBase + 10) return kOpMax;
+  if (f == kWsBase + 11) return kOpMin;
+  if (f == kWsBase + 9) return kOpArg;      // rank of the slowest read: follows field kWsBase + 8
+#endif
+  return kOpSum;
+}
+
+__global__ __launch_bounds__(1024) void k_reduce_wstat(const unsigned long long* __restrict__ ws, int nwaves,
+                                                       unsigned long long* __restrict__ counters, int* err) {
+  constexpr int kGroups = 1024 / kWStride;
+  __shared__ unsigned long long val[kGroups][kWStride], key[kGroups][kWStride];
+  const int f = threadIdx.x % kWStride, grp = threadIdx.x / kWStride;
+  const WsOp op = ws_op(f);
+  unsigned long long acc = op == kOpMin ? ~0ull : 0ull, k = 0ull;
+  if (f < kWsProf) {
+    for (int w = grp; w < nwaves; w += kGroups) {
+      const unsigned long long* row = ws + static_cast<long long>(w) * kWStride;
+      const unsigned long long x = row[f];
+      if (op == kOpSum) acc += x;
+      else if (op == kOpMax) acc = acc > x ? acc : x;
+      else if (op == kOpMin) acc = acc < x ? acc : x;
+      else if (row[kWsBase + 8] >= k) { k = row[kWsBase + 8]; acc = x; }
+    }
+  }
+  val[grp][f] = acc;
+  key[grp][f] = k;
+  __syncthreads();
+  if (threadIdx.x >= kWsProf) return;
+  const int fi = threadIdx.x;
+  const WsOp o = ws_op(fi);
+  unsigned long long r = val[0][fi], rk = key[0][fi];
+  for (int g2 = 1; g2 < kGroups; ++g2) {
+    const unsigned long long x = val[g2][fi];
+    if (o == kOpSum) r += x;
+    else if (o == kOpMax) r = r > x ? r : x;
+    else if (o == kOpMin) r = r < x ? r : x;
+    else if (key[g2][fi] > rk) { rk = key[g2][fi]; r = x; }
+  }
+  if (fi == kWsMaxFwd) {
+    if (r) atomicMax(err + 3, static_cast<int>(r));
+  } else if (fi < kWsBase) {
+    const int dst = fi == kWsEval ? kEval : fi == kWsJacc ? kJacc : fi == kWsCand ? kCand
+                  : fi == kWsAlgoBytes ? kAlgoBytes : fi == kWsOverflow ? kOverflow
+                  : fi == kWsMatchEntries ? kMatchEntries : kMatchedPairs;
+    counters[dst] += r;
+  } else {
+    counters[kSecBase + (fi - kWsBase)] = r;
   }
 }
 
@@ -673,19 +765,28 @@ int resident_blocks() {
 
 }  // namespace
 
+int query_max_waves() {
+  const int b0 = resident_blocks<0>(), b1 = resident_blocks<1>();
+  return (b0 > b1 ? b0 : b1) * kWavesPerBlock;
+}
+
 hipError_t launch_query(const QueryArgs& a, int thr_mode, hipStream_t s) {
   const long long span = static_cast<long long>(a.a_end) - a.a_begin;
   const long long nq = (span + a.n_shards - 1) / a.n_shards + kShardMask;   // reads of this shard (bound)
   if (span > 0) {
     k_len_bounds<<<grid_for(span), 256, 0, s>>>(a.rmeta, a.a_begin, a.a_end, a.qlen_cut, a.nal_cut, a.lb);
-    const long long want = (nq + kWavesPerBlock - 1) / kWavesPerBlock;
-    if (thr_mode == 0) {
-      const int cap = resident_blocks<0>();
-      query_kernel<0><<<static_cast<int>(want < cap ? want : cap), kBlock, 0, s>>>(a);
-    } else {
-      const int cap = resident_blocks<1>();
-      query_kernel<1><<<static_cast<int>(want < cap ? want : cap), kBlock, 0, s>>>(a);
-    }
+    long long want = (nq + kWavesPerBlock - 1) / kWavesPerBlock;
+#ifdef FSLR_SECTION_PROF
+    if (const char* e = getenv("FSLR_QUERY_BLOCKS")) want = std::min(want, std::max(1ll, atoll(e)));
+#endif
+    const int cap = thr_mode == 0 ? resident_blocks<0>() : resident_blocks<1>();
+    const int blocks = static_cast<int>(want < cap ? want : cap);
+    if (blocks * kWavesPerBlock > a.wstat_waves) return hipErrorInvalidValue;   // capi sizes wstat
+    if (thr_mode == 0)
+      query_kernel<0><<<blocks, kBlock, 0, s>>>(a);
+    else
+      query_kernel<1><<<blocks, kBlock, 0, s>>>(a);
+    k_reduce_wstat<<<1, 1024, 0, s>>>(a.wstat, blocks * kWavesPerBlock, a.counters, a.err);
   }
   // the deferred list's length is only known on the device: a fixed grid walks it
   deferred_kernel<<<2048, 256, 0, s>>>(a);

@@ -210,15 +210,19 @@ def generate(n_reads: int, lmax: int, seed: int, dist: str = 'uniform', cluster_
     f_len = ev_len[f_ev_fill] + rng.integers(-20, 21, size=nf)
 
     # globally distinct starts: keep the first (stable order) of every value, re-draw
-    # the jitter of the others until they hit a free value
+    # the jitter of the others until they hit a free value (membership in a bitmap of used
+    # values; same draws and outcome as a sorted-set test)
     order = np.argsort(f_start, kind='stable')
     s_sorted = f_start[order]
     dup_sorted = np.zeros(nf, dtype=bool)
     if nf > 1:
         dup_sorted[1:] = s_sorted[1:] == s_sorted[:-1]
     pending = np.sort(order[dup_sorted])
-    taken = s_sorted[~dup_sorted]                  # sorted, unique
-    extra = np.zeros(0, dtype=np.int64)
+    del order, s_sorted, dup_sorted
+    lo_v = int(ev_start.min()) - 6000 if ev_start.size else 0
+    hi_v = int(ev_start.max()) + 6000 if ev_start.size else 1
+    used = np.zeros(hi_v - lo_v, dtype=bool)
+    used[f_start - lo_v] = True
     jit = 20
     for it in range(400):
         if pending.size == 0:
@@ -226,16 +230,17 @@ def generate(n_reads: int, lmax: int, seed: int, dist: str = 'uniform', cluster_
         if it >= 8:
             jit = min(jit * 2, 5000)
         cand = ev_start[f_ev_fill[pending]] + rng.integers(-jit, jit + 1, size=pending.size)
-        clash = _member(taken, cand) | _member(extra, cand)
+        clash = used[cand - lo_v]
         _, first = np.unique(cand, return_index=True)
         firstmask = np.zeros(pending.size, dtype=bool)
         firstmask[first] = True
         ok = ~clash & firstmask
         f_start[pending[ok]] = cand[ok]
-        extra = np.union1d(extra, cand[ok])
+        used[cand[ok] - lo_v] = True
         pending = pending[~ok]
     else:  # pragma: no cover
         raise RuntimeError("could not make filling starts distinct")
+    del used
 
     # query coordinates: fillings start at qstart 20, contiguous
     csum = np.cumsum(f_len)

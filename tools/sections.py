@@ -40,7 +40,7 @@ def main():
         ctx.build_index()
         ctx.query(1 - 0.04, 1 - 0.25, pt, 10, 0, csr.n_reads)
         ctx.sync()
-        acc += ctx.counters(32)[16:24].astype(np.float64)
+        acc += ctx.counters(80)[48:56].astype(np.float64)
     tot = acc[7]
     out = {n: round(float(v / tot), 4) for n, v in zip(NAMES, acc)}
     out['unaccounted'] = round(float(1 - acc[:7].sum() / tot), 4)
