@@ -35,7 +35,9 @@ enum Counter { kEdgeCount = 0,          // atomic (own 128-B line)
                kEval = 32, kJacc = 33, kCand = 34, kAlgoBytes = 35, kOverflow = 36, kGather = 37,
                kMatchEntries = 38, kMatchedPairs = 39, kMaxFwd = 40,
                kSecBase = 48,           // FSLR_SECTION_PROF builds: per-section cycle sums of the pair kernel
-               kNumCounters = 80 };
+               kQueueBase = 80,         // pair kernel work queues: 8 counters, one 128-B line each
+               kQueueStride = 16,
+               kNumCounters = kQueueBase + 8 * kQueueStride };
 // per-wave statistics of query_kernel: fields 0..8 (sum, except kWsMaxFwd: max), then (section-
 // timing builds) 8 section sums, slowest read cycles (max), its rank, wave cycles max / min,
 // wave count, cycle sums of reads 0, 1 and >= 2 of the wave
@@ -84,6 +86,8 @@ struct QueryArgs {
   double qlen_cut, nal_cut;
   int a_begin, a_end;
   int shard, n_shards;                // query reads: blocks of 64 ranks of [a_begin, a_end) dealt round robin
+  int nv;                             // (launch_query) number of this shard's query reads
+  int k_static;                       // (launch_query) grid-stride sweeps before the work queues
   int2* edges;
   unsigned short* edge_iu;
   long long edge_cap;

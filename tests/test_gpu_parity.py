@@ -345,6 +345,37 @@ def test_query_shards_partition_the_pairs(ctx, n_shards):
     np.testing.assert_array_equal(fwd, o['fwd'])
 
 
+@pytest.mark.parametrize('n_shards', [1, 3])
+def test_work_queue_read_assignment_vs_oracle(ctx, monkeypatch, n_shards):
+    """The pair kernel's work-queue read assignment (used when every wave holds >= 64 reads, e.g.
+    1M reads on one GPU) forced on at 60k reads: same edges, degrees and pair counts as the oracle."""
+    monkeypatch.setenv('FSLR_DYNAMIC_MIN_READS', '0')
+    s = synth.generate(60_000, 16, 31)
+    csr = s.interval_data().csr()
+    o = O.run_core(oracle_from_csr(csr), use_cap=False)
+    if n_shards == 1:
+        compare_with_oracle(gpu_run(ctx, csr), o, csr.n_reads)
+        return
+    thr = fold_overlap_threshold(csr.iv_aln, 0.8)
+    ctx.load_csr(csr, thr)
+    ctx.reserve_edges(12 * csr.n_reads)
+    ctx.build_index()
+    pt = pass_table([1, 1, 0.66, 0.66, 0.66, 0.5])
+    edges, pairs = [], 0
+    fwd = np.zeros(csr.n_reads, np.int64)
+    for r in range(n_shards):
+        ctx.query_shard(1 - 0.04, 1 - 0.25, pt, r, n_shards)
+        st = ctx.stats()
+        pairs += st['evaluated_pairs']
+        edges += list(zip(*[x.tolist() for x in ctx.edges(st['n_edges'])]))
+        own = (np.arange(csr.n_reads) // 64) % n_shards == r
+        fwd[own] = ctx.fwd_degree()[own]
+    assert pairs == o['stats']['evaluated_pairs']
+    assert sorted(edges) == sorted(zip(o['edge_a'].tolist(), o['edge_b'].tolist(), o['edge_I'].tolist(),
+                                       o['edge_U'].tolist()))
+    np.testing.assert_array_equal(fwd, o['fwd'])
+
+
 def test_shard_built_index_matches_full_index():
     """fslr_set_shard: an index whose query-side data covers one shard gives that shard exactly
     the edges of a fully built index; the full-range query is refused on it."""
