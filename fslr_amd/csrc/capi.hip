@@ -34,6 +34,8 @@ struct fslr_ctx {
   int* data_pos = nullptr;
   unsigned* dchrom = nullptr;    // data order (start-sorted `data` list): chromosome
   int4* drec = nullptr;          // data order: {start, end, thr, read << 6 | j}
+  int2* dgate = nullptr;         // data order: the owning read's gate word {qlen2, nal | L << 24 | haz << 31}
+  int* chist = nullptr;          // index build scratch: per-chromosome counts per 1024-position sub-tile
   int* s_start = nullptr;
   int2* crange = nullptr;
   unsigned long long* keys = nullptr;
@@ -108,7 +110,8 @@ int ensure_capacity(fslr_ctx* c, int64_t n, int64_t ni, int n_chroms) {
   if (ni > c->cap_ni) {
     if ((rc = dalloc(c, &c->iv, ni)) || (rc = dalloc(c, &c->qpos, ni)) || (rc = dalloc(c, &c->rng_s, ni)) || (rc = dalloc(c, &c->idx4, ni)) ||
         (rc = dalloc(c, &c->idx_gate, ni)) || (rc = dalloc(c, &c->data_pos, ni)) ||
-        (rc = dalloc(c, &c->dchrom, ni)) || (rc = dalloc(c, &c->drec, ni)) || (rc = dalloc(c, &c->s_start, ni)) ||
+        (rc = dalloc(c, &c->dchrom, ni)) || (rc = dalloc(c, &c->drec, ni)) || (rc = dalloc(c, &c->dgate, ni)) ||
+        (rc = dalloc(c, &c->chist, (ni / 1024 + 1) * 64)) || (rc = dalloc(c, &c->s_start, ni)) ||
         (rc = dalloc(c, &c->keys, ni)) || (rc = dalloc(c, &c->keys2, ni)) || (rc = dalloc(c, &c->vals, ni)) ||
         (rc = dalloc(c, &c->vals2, ni)) || (rc = dalloc(c, &c->endkey, ni)) || (rc = dalloc(c, &c->pmaxkey, 2 * (ni / 256) + ni / (256 * 1024) + 8)) ||
         (rc = dalloc(c, &c->thr_tmp, ni)))
@@ -179,7 +182,8 @@ void fslr_ctx_destroy(fslr_ctx* c) {
   void* bufs[] = {c->rmeta,  c->iv,     c->qpos,    c->rng_s,  c->idx4,    c->idx_gate, c->data_pos, c->s_start,
                   c->crange, c->keys,   c->keys2,   c->vals,    c->vals2,   c->endkey,  c->pmaxkey,
                   c->temp,   c->umax,   c->edges,   c->edge_iu, c->fwd,     c->parent,  c->counters,
-                  c->errw,   c->thr_tmp, c->defer,   c->dchrom,  c->drec,    c->lbounds, c->diag, c->wstat};
+                  c->errw,   c->thr_tmp, c->defer,   c->dchrom,  c->drec,    c->lbounds, c->diag, c->wstat,
+                  c->dgate,  c->chist};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->ev_ok)
@@ -264,20 +268,29 @@ int fslr_set_reads(fslr_ctx* c, const fslr_reads* r) {
   HIP_TRY(c, hipMemcpyAsync(c->crange, cr.data(), cr.size() * sizeof(int2), hipMemcpyHostToDevice, c->stream));
   std::vector<unsigned> dch;
   std::vector<int4> drc;
+  std::vector<int2> dgt;
   if (use_dp && ni) {
     // the `data` list itself (cluster.py:116-121) in its start-sorted order
     dch.resize(static_cast<size_t>(ni));
     drc.resize(static_cast<size_t>(ni));
-    for (int64_t i = 0; i < n; ++i)
+    dgt.resize(static_cast<size_t>(ni));
+    for (int64_t i = 0; i < n; ++i) {
+      // the gate word of kernels.hpp idx_gate, per interval like the reference's IntervalItem
+      // (which carries qlen2 and n_alignments, cluster.py:10-11)
+      const int4 m = rm[i];
+      const int2 gate = make_int2(m.z, (m.w & 0xFFFFFF) | ((m.y & 0x7F) << 24) | (((m.y >> 16) & 1) << 31));
       for (int k = r->read_off[i]; k < r->read_off[i + 1]; ++k) {
         const int d = r->iv_data_pos[k];
         dch[d] = static_cast<unsigned>(r->iv_chrom[k]);
         drc[d] = make_int4(r->iv_start[k], r->iv_end[k], r->iv_thr[k],
                            static_cast<int>((i << 6) | (k - r->read_off[i])));
+        dgt[d] = gate;
       }
+    }
     HIP_TRY(c, hipMemcpyAsync(c->data_pos, r->iv_data_pos, ni * sizeof(int), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(c, hipMemcpyAsync(c->dchrom, dch.data(), ni * sizeof(unsigned), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(c, hipMemcpyAsync(c->drec, drc.data(), ni * sizeof(int4), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->dgate, dgt.data(), ni * sizeof(int2), hipMemcpyHostToDevice, c->stream));
   }
   c->have_data_pos = use_dp;
   c->n = n;
@@ -353,6 +366,9 @@ int fslr_build_index(fslr_ctx* c) {
   b.n_shards = c->n_shards;
   b.dchrom = c->have_data_pos ? c->dchrom : nullptr;
   b.drec = c->have_data_pos ? c->drec : nullptr;
+  b.dgate = c->dgate;
+  b.data_pos = c->data_pos;
+  b.chist = c->chist;
   b.keys = c->keys;
   b.keys2 = c->keys2;
   b.vals = c->vals;

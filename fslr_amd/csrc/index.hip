@@ -2,9 +2,10 @@
 // superintervals IntervalMap it builds per chromosome).
 //
 // Fast path (the start-sorted `data` list of cluster.py:114-121 is resident in HBM, one
-// {start, end, thr, tag} record per data position, tag = read << 6 | j):
-//   1. one stable radix pass on the chromosome carries the 16-B records: (chrom, start) order
-//   2. per sorted position q (coalesced): the read's packed gate fields, start, (chrom, end) key
+// {start, end, thr, tag} record, gate word and CSR index per data position, tag = read << 6 | j):
+//   1-2. a stable counting sort on the chromosome (<= 64 chromosomes: k_chrom_*; otherwise one
+//        radix pass + k_finish) writes the records, gate words, starts and (chrom, end) keys at
+//        their (chrom, start) positions and the CSR -> sorted position map
 // General path (CSR only): radix sort of (chrom << 32 | start) → gather the records.
 // Then, both paths:
 //   3. per 256-position tile, the max of (chrom << 32 | end) (written by k_finish), and their
@@ -82,6 +83,166 @@ __global__ __launch_bounds__(kTile) void k_finish(const int4* __restrict__ idx4,
       key = (static_cast<unsigned long long>(c) << 32) | static_cast<unsigned>(rec.y);
       endkey[q] = key;
     }
+    for (int o = 32; o > 0; o >>= 1) key = max_u64(key, __shfl_xor(key, o));
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = key;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long mx = wmax[0];
+      for (int w = 1; w < kTile / 64; ++w) mx = max_u64(mx, wmax[w]);
+      tile_max[t] = mx;
+    }
+    __syncthreads();
+  }
+}
+
+// ---- fused data-order path (n_chroms <= 64) --------------------------------------------------
+// A stable counting sort on the chromosome, one wavefront per sub-tile of kSub data positions
+// (16 rounds of 64, data order).  Lane l of a wave owns chromosome l: six ballots of the chromosome
+// bits give every lane both the mask of lanes sharing its own chromosome (its rank among them) and
+// the mask of lanes holding chromosome l (lane l's running count) — no LDS, no barriers.
+//   k_chrom_count    counts per (chromosome, sub-tile)                  reads 4 B / interval
+//   k_chrom_scan     exclusive scan per chromosome (one block each) + the chromosome's begin
+//   k_chrom_scatter  q = run[c] + rank: writes idx4, idx_gate, start, (chrom, end) key and the
+//                    CSR -> sorted position map           reads 32 B, writes 40 B / interval
+// The result is the stable partition of the start-sorted `data` list by chromosome, i.e. the
+// same (chrom, start) order, ties included, as the radix pass it replaces.
+constexpr int kSub = 1024;
+constexpr int kChromBits = 6;
+constexpr int kMaxFusedChroms = 1 << kChromBits;
+
+__device__ __forceinline__ unsigned long long lane_mask_lt() {
+  return (1ull << (threadIdx.x & 63)) - 1ull;
+}
+
+__global__ __launch_bounds__(256) void k_chrom_count(const unsigned* __restrict__ dchrom, int ni, int nsub,
+                                                     int* __restrict__ chist) {
+  const int lane = threadIdx.x & 63;
+  const int sub = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (sub >= nsub) return;
+  const int e0 = sub * kSub;
+  unsigned cs[kSub / 64];
+#pragma unroll
+  for (int r = 0; r < kSub / 64; ++r) {
+    const int e = e0 + r * 64 + lane;
+    cs[r] = e < ni ? dchrom[e] : 0u;
+  }
+  int cnt = 0;
+#pragma unroll
+  for (int r = 0; r < kSub / 64; ++r) {
+    unsigned long long m = __ballot(e0 + r * 64 + lane < ni);
+#pragma unroll
+    for (int b = 0; b < kChromBits; ++b) {
+      const unsigned long long bb = __ballot((cs[r] >> b) & 1u);
+      m &= ((lane >> b) & 1) ? bb : ~bb;
+    }
+    cnt += __popcll(m);
+  }
+  chist[lane * nsub + sub] = cnt;
+}
+
+__global__ __launch_bounds__(1024) void k_chrom_scan(int* __restrict__ chist, int nsub,
+                                                     const int2* __restrict__ crange) {
+  __shared__ int part[1024];
+  int* row = chist + blockIdx.x * nsub;
+  const int per = (nsub + 1023) / 1024;
+  const int b = threadIdx.x * per, e = min(b + per, nsub);
+  int sum = 0;
+  for (int i = b; i < e; ++i) sum += row[i];
+  part[threadIdx.x] = sum;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const int v = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  int acc = crange[blockIdx.x].x + (threadIdx.x ? part[threadIdx.x - 1] : 0);
+  for (int i = b; i < e; ++i) {
+    const int x = row[i];
+    row[i] = acc;
+    acc += x;
+  }
+}
+
+// Per wave: its sub-tile in data order, 64 positions per round; lane l carries the next sorted
+// position of chromosome l.  Every element lands at q = run[c] + (its rank among the round's lanes
+// of chromosome c); the stores of one round form <= n_chroms runs of consecutive positions, which
+// later rounds extend, so the cache lines fill up before they leave L2.  qd[e] = q is written in
+// data order for the CSR -> sorted position gather.
+__global__ __launch_bounds__(256) void k_chrom_scatter(const unsigned* __restrict__ dchrom,
+                                                       const int4* __restrict__ drec,
+                                                       const int2* __restrict__ dgate,
+                                                       const int* __restrict__ chist, int ni, int nsub,
+                                                       int4* __restrict__ idx4, int2* __restrict__ idx_gate,
+                                                       int* __restrict__ s_start,
+                                                       unsigned long long* __restrict__ endkey,
+                                                       int* __restrict__ qd) {
+  const int lane = threadIdx.x & 63;
+  const int sub = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (sub >= nsub) return;
+  const int e0 = sub * kSub;
+  const int nvalid = min(kSub, ni - e0);
+  const unsigned long long lt = lane_mask_lt();
+  int run = chist[lane * nsub + sub];                 // lane l: next sorted position of chromosome l
+#pragma unroll 2
+  for (int r = 0; r < kSub / 64; ++r) {
+    const bool valid = r * 64 + lane < nvalid;
+    const int e = e0 + r * 64 + lane;
+    unsigned c = 0u;
+    int4 rec = make_int4(0, 0, 0, 0);
+    int2 gate = make_int2(0, 0);
+    if (valid) {
+      c = dchrom[e];
+      rec = drec[e];
+      gate = dgate[e];
+    }
+    const unsigned long long v = __ballot(valid);
+    unsigned long long mine = v, mylane = v;
+#pragma unroll
+    for (int b = 0; b < kChromBits; ++b) {
+      const unsigned long long bb = __ballot((c >> b) & 1u);
+      mine &= ((c >> b) & 1u) ? bb : ~bb;
+      mylane &= ((lane >> b) & 1) ? bb : ~bb;
+    }
+    const int q = __shfl(run, static_cast<int>(c)) + __popcll(mine & lt);
+    run += __popcll(mylane);
+    if (valid) {
+      idx4[q] = rec;
+      idx_gate[q] = gate;
+      s_start[q] = rec.x;
+      endkey[q] = (static_cast<unsigned long long>(c) << 32) | static_cast<unsigned>(rec.y);
+      qd[e] = q;
+    }
+  }
+}
+
+// CSR -> sorted position map as a gather: qpos[k] = qd[data_pos[k]], one wavefront per block of 64
+// ranks (the query-shard unit), whose intervals are one contiguous CSR span; blocks of other shards
+// are skipped.  Coalesced reads of data_pos and writes of qpos; the random 4-B reads of qd hit the
+// caches, where the scatter it replaces (qpos[k] = q in sorted order) wrote 8.5M partial lines
+// (150 us at 1M reads, now ~1/3 of that).
+__global__ __launch_bounds__(256) void k_qpos_gather(const int4* __restrict__ rmeta, const int* __restrict__ data_pos,
+                                                     const int* __restrict__ qd, int n, int ni, int shard,
+                                                     int n_shards, int* __restrict__ qpos) {
+  const int lane = threadIdx.x & 63;
+  const int nblk = (n + 63) >> kShardShift;
+  for (int blk = blockIdx.x * 4 + (threadIdx.x >> 6); blk < nblk; blk += gridDim.x * 4) {
+    if (!shard_owns(blk << kShardShift, shard, n_shards)) continue;
+    const int r0 = blk << kShardShift, r1 = min(r0 + 64, n);
+    const int k0 = rmeta[r0].x;
+    const int k1 = r1 < n ? rmeta[r1].x : ni;
+    for (int k = k0 + lane; k < k1; k += 64) qpos[k] = qd[data_pos[k]];
+  }
+}
+
+// per tile of kTile sorted positions: the max (chrom, end) key
+__global__ __launch_bounds__(kTile) void k_tile_max(const unsigned long long* __restrict__ endkey, int ni,
+                                                    unsigned long long* __restrict__ tile_max) {
+  __shared__ unsigned long long wmax[kTile / 64];
+  const int n_tiles = (ni + kTile - 1) / kTile;
+  for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+    const int q = t * kTile + threadIdx.x;
+    unsigned long long key = q < ni ? endkey[q] : 0ull;
     for (int o = 32; o > 0; o >>= 1) key = max_u64(key, __shfl_xor(key, o));
     if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = key;
     __syncthreads();
@@ -281,7 +442,16 @@ hipError_t launch_build_index(const IndexBufs& b, int n, int ni, int n_chroms, h
   if (ni <= 0) return hipSuccess;
   hipError_t e;
   size_t tb = b.temp_bytes;
-  if (b.dchrom) {
+  if (b.dchrom && n_chroms <= kMaxFusedChroms) {
+    const int nsub = (ni + kSub - 1) / kSub;
+    k_chrom_count<<<(nsub + 3) / 4, 256, 0, s>>>(b.dchrom, ni, nsub, b.chist);
+    k_chrom_scan<<<n_chroms, 1024, 0, s>>>(b.chist, nsub, b.crange);
+    k_chrom_scatter<<<(nsub + 3) / 4, 256, 0, s>>>(b.dchrom, b.drec, b.dgate, b.chist, ni, nsub, b.idx4, b.idx_gate,
+                                                   b.s_start, b.endkey, b.vals);
+    k_qpos_gather<<<grid_for((n + 63) / 64, 4), 256, 0, s>>>(b.rmeta, b.data_pos, b.vals, n, ni, b.shard, b.n_shards,
+                                                              b.qpos);
+    k_tile_max<<<grid_for(ni, kTile), kTile, 0, s>>>(b.endkey, ni, b.pmaxkey);
+  } else if (b.dchrom) {
     unsigned* k32 = reinterpret_cast<unsigned*>(b.keys2);
     e = hipcub::DeviceRadixSort::SortPairs(b.temp, tb, b.dchrom, k32, b.drec, b.idx4, ni, 0, bits_for(n_chroms), s);
     if (e != hipSuccess) return e;

@@ -51,6 +51,9 @@ struct IndexBufs {
   const int4* iv;
   const unsigned* dchrom;             // [NI] or nullptr: chromosome per data position (start-sorted
   const int4* drec;                   //      order given) and {start, end, thr, tag} per data position
+  const int2* dgate;                  // [NI] data order: the owning read's gate word (idx_gate)
+  const int* data_pos;                // [NI] CSR index -> data position
+  int* chist;                         // scratch [64 x (NI / 1024 + 1)] chromosome counts per sub-tile
   unsigned long long* keys;           // scratch [NI] x2 (double buffer for the sort)
   unsigned long long* keys2;
   int* vals;

@@ -237,6 +237,24 @@ def test_full_sort_index_path_matches_data_order_path(ctx):
     assert g1['stats']['evaluated_pairs'] == g2['stats']['evaluated_pairs']
 
 
+@pytest.mark.parametrize('split,mod', [(3, 64), (5, None)])
+def test_many_chromosomes_vs_oracle(ctx, split, mod):
+    """Chromosome counts at the index build's limits: 64 ids (the largest the counting-sort pass
+    takes, every chromosome bit in use) and 115 ids (the radix-pass fallback)."""
+    import dataclasses
+    s = synth.generate(30_000, 16, 37)
+    csr = s.interval_data().csr()
+    ch = csr.iv_chrom.astype(np.int64) * split + (csr.iv_start.astype(np.int64) // 1000) % split
+    if mod:
+        ch %= mod
+    _, dense = np.unique(ch, return_inverse=True)
+    csr = dataclasses.replace(csr, iv_chrom=dense.astype(np.int32), n_chroms=int(dense.max()) + 1)
+    assert csr.n_chroms == (mod or 23 * split)
+    g = gpu_run(ctx, csr)
+    o = O.run_core(oracle_from_csr(csr), use_cap=False)
+    compare_with_oracle(g, o, csr.n_reads)
+
+
 def test_rerun_is_deterministic(ctx):
     s = synth.generate(30_000, 16, 2)
     csr = s.interval_data().csr()
