@@ -25,8 +25,9 @@
 namespace fslr {
 namespace {
 
-constexpr int kRangeBlock = 256;
-constexpr int kTile = kRangeBlock;      // pmax tiles == range blocks (window edges are tile-aligned)
+constexpr int kRangeBlock = 256;        // threads of k_ranges
+constexpr int kRangeSpan = 1024;        // sorted positions per k_ranges block (4 per thread)
+constexpr int kTile = 256;              // pmax tiles (window edges are tile-aligned)
 constexpr int kWin = 512;
 
 __global__ void k_keys_csr(const int4* __restrict__ rmeta, const int4* __restrict__ iv, int n,
@@ -96,17 +97,19 @@ __global__ __launch_bounds__(kTile) void k_finish(const int4* __restrict__ idx4,
 }
 
 // ---- fused data-order path (n_chroms <= 64) --------------------------------------------------
-// A stable counting sort on the chromosome, one wavefront per sub-tile of kSub data positions
-// (16 rounds of 64, data order).  Lane l of a wave owns chromosome l: six ballots of the chromosome
-// bits give every lane both the mask of lanes sharing its own chromosome (its rank among them) and
-// the mask of lanes holding chromosome l (lane l's running count) — no LDS, no barriers.
-//   k_chrom_count    counts per (chromosome, sub-tile)                  reads 4 B / interval
+// A stable counting sort on the chromosome, one block per tile of kChromTile data positions.
+// Within a round of 64 lanes, six ballots of the chromosome bits give every lane the mask of lanes
+// sharing its chromosome (its rank among them) and lane l the count of chromosome l.
+//   k_chrom_count    counts per (chromosome, tile)                      reads 4 B / interval
 //   k_chrom_scan     exclusive scan per chromosome (one block each) + the chromosome's begin
 //   k_chrom_scatter  q = run[c] + rank: writes idx4, idx_gate, start, (chrom, end) key and the
-//                    CSR -> sorted position map           reads 32 B, writes 40 B / interval
+//                    data -> sorted position map          reads 28 B, writes 40 B / interval
+//   k_qpos_gather    CSR -> sorted position map
 // The result is the stable partition of the start-sorted `data` list by chromosome, i.e. the
 // same (chrom, start) order, ties included, as the radix pass it replaces.
-constexpr int kSub = 1024;
+constexpr int kTileThreads = 1024;
+constexpr int kTileWaves = kTileThreads / 64;
+constexpr int kChromTile = 16 * kTileThreads;     // data positions per block tile
 constexpr int kChromBits = 6;
 constexpr int kMaxFusedChroms = 1 << kChromBits;
 
@@ -114,30 +117,32 @@ __device__ __forceinline__ unsigned long long lane_mask_lt() {
   return (1ull << (threadIdx.x & 63)) - 1ull;
 }
 
-__global__ __launch_bounds__(256) void k_chrom_count(const unsigned* __restrict__ dchrom, int ni, int nsub,
-                                                     int* __restrict__ chist) {
-  const int lane = threadIdx.x & 63;
-  const int sub = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (sub >= nsub) return;
-  const int e0 = sub * kSub;
-  unsigned cs[kSub / 64];
-#pragma unroll
-  for (int r = 0; r < kSub / 64; ++r) {
-    const int e = e0 + r * 64 + lane;
-    cs[r] = e < ni ? dchrom[e] : 0u;
-  }
+__global__ __launch_bounds__(kTileThreads) void k_chrom_count(const unsigned* __restrict__ dchrom, int ni,
+                                                              int ntl, int* __restrict__ chist) {
+  __shared__ int wc[kTileWaves][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int tl = blockIdx.x;
+  const int e0 = tl * kChromTile;
   int cnt = 0;
-#pragma unroll
-  for (int r = 0; r < kSub / 64; ++r) {
-    unsigned long long m = __ballot(e0 + r * 64 + lane < ni);
+#pragma unroll 4
+  for (int r = 0; r < kChromTile / kTileThreads; ++r) {
+    const int e = e0 + r * kTileThreads + threadIdx.x;
+    const unsigned c = e < ni ? dchrom[e] : 0u;
+    unsigned long long m = __ballot(e < ni);
 #pragma unroll
     for (int b = 0; b < kChromBits; ++b) {
-      const unsigned long long bb = __ballot((cs[r] >> b) & 1u);
+      const unsigned long long bb = __ballot((c >> b) & 1u);
       m &= ((lane >> b) & 1) ? bb : ~bb;
     }
     cnt += __popcll(m);
   }
-  chist[lane * nsub + sub] = cnt;
+  wc[w][lane] = cnt;
+  __syncthreads();
+  if (w == 0) {
+    int t = 0;
+    for (int k = 0; k < kTileWaves; ++k) t += wc[k][lane];
+    chist[lane * ntl + tl] = t;
+  }
 }
 
 __global__ __launch_bounds__(1024) void k_chrom_scan(int* __restrict__ chist, int nsub,
@@ -164,38 +169,51 @@ __global__ __launch_bounds__(1024) void k_chrom_scan(int* __restrict__ chist, in
   }
 }
 
-// Per wave: its sub-tile in data order, 64 positions per round; lane l carries the next sorted
-// position of chromosome l.  Every element lands at q = run[c] + (its rank among the round's lanes
-// of chromosome c); the stores of one round form <= n_chroms runs of consecutive positions, which
-// later rounds extend, so the cache lines fill up before they leave L2.  qd[e] = q is written in
-// data order for the CSR -> sorted position gather.
-__global__ __launch_bounds__(256) void k_chrom_scatter(const unsigned* __restrict__ dchrom,
-                                                       const int4* __restrict__ drec,
-                                                       const int2* __restrict__ dgate,
-                                                       const int* __restrict__ chist, int ni, int nsub,
-                                                       int4* __restrict__ idx4, int2* __restrict__ idx_gate,
-                                                       int* __restrict__ s_start,
-                                                       unsigned long long* __restrict__ endkey,
-                                                       int* __restrict__ qd) {
-  const int lane = threadIdx.x & 63;
-  const int sub = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (sub >= nsub) return;
-  const int e0 = sub * kSub;
-  const int nvalid = min(kSub, ni - e0);
+// One block of 16 waves per tile of kChromTile data positions, 16 rounds of 1024 in data order.
+// Per round each wave ranks its lanes within their chromosome (ballots), the waves' per-chromosome
+// counts are prefixed in LDS, and every element lands at q = run[c] + (earlier waves' count of c)
+// + rank.  A chromosome's run in a tile (~700 positions at 23 chromosomes) is written by one block,
+// so its cache lines fill up in one L2; with 1024-position tiles per wave the runs were ~45 long,
+// most lines were shared by waves on different XCDs and the stores cost 155 of 215 us.
+// qd[e] = q is written in data order for the CSR -> sorted position gather.
+__global__ __launch_bounds__(kTileThreads) void k_chrom_scatter(const unsigned* __restrict__ dchrom,
+                                                              const int4* __restrict__ drec,
+                                                              const int2* __restrict__ dgate,
+                                                              const int* __restrict__ chist, int ni, int ntl,
+                                                              int4* __restrict__ idx4, int2* __restrict__ idx_gate,
+                                                              int* __restrict__ s_start,
+                                                              unsigned long long* __restrict__ endkey,
+                                                              int* __restrict__ qd) {
+  __shared__ int wc[kTileWaves][64];      // this round: count of chromosome l in wave w
+  __shared__ int wp[kTileWaves][64];      // this round: count of chromosome l in waves < w
+  __shared__ int runs[2][64];             // next sorted position of chromosome l (double buffered)
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int tl = blockIdx.x;
+  const int e0 = tl * kChromTile;
   const unsigned long long lt = lane_mask_lt();
-  int run = chist[lane * nsub + sub];                 // lane l: next sorted position of chromosome l
-#pragma unroll 2
-  for (int r = 0; r < kSub / 64; ++r) {
-    const bool valid = r * 64 + lane < nvalid;
-    const int e = e0 + r * 64 + lane;
-    unsigned c = 0u;
-    int4 rec = make_int4(0, 0, 0, 0);
-    int2 gate = make_int2(0, 0);
-    if (valid) {
+  if (threadIdx.x < 64) runs[0][threadIdx.x] = chist[threadIdx.x * ntl + tl];
+  auto load = [&](int r, unsigned& c, int4& rec, int2& gate) {
+    const int e = e0 + r * kTileThreads + threadIdx.x;
+    c = 0u;
+    rec = make_int4(0, 0, 0, 0);
+    gate = make_int2(0, 0);
+    if (e < ni) {
       c = dchrom[e];
       rec = drec[e];
       gate = dgate[e];
     }
+  };
+  unsigned c_n;
+  int4 rec_n;
+  int2 gate_n;
+  load(0, c_n, rec_n, gate_n);
+  for (int r = 0; r < kChromTile / kTileThreads; ++r) {
+    const unsigned c = c_n;
+    const int4 rec = rec_n;
+    const int2 gate = gate_n;
+    const int e = e0 + r * kTileThreads + threadIdx.x;
+    const bool valid = e < ni;
+    if (r + 1 < kChromTile / kTileThreads) load(r + 1, c_n, rec_n, gate_n);
     const unsigned long long v = __ballot(valid);
     unsigned long long mine = v, mylane = v;
 #pragma unroll
@@ -204,9 +222,18 @@ __global__ __launch_bounds__(256) void k_chrom_scatter(const unsigned* __restric
       mine &= ((c >> b) & 1u) ? bb : ~bb;
       mylane &= ((lane >> b) & 1) ? bb : ~bb;
     }
-    const int q = __shfl(run, static_cast<int>(c)) + __popcll(mine & lt);
-    run += __popcll(mylane);
+    wc[w][lane] = __popcll(mylane);
+    __syncthreads();
+    {
+      // thread (w, l): chromosome l's count in waves < w; the last wave also advances the run
+      int pre = 0;
+      for (int k = 0; k < w; ++k) pre += wc[k][lane];
+      wp[w][lane] = pre;
+      if (w == kTileWaves - 1) runs[(r + 1) & 1][lane] = runs[r & 1][lane] + pre + wc[w][lane];
+    }
+    __syncthreads();
     if (valid) {
+      const int q = runs[r & 1][c] + wp[w][c] + __popcll(mine & lt);
       idx4[q] = rec;
       idx_gate[q] = gate;
       s_start[q] = rec.x;
@@ -231,7 +258,20 @@ __global__ __launch_bounds__(256) void k_qpos_gather(const int4* __restrict__ rm
     const int r0 = blk << kShardShift, r1 = min(r0 + 64, n);
     const int k0 = rmeta[r0].x;
     const int k1 = r1 < n ? rmeta[r1].x : ni;
-    for (int k = k0 + lane; k < k1; k += 64) qpos[k] = qd[data_pos[k]];
+    for (int kb = k0; kb < k1; kb += 4 * 64) {
+      int d[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = kb + u * 64 + lane;
+        d[u] = k < k1 ? data_pos[k] : -1;
+      }
+      int q[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) q[u] = d[u] >= 0 ? qd[d[u]] : 0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (d[u] >= 0) qpos[kb + u * 64 + lane] = q[u];
+    }
   }
 }
 
@@ -311,17 +351,17 @@ __global__ __launch_bounds__(kRangeBlock) void k_ranges(const int4* __restrict__
                                                         TilePrefix tile_incl,
                                                         const int2* __restrict__ crange, int ni,
                                                         int2* __restrict__ rng_s) {
-  __shared__ int w_st[kRangeBlock + 2 * kWin];   // starts of [w0, w1)
-  __shared__ int w_pm[kRangeBlock + kWin];       // pmax (end part) of [w0, q0 + kRangeBlock)
+  __shared__ int w_st[kRangeSpan + 2 * kWin];    // starts of [w0, w1)
+  __shared__ int w_pm[kRangeSpan + kWin];        // pmax (end part) of [w0, q0 + kRangeSpan)
   __shared__ unsigned long long t_part[kRangeBlock];
-  const int q0 = blockIdx.x * kRangeBlock;
+  const int q0 = blockIdx.x * kRangeSpan;
   const int w0 = max(q0 - kWin, 0);              // tile-aligned
-  const int w1 = min(q0 + kRangeBlock + kWin, ni);
-  const int wp1 = min(q0 + kRangeBlock, ni);
+  const int w1 = min(q0 + kRangeSpan + kWin, ni);
+  const int wp1 = min(q0 + kRangeSpan, ni);
   for (int t = threadIdx.x; t < w1 - w0; t += kRangeBlock) w_st[t] = s_start[w0 + t];
   // pmax over [w0, wp1): prefix of the tiles before w0, then a scan of the window's keys
   {
-    constexpr int kPer = (kRangeBlock + kWin) / kRangeBlock;   // consecutive keys per thread
+    constexpr int kPer = (kRangeSpan + kWin) / kRangeBlock;   // consecutive keys per thread
     unsigned long long k[kPer];
     unsigned long long m = 0ull;
     for (int u = 0; u < kPer; ++u) {
@@ -345,63 +385,63 @@ __global__ __launch_bounds__(kRangeBlock) void k_ranges(const int4* __restrict__
     }
   }
   __syncthreads();
-  const int q = q0 + threadIdx.x;
-  if (q >= ni) return;
-  if (n_shards > 1 && !shard_owns(idx4[q].w >> 6, shard, n_shards)) return;   // another shard's A side
-  const unsigned long long ek = endkey[q];
-  const int c = static_cast<int>(ek >> 32);
-  const int2 cr = crange[c];
-  const int s = w_st[q - w0], e = static_cast<int>(static_cast<unsigned>(ek));
-  // forward: first p in (q, cr.y) with start_p > e
-  int hi_lim = min(cr.y, w1);
-  int lo = q + 1, hi = hi_lim;
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if (w_st[mid - w0] <= e) lo = mid + 1; else hi = mid;
-  }
-  if (lo == hi_lim && hi_lim < cr.y) {   // range leaves the window: gallop on in global memory
-    int step = 1;
-    hi = lo;
-    while (hi < cr.y && s_start[hi] <= e) {
-      lo = hi + 1;
-      hi = lo + step;
-      step <<= 1;
-    }
-    if (hi > cr.y) hi = cr.y;
+  for (int q = q0 + threadIdx.x; q < wp1; q += kRangeBlock) {
+    if (n_shards > 1 && !shard_owns(idx4[q].w >> 6, shard, n_shards)) continue;   // another shard's A side
+    const unsigned long long ek = endkey[q];
+    const int c = static_cast<int>(ek >> 32);
+    const int2 cr = crange[c];
+    const int s = w_st[q - w0], e = static_cast<int>(static_cast<unsigned>(ek));
+    // forward: first p in (q, cr.y) with start_p > e
+    const int hi_lim = min(cr.y, w1);
+    int lo = q + 1, hi = hi_lim;
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
-      if (s_start[mid] <= e) lo = mid + 1; else hi = mid;
+      if (w_st[mid - w0] <= e) lo = mid + 1; else hi = mid;
     }
-  }
-  const int n_fwd = lo - q - 1;
-  // backward: first p in [cr.x, q) with pmax_p >= s (pmax non-decreasing inside a chromosome)
-  const int lo_lim = max(cr.x, w0);
-  lo = lo_lim;
-  hi = q;
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if (w_pm[mid - w0] >= s) hi = mid; else lo = mid + 1;
-  }
-  if (lo == lo_lim && lo_lim > cr.x && lo < q) {
-    // the answer may lie below the window: first tile (from the chromosome's) whose inclusive
-    // prefix reaches (c, s), then the first position inside it
-    const unsigned long long key = (static_cast<unsigned long long>(c) << 32) | static_cast<unsigned>(s);
-    int tb = cr.x / kTile, te = w0 / kTile;
-    while (tb < te) {
-      const int mid = (tb + te) >> 1;
-      if (tile_incl.incl(mid) >= key) te = mid; else tb = mid + 1;
-    }
-    if (tb < w0 / kTile) {
-      unsigned long long m = tb > 0 ? tile_incl.incl(tb - 1) : 0ull;
-      int p = tb * kTile;
-      for (; p < w0; ++p) {
-        m = max_u64(m, endkey[p]);
-        if (m >= key) break;
+    if (lo == hi_lim && hi_lim < cr.y) {   // range leaves the window: gallop on in global memory
+      int step = 1;
+      hi = lo;
+      while (hi < cr.y && s_start[hi] <= e) {
+        lo = hi + 1;
+        hi = lo + step;
+        step <<= 1;
       }
-      lo = max(p, cr.x);
+      if (hi > cr.y) hi = cr.y;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (s_start[mid] <= e) lo = mid + 1; else hi = mid;
+      }
     }
+    const int n_fwd = lo - q - 1;
+    // backward: first p in [cr.x, q) with pmax_p >= s (pmax non-decreasing inside a chromosome)
+    const int lo_lim = max(cr.x, w0);
+    lo = lo_lim;
+    hi = q;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (w_pm[mid - w0] >= s) hi = mid; else lo = mid + 1;
+    }
+    if (lo == lo_lim && lo_lim > cr.x && lo < q) {
+      // the answer may lie below the window: first tile (from the chromosome's) whose inclusive
+      // prefix reaches (c, s), then the first position inside it
+      const unsigned long long key = (static_cast<unsigned long long>(c) << 32) | static_cast<unsigned>(s);
+      int tb = cr.x / kTile, te = w0 / kTile;
+      while (tb < te) {
+        const int mid = (tb + te) >> 1;
+        if (tile_incl.incl(mid) >= key) te = mid; else tb = mid + 1;
+      }
+      if (tb < w0 / kTile) {
+        unsigned long long m = tb > 0 ? tile_incl.incl(tb - 1) : 0ull;
+        int p = tb * kTile;
+        for (; p < w0; ++p) {
+          m = max_u64(m, endkey[p]);
+          if (m >= key) break;
+        }
+        lo = max(p, cr.x);
+      }
+    }
+    rng_s[q] = make_int2(n_fwd, lo);
   }
-  rng_s[q] = make_int2(n_fwd, lo);
 }
 
 __global__ void k_set_thr(const int* __restrict__ thr, int4* __restrict__ iv, const int* __restrict__ qpos,
@@ -443,11 +483,11 @@ hipError_t launch_build_index(const IndexBufs& b, int n, int ni, int n_chroms, h
   hipError_t e;
   size_t tb = b.temp_bytes;
   if (b.dchrom && n_chroms <= kMaxFusedChroms) {
-    const int nsub = (ni + kSub - 1) / kSub;
-    k_chrom_count<<<(nsub + 3) / 4, 256, 0, s>>>(b.dchrom, ni, nsub, b.chist);
-    k_chrom_scan<<<n_chroms, 1024, 0, s>>>(b.chist, nsub, b.crange);
-    k_chrom_scatter<<<(nsub + 3) / 4, 256, 0, s>>>(b.dchrom, b.drec, b.dgate, b.chist, ni, nsub, b.idx4, b.idx_gate,
-                                                   b.s_start, b.endkey, b.vals);
+    const int ntl = (ni + kChromTile - 1) / kChromTile;
+    k_chrom_count<<<ntl, kTileThreads, 0, s>>>(b.dchrom, ni, ntl, b.chist);
+    k_chrom_scan<<<n_chroms, 1024, 0, s>>>(b.chist, ntl, b.crange);
+    k_chrom_scatter<<<ntl, kTileThreads, 0, s>>>(b.dchrom, b.drec, b.dgate, b.chist, ni, ntl, b.idx4, b.idx_gate,
+                                                 b.s_start, b.endkey, b.vals);
     k_qpos_gather<<<grid_for((n + 63) / 64, 4), 256, 0, s>>>(b.rmeta, b.data_pos, b.vals, n, ni, b.shard, b.n_shards,
                                                               b.qpos);
     k_tile_max<<<grid_for(ni, kTile), kTile, 0, s>>>(b.endkey, ni, b.pmaxkey);
@@ -471,7 +511,7 @@ hipError_t launch_build_index(const IndexBufs& b, int n, int ni, int n_chroms, h
   unsigned long long *tmax = b.pmaxkey, *tloc = b.pmaxkey + nt, *grp = b.pmaxkey + 2 * nt;
   k_tile_scan_local<<<ng, kGroup, 0, s>>>(tmax, nt, tloc, grp);
   k_group_scan<<<1, kGroup, 0, s>>>(grp, ng);
-  k_ranges<<<nt, kRangeBlock, 0, s>>>(b.idx4, b.shard, b.n_shards, b.s_start, b.endkey, TilePrefix{tloc, grp},
+  k_ranges<<<(ni + kRangeSpan - 1) / kRangeSpan, kRangeBlock, 0, s>>>(b.idx4, b.shard, b.n_shards, b.s_start, b.endkey, TilePrefix{tloc, grp},
                                       b.crange, ni, b.rng_s);
   return hipGetLastError();
 }
