@@ -52,6 +52,7 @@ struct fslr_ctx {
   unsigned short* edge_iu = nullptr;
   int64_t edge_cap = 0;
   int* fwd = nullptr;
+  int* heavy = nullptr;      // [N] reads handed to the partitioned pair-kernel launch
   int* parent = nullptr;
   unsigned long long* counters = nullptr;
   unsigned long long* wstat = nullptr;       // [wstat_waves x kWStride] per-wave statistics of the pair kernel
@@ -100,6 +101,7 @@ int ensure_capacity(fslr_ctx* c, int64_t n, int64_t ni, int n_chroms) {
   int rc;
   if (n > c->cap_n) {
     if ((rc = dalloc(c, &c->rmeta, n)) || (rc = dalloc(c, &c->fwd, n)) || (rc = dalloc(c, &c->parent, n)) ||
+        (rc = dalloc(c, &c->heavy, n)) ||
         (rc = dalloc(c, &c->lbounds, n)))
       return rc;
 #ifdef FSLR_SECTION_PROF
@@ -183,7 +185,7 @@ void fslr_ctx_destroy(fslr_ctx* c) {
                   c->crange, c->keys,   c->keys2,   c->vals,    c->vals2,   c->endkey,  c->pmaxkey,
                   c->temp,   c->umax,   c->edges,   c->edge_iu, c->fwd,     c->parent,  c->counters,
                   c->errw,   c->thr_tmp, c->defer,   c->dchrom,  c->drec,    c->lbounds, c->diag, c->wstat,
-                  c->dgate,  c->chist};
+                  c->dgate,  c->chist,  c->heavy};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->ev_ok)
@@ -468,6 +470,7 @@ static int query_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_
   g.edge_iu = c->edge_iu;
   g.edge_cap = c->edge_cap;
   g.fwd = c->fwd;
+  g.heavy = c->heavy;
   g.counters = c->counters;
   g.err = c->errw;
   g.mode = c->ablate;

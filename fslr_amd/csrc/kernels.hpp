@@ -35,9 +35,11 @@ enum Counter { kEdgeCount = 0,          // atomic (own 128-B line)
                kEval = 32, kJacc = 33, kCand = 34, kAlgoBytes = 35, kOverflow = 36, kGather = 37,
                kMatchEntries = 38, kMatchedPairs = 39, kMaxFwd = 40,
                kSecBase = 48,           // FSLR_SECTION_PROF builds: per-section cycle sums of the pair kernel
+               kHeavyCount = 64,        // atomic (own 128-B line): reads handed to the partitioned launch
                kQueueBase = 80,         // pair kernel work queues: 8 counters, one 128-B line each
                kQueueStride = 16,
-               kNumCounters = kQueueBase + 8 * kQueueStride };
+               kQueueBase2 = kQueueBase + 8 * kQueueStride,   // the partitioned launch's queues
+               kNumCounters = kQueueBase2 + 8 * kQueueStride };
 // per-wave statistics of query_kernel: fields 0..8 (sum, except kWsMaxFwd: max), then (section-
 // timing builds) 8 section sums, slowest read cycles (max), its rank, wave cycles max / min,
 // wave count, cycle sums of reads 0, 1 and >= 2 of the wave
@@ -91,6 +93,8 @@ struct QueryArgs {
   int shard, n_shards;                // query reads: blocks of 64 ranks of [a_begin, a_end) dealt round robin
   int nv;                             // (launch_query) number of this shard's query reads
   int k_static;                       // (launch_query) grid-stride sweeps before the work queues
+  int pass_records;                   // (launch_query) forward records per partner partition (0: one pass)
+  int* heavy;                         // [a_end] reads for the partitioned launch (query_kernel<., true>)
   int2* edges;
   unsigned short* edge_iu;
   long long edge_cap;

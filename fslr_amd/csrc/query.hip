@@ -26,6 +26,7 @@
 #include "fslr_hip.h"
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "kernels.hpp"
 
@@ -42,6 +43,7 @@ constexpr int kHashBits = 9;
 constexpr int kHashSize = 1 << kHashBits;
 constexpr int kHashLimit = 320;           // insert while distinct partners < limit (load <= 75 %)
 constexpr int kMatchCap = 192;            // match-list entries per query read
+constexpr int kPassRecords = 512;         // walk records per partner partition (the hash holds 320)
 constexpr unsigned kEpochShift = 25;      // key = epoch << 25 | B  (B < FSLR_MAX_READS = 2^25)
 constexpr unsigned kEpochMax = 127;
 constexpr unsigned kBMask = 0x1FFFFFFu;
@@ -109,6 +111,11 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// partner partition of read B (a multiplier independent of the hash slot's)
+__device__ __forceinline__ int part_of(int B, int npass) {
+  return static_cast<int>(((static_cast<unsigned>(B) * 0x85EBCA6Bu) >> 8) % static_cast<unsigned>(npass));
 }
 
 // interval accepts overlap o (fslr_hip.h: thr >= 0 ? o >= thr : o <= ~thr)
@@ -239,7 +246,11 @@ struct DeferStage {
   }
 };
 
-template <int kThrMode>
+// kMulti = false: every query read of the shard; a read whose walk exceeds 1.5 pass_records records
+// (more partners than the hash holds) is handed to the kMulti = true launch (fwd[a] = -1, listed
+// by k_collect_heavy).
+// kMulti = true: the handed-over reads, each in ceil(R / pass_records) partner partitions.
+template <int kThrMode, bool kMulti>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) void query_kernel(QueryArgs g) {
   __shared__ unsigned hash_all[kWavesPerBlock][kHashSize];
   __shared__ unsigned state_all[kWavesPerBlock][kHashSize];
@@ -272,15 +283,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
   const int nwaves = gridDim.x * kWavesPerBlock;
   const int wid = blockIdx.x * kWavesPerBlock + threadIdx.x / kWave;
   const int a_hi = g.a_end;
+  // kMulti: the list's length is only known on the device (written by the kMulti = false launch)
+  const int nv = kMulti ? static_cast<int>(min(static_cast<long long>(g.counters[kHeavyCount]),
+                                               static_cast<long long>(g.a_end)))
+                        : g.nv;
   auto rank_of = [&](int v) {
+    if (kMulti) return v < 0 || v >= nv ? a_hi : ((const_i32_ptr)(g.heavy))[v];
     return v < 0 ? a_hi
                  : g.a_begin + ((((v >> kShardShift) * g.n_shards + g.shard) << kShardShift) | (v & kShardMask));
   };
   const int k_static = g.k_static;
   const int v0 = k_static * nwaves;                           // first dynamic index
-  const int nchunks = (g.nv - v0 + kChunk - 1) / kChunk;
+  const int nchunks = (nv - v0 + kChunk - 1) / kChunk;
   const int q_home = static_cast<int>(__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20)) & 7;   // XCC_ID
-  unsigned long long* queues = g.counters + kQueueBase;
+  unsigned long long* queues = g.counters + (kMulti ? kQueueBase2 : kQueueBase);
   auto reserve = [&](int q) -> int {       // ticket on queue q (wave-uniform)
     int k = 0;
     if (lane_id() == 0) k = static_cast<int>(atomicAdd(&queues[q * kQueueStride], 1ull));
@@ -301,7 +317,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
     while (true) {
       if (cur_c >= 0 && cur_i < kChunk) {
         const int v = v0 + cur_c * kChunk + cur_i++;
-        if (v < g.nv) return v;
+        if (v < nv) return v;
       }
       if (cur_c == -1 || nchunks <= 0) return -1;
       // take the reserved chunk; if its queue is drained, steal from the next queues
@@ -373,11 +389,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
     // issued and the walk's first loads, instead of stalling the next wait on its own
     v_4 = pull();
     const int4 alb = sload4(g.lb, a);
-    if (++epoch > kEpochMax) {
-      wave_lds_sync();
-      for (int k = lane; k < kHashSize; k += kWave) H[k] = 0u;
-      epoch = 1;
-    }
     const int amy = am.y;
     const int LA = amy & 0xffff;
     const bool hazA = (static_cast<unsigned>(amy) >> 16) & 1u;
@@ -393,7 +404,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
     // interval i's records r in [ex, ex + cnt) are two runs of sorted positions:
     // forward r < bnd: p = r + off_f;  backward: p = r + off_b
     const int bnd = ex + rg.y, off_f = rg.x + 1 - ex, off_b = rg.z - rg.y - ex;
-    int uniq = 0, mln = 0, mpn = 0, fwdA = 0;
+    int fwdA = 0;
 
     // record r of A's walk → (interval mi, sorted position p, forward?)
     auto map_record = [&](int base, int& mi, int& p, bool& fwd) {
@@ -410,6 +421,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
       p = r + (fwd ? of_i : ob_i);
     };
 
+    // Partner partitions: a read whose walk is longer than kPassRecords records may have more
+    // distinct partners than the hash holds, so its walk is repeated npass times, pass k taking the
+    // partners B with part(B) == k (each pair still evaluated exactly once, in one pass).  Dense
+    // inputs (10M reads on the same genome: ~700 hits per read) would otherwise defer most
+    // candidates to the witness path, one wavefront per candidate.
+    // one pass of the walk + greedy over the partners of partition `pass` (kParts: of npass > 1)
+    auto walk_pass = [&](auto multi, int pass, int npass) __attribute__((always_inline)) {
+    constexpr bool kParts = decltype(multi)::value;
+    if (++epoch > kEpochMax) {
+      wave_lds_sync();
+      for (int k = lane; k < kHashSize; k += kWave) H[k] = 0u;
+      epoch = 1;
+    }
+    int uniq = 0, mln = 0, mpn = 0;
     int mi_c = 0, p_c = 0;
     bool fwd_c = false;
     int4 rec_c = make_int4(0, -1, 0, 0);
@@ -442,9 +467,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
       SEC_NOW(t_s2);
       const int s_i = __shfl(my.x, mi), e_i = __shfl(my.y, mi), t_i = __shfl(my.z, mi);
       const bool hit = valid && (fwd || rec.y >= s_i);
-      w_cand += __popcll(__ballot(hit));
+      if (!kParts || pass == 0) w_cand += __popcll(__ballot(hit));
       const int B = rec.w >> 6;
-      const bool cand = hit && B > a;
+      const bool cand = hit && B > a && (!kParts || part_of(B, npass) == pass);
       // ---- dedupe: per-wave LDS hash set of partners (the reference's seen-set) ----------
       const bool ins_mode = uniq < kHashLimit;
       bool isnew = false, over = false;
@@ -609,7 +634,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
     SEC_ADD(6, t_s6);
     w_ml += mln;
     w_mp += mpn;
-    if (lane == 0) g.fwd[a] = fwdA;
+    };
+    // R (the walk's records) bounds the distinct partners; a read whose walk is more than 1.5
+    // partitions long goes to the partitioned launch, which splits it into ~pass_records-record parts
+    const int pr = g.pass_records;
+    bool handed = false;
+    if constexpr (!kMulti) {
+      // to the partitioned launch: marked by fwd[a] = -1 (k_collect_heavy lists the marked reads;
+      // a pointer and an atomic here cost the kernel registers it does not have)
+      handed = pr > 0 && R > pr + (pr >> 1);
+      if (!handed) walk_pass(std::false_type{}, 0, 1);
+    } else {
+      const int npass = pr > 0 ? max(1, (R + pr - 1) / pr) : 1;
+      for (int pass = 0; pass < npass; ++pass) walk_pass(std::true_type{}, pass, npass);
+    }
+    if (lane == 0) g.fwd[a] = handed ? -1 : fwdA;
     w_maxfwd = max(w_maxfwd, fwdA);
 #ifdef FSLR_SECTION_PROF
     {
@@ -661,7 +700,38 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
     f = lane == kWsBase + 12 ? 1ull : f;
     for (int k = 0; k < 3; ++k) f = lane == kWsBase + 13 + k ? it_sum[k] : f;
 #endif
-    if (lane < kWsProf) g.wstat[static_cast<long long>(wid) * kWStride + lane] = f;
+    if constexpr (!kMulti) {
+      if (lane < kWsProf) g.wstat[static_cast<long long>(wid) * kWStride + lane] = f;
+    } else if (w_cand != 0) {
+      // the partitioned launch: few waves have work at typical densities, so those add their
+      // statistics directly (no per-wave slots, no reduction launch)
+      if (lane == kWsMaxFwd) {
+        if (f) atomicMax(g.err + 3, static_cast<int>(f));
+      } else if (lane < kWsBase && f) {
+        const int dst = lane == kWsEval ? kEval : lane == kWsJacc ? kJacc : lane == kWsCand ? kCand
+                      : lane == kWsAlgoBytes ? kAlgoBytes : lane == kWsOverflow ? kOverflow
+                      : lane == kWsMatchEntries ? kMatchEntries : kMatchedPairs;
+        atomicAdd(&g.counters[dst], f);
+      }
+    }
+  }
+}
+
+// The reads query_kernel<., false> handed over (fwd == -1) as a list for query_kernel<., true>:
+// one atomic per wave with marked reads; list order is irrelevant (work queues deal it).
+__global__ __launch_bounds__(256) void k_collect_heavy(const int* __restrict__ fwd, int a0, int a1,
+                                                       int* __restrict__ heavy,
+                                                       unsigned long long* __restrict__ counters) {
+  const int lane = threadIdx.x & 63;
+  for (int b = a0 + (blockIdx.x * blockDim.x + threadIdx.x - lane); b < a1; b += gridDim.x * blockDim.x) {
+    const int a = b + lane;
+    const bool h = a < a1 && fwd[a] < 0;
+    const unsigned long long m = __ballot(h);
+    if (!m) continue;
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(&counters[kHeavyCount], static_cast<unsigned long long>(__popcll(m)));
+    base = __shfl(base, 0);
+    if (h) heavy[base + mbcnt(m)] = a;
   }
 }
 
@@ -815,13 +885,13 @@ __global__ __launch_bounds__(256) void deferred_kernel(QueryArgs g) {
 }
 
 // resident grid: waves walk the read ranks grid-stride, so launch exactly what fits on the chip
-template <int kThrMode>
+template <int kThrMode, bool kMulti>
 int resident_blocks() {
   static int cached = 0;
   if (cached) return cached;
   int dev = 0, cus = 256, per_cu = 0;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, query_kernel<kThrMode>, kBlock, 0) != hipSuccess ||
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, query_kernel<kThrMode, kMulti>, kBlock, 0) != hipSuccess ||
       per_cu < 1)
     per_cu = 4;
   cached = cus * per_cu;
@@ -831,8 +901,9 @@ int resident_blocks() {
 }  // namespace
 
 int query_max_waves() {
-  const int b0 = resident_blocks<0>(), b1 = resident_blocks<1>();
-  return (b0 > b1 ? b0 : b1) * kWavesPerBlock;
+  const int b = std::max(std::max(resident_blocks<0, false>(), resident_blocks<1, false>()),
+                         std::max(resident_blocks<0, true>(), resident_blocks<1, true>()));
+  return b * kWavesPerBlock;
 }
 
 hipError_t launch_query(const QueryArgs& a_in, int thr_mode, hipStream_t s) {
@@ -854,7 +925,7 @@ hipError_t launch_query(const QueryArgs& a_in, int thr_mode, hipStream_t s) {
 #ifdef FSLR_SECTION_PROF
     if (const char* e = getenv("FSLR_QUERY_BLOCKS")) want = std::min(want, std::max(1ll, atoll(e)));
 #endif
-    const int cap = thr_mode == 0 ? resident_blocks<0>() : resident_blocks<1>();
+    const int cap = thr_mode == 0 ? resident_blocks<0, false>() : resident_blocks<1, false>();
     const int blocks = static_cast<int>(want < cap ? want : cap);
     if (blocks * kWavesPerBlock > a.wstat_waves) return hipErrorInvalidValue;   // capi sizes wstat
     if (blocks > 0) {
@@ -862,17 +933,32 @@ hipError_t launch_query(const QueryArgs& a_in, int thr_mode, hipStream_t s) {
       // imbalance of a static deal is then large and each ticket's atomic is amortised over
       // kChunk reads); a static grid-stride deal when the shard is small (multi-GPU shards)
       const long long nw = static_cast<long long>(blocks) * kWavesPerBlock;
+      a.pass_records = kPassRecords;
+      // FSLR_PASS_RECORDS (tests): 0 turns partner partitions off, so the hash-overflow (witness)
+      // path is exercised at small sizes
+      if (const char* e = getenv("FSLR_PASS_RECORDS")) a.pass_records = atoi(e);
       long long dyn_min = kDynamicMinReads;
       // FSLR_DYNAMIC_MIN_READS: lets the parity tests drive the work-queue path at small sizes
       if (const char* e = getenv("FSLR_DYNAMIC_MIN_READS")) dyn_min = std::max(0ll, atoll(e));
       a.k_static = nq >= dyn_min * nw ? 0 : static_cast<int>((nq + nw - 1) / nw);
       if (thr_mode == 0)
-        query_kernel<0><<<blocks, kBlock, 0, s>>>(a);
+        query_kernel<0, false><<<blocks, kBlock, 0, s>>>(a);
       else
-        query_kernel<1><<<blocks, kBlock, 0, s>>>(a);
+        query_kernel<1, false><<<blocks, kBlock, 0, s>>>(a);
       const int nwv = blocks * kWavesPerBlock;
       const int rb = std::min(kReduceMaxBlocks, (nwv + kWave - 1) / kWave);
       k_reduce_wstat<<<rb, kReduceBlock, 0, s>>>(a.wstat, nwv, a.counters, a.err);
+      if (a.heavy != nullptr && a.pass_records > 0) {
+        // the reads handed over (their number is on the device): a resident grid on work queues
+        k_collect_heavy<<<grid_for(span), 256, 0, s>>>(a.fwd, a.a_begin, a.a_end, a.heavy, a.counters);
+        const int hb = thr_mode == 0 ? resident_blocks<0, true>() : resident_blocks<1, true>();
+        if (hb * kWavesPerBlock > a.wstat_waves) return hipErrorInvalidValue;
+        a.k_static = 0;
+        if (thr_mode == 0)
+          query_kernel<0, true><<<hb, kBlock, 0, s>>>(a);
+        else
+          query_kernel<1, true><<<hb, kBlock, 0, s>>>(a);
+      }
     }
   }
   // the deferred list's length is only known on the device: a fixed grid walks it

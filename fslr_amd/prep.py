@@ -47,6 +47,19 @@ def first_last_masks(codes: np.ndarray):
     last = np.zeros(n, dtype=bool)
     if n == 0:
         return first, last
+    codes = np.asarray(codes)
+    # fast path, O(n): every code's rows form one contiguous run (a BED sorted by qname, as
+    # collect_mapping_info.py:174 writes it) -> first / last rows are the run boundaries
+    brk = np.flatnonzero(codes[1:] != codes[:-1]) + 1
+    starts = np.concatenate(([0], brk))
+    if codes.dtype.kind in 'iu' and codes.min() >= 0 and codes.max() < 4 * n + 1024:
+        n_distinct = int(np.count_nonzero(np.bincount(codes)))
+    else:
+        n_distinct = int(np.unique(codes[starts]).size) if starts.size < n else n
+    if n_distinct == starts.size:
+        first[starts] = True
+        last[np.concatenate((brk - 1, [n - 1]))] = True
+        return first, last
     _, fi = np.unique(codes, return_index=True)
     _, li = np.unique(codes[::-1], return_index=True)
     first[fi] = True
@@ -173,12 +186,23 @@ def build_csr(data: IntervalData) -> CSR:
     n_iv = len(data)
     codes = np.asarray(data.qcode, dtype=np.int64)
     if n_iv:
-        uniq, first = np.unique(codes, return_index=True)
+        # rank = order of first appearance (cluster.py:189-191); codes are non-negative ints
+        if codes.min() >= 0 and codes.max() < 4 * n_iv + 1024:
+            first_at = np.full(int(codes.max()) + 1, n_iv, dtype=np.int64)
+            np.minimum.at(first_at, codes, np.arange(n_iv, dtype=np.int64))
+            uniq = np.flatnonzero(first_at < n_iv)
+            first = first_at[uniq]
+        else:
+            uniq, first = np.unique(codes, return_index=True)
         order = np.argsort(first, kind='stable')
         rank_of = np.empty(int(uniq.max()) + 1, dtype=np.int64)
         rank_of[uniq[order]] = np.arange(uniq.size, dtype=np.int64)
         rank = rank_of[codes]
-        perm = np.argsort(rank, kind='stable')
+        # stable grouping by rank == sort of the distinct keys rank << 32 | data position
+        key = (rank << 32) | np.arange(n_iv, dtype=np.int64)
+        key.sort()
+        perm = key & 0xFFFFFFFF
+        del key
         counts = np.bincount(rank, minlength=uniq.size)
         read_qcode = uniq[order]
     else:
@@ -197,7 +221,14 @@ def build_csr(data: IntervalData) -> CSR:
     if n_iv and (start.min() < 0 or end.max() >= MAX_COORD):
         raise ValueError('interval coordinates must lie in [0, 2**30) for the device path')
     chrom_raw = np.asarray(data.chrom, np.int64)[perm]
-    cids, chrom_dense = np.unique(chrom_raw, return_inverse=True) if n_iv else (np.zeros(0), np.zeros(0, np.int64))
+    if n_iv and chrom_raw.min() >= 0 and chrom_raw.max() < (1 << 24):
+        present = np.bincount(chrom_raw) > 0          # chromosome ids are small ints: O(n) dense ids
+        cids = np.flatnonzero(present)
+        chrom_dense = (np.cumsum(present) - 1)[chrom_raw]
+    elif n_iv:
+        cids, chrom_dense = np.unique(chrom_raw, return_inverse=True)
+    else:
+        cids, chrom_dense = np.zeros(0), np.zeros(0, np.int64)
     first_iv = perm[off[:-1]] if n else np.zeros(0, dtype=np.int64)
     qlen2 = np.asarray(data.qlen2, np.int64)
     nal = np.asarray(data.n_alignments, np.int64)

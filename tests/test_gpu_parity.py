@@ -255,6 +255,52 @@ def test_many_chromosomes_vs_oracle(ctx, split, mod):
     compare_with_oracle(g, o, csr.n_reads)
 
 
+@pytest.mark.parametrize('squeeze', [100, 400])
+def test_dense_overlaps_vs_oracle(ctx, squeeze):
+    """Dense inputs (the 10M-read config's regime): starts squeezed onto 1/squeeze of the genome,
+    so walks run to ~350 / ~1400 records per read and reads take several partner partitions."""
+    import dataclasses
+    s = synth.generate(30_000, 16, 41)
+    csr = s.interval_data().csr()
+    st = csr.iv_start.astype(np.int64) // squeeze          # monotone: the data order stays start-sorted
+    en = st + (csr.iv_end.astype(np.int64) - csr.iv_start)
+    csr = dataclasses.replace(csr, iv_start=st.astype(np.int32), iv_end=en.astype(np.int32))
+    g = gpu_run(ctx, csr)
+    o = O.run_core(oracle_from_csr(csr), use_cap=False)
+    compare_with_oracle(g, o, csr.n_reads)
+
+
+@pytest.mark.parametrize('pass_records', [None, '0', '500'])
+def test_one_locus_many_partners_vs_oracle(ctx, monkeypatch, pass_records):
+    """1500 reads on one interval: every pair overlaps.  Default: up to 6 partner partitions per
+    read; '0': one partition, the hash overflows (witness path); '500': partitions of ~500 partners,
+    which overflow within a partition."""
+    if pass_records is not None:
+        monkeypatch.setenv('FSLR_PASS_RECORDS', pass_records)
+    n = 1500
+    off = np.arange(n + 1, dtype=np.int64)
+    chrom = np.zeros(n, np.int32)
+    start = np.full(n, 5000, np.int32) + (np.arange(n) % 7).astype(np.int32)
+    start = np.sort(start)
+    end = start + 1000
+    aln = np.full(n, 1000, np.int64)
+    q = np.full(n, 100, np.int32)
+    m = np.full(n, 3, np.int32)
+    thr = fold_overlap_threshold(aln, 0.8)
+    ctx.set_reads(off, q, m, chrom, start, end, thr, 1, iv_data_pos=np.arange(n))
+    ctx.reserve_edges(n * n)
+    ctx.build_index()
+    st = ctx.run_query(1 - 0.04, 1 - 0.25, pass_table([1.0]))
+    ctx.components()
+    a, b, I, U = ctx.edges(st['n_edges'])
+    g = dict(stats=st, labels=ctx.labels(), fwd=ctx.fwd_degree(), a=a, b=b, I=I, U=U)
+    o = O.run_core(O.OracleCSR(off, chrom, start, end, aln, q, m, np.arange(n)), 0.8, (1.0,), 0.04, 0.25,
+                   use_cap=False)
+    if pass_records is not None:
+        assert st['overflow_candidates'] > 0
+    compare_with_oracle(g, o, n)
+
+
 def test_rerun_is_deterministic(ctx):
     s = synth.generate(30_000, 16, 2)
     csr = s.interval_data().csr()
@@ -305,10 +351,11 @@ def _boundary_pool(cut, top, rng):
 
 @pytest.mark.parametrize('qlen_diff,nal_diff', [(0.04, 0.25), (0.0, 0.0), (1.0, 1.0), (1.5, -0.5), (-0.5, 1.5),
                                                 (0.34, 0.999999), (1e-12, 0.5)])
-def test_length_gate_boundaries_vs_oracle(ctx, qlen_diff, nal_diff):
+def test_length_gate_boundaries_vs_oracle(ctx, monkeypatch, qlen_diff, nal_diff):
     """400 reads with one identical interval each (every pair overlaps, so every pair is evaluated
     and the first reads overflow the per-read partner hash): qlen2 / n_alignments drawn around the
     exact ratio boundaries of cluster.py:178-183; one read each with qlen2 == 0 and nal == 0."""
+    monkeypatch.setenv('FSLR_PASS_RECORDS', '0')      # one partner partition: the hash overflows
     rng = np.random.default_rng(int(1000 * (qlen_diff + 2 * nal_diff)) & 0xFFFF)
     n = 400
     q = _boundary_pool(1 - qlen_diff, (1 << 31) - 1, rng)

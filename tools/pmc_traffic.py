@@ -38,7 +38,7 @@ def collect(root, kernel):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('root')
-    ap.add_argument('--kernel', default='query_kernel<0>')
+    ap.add_argument('--kernel', default='query_kernel<0, false>')
     ap.add_argument('-o', '--out', default=None)
     ap.add_argument('--source-hash', default=None, help='hash of the kernel sources the counters were taken on')
     args = ap.parse_args()
