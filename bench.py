@@ -169,7 +169,8 @@ def main():
     achieved = st['algo_bytes'] / (kernel_ms / 1000.0)
     traffic = None
     traffic_src = None
-    if args.traffic_json and os.path.exists(args.traffic_json):
+    # the committed PMC summary is of the single-GPU launch (all query reads); a shard's launch moves less
+    if world == 1 and args.traffic_json and os.path.exists(args.traffic_json):
         with open(args.traffic_json) as fh:
             tj = json.load(fh)
         if tj.get('source_hash') == kernel_source_hash():
