@@ -293,7 +293,7 @@ class Context:
         self._check(self._L.fslr_copy_fwd_device(self._h, ctypes.c_void_p(dptr)))
 
     def union_pairs(self, src, dst, n, on_device: bool):
-        """Union (src[k], dst[k]); ``src`` None means src[k] = k.  Pointers are ints when on_device."""
+        """Union (src[k], dst[k]); ``src`` None means src[k] = k mod n_reads.  Pointers are ints when on_device."""
         if on_device:
             self._check(self._L.fslr_union_pairs(self._h, ctypes.c_void_p(src) if src else None,
                                                  ctypes.c_void_p(dst), int(n), 1))

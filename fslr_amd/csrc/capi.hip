@@ -655,7 +655,8 @@ int fslr_union_pairs(fslr_ctx* c, const int32_t* src, const int32_t* dst, int64_
       ds = tmp + n;
     }
   }
-  HIP_TRY(c, launch_uf_pairs(c->parent, ds, dd, n, c->stream));
+  if (!src && !c->n) return fail(c, FSLR_ERR_INVALID, "no reads");
+  HIP_TRY(c, launch_uf_pairs(c->parent, ds, dd, n, static_cast<int>(c->n), c->stream));
   if (tmp) {
     HIP_TRY(c, hipFreeAsync(tmp, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));

@@ -59,10 +59,11 @@ __global__ void k_uf_edges(int* p, const int2* __restrict__ edges, const unsigne
   }
 }
 
-__global__ void k_uf_pairs(int* p, const int* __restrict__ src, const int* __restrict__ dst, long long n) {
+__global__ void k_uf_pairs(int* p, const int* __restrict__ src, const int* __restrict__ dst, long long n,
+                           int period) {
   for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < n;
        k += static_cast<long long>(gridDim.x) * blockDim.x) {
-    const int s = src ? src[k] : static_cast<int>(k);
+    const int s = src ? src[k] : static_cast<int>(k % period);
     uf_union(p, s, dst[k]);
   }
 }
@@ -85,8 +86,8 @@ hipError_t launch_uf_edges(int* parent, const int2* edges, const unsigned long l
   return hipGetLastError();
 }
 
-hipError_t launch_uf_pairs(int* parent, const int* src, const int* dst, long long n, hipStream_t s) {
-  if (n > 0) k_uf_pairs<<<grid_for(n), 256, 0, s>>>(parent, src, dst, n);
+hipError_t launch_uf_pairs(int* parent, const int* src, const int* dst, long long n, int period, hipStream_t s) {
+  if (n > 0 && period > 0) k_uf_pairs<<<grid_for(n), 256, 0, s>>>(parent, src, dst, n, period);
   return hipGetLastError();
 }
 

@@ -117,7 +117,8 @@ int query_max_waves();
 hipError_t launch_uf_init(int* parent, int n, hipStream_t s);
 hipError_t launch_uf_edges(int* parent, const int2* edges, const unsigned long long* count, long long cap,
                            hipStream_t s);
-hipError_t launch_uf_pairs(int* parent, const int* src, const int* dst, long long n, hipStream_t s);
+// src == nullptr: src[k] = k mod period
+hipError_t launch_uf_pairs(int* parent, const int* src, const int* dst, long long n, int period, hipStream_t s);
 hipError_t launch_uf_finalize(int* parent, int n, hipStream_t s);
 
 inline int grid_for(long long n, int block = 256, int cap = 256 * 16) {

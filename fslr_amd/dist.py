@@ -91,8 +91,7 @@ class DeviceShardMerge:
             self.gathered.copy_(out)
         else:
             dist.all_gather_into_tensor(self.gathered, self.local)
-        base = self.gathered.data_ptr()
-        for g in range(self.world):
-            if g != self.rank:
-                self.ctx.union_pairs(None, base + 4 * g * self.n, self.n, on_device=True)
+        # one launch over all W label vectors (src = k mod n; this rank's own vector unions each
+        # read with its own root, a no-op)
+        self.ctx.union_pairs(None, self.gathered.data_ptr(), self.world * self.n, on_device=True)
         self.ctx.finalize_labels()

@@ -177,8 +177,9 @@ int  fslr_copy_labels_device(fslr_ctx *ctx, int32_t *dst);
 /* Copy the [n_reads] forward degrees into a caller-owned device buffer (async, ctx stream). */
 int  fslr_copy_fwd_device(fslr_ctx *ctx, int32_t *dst);
 /* Union (src[k], dst[k]) into the context's forest; pointers are device pointers
- * on this context's device when on_device != 0, else host.  Follow with
- * fslr_finalize_labels.  Async. */
+ * on this context's device when on_device != 0, else host.  src == NULL means
+ * src[k] = k mod n_reads, so W concatenated label vectors merge in one call.
+ * Follow with fslr_finalize_labels.  Async. */
 int  fslr_union_pairs(fslr_ctx *ctx, const int32_t *src, const int32_t *dst, int64_t n, int on_device);
 int  fslr_finalize_labels(fslr_ctx *ctx);
 
