@@ -270,6 +270,42 @@ def test_dense_overlaps_vs_oracle(ctx, squeeze):
     compare_with_oracle(g, o, csr.n_reads)
 
 
+@pytest.mark.parametrize('n_shards', [3])
+def test_dense_shards_with_partitioned_launch_vs_oracle(n_shards):
+    """Dense input (most reads handed to the partitioned launch) queried as shards of a
+    shard-built index (fslr_set_shard), one context per shard: the union of the shards' edges,
+    forward degrees and pair counts equals the oracle's."""
+    import dataclasses
+    s = synth.generate(20_000, 16, 43)
+    csr = s.interval_data().csr()
+    st0 = csr.iv_start.astype(np.int64) // 400
+    en0 = st0 + (csr.iv_end.astype(np.int64) - csr.iv_start)
+    csr = dataclasses.replace(csr, iv_start=st0.astype(np.int32), iv_end=en0.astype(np.int32))
+    o = O.run_core(oracle_from_csr(csr), use_cap=False)
+    thr = fold_overlap_threshold(csr.iv_aln, 0.8)
+    pt = pass_table([1, 1, 0.66, 0.66, 0.66, 0.5])
+    edges, pairs = [], 0
+    fwd = np.zeros(csr.n_reads, np.int64)
+    for r in range(n_shards):
+        c = _lib.Context(0)
+        c.load_csr(csr, thr)
+        c.reserve_edges(64 * csr.n_reads)
+        c.set_shard(r, n_shards)
+        c.build_index()
+        c.reserve_deferred(1 << 24)
+        c.query_shard(1 - 0.04, 1 - 0.25, pt, r, n_shards)
+        st = c.stats()
+        pairs += st['evaluated_pairs']
+        edges += list(zip(*[x.tolist() for x in c.edges(st['n_edges'])]))
+        own = (np.arange(csr.n_reads) // 64) % n_shards == r
+        fwd[own] = c.fwd_degree()[own]
+        c.close()
+    assert pairs == o['stats']['evaluated_pairs']
+    assert sorted(edges) == sorted(zip(o['edge_a'].tolist(), o['edge_b'].tolist(), o['edge_I'].tolist(),
+                                       o['edge_U'].tolist()))
+    np.testing.assert_array_equal(fwd, o['fwd'])
+
+
 @pytest.mark.parametrize('pass_records', [None, '0', '500'])
 def test_one_locus_many_partners_vs_oracle(ctx, monkeypatch, pass_records):
     """1500 reads on one interval: every pair overlaps.  Default: up to 6 partner partitions per
