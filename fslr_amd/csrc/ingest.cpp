@@ -1,0 +1,312 @@
+// ingest.cpp — threaded reader for `{name}.mappings.bed` (include/fslr_ingest.h).
+// Host-only C++17; built with g++ into fslr_amd/libfslr_ingest.so.
+//
+// Layout: the file is read whole into one buffer; line starts are found by a
+// per-thread newline count + prefix sum; a column is produced by re-walking each
+// line to its k-th tab (the file stays hot in the CPU caches per chunk, and only
+// the requested columns are ever materialised).
+#include "fslr_ingest.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <string_view>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+struct FslrTsv {
+    std::string buf;                      // file contents
+    std::vector<int64_t> line;            // [rows starts | file size | rows ends] (header excluded)
+    std::vector<std::string> names;       // header
+    int n_threads = 1;
+    // last factorize result per column
+    std::vector<std::vector<std::string_view>> uniq;
+};
+
+namespace {
+
+void set_err(char *err, size_t n, const std::string &m) {
+    if (err && n) { std::snprintf(err, n, "%s", m.c_str()); }
+}
+
+template <class F>
+void parallel_for(int64_t n, int threads, F f) {
+    if (n <= 0) return;
+    int t = (int)std::min<int64_t>(threads, std::max<int64_t>(1, n / 4096));
+    if (t <= 1) { f(0, n, 0); return; }
+    std::vector<std::thread> pool;
+    for (int i = 0; i < t; ++i) {
+        int64_t a = n * i / t, b = n * (i + 1) / t;
+        pool.emplace_back([=, &f] { f(a, b, i); });
+    }
+    for (auto &th : pool) th.join();
+}
+
+// Field `col` of the line starting at `s` (line ends at `e`, '\n' and '\r' excluded).
+inline std::string_view field(const char *s, const char *e, int col) {
+    const char *p = s;
+    for (int k = 0; k < col; ++k) {
+        const void *q = std::memchr(p, '\t', (size_t)(e - p));
+        if (!q) return std::string_view(nullptr, 0);   // missing field: pandas gives NaN
+        p = (const char *)q + 1;
+    }
+    const void *q = std::memchr(p, '\t', (size_t)(e - p));
+    const char *fe = q ? (const char *)q : e;
+    return std::string_view(p, (size_t)(fe - p));
+}
+
+// Canonical decimal int64: "0" or -?[1-9][0-9]*, no "-0", in range.
+inline bool canon_int(std::string_view f, int64_t *v) {
+    size_t n = f.size(), i = 0;
+    if (n == 0 || !f.data()) return false;
+    bool neg = f[0] == '-';
+    if (neg) { if (n == 1) return false; i = 1; }
+    if (f[i] == '0') { if (n != i + 1 || neg) return false; *v = 0; return true; }
+    if (n - i > 19) return false;
+    unsigned long long x = 0;
+    for (; i < n; ++i) {
+        unsigned d = (unsigned char)f[i] - '0';
+        if (d > 9) return false;
+        x = x * 10 + d;
+    }
+    if (!neg && x > 9223372036854775807ULL) return false;
+    if (neg && x > 9223372036854775808ULL) return false;
+    *v = neg ? (int64_t)(0 - x) : (int64_t)x;
+    return true;
+}
+
+// pandas' default na_values (read_csv keep_default_na=True).
+bool is_na(std::string_view f) {
+    static const char *na[] = {"", "#N/A", "#N/A N/A", "#NA", "-1.#IND", "-1.#QNAN", "-NaN", "-nan",
+                               "1.#IND", "1.#QNAN", "<NA>", "N/A", "NA", "NULL", "NaN", "None",
+                               "n/a", "nan", "null"};
+    if (!f.data()) return true;
+    for (const char *s : na)
+        if (f == s) return true;
+    return false;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fslr_tsv_open(const char *path, int n_threads, FslrTsv **out, char *err, size_t errlen) {
+    *out = nullptr;
+    FILE *fp = std::fopen(path, "rb");
+    if (!fp) { set_err(err, errlen, std::string("cannot open ") + path); return FSLR_INGEST_ERROR; }
+    auto *t = new FslrTsv();
+    std::fseek(fp, 0, SEEK_END);
+    long sz = std::ftell(fp);
+    std::fseek(fp, 0, SEEK_SET);
+    t->buf.resize((size_t)std::max(0L, sz));
+    size_t got = sz > 0 ? std::fread(&t->buf[0], 1, (size_t)sz, fp) : 0;
+    std::fclose(fp);
+    if ((long)got != sz) { delete t; set_err(err, errlen, "short read"); return FSLR_INGEST_ERROR; }
+    t->n_threads = n_threads > 0 ? n_threads : (int)std::max(1u, std::thread::hardware_concurrency());
+    const char *b = t->buf.data();
+    const int64_t n = (int64_t)t->buf.size();
+    if (std::memchr(b, '"', (size_t)n)) { delete t; set_err(err, errlen, "quoted fields"); return FSLR_INGEST_DECLINE; }
+    // header
+    const char *nl = (const char *)std::memchr(b, '\n', (size_t)n);
+    int64_t h_end = nl ? (int64_t)(nl - b) : n;
+    int64_t body = nl ? h_end + 1 : n;
+    {
+        std::string_view h(b, (size_t)h_end);
+        if (!h.empty() && h.back() == '\r') h.remove_suffix(1);
+        size_t p = 0;
+        while (true) {
+            size_t q = h.find('\t', p);
+            t->names.emplace_back(h.substr(p, q == std::string_view::npos ? std::string_view::npos : q - p));
+            if (q == std::string_view::npos) break;
+            p = q + 1;
+        }
+    }
+    // line starts: count per chunk, prefix, fill. Blank lines are skipped (skip_blank_lines=True).
+    const int T = t->n_threads;
+    const int64_t len = n - body;
+    std::vector<int64_t> cnt(T + 1, 0);
+    auto chunk = [&](int i) { return std::make_pair(body + len * i / T, body + len * (i + 1) / T); };
+    auto nonblank = [&](int64_t p) {   // p (a line start) begins a non-blank line
+        return p < n && !(b[p] == '\n' || (b[p] == '\r' && (p + 1 >= n || b[p + 1] == '\n')));
+    };
+    // f(p) for every non-blank line start p in [a, e): body itself, and one past each '\n' (memchr scan).
+    auto for_starts = [&](int64_t a, int64_t e, auto &&f) {
+        if (a >= e) return;
+        if (a == body && nonblank(a)) f(a);
+        int64_t x = a == body ? a : a - 1;   // a newline at a-1 makes a a start
+        while (x < e - 1) {
+            const void *q = std::memchr(b + x, '\n', (size_t)(e - 1 - x));
+            if (!q) break;
+            int64_t p = (int64_t)((const char *)q - b) + 1;
+            if (nonblank(p)) f(p);
+            x = p;
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int i = 0; i < T; ++i)
+        pool.emplace_back([&, i] {
+            auto [a, e] = chunk(i);
+            int64_t c = 0;
+            for_starts(a, e, [&](int64_t) { ++c; });
+            cnt[i + 1] = c;
+        });
+    for (auto &th : pool) th.join();
+    pool.clear();
+    for (int i = 0; i < T; ++i) cnt[i + 1] += cnt[i];
+    t->line.resize((size_t)cnt[T] + 1);
+    for (int i = 0; i < T; ++i)
+        pool.emplace_back([&, i] {
+            auto [a, e] = chunk(i);
+            int64_t k = cnt[i];
+            for_starts(a, e, [&](int64_t p) { t->line[k++] = p; });
+        });
+    for (auto &th : pool) th.join();
+    // Each line ends at its own first newline (blank lines between data lines are skipped,
+    // so the next start is not the end). Layout: line[0..rows) starts, line[rows] = n,
+    // line[rows+1 .. 2*rows] ends.
+    const int64_t rows = cnt[T];
+    std::vector<int64_t> ends((size_t)rows);
+    parallel_for(rows, T, [&](int64_t a, int64_t e, int) {
+        for (int64_t i = a; i < e; ++i) {
+            const void *q = std::memchr(b + t->line[i], '\n', (size_t)(n - t->line[i]));
+            ends[i] = q ? (int64_t)((const char *)q - b) + 1 : n;
+        }
+    });
+    t->line.resize((size_t)rows * 2 + 1);
+    std::copy(ends.begin(), ends.end(), t->line.begin() + rows + 1);
+    t->line[rows] = n;
+    t->uniq.assign(t->names.size(), {});
+    *out = t;
+    return FSLR_INGEST_OK;
+}
+
+void fslr_tsv_close(FslrTsv *t) { delete t; }
+
+int64_t fslr_tsv_rows(const FslrTsv *t) { return (int64_t)(t->line.size() / 2); }
+
+int fslr_tsv_cols(const FslrTsv *t) { return (int)t->names.size(); }
+
+const char *fslr_tsv_colname(const FslrTsv *t, int col) {
+    return (col >= 0 && col < (int)t->names.size()) ? t->names[col].c_str() : nullptr;
+}
+
+int fslr_tsv_find(const FslrTsv *t, const char *name) {
+    for (size_t i = 0; i < t->names.size(); ++i)
+        if (t->names[i] == name) return (int)i;
+    return -1;
+}
+
+}  // extern "C"
+
+namespace {
+inline std::string_view row_field(const FslrTsv *t, int64_t i, int col) {
+    const int64_t rows = fslr_tsv_rows(t);
+    const char *b = t->buf.data();
+    const char *s = b + t->line[i];
+    const char *e = b + t->line[rows + 1 + i];
+    if (e > s && e[-1] == '\n') --e;
+    if (e > s && e[-1] == '\r') --e;
+    return field(s, e, col);
+}
+}  // namespace
+
+extern "C" {
+
+int fslr_tsv_int_column(const FslrTsv *t, int col, int64_t *out) {
+    if (col < 0 || col >= (int)t->names.size()) return FSLR_INGEST_ERROR;
+    std::atomic<bool> ok{true};
+    parallel_for(fslr_tsv_rows(t), t->n_threads, [&](int64_t a, int64_t e, int) {
+        for (int64_t i = a; i < e && ok.load(std::memory_order_relaxed); ++i)
+            if (!canon_int(row_field(t, i, col), &out[i])) ok = false;
+    });
+    return ok ? FSLR_INGEST_OK : FSLR_INGEST_DECLINE;
+}
+
+int fslr_tsv_factorize(FslrTsv *t, int col, int32_t *codes, int64_t *n_uniq, int64_t *uniq_bytes) {
+    if (col < 0 || col >= (int)t->names.size()) return FSLR_INGEST_ERROR;
+    const int64_t rows = fslr_tsv_rows(t);
+    const int T = (int)std::min<int64_t>(t->n_threads, std::max<int64_t>(1, rows / 4096));
+    // pass 1: per-chunk first-appearance dictionaries (local ids in local order)
+    std::vector<std::unordered_map<std::string_view, int32_t>> loc((size_t)T);
+    std::vector<std::vector<std::string_view>> loc_order((size_t)T);
+    std::atomic<bool> ok{true}, all_int{true};
+    std::vector<std::thread> pool;
+    for (int c = 0; c < T; ++c)
+        pool.emplace_back([&, c] {
+            const int64_t a = rows * c / T, e = rows * (c + 1) / T;
+            auto &m = loc[c];
+            auto &ord = loc_order[c];
+            bool local_int = true;
+            std::string_view prev;
+            int32_t prev_id = -1;
+            for (int64_t i = a; i < e; ++i) {
+                std::string_view f = row_field(t, i, col);
+                if (is_na(f)) { ok = false; return; }
+                int64_t dummy;
+                if (local_int && !canon_int(f, &dummy)) local_int = false;
+                int32_t id;
+                if (i > a && f == prev) {
+                    id = prev_id;   // rows of one read are adjacent: skip the hash lookup
+                } else {
+                    auto it = m.find(f);
+                    if (it == m.end()) { id = (int32_t)ord.size(); m.emplace(f, id); ord.push_back(f); }
+                    else id = it->second;
+                }
+                prev = f;
+                prev_id = id;
+                codes[i] = id;   // local id for now
+            }
+            if (!local_int) all_int = false;
+        });
+    for (auto &th : pool) th.join();
+    pool.clear();
+    if (!ok) return FSLR_INGEST_DECLINE;
+    if (all_int && rows > 0) return FSLR_INGEST_DECLINE;   // pandas would type the column as int64
+    // merge in chunk order = global first-appearance order
+    std::unordered_map<std::string_view, int32_t> glob;
+    std::vector<std::string_view> &order = t->uniq[col];
+    order.clear();
+    std::vector<std::vector<int32_t>> remap((size_t)T);
+    for (int c = 0; c < T; ++c) {
+        remap[c].resize(loc_order[c].size());
+        for (size_t k = 0; k < loc_order[c].size(); ++k) {
+            auto it = glob.find(loc_order[c][k]);
+            if (it == glob.end()) {
+                int32_t id = (int32_t)order.size();
+                glob.emplace(loc_order[c][k], id);
+                order.push_back(loc_order[c][k]);
+                remap[c][k] = id;
+            } else {
+                remap[c][k] = it->second;
+            }
+        }
+    }
+    for (int c = 0; c < T; ++c)
+        pool.emplace_back([&, c] {
+            const int64_t a = rows * c / T, e = rows * (c + 1) / T;
+            const int32_t *r = remap[c].data();
+            for (int64_t i = a; i < e; ++i) codes[i] = r[codes[i]];
+        });
+    for (auto &th : pool) th.join();
+    int64_t bytes = 0;
+    for (auto &s : order) bytes += (int64_t)s.size();
+    *n_uniq = (int64_t)order.size();
+    *uniq_bytes = bytes;
+    return FSLR_INGEST_OK;
+}
+
+int fslr_tsv_uniques(const FslrTsv *t, int col, char *buf, int64_t *ends) {
+    if (col < 0 || col >= (int)t->names.size()) return FSLR_INGEST_ERROR;
+    int64_t off = 0, k = 0;
+    for (auto &s : t->uniq[col]) {
+        std::memcpy(buf + off, s.data(), s.size());
+        off += (int64_t)s.size();
+        ends[k++] = off;
+    }
+    return FSLR_INGEST_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,135 @@
+"""Native reader for ``{name}.mappings.bed`` (C ABI ``include/fslr_ingest.h``).
+
+Replaces ``pd.read_csv(f'{basename}.mappings.bed', sep='\\t')`` (reference ``fslr/main.py:209``)
+for the columns the clustering path reads (``cluster.py:14`` keep_fillings, ``cluster.py:109``
+prepare_data).  :func:`read_hot_columns` returns the frame
+``pd.read_csv(path, sep='\\t', usecols=HOT_COLUMNS)`` would give, or ``None`` when the file is one
+the fast path does not type exactly like pandas (quoted fields, NA spellings, non-canonical
+integers, an all-integer string column); the caller then reads it with pandas.  Host code only:
+this is the input side of the path, not the GPU product path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+import pandas as pd
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libfslr_ingest.so')
+OK, ERROR, DECLINE = 0, 1, 2
+
+INT_COLUMNS = ('rstart', 'rend', 'n_alignments', 'aln_size', 'qstart', 'qend')
+STR_COLUMNS = ('chrom', 'qname')
+HOT_COLUMNS = ('chrom', 'rstart', 'rend', 'qname', 'n_alignments', 'aln_size', 'qstart', 'qend')
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise FileNotFoundError(f'{path} is not built: run `make -C fslr_amd/csrc`')
+    L = ctypes.CDLL(path)
+    vp, i64, i32, cp = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_char_p
+    sig = {
+        'fslr_tsv_open': (i32, [cp, i32, ctypes.POINTER(vp), cp, ctypes.c_size_t]),
+        'fslr_tsv_close': (None, [vp]),
+        'fslr_tsv_rows': (i64, [vp]),
+        'fslr_tsv_cols': (i32, [vp]),
+        'fslr_tsv_colname': (cp, [vp, i32]),
+        'fslr_tsv_find': (i32, [vp, cp]),
+        'fslr_tsv_int_column': (i32, [vp, i32, vp]),
+        'fslr_tsv_factorize': (i32, [vp, i32, vp, ctypes.POINTER(i64), ctypes.POINTER(i64)]),
+        'fslr_tsv_uniques': (i32, [vp, i32, vp, vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype, f.argtypes = res, args
+    _lib = L
+    return L
+
+
+class TsvFile:
+    """An opened, line-split TSV file (library-owned buffer)."""
+
+    def __init__(self, path: str, n_threads: int = 0):
+        L = load()
+        err = ctypes.create_string_buffer(512)
+        h = ctypes.c_void_p()
+        rc = L.fslr_tsv_open(os.fsencode(path), int(n_threads), ctypes.byref(h), err, len(err))
+        self.declined = rc == DECLINE
+        if rc == ERROR:
+            raise OSError(err.value.decode())
+        self._h = h if rc == OK else None
+        self._L = L
+
+    def close(self):
+        if self._h is not None:
+            self._L.fslr_tsv_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def rows(self) -> int:
+        return int(self._L.fslr_tsv_rows(self._h))
+
+    @property
+    def columns(self) -> list:
+        return [self._L.fslr_tsv_colname(self._h, i).decode() for i in range(self._L.fslr_tsv_cols(self._h))]
+
+    def _col(self, name: str) -> int:
+        c = self._L.fslr_tsv_find(self._h, name.encode())
+        if c < 0:
+            raise KeyError(name)
+        return c
+
+    def int_column(self, name: str):
+        out = np.empty(self.rows, dtype=np.int64)
+        rc = self._L.fslr_tsv_int_column(self._h, self._col(name), out.ctypes.data)
+        return out if rc == OK else None
+
+    def factorize(self, name: str):
+        """(codes int32[rows], uniques object[k]) as ``pd.factorize(col, sort=False)``, or None."""
+        c = self._col(name)
+        codes = np.empty(self.rows, dtype=np.int32)
+        nu, nb = ctypes.c_int64(), ctypes.c_int64()
+        rc = self._L.fslr_tsv_factorize(self._h, c, codes.ctypes.data, ctypes.byref(nu), ctypes.byref(nb))
+        if rc != OK:
+            return None
+        buf = np.empty(max(nb.value, 1), dtype=np.uint8)
+        ends = np.empty(max(nu.value, 1), dtype=np.int64)
+        self._L.fslr_tsv_uniques(self._h, c, buf.ctypes.data, ends.ctypes.data)
+        raw = buf.tobytes()
+        starts = np.concatenate(([0], ends[:nu.value - 1])) if nu.value else ends[:0]
+        uniq = np.array([raw[s:e].decode() for s, e in zip(starts.tolist(), ends[:nu.value].tolist())],
+                        dtype=object)
+        return codes, uniq
+
+
+def read_hot_columns(path: str, n_threads: int = 0):
+    """``pd.read_csv(path, sep='\\t', usecols=HOT_COLUMNS)`` natively, or None (read with pandas)."""
+    with TsvFile(path, n_threads) as t:
+        if t.declined or not set(HOT_COLUMNS) <= set(t.columns):
+            return None
+        cols = {}
+        for name in HOT_COLUMNS:
+            if name in STR_COLUMNS:
+                f = t.factorize(name)
+                if f is None:
+                    return None
+                cols[name] = f[1][f[0]]
+            else:
+                v = t.int_column(name)
+                if v is None:
+                    return None
+                cols[name] = v
+        order = [c for c in t.columns if c in cols]   # usecols keeps file order
+        return pd.DataFrame({c: cols[c] for c in order})

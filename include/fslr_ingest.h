@@ -1,0 +1,56 @@
+/*
+ * fslr_ingest.h — host-side C ABI for reading `{name}.mappings.bed`.
+ *
+ * Replaces the reference's `pd.read_csv(f'{basename}.mappings.bed', sep='\t')`
+ * (fslr/main.py:209 in /root/reference) for the columns the clustering path reads
+ * (cluster.py:14 keep_fillings, cluster.py:109 prepare_data: chrom, rstart, rend, qname,
+ * n_alignments, aln_size, qstart, qend), and `pd.factorize(col, sort=False)` on
+ * the string columns.  It never guesses: a column is handed back as int64 only
+ * when every field is a canonical decimal integer (pandas infers int64 for it and
+ * writes it back unchanged); a string column is factorized only when no field is
+ * empty or one of pandas' default NA spellings and the column is not all-integer.
+ * Otherwise the call returns FSLR_INGEST_DECLINE and the caller reads the file
+ * with pandas.  Quoted fields (any '"') make fslr_tsv_open decline.
+ *
+ * Plain C types, caller-owned output arrays, library-owned parse state behind an
+ * opaque handle.  Lines are split over std::thread workers (memory-bound scan).
+ */
+#ifndef FSLR_INGEST_H
+#define FSLR_INGEST_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FSLR_INGEST_OK 0
+#define FSLR_INGEST_ERROR 1
+#define FSLR_INGEST_DECLINE 2   /* valid file, but pandas would not type it the way this fast path does */
+
+typedef struct FslrTsv FslrTsv;
+
+/* Read the whole file, split lines and the header. n_threads <= 0: hardware concurrency. */
+int fslr_tsv_open(const char *path, int n_threads, FslrTsv **out, char *err, size_t errlen);
+void fslr_tsv_close(FslrTsv *t);
+int64_t fslr_tsv_rows(const FslrTsv *t);
+int fslr_tsv_cols(const FslrTsv *t);
+/* Header name of column `col` (NUL-terminated, owned by the handle). */
+const char *fslr_tsv_colname(const FslrTsv *t, int col);
+/* Column index of `name`, or -1. */
+int fslr_tsv_find(const FslrTsv *t, const char *name);
+
+/* out[rows]: the column as int64 if every field is a canonical integer, else DECLINE. */
+int fslr_tsv_int_column(const FslrTsv *t, int col, int64_t *out);
+
+/* codes[rows] (int32, first-appearance order like pd.factorize(sort=False)).
+ * Returns the number of unique values in *n_uniq and their total byte length in
+ * *uniq_bytes; fetch them with fslr_tsv_uniques. */
+int fslr_tsv_factorize(FslrTsv *t, int col, int32_t *codes, int64_t *n_uniq, int64_t *uniq_bytes);
+/* After fslr_tsv_factorize on `col`: concatenated unique values (buf[uniq_bytes])
+ * and their end offsets (ends[n_uniq]). */
+int fslr_tsv_uniques(const FslrTsv *t, int col, char *buf, int64_t *ends);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
