@@ -265,32 +265,51 @@ int fslr_tsv_factorize(FslrTsv *t, int col, int32_t *codes, int64_t *n_uniq, int
     pool.clear();
     if (!ok) return FSLR_INGEST_DECLINE;
     if (all_int && rows > 0) return FSLR_INGEST_DECLINE;   // pandas would type the column as int64
-    // merge in chunk order = global first-appearance order
-    std::unordered_map<std::string_view, int32_t> glob;
-    std::vector<std::string_view> &order = t->uniq[col];
-    order.clear();
+    // Merge, sharded by hash: shard s owns the keys with hash % T == s and walks the chunks
+    // in order, so the first chunk holding a key is its global first appearance. Global ids
+    // are then dense in (chunk, local order) of first appearances = pd.factorize order.
+    auto run = [&](auto &&f) {
+        for (int c = 0; c < T; ++c) pool.emplace_back([&, c] { f(c); });
+        for (auto &th : pool) th.join();
+        pool.clear();
+    };
+    std::vector<std::vector<uint32_t>> hs((size_t)T);
+    std::vector<std::vector<int64_t>> first((size_t)T);   // -1: first appearance; else (chunk << 32 | k)
     std::vector<std::vector<int32_t>> remap((size_t)T);
-    for (int c = 0; c < T; ++c) {
-        remap[c].resize(loc_order[c].size());
-        for (size_t k = 0; k < loc_order[c].size(); ++k) {
-            auto it = glob.find(loc_order[c][k]);
-            if (it == glob.end()) {
-                int32_t id = (int32_t)order.size();
-                glob.emplace(loc_order[c][k], id);
-                order.push_back(loc_order[c][k]);
-                remap[c][k] = id;
-            } else {
-                remap[c][k] = it->second;
+    run([&](int c) {
+        const auto &ord = loc_order[c];
+        hs[c].resize(ord.size());
+        first[c].resize(ord.size());
+        remap[c].resize(ord.size());
+        for (size_t k = 0; k < ord.size(); ++k) hs[c][k] = (uint32_t)(std::hash<std::string_view>{}(ord[k]) % T);
+        loc[c] = {};   // local maps are no longer needed
+    });
+    run([&](int s) {
+        std::unordered_map<std::string_view, int64_t> m;
+        for (int c = 0; c < T; ++c)
+            for (size_t k = 0; k < loc_order[c].size(); ++k) {
+                if ((int)hs[c][k] != s) continue;
+                auto r = m.try_emplace(loc_order[c][k], ((int64_t)c << 32) | (int64_t)k);
+                first[c][k] = r.second ? -1 : r.first->second;
             }
-        }
-    }
+    });
+    std::vector<int64_t> base((size_t)T + 1, 0);
     for (int c = 0; c < T; ++c)
-        pool.emplace_back([&, c] {
-            const int64_t a = rows * c / T, e = rows * (c + 1) / T;
-            const int32_t *r = remap[c].data();
-            for (int64_t i = a; i < e; ++i) codes[i] = r[codes[i]];
-        });
-    for (auto &th : pool) th.join();
+        base[c + 1] = base[c] + std::count(first[c].begin(), first[c].end(), (int64_t)-1);
+    std::vector<std::string_view> &order = t->uniq[col];
+    order.assign((size_t)base[T], std::string_view());
+    run([&](int c) {
+        int64_t id = base[c];
+        for (size_t k = 0; k < first[c].size(); ++k)
+            if (first[c][k] < 0) { remap[c][k] = (int32_t)id; order[(size_t)id++] = loc_order[c][k]; }
+    });
+    run([&](int c) {
+        for (size_t k = 0; k < first[c].size(); ++k)
+            if (first[c][k] >= 0) remap[c][k] = remap[first[c][k] >> 32][first[c][k] & 0xffffffff];
+        const int64_t a = rows * c / T, e = rows * (c + 1) / T;
+        const int32_t *r = remap[c].data();
+        for (int64_t i = a; i < e; ++i) codes[i] = r[codes[i]];
+    });
     int64_t bytes = 0;
     for (auto &s : order) bytes += (int64_t)s.size();
     *n_uniq = (int64_t)order.size();

@@ -82,3 +82,27 @@ def test_library_exports_every_declared_symbol():
     import re
     names = set(re.findall(r'\b(fslr_tsv_\w+)\s*\(', hdr))
     assert names and all(hasattr(L, n) for n in names)
+
+
+@pytest.mark.parametrize('name', ['cfg1_1k_x3', 'mixed_1500_l16', 'ties_600', 'edge_cases', 'zipf_800_l64'])
+def test_clustering_input_from_native_columns_matches_pandas(tmp_path, name):
+    """keep_fillings → prepare_data (cluster.py:14,109) read only HOT_COLUMNS, so the device input
+    built from the native reader equals the one built from the full pandas frame."""
+    import dataclasses
+    import numpy as np
+    import fixtures as fx
+    from host_pipeline import host_prepare
+    p = tmp_path / 'x.mappings.bed'
+    p.write_text(fx.input_bed_text(name), newline='')
+    native = ingest.read_hot_columns(str(p), 4)
+    assert native is not None
+    a, _, _ = host_prepare(name)
+    b, _, _ = host_prepare(name, bed=native)
+    for f in dataclasses.fields(a):
+        if f.name == '_csr':
+            continue
+        x, y = getattr(a, f.name), getattr(b, f.name)
+        assert x.dtype == y.dtype and np.array_equal(x, y), f.name
+    ca, cb = a.csr(), b.csr()
+    for f in dataclasses.fields(ca):
+        assert np.array_equal(np.asarray(getattr(ca, f.name)), np.asarray(getattr(cb, f.name))), f.name
