@@ -329,3 +329,106 @@ int fslr_tsv_uniques(const FslrTsv *t, int col, char *buf, int64_t *ends) {
 }
 
 }  // extern "C"
+
+// ---- writer: rows copied verbatim + a per-row suffix (main.py:344,351 to_csv) ----
+namespace {
+// pandas would infer a bool column from these (true_values/false_values defaults, case-insensitive).
+bool boolish(std::string_view f) {
+    auto eq = [&](const char *w) {
+        size_t n = std::strlen(w);
+        if (f.size() != n) return false;
+        for (size_t i = 0; i < n; ++i)
+            if ((f[i] | 0x20) != w[i]) return false;
+        return true;
+    };
+    return eq("true") || eq("false");
+}
+// Any field pandas' C parser could turn into a number.
+bool numeric(std::string_view f) {
+    if (f.empty()) return false;
+    std::string s(f);
+    char *end = nullptr;
+    std::strtod(s.c_str(), &end);
+    return end == s.c_str() + s.size();
+}
+}  // namespace
+
+extern "C" {
+
+int fslr_tsv_verbatim(const FslrTsv *t) {
+    const int ncol = (int)t->names.size();
+    const int64_t rows = fslr_tsv_rows(t);
+    if (rows == 0) return FSLR_INGEST_DECLINE;
+    for (int c = 0; c < ncol; ++c) {
+        // 0: every field a canonical int; else the column must be text with no numeric-looking,
+        // bool-looking or non-empty NA field (empty fields come back as '' either way).
+        std::atomic<int> all_int{1}, text_ok{1}, any_text{0};
+        parallel_for(rows, t->n_threads, [&](int64_t a, int64_t e, int) {
+            bool ai = true, tk = true, at = false;
+            for (int64_t i = a; i < e; ++i) {
+                std::string_view f = row_field(t, i, c);
+                int64_t v;
+                if (ai && !canon_int(f, &v)) ai = false;
+                if (!f.data()) { tk = false; continue; }   // missing field
+                if (f.empty()) continue;
+                if (is_na(f) || boolish(f) || numeric(f)) tk = false;
+                else at = true;
+            }
+            if (!ai) all_int = 0;
+            if (!tk) text_ok = 0;
+            if (at) any_text = 1;
+        });
+        if (all_int) continue;
+        if (!(text_ok && any_text)) return FSLR_INGEST_DECLINE;
+    }
+    return FSLR_INGEST_OK;
+}
+
+int fslr_tsv_write(const FslrTsv *t, const char *path, const char *header_suffix, const int64_t *rows_out,
+                   int64_t n_out, const int32_t *suffix_id, const char *suffix_buf, const int64_t *suffix_ends,
+                   char *err, size_t errlen) {
+    FILE *fp = std::fopen(path, "wb");
+    if (!fp) { set_err(err, errlen, std::string("cannot write ") + path); return FSLR_INGEST_ERROR; }
+    std::string head;
+    for (size_t c = 0; c < t->names.size(); ++c) { if (c) head += '\t'; head += t->names[c]; }
+    head += header_suffix;
+    head += '\n';
+    std::fwrite(head.data(), 1, head.size(), fp);
+    const int64_t rows = fslr_tsv_rows(t);
+    const char *b = t->buf.data();
+    const int T = std::max(1, t->n_threads);
+    const int64_t block = 1 << 18;   // rows per formatting round (bounded memory)
+    std::vector<std::string> part((size_t)T);
+    bool bad = false;
+    for (int64_t r0 = 0; r0 < n_out && !bad; r0 += block) {
+        const int64_t r1 = std::min(n_out, r0 + block);
+        std::atomic<bool> oob{false};
+        parallel_for(r1 - r0, T, [&](int64_t a, int64_t e, int w) {
+            std::string &o = part[(size_t)w];
+            o.clear();
+            for (int64_t k = r0 + a; k < r0 + e; ++k) {
+                const int64_t i = rows_out[k];
+                if (i < 0 || i >= rows) { oob = true; return; }
+                const char *s = b + t->line[i];
+                const char *le = b + t->line[rows + 1 + i];
+                if (le > s && le[-1] == '\n') --le;
+                if (le > s && le[-1] == '\r') --le;
+                o.append(s, (size_t)(le - s));
+                const int32_t u = suffix_id[k];
+                const int64_t ss = u ? suffix_ends[u - 1] : 0;
+                o.append(suffix_buf + ss, (size_t)(suffix_ends[u] - ss));
+                o += '\n';
+            }
+        });
+        if (oob) { bad = true; break; }
+        const int used = (int)std::min<int64_t>(T, std::max<int64_t>(1, (r1 - r0) / 4096));
+        for (int w = 0; w < used; ++w) std::fwrite(part[(size_t)w].data(), 1, part[(size_t)w].size(), fp);
+    }
+    if (std::fclose(fp) != 0 || bad) {
+        set_err(err, errlen, bad ? "row index out of range" : "write failed");
+        return FSLR_INGEST_ERROR;
+    }
+    return FSLR_INGEST_OK;
+}
+
+}  // extern "C"

@@ -44,6 +44,8 @@ def load(path: str = LIB_PATH):
         'fslr_tsv_int_column': (i32, [vp, i32, vp]),
         'fslr_tsv_factorize': (i32, [vp, i32, vp, ctypes.POINTER(i64), ctypes.POINTER(i64)]),
         'fslr_tsv_uniques': (i32, [vp, i32, vp, vp]),
+        'fslr_tsv_verbatim': (i32, [vp]),
+        'fslr_tsv_write': (i32, [vp, cp, cp, vp, i64, vp, vp, vp, cp, ctypes.c_size_t]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -113,23 +115,54 @@ class TsvFile:
                         dtype=object)
         return codes, uniq
 
+    def verbatim(self) -> bool:
+        return self._L.fslr_tsv_verbatim(self._h) == OK
+
+    def write_rows(self, path: str, rows, suffix_frame: pd.DataFrame, suffix_key) -> None:
+        """Write input rows ``rows`` + the columns of ``suffix_frame`` like ``DataFrame.to_csv``.
+
+        ``suffix_frame`` is constant per ``suffix_key`` value (one value per output row); pandas
+        formats one row per distinct key, so the appended numbers are pandas' own text.
+        """
+        rows = np.ascontiguousarray(rows, dtype=np.int64)
+        codes, uniq = pd.factorize(suffix_key, sort=False)
+        first = np.full(len(uniq), -1, dtype=np.int64)
+        first[codes[::-1]] = np.arange(len(codes) - 1, -1, -1)
+        per_key = suffix_frame.iloc[first]
+        text = per_key.to_csv(sep='\t', header=False, index=False, lineterminator='\n')
+        lines = text.split('\n')[:len(uniq)]
+        enc = [('\t' + ln).encode() for ln in lines]
+        ends = np.cumsum([len(x) for x in enc], dtype=np.int64) if enc else np.zeros(1, np.int64)
+        buf = b''.join(enc) or b'\0'
+        head = ''.join('\t' + str(c) for c in suffix_frame.columns).encode()
+        sid = np.ascontiguousarray(codes, dtype=np.int32)
+        err = ctypes.create_string_buffer(512)
+        rc = self._L.fslr_tsv_write(self._h, os.fsencode(path), head, rows.ctypes.data, len(rows), sid.ctypes.data,
+                                    buf, ends.ctypes.data, err, len(err))
+        if rc != OK:
+            raise OSError(err.value.decode())
+
+
+def frame_from(t: 'TsvFile', int_columns=INT_COLUMNS, str_columns=STR_COLUMNS):
+    """The columns (file order) as pandas would type them, or None."""
+    if t.declined or not (set(int_columns) | set(str_columns)) <= set(t.columns):
+        return None
+    cols = {}
+    for name in set(int_columns) | set(str_columns):
+        if name in str_columns:
+            f = t.factorize(name)
+            if f is None:
+                return None
+            cols[name] = f[1][f[0]]
+        else:
+            v = t.int_column(name)
+            if v is None:
+                return None
+            cols[name] = v
+    return pd.DataFrame({c: cols[c] for c in t.columns if c in cols})
+
 
 def read_hot_columns(path: str, n_threads: int = 0):
     """``pd.read_csv(path, sep='\\t', usecols=HOT_COLUMNS)`` natively, or None (read with pandas)."""
     with TsvFile(path, n_threads) as t:
-        if t.declined or not set(HOT_COLUMNS) <= set(t.columns):
-            return None
-        cols = {}
-        for name in HOT_COLUMNS:
-            if name in STR_COLUMNS:
-                f = t.factorize(name)
-                if f is None:
-                    return None
-                cols[name] = f[1][f[0]]
-            else:
-                v = t.int_column(name)
-                if v is None:
-                    return None
-                cols[name] = v
-        order = [c for c in t.columns if c in cols]   # usecols keeps file order
-        return pd.DataFrame({c: cols[c] for c in order})
+        return frame_from(t)

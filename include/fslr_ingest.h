@@ -50,6 +50,18 @@ int fslr_tsv_factorize(FslrTsv *t, int col, int32_t *codes, int64_t *n_uniq, int
  * and their end offsets (ends[n_uniq]). */
 int fslr_tsv_uniques(const FslrTsv *t, int col, char *buf, int64_t *ends);
 
+/* Writer for the outputs (reference main.py:349 `.mappings.cluster.bed`, main.py:352
+ * `.mappings.representative.bed`, both `to_csv(sep='\t', index=False)`): the input's own bytes
+ * per kept row plus a suffix.  fslr_tsv_verbatim is OK only when pandas would write every input
+ * column back byte-identically (canonical int64 columns, or text columns with no numeric,
+ * bool or NA spelling besides empty); otherwise DECLINE and the caller writes with pandas. */
+int fslr_tsv_verbatim(const FslrTsv *t);
+/* Header = input header + header_suffix.  Row k of the output = input row rows_out[k] (LF line
+ * end) + suffix suffix_id[k], where suffix u is suffix_buf[suffix_ends[u-1] .. suffix_ends[u]). */
+int fslr_tsv_write(const FslrTsv *t, const char *path, const char *header_suffix, const int64_t *rows_out,
+                   int64_t n_out, const int32_t *suffix_id, const char *suffix_buf, const int64_t *suffix_ends,
+                   char *err, size_t errlen);
+
 #ifdef __cplusplus
 }
 #endif
