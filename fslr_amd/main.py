@@ -21,7 +21,7 @@ import click
 import numpy as np
 import pandas as pd
 
-from . import __version__, cluster
+from . import __version__, cluster, ingest
 
 # primer names of the reference's primers.csv (fslr/primers.csv:2-7); main.py:59-67 validates
 # --primers against them even under --skip-alignment
@@ -87,6 +87,9 @@ def assign_clusters(bed_file: pd.DataFrame, G: cluster.ClusterGraph):
 @click.option('--filter-false', required=False, is_flag=True, help='Use reads with both primers labeled')
 @click.option('--device', required=False, default=None, type=int, help='HIP device ordinal for the clustering kernels (default: $LOCAL_RANK or 0)')
 @click.option('--timings', required=False, is_flag=True, help='Print per-stage wall times to stderr')
+@click.option('--native-io/--pandas-io', default=True, show_default=True,
+              help='Read .mappings.bed and write the outputs with the native threaded reader/writer '
+                   '(fslr_ingest.h); inputs it cannot type exactly like pandas fall back to pandas')
 @click.version_option(__version__)
 def pipeline(**args):
     for cat in (pd.errors.SettingWithCopyWarning, FutureWarning):    # the reference ignores all warnings (main.py:13)
@@ -114,8 +117,37 @@ def run_clustering(args, basename):
     t = {}
     t0 = time.perf_counter()
     print('Making clusters')
-    bed_file = pd.read_csv(f'{basename}.mappings.bed', sep='\t')
+    tsv, bed_file = _native_open(f'{basename}.mappings.bed') if args.get('native_io', True) else (None, None)
+    if bed_file is None:
+        bed_file = pd.read_csv(f'{basename}.mappings.bed', sep='\t')
     t['read_csv'] = time.perf_counter() - t0
+    try:
+        return _cluster_and_write(args, basename, bed_file, tsv, t)
+    finally:
+        if tsv is not None:
+            tsv.close()
+
+
+def _native_open(path):
+    """(TsvFile, frame of the columns clustering and the writers read) or (None, None).
+
+    Only when every input column would round-trip through pandas unchanged, so that writing the
+    input's own row bytes equals ``to_csv`` of the pandas frame (reference main.py:349,352).
+    """
+    try:
+        tsv = ingest.TsvFile(path)
+    except (FileNotFoundError, OSError):
+        return None, None
+    bed = None
+    if not tsv.declined and tsv.verbatim():
+        bed = ingest.frame_from(tsv, int_columns=ingest.INT_COLUMNS + ('alignment_score',))
+    if bed is None:
+        tsv.close()
+        return None, None
+    return tsv, bed
+
+
+def _cluster_and_write(args, basename, bed_file, tsv, t):
     chromosome_mask = set()
     if args['cluster_mask']:
         allowed = set(bed_file['chrom'])
@@ -149,9 +181,19 @@ def run_clustering(args, basename):
     t3 = time.perf_counter()
     assign_clusters(bed_file, network)
     bed_file = cluster.chrom_to_str(bed_file, chrom_to_num_map)
-    bed_file.to_csv(f'{basename}.mappings.cluster.bed', index=False, sep='\t')
+    if tsv is not None:
+        added = [c for c in bed_file.columns if c not in set(tsv.columns)]
+        tsv.write_rows(f'{basename}.mappings.cluster.bed', bed_file.index.to_numpy(), bed_file[added],
+                       bed_file['qname'])
+    else:
+        bed_file.to_csv(f'{basename}.mappings.cluster.bed', index=False, sep='\t')
     bed_representative = cluster.choose_alignment(bed_file)
-    bed_representative.to_csv(f'{basename}.mappings.representative.bed', index=False, sep='\t')
+    if tsv is not None:
+        added = [c for c in bed_representative.columns if c not in set(tsv.columns)]
+        tsv.write_rows(f'{basename}.mappings.representative.bed', bed_representative.index.to_numpy(),
+                       bed_representative[added], bed_representative['qname'])
+    else:
+        bed_representative.to_csv(f'{basename}.mappings.representative.bed', index=False, sep='\t')
     t['write'] = time.perf_counter() - t3
     if args.get('timings'):
         st = network.stats

@@ -78,22 +78,23 @@ def compare_with_oracle(g, o, n):
 CLI_FIXTURES = [f for f in fx.FIXTURES if f != 'capbind_1500']
 
 
-def run_product_cli(name, tmp):
+def run_product_cli(name, tmp, io_flag='--native-io'):
     from click.testing import CliRunner
     from fslr_amd.main import pipeline
     with open(os.path.join(tmp, 'fx.mappings.bed'), 'w') as fh:
         fh.write(fx.input_bed_text(name))
     shutil.copy(fx.input_bam(name), os.path.join(tmp, 'fx.bwa_dodi.bam'))
     args = ['--name', 'fx', '--out', tmp, '--ref', 'unused.fa', '--primers', '21q1', '--skip-alignment'] + \
-        fx.meta(name)['args']
+        fx.meta(name)['args'] + [io_flag]
     return CliRunner().invoke(pipeline, args, catch_exceptions=True)
 
 
+@pytest.mark.parametrize('io_flag', ['--native-io', '--pandas-io'])
 @pytest.mark.parametrize('name', CLI_FIXTURES)
-def test_cli_matches_reference_outputs(name):
+def test_cli_matches_reference_outputs(name, io_flag):
     meta = fx.meta(name)
     with tempfile.TemporaryDirectory() as tmp:
-        res = run_product_cli(name, tmp)
+        res = run_product_cli(name, tmp, io_flag)
         if meta['exception']:
             assert isinstance(res.exception, ZeroDivisionError), res.output
             return
