@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <string_view>
@@ -105,7 +106,12 @@ int fslr_tsv_open(const char *path, int n_threads, FslrTsv **out, char *err, siz
     size_t got = sz > 0 ? std::fread(&t->buf[0], 1, (size_t)sz, fp) : 0;
     std::fclose(fp);
     if ((long)got != sz) { delete t; set_err(err, errlen, "short read"); return FSLR_INGEST_ERROR; }
-    t->n_threads = n_threads > 0 ? n_threads : (int)std::max(1u, std::thread::hardware_concurrency());
+    if (n_threads <= 0) {   // the CPU share, not the whole machine: OMP_NUM_THREADS, else min(cores, 16)
+        const char *env = std::getenv("OMP_NUM_THREADS");
+        n_threads = env ? std::atoi(env) : 0;
+        if (n_threads <= 0) n_threads = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    }
+    t->n_threads = std::min(n_threads, 256);
     const char *b = t->buf.data();
     const int64_t n = (int64_t)t->buf.size();
     if (std::memchr(b, '"', (size_t)n)) { delete t; set_err(err, errlen, "quoted fields"); return FSLR_INGEST_DECLINE; }

@@ -29,7 +29,8 @@ extern "C" {
 
 typedef struct FslrTsv FslrTsv;
 
-/* Read the whole file, split lines and the header. n_threads <= 0: hardware concurrency. */
+/* Read the whole file, split lines and the header. n_threads <= 0: $OMP_NUM_THREADS, else
+ * min(hardware concurrency, 16). */
 int fslr_tsv_open(const char *path, int n_threads, FslrTsv **out, char *err, size_t errlen);
 void fslr_tsv_close(FslrTsv *t);
 int64_t fslr_tsv_rows(const FslrTsv *t);
