@@ -180,7 +180,8 @@ def _cluster_and_write(args, basename, bed_file, tsv, t):
         return False
     t3 = time.perf_counter()
     assign_clusters(bed_file, network)
-    bed_file = cluster.chrom_to_str(bed_file, chrom_to_num_map)
+    if tsv is None:                              # the native writer copies the input's own chrom text
+        bed_file = cluster.chrom_to_str(bed_file, chrom_to_num_map)
     if tsv is not None:
         added = [c for c in bed_file.columns if c not in set(tsv.columns)]
         tsv.write_rows(f'{basename}.mappings.cluster.bed', bed_file.index.to_numpy(), bed_file[added],
