@@ -13,6 +13,7 @@ import numpy as np
 
 LIB_PATH = os.environ.get('FSLR_LIB') or os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libfslr_hip.so')
 
+ABI_VERSION = 2          # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
 FSLR_OK, FSLR_ERR_ZERO_DIVISION, FSLR_ERR_INVALID, FSLR_ERR_HIP, FSLR_ERR_NOMEM, FSLR_ERR_STATE = range(6)
 FSLR_MAX_L = 64
 FSLR_MAX_READS = 1 << 25
@@ -26,7 +27,7 @@ EXPORTED = ['fslr_abi_version', 'fslr_last_error', 'fslr_ctx_create', 'fslr_ctx_
             'fslr_components', 'fslr_run', 'fslr_sync', 'fslr_read_stats', 'fslr_get_timings', 'fslr_read_counters',
             'fslr_get_labels',
             'fslr_get_fwd_degree', 'fslr_get_edges', 'fslr_labels_device_ptr', 'fslr_copy_labels_device',
-            'fslr_copy_fwd_device', 'fslr_union_pairs', 'fslr_finalize_labels']
+            'fslr_copy_fwd_device', 'fslr_union_pairs', 'fslr_finalize_labels', 'fslr_apply_edge_cap']
 
 
 class HipUnavailable(RuntimeError):
@@ -59,6 +60,14 @@ class QueryStats(ctypes.Structure):
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+class CapStats(ctypes.Structure):
+    _fields_ = [('applied', ctypes.c_int32), ('max_fwd', ctypes.c_int32)] + [
+        (f, ctypes.c_int64) for f in ('candidates', 'capped', 'hits', 'pairs', 'dropped', 'backward')]
+
+    def as_dict(self):
+        return {f: int(getattr(self, f)) for f, _ in self._fields_}
 
 
 class Timings(ctypes.Structure):
@@ -110,11 +119,14 @@ def load(path: str = LIB_PATH):
         'fslr_copy_fwd_device': (ctypes.c_int, [vp, vp]),
         'fslr_union_pairs': (ctypes.c_int, [vp, vp, vp, i64, ctypes.c_int]),
         'fslr_finalize_labels': (ctypes.c_int, [vp]),
+        'fslr_apply_edge_cap': (ctypes.c_int, [vp, i32, ctypes.POINTER(CapStats)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
+    if L.fslr_abi_version() != ABI_VERSION:
+        raise HipUnavailable(f'{path} has ABI {L.fslr_abi_version()}, this binding needs {ABI_VERSION}: rebuild it')
     _lib = L
     return L
 
@@ -210,6 +222,12 @@ class Context:
         """Query shard `shard` of `n_shards` (rank blocks of 64 dealt round robin; fslr_query_shard)."""
         p = self._params(qlen_cut, nal_cut, pass_table, edge_threshold)
         self._check(self._L.fslr_query_shard(self._h, ctypes.byref(p), int(shard), int(n_shards)))
+
+    def apply_edge_cap(self, edge_threshold=10) -> dict:
+        """Replay the reference's per-read edge cap (cluster.py:223-224) on the last full query."""
+        cs = CapStats()
+        self._check(self._L.fslr_apply_edge_cap(self._h, int(edge_threshold), ctypes.byref(cs)))
+        return cs.as_dict()
 
     def components(self):
         self._check(self._L.fslr_components(self._h))

@@ -41,8 +41,9 @@ __all__ = ['IntervalItem', 'keep_fillings', 'rename_chromosomes', 'chrom_to_str'
 
 
 class EdgeCapWarning(UserWarning):
-    """A read has more than ``edge_threshold`` forward partners: the reference's
-    result then depends on superintervals' result order (cluster.py:223-224)."""
+    """The reference's result depends on an order this build cannot pin: n_alignments
+    that differ between rows of one read (cluster.py:209 reads the row its search
+    reaches first)."""
 
 
 def _default_device() -> int:
@@ -255,18 +256,20 @@ class ClusterGraph:
 def query_interval_trees(interval_trees, data, overlap_cutoff, jaccard_threshold, edge_threshold, qlen_diff, diff):
     """cluster.py:187-227 on the GPU.
 
-    Returns ``(match_df, G)``.  ``match_df`` rows are the graph's edges
-    (query1 = lower-rank read, jaccard = I/U as a Python float) sorted by
-    (query1 rank, query2 rank); the reference's row order is set order
-    (arbitrary).  Every pair is evaluated without the per-read edge cap: the
-    result equals the reference whenever no read has more than
-    ``edge_threshold`` forward partners; otherwise an
-    ``EdgeCapWarning`` is issued.
+    Returns ``(match_df, G)``.  The pair kernels evaluate every candidate pair
+    (E*); when a read has more than ``edge_threshold`` forward partners, the
+    reference's per-read cap (cluster.py:223-224) is replayed exactly
+    (``fslr_apply_edge_cap``; search order of the superintervals stand-in,
+    SURVEY.md §8c).  ``match_df`` rows are the graph's edges as the reference
+    records them — (read whose loop formed the edge, partner, I/U as a Python
+    float) — sorted by (query1 rank, query2 rank); the reference's row order is
+    set order (arbitrary).
     """
     min(jaccard_threshold)                              # cluster.py:188 raises on an empty list
     if not isinstance(interval_trees, DeviceIntervalIndex) or interval_trees.data is not data:
         interval_trees = DeviceIntervalIndex(data)
     idx = interval_trees
+    data = idx.data
     csr = idx.csr
     ctx = idx.ctx
     qnames_by_rank = data.qnames[csr.read_qcode]
@@ -279,15 +282,14 @@ def query_interval_trees(interval_trees, data, overlap_cutoff, jaccard_threshold
     ncut = 1 - diff
     ctx.reserve_edges(max(1 << 16, 12 * csr.n_reads))
     st = ctx.run_query(qcut, ncut, pt, int(edge_threshold))
+    st['cap'] = ctx.apply_edge_cap(int(edge_threshold))
+    st['n_edges'] = ctx.stats()['n_edges']
+    st['max_fwd'] = st['cap']['max_fwd']
     ctx.components()
     labels = ctx.labels()
     ne = st['n_edges']
     a, b, I, U = ctx.edges(ne)
     fwd = ctx.fwd_degree()
-    if st['max_fwd'] > edge_threshold:
-        warnings.warn(f'a read has {st["max_fwd"]} forward partners > edge_threshold={edge_threshold}: the '
-                      'reference result depends on superintervals result order here (parity unpinned); '
-                      'all edges are kept', EdgeCapWarning)
     order = np.lexsort((b, a))
     a, b, I, U = a[order], b[order], I[order], U[order]
     match_df = pd.DataFrame({'query1': qnames_by_rank[a] if ne else np.zeros(0, object),

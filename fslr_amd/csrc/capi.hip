@@ -7,95 +7,12 @@
 #include <vector>
 
 #include "fslr_hip.h"
+#include "ctx.hpp"
 #include "kernels.hpp"
 
 using namespace fslr;
 
-struct fslr_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  bool own_stream = false;
-  std::string err;
-  int64_t n = 0, ni = 0;
-  int n_chroms = 0;
-  int thr_mode = 0;
-  bool reads_set = false, index_built = false, have_data_pos = false;
-  int shard = 0, n_shards = 1;             // fslr_set_shard: A-side index data for this shard only
-  int built_shard = 0, built_n_shards = 1;
-  // device buffers
-  int4* rmeta = nullptr;
-  int4* iv = nullptr;
-  int* qpos = nullptr;       // [NI] CSR interval -> its position in the sorted index
-  int2* rng_s = nullptr;     // [NI] sorted position -> {n_fwd, bwd_begin}
-  int4* idx4 = nullptr;
-  int2* idx_gate = nullptr;
-  unsigned long long* defer = nullptr;
-  int64_t defer_cap = 0;
-  int* data_pos = nullptr;
-  unsigned* dchrom = nullptr;    // data order (start-sorted `data` list): chromosome
-  int4* drec = nullptr;          // data order: {start, end, thr, read << 6 | j}
-  int2* dgate = nullptr;         // data order: the owning read's gate word {qlen2, nal | L << 24 | haz << 31}
-  int* chist = nullptr;          // index build scratch: per-chromosome counts per 1024-position sub-tile
-  int* s_start = nullptr;
-  int2* crange = nullptr;
-  unsigned long long* keys = nullptr;
-  unsigned long long* keys2 = nullptr;
-  int* vals = nullptr;
-  int* vals2 = nullptr;
-  unsigned long long* endkey = nullptr;
-  unsigned long long* pmaxkey = nullptr;   // per 256-position tile: max (chrom, end) key, then its scan
-  void* temp = nullptr;
-  size_t temp_bytes = 0;
-  int* umax = nullptr;     // [FSLR_MAX_L] derived from the pass table
-  int4* lbounds = nullptr; // [N] per query read: exact integer ranges of the length gate
-  int2* edges = nullptr;
-  unsigned short* edge_iu = nullptr;
-  int64_t edge_cap = 0;
-  int* fwd = nullptr;
-  int* heavy = nullptr;      // [N] reads handed to the partitioned pair-kernel launch
-  int* parent = nullptr;
-  unsigned long long* counters = nullptr;
-  unsigned long long* wstat = nullptr;       // [wstat_waves x kWStride] per-wave statistics of the pair kernel
-  int wstat_waves = 0;
-  unsigned long long* diag = nullptr;        // FSLR_SECTION_PROF builds: per-read timing of the pair kernel
-  int* errw = nullptr;     // [0..2] error, [3] max_fwd
-  int* thr_tmp = nullptr;
-  int64_t cap_n = 0, cap_ni = 0, cap_chroms = 0;
-  std::vector<int> umax_host, umax_dev_copy;   // dev copy: what c->umax holds
-  std::vector<unsigned char> aln_zero_host;   // per CSR interval: FSLR_THR_ZERO_ALN at set_reads
-  int ablate = 0;
-  // profiling
-  bool profiling = false;
-  hipEvent_t ev[8] = {};
-  bool ev_ok = false;
-  bool t_index_rec = false, t_query_rec = false, t_comp_rec = false;
-};
-
 namespace {
-
-int fail(fslr_ctx* c, int code, const std::string& msg) {
-  if (c) c->err = msg;
-  return code;
-}
-
-#define HIP_TRY(ctx, expr)                                                                       \
-  do {                                                                                           \
-    hipError_t e_ = (expr);                                                                      \
-    if (e_ != hipSuccess)                                                                        \
-      return fail((ctx), FSLR_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));       \
-  } while (0)
-
-template <typename T>
-int dalloc(fslr_ctx* c, T** p, size_t count) {
-  if (*p) {
-    (void)hipFree(*p);
-    *p = nullptr;
-  }
-  if (count == 0) count = 1;
-  hipError_t e = hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T));
-  if (e != hipSuccess) return fail(c, FSLR_ERR_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
-  return FSLR_OK;
-}
 
 int ensure_capacity(fslr_ctx* c, int64_t n, int64_t ni, int n_chroms) {
   int rc;
@@ -135,7 +52,7 @@ int ensure_capacity(fslr_ctx* c, int64_t n, int64_t ni, int n_chroms) {
   if (!c->umax) {
     if ((rc = dalloc(c, &c->umax, FSLR_MAX_L))) return rc;
     if ((rc = dalloc(c, &c->counters, kNumCounters))) return rc;
-    if ((rc = dalloc(c, &c->errw, 4))) return rc;
+    if ((rc = dalloc(c, &c->errw, kErrWords))) return rc;
   }
   return FSLR_OK;
 }
@@ -447,7 +364,7 @@ static int query_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_
     if (rc) return rc;
     c->wstat_waves = w;
   }
-  HIP_TRY(c, hipMemsetAsync(c->errw, 0, 4 * sizeof(int), c->stream));
+  HIP_TRY(c, hipMemsetAsync(c->errw, 0, kErrWords * sizeof(int), c->stream));
   if (c->n) HIP_TRY(c, hipMemsetAsync(c->fwd, 0, c->n * sizeof(int), c->stream));
   QueryArgs g;
   g.rmeta = c->rmeta;
@@ -477,6 +394,10 @@ static int query_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_
   g.diag = c->diag;
   g.wstat = c->wstat;
   g.wstat_waves = c->wstat_waves;
+  c->last_full = a_begin == 0 && a_end == c->n && n_shards == 1;
+  c->last_qcut = p->qlen_cut;
+  c->last_ncut = p->nal_cut;
+  std::memset(&c->cap_stats, 0, sizeof(c->cap_stats));
   if (c->profiling) HIP_TRY(c, hipEventRecord(c->ev[2], c->stream));
   HIP_TRY(c, launch_query(g, c->thr_mode, c->stream));
   if (c->profiling) HIP_TRY(c, hipEventRecord(c->ev[3], c->stream));
@@ -491,7 +412,7 @@ int fslr_components(fslr_ctx* c) {
   if (c->profiling) HIP_TRY(c, hipEventRecord(c->ev[4], c->stream));
   const int n = static_cast<int>(c->n);
   HIP_TRY(c, launch_uf_init(c->parent, n, c->stream));
-  if (c->edge_cap) HIP_TRY(c, launch_uf_edges(c->parent, c->edges, c->counters, c->edge_cap, c->stream));
+  if (c->edge_cap) HIP_TRY(c, launch_uf_edges(c->parent, c->edges, c->counters, c->edge_cap, c->errw, c->stream));
   HIP_TRY(c, launch_uf_finalize(c->parent, n, c->stream));
   if (c->profiling) HIP_TRY(c, hipEventRecord(c->ev[5], c->stream));
   c->t_comp_rec = c->profiling;
@@ -537,7 +458,7 @@ int fslr_read_stats(fslr_ctx* c, fslr_query_stats* out) {
   if (!c || !out) return FSLR_ERR_INVALID;
   HIP_TRY(c, hipSetDevice(c->device));
   unsigned long long cnt[kNumCounters] = {};
-  int ew[4] = {};
+  int ew[kErrWords] = {};
   if (c->counters) {
     HIP_TRY(c, hipMemcpyAsync(cnt, c->counters, sizeof(cnt), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipMemcpyAsync(ew, c->errw, sizeof(ew), hipMemcpyDeviceToHost, c->stream));
@@ -565,6 +486,7 @@ int fslr_read_stats(fslr_ctx* c, fslr_query_stats* out) {
     return FSLR_ERR_ZERO_DIVISION;
   }
   if (out->deferred > c->defer_cap) return fail(c, FSLR_ERR_STATE, "deferred list overflowed; reserve and rerun");
+  if (out->n_edges > c->edge_cap) return fail(c, FSLR_ERR_STATE, "edge buffer overflowed; reserve and rerun");
   return FSLR_OK;
 }
 
@@ -584,8 +506,13 @@ int fslr_get_timings(fslr_ctx* c, fslr_timings* out) {
 int fslr_get_labels(fslr_ctx* c, int32_t* labels) {
   if (!c || (!labels && c->n)) return FSLR_ERR_INVALID;
   HIP_TRY(c, hipSetDevice(c->device));
+  int ovf = 0;
+  if (c->errw) HIP_TRY(c, hipMemcpyAsync(&ovf, c->errw + kErrOverflow, sizeof(int), hipMemcpyDeviceToHost, c->stream));
   if (c->n) HIP_TRY(c, hipMemcpyAsync(labels, c->parent, c->n * sizeof(int), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (ovf)
+    return fail(c, FSLR_ERR_STATE, "the query behind these labels overflowed its edge or deferred buffer: "
+                                   "reserve and rerun it");
   return FSLR_OK;
 }
 

@@ -50,8 +50,10 @@ __global__ void k_uf_init(int* p, int n) {
 }
 
 __global__ void k_uf_edges(int* p, const int2* __restrict__ edges, const unsigned long long* __restrict__ count,
-                           long long cap) {
-  const long long ne = min(static_cast<long long>(*count), cap);
+                           long long cap, int* err) {
+  const long long cnt = static_cast<long long>(*count);
+  if (cnt > cap && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(err + kErrOverflow, 2);
+  const long long ne = min(cnt, cap);
   for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < ne;
        k += static_cast<long long>(gridDim.x) * blockDim.x) {
     const int2 e = edges[k];
@@ -68,9 +70,20 @@ __global__ void k_uf_pairs(int* p, const int* __restrict__ src, const int* __res
   }
 }
 
+// find without path halving: the finalize pass's only store is each node's own root.  (With
+// halving here, another thread's late halving store into p[x] — an ancestor that is not the root —
+// could land after x's own root store and leave x labelled with a non-root.)
+__device__ int uf_root(int* p, int x) {
+  while (true) {
+    const int px = ld_rlx(p + x);
+    if (px == x) return x;
+    x = px;
+  }
+}
+
 __global__ void k_uf_finalize(int* p, int n) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-    st_rlx(p + i, uf_find(p, i));
+    st_rlx(p + i, uf_root(p, i));
 }
 
 }  // namespace
@@ -80,9 +93,9 @@ hipError_t launch_uf_init(int* parent, int n, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_uf_edges(int* parent, const int2* edges, const unsigned long long* count, long long cap,
+hipError_t launch_uf_edges(int* parent, const int2* edges, const unsigned long long* count, long long cap, int* err,
                            hipStream_t s) {
-  if (cap > 0) k_uf_edges<<<grid_for(cap), 256, 0, s>>>(parent, edges, count, cap);
+  if (cap > 0) k_uf_edges<<<grid_for(cap), 256, 0, s>>>(parent, edges, count, cap, err);
   return hipGetLastError();
 }
 

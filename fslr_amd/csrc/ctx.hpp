@@ -1,0 +1,102 @@
+// ctx.hpp — the context behind the C ABI's opaque fslr_ctx (internal to libfslr_hip.so):
+// HBM buffers, stream, the last query's parameters, error text.  Shared by capi.hip and cap.hip.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "fslr_hip.h"
+#include "kernels.hpp"
+
+struct fslr_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  std::string err;
+  int64_t n = 0, ni = 0;
+  int n_chroms = 0;
+  int thr_mode = 0;
+  bool reads_set = false, index_built = false, have_data_pos = false;
+  int shard = 0, n_shards = 1;             // fslr_set_shard: A-side index data for this shard only
+  int built_shard = 0, built_n_shards = 1;
+  // device buffers
+  int4* rmeta = nullptr;
+  int4* iv = nullptr;
+  int* qpos = nullptr;       // [NI] CSR interval -> its position in the sorted index
+  int2* rng_s = nullptr;     // [NI] sorted position -> {n_fwd, bwd_begin}
+  int4* idx4 = nullptr;
+  int2* idx_gate = nullptr;
+  unsigned long long* defer = nullptr;
+  int64_t defer_cap = 0;
+  int* data_pos = nullptr;
+  unsigned* dchrom = nullptr;    // data order (start-sorted `data` list): chromosome
+  int4* drec = nullptr;          // data order: {start, end, thr, read << 6 | j}
+  int2* dgate = nullptr;         // data order: the owning read's gate word {qlen2, nal | L << 24 | haz << 31}
+  int* chist = nullptr;          // index build scratch: per-chromosome counts per 1024-position sub-tile
+  int* s_start = nullptr;
+  int2* crange = nullptr;
+  unsigned long long* keys = nullptr;
+  unsigned long long* keys2 = nullptr;
+  int* vals = nullptr;
+  int* vals2 = nullptr;
+  unsigned long long* endkey = nullptr;
+  unsigned long long* pmaxkey = nullptr;   // per 256-position tile: max (chrom, end) key, then its scan
+  void* temp = nullptr;
+  size_t temp_bytes = 0;
+  int* umax = nullptr;     // [FSLR_MAX_L] derived from the pass table
+  int4* lbounds = nullptr; // [N] per query read: exact integer ranges of the length gate
+  int2* edges = nullptr;
+  unsigned short* edge_iu = nullptr;
+  int64_t edge_cap = 0;
+  int* fwd = nullptr;
+  int* heavy = nullptr;      // [N] reads handed to the partitioned pair-kernel launch
+  int* parent = nullptr;
+  unsigned long long* counters = nullptr;
+  unsigned long long* wstat = nullptr;       // [wstat_waves x kWStride] per-wave statistics of the pair kernel
+  int wstat_waves = 0;
+  unsigned long long* diag = nullptr;        // FSLR_SECTION_PROF builds: per-read timing of the pair kernel
+  int* errw = nullptr;     // [0..2] error, [3] max_fwd
+  int* thr_tmp = nullptr;
+  int64_t cap_n = 0, cap_ni = 0, cap_chroms = 0;
+  std::vector<int> umax_host, umax_dev_copy;   // dev copy: what c->umax holds
+  std::vector<unsigned char> aln_zero_host;   // per CSR interval: FSLR_THR_ZERO_ALN at set_reads
+  int ablate = 0;
+  // the last query (fslr_query / fslr_query_shard): what fslr_apply_edge_cap replays
+  bool last_full = false;                // covered every read [0, n) with one shard
+  double last_qcut = 0.0, last_ncut = 0.0;
+  fslr_cap_stats cap_stats = {};
+  // profiling
+  bool profiling = false;
+  hipEvent_t ev[8] = {};
+  bool ev_ok = false;
+  bool t_index_rec = false, t_query_rec = false, t_comp_rec = false;
+};
+
+namespace fslr {
+
+
+inline int fail(fslr_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+#define HIP_TRY(ctx, expr)                                                                       \
+  do {                                                                                           \
+    hipError_t e_ = (expr);                                                                      \
+    if (e_ != hipSuccess)                                                                        \
+      return fail((ctx), FSLR_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));       \
+  } while (0)
+
+template <typename T>
+int dalloc(fslr_ctx* c, T** p, size_t count) {
+  if (*p) {
+    (void)hipFree(*p);
+    *p = nullptr;
+  }
+  if (count == 0) count = 1;
+  hipError_t e = hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T));
+  if (e != hipSuccess) return fail(c, FSLR_ERR_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+  return FSLR_OK;
+}
+
+}  // namespace fslr

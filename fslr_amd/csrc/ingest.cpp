@@ -365,6 +365,34 @@ int fslr_tsv_verbatim(const FslrTsv *t) {
     const int ncol = (int)t->names.size();
     const int64_t rows = fslr_tsv_rows(t);
     if (rows == 0) return FSLR_INGEST_DECLINE;
+    // pandas renames empty header names ('Unnamed: N') and repeated ones ('x.1'): the input's own
+    // header line would then not be what to_csv writes
+    {
+        std::vector<std::string> nm(t->names.begin(), t->names.end());
+        for (const std::string &x : nm)
+            if (x.empty()) return FSLR_INGEST_DECLINE;
+        std::sort(nm.begin(), nm.end());
+        if (std::adjacent_find(nm.begin(), nm.end()) != nm.end()) return FSLR_INGEST_DECLINE;
+    }
+    // every row exactly ncol fields: a longer row makes pandas raise (or index by the first
+    // column), a shorter one NaN-fills — either way the row bytes are not what to_csv writes
+    {
+        std::atomic<int> ragged{0};
+        const char *b = t->buf.data();
+        parallel_for(rows, t->n_threads, [&](int64_t a, int64_t e, int) {
+            for (int64_t i = a; i < e && !ragged.load(std::memory_order_relaxed); ++i) {
+                const char *s = b + t->line[i];
+                const char *le = b + t->line[rows + 1 + i];
+                if (le > s && le[-1] == '\n') --le;
+                if (le > s && le[-1] == '\r') --le;
+                int tabs = 0;
+                for (const char *q = s; (q = static_cast<const char *>(std::memchr(q, '\t', (size_t)(le - q)))) != nullptr; ++q)
+                    ++tabs;
+                if (tabs != ncol - 1) ragged = 1;
+            }
+        });
+        if (ragged) return FSLR_INGEST_DECLINE;
+    }
     for (int c = 0; c < ncol; ++c) {
         // 0: every field a canonical int; else the column must be text with no numeric-looking,
         // bool-looking or non-empty NA field (empty fields come back as '' either way).

@@ -21,7 +21,11 @@ namespace fslr {
 constexpr int kWave = 64;
 constexpr int kPassStride = 128;      // 2 * FSLR_MAX_L
 constexpr int kMaxCoord = 1 << 30;
-constexpr int kShardShift = 6;        // query shards own blocks of 64 consecutive ranks, round robin
+constexpr int kShardShift = 6;
+// error words (QueryArgs::err): [0] code, [1] a, [2] b, [3] max forward degree, [4] overflow flags
+// (1: deferred list, 2: edge buffer) — a query that lost pairs; its labels are refused
+constexpr int kErrWords = 8;
+constexpr int kErrOverflow = 4;        // query shards own blocks of 64 consecutive ranks, round robin
 
 __host__ __device__ inline bool shard_owns(int read, int shard, int n_shards) {
   return n_shards == 1 || ((read >> kShardShift) % n_shards) == shard;
@@ -45,6 +49,28 @@ enum Counter { kEdgeCount = 0,          // atomic (own 128-B line)
 // wave count, cycle sums of reads 0, 1 and >= 2 of the wave
 enum WaveStat { kWsEval = 0, kWsJacc, kWsCand, kWsAlgoBytes, kWsOverflow, kWsMatchEntries, kWsMatchedPairs,
                 kWsMaxFwd, kWsBase = 8, kWsProf = kWsBase + 16, kWStride = 32 };
+
+// ---- pair predicates shared by the pair kernels (query.hip) and the cap replay (cap.hip) ----
+// interval accepts overlap o (fslr_hip.h: thr >= 0 ? o >= thr : o <= ~thr)
+__device__ __forceinline__ bool thr_ok(int o, int t) { return t >= 0 ? o >= t : o <= ~t; }
+
+// calculate_overlap(i1, i2) >= overlap (cluster.py:133-136), same chromosome already checked
+__device__ __forceinline__ bool iv_match_general(int sa, int ea, int ta, int sb, int eb, int tb) {
+  const int o = max(min(ea, eb) - max(sa, sb), 0);
+  return thr_ok(o, ta) && thr_ok(o, tb);
+}
+
+// different_lengths_or_alignments (cluster.py:178-183) → true = pair passes (not different);
+// *zd = the reference would raise ZeroDivisionError (max == 0).
+__device__ __forceinline__ bool lengths_pass(int q1, int q2, int n1, int n2, double qcut, double ncut, bool* zd) {
+  int mn = min(q1, q2), mx = max(q1, q2);
+  if (mx == 0) { *zd = true; return false; }
+  if (static_cast<double>(mn) / static_cast<double>(mx) >= qcut) return true;
+  mn = min(n1, n2);
+  mx = max(n1, n2);
+  if (mx == 0) { *zd = true; return false; }
+  return static_cast<double>(mn) / static_cast<double>(mx) >= ncut;
+}
 
 // ---- index build (index.hip) -------------------------------------------------------------
 struct IndexBufs {
@@ -113,9 +139,22 @@ hipError_t launch_query(const QueryArgs& a, int thr_mode, hipStream_t s);
 // waves of the largest query_kernel grid (the size of QueryArgs::wstat)
 int query_max_waves();
 
+// ---- edge-cap replay (cap.hip) --------------------------------------------------------------
+// per listed read: upper bound of its interval hits (sum over its intervals of the scan range)
+hipError_t launch_cap_hit_counts(const int* reads, int n, const int4* rmeta, const int* qpos, const int2* rng_s,
+                                 long long* counts, hipStream_t s);
+// per listed read, into hits[off[t] ..]: {partner, interval i, start, end} of every end-inclusive
+// overlap of its intervals (CSR order), each interval's hits in ascending index position; nout[t] = count
+hipError_t launch_cap_hit_emit(const int* reads, int n, const long long* off, const int4* rmeta, const int* qpos,
+                               const int2* rng_s, const int4* idx4, int4* hits, int* nout, hipStream_t s);
+// per pair (a, b): zd | lenok << 1 | edge << 2 | I << 8 | U << 20 (the reference's predicates in full)
+hipError_t launch_eval_pairs(const int2* pairs, long long n, const int4* rmeta, const int4* iv, double qcut,
+                             double ncut, const int* umax, int* flags, hipStream_t s);
+
 // ---- components (components.hip) ---------------------------------------------------------
 hipError_t launch_uf_init(int* parent, int n, hipStream_t s);
-hipError_t launch_uf_edges(int* parent, const int2* edges, const unsigned long long* count, long long cap,
+// count > cap (edges were lost) sets err[kErrOverflow]
+hipError_t launch_uf_edges(int* parent, const int2* edges, const unsigned long long* count, long long cap, int* err,
                            hipStream_t s);
 // src == nullptr: src[k] = k mod period
 hipError_t launch_uf_pairs(int* parent, const int* src, const int* dst, long long n, int period, hipStream_t s);

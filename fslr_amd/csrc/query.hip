@@ -118,27 +118,6 @@ __device__ __forceinline__ int part_of(int B, int npass) {
   return static_cast<int>(((static_cast<unsigned>(B) * 0x85EBCA6Bu) >> 8) % static_cast<unsigned>(npass));
 }
 
-// interval accepts overlap o (fslr_hip.h: thr >= 0 ? o >= thr : o <= ~thr)
-__device__ __forceinline__ bool thr_ok(int o, int t) { return t >= 0 ? o >= t : o <= ~t; }
-
-// calculate_overlap(i1, i2) >= overlap (cluster.py:133-136), same chromosome already checked
-__device__ __forceinline__ bool iv_match_general(int sa, int ea, int ta, int sb, int eb, int tb) {
-  const int o = max(min(ea, eb) - max(sa, sb), 0);
-  return thr_ok(o, ta) && thr_ok(o, tb);
-}
-
-// different_lengths_or_alignments (cluster.py:178-183) → true = pair passes (not different);
-// *zd = the reference would raise ZeroDivisionError (max == 0).
-__device__ __forceinline__ bool lengths_pass(int q1, int q2, int n1, int n2, double qcut, double ncut, bool* zd) {
-  int mn = min(q1, q2), mx = max(q1, q2);
-  if (mx == 0) { *zd = true; return false; }
-  if (static_cast<double>(mn) / static_cast<double>(mx) >= qcut) return true;
-  mn = min(n1, n2);
-  mx = max(n1, n2);
-  if (mx == 0) { *zd = true; return false; }
-  return static_cast<double>(mn) / static_cast<double>(mx) >= ncut;
-}
-
 // The gate of one query read as integer ranges (exact: IEEE division is monotone, so the
 // reference's double test fl(min/max) >= cut, cluster.py:178-183, holds on a contiguous range of
 // the partner's value).  {lo, hi}: partner values x in [lo, hi] pass; lo < 0 marks v == 0, where
@@ -810,7 +789,9 @@ __global__ __launch_bounds__(256) void deferred_kernel(QueryArgs g) {
   __shared__ unsigned long long es_all[4][kStageCap];
   const int lane = lane_id();
   EdgeStage es{es_all[threadIdx.x >> 6], 0};
-  const long long n = min(static_cast<long long>(g.counters[kDeferCount]), g.defer_cap);
+  const long long n_all = static_cast<long long>(g.counters[kDeferCount]);
+  if (n_all > g.defer_cap && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(g.err + kErrOverflow, 1);
+  const long long n = min(n_all, g.defer_cap);
   const int umax_v = g.umax[lane];
   unsigned long long w_eval = 0, w_jacc = 0, w_gather = 0, w_bytes = 0;
   const long long nw = static_cast<long long>(gridDim.x) * (blockDim.x >> 6);

@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define FSLR_ABI_VERSION 1
+#define FSLR_ABI_VERSION 2
 #define FSLR_MAX_L 64                /* max intervals per read (bitmask width) */
 #define FSLR_MAX_READS (1 << 25)     /* read rank packs into bits 6..30 of the index record */
 #define FSLR_THR_ZERO_ALN INT32_MIN
@@ -119,6 +119,18 @@ typedef struct {
     float total_ms;                /* first to last event of the last fslr_run/individual calls */
 } fslr_timings;
 
+/* The reference's per-query-read edge cap (cluster.py:223-224), see fslr_apply_edge_cap. */
+typedef struct {
+    int32_t applied;               /* 1: the cap bound (max forward degree > edge_threshold) and was replayed */
+    int32_t max_fwd;               /* max over reads of the edges formed in the read's own loop */
+    int64_t candidates;            /* reads whose loop could reach the cap (replayed) */
+    int64_t capped;                /* reads whose loop reached it (left hits unvisited) */
+    int64_t hits;                  /* index hits of the replayed loops */
+    int64_t pairs;                 /* distinct pairs of those hits, evaluated on the device */
+    int64_t dropped;               /* E* edges that no loop reached (absent from the reference graph) */
+    int64_t backward;              /* edges formed in the higher-rank read's loop */
+} fslr_cap_stats;
+
 int  fslr_abi_version(void);
 const char *fslr_last_error(const fslr_ctx *ctx);
 
@@ -152,20 +164,32 @@ int  fslr_query(fslr_ctx *ctx, const fslr_params *params, int64_t a_begin, int64
  * (balanced: low ranks have more higher-rank partners).  The shards of 0..n_shards-1 together
  * evaluate exactly the pairs of fslr_query(ctx, params, 0, n_reads).  Async. */
 int  fslr_query_shard(fslr_ctx *ctx, const fslr_params *params, int32_t shard, int32_t n_shards);
+/* cluster.py:197-224 — the edge cap.  The query computes E* (every candidate pair); when a read
+ * has more than edge_threshold forward edges, the reference's graph depends on the order its loops
+ * visit pairs.  This replays those loops exactly (search order of the superintervals stand-in the
+ * golden fixtures were made with: descending (start, -end, data position)) for the reads that can
+ * reach the cap, drops the E* edges no loop reaches, re-orients edges as (read whose loop formed
+ * it, partner) and sets forward degrees to the edges formed per loop.  No-op (no sync beyond one
+ * counter read) when the cap does not bind.  Needs the last query to be fslr_query over all reads.
+ * Call between fslr_query and fslr_components.  Syncs; out may be NULL. */
+int  fslr_apply_edge_cap(fslr_ctx *ctx, int32_t edge_threshold, fslr_cap_stats *out);
 /* cluster.py:230-234 — union-find over the edges: label = min rank in component.  Async. */
 int  fslr_components(fslr_ctx *ctx);
 /* build_index + query(all reads) + components, enqueued back to back.  Async. */
 int  fslr_run(fslr_ctx *ctx, const fslr_params *params);
 
 int  fslr_sync(fslr_ctx *ctx);
-int  fslr_read_stats(fslr_ctx *ctx, fslr_query_stats *out);     /* syncs; returns stats.error */
+/* syncs; returns stats.error, or FSLR_ERR_STATE when the edge or deferred buffer overflowed
+ * (reserve and rerun the query: components and labels of an overflowed query are refused) */
+int  fslr_read_stats(fslr_ctx *ctx, fslr_query_stats *out);
 int  fslr_get_timings(fslr_ctx *ctx, fslr_timings *out);        /* syncs */
 /* Raw device counters of the last query (diagnostics; layout is internal, kernels.hpp:
  * Counter).  Copies min(n, 32) words, syncs, returns the count or -error. */
 int  fslr_read_counters(fslr_ctx *ctx, uint64_t *out, int n);
 
 /* D2H copies (sync). */
-int  fslr_get_labels(fslr_ctx *ctx, int32_t *labels);          /* [n_reads] min-rank root */
+int  fslr_get_labels(fslr_ctx *ctx, int32_t *labels);          /* [n_reads] min-rank root; FSLR_ERR_STATE
+                                                                   after an overflowed query */
 int  fslr_get_fwd_degree(fslr_ctx *ctx, int32_t *fwd);         /* [n_reads] */
 int  fslr_get_edges(fslr_ctx *ctx, int32_t *a, int32_t *b, uint16_t *iu, int64_t capacity);
                                                                 /* iu = I | (U << 8); returns count via stats */

@@ -39,7 +39,8 @@ def oracle_from_csr(c):
 
 
 def gpu_run(ctx, csr, overlap=0.8, cutoffs=(1, 1, 0.66, 0.66, 0.66, 0.5), qlen_diff=0.04, nal_diff=0.25,
-            full_sort=False):
+            full_sort=False, cap=None):
+    """E* (every candidate pair) or, with ``cap`` = edge_threshold, the reference's capped graph."""
     thr = fold_overlap_threshold(csr.iv_aln, overlap)
     if full_sort:
         ctx.set_reads(csr.read_off, csr.read_qlen2, csr.read_nal, csr.iv_chrom, csr.iv_start, csr.iv_end, thr,
@@ -49,9 +50,30 @@ def gpu_run(ctx, csr, overlap=0.8, cutoffs=(1, 1, 0.66, 0.66, 0.66, 0.5), qlen_d
     ctx.reserve_edges(max(1 << 16, 12 * csr.n_reads))
     ctx.build_index()
     st = ctx.run_query(1 - qlen_diff, 1 - nal_diff, pass_table(cutoffs))
+    if cap is not None:
+        st['cap'] = ctx.apply_edge_cap(cap)
+        st['n_edges'] = ctx.stats()['n_edges']
+        st['max_fwd'] = st['cap']['max_fwd']
     ctx.components()
     a, b, I, U = ctx.edges(st['n_edges'])
     return dict(stats=st, labels=ctx.labels(), fwd=ctx.fwd_degree(), a=a, b=b, I=I, U=U)
+
+
+def compare_capped_with_oracle(g, o, n):
+    """Capped graph: the same edges oriented as (read whose loop formed it, partner), the same
+    edges-per-loop counts and the same components (cluster ids) as the oracle's reference loop."""
+    ge = sorted(zip(g['a'].tolist(), g['b'].tolist(), g['I'].tolist(), g['U'].tolist()))
+    oe = sorted(zip(o['edge_a'].tolist(), o['edge_b'].tolist(), o['edge_I'].tolist(), o['edge_U'].tolist()))
+    assert len(ge) == len(oe)
+    assert ge == oe
+    np.testing.assert_array_equal(g['fwd'], o['fwd'])
+    assert g['stats']['max_fwd'] == o['stats']['max_fwd']
+    lab = g['labels']
+    sizes = np.bincount(lab, minlength=n)
+    roots = np.flatnonzero(sizes >= 2)
+    rid = np.full(n, -1)
+    rid[roots] = np.arange(roots.size)
+    np.testing.assert_array_equal(np.where(sizes[lab] >= 2, rid[lab], -1), o['comp'])
 
 
 def compare_with_oracle(g, o, n):
@@ -75,7 +97,7 @@ def compare_with_oracle(g, o, n):
 
 
 # ------------------------------------------------------------------ end-to-end CLI vs golden
-CLI_FIXTURES = [f for f in fx.FIXTURES if f != 'capbind_1500']
+CLI_FIXTURES = list(fx.FIXTURES)
 
 
 def run_product_cli(name, tmp, io_flag='--native-io'):
@@ -122,14 +144,10 @@ def test_query_interval_trees_edges_match_reference(name):
                                                    kw['n_alignment_diff'])
     got = sorted([a, b, j] for a, b, j in match_df.itertuples(index=False))
     want = fx.stage(name)['edges']
-    if fx.meta(name)['stage']['max_fwd'] <= 10:
-        assert got == want
-        assert [sorted(c) for c in cluster.get_subgraphs(G)] == fx.stage(name)['components']
-    else:
-        # cap binds: the device graph is E*, a superset of the reference's capped graph (whose
-        # late edges come from the higher-rank read's loop, so compare unordered pairs)
-        norm = lambda rows: {(frozenset((a, b)), j) for a, b, j in rows}
-        assert norm(want) <= norm(got)
+    # the reference's match set, rows (query read, partner, j) — also where the cap binds
+    # (capbind_1500: max forward degree 15 > 10), edges formed in the partner's loop included
+    assert got == want
+    assert [sorted(c) for c in cluster.get_subgraphs(G)] == fx.stage(name)['components']
 
 
 def test_capbind_device_equals_uncapped_oracle(ctx):
@@ -139,6 +157,94 @@ def test_capbind_device_equals_uncapped_oracle(ctx):
     o = O.run_core(oracle_from_csr(csr), use_cap=False)
     compare_with_oracle(g, o, csr.n_reads)
     assert g['stats']['max_fwd'] > 10
+
+
+def test_capbind_device_capped_equals_reference_loop(ctx):
+    data, _, _ = host_prepare('capbind_1500')
+    csr = data.csr()
+    g = gpu_run(ctx, csr, cap=10)
+    o = O.run_core(oracle_from_csr(csr), use_cap=True)
+    assert g['stats']['cap']['applied'] == 1 and g['stats']['cap']['capped'] > 0
+    compare_capped_with_oracle(g, o, csr.n_reads)
+
+
+def _squeezed(n, lmax, seed, squeeze, dist='uniform', cluster_cap=10, size_p=1 / 3):
+    import dataclasses
+    s = synth.generate(n, lmax, seed, dist=dist, cluster_cap=cluster_cap, size_p=size_p)
+    csr = s.interval_data().csr()
+    st = csr.iv_start.astype(np.int64) // squeeze          # monotone: the data order stays start-sorted
+    en = st + (csr.iv_end.astype(np.int64) - csr.iv_start)
+    return dataclasses.replace(csr, iv_start=st.astype(np.int32), iv_end=en.astype(np.int32))
+
+
+@pytest.mark.parametrize('n,lmax,seed,squeeze,dist,ccap,thr', [
+    (30_000, 16, 41, 400, 'uniform', 60, 10),
+    (20_000, 64, 13, 300, 'zipf', 40, 10),
+    (20_000, 16, 47, 100, 'uniform', 30, 3),
+    (8_000, 8, 53, 2000, 'uniform', 10, 1),
+    (8_000, 8, 59, 50, 'uniform', 200, 40),
+])
+def test_dense_capped_vs_oracle(ctx, n, lmax, seed, squeeze, dist, ccap, thr):
+    """Events of up to `ccap` reads (forward degrees far above the cap) on a squeezed genome: the
+    cap binds for many reads, with chains of pairs left unseen by capped loops; the replayed graph
+    equals the oracle's reference loop exactly."""
+    csr = _squeezed(n, lmax, seed, squeeze, dist, cluster_cap=ccap, size_p=0.05)
+    g = gpu_run(ctx, csr, cap=thr)
+    o = O.run_core(oracle_from_csr(csr), edge_threshold=thr, use_cap=True)
+    assert g['stats']['cap']['applied'] == 1 and g['stats']['cap']['capped'] > 0
+    assert g['stats']['cap']['dropped'] > 0 or thr == 40
+    compare_capped_with_oracle(g, o, csr.n_reads)
+
+
+@pytest.mark.parametrize('thr', [1, 10])
+def test_one_locus_capped_vs_oracle(ctx, thr):
+    """1500 reads on one locus with runs of equal starts (the search order's tie rule decides
+    which pairs a capped loop reaches)."""
+    n = 1500
+    off = np.arange(n + 1, dtype=np.int64)
+    chrom = np.zeros(n, np.int32)
+    start = np.sort(np.full(n, 5000, np.int32) + (np.arange(n) % 7).astype(np.int32))
+    end = start + 1000 - (np.arange(n) % 3).astype(np.int32)
+    aln = np.full(n, 1000, np.int64)
+    q = np.full(n, 100, np.int32)
+    m = np.full(n, 3, np.int32)
+    thr_iv = fold_overlap_threshold(aln, 0.8)
+    ctx.set_reads(off, q, m, chrom, start, end, thr_iv, 1, iv_data_pos=np.arange(n))
+    ctx.reserve_edges(n * n)
+    ctx.build_index()
+    st = ctx.run_query(1 - 0.04, 1 - 0.25, pass_table([1.0]))
+    st['cap'] = ctx.apply_edge_cap(thr)
+    st['n_edges'] = ctx.stats()['n_edges']
+    st['max_fwd'] = st['cap']['max_fwd']
+    ctx.components()
+    a, b, I, U = ctx.edges(st['n_edges'])
+    g = dict(stats=st, labels=ctx.labels(), fwd=ctx.fwd_degree(), a=a, b=b, I=I, U=U)
+    o = O.run_core(O.OracleCSR(off, chrom, start, end, aln, q, m, np.arange(n)), 0.8, (1.0,), 0.04, 0.25,
+                   edge_threshold=thr, use_cap=True)
+    compare_capped_with_oracle(g, o, n)
+
+
+def test_cap_not_binding_is_identity(ctx):
+    s = synth.generate(30_000, 16, 2)
+    csr = s.interval_data().csr()
+    g1 = gpu_run(ctx, csr)
+    g2 = gpu_run(ctx, csr, cap=10)
+    assert g2['stats']['cap']['applied'] == 0
+    assert sorted(zip(g1['a'], g1['b'], g1['I'])) == sorted(zip(g2['a'], g2['b'], g2['I']))
+    np.testing.assert_array_equal(g1['labels'], g2['labels'])
+
+
+def test_union_find_labels_stable_over_repeats(ctx):
+    """Labels of the device union-find equal a host union-find over the same edges on every one of
+    30 repeats (the finalize pass once raced with path halving, ~1 run in 40 on capbind_1500)."""
+    from fslr_amd.dist import union_find_labels
+    data, _, _ = host_prepare('capbind_1500')
+    csr = data.csr()
+    g = gpu_run(ctx, csr, cap=10)
+    want = union_find_labels(csr.n_reads, g['a'], g['b'])
+    for _ in range(30):
+        ctx.components()
+        np.testing.assert_array_equal(ctx.labels(), want)
 
 
 def test_zero_division_raises(ctx):

@@ -76,6 +76,34 @@ def test_inputs_pandas_types_differently_are_declined(tmp_path, mutate):
     assert ingest.read_hot_columns(str(p), 2) is None
 
 
+@pytest.mark.parametrize('text', [
+    HEADER + _rows(30).replace('\tAC\n', '\tAC\textra\n', 1),                       # a row wider than the header
+    HEADER + _rows(30).replace('\t+\tAC\n', '\t+\n', 2),                             # rows narrower than it
+    HEADER.replace('strand', 'seq') + _rows(30),                                    # repeated name -> 'seq.1'
+    HEADER.replace('strand', '') + _rows(30),                                       # empty name -> 'Unnamed: 8'
+], ids=['wide_row', 'short_rows', 'dup_name', 'empty_name'])
+def test_verbatim_declines_rows_pandas_would_rewrite(tmp_path, text):
+    """The writer copies input row bytes only when to_csv would write them unchanged: ragged rows
+    and header names pandas renames send the CLI to the pandas path."""
+    p = tmp_path / 'x.bed'
+    p.write_text(text, newline='')
+    t = ingest.TsvFile(str(p))
+    try:
+        assert t.declined or not t.verbatim()
+    finally:
+        t.close()
+
+
+def test_verbatim_accepts_a_clean_file(tmp_path):
+    p = tmp_path / 'x.bed'
+    p.write_text(HEADER + _rows(30), newline='')
+    t = ingest.TsvFile(str(p))
+    try:
+        assert not t.declined and t.verbatim()
+    finally:
+        t.close()
+
+
 def test_library_exports_every_declared_symbol():
     L = ingest.load()
     hdr = open(os.path.join(os.path.dirname(__file__), '..', 'include', 'fslr_ingest.h')).read()
