@@ -27,7 +27,11 @@
 // Edges are re-oriented as (the read whose loop formed it, the partner), like the reference's
 // match set (:220); forward degrees become the edges formed in each read's own loop.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "ctx.hpp"
@@ -168,9 +172,22 @@ struct DevBuf {
 
 constexpr int kFlagZd = 1, kFlagLenOk = 2, kFlagEdge = 4;
 
-inline unsigned long long pair_key(int a, int b) {
-  const unsigned lo = static_cast<unsigned>(std::min(a, b)), hi = static_cast<unsigned>(std::max(a, b));
-  return (static_cast<unsigned long long>(lo) << 32) | hi;
+// f(begin, end) over [0, n) split across the host's cores
+template <typename F>
+void parallel_for(int n, F&& f) {
+  const int hw = static_cast<int>(std::max(1u, std::thread::hardware_concurrency()));
+  const int nth = std::max(1, std::min({hw, 16, n / 256}));
+  if (nth == 1) {
+    f(0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int k = 0; k < nth; ++k) {
+    const int b = static_cast<int>(static_cast<long long>(n) * k / nth);
+    const int e = static_cast<int>(static_cast<long long>(n) * (k + 1) / nth);
+    th.emplace_back([&f, b, e] { f(b, e); });
+  }
+  for (auto& x : th) x.join();
 }
 
 }  // namespace
@@ -200,6 +217,15 @@ extern "C" int fslr_apply_edge_cap(fslr_ctx* c, int32_t thr, fslr_cap_stats* out
     return fail(c, FSLR_ERR_STATE, "the edge cap binds: its replay needs the last query to cover every read on "
                                    "one context (fslr_query over [0, n_reads))");
   const int64_t n = c->n;
+  // FSLR_CAP_TIMING=1: host wall time per stage on stderr (diagnostics)
+  const bool timing = std::getenv("FSLR_CAP_TIMING") != nullptr;
+  auto t_last = std::chrono::steady_clock::now();
+  auto stage = [&](const char* what) {
+    if (!timing) return;
+    const auto now = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "[cap] %-28s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(now - t_last).count());
+    t_last = now;
+  };
   std::vector<int> fwd(static_cast<size_t>(n));
   std::vector<int2> edges(static_cast<size_t>(ne));
   std::vector<unsigned short> iu(static_cast<size_t>(ne));
@@ -222,6 +248,7 @@ extern "C" int fslr_apply_edge_cap(fslr_ctx* c, int32_t thr, fslr_cap_stats* out
     std::vector<int64_t> fill(aoff.begin(), aoff.end() - 1);
     for (const int2& e : edges) adj[fill[e.x]++] = e.y;
   }
+  stage("D2H fwd + edges, adjacency");
   // 1. candidate readers T (closure bound, rank order)
   std::vector<int> back(static_cast<size_t>(n), 0);
   std::vector<char> in_t(static_cast<size_t>(n), 0);
@@ -235,6 +262,7 @@ extern "C" int fslr_apply_edge_cap(fslr_ctx* c, int32_t thr, fslr_cap_stats* out
   cs.candidates = static_cast<int64_t>(T.size());
   const int nt = static_cast<int>(T.size());
 
+  stage("closure T");
   // 2. hit lists of the candidates from the device index
   DevBuf d_reads, d_cnt, d_hits, d_nout;
   HIP_TRY(c, hipMalloc(&d_reads.p, std::max(1, nt) * sizeof(int)));
@@ -259,48 +287,79 @@ extern "C" int fslr_apply_edge_cap(fslr_ctx* c, int32_t thr, fslr_cap_stats* out
   HIP_TRY(c, hipMemcpyAsync(nout.data(), d_nout.p, nt * sizeof(int), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
 
+  stage("hit lists (device) + D2H");
   // search order of each interval: the stand-in sorts by (start asc, end desc, data position asc)
   // and returns hits from the highest sorted position down.  Device positions of equal start are
-  // in data order, so a stable sort of each interval's hits on (start asc, end desc) gives the
-  // sorted order; it is then read backwards.  seq: per read, partners in visit order, -1 between
-  // intervals; own intervals dropped (cluster.py:203-204).
-  std::vector<int64_t> soff(static_cast<size_t>(nt) + 1, 0);
-  std::vector<int> seq;
-  seq.reserve(static_cast<size_t>(cap_hits));
-  std::vector<unsigned long long> keys;
+  // in data order, so reading an interval's hits backwards is that order except inside runs of
+  // equal start, which are stably re-sorted on (start asc, end desc) first.  seq: per read,
+  // partners in visit order, -1 after each interval; own intervals dropped (cluster.py:203-204).
+  // uq: per read, its distinct partners (sorted) — the pairs evaluated in step 3, flags aligned.
+  std::vector<int64_t> soff(static_cast<size_t>(nt) + 1, 0), uoff(static_cast<size_t>(nt) + 1, 0);
   for (int t = 0; t < nt; ++t) {
-    const int x = T[t];
-    int4* h = hits.data() + hoff[t];
-    const int cnt = nout[t];
-    cs.hits += cnt;
-    int g0 = 0;
-    while (g0 < cnt) {
-      int g1 = g0 + 1;
-      while (g1 < cnt && h[g1].y == h[g0].y) ++g1;
-      std::stable_sort(h + g0, h + g1, [](const int4& u, const int4& v) {
-        return u.z != v.z ? u.z < v.z : u.w > v.w;
-      });
-      for (int k = g1 - 1; k >= g0; --k)
-        if (h[k].x != x) {
-          seq.push_back(h[k].x);
-          keys.push_back(pair_key(x, h[k].x));
-        }
-      seq.push_back(-1);
-      g0 = g1;
-    }
-    soff[t + 1] = static_cast<int64_t>(seq.size());
+    soff[t + 1] = soff[t] + nout[t] + 64;            // hits + one separator per interval (<= 64)
+    uoff[t + 1] = uoff[t] + nout[t];
   }
+  std::vector<int> seq(static_cast<size_t>(soff[nt]), -2);   // -2: unused tail of a read's slot
+  std::vector<int> uq(static_cast<size_t>(uoff[nt]));
+  std::vector<int> nuq(static_cast<size_t>(nt), 0);
+  parallel_for(nt, [&](int t0, int t1) {
+    std::vector<int> tmp;
+    for (int t = t0; t < t1; ++t) {
+      const int x = T[t];
+      int4* h = hits.data() + hoff[t];
+      const int cnt = nout[t];
+      int64_t w = soff[t];
+      tmp.clear();
+      int g0 = 0;
+      while (g0 < cnt) {
+        int g1 = g0 + 1;
+        bool ties = false;
+        while (g1 < cnt && h[g1].y == h[g0].y) {
+          ties |= h[g1].z == h[g1 - 1].z;
+          ++g1;
+        }
+        if (ties)
+          std::stable_sort(h + g0, h + g1, [](const int4& u, const int4& v) {
+            return u.z != v.z ? u.z < v.z : u.w > v.w;
+          });
+        for (int k = g1 - 1; k >= g0; --k)
+          if (h[k].x != x) {
+            seq[w++] = h[k].x;
+            tmp.push_back(h[k].x);
+          }
+        seq[w++] = -1;
+        g0 = g1;
+      }
+      std::sort(tmp.begin(), tmp.end());
+      tmp.erase(std::unique(tmp.begin(), tmp.end()), tmp.end());
+      std::copy(tmp.begin(), tmp.end(), uq.begin() + uoff[t]);
+      nuq[t] = static_cast<int>(tmp.size());
+    }
+  });
+  for (int t = 0; t < nt; ++t) cs.hits += nout[t];
   std::vector<int4>().swap(hits);
-  std::sort(keys.begin(), keys.end());
-  keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
-  cs.pairs = static_cast<int64_t>(keys.size());
+  // compact the distinct partner lists (pairs of step 3, one per (read of T, partner))
+  {
+    int64_t w = 0;
+    for (int t = 0; t < nt; ++t) {
+      std::copy(uq.begin() + uoff[t], uq.begin() + uoff[t] + nuq[t], uq.begin() + w);
+      uoff[t] = w;
+      w += nuq[t];
+    }
+    uoff[nt] = w;
+    uq.resize(static_cast<size_t>(w));
+  }
+  cs.pairs = static_cast<int64_t>(uq.size());
 
-  // 3. the full predicate of every distinct pair
-  std::vector<int> flags(keys.size());
-  if (!keys.empty()) {
-    std::vector<int2> pv(keys.size());
-    for (size_t k = 0; k < keys.size(); ++k)
-      pv[k] = make_int2(static_cast<int>(keys[k] >> 32), static_cast<int>(keys[k] & 0xffffffffu));
+  stage("visit order + partner lists");
+  // 3. the full predicate of every (read of T, partner) pair
+  std::vector<int> flags(uq.size());
+  if (!uq.empty()) {
+    std::vector<int2> pv(uq.size());
+    parallel_for(nt, [&](int t0, int t1) {
+      for (int t = t0; t < t1; ++t)
+        for (int64_t k = uoff[t]; k < uoff[t + 1]; ++k) pv[k] = make_int2(std::min(T[t], uq[k]), std::max(T[t], uq[k]));
+    });
     DevBuf d_pairs, d_flags;
     HIP_TRY(c, hipMalloc(&d_pairs.p, pv.size() * sizeof(int2)));
     HIP_TRY(c, hipMalloc(&d_flags.p, pv.size() * sizeof(int)));
@@ -310,16 +369,18 @@ extern "C" int fslr_apply_edge_cap(fslr_ctx* c, int32_t thr, fslr_cap_stats* out
     HIP_TRY(c, hipMemcpyAsync(flags.data(), d_flags.p, flags.size() * sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
   }
-  auto flag_of = [&](int a, int b) {
-    const unsigned long long k = pair_key(a, b);
-    return flags[std::lower_bound(keys.begin(), keys.end(), k) - keys.begin()];
+  std::vector<int> t_of(static_cast<size_t>(n), -1);
+  for (int t = 0; t < nt; ++t) t_of[T[t]] = t;
+  auto flag_of = [&](int x, int y) {   // x in T
+    const int t = t_of[x];
+    return flags[std::lower_bound(uq.begin() + uoff[t], uq.begin() + uoff[t + 1], y) - uq.begin()];
   };
 
+  stage("pair predicates (device)");
   // 4. the loops of T in rank order
   std::vector<char> broke(static_cast<size_t>(n), 0);
   std::vector<int64_t> roff(static_cast<size_t>(nt) + 1, 0);   // reached partners of read T[t] (sorted)
   std::vector<int> reached;
-  std::vector<int> t_of(static_cast<size_t>(n), -1);
   std::vector<int> stamp(static_cast<size_t>(n), -1);
   std::vector<int> own_edges(static_cast<size_t>(nt), 0);
   auto reached_by = [&](int y, int x) {   // did broken read y's loop reach x?
@@ -328,12 +389,12 @@ extern "C" int fslr_apply_edge_cap(fslr_ctx* c, int32_t thr, fslr_cap_stats* out
   };
   for (int t = 0; t < nt; ++t) {
     const int x = T[t];
-    t_of[x] = t;
     int edges_x = 0;
     bool br = false;
     const size_t r0 = reached.size();
     for (int64_t k = soff[t]; k < soff[t + 1]; ++k) {
       const int y = seq[k];
+      if (y == -2) break;                                      // end of this read's hits
       if (y < 0) continue;                                     // next interval
       if (stamp[y] == x) continue;                             // seen in this loop
       if (y < x && (!broke[y] || reached_by(y, x))) continue;  // seen in y's loop
@@ -359,6 +420,7 @@ extern "C" int fslr_apply_edge_cap(fslr_ctx* c, int32_t thr, fslr_cap_stats* out
     roff[t + 1] = static_cast<int64_t>(reached.size());
   }
 
+  stage("replay loops");
   // E* pair (a, b) is an edge iff a's loop or, failing that, b's loop reaches it
   std::vector<int2> kept;
   std::vector<unsigned short> kept_iu;
@@ -388,6 +450,7 @@ extern "C" int fslr_apply_edge_cap(fslr_ctx* c, int32_t thr, fslr_cap_stats* out
   cs.applied = 1;
   cs.max_fwd = max_fwd;
 
+  stage("classify edges");
   // write the capped graph back: edges (former, partner), forward degree = edges formed per loop
   const unsigned long long nk = kept.size();
   if (nk) {
@@ -399,6 +462,7 @@ extern "C" int fslr_apply_edge_cap(fslr_ctx* c, int32_t thr, fslr_cap_stats* out
   HIP_TRY(c, hipMemcpyAsync(c->fwd, formed.data(), n * sizeof(int), hipMemcpyHostToDevice, c->stream));
   HIP_TRY(c, hipMemcpyAsync(c->errw + 3, &max_fwd, sizeof(int), hipMemcpyHostToDevice, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  stage("H2D capped graph");
   c->cap_stats = cs;
   if (out) *out = cs;
   return FSLR_OK;
