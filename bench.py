@@ -1,17 +1,32 @@
 #!/usr/bin/env python3
-"""Headline benchmark: evaluated Jaccard read-pair compares / s on the 1M-read interval cluster.
+"""Headline benchmark: Jaccard-evaluated read pairs / s on the 1M-read interval cluster.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
 
 Workload (BASELINE.json configs[2]): 1,000,000 synthetic reads,
 1-16 fillings each (seed 11), default clustering parameters.  Inputs are resident
-in HBM before timing.  One step = the whole device hot path:
-build_index (cluster.py:124) + pair kernel over this rank's query reads
-(cluster.py:187-227) + union-find components (cluster.py:230) [+ RCCL label
-exchange when N > 1].  ``value`` = evaluated read pairs of the whole job per
-second (unit of work: a unique candidate pair whose predicate is evaluated,
-SURVEY.md §8d).  Prints ONE JSON line on rank 0.
+in HBM before timing.  One step = the whole device hot path: build_index
+(cluster.py:124) + pair kernels over this rank's query reads (cluster.py:187-222)
++ the edge-cap check/replay (cluster.py:223-224; one rank) + union-find components
+(cluster.py:230) [+ RCCL label exchange when N > 1].
+
+``value`` = read pairs whose full predicate is evaluated (the length gate passes and
+overall_jaccard_similarity runs: the unit SURVEY.md §8d defines and the reference's
+measured 2.27e4 pairs/s counts) of the whole job per second.  Candidate
+pairs (gate-rejected ones included) and the dense-equivalent rate are secondary fields.
+
+``roofline``: the dominant kernel is the pair kernel (query_kernel).  Its algorithmic
+bytes per launch are those of this design's walk: every walked index
+record (16-B interval record + 8-B gate word) read once, each query read's header,
+length-gate bounds and forward degree, each of its intervals' sorted position, row and
+scan range, and the edge / deferred-list output.  ``achieved`` = those bytes ÷ the
+mean duration of the timed launches, measured with hipEvents the library records
+around each launch on its stream (fslr_get_pair_kernel_times).  ``traffic`` = HBM
+bytes per launch from rocprofv3 PMC counters (tools/pmc_traffic.py), used only when
+that summary was measured on the current pair-kernel sources.
+
+Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
@@ -28,6 +43,13 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK = 8.0e12          # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
 TRAFFIC_JSON = os.path.join(REPO, 'profiles', 'pmc_traffic_latest.json')
+# bytes per walked record / per query read / per query interval / per edge / per deferred entry
+B_WALK, B_READ, B_IVL, B_EDGE, B_DEFER = 24, 8 + 16 + 4, 4 + 12 + 8, 8 + 2, 8
+# the reference's own rate on this config: 33,020,021 Jaccard-evaluated
+# pairs in 1454.0 s of query_interval_trees, 1 core of the survey container, pure Python
+REFERENCE_PY = {'value': 33_020_021 / 1454.0, 'unit': 'Jaccard-evaluated read pairs/s', 'cores': 1,
+                'kind': 'reference', 'where': 'survey container (8-vCPU Xeon), not the GPU box',
+                'sample': 'reference cluster.py, 1M reads x 1-16, query_interval_trees stage (BASELINE.md)'}
 
 
 def kernel_source_hash():
@@ -49,8 +71,11 @@ def parse():
     ap.add_argument('--lmax', type=int, default=16)
     ap.add_argument('--seed', type=int, default=11)
     ap.add_argument('--dist', default='uniform')
-    ap.add_argument('--cpu-sample-reads', type=int, default=200_000,
-                    help='query reads in the bounded CPU-oracle baseline sample (0 = skip)')
+    ap.add_argument('--cpu-sample-stride', type=int, default=16,
+                    help='single-thread CPU baseline: query reads of every k-th 64-rank block (0 = skip the '
+                         'CPU baseline)')
+    ap.add_argument('--cpu-threads', type=int, default=0,
+                    help='threads of the all-core CPU baseline (0 = the process CPU share, at most 16)')
     ap.add_argument('--verify', action='store_true',
                     help='after timing, rank 0 checks its labels against a single-context run of all reads')
     ap.add_argument('--traffic-json', default=TRAFFIC_JSON,
@@ -61,6 +86,14 @@ def parse():
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_share():
+    n = len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else (os.cpu_count() or 1)
+    env = os.environ.get('OMP_NUM_THREADS')
+    if env and env.isdigit():
+        n = min(n, int(env))
+    return max(1, min(n, 16))
 
 
 def main():
@@ -83,7 +116,7 @@ def main():
             dist.init_process_group(backend)
 
     from fslr_amd import _lib, synth
-    from fslr_amd.dist import DeviceShardMerge
+    from fslr_amd.dist import DeviceShardMerge, shard_of
     from fslr_amd.prep import fold_overlap_threshold, pass_table
 
     t0 = time.perf_counter()
@@ -98,7 +131,10 @@ def main():
     torch.cuda.set_stream(stream)
     ctx = _lib.Context(dev_index, stream=stream.cuda_stream, profiling=True)
     thr = fold_overlap_threshold(csr.iv_aln, 0.8)
-    ctx.load_csr(csr, thr)
+    t_up = time.perf_counter()
+    ctx.load_csr(csr, thr)                 # host packing + H2D of the CSR (synchronous)
+    upload_s = time.perf_counter() - t_up
+    h2d_bytes = 16 * csr.n_reads + csr.n_intervals * (16 + 4 + 4 + 16 + 8)
     ctx.reserve_edges(12 * csr.n_reads)
     pt = pass_table([1, 1, 0.66, 0.66, 0.66, 0.5])
     qcut, ncut = 1 - 0.04, 1 - 0.25
@@ -106,20 +142,13 @@ def main():
     if world > 1:
         ctx.set_shard(rank, world)      # query-side index data (positions, ranges) for this shard's reads
 
-    # pair-phase events per timed step (read after the timed region: no host sync between steps)
-    ev_q = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            for _ in range(args.steps)]
-
-    def step(k=None):
+    def step():
         ctx.build_index()
-        if k is not None:
-            ev_q[k][0].record(stream)
         if world > 1:
             ctx.query_shard(qcut, ncut, pt, rank, world)      # balanced rank blocks (fslr_query_shard)
         else:
             ctx.query(qcut, ncut, pt, 10)
-        if k is not None:
-            ev_q[k][1].record(stream)
+            ctx.apply_edge_cap(10)                            # cluster.py:223-224 (no-op unless it binds)
         ctx.components()
         if merge is not None:
             merge()
@@ -128,7 +157,7 @@ def main():
     for w in range(max(1, args.warmup)):
         step()
         if w == 0:
-            st = ctx.stats()
+            st = ctx.stats(check=False)
             if st['n_edges'] > ctx.edge_capacity:
                 ctx.reserve_edges(st['n_edges'] + 4096)
     torch.cuda.synchronize()
@@ -139,32 +168,43 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
-    for k in range(args.steps):
-        step(k)
+    for _ in range(args.steps):
+        step()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     st = ctx.stats()
+    kern = ctx.pair_kernel_times(args.steps)       # the timed steps' main pair-kernel launches
+    kernel_ms = float(np.mean(kern)) if kern.size else float('nan')
 
-    tot = torch.tensor([elapsed, float(st['evaluated_pairs']), float(st['algo_bytes']), float(st['n_edges']),
-                        float(st['jaccard_evals'])], dtype=torch.float64,
-                       device=dev if backend == 'nccl' else 'cpu')
+    own = shard_of(np.arange(csr.n_reads), world) == rank if world > 1 else np.ones(csr.n_reads, bool)
+    q_reads = int(own.sum())
+    q_ivls = int(np.diff(csr.read_off)[own].sum())
+    algo_bytes = (B_WALK * st['walked_records'] + B_READ * q_reads + B_IVL * q_ivls + B_EDGE * st['n_edges'] +
+                  B_DEFER * st['deferred'])
+    tot = torch.tensor([elapsed, float(st['evaluated_pairs']), float(st['jaccard_evals']), float(st['n_edges']),
+                        float(st['max_fwd'])], dtype=torch.float64, device=dev if backend == 'nccl' else 'cpu')
     if dist:
         t_max = tot[:1].clone()
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-        sums = tot[1:].clone()
+        sums = tot[1:4].clone()
         dist.all_reduce(sums)
+        mf = tot[4:5].clone()
+        dist.all_reduce(mf, op=dist.ReduceOp.MAX)
         elapsed = float(t_max.item())
-        pairs, algo_bytes, n_edges, jacc = (float(x) for x in sums.tolist())
+        pairs, jacc, n_edges = (float(x) for x in sums.tolist())
+        max_fwd = int(mf.item())
+        if max_fwd > 10:
+            raise SystemExit('the edge cap binds on this input: its replay runs on one context (fslr_query over '
+                             'all reads); the sharded bench does not cover it')
     else:
-        pairs, algo_bytes, n_edges, jacc = (float(x) for x in tot[1:].tolist())
+        pairs, jacc, n_edges = (float(x) for x in tot[1:4].tolist())
+        max_fwd = int(st['max_fwd'])
     lib_t = ctx.timings()                     # hipEvents of the last step (library side)
     ms_per_step = 1000.0 * elapsed / args.steps
-    value = pairs / (elapsed / args.steps)
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_q]))
-    # per-launch algorithmic bytes of this rank's pair kernel (SURVEY §8d B_pair summed over its pairs)
-    achieved = st['algo_bytes'] / (kernel_ms / 1000.0)
+    value = jacc / (elapsed / args.steps)
+    achieved = algo_bytes / (kernel_ms / 1000.0)
     traffic = None
     traffic_src = None
     # the committed PMC summary is of the single-GPU launch (all query reads); a shard's launch moves less
@@ -175,27 +215,41 @@ def main():
             traffic = tj.get('query_kernel_hbm_bytes_per_launch')
             traffic_src = os.path.relpath(args.traffic_json, REPO)
 
+    # transfers around the device path (not in `value`): CSR upload before, labels / edges after
+    t = time.perf_counter()
+    labels = ctx.labels()
+    d2h_labels_s = time.perf_counter() - t
+    t = time.perf_counter()
+    ctx.edges(st['n_edges'])
+    d2h_edges_s = time.perf_counter() - t
+    transfer = {
+        'upload_csr_s': upload_s, 'upload_csr_bytes': h2d_bytes,
+        'd2h_labels_s': d2h_labels_s, 'd2h_edges_s': d2h_edges_s,
+        'pcie_inclusive_value': jacc / (elapsed / args.steps + upload_s + d2h_labels_s + d2h_edges_s),
+        'note': 'upload = host packing/validation + H2D of the CSR and data-order records, once per input; '
+                'the step keeps inputs resident in HBM',
+    }
+
     verified = None
     if args.verify and rank == 0:
-        got = ctx.labels()
         ref = _lib.Context(dev_index)      # full, unsharded
         ref.load_csr(csr, thr)
         ref.reserve_edges(12 * csr.n_reads)
         ref.run(qcut, ncut, pt)
-        verified = bool(np.array_equal(got, ref.labels()))
+        verified = bool(np.array_equal(labels, ref.labels()))
         ref.close()
         log(f'[rank 0] labels identical to a single-context run: {verified}')
 
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_sample_reads > 0:
-        cpu = cpu_baseline(csr, args.cpu_sample_reads)
+    if rank == 0 and world == 1 and args.cpu_sample_stride > 0:
+        cpu = cpu_baseline(csr, args.cpu_sample_stride, args.cpu_threads or cpu_share(), int(jacc))
 
     if rank == 0:
         n = csr.n_reads
         out = {
             'metric': 'Jaccard pair-compares/sec + HBM GB/s vs roofline, 1M-read interval cluster',
             'value': value,
-            'unit': 'evaluated read pairs/s',
+            'unit': 'Jaccard-evaluated read pairs/s',
             'n_gpus': world,
             'steps': args.steps,
             'warmup': args.warmup,
@@ -209,13 +263,17 @@ def main():
                 'workload': f'cfg3: {n} reads x 1-{args.lmax} fillings ({args.dist}), seed {args.seed}, '
                             'overlap 0.8, cutoffs 1,1,.66,.66,.66,.5, qlen-diff .04, n-aln-diff .25',
                 'n_reads': n, 'n_intervals': csr.n_intervals,
-                'evaluated_pairs_per_step': int(pairs), 'jaccard_evals_per_step': int(jacc),
-                'edges': int(n_edges), 'max_fwd_degree': int(st['max_fwd']),
-                'kernel_stats_rank0': {k: int(st[k]) for k in ('candidates', 'overflow_candidates', 'gather_pairs',
-                                                               'match_entries', 'matched_pairs')},
+                'jaccard_evals_per_step': int(jacc),
+                'candidate_pairs_per_step': int(pairs),
+                'candidate_pairs_per_s': pairs / (elapsed / args.steps),
+                'edges': int(n_edges), 'max_fwd_degree': max_fwd,
+                'kernel_stats_rank0': {k: int(st[k]) for k in ('candidates', 'walked_records', 'overflow_candidates',
+                                                               'gather_pairs', 'match_entries', 'matched_pairs',
+                                                               'deferred')},
                 'dense_equivalent_pairs_per_s': (n * (n - 1) / 2) / (elapsed / args.steps),
                 'parallelism': f'query-read shards x{world} (64-rank blocks round robin) + RCCL label all_gather'
                 if world > 1 else 'single GPU',
+                'transfer': transfer,
             },
             'roofline': {
                 'bound': 'hbm',
@@ -226,8 +284,13 @@ def main():
                 'frac': achieved / HBM_PEAK,
                 'traffic': traffic,
                 'traffic_source': traffic_src,
+                'waste_ratio': (traffic / algo_bytes) if traffic else None,
                 'kernel_ms': kernel_ms,
-                'algo_bytes_per_launch': int(st['algo_bytes']),
+                'kernel_launches_timed': int(kern.size),
+                'algo_bytes_per_launch': int(algo_bytes),
+                'algo_bytes_model': f'{B_WALK} B x walked records ({st["walked_records"]}) + {B_READ} B x query '
+                                    f'reads + {B_IVL} B x query intervals + {B_EDGE} B x edges + {B_DEFER} B x '
+                                    'deferred entries',
                 'phase_ms_last_step': lib_t,
             },
             'cpu_baseline': cpu,
@@ -240,9 +303,10 @@ def main():
     ctx.close()
 
 
-def cpu_baseline(csr, sample_reads):
-    """Bounded CPU-oracle sample (oracle/fslr_oracle.c, 1 thread): query reads [0, sample)
-    against all reads, index build included; evaluated pairs / s."""
+def cpu_baseline(csr, stride, threads, gpu_jacc):
+    """The C restatement (oracle/fslr_oracle.c) on the box's host cores, same input and unit:
+    1 thread on the query reads of every ``stride``-th 64-rank block, then ``threads`` threads
+    sharing one index over all query reads (E*; the cap does not bind on this input)."""
     try:
         from oracle import oracle as O
     except Exception as e:  # pragma: no cover
@@ -250,14 +314,22 @@ def cpu_baseline(csr, sample_reads):
     cnt = np.diff(csr.read_off)
     oc = O.OracleCSR(csr.read_off, csr.iv_chrom, csr.iv_start, csr.iv_end, csr.iv_aln,
                      np.repeat(csr.read_qlen2, cnt), np.repeat(csr.read_nal, cnt), csr.data_pos)
-    sample = min(sample_reads, csr.n_reads)
     t = time.perf_counter()
-    r = O.run_core(oc, use_cap=True, query_end=sample)
-    dt = time.perf_counter() - t
-    return {'value': r['stats']['evaluated_pairs'] / dt, 'unit': 'evaluated read pairs/s', 'cores': 1,
-            'kind': 'port', 'seconds': dt,
-            'sample': f'oracle/fslr_oracle.c on query reads [0, {sample}) of the same 1M-read input '
-                      f'({r["stats"]["evaluated_pairs"]} evaluated pairs, index over all reads)'}
+    one = O.count_threads(oc, nthreads=1, stride=stride)
+    dt1 = time.perf_counter() - t
+    t = time.perf_counter()
+    allc = O.count_threads(oc, nthreads=threads, stride=1)
+    dta = time.perf_counter() - t
+    return {'value': allc['jaccard_evals'] / dta, 'unit': 'Jaccard-evaluated read pairs/s', 'cores': threads,
+            'kind': 'port', 'seconds': dta,
+            'sample': f'oracle/fslr_oracle.c oracle_count_threads, all {csr.n_reads} query reads of the same input, '
+                      f'{threads} threads sharing one index (index build included); {allc["jaccard_evals"]} '
+                      f'Jaccard-evaluated pairs (GPU: {gpu_jacc})',
+            'host_cpus_visible': os.cpu_count(),
+            'single_thread': {'value': one['jaccard_evals'] / dt1, 'cores': 1, 'seconds': dt1,
+                              'sample': f'query reads of every {stride}th 64-rank block '
+                                        f'({one["jaccard_evals"]} pairs, index build included)'},
+            'reference_python': REFERENCE_PY}
 
 
 if __name__ == '__main__':

@@ -27,7 +27,8 @@ EXPORTED = ['fslr_abi_version', 'fslr_last_error', 'fslr_ctx_create', 'fslr_ctx_
             'fslr_components', 'fslr_run', 'fslr_sync', 'fslr_read_stats', 'fslr_get_timings', 'fslr_read_counters',
             'fslr_get_labels',
             'fslr_get_fwd_degree', 'fslr_get_edges', 'fslr_labels_device_ptr', 'fslr_copy_labels_device',
-            'fslr_copy_fwd_device', 'fslr_union_pairs', 'fslr_finalize_labels', 'fslr_apply_edge_cap']
+            'fslr_copy_fwd_device', 'fslr_union_pairs', 'fslr_finalize_labels', 'fslr_apply_edge_cap',
+            'fslr_get_pair_kernel_times']
 
 
 class HipUnavailable(RuntimeError):
@@ -56,7 +57,8 @@ class QueryStats(ctypes.Structure):
                 ('algo_bytes', ctypes.c_int64), ('overflow_candidates', ctypes.c_int64),
                 ('gather_pairs', ctypes.c_int64), ('match_entries', ctypes.c_int64),
                 ('matched_pairs', ctypes.c_int64), ('deferred', ctypes.c_int64),
-                ('deferred_capacity', ctypes.c_int64), ('edge_capacity', ctypes.c_int64)]
+                ('deferred_capacity', ctypes.c_int64), ('edge_capacity', ctypes.c_int64),
+                ('walked_records', ctypes.c_int64)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
@@ -72,7 +74,7 @@ class CapStats(ctypes.Structure):
 
 class Timings(ctypes.Structure):
     _fields_ = [('index_ms', ctypes.c_float), ('query_ms', ctypes.c_float), ('components_ms', ctypes.c_float),
-                ('total_ms', ctypes.c_float)]
+                ('total_ms', ctypes.c_float), ('pair_kernel_ms', ctypes.c_float)]
 
     def as_dict(self):
         return {f: float(getattr(self, f)) for f, _ in self._fields_}
@@ -120,6 +122,7 @@ def load(path: str = LIB_PATH):
         'fslr_union_pairs': (ctypes.c_int, [vp, vp, vp, i64, ctypes.c_int]),
         'fslr_finalize_labels': (ctypes.c_int, [vp]),
         'fslr_apply_edge_cap': (ctypes.c_int, [vp, i32, ctypes.POINTER(CapStats)]),
+        'fslr_get_pair_kernel_times': (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_float), i32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -273,6 +276,14 @@ class Context:
         t = Timings()
         self._check(self._L.fslr_get_timings(self._h, ctypes.byref(t)))
         return t.as_dict()
+
+    def pair_kernel_times(self, n: int = 256) -> np.ndarray:
+        """Durations (ms) of the main pair-kernel launch of the last ``n`` queries (profiling contexts)."""
+        out = np.zeros(n, np.float32)
+        got = self._L.fslr_get_pair_kernel_times(self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), n)
+        if got < 0:
+            self._check(-got)
+        return out[:got]
 
     def counters(self, n: int = 80) -> np.ndarray:
         """Raw device counters of the last query (kernels.hpp Counter; diagnostics)."""

@@ -105,8 +105,10 @@ void fslr_ctx_destroy(fslr_ctx* c) {
                   c->dgate,  c->chist,  c->heavy};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
-  if (c->ev_ok)
+  if (c->ev_ok) {
     for (auto& e : c->ev) (void)hipEventDestroy(e);
+    for (auto& e : c->kev) (void)hipEventDestroy(e);
+  }
   if (c->own_stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -116,6 +118,8 @@ int fslr_set_profiling(fslr_ctx* c, int enable) {
   HIP_TRY(c, hipSetDevice(c->device));
   if (enable && !c->ev_ok) {
     for (auto& e : c->ev) HIP_TRY(c, hipEventCreate(&e));
+    c->kev.assign(2 * fslr_ctx::kKernRing, nullptr);
+    for (auto& e : c->kev) HIP_TRY(c, hipEventCreate(&e));
     c->ev_ok = true;
   }
   c->profiling = enable != 0;
@@ -394,6 +398,12 @@ static int query_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_
   g.diag = c->diag;
   g.wstat = c->wstat;
   g.wstat_waves = c->wstat_waves;
+  g.ev_k0 = g.ev_k1 = nullptr;
+  if (c->profiling && c->n > 0 && a_end > a_begin) {
+    const int slot = static_cast<int>(c->n_kern++ % fslr_ctx::kKernRing);
+    g.ev_k0 = c->kev[2 * slot];
+    g.ev_k1 = c->kev[2 * slot + 1];
+  }
   c->last_full = a_begin == 0 && a_end == c->n && n_shards == 1;
   c->last_qcut = p->qlen_cut;
   c->last_ncut = p->nal_cut;
@@ -402,6 +412,7 @@ static int query_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_
   HIP_TRY(c, launch_query(g, c->thr_mode, c->stream));
   if (c->profiling) HIP_TRY(c, hipEventRecord(c->ev[3], c->stream));
   c->t_query_rec = c->profiling;
+  c->t_kernel_rec = c->profiling && c->n > 0 && a_end > a_begin;
   return FSLR_OK;
 }
 
@@ -474,6 +485,7 @@ int fslr_read_stats(fslr_ctx* c, fslr_query_stats* out) {
   out->gather_pairs = static_cast<int64_t>(cnt[kGather]);
   out->match_entries = static_cast<int64_t>(cnt[kMatchEntries]);
   out->matched_pairs = static_cast<int64_t>(cnt[kMatchedPairs]);
+  out->walked_records = static_cast<int64_t>(cnt[kWalked]);
   out->deferred = static_cast<int64_t>(cnt[kDeferCount]);
   out->deferred_capacity = c->defer_cap;
   out->edge_capacity = c->edge_cap;
@@ -498,9 +510,28 @@ int fslr_get_timings(fslr_ctx* c, fslr_timings* out) {
   if (!c->ev_ok) return FSLR_OK;
   if (c->t_index_rec) HIP_TRY(c, hipEventElapsedTime(&out->index_ms, c->ev[0], c->ev[1]));
   if (c->t_query_rec) HIP_TRY(c, hipEventElapsedTime(&out->query_ms, c->ev[2], c->ev[3]));
+  if (c->t_kernel_rec && c->n_kern > 0) {
+    const int slot = static_cast<int>((c->n_kern - 1) % fslr_ctx::kKernRing);
+    HIP_TRY(c, hipEventElapsedTime(&out->pair_kernel_ms, c->kev[2 * slot], c->kev[2 * slot + 1]));
+  }
   if (c->t_comp_rec) HIP_TRY(c, hipEventElapsedTime(&out->components_ms, c->ev[4], c->ev[5]));
   if (c->t_index_rec && c->t_comp_rec) HIP_TRY(c, hipEventElapsedTime(&out->total_ms, c->ev[0], c->ev[5]));
   return FSLR_OK;
+}
+
+int fslr_get_pair_kernel_times(fslr_ctx* c, float* ms, int32_t n) {
+  if (!c || (!ms && n > 0) || n < 0) return -FSLR_ERR_INVALID;
+  if (!c->ev_ok) return 0;
+  if (hipSetDevice(c->device) != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess)
+    return -fail(c, FSLR_ERR_HIP, "sync");
+  const int64_t have = std::min<int64_t>(c->n_kern, fslr_ctx::kKernRing);
+  const int k = static_cast<int>(std::min<int64_t>(have, n));
+  for (int i = 0; i < k; ++i) {
+    const int slot = static_cast<int>((c->n_kern - k + i) % fslr_ctx::kKernRing);
+    if (hipEventElapsedTime(&ms[i], c->kev[2 * slot], c->kev[2 * slot + 1]) != hipSuccess)
+      return -fail(c, FSLR_ERR_HIP, "hipEventElapsedTime");
+  }
+  return k;
 }
 
 int fslr_get_labels(fslr_ctx* c, int32_t* labels) {

@@ -68,8 +68,12 @@ struct fslr_ctx {
   // profiling
   bool profiling = false;
   hipEvent_t ev[8] = {};
+  // (profiling) a ring of event pairs around the main pair-kernel launch of the last kKernRing queries
+  static constexpr int kKernRing = 256;
+  std::vector<hipEvent_t> kev;
+  int64_t n_kern = 0;
   bool ev_ok = false;
-  bool t_index_rec = false, t_query_rec = false, t_comp_rec = false;
+  bool t_index_rec = false, t_query_rec = false, t_comp_rec = false, t_kernel_rec = false;
 };
 
 namespace fslr {

@@ -37,18 +37,19 @@ __host__ __device__ inline bool shard_owns(int read, int shard, int n_shards) {
 enum Counter { kEdgeCount = 0,          // atomic (own 128-B line)
                kDeferCount = 16,        // atomic (own 128-B line)
                kEval = 32, kJacc = 33, kCand = 34, kAlgoBytes = 35, kOverflow = 36, kGather = 37,
-               kMatchEntries = 38, kMatchedPairs = 39, kMaxFwd = 40,
+               kMatchEntries = 38, kMatchedPairs = 39, kMaxFwd = 40, kWalked = 41,
                kSecBase = 48,           // FSLR_SECTION_PROF builds: per-section cycle sums of the pair kernel
                kHeavyCount = 64,        // atomic (own 128-B line): reads handed to the partitioned launch
                kQueueBase = 80,         // pair kernel work queues: 8 counters, one 128-B line each
                kQueueStride = 16,
                kQueueBase2 = kQueueBase + 8 * kQueueStride,   // the partitioned launch's queues
                kNumCounters = kQueueBase2 + 8 * kQueueStride };
-// per-wave statistics of query_kernel: fields 0..8 (sum, except kWsMaxFwd: max), then (section-
+// per-wave statistics of query_kernel: fields 0..8 (sum, except kWsMaxFwd: max; kWsWalked: index
+// records walked, every pass counted), then (section-
 // timing builds) 8 section sums, slowest read cycles (max), its rank, wave cycles max / min,
 // wave count, cycle sums of reads 0, 1 and >= 2 of the wave
 enum WaveStat { kWsEval = 0, kWsJacc, kWsCand, kWsAlgoBytes, kWsOverflow, kWsMatchEntries, kWsMatchedPairs,
-                kWsMaxFwd, kWsBase = 8, kWsProf = kWsBase + 16, kWStride = 32 };
+                kWsMaxFwd, kWsWalked, kWsBase = 9, kWsProf = kWsBase + 16, kWStride = 32 };
 
 // ---- pair predicates shared by the pair kernels (query.hip) and the cap replay (cap.hip) ----
 // interval accepts overlap o (fslr_hip.h: thr >= 0 ? o >= thr : o <= ~thr)
@@ -133,6 +134,7 @@ struct QueryArgs {
   unsigned long long* wstat;          // [wstat_waves x kWStride] per-wave statistics (plain stores)
   int wstat_waves;
   unsigned long long* diag;           // FSLR_SECTION_PROF: [N] per read (start cycle in its wave) << 32 | cycles
+  hipEvent_t ev_k0, ev_k1;            // (profiling) recorded around the main pair-kernel launch, or null
 };
 // thr_mode: 0 = every non-sentinel threshold >= 1 (fast match), 1 = general encoding
 hipError_t launch_query(const QueryArgs& a, int thr_mode, hipStream_t s);

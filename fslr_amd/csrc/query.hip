@@ -316,7 +316,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
     }
   };
   int v = pull();
-  unsigned long long w_eval = 0, w_jacc = 0, w_cand = 0, w_over = 0, w_ml = 0, w_mp = 0;
+  unsigned long long w_eval = 0, w_jacc = 0, w_cand = 0, w_over = 0, w_ml = 0, w_mp = 0, w_walk = 0;
   // algorithmic bytes of evaluated pairs: 16 (LA + LB) + 32 each
   unsigned long long w_la_pairs = 0;
   unsigned l_lb = 0;
@@ -613,6 +613,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
     SEC_ADD(6, t_s6);
     w_ml += mln;
     w_mp += mpn;
+    w_walk += static_cast<unsigned long long>(R);
     };
     // R (the walk's records) bounds the distinct partners; a read whose walk is more than 1.5
     // partitions long goes to the partitioned launch, which splits it into ~pass_records-record parts
@@ -670,6 +671,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
     f = lane == kWsMatchEntries ? w_ml : f;
     f = lane == kWsMatchedPairs ? w_mp : f;
     f = lane == kWsMaxFwd ? static_cast<unsigned long long>(w_maxfwd) : f;
+    f = lane == kWsWalked ? w_walk : f;
 #ifdef FSLR_SECTION_PROF
     for (int k = 0; k < kSections; ++k) f = lane == kWsBase + k ? sec[k] : f;
     f = lane == kWsBase + 8 ? read_max : f;
@@ -689,7 +691,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
       } else if (lane < kWsBase && f) {
         const int dst = lane == kWsEval ? kEval : lane == kWsJacc ? kJacc : lane == kWsCand ? kCand
                       : lane == kWsAlgoBytes ? kAlgoBytes : lane == kWsOverflow ? kOverflow
-                      : lane == kWsMatchEntries ? kMatchEntries : kMatchedPairs;
+                      : lane == kWsMatchEntries ? kMatchEntries : lane == kWsWalked ? kWalked : kMatchedPairs;
         atomicAdd(&g.counters[dst], f);
       }
     }
@@ -766,7 +768,7 @@ __global__ __launch_bounds__(kReduceBlock) void k_reduce_wstat(const unsigned lo
   } else if (fi < kWsBase) {
     const int dst = fi == kWsEval ? kEval : fi == kWsJacc ? kJacc : fi == kWsCand ? kCand
                   : fi == kWsAlgoBytes ? kAlgoBytes : fi == kWsOverflow ? kOverflow
-                  : fi == kWsMatchEntries ? kMatchEntries : kMatchedPairs;
+                  : fi == kWsMatchEntries ? kMatchEntries : fi == kWsWalked ? kWalked : kMatchedPairs;
     if (r) atomicAdd(&counters[dst], r);
   } else if (r) {
     if (o == kOpSum) atomicAdd(&counters[kSecBase + (fi - kWsBase)], r);
@@ -922,10 +924,12 @@ hipError_t launch_query(const QueryArgs& a_in, int thr_mode, hipStream_t s) {
       // FSLR_DYNAMIC_MIN_READS: lets the parity tests drive the work-queue path at small sizes
       if (const char* e = getenv("FSLR_DYNAMIC_MIN_READS")) dyn_min = std::max(0ll, atoll(e));
       a.k_static = nq >= dyn_min * nw ? 0 : static_cast<int>((nq + nw - 1) / nw);
+      if (a.ev_k0) (void)hipEventRecord(a.ev_k0, s);
       if (thr_mode == 0)
         query_kernel<0, false><<<blocks, kBlock, 0, s>>>(a);
       else
         query_kernel<1, false><<<blocks, kBlock, 0, s>>>(a);
+      if (a.ev_k1) (void)hipEventRecord(a.ev_k1, s);
       const int nwv = blocks * kWavesPerBlock;
       const int rb = std::min(kReduceMaxBlocks, (nwv + kWave - 1) / kWave);
       k_reduce_wstat<<<rb, kReduceBlock, 0, s>>>(a.wstat, nwv, a.counters, a.err);

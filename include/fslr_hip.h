@@ -110,6 +110,7 @@ typedef struct {
     int64_t deferred;              /* entries on the deferred (gather-evaluated) list */
     int64_t deferred_capacity;     /* its capacity; deferred > capacity ⇒ FSLR_ERR_STATE, reserve + rerun */
     int64_t edge_capacity;         /* edge buffer capacity; n_edges > capacity ⇒ reserve + rerun */
+    int64_t walked_records;        /* index records the pair kernels walked (every partner-partition pass) */
 } fslr_query_stats;
 
 typedef struct {
@@ -117,6 +118,7 @@ typedef struct {
     float query_ms;                /* fslr_query: pair kernel device time (events around the launch) */
     float components_ms;           /* union-find device time */
     float total_ms;                /* first to last event of the last fslr_run/individual calls */
+    float pair_kernel_ms;          /* the main pair-kernel launch alone (query_kernel) */
 } fslr_timings;
 
 /* The reference's per-query-read edge cap (cluster.py:223-224), see fslr_apply_edge_cap. */
@@ -183,6 +185,10 @@ int  fslr_sync(fslr_ctx *ctx);
  * (reserve and rerun the query: components and labels of an overflowed query are refused) */
 int  fslr_read_stats(fslr_ctx *ctx, fslr_query_stats *out);
 int  fslr_get_timings(fslr_ctx *ctx, fslr_timings *out);        /* syncs */
+/* Profiling: durations (ms) of the main pair-kernel launch of the last min(n, 256) queries since
+ * profiling was enabled, oldest first (hipEvents recorded on the context's stream around that one
+ * launch).  Syncs; returns the count or -error. */
+int  fslr_get_pair_kernel_times(fslr_ctx *ctx, float *ms, int32_t n);
 /* Raw device counters of the last query (diagnostics; layout is internal, kernels.hpp:
  * Counter).  Copies min(n, 32) words, syncs, returns the count or -error. */
 int  fslr_read_counters(fslr_ctx *ctx, uint64_t *out, int n);

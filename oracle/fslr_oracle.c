@@ -187,38 +187,50 @@ static int64_t jaccard(const oracle_input *in, int64_t a0, int64_t la, int64_t b
 
 /* ---------------- driver ---------------- */
 
-int oracle_query(const oracle_input *in, const oracle_params *p,
-                 int64_t *edge_a, int64_t *edge_b, int32_t *edge_I, int32_t *edge_U, int64_t edge_capacity,
-                 int32_t *fwd_count, int32_t *comp, oracle_stats *st) {
-    memset(st, 0, sizeof(*st));
-    st->err_a = st->err_b = -1;
+/* per-chromosome indexes over all intervals (build_interval_trees, cluster.py:124-130) */
+typedef struct {
+    int64_t *read_of;     /* interval -> read rank */
+    chrom_index *ci;
+    int64_t nc;
+    int64_t *cnt, *all;
+    int64_t maxlen;
+} oracle_index;
+
+static void index_free(oracle_index *ix) {
+    free(ix->read_of); free(ix->ci); free(ix->cnt); free(ix->all);
+    memset(ix, 0, sizeof(*ix));
+}
+
+static int index_build(const oracle_input *in, oracle_index *ix) {
+    memset(ix, 0, sizeof(*ix));
     const int64_t N = in->n_reads;
     if (N < 0 || !in->read_off) return ORACLE_BAD_INPUT;
     const int64_t NI = in->read_off[N];
-    int64_t *read_of = (int64_t *)malloc((size_t)(NI > 0 ? NI : 1) * sizeof(int64_t));
-    if (!read_of) return ORACLE_NOMEM;
+    ix->read_of = (int64_t *)malloc((size_t)(NI > 0 ? NI : 1) * sizeof(int64_t));
+    if (!ix->read_of) return ORACLE_NOMEM;
     int64_t maxlen = 1, cmax = -1, cmin = 0;
     for (int64_t r = 0; r < N; r++) {
-        for (int64_t k = in->read_off[r]; k < in->read_off[r + 1]; k++) read_of[k] = r;
+        for (int64_t k = in->read_off[r]; k < in->read_off[r + 1]; k++) ix->read_of[k] = r;
         if (in->read_off[r + 1] - in->read_off[r] > maxlen) maxlen = in->read_off[r + 1] - in->read_off[r];
     }
     for (int64_t k = 0; k < NI; k++) {
         if (in->chrom[k] > cmax) cmax = in->chrom[k];
         if (in->chrom[k] < cmin) cmin = in->chrom[k];
     }
-    if (cmin < 0 || cmax > (1 << 24)) { free(read_of); return ORACLE_BAD_INPUT; }
-    int64_t nc = cmax + 1;
-    /* build per-chrom indexes */
-    chrom_index *ci = (chrom_index *)calloc((size_t)(nc > 0 ? nc : 1), sizeof(chrom_index));
-    int64_t *cnt = (int64_t *)calloc((size_t)(nc > 0 ? nc : 1), sizeof(int64_t));
-    int64_t *all = (int64_t *)malloc((size_t)(NI > 0 ? NI : 1) * 3 * sizeof(int64_t));
-    unsigned char *used = (unsigned char *)malloc((size_t)maxlen);
-    if (!ci || !cnt || !all || !used) { free(read_of); free(ci); free(cnt); free(all); free(used); return ORACLE_NOMEM; }
-    for (int64_t k = 0; k < NI; k++) cnt[in->chrom[k]]++;
+    if (cmin < 0 || cmax > (1 << 24)) { index_free(ix); return ORACLE_BAD_INPUT; }
+    const int64_t nc = cmax + 1;
+    ix->nc = nc;
+    ix->maxlen = maxlen;
+    ix->ci = (chrom_index *)calloc((size_t)(nc > 0 ? nc : 1), sizeof(chrom_index));
+    ix->cnt = (int64_t *)calloc((size_t)(nc > 0 ? nc : 1), sizeof(int64_t));
+    ix->all = (int64_t *)malloc((size_t)(NI > 0 ? NI : 1) * 3 * sizeof(int64_t));
+    if (!ix->ci || !ix->cnt || !ix->all) { index_free(ix); return ORACLE_NOMEM; }
+    chrom_index *ci = ix->ci;
+    for (int64_t k = 0; k < NI; k++) ix->cnt[in->chrom[k]]++;
     int64_t off = 0;
     for (int64_t c = 0; c < nc; c++) {
-        ci[c].n = 0; ci[c].iv = all + off; ci[c].st = all + NI + off; ci[c].pmax = all + 2 * NI + off;
-        off += cnt[c];
+        ci[c].n = 0; ci[c].iv = ix->all + off; ci[c].st = ix->all + NI + off; ci[c].pmax = ix->all + 2 * NI + off;
+        off += ix->cnt[c];
     }
     for (int64_t k = 0; k < NI; k++) { chrom_index *x = &ci[in->chrom[k]]; x->iv[x->n++] = k; }
     g_in = in;
@@ -232,9 +244,25 @@ int oracle_query(const oracle_input *in, const oracle_params *p,
             x->pmax[t] = m;
         }
     }
+    return ORACLE_OK;
+}
+
+int oracle_query(const oracle_input *in, const oracle_params *p,
+                 int64_t *edge_a, int64_t *edge_b, int32_t *edge_I, int32_t *edge_U, int64_t edge_capacity,
+                 int32_t *fwd_count, int32_t *comp, oracle_stats *st) {
+    memset(st, 0, sizeof(*st));
+    st->err_a = st->err_b = -1;
+    const int64_t N = in->n_reads;
+    oracle_index ix;
+    int brc = index_build(in, &ix);
+    if (brc != ORACLE_OK) return brc;
+    int64_t *read_of = ix.read_of;
+    chrom_index *ci = ix.ci;
+    unsigned char *used = (unsigned char *)malloc((size_t)ix.maxlen);
+    if (!used) { index_free(&ix); return ORACLE_NOMEM; }
 
     pairset seen;
-    if (ps_init(&seen, 1 << 16) != 0) { free(read_of); free(ci); free(cnt); free(all); free(used); return ORACLE_NOMEM; }
+    if (ps_init(&seen, 1 << 16) != 0) { index_free(&ix); free(used); return ORACLE_NOMEM; }
     int rc = ORACLE_OK;
     int64_t ne = 0;
     /* graph node insertion order (networkx dict order) */
@@ -316,7 +344,7 @@ int oracle_query(const oracle_input *in, const oracle_params *p,
         free(root_comp);
     }
 done:
-    free(seen.slot); free(read_of); free(ci); free(cnt); free(all); free(used);
+    free(seen.slot); index_free(&ix); free(used);
     free(ins_order); free(ins_pos); free(uf);
     return rc;
 }
@@ -352,4 +380,99 @@ int oracle_lengths_differ(int64_t q1, int64_t q2, int64_t n1, int64_t n2, double
     if (zd) return ORACLE_ZERO_DIVISION;
     *out = r;
     return ORACLE_OK;
+}
+
+/* ---------------- CPU baseline (bench.py's cpu_baseline leg only) ----------------
+ * The uncapped graph E* (every candidate pair evaluated once, in its lower-rank read's loop: the
+ * reference's result whenever the edge cap does not bind) over the query reads whose 64-rank block
+ * k has k % stride == 0, spread over nthreads POSIX threads sharing one index (blocks dealt round
+ * robin, as the GPU shards deal them).  Counts only; no graph. */
+#include <pthread.h>
+
+typedef struct {
+    const oracle_input *in;
+    const oracle_params *p;
+    const oracle_index *ix;
+    int64_t tid, nthreads, stride;
+    oracle_stats st;
+    int rc;
+} count_job;
+
+static void *count_worker(void *arg) {
+    count_job *j = (count_job *)arg;
+    const oracle_input *in = j->in;
+    const oracle_params *p = j->p;
+    const int64_t N = in->n_reads;
+    int64_t *stamp = (int64_t *)malloc((size_t)(N > 0 ? N : 1) * sizeof(int64_t));
+    unsigned char *used = (unsigned char *)malloc((size_t)j->ix->maxlen);
+    if (!stamp || !used) { free(stamp); free(used); j->rc = ORACLE_NOMEM; return NULL; }
+    for (int64_t r = 0; r < N; r++) stamp[r] = -1;
+    const int64_t nblk = (N + 63) / 64;
+    int64_t k_own = 0;
+    for (int64_t blk = 0; blk < nblk && j->rc == ORACLE_OK; blk += j->stride) {
+        if ((k_own++ % j->nthreads) != j->tid) continue;
+        const int64_t a_hi = (blk + 1) * 64 < N ? (blk + 1) * 64 : N;
+        for (int64_t a = blk * 64; a < a_hi && j->rc == ORACLE_OK; a++) {
+            const int64_t a0 = in->read_off[a], la = in->read_off[a + 1] - a0;
+            for (int64_t i = 0; i < la; i++) {
+                const int64_t itv = a0 + i;
+                const chrom_index *x = &j->ix->ci[in->chrom[itv]];
+                const int64_t qs = in->start[itv], qe = in->end[itv];
+                int64_t lo = 0, hi = x->n;
+                while (lo < hi) { int64_t mid = (lo + hi) >> 1; if (x->st[mid] <= qe) lo = mid + 1; else hi = mid; }
+                for (int64_t t = lo - 1; t >= 0 && x->pmax[t] >= qs; t--) {
+                    const int64_t o = x->iv[t];
+                    if (in->end[o] < qs) continue;
+                    j->st.interval_hits++;
+                    const int64_t b = j->ix->read_of[o];
+                    if (b <= a || stamp[b] == a) continue;   /* own read, lower rank (its loop), seen */
+                    stamp[b] = a;
+                    j->st.evaluated_pairs++;
+                    int zd = 0;
+                    if (lengths_differ(in->qlen2[itv], in->qlen2[o], in->nal[itv], in->nal[o], p->qlen_diff,
+                                       p->nal_diff, &zd) || zd) {
+                        if (zd) j->rc = ORACLE_ZERO_DIVISION;
+                        continue;
+                    }
+                    j->st.jaccard_evals++;
+                    const int64_t b0 = in->read_off[b], lb = in->read_off[b + 1] - b0;
+                    int64_t U = 0;
+                    const int64_t I = jaccard(in, a0, la, b0, lb, p->overlap, used, &U, &zd);
+                    if (zd) { j->rc = ORACLE_ZERO_DIVISION; continue; }
+                    if (I == 0) continue;
+                    const double target = (I - 1 < p->n_cutoffs) ? p->cutoffs[I - 1] : p->cutoffs[p->n_cutoffs - 1];
+                    if ((double)I / (double)U >= target) j->st.n_edges++;
+                }
+            }
+        }
+    }
+    free(stamp); free(used);
+    return NULL;
+}
+
+int oracle_count_threads(const oracle_input *in, const oracle_params *p, int64_t nthreads, int64_t stride,
+                         oracle_stats *st) {
+    memset(st, 0, sizeof(*st));
+    if (nthreads < 1 || nthreads > 1024 || stride < 1) return ORACLE_BAD_INPUT;
+    oracle_index ix;
+    int rc = index_build(in, &ix);
+    if (rc != ORACLE_OK) return rc;
+    count_job *jobs = (count_job *)calloc((size_t)nthreads, sizeof(count_job));
+    pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+    if (!jobs || !th) { free(jobs); free(th); index_free(&ix); return ORACLE_NOMEM; }
+    for (int64_t t = 0; t < nthreads; t++) {
+        jobs[t].in = in; jobs[t].p = p; jobs[t].ix = &ix;
+        jobs[t].tid = t; jobs[t].nthreads = nthreads; jobs[t].stride = stride; jobs[t].rc = ORACLE_OK;
+        if (pthread_create(&th[t], NULL, count_worker, &jobs[t]) != 0) { jobs[t].rc = ORACLE_NOMEM; th[t] = 0; }
+    }
+    for (int64_t t = 0; t < nthreads; t++) {
+        if (th[t]) pthread_join(th[t], NULL);
+        st->interval_hits += jobs[t].st.interval_hits;
+        st->evaluated_pairs += jobs[t].st.evaluated_pairs;
+        st->jaccard_evals += jobs[t].st.jaccard_evals;
+        st->n_edges += jobs[t].st.n_edges;
+        if (jobs[t].rc != ORACLE_OK) rc = jobs[t].rc;
+    }
+    free(jobs); free(th); index_free(&ix);
+    return rc;
 }

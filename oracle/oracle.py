@@ -64,6 +64,9 @@ def lib():
         L.oracle_jaccard_lists.restype = ctypes.c_int
         L.oracle_jaccard_lists.argtypes = [ctypes.c_int64] + [ctypes.c_void_p] * 4 + [ctypes.c_int64] + \
             [ctypes.c_void_p] * 4 + [ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_count_threads.restype = ctypes.c_int
+        L.oracle_count_threads.argtypes = [ctypes.POINTER(_Input), ctypes.POINTER(_Params), ctypes.c_int64,
+                                           ctypes.c_int64, ctypes.POINTER(_Stats)]
         L.oracle_lengths_differ.restype = ctypes.c_int
         L.oracle_lengths_differ.argtypes = [ctypes.c_int64] * 4 + [ctypes.c_double] * 2 + [ctypes.c_void_p]
         _lib = L
@@ -134,6 +137,24 @@ def run_core(csr: OracleCSR, overlap=0.8, cutoffs=(1, 1, 0.66, 0.66, 0.66, 0.5),
     return dict(edge_a=ea[:ne].copy(), edge_b=eb[:ne].copy(), edge_I=eI[:ne].copy(), edge_U=eU[:ne].copy(),
                 fwd=fwd[:N].copy(), comp=comp[:N].copy(),
                 stats={f: getattr(st, f) for f, _ in _Stats._fields_})
+
+
+def count_threads(csr: OracleCSR, nthreads=1, stride=1, overlap=0.8, cutoffs=(1, 1, 0.66, 0.66, 0.66, 0.5),
+                  qlen_diff=0.04, n_aln_diff=0.25):
+    """CPU baseline: E* pair / edge counts over the query reads of every ``stride``-th 64-rank block,
+    ``nthreads`` POSIX threads sharing one index (``fslr_oracle.c:oracle_count_threads``)."""
+    L = lib()
+    inp = _Input(csr.n_reads, *(_p(getattr(csr, f)) for f in ('read_off', 'chrom', 'start', 'end', 'aln', 'qlen2',
+                                                               'nal', 'data_pos')))
+    cut = np.ascontiguousarray(cutoffs, dtype=np.float64)
+    prm = _Params(float(overlap), _p(cut), len(cut), float(qlen_diff), float(n_aln_diff), 10, 0, -1)
+    st = _Stats()
+    rc = L.oracle_count_threads(ctypes.byref(inp), ctypes.byref(prm), int(nthreads), int(stride), ctypes.byref(st))
+    if rc == ORACLE_ZERO_DIVISION:
+        raise OracleZeroDivision('division by zero')
+    if rc != ORACLE_OK:
+        raise RuntimeError(f'oracle_count_threads failed rc={rc}')
+    return {f: getattr(st, f) for f, _ in _Stats._fields_}
 
 
 def jaccard_lists(l1, l2, overlap):

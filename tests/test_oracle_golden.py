@@ -121,3 +121,23 @@ def test_oracle_vectors(vec):
     np.testing.assert_array_equal(comp, z['comp'])
     np.testing.assert_array_equal(fwd, z['fwd'])
     assert res['stats']['n_edges'] == int(z['n_edges'])
+
+
+@pytest.mark.parametrize('nthreads', [1, 4])
+def test_threaded_cpu_baseline_counts_equal_the_oracle(nthreads):
+    """bench.py's all-core CPU baseline (oracle_count_threads) evaluates exactly the pairs of the
+    uncapped reference loop; a block-strided sample evaluates the sampled reads' forward pairs."""
+    from fslr_amd import synth
+    s = synth.generate(20_000, 16, 11)
+    csr = s.interval_data().csr()
+    cnt = np.diff(csr.read_off)
+    oc = O.OracleCSR(csr.read_off, csr.iv_chrom, csr.iv_start, csr.iv_end, csr.iv_aln, np.repeat(csr.read_qlen2, cnt),
+                     np.repeat(csr.read_nal, cnt), csr.data_pos)
+    full = O.run_core(oc, use_cap=False)
+    got = O.count_threads(oc, nthreads=nthreads)
+    for k in ('evaluated_pairs', 'jaccard_evals', 'n_edges'):
+        assert got[k] == full['stats'][k], k
+    # stride 4: query reads of blocks 0, 4, 8, ... == forward edges of those reads in the full run
+    part = O.count_threads(oc, nthreads=nthreads, stride=4)
+    own = (np.arange(csr.n_reads) // 64) % 4 == 0
+    assert part['n_edges'] == int(full['fwd'][own].sum())

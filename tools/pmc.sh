@@ -11,7 +11,7 @@ for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_
            "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $set --kernel-include-regex "query_kernel" -d $ROOT/$OUT/p$i -o pmc \
-      --output-format csv -- python3 $ROOT/bench.py --steps 2 --warmup 1 --cpu-sample-reads 0 "$@" \
+      --output-format csv -- python3 $ROOT/bench.py --steps 2 --warmup 1 --cpu-sample-stride 0 "$@" \
       > $ROOT/$OUT/p$i.log 2>&1
 done
 cd $ROOT
