@@ -191,8 +191,10 @@ class Context:
 
     def load_csr(self, csr, iv_thr):
         """Upload a ``fslr_amd.prep.CSR`` (with its start-sorted data order) and thresholds."""
+        # the data-order index build needs the list in start order (prepare_data's sort); any other
+        # order (a caller-built list) takes the full (chrom, start) sort
         self.set_reads(csr.read_off, csr.read_qlen2, csr.read_nal, csr.iv_chrom, csr.iv_start, csr.iv_end, iv_thr,
-                       csr.n_chroms, iv_data_pos=csr.data_pos)
+                       csr.n_chroms, iv_data_pos=csr.data_pos if getattr(csr, 'start_sorted', True) else None)
 
     def set_thresholds(self, iv_thr):
         t = np.ascontiguousarray(iv_thr, dtype=np.int32)

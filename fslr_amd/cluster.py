@@ -178,9 +178,11 @@ def get_chromosome_lengths(bam_path):
 class DeviceIntervalIndex:
     """What build_interval_trees returns: the CSR in HBM plus the sorted interval index."""
 
-    def __init__(self, data: IntervalData, device: int | None = None, ctx: Context | None = None):
+    def __init__(self, data, device: int | None = None, ctx: Context | None = None):
+        self.source = data                      # what the caller passed (query_interval_trees checks it)
         if not isinstance(data, IntervalData):
-            raise TypeError('build_interval_trees expects the IntervalData returned by prepare_data')
+            # the reference's own prepare_data output: a list of IntervalItem (cluster.py:116-121)
+            data = IntervalData.from_items(data)
         self.data = data
         self.csr = data.csr()
         self.ctx = ctx or Context(_default_device() if device is None else device)
@@ -191,7 +193,9 @@ class DeviceIntervalIndex:
 
 
 def build_interval_trees(data, device: int | None = None) -> DeviceIntervalIndex:
-    """cluster.py:124-130: upload the prepared intervals and build the (chrom, start) index on the GPU."""
+    """cluster.py:124-130: upload the prepared intervals and build the (chrom, start) index on the GPU.
+
+    ``data`` is this module's ``prepare_data`` result or the reference's (a list of IntervalItem)."""
     return DeviceIntervalIndex(data, device)
 
 
@@ -266,7 +270,8 @@ def query_interval_trees(interval_trees, data, overlap_cutoff, jaccard_threshold
     set order (arbitrary).
     """
     min(jaccard_threshold)                              # cluster.py:188 raises on an empty list
-    if not isinstance(interval_trees, DeviceIntervalIndex) or interval_trees.data is not data:
+    if not isinstance(interval_trees, DeviceIntervalIndex) or (interval_trees.source is not data and
+                                                               interval_trees.data is not data):
         interval_trees = DeviceIntervalIndex(data)
     idx = interval_trees
     data = idx.data

@@ -53,6 +53,9 @@ int ensure_capacity(fslr_ctx* c, int64_t n, int64_t ni, int n_chroms) {
     if ((rc = dalloc(c, &c->umax, FSLR_MAX_L))) return rc;
     if ((rc = dalloc(c, &c->counters, kNumCounters))) return rc;
     if ((rc = dalloc(c, &c->errw, kErrWords))) return rc;
+    // no query yet: no edges, no errors (fslr_components before any query gives singleton labels)
+    HIP_TRY(c, hipMemsetAsync(c->counters, 0, kNumCounters * sizeof(unsigned long long), c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->errw, 0, kErrWords * sizeof(int), c->stream));
   }
   return FSLR_OK;
 }

@@ -126,6 +126,25 @@ class IntervalData:
             self._csr = build_csr(self)
         return self._csr
 
+    @classmethod
+    def from_items(cls, items) -> 'IntervalData':
+        """The columns of a reference-built ``data`` list (a sequence of ``IntervalItem``, the
+        return value of the reference's prepare_data, cluster.py:116-121), in list order."""
+        import pandas as pd
+        items = list(items)
+        n = len(items)
+        cols = list(zip(*items)) if n else [()] * 9
+        chrom_raw = np.asarray(cols[0], dtype=object) if n else np.zeros(0, object)
+        try:
+            chrom = np.asarray(cols[0], dtype=np.int64) if n else np.zeros(0, np.int64)
+        except (TypeError, ValueError):                  # names (rename_chromosomes not applied)
+            chrom = pd.factorize(chrom_raw, sort=False)[0].astype(np.int64)
+        codes, uniq = pd.factorize(np.asarray(cols[4], dtype=object) if n else np.zeros(0, object), sort=False)
+        i64 = lambda k: np.asarray(cols[k], dtype=np.int64) if n else np.zeros(0, np.int64)
+        return cls(chrom=chrom, start=i64(1), end=i64(2), aln_size=i64(3), qcode=codes.astype(np.int64),
+                   qnames=np.asarray(uniq, dtype=object), n_alignments=i64(5), qlen2=i64(6), middle=i64(7),
+                   index=np.asarray(cols[8], dtype=object) if n else np.zeros(0, object))
+
 
 def data_order(start: np.ndarray) -> np.ndarray:
     """Row order of ``df.sort_values('start')`` (pandas nargsort: quicksort argsort, no NaN)."""
@@ -172,6 +191,7 @@ class CSR:
     read_qcode: np.ndarray   # int64 [n] code of each rank's qname
     data_pos: np.ndarray     # int64 [ni] position in the data list
     nal_varies: bool         # n_alignments not constant within some read (order-dependent in the reference)
+    start_sorted: bool = True  # the data list is in non-decreasing start order (prepare_data's sort)
 
     @property
     def n_reads(self):
@@ -242,7 +262,8 @@ def build_csr(data: IntervalData) -> CSR:
                read_nal=read_nal.astype(np.int32), iv_chrom=chrom_dense.astype(np.int32),
                iv_start=start.astype(np.int32), iv_end=end.astype(np.int32),
                iv_aln=np.asarray(data.aln_size, np.int64)[perm], n_chroms=max(1, int(len(cids))),
-               read_qcode=read_qcode, data_pos=perm.astype(np.int64), nal_varies=nal_varies)
+               read_qcode=read_qcode, data_pos=perm.astype(np.int64), nal_varies=nal_varies,
+               start_sorted=bool(n_iv < 2 or np.all(np.diff(np.asarray(data.start, np.int64)) >= 0)))
 
 
 # ------------------------------------------------------------------------------------------

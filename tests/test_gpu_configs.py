@@ -1,0 +1,110 @@
+"""BASELINE configs 4 and 5 on the GPU (the largest inputs of the parity suite).
+
+* cfg4: 1M reads split into 8 query shards (the multi-GPU partition, fslr_set_shard /
+  fslr_query_shard, one context per shard on one GPU), per-shard components merged by
+  union of the shards' label vectors (what DeviceShardMerge does after its RCCL
+  all_gather): identical labels, edges and pair counts to one full context, and the
+  CPU oracle's pair / edge counts.
+* cfg5: 10M reads, 1-64 fillings (truncated Zipf 1.5): the edge cap binds (forward
+  degrees up to 28); the capped graph of the full run, restricted to the loops of query
+  reads [0, 50000), equals the oracle's reference loop over those reads
+  (tests/golden/cfg5/sample50k_capped.npz, made by tests/golden/make_cfg5_sample.py).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from fslr_amd import _lib, synth
+from fslr_amd.prep import fold_overlap_threshold, pass_table
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), 'golden')
+CUTS = [1, 1, 0.66, 0.66, 0.66, 0.5]
+
+
+@pytest.mark.slow
+def test_config4_1m_eight_shards_merge_to_the_full_run():
+    s = synth.generate(1_000_000, 16, 11)
+    csr = s.interval_data().csr()
+    thr = fold_overlap_threshold(csr.iv_aln, 0.8)
+    pt = pass_table(CUTS)
+    full = _lib.Context(0)
+    full.load_csr(csr, thr)
+    full.reserve_edges(12 * csr.n_reads)
+    full.build_index()
+    fst = full.run_query(1 - 0.04, 1 - 0.25, pt)
+    assert full.apply_edge_cap(10)['applied'] == 0          # cfg3/4: the cap does not bind
+    full.components()
+    want_labels = full.labels()
+    want_edges = sorted(zip(*[x.tolist() for x in full.edges(fst['n_edges'])]))
+    W = 8
+    labels, edges, pairs, jacc = [], [], 0, 0
+    for r in range(W):
+        c = _lib.Context(0)
+        c.load_csr(csr, thr)
+        c.reserve_edges(4 * csr.n_reads)
+        c.set_shard(r, W)
+        c.build_index()
+        c.query_shard(1 - 0.04, 1 - 0.25, pt, r, W)
+        st = c.stats()
+        pairs += st['evaluated_pairs']
+        jacc += st['jaccard_evals']
+        a, b, I, U = c.edges(st['n_edges'])
+        assert np.all((a // 64) % W == r)
+        edges += list(zip(a.tolist(), b.tolist(), I.tolist(), U.tolist()))
+        c.components()
+        labels.append(c.labels())
+        c.close()
+    assert pairs == fst['evaluated_pairs'] and jacc == fst['jaccard_evals']
+    assert sorted(edges) == want_edges
+    # the merge: union (k, label_g[k]) over every shard g, on one context's forest
+    m = _lib.Context(0)
+    m.load_csr(csr, thr)
+    m.components()                       # no query: every read its own root
+    m.union_pairs(None, np.concatenate(labels), W * csr.n_reads, on_device=False)
+    m.finalize_labels()
+    np.testing.assert_array_equal(m.labels(), want_labels)
+    m.close()
+    full.close()
+    # the CPU restatement's counts (all cores, E*)
+    cnt = np.diff(csr.read_off)
+    oc = O.OracleCSR(csr.read_off, csr.iv_chrom, csr.iv_start, csr.iv_end, csr.iv_aln,
+                     np.repeat(csr.read_qlen2, cnt), np.repeat(csr.read_nal, cnt), csr.data_pos)
+    oct_ = O.count_threads(oc, nthreads=min(16, os.cpu_count() or 1))
+    assert (oct_['evaluated_pairs'], oct_['jaccard_evals'], oct_['n_edges']) == (pairs, jacc, len(edges))
+
+
+@pytest.mark.slow
+def test_config5_10m_capped_sample_vs_oracle():
+    with open(os.path.join(GOLDEN, 'cfg5', 'sample50k_capped.json')) as fh:
+        meta = json.load(fh)
+    z = np.load(os.path.join(GOLDEN, 'cfg5', 'sample50k_capped.npz'))
+    s = synth.generate(meta['reads'], meta['lmax'], meta['seed'], dist=meta['dist'])
+    csr = s.interval_data().csr()
+    del s
+    assert csr.n_intervals == meta['n_intervals']
+    S = meta['sample']
+    ctx = _lib.Context(0)
+    ctx.load_csr(csr, fold_overlap_threshold(csr.iv_aln, 0.8))
+    ctx.reserve_edges(12 * csr.n_reads)
+    ctx.reserve_deferred(64 << 20)
+    ctx.build_index()
+    st = ctx.run_query(1 - 0.04, 1 - 0.25, pass_table(CUTS))
+    assert st['max_fwd'] > 10                               # the cap binds at this density
+    cap = ctx.apply_edge_cap(10)
+    assert cap['applied'] == 1 and cap['dropped'] > 0
+    ne = ctx.stats()['n_edges']
+    a, b, I, U = ctx.edges(ne)
+    own = a < S                                              # edges formed in the loops of reads < S
+    got = sorted(zip(a[own].tolist(), b[own].tolist(), I[own].tolist(), U[own].tolist()))
+    want = sorted(zip(z['a'].tolist(), z['b'].tolist(), z['I'].tolist(), z['U'].tolist()))
+    assert len(got) == len(want) == meta['n_edges']
+    assert got == want
+    np.testing.assert_array_equal(ctx.fwd_degree()[:S], z['fwd'])
+    ctx.components()
+    lab = ctx.labels()
+    assert lab.shape == (csr.n_reads,) and np.all(lab <= np.arange(csr.n_reads))
+    ctx.close()

@@ -150,6 +150,21 @@ def test_query_interval_trees_edges_match_reference(name):
     assert [sorted(c) for c in cluster.get_subgraphs(G)] == fx.stage(name)['components']
 
 
+@pytest.mark.parametrize('name', ['mixed_2k_l8', 'capbind_1500'])
+def test_reference_item_list_drops_in(name):
+    """build_interval_trees / query_interval_trees given the reference's prepare_data output (a
+    list of IntervalItem) return the same match set and components as given IntervalData."""
+    data, _, kw = host_prepare(name)
+    cut = [float(x) for x in kw['jaccard_cutoffs'].split(',')]
+    args = (kw['overlap'], cut, 10, kw['qlen_diff'], kw['n_alignment_diff'])
+    m1, G1 = cluster.query_interval_trees(cluster.build_interval_trees(data), data, *args)
+    items = list(data)
+    m2, G2 = cluster.query_interval_trees(cluster.build_interval_trees(items), items, *args)
+    assert sorted(map(tuple, m1.itertuples(index=False))) == sorted(map(tuple, m2.itertuples(index=False)))
+    assert [sorted(c) for c in cluster.get_subgraphs(G1)] == [sorted(c) for c in cluster.get_subgraphs(G2)]
+    assert sorted(map(tuple, m2.itertuples(index=False))) == sorted(map(tuple, fx.stage(name)['edges']))
+
+
 def test_capbind_device_equals_uncapped_oracle(ctx):
     data, _, _ = host_prepare('capbind_1500')
     csr = data.csr()

@@ -84,3 +84,20 @@ def test_pandas_sort_equivalence_on_ties():
         s = rng.integers(0, max(2, n // 7), size=n)
         df = pd.DataFrame({'start': s})
         np.testing.assert_array_equal(df.sort_values('start').index.to_numpy(), prep.data_order(s))
+
+
+def test_interval_data_from_reference_items_round_trips():
+    """build_interval_trees / query_interval_trees accept the reference's prepare_data output (a
+    list of IntervalItem): its columns, ranks and CSR equal those of the columnar data."""
+    from fslr_amd import synth
+    from fslr_amd.prep import IntervalData
+    data = synth.generate(3000, 8, 5).interval_data()
+    items = list(data)
+    back = IntervalData.from_items(items)
+    for f in ('chrom', 'start', 'end', 'aln_size', 'n_alignments', 'qlen2', 'middle'):
+        np.testing.assert_array_equal(getattr(back, f), getattr(data, f))
+    assert [back.qnames[c] for c in back.qcode] == [data.qnames[c] for c in data.qcode]
+    a, b = back.csr(), data.csr()
+    for f in ('read_off', 'read_qlen2', 'read_nal', 'iv_chrom', 'iv_start', 'iv_end', 'iv_aln', 'data_pos'):
+        np.testing.assert_array_equal(getattr(a, f), getattr(b, f))
+    assert list(back.qnames[a.read_qcode]) == list(data.qnames[b.read_qcode])
