@@ -71,6 +71,9 @@ def parse():
     ap.add_argument('--lmax', type=int, default=16)
     ap.add_argument('--seed', type=int, default=11)
     ap.add_argument('--dist', default='uniform')
+    ap.add_argument('--engine', default='auto', choices=['auto', 'walk', 'sweep'],
+                    help='pair engine of the timed step (fslr_hip.h FSLR_ENGINE_*); the walk engine always runs '
+                         'once before timing to count the Jaccard-evaluated pairs of the input')
     ap.add_argument('--cpu-sample-stride', type=int, default=16,
                     help='single-thread CPU baseline: query reads of every k-th 64-rank block (0 = skip the '
                          'CPU baseline)')
@@ -147,12 +150,20 @@ def main():
         if world > 1:
             ctx.query_shard(qcut, ncut, pt, rank, world)      # balanced rank blocks (fslr_query_shard)
         else:
-            ctx.query(qcut, ncut, pt, 10)
+            ctx.query(qcut, ncut, pt, 10, engine=args.engine)
             ctx.apply_edge_cap(10)                            # cluster.py:223-224 (no-op unless it binds)
         ctx.components()
         if merge is not None:
             merge()
 
+    # the input's unit count: the walk engine dedupes partners (the reference's seen-set) and counts
+    # the pairs whose predicate is evaluated; the sweep evaluates the same pairs without counting them
+    counted = None
+    if world == 1:
+        ctx.build_index()
+        counted = ctx.run_query(qcut, ncut, pt, 10, engine='walk')
+        walk_edges = sorted(zip(*[x.tolist() for x in ctx.edges(counted['n_edges'])]))
+        walk_fwd = ctx.fwd_degree()
     # warmup (also sizes the edge buffer)
     for w in range(max(1, args.warmup)):
         step()
@@ -162,6 +173,15 @@ def main():
                 ctx.reserve_edges(st['n_edges'] + 4096)
     torch.cuda.synchronize()
     st = ctx.stats()
+    engine = st['engine']
+    if counted is not None and engine != 'walk':
+        ctx.query(qcut, ncut, pt, 10, engine=args.engine)
+        se = ctx.stats()
+        same = (sorted(zip(*[x.tolist() for x in ctx.edges(se['n_edges'])])) == walk_edges and
+                bool(np.array_equal(ctx.fwd_degree(), walk_fwd)))
+        if not same:
+            raise SystemExit(f'{engine} engine differs from the walk engine on this input')
+        log(f'[rank 0] {engine} engine: edges and forward degrees identical to the walk engine')
 
     # timed region
     if dist:
@@ -183,7 +203,8 @@ def main():
     q_ivls = int(np.diff(csr.read_off)[own].sum())
     algo_bytes = (B_WALK * st['walked_records'] + B_READ * q_reads + B_IVL * q_ivls + B_EDGE * st['n_edges'] +
                   B_DEFER * st['deferred'])
-    tot = torch.tensor([elapsed, float(st['evaluated_pairs']), float(st['jaccard_evals']), float(st['n_edges']),
+    cs = counted if counted is not None else st        # the walk engine's counts of this input
+    tot = torch.tensor([elapsed, float(cs['evaluated_pairs']), float(cs['jaccard_evals']), float(st['n_edges']),
                         float(st['max_fwd'])], dtype=torch.float64, device=dev if backend == 'nccl' else 'cpu')
     if dist:
         t_max = tot[:1].clone()

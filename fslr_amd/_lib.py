@@ -13,12 +13,15 @@ import numpy as np
 
 LIB_PATH = os.environ.get('FSLR_LIB') or os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libfslr_hip.so')
 
-ABI_VERSION = 2          # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
+ABI_VERSION = 3          # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
 FSLR_OK, FSLR_ERR_ZERO_DIVISION, FSLR_ERR_INVALID, FSLR_ERR_HIP, FSLR_ERR_NOMEM, FSLR_ERR_STATE = range(6)
 FSLR_MAX_L = 64
 FSLR_MAX_READS = 1 << 25
 FSLR_THR_ZERO_ALN = -(1 << 31)
 PASS_STRIDE = 2 * FSLR_MAX_L
+# pair engines (fslr_params.flags & 3, include/fslr_hip.h)
+ENGINES = {'auto': 0, 'walk': 1, 'sweep': 2}
+ENGINE_NAMES = {1: 'walk', 2: 'sweep'}
 
 # every symbol include/fslr_hip.h declares (checked by tests/test_abi.py)
 EXPORTED = ['fslr_abi_version', 'fslr_last_error', 'fslr_ctx_create', 'fslr_ctx_destroy', 'fslr_set_profiling',
@@ -58,10 +61,13 @@ class QueryStats(ctypes.Structure):
                 ('gather_pairs', ctypes.c_int64), ('match_entries', ctypes.c_int64),
                 ('matched_pairs', ctypes.c_int64), ('deferred', ctypes.c_int64),
                 ('deferred_capacity', ctypes.c_int64), ('edge_capacity', ctypes.c_int64),
-                ('walked_records', ctypes.c_int64)]
+                ('walked_records', ctypes.c_int64), ('engine', ctypes.c_int32), ('overflow_flags', ctypes.c_int32),
+                ('pair_tests', ctypes.c_int64), ('entry_capacity', ctypes.c_int64)]
 
     def as_dict(self):
-        return {f: getattr(self, f) for f, _ in self._fields_}
+        d = {f: getattr(self, f) for f, _ in self._fields_}
+        d['engine'] = ENGINE_NAMES.get(d['engine'], d['engine'])
+        return d
 
 
 class CapStats(ctypes.Structure):
@@ -74,7 +80,8 @@ class CapStats(ctypes.Structure):
 
 class Timings(ctypes.Structure):
     _fields_ = [('index_ms', ctypes.c_float), ('query_ms', ctypes.c_float), ('components_ms', ctypes.c_float),
-                ('total_ms', ctypes.c_float), ('pair_kernel_ms', ctypes.c_float)]
+                ('total_ms', ctypes.c_float), ('pair_kernel_ms', ctypes.c_float), ('sweep_count_ms', ctypes.c_float),
+                ('sweep_emit_ms', ctypes.c_float), ('sweep_sort_ms', ctypes.c_float), ('sweep_pairs_ms', ctypes.c_float)]
 
     def as_dict(self):
         return {f: float(getattr(self, f)) for f, _ in self._fields_}
@@ -205,17 +212,19 @@ class Context:
         self.edge_capacity = max(self.edge_capacity, int(cap))
 
     # -- compute (async) ------------------------------------------------------------------
-    def _params(self, qlen_cut, nal_cut, pass_table, edge_threshold):
+    def _params(self, qlen_cut, nal_cut, pass_table, edge_threshold, engine='auto'):
         pt = np.ascontiguousarray(pass_table, dtype=np.uint8)
         assert pt.size == FSLR_MAX_L * PASS_STRIDE
         self._keep = (pt,)
-        return Params(float(qlen_cut), float(nal_cut), _ptr(pt), int(edge_threshold), 0)
+        return Params(float(qlen_cut), float(nal_cut), _ptr(pt), int(edge_threshold), ENGINES[engine])
 
     def build_index(self):
         self._check(self._L.fslr_build_index(self._h))
 
-    def query(self, qlen_cut, nal_cut, pass_table, edge_threshold=10, a_begin=0, a_end=None):
-        p = self._params(qlen_cut, nal_cut, pass_table, edge_threshold)
+    def query(self, qlen_cut, nal_cut, pass_table, edge_threshold=10, a_begin=0, a_end=None, engine='auto'):
+        """``engine``: 'auto' (the sweep when the input allows it and the query covers every read),
+        'walk' (counts evaluated_pairs / jaccard_evals) or 'sweep' (fslr_hip.h FSLR_ENGINE_*)."""
+        p = self._params(qlen_cut, nal_cut, pass_table, edge_threshold, engine)
         a_end = self.n_reads if a_end is None else a_end
         self._check(self._L.fslr_query(self._h, ctypes.byref(p), int(a_begin), int(a_end)))
 
@@ -237,8 +246,8 @@ class Context:
     def components(self):
         self._check(self._L.fslr_components(self._h))
 
-    def run(self, qlen_cut, nal_cut, pass_table, edge_threshold=10):
-        p = self._params(qlen_cut, nal_cut, pass_table, edge_threshold)
+    def run(self, qlen_cut, nal_cut, pass_table, edge_threshold=10, engine='auto'):
+        p = self._params(qlen_cut, nal_cut, pass_table, edge_threshold, engine)
         self._check(self._L.fslr_run(self._h, ctypes.byref(p)))
 
     def sync(self):
@@ -258,12 +267,17 @@ class Context:
         self._check(rc)
         return s.as_dict()
 
-    def run_query(self, qlen_cut, nal_cut, pass_table, edge_threshold=10, a_begin=0, a_end=None) -> dict:
-        """query + stats, growing the edge / deferred buffers and rerunning on overflow."""
+    def run_query(self, qlen_cut, nal_cut, pass_table, edge_threshold=10, a_begin=0, a_end=None,
+                  engine='auto') -> dict:
+        """query + stats, growing the edge / deferred buffers and rerunning on overflow (and with the
+        walk engine if the sweep's per-read partner table overflowed)."""
         while True:
-            self.query(qlen_cut, nal_cut, pass_table, edge_threshold, a_begin, a_end)
+            self.query(qlen_cut, nal_cut, pass_table, edge_threshold, a_begin, a_end, engine)
             st = self.stats(check=False)
             grow = False
+            if st['overflow_flags'] & 4:
+                engine = 'walk'
+                grow = True
             if st['n_edges'] > st['edge_capacity']:
                 self.reserve_edges(int(st['n_edges'] * 1.25) + 4096)
                 grow = True

@@ -60,6 +60,24 @@ int ensure_capacity(fslr_ctx* c, int64_t n, int64_t ni, int n_chroms) {
   return FSLR_OK;
 }
 
+// the sweep's match-entry buffers and their grouping-sort scratch (grow only)
+int reserve_entries(fslr_ctx* c, int64_t capacity) {
+  if (capacity <= c->ent_cap) return FSLR_OK;
+  if (capacity >= (int64_t(1) << 31)) return fail(c, FSLR_ERR_NOMEM, "more than 2^31 match entries");
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  int rc;
+  if ((rc = dalloc(c, &c->ent, capacity)) || (rc = dalloc(c, &c->ent_sorted, capacity))) return rc;
+  const size_t need = sweep_temp_bytes(capacity, std::max<int64_t>(c->ni, 64), c->stream);
+  if (need > c->sweep_temp_bytes) {
+    if (c->sweep_temp) (void)hipFree(c->sweep_temp);
+    c->sweep_temp = nullptr;
+    HIP_TRY(c, hipMalloc(&c->sweep_temp, need));
+    c->sweep_temp_bytes = need;
+  }
+  c->ent_cap = capacity;
+  return FSLR_OK;
+}
+
 int thr_mode_of(const int32_t* thr, int64_t ni) {
   for (int64_t k = 0; k < ni; ++k)
     if (thr[k] != FSLR_THR_ZERO_ALN && thr[k] < 1) return 1;
@@ -105,12 +123,13 @@ void fslr_ctx_destroy(fslr_ctx* c) {
                   c->crange, c->keys,   c->keys2,   c->vals,    c->vals2,   c->endkey,  c->pmaxkey,
                   c->temp,   c->umax,   c->edges,   c->edge_iu, c->fwd,     c->parent,  c->counters,
                   c->errw,   c->thr_tmp, c->defer,   c->dchrom,  c->drec,    c->lbounds, c->diag, c->wstat,
-                  c->dgate,  c->chist,  c->heavy};
+                  c->dgate,  c->chist,  c->heavy, c->ent, c->ent_sorted, c->sweep_temp, c->sw_tile, c->sw_total, c->sw_wstat};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->ev_ok) {
     for (auto& e : c->ev) (void)hipEventDestroy(e);
     for (auto& e : c->kev) (void)hipEventDestroy(e);
+    for (auto& e : c->sw_ev) (void)hipEventDestroy(e);
   }
   if (c->own_stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -123,6 +142,7 @@ int fslr_set_profiling(fslr_ctx* c, int enable) {
     for (auto& e : c->ev) HIP_TRY(c, hipEventCreate(&e));
     c->kev.assign(2 * fslr_ctx::kKernRing, nullptr);
     for (auto& e : c->kev) HIP_TRY(c, hipEventCreate(&e));
+    for (auto& e : c->sw_ev) HIP_TRY(c, hipEventCreate(&e));
     c->ev_ok = true;
   }
   c->profiling = enable != 0;
@@ -223,6 +243,7 @@ int fslr_set_reads(fslr_ctx* c, const fslr_reads* r) {
   c->ni = ni;
   c->n_chroms = r->n_chroms;
   c->thr_mode = thr_mode_of(r->iv_thr, ni);
+  c->any_zero_aln = std::find(zero.begin(), zero.end(), 1) != zero.end();
   c->aln_zero_host.swap(zero);
   if (n) HIP_TRY(c, hipMemcpyAsync(c->rmeta, rm.data(), n * sizeof(int4), hipMemcpyHostToDevice, c->stream));
   if (ni) HIP_TRY(c, hipMemcpyAsync(c->iv, iv.data(), ni * sizeof(int4), hipMemcpyHostToDevice, c->stream));
@@ -336,6 +357,72 @@ int fslr_query_shard(fslr_ctx* c, const fslr_params* p, int32_t shard, int32_t n
   return query_impl(c, p, 0, c->n, shard, n_shards);
 }
 
+// The position-sweep engine (sweep.hip): count pass + tile scan, one sync to read the entry count
+// (the grouping sort is sized on the host; the entry buffer grows to fit), then the emit pass, the
+// grouping sort and the per-read pair evaluation.
+static int sweep_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_t a_end, hipEvent_t e0,
+                      hipEvent_t e1) {
+  const int64_t tiles = (c->ni + 63) / 64 + 1;
+  int rc;
+  if (tiles > c->sw_tiles) {
+    if ((rc = dalloc(c, &c->sw_tile, 2 * tiles))) return rc;
+    c->sw_tiles = tiles;
+    c->ent_cap = 0;                                  // re-size the scan scratch with the entries
+  }
+  if (!c->sw_total && (rc = dalloc(c, &c->sw_total, 2))) return rc;
+  if (!c->sw_wstat) {
+    const int w = sweep_max_waves();
+    if ((rc = dalloc(c, &c->sw_wstat, static_cast<size_t>(w) * 4))) return rc;
+    c->sw_wstat_waves = w;
+  }
+  if (c->ent_cap == 0 && (rc = reserve_entries(c, std::max<int64_t>(1 << 20, c->ni)))) return rc;
+  SweepArgs s;
+  s.rmeta = c->rmeta;
+  s.idx4 = c->idx4;
+  s.idx_gate = c->idx_gate;
+  s.rng_s = c->rng_s;
+  s.umax = c->umax;
+  s.ni = static_cast<int>(c->ni);
+  s.n_reads = static_cast<int>(c->n);
+  s.a_begin = static_cast<int>(a_begin);
+  s.a_end = static_cast<int>(a_end);
+  s.qlen_cut = p->qlen_cut;
+  s.nal_cut = p->nal_cut;
+  s.lb = c->lbounds;
+  s.tile_cnt = c->sw_tile;
+  s.tile_off = c->sw_tile + c->sw_tiles;
+  s.edges = c->edges;
+  s.edge_iu = c->edge_iu;
+  s.edge_cap = c->edge_cap;
+  s.fwd = c->fwd;
+  s.counters = c->counters;
+  s.err = c->errw;
+  s.wstat = c->sw_wstat;
+  s.wstat_waves = c->sw_wstat_waves;
+  for (int k = 0; k < 5; ++k) s.ev[k] = c->profiling ? c->sw_ev[k] : nullptr;
+  if (e0) s.ev[0] = nullptr;                        // the ring pair below brackets the count pass
+  s.temp = c->sweep_temp;
+  s.temp_bytes = c->sweep_temp_bytes;
+  if (e0) HIP_TRY(c, hipEventRecord(e0, c->stream));
+  if (c->profiling) HIP_TRY(c, hipEventRecord(c->sw_ev[0], c->stream));
+  HIP_TRY(c, launch_len_bounds(c->rmeta, 0, static_cast<int>(c->n), p->qlen_cut, p->nal_cut, c->lbounds, c->stream));
+  HIP_TRY(c, launch_sweep_count(s, c->sw_total, c->stream));
+  if (e1) HIP_TRY(c, hipEventRecord(e1, c->stream));
+  long long tot[2] = {0, 0};
+  HIP_TRY(c, hipMemcpyAsync(tot, c->sw_total, sizeof(tot), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  const int64_t n_ent = tot[0] + tot[1];
+  if (n_ent > c->ent_cap && (rc = reserve_entries(c, n_ent + (n_ent >> 3) + 4096))) return rc;
+  s.ent = c->ent;
+  s.ent_sorted = c->ent_sorted;
+  s.n_ent = n_ent;
+  s.temp = c->sweep_temp;
+  s.temp_bytes = c->sweep_temp_bytes;
+  HIP_TRY(c, launch_sweep_pairs(s, c->stream));
+  c->sw_ev_rec = c->profiling;
+  return FSLR_OK;
+}
+
 static int query_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_t a_end, int shard, int n_shards) {
   if (!c->index_built) return fail(c, FSLR_ERR_STATE, "fslr_build_index first");
   HIP_TRY(c, hipSetDevice(c->device));
@@ -411,8 +498,20 @@ static int query_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_
   c->last_qcut = p->qlen_cut;
   c->last_ncut = p->nal_cut;
   std::memset(&c->cap_stats, 0, sizeof(c->cap_stats));
+  const int want = p->flags & 3;
+  const bool sweep_ok = c->thr_mode == 0 && !c->any_zero_aln && n_shards == 1;
+  if (want == FSLR_ENGINE_SWEEP && !sweep_ok)
+    return fail(c, FSLR_ERR_INVALID, "the sweep engine needs overlap thresholds >= 1, no aln_size == 0 interval "
+                                     "and one query shard");
+  const bool sweep = want == FSLR_ENGINE_SWEEP || (want == FSLR_ENGINE_AUTO && sweep_ok && c->last_full);
+  c->last_engine = sweep ? FSLR_ENGINE_SWEEP : FSLR_ENGINE_WALK;
   if (c->profiling) HIP_TRY(c, hipEventRecord(c->ev[2], c->stream));
-  HIP_TRY(c, launch_query(g, c->thr_mode, c->stream));
+  if (sweep) {
+    int rc = sweep_impl(c, p, a_begin, a_end, g.ev_k0, g.ev_k1);
+    if (rc) return rc;
+  } else {
+    HIP_TRY(c, launch_query(g, c->thr_mode, c->stream));
+  }
   if (c->profiling) HIP_TRY(c, hipEventRecord(c->ev[3], c->stream));
   c->t_query_rec = c->profiling;
   c->t_kernel_rec = c->profiling && c->n > 0 && a_end > a_begin;
@@ -492,6 +591,12 @@ int fslr_read_stats(fslr_ctx* c, fslr_query_stats* out) {
   out->deferred = static_cast<int64_t>(cnt[kDeferCount]);
   out->deferred_capacity = c->defer_cap;
   out->edge_capacity = c->edge_cap;
+  out->engine = c->last_engine;
+  out->overflow_flags = ew[kErrOverflow];
+  out->pair_tests = static_cast<int64_t>(cnt[kSwTests]);
+  out->entry_capacity = c->ent_cap;
+  if (c->last_engine == FSLR_ENGINE_SWEEP)
+    out->evaluated_pairs = out->jaccard_evals = -1;   // the sweep has no seen-set (fslr_hip.h)
   out->error = ew[0];
   out->err_a = ew[1];
   out->err_b = ew[2];
@@ -502,6 +607,8 @@ int fslr_read_stats(fslr_ctx* c, fslr_query_stats* out) {
   }
   if (out->deferred > c->defer_cap) return fail(c, FSLR_ERR_STATE, "deferred list overflowed; reserve and rerun");
   if (out->n_edges > c->edge_cap) return fail(c, FSLR_ERR_STATE, "edge buffer overflowed; reserve and rerun");
+  if (ew[kErrOverflow] & 4)
+    return fail(c, FSLR_ERR_STATE, "sweep partner table overflowed; rerun with FSLR_ENGINE_WALK");
   return FSLR_OK;
 }
 
@@ -518,6 +625,12 @@ int fslr_get_timings(fslr_ctx* c, fslr_timings* out) {
     HIP_TRY(c, hipEventElapsedTime(&out->pair_kernel_ms, c->kev[2 * slot], c->kev[2 * slot + 1]));
   }
   if (c->t_comp_rec) HIP_TRY(c, hipEventElapsedTime(&out->components_ms, c->ev[4], c->ev[5]));
+  if (c->sw_ev_rec && c->t_query_rec && c->last_engine == FSLR_ENGINE_SWEEP) {
+    HIP_TRY(c, hipEventElapsedTime(&out->sweep_count_ms, c->sw_ev[0], c->sw_ev[1]));
+    HIP_TRY(c, hipEventElapsedTime(&out->sweep_emit_ms, c->sw_ev[2], c->sw_ev[3]));
+    HIP_TRY(c, hipEventElapsedTime(&out->sweep_sort_ms, c->sw_ev[3], c->sw_ev[4]));
+    HIP_TRY(c, hipEventElapsedTime(&out->sweep_pairs_ms, c->sw_ev[4], c->ev[3]));
+  }
   if (c->t_index_rec && c->t_comp_rec) HIP_TRY(c, hipEventElapsedTime(&out->total_ms, c->ev[0], c->ev[5]));
   return FSLR_OK;
 }

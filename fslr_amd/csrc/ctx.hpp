@@ -56,6 +56,21 @@ struct fslr_ctx {
   int wstat_waves = 0;
   unsigned long long* diag = nullptr;        // FSLR_SECTION_PROF builds: per-read timing of the pair kernel
   int* errw = nullptr;     // [0..2] error, [3] max_fwd
+  // position-sweep engine (sweep.hip)
+  long long* sw_tile = nullptr;             // [2 x tiles]: entries per 64-position tile, their exclusive scan
+  long long* sw_total = nullptr;            // [2] last tile's offset and count
+  int64_t sw_tiles = 0;
+  unsigned long long* sw_wstat = nullptr;   // per-wave statistics slots of the sweep kernels
+  int sw_wstat_waves = 0;
+  hipEvent_t sw_ev[5] = {};                 // (profiling) count | scan | emit | sort | pairs
+  bool sw_ev_rec = false;
+  unsigned long long* ent = nullptr;        // match entries, tile order
+  unsigned long long* ent_sorted = nullptr; // grouped by read A
+  int64_t ent_cap = 0;
+  void* sweep_temp = nullptr;
+  size_t sweep_temp_bytes = 0;
+  bool any_zero_aln = false;                // an aln_size == 0 interval: the walk engine replays it
+  int last_engine = FSLR_ENGINE_WALK;
   int* thr_tmp = nullptr;
   int64_t cap_n = 0, cap_ni = 0, cap_chroms = 0;
   std::vector<int> umax_host, umax_dev_copy;   // dev copy: what c->umax holds

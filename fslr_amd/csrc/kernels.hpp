@@ -43,7 +43,8 @@ enum Counter { kEdgeCount = 0,          // atomic (own 128-B line)
                kQueueBase = 80,         // pair kernel work queues: 8 counters, one 128-B line each
                kQueueStride = 16,
                kQueueBase2 = kQueueBase + 8 * kQueueStride,   // the partitioned launch's queues
-               kNumCounters = kQueueBase2 + 8 * kQueueStride };
+               kSwTests = kQueueBase2 + 8 * kQueueStride,     // sweep: interval pairs tested
+               kNumCounters = kSwTests + 16 };
 // per-wave statistics of query_kernel: fields 0..8 (sum, except kWsMaxFwd: max; kWsWalked: index
 // records walked, every pass counted), then (section-
 // timing builds) 8 section sums, slowest read cycles (max), its rank, wave cycles max / min,
@@ -138,8 +139,45 @@ struct QueryArgs {
 };
 // thr_mode: 0 = every non-sentinel threshold >= 1 (fast match), 1 = general encoding
 hipError_t launch_query(const QueryArgs& a, int thr_mode, hipStream_t s);
+// per read a in [a0, a1): lb[a] = the length gate as integer ranges {qlo, qhi, nlo, nhi}
+hipError_t launch_len_bounds(const int4* rmeta, int a0, int a1, double qcut, double ncut, int4* lb, hipStream_t s);
 // waves of the largest query_kernel grid (the size of QueryArgs::wstat)
 int query_max_waves();
+
+// ---- position sweep (sweep.hip) ------------------------------------------------------------
+struct SweepArgs {
+  const int4* rmeta;
+  const int4* idx4;
+  const int2* idx_gate;
+  const int2* rng_s;
+  const int* umax;
+  int ni, n_reads;
+  int a_begin, a_end;                 // reads whose pairs (as the lower rank A) are evaluated
+  double qlen_cut, nal_cut;
+  int4* lb;                           // [n_reads] length-gate ranges (launch_len_bounds)
+  long long* tile_cnt;                // [ceil(ni / 64)] match entries of each 64-position tile (count pass)
+  long long* tile_off;                // its exclusive scan: where the emit pass writes the tile's entries
+  unsigned long long* ent;            // [n_ent] match entries A << 39 | B << 14 | i << 7 | j, tile order
+  unsigned long long* ent_sorted;     // [n_ent] grouped by A
+  long long n_ent;                    // (emit / pairs) entries of the count pass
+  void* temp;                         // hipcub scratch (tile scan, grouping sort)
+  size_t temp_bytes;
+  int2* edges;
+  unsigned short* edge_iu;
+  long long edge_cap;
+  int* fwd;
+  unsigned long long* counters;
+  int* err;
+  unsigned long long* wstat;          // per-wave statistics slots [waves x 4] (no contended atomics)
+  int wstat_waves;
+  hipEvent_t ev[5];                   // (profiling) count | scan | emit | sort | pairs boundaries, or null
+};
+size_t sweep_temp_bytes(long long ent_cap, long long ni, hipStream_t s);
+int sweep_max_waves();
+// count pass + tile scan; *total_dev receives the entry count (device memory, read after a sync)
+hipError_t launch_sweep_count(const SweepArgs& a, long long* total_dev, hipStream_t s);
+// emit pass + grouping sort + per-read pair evaluation (a.n_ent from the count pass)
+hipError_t launch_sweep_pairs(const SweepArgs& a, hipStream_t s);
 
 // ---- edge-cap replay (cap.hip) --------------------------------------------------------------
 // per listed read: upper bound of its interval hits (sum over its intervals of the scan range)

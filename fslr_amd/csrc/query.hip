@@ -29,6 +29,7 @@
 #include <type_traits>
 
 #include "kernels.hpp"
+#include "wave.hpp"
 
 namespace fslr {
 namespace {
@@ -69,75 +70,9 @@ constexpr int kSections = 8;
 #define SEC_ADD(k, t0) (void)0
 #endif
 
-__device__ __forceinline__ int lane_id() { return static_cast<int>(__lane_id()); }
-
-__device__ __forceinline__ int mbcnt(unsigned long long m) {
-  return __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(m >> 32),
-                                   __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(m), 0u));
-}
-
-// wave-uniform loads through the scalar cache (constant address space => s_load)
-typedef const __attribute__((address_space(4))) int* const_i32_ptr;
-__device__ __forceinline__ int2 sload2(const void* p, int i) {
-  const_i32_ptr q = (const_i32_ptr)(p) + 2 * i;
-  return make_int2(q[0], q[1]);
-}
-__device__ __forceinline__ int4 sload4(const void* p, int i) {
-  const_i32_ptr q = (const_i32_ptr)(p) + 4 * i;
-  return make_int4(q[0], q[1], q[2], q[3]);
-}
-
-// three consecutive dwords of a 16-B record, starting at dword `first`
-__device__ __forceinline__ int3 load3(const int4* p, int k, int first) {
-  const int* q = reinterpret_cast<const int*>(p + k) + first;
-  return make_int3(q[0], q[1], q[2]);
-}
-
-// inclusive wave64 prefix sum on DPP: row_shr 1/2/4/8 inside each row of 16 lanes, then
-// row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3) — six VALU ops, no LDS round trips
-__device__ __forceinline__ int wave_incl_scan(int x) {
-  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);
-  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);
-  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);
-  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);
-  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);
-  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);
-  return x;
-}
-
-__device__ __forceinline__ int rdl(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
-
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 // partner partition of read B (a multiplier independent of the hash slot's)
 __device__ __forceinline__ int part_of(int B, int npass) {
   return static_cast<int>(((static_cast<unsigned>(B) * 0x85EBCA6Bu) >> 8) % static_cast<unsigned>(npass));
-}
-
-// The gate of one query read as integer ranges (exact: IEEE division is monotone, so the
-// reference's double test fl(min/max) >= cut, cluster.py:178-183, holds on a contiguous range of
-// the partner's value).  {lo, hi}: partner values x in [lo, hi] pass; lo < 0 marks v == 0, where
-// x == 0 raises ZeroDivisionError and the passing range is [1, hi].
-__device__ int2 ratio_range(int v, double cut) {
-  constexpr int kTop = 0x7FFFFFFF;
-  if (v == 0) return make_int2(-1, 0.0 >= cut ? kTop : 0);
-  if (!(1.0 >= cut)) return make_int2(1, 0);
-  const double dv = static_cast<double>(v);
-  if (!(cut > 0.0)) return make_int2(0, kTop);      // every ratio >= 0 >= cut
-  // smallest x <= v with fl(x / v) >= cut: start at the estimate, then walk with the exact test
-  // (monotone, so the walks end at the true bound whatever the estimate; here they take 1-2 steps)
-  int lo = static_cast<int>(fmin(fmax(ceil(cut * dv), 0.0), dv));
-  while (lo > 0 && static_cast<double>(lo - 1) / dv >= cut) --lo;
-  while (!(static_cast<double>(lo) / dv >= cut)) ++lo;
-  // largest x >= v with fl(v / x) >= cut
-  int hi = static_cast<int>(fmin(fmax(floor(dv / cut), dv), static_cast<double>(kTop)));
-  while (hi < kTop && dv / static_cast<double>(hi + 1) >= cut) ++hi;
-  while (!(dv / static_cast<double>(hi) >= cut)) --hi;
-  return make_int2(lo, hi);
 }
 
 __global__ void k_len_bounds(const int4* __restrict__ rmeta, int a0, int a1, double qcut, double ncut,
@@ -148,50 +83,6 @@ __global__ void k_len_bounds(const int4* __restrict__ rmeta, int a0, int a1, dou
     lb[a] = make_int4(q.x, q.y, n.x, n.y);
   }
 }
-
-__device__ __forceinline__ void raise_zd(int* err, bool zd, int a, int b) {
-  if (zd && atomicCAS(err, 0, FSLR_ERR_ZERO_DIVISION) == 0) {
-    err[1] = a;
-    err[2] = b;
-  }
-}
-
-// Wave-level edge staging in LDS (64-edge flushes).  `ES` holds a << 39 | B << 14 | I << 7 | U.
-struct EdgeStage {
-  unsigned long long* ES;
-  int n;
-  __device__ void flush(const QueryArgs& g, int nb, int lane) {
-    wave_lds_sync();
-    const bool act = lane < nb;
-    const unsigned long long e = act ? ES[lane] : 0ull;
-    const int rem = n - nb;
-    const unsigned long long mv = lane < rem ? ES[nb + lane] : 0ull;
-    wave_lds_sync();
-    if (lane < rem) ES[lane] = mv;
-    n = rem;
-    unsigned long long base = 0;
-    if (lane == 0) base = atomicAdd(&g.counters[kEdgeCount], static_cast<unsigned long long>(nb));
-    base = __shfl(base, 0);
-    const long long k = static_cast<long long>(base) + lane;
-    if (act && k < g.edge_cap) {
-      g.edges[k] = make_int2(static_cast<int>(e >> 39), static_cast<int>((e >> 14) & kBMask));
-      g.edge_iu[k] = static_cast<unsigned short>(((e >> 7) & 127u) | ((e & 127u) << 8));
-    }
-  }
-  // stage the lanes' edges; returns the number staged
-  __device__ int put(const QueryArgs& g, bool edge, int a, int B, int I, int U, int lane) {
-    const unsigned long long em = __ballot(edge);
-    const int ne = __popcll(em);
-    if (ne) {
-      if (n + ne > kStageCap) flush(g, n, lane);
-      if (edge)
-        ES[n + mbcnt(em)] = (static_cast<unsigned long long>(a) << 39) | (static_cast<unsigned long long>(B) << 14) |
-                            (static_cast<unsigned long long>(I) << 7) | static_cast<unsigned long long>(U);
-      n += ne;
-    }
-    return ne;
-  }
-};
 
 // Deferred-list appends, staged in LDS like the edges.
 struct DeferStage {
@@ -244,6 +135,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
   unsigned* ML = ml_all[wv];
   unsigned short* MP = mp_all[wv];     // partners (hash slots) with at least one match, first-match order
   EdgeStage es{es_all[wv], 0};
+  const EdgeOut eo{g.edges, g.edge_iu, g.edge_cap, &g.counters[kEdgeCount]};
   DeferStage ds{dq_all[wv], 0};
   for (int k = lane; k < kHashSize; k += kWave) H[k] = 0u;
   unsigned epoch = 0;
@@ -606,7 +498,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
         }
         const int U = LA + LB - I;
         const bool pass = U <= __shfl(umax_v, max(I, 1) - 1);
-        fwdA += es.put(g, pass && need && I > 0, a, B, I, U, lane);
+        fwdA += es.put(eo, pass && need && I > 0, a, B, I, U, lane);
         ds.put(g, spill, a, B, 0, 0, kDefPair, lane);
       }
     }
@@ -653,7 +545,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
     my = my_next;
     rg = rg_next;
   }
-  if (es.n > 0) es.flush(g, es.n, lane);
+  if (es.n > 0) es.flush(eo, es.n, lane);
   if (ds.n > 0) ds.flush(g, ds.n, lane);
   SEC_ADD(7, t_wave);
   unsigned long long l_bytes = l_lb;
@@ -791,6 +683,7 @@ __global__ __launch_bounds__(256) void deferred_kernel(QueryArgs g) {
   __shared__ unsigned long long es_all[4][kStageCap];
   const int lane = lane_id();
   EdgeStage es{es_all[threadIdx.x >> 6], 0};
+  const EdgeOut eo{g.edges, g.edge_iu, g.edge_cap, &g.counters[kEdgeCount]};
   const long long n_all = static_cast<long long>(g.counters[kDeferCount]);
   if (n_all > g.defer_cap && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(g.err + kErrOverflow, 1);
   const long long n = min(n_all, g.defer_cap);
@@ -852,13 +745,13 @@ __global__ __launch_bounds__(256) void deferred_kernel(QueryArgs g) {
     const int U = LA + LB - I;
     const bool pass = U <= __shfl(umax_v, max(I, 1) - 1);
     const bool edge = pass && work && !zd && I > 0;
-    es.put(g, edge && lane == 0, a, B, I, U, lane);
+    es.put(eo, edge && lane == 0, a, B, I, U, lane);
     if (edge && lane == 0) {
       const int old = atomicAdd(&g.fwd[a], 1);
       atomicMax(g.err + 3, old + 1);
     }
   }
-  if (es.n > 0) es.flush(g, es.n, lane);
+  if (es.n > 0) es.flush(eo, es.n, lane);
   if (lane == 0) {
     if (w_bytes) atomicAdd(&g.counters[kAlgoBytes], w_bytes);
     if (w_eval) atomicAdd(&g.counters[kEval], w_eval);
@@ -887,6 +780,11 @@ int query_max_waves() {
   const int b = std::max(std::max(resident_blocks<0, false>(), resident_blocks<1, false>()),
                          std::max(resident_blocks<0, true>(), resident_blocks<1, true>()));
   return b * kWavesPerBlock;
+}
+
+hipError_t launch_len_bounds(const int4* rmeta, int a0, int a1, double qcut, double ncut, int4* lb, hipStream_t s) {
+  if (a1 > a0) k_len_bounds<<<grid_for(a1 - a0), 256, 0, s>>>(rmeta, a0, a1, qcut, ncut, lb);
+  return hipGetLastError();
 }
 
 hipError_t launch_query(const QueryArgs& a_in, int thr_mode, hipStream_t s) {

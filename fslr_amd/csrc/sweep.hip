@@ -1,0 +1,605 @@
+// sweep.hip — the position-sweep pair engine: the driver of query_interval_trees (cluster.py:187-227)
+// reorganised around the (chrom, start)-sorted index instead of the query reads.
+//
+// Every pair of end-inclusive overlapping intervals (the hits of superintervals' search_values,
+// cluster.py:201) is q < p in sorted order with p in q + 1 .. q + n_fwd(q) (kernels.hpp: rng_s), so
+// one forward sweep over the sorted positions meets each of them exactly once, in position order —
+// consecutive positions share their windows, so the index streams through L1/L2 once instead of
+// once per query read.  The rest of the reference's per-pair work is then:
+//   1. k_sweep: per overlapping interval pair of two different reads X != Y (A = min, B = max rank):
+//      the pair gate different_lengths_or_alignments (:178-183, the integer ranges of ratio_range),
+//      and calculate_overlap >= overlap (:133-136, folded thresholds: o >= max(thr)).  A pair that
+//      passes both is a match entry A << 39 | B << 14 | i << 7 | j (i, j: the intervals' indices in
+//      their reads' lists, cluster.py:189-191).  Two passes over 64-position tiles: the first counts
+//      each tile's entries, a scan places the tiles, the second writes them — no global atomics
+//      (one contended counter saturates near 90 returning atomics per microsecond).
+//   2. the entries are grouped by A (hipcub radix sort on A's bits only).
+//   3. k_sweep_pairs: per run of one read A, an LDS hash over its partners B collects each pair's
+//      match matrix as row / column masks; first-fit greedy (overall_jaccard_similarity, :152-161)
+//      is the entry count unless two entries share a row or a column, where the rows are walked in
+//      the reference's order (i ascending, lowest unused j).  Edge iff U <= umax[I - 1] (:216-219).
+// A pair with overlapping intervals but no match entry is evaluated too — its I is 0 — so the
+// edge set is the walk engine's E*, bit for bit.  The sweep does not count evaluated pairs (the
+// reference's seen-set size): that is the walk engine's job (query.hip), which the parity tests
+// and bench.py use for the counts.
+// Scope: thresholds >= 1 (overlap > 0) and no aln_size == 0 interval; other inputs take the walk
+// engine (capi.hip picks).
+#include <hipcub/hipcub.hpp>
+
+#include "fslr_hip.h"
+#include "kernels.hpp"
+#include "wave.hpp"
+
+namespace fslr {
+namespace {
+
+constexpr int kSwWaves = 4;
+constexpr int kSwBlock = kSwWaves * kWave;
+constexpr int kPairLimit = 160;            // long runs: insert while partners < limit (+64 per step < 256)
+constexpr int kPerPass = 80;               // entries per partner partition of a long run
+constexpr int kEdgeStage = 256;            // staged edges per wave
+constexpr int kWsFields = 4;               // per-wave statistics slots
+
+__device__ __forceinline__ unsigned long long pack_entry(int a, int b, int i, int j) {
+  return (static_cast<unsigned long long>(a) << 39) | (static_cast<unsigned long long>(b) << 14) |
+         (static_cast<unsigned long long>(i) << 7) | static_cast<unsigned long long>(j);
+}
+__device__ __forceinline__ int entry_a(unsigned long long e) { return static_cast<int>(e >> 39); }
+// lane masks: bits above / up to position h (0 <= h < 64)
+__device__ __forceinline__ unsigned long long above(int h) { return h >= 63 ? 0ull : (~0ull << (h + 1)); }
+__device__ __forceinline__ unsigned long long upto(int h) { return h >= 63 ? ~0ull : ((2ull << h) - 1); }
+
+// same multiplier as the walk engine's partner partitions
+__device__ __forceinline__ int part_of(int B, int npass) {
+  return static_cast<int>(((static_cast<unsigned>(B) * 0x85EBCA6Bu) >> 8) % static_cast<unsigned>(npass));
+}
+
+// ---- 1. the sweep -------------------------------------------------------------------------------
+// One wavefront per tile of 64 consecutive sorted positions (lane l holds q = q0 + l), tiles dealt
+// grid-stride over a resident grid.  The tile's forward ranges are flattened into an LDS map (item
+// r -> the lane whose range holds it), then walked 64 interval pairs per step, one per lane, the
+// next step's index records loaded while the current step is tested.  The q side of a pair comes
+// from LDS (written once per tile), the p side is the index record and gate word at p (a tile's
+// window is a few hundred consecutive positions, so these loads hit L1 / L2).  kEmit = false counts
+// the tile's entries (and the statistics); kEmit = true writes them at the tile's scanned offset.
+constexpr int kMapCap = 2048;              // items per map segment (a longer tile takes several)
+
+template <bool kEmit>
+__global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
+  __shared__ int4 qa_all[kSwWaves][kWave];     // {end, thr, tag, qlo}
+  __shared__ int4 qb_all[kSwWaves][kWave];     // {qhi, nlo, nhi, offv}
+  __shared__ unsigned char map_all[kSwWaves][kMapCap];
+  __shared__ unsigned long long st_all[kSwWaves][kEmit ? kWave : 1];
+  const int lane = lane_id();
+  const int wv = threadIdx.x >> 6;
+  int4* QA = qa_all[wv];
+  int4* QB = qb_all[wv];
+  unsigned char* MAP = map_all[wv];
+  unsigned long long* ST = st_all[wv];
+  unsigned long long w_tests = 0, w_hits = 0, w_ent = 0;
+  const int nt = (g.ni + kWave - 1) / kWave;
+  const int nw = gridDim.x * kSwWaves;
+  const int wid = blockIdx.x * kSwWaves + wv;
+  for (int tile = wid; tile < nt; tile += nw) {
+    const int q0 = tile * kWave;
+    const int q = q0 + lane;
+    const bool qv = q < g.ni;
+    const int qc = qv ? q : q0;
+    int4 rq = g.idx4[qc];
+    const int nf = qv ? g.rng_s[qc].x : 0;
+    const int4 lbq = g.lb[rq.w >> 6];            // the gate of q's read as integer ranges
+    const int pre = wave_incl_scan(nf);
+    const int ex = pre - nf;
+    const int T = rdl(pre, kWave - 1);
+    wave_lds_sync();
+    QA[lane] = make_int4(rq.y, rq.z, rq.w, lbq.x);
+    QB[lane] = make_int4(lbq.y, lbq.z, lbq.w, q + 1 - ex);   // item r of lane k is position r + offv_k
+    long long out = 0;                           // kEmit: next entry slot of this tile
+    if constexpr (kEmit) out = g.tile_off[tile];
+    int sn = 0, cnt = 0;                         // staged entries (kEmit) / entries of the tile
+    if constexpr (!kEmit) w_tests += static_cast<unsigned long long>(T);
+    for (int seg = 0; seg < T; seg += kMapCap) {
+      const int se = min(T, seg + kMapCap);
+      wave_lds_sync();
+      for (int r = max(ex, seg); r < min(pre, se); ++r) MAP[r - seg] = static_cast<unsigned char>(lane);
+      wave_lds_sync();
+      // step loads: the mapped lane's offset, then the p-side record and gate word
+      auto step_load = [&](int base, int& mi, int4& b4, int4& rp, int2& gp) {
+        const int r = base + lane;
+        mi = r < se ? MAP[r - seg] : 0;
+        b4 = QB[mi];
+        const int p = r < se ? r + b4.w : q0;
+        rp = g.idx4[p];
+        gp = g.idx_gate[p];
+      };
+      int mi_n, mi;
+      int4 b4_n, b4, rp_n, rp;
+      int2 gp_n, gp;
+      step_load(seg, mi_n, b4_n, rp_n, gp_n);
+      for (int base = seg; base < se; base += kWave) {
+        mi = mi_n;
+        b4 = b4_n;
+        rp = rp_n;
+        gp = gp_n;
+        if (base + kWave < se) step_load(base + kWave, mi_n, b4_n, rp_n, gp_n);
+        const bool valid = base + lane < se;
+        const int4 a4 = QA[mi];
+        const int X = a4.z >> 6, Y = rp.w >> 6;
+        const bool hit = valid && X != Y;
+        // calculate_overlap >= overlap for both intervals: start_p >= start_q, start_p <= end_q
+        const int o = min(a4.x, rp.y) - rp.x;
+        const bool match = o >= max(a4.y, rp.z);
+        // different_lengths_or_alignments: passes when either ratio is close (idx_gate word of p)
+        const int q2 = gp.x, n2 = gp.y & 0xFFFFFF;
+        const int qlo = a4.w, qhi = b4.x, nlo = b4.y, nhi = b4.z;
+        const bool pq = q2 >= (qlo < 0 ? 1 : qlo) && q2 <= qhi;
+        const bool zd = hit && ((qlo < 0 && q2 == 0) || (!pq && nlo < 0 && n2 == 0));
+        const bool lenok = pq || (n2 >= (nlo < 0 ? 1 : nlo) && n2 <= nhi);
+        const bool emit = hit && !zd && lenok && match;
+        const unsigned long long em = __ballot(emit);
+        const int ne = __popcll(em);
+        if constexpr (!kEmit) {
+          if (__ballot(zd)) raise_zd(g.err, zd, min(X, Y), max(X, Y));
+          w_hits += __popcll(__ballot(hit));
+          cnt += ne;
+        } else if (ne) {
+          if (sn + ne > kWave) {
+            wave_lds_sync();
+            if (lane < sn) g.ent[out + lane] = ST[lane];
+            out += sn;
+            sn = 0;
+            wave_lds_sync();
+          }
+          if (emit) {
+            const int iq = a4.z & 63, jp = rp.w & 63;
+            ST[sn + mbcnt(em)] = X < Y ? pack_entry(X, Y, iq, jp) : pack_entry(Y, X, jp, iq);
+          }
+          sn += ne;
+        }
+      }
+    }
+    if constexpr (kEmit) {
+      if (sn > 0) {
+        wave_lds_sync();
+        if (lane < sn) g.ent[out + lane] = ST[lane];
+      }
+    } else {
+      if (lane == 0) g.tile_cnt[tile] = cnt;
+      w_ent += static_cast<unsigned long long>(cnt);
+    }
+  }
+  if constexpr (!kEmit) {
+    // statistics: plain stores into this wave's slots, summed by k_sum_slots
+    const unsigned long long f = lane == 0 ? w_tests : lane == 1 ? w_hits : w_ent;
+    if (lane < 3) g.wstat[static_cast<long long>(wid) * kWsFields + lane] = f;
+  }
+}
+
+// Sum (fields 0..2) / max (field 3) of the per-wave slots [f0, f1) into counters / an err word.
+__global__ __launch_bounds__(256) void k_sum_slots(const unsigned long long* __restrict__ ws, int nwaves, int f0,
+                                                    int f1, int c0, int c1, int c2, unsigned long long* counters,
+                                                    int* err_max) {
+  __shared__ unsigned long long part[256][kWsFields];
+  unsigned long long acc[kWsFields] = {0, 0, 0, 0};
+  for (int w = threadIdx.x; w < nwaves; w += 256)
+    for (int f = f0; f < f1; ++f) {
+      const unsigned long long x = ws[static_cast<long long>(w) * kWsFields + f];
+      acc[f] = (f == 3) ? (acc[f] > x ? acc[f] : x) : acc[f] + x;
+    }
+  for (int f = 0; f < kWsFields; ++f) part[threadIdx.x][f] = acc[f];
+  __syncthreads();
+  if (threadIdx.x < kWsFields) {
+    const int f = threadIdx.x;
+    unsigned long long r = 0;
+    for (int t = 0; t < 256; ++t) r = f == 3 ? (r > part[t][f] ? r : part[t][f]) : r + part[t][f];
+    const int dst = f == 0 ? c0 : f == 1 ? c1 : c2;
+    if (f < 3 && f >= f0 && f < f1 && dst >= 0) counters[dst] += r;
+    if (f == 3 && f >= f0 && f < f1 && err_max) *err_max = max(*err_max, static_cast<int>(r));
+  }
+}
+
+// ---- 3. pairs from the entries grouped by A ------------------------------------------------------
+// Work item: a chunk of kChunk2 sorted entries; the runs (reads A) that start in it.  Whole runs are
+// staged in LDS a group of at most kStageE entries at a time and evaluated together: one LDS hash
+// over (run, B) collects every pair's entry count and row / column masks, then one lane per pair
+// decides it (I = count unless two entries share a row or a column, then first-fit in the reference's
+// order from the staged entries).  A run longer than the stage is evaluated alone, streamed from HBM,
+// in partner partitions (pass k takes the partners with part(B) == k).
+constexpr int kChunk2 = 128;
+constexpr int kStageE = 128;
+constexpr int kHash2 = 256;
+constexpr unsigned kEmpty = 0xFFFFFFFFu;
+
+__global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
+  __shared__ unsigned long long ste_all[kSwWaves][kStageE];   // staged entries of the group
+  __shared__ unsigned key_all[kSwWaves][kHash2];              // run << 24 | B (group) or B (long run)
+  __shared__ unsigned cnt_all[kSwWaves][kHash2];              // entry count | conflict << 31
+  __shared__ uint2 rm_all[kSwWaves][kHash2];                  // rows i of A used by the pair's entries
+  __shared__ uint2 cm_all[kSwWaves][kHash2];                  // columns j of B
+  __shared__ unsigned short mp_all[kSwWaves][kPairLimit + kWave];
+  __shared__ int runa_all[kSwWaves][kStageE];                 // per run of the group: A, L_A, edges formed
+  __shared__ int runl_all[kSwWaves][kStageE];
+  __shared__ int runf_all[kSwWaves][kStageE];
+  __shared__ uint2 rr_all[kSwWaves][kWave];                   // ordered path: row masks of one partner
+  __shared__ unsigned long long es_all[kSwWaves][kEdgeStage];
+  const int lane = lane_id();
+  const int wv = threadIdx.x >> 6;
+  unsigned long long* STE = ste_all[wv];
+  unsigned* KEY = key_all[wv];
+  unsigned* CNT = cnt_all[wv];
+  uint2* RM = rm_all[wv];
+  uint2* CM = cm_all[wv];
+  unsigned short* MP = mp_all[wv];
+  int* RUNA = runa_all[wv];
+  int* RUNL = runl_all[wv];
+  int* RUNF = runf_all[wv];
+  uint2* RR = rr_all[wv];
+  EdgeStageN<kEdgeStage> es{es_all[wv], 0};
+  const EdgeOut eo{g.edges, g.edge_iu, g.edge_cap, &g.counters[kEdgeCount]};
+  const int umax_v = g.umax[lane];
+  const long long n = g.n_ent;
+  const unsigned long long* E = g.ent_sorted;
+  const long long nchunks = (n + kChunk2 - 1) / kChunk2;
+  const long long nw = static_cast<long long>(gridDim.x) * kSwWaves;
+  const int wid = blockIdx.x * kSwWaves + wv;
+  const bool group_keys = g.n_reads < (1 << 24) - 1;     // run << 24 | B fits 32 bits
+  int w_maxfwd = 0;
+  unsigned long long w_pairs = 0;
+  auto a_at = [&](long long k) -> int {   // A of sorted entry k (wave-uniform, scalar cache)
+    const_i32_ptr p = (const_i32_ptr)(E + k);
+    return static_cast<int>(static_cast<unsigned>(p[1]) >> 7);
+  };
+  // first k in [k, lim) whose A differs from `a` (lim if none); lanes scan 64 entries per step
+  auto next_run = [&](long long k, long long lim, int a) -> long long {
+    for (; k < lim; k += kWave) {
+      const long long t = k + lane;
+      const bool diff = t < lim && entry_a(E[min(t, n - 1)]) != a;
+      const unsigned long long m = __ballot(diff);
+      if (m) return k + __builtin_ctzll(m);
+    }
+    return lim;
+  };
+  auto clear_hash = [&]() {
+    for (int t = lane; t < kHash2; t += kWave) KEY[t] = kEmpty;
+    wave_lds_sync();
+  };
+  // insert `key` (lanes with `mine`); returns the slot; isnew for the lane that created it
+  auto insert = [&](bool mine, unsigned key, unsigned hseed, bool& isnew) -> int {
+    unsigned h = (hseed * 2654435761u) >> 24;       // 8 bits: kHash2
+    isnew = false;
+    if (mine) {
+      while (true) {
+        unsigned cur = KEY[h];
+        if (cur == kEmpty) {
+          const unsigned old = atomicCAS(&KEY[h], kEmpty, key);
+          if (old == kEmpty) { isnew = true; break; }
+          cur = old;
+        }
+        if (cur == key) break;
+        h = (h + 1) & (kHash2 - 1);
+      }
+    }
+    return static_cast<int>(h);
+  };
+  // first-fit in the reference's order (cluster.py:152-161) from row masks in lanes i < LA
+  auto ordered_I = [&](int LA) -> int {
+    const uint2 rv = RR[lane];
+    unsigned used_lo = 0u, used_hi = 0u;
+    int Ic = 0;
+    for (int ii = 0; ii < LA; ++ii) {
+      const unsigned m_lo = static_cast<unsigned>(rdl(static_cast<int>(rv.x), ii)) & ~used_lo;
+      const unsigned m_hi = static_cast<unsigned>(rdl(static_cast<int>(rv.y), ii)) & ~used_hi;
+      if (m_lo) used_lo |= m_lo & (0u - m_lo);
+      else if (m_hi) used_hi |= m_hi & (0u - m_hi);
+      Ic += (m_lo | m_hi) != 0u;
+    }
+    return Ic;
+  };
+  // the pair's entry counts and masks (lanes with `mine`, slot h)
+  auto record = [&](bool mine, int h, int i, int j) {
+    if (mine) {
+      const unsigned bi = 1u << (i & 31), bj = 1u << (j & 31);
+      const unsigned oi = i < 32 ? atomicOr(&RM[h].x, bi) : atomicOr(&RM[h].y, bi);
+      const unsigned oj = j < 32 ? atomicOr(&CM[h].x, bj) : atomicOr(&CM[h].y, bj);
+      atomicAdd(&CNT[h], 1u);
+      if ((oi & bi) | (oj & bj)) atomicOr(&CNT[h], 0x80000000u);
+    }
+  };
+
+  // ---- a run longer than the stage: alone, streamed, in partner partitions ----
+  auto long_run = [&](long long rs, long long re) {
+    const int A = a_at(rs);
+    const int LA = sload4(g.rmeta, A).y & 0xffff;
+    const long long len = re - rs;
+    const int npass = len <= kPairLimit ? 1 : static_cast<int>((len + kPerPass - 1) / kPerPass);
+    int fwdA = 0;
+    for (int pass = 0; pass < npass; ++pass) {
+      clear_hash();
+      int uniq = 0;
+      bool full_any = false;
+      for (long long b = rs; b < re; b += kWave) {
+        const long long t = b + lane;
+        const bool act = t < re;
+        const unsigned long long e = act ? E[t] : 0ull;
+        const int B = static_cast<int>((e >> 14) & kRankMask);
+        const int i = static_cast<int>((e >> 7) & 127u), j = static_cast<int>(e & 127u);
+        bool mine = act && (npass == 1 || part_of(B, npass) == pass);
+        // insert while fewer than kPairLimit partners (+ 64 per step < 256 slots)
+        const bool full = mine && uniq >= kPairLimit;
+        full_any |= __ballot(full) != 0ull;
+        mine = mine && !full;
+        bool isnew;
+        const int h = insert(mine, static_cast<unsigned>(B), static_cast<unsigned>(B), isnew);
+        if (isnew) {
+          CNT[h] = 0u;
+          RM[h] = make_uint2(0u, 0u);
+          CM[h] = make_uint2(0u, 0u);
+        }
+        const unsigned long long nm = __ballot(isnew);
+        if (isnew) MP[uniq + mbcnt(nm)] = static_cast<unsigned short>(h);
+        uniq += __popcll(nm);
+        wave_lds_sync();
+        record(mine, h, i, j);
+      }
+      if (full_any && lane == 0) atomicOr(g.err + kErrOverflow, 4);
+      wave_lds_sync();
+      for (int k0 = 0; k0 < uniq; k0 += kWave) {
+        const bool act = k0 + lane < uniq;
+        const int h = act ? static_cast<int>(MP[k0 + lane]) : 0;
+        const int B = static_cast<int>(KEY[h]);
+        const unsigned st = act ? CNT[h] : 0u;
+        int I = static_cast<int>(st & 0xFFFFu);
+        const int LB = act ? (g.rmeta[B].y & 0xffff) : 0;
+        unsigned long long cm = __ballot(act && (st >> 31));
+        while (cm) {
+          const int c = __builtin_ctzll(cm);
+          cm &= cm - 1;
+          const int Bc = rdl(B, c);
+          RR[lane] = make_uint2(0u, 0u);
+          wave_lds_sync();
+          for (long long b = rs; b < re; b += kWave) {
+            const long long t = b + lane;
+            const unsigned long long e = t < re ? E[t] : 0ull;
+            if (t < re && static_cast<int>((e >> 14) & kRankMask) == Bc) {
+              const int ii = static_cast<int>((e >> 7) & 127u), jj = static_cast<int>(e & 127u);
+              if (jj < 32) atomicOr(&RR[ii].x, 1u << jj);
+              else atomicOr(&RR[ii].y, 1u << (jj - 32));
+            }
+          }
+          wave_lds_sync();
+          const int Ic = ordered_I(LA);
+          if (lane == c) I = Ic;
+          wave_lds_sync();
+        }
+        const int U = LA + LB - I;
+        const int um = __shfl(umax_v, max(I, 1) - 1);     // every lane reads (no && in front)
+        const bool edge = act && I > 0 && U <= um;
+        fwdA += es.put(eo, edge, A, B, I, U, lane);
+        w_pairs += __popcll(__ballot(act));
+      }
+    }
+    if (lane == 0) g.fwd[A] = fwdA;
+    w_maxfwd = max(w_maxfwd, fwdA);
+  };
+
+  for (long long c = wid; c < nchunks; c += nw) {
+    const long long c0 = c * kChunk2, c1 = min(c0 + kChunk2, n);
+    long long s = c0;
+    if (s > 0) s = next_run(s, c1, a_at(s - 1));       // the run in progress belongs to the previous chunk
+    while (s < c1) {
+      // stage [s, s + lim): two entries per lane
+      const int lim = static_cast<int>(min(static_cast<long long>(kStageE), n - s));
+      wave_lds_sync();
+      unsigned long long e0 = lane < lim ? E[s + lane] : ~0ull;
+      unsigned long long e1 = lane + kWave < lim ? E[s + kWave + lane] : ~0ull;
+      STE[lane] = e0;
+      STE[lane + kWave] = e1;
+      const bool last_done = s + lim >= n || a_at(s + lim) != entry_a(lim <= kWave ? __shfl(e0, lim - 1)
+                                                                                  : __shfl(e1, lim - 1 - kWave));
+      wave_lds_sync();
+      const unsigned long long p0 = lane > 0 ? STE[lane - 1] : ~0ull;
+      const unsigned long long p1 = STE[lane + kWave - 1];
+      const bool h0 = lane < lim && (lane == 0 || entry_a(e0) != entry_a(p0));
+      const bool h1 = lane + kWave < lim && entry_a(e1) != entry_a(p1);
+      const unsigned long long H0 = __ballot(h0), H1 = __ballot(h1);
+      // owned heads: runs starting before c1
+      const long long own = min(c1 - s, static_cast<long long>(lim));
+      const unsigned long long O0 = own >= kWave ? ~0ull : ((1ull << own) - 1);
+      const unsigned long long O1 = own <= kWave ? 0ull : own >= 2 * kWave ? ~0ull : ((1ull << (own - kWave)) - 1);
+      const unsigned long long OH0 = H0 & O0, OH1 = H1 & O1;
+      const int h_top = OH1 ? kWave + 63 - __builtin_clzll(OH1) : 63 - __builtin_clzll(OH0);   // OH0 has bit 0
+      // the next head after h_top (owned or not) ends its run
+      const unsigned long long A0 = h_top >= kWave ? 0ull : H0 & above(h_top);
+      const unsigned long long A1 = h_top >= kWave ? H1 & above(h_top - kWave) : H1;
+      int gend;
+      if (A0) gend = __builtin_ctzll(A0);
+      else if (A1) gend = kWave + __builtin_ctzll(A1);
+      else gend = last_done ? lim : h_top;
+      if (gend == 0 || !group_keys) {
+        // the run at s does not fit the stage (or ranks need 25 bits): alone
+        const long long re = gend == 0 ? next_run(s + lim, n, entry_a(__shfl(e0, 0))) : next_run(s + 1, n, entry_a(__shfl(e0, 0)));
+        long_run(s, re);
+        s = re;
+        continue;
+      }
+      // ---- the group [s, s + gend): whole runs, evaluated together ----
+      const int r0 = __popcll(H0 & upto(lane)) - 1;                 // run (in the group) of entry lane
+      const int r1 = __popcll(H0) + __popcll(H1 & upto(lane)) - 1;
+      const bool v0 = lane < gend, v1 = lane + kWave < gend;
+      int la0 = 0, la1 = 0;
+      if (h0 && v0) la0 = g.rmeta[entry_a(e0)].y & 0xffff;      // gathered now, stored after the hash
+      if (h1 && v1) la1 = g.rmeta[entry_a(e1)].y & 0xffff;
+      clear_hash();
+      int uniq = 0;
+      for (int half = 0; half < 2; ++half) {
+        const unsigned long long e = half ? e1 : e0;
+        const bool act = half ? v1 : v0;
+        const int r = half ? r1 : r0;
+        const int B = static_cast<int>((e >> 14) & kRankMask);
+        const int i = static_cast<int>((e >> 7) & 127u), j = static_cast<int>(e & 127u);
+        const unsigned key = (static_cast<unsigned>(r) << 24) | static_cast<unsigned>(B);
+        bool isnew;
+        const int h = insert(act, key, key, isnew);
+        if (isnew) {
+          CNT[h] = 0u;
+          RM[h] = make_uint2(0u, 0u);
+          CM[h] = make_uint2(0u, 0u);
+        }
+        const unsigned long long nm = __ballot(isnew);
+        if (isnew) MP[uniq + mbcnt(nm)] = static_cast<unsigned short>(h);
+        uniq += __popcll(nm);
+        wave_lds_sync();
+        record(act, h, i, j);
+      }
+      if (h0 && v0) {
+        RUNA[r0] = entry_a(e0);
+        RUNL[r0] = la0;
+        RUNF[r0] = 0;
+      }
+      if (h1 && v1) {
+        RUNA[r1] = entry_a(e1);
+        RUNL[r1] = la1;
+        RUNF[r1] = 0;
+      }
+      wave_lds_sync();
+      for (int k0 = 0; k0 < uniq; k0 += kWave) {
+        const bool act = k0 + lane < uniq;
+        const int h = act ? static_cast<int>(MP[k0 + lane]) : 0;
+        const unsigned key = KEY[h];
+        const int r = static_cast<int>(key >> 24);
+        const int B = static_cast<int>(key & 0xFFFFFFu);
+        const unsigned st = act ? CNT[h] : 0u;
+        int I = static_cast<int>(st & 0xFFFFu);
+        const int LB = act ? (g.rmeta[B].y & 0xffff) : 0;
+        const int A = RUNA[r], LA = RUNL[r];
+        unsigned long long cm = __ballot(act && (st >> 31));
+        while (cm) {
+          const int c = __builtin_ctzll(cm);
+          cm &= cm - 1;
+          const unsigned kc = static_cast<unsigned>(rdl(static_cast<int>(key), c));
+          RR[lane] = make_uint2(0u, 0u);
+          wave_lds_sync();
+          for (int half = 0; half < 2; ++half) {
+            const unsigned long long e = half ? e1 : e0;
+            const bool in = half ? v1 : v0;
+            const int re_ = half ? r1 : r0;
+            const unsigned ke = (static_cast<unsigned>(re_) << 24) | static_cast<unsigned>((e >> 14) & kRankMask);
+            if (in && ke == kc) {
+              const int ii = static_cast<int>((e >> 7) & 127u), jj = static_cast<int>(e & 127u);
+              if (jj < 32) atomicOr(&RR[ii].x, 1u << jj);
+              else atomicOr(&RR[ii].y, 1u << (jj - 32));
+            }
+          }
+          wave_lds_sync();
+          const int Ic = ordered_I(rdl(LA, c));
+          if (lane == c) I = Ic;
+          wave_lds_sync();
+        }
+        const int U = LA + LB - I;
+        const int um = __shfl(umax_v, max(I, 1) - 1);     // every lane reads (no && in front)
+        const bool edge = act && I > 0 && U <= um;
+        es.put(eo, edge, A, B, I, U, lane);
+        if (edge) atomicAdd(&RUNF[r], 1);
+        w_pairs += __popcll(__ballot(act));
+      }
+      wave_lds_sync();
+      if (h0 && v0) {
+        const int f = RUNF[r0];
+        g.fwd[entry_a(e0)] = f;
+        w_maxfwd = max(w_maxfwd, f);
+      }
+      if (h1 && v1) {
+        const int f = RUNF[r1];
+        g.fwd[entry_a(e1)] = f;
+        w_maxfwd = max(w_maxfwd, f);
+      }
+      s += gend;
+    }
+  }
+  if (es.n > 0) es.flush(eo, lane);
+  // statistics: plain stores into this wave's slots (field 2: matched pairs, field 3: max fwd)
+  for (int o = 32; o > 0; o >>= 1) w_maxfwd = max(w_maxfwd, __shfl_xor(w_maxfwd, o));
+  const unsigned long long f = lane == 2 ? w_pairs : static_cast<unsigned long long>(w_maxfwd);
+  if (lane == 2 || lane == 3) g.wstat[static_cast<long long>(wid) * kWsFields + lane] = f;
+}
+
+int bits_for(long long v) {
+  int b = 1;
+  while ((1ll << b) <= v) ++b;
+  return b;
+}
+
+template <typename K>
+int resident_blocks(K kernel) {
+  int dev = 0, cus = 256, per_cu = 0;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kSwBlock, 0) != hipSuccess || per_cu < 1)
+    per_cu = 4;
+  return cus * per_cu;
+}
+
+int blocks_count() { static const int b = resident_blocks(k_sweep<false>); return b; }
+int blocks_emit() { static const int b = resident_blocks(k_sweep<true>); return b; }
+int blocks_pairs() { static const int b = resident_blocks(k_sweep_pairs); return b; }
+
+}  // namespace
+
+int sweep_max_waves() { return std::max(std::max(blocks_count(), blocks_emit()), blocks_pairs()) * kSwWaves; }
+
+size_t sweep_temp_bytes(long long ent_cap, long long ni, hipStream_t s) {
+  size_t a = 0, b = 0;
+  (void)hipcub::DeviceRadixSort::SortKeys(nullptr, a, static_cast<unsigned long long*>(nullptr),
+                                          static_cast<unsigned long long*>(nullptr), static_cast<int>(ent_cap), 39,
+                                          64, s);
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, static_cast<long long*>(nullptr),
+                                         static_cast<long long*>(nullptr), static_cast<int>((ni + kWave - 1) / kWave),
+                                         s);
+  return std::max(a, b);
+}
+
+hipError_t launch_sweep_count(const SweepArgs& a, long long* total_dev, hipStream_t s) {
+  const int nt = static_cast<int>((static_cast<long long>(a.ni) + kWave - 1) / kWave);
+  if (nt == 0) return hipMemsetAsync(total_dev, 0, sizeof(long long), s);
+  const int blocks = std::min(blocks_count(), (nt + kSwWaves - 1) / kSwWaves);
+  if (blocks * kSwWaves > a.wstat_waves) return hipErrorInvalidValue;
+  if (a.ev[0]) (void)hipEventRecord(a.ev[0], s);
+  k_sweep<false><<<blocks, kSwBlock, 0, s>>>(a);
+  k_sum_slots<<<1, 256, 0, s>>>(a.wstat, blocks * kSwWaves, 0, 3, kSwTests, kCand, kMatchEntries, a.counters,
+                                nullptr);
+  if (a.ev[1]) (void)hipEventRecord(a.ev[1], s);
+  size_t tb = a.temp_bytes;
+  hipError_t e = hipcub::DeviceScan::ExclusiveSum(a.temp, tb, a.tile_cnt, a.tile_off, nt, s);
+  if (e != hipSuccess) return e;
+  // total = last offset + last count
+  e = hipMemcpyAsync(total_dev, a.tile_off + nt - 1, sizeof(long long), hipMemcpyDeviceToDevice, s);
+  if (e != hipSuccess) return e;
+  e = hipMemcpyAsync(total_dev + 1, a.tile_cnt + nt - 1, sizeof(long long), hipMemcpyDeviceToDevice, s);
+  if (e != hipSuccess) return e;
+  return hipGetLastError();
+}
+
+hipError_t launch_sweep_pairs(const SweepArgs& a, hipStream_t s) {
+  const int nt = static_cast<int>((static_cast<long long>(a.ni) + kWave - 1) / kWave);
+  if (a.ev[2]) (void)hipEventRecord(a.ev[2], s);
+  if (a.n_ent > 0) {
+    const int be = std::min(blocks_emit(), (nt + kSwWaves - 1) / kSwWaves);
+    k_sweep<true><<<be, kSwBlock, 0, s>>>(a);
+    if (a.ev[3]) (void)hipEventRecord(a.ev[3], s);
+    size_t tb = a.temp_bytes;
+    const int end_bit = 39 + bits_for(std::max(1, a.n_reads - 1));
+    hipError_t e = hipcub::DeviceRadixSort::SortKeys(a.temp, tb, a.ent, a.ent_sorted, static_cast<int>(a.n_ent), 39,
+                                                     std::min(end_bit, 64), s);
+    if (e != hipSuccess) return e;
+  } else if (a.ev[3]) {
+    (void)hipEventRecord(a.ev[3], s);
+  }
+  if (a.ev[4]) (void)hipEventRecord(a.ev[4], s);
+  const long long chunks = (a.n_ent + kChunk2 - 1) / kChunk2;
+  const int blocks = static_cast<int>(std::max(1ll, std::min<long long>(blocks_pairs(), (chunks + kSwWaves - 1) / kSwWaves)));
+  if (blocks * kSwWaves > a.wstat_waves) return hipErrorInvalidValue;
+  k_sweep_pairs<<<blocks, kSwBlock, 0, s>>>(a);
+  k_sum_slots<<<1, 256, 0, s>>>(a.wstat, blocks * kSwWaves, 2, 4, -1, -1, kMatchedPairs, a.counters, a.err + 3);
+  return hipGetLastError();
+}
+
+}  // namespace fslr

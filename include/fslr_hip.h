@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define FSLR_ABI_VERSION 2
+#define FSLR_ABI_VERSION 3
 #define FSLR_MAX_L 64                /* max intervals per read (bitmask width) */
 #define FSLR_MAX_READS (1 << 25)     /* read rank packs into bits 6..30 of the index record */
 #define FSLR_THR_ZERO_ALN INT32_MIN
@@ -85,18 +85,32 @@ typedef struct {
                                       stable pass on chromosome instead of a (chrom, start) sort. */
 } fslr_reads;
 
+/* fslr_params.flags & 3: the pair engine of fslr_query.  Both compute the same edge set E*,
+ * forward degrees and ZeroDivisionError; they differ in what they count (fslr_query_stats).
+ *   WALK   one wavefront per query read walks its intervals' hits and dedupes its partners
+ *          (the reference's seen-set): counts evaluated_pairs and jaccard_evals.  Any input.
+ *   SWEEP  one forward sweep over the sorted index meets every overlapping interval pair once;
+ *          match entries are grouped per read and the greedy runs per pair (sweep.hip).  Needs
+ *          overlap thresholds >= 1 (overlap > 0) and no aln_size == 0 interval; does not count
+ *          evaluated_pairs / jaccard_evals (reported as -1).
+ *   AUTO   SWEEP when the input allows it and the query covers all reads, else WALK. */
+#define FSLR_ENGINE_AUTO 0
+#define FSLR_ENGINE_WALK 1
+#define FSLR_ENGINE_SWEEP 2
+
 typedef struct {
     double qlen_cut;               /* 1 - qlen_diff */
     double nal_cut;                /* 1 - n_alignment_diff */
     const uint8_t *pass_table;     /* host pointer, FSLR_MAX_L * 2*FSLR_MAX_L bytes */
     int32_t edge_threshold;        /* main.py:221 (10); reported against, see max_fwd */
-    int32_t flags;                 /* reserved, 0 */
+    int32_t flags;                 /* FSLR_ENGINE_* in bits 0..1; other bits reserved, 0 */
 } fslr_params;
 
 typedef struct {
     int64_t evaluated_pairs;       /* unique candidate read pairs (the reference's seen-set size) */
     int64_t jaccard_evals;         /* pairs that passed different_lengths_or_alignments */
-    int64_t candidates;            /* interval-level index hits (before pair dedupe) */
+    int64_t candidates;            /* WALK: interval-level index hits (before pair dedupe); SWEEP: overlapping
+                                      interval pairs of two different reads */
     int64_t n_edges;               /* edges of E* (may exceed edge capacity, see fslr_reserve_edges) */
     int32_t max_fwd;               /* max over reads of forward (higher-rank) edges */
     int32_t error;                 /* FSLR_OK or FSLR_ERR_ZERO_DIVISION */
@@ -105,12 +119,17 @@ typedef struct {
     int64_t overflow_candidates;   /* candidates of reads past the per-wave partner-set limit (witness path) */
     int64_t gather_pairs;          /* pairs evaluated by gathering B's intervals (general thresholds,
                                       aln_size==0 replay, match-list overflow) */
-    int64_t match_entries;         /* matching interval pairs recorded in the per-read match lists */
-    int64_t matched_pairs;         /* read pairs with at least one matching interval pair */
+    int64_t match_entries;         /* matching interval pairs recorded in the per-read match lists (SWEEP:
+                                      of read pairs that pass different_lengths_or_alignments) */
+    int64_t matched_pairs;         /* read pairs with at least one matching interval pair (SWEEP: gate-passing) */
     int64_t deferred;              /* entries on the deferred (gather-evaluated) list */
     int64_t deferred_capacity;     /* its capacity; deferred > capacity ⇒ FSLR_ERR_STATE, reserve + rerun */
     int64_t edge_capacity;         /* edge buffer capacity; n_edges > capacity ⇒ reserve + rerun */
     int64_t walked_records;        /* index records the pair kernels walked (every partner-partition pass) */
+    int32_t engine;                /* FSLR_ENGINE_WALK or FSLR_ENGINE_SWEEP: the engine that ran */
+    int32_t overflow_flags;        /* 1 deferred list, 2 edge buffer, 4 sweep partner table (rerun with WALK) */
+    int64_t pair_tests;            /* SWEEP: overlapping interval pairs tested (each pair once) */
+    int64_t entry_capacity;        /* SWEEP: match-entry buffer (grown automatically) */
 } fslr_query_stats;
 
 typedef struct {
@@ -118,7 +137,11 @@ typedef struct {
     float query_ms;                /* fslr_query: pair kernel device time (events around the launch) */
     float components_ms;           /* union-find device time */
     float total_ms;                /* first to last event of the last fslr_run/individual calls */
-    float pair_kernel_ms;          /* the main pair-kernel launch alone (query_kernel) */
+    float pair_kernel_ms;          /* the main pair-kernel launch alone (WALK: query_kernel; SWEEP: the count pass) */
+    float sweep_count_ms;          /* SWEEP phases of the last query: count pass (+ statistics), */
+    float sweep_emit_ms;           /*   emit pass, */
+    float sweep_sort_ms;           /*   grouping sort, */
+    float sweep_pairs_ms;          /*   per-read pair evaluation */
 } fslr_timings;
 
 /* The reference's per-query-read edge cap (cluster.py:223-224), see fslr_apply_edge_cap. */

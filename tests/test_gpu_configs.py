@@ -35,11 +35,19 @@ def test_config4_1m_eight_shards_merge_to_the_full_run():
     full.load_csr(csr, thr)
     full.reserve_edges(12 * csr.n_reads)
     full.build_index()
-    fst = full.run_query(1 - 0.04, 1 - 0.25, pt)
+    fst = full.run_query(1 - 0.04, 1 - 0.25, pt, engine='walk')
     assert full.apply_edge_cap(10)['applied'] == 0          # cfg3/4: the cap does not bind
     full.components()
     want_labels = full.labels()
     want_edges = sorted(zip(*[x.tolist() for x in full.edges(fst['n_edges'])]))
+    want_fwd = full.fwd_degree()
+    # the position-sweep engine on the same context: the same edges, degrees and components
+    sst = full.run_query(1 - 0.04, 1 - 0.25, pt, engine='sweep')
+    assert sst['engine'] == 'sweep' and sst['n_edges'] == fst['n_edges']
+    assert sorted(zip(*[x.tolist() for x in full.edges(sst['n_edges'])])) == want_edges
+    np.testing.assert_array_equal(full.fwd_degree(), want_fwd)
+    full.components()
+    np.testing.assert_array_equal(full.labels(), want_labels)
     W = 8
     labels, edges, pairs, jacc = [], [], 0, 0
     for r in range(W):
@@ -92,19 +100,23 @@ def test_config5_10m_capped_sample_vs_oracle():
     ctx.reserve_edges(12 * csr.n_reads)
     ctx.reserve_deferred(64 << 20)
     ctx.build_index()
-    st = ctx.run_query(1 - 0.04, 1 - 0.25, pass_table(CUTS))
-    assert st['max_fwd'] > 10                               # the cap binds at this density
-    cap = ctx.apply_edge_cap(10)
-    assert cap['applied'] == 1 and cap['dropped'] > 0
-    ne = ctx.stats()['n_edges']
-    a, b, I, U = ctx.edges(ne)
-    own = a < S                                              # edges formed in the loops of reads < S
-    got = sorted(zip(a[own].tolist(), b[own].tolist(), I[own].tolist(), U[own].tolist()))
     want = sorted(zip(z['a'].tolist(), z['b'].tolist(), z['I'].tolist(), z['U'].tolist()))
-    assert len(got) == len(want) == meta['n_edges']
-    assert got == want
-    np.testing.assert_array_equal(ctx.fwd_degree()[:S], z['fwd'])
-    ctx.components()
-    lab = ctx.labels()
-    assert lab.shape == (csr.n_reads,) and np.all(lab <= np.arange(csr.n_reads))
+    labels = {}
+    for engine in ('sweep', 'walk'):
+        st = ctx.run_query(1 - 0.04, 1 - 0.25, pass_table(CUTS), engine=engine)
+        assert st['engine'] == engine
+        assert st['max_fwd'] > 10                               # the cap binds at this density
+        cap = ctx.apply_edge_cap(10)
+        assert cap['applied'] == 1 and cap['dropped'] > 0
+        ne = ctx.stats()['n_edges']
+        a, b, I, U = ctx.edges(ne)
+        own = a < S                                              # edges formed in the loops of reads < S
+        got = sorted(zip(a[own].tolist(), b[own].tolist(), I[own].tolist(), U[own].tolist()))
+        assert len(got) == len(want) == meta['n_edges']
+        assert got == want
+        np.testing.assert_array_equal(ctx.fwd_degree()[:S], z['fwd'])
+        ctx.components()
+        labels[engine] = lab = ctx.labels()
+        assert lab.shape == (csr.n_reads,) and np.all(lab <= np.arange(csr.n_reads))
+    np.testing.assert_array_equal(labels['sweep'], labels['walk'])
     ctx.close()

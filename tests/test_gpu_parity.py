@@ -23,6 +23,9 @@ from fslr_amd.prep import fold_overlap_threshold, pass_table
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
+# the two pair engines (fslr_hip.h FSLR_ENGINE_*): the read walk counts evaluated pairs, the
+# position sweep does not; both must give the oracle's edges, degrees and components
+ENGINES = ['walk', 'sweep']
 
 
 @pytest.fixture(scope='module')
@@ -39,7 +42,7 @@ def oracle_from_csr(c):
 
 
 def gpu_run(ctx, csr, overlap=0.8, cutoffs=(1, 1, 0.66, 0.66, 0.66, 0.5), qlen_diff=0.04, nal_diff=0.25,
-            full_sort=False, cap=None):
+            full_sort=False, cap=None, engine='walk'):
     """E* (every candidate pair) or, with ``cap`` = edge_threshold, the reference's capped graph."""
     thr = fold_overlap_threshold(csr.iv_aln, overlap)
     if full_sort:
@@ -49,7 +52,9 @@ def gpu_run(ctx, csr, overlap=0.8, cutoffs=(1, 1, 0.66, 0.66, 0.66, 0.5), qlen_d
         ctx.load_csr(csr, thr)
     ctx.reserve_edges(max(1 << 16, 12 * csr.n_reads))
     ctx.build_index()
-    st = ctx.run_query(1 - qlen_diff, 1 - nal_diff, pass_table(cutoffs))
+    st = ctx.run_query(1 - qlen_diff, 1 - nal_diff, pass_table(cutoffs), engine=engine)
+    if engine != 'auto':
+        assert st['engine'] == engine
     if cap is not None:
         st['cap'] = ctx.apply_edge_cap(cap)
         st['n_edges'] = ctx.stats()['n_edges']
@@ -82,8 +87,11 @@ def compare_with_oracle(g, o, n):
     assert len(ge) == len(oe)
     assert ge == oe
     np.testing.assert_array_equal(g['fwd'], o['fwd'])
-    assert g['stats']['evaluated_pairs'] == o['stats']['evaluated_pairs']
-    assert g['stats']['jaccard_evals'] == o['stats']['jaccard_evals']
+    if g['stats']['engine'] == 'walk':
+        assert g['stats']['evaluated_pairs'] == o['stats']['evaluated_pairs']
+        assert g['stats']['jaccard_evals'] == o['stats']['jaccard_evals']
+    else:
+        assert g['stats']['evaluated_pairs'] == -1
     assert g['stats']['max_fwd'] == o['stats']['max_fwd']
     # components: oracle numbers by first insertion (== min rank), device labels = min rank
     lab = g['labels']
@@ -165,19 +173,21 @@ def test_reference_item_list_drops_in(name):
     assert sorted(map(tuple, m2.itertuples(index=False))) == sorted(map(tuple, fx.stage(name)['edges']))
 
 
-def test_capbind_device_equals_uncapped_oracle(ctx):
+@pytest.mark.parametrize('engine', ENGINES)
+def test_capbind_device_equals_uncapped_oracle(ctx, engine):
     data, _, _ = host_prepare('capbind_1500')
     csr = data.csr()
-    g = gpu_run(ctx, csr)
+    g = gpu_run(ctx, csr, engine=engine)
     o = O.run_core(oracle_from_csr(csr), use_cap=False)
     compare_with_oracle(g, o, csr.n_reads)
     assert g['stats']['max_fwd'] > 10
 
 
-def test_capbind_device_capped_equals_reference_loop(ctx):
+@pytest.mark.parametrize('engine', ENGINES)
+def test_capbind_device_capped_equals_reference_loop(ctx, engine):
     data, _, _ = host_prepare('capbind_1500')
     csr = data.csr()
-    g = gpu_run(ctx, csr, cap=10)
+    g = gpu_run(ctx, csr, cap=10, engine=engine)
     o = O.run_core(oracle_from_csr(csr), use_cap=True)
     assert g['stats']['cap']['applied'] == 1 and g['stats']['cap']['capped'] > 0
     compare_capped_with_oracle(g, o, csr.n_reads)
@@ -199,20 +209,22 @@ def _squeezed(n, lmax, seed, squeeze, dist='uniform', cluster_cap=10, size_p=1 /
     (8_000, 8, 53, 2000, 'uniform', 10, 1),
     (8_000, 8, 59, 50, 'uniform', 200, 40),
 ])
-def test_dense_capped_vs_oracle(ctx, n, lmax, seed, squeeze, dist, ccap, thr):
+@pytest.mark.parametrize('engine', ENGINES)
+def test_dense_capped_vs_oracle(ctx, n, lmax, seed, squeeze, dist, ccap, thr, engine):
     """Events of up to `ccap` reads (forward degrees far above the cap) on a squeezed genome: the
     cap binds for many reads, with chains of pairs left unseen by capped loops; the replayed graph
     equals the oracle's reference loop exactly."""
     csr = _squeezed(n, lmax, seed, squeeze, dist, cluster_cap=ccap, size_p=0.05)
-    g = gpu_run(ctx, csr, cap=thr)
+    g = gpu_run(ctx, csr, cap=thr, engine=engine)
     o = O.run_core(oracle_from_csr(csr), edge_threshold=thr, use_cap=True)
     assert g['stats']['cap']['applied'] == 1 and g['stats']['cap']['capped'] > 0
     assert g['stats']['cap']['dropped'] > 0 or thr == 40
     compare_capped_with_oracle(g, o, csr.n_reads)
 
 
+@pytest.mark.parametrize('engine', ENGINES)
 @pytest.mark.parametrize('thr', [1, 10])
-def test_one_locus_capped_vs_oracle(ctx, thr):
+def test_one_locus_capped_vs_oracle(ctx, thr, engine):
     """1500 reads on one locus with runs of equal starts (the search order's tie rule decides
     which pairs a capped loop reaches)."""
     n = 1500
@@ -227,7 +239,7 @@ def test_one_locus_capped_vs_oracle(ctx, thr):
     ctx.set_reads(off, q, m, chrom, start, end, thr_iv, 1, iv_data_pos=np.arange(n))
     ctx.reserve_edges(n * n)
     ctx.build_index()
-    st = ctx.run_query(1 - 0.04, 1 - 0.25, pass_table([1.0]))
+    st = ctx.run_query(1 - 0.04, 1 - 0.25, pass_table([1.0]), engine=engine)
     st['cap'] = ctx.apply_edge_cap(thr)
     st['n_edges'] = ctx.stats()['n_edges']
     st['max_fwd'] = st['cap']['max_fwd']
@@ -239,11 +251,12 @@ def test_one_locus_capped_vs_oracle(ctx, thr):
     compare_capped_with_oracle(g, o, n)
 
 
-def test_cap_not_binding_is_identity(ctx):
+@pytest.mark.parametrize('engine', ENGINES)
+def test_cap_not_binding_is_identity(ctx, engine):
     s = synth.generate(30_000, 16, 2)
     csr = s.interval_data().csr()
-    g1 = gpu_run(ctx, csr)
-    g2 = gpu_run(ctx, csr, cap=10)
+    g1 = gpu_run(ctx, csr, engine=engine)
+    g2 = gpu_run(ctx, csr, cap=10, engine=engine)
     assert g2['stats']['cap']['applied'] == 0
     assert sorted(zip(g1['a'], g1['b'], g1['I'])) == sorted(zip(g2['a'], g2['b'], g2['I']))
     np.testing.assert_array_equal(g1['labels'], g2['labels'])
@@ -262,18 +275,39 @@ def test_union_find_labels_stable_over_repeats(ctx):
         np.testing.assert_array_equal(ctx.labels(), want)
 
 
-def test_zero_division_raises(ctx):
+@pytest.mark.parametrize('engine', ['walk', 'auto'])
+def test_zero_division_raises(ctx, engine):
     data, _, _ = host_prepare('zerodiv')
     csr = data.csr()
     with pytest.raises(ZeroDivisionError):
-        gpu_run(ctx, csr)
+        gpu_run(ctx, csr, engine=engine)
+
+
+@pytest.mark.parametrize('engine', ENGINES)
+def test_zero_qlen2_pair_raises(ctx, engine):
+    """Two overlapping reads with qlen2 == 0 (no aln_size == 0 interval, so the sweep may run):
+    different_lengths_or_alignments divides by zero (cluster.py:178-183)."""
+    off = np.array([0, 1, 2], np.int64)
+    chrom = np.zeros(2, np.int32)
+    start = np.array([5000, 5010], np.int32)
+    end = start + 1000
+    aln = np.full(2, 1000, np.int64)
+    ctx.set_reads(off, np.zeros(2, np.int32), np.zeros(2, np.int32), chrom, start, end,
+                  fold_overlap_threshold(aln, 0.8), 1, iv_data_pos=np.arange(2))
+    ctx.reserve_edges(16)
+    ctx.build_index()
+    with pytest.raises(ZeroDivisionError):
+        ctx.run_query(1 - 0.04, 1 - 0.25, pass_table([1.0]), engine=engine)
 
 
 # ------------------------------------------------------------------ KATs through the device
-def test_kat_jaccard_on_device(ctx):
+@pytest.mark.parametrize('engine', ENGINES)
+def test_kat_jaccard_on_device(ctx, engine):
     """Each KAT pair becomes two reads on a private coordinate range; the device
     must report exactly the reference's n_i (I) and U for every pair with I > 0."""
     kats = [k for k in fx.kats()['jaccard'] if 'raises' not in k and k['pct'] > 0]
+    if engine == 'sweep':      # an aln_size == 0 interval is the walk engine's (exact ZeroDivision replay)
+        kats = [k for k in kats if all(x[3] > 0 for x in k['a'] + k['b'])]
     reads = []
     for t, k in enumerate(kats):
         base = 10_000 + t * 10_000
@@ -295,8 +329,9 @@ def test_kat_jaccard_on_device(ctx):
                       int(chrom.max()) + 1)
         ctx.reserve_edges(4 * n)
         ctx.build_index()
-        ctx.query(1.0, 1.0, pass_table([0.0]))
+        ctx.query(1.0, 1.0, pass_table([0.0]), engine=engine)
         st = ctx.stats()
+        assert st['engine'] == engine
         a, b, I, U = ctx.edges(st['n_edges'])
         for x, y, i, u in zip(a.tolist(), b.tolist(), I.tolist(), U.tolist()):
             res[(pct, min(x, y) // 2)] = (i, u)
@@ -315,10 +350,11 @@ def test_kat_jaccard_on_device(ctx):
     (20_000, 64, 13, 'zipf'),         # config 5 shape (skewed 1..64), reduced size
     (50_000, 16, 5, 'uniform'),
 ])
-def test_synthetic_vs_oracle(ctx, n, lmax, seed, dist):
+@pytest.mark.parametrize('engine', ENGINES)
+def test_synthetic_vs_oracle(ctx, n, lmax, seed, dist, engine):
     s = synth.generate(n, lmax, seed, dist=dist)
     csr = s.interval_data().csr()
-    g = gpu_run(ctx, csr)
+    g = gpu_run(ctx, csr, engine=engine)
     o = O.run_core(oracle_from_csr(csr), use_cap=False)
     compare_with_oracle(g, o, csr.n_reads)
 
@@ -328,10 +364,13 @@ def test_synthetic_vs_oracle(ctx, n, lmax, seed, dist):
     dict(overlap=0.0, cutoffs=(0.2,), qlen_diff=0.04, nal_diff=0.25),
     dict(overlap=0.95, cutoffs=(0.3,), qlen_diff=0.0, nal_diff=0.0),
 ])
-def test_parameter_variants_vs_oracle(ctx, params):
+@pytest.mark.parametrize('engine', ['walk', 'auto'])
+def test_parameter_variants_vs_oracle(ctx, params, engine):
     s = synth.generate(20_000, 8, 23)
     csr = s.interval_data().csr()
-    g = gpu_run(ctx, csr, **params)
+    g = gpu_run(ctx, csr, engine=engine, **params)
+    # overlap <= 0 (thresholds < 1: matches need not overlap) is the walk engine's
+    assert g['stats']['engine'] == ('walk' if engine == 'walk' or params['overlap'] <= 0 else 'sweep')
     o = O.run_core(oracle_from_csr(csr), params['overlap'], params['cutoffs'], params['qlen_diff'],
                    params['nal_diff'], use_cap=False)
     compare_with_oracle(g, o, csr.n_reads)
@@ -339,20 +378,22 @@ def test_parameter_variants_vs_oracle(ctx, params):
 
 @pytest.mark.slow
 def test_config3_1m_vs_oracle(ctx):
-    """BASELINE config 3 (1M reads, 1-16 fillings): full bit-exact comparison."""
+    """BASELINE config 3 (1M reads, 1-16 fillings): full bit-exact comparison, both engines."""
     s = synth.generate(1_000_000, 16, 11)
     csr = s.interval_data().csr()
-    g = gpu_run(ctx, csr)
     o = O.run_core(oracle_from_csr(csr), use_cap=False)
-    compare_with_oracle(g, o, csr.n_reads)
+    for engine in ENGINES:
+        g = gpu_run(ctx, csr, engine=engine)
+        compare_with_oracle(g, o, csr.n_reads)
 
 
-def test_full_sort_index_path_matches_data_order_path(ctx):
+@pytest.mark.parametrize('engine', ENGINES)
+def test_full_sort_index_path_matches_data_order_path(ctx, engine):
     """Index built by the (chrom, start) radix sort == index built from the host's start order."""
     s = synth.generate(40_000, 16, 4)
     csr = s.interval_data().csr()
-    g1 = gpu_run(ctx, csr, full_sort=True)
-    g2 = gpu_run(ctx, csr)
+    g1 = gpu_run(ctx, csr, full_sort=True, engine=engine)
+    g2 = gpu_run(ctx, csr, engine=engine)
     np.testing.assert_array_equal(g1['labels'], g2['labels'])
     np.testing.assert_array_equal(g1['fwd'], g2['fwd'])
     assert sorted(zip(g1['a'], g1['b'], g1['I'])) == sorted(zip(g2['a'], g2['b'], g2['I']))
@@ -360,7 +401,8 @@ def test_full_sort_index_path_matches_data_order_path(ctx):
 
 
 @pytest.mark.parametrize('split,mod', [(3, 64), (5, None)])
-def test_many_chromosomes_vs_oracle(ctx, split, mod):
+@pytest.mark.parametrize('engine', ENGINES)
+def test_many_chromosomes_vs_oracle(ctx, split, mod, engine):
     """Chromosome counts at the index build's limits: 64 ids (the largest the counting-sort pass
     takes, every chromosome bit in use) and 115 ids (the radix-pass fallback)."""
     import dataclasses
@@ -372,13 +414,14 @@ def test_many_chromosomes_vs_oracle(ctx, split, mod):
     _, dense = np.unique(ch, return_inverse=True)
     csr = dataclasses.replace(csr, iv_chrom=dense.astype(np.int32), n_chroms=int(dense.max()) + 1)
     assert csr.n_chroms == (mod or 23 * split)
-    g = gpu_run(ctx, csr)
+    g = gpu_run(ctx, csr, engine=engine)
     o = O.run_core(oracle_from_csr(csr), use_cap=False)
     compare_with_oracle(g, o, csr.n_reads)
 
 
+@pytest.mark.parametrize('engine', ENGINES)
 @pytest.mark.parametrize('squeeze', [100, 400])
-def test_dense_overlaps_vs_oracle(ctx, squeeze):
+def test_dense_overlaps_vs_oracle(ctx, squeeze, engine):
     """Dense inputs (the 10M-read config's regime): starts squeezed onto 1/squeeze of the genome,
     so walks run to ~350 / ~1400 records per read and reads take several partner partitions."""
     import dataclasses
@@ -387,7 +430,7 @@ def test_dense_overlaps_vs_oracle(ctx, squeeze):
     st = csr.iv_start.astype(np.int64) // squeeze          # monotone: the data order stays start-sorted
     en = st + (csr.iv_end.astype(np.int64) - csr.iv_start)
     csr = dataclasses.replace(csr, iv_start=st.astype(np.int32), iv_end=en.astype(np.int32))
-    g = gpu_run(ctx, csr)
+    g = gpu_run(ctx, csr, engine=engine)
     o = O.run_core(oracle_from_csr(csr), use_cap=False)
     compare_with_oracle(g, o, csr.n_reads)
 
@@ -428,8 +471,8 @@ def test_dense_shards_with_partitioned_launch_vs_oracle(n_shards):
     np.testing.assert_array_equal(fwd, o['fwd'])
 
 
-@pytest.mark.parametrize('pass_records', [None, '0', '500'])
-def test_one_locus_many_partners_vs_oracle(ctx, monkeypatch, pass_records):
+@pytest.mark.parametrize('pass_records,engine', [(None, 'walk'), ('0', 'walk'), ('500', 'walk'), (None, 'sweep')])
+def test_one_locus_many_partners_vs_oracle(ctx, monkeypatch, pass_records, engine):
     """1500 reads on one interval: every pair overlaps.  Default: up to 6 partner partitions per
     read; '0': one partition, the hash overflows (witness path); '500': partitions of ~500 partners,
     which overflow within a partition."""
@@ -448,7 +491,8 @@ def test_one_locus_many_partners_vs_oracle(ctx, monkeypatch, pass_records):
     ctx.set_reads(off, q, m, chrom, start, end, thr, 1, iv_data_pos=np.arange(n))
     ctx.reserve_edges(n * n)
     ctx.build_index()
-    st = ctx.run_query(1 - 0.04, 1 - 0.25, pass_table([1.0]))
+    st = ctx.run_query(1 - 0.04, 1 - 0.25, pass_table([1.0]), engine=engine)
+    assert st['engine'] == engine
     ctx.components()
     a, b, I, U = ctx.edges(st['n_edges'])
     g = dict(stats=st, labels=ctx.labels(), fwd=ctx.fwd_degree(), a=a, b=b, I=I, U=U)
@@ -459,17 +503,19 @@ def test_one_locus_many_partners_vs_oracle(ctx, monkeypatch, pass_records):
     compare_with_oracle(g, o, n)
 
 
-def test_rerun_is_deterministic(ctx):
+@pytest.mark.parametrize('engine', ENGINES)
+def test_rerun_is_deterministic(ctx, engine):
     s = synth.generate(30_000, 16, 2)
     csr = s.interval_data().csr()
-    g1 = gpu_run(ctx, csr)
-    g2 = gpu_run(ctx, csr)
+    g1 = gpu_run(ctx, csr, engine=engine)
+    g2 = gpu_run(ctx, csr, engine=engine)
     np.testing.assert_array_equal(g1['labels'], g2['labels'])
     np.testing.assert_array_equal(g1['fwd'], g2['fwd'])
     assert sorted(zip(g1['a'], g1['b'])) == sorted(zip(g2['a'], g2['b']))
 
 
-def test_vectors_cluster_ids(ctx):
+@pytest.mark.parametrize('engine', ENGINES)
+def test_vectors_cluster_ids(ctx, engine):
     """Committed reference cluster-id vectors (10k / 20k reads) through the device path."""
     for vec in ('v10k_l8_s7', 'v20k_l16_s11'):
         z = np.load(os.path.join(fx.GOLDEN, 'vectors', f'{vec}.npz'))
@@ -477,7 +523,7 @@ def test_vectors_cluster_ids(ctx):
         s = synth.generate(n, lmax, seed)
         data = s.interval_data()
         csr = data.csr()
-        g = gpu_run(ctx, csr)
+        g = gpu_run(ctx, csr, engine=engine)
         lab = g['labels']
         sizes = np.bincount(lab, minlength=csr.n_reads)
         roots = np.flatnonzero(sizes >= 2)
@@ -507,9 +553,10 @@ def _boundary_pool(cut, top, rng):
     return pool[rng.integers(0, pool.size, 400)]
 
 
+@pytest.mark.parametrize('engine', ENGINES)
 @pytest.mark.parametrize('qlen_diff,nal_diff', [(0.04, 0.25), (0.0, 0.0), (1.0, 1.0), (1.5, -0.5), (-0.5, 1.5),
                                                 (0.34, 0.999999), (1e-12, 0.5)])
-def test_length_gate_boundaries_vs_oracle(ctx, monkeypatch, qlen_diff, nal_diff):
+def test_length_gate_boundaries_vs_oracle(ctx, monkeypatch, qlen_diff, nal_diff, engine):
     """400 reads with one identical interval each (every pair overlaps, so every pair is evaluated
     and the first reads overflow the per-read partner hash): qlen2 / n_alignments drawn around the
     exact ratio boundaries of cluster.py:178-183; one read each with qlen2 == 0 and nal == 0."""
@@ -529,13 +576,13 @@ def test_length_gate_boundaries_vs_oracle(ctx, monkeypatch, qlen_diff, nal_diff)
     ctx.set_reads(off, q.astype(np.int32), m.astype(np.int32), chrom, start, end, thr, 1)
     ctx.reserve_edges(n * n)
     ctx.build_index()
-    st = ctx.run_query(1 - qlen_diff, 1 - nal_diff, pass_table([1.0]))
+    st = ctx.run_query(1 - qlen_diff, 1 - nal_diff, pass_table([1.0]), engine=engine)
     ctx.components()
     a, b, I, U = ctx.edges(st['n_edges'])
     g = dict(stats=st, labels=ctx.labels(), fwd=ctx.fwd_degree(), a=a, b=b, I=I, U=U)
     o = O.run_core(O.OracleCSR(off, chrom, start, end, aln, q, m, np.arange(n)), 0.8, (1.0,), qlen_diff, nal_diff,
                    use_cap=False)
-    assert st['overflow_candidates'] > 0
+    assert engine == 'sweep' or st['overflow_candidates'] > 0
     compare_with_oracle(g, o, n)
 
 
