@@ -151,8 +151,10 @@ def main():
             ctx.query_shard(qcut, ncut, pt, rank, world)      # balanced rank blocks (fslr_query_shard)
         else:
             ctx.query(qcut, ncut, pt, 10, engine=args.engine)
-            ctx.apply_edge_cap(10)                            # cluster.py:223-224 (no-op unless it binds)
         ctx.components()
+        # cluster.py:223-224: the edge cap (one counter read; a replay + new components only if it binds)
+        if world == 1 and ctx.apply_edge_cap(10)['applied']:
+            ctx.components()
         if merge is not None:
             merge()
 

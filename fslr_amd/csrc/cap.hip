@@ -200,10 +200,14 @@ extern "C" int fslr_apply_edge_cap(fslr_ctx* c, int32_t thr, fslr_cap_stats* out
   unsigned long long ne_u = 0;
   int ew[4] = {};
   if (c->counters) {
-    HIP_TRY(c, hipMemcpyAsync(&ne_u, c->counters + kEdgeCount, sizeof(ne_u), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipMemcpyAsync(ew, c->errw, sizeof(ew), hipMemcpyDeviceToHost, c->stream));
+    long long pk[3];
+    if (int rc = peek_counts(c, pk)) return rc;
+    ne_u = static_cast<unsigned long long>(pk[0]);
+    ew[0] = static_cast<int>(pk[1]);
+    ew[3] = static_cast<int>(pk[2]);
+  } else {
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
   }
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
   if (ew[0] == FSLR_ERR_ZERO_DIVISION) return fail(c, FSLR_ERR_ZERO_DIVISION, "division by zero");
   const int64_t ne = static_cast<int64_t>(ne_u);
   if (ne > c->edge_cap) return fail(c, FSLR_ERR_STATE, "edge buffer overflowed; reserve and rerun the query");
@@ -216,6 +220,7 @@ extern "C" int fslr_apply_edge_cap(fslr_ctx* c, int32_t thr, fslr_cap_stats* out
   if (!c->last_full)
     return fail(c, FSLR_ERR_STATE, "the edge cap binds: its replay needs the last query to cover every read on "
                                    "one context (fslr_query over [0, n_reads))");
+  if (int rc = ensure_walk_index(c)) return rc;       // the replayed loops walk qpos and the scan ranges
   const int64_t n = c->n;
   // FSLR_CAP_TIMING=1: host wall time per stage on stderr (diagnostics)
   const bool timing = std::getenv("FSLR_CAP_TIMING") != nullptr;

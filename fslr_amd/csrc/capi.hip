@@ -123,9 +123,10 @@ void fslr_ctx_destroy(fslr_ctx* c) {
                   c->crange, c->keys,   c->keys2,   c->vals,    c->vals2,   c->endkey,  c->pmaxkey,
                   c->temp,   c->umax,   c->edges,   c->edge_iu, c->fwd,     c->parent,  c->counters,
                   c->errw,   c->thr_tmp, c->defer,   c->dchrom,  c->drec,    c->lbounds, c->diag, c->wstat,
-                  c->dgate,  c->chist,  c->heavy, c->ent, c->ent_sorted, c->sweep_temp, c->sw_tile, c->sw_total, c->sw_wstat};
+                  c->dgate,  c->chist,  c->heavy, c->ent, c->ent_sorted, c->sweep_temp, c->sw_tile, c->sw_wstat, c->ent_ub};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
+  if (c->sw_total) (void)hipHostFree(c->sw_total);
   if (c->ev_ok) {
     for (auto& e : c->ev) (void)hipEventDestroy(e);
     for (auto& e : c->kev) (void)hipEventDestroy(e);
@@ -263,6 +264,8 @@ int fslr_set_thresholds(fslr_ctx* c, const int32_t* thr) {
   if (c->ni) {
     HIP_TRY(c, hipMemcpyAsync(c->thr_tmp, thr, c->ni * sizeof(int), hipMemcpyHostToDevice, c->stream));
     if (c->index_built && c->built_n_shards != 1) c->index_built = false;   // qpos is partial: rebuild
+    int rc = ensure_walk_index(c);                                           // idx4 is updated through qpos
+    if (rc) return rc;
     HIP_TRY(c, launch_set_thr(c->thr_tmp, c->iv, c->qpos, c->index_built ? c->idx4 : nullptr, c->data_pos,
                               c->have_data_pos ? c->drec : nullptr, static_cast<int>(c->ni), c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -301,11 +304,9 @@ int fslr_set_shard(fslr_ctx* c, int32_t shard, int32_t n_shards) {
   return FSLR_OK;
 }
 
-int fslr_build_index(fslr_ctx* c) {
-  if (!c) return FSLR_ERR_INVALID;
-  if (!c->reads_set) return fail(c, FSLR_ERR_STATE, "fslr_set_reads first");
-  HIP_TRY(c, hipSetDevice(c->device));
-  if (c->profiling) HIP_TRY(c, hipEventRecord(c->ev[0], c->stream));
+}  // extern "C"
+
+static IndexBufs index_bufs(fslr_ctx* c) {
   IndexBufs b;
   b.rmeta = c->rmeta;
   b.iv = c->iv;
@@ -330,10 +331,55 @@ int fslr_build_index(fslr_ctx* c) {
   b.rng_s = c->rng_s;
   b.idx4 = c->idx4;
   b.idx_gate = c->idx_gate;
-  HIP_TRY(c, launch_build_index(b, static_cast<int>(c->n), static_cast<int>(c->ni), c->n_chroms, c->stream));
+  return b;
+}
+
+// edge count, error code and max forward degree of the last query, written by one tiny kernel into
+// pinned host memory (no copy engine round trips); syncs
+__global__ void k_peek(const unsigned long long* counters, const int* err, long long* out) {
+  if (threadIdx.x == 0) {
+    out[0] = static_cast<long long>(counters[kEdgeCount]);
+    out[1] = err[0];
+    out[2] = err[3];
+  }
+}
+
+int fslr::peek_counts(fslr_ctx* c, long long out[3]) {
+  if (!c->sw_total) {
+    HIP_TRY(c, hipHostMalloc(reinterpret_cast<void**>(&c->sw_total), 8 * sizeof(long long), hipHostMallocMapped));
+    HIP_TRY(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->sw_total_dev), c->sw_total, 0));
+  }
+  k_peek<<<1, 64, 0, c->stream>>>(c->counters, c->errw, c->sw_total_dev + 4);
+  HIP_TRY(c, hipGetLastError());
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  const volatile long long* v = c->sw_total + 4;
+  for (int k = 0; k < 3; ++k) out[k] = v[k];
+  return FSLR_OK;
+}
+
+int fslr::ensure_walk_index(fslr_ctx* c) {
+  if (!c->index_built || c->index_full) return FSLR_OK;
+  HIP_TRY(c, launch_index_walk_parts(index_bufs(c), static_cast<int>(c->n), static_cast<int>(c->ni), c->stream));
+  c->index_full = true;
+  return FSLR_OK;
+}
+
+extern "C" {
+
+int fslr_build_index(fslr_ctx* c) {
+  if (!c) return FSLR_ERR_INVALID;
+  if (!c->reads_set) return fail(c, FSLR_ERR_STATE, "fslr_set_reads first");
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (c->profiling) HIP_TRY(c, hipEventRecord(c->ev[0], c->stream));
+  // the sweep engine's index only (the walk engine's parts follow on demand, ensure_walk_index)
+  // where the data-order path applies and one context covers every query read
+  const bool full = !(c->have_data_pos && c->n_chroms <= 64 && c->n_shards == 1);
+  HIP_TRY(c, launch_build_index(index_bufs(c), static_cast<int>(c->n), static_cast<int>(c->ni), c->n_chroms, full,
+                                c->stream));
   if (c->profiling) HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));
   c->t_index_rec = c->profiling;
   c->index_built = true;
+  c->index_full = full;
   c->built_shard = c->shard;
   c->built_n_shards = c->n_shards;
   return FSLR_OK;
@@ -357,25 +403,35 @@ int fslr_query_shard(fslr_ctx* c, const fslr_params* p, int32_t shard, int32_t n
   return query_impl(c, p, 0, c->n, shard, n_shards);
 }
 
-// The position-sweep engine (sweep.hip): count pass + tile scan, one sync to read the entry count
-// (the grouping sort is sized on the host; the entry buffer grows to fit), then the emit pass, the
-// grouping sort and the per-read pair evaluation.
+// The position-sweep engine (sweep.hip).  One pass: the sweep writes each tile's entries at an
+// upper-bound slot (its pair tests, scanned); one sync reads the entry count, the upper-bound total
+// and an overflow flag from pinned host memory the kernels write; the tiles are packed, grouped by
+// A and evaluated.  A too-small upper-bound buffer is grown and the sweep rerun (first query on an
+// input); an upper bound beyond kUbBudget entries takes the two-pass fallback (count, then emit).
 static int sweep_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_t a_end, hipEvent_t e0,
                       hipEvent_t e1) {
+  constexpr int64_t kUbBudget = int64_t(1) << 30;     // 8 GB of upper-bound slots
   const int64_t tiles = (c->ni + 63) / 64 + 1;
   int rc;
   if (tiles > c->sw_tiles) {
-    if ((rc = dalloc(c, &c->sw_tile, 2 * tiles))) return rc;
+    if ((rc = dalloc(c, &c->sw_tile, 4 * tiles))) return rc;
     c->sw_tiles = tiles;
     c->ent_cap = 0;                                  // re-size the scan scratch with the entries
   }
-  if (!c->sw_total && (rc = dalloc(c, &c->sw_total, 2))) return rc;
+  if (!c->sw_total) {
+    HIP_TRY(c, hipHostMalloc(reinterpret_cast<void**>(&c->sw_total), 8 * sizeof(long long), hipHostMallocMapped));
+    HIP_TRY(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->sw_total_dev), c->sw_total, 0));
+  }
   if (!c->sw_wstat) {
     const int w = sweep_max_waves();
     if ((rc = dalloc(c, &c->sw_wstat, static_cast<size_t>(w) * 4))) return rc;
     c->sw_wstat_waves = w;
   }
   if (c->ent_cap == 0 && (rc = reserve_entries(c, std::max<int64_t>(1 << 20, c->ni)))) return rc;
+  if (c->ent_ub_cap == 0) {
+    if ((rc = dalloc(c, &c->ent_ub, std::max<int64_t>(1 << 20, 4 * c->ni)))) return rc;
+    c->ent_ub_cap = std::max<int64_t>(1 << 20, 4 * c->ni);
+  }
   SweepArgs s;
   s.rmeta = c->rmeta;
   s.idx4 = c->idx4;
@@ -391,6 +447,8 @@ static int sweep_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_
   s.lb = c->lbounds;
   s.tile_cnt = c->sw_tile;
   s.tile_off = c->sw_tile + c->sw_tiles;
+  s.tile_tests = c->sw_tile + 2 * c->sw_tiles;
+  s.tile_ub = c->sw_tile + 3 * c->sw_tiles;
   s.edges = c->edges;
   s.edge_iu = c->edge_iu;
   s.edge_cap = c->edge_cap;
@@ -399,26 +457,47 @@ static int sweep_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_
   s.err = c->errw;
   s.wstat = c->sw_wstat;
   s.wstat_waves = c->sw_wstat_waves;
+  s.n_ent = 0;
   for (int k = 0; k < 5; ++k) s.ev[k] = c->profiling ? c->sw_ev[k] : nullptr;
-  if (e0) s.ev[0] = nullptr;                        // the ring pair below brackets the count pass
-  s.temp = c->sweep_temp;
-  s.temp_bytes = c->sweep_temp_bytes;
-  if (e0) HIP_TRY(c, hipEventRecord(e0, c->stream));
-  if (c->profiling) HIP_TRY(c, hipEventRecord(c->sw_ev[0], c->stream));
+  s.ev[0] = nullptr;                                // recorded here, around the sweep pass
   HIP_TRY(c, launch_len_bounds(c->rmeta, 0, static_cast<int>(c->n), p->qlen_cut, p->nal_cut, c->lbounds, c->stream));
-  HIP_TRY(c, launch_sweep_count(s, c->sw_total, c->stream));
-  if (e1) HIP_TRY(c, hipEventRecord(e1, c->stream));
-  long long tot[2] = {0, 0};
-  HIP_TRY(c, hipMemcpyAsync(tot, c->sw_total, sizeof(tot), hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
-  const int64_t n_ent = tot[0] + tot[1];
-  if (n_ent > c->ent_cap && (rc = reserve_entries(c, n_ent + (n_ent >> 3) + 4096))) return rc;
+  int mode = 2;
+  for (int attempt = 0; attempt < 3; ++attempt) {
+    s.ent = c->ent;
+    s.ent_sorted = c->ent_sorted;
+    s.ent_ub = c->ent_ub;
+    s.ub_cap = c->ent_ub_cap;
+    s.temp = c->sweep_temp;
+    s.temp_bytes = c->sweep_temp_bytes;
+    if (mode == 2) HIP_TRY(c, launch_sweep_plan(s, c->stream));
+    if (e0) HIP_TRY(c, hipEventRecord(e0, c->stream));
+    if (c->profiling) HIP_TRY(c, hipEventRecord(c->sw_ev[0], c->stream));
+    HIP_TRY(c, launch_sweep_count(s, mode, c->sw_total_dev, c->stream));
+    if (e1) HIP_TRY(c, hipEventRecord(e1, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    const volatile long long* tot = c->sw_total;
+    if (mode == 2 && (tot[2] & 8)) {
+      // upper-bound buffer too small (or beyond the budget: two passes); clear the flag and counters
+      const int64_t need = tot[1];
+      if (need > kUbBudget) {
+        mode = 0;
+      } else {
+        if ((rc = dalloc(c, &c->ent_ub, need + (need >> 3) + 4096))) return rc;
+        c->ent_ub_cap = need + (need >> 3) + 4096;
+      }
+      HIP_TRY(c, hipMemsetAsync(c->counters, 0, kNumCounters * sizeof(unsigned long long), c->stream));
+      HIP_TRY(c, hipMemsetAsync(c->errw, 0, kErrWords * sizeof(int), c->stream));
+      continue;
+    }
+    s.n_ent = tot[0];
+    break;
+  }
+  if (s.n_ent > c->ent_cap && (rc = reserve_entries(c, s.n_ent + (s.n_ent >> 3) + 4096))) return rc;
   s.ent = c->ent;
   s.ent_sorted = c->ent_sorted;
-  s.n_ent = n_ent;
   s.temp = c->sweep_temp;
   s.temp_bytes = c->sweep_temp_bytes;
-  HIP_TRY(c, launch_sweep_pairs(s, c->stream));
+  HIP_TRY(c, launch_sweep_pairs(s, mode, c->stream));
   c->sw_ev_rec = c->profiling;
   return FSLR_OK;
 }
@@ -506,6 +585,10 @@ static int query_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_
   const bool sweep = want == FSLR_ENGINE_SWEEP || (want == FSLR_ENGINE_AUTO && sweep_ok && c->last_full);
   c->last_engine = sweep ? FSLR_ENGINE_SWEEP : FSLR_ENGINE_WALK;
   if (c->profiling) HIP_TRY(c, hipEventRecord(c->ev[2], c->stream));
+  if (!sweep) {
+    int rc = ensure_walk_index(c);
+    if (rc) return rc;
+  }
   if (sweep) {
     int rc = sweep_impl(c, p, a_begin, a_end, g.ev_k0, g.ev_k1);
     if (rc) return rc;

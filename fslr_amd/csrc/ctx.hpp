@@ -17,6 +17,7 @@ struct fslr_ctx {
   int n_chroms = 0;
   int thr_mode = 0;
   bool reads_set = false, index_built = false, have_data_pos = false;
+  bool index_full = false;                 // the walk engine's index parts exist (qpos, backward ranges)
   int shard = 0, n_shards = 1;             // fslr_set_shard: A-side index data for this shard only
   int built_shard = 0, built_n_shards = 1;
   // device buffers
@@ -57,8 +58,11 @@ struct fslr_ctx {
   unsigned long long* diag = nullptr;        // FSLR_SECTION_PROF builds: per-read timing of the pair kernel
   int* errw = nullptr;     // [0..2] error, [3] max_fwd
   // position-sweep engine (sweep.hip)
-  long long* sw_tile = nullptr;             // [2 x tiles]: entries per 64-position tile, their exclusive scan
-  long long* sw_total = nullptr;            // [2] last tile's offset and count
+  long long* sw_tile = nullptr;             // [4 x tiles]: entries, their scan, pair tests, their scan
+  long long* sw_total = nullptr;            // [4] pinned host memory, device-mapped: entries, bound, flags
+  long long* sw_total_dev = nullptr;        // its device address
+  unsigned long long* ent_ub = nullptr;     // one-pass sweep output at upper-bound tile slots
+  int64_t ent_ub_cap = 0;
   int64_t sw_tiles = 0;
   unsigned long long* sw_wstat = nullptr;   // per-wave statistics slots of the sweep kernels
   int sw_wstat_waves = 0;
@@ -92,6 +96,11 @@ struct fslr_ctx {
 };
 
 namespace fslr {
+
+// builds the walk engine's index parts of a sweep-only index (capi.hip); no-op when present
+int ensure_walk_index(fslr_ctx* c);
+// {edge count, error code, max forward degree} of the last query through pinned memory; syncs
+int peek_counts(fslr_ctx* c, long long out[3]);
 
 
 inline int fail(fslr_ctx* c, int code, const std::string& msg) {

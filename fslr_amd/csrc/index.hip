@@ -345,6 +345,8 @@ struct TilePrefix {
   __device__ __forceinline__ unsigned long long incl(int t) const { return max_u64(group_excl[t / kGroup], loc[t]); }
 };
 
+// kBwd = false (the sweep engine): forward counts only, no pmax window (rng_s[q].y = -1)
+template <bool kBwd>
 __global__ __launch_bounds__(kRangeBlock) void k_ranges(const int4* __restrict__ idx4, int shard, int n_shards,
                                                         const int* __restrict__ s_start,
                                                         const unsigned long long* __restrict__ endkey,
@@ -360,7 +362,7 @@ __global__ __launch_bounds__(kRangeBlock) void k_ranges(const int4* __restrict__
   const int wp1 = min(q0 + kRangeSpan, ni);
   for (int t = threadIdx.x; t < w1 - w0; t += kRangeBlock) w_st[t] = s_start[w0 + t];
   // pmax over [w0, wp1): prefix of the tiles before w0, then a scan of the window's keys
-  {
+  if constexpr (kBwd) {
     constexpr int kPer = (kRangeSpan + kWin) / kRangeBlock;   // consecutive keys per thread
     unsigned long long k[kPer];
     unsigned long long m = 0ull;
@@ -413,6 +415,10 @@ __global__ __launch_bounds__(kRangeBlock) void k_ranges(const int4* __restrict__
       }
     }
     const int n_fwd = lo - q - 1;
+    if constexpr (!kBwd) {
+      rng_s[q] = make_int2(n_fwd, -1);
+      continue;
+    }
     // backward: first p in [cr.x, q) with pmax_p >= s (pmax non-decreasing inside a chromosome)
     const int lo_lim = max(cr.x, w0);
     lo = lo_lim;
@@ -478,7 +484,31 @@ hipError_t index_temp_bytes(int ni, size_t* bytes, hipStream_t s) {
   return hipSuccess;
 }
 
-hipError_t launch_build_index(const IndexBufs& b, int n, int ni, int n_chroms, hipStream_t s) {
+// the walk engine's part of the index (data-order path): the CSR -> sorted position map, the
+// tile prefix of end, and the backward scan ranges
+static hipError_t launch_walk_parts(const IndexBufs& b, int n, int ni, hipStream_t s, bool qpos_and_tiles) {
+  if (qpos_and_tiles) {
+    k_qpos_gather<<<grid_for((n + 63) / 64, 4), 256, 0, s>>>(b.rmeta, b.data_pos, b.vals, n, ni, b.shard, b.n_shards,
+                                                              b.qpos);
+    k_tile_max<<<grid_for(ni, kTile), kTile, 0, s>>>(b.endkey, ni, b.pmaxkey);
+  }
+  // pmaxkey: tile maxima [0, nt), local group prefixes [nt, 2 nt), group prefixes [2 nt, 2 nt + ng)
+  const int nt = (ni + kTile - 1) / kTile, ng = (nt + kGroup - 1) / kGroup;
+  unsigned long long *tmax = b.pmaxkey, *tloc = b.pmaxkey + nt, *grp = b.pmaxkey + 2 * nt;
+  k_tile_scan_local<<<ng, kGroup, 0, s>>>(tmax, nt, tloc, grp);
+  k_group_scan<<<1, kGroup, 0, s>>>(grp, ng);
+  k_ranges<true><<<(ni + kRangeSpan - 1) / kRangeSpan, kRangeBlock, 0, s>>>(b.idx4, b.shard, b.n_shards, b.s_start,
+                                                                            b.endkey, TilePrefix{tloc, grp}, b.crange,
+                                                                            ni, b.rng_s);
+  return hipGetLastError();
+}
+
+hipError_t launch_index_walk_parts(const IndexBufs& b, int n, int ni, hipStream_t s) {
+  if (ni <= 0) return hipSuccess;
+  return launch_walk_parts(b, n, ni, s, true);
+}
+
+hipError_t launch_build_index(const IndexBufs& b, int n, int ni, int n_chroms, bool full, hipStream_t s) {
   if (ni <= 0) return hipSuccess;
   hipError_t e;
   size_t tb = b.temp_bytes;
@@ -488,9 +518,13 @@ hipError_t launch_build_index(const IndexBufs& b, int n, int ni, int n_chroms, h
     k_chrom_scan<<<n_chroms, 1024, 0, s>>>(b.chist, ntl, b.crange);
     k_chrom_scatter<<<ntl, kTileThreads, 0, s>>>(b.dchrom, b.drec, b.dgate, b.chist, ni, ntl, b.idx4, b.idx_gate,
                                                  b.s_start, b.endkey, b.vals);
-    k_qpos_gather<<<grid_for((n + 63) / 64, 4), 256, 0, s>>>(b.rmeta, b.data_pos, b.vals, n, ni, b.shard, b.n_shards,
-                                                              b.qpos);
-    k_tile_max<<<grid_for(ni, kTile), kTile, 0, s>>>(b.endkey, ni, b.pmaxkey);
+    if (!full) {
+      // the sweep engine's index: records, gate words and forward counts
+      k_ranges<false><<<(ni + kRangeSpan - 1) / kRangeSpan, kRangeBlock, 0, s>>>(
+          b.idx4, b.shard, b.n_shards, b.s_start, b.endkey, TilePrefix{nullptr, nullptr}, b.crange, ni, b.rng_s);
+      return hipGetLastError();
+    }
+    return launch_walk_parts(b, n, ni, s, true);
   } else if (b.dchrom) {
     unsigned* k32 = reinterpret_cast<unsigned*>(b.keys2);
     e = hipcub::DeviceRadixSort::SortPairs(b.temp, tb, b.dchrom, k32, b.drec, b.idx4, ni, 0, bits_for(n_chroms), s);
@@ -506,14 +540,7 @@ hipError_t launch_build_index(const IndexBufs& b, int n, int ni, int n_chroms, h
     k_finish<true><<<grid_for(ni, kTile), kTile, 0, s>>>(b.idx4, b.keys2, b.rmeta, ni, b.idx_gate, b.s_start, b.endkey,
                                                          b.pmaxkey, b.qpos, b.shard, b.n_shards);
   }
-  // pmaxkey: tile maxima [0, nt), local group prefixes [nt, 2 nt), group prefixes [2 nt, 2 nt + ng)
-  const int nt = (ni + kTile - 1) / kTile, ng = (nt + kGroup - 1) / kGroup;
-  unsigned long long *tmax = b.pmaxkey, *tloc = b.pmaxkey + nt, *grp = b.pmaxkey + 2 * nt;
-  k_tile_scan_local<<<ng, kGroup, 0, s>>>(tmax, nt, tloc, grp);
-  k_group_scan<<<1, kGroup, 0, s>>>(grp, ng);
-  k_ranges<<<(ni + kRangeSpan - 1) / kRangeSpan, kRangeBlock, 0, s>>>(b.idx4, b.shard, b.n_shards, b.s_start, b.endkey, TilePrefix{tloc, grp},
-                                      b.crange, ni, b.rng_s);
-  return hipGetLastError();
+  return launch_walk_parts(b, n, ni, s, false);
 }
 
 hipError_t launch_set_thr(const int* thr, int4* iv, const int* qpos, int4* idx4, const int* data_pos,

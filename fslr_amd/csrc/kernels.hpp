@@ -101,7 +101,11 @@ struct IndexBufs {
 };
 // bytes of hipcub temp storage the index build needs for ni intervals
 hipError_t index_temp_bytes(int ni, size_t* bytes, hipStream_t s);
-hipError_t launch_build_index(const IndexBufs& b, int n_reads, int ni, int n_chroms, hipStream_t s);
+// full = false: only what the sweep engine reads (records, gate words, forward counts); applies to
+// the data-order path with <= 64 chromosomes (the other paths always build everything)
+hipError_t launch_build_index(const IndexBufs& b, int n_reads, int ni, int n_chroms, bool full, hipStream_t s);
+// the walk engine's parts of a sweep-only index (qpos, tile prefix, backward ranges)
+hipError_t launch_index_walk_parts(const IndexBufs& b, int n_reads, int ni, hipStream_t s);
 // thresholds into iv[k].w and (when the index exists) idx4[qpos[k]].z
 hipError_t launch_set_thr(const int* thr, int4* iv, const int* qpos, int4* idx4, const int* data_pos,
                           int4* drec, int ni, hipStream_t s);
@@ -155,8 +159,12 @@ struct SweepArgs {
   int a_begin, a_end;                 // reads whose pairs (as the lower rank A) are evaluated
   double qlen_cut, nal_cut;
   int4* lb;                           // [n_reads] length-gate ranges (launch_len_bounds)
-  long long* tile_cnt;                // [ceil(ni / 64)] match entries of each 64-position tile (count pass)
-  long long* tile_off;                // its exclusive scan: where the emit pass writes the tile's entries
+  long long* tile_cnt;                // [ceil(ni / 64)] match entries of each 64-position tile
+  long long* tile_off;                // its exclusive scan: the tile's place in `ent`
+  long long* tile_tests;              // [tiles] pair tests of the tile (its forward-range total)
+  long long* tile_ub;                 // their exclusive scan: the tile's upper-bound slot in ent_ub
+  unsigned long long* ent_ub;         // (one pass) entries at their tiles' upper-bound slots
+  long long ub_cap;
   unsigned long long* ent;            // [n_ent] match entries A << 39 | B << 14 | i << 7 | j, tile order
   unsigned long long* ent_sorted;     // [n_ent] grouped by A
   long long n_ent;                    // (emit / pairs) entries of the count pass
@@ -174,10 +182,13 @@ struct SweepArgs {
 };
 size_t sweep_temp_bytes(long long ent_cap, long long ni, hipStream_t s);
 int sweep_max_waves();
-// count pass + tile scan; *total_dev receives the entry count (device memory, read after a sync)
-hipError_t launch_sweep_count(const SweepArgs& a, long long* total_dev, hipStream_t s);
-// emit pass + grouping sort + per-read pair evaluation (a.n_ent from the count pass)
-hipError_t launch_sweep_pairs(const SweepArgs& a, hipStream_t s);
+// per tile: pair tests and their scan (the one-pass upper-bound slots)
+hipError_t launch_sweep_plan(const SweepArgs& a, hipStream_t s);
+// mode 2: the one-pass sweep (entries to ent_ub); mode 0: the count pass of the two-pass fallback.
+// Then the tile scan; total_dev[0..2] = entries, upper-bound total, overflow flags (read after a sync)
+hipError_t launch_sweep_count(const SweepArgs& a, int mode, long long* total_dev, hipStream_t s);
+// packs (mode 2) or writes (mode 0: emit pass) the entries to `ent`, groups them by A, evaluates the pairs
+hipError_t launch_sweep_pairs(const SweepArgs& a, int mode, hipStream_t s);
 
 // ---- edge-cap replay (cap.hip) --------------------------------------------------------------
 // per listed read: upper bound of its interval hits (sum over its intervals of the scan range)

@@ -25,6 +25,7 @@
 // Scope: thresholds >= 1 (overlap > 0) and no aln_size == 0 interval; other inputs take the walk
 // engine (capi.hip picks).
 #include <hipcub/hipcub.hpp>
+#include <type_traits>
 
 #include "fslr_hip.h"
 #include "kernels.hpp"
@@ -40,10 +41,6 @@ constexpr int kPerPass = 80;               // entries per partner partition of a
 constexpr int kEdgeStage = 256;            // staged edges per wave
 constexpr int kWsFields = 4;               // per-wave statistics slots
 
-__device__ __forceinline__ unsigned long long pack_entry(int a, int b, int i, int j) {
-  return (static_cast<unsigned long long>(a) << 39) | (static_cast<unsigned long long>(b) << 14) |
-         (static_cast<unsigned long long>(i) << 7) | static_cast<unsigned long long>(j);
-}
 __device__ __forceinline__ int entry_a(unsigned long long e) { return static_cast<int>(e >> 39); }
 // lane masks: bits above / up to position h (0 <= h < 64)
 __device__ __forceinline__ unsigned long long above(int h) { return h >= 63 ? 0ull : (~0ull << (h + 1)); }
@@ -63,24 +60,37 @@ __device__ __forceinline__ int part_of(int B, int npass) {
 // window is a few hundred consecutive positions, so these loads hit L1 / L2).  kEmit = false counts
 // the tile's entries (and the statistics); kEmit = true writes them at the tile's scanned offset.
 constexpr int kMapCap = 2048;              // items per map segment (a longer tile takes several)
+constexpr int kTileRun = 8;                // consecutive tiles per work item
 
-template <bool kEmit>
+// kMode 0: count the tile's entries (two-pass fallback), 1: write them at the tile's scanned offset
+// (two-pass fallback), 2: one pass — write them at the tile's upper-bound slot (its forward-range
+// total, the pair tests) and count them; k_compact then packs the tiles.
+template <int kMode>
 __global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
+  constexpr bool kEmit = kMode != 0;
+  constexpr bool kCount = kMode != 1;
   __shared__ int4 qa_all[kSwWaves][kWave];     // {end, thr, tag, qlo}
   __shared__ int4 qb_all[kSwWaves][kWave];     // {qhi, nlo, nhi, offv}
-  __shared__ unsigned char map_all[kSwWaves][kMapCap];
+  __shared__ unsigned char zf_all[kSwWaves][kWave];   // q's read has qlen2 == 0 (1) / n_alignments == 0 (2)
+  __shared__ unsigned char map_all[kSwWaves][kMapCap];          // item -> its lane (position q0 + mi)
   __shared__ unsigned long long st_all[kSwWaves][kEmit ? kWave : 1];
+  unsigned long long* const dst = kMode == 2 ? g.ent_ub : g.ent;
   const int lane = lane_id();
   const int wv = threadIdx.x >> 6;
   int4* QA = qa_all[wv];
   int4* QB = qb_all[wv];
+  unsigned char* ZF = zf_all[wv];
   unsigned char* MAP = map_all[wv];
   unsigned long long* ST = st_all[wv];
   unsigned long long w_tests = 0, w_hits = 0, w_ent = 0;
   const int nt = (g.ni + kWave - 1) / kWave;
   const int nw = gridDim.x * kSwWaves;
   const int wid = blockIdx.x * kSwWaves + wv;
-  for (int tile = wid; tile < nt; tile += nw) {
+  // tiles in chunks of kTileRun consecutive tiles per wave (a tile's forward window reaches into the
+  // next tile, whose records the same wave then finds in its caches), chunks dealt grid-stride
+  const int nchunks = (nt + kTileRun - 1) / kTileRun;
+  for (int chunk = wid; chunk < nchunks; chunk += nw)
+  for (int tile = chunk * kTileRun; tile < min(nt, (chunk + 1) * kTileRun); ++tile) {
     const int q0 = tile * kWave;
     const int q = q0 + lane;
     const bool qv = q < g.ni;
@@ -88,113 +98,195 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
     int4 rq = g.idx4[qc];
     const int nf = qv ? g.rng_s[qc].x : 0;
     const int4 lbq = g.lb[rq.w >> 6];            // the gate of q's read as integer ranges
+    const bool any_zero = __ballot(qv && (lbq.x < 0 || lbq.z < 0)) != 0ull;   // v == 0 (ZeroDivision)
     const int pre = wave_incl_scan(nf);
     const int ex = pre - nf;
     const int T = rdl(pre, kWave - 1);
     wave_lds_sync();
-    QA[lane] = make_int4(rq.y, rq.z, rq.w, lbq.x);
-    QB[lane] = make_int4(lbq.y, lbq.z, lbq.w, q + 1 - ex);   // item r of lane k is position r + offv_k
+    // lower bounds with v == 0 (lo < 0: partner 0 raises, [1, hi] passes) folded to 1
+    QA[lane] = make_int4(rq.y, rq.z, rq.w, lbq.x < 0 ? 1 : lbq.x);
+    QB[lane] = make_int4(lbq.y, lbq.z < 0 ? 1 : lbq.z, lbq.w, q + 1 - ex);   // item r of lane k: position r + offv_k
+    ZF[lane] = static_cast<unsigned char>((lbq.x < 0 ? 1 : 0) | (lbq.z < 0 ? 2 : 0));
     long long out = 0;                           // kEmit: next entry slot of this tile
-    if constexpr (kEmit) out = g.tile_off[tile];
+    if constexpr (kMode == 1) out = g.tile_off[tile];
+    if constexpr (kMode == 2) {
+      out = g.tile_ub[tile];
+      if (out + T > g.ub_cap) {                  // the upper-bound buffer is too small: grow + rerun
+        if (lane == 0) atomicOr(g.err + kErrOverflow, 8);
+        continue;
+      }
+    }
     int sn = 0, cnt = 0;                         // staged entries (kEmit) / entries of the tile
-    if constexpr (!kEmit) w_tests += static_cast<unsigned long long>(T);
+    if constexpr (kCount) w_tests += static_cast<unsigned long long>(T);
     for (int seg = 0; seg < T; seg += kMapCap) {
       const int se = min(T, seg + kMapCap);
       wave_lds_sync();
       for (int r = max(ex, seg); r < min(pre, se); ++r) MAP[r - seg] = static_cast<unsigned char>(lane);
       wave_lds_sync();
       // step loads: the mapped lane's offset, then the p-side record and gate word
-      auto step_load = [&](int base, int& mi, int4& b4, int4& rp, int2& gp) {
-        const int r = base + lane;
-        mi = r < se ? MAP[r - seg] : 0;
-        b4 = QB[mi];
-        const int p = r < se ? r + b4.w : q0;
-        rp = g.idx4[p];
-        gp = g.idx_gate[p];
+      struct Step {
+        int mi;
+        int4 b4, rp;
+        int2 gp;
       };
-      int mi_n, mi;
-      int4 b4_n, b4, rp_n, rp;
-      int2 gp_n, gp;
-      step_load(seg, mi_n, b4_n, rp_n, gp_n);
-      for (int base = seg; base < se; base += kWave) {
-        mi = mi_n;
-        b4 = b4_n;
-        rp = rp_n;
-        gp = gp_n;
-        if (base + kWave < se) step_load(base + kWave, mi_n, b4_n, rp_n, gp_n);
+      auto step_load = [&](int base, Step& t) {
+        const int r = base + lane;
+        t.mi = r < se ? MAP[r - seg] : 0;
+        t.b4 = QB[t.mi];
+        const int p = r < se ? r + t.b4.w : q0;
+        t.rp = g.idx4[p];
+        t.gp = g.idx_gate[p];
+      };
+      // one step of 64 interval pairs; kZero: some q of the tile has qlen2 or n_alignments == 0
+      // (only then can a pair raise ZeroDivisionError)
+      auto step = [&](auto zero_tag, int base, const Step& t) __attribute__((always_inline)) {
+        constexpr bool kZero = decltype(zero_tag)::value;
         const bool valid = base + lane < se;
-        const int4 a4 = QA[mi];
-        const int X = a4.z >> 6, Y = rp.w >> 6;
-        const bool hit = valid && X != Y;
+        const int4 a4 = QA[t.mi];
+        const int X = a4.z >> 6, Y = t.rp.w >> 6;
+        const bool hit = valid & (X != Y);
         // calculate_overlap >= overlap for both intervals: start_p >= start_q, start_p <= end_q
-        const int o = min(a4.x, rp.y) - rp.x;
-        const bool match = o >= max(a4.y, rp.z);
+        const int o = min(a4.x, t.rp.y) - t.rp.x;
+        const bool match = o >= max(a4.y, t.rp.z);
         // different_lengths_or_alignments: passes when either ratio is close (idx_gate word of p)
-        const int q2 = gp.x, n2 = gp.y & 0xFFFFFF;
-        const int qlo = a4.w, qhi = b4.x, nlo = b4.y, nhi = b4.z;
-        const bool pq = q2 >= (qlo < 0 ? 1 : qlo) && q2 <= qhi;
-        const bool zd = hit && ((qlo < 0 && q2 == 0) || (!pq && nlo < 0 && n2 == 0));
-        const bool lenok = pq || (n2 >= (nlo < 0 ? 1 : nlo) && n2 <= nhi);
-        const bool emit = hit && !zd && lenok && match;
+        const int q2 = t.gp.x, n2 = t.gp.y & 0xFFFFFF;
+        const int qlo = a4.w, qhi = t.b4.x, nlo = t.b4.y, nhi = t.b4.z;
+        const bool pq = (q2 >= qlo) & (q2 <= qhi);
+        const bool lenok = pq | ((n2 >= nlo) & (n2 <= nhi));
+        bool emit = hit & lenok & match;
+        if constexpr (kZero) {
+          const unsigned zf = ZF[t.mi];
+          const bool zd = hit & ((((zf & 1u) != 0) & (q2 == 0)) | (!pq & ((zf & 2u) != 0) & (n2 == 0)));
+          emit = emit & !zd;
+          if (__ballot(zd)) raise_zd(g.err, zd, min(X, Y), max(X, Y));
+        }
         const unsigned long long em = __ballot(emit);
         const int ne = __popcll(em);
-        if constexpr (!kEmit) {
-          if (__ballot(zd)) raise_zd(g.err, zd, min(X, Y), max(X, Y));
+        if constexpr (kCount) {
           w_hits += __popcll(__ballot(hit));
           cnt += ne;
-        } else if (ne) {
+        }
+        if (kEmit && ne) {
           if (sn + ne > kWave) {
             wave_lds_sync();
-            if (lane < sn) g.ent[out + lane] = ST[lane];
+            if (lane < sn) dst[out + lane] = ST[lane];
             out += sn;
             sn = 0;
             wave_lds_sync();
           }
           if (emit) {
-            const int iq = a4.z & 63, jp = rp.w & 63;
-            ST[sn + mbcnt(em)] = X < Y ? pack_entry(X, Y, iq, jp) : pack_entry(Y, X, jp, iq);
+            // A << 39 | B << 14 | i << 7 | j as two dwords
+            const int A = min(X, Y), B = max(X, Y);
+            const int iq = a4.z & 63, jp = t.rp.w & 63;
+            const unsigned ij = X < Y ? static_cast<unsigned>(iq << 7 | jp) : static_cast<unsigned>(jp << 7 | iq);
+            const unsigned lo = (static_cast<unsigned>(B) << 14) | ij;
+            const unsigned hi = (static_cast<unsigned>(A) << 7) | (static_cast<unsigned>(B) >> 18);
+            ST[sn + mbcnt(em)] = (static_cast<unsigned long long>(hi) << 32) | lo;
           }
           sn += ne;
         }
-      }
+      };
+      auto run_steps = [&](auto zero_tag) __attribute__((always_inline)) {
+        // double buffer unrolled by two: the loads of the next step are in flight while one is tested
+        Step s0, s1;
+        step_load(seg, s0);
+        for (int base = seg; base < se; base += 2 * kWave) {
+          const bool two = base + kWave < se;
+          if (two) step_load(base + kWave, s1);
+          step(zero_tag, base, s0);
+          if (!two) break;
+          if (base + 2 * kWave < se) step_load(base + 2 * kWave, s0);
+          step(zero_tag, base + kWave, s1);
+        }
+      };
+      if (any_zero) run_steps(std::true_type{});
+      else run_steps(std::false_type{});
     }
     if constexpr (kEmit) {
       if (sn > 0) {
         wave_lds_sync();
-        if (lane < sn) g.ent[out + lane] = ST[lane];
+        if (lane < sn) dst[out + lane] = ST[lane];
       }
-    } else {
+    }
+    if constexpr (kCount) {
       if (lane == 0) g.tile_cnt[tile] = cnt;
       w_ent += static_cast<unsigned long long>(cnt);
     }
   }
-  if constexpr (!kEmit) {
+  if constexpr (kCount) {
     // statistics: plain stores into this wave's slots, summed by k_sum_slots
     const unsigned long long f = lane == 0 ? w_tests : lane == 1 ? w_hits : w_ent;
     if (lane < 3) g.wstat[static_cast<long long>(wid) * kWsFields + lane] = f;
   }
 }
 
-// Sum (fields 0..2) / max (field 3) of the per-wave slots [f0, f1) into counters / an err word.
+// Sum (fields 0..2) / max (field 3) of the per-wave slots [f0, f1) into counters / an err word: each
+// block reduces a slice of waves, then one atomic per field and block (few blocks: no contention).
+constexpr int kSumBlocks = 32;
 __global__ __launch_bounds__(256) void k_sum_slots(const unsigned long long* __restrict__ ws, int nwaves, int f0,
                                                     int f1, int c0, int c1, int c2, unsigned long long* counters,
                                                     int* err_max) {
   __shared__ unsigned long long part[256][kWsFields];
   unsigned long long acc[kWsFields] = {0, 0, 0, 0};
-  for (int w = threadIdx.x; w < nwaves; w += 256)
+  const int per = (nwaves + gridDim.x - 1) / gridDim.x;
+  const int w0 = blockIdx.x * per, w1 = min(w0 + per, nwaves);
+  for (int w = w0 + threadIdx.x; w < w1; w += 256)
     for (int f = f0; f < f1; ++f) {
       const unsigned long long x = ws[static_cast<long long>(w) * kWsFields + f];
       acc[f] = (f == 3) ? (acc[f] > x ? acc[f] : x) : acc[f] + x;
     }
   for (int f = 0; f < kWsFields; ++f) part[threadIdx.x][f] = acc[f];
   __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o)
+      for (int f = 0; f < kWsFields; ++f) {
+        const unsigned long long x = part[threadIdx.x + o][f];
+        part[threadIdx.x][f] = f == 3 ? (part[threadIdx.x][f] > x ? part[threadIdx.x][f] : x) : part[threadIdx.x][f] + x;
+      }
+    __syncthreads();
+  }
   if (threadIdx.x < kWsFields) {
     const int f = threadIdx.x;
-    unsigned long long r = 0;
-    for (int t = 0; t < 256; ++t) r = f == 3 ? (r > part[t][f] ? r : part[t][f]) : r + part[t][f];
+    const unsigned long long r = part[0][f];
     const int dst = f == 0 ? c0 : f == 1 ? c1 : c2;
-    if (f < 3 && f >= f0 && f < f1 && dst >= 0) counters[dst] += r;
-    if (f == 3 && f >= f0 && f < f1 && err_max) *err_max = max(*err_max, static_cast<int>(r));
+    if (f < 3 && f >= f0 && f < f1 && dst >= 0 && r) atomicAdd(&counters[dst], r);
+    if (f == 3 && f >= f0 && f < f1 && err_max && r) atomicMax(err_max, static_cast<int>(r));
+  }
+}
+
+// entries of the count pass: last tile offset + last tile count; (one-pass) also the upper-bound
+// total and the overflow flag, for the host
+__global__ void k_total(const long long* __restrict__ off, const long long* __restrict__ cnt,
+                        const long long* __restrict__ ub, const long long* __restrict__ tests, const int* err, int nt,
+                        long long* total) {
+  if (threadIdx.x == 0) {
+    total[0] = off[nt - 1] + cnt[nt - 1];
+    total[1] = ub ? ub[nt - 1] + tests[nt - 1] : 0;
+    total[2] = err ? err[kErrOverflow] : 0;
+  }
+}
+
+// pair tests of each tile: the sum of its positions' forward counts (an upper bound of its entries)
+__global__ __launch_bounds__(256) void k_tile_tests(const int2* __restrict__ rng_s, int ni, long long* __restrict__ tests) {
+  const int nt = (ni + kWave - 1) / kWave;
+  const int lane = lane_id();
+  for (int t = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; t < nt; t += (gridDim.x * blockDim.x) >> 6) {
+    const int q = t * kWave + lane;
+    int v = q < ni ? rng_s[q].x : 0;
+    v = wave_incl_scan(v);
+    if (lane == kWave - 1) tests[t] = v;
+  }
+}
+
+// pack each tile's entries from its upper-bound slot to its scanned offset (one wave per tile)
+__global__ __launch_bounds__(256) void k_compact(const unsigned long long* __restrict__ src,
+                                                 const long long* __restrict__ ub, const long long* __restrict__ off,
+                                                 const long long* __restrict__ cnt, int nt,
+                                                 unsigned long long* __restrict__ dst) {
+  const int lane = lane_id();
+  for (int t = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; t < nt; t += (gridDim.x * blockDim.x) >> 6) {
+    const long long n = cnt[t], a = ub[t], b = off[t];
+    for (long long k = lane; k < n; k += kWave) dst[b + k] = src[a + k];
   }
 }
 
@@ -330,16 +422,19 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
         mine = mine && !full;
         bool isnew;
         const int h = insert(mine, static_cast<unsigned>(B), static_cast<unsigned>(B), isnew);
+        int lbn = 0;
         if (isnew) {
           CNT[h] = 0u;
           RM[h] = make_uint2(0u, 0u);
           CM[h] = make_uint2(0u, 0u);
+          lbn = g.rmeta[B].y & 0xffff;
         }
         const unsigned long long nm = __ballot(isnew);
         if (isnew) MP[uniq + mbcnt(nm)] = static_cast<unsigned short>(h);
         uniq += __popcll(nm);
         wave_lds_sync();
         record(mine, h, i, j);
+        if (isnew) atomicOr(&CNT[h], static_cast<unsigned>(lbn) << 16);   // bits 16..22: L_B
       }
       if (full_any && lane == 0) atomicOr(g.err + kErrOverflow, 4);
       wave_lds_sync();
@@ -349,7 +444,7 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
         const int B = static_cast<int>(KEY[h]);
         const unsigned st = act ? CNT[h] : 0u;
         int I = static_cast<int>(st & 0xFFFFu);
-        const int LB = act ? (g.rmeta[B].y & 0xffff) : 0;
+        const int LB = static_cast<int>((st >> 16) & 127u);
         unsigned long long cm = __ballot(act && (st >> 31));
         while (cm) {
           const int c = __builtin_ctzll(cm);
@@ -440,16 +535,19 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
         const unsigned key = (static_cast<unsigned>(r) << 24) | static_cast<unsigned>(B);
         bool isnew;
         const int h = insert(act, key, key, isnew);
+        int lbn = 0;
         if (isnew) {
           CNT[h] = 0u;
           RM[h] = make_uint2(0u, 0u);
           CM[h] = make_uint2(0u, 0u);
+          lbn = g.rmeta[B].y & 0xffff;             // L_B, in flight while the masks are recorded
         }
         const unsigned long long nm = __ballot(isnew);
         if (isnew) MP[uniq + mbcnt(nm)] = static_cast<unsigned short>(h);
         uniq += __popcll(nm);
         wave_lds_sync();
         record(act, h, i, j);
+        if (isnew) atomicOr(&CNT[h], static_cast<unsigned>(lbn) << 16);   // bits 16..22: L_B
       }
       if (h0 && v0) {
         RUNA[r0] = entry_a(e0);
@@ -470,7 +568,7 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
         const int B = static_cast<int>(key & 0xFFFFFFu);
         const unsigned st = act ? CNT[h] : 0u;
         int I = static_cast<int>(st & 0xFFFFu);
-        const int LB = act ? (g.rmeta[B].y & 0xffff) : 0;
+        const int LB = static_cast<int>((st >> 16) & 127u);
         const int A = RUNA[r], LA = RUNL[r];
         unsigned long long cm = __ballot(act && (st >> 31));
         while (cm) {
@@ -538,13 +636,18 @@ int resident_blocks(K kernel) {
   return cus * per_cu;
 }
 
-int blocks_count() { static const int b = resident_blocks(k_sweep<false>); return b; }
-int blocks_emit() { static const int b = resident_blocks(k_sweep<true>); return b; }
+int blocks_mode(int m) {
+  static const int b0 = resident_blocks(k_sweep<0>), b1 = resident_blocks(k_sweep<1>), b2 = resident_blocks(k_sweep<2>);
+  return m == 0 ? b0 : m == 1 ? b1 : b2;
+}
 int blocks_pairs() { static const int b = resident_blocks(k_sweep_pairs); return b; }
+int tiles_of(const SweepArgs& a) { return static_cast<int>((static_cast<long long>(a.ni) + kWave - 1) / kWave); }
 
 }  // namespace
 
-int sweep_max_waves() { return std::max(std::max(blocks_count(), blocks_emit()), blocks_pairs()) * kSwWaves; }
+int sweep_max_waves() {
+  return std::max(std::max(blocks_mode(0), blocks_mode(1)), std::max(blocks_mode(2), blocks_pairs())) * kSwWaves;
+}
 
 size_t sweep_temp_bytes(long long ent_cap, long long ni, hipStream_t s) {
   size_t a = 0, b = 0;
@@ -557,33 +660,44 @@ size_t sweep_temp_bytes(long long ent_cap, long long ni, hipStream_t s) {
   return std::max(a, b);
 }
 
-hipError_t launch_sweep_count(const SweepArgs& a, long long* total_dev, hipStream_t s) {
-  const int nt = static_cast<int>((static_cast<long long>(a.ni) + kWave - 1) / kWave);
-  if (nt == 0) return hipMemsetAsync(total_dev, 0, sizeof(long long), s);
-  const int blocks = std::min(blocks_count(), (nt + kSwWaves - 1) / kSwWaves);
+hipError_t launch_sweep_plan(const SweepArgs& a, hipStream_t s) {
+  const int nt = tiles_of(a);
+  if (nt == 0) return hipSuccess;
+  k_tile_tests<<<grid_for(static_cast<long long>(nt) * kWave, 256, 4096), 256, 0, s>>>(a.rng_s, a.ni, a.tile_tests);
+  size_t tb = a.temp_bytes;
+  return hipcub::DeviceScan::ExclusiveSum(a.temp, tb, a.tile_tests, a.tile_ub, nt, s);
+}
+
+hipError_t launch_sweep_count(const SweepArgs& a, int mode, long long* total_dev, hipStream_t s) {
+  const int nt = tiles_of(a);
+  if (nt == 0) return hipMemsetAsync(total_dev, 0, 3 * sizeof(long long), s);
+  const int blocks = std::min(blocks_mode(mode), (nt + kSwWaves - 1) / kSwWaves);
   if (blocks * kSwWaves > a.wstat_waves) return hipErrorInvalidValue;
-  if (a.ev[0]) (void)hipEventRecord(a.ev[0], s);
-  k_sweep<false><<<blocks, kSwBlock, 0, s>>>(a);
-  k_sum_slots<<<1, 256, 0, s>>>(a.wstat, blocks * kSwWaves, 0, 3, kSwTests, kCand, kMatchEntries, a.counters,
-                                nullptr);
+  if (mode == 2)
+    k_sweep<2><<<blocks, kSwBlock, 0, s>>>(a);
+  else
+    k_sweep<0><<<blocks, kSwBlock, 0, s>>>(a);
+  k_sum_slots<<<kSumBlocks, 256, 0, s>>>(a.wstat, blocks * kSwWaves, 0, 3, kSwTests, kCand, kMatchEntries,
+                                         a.counters, nullptr);
   if (a.ev[1]) (void)hipEventRecord(a.ev[1], s);
   size_t tb = a.temp_bytes;
   hipError_t e = hipcub::DeviceScan::ExclusiveSum(a.temp, tb, a.tile_cnt, a.tile_off, nt, s);
   if (e != hipSuccess) return e;
-  // total = last offset + last count
-  e = hipMemcpyAsync(total_dev, a.tile_off + nt - 1, sizeof(long long), hipMemcpyDeviceToDevice, s);
-  if (e != hipSuccess) return e;
-  e = hipMemcpyAsync(total_dev + 1, a.tile_cnt + nt - 1, sizeof(long long), hipMemcpyDeviceToDevice, s);
-  if (e != hipSuccess) return e;
+  k_total<<<1, 64, 0, s>>>(a.tile_off, a.tile_cnt, mode == 2 ? a.tile_ub : nullptr, a.tile_tests, a.err, nt, total_dev);
   return hipGetLastError();
 }
 
-hipError_t launch_sweep_pairs(const SweepArgs& a, hipStream_t s) {
-  const int nt = static_cast<int>((static_cast<long long>(a.ni) + kWave - 1) / kWave);
+hipError_t launch_sweep_pairs(const SweepArgs& a, int mode, hipStream_t s) {
+  const int nt = tiles_of(a);
   if (a.ev[2]) (void)hipEventRecord(a.ev[2], s);
   if (a.n_ent > 0) {
-    const int be = std::min(blocks_emit(), (nt + kSwWaves - 1) / kSwWaves);
-    k_sweep<true><<<be, kSwBlock, 0, s>>>(a);
+    if (mode == 2) {
+      k_compact<<<grid_for(static_cast<long long>(nt) * kWave, 256, 8192), 256, 0, s>>>(a.ent_ub, a.tile_ub, a.tile_off,
+                                                                                      a.tile_cnt, nt, a.ent);
+    } else {
+      const int be = std::min(blocks_mode(1), (nt + kSwWaves - 1) / kSwWaves);
+      k_sweep<1><<<be, kSwBlock, 0, s>>>(a);
+    }
     if (a.ev[3]) (void)hipEventRecord(a.ev[3], s);
     size_t tb = a.temp_bytes;
     const int end_bit = 39 + bits_for(std::max(1, a.n_reads - 1));
@@ -598,7 +712,8 @@ hipError_t launch_sweep_pairs(const SweepArgs& a, hipStream_t s) {
   const int blocks = static_cast<int>(std::max(1ll, std::min<long long>(blocks_pairs(), (chunks + kSwWaves - 1) / kSwWaves)));
   if (blocks * kSwWaves > a.wstat_waves) return hipErrorInvalidValue;
   k_sweep_pairs<<<blocks, kSwBlock, 0, s>>>(a);
-  k_sum_slots<<<1, 256, 0, s>>>(a.wstat, blocks * kSwWaves, 2, 4, -1, -1, kMatchedPairs, a.counters, a.err + 3);
+  k_sum_slots<<<kSumBlocks, 256, 0, s>>>(a.wstat, blocks * kSwWaves, 2, 4, -1, -1, kMatchedPairs, a.counters,
+                                         a.err + 3);
   return hipGetLastError();
 }
 
