@@ -16,15 +16,17 @@ overall_jaccard_similarity runs: the unit SURVEY.md §8d defines and the referen
 measured 2.27e4 pairs/s counts) of the whole job per second.  Candidate
 pairs (gate-rejected ones included) and the dense-equivalent rate are secondary fields.
 
-``roofline``: the dominant kernel is the pair kernel (query_kernel).  Its algorithmic
-bytes per launch are those of this design's walk: every walked index
-record (16-B interval record + 8-B gate word) read once, each query read's header,
-length-gate bounds and forward degree, each of its intervals' sorted position, row and
-scan range, and the edge / deferred-list output.  ``achieved`` = those bytes ÷ the
-mean duration of the timed launches, measured with hipEvents the library records
-around each launch on its stream (fslr_get_pair_kernel_times).  ``traffic`` = HBM
-bytes per launch from rocprofv3 PMC counters (tools/pmc_traffic.py), used only when
-that summary was measured on the current pair-kernel sources.
+``roofline``: the dominant kernel of the engine that ran.  Sweep engine (default): the
+position sweep k_sweep<2>; its algorithmic bytes per launch are every
+sorted position's index record, gate word and forward count and its read's gate ranges
+read once (48 B), plus each match entry written (8 B).  Walk engine: query_kernel, every
+walked index record (16-B record + 8-B gate word) read once, each query read's header,
+gate bounds and forward degree, each of its intervals' sorted position, row and scan
+range, and the edge / deferred-list output.  ``achieved`` = those bytes ÷ the mean
+duration of the timed launches, measured with hipEvents the library records around
+that one launch on its stream (fslr_get_pair_kernel_times).  ``traffic`` = HBM bytes
+per launch from rocprofv3 PMC counters (tools/pmc_traffic.py), used only when that
+summary was measured on the current sources of that kernel.
 
 Prints ONE JSON line on rank 0.
 """
@@ -43,8 +45,12 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK = 8.0e12          # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
 TRAFFIC_JSON = os.path.join(REPO, 'profiles', 'pmc_traffic_latest.json')
-# bytes per walked record / per query read / per query interval / per edge / per deferred entry
+# walk engine: bytes per walked record / per query read / per query interval / per edge / per deferred entry
 B_WALK, B_READ, B_IVL, B_EDGE, B_DEFER = 24, 8 + 16 + 4, 4 + 12 + 8, 8 + 2, 8
+# sweep engine: bytes per sorted position (record, gate word, forward count, read gate ranges) / per entry
+B_POS, B_ENT = 16 + 8 + 8 + 16, 8
+KERNEL_SOURCES = {'sweep': ('sweep.hip', 'wave.hpp', 'kernels.hpp'), 'walk': ('query.hip', 'kernels.hpp')}
+KERNEL_NAME = {'sweep': 'k_sweep<2>', 'walk': 'query_kernel<0, false>'}
 # the reference's own rate on this config: 33,020,021 Jaccard-evaluated
 # pairs in 1454.0 s of query_interval_trees, 1 core of the survey container, pure Python
 REFERENCE_PY = {'value': 33_020_021 / 1454.0, 'unit': 'Jaccard-evaluated read pairs/s', 'cores': 1,
@@ -52,11 +58,11 @@ REFERENCE_PY = {'value': 33_020_021 / 1454.0, 'unit': 'Jaccard-evaluated read pa
                 'sample': 'reference cluster.py, 1M reads x 1-16, query_interval_trees stage (BASELINE.md)'}
 
 
-def kernel_source_hash():
-    """sha256 of the pair-kernel sources: ties a committed PMC summary to the code it measured."""
+def kernel_source_hash(engine='sweep'):
+    """sha256 of the dominant kernel's sources: ties a committed PMC summary to the code it measured."""
     import hashlib
     h = hashlib.sha256()
-    for f in ('query.hip', 'kernels.hpp'):
+    for f in KERNEL_SOURCES[engine]:
         with open(os.path.join(REPO, 'fslr_amd', 'csrc', f), 'rb') as fh:
             h.update(fh.read())
     return h.hexdigest()[:16]
@@ -203,8 +209,15 @@ def main():
     own = shard_of(np.arange(csr.n_reads), world) == rank if world > 1 else np.ones(csr.n_reads, bool)
     q_reads = int(own.sum())
     q_ivls = int(np.diff(csr.read_off)[own].sum())
-    algo_bytes = (B_WALK * st['walked_records'] + B_READ * q_reads + B_IVL * q_ivls + B_EDGE * st['n_edges'] +
-                  B_DEFER * st['deferred'])
+    if st['engine'] == 'sweep':
+        algo_bytes = B_POS * csr.n_intervals + B_ENT * st['match_entries']
+        algo_model = (f'{B_POS} B x sorted positions ({csr.n_intervals}: record, gate word, forward count, read gate '
+                      f'ranges) + {B_ENT} B x match entries written ({st["match_entries"]})')
+    else:
+        algo_bytes = (B_WALK * st['walked_records'] + B_READ * q_reads + B_IVL * q_ivls + B_EDGE * st['n_edges'] +
+                      B_DEFER * st['deferred'])
+        algo_model = (f'{B_WALK} B x walked records ({st["walked_records"]}) + {B_READ} B x query reads + {B_IVL} B x '
+                      'query intervals + {B_EDGE} B x edges + {B_DEFER} B x deferred entries')
     cs = counted if counted is not None else st        # the walk engine's counts of this input
     tot = torch.tensor([elapsed, float(cs['evaluated_pairs']), float(cs['jaccard_evals']), float(st['n_edges']),
                         float(st['max_fwd'])], dtype=torch.float64, device=dev if backend == 'nccl' else 'cpu')
@@ -234,8 +247,8 @@ def main():
     if world == 1 and args.traffic_json and os.path.exists(args.traffic_json):
         with open(args.traffic_json) as fh:
             tj = json.load(fh)
-        if tj.get('source_hash') == kernel_source_hash():
-            traffic = tj.get('query_kernel_hbm_bytes_per_launch')
+        if tj.get('source_hash') == kernel_source_hash(st['engine']) and tj.get('kernel') == KERNEL_NAME[st['engine']]:
+            traffic = tj.get('hbm_bytes_per_launch', tj.get('query_kernel_hbm_bytes_per_launch'))
             traffic_src = os.path.relpath(args.traffic_json, REPO)
 
     # transfers around the device path (not in `value`): CSR upload before, labels / edges after
@@ -290,9 +303,15 @@ def main():
                 'candidate_pairs_per_step': int(pairs),
                 'candidate_pairs_per_s': pairs / (elapsed / args.steps),
                 'edges': int(n_edges), 'max_fwd_degree': max_fwd,
+                'engine': st['engine'],
                 'kernel_stats_rank0': {k: int(st[k]) for k in ('candidates', 'walked_records', 'overflow_candidates',
                                                                'gather_pairs', 'match_entries', 'matched_pairs',
-                                                               'deferred')},
+                                                               'deferred', 'pair_tests')},
+                'interval_pair_tests_per_s': st['pair_tests'] / (elapsed / args.steps) if st['engine'] == 'sweep'
+                else None,
+                'unit_count_source': 'walk engine run on the same input before timing (its seen-set counts the '
+                                     'pairs whose predicate is evaluated; the sweep decides the same pairs, '
+                                     'DESIGN.md §4)' if world == 1 else 'walk engine, per shard',
                 'dense_equivalent_pairs_per_s': (n * (n - 1) / 2) / (elapsed / args.steps),
                 'parallelism': f'query-read shards x{world} (64-rank blocks round robin) + RCCL label all_gather'
                 if world > 1 else 'single GPU',
@@ -300,7 +319,7 @@ def main():
             },
             'roofline': {
                 'bound': 'hbm',
-                'kernel': 'query_kernel',
+                'kernel': KERNEL_NAME[st['engine']],
                 'achieved': achieved / 1e9,
                 'peak': HBM_PEAK / 1e9,
                 'unit': 'GB/s',
@@ -311,9 +330,7 @@ def main():
                 'kernel_ms': kernel_ms,
                 'kernel_launches_timed': int(kern.size),
                 'algo_bytes_per_launch': int(algo_bytes),
-                'algo_bytes_model': f'{B_WALK} B x walked records ({st["walked_records"]}) + {B_READ} B x query '
-                                    f'reads + {B_IVL} B x query intervals + {B_EDGE} B x edges + {B_DEFER} B x '
-                                    'deferred entries',
+                'algo_bytes_model': algo_model,
                 'phase_ms_last_step': lib_t,
             },
             'cpu_baseline': cpu,

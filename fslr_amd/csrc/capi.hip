@@ -470,10 +470,10 @@ static int sweep_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_
     s.temp = c->sweep_temp;
     s.temp_bytes = c->sweep_temp_bytes;
     if (mode == 2) HIP_TRY(c, launch_sweep_plan(s, c->stream));
-    if (e0) HIP_TRY(c, hipEventRecord(e0, c->stream));
+    s.k0 = e0;                                       // the pair-kernel ring: the sweep kernel alone
+    s.k1 = e1;
     if (c->profiling) HIP_TRY(c, hipEventRecord(c->sw_ev[0], c->stream));
     HIP_TRY(c, launch_sweep_count(s, mode, c->sw_total_dev, c->stream));
-    if (e1) HIP_TRY(c, hipEventRecord(e1, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     const volatile long long* tot = c->sw_total;
     if (mode == 2 && (tot[2] & 8)) {

@@ -179,6 +179,7 @@ struct SweepArgs {
   unsigned long long* wstat;          // per-wave statistics slots [waves x 4] (no contended atomics)
   int wstat_waves;
   hipEvent_t ev[5];                   // (profiling) count | scan | emit | sort | pairs boundaries, or null
+  hipEvent_t k0, k1;                  // (profiling) around the sweep kernel launch alone, or null
 };
 size_t sweep_temp_bytes(long long ent_cap, long long ni, hipStream_t s);
 int sweep_max_waves();

@@ -673,10 +673,12 @@ hipError_t launch_sweep_count(const SweepArgs& a, int mode, long long* total_dev
   if (nt == 0) return hipMemsetAsync(total_dev, 0, 3 * sizeof(long long), s);
   const int blocks = std::min(blocks_mode(mode), (nt + kSwWaves - 1) / kSwWaves);
   if (blocks * kSwWaves > a.wstat_waves) return hipErrorInvalidValue;
+  if (a.k0) (void)hipEventRecord(a.k0, s);
   if (mode == 2)
     k_sweep<2><<<blocks, kSwBlock, 0, s>>>(a);
   else
     k_sweep<0><<<blocks, kSwBlock, 0, s>>>(a);
+  if (a.k1) (void)hipEventRecord(a.k1, s);
   k_sum_slots<<<kSumBlocks, 256, 0, s>>>(a.wstat, blocks * kSwWaves, 0, 3, kSwTests, kCand, kMatchEntries,
                                          a.counters, nullptr);
   if (a.ev[1]) (void)hipEventRecord(a.ev[1], s);

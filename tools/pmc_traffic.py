@@ -38,7 +38,7 @@ def collect(root, kernel):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('root')
-    ap.add_argument('--kernel', default='query_kernel<0, false>')
+    ap.add_argument('--kernel', default='k_sweep<2>')
     ap.add_argument('-o', '--out', default=None)
     ap.add_argument('--source-hash', default=None, help='hash of the kernel sources the counters were taken on')
     args = ap.parse_args()
@@ -49,7 +49,7 @@ def main():
     write = c.get('WRITE_SIZE', 0.0) * 1024.0
     out = {
         'kernel': args.kernel,
-        'query_kernel_hbm_bytes_per_launch': 2.0 * fetch + write,
+        'hbm_bytes_per_launch': 2.0 * fetch + write,
         'fetch_bytes_raw': fetch,
         'fetch_bytes_corrected_x2': 2.0 * fetch,
         'write_bytes': write,
