@@ -13,7 +13,7 @@ import numpy as np
 
 LIB_PATH = os.environ.get('FSLR_LIB') or os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libfslr_hip.so')
 
-ABI_VERSION = 3          # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
+ABI_VERSION = 4          # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
 FSLR_OK, FSLR_ERR_ZERO_DIVISION, FSLR_ERR_INVALID, FSLR_ERR_HIP, FSLR_ERR_NOMEM, FSLR_ERR_STATE = range(6)
 FSLR_MAX_L = 64
 FSLR_MAX_READS = 1 << 25
@@ -31,7 +31,7 @@ EXPORTED = ['fslr_abi_version', 'fslr_last_error', 'fslr_ctx_create', 'fslr_ctx_
             'fslr_get_labels',
             'fslr_get_fwd_degree', 'fslr_get_edges', 'fslr_labels_device_ptr', 'fslr_copy_labels_device',
             'fslr_copy_fwd_device', 'fslr_union_pairs', 'fslr_finalize_labels', 'fslr_apply_edge_cap',
-            'fslr_get_pair_kernel_times']
+            'fslr_get_pair_kernel_times', 'fslr_set_chrom_filter', 'fslr_sweep_partition', 'fslr_sweep_evaluate']
 
 
 class HipUnavailable(RuntimeError):
@@ -130,6 +130,10 @@ def load(path: str = LIB_PATH):
         'fslr_finalize_labels': (ctypes.c_int, [vp]),
         'fslr_apply_edge_cap': (ctypes.c_int, [vp, i32, ctypes.POINTER(CapStats)]),
         'fslr_get_pair_kernel_times': (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_float), i32]),
+        'fslr_set_chrom_filter': (ctypes.c_int, [vp, vp]),
+        'fslr_sweep_partition': (ctypes.c_int, [vp, ctypes.POINTER(Params), i32, i32, vp, i64,
+                                                ctypes.POINTER(ctypes.c_int64)]),
+        'fslr_sweep_evaluate': (ctypes.c_int, [vp, ctypes.POINTER(Params), vp, i64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -236,6 +240,47 @@ class Context:
         """Query shard `shard` of `n_shards` (rank blocks of 64 dealt round robin; fslr_query_shard)."""
         p = self._params(qlen_cut, nal_cut, pass_table, edge_threshold)
         self._check(self._L.fslr_query_shard(self._h, ctypes.byref(p), int(shard), int(n_shards)))
+
+    # -- multi-GPU sweep (fslr_hip.h fslr_set_chrom_filter / fslr_sweep_partition / _evaluate) ----
+    def set_chrom_filter(self, owned):
+        """Index only the chromosomes with ``owned[c]`` true at the next build_index (None: all)."""
+        if owned is None:
+            self._check(self._L.fslr_set_chrom_filter(self._h, None))
+            return
+        o = np.ascontiguousarray(np.asarray(owned, dtype=bool).astype(np.uint8))
+        self._check(self._L.fslr_set_chrom_filter(self._h, _ptr(o)))
+
+    def sweep_partition(self, qlen_cut, nal_cut, pass_table, n_dest, block_shift, dst, edge_threshold=10):
+        """Sweep the (filtered) index and write the match entries grouped by destination
+        (a >> block_shift) % n_dest into ``dst`` (an int64 device tensor on this context's device).
+        Returns (ok, counts[n_dest]); ok False means ``dst`` was too small and nothing usable was
+        written: grow it to counts.sum() and call again."""
+        p = self._params(qlen_cut, nal_cut, pass_table, edge_threshold)
+        counts = np.zeros(int(n_dest), np.int64)
+        cap = int(dst.numel())
+        rc = self._L.fslr_sweep_partition(self._h, ctypes.byref(p), int(n_dest), int(block_shift),
+                                          ctypes.c_void_p(dst.data_ptr()) if cap else None, cap,
+                                          counts.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)))
+        if rc == FSLR_ERR_STATE and counts.sum() > cap:
+            return False, counts
+        self._check(rc)
+        return True, counts
+
+    def sweep_evaluate(self, qlen_cut, nal_cut, pass_table, entries, n, edge_threshold=10):
+        """Evaluate the pairs of the first ``n`` entries of the int64 device tensor ``entries`` (async)."""
+        p = self._params(qlen_cut, nal_cut, pass_table, edge_threshold)
+        self._check(self._L.fslr_sweep_evaluate(self._h, ctypes.byref(p),
+                                                ctypes.c_void_p(entries.data_ptr()) if n else None, int(n)))
+
+    def labels_into(self, t):
+        """Copy the [n_reads] labels into the int32 device tensor ``t`` (async, context stream)."""
+        self._check(self._L.fslr_copy_labels_device(self._h, ctypes.c_void_p(t.data_ptr())))
+
+    def union_label_vectors(self, t):
+        """Union (k mod n_reads, t[k]) for the int32 device tensor ``t`` of W label vectors, then
+        finalise the labels (async)."""
+        self._check(self._L.fslr_union_pairs(self._h, None, ctypes.c_void_p(t.data_ptr()), int(t.numel()), 1))
+        self._check(self._L.fslr_finalize_labels(self._h))
 
     def apply_edge_cap(self, edge_threshold=10) -> dict:
         """Replay the reference's per-read edge cap (cluster.py:223-224) on the last full query."""

@@ -123,7 +123,8 @@ void fslr_ctx_destroy(fslr_ctx* c) {
                   c->crange, c->keys,   c->keys2,   c->vals,    c->vals2,   c->endkey,  c->pmaxkey,
                   c->temp,   c->umax,   c->edges,   c->edge_iu, c->fwd,     c->parent,  c->counters,
                   c->errw,   c->thr_tmp, c->defer,   c->dchrom,  c->drec,    c->lbounds, c->diag, c->wstat,
-                  c->dgate,  c->chist,  c->heavy, c->ent, c->ent_sorted, c->sweep_temp, c->sw_tile, c->sw_wstat, c->ent_ub};
+                  c->dgate,  c->chist,  c->heavy, c->ent, c->ent_sorted, c->sweep_temp, c->sw_tile, c->sw_wstat, c->ent_ub,
+                  c->fdchrom, c->fdrec, c->fdgate, c->crange_f, c->part_cnt};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->sw_total) (void)hipHostFree(c->sw_total);
@@ -187,8 +188,9 @@ int fslr_set_reads(fslr_ctx* c, const fslr_reads* r) {
   }
   // chromosome ranges of the (chrom, start)-sorted index: chromosome ids ascending (host counts)
   std::vector<int2> cr(static_cast<size_t>(r->n_chroms), make_int2(0, 0));
+  std::vector<int64_t> chrom_counts(static_cast<size_t>(r->n_chroms), 0);
   {
-    std::vector<int64_t> cnt(static_cast<size_t>(r->n_chroms), 0);
+    std::vector<int64_t>& cnt = chrom_counts;
     for (int64_t k = 0; k < ni; ++k) cnt[r->iv_chrom[k]]++;
     int64_t acc = 0;
     for (int ch = 0; ch < r->n_chroms; ++ch) {
@@ -242,6 +244,9 @@ int fslr_set_reads(fslr_ctx* c, const fslr_reads* r) {
   c->have_data_pos = use_dp;
   c->n = n;
   c->ni = ni;
+  c->ni_idx = ni;
+  c->filter_active = false;
+  c->chrom_counts.swap(chrom_counts);
   c->n_chroms = r->n_chroms;
   c->thr_mode = thr_mode_of(r->iv_thr, ni);
   c->any_zero_aln = std::find(zero.begin(), zero.end(), 1) != zero.end();
@@ -263,11 +268,16 @@ int fslr_set_thresholds(fslr_ctx* c, const int32_t* thr) {
       return fail(c, FSLR_ERR_INVALID, "FSLR_THR_ZERO_ALN must mark the same intervals as in fslr_set_reads");
   if (c->ni) {
     HIP_TRY(c, hipMemcpyAsync(c->thr_tmp, thr, c->ni * sizeof(int), hipMemcpyHostToDevice, c->stream));
-    if (c->index_built && c->built_n_shards != 1) c->index_built = false;   // qpos is partial: rebuild
+    if (c->index_built && (c->built_n_shards != 1 || c->filter_active))
+      c->index_built = false;                                               // qpos is partial: rebuild
     int rc = ensure_walk_index(c);                                           // idx4 is updated through qpos
     if (rc) return rc;
     HIP_TRY(c, launch_set_thr(c->thr_tmp, c->iv, c->qpos, c->index_built ? c->idx4 : nullptr, c->data_pos,
                               c->have_data_pos ? c->drec : nullptr, static_cast<int>(c->ni), c->stream));
+    if (c->filter_active)                                                    // refresh the filtered records
+      HIP_TRY(c, launch_chrom_filter(c->dchrom, c->drec, c->dgate, c->filter_mask, static_cast<int>(c->ni),
+                                     c->fdchrom, c->fdrec, c->fdgate, c->vals2, c->vals, c->temp, c->temp_bytes,
+                                     c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
   }
   c->thr_mode = thr_mode_of(thr, c->ni);
@@ -312,9 +322,9 @@ static IndexBufs index_bufs(fslr_ctx* c) {
   b.iv = c->iv;
   b.shard = c->shard;
   b.n_shards = c->n_shards;
-  b.dchrom = c->have_data_pos ? c->dchrom : nullptr;
-  b.drec = c->have_data_pos ? c->drec : nullptr;
-  b.dgate = c->dgate;
+  b.dchrom = c->filter_active ? c->fdchrom : c->have_data_pos ? c->dchrom : nullptr;
+  b.drec = c->filter_active ? c->fdrec : c->have_data_pos ? c->drec : nullptr;
+  b.dgate = c->filter_active ? c->fdgate : c->dgate;
   b.data_pos = c->data_pos;
   b.chist = c->chist;
   b.keys = c->keys;
@@ -326,7 +336,7 @@ static IndexBufs index_bufs(fslr_ctx* c) {
   b.pmaxkey = c->pmaxkey;
   b.temp = c->temp;
   b.temp_bytes = c->temp_bytes;
-  b.crange = c->crange;
+  b.crange = c->filter_active ? c->crange_f : c->crange;
   b.qpos = c->qpos;
   b.rng_s = c->rng_s;
   b.idx4 = c->idx4;
@@ -359,6 +369,7 @@ int fslr::peek_counts(fslr_ctx* c, long long out[3]) {
 
 int fslr::ensure_walk_index(fslr_ctx* c) {
   if (!c->index_built || c->index_full) return FSLR_OK;
+  if (c->filter_active) return fail(c, FSLR_ERR_STATE, "the walk engine needs every chromosome's index");
   HIP_TRY(c, launch_index_walk_parts(index_bufs(c), static_cast<int>(c->n), static_cast<int>(c->ni), c->stream));
   c->index_full = true;
   return FSLR_OK;
@@ -373,8 +384,8 @@ int fslr_build_index(fslr_ctx* c) {
   if (c->profiling) HIP_TRY(c, hipEventRecord(c->ev[0], c->stream));
   // the sweep engine's index only (the walk engine's parts follow on demand, ensure_walk_index)
   // where the data-order path applies and one context covers every query read
-  const bool full = !(c->have_data_pos && c->n_chroms <= 64 && c->n_shards == 1);
-  HIP_TRY(c, launch_build_index(index_bufs(c), static_cast<int>(c->n), static_cast<int>(c->ni), c->n_chroms, full,
+  const bool full = !c->filter_active && !(c->have_data_pos && c->n_chroms <= 64 && c->n_shards == 1);
+  HIP_TRY(c, launch_build_index(index_bufs(c), static_cast<int>(c->n), static_cast<int>(c->ni_idx), c->n_chroms, full,
                                 c->stream));
   if (c->profiling) HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));
   c->t_index_rec = c->profiling;
@@ -408,10 +419,11 @@ int fslr_query_shard(fslr_ctx* c, const fslr_params* p, int32_t shard, int32_t n
 // and an overflow flag from pinned host memory the kernels write; the tiles are packed, grouped by
 // A and evaluated.  A too-small upper-bound buffer is grown and the sweep rerun (first query on an
 // input); an upper bound beyond kUbBudget entries takes the two-pass fallback (count, then emit).
-static int sweep_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_t a_end, hipEvent_t e0,
-                      hipEvent_t e1) {
+static int sweep_front(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_t a_end, hipEvent_t e0,
+                       hipEvent_t e1, SweepArgs& s, int& mode) {
   constexpr int64_t kUbBudget = int64_t(1) << 30;     // 8 GB of upper-bound slots
-  const int64_t tiles = (c->ni + 63) / 64 + 1;
+  const int64_t nix = c->ni_idx;                      // positions of the (possibly chromosome-filtered) index
+  const int64_t tiles = (nix + 63) / 64 + 1;
   int rc;
   if (tiles > c->sw_tiles) {
     if ((rc = dalloc(c, &c->sw_tile, 4 * tiles))) return rc;
@@ -427,18 +439,17 @@ static int sweep_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_
     if ((rc = dalloc(c, &c->sw_wstat, static_cast<size_t>(w) * 4))) return rc;
     c->sw_wstat_waves = w;
   }
-  if (c->ent_cap == 0 && (rc = reserve_entries(c, std::max<int64_t>(1 << 20, c->ni)))) return rc;
+  if (c->ent_cap == 0 && (rc = reserve_entries(c, std::max<int64_t>(1 << 20, nix)))) return rc;
   if (c->ent_ub_cap == 0) {
-    if ((rc = dalloc(c, &c->ent_ub, std::max<int64_t>(1 << 20, 4 * c->ni)))) return rc;
-    c->ent_ub_cap = std::max<int64_t>(1 << 20, 4 * c->ni);
+    if ((rc = dalloc(c, &c->ent_ub, std::max<int64_t>(1 << 20, 4 * nix)))) return rc;
+    c->ent_ub_cap = std::max<int64_t>(1 << 20, 4 * nix);
   }
-  SweepArgs s;
   s.rmeta = c->rmeta;
   s.idx4 = c->idx4;
   s.idx_gate = c->idx_gate;
   s.rng_s = c->rng_s;
   s.umax = c->umax;
-  s.ni = static_cast<int>(c->ni);
+  s.ni = static_cast<int>(nix);
   s.n_reads = static_cast<int>(c->n);
   s.a_begin = static_cast<int>(a_begin);
   s.a_end = static_cast<int>(a_end);
@@ -461,7 +472,7 @@ static int sweep_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_
   for (int k = 0; k < 5; ++k) s.ev[k] = c->profiling ? c->sw_ev[k] : nullptr;
   s.ev[0] = nullptr;                                // recorded here, around the sweep pass
   HIP_TRY(c, launch_len_bounds(c->rmeta, 0, static_cast<int>(c->n), p->qlen_cut, p->nal_cut, c->lbounds, c->stream));
-  int mode = 2;
+  mode = 2;
   for (int attempt = 0; attempt < 3; ++attempt) {
     s.ent = c->ent;
     s.ent_sorted = c->ent_sorted;
@@ -497,13 +508,22 @@ static int sweep_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_
   s.ent_sorted = c->ent_sorted;
   s.temp = c->sweep_temp;
   s.temp_bytes = c->sweep_temp_bytes;
+  return FSLR_OK;
+}
+
+static int sweep_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_t a_end, hipEvent_t e0,
+                      hipEvent_t e1) {
+  SweepArgs s;
+  int mode = 2;
+  int rc = sweep_front(c, p, a_begin, a_end, e0, e1, s, mode);
+  if (rc) return rc;
   HIP_TRY(c, launch_sweep_pairs(s, mode, c->stream));
   c->sw_ev_rec = c->profiling;
   return FSLR_OK;
 }
 
-static int query_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_t a_end, int shard, int n_shards) {
-  if (!c->index_built) return fail(c, FSLR_ERR_STATE, "fslr_build_index first");
+// buffers, the folded cut table and cleared counters / errors / forward degrees for one query
+static int prepare_query(fslr_ctx* c, const fslr_params* p) {
   HIP_TRY(c, hipSetDevice(c->device));
   if (c->edge_cap == 0) {
     int rc = fslr_reserve_edges(c, std::max<int64_t>(1 << 16, 12 * c->n));
@@ -539,6 +559,16 @@ static int query_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_
   }
   HIP_TRY(c, hipMemsetAsync(c->errw, 0, kErrWords * sizeof(int), c->stream));
   if (c->n) HIP_TRY(c, hipMemsetAsync(c->fwd, 0, c->n * sizeof(int), c->stream));
+  std::memset(&c->cap_stats, 0, sizeof(c->cap_stats));
+  return FSLR_OK;
+}
+
+static int query_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_t a_end, int shard, int n_shards) {
+  if (!c->index_built) return fail(c, FSLR_ERR_STATE, "fslr_build_index first");
+  if (c->filter_active)
+    return fail(c, FSLR_ERR_STATE, "the index covers a chromosome subset (fslr_set_chrom_filter): use "
+                                   "fslr_sweep_partition / fslr_sweep_evaluate");
+  if (int rc = prepare_query(c, p)) return rc;
   QueryArgs g;
   g.rmeta = c->rmeta;
   g.iv = c->iv;
@@ -576,7 +606,6 @@ static int query_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_
   c->last_full = a_begin == 0 && a_end == c->n && n_shards == 1;
   c->last_qcut = p->qlen_cut;
   c->last_ncut = p->nal_cut;
-  std::memset(&c->cap_stats, 0, sizeof(c->cap_stats));
   const int want = p->flags & 3;
   const bool sweep_ok = c->thr_mode == 0 && !c->any_zero_aln && n_shards == 1;
   if (want == FSLR_ENGINE_SWEEP && !sweep_ok)
@@ -598,6 +627,120 @@ static int query_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_
   if (c->profiling) HIP_TRY(c, hipEventRecord(c->ev[3], c->stream));
   c->t_query_rec = c->profiling;
   c->t_kernel_rec = c->profiling && c->n > 0 && a_end > a_begin;
+  return FSLR_OK;
+}
+
+// ---- multi-GPU sweep: chromosome-filtered index, entry partition by owner, owner evaluation ----
+int fslr_set_chrom_filter(fslr_ctx* c, const uint8_t* owned) {
+  if (!c) return FSLR_ERR_INVALID;
+  if (!c->reads_set) return fail(c, FSLR_ERR_STATE, "fslr_set_reads first");
+  HIP_TRY(c, hipSetDevice(c->device));
+  c->index_built = false;
+  if (!owned) {
+    c->filter_active = false;
+    c->ni_idx = c->ni;
+    return FSLR_OK;
+  }
+  if (!c->have_data_pos || c->n_chroms > 64)
+    return fail(c, FSLR_ERR_INVALID, "a chromosome filter needs the start-sorted data order (iv_data_pos) and at "
+                                     "most 64 chromosomes");
+  std::vector<int2> cr(static_cast<size_t>(c->n_chroms));
+  unsigned long long mask = 0;
+  int64_t acc = 0;
+  for (int ch = 0; ch < c->n_chroms; ++ch) {
+    const int64_t k = owned[ch] ? c->chrom_counts[ch] : 0;
+    if (owned[ch]) mask |= 1ull << ch;
+    cr[ch] = make_int2(static_cast<int>(acc), static_cast<int>(acc + k));
+    acc += k;
+  }
+  const int64_t nf = acc;
+  int rc;
+  if (nf > c->f_cap) {
+    if ((rc = dalloc(c, &c->fdchrom, nf)) || (rc = dalloc(c, &c->fdrec, nf)) || (rc = dalloc(c, &c->fdgate, nf)))
+      return rc;
+    c->f_cap = nf;
+  }
+  if (!c->crange_f && (rc = dalloc(c, &c->crange_f, 64))) return rc;
+  HIP_TRY(c, hipMemcpyAsync(c->crange_f, cr.data(), cr.size() * sizeof(int2), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, launch_chrom_filter(c->dchrom, c->drec, c->dgate, mask, static_cast<int>(c->ni), c->fdchrom, c->fdrec,
+                                 c->fdgate, c->vals2, c->vals, c->temp, c->temp_bytes, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->filter_active = true;
+  c->filter_mask = mask;
+  c->ni_idx = nf;
+  return FSLR_OK;
+}
+
+int fslr_sweep_partition(fslr_ctx* c, const fslr_params* p, int32_t n_dest, int32_t block_shift, void* dst,
+                         int64_t dst_cap, int64_t* counts) {
+  if (!c || !p || !p->pass_table || n_dest < 1 || n_dest > kMaxDest || block_shift < 0 || block_shift > 24 ||
+      !counts || dst_cap < 0 || (!dst && dst_cap))
+    return FSLR_ERR_INVALID;
+  if (!c->index_built) return fail(c, FSLR_ERR_STATE, "fslr_build_index first");
+  if (c->thr_mode != 0 || c->any_zero_aln)
+    return fail(c, FSLR_ERR_INVALID, "the sweep engine needs overlap thresholds >= 1 and no aln_size == 0 interval");
+  if (int rc = prepare_query(c, p)) return rc;
+  c->last_full = false;
+  c->last_engine = FSLR_ENGINE_SWEEP;
+  SweepArgs s;
+  int mode = 2;
+  if (int rc = sweep_front(c, p, 0, c->n, nullptr, nullptr, s, mode)) return rc;
+  // dense entries in `ent` (pack, or the emit pass of the two-pass fallback), then by destination
+  HIP_TRY(c, launch_sweep_dense(s, mode, c->stream));
+  if (!c->part_cnt && dalloc(c, &c->part_cnt, 2 * kMaxDest * kPartBlocks + kMaxDest)) return FSLR_ERR_NOMEM;
+  if (partition_temp_bytes(c->stream) > c->sweep_temp_bytes) return fail(c, FSLR_ERR_STATE, "partition scratch");
+  long long* totals = c->part_cnt + 2 * kMaxDest * kPartBlocks;
+  HIP_TRY(c, launch_partition_by_dest(c->ent, s.n_ent, block_shift, n_dest, c->part_cnt, c->sweep_temp,
+                                      c->sweep_temp_bytes, static_cast<unsigned long long*>(dst), dst_cap, totals,
+                                      c->stream));
+  long long tot[kMaxDest];
+  int ew[kErrWords] = {};
+  HIP_TRY(c, hipMemcpyAsync(tot, totals, n_dest * sizeof(long long), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(ew, c->errw, sizeof(ew), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (ew[0] == FSLR_ERR_ZERO_DIVISION) {
+    c->err = "division by zero";
+    return FSLR_ERR_ZERO_DIVISION;
+  }
+  int64_t sum = 0;
+  for (int k = 0; k < n_dest; ++k) sum += (counts[k] = tot[k]);
+  if (sum > dst_cap) return fail(c, FSLR_ERR_STATE, "destination buffer too small for the entries (see counts)");
+  return FSLR_OK;
+}
+
+int fslr_sweep_evaluate(fslr_ctx* c, const fslr_params* p, const void* entries, int64_t n) {
+  if (!c || !p || !p->pass_table || (!entries && n) || n < 0) return FSLR_ERR_INVALID;
+  if (!c->reads_set) return fail(c, FSLR_ERR_STATE, "fslr_set_reads first");
+  if (int rc = prepare_query(c, p)) return rc;
+  if (n > c->ent_cap && reserve_entries(c, n + (n >> 3) + 4096)) return FSLR_ERR_NOMEM;
+  if (!c->sw_wstat) {
+    const int w = sweep_max_waves();
+    if (int rc = dalloc(c, &c->sw_wstat, static_cast<size_t>(w) * 4)) return rc;
+    c->sw_wstat_waves = w;
+  }
+  c->last_full = false;
+  c->last_engine = FSLR_ENGINE_SWEEP;
+  SweepArgs s{};
+  s.rmeta = c->rmeta;
+  s.umax = c->umax;
+  s.ni = 0;
+  s.n_reads = static_cast<int>(c->n);
+  s.a_begin = 0;
+  s.a_end = static_cast<int>(c->n);
+  s.ent = static_cast<unsigned long long*>(const_cast<void*>(entries));
+  s.ent_sorted = c->ent_sorted;
+  s.n_ent = n;
+  s.temp = c->sweep_temp;
+  s.temp_bytes = c->sweep_temp_bytes;
+  s.edges = c->edges;
+  s.edge_iu = c->edge_iu;
+  s.edge_cap = c->edge_cap;
+  s.fwd = c->fwd;
+  s.counters = c->counters;
+  s.err = c->errw;
+  s.wstat = c->sw_wstat;
+  s.wstat_waves = c->sw_wstat_waves;
+  HIP_TRY(c, launch_sweep_pairs(s, 3, c->stream));
   return FSLR_OK;
 }
 

@@ -18,6 +18,17 @@ struct fslr_ctx {
   int thr_mode = 0;
   bool reads_set = false, index_built = false, have_data_pos = false;
   bool index_full = false;                 // the walk engine's index parts exist (qpos, backward ranges)
+  // multi-GPU sweep: the index covers the chromosomes of a filter (fslr_set_chrom_filter)
+  bool filter_active = false;
+  unsigned long long filter_mask = 0;
+  int64_t ni_idx = 0;                       // positions of the index (ni, or the filtered count)
+  std::vector<int64_t> chrom_counts;        // intervals per chromosome (set_reads)
+  unsigned* fdchrom = nullptr;              // the filtered data-order arrays
+  int4* fdrec = nullptr;
+  int2* fdgate = nullptr;
+  int64_t f_cap = 0;
+  int2* crange_f = nullptr;                 // [64] chromosome ranges of the filtered index
+  long long* part_cnt = nullptr;            // partition scratch: per (destination, block) counts + offsets
   int shard = 0, n_shards = 1;             // fslr_set_shard: A-side index data for this shard only
   int built_shard = 0, built_n_shards = 1;
   // device buffers

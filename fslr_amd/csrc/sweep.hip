@@ -689,25 +689,32 @@ hipError_t launch_sweep_count(const SweepArgs& a, int mode, long long* total_dev
   return hipGetLastError();
 }
 
-hipError_t launch_sweep_pairs(const SweepArgs& a, int mode, hipStream_t s) {
+hipError_t launch_sweep_dense(const SweepArgs& a, int mode, hipStream_t s) {
   const int nt = tiles_of(a);
+  if (a.n_ent <= 0 || nt == 0) return hipSuccess;
+  if (mode == 2) {
+    k_compact<<<grid_for(static_cast<long long>(nt) * kWave, 256, 8192), 256, 0, s>>>(a.ent_ub, a.tile_ub, a.tile_off,
+                                                                                    a.tile_cnt, nt, a.ent);
+  } else {
+    const int be = std::min(blocks_mode(1), (nt + kSwWaves - 1) / kSwWaves);
+    k_sweep<1><<<be, kSwBlock, 0, s>>>(a);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_sweep_pairs(const SweepArgs& a, int mode, hipStream_t s) {
   if (a.ev[2]) (void)hipEventRecord(a.ev[2], s);
+  if (mode != 3) {
+    hipError_t e = launch_sweep_dense(a, mode, s);
+    if (e != hipSuccess) return e;
+  }
+  if (a.ev[3]) (void)hipEventRecord(a.ev[3], s);
   if (a.n_ent > 0) {
-    if (mode == 2) {
-      k_compact<<<grid_for(static_cast<long long>(nt) * kWave, 256, 8192), 256, 0, s>>>(a.ent_ub, a.tile_ub, a.tile_off,
-                                                                                      a.tile_cnt, nt, a.ent);
-    } else {
-      const int be = std::min(blocks_mode(1), (nt + kSwWaves - 1) / kSwWaves);
-      k_sweep<1><<<be, kSwBlock, 0, s>>>(a);
-    }
-    if (a.ev[3]) (void)hipEventRecord(a.ev[3], s);
     size_t tb = a.temp_bytes;
     const int end_bit = 39 + bits_for(std::max(1, a.n_reads - 1));
     hipError_t e = hipcub::DeviceRadixSort::SortKeys(a.temp, tb, a.ent, a.ent_sorted, static_cast<int>(a.n_ent), 39,
                                                      std::min(end_bit, 64), s);
     if (e != hipSuccess) return e;
-  } else if (a.ev[3]) {
-    (void)hipEventRecord(a.ev[3], s);
   }
   if (a.ev[4]) (void)hipEventRecord(a.ev[4], s);
   const long long chunks = (a.n_ent + kChunk2 - 1) / kChunk2;

@@ -1,6 +1,17 @@
-"""Multi-GPU sharding of the pair space (one process per GPU, torch.distributed over RCCL).
+"""Multi-GPU sharding (one process per GPU, torch.distributed over RCCL).
 
-Partition: query reads are split into blocks of SHARD_BLOCK
+Two splits:
+
+* SweepShard (the sweep engine, the default): every rank indexes and sweeps only the chromosomes it
+  owns (chrom_owner: largest-first onto the least-loaded rank), and routes the match entries of
+  each read pair to the rank owning the pair's first read (64-rank blocks dealt round robin) with
+  one RCCL all_to_all; that rank evaluates the pair.  Exact because an interval only meets
+  intervals of its own chromosome (cluster.py:159-160): a pair's first-fit matching is the union of
+  its per-chromosome matchings, and all of them meet at one evaluator.  The index build, the sweep
+  and the pair evaluation all split W ways; the label exchange below is the one replicated step.
+* Query-read shards (the walk engine, fslr_query_shard): described next.
+
+Query-read shards: query reads are split into blocks of SHARD_BLOCK
 consecutive ranks dealt round robin to the processes (fslr_query_shard; low
 ranks have more higher-rank partners, so contiguous ranges would not balance);
 every process holds the full CSR and index in its HBM and evaluates the pairs
@@ -95,3 +106,166 @@ class DeviceShardMerge:
         # read with its own root, a no-op)
         self.ctx.union_pairs(None, self.gathered.data_ptr(), self.world * self.n, on_device=True)
         self.ctx.finalize_labels()
+
+
+def chrom_owner(chrom_counts, world: int) -> np.ndarray:
+    """Owner rank of each chromosome: largest interval count first onto the least-loaded rank
+    (ties to the lower rank), so every rank's index and sweep cover about 1/W of the intervals."""
+    cnt = np.asarray(chrom_counts, dtype=np.int64)
+    owner = np.zeros(cnt.size, dtype=np.int64)
+    load = np.zeros(world, dtype=np.int64)
+    for c in sorted(range(cnt.size), key=lambda k: (-cnt[k], k)):
+        r = int(np.argmin(load))
+        owner[c] = r
+        load[r] += cnt[c]
+    return owner
+
+
+def chrom_counts_of(csr) -> np.ndarray:
+    return np.bincount(np.asarray(csr.iv_chrom), minlength=int(csr.n_chroms))
+
+
+class SweepShard:
+    """One rank of the chromosome-split sweep (fslr_set_chrom_filter / fslr_sweep_partition /
+    fslr_sweep_evaluate, then the label exchange).  ``ctx`` holds every read (set_reads); this
+    rank's index covers the chromosomes ``owner == rank``.  Entries travel as int64 tensors on
+    ``device``; with the gloo backend they are staged through host memory (CPU rehearsal).
+
+    step() leaves this rank's edges / forward degrees (pairs whose first read it owns) in ``ctx``
+    and the global min-rank labels in ``ctx`` (labels()).  When the reference's edge cap binds
+    (some read has more than ``edge_threshold`` forward edges) the graph depends on the sequential
+    order of the reference's loops: rank 0 then reruns the whole query on all chromosomes, replays
+    the cap (fslr_apply_edge_cap) and broadcasts the labels (``capped`` in the step's result).
+    """
+
+    def __init__(self, ctx, n_reads: int, chrom_counts, world: int, rank: int, device, block_shift: int = 6,
+                 owner=None):
+        import torch
+        self.ctx = ctx
+        self.n = int(n_reads)
+        self.world = int(world)
+        self.rank = int(rank)
+        self.device = torch.device(device)
+        self.block_shift = int(block_shift)
+        self.owner = chrom_owner(chrom_counts, world) if owner is None else np.asarray(owner)
+        self.owned = self.owner == rank
+        self.send = torch.empty(1 << 16, dtype=torch.int64, device=self.device)
+        self.recv = torch.empty(1 << 16, dtype=torch.int64, device=self.device)
+        self.local = torch.empty(self.n, dtype=torch.int32, device=self.device)
+        self.gathered = torch.empty(self.world * self.n, dtype=torch.int32, device=self.device)
+        self._labels = None
+        ctx.set_chrom_filter(self.owned if world > 1 else None)
+
+    # -- collectives (RCCL; gloo stages device tensors through host memory) -----------------------
+    def _gloo(self):
+        import torch.distributed as dist
+        return dist.get_backend() == 'gloo'
+
+    def _all_to_all(self, out, inp, out_splits, in_splits):
+        import torch.distributed as dist
+        if self._gloo() and out.device.type != 'cpu':
+            o = out.cpu()
+            dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits)
+            out.copy_(o)
+        else:
+            dist.all_to_all_single(out, inp, out_splits, in_splits)
+
+    def _all_gather(self, out, inp):
+        import torch.distributed as dist
+        if self._gloo() and out.device.type != 'cpu':
+            o = out.new_empty(out.shape, device='cpu')
+            dist.all_gather_into_tensor(o, inp.cpu())
+            out.copy_(o)
+        else:
+            dist.all_gather_into_tensor(out, inp)
+
+    def _grow(self, t, need):
+        import torch
+        if t.numel() >= need:
+            return t
+        return torch.empty(int(need * 1.125) + 4096, dtype=torch.int64, device=self.device)
+
+    # -- one step -----------------------------------------------------------------------------
+    def step(self, qlen_cut, nal_cut, pass_table, edge_threshold=10) -> dict:
+        import torch
+        import torch.distributed as dist
+        ctx, W = self.ctx, self.world
+        self._labels = None
+        ctx.build_index()
+        ok, counts = ctx.sweep_partition(qlen_cut, nal_cut, pass_table, W, self.block_shift, self.send,
+                                         edge_threshold)
+        if not ok:
+            self.send = self._grow(self.send, int(counts.sum()))
+            ok, counts = ctx.sweep_partition(qlen_cut, nal_cut, pass_table, W, self.block_shift, self.send,
+                                             edge_threshold)
+            assert ok
+        sent_total = int(counts.sum())
+        if W > 1:
+            cdev = 'cpu' if self._gloo() else self.device
+            cin = torch.from_numpy(counts).to(cdev)
+            cout = torch.empty_like(cin)
+            dist.all_to_all_single(cout, cin)
+            recv_counts = cout.cpu().numpy()
+            n_recv = int(recv_counts.sum())
+            self.recv = self._grow(self.recv, n_recv)
+            self._all_to_all(self.recv[:n_recv], self.send[:sent_total], recv_counts.tolist(), counts.tolist())
+            entries = self.recv
+        else:
+            n_recv = sent_total
+            entries = self.send
+        ctx.sweep_evaluate(qlen_cut, nal_cut, pass_table, entries, n_recv, edge_threshold)
+        st = ctx.stats(check=False)
+        while st['n_edges'] > st['edge_capacity']:
+            ctx.reserve_edges(int(st['n_edges'] * 1.25) + 4096)
+            ctx.sweep_evaluate(qlen_cut, nal_cut, pass_table, entries, n_recv, edge_threshold)
+            st = ctx.stats(check=False)
+        ctx.stats()                                     # raises on a device-side error
+        mf = int(st['max_fwd'])
+        if W > 1:
+            t = torch.tensor([mf], dtype=torch.int64, device='cpu' if self._gloo() else self.device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            mf = int(t.item())
+        out = {'entries_sent': sent_total, 'entries_received': n_recv, 'n_edges_local': int(st['n_edges']),
+               'max_fwd': mf, 'capped': False}
+        if mf > edge_threshold:
+            out['capped'] = True
+            out['cap'] = self._capped_labels(qlen_cut, nal_cut, pass_table, edge_threshold)
+            return out
+        ctx.components()
+        if W > 1:
+            ctx.labels_into(self.local)
+            self._all_gather(self.gathered, self.local)
+            ctx.union_label_vectors(self.gathered)
+        return out
+
+    def _capped_labels(self, qlen_cut, nal_cut, pass_table, edge_threshold):
+        """The cap binds: the reference's graph is order dependent, so rank 0 replays it on the
+        whole input (one context, every chromosome) and broadcasts the labels."""
+        import torch
+        import torch.distributed as dist
+        ctx, W = self.ctx, self.world
+        cap = {}
+        if self.rank == 0:
+            if W > 1:
+                ctx.set_chrom_filter(None)
+            ctx.build_index()
+            ctx.run_query(qlen_cut, nal_cut, pass_table, edge_threshold)
+            cap = ctx.apply_edge_cap(edge_threshold)
+            ctx.components()
+            if W > 1:
+                ctx.labels_into(self.local)
+                ctx.set_chrom_filter(self.owned)
+        if W > 1:
+            if self._gloo() and self.local.device.type != 'cpu':
+                h = self.local.cpu()
+                dist.broadcast(h, 0)
+                self.local.copy_(h)
+            else:
+                dist.broadcast(self.local, 0)
+            if self.rank != 0:
+                self._labels = self.local.cpu().numpy().astype(np.int32)
+        return cap
+
+    def labels(self) -> np.ndarray:
+        """Global min-rank labels after step() (every rank)."""
+        return self._labels if self._labels is not None else self.ctx.labels()

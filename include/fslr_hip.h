@@ -18,6 +18,10 @@
  *   fslr_query_shard      the same over one multi-GPU shard of the query reads
  *   fslr_components       cluster.py:230-234  get_subgraphs (networkx
  *                         connected_components)
+ *   fslr_set_chrom_filter,
+ *   fslr_sweep_partition,
+ *   fslr_sweep_evaluate   cluster.py:187-227 split over ranks by chromosome (the sweep engine's
+ *                         multi-GPU path)
  *   fslr_union_pairs      (multi-GPU merge of per-shard component labels; no
  *                         reference counterpart — the reference is single-process)
  *
@@ -50,7 +54,7 @@
 extern "C" {
 #endif
 
-#define FSLR_ABI_VERSION 3
+#define FSLR_ABI_VERSION 4
 #define FSLR_MAX_L 64                /* max intervals per read (bitmask width) */
 #define FSLR_MAX_READS (1 << 25)     /* read rank packs into bits 6..30 of the index record */
 #define FSLR_THR_ZERO_ALN INT32_MIN
@@ -200,6 +204,30 @@ int  fslr_query_shard(fslr_ctx *ctx, const fslr_params *params, int32_t shard, i
 int  fslr_apply_edge_cap(fslr_ctx *ctx, int32_t edge_threshold, fslr_cap_stats *out);
 /* cluster.py:230-234 — union-find over the edges: label = min rank in component.  Async. */
 int  fslr_components(fslr_ctx *ctx);
+/* Multi-GPU sweep.  A rank indexes only the chromosomes it owns, sweeps them and
+ * routes the match entries to the rank owning each pair's first read, which evaluates the pairs.
+ * An interval only meets intervals of its own chromosome (cluster.py:159-160), so the first-fit
+ * matching of a pair is the union of its per-chromosome matchings and the split is exact.
+ *
+ * fslr_set_chrom_filter: owned[n_chroms] != 0 marks the chromosomes the next fslr_build_index
+ * indexes (NULL: all).  Needs iv_data_pos and n_chroms <= 64.  The filtered index serves only
+ * fslr_sweep_partition (fslr_query refuses it).  Syncs.
+ * fslr_sweep_partition: sweep the filtered index (every query read, the pair gates applied) and
+ * write its match entries (8 bytes each, layout internal to the library) to the device buffer dst
+ * grouped by destination k = (a >> block_shift) % n_dest, a = the pair's first (lower-rank) read:
+ * rank blocks dealt round robin, n_dest <= 64; counts[k] = entries for k.  Syncs; FSLR_ERR_STATE if
+ * sum(counts) > dst_cap (counts are still filled: grow dst and call again), FSLR_ERR_ZERO_DIVISION
+ * as fslr_read_stats.
+ * fslr_sweep_evaluate: evaluate the pairs of the n entries (a device buffer: every rank's segment
+ * for this rank, concatenated in any order) into this context's edges and forward degrees.  Every
+ * entry of a pair must be present, so each pair's first read belongs to one destination.  Needs only
+ * fslr_set_reads.  Async; fslr_read_stats / fslr_components / fslr_get_edges follow as after
+ * fslr_query. */
+int  fslr_set_chrom_filter(fslr_ctx *ctx, const uint8_t *owned);
+int  fslr_sweep_partition(fslr_ctx *ctx, const fslr_params *params, int32_t n_dest, int32_t block_shift,
+                          void *dst, int64_t dst_cap, int64_t *counts);
+int  fslr_sweep_evaluate(fslr_ctx *ctx, const fslr_params *params, const void *entries, int64_t n);
+
 /* build_index + query(all reads) + components, enqueued back to back.  Async. */
 int  fslr_run(fslr_ctx *ctx, const fslr_params *params);
 

@@ -1,0 +1,187 @@
+"""Host emulation of the sweep engine's multi-GPU entry points, for the CPU (gloo) tests of
+fslr_amd.dist.SweepShard.  Test infrastructure only.
+
+EmuSweepContext implements the Context methods SweepShard calls (fslr_hip.h
+fslr_set_chrom_filter / fslr_sweep_partition / fslr_sweep_evaluate, components, the label
+exchange) in numpy, with the device's entry encoding (a << 39 | b << 14 | i << 7 | j, a < b read
+ranks, i / j interval slots in the reads) and its routing ((a >> shift) % n_dest).  It restates
+what the kernels compute, not how; the device kernels are checked against the C oracle by the GPU
+tests.  Here it lets the real torch.distributed exchange in dist.py run over gloo and be compared
+with the oracle:
+  * entries: every same-chromosome interval pair of two different reads whose overlap passes both
+    intervals' folded thresholds (cluster.py:133-136, 159-160), for read pairs that pass the length
+    gate (cluster.py:178-183);
+  * evaluation: first-fit greedy over the pair's entries in (i, j) order (cluster.py:140-170),
+    edge iff I > 0 and the cut table passes (cluster.py:216-219).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from fslr_amd.prep import FSLR_MAX_L, PASS_STRIDE
+
+
+class EmuSweepContext:
+    def __init__(self, csr, iv_thr, qlen_diff=0.04, n_aln_diff=0.25, overlap=0.8):
+        self.csr = csr
+        self.diffs = (qlen_diff, n_aln_diff, overlap)     # the cap fallback hands these to the oracle
+        self.thr = np.asarray(iv_thr, dtype=np.int64)
+        assert (self.thr >= 1).all(), 'the sweep split needs overlap thresholds >= 1'
+        self.n_reads = csr.n_reads
+        off = np.asarray(csr.read_off, dtype=np.int64)
+        self.read_of = np.repeat(np.arange(csr.n_reads), np.diff(off))
+        self.slot = np.arange(off[-1]) - off[self.read_of]
+        self.L = np.diff(off)
+        self.owned = None
+        self.edge_capacity = 1 << 30
+        self._edges = np.zeros((0, 4), np.int64)
+        self._parent = np.arange(self.n_reads)
+        self._st = {}
+
+    # -- filter / index ------------------------------------------------------------------------
+    def set_chrom_filter(self, owned):
+        self.owned = None if owned is None else np.asarray(owned, dtype=bool)
+
+    def build_index(self):
+        pass
+
+    def reserve_edges(self, cap):
+        pass
+
+    # -- partition ------------------------------------------------------------------------------
+    def _gate(self, a, b, qcut, ncut):
+        q1, q2 = int(self.csr.read_qlen2[a]), int(self.csr.read_qlen2[b])
+        mn, mx = min(q1, q2), max(q1, q2)
+        if mx == 0:
+            raise ZeroDivisionError('division by zero')
+        if mn / mx >= qcut:
+            return True
+        n1, n2 = int(self.csr.read_nal[a]), int(self.csr.read_nal[b])
+        mn, mx = min(n1, n2), max(n1, n2)
+        if mx == 0:
+            raise ZeroDivisionError('division by zero')
+        return mn / mx >= ncut
+
+    def _entries(self, qcut, ncut):
+        c = self.csr
+        chrom = np.asarray(c.iv_chrom)
+        start, end = np.asarray(c.iv_start, np.int64), np.asarray(c.iv_end, np.int64)
+        out = []
+        for ch in np.unique(chrom):
+            if self.owned is not None and not self.owned[ch]:
+                continue
+            ks = np.flatnonzero(chrom == ch)
+            s, e = start[ks], end[ks]
+            o = np.minimum(e[:, None], e[None, :]) - np.maximum(s[:, None], s[None, :])
+            ok = (o >= self.thr[ks][:, None]) & (o >= self.thr[ks][None, :])
+            ra, rb = self.read_of[ks][:, None], self.read_of[ks][None, :]
+            ok &= ra < rb
+            x, y = np.nonzero(ok)
+            for p, q in zip(ks[x].tolist(), ks[y].tolist()):
+                a, b = int(self.read_of[p]), int(self.read_of[q])
+                if self._gate(a, b, qcut, ncut):
+                    out.append((a << 39) | (b << 14) | (int(self.slot[p]) << 7) | int(self.slot[q]))
+        return np.array(out, dtype=np.int64)
+
+    def sweep_partition(self, qlen_cut, nal_cut, pass_table, n_dest, block_shift, dst, edge_threshold=10):
+        ent = self._entries(qlen_cut, nal_cut)
+        dest = (ent >> (39 + block_shift)) % n_dest
+        order = np.argsort(dest, kind='stable')
+        counts = np.bincount(dest, minlength=n_dest).astype(np.int64)
+        if counts.sum() > dst.numel():
+            return False, counts
+        dst.numpy()[:ent.size] = ent[order]
+        self._st = {'match_entries': int(ent.size)}
+        return True, counts
+
+    # -- evaluation -----------------------------------------------------------------------------
+    def sweep_evaluate(self, qlen_cut, nal_cut, pass_table, entries, n, edge_threshold=10):
+        ent = entries.numpy()[:n].astype(np.int64)
+        pt = np.asarray(pass_table).reshape(FSLR_MAX_L, PASS_STRIDE)
+        a = ent >> 39
+        b = (ent >> 14) & 0x1FFFFFF
+        i = (ent >> 7) & 127
+        j = ent & 127
+        order = np.lexsort((j, i, b, a))
+        a, b, i, j = a[order], b[order], i[order], j[order]
+        edges = []
+        fwd = np.zeros(self.n_reads, np.int64)
+        k = 0
+        while k < a.size:
+            m = k
+            while m < a.size and a[m] == a[k] and b[m] == b[k]:
+                m += 1
+            used_i, used_j = set(), set()
+            for t in range(k, m):                # (i, j) ascending: first free j for each i
+                if i[t] in used_i or j[t] in used_j:
+                    continue
+                used_i.add(i[t])
+                used_j.add(j[t])
+            I = len(used_i)
+            U = int(self.L[a[k]] + self.L[b[k]] - I)
+            if I > 0 and pt[I - 1, U - 1]:
+                edges.append((int(a[k]), int(b[k]), I, U))
+                fwd[a[k]] += 1
+            k = m
+        self._edges = np.array(edges, dtype=np.int64).reshape(-1, 4)
+        self._fwd = fwd
+        self._st = {'n_edges': len(edges), 'edge_capacity': self.edge_capacity,
+                    'max_fwd': int(fwd.max()) if fwd.size else 0}
+
+    def stats(self, check=True):
+        return dict(self._st)
+
+    def edges(self, n_edges):
+        e = self._edges[:n_edges]
+        return e[:, 0], e[:, 1], e[:, 2], e[:, 3]
+
+    def fwd_degree(self):
+        return self._fwd.astype(np.int32)
+
+    # -- components and the label exchange --------------------------------------------------------
+    def _find(self, x):
+        p = self._parent
+        r = x
+        while p[r] != r:
+            r = p[r]
+        while p[x] != r:
+            p[x], x = r, p[x]
+        return r
+
+    def _union(self, x, y):
+        rx, ry = self._find(x), self._find(y)
+        if rx != ry:
+            self._parent[max(rx, ry)] = min(rx, ry)
+
+    def components(self):
+        self._parent = np.arange(self.n_reads)
+        for x, y in self._edges[:, :2].tolist():
+            self._union(x, y)
+
+    def labels(self):
+        return np.array([self._find(v) for v in range(self.n_reads)], dtype=np.int32)
+
+    def labels_into(self, t):
+        t.numpy()[:] = self.labels()
+
+    def union_label_vectors(self, t):
+        lab = t.numpy()
+        n = self.n_reads
+        for k in range(lab.size):
+            self._union(k % n, int(lab[k]))
+
+    # -- the cap fallback (rank 0 reruns the whole query and replays the cap): the oracle's loops --
+    def run_query(self, qlen_cut, nal_cut, pass_table, edge_threshold=10, *a, **k):
+        self._full = (qlen_cut, nal_cut, edge_threshold)
+        return {}
+
+    def apply_edge_cap(self, edge_threshold=10):
+        from oracle import oracle as O
+        c = self.csr
+        cnt = np.diff(c.read_off)
+        oc = O.OracleCSR(c.read_off, c.iv_chrom, c.iv_start, c.iv_end, c.iv_aln, np.repeat(c.read_qlen2, cnt),
+                         np.repeat(c.read_nal, cnt), c.data_pos)
+        qd, nd, ov = self.diffs
+        o = O.run_core(oc, overlap=ov, use_cap=True, qlen_diff=qd, n_aln_diff=nd, edge_threshold=edge_threshold)
+        self._edges = np.stack([o['edge_a'], o['edge_b'], o['edge_I'], o['edge_U']], axis=1).astype(np.int64)
+        return {'applied': 1}

@@ -176,3 +176,229 @@ def test_device_shard_merge_two_contexts_one_gpu(monkeypatch):
         assert sorted(zip(a.tolist(), b.tolist())) == sorted(zip(o['edge_a'][mine].tolist(), o['edge_b'][mine].tolist()))
     for c in ctxs + [ref]:
         c.close()
+
+
+# ---- chromosome-split sweep (dist.SweepShard) ----------------------------------------------------
+
+def test_chrom_owner_balances():
+    from fslr_amd.dist import chrom_owner
+    cnt = np.array([100] * 23)
+    for world in (1, 2, 3, 8):
+        own = chrom_owner(cnt, world)
+        load = np.bincount(own, weights=cnt, minlength=world)
+        assert load.max() - load.min() <= 100
+    own = chrom_owner([5, 90, 10, 40, 50], 2)
+    load = np.bincount(own, weights=[5, 90, 10, 40, 50], minlength=2)
+    assert sorted(load.tolist()) == [95, 100]
+
+
+def test_emulated_sweep_split_equals_oracle(world_case):
+    """The decomposition itself, in one process: entries of each rank's chromosomes, routed by
+    first-read block, evaluated per destination — the union of the destinations' edges is the
+    oracle's edge set (with I, U), and no pair is evaluated twice."""
+    import torch
+    from fslr_amd.dist import chrom_counts_of, chrom_owner
+    from fslr_amd.prep import fold_overlap_threshold, pass_table
+    from tests.sweep_emu import EmuSweepContext
+    csr, o = world_case
+    thr = fold_overlap_threshold(csr.iv_aln, 0.8)
+    pt = pass_table([1, 1, 0.66, 0.66, 0.66, 0.5])
+    W = 3
+    owner = chrom_owner(chrom_counts_of(csr), W)
+    parts = [[] for _ in range(W)]
+    for r in range(W):
+        e = EmuSweepContext(csr, thr)
+        e.set_chrom_filter(owner == r)
+        buf = torch.empty(1 << 22, dtype=torch.int64)
+        ok, counts = e.sweep_partition(1 - 0.04, 1 - 0.25, pt, W, 6, buf)
+        assert ok
+        pos = np.concatenate([[0], np.cumsum(counts)])
+        for d in range(W):
+            parts[d].append(buf[pos[d]:pos[d + 1]].clone())
+    got = []
+    for d in range(W):
+        e = EmuSweepContext(csr, thr)
+        ent = torch.cat(parts[d])
+        assert ((ent >> (39 + 6)) % W == d).all()
+        e.sweep_evaluate(1 - 0.04, 1 - 0.25, pt, ent, ent.numel())
+        a, b, I, U = e.edges(e.stats()['n_edges'])
+        got += list(zip(a.tolist(), b.tolist(), I.tolist(), U.tolist()))
+    want = sorted(zip(o['edge_a'].tolist(), o['edge_b'].tolist(), o['edge_I'].tolist(), o['edge_U'].tolist()))
+    assert len(got) == len(set(got))
+    assert sorted(got) == want
+
+
+def _sweep_worker(rank, world, port, csr, thr, out_dir, edge_threshold):
+    import torch.distributed as dist
+    from fslr_amd.dist import SweepShard, chrom_counts_of
+    from fslr_amd.prep import pass_table
+    from tests.sweep_emu import EmuSweepContext
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    ctx = EmuSweepContext(csr, thr)
+    sh = SweepShard(ctx, csr.n_reads, chrom_counts_of(csr), world, rank, 'cpu')
+    info = sh.step(1 - 0.04, 1 - 0.25, pass_table([1, 1, 0.66, 0.66, 0.66, 0.5]), edge_threshold)
+    np.save(os.path.join(out_dir, f'labels{rank}.npy'), sh.labels())
+    a, b, I, U = ctx.edges(ctx.stats().get('n_edges', 0)) if not info['capped'] else (np.zeros(0),) * 4
+    np.save(os.path.join(out_dir, f'edges{rank}.npy'), np.stack([a, b, I, U], axis=1) if len(a) else np.zeros((0, 4)))
+    np.save(os.path.join(out_dir, f'info{rank}.npy'), np.array([info['capped'], info['max_fwd']]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('edge_threshold', [10, 2])
+def test_gloo_world2_sweep_shard_equals_oracle(world_case, tmp_path, edge_threshold):
+    """dist.SweepShard over gloo with world_size 2 (real all_to_all of entries, all-reduce of the
+    forward degree, all-gather of labels) on the emulated device: both ranks end with the oracle's
+    components; the ranks' edges partition the oracle's edges.  edge_threshold 2 makes the cap bind,
+    which takes the rank-0 replay and label broadcast."""
+    import torch.multiprocessing as mp
+    from fslr_amd.prep import fold_overlap_threshold
+    csr, o = world_case
+    thr = fold_overlap_threshold(csr.iv_aln, 0.8)
+    mp.start_processes(_sweep_worker, args=(2, _free_port(), csr, thr, str(tmp_path), edge_threshold), nprocs=2,
+                       join=True, start_method='spawn')
+    oc = _oracle_csr(csr)
+    ref = o if edge_threshold == 10 else O.run_core(oc, use_cap=True, edge_threshold=edge_threshold)
+    capped = [bool(np.load(tmp_path / f'info{r}.npy')[0]) for r in range(2)]
+    assert capped[0] == capped[1] == (int(o['fwd'].max()) > edge_threshold)     # o: uncapped E*
+    assert capped[0] == (edge_threshold == 2)
+    for r in range(2):
+        got = np.load(tmp_path / f'labels{r}.npy')
+        np.testing.assert_array_equal(_components_from_labels(got), ref['comp'])
+    if not capped[0]:
+        e = np.concatenate([np.load(tmp_path / f'edges{r}.npy') for r in range(2)]).astype(np.int64)
+        got = sorted(map(tuple, e.tolist()))
+        want = sorted(zip(o['edge_a'].tolist(), o['edge_b'].tolist(), o['edge_I'].tolist(), o['edge_U'].tolist()))
+        assert got == want
+
+
+def _sweep_split_on_device(csr, thr, pt, W, edge_threshold=10, block_shift=6):
+    """Run the chromosome split with W contexts on cuda:0, the exchange done in-process (the
+    concatenation of every rank's segment for each destination).  Returns the contexts (their
+    edges and labels after the in-process label merge) and the per-rank entry counts."""
+    import torch
+    from fslr_amd import _lib
+    from fslr_amd.dist import chrom_counts_of, chrom_owner
+    dev = torch.device('cuda', 0)
+    owner = chrom_owner(chrom_counts_of(csr), W)
+    segs = [[] for _ in range(W)]
+    sent = []
+    for r in range(W):
+        c = _lib.Context(0)
+        c.load_csr(csr, thr)
+        c.set_chrom_filter(owner == r)
+        c.build_index()
+        buf = torch.empty(1 << 16, dtype=torch.int64, device=dev)
+        ok, counts = c.sweep_partition(1 - 0.04, 1 - 0.25, pt, W, block_shift, buf)
+        if not ok:
+            buf = torch.empty(int(counts.sum()) + 16, dtype=torch.int64, device=dev)
+            ok, counts = c.sweep_partition(1 - 0.04, 1 - 0.25, pt, W, block_shift, buf)
+        assert ok
+        pos = np.concatenate([[0], np.cumsum(counts)])
+        for d in range(W):
+            segs[d].append(buf[pos[d]:pos[d + 1]].clone())
+        sent.append(counts)
+        c.close()
+    ctxs = []
+    for d in range(W):
+        c = _lib.Context(0)
+        c.load_csr(csr, thr)
+        c.reserve_edges(12 * csr.n_reads)
+        ent = torch.cat(segs[d]) if segs[d] else torch.empty(0, dtype=torch.int64, device=dev)
+        c.sweep_evaluate(1 - 0.04, 1 - 0.25, pt, ent, ent.numel(), edge_threshold)
+        torch.cuda.synchronize()
+        c.components()
+        ctxs.append(c)
+    n = csr.n_reads
+    locals_ = []
+    for c in ctxs:
+        t = torch.empty(n, dtype=torch.int32, device=dev)
+        c.labels_into(t)
+        locals_.append(t)
+    torch.cuda.synchronize()
+    gathered = torch.cat(locals_)
+    for c in ctxs:
+        c.union_label_vectors(gathered)
+    torch.cuda.synchronize()
+    return ctxs, np.array(sent)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('W', [2, 3, 8])
+def test_sweep_split_contexts_one_gpu_equals_oracle(W):
+    """fslr_set_chrom_filter / fslr_sweep_partition / fslr_sweep_evaluate with W contexts on one
+    GPU: the destinations' edges (a, b, I, U) partition the oracle's edges, their forward degrees
+    add up to the oracle's, and after the label merge every context has the oracle's components."""
+    from fslr_amd.dist import shard_of
+    from fslr_amd.prep import fold_overlap_threshold, pass_table
+    s = synth.generate(40_000, 16, 21)
+    csr = s.interval_data().csr()
+    thr = fold_overlap_threshold(csr.iv_aln, 0.8)
+    pt = pass_table([1, 1, 0.66, 0.66, 0.66, 0.5])
+    o = O.run_core(_oracle_csr(csr), use_cap=False)
+    ctxs, sent = _sweep_split_on_device(csr, thr, pt, W)
+    want = sorted(zip(o['edge_a'].tolist(), o['edge_b'].tolist(), o['edge_I'].tolist(), o['edge_U'].tolist()))
+    got = []
+    fwd = np.zeros(csr.n_reads, np.int64)
+    for d, c in enumerate(ctxs):
+        st = c.stats()
+        a, b, I, U = c.edges(st['n_edges'])
+        assert (shard_of(a, W) == d).all()           # 64-rank blocks round robin, as shard_of
+        got += list(zip(a.tolist(), b.tolist(), I.tolist(), U.tolist()))
+        fwd += c.fwd_degree()
+    assert sorted(got) == want
+    np.testing.assert_array_equal(fwd, o['fwd'])
+    for c in ctxs:
+        np.testing.assert_array_equal(_components_from_labels(c.labels()), o['comp'])
+        c.close()
+    # every rank sent something and the chromosome split is roughly balanced
+    per_rank = sent.sum(axis=1)
+    assert per_rank.min() > 0 and per_rank.max() < 2.0 * per_rank.mean()
+
+
+def _sweep_gpu_worker(rank, world, port, out_dir):
+    import torch
+    import torch.distributed as dist
+    from fslr_amd import _lib
+    from fslr_amd.dist import SweepShard, chrom_counts_of
+    from fslr_amd.prep import fold_overlap_threshold, pass_table
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    s = synth.generate(40_000, 16, 21)
+    csr = s.interval_data().csr()
+    dev = torch.device('cuda', 0)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    ctx = _lib.Context(0, stream=stream.cuda_stream)
+    ctx.load_csr(csr, fold_overlap_threshold(csr.iv_aln, 0.8))
+    sh = SweepShard(ctx, csr.n_reads, chrom_counts_of(csr), world, rank, dev)
+    pt = pass_table([1, 1, 0.66, 0.66, 0.66, 0.5])
+    for _ in range(2):                               # the second step reuses the grown buffers
+        info = sh.step(1 - 0.04, 1 - 0.25, pt, 10)
+    np.save(os.path.join(out_dir, f'labels{rank}.npy'), sh.labels())
+    st = ctx.stats()
+    a, b, I, U = ctx.edges(st['n_edges'])
+    np.save(os.path.join(out_dir, f'edges{rank}.npy'), np.stack([a, b, I, U], axis=1))
+    np.save(os.path.join(out_dir, f'info{rank}.npy'), np.array([info['capped'], info['entries_sent']]))
+    dist.barrier()
+    ctx.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sweep_shard_gloo_two_processes_one_gpu(tmp_path):
+    """dist.SweepShard as bench.py runs it, two processes sharing cuda:0 over gloo (entries and
+    labels staged through host memory): edges partition the oracle's, labels are the oracle's."""
+    import torch.multiprocessing as mp
+    mp.start_processes(_sweep_gpu_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True,
+                       start_method='spawn')
+    s = synth.generate(40_000, 16, 21)
+    csr = s.interval_data().csr()
+    o = O.run_core(_oracle_csr(csr), use_cap=False)
+    e = np.concatenate([np.load(tmp_path / f'edges{r}.npy') for r in range(2)]).astype(np.int64)
+    want = sorted(zip(o['edge_a'].tolist(), o['edge_b'].tolist(), o['edge_I'].tolist(), o['edge_U'].tolist()))
+    assert sorted(map(tuple, e.tolist())) == want
+    for r in range(2):
+        np.testing.assert_array_equal(_components_from_labels(np.load(tmp_path / f'labels{r}.npy')), o['comp'])
+        assert not np.load(tmp_path / f'info{r}.npy')[0]

@@ -1,22 +1,24 @@
 #!/usr/bin/env python3
-"""Per-rank device time of the multi-GPU step, measured on ONE GPU (no collective).
+"""Per-rank phase timing of the chromosome-split sweep, measured on ONE GPU.
 
-For world sizes W in --worlds, every shard r of W runs the rank's device work
-(build_index for its shard, fslr_query_shard, local union-find) in its own
-context, timed with HIP events over --steps repetitions; the merge that follows
-the RCCL all-gather (W-1 label unions + finalize) is timed on stand-in labels.
-Prints one JSON object: per W the max / mean over shards of each phase, the
-label-merge time, and the single-GPU step for comparison.  The all-gather
-itself needs W GPUs and is not measured here.
+For each world size W the ranks' work is run one rank at a time on cuda:0 with the data a rank
+would hold (every read; the index of its own chromosomes):
+  part[r]  = build_index (filtered) + fslr_sweep_partition (sweep, pack, route; ends in a sync)
+  eval[d]  = fslr_sweep_evaluate (sort + pair kernel) + components over the entries destined to d
+  merge    = union of W label vectors + finalize (the replicated step)
+and the single-context step (build_index + sweep query + components) as the W = 1 baseline.
+The exchange itself cannot run on one GPU; it is priced from the bytes each rank moves
+(entries all_to_all: the off-rank share of its entries; labels all_gather: 4 N (W - 1)) at an
+assumed per-GPU xGMI rate (--xgmi-gbs, default 300 GB/s of the 7 x ~153 GB/s links, both
+directions shared) plus a fixed per-collective latency (--coll-us).
 
-    python tools/shard_timing.py [--reads 1000000] [--worlds 1,2,4,8]
+    python tools/shard_timing.py --reads 1000000 --lmax 16 > gpurun_out/shard_cfg4.json
 """
-from __future__ import annotations
-
 import argparse
 import json
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -24,88 +26,129 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--reads', type=int, default=1_000_000)
     ap.add_argument('--lmax', type=int, default=16)
-    ap.add_argument('--seed', type=int, default=11)
     ap.add_argument('--dist', default='uniform')
+    ap.add_argument('--seed', type=int, default=1)
     ap.add_argument('--worlds', default='1,2,4,8')
-    ap.add_argument('--steps', type=int, default=5)
+    ap.add_argument('--reps', type=int, default=5)
+    ap.add_argument('--xgmi-gbs', type=float, default=300.0)
+    ap.add_argument('--coll-us', type=float, default=30.0)
     args = ap.parse_args()
-
     import torch
     from fslr_amd import _lib, synth
+    from fslr_amd.dist import chrom_counts_of, chrom_owner
     from fslr_amd.prep import fold_overlap_threshold, pass_table
 
+    t = time.perf_counter()
     s = synth.generate(args.reads, args.lmax, args.seed, dist=args.dist)
     csr = s.interval_data().csr()
+    del s
+    log(f'data: {csr.n_reads} reads, {csr.n_intervals} intervals in {time.perf_counter() - t:.0f}s')
+    n = csr.n_reads
     thr = fold_overlap_threshold(csr.iv_aln, 0.8)
     pt = pass_table([1, 1, 0.66, 0.66, 0.66, 0.5])
-    qcut, ncut = 1 - 0.04, 1 - 0.25
-    stream = torch.cuda.Stream()
+    qc, nc = 1 - 0.04, 1 - 0.25
+    dev = torch.device('cuda', 0)
+    stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
-    n = csr.n_reads
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
-    out = {'n_reads': n, 'n_intervals': int(csr.n_intervals), 'worlds': {}}
-    print(f'input {n} reads, {csr.n_intervals} intervals', file=sys.stderr, flush=True)
 
-    ctx = _lib.Context(0, stream=stream.cuda_stream)
-    ctx.load_csr(csr, thr)
-    ctx.reserve_edges(12 * n)
+    def timed(fn, reps):
+        fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            ts.append(1000 * (time.perf_counter() - t0))
+        return float(np.median(ts))
+
+    # W = 1: the single-context step (the bench's step without the cap)
+    c1 = _lib.Context(0, stream=stream.cuda_stream)
+    c1.load_csr(csr, thr)
+    c1.reserve_edges(12 * n)
+
+    def single():
+        c1.build_index()
+        c1.query(qc, nc, pt, 10, engine='sweep')
+        c1.components()
+    t1 = timed(single, args.reps)
+    st1 = c1.stats()
+    log(f'W=1 step {t1:.3f} ms, {st1["n_edges"]} edges, {st1["match_entries"]} entries')
+    c1.close()
+
+    cp = _lib.Context(0, stream=stream.cuda_stream)
+    cp.load_csr(csr, thr)
+    ce = _lib.Context(0, stream=stream.cuda_stream)
+    ce.load_csr(csr, thr)
+    ce.reserve_edges(12 * n)
+    out = {'workload': f'{n} reads x 1-{args.lmax} ({args.dist}), seed {args.seed}', 'n_reads': n,
+           'n_intervals': int(csr.n_intervals), 'single_step_ms': t1, 'match_entries': int(st1['match_entries']),
+           'edges': int(st1['n_edges']), 'xgmi_gbs_assumed': args.xgmi_gbs, 'collective_latency_us': args.coll_us,
+           'worlds': []}
+    counts = chrom_counts_of(csr)
     for W in [int(x) for x in args.worlds.split(',')]:
-        per = []
+        owner = chrom_owner(counts, W)
+        part, segs, sent = [], [[] for _ in range(W)], []
+        buf = torch.empty(max(1 << 16, int(1.2 * st1['match_entries'] / W) + 4096), dtype=torch.int64, device=dev)
         for r in range(W):
-            ctx.set_shard(r, W)
-            t = np.zeros((args.steps, 4))
-            for k in range(args.steps + 1):
-                ev[0].record(stream)
-                ctx.build_index()
-                ev[1].record(stream)
-                if W == 1:
-                    ctx.query(qcut, ncut, pt, 10)
-                else:
-                    ctx.query_shard(qcut, ncut, pt, r, W)
-                ev[2].record(stream)
-                ctx.components()
-                ev[3].record(stream)
-                torch.cuda.synchronize()
-                if k:
-                    t[k - 1] = [ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2]), ev[2].elapsed_time(ev[3]),
-                                ev[0].elapsed_time(ev[3])]
-            st = ctx.stats()
-            per.append(dict(zip(('index_ms', 'query_ms', 'components_ms', 'total_ms'), np.median(t, 0).tolist()),
-                            pairs=int(st['evaluated_pairs']), edges=int(st['n_edges'])))
-            print(f'W={W} r={r} {per[-1]}', file=sys.stderr, flush=True)
-        # merge after the all-gather: W-1 unions of N (k, label_g[k]) pairs + finalize
-        merge_ms = 0.0
-        if W > 1:
-            lab = torch.from_numpy(ctx.labels().astype(np.int32)).to('cuda')
-            g = lab.repeat(W)
-            tm = []
-            for k in range(args.steps + 1):
-                ev[0].record(stream)
-                ctx.union_pairs(None, g.data_ptr(), W * n, on_device=True)     # as DeviceShardMerge
-                ctx.finalize_labels()
-                ev[1].record(stream)
-                torch.cuda.synchronize()
-                if k:
-                    tm.append(ev[0].elapsed_time(ev[1]))
-            merge_ms = float(np.median(tm))
-        agg = {k: {'max': max(p[k] for p in per), 'mean': float(np.mean([p[k] for p in per]))}
-               for k in ('index_ms', 'query_ms', 'components_ms', 'total_ms')}
-        agg['merge_ms'] = merge_ms
-        agg['pairs_sum'] = sum(p['pairs'] for p in per)
-        agg['per_shard'] = per
-        out['worlds'][W] = agg
-    one = out['worlds'].get(1)
-    for W, a in out['worlds'].items():
-        step = a['total_ms']['max'] + a['merge_ms']
-        a['est_step_ms_excl_allgather'] = step
-        if one:
-            a['est_speedup_excl_allgather'] = one['total_ms']['max'] / step
-    ctx.close()
-    print(json.dumps(out))
+            cp.set_chrom_filter(owner == r if W > 1 else None)
+            res = {}
+
+            def p():
+                nonlocal buf
+                cp.build_index()
+                ok, cnt = cp.sweep_partition(qc, nc, pt, W, 6, buf)
+                if not ok:
+                    buf = torch.empty(int(cnt.sum() * 1.1) + 4096, dtype=torch.int64, device=dev)
+                    ok, cnt = cp.sweep_partition(qc, nc, pt, W, 6, buf)
+                res['cnt'] = cnt
+            part.append(timed(p, args.reps))
+            cnt = res['cnt']
+            pos = np.concatenate([[0], np.cumsum(cnt)])
+            for d in range(W):
+                segs[d].append(buf[pos[d]:pos[d + 1]].clone())
+            sent.append(cnt)
+        evl, nedges = [], 0
+        for d in range(W):
+            ent = torch.cat(segs[d])
+
+            def e():
+                ce.sweep_evaluate(qc, nc, pt, ent, ent.numel())
+                ce.components()
+            evl.append(timed(e, args.reps))
+            nedges += ce.stats()['n_edges']
+            segs[d] = None
+            del ent
+        assert nedges == st1['n_edges'], (nedges, st1['n_edges'])
+        gathered = torch.zeros(W * n, dtype=torch.int32, device=dev)
+        ce.labels_into(gathered[:n])
+        merge = timed(lambda: ce.union_label_vectors(gathered), args.reps) if W > 1 else 0.0
+        sent = np.array(sent)
+        off_rank = np.array([sent[r].sum() - sent[r, r] for r in range(W)])
+        recv = sent.sum(axis=0)
+        a2a_ms = 0.0 if W == 1 else (8 * max(off_rank.max(), (recv - np.diag(sent)).max()) / (args.xgmi_gbs * 1e6)
+                                     + 2 * args.coll_us / 1000)
+        gather_ms = 0.0 if W == 1 else 4 * n * (W - 1) / (args.xgmi_gbs * 1e6) + args.coll_us / 1000
+        step = max(part) + a2a_ms + max(evl) + gather_ms + merge
+        row = {'W': W, 'part_ms': part, 'eval_ms': evl, 'merge_ms': merge, 'a2a_ms_model': a2a_ms,
+               'gather_ms_model': gather_ms, 'entries_sent_per_rank': sent.sum(axis=1).tolist(),
+               'entries_recv_per_rank': recv.tolist(), 'projected_step_ms': step,
+               'projected_speedup': t1 / step}
+        log(f'W={W}: part max {max(part):.3f} ms, eval max {max(evl):.3f} ms, merge {merge:.3f} ms, '
+            f'a2a {a2a_ms:.3f} ms, gather {gather_ms:.3f} ms -> {step:.3f} ms ({t1 / step:.2f}x)')
+        out['worlds'].append(row)
+        print(json.dumps(row), flush=True)
+    print(json.dumps(out), flush=True)
+    cp.close()
+    ce.close()
 
 
 if __name__ == '__main__':
