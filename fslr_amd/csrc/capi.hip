@@ -67,7 +67,7 @@ int reserve_entries(fslr_ctx* c, int64_t capacity) {
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   int rc;
   if ((rc = dalloc(c, &c->ent, capacity)) || (rc = dalloc(c, &c->ent_sorted, capacity))) return rc;
-  const size_t need = sweep_temp_bytes(capacity, std::max<int64_t>(c->ni, 64), c->stream);
+  const size_t need = sweep_temp_bytes(capacity, std::max<int64_t>(std::max(c->ni, c->n), 64), c->stream);
   if (need > c->sweep_temp_bytes) {
     if (c->sweep_temp) (void)hipFree(c->sweep_temp);
     c->sweep_temp = nullptr;
@@ -76,6 +76,12 @@ int reserve_entries(fslr_ctx* c, int64_t capacity) {
   }
   c->ent_cap = capacity;
   return FSLR_OK;
+}
+
+// the grouping sort's bucket counts and offsets (fixed size)
+static int ensure_grp(fslr_ctx* c) {
+  if (c->grp) return FSLR_OK;
+  return dalloc(c, &c->grp, grp_ints());
 }
 
 int thr_mode_of(const int32_t* thr, int64_t ni) {
@@ -124,7 +130,7 @@ void fslr_ctx_destroy(fslr_ctx* c) {
                   c->temp,   c->umax,   c->edges,   c->edge_iu, c->fwd,     c->parent,  c->counters,
                   c->errw,   c->thr_tmp, c->defer,   c->dchrom,  c->drec,    c->lbounds, c->diag, c->wstat,
                   c->dgate,  c->chist,  c->heavy, c->ent, c->ent_sorted, c->sweep_temp, c->sw_tile, c->sw_wstat, c->ent_ub,
-                  c->fdchrom, c->fdrec, c->fdgate, c->crange_f, c->part_cnt};
+                  c->fdchrom, c->fdrec, c->fdgate, c->crange_f, c->part_cnt, c->grp};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->sw_total) (void)hipHostFree(c->sw_total);
@@ -444,6 +450,8 @@ static int sweep_front(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64
     if ((rc = dalloc(c, &c->ent_ub, std::max<int64_t>(1 << 20, 4 * nix)))) return rc;
     c->ent_ub_cap = std::max<int64_t>(1 << 20, 4 * nix);
   }
+  if ((rc = ensure_grp(c))) return rc;
+  s.grp = c->grp;
   s.rmeta = c->rmeta;
   s.idx4 = c->idx4;
   s.idx_gate = c->idx_gate;
@@ -720,7 +728,9 @@ int fslr_sweep_evaluate(fslr_ctx* c, const fslr_params* p, const void* entries, 
   }
   c->last_full = false;
   c->last_engine = FSLR_ENGINE_SWEEP;
+  if (int rc = ensure_grp(c)) return rc;
   SweepArgs s{};
+  s.grp = c->grp;
   s.rmeta = c->rmeta;
   s.umax = c->umax;
   s.ni = 0;
@@ -728,6 +738,7 @@ int fslr_sweep_evaluate(fslr_ctx* c, const fslr_params* p, const void* entries, 
   s.a_begin = 0;
   s.a_end = static_cast<int>(c->n);
   s.ent = static_cast<unsigned long long*>(const_cast<void*>(entries));
+  s.ent_mid = c->ent;
   s.ent_sorted = c->ent_sorted;
   s.n_ent = n;
   s.temp = c->sweep_temp;

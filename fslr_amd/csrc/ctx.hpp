@@ -28,6 +28,7 @@ struct fslr_ctx {
   int2* fdgate = nullptr;
   int64_t f_cap = 0;
   int2* crange_f = nullptr;                 // [64] chromosome ranges of the filtered index
+  int* grp = nullptr;                       // [grp_ints()] grouping sort: bucket counts / offsets
   long long* part_cnt = nullptr;            // partition scratch: per (destination, block) counts + offsets
   int shard = 0, n_shards = 1;             // fslr_set_shard: A-side index data for this shard only
   int built_shard = 0, built_n_shards = 1;

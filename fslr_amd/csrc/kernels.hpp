@@ -167,6 +167,8 @@ struct SweepArgs {
   long long ub_cap;
   unsigned long long* ent;            // [n_ent] match entries A << 39 | B << 14 | i << 7 | j, tile order
   unsigned long long* ent_sorted;     // [n_ent] grouped by A
+  unsigned long long* ent_mid;        // (mode 3) [n_ent] grouping scratch
+  int* grp;                           // [grp_ints()] grouping-sort bucket counts / offsets (null: radix sort)
   long long n_ent;                    // (emit / pairs) entries of the count pass
   void* temp;                         // hipcub scratch (tile scan, grouping sort)
   size_t temp_bytes;
@@ -193,6 +195,7 @@ hipError_t launch_sweep_count(const SweepArgs& a, int mode, long long* total_dev
 hipError_t launch_sweep_pairs(const SweepArgs& a, int mode, hipStream_t s);
 // only the packing / emit step of launch_sweep_pairs: dense entries in a.ent
 hipError_t launch_sweep_dense(const SweepArgs& a, int mode, hipStream_t s);
+int grp_ints();
 
 // ---- multi-GPU sweep (shard.hip) -------------------------------------------------------------
 constexpr int kMaxDest = 64;          // destination ranks of one partition

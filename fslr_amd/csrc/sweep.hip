@@ -621,6 +621,104 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
   if (lane == 2 || lane == 3) g.wstat[static_cast<long long>(wid) * kWsFields + lane] = f;
 }
 
+// ---- 2. grouping by A: a two-level counting sort ---------------------------------------------------
+// Pass 1 scatters the entries into H buckets of A's high bits (per-block LDS histograms, one scan
+// over the [bucket][block] counts, LDS cursors); pass 2 groups each bucket by A's low bits in one
+// workgroup (LDS histogram and cursors; the bucket, a few thousand entries, stays in L2 between its
+// two reads).  Two reads + one write per pass instead of the radix sort's three 8-bit passes, and
+// pass 1 reads the sweep's upper-bound tile slots directly (no packing).  Unstable: the order inside
+// a run is free (k_sweep_pairs hashes its partners).
+constexpr int kMsdBlocks = 256;            // pass-1 workgroups
+constexpr int kMsdThreads = 1024;
+constexpr int kMsdMaxH = 8192;             // buckets (LDS histogram of pass 1)
+constexpr int kMsdMaxLo = 4096;            // low-digit bins (LDS histogram of pass 2)
+constexpr int kGrpInts = 2 * kMsdMaxH * kMsdBlocks;
+
+// kTiles: entries of tile t at src[ub[t] .. ub[t] + cnt[t]) (one wave per tile, the block's tiles a
+// contiguous range); else dense src[0, n) in contiguous block chunks.  kScatter = false: histogram.
+template <bool kTiles, bool kScatter>
+__global__ __launch_bounds__(kMsdThreads) void k_msd_pass1(const unsigned long long* __restrict__ src, long long n,
+                                                           const long long* __restrict__ ub,
+                                                           const long long* __restrict__ cnt, int nt, int shift,
+                                                           int H, int* __restrict__ mat,
+                                                           unsigned long long* __restrict__ dst) {
+  __shared__ int hist[kMsdMaxH];
+  const int tid = threadIdx.x;
+  const int P = gridDim.x;
+  for (int i = tid; i < H; i += kMsdThreads) hist[i] = kScatter ? mat[i * P + blockIdx.x] : 0;
+  __syncthreads();
+  auto visit = [&](unsigned long long v) {
+    const int d = static_cast<int>(v >> shift);
+    if (kScatter)
+      dst[atomicAdd(&hist[d], 1)] = v;
+    else
+      atomicAdd(&hist[d], 1);
+  };
+  if (kTiles) {
+    const int per = (nt + P - 1) / P;
+    const int t0 = blockIdx.x * per, t1 = min(nt, t0 + per);
+    const int lane = tid & (kWave - 1), w = tid >> 6;
+    for (int t = t0 + w; t < t1; t += kMsdThreads / kWave) {
+      const long long c = cnt[t], a = ub[t];
+      for (long long k = lane; k < c; k += kWave) visit(src[a + k]);
+    }
+  } else {
+    const long long chunk = (n + P - 1) / P;
+    const long long b0 = blockIdx.x * chunk, b1 = min(n, b0 + chunk);
+    for (long long k = b0 + tid; k < b1; k += kMsdThreads) visit(src[k]);
+  }
+  if (!kScatter) {
+    __syncthreads();
+    for (int i = tid; i < H; i += kMsdThreads) mat[i * P + blockIdx.x] = hist[i];
+  }
+}
+
+// one workgroup per bucket: group [off[b P], off[(b + 1) P]) by A's low `lo_bits` bits into dst
+__global__ __launch_bounds__(256) void k_msd_pass2(const unsigned long long* __restrict__ src, long long n,
+                                                   const int* __restrict__ off, int P, int H, int lo_bits,
+                                                   unsigned long long* __restrict__ dst) {
+  __shared__ int hist[kMsdMaxLo];
+  __shared__ int wsum[4];
+  const int tid = threadIdx.x;
+  const int nb = 1 << lo_bits;
+  const int b = blockIdx.x;
+  const long long s = off[static_cast<long long>(b) * P];
+  const long long e = b + 1 < H ? off[static_cast<long long>(b + 1) * P] : n;
+  if (e - s <= 1) {
+    if (tid == 0 && e > s) dst[s] = src[s];
+    return;
+  }
+  for (int i = tid; i < nb; i += 256) hist[i] = 0;
+  __syncthreads();
+  const unsigned mask = static_cast<unsigned>(nb - 1);
+  for (long long k = s + tid; k < e; k += 256) atomicAdd(&hist[static_cast<unsigned>(src[k] >> 39) & mask], 1);
+  __syncthreads();
+  // exclusive scan of hist: each thread owns a contiguous run of per = nb / 256 bins (or one bin)
+  const int per = nb >= 256 ? nb / 256 : 1;
+  const int first = tid * per;
+  int loc = 0;
+  if (first < nb)
+    for (int i = 0; i < per; ++i) loc += hist[first + i];
+  const int inc = wave_incl_scan(loc);
+  if ((tid & 63) == 63) wsum[tid >> 6] = inc;
+  __syncthreads();
+  int base = inc - loc;
+  for (int w = 0; w < (tid >> 6); ++w) base += wsum[w];
+  if (first < nb) {
+    int run = static_cast<int>(s) + base;          // positions fit 31 bits (n < 2^31)
+    for (int i = 0; i < per; ++i) {
+      const int c = hist[first + i];
+      hist[first + i] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  for (long long k = s + tid; k < e; k += 256) {
+    const unsigned long long v = src[k];
+    dst[atomicAdd(&hist[static_cast<unsigned>(v >> 39) & mask], 1)] = v;
+  }
+}
+
 int bits_for(long long v) {
   int b = 1;
   while ((1ll << b) <= v) ++b;
@@ -650,14 +748,16 @@ int sweep_max_waves() {
 }
 
 size_t sweep_temp_bytes(long long ent_cap, long long ni, hipStream_t s) {
-  size_t a = 0, b = 0;
+  size_t a = 0, b = 0, c = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, c, static_cast<int*>(nullptr), static_cast<int*>(nullptr),
+                                         kGrpInts / 2, s);
   (void)hipcub::DeviceRadixSort::SortKeys(nullptr, a, static_cast<unsigned long long*>(nullptr),
                                           static_cast<unsigned long long*>(nullptr), static_cast<int>(ent_cap), 39,
                                           64, s);
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, static_cast<long long*>(nullptr),
                                          static_cast<long long*>(nullptr), static_cast<int>((ni + kWave - 1) / kWave),
                                          s);
-  return std::max(a, b);
+  return std::max(std::max(a, b), c);
 }
 
 hipError_t launch_sweep_plan(const SweepArgs& a, hipStream_t s) {
@@ -702,14 +802,64 @@ hipError_t launch_sweep_dense(const SweepArgs& a, int mode, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_sweep_pairs(const SweepArgs& a, int mode, hipStream_t s) {
+int grp_ints() { return kGrpInts; }
+
+// group the entries by A: from the tile slots (mode 2) or dense `src` into `mid`, then into `out`
+static hipError_t group_by_a(const SweepArgs& a, int mode, const unsigned long long* src, unsigned long long* mid,
+                             unsigned long long* out, hipStream_t s) {
+  const long long n = a.n_ent;
+  const int nbits = bits_for(std::max(1, a.n_reads - 1));
+  int hb = 0;                                               // H = 2^hb buckets of ~4096 entries
+  while (hb < 13 && (n >> (12 + hb)) > 0) ++hb;
+  hb = std::max(hb, nbits - 12);                            // low digit <= 12 bits (LDS bins)
+  hb = std::min(hb, nbits);
+  const int H = 1 << hb, lo = nbits - hb;
+  const int shift = 39 + lo;
+  int* mat = a.grp;
+  int* off = a.grp + kGrpInts / 2;
+  const int nt = tiles_of(a);
+  if (mode == 2) {
+    k_msd_pass1<true, false><<<kMsdBlocks, kMsdThreads, 0, s>>>(a.ent_ub, n, a.tile_ub, a.tile_cnt, nt, shift, H,
+                                                                mat, nullptr);
+  } else {
+    k_msd_pass1<false, false><<<kMsdBlocks, kMsdThreads, 0, s>>>(src, n, nullptr, nullptr, 0, shift, H, mat, nullptr);
+  }
+  size_t tb = a.temp_bytes;
+  hipError_t e = hipcub::DeviceScan::ExclusiveSum(a.temp, tb, mat, off, H * kMsdBlocks, s);
+  if (e != hipSuccess) return e;
+  if (mode == 2) {
+    k_msd_pass1<true, true><<<kMsdBlocks, kMsdThreads, 0, s>>>(a.ent_ub, n, a.tile_ub, a.tile_cnt, nt, shift, H,
+                                                               off, mid);
+  } else {
+    k_msd_pass1<false, true><<<kMsdBlocks, kMsdThreads, 0, s>>>(src, n, nullptr, nullptr, 0, shift, H, off, mid);
+  }
+  k_msd_pass2<<<H, 256, 0, s>>>(mid, n, off, kMsdBlocks, H, lo, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_sweep_pairs(const SweepArgs& a0, int mode, hipStream_t s) {
+  SweepArgs a = a0;
   if (a.ev[2]) (void)hipEventRecord(a.ev[2], s);
-  if (mode != 3) {
-    hipError_t e = launch_sweep_dense(a, mode, s);
+  const bool msd = a.grp && a.n_ent > 0 && a.n_ent < (1ll << 31);
+  if (mode == 0 || (mode == 2 && !msd)) {
+    hipError_t e = launch_sweep_dense(a, mode, s);          // dense entries in a.ent
     if (e != hipSuccess) return e;
   }
   if (a.ev[3]) (void)hipEventRecord(a.ev[3], s);
-  if (a.n_ent > 0) {
+  if (msd) {
+    // mode 2: tile slots -> ent -> ent_sorted; mode 0: ent -> ent_sorted -> ent (the pair kernel
+    // then reads ent); mode 3: the caller's entries -> ent_mid -> ent_sorted
+    hipError_t e;
+    if (mode == 2) {
+      e = group_by_a(a, 2, nullptr, a.ent, a.ent_sorted, s);
+    } else if (mode == 0) {
+      e = group_by_a(a, 0, a.ent, a.ent_sorted, a.ent, s);
+      a.ent_sorted = a.ent;
+    } else {
+      e = group_by_a(a, 3, a.ent, a.ent_mid, a.ent_sorted, s);
+    }
+    if (e != hipSuccess) return e;
+  } else if (a.n_ent > 0) {
     size_t tb = a.temp_bytes;
     const int end_bit = 39 + bits_for(std::max(1, a.n_reads - 1));
     hipError_t e = hipcub::DeviceRadixSort::SortKeys(a.temp, tb, a.ent, a.ent_sorted, static_cast<int>(a.n_ent), 39,
