@@ -13,7 +13,7 @@
 //      their reads' lists, cluster.py:189-191).  Two passes over 64-position tiles: the first counts
 //      each tile's entries, a scan places the tiles, the second writes them — no global atomics
 //      (one contended counter saturates near 90 returning atomics per microsecond).
-//   2. the entries are grouped by A (hipcub radix sort on A's bits only).
+//   2. the entries are grouped by A (a two-level counting sort, group_by_a).
 //   3. k_sweep_pairs: per run of one read A, an LDS hash over its partners B collects each pair's
 //      match matrix as row / column masks; first-fit greedy (overall_jaccard_similarity, :152-161)
 //      is the entry count unless two entries share a row or a column, where the rows are walked in
@@ -622,50 +622,143 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
 }
 
 // ---- 2. grouping by A: a two-level counting sort ---------------------------------------------------
-// Pass 1 scatters the entries into H buckets of A's high bits (per-block LDS histograms, one scan
-// over the [bucket][block] counts, LDS cursors); pass 2 groups each bucket by A's low bits in one
-// workgroup (LDS histogram and cursors; the bucket, a few thousand entries, stays in L2 between its
-// two reads).  Two reads + one write per pass instead of the radix sort's three 8-bit passes, and
-// pass 1 reads the sweep's upper-bound tile slots directly (no packing).  Unstable: the order inside
-// a run is free (k_sweep_pairs hashes its partners).
-constexpr int kMsdBlocks = 256;            // pass-1 workgroups
+// Pass 1 scatters the entries into H = 2^hb buckets of A's high bits with per-block LDS histograms,
+// one scan over the [bucket][block] counts and LDS cursors; pass 2 groups each bucket by A's low bits
+// in one workgroup (LDS histogram and cursors; the bucket, a few thousand entries, stays in L2
+// between its two reads).  A read's entries arrive in runs (the sweep emits a position's partners
+// together), so each wave adds one run's length with one atomic from the run's first lane.  Reads
+// come out in ascending order (the union-find over the edges k_sweep_pairs writes in that order keeps
+// its locality); inside a run the order is free (k_sweep_pairs hashes the partners).
+// Two reads and one write per pass; pass 1 reads the sweep's upper-bound tile slots (no packing).
+constexpr int kMsdMaxBlocks = 1024;       // pass-1 workgroups (at most)
 constexpr int kMsdThreads = 1024;
 constexpr int kMsdMaxH = 8192;             // buckets (LDS histogram of pass 1)
-constexpr int kMsdMaxLo = 4096;            // low-digit bins (LDS histogram of pass 2)
-constexpr int kGrpInts = 2 * kMsdMaxH * kMsdBlocks;
+constexpr int kMsdMaxLo = 4096;            // in-bucket bins (LDS histogram of pass 2)
+constexpr int kGrpInts = 2 * (1 << 21);    // [bucket][block] counts and their scan (H P <= 2^21)
+constexpr int kMsdUnroll = 8;              // entries loaded per lane before their atomics
+
+// One wave-instruction of keys (lanes with `act`, a contiguous prefix): equal keys on adjacent lanes
+// form runs; the run's first lane adds its length to bin[key] (returning the base when `ret`), every
+// lane gets base + its offset in the run.
+template <bool kRet>
+__device__ __forceinline__ int run_add(int* bin, int key, bool act, int lane) {
+  const int prev = __shfl_up(key, 1);
+  const bool head = act && (lane == 0 || prev != key);
+  const unsigned long long hm = __ballot(head);
+  const unsigned long long am = __ballot(act);
+  const int n_act = __popcll(am);
+  int base = 0;
+  if (head) {
+    const unsigned long long nx = hm & above(lane);
+    const int len = (nx ? __builtin_ctzll(nx) : n_act) - lane;
+    if (kRet) base = atomicAdd(&bin[key], len);
+    else atomicAdd(&bin[key], len);
+  }
+  if (!kRet) return 0;
+  const int my_head = 63 - __builtin_clzll(hm & upto(lane));   // lane 0 is a head when active
+  return __shfl(base, act ? my_head : 0) + (lane - my_head);
+}
 
 // kTiles: entries of tile t at src[ub[t] .. ub[t] + cnt[t]) (one wave per tile, the block's tiles a
 // contiguous range); else dense src[0, n) in contiguous block chunks.  kScatter = false: histogram.
 template <bool kTiles, bool kScatter>
 __global__ __launch_bounds__(kMsdThreads) void k_msd_pass1(const unsigned long long* __restrict__ src, long long n,
                                                            const long long* __restrict__ ub,
-                                                           const long long* __restrict__ cnt, int nt, int shift,
-                                                           int H, int* __restrict__ mat,
+                                                           const long long* __restrict__ cnt, int nt,
+                                                           int lo_bits, int H, int* __restrict__ mat,
                                                            unsigned long long* __restrict__ dst) {
   __shared__ int hist[kMsdMaxH];
   const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1), w = tid >> 6;
   const int P = gridDim.x;
   for (int i = tid; i < H; i += kMsdThreads) hist[i] = kScatter ? mat[i * P + blockIdx.x] : 0;
   __syncthreads();
-  auto visit = [&](unsigned long long v) {
-    const int d = static_cast<int>(v >> shift);
-    if (kScatter)
-      dst[atomicAdd(&hist[d], 1)] = v;
-    else
-      atomicAdd(&hist[d], 1);
+  // a span [a, a + c) of consecutive entries: kMsdUnroll wave-loads in flight, then their runs
+  auto span = [&](long long a, long long c) {
+    for (long long k0 = 0; k0 < c; k0 += kMsdUnroll * kWave) {
+      unsigned long long v[kMsdUnroll];
+#pragma unroll
+      for (int u = 0; u < kMsdUnroll; ++u) {
+        const long long k = k0 + u * kWave + lane;
+        v[u] = k < c ? src[a + k] : 0ull;
+      }
+#pragma unroll
+      for (int u = 0; u < kMsdUnroll; ++u) {
+        const long long k = k0 + u * kWave + lane;
+        if (k0 + u * kWave >= c) break;                     // wave-uniform
+        const bool act = k < c;
+        const int d = static_cast<int>(static_cast<unsigned>(v[u] >> 39) >> lo_bits);
+        if (kScatter) {
+          const int p = run_add<true>(hist, d, act, lane);
+          if (act) dst[p] = v[u];
+        } else {
+          run_add<false>(hist, d, act, lane);
+        }
+      }
+    }
   };
   if (kTiles) {
-    const int per = (nt + P - 1) / P;
-    const int t0 = blockIdx.x * per, t1 = min(nt, t0 + per);
-    const int lane = tid & (kWave - 1), w = tid >> 6;
-    for (int t = t0 + w; t < t1; t += kMsdThreads / kWave) {
-      const long long c = cnt[t], a = ub[t];
-      for (long long k = lane; k < c; k += kWave) visit(src[a + k]);
+    // groups of G consecutive tiles per wave (G <= 64, about one group per wave of the grid): lane l
+    // holds tile g G + l's count and slot; the group's entries are walked as one dense range of
+    // kMsdUnroll x 64 entries per step, each lane finding its tile by a binary search over the lanes
+    const int nwave = P * (kMsdThreads / kWave);
+    const int G = max(1, min(kWave, (nt + nwave - 1) / nwave));
+    const int ngroups = (nt + G - 1) / G;
+    for (int g = blockIdx.x * (kMsdThreads / kWave) + w; g < ngroups; g += nwave) {
+      const int t = g * G + lane;
+      const bool tv = lane < G && t < nt;
+      const int c = tv ? static_cast<int>(cnt[t]) : 0;
+      const long long u0 = tv ? ub[t] : 0;
+      const int inc = wave_incl_scan(c);
+      const int exc = inc - c;
+      const int T = rdl(inc, kWave - 1);
+      for (int k0 = 0; k0 < T; k0 += kMsdUnroll * kWave) {
+        unsigned long long v[kMsdUnroll];
+#pragma unroll
+        for (int q = 0; q < kMsdUnroll; ++q) {
+          const int kc = k0 + q * kWave;                    // chunk start (wave-uniform)
+          const int k = kc + lane;
+          // lane k's tile: the tile holding the chunk start, then the tiles starting inside the
+          // chunk (usually 0-2 of them; a binary search over the lanes when there are many)
+          int j = 63 - __builtin_clzll(__ballot(c > 0 && exc <= kc) | 1ull);
+          const unsigned long long st = __ballot(c > 0 && exc > kc && exc < kc + kWave);
+          if (__popcll(st) <= 4) {
+            for (unsigned long long m = st; m; m &= m - 1) {
+              const int jj = __builtin_ctzll(m);
+              if (k >= rdl(exc, jj)) j = jj;
+            }
+          } else {
+            int lo = 0, hi = kWave - 1;                     // largest lane j with exc[j] <= k
+#pragma unroll
+            for (int it = 0; it < 6; ++it) {
+              const int mid = (lo + hi + 1) >> 1;
+              if (__shfl(exc, mid) <= k) lo = mid; else hi = mid - 1;
+            }
+            j = lo;
+          }
+          const long long at = __shfl(u0, j) + (k - __shfl(exc, j));
+          v[q] = k < T ? src[at] : 0ull;
+        }
+#pragma unroll
+        for (int q = 0; q < kMsdUnroll; ++q) {
+          if (k0 + q * kWave >= T) break;                   // wave-uniform
+          const bool act = k0 + q * kWave + lane < T;
+          const int d = static_cast<int>(static_cast<unsigned>(v[q] >> 39) >> lo_bits);
+          if (kScatter) {
+            const int p = run_add<true>(hist, d, act, lane);
+            if (act) dst[p] = v[q];
+          } else {
+            run_add<false>(hist, d, act, lane);
+          }
+        }
+      }
     }
   } else {
     const long long chunk = (n + P - 1) / P;
     const long long b0 = blockIdx.x * chunk, b1 = min(n, b0 + chunk);
-    for (long long k = b0 + tid; k < b1; k += kMsdThreads) visit(src[k]);
+    // the block's chunk in wave-sized spans of 4 x 64 entries, dealt to its waves
+    const long long step = kMsdUnroll * kWave;
+    for (long long a = b0 + w * step; a < b1; a += (kMsdThreads / kWave) * step) span(a, min(step, b1 - a));
   }
   if (!kScatter) {
     __syncthreads();
@@ -673,13 +766,14 @@ __global__ __launch_bounds__(kMsdThreads) void k_msd_pass1(const unsigned long l
   }
 }
 
-// one workgroup per bucket: group [off[b P], off[(b + 1) P]) by A's low `lo_bits` bits into dst
+// one workgroup per bucket: group [off[b P], off[(b + 1) P]) by A >> hb into dst
 __global__ __launch_bounds__(256) void k_msd_pass2(const unsigned long long* __restrict__ src, long long n,
-                                                   const int* __restrict__ off, int P, int H, int lo_bits,
+                                                   const int* __restrict__ off, int P, int H, int hb, int lo_bits,
                                                    unsigned long long* __restrict__ dst) {
   __shared__ int hist[kMsdMaxLo];
   __shared__ int wsum[4];
   const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1), w = tid >> 6;
   const int nb = 1 << lo_bits;
   const int b = blockIdx.x;
   const long long s = off[static_cast<long long>(b) * P];
@@ -691,7 +785,22 @@ __global__ __launch_bounds__(256) void k_msd_pass2(const unsigned long long* __r
   for (int i = tid; i < nb; i += 256) hist[i] = 0;
   __syncthreads();
   const unsigned mask = static_cast<unsigned>(nb - 1);
-  for (long long k = s + tid; k < e; k += 256) atomicAdd(&hist[static_cast<unsigned>(src[k] >> 39) & mask], 1);
+  auto key_of = [&](unsigned long long v) { return static_cast<int>(static_cast<unsigned>(v >> 39) & mask); };
+  // each wave takes spans of 4 x 64 consecutive entries, loads first (runs stay on adjacent lanes)
+  constexpr int kU2 = 4;
+  for (long long a = s + w * (kU2 * kWave); a < e; a += 4 * kU2 * kWave) {
+    int kv[kU2];
+#pragma unroll
+    for (int q = 0; q < kU2; ++q) {
+      const long long k = a + q * kWave + lane;
+      kv[q] = k < e ? key_of(src[k]) : 0;
+    }
+#pragma unroll
+    for (int q = 0; q < kU2; ++q) {
+      if (a + q * kWave >= e) break;
+      run_add<false>(hist, kv[q], a + q * kWave + lane < e, lane);
+    }
+  }
   __syncthreads();
   // exclusive scan of hist: each thread owns a contiguous run of per = nb / 256 bins (or one bin)
   const int per = nb >= 256 ? nb / 256 : 1;
@@ -700,10 +809,11 @@ __global__ __launch_bounds__(256) void k_msd_pass2(const unsigned long long* __r
   if (first < nb)
     for (int i = 0; i < per; ++i) loc += hist[first + i];
   const int inc = wave_incl_scan(loc);
-  if ((tid & 63) == 63) wsum[tid >> 6] = inc;
+  if (lane == 63) wsum[w] = inc;
   __syncthreads();
   int base = inc - loc;
-  for (int w = 0; w < (tid >> 6); ++w) base += wsum[w];
+  for (int x = 0; x < w; ++x) base += wsum[x];
+  __syncthreads();
   if (first < nb) {
     int run = static_cast<int>(s) + base;          // positions fit 31 bits (n < 2^31)
     for (int i = 0; i < per; ++i) {
@@ -713,9 +823,20 @@ __global__ __launch_bounds__(256) void k_msd_pass2(const unsigned long long* __r
     }
   }
   __syncthreads();
-  for (long long k = s + tid; k < e; k += 256) {
-    const unsigned long long v = src[k];
-    dst[atomicAdd(&hist[static_cast<unsigned>(v >> 39) & mask], 1)] = v;
+  for (long long a = s + w * (kU2 * kWave); a < e; a += 4 * kU2 * kWave) {
+    unsigned long long v[kU2];
+#pragma unroll
+    for (int q = 0; q < kU2; ++q) {
+      const long long k = a + q * kWave + lane;
+      v[q] = k < e ? src[k] : 0ull;
+    }
+#pragma unroll
+    for (int q = 0; q < kU2; ++q) {
+      if (a + q * kWave >= e) break;
+      const bool act = a + q * kWave + lane < e;
+      const int p = run_add<true>(hist, act ? key_of(v[q]) : 0, act, lane);
+      if (act) dst[p] = v[q];
+    }
   }
 }
 
@@ -809,31 +930,31 @@ static hipError_t group_by_a(const SweepArgs& a, int mode, const unsigned long l
                              unsigned long long* out, hipStream_t s) {
   const long long n = a.n_ent;
   const int nbits = bits_for(std::max(1, a.n_reads - 1));
-  int hb = 0;                                               // H = 2^hb buckets of ~4096 entries
+  // H = 2^hb buckets of ~4096 entries; P pass-1 workgroups with H P <= kGrpInts / 2 (pass 1 is
+  // latency bound, so it wants waves in flight more than wide per-block histograms)
+  int hb = 0;
   while (hb < 13 && (n >> (12 + hb)) > 0) ++hb;
   hb = std::max(hb, nbits - 12);                            // low digit <= 12 bits (LDS bins)
   hb = std::min(hb, nbits);
   const int H = 1 << hb, lo = nbits - hb;
-  const int shift = 39 + lo;
+  const int P = std::max(64, std::min(kMsdMaxBlocks, (kGrpInts / 2) / H));
   int* mat = a.grp;
   int* off = a.grp + kGrpInts / 2;
   const int nt = tiles_of(a);
   if (mode == 2) {
-    k_msd_pass1<true, false><<<kMsdBlocks, kMsdThreads, 0, s>>>(a.ent_ub, n, a.tile_ub, a.tile_cnt, nt, shift, H,
-                                                                mat, nullptr);
+    k_msd_pass1<true, false><<<P, kMsdThreads, 0, s>>>(a.ent_ub, n, a.tile_ub, a.tile_cnt, nt, lo, H, mat, nullptr);
   } else {
-    k_msd_pass1<false, false><<<kMsdBlocks, kMsdThreads, 0, s>>>(src, n, nullptr, nullptr, 0, shift, H, mat, nullptr);
+    k_msd_pass1<false, false><<<P, kMsdThreads, 0, s>>>(src, n, nullptr, nullptr, 0, lo, H, mat, nullptr);
   }
   size_t tb = a.temp_bytes;
-  hipError_t e = hipcub::DeviceScan::ExclusiveSum(a.temp, tb, mat, off, H * kMsdBlocks, s);
+  hipError_t e = hipcub::DeviceScan::ExclusiveSum(a.temp, tb, mat, off, H * P, s);
   if (e != hipSuccess) return e;
   if (mode == 2) {
-    k_msd_pass1<true, true><<<kMsdBlocks, kMsdThreads, 0, s>>>(a.ent_ub, n, a.tile_ub, a.tile_cnt, nt, shift, H,
-                                                               off, mid);
+    k_msd_pass1<true, true><<<P, kMsdThreads, 0, s>>>(a.ent_ub, n, a.tile_ub, a.tile_cnt, nt, lo, H, off, mid);
   } else {
-    k_msd_pass1<false, true><<<kMsdBlocks, kMsdThreads, 0, s>>>(src, n, nullptr, nullptr, 0, shift, H, off, mid);
+    k_msd_pass1<false, true><<<P, kMsdThreads, 0, s>>>(src, n, nullptr, nullptr, 0, lo, H, off, mid);
   }
-  k_msd_pass2<<<H, 256, 0, s>>>(mid, n, off, kMsdBlocks, H, lo, out);
+  k_msd_pass2<<<H, 256, 0, s>>>(mid, n, off, P, H, hb, lo, out);
   return hipGetLastError();
 }
 
