@@ -125,7 +125,7 @@ def main():
             dist.init_process_group(backend)
 
     from fslr_amd import _lib, synth
-    from fslr_amd.dist import DeviceShardMerge, shard_of
+    from fslr_amd.dist import SweepShard, chrom_counts_of, chrom_owner, shard_range
     from fslr_amd.prep import fold_overlap_threshold, pass_table
 
     t0 = time.perf_counter()
@@ -147,42 +147,44 @@ def main():
     ctx.reserve_edges(12 * csr.n_reads)
     pt = pass_table([1, 1, 0.66, 0.66, 0.66, 0.5])
     qcut, ncut = 1 - 0.04, 1 - 0.25
-    merge = DeviceShardMerge(ctx, csr.n_reads, world, rank, dev) if world > 1 else None
-    if world > 1:
-        ctx.set_shard(rank, world)      # query-side index data (positions, ranges) for this shard's reads
-
-    def step():
-        ctx.build_index()
-        if world > 1:
-            ctx.query_shard(qcut, ncut, pt, rank, world)      # balanced rank blocks (fslr_query_shard)
-        else:
-            ctx.query(qcut, ncut, pt, 10, engine=args.engine)
-        ctx.components()
-        # cluster.py:223-224: the edge cap (one counter read; a replay + new components only if it binds)
-        if world == 1 and ctx.apply_edge_cap(10)['applied']:
-            ctx.components()
-        if merge is not None:
-            merge()
-
     # the input's unit count: the walk engine dedupes partners (the reference's seen-set) and counts
-    # the pairs whose predicate is evaluated; the sweep evaluates the same pairs without counting them
-    counted = None
+    # the pairs whose predicate is evaluated; the sweep evaluates the same pairs without counting them.
+    # With N ranks each counts the pairs whose first read lies in its contiguous range (summed below).
+    a0, a1 = shard_range(csr.n_reads, rank, world)
+    ctx.build_index()
+    counted = ctx.run_query(qcut, ncut, pt, 10, a0, a1, engine='walk')
     if world == 1:
-        ctx.build_index()
-        counted = ctx.run_query(qcut, ncut, pt, 10, engine='walk')
         walk_edges = sorted(zip(*[x.tolist() for x in ctx.edges(counted['n_edges'])]))
         walk_fwd = ctx.fwd_degree()
-    # warmup (also sizes the edge buffer)
+    shard = None
+    if world > 1:
+        # chromosome-split sweep: this rank indexes and sweeps its chromosomes, routes
+        # the match entries to the first read's owner (RCCL all_to_all), evaluates, merges labels
+        shard = SweepShard(ctx, csr.n_reads, chrom_counts_of(csr), world, rank, dev)
+
+    def step(collect=False):
+        if shard is not None:
+            return shard.step(qcut, ncut, pt, 10, collect=collect)
+        ctx.build_index()
+        ctx.query(qcut, ncut, pt, 10, engine=args.engine)
+        ctx.components()
+        # cluster.py:223-224: the edge cap (one counter read; a replay + new components only if it binds)
+        if ctx.apply_edge_cap(10)['applied']:
+            ctx.components()
+        return None
+
+    # warmup (also sizes the edge buffer); the last one reads the sweep's counters (multi-GPU)
+    info = None
     for w in range(max(1, args.warmup)):
-        step()
-        if w == 0:
+        info = step(collect=(w == max(1, args.warmup) - 1))
+        if w == 0 and shard is None:
             st = ctx.stats(check=False)
             if st['n_edges'] > ctx.edge_capacity:
                 ctx.reserve_edges(st['n_edges'] + 4096)
     torch.cuda.synchronize()
     st = ctx.stats()
     engine = st['engine']
-    if counted is not None and engine != 'walk':
+    if world == 1 and engine != 'walk':
         ctx.query(qcut, ncut, pt, 10, engine=args.engine)
         se = ctx.stats()
         same = (sorted(zip(*[x.tolist() for x in ctx.edges(se['n_edges'])])) == walk_edges and
@@ -206,21 +208,28 @@ def main():
     kern = ctx.pair_kernel_times(args.steps)       # the timed steps' main pair-kernel launches
     kernel_ms = float(np.mean(kern)) if kern.size else float('nan')
 
-    own = shard_of(np.arange(csr.n_reads), world) == rank if world > 1 else np.ones(csr.n_reads, bool)
-    q_reads = int(own.sum())
-    q_ivls = int(np.diff(csr.read_off)[own].sum())
-    if st['engine'] == 'sweep':
-        algo_bytes = B_POS * csr.n_intervals + B_ENT * st['match_entries']
-        algo_model = (f'{B_POS} B x sorted positions ({csr.n_intervals}: record, gate word, forward count, read gate '
-                      f'ranges) + {B_ENT} B x match entries written ({st["match_entries"]})')
+    sw = info['sweep_stats'] if info is not None else st          # this rank's sweep counters
+    if world > 1:
+        own_chroms = chrom_owner(chrom_counts_of(csr), world) == rank
+        n_pos = int(chrom_counts_of(csr)[own_chroms].sum())          # positions of this rank's index
     else:
+        n_pos = csr.n_intervals
+    if st['engine'] == 'sweep':
+        algo_bytes = B_POS * n_pos + B_ENT * sw['match_entries']
+        algo_model = (f'{B_POS} B x sorted positions ({n_pos}: record, gate word, forward count, read gate '
+                      f'ranges) + {B_ENT} B x match entries written ({sw["match_entries"]})')
+    else:
+        own = np.ones(csr.n_reads, bool)
+        q_reads = int(own.sum())
+        q_ivls = int(np.diff(csr.read_off)[own].sum())
         algo_bytes = (B_WALK * st['walked_records'] + B_READ * q_reads + B_IVL * q_ivls + B_EDGE * st['n_edges'] +
                       B_DEFER * st['deferred'])
         algo_model = (f'{B_WALK} B x walked records ({st["walked_records"]}) + {B_READ} B x query reads + {B_IVL} B x '
                       'query intervals + {B_EDGE} B x edges + {B_DEFER} B x deferred entries')
-    cs = counted if counted is not None else st        # the walk engine's counts of this input
+    cs = counted                                      # the walk engine's counts of this rank's read range
     tot = torch.tensor([elapsed, float(cs['evaluated_pairs']), float(cs['jaccard_evals']), float(st['n_edges']),
                         float(st['max_fwd'])], dtype=torch.float64, device=dev if backend == 'nccl' else 'cpu')
+    capped = bool(info['capped']) if info is not None else False
     if dist:
         t_max = tot[:1].clone()
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
@@ -231,13 +240,10 @@ def main():
         elapsed = float(t_max.item())
         pairs, jacc, n_edges = (float(x) for x in sums.tolist())
         max_fwd = int(mf.item())
-        if max_fwd > 10:
-            raise SystemExit('the edge cap binds on this input: its replay runs on one context (fslr_query over '
-                             'all reads); the sharded bench does not cover it')
     else:
         pairs, jacc, n_edges = (float(x) for x in tot[1:4].tolist())
         max_fwd = int(st['max_fwd'])
-    lib_t = ctx.timings()                     # hipEvents of the last step (library side)
+    lib_t = ctx.timings() if world == 1 else None     # hipEvents of the last step (library side)
     ms_per_step = 1000.0 * elapsed / args.steps
     value = jacc / (elapsed / args.steps)
     achieved = algo_bytes / (kernel_ms / 1000.0)
@@ -253,7 +259,7 @@ def main():
 
     # transfers around the device path (not in `value`): CSR upload before, labels / edges after
     t = time.perf_counter()
-    labels = ctx.labels()
+    labels = shard.labels() if shard is not None else ctx.labels()
     d2h_labels_s = time.perf_counter() - t
     t = time.perf_counter()
     ctx.edges(st['n_edges'])
@@ -304,16 +310,21 @@ def main():
                 'candidate_pairs_per_s': pairs / (elapsed / args.steps),
                 'edges': int(n_edges), 'max_fwd_degree': max_fwd,
                 'engine': st['engine'],
-                'kernel_stats_rank0': {k: int(st[k]) for k in ('candidates', 'walked_records', 'overflow_candidates',
+                'kernel_stats_rank0': {k: int(sw[k]) for k in ('candidates', 'walked_records', 'overflow_candidates',
                                                                'gather_pairs', 'match_entries', 'matched_pairs',
                                                                'deferred', 'pair_tests')},
-                'interval_pair_tests_per_s': st['pair_tests'] / (elapsed / args.steps) if st['engine'] == 'sweep'
-                else None,
+                'interval_pair_tests_per_s_rank0': sw['pair_tests'] / (elapsed / args.steps)
+                if st['engine'] == 'sweep' else None,
                 'unit_count_source': 'walk engine run on the same input before timing (its seen-set counts the '
                                      'pairs whose predicate is evaluated; the sweep decides the same pairs, '
-                                     'DESIGN.md §4)' if world == 1 else 'walk engine, per shard',
+                                     'DESIGN.md §4)' + ('' if world == 1 else
+                                                        '; each rank counts the pairs whose first read lies in '
+                                                        'its contiguous read range, summed'),
+                'edge_cap_bound': capped,
                 'dense_equivalent_pairs_per_s': (n * (n - 1) / 2) / (elapsed / args.steps),
-                'parallelism': f'query-read shards x{world} (64-rank blocks round robin) + RCCL label all_gather'
+                'parallelism': f'chromosome-split sweep x{world}: each rank indexes and sweeps its chromosomes, '
+                               'RCCL all_to_all of match entries to the first read\'s owner (64-rank blocks '
+                               'round robin), evaluation there, RCCL label all_gather + union'
                 if world > 1 else 'single GPU',
                 'transfer': transfer,
             },

@@ -424,10 +424,16 @@ int fslr_query_shard(fslr_ctx* c, const fslr_params* p, int32_t shard, int32_t n
 // upper-bound slot (its pair tests, scanned); one sync reads the entry count, the upper-bound total
 // and an overflow flag from pinned host memory the kernels write; the tiles are packed, grouped by
 // A and evaluated.  A too-small upper-bound buffer is grown and the sweep rerun (first query on an
-// input); an upper bound beyond kUbBudget entries takes the two-pass fallback (count, then emit).
+// input); an upper bound beyond the budget (half the free HBM, at least 8 GB) takes the two-pass
+// fallback (count, then emit: the sweep runs twice).
 static int sweep_front(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_t a_end, hipEvent_t e0,
-                       hipEvent_t e1, SweepArgs& s, int& mode) {
-  constexpr int64_t kUbBudget = int64_t(1) << 30;     // 8 GB of upper-bound slots
+                       hipEvent_t e1, SweepArgs& s, int& mode, bool defer = false) {
+  int64_t ub_budget = int64_t(1) << 30;              // upper-bound slots (8 B each)
+  {
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess)
+      ub_budget = std::max<int64_t>(ub_budget, static_cast<int64_t>(fr / 2 / sizeof(unsigned long long)));
+  }
   const int64_t nix = c->ni_idx;                      // positions of the (possibly chromosome-filtered) index
   const int64_t tiles = (nix + 63) / 64 + 1;
   int rc;
@@ -493,12 +499,16 @@ static int sweep_front(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64
     s.k1 = e1;
     if (c->profiling) HIP_TRY(c, hipEventRecord(c->sw_ev[0], c->stream));
     HIP_TRY(c, launch_sweep_count(s, mode, c->sw_total_dev, c->stream));
+    if (defer) {                                     // the caller reads the counts and flags later
+      s.n_ent = -1;
+      return FSLR_OK;
+    }
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     const volatile long long* tot = c->sw_total;
     if (mode == 2 && (tot[2] & 8)) {
       // upper-bound buffer too small (or beyond the budget: two passes); clear the flag and counters
       const int64_t need = tot[1];
-      if (need > kUbBudget) {
+      if (need > ub_budget) {
         mode = 0;
       } else {
         if ((rc = dalloc(c, &c->ent_ub, need + (need >> 3) + 4096))) return rc;
@@ -690,22 +700,40 @@ int fslr_sweep_partition(fslr_ctx* c, const fslr_params* p, int32_t n_dest, int3
   if (int rc = prepare_query(c, p)) return rc;
   c->last_full = false;
   c->last_engine = FSLR_ENGINE_SWEEP;
-  SweepArgs s;
-  int mode = 2;
-  if (int rc = sweep_front(c, p, 0, c->n, nullptr, nullptr, s, mode)) return rc;
-  // dense entries in `ent` (pack, or the emit pass of the two-pass fallback), then by destination
-  HIP_TRY(c, launch_sweep_dense(s, mode, c->stream));
-  if (!c->part_cnt && dalloc(c, &c->part_cnt, 2 * kMaxDest * kPartBlocks + kMaxDest)) return FSLR_ERR_NOMEM;
-  if (partition_temp_bytes(c->stream) > c->sweep_temp_bytes) return fail(c, FSLR_ERR_STATE, "partition scratch");
-  long long* totals = c->part_cnt + 2 * kMaxDest * kPartBlocks;
-  HIP_TRY(c, launch_partition_by_dest(c->ent, s.n_ent, block_shift, n_dest, c->part_cnt, c->sweep_temp,
-                                      c->sweep_temp_bytes, static_cast<unsigned long long*>(dst), dst_cap, totals,
-                                      c->stream));
+  if (!c->part_cnt && dalloc(c, &c->part_cnt, kMaxDest)) return FSLR_ERR_NOMEM;
+  long long* totals = c->part_cnt;
+  auto* out = static_cast<unsigned long long*>(dst);
   long long tot[kMaxDest];
   int ew[kErrWords] = {};
-  HIP_TRY(c, hipMemcpyAsync(tot, totals, n_dest * sizeof(long long), hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(c, hipMemcpyAsync(ew, c->errw, sizeof(ew), hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  auto read_back = [&]() -> int {
+    HIP_TRY(c, hipMemcpyAsync(tot, totals, n_dest * sizeof(long long), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(ew, c->errw, sizeof(ew), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return FSLR_OK;
+  };
+  // one sync: the sweep writes its tile slots, the partition reads them straight into dst; the
+  // slot-overflow flag is checked at the end (first call on an input: grow, rerun synchronously)
+  hipEvent_t k0 = nullptr, k1 = nullptr;           // the pair-kernel ring: the sweep kernel
+  if (c->profiling && c->n > 0) {
+    const int slot = static_cast<int>(c->n_kern++ % fslr_ctx::kKernRing);
+    k0 = c->kev[2 * slot];
+    k1 = c->kev[2 * slot + 1];
+  }
+  SweepArgs s;
+  int mode = 2;
+  if (int rc = sweep_front(c, p, 0, c->n, k0, k1, s, mode, true)) return rc;
+  HIP_TRY(c, launch_sweep_partition(s, 2, block_shift, n_dest, out, dst_cap, totals, c->stream));
+  if (int rc = read_back()) return rc;
+  const volatile long long* st = c->sw_total;
+  if (st[2] & 8) {
+    if (int rc = prepare_query(c, p)) return rc;
+    mode = 2;
+    if (int rc = sweep_front(c, p, 0, c->n, k0, k1, s, mode)) return rc;
+    if (mode == 0) HIP_TRY(c, launch_sweep_dense(s, 0, c->stream));     // dense entries in `ent`
+    HIP_TRY(c, launch_sweep_partition(s, mode, block_shift, n_dest, out, dst_cap, totals, c->stream));
+    if (int rc = read_back()) return rc;
+  }
+  c->t_kernel_rec = k0 != nullptr;
   if (ew[0] == FSLR_ERR_ZERO_DIVISION) {
     c->err = "division by zero";
     return FSLR_ERR_ZERO_DIVISION;

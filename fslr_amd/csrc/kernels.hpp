@@ -196,20 +196,18 @@ hipError_t launch_sweep_pairs(const SweepArgs& a, int mode, hipStream_t s);
 // only the packing / emit step of launch_sweep_pairs: dense entries in a.ent
 hipError_t launch_sweep_dense(const SweepArgs& a, int mode, hipStream_t s);
 int grp_ints();
+// multi-GPU: the sweep's entries (mode 2: in the tile slots; 0: dense in a.ent) grouped by destination
+// (A >> shift) % n_dest into dst (entries beyond dst_cap dropped); totals[k] (device) per destination
+hipError_t launch_sweep_partition(const SweepArgs& a, int mode, int shift, int n_dest, unsigned long long* dst,
+                                  long long dst_cap, long long* totals, hipStream_t s);
 
 // ---- multi-GPU sweep (shard.hip) -------------------------------------------------------------
 constexpr int kMaxDest = 64;          // destination ranks of one partition
-constexpr int kPartBlocks = 1024;     // blocks of the partition kernels
 // the data-order records of the owned chromosomes, compacted in data order (stable)
 hipError_t launch_chrom_filter(const unsigned* dchrom, const int4* drec, const int2* dgate, unsigned long long owned,
                                int ni, unsigned* fdchrom, int4* fdrec, int2* fdgate, int* flags, int* offs,
                                void* temp, size_t temp_bytes, hipStream_t s);
-size_t partition_temp_bytes(hipStream_t s);
-// entries -> dst grouped by destination k = (A >> shift) % n_dest, in destination order;
-// totals[k] (device) = entries for k; scratch holds 2 * kMaxDest * kPartBlocks long longs
-hipError_t launch_partition_by_dest(const unsigned long long* ent, long long n, int shift, int n_dest,
-                                    long long* scratch, void* temp, size_t temp_bytes, unsigned long long* dst,
-                                    long long dst_cap, long long* totals, hipStream_t s);
+
 
 // ---- edge-cap replay (cap.hip) --------------------------------------------------------------
 // per listed read: upper bound of its interval hits (sum over its intervals of the scan range)

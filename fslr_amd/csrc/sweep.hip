@@ -659,14 +659,18 @@ __device__ __forceinline__ int run_add(int* bin, int key, bool act, int lane) {
   return __shfl(base, act ? my_head : 0) + (lane - my_head);
 }
 
-// kTiles: entries of tile t at src[ub[t] .. ub[t] + cnt[t]) (one wave per tile, the block's tiles a
-// contiguous range); else dense src[0, n) in contiguous block chunks.  kScatter = false: histogram.
-template <bool kTiles, bool kScatter>
+// kTiles: entries of tile t at src[ub[t] .. ub[t] + cnt[t]) (slots at or beyond n, the buffer's size,
+// are not read: an overflowed sweep's result is discarded by the caller); else dense src[0, n) in
+// contiguous block chunks.  kScatter = false: histogram.
+// kMod: bucket (A >> lo_bits) % H (the multi-GPU destination of fslr_sweep_partition) instead of
+// A >> lo_bits; scattered entries at positions >= cap are dropped (the caller sees the totals).
+template <bool kTiles, bool kScatter, bool kMod = false>
 __global__ __launch_bounds__(kMsdThreads) void k_msd_pass1(const unsigned long long* __restrict__ src, long long n,
                                                            const long long* __restrict__ ub,
                                                            const long long* __restrict__ cnt, int nt,
                                                            int lo_bits, int H, int* __restrict__ mat,
-                                                           unsigned long long* __restrict__ dst) {
+                                                           unsigned long long* __restrict__ dst,
+                                                           long long cap = 0x7FFFFFFFFFFFFFFFll) {
   __shared__ int hist[kMsdMaxH];
   const int tid = threadIdx.x;
   const int lane = tid & (kWave - 1), w = tid >> 6;
@@ -687,10 +691,11 @@ __global__ __launch_bounds__(kMsdThreads) void k_msd_pass1(const unsigned long l
         const long long k = k0 + u * kWave + lane;
         if (k0 + u * kWave >= c) break;                     // wave-uniform
         const bool act = k < c;
-        const int d = static_cast<int>(static_cast<unsigned>(v[u] >> 39) >> lo_bits);
+        const unsigned a_hi = static_cast<unsigned>(v[u] >> 39) >> lo_bits;
+        const int d = static_cast<int>(kMod ? a_hi % static_cast<unsigned>(H) : a_hi);
         if (kScatter) {
           const int p = run_add<true>(hist, d, act, lane);
-          if (act) dst[p] = v[u];
+          if (act && p < cap) dst[p] = v[u];
         } else {
           run_add<false>(hist, d, act, lane);
         }
@@ -737,16 +742,17 @@ __global__ __launch_bounds__(kMsdThreads) void k_msd_pass1(const unsigned long l
             j = lo;
           }
           const long long at = __shfl(u0, j) + (k - __shfl(exc, j));
-          v[q] = k < T ? src[at] : 0ull;
+          v[q] = k < T && at < n ? src[at] : 0ull;              // n: the slot buffer's size
         }
 #pragma unroll
         for (int q = 0; q < kMsdUnroll; ++q) {
           if (k0 + q * kWave >= T) break;                   // wave-uniform
           const bool act = k0 + q * kWave + lane < T;
-          const int d = static_cast<int>(static_cast<unsigned>(v[q] >> 39) >> lo_bits);
+          const unsigned a_hi = static_cast<unsigned>(v[q] >> 39) >> lo_bits;
+          const int d = static_cast<int>(kMod ? a_hi % static_cast<unsigned>(H) : a_hi);
           if (kScatter) {
             const int p = run_add<true>(hist, d, act, lane);
-            if (act) dst[p] = v[q];
+            if (act && p < cap) dst[p] = v[q];
           } else {
             run_add<false>(hist, d, act, lane);
           }
@@ -942,7 +948,7 @@ static hipError_t group_by_a(const SweepArgs& a, int mode, const unsigned long l
   int* off = a.grp + kGrpInts / 2;
   const int nt = tiles_of(a);
   if (mode == 2) {
-    k_msd_pass1<true, false><<<P, kMsdThreads, 0, s>>>(a.ent_ub, n, a.tile_ub, a.tile_cnt, nt, lo, H, mat, nullptr);
+    k_msd_pass1<true, false><<<P, kMsdThreads, 0, s>>>(a.ent_ub, a.ub_cap, a.tile_ub, a.tile_cnt, nt, lo, H, mat, nullptr);
   } else {
     k_msd_pass1<false, false><<<P, kMsdThreads, 0, s>>>(src, n, nullptr, nullptr, 0, lo, H, mat, nullptr);
   }
@@ -950,11 +956,47 @@ static hipError_t group_by_a(const SweepArgs& a, int mode, const unsigned long l
   hipError_t e = hipcub::DeviceScan::ExclusiveSum(a.temp, tb, mat, off, H * P, s);
   if (e != hipSuccess) return e;
   if (mode == 2) {
-    k_msd_pass1<true, true><<<P, kMsdThreads, 0, s>>>(a.ent_ub, n, a.tile_ub, a.tile_cnt, nt, lo, H, off, mid);
+    k_msd_pass1<true, true><<<P, kMsdThreads, 0, s>>>(a.ent_ub, a.ub_cap, a.tile_ub, a.tile_cnt, nt, lo, H, off, mid);
   } else {
     k_msd_pass1<false, true><<<P, kMsdThreads, 0, s>>>(src, n, nullptr, nullptr, 0, lo, H, off, mid);
   }
   k_msd_pass2<<<H, 256, 0, s>>>(mid, n, off, P, H, hb, lo, out);
+  return hipGetLastError();
+}
+
+// totals[k] = entries of destination k from the [k][block] counts and their scan
+__global__ void k_dest_totals(const int* __restrict__ mat, const int* __restrict__ off, int H, int P,
+                              long long* __restrict__ totals) {
+  const int k = threadIdx.x;
+  if (k >= H) return;
+  const long long last = static_cast<long long>(k) * P + P - 1;
+  totals[k] = static_cast<long long>(off[last]) + mat[last] - off[static_cast<long long>(k) * P];
+}
+
+hipError_t launch_sweep_partition(const SweepArgs& a, int mode, int shift, int n_dest, unsigned long long* dst,
+                                  long long dst_cap, long long* totals, hipStream_t s) {
+  if (n_dest < 1 || n_dest > kMsdMaxH) return hipErrorInvalidValue;
+  const int P = kMsdMaxBlocks;
+  int* mat = a.grp;
+  int* off = a.grp + kGrpInts / 2;
+  const int nt = tiles_of(a);
+  const long long n = a.n_ent;
+  if (mode == 2)
+    k_msd_pass1<true, false, true><<<P, kMsdThreads, 0, s>>>(a.ent_ub, a.ub_cap, a.tile_ub, a.tile_cnt, nt, shift, n_dest,
+                                                             mat, nullptr);
+  else
+    k_msd_pass1<false, false, true><<<P, kMsdThreads, 0, s>>>(a.ent, n, nullptr, nullptr, 0, shift, n_dest, mat,
+                                                              nullptr);
+  size_t tb = a.temp_bytes;
+  hipError_t e = hipcub::DeviceScan::ExclusiveSum(a.temp, tb, mat, off, n_dest * P, s);
+  if (e != hipSuccess) return e;
+  k_dest_totals<<<1, 64, 0, s>>>(mat, off, n_dest, P, totals);
+  if (mode == 2)
+    k_msd_pass1<true, true, true><<<P, kMsdThreads, 0, s>>>(a.ent_ub, a.ub_cap, a.tile_ub, a.tile_cnt, nt, shift, n_dest,
+                                                            off, dst, dst_cap);
+  else
+    k_msd_pass1<false, true, true><<<P, kMsdThreads, 0, s>>>(a.ent, n, nullptr, nullptr, 0, shift, n_dest, off, dst,
+                                                             dst_cap);
   return hipGetLastError();
 }
 

@@ -186,7 +186,9 @@ class SweepShard:
         return torch.empty(int(need * 1.125) + 4096, dtype=torch.int64, device=self.device)
 
     # -- one step -----------------------------------------------------------------------------
-    def step(self, qlen_cut, nal_cut, pass_table, edge_threshold=10) -> dict:
+    def step(self, qlen_cut, nal_cut, pass_table, edge_threshold=10, collect=False) -> dict:
+        """One step.  ``collect``: also read the sweep's counters after the partition (one more
+        sync; bench.py does it outside the timed steps)."""
         import torch
         import torch.distributed as dist
         ctx, W = self.ctx, self.world
@@ -199,6 +201,7 @@ class SweepShard:
             ok, counts = ctx.sweep_partition(qlen_cut, nal_cut, pass_table, W, self.block_shift, self.send,
                                              edge_threshold)
             assert ok
+        sweep_stats = ctx.stats(check=False) if collect else None
         sent_total = int(counts.sum())
         if W > 1:
             cdev = 'cpu' if self._gloo() else self.device
@@ -226,7 +229,7 @@ class SweepShard:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             mf = int(t.item())
         out = {'entries_sent': sent_total, 'entries_received': n_recv, 'n_edges_local': int(st['n_edges']),
-               'max_fwd': mf, 'capped': False}
+               'max_fwd': mf, 'capped': False, 'sweep_stats': sweep_stats}
         if mf > edge_threshold:
             out['capped'] = True
             out['cap'] = self._capped_labels(qlen_cut, nal_cut, pass_table, edge_threshold)
