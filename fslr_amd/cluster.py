@@ -29,7 +29,7 @@ import warnings
 import numpy as np
 import pandas as pd
 
-from . import bam_header
+from . import bam_header, multi
 from ._lib import FSLR_THR_ZERO_ALN, Context
 from .prep import (IntervalData, IntervalItem, build_csr, data_order, first_last_masks, fold_overlap_threshold,
                    group_span, mask_keep, pass_table)
@@ -37,7 +37,7 @@ from .prep import (IntervalData, IntervalItem, build_csr, data_order, first_last
 __all__ = ['IntervalItem', 'keep_fillings', 'rename_chromosomes', 'chrom_to_str', 'calc_coverage',
            'filter_high_coverage', 'delete_false', 'mask_sequences2', 'prepare_data', 'build_interval_trees',
            'get_chromosome_lengths', 'query_interval_trees', 'get_subgraphs', 'choose_alignment',
-           'ClusterGraph', 'DeviceIntervalIndex', 'EdgeCapWarning']
+           'ClusterGraph', 'DeviceIntervalIndex', 'MultiGpuIndex', 'EdgeCapWarning']
 
 
 class EdgeCapWarning(UserWarning):
@@ -192,10 +192,29 @@ class DeviceIntervalIndex:
         self.ctx.build_index()
 
 
-def build_interval_trees(data, device: int | None = None) -> DeviceIntervalIndex:
+class MultiGpuIndex:
+    """What build_interval_trees returns for ``n_gpus > 1``: the prepared CSR on the host.  The ranks
+    (one process per GPU, fslr_amd.multi) upload it and build their chromosomes' index inside
+    query_interval_trees; this process must not have initialised the GPU before then."""
+
+    def __init__(self, data, n_gpus: int, device: int | None = None):
+        self.source = data
+        if not isinstance(data, IntervalData):
+            data = IntervalData.from_items(data)
+        self.data = data
+        self.csr = data.csr()
+        self.n_gpus = int(n_gpus)
+        self.first_device = 0 if device is None else int(device)
+
+
+def build_interval_trees(data, device: int | None = None, n_gpus: int = 1):
     """cluster.py:124-130: upload the prepared intervals and build the (chrom, start) index on the GPU.
 
-    ``data`` is this module's ``prepare_data`` result or the reference's (a list of IntervalItem)."""
+    ``data`` is this module's ``prepare_data`` result or the reference's (a list of IntervalItem).
+    ``n_gpus > 1``: the chromosome-split multi-GPU query; the upload happens in the
+    per-GPU processes that query_interval_trees starts."""
+    if int(n_gpus) > 1:
+        return MultiGpuIndex(data, n_gpus, device)
     return DeviceIntervalIndex(data, device)
 
 
@@ -270,6 +289,13 @@ def query_interval_trees(interval_trees, data, overlap_cutoff, jaccard_threshold
     set order (arbitrary).
     """
     min(jaccard_threshold)                              # cluster.py:188 raises on an empty list
+    if isinstance(interval_trees, MultiGpuIndex) and (interval_trees.source is data or interval_trees.data is data):
+        mg = interval_trees
+        thr = fold_overlap_threshold(mg.csr.iv_aln, overlap_cutoff)
+        if multi.sweep_applies(mg.csr, thr):
+            return _query_multi_gpu(mg, thr, jaccard_threshold, edge_threshold, qlen_diff, diff)
+        # overlap <= 0 or an aln_size == 0 interval: the walk engine on one GPU (DESIGN.md §6)
+        interval_trees = DeviceIntervalIndex(mg.data, mg.first_device)
     if not isinstance(interval_trees, DeviceIntervalIndex) or (interval_trees.source is not data and
                                                                interval_trees.data is not data):
         interval_trees = DeviceIntervalIndex(data)
@@ -295,13 +321,33 @@ def query_interval_trees(interval_trees, data, overlap_cutoff, jaccard_threshold
     ne = st['n_edges']
     a, b, I, U = ctx.edges(ne)
     fwd = ctx.fwd_degree()
+    return _graph_outputs(qnames_by_rank, labels, a, b, I, U, fwd, st)
+
+
+def _graph_outputs(qnames_by_rank, labels, a, b, I, U, fwd, st):
     order = np.lexsort((b, a))
     a, b, I, U = a[order], b[order], I[order], U[order]
+    ne = int(a.shape[0])
     match_df = pd.DataFrame({'query1': qnames_by_rank[a] if ne else np.zeros(0, object),
                              'query2': qnames_by_rank[b] if ne else np.zeros(0, object),
                              'jaccard_similarity': I / U if ne else np.zeros(0)})
-    G = ClusterGraph(qnames_by_rank, labels, (a, b), fwd, st)
-    return match_df, G
+    return match_df, ClusterGraph(qnames_by_rank, labels, (a, b), fwd, st)
+
+
+def _query_multi_gpu(mg, thr, jaccard_threshold, edge_threshold, qlen_diff, diff):
+    """query_interval_trees over ``mg.n_gpus`` ranks (fslr_amd.multi): same edges, forward degrees and
+    labels as one GPU (union of per-chromosome matchings, label union; the cap replayed on rank 0)."""
+    data, csr = mg.data, mg.csr
+    qnames_by_rank = data.qnames[csr.read_qcode]
+    if csr.nal_varies:
+        warnings.warn('n_alignments differs between rows of one read; the reference then uses the row its '
+                      'search reaches first (order-dependent); the first row in data order is used', EdgeCapWarning)
+    r = multi.query(csr, thr, 1 - qlen_diff, 1 - diff, pass_table(jaccard_threshold), int(edge_threshold),
+                    mg.n_gpus, first_device=mg.first_device)
+    a, b, I, U = r['edges']
+    st = {'engine': 'sweep', 'n_gpus': mg.n_gpus, 'backend': r['backend'], 'evaluated_pairs': -1,
+          'n_edges': int(a.shape[0]), 'max_fwd': r['max_fwd'], 'cap': r['cap'], 'capped': r['capped']}
+    return _graph_outputs(qnames_by_rank, np.asarray(r['labels']), a, b, I, U, r['fwd'], st)
 
 
 def get_subgraphs(G):

@@ -479,6 +479,9 @@ hipError_t index_temp_bytes(int ni, size_t* bytes, hipStream_t s) {
                                          static_cast<unsigned*>(nullptr), static_cast<int4*>(nullptr),
                                          static_cast<int4*>(nullptr), ni, 0, 32, s);
   if (e != hipSuccess) return e;
+  // the chromosome filter's scan of the owned flags (launch_chrom_filter) shares this buffer
+  e = hipcub::DeviceScan::ExclusiveSum(nullptr, b2, static_cast<int*>(nullptr), static_cast<int*>(nullptr), ni, s);
+  if (e != hipSuccess) return e;
   *bytes = b1 > b2 ? b1 : b2;
   if (b3 > *bytes) *bytes = b3;
   return hipSuccess;

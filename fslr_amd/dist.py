@@ -193,15 +193,23 @@ class SweepShard:
         import torch.distributed as dist
         ctx, W = self.ctx, self.world
         self._labels = None
-        ctx.build_index()
-        ok, counts = ctx.sweep_partition(qlen_cut, nal_cut, pass_table, W, self.block_shift, self.send,
-                                         edge_threshold)
-        if not ok:
-            self.send = self._grow(self.send, int(counts.sum()))
+        err = None
+        try:
+            ctx.build_index()
             ok, counts = ctx.sweep_partition(qlen_cut, nal_cut, pass_table, W, self.block_shift, self.send,
                                              edge_threshold)
-            assert ok
-        sweep_stats = ctx.stats(check=False) if collect else None
+            if not ok:
+                self.send = self._grow(self.send, int(counts.sum()))
+                ok, counts = ctx.sweep_partition(qlen_cut, nal_cut, pass_table, W, self.block_shift, self.send,
+                                                 edge_threshold)
+                assert ok
+        except Exception as e:                          # noqa: BLE001 - re-raised on every rank below
+            if W == 1:
+                raise
+            # a negative count tells every destination (the counts exchange is the next collective)
+            err = e
+            counts = np.full(W, -1 if isinstance(e, ZeroDivisionError) else -2, dtype=np.int64)
+        sweep_stats = ctx.stats(check=False) if collect and err is None else None
         sent_total = int(counts.sum())
         if W > 1:
             cdev = 'cpu' if self._gloo() else self.device
@@ -209,6 +217,12 @@ class SweepShard:
             cout = torch.empty_like(cin)
             dist.all_to_all_single(cout, cin)
             recv_counts = cout.cpu().numpy()
+            if err is not None or (recv_counts < 0).any():
+                if err is None:
+                    from ._lib import FslrError
+                    err = (ZeroDivisionError('division by zero') if (recv_counts == -1).any()
+                           else FslrError('error on another rank'))
+                raise err
             n_recv = int(recv_counts.sum())
             self.recv = self._grow(self.recv, n_recv)
             self._all_to_all(self.recv[:n_recv], self.send[:sent_total], recv_counts.tolist(), counts.tolist())
@@ -222,12 +236,24 @@ class SweepShard:
             ctx.reserve_edges(int(st['n_edges'] * 1.25) + 4096)
             ctx.sweep_evaluate(qlen_cut, nal_cut, pass_table, entries, n_recv, edge_threshold)
             st = ctx.stats(check=False)
-        ctx.stats()                                     # raises on a device-side error
+        err = None
+        try:
+            ctx.stats()                                 # raises on a device-side error (ZeroDivisionError)
+        except Exception as e:                          # noqa: BLE001 - re-raised on every rank below
+            err = e
         mf = int(st['max_fwd'])
         if W > 1:
-            t = torch.tensor([mf], dtype=torch.int64, device='cpu' if self._gloo() else self.device)
+            # the error flag rides with the forward-degree maximum, so a pair that raises on one
+            # evaluator raises on every rank instead of leaving the others in a collective
+            code = 0 if err is None else (1 if isinstance(err, ZeroDivisionError) else 2)
+            t = torch.tensor([mf, code], dtype=torch.int64, device='cpu' if self._gloo() else self.device)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            mf = int(t.item())
+            mf, code = int(t[0].item()), int(t[1].item())
+            if err is None and code:
+                from ._lib import FslrError
+                err = ZeroDivisionError('division by zero') if code == 1 else FslrError('error on another rank')
+        if err is not None:
+            raise err
         out = {'entries_sent': sent_total, 'entries_received': n_recv, 'n_edges_local': int(st['n_edges']),
                'max_fwd': mf, 'capped': False, 'sweep_stats': sweep_stats}
         if mf > edge_threshold:

@@ -86,6 +86,9 @@ def assign_clusters(bed_file: pd.DataFrame, G: cluster.ClusterGraph):
 @click.option('--filter-high-coverage', required=False, is_flag=True, help='Filter regions with high coverage')
 @click.option('--filter-false', required=False, is_flag=True, help='Use reads with both primers labeled')
 @click.option('--device', required=False, default=None, type=int, help='HIP device ordinal for the clustering kernels (default: $LOCAL_RANK or 0)')
+@click.option('--gpus', required=False, default=1, show_default=True, type=click.IntRange(1, 64),
+              help='GPUs for the clustering query: one process per GPU, chromosome-split sweep with RCCL '
+                   'exchange (ranks share devices over gloo when fewer are visible)')
 @click.option('--timings', required=False, is_flag=True, help='Print per-stage wall times to stderr')
 @click.option('--native-io/--pandas-io', default=True, show_default=True,
               help='Read .mappings.bed and write the outputs with the native threaded reader/writer '
@@ -171,7 +174,7 @@ def _cluster_and_write(args, basename, bed_file, tsv, t):
     data = cluster.prepare_data(fillings, chromosome_mask, chr_lengths, threshold=500_000)
     t['prepare'] = time.perf_counter() - t1
     t2 = time.perf_counter()
-    interval_tree = cluster.build_interval_trees(data, device=args.get('device'))
+    interval_tree = cluster.build_interval_trees(data, device=args.get('device'), n_gpus=args.get('gpus') or 1)
     match_data, network = cluster.query_interval_trees(interval_tree, data, overlap, jaccard_cutoffs,
                                                        edge_threshold, qlen_diff, n_alignments_diff)
     t['device'] = time.perf_counter() - t2

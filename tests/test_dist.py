@@ -402,3 +402,68 @@ def test_sweep_shard_gloo_two_processes_one_gpu(tmp_path):
     for r in range(2):
         np.testing.assert_array_equal(_components_from_labels(np.load(tmp_path / f'labels{r}.npy')), o['comp'])
         assert not np.load(tmp_path / f'info{r}.npy')[0]
+
+
+def test_multi_csr_handoff_roundtrip(tmp_path, world_case):
+    """fslr_amd.multi hands the prepared CSR to the rank processes as .npy files: every field the
+    ranks upload comes back unchanged, with the query parameters."""
+    from fslr_amd import multi
+    from fslr_amd.prep import fold_overlap_threshold, pass_table
+    csr, _ = world_case
+    thr = fold_overlap_threshold(csr.iv_aln, 0.8)
+    pt = pass_table([1, 1, 0.66])
+    multi._save(str(tmp_path), csr, thr, dict(qlen_cut=0.96, nal_cut=0.75, pass_table=pt, edge_threshold=10))
+    c2, thr2, pt2, meta = multi._load(str(tmp_path))
+    for f in multi._CSR_FIELDS:
+        np.testing.assert_array_equal(np.asarray(getattr(c2, f)), np.asarray(getattr(csr, f)))
+    np.testing.assert_array_equal(thr2, thr)
+    np.testing.assert_array_equal(pt2, pt)
+    assert c2.n_chroms == csr.n_chroms and meta['edge_threshold'] == 10 and meta['qlen_cut'] == 0.96
+    assert multi.sweep_applies(csr, thr)
+    assert not multi.sweep_applies(csr, fold_overlap_threshold(csr.iv_aln, 0.0))
+
+
+def test_cli_exposes_gpus_option():
+    from click.testing import CliRunner
+    from fslr_amd.main import pipeline
+    out = CliRunner().invoke(pipeline, ['--help']).output
+    assert '--gpus' in out
+
+
+def _sweep_zerodiv_worker(rank, world, port, csr, thr, out_dir):
+    import torch.distributed as dist
+    from fslr_amd.dist import SweepShard, chrom_counts_of
+    from fslr_amd.prep import pass_table
+    from tests.sweep_emu import EmuSweepContext
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    ctx = EmuSweepContext(csr, thr)
+    sh = SweepShard(ctx, csr.n_reads, chrom_counts_of(csr), world, rank, 'cpu')
+    raised = ''
+    try:
+        sh.step(1 - 0.04, 1 - 0.25, pass_table([1, 1, 0.66, 0.66, 0.66, 0.5]), 10)
+    except ZeroDivisionError as e:
+        raised = f'ZeroDivisionError: {e}'
+    with open(os.path.join(out_dir, f'raised{rank}.txt'), 'w') as fh:
+        fh.write(raised)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_zero_division_raises_on_every_rank(world_case, tmp_path):
+    """The reference raises ZeroDivisionError when both reads of a candidate pair have qlen2 0
+    (cluster.py:178-183).  Only the rank that sweeps that pair's chromosome sees it; the negative
+    count it sends in the counts exchange makes every rank raise instead of waiting in a collective."""
+    import dataclasses
+    import torch.multiprocessing as mp
+    from fslr_amd.prep import fold_overlap_threshold
+    csr, o = world_case
+    a, b = int(o['edge_a'][0]), int(o['edge_b'][0])
+    q = np.array(csr.read_qlen2, copy=True)
+    q[[a, b]] = 0
+    bad = dataclasses.replace(csr, read_qlen2=q)
+    thr = fold_overlap_threshold(bad.iv_aln, 0.8)
+    mp.start_processes(_sweep_zerodiv_worker, args=(2, _free_port(), bad, thr, str(tmp_path)), nprocs=2,
+                       join=True, start_method='spawn')
+    for r in range(2):
+        assert (tmp_path / f'raised{r}.txt').read_text().startswith('ZeroDivisionError')

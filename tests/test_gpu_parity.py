@@ -141,6 +141,30 @@ def test_cli_matches_reference_outputs(name, io_flag):
         assert ('fslr finished' in res.output) == ('fslr finished' in meta['stdout'])
 
 
+@pytest.mark.parametrize('name', ['cfg1_1k_x3', 'capbind_1500', 'zerodiv', 'noclusters', 'params_a',
+                                  'edge_cases_p0', 'zipf_800_l64'])
+def test_cli_multi_gpu_matches_reference_outputs(name):
+    """``fslr --gpus 2``: two rank processes (sharing this box's one GPU over gloo) run the
+    chromosome-split sweep (fslr_amd.multi); outputs byte-identical to the reference's.  Covers the
+    cap replay on rank 0 (capbind_1500), a ZeroDivisionError raised on every rank (zerodiv), the
+    empty graph and the one-GPU fallback for overlap <= 0 (edge_cases_p0)."""
+    meta = fx.meta(name)
+    with tempfile.TemporaryDirectory() as tmp:
+        res = run_product_cli(name, tmp, '--gpus=2')
+        if meta['exception']:
+            assert isinstance(res.exception, ZeroDivisionError), (res.output, res.exception)
+            return
+        assert res.exit_code == 0, (res.output, res.exception)
+        for which in ('cluster', 'representative'):
+            want = fx.expected_text(name, which)
+            path = os.path.join(tmp, f'fx.mappings.{which}.bed')
+            if want is None:
+                assert not os.path.exists(path)
+                assert 'No clusters were found.' in res.output
+            else:
+                assert open(path).read() == want, f'{name}: {which} output differs'
+
+
 @pytest.mark.parametrize('name', [f for f in fx.FIXTURES if fx.stage(f) is not None])
 def test_query_interval_trees_edges_match_reference(name):
     data, _, kw = host_prepare(name)
