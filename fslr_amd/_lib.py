@@ -13,7 +13,7 @@ import numpy as np
 
 LIB_PATH = os.environ.get('FSLR_LIB') or os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libfslr_hip.so')
 
-ABI_VERSION = 4          # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
+ABI_VERSION = 5          # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
 FSLR_OK, FSLR_ERR_ZERO_DIVISION, FSLR_ERR_INVALID, FSLR_ERR_HIP, FSLR_ERR_NOMEM, FSLR_ERR_STATE = range(6)
 FSLR_MAX_L = 64
 FSLR_MAX_READS = 1 << 25
@@ -31,7 +31,8 @@ EXPORTED = ['fslr_abi_version', 'fslr_last_error', 'fslr_ctx_create', 'fslr_ctx_
             'fslr_get_labels',
             'fslr_get_fwd_degree', 'fslr_get_edges', 'fslr_labels_device_ptr', 'fslr_copy_labels_device',
             'fslr_copy_fwd_device', 'fslr_union_pairs', 'fslr_finalize_labels', 'fslr_apply_edge_cap',
-            'fslr_get_pair_kernel_times', 'fslr_set_chrom_filter', 'fslr_sweep_partition', 'fslr_sweep_evaluate']
+            'fslr_get_pair_kernel_times', 'fslr_set_chrom_filter', 'fslr_sweep_partition', 'fslr_sweep_evaluate',
+            'fslr_copy_edges_device', 'fslr_components_from_pairs']
 
 
 class HipUnavailable(RuntimeError):
@@ -134,6 +135,8 @@ def load(path: str = LIB_PATH):
         'fslr_sweep_partition': (ctypes.c_int, [vp, ctypes.POINTER(Params), i32, i32, vp, i64,
                                                 ctypes.POINTER(ctypes.c_int64)]),
         'fslr_sweep_evaluate': (ctypes.c_int, [vp, ctypes.POINTER(Params), vp, i64]),
+        'fslr_copy_edges_device': (ctypes.c_int, [vp, vp, i64]),
+        'fslr_components_from_pairs': (ctypes.c_int, [vp, vp, i64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -275,6 +278,17 @@ class Context:
     def labels_into(self, t):
         """Copy the [n_reads] labels into the int32 device tensor ``t`` (async, context stream)."""
         self._check(self._L.fslr_copy_labels_device(self._h, ctypes.c_void_p(t.data_ptr())))
+
+    def edges_into(self, t, n_pad: int):
+        """Copy this context's edges as (a, b) int32 pairs into the device tensor ``t`` (at least
+        2 * n_pad int32), padded with (-1, -1) to n_pad pairs (async, context stream)."""
+        assert t.numel() * t.element_size() >= 8 * n_pad
+        self._check(self._L.fslr_copy_edges_device(self._h, ctypes.c_void_p(t.data_ptr()), int(n_pad)))
+
+    def components_from_pairs(self, t, n_pairs: int):
+        """Labels = components of the n_pairs (a, b) int32 pairs in the device tensor ``t``
+        (a < 0 = padding): the union of the ranks' gathered edge lists (async)."""
+        self._check(self._L.fslr_components_from_pairs(self._h, ctypes.c_void_p(t.data_ptr()), int(n_pairs)))
 
     def union_label_vectors(self, t):
         """Union (k mod n_reads, t[k]) for the int32 device tensor ``t`` of W label vectors, then

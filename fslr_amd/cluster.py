@@ -29,7 +29,7 @@ import warnings
 import numpy as np
 import pandas as pd
 
-from . import bam_header, multi
+from . import bam_header, ingest, multi
 from ._lib import FSLR_THR_ZERO_ALN, Context
 from .prep import (IntervalData, IntervalItem, build_csr, data_order, first_last_masks, fold_overlap_threshold,
                    group_span, mask_keep, pass_table)
@@ -53,7 +53,7 @@ def _default_device() -> int:
 # ------------------------------------------------------------------ host stages
 def keep_fillings(bed_file: pd.DataFrame) -> pd.DataFrame:
     """cluster.py:14-31: drop the first and last row (file order) of every qname; add qlen2."""
-    codes, uniq = pd.factorize(bed_file['qname'], sort=False)
+    codes, uniq = ingest.factorize_qname(bed_file)
     first, last = first_last_masks(codes)
     keep = ~(first | last)
     out = bed_file[keep]
@@ -154,7 +154,7 @@ def prepare_data(bed_df, cluster_mask, chromosome_lengths, threshold=500_000) ->
         bed_df['end'] = end
         bed_df['middle'] = aln // 2 + start
     order = data_order(start)
-    codes, uniq = pd.factorize(bed_df['qname'], sort=False)
+    codes, uniq = ingest.factorize_qname(bed_df)
     chrom = bed_df['chrom'].to_numpy()
     if chrom.dtype.kind not in 'iu':                    # not renamed (rename_chromosomes not called)
         chrom = pd.factorize(bed_df['chrom'], sort=False)[0]
@@ -360,8 +360,56 @@ def get_subgraphs(G):
 
 def choose_alignment(bed_file):
     """cluster.py:237-254: per cluster the read with the highest mean alignment_score (first on ties)."""
+    fast = _choose_alignment_codes(bed_file)
+    if fast is not None:
+        return fast
     avg = bed_file.groupby('qname')['alignment_score'].mean()
     bed_file['avg_alignment_score'] = bed_file['qname'].map(avg)
     sel = bed_file.groupby('cluster')['avg_alignment_score'].idxmax()
     chosen = bed_file.loc[sel.to_numpy(), 'qname']
     return bed_file[bed_file['qname'].isin(chosen)]
+
+
+def _choose_alignment_codes(bed_file):
+    """choose_alignment from the reader's qname codes (ingest.QnameCodes), for an int64
+    alignment_score and numeric cluster ids, or None.
+
+    groupby('qname').mean() of int64 scores: the float64 sum of integers below 2**53 is exact in any
+    order (pandas' compensated sum included), divided by the count, so bincount gives the same
+    doubles.  groupby('cluster').idxmax() = the first row (in frame order) holding its cluster's
+    maximum; scores and clusters are constant per qname, so it is the earliest first row among
+    the cluster's qnames with the maximal mean."""
+    if not isinstance(bed_file.attrs.get(ingest.ATTR), ingest.QnameCodes) or 'cluster' not in bed_file:
+        return None
+    score = bed_file['alignment_score'].to_numpy()
+    cl = bed_file['cluster'].to_numpy()
+    if score.dtype != np.int64 or cl.dtype.kind not in 'iuf' or not len(cl):
+        return None
+    if np.abs(score).max() >= (1 << 53) // max(1, len(score)):
+        return None
+    codes, uniq = ingest.factorize_qname(bed_file)
+    nq = len(uniq)
+    sums = np.bincount(codes, weights=score.astype(np.float64), minlength=nq)
+    cnt = np.bincount(codes, minlength=nq)
+    avg_q = sums / cnt
+    with warnings.catch_warnings():
+        warnings.simplefilter('ignore')
+        bed_file['avg_alignment_score'] = avg_q[codes]
+    first_row = np.full(nq, -1, dtype=np.int64)
+    first_row[codes[::-1]] = np.arange(len(codes) - 1, -1, -1)
+    cl_q = cl[first_row]
+    if cl.dtype.kind == 'f':
+        if np.isnan(cl_q).any() or (cl_q != np.floor(cl_q)).any() or cl_q.min() < 0:
+            return None
+    if (cl != cl_q[codes]).any():                      # cluster not constant per qname
+        return None
+    cid = cl_q.astype(np.int64)
+    k = int(cid.max()) + 1
+    best = np.full(k, -np.inf)
+    np.maximum.at(best, cid, avg_q)
+    cand = np.flatnonzero(avg_q == best[cid])
+    win_row = np.full(k, len(codes), dtype=np.int64)
+    np.minimum.at(win_row, cid[cand], first_row[cand])
+    chosen = np.zeros(nq, dtype=bool)
+    chosen[codes[win_row[win_row < len(codes)]]] = True
+    return bed_file[chosen[codes]]

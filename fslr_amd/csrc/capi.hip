@@ -1003,6 +1003,28 @@ int fslr_union_pairs(fslr_ctx* c, const int32_t* src, const int32_t* dst, int64_
   return FSLR_OK;
 }
 
+int fslr_copy_edges_device(fslr_ctx* c, int32_t* dst, int64_t n_pad) {
+  if (!c || (!dst && n_pad) || n_pad < 0) return FSLR_ERR_INVALID;
+  if (!c->reads_set) return fail(c, FSLR_ERR_STATE, "fslr_set_reads first");
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (n_pad == 0) return FSLR_OK;
+  if (!c->edge_cap) return fail(c, FSLR_ERR_STATE, "no query has run");
+  HIP_TRY(c, launch_copy_edges(c->edges, &c->counters[kEdgeCount], c->edge_cap, reinterpret_cast<int2*>(dst), n_pad,
+                               c->stream));
+  return FSLR_OK;
+}
+
+int fslr_components_from_pairs(fslr_ctx* c, const int32_t* pairs, int64_t n) {
+  if (!c || (!pairs && n) || n < 0) return FSLR_ERR_INVALID;
+  if (!c->reads_set) return fail(c, FSLR_ERR_STATE, "fslr_set_reads first");
+  HIP_TRY(c, hipSetDevice(c->device));
+  const int nr = static_cast<int>(c->n);
+  HIP_TRY(c, launch_uf_init(c->parent, nr, c->stream));
+  HIP_TRY(c, launch_uf_pair_list(c->parent, reinterpret_cast<const int2*>(pairs), n, c->stream));
+  HIP_TRY(c, launch_uf_finalize(c->parent, nr, c->stream));
+  return FSLR_OK;
+}
+
 int fslr_finalize_labels(fslr_ctx* c) {
   if (!c) return FSLR_ERR_INVALID;
   HIP_TRY(c, hipSetDevice(c->device));

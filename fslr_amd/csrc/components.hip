@@ -70,6 +70,24 @@ __global__ void k_uf_pairs(int* p, const int* __restrict__ src, const int* __res
   }
 }
 
+// a gathered edge list (the multi-GPU merge): (a, b) pairs, a < 0 = padding
+__global__ void k_uf_pair_list(int* p, const int2* __restrict__ pairs, long long n) {
+  for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < n;
+       k += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const int2 e = pairs[k];
+    if (e.x >= 0) uf_union(p, e.x, e.y);
+  }
+}
+
+// this context's edges as (a, b) pairs, padded with (-1, -1) to n_pad (count read on the device)
+__global__ void k_copy_edges(const int2* __restrict__ edges, const unsigned long long* __restrict__ count,
+                             long long cap, int2* __restrict__ out, long long n_pad) {
+  const long long ne = min(min(static_cast<long long>(*count), cap), n_pad);
+  for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < n_pad;
+       k += static_cast<long long>(gridDim.x) * blockDim.x)
+    out[k] = k < ne ? edges[k] : make_int2(-1, -1);
+}
+
 // find without path halving: the finalize pass's only store is each node's own root.  (With
 // halving here, another thread's late halving store into p[x] — an ancestor that is not the root —
 // could land after x's own root store and leave x labelled with a non-root.)
@@ -101,6 +119,17 @@ hipError_t launch_uf_edges(int* parent, const int2* edges, const unsigned long l
 
 hipError_t launch_uf_pairs(int* parent, const int* src, const int* dst, long long n, int period, hipStream_t s) {
   if (n > 0 && period > 0) k_uf_pairs<<<grid_for(n), 256, 0, s>>>(parent, src, dst, n, period);
+  return hipGetLastError();
+}
+
+hipError_t launch_uf_pair_list(int* parent, const int2* pairs, long long n, hipStream_t s) {
+  if (n > 0) k_uf_pair_list<<<grid_for(n), 256, 0, s>>>(parent, pairs, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_copy_edges(const int2* edges, const unsigned long long* count, long long cap, int2* out,
+                             long long n_pad, hipStream_t s) {
+  if (n_pad > 0) k_copy_edges<<<grid_for(n_pad), 256, 0, s>>>(edges, count, cap, out, n_pad);
   return hipGetLastError();
 }
 

@@ -8,6 +8,8 @@
 #include "fslr_ingest.h"
 
 #include <algorithm>
+#include <charconv>
+#include <cmath>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -463,6 +465,96 @@ int fslr_tsv_write(const FslrTsv *t, const char *path, const char *header_suffix
         return FSLR_INGEST_ERROR;
     }
     return FSLR_INGEST_OK;
+}
+
+}  // extern "C"
+
+// ---- suffix text: the numbers DataFrame.to_csv appends (cluster, n_reads, avg_alignment_score) ----
+// pandas writes an int64 value as its decimal text and a float64 value as numpy's str() of it
+// (get_values_for_csv: values.astype(str) when float_format is None), i.e. Python's repr: the
+// shortest digits that round-trip, positional for decimal exponents -4 <= x < 16 (with ".0" when
+// integral), otherwise d[.ddd]e+XX.  std::to_chars gives the shortest round-trip digits.
+
+namespace {
+
+int repr_double(double v, char *out) {
+  char sci[64];
+  auto r = std::to_chars(sci, sci + sizeof(sci), v, std::chars_format::scientific);
+  if (r.ec != std::errc()) return -1;
+  const char *p = sci;
+  const char *end = r.ptr;
+  char *o = out;
+  if (*p == '-') *o++ = *p++;
+  std::string digits;
+  const char *e = std::find(p, end, 'e');
+  for (const char *q = p; q < e; ++q)
+    if (*q != '.') digits.push_back(*q);
+  const int x = std::atoi(std::string(e + 1, end).c_str());        // v = d.ddd x 10^x
+  while (digits.size() > 1 && digits.back() == '0') digits.pop_back();
+  const int nd = static_cast<int>(digits.size());
+  if (x >= -4 && x < 16) {
+    const int decpt = x + 1;                                           // digits before the point
+    if (decpt <= 0) {
+      *o++ = '0';
+      *o++ = '.';
+      for (int k = 0; k < -decpt; ++k) *o++ = '0';
+      for (char c : digits) *o++ = c;
+    } else if (decpt >= nd) {
+      for (char c : digits) *o++ = c;
+      for (int k = nd; k < decpt; ++k) *o++ = '0';
+      *o++ = '.';
+      *o++ = '0';
+    } else {
+      for (int k = 0; k < nd; ++k) {
+        if (k == decpt) *o++ = '.';
+        *o++ = digits[k];
+      }
+    }
+  } else {
+    *o++ = digits[0];
+    if (nd > 1) {
+      *o++ = '.';
+      for (int k = 1; k < nd; ++k) *o++ = digits[k];
+    }
+    *o++ = 'e';
+    *o++ = x < 0 ? '-' : '+';
+    const int ax = x < 0 ? -x : x;
+    if (ax < 10) *o++ = '0';
+    o += std::sprintf(o, "%d", ax);
+  }
+  return static_cast<int>(o - out);
+}
+
+}  // namespace
+
+extern "C" {
+
+int fslr_format_suffix(int n_cols, const int32_t *kinds, const void *const *cols, int64_t n_keys, char *out,
+                       int64_t cap, int64_t *ends) {
+  if (n_cols < 0 || n_keys < 0 || (!out && cap) || (n_keys && !ends)) return FSLR_INGEST_ERROR;
+  for (int c = 0; c < n_cols; ++c)
+    if (kinds[c] != 0 && kinds[c] != 1) return FSLR_INGEST_ERROR;
+  int64_t pos = 0;
+  char tmp[64];
+  for (int64_t k = 0; k < n_keys; ++k) {
+    for (int c = 0; c < n_cols; ++c) {
+      int len;
+      if (kinds[c] == 0) {
+        len = std::sprintf(tmp, "%lld", static_cast<long long>(static_cast<const int64_t *>(cols[c])[k]));
+      } else {
+        const double v = static_cast<const double *>(cols[c])[k];
+        if (!std::isfinite(v)) return FSLR_INGEST_DECLINE;                // NaN / inf: pandas' own text
+        len = repr_double(v, tmp);
+        if (len < 0) return FSLR_INGEST_ERROR;
+      }
+      if (pos + len + 1 > cap) return FSLR_INGEST_ERROR;
+      out[pos++] = '\t';
+      std::memcpy(out + pos, tmp, static_cast<size_t>(len));
+      pos += len;
+    }
+    ends[k] = pos;
+  }
+  return FSLR_INGEST_OK;
 }
 
 }  // extern "C"

@@ -229,6 +229,9 @@ hipError_t launch_uf_edges(int* parent, const int2* edges, const unsigned long l
 // src == nullptr: src[k] = k mod period
 hipError_t launch_uf_pairs(int* parent, const int* src, const int* dst, long long n, int period, hipStream_t s);
 hipError_t launch_uf_finalize(int* parent, int n, hipStream_t s);
+hipError_t launch_uf_pair_list(int* parent, const int2* pairs, long long n, hipStream_t s);
+hipError_t launch_copy_edges(const int2* edges, const unsigned long long* count, long long cap, int2* out,
+                             long long n_pad, hipStream_t s);
 
 inline int grid_for(long long n, int block = 256, int cap = 256 * 16) {
   long long g = (n + block - 1) / block;

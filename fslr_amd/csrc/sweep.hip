@@ -86,11 +86,14 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
   const int nt = (g.ni + kWave - 1) / kWave;
   const int nw = gridDim.x * kSwWaves;
   const int wid = blockIdx.x * kSwWaves + wv;
-  // tiles in chunks of kTileRun consecutive tiles per wave (a tile's forward window reaches into the
-  // next tile, whose records the same wave then finds in its caches), chunks dealt grid-stride
-  const int nchunks = (nt + kTileRun - 1) / kTileRun;
+  // tiles in chunks of up to kTileRun consecutive tiles per wave (a tile's forward window reaches
+  // into the next tile, whose records the same wave then finds in its caches), chunks dealt
+  // grid-stride; shorter chunks when there are fewer than kTileRun tiles per wave of the grid (a
+  // rank's share of the multi-GPU split), so every wave gets work: the sweep is latency bound
+  const int run = max(1, min(kTileRun, nt / nw));
+  const int nchunks = (nt + run - 1) / run;
   for (int chunk = wid; chunk < nchunks; chunk += nw)
-  for (int tile = chunk * kTileRun; tile < min(nt, (chunk + 1) * kTileRun); ++tile) {
+  for (int tile = chunk * run; tile < min(nt, (chunk + 1) * run); ++tile) {
     const int q0 = tile * kWave;
     const int q = q0 + lane;
     const bool qv = q < g.ni;

@@ -8,7 +8,8 @@ Two splits:
   one RCCL all_to_all; that rank evaluates the pair.  Exact because an interval only meets
   intervals of its own chromosome (cluster.py:159-160): a pair's first-fit matching is the union of
   its per-chromosome matchings, and all of them meet at one evaluator.  The index build, the sweep
-  and the pair evaluation all split W ways; the label exchange below is the one replicated step.
+  and the pair evaluation all split W ways.  Connectivity: the ranks' edge lists (8 B per edge)
+  are all-gathered and every rank runs one union-find over their union (the replicated step).
 * Query-read shards (the walk engine, fslr_query_shard): described next.
 
 Query-read shards: query reads are split into blocks of SHARD_BLOCK
@@ -127,7 +128,7 @@ def chrom_counts_of(csr) -> np.ndarray:
 
 class SweepShard:
     """One rank of the chromosome-split sweep (fslr_set_chrom_filter / fslr_sweep_partition /
-    fslr_sweep_evaluate, then the label exchange).  ``ctx`` holds every read (set_reads); this
+    fslr_sweep_evaluate, then the edge exchange).  ``ctx`` holds every read (set_reads); this
     rank's index covers the chromosomes ``owner == rank``.  Entries travel as int64 tensors on
     ``device``; with the gloo backend they are staged through host memory (CPU rehearsal).
 
@@ -152,7 +153,8 @@ class SweepShard:
         self.send = torch.empty(1 << 16, dtype=torch.int64, device=self.device)
         self.recv = torch.empty(1 << 16, dtype=torch.int64, device=self.device)
         self.local = torch.empty(self.n, dtype=torch.int32, device=self.device)
-        self.gathered = torch.empty(self.world * self.n, dtype=torch.int32, device=self.device)
+        self.esend = torch.empty(1 << 12, dtype=torch.int64, device=self.device)    # (a, b) int32 pairs
+        self.egath = torch.empty(1 << 12, dtype=torch.int64, device=self.device)
         self._labels = None
         ctx.set_chrom_filter(self.owned if world > 1 else None)
 
@@ -242,13 +244,15 @@ class SweepShard:
         except Exception as e:                          # noqa: BLE001 - re-raised on every rank below
             err = e
         mf = int(st['max_fwd'])
+        max_ne = int(st['n_edges'])
         if W > 1:
-            # the error flag rides with the forward-degree maximum, so a pair that raises on one
-            # evaluator raises on every rank instead of leaving the others in a collective
+            # the error flag and the edge count ride with the forward-degree maximum, so a pair that
+            # raises on one evaluator raises on every rank instead of leaving the others in a
+            # collective, and every rank knows the padded size of the edge exchange
             code = 0 if err is None else (1 if isinstance(err, ZeroDivisionError) else 2)
-            t = torch.tensor([mf, code], dtype=torch.int64, device='cpu' if self._gloo() else self.device)
+            t = torch.tensor([mf, code, max_ne], dtype=torch.int64, device='cpu' if self._gloo() else self.device)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            mf, code = int(t[0].item()), int(t[1].item())
+            mf, code, max_ne = (int(x) for x in t.tolist())
             if err is None and code:
                 from ._lib import FslrError
                 err = ZeroDivisionError('division by zero') if code == 1 else FslrError('error on another rank')
@@ -260,11 +264,18 @@ class SweepShard:
             out['capped'] = True
             out['cap'] = self._capped_labels(qlen_cut, nal_cut, pass_table, edge_threshold)
             return out
-        ctx.components()
-        if W > 1:
-            ctx.labels_into(self.local)
-            self._all_gather(self.gathered, self.local)
-            ctx.union_label_vectors(self.gathered)
+        if W == 1:
+            ctx.components()
+            return out
+        # components of the union of the ranks' edges: all_gather of the edge lists, padded to the
+        # largest count (8 B per edge: 1.8M edges at 1M reads, against 4 B per read per rank for
+        # a label exchange), then one union-find over all of them on every rank
+        m = max(1, max_ne)
+        self.esend = self._grow(self.esend, m)
+        self.egath = self._grow(self.egath, W * m)
+        ctx.edges_into(self.esend, m)
+        self._all_gather(self.egath[:W * m], self.esend[:m])
+        ctx.components_from_pairs(self.egath, W * m)
         return out
 
     def _capped_labels(self, qlen_cut, nal_cut, pass_table, edge_threshold):

@@ -46,6 +46,7 @@ def load(path: str = LIB_PATH):
         'fslr_tsv_uniques': (i32, [vp, i32, vp, vp]),
         'fslr_tsv_verbatim': (i32, [vp]),
         'fslr_tsv_write': (i32, [vp, cp, cp, vp, i64, vp, vp, vp, cp, ctypes.c_size_t]),
+        'fslr_format_suffix': (i32, [i32, vp, vp, i64, vp, i64, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -123,17 +124,25 @@ class TsvFile:
 
         ``suffix_frame`` is constant per ``suffix_key`` value (one value per output row); pandas
         formats one row per distinct key, so the appended numbers are pandas' own text.
+        ``suffix_key``: a Series / array of keys, or ``(codes, uniques)`` already factorized.
         """
         rows = np.ascontiguousarray(rows, dtype=np.int64)
-        codes, uniq = pd.factorize(suffix_key, sort=False)
+        if isinstance(suffix_key, tuple):
+            codes, uniq = suffix_key
+        else:
+            codes, uniq = pd.factorize(suffix_key, sort=False)
         first = np.full(len(uniq), -1, dtype=np.int64)
         first[codes[::-1]] = np.arange(len(codes) - 1, -1, -1)
         per_key = suffix_frame.iloc[first]
-        text = per_key.to_csv(sep='\t', header=False, index=False, lineterminator='\n')
-        lines = text.split('\n')[:len(uniq)]
-        enc = [('\t' + ln).encode() for ln in lines]
-        ends = np.cumsum([len(x) for x in enc], dtype=np.int64) if enc else np.zeros(1, np.int64)
-        buf = b''.join(enc) or b'\0'
+        got = format_suffix(per_key)
+        if got is not None:
+            buf, ends = got
+        else:
+            text = per_key.to_csv(sep='\t', header=False, index=False, lineterminator='\n')
+            lines = text.split('\n')[:len(uniq)]
+            enc = [('\t' + ln).encode() for ln in lines]
+            ends = np.cumsum([len(x) for x in enc], dtype=np.int64) if enc else np.zeros(1, np.int64)
+            buf = b''.join(enc) or b'\0'
         head = ''.join('\t' + str(c) for c in suffix_frame.columns).encode()
         sid = np.ascontiguousarray(codes, dtype=np.int32)
         err = ctypes.create_string_buffer(512)
@@ -143,23 +152,102 @@ class TsvFile:
             raise OSError(err.value.decode())
 
 
+def format_suffix(frame: pd.DataFrame):
+    """(buffer, ends) of ``frame.to_csv(sep='\\t', header=False, index=False)``'s rows, each prefixed
+    by a tab, formatted natively (fslr_format_suffix) for int64 / finite float64 columns, or None
+    (the caller formats with pandas)."""
+    L = load()
+    n = len(frame)
+    kinds, arrs = [], []
+    for c in frame.columns:
+        v = frame[c].to_numpy()
+        if v.dtype == np.int64:
+            kinds.append(0)
+        elif v.dtype == np.float64:
+            kinds.append(1)
+        else:
+            return None
+        arrs.append(np.ascontiguousarray(v))
+    if not arrs or n == 0:
+        return None
+    cap = n * len(arrs) * 40 + 16
+    out = np.empty(cap, dtype=np.uint8)
+    ends = np.empty(n, dtype=np.int64)
+    k = np.asarray(kinds, dtype=np.int32)
+    ptrs = (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+    rc = L.fslr_format_suffix(len(arrs), k.ctypes.data, ctypes.cast(ptrs, ctypes.c_void_p), n, out.ctypes.data, cap,
+                              ends.ctypes.data)
+    if rc != OK:
+        return None
+    return out[:int(ends[-1])].tobytes() or b'\0', ends
+
+
+class QnameCodes:
+    """``pd.factorize(qname, sort=False)`` of a file's rows, made by the reader.  Frames derived
+    from the read frame carry it in ``attrs`` (shared, never copied: pandas deep-copies attrs), so
+    the clustering block does not hash 10M qname strings once per stage; :func:`factorize_qname`
+    takes the rows a derived frame kept by its index (the file's row numbers)."""
+
+    def __init__(self, codes, uniq):
+        self.codes = codes
+        self.uniq = uniq
+
+    def __deepcopy__(self, memo):
+        return self
+
+    def __copy__(self):
+        return self
+
+
+ATTR = 'fslr_qname_codes'
+
+
+def factorize_qname(df: pd.DataFrame):
+    """``pd.factorize(df['qname'], sort=False)``: codes in first-appearance order and the uniques.
+
+    From the reader's codes when ``df`` came from :func:`frame_from` (its rows are file rows, its
+    index their row numbers, its qname column unchanged); otherwise by pandas."""
+    qc = df.attrs.get(ATTR)
+    if not isinstance(qc, QnameCodes):
+        return pd.factorize(df['qname'], sort=False)
+    idx = df.index
+    if isinstance(idx, pd.RangeIndex) and idx.start == 0 and idx.step == 1 and len(idx) == len(qc.codes):
+        return qc.codes, qc.uniq
+    c = qc.codes[idx.to_numpy()]
+    n_u = len(qc.uniq)
+    first = np.full(n_u, -1, dtype=np.int64)
+    first[c[::-1]] = np.arange(len(c) - 1, -1, -1)          # first row of each code present
+    present = np.flatnonzero(first >= 0)
+    order = present[np.argsort(first[present], kind='stable')]
+    remap = np.full(n_u, -1, dtype=np.int64)
+    remap[order] = np.arange(order.size)
+    return remap[c], qc.uniq[order]
+
+
 def frame_from(t: 'TsvFile', int_columns=INT_COLUMNS, str_columns=STR_COLUMNS):
-    """The columns (file order) as pandas would type them, or None."""
+    """The columns (file order) as pandas would type them, or None.  The qname codes ride along
+    in ``attrs`` (:class:`QnameCodes`)."""
     if t.declined or not (set(int_columns) | set(str_columns)) <= set(t.columns):
         return None
     cols = {}
+    qcodes = None
     for name in set(int_columns) | set(str_columns):
         if name in str_columns:
             f = t.factorize(name)
             if f is None:
                 return None
             cols[name] = f[1][f[0]]
+            if name == 'qname':
+                qcodes = QnameCodes(f[0], f[1])
         else:
             v = t.int_column(name)
             if v is None:
                 return None
             cols[name] = v
-    return pd.DataFrame({c: cols[c] for c in t.columns if c in cols})
+    df = pd.DataFrame({c: cols[c] for c in t.columns if c in cols})
+    if qcodes is not None:
+        df.attrs[ATTR] = qcodes
+    return df
 
 
 def read_hot_columns(path: str, n_threads: int = 0):

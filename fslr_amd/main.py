@@ -37,8 +37,7 @@ def assign_clusters(bed_file: pd.DataFrame, G: cluster.ClusterGraph):
     n_reads 1.  Both columns are float when any such singleton exists (the
     reference's left merge introduces NaN before fillna), int otherwise.
     """
-    qn = bed_file['qname']
-    codes, uniq = pd.factorize(qn, sort=False)
+    codes, uniq = ingest.factorize_qname(bed_file)
     rank_names = G.qnames_by_rank
     node = G.node_mask
     cid_by_name = pd.Series(G.component_id[node], index=pd.Index(rank_names[node], dtype=object))
@@ -188,14 +187,14 @@ def _cluster_and_write(args, basename, bed_file, tsv, t):
     if tsv is not None:
         added = [c for c in bed_file.columns if c not in set(tsv.columns)]
         tsv.write_rows(f'{basename}.mappings.cluster.bed', bed_file.index.to_numpy(), bed_file[added],
-                       bed_file['qname'])
+                       ingest.factorize_qname(bed_file))
     else:
         bed_file.to_csv(f'{basename}.mappings.cluster.bed', index=False, sep='\t')
     bed_representative = cluster.choose_alignment(bed_file)
     if tsv is not None:
         added = [c for c in bed_representative.columns if c not in set(tsv.columns)]
         tsv.write_rows(f'{basename}.mappings.representative.bed', bed_representative.index.to_numpy(),
-                       bed_representative[added], bed_representative['qname'])
+                       bed_representative[added], ingest.factorize_qname(bed_representative))
     else:
         bed_representative.to_csv(f'{basename}.mappings.representative.bed', index=False, sep='\t')
     t['write'] = time.perf_counter() - t3

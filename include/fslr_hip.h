@@ -24,6 +24,9 @@
  *                         multi-GPU path)
  *   fslr_union_pairs      (multi-GPU merge of per-shard component labels; no
  *                         reference counterpart — the reference is single-process)
+ *   fslr_copy_edges_device, fslr_components_from_pairs
+ *                         (multi-GPU merge of the ranks' gathered edge lists: get_subgraphs,
+ *                         cluster.py:230-234, over the union of the ranks' edges)
  *
  * Conventions: plain C types, caller-owned host arrays, library-owned device
  * memory behind an opaque context.  Every function returns FSLR_OK (0) or an
@@ -54,7 +57,7 @@
 extern "C" {
 #endif
 
-#define FSLR_ABI_VERSION 4
+#define FSLR_ABI_VERSION 5
 #define FSLR_MAX_L 64                /* max intervals per read (bitmask width) */
 #define FSLR_MAX_READS (1 << 25)     /* read rank packs into bits 6..30 of the index record */
 #define FSLR_THR_ZERO_ALN INT32_MIN
@@ -263,6 +266,13 @@ int  fslr_copy_fwd_device(fslr_ctx *ctx, int32_t *dst);
  * Follow with fslr_finalize_labels.  Async. */
 int  fslr_union_pairs(fslr_ctx *ctx, const int32_t *src, const int32_t *dst, int64_t n, int on_device);
 int  fslr_finalize_labels(fslr_ctx *ctx);
+/* Copy this context's edges as int32 (a, b) pairs into a caller-owned device buffer of n_pad pairs,
+ * padded with (-1, -1); the edge count is read on the device, so n_pad only has to be at least it
+ * (the multi-GPU merge pads every rank to the largest count).  Async, ctx stream. */
+int  fslr_copy_edges_device(fslr_ctx *ctx, int32_t *dst, int64_t n_pad);
+/* Labels = connected components (min-rank roots) of the n int32 (a, b) device pairs at `pairs`
+ * (pairs with a < 0 are skipped): the union of W ranks' gathered edge lists.  Async. */
+int  fslr_components_from_pairs(fslr_ctx *ctx, const int32_t *pairs, int64_t n);
 
 #ifdef __cplusplus
 }

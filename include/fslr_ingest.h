@@ -63,6 +63,13 @@ int fslr_tsv_write(const FslrTsv *t, const char *path, const char *header_suffix
                    int64_t n_out, const int32_t *suffix_id, const char *suffix_buf, const int64_t *suffix_ends,
                    char *err, size_t errlen);
 
+/* Suffix text DataFrame.to_csv writes for n_keys rows of n_cols numeric columns: per key,
+ * "\t" + value for each column, concatenated into out (cap bytes), ends[k] = end of key k.
+ * kinds[c]: 0 = int64 (decimal), 1 = float64 (numpy str(): Python's shortest round-trip repr).
+ * DECLINE on a NaN / inf value (pandas writes its na_rep / own text). */
+int fslr_format_suffix(int n_cols, const int32_t *kinds, const void *const *cols, int64_t n_keys, char *out,
+                       int64_t cap, int64_t *ends);
+
 #ifdef __cplusplus
 }
 #endif

@@ -164,6 +164,19 @@ class EmuSweepContext:
     def labels_into(self, t):
         t.numpy()[:] = self.labels()
 
+    def edges_into(self, t, n_pad):
+        e = self._edges[:n_pad]
+        pairs = np.full((n_pad, 2), -1, dtype=np.int32)
+        pairs[:len(e)] = e[:, :2]
+        t.numpy()[:n_pad] = pairs.view(np.int64)[:, 0]
+
+    def components_from_pairs(self, t, n):
+        pairs = t.numpy()[:n].view(np.int32).reshape(-1, 2)
+        self._parent = np.arange(self.n_reads)
+        for x, y in pairs.tolist():
+            if x >= 0:
+                self._union(x, y)
+
     def union_label_vectors(self, t):
         lab = t.numpy()
         n = self.n_reads

@@ -168,3 +168,59 @@ def test_writer_reproduces_reference_outputs_byte_exact(tmp_path, name, kind):
         o = tmp_path / 'out.bed'
         t.write_rows(str(o), rows, exp_df.iloc[:, n_in:], exp_df['qname'])
     assert o.read_bytes() == exp
+
+
+@pytest.mark.parametrize('name', _golden_with_outputs())
+def test_shared_qname_codes_match_pandas(tmp_path, name):
+    """The reader's qname codes (ingest.QnameCodes in attrs) give pd.factorize(sort=False) of every
+    frame the clustering block derives (keep_fillings' rows, the representative rows), and
+    choose_alignment's bincount path equals pandas' groupby mean / idxmax on the reference's own
+    cluster assignment (cluster.py:237-254)."""
+    import io
+    import numpy as np
+    from fslr_amd import cluster
+    src = gzip.open(os.path.join(GOLDEN, name, 'input.mappings.bed.gz')).read()
+    exp = pd.read_csv(io.BytesIO(gzip.open(os.path.join(GOLDEN, name, 'expected.cluster.bed.gz')).read()), sep='\t')
+    p = tmp_path / 'in.bed'
+    p.write_bytes(src)
+    with ingest.TsvFile(str(p), 3) as t:
+        bed = ingest.frame_from(t, int_columns=ingest.INT_COLUMNS + ('alignment_score',))
+    if bed is None or len(exp) == 0:
+        pytest.skip('input declined by the native reader')
+    assert isinstance(bed.attrs.get(ingest.ATTR), ingest.QnameCodes)
+    rng = np.random.default_rng(5)
+    subsets = [bed, bed[rng.random(len(bed)) < 0.5], cluster.keep_fillings(bed.copy())]
+    for df in subsets:
+        c1, u1 = ingest.factorize_qname(df)
+        c2, u2 = pd.factorize(df['qname'], sort=False)
+        assert np.array_equal(c1, c2) and list(u1) == list(u2)
+    per_q = exp.drop_duplicates('qname').set_index('qname')
+    for col in ('cluster', 'n_reads'):
+        bed[col] = bed['qname'].map(per_q[col]).to_numpy()
+    assert cluster._choose_alignment_codes(bed.copy()) is not None      # the bincount path runs
+    plain = bed.copy()
+    plain.attrs = {}
+    fast = cluster.choose_alignment(bed)
+    slow = cluster.choose_alignment(plain)
+    assert fast.index.equals(slow.index)
+    np.testing.assert_array_equal(fast['avg_alignment_score'].to_numpy(), slow['avg_alignment_score'].to_numpy())
+    np.testing.assert_array_equal(bed['avg_alignment_score'].to_numpy(), plain['avg_alignment_score'].to_numpy())
+
+
+def test_native_suffix_text_equals_pandas_to_csv():
+    """fslr_format_suffix writes int64 and float64 columns exactly as DataFrame.to_csv does (numpy's
+    str(): shortest round-trip digits, positional for exponents -4..15, '.0' when integral)."""
+    import numpy as np
+    rng = np.random.default_rng(1)
+    vals = np.concatenate([rng.random(20000) * 10.0 ** rng.integers(-8, 20, 20000),
+                           np.arange(-5, 3000, dtype=float),
+                           rng.integers(0, 10 ** 6, 5000) / rng.integers(1, 1000, 5000),
+                           [0.0, -0.0, 1e16, 1e15, 9999999999999998.0, 1e-4, 1e-5, 0.1, 0.3, 1 / 3, 2.0 ** 53,
+                            1.5e300, 5e-324, 123456789.125, -2.5e-7, 45.0, 1234.5]])
+    df = pd.DataFrame({'a': rng.integers(-10 ** 15, 10 ** 15, len(vals)), 'b': vals, 'c': vals * 3})
+    buf, ends = ingest.format_suffix(df)
+    text = df.to_csv(sep='\t', header=False, index=False, lineterminator='\n')
+    assert buf == b''.join(('\t' + ln).encode() for ln in text.split('\n')[:len(df)])
+    assert ends[-1] == len(buf)
+    assert ingest.format_suffix(pd.DataFrame({'x': [1.0, float('nan')]})) is None        # na_rep: pandas
+    assert ingest.format_suffix(pd.DataFrame({'x': ['a', 'b']})) is None

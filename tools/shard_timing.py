@@ -4,11 +4,13 @@
 For each world size W the ranks' work is run one rank at a time on cuda:0 with the data a rank
 would hold (every read; the index of its own chromosomes):
   part[r]  = build_index (filtered) + fslr_sweep_partition (sweep, pack, route; ends in a sync)
-  eval[d]  = fslr_sweep_evaluate (sort + pair kernel) + components over the entries destined to d
-  merge    = union of W label vectors + finalize (the replicated step)
+  eval[d]  = fslr_sweep_evaluate (sort + pair kernel) over the entries destined to d, + the copy of
+             its edges into the padded exchange buffer
+  merge    = union-find over the W gathered edge lists (the replicated step)
 and the single-context step (build_index + sweep query + components) as the W = 1 baseline.
 The exchange itself cannot run on one GPU; it is priced from the bytes each rank moves
-(entries all_to_all: the off-rank share of its entries; labels all_gather: 4 N (W - 1)) at an
+(entries all_to_all: the off-rank share of its entries; edges all_gather: 8 B x the largest
+rank's edge count x (W - 1)) at an
 assumed per-GPU xGMI rate (--xgmi-gbs, default 300 GB/s of the 7 x ~153 GB/s links, both
 directions shared) plus a fixed per-collective latency (--coll-us).
 
@@ -81,6 +83,7 @@ def main():
         c1.components()
     t1 = timed(single, args.reps)
     st1 = c1.stats()
+    c1_labels = c1.labels()
     log(f'W=1 step {t1:.3f} ms, {st1["n_edges"]} edges, {st1["match_entries"]} entries')
     c1.close()
 
@@ -116,31 +119,44 @@ def main():
             for d in range(W):
                 segs[d].append(buf[pos[d]:pos[d + 1]].clone())
             sent.append(cnt)
-        evl, nedges = [], 0
+        evl, nedges, elists = [], [], []
         for d in range(W):
             ent = torch.cat(segs[d])
+            ebuf = torch.empty(max(1, int(1.5 * st1['n_edges'] / W) + 4096), dtype=torch.int64, device=dev)
 
             def e():
                 ce.sweep_evaluate(qc, nc, pt, ent, ent.numel())
-                ce.components()
+                if W == 1:
+                    ce.components()
+                else:
+                    ce.edges_into(ebuf, ebuf.numel())
             evl.append(timed(e, args.reps))
-            nedges += ce.stats()['n_edges']
+            ne = ce.stats()['n_edges']
+            nedges.append(ne)
+            elists.append(ebuf[:ne].clone())
             segs[d] = None
             del ent
-        assert nedges == st1['n_edges'], (nedges, st1['n_edges'])
-        gathered = torch.zeros(W * n, dtype=torch.int32, device=dev)
-        ce.labels_into(gathered[:n])
-        merge = timed(lambda: ce.union_label_vectors(gathered), args.reps) if W > 1 else 0.0
+        assert sum(nedges) == st1['n_edges'], (nedges, st1['n_edges'])
+        m = max(nedges)
+        gathered = torch.full((W * m,), -1, dtype=torch.int64, device=dev)
+        for d in range(W):
+            gathered[d * m:d * m + nedges[d]] = elists[d]
+        merge = timed(lambda: ce.components_from_pairs(gathered, W * m), args.reps) if W > 1 else 0.0
+        if W > 1:
+            ref = c1_labels
+            got = ce.labels()
+            assert np.array_equal(got, ref), 'merged labels differ from the single context'
         sent = np.array(sent)
         off_rank = np.array([sent[r].sum() - sent[r, r] for r in range(W)])
         recv = sent.sum(axis=0)
         a2a_ms = 0.0 if W == 1 else (8 * max(off_rank.max(), (recv - np.diag(sent)).max()) / (args.xgmi_gbs * 1e6)
                                      + 2 * args.coll_us / 1000)
-        gather_ms = 0.0 if W == 1 else 4 * n * (W - 1) / (args.xgmi_gbs * 1e6) + args.coll_us / 1000
-        step = max(part) + a2a_ms + max(evl) + gather_ms + merge
+        gather_ms = 0.0 if W == 1 else 8 * m * (W - 1) / (args.xgmi_gbs * 1e6) + args.coll_us / 1000
+        # + the all_reduce of (max forward degree, error flag, edge count) between evaluation and gather
+        step = max(part) + a2a_ms + max(evl) + gather_ms + merge + (args.coll_us / 1000 if W > 1 else 0.0)
         row = {'W': W, 'part_ms': part, 'eval_ms': evl, 'merge_ms': merge, 'a2a_ms_model': a2a_ms,
                'gather_ms_model': gather_ms, 'entries_sent_per_rank': sent.sum(axis=1).tolist(),
-               'entries_recv_per_rank': recv.tolist(), 'projected_step_ms': step,
+               'entries_recv_per_rank': recv.tolist(), 'edges_per_rank': nedges, 'projected_step_ms': step,
                'projected_speedup': t1 / step}
         log(f'W={W}: part max {max(part):.3f} ms, eval max {max(evl):.3f} ms, merge {merge:.3f} ms, '
             f'a2a {a2a_ms:.3f} ms, gather {gather_ms:.3f} ms -> {step:.3f} ms ({t1 / step:.2f}x)')
