@@ -158,15 +158,18 @@ def prepare_data(bed_df, cluster_mask, chromosome_lengths, threshold=500_000) ->
     chrom = bed_df['chrom'].to_numpy()
     if chrom.dtype.kind not in 'iu':                    # not renamed (rename_chromosomes not called)
         chrom = pd.factorize(bed_df['chrom'], sort=False)[0]
-    data = IntervalData(
-        chrom=chrom.astype(np.int64)[order], start=start.astype(np.int64)[order],
-        end=end.astype(np.int64)[order], aln_size=aln.astype(np.int64)[order], qcode=codes.astype(np.int64)[order],
-        qnames=np.asarray(uniq, dtype=object), n_alignments=bed_df['n_alignments'].to_numpy().astype(np.int64)[order],
-        qlen2=bed_df['qlen2'].to_numpy().astype(np.int64)[order],
-        middle=(aln // 2 + start).astype(np.int64)[order], index=bed_df.index.to_numpy()[order])
     if cluster_mask:
-        data = mask_sequences2(data, cluster_mask, chromosome_lengths, threshold)
-    return data
+        # mask_sequences2 (cluster.py:89-106) is a per-interval predicate applied to the sorted list:
+        # evaluated before the sort, one gather does both
+        keep = mask_keep(np.asarray(chrom, np.int64), np.asarray(start, np.int64), np.asarray(end, np.int64),
+                         cluster_mask, chromosome_lengths, threshold)
+        order = order[keep[order]]
+    cols = ingest.gather_columns([chrom, start, end, aln, codes, bed_df['n_alignments'].to_numpy(),
+                                  bed_df['qlen2'].to_numpy(), aln // 2 + start], order)
+    c, s, e, a, q, nal, ql2, mid = cols
+    ix = bed_df.index.to_numpy()[order]
+    return IntervalData(chrom=c, start=s, end=e, aln_size=a, qcode=q, qnames=np.asarray(uniq, dtype=object),
+                        n_alignments=nal, qlen2=ql2, middle=mid, index=ix)
 
 
 def get_chromosome_lengths(bam_path):

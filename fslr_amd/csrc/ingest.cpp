@@ -558,3 +558,61 @@ int fslr_format_suffix(int n_cols, const int32_t *kinds, const void *const *cols
 }
 
 }  // extern "C"
+
+// ---- CSR grouping of the prepared interval list (prepare_data order -> reads by rank) ----
+extern "C" {
+
+int fslr_group_by_first_appearance(const int64_t *codes, int64_t n, int64_t n_codes, int64_t *read_code,
+                                   int64_t *n_reads, int64_t *off, int64_t *perm) {
+  if (n < 0 || n_codes < 0 || (n && (!codes || !perm)) || !n_reads || !off) return FSLR_INGEST_ERROR;
+  std::vector<int64_t> rank_of(static_cast<size_t>(n_codes), -1);
+  int64_t nr = 0;
+  for (int64_t k = 0; k < n; ++k) {                 // rank = order of first appearance (cluster.py:189-191)
+    const int64_t c = codes[k];
+    if (c < 0 || c >= n_codes) return FSLR_INGEST_ERROR;
+    if (rank_of[c] < 0) {
+      rank_of[c] = nr;
+      read_code[nr] = c;
+      ++nr;
+    }
+  }
+  std::vector<int64_t> cur(static_cast<size_t>(nr) + 1, 0);
+  for (int64_t k = 0; k < n; ++k) ++cur[rank_of[codes[k]] + 1];
+  for (int64_t r = 0; r < nr; ++r) cur[r + 1] += cur[r];
+  for (int64_t r = 0; r <= nr; ++r) off[r] = cur[r];
+  for (int64_t k = 0; k < n; ++k) perm[cur[rank_of[codes[k]]]++] = k;   // stable: data order inside a read
+  *n_reads = nr;
+  return FSLR_INGEST_OK;
+}
+
+}  // extern "C"
+
+// ---- threaded gather of several int64 columns by one index (prepare_data's sort + mask) ----
+extern "C" {
+
+int fslr_gather_i64(int n_arrays, const int64_t *const *src, int64_t *const *dst, const int64_t *idx, int64_t n,
+                    int n_threads) {
+  if (n_arrays < 0 || n < 0 || (n && !idx)) return FSLR_INGEST_ERROR;
+  const int64_t per = 1 << 16;
+  const int64_t chunks = (n + per - 1) / per;
+  int t = n_threads > 0 ? n_threads : static_cast<int>(std::thread::hardware_concurrency());
+  t = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>({static_cast<int64_t>(t), chunks, 64})));
+  std::atomic<int64_t> next{0};
+  auto work = [&]() {
+    for (int64_t c; (c = next.fetch_add(1)) < chunks;) {
+      const int64_t b = c * per, e = std::min(n, b + per);
+      for (int a = 0; a < n_arrays; ++a) {
+        const int64_t *s = src[a];
+        int64_t *d = dst[a];
+        for (int64_t k = b; k < e; ++k) d[k] = s[idx[k]];
+      }
+    }
+  };
+  std::vector<std::thread> pool;
+  for (int k = 1; k < t; ++k) pool.emplace_back(work);
+  work();
+  for (auto &th : pool) th.join();
+  return FSLR_INGEST_OK;
+}
+
+}  // extern "C"

@@ -47,6 +47,8 @@ def load(path: str = LIB_PATH):
         'fslr_tsv_verbatim': (i32, [vp]),
         'fslr_tsv_write': (i32, [vp, cp, cp, vp, i64, vp, vp, vp, cp, ctypes.c_size_t]),
         'fslr_format_suffix': (i32, [i32, vp, vp, i64, vp, i64, vp]),
+        'fslr_group_by_first_appearance': (i32, [vp, i64, i64, vp, vp, vp, vp]),
+        'fslr_gather_i64': (i32, [i32, vp, vp, vp, i64, i32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -180,6 +182,47 @@ def format_suffix(frame: pd.DataFrame):
     if rc != OK:
         return None
     return out[:int(ends[-1])].tobytes() or b'\0', ends
+
+
+def group_by_first_appearance(codes):
+    """(read_code, off, perm) of the codes grouped by first appearance (fslr_group_by_first_appearance),
+    or None when the codes are not small non-negative ints or the library is not built."""
+    c = np.ascontiguousarray(codes, dtype=np.int64)
+    n = c.size
+    if n == 0 or c.min() < 0 or c.max() >= 4 * n + 1024:
+        return None
+    try:
+        L = load()
+    except FileNotFoundError:
+        return None
+    read_code = np.empty(n, dtype=np.int64)
+    off = np.empty(n + 1, dtype=np.int64)
+    perm = np.empty(n, dtype=np.int64)
+    nr = ctypes.c_int64()
+    rc = L.fslr_group_by_first_appearance(c.ctypes.data, n, int(c.max()) + 1, read_code.ctypes.data,
+                                          ctypes.byref(nr), off.ctypes.data, perm.ctypes.data)
+    if rc != OK:
+        return None
+    return read_code[:nr.value], off[:nr.value + 1], perm
+
+
+def gather_columns(columns, idx, n_threads: int = 0):
+    """[c[idx] for c in columns] as int64, in one threaded native pass (fslr_gather_i64); numpy when
+    the library is not built.  ``idx`` must index every column in range."""
+    idx = np.ascontiguousarray(idx, dtype=np.int64)
+    src = [np.ascontiguousarray(c, dtype=np.int64) for c in columns]
+    try:
+        L = load()
+    except FileNotFoundError:
+        return [c[idx] for c in src]
+    out = [np.empty(idx.size, dtype=np.int64) for _ in src]
+    sp = (ctypes.c_void_p * len(src))(*[c.ctypes.data for c in src])
+    dp = (ctypes.c_void_p * len(out))(*[o.ctypes.data for o in out])
+    rc = L.fslr_gather_i64(len(src), ctypes.cast(sp, ctypes.c_void_p), ctypes.cast(dp, ctypes.c_void_p),
+                           idx.ctypes.data, idx.size, int(n_threads))
+    if rc != OK:
+        raise RuntimeError('fslr_gather_i64 failed')
+    return out
 
 
 class QnameCodes:

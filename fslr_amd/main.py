@@ -172,11 +172,16 @@ def _cluster_and_write(args, basename, bed_file, tsv, t):
         fillings = cluster.filter_high_coverage(fillings, bed_file, chr_lengths, threshold=10000)
     data = cluster.prepare_data(fillings, chromosome_mask, chr_lengths, threshold=500_000)
     t['prepare'] = time.perf_counter() - t1
+    t1 = time.perf_counter()
+    data.csr()                                   # the device layout (host; cached on data)
+    t['csr'] = time.perf_counter() - t1
     t2 = time.perf_counter()
     interval_tree = cluster.build_interval_trees(data, device=args.get('device'), n_gpus=args.get('gpus') or 1)
+    t['upload'] = time.perf_counter() - t2       # context, CSR H2D, index build
+    t2 = time.perf_counter()
     match_data, network = cluster.query_interval_trees(interval_tree, data, overlap, jaccard_cutoffs,
                                                        edge_threshold, qlen_diff, n_alignments_diff)
-    t['device'] = time.perf_counter() - t2
+    t['query'] = time.perf_counter() - t2        # pair engine, cap, components, D2H, match_df
     if network.number_of_edges() == 0:          # main.py:247: #components == #nodes only for an empty graph
         print('No clusters were found.')
         return False

@@ -205,7 +205,13 @@ class CSR:
 def build_csr(data: IntervalData) -> CSR:
     n_iv = len(data)
     codes = np.asarray(data.qcode, dtype=np.int64)
-    if n_iv:
+    from . import ingest
+    grouped = ingest.group_by_first_appearance(codes) if n_iv else None
+    if grouped is not None:
+        # one native O(n) pass: ranks by first appearance, counting-sort grouping
+        read_qcode, off_g, perm = grouped
+        counts = np.diff(off_g)
+    elif n_iv:
         # rank = order of first appearance (cluster.py:189-191); codes are non-negative ints
         if codes.min() >= 0 and codes.max() < 4 * n_iv + 1024:
             first_at = np.full(int(codes.max()) + 1, n_iv, dtype=np.int64)
@@ -236,11 +242,11 @@ def build_csr(data: IntervalData) -> CSR:
         raise ValueError(f'a read has {int(counts.max())} intervals; the device path supports at most {FSLR_MAX_L}')
     off = np.zeros(n + 1, dtype=np.int64)
     np.cumsum(counts, out=off[1:])
-    start = np.asarray(data.start, np.int64)[perm]
-    end = np.asarray(data.end, np.int64)[perm]
+    start, end, chrom_raw, aln_p, nal_p = ingest.gather_columns(
+        [data.start, data.end, data.chrom, data.aln_size, data.n_alignments], perm) if n_iv else \
+        [np.zeros(0, np.int64)] * 5
     if n_iv and (start.min() < 0 or end.max() >= MAX_COORD):
         raise ValueError('interval coordinates must lie in [0, 2**30) for the device path')
-    chrom_raw = np.asarray(data.chrom, np.int64)[perm]
     if n_iv and chrom_raw.min() >= 0 and chrom_raw.max() < (1 << 24):
         present = np.bincount(chrom_raw) > 0          # chromosome ids are small ints: O(n) dense ids
         cids = np.flatnonzero(present)
@@ -257,11 +263,11 @@ def build_csr(data: IntervalData) -> CSR:
     for name, v in (('qlen2', read_qlen2), ('n_alignments', read_nal)):
         if v.size and (v.min() < np.iinfo(np.int32).min or v.max() > np.iinfo(np.int32).max):
             raise ValueError(f'{name} outside int32')
-    nal_varies = bool(n_iv and np.any(nal[perm] != np.repeat(read_nal, counts)))
+    nal_varies = bool(n_iv and np.any(nal_p != np.repeat(read_nal, counts)))
     return CSR(read_off=off.astype(np.int32), read_qlen2=read_qlen2.astype(np.int32),
                read_nal=read_nal.astype(np.int32), iv_chrom=chrom_dense.astype(np.int32),
                iv_start=start.astype(np.int32), iv_end=end.astype(np.int32),
-               iv_aln=np.asarray(data.aln_size, np.int64)[perm], n_chroms=max(1, int(len(cids))),
+               iv_aln=aln_p, n_chroms=max(1, int(len(cids))),
                read_qcode=read_qcode, data_pos=perm.astype(np.int64), nal_varies=nal_varies,
                start_sorted=bool(n_iv < 2 or np.all(np.diff(np.asarray(data.start, np.int64)) >= 0)))
 

@@ -70,6 +70,18 @@ int fslr_tsv_write(const FslrTsv *t, const char *path, const char *header_suffix
 int fslr_format_suffix(int n_cols, const int32_t *kinds, const void *const *cols, int64_t n_keys, char *out,
                        int64_t cap, int64_t *ends);
 
+/* Reads of the prepared interval list (prepare_data order, cluster.py:109-121) grouped by rank =
+ * order of first appearance of their code (cluster.py:189-191): read_code[r] (capacity n), off[r]
+ * (capacity n + 1) and perm = the list positions in CSR order (by rank, list order inside a read).
+ * codes must lie in [0, n_codes). */
+int fslr_group_by_first_appearance(const int64_t *codes, int64_t n, int64_t n_codes, int64_t *read_code,
+                                   int64_t *n_reads, int64_t *off, int64_t *perm);
+
+/* dst[a][k] = src[a][idx[k]] for k < n and each of the n_arrays int64 columns (n_threads <= 0: all
+ * cores).  prepare_data's start sort + mask as one threaded pass. */
+int fslr_gather_i64(int n_arrays, const int64_t *const *src, int64_t *const *dst, const int64_t *idx, int64_t n,
+                    int n_threads);
+
 #ifdef __cplusplus
 }
 #endif

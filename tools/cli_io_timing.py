@@ -1,6 +1,8 @@
 """End-to-end `fslr --skip-alignment` wall time with the native reader/writer vs pandas I/O.
 
-Usage: python tools/cli_io_timing.py N_READS LMAX SEED OUT_JSON
+Usage: python tools/cli_io_timing.py N_READS LMAX SEED OUT_JSON [DIST] [FLAGS]
+  DIST: uniform (default) or zipf; FLAGS: comma-separated I/O modes to run (default
+  --native-io,--pandas-io) plus extra CLI options, e.g. "--native-io,--gpus=2"
 Writes a synthetic `{name}.mappings.bed` + header-only BAM (SURVEY §8d generator), runs the CLI
 in-process twice (`--native-io`, then `--pandas-io`) with `--timings`, checks the two output pairs
 are byte-identical, and records the per-stage seconds from the `timings_s` line.
@@ -23,16 +25,21 @@ from fslr_amd.main import pipeline  # noqa: E402
 
 def main():
     n, lmax, seed, out_json = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
+    dist = sys.argv[5] if len(sys.argv) > 5 else 'uniform'
+    flags = sys.argv[6].split(',') if len(sys.argv) > 6 else ['--native-io', '--pandas-io']
+    modes = [f for f in flags if f in ('--native-io', '--pandas-io')]
+    extra = [f for f in flags if f not in modes]
     td = tempfile.mkdtemp(dir=os.environ.get('TMPDIR', '/tmp'))
     t0 = time.perf_counter()
-    s = synth.generate(n, lmax, seed)
+    s = synth.generate(n, lmax, seed, dist=dist)
     s.write_tsv(os.path.join(td, 'x.mappings.bed'))
     bam_header.write_bam_header(os.path.join(td, 'x.bwa_dodi.bam'), list(s.chrom_lengths.items()))
-    res = {'n_reads': n, 'lmax': lmax, 'seed': seed, 'gen_s': time.perf_counter() - t0,
+    del s
+    res = {'n_reads': n, 'lmax': lmax, 'seed': seed, 'dist': dist, 'extra_args': extra, 'gen_s': time.perf_counter() - t0,
            'bed_bytes': os.path.getsize(os.path.join(td, 'x.mappings.bed'))}
     print(json.dumps(res), flush=True)
     outs = {}
-    for flag in ('--native-io', '--pandas-io'):
+    for flag in modes:
         od = os.path.join(td, flag.strip('-'))
         os.makedirs(od)
         for f in ('x.mappings.bed', 'x.bwa_dodi.bam'):
@@ -41,13 +48,13 @@ def main():
         t1 = time.perf_counter()
         with contextlib.redirect_stderr(err):
             r = CliRunner().invoke(pipeline, ['--name', 'x', '--out', od, '--ref', 'u.fa', '--primers', '21q1',
-                                              '--skip-alignment', '--timings', flag], catch_exceptions=False)
+                                              '--skip-alignment', '--timings', flag] + extra, catch_exceptions=False)
         wall = time.perf_counter() - t1
         line = [ln for ln in (r.output + err.getvalue()).splitlines() if ln.startswith('timings_s')]
         res[flag.strip('-')] = {'wall_s': wall, 'exit': r.exit_code, 'timings': line[-1] if line else None}
         outs[flag] = od
         print(json.dumps(res[flag.strip('-')]), flush=True)
-    res['outputs_identical'] = all(
+    res['outputs_identical'] = None if len(modes) < 2 else all(
         filecmp.cmp(os.path.join(outs['--native-io'], f), os.path.join(outs['--pandas-io'], f), shallow=False)
         for f in ('x.mappings.cluster.bed', 'x.mappings.representative.bed'))
     with open(out_json, 'w') as fh:
