@@ -26,6 +26,10 @@ from . import __version__, cluster, ingest
 # primer names of the reference's primers.csv (fslr/primers.csv:2-7); main.py:59-67 validates
 # --primers against them even under --skip-alignment
 PRIMER_NAMES = ('21q1', '17p6', 'XpYpM', '16p1', 'M613', 'M615')
+# primer_seq column of the reference's primers.csv: collect_mapping_info's 'missing bread' rows take
+# their query span from the primer length (collect_mapping_info.py:130,148)
+PRIMER_SEQS = {'21q1': 'CTACCTCTCTCGACACCAAG', '17p6': 'GGCTGAACTATAGCCTCTGC', 'XpYpM': 'AACACACTGGAAAACCTGGT',
+               '16p1': 'CTGCCCTAGAAGTGAGAAGTCCA', 'M613': 'GGAGGAAAGCATGTTTCTGAG', 'M615': 'TAGTGGACAAACACGAGAGGC'}
 
 
 def assign_clusters(bed_file: pd.DataFrame, G: cluster.ClusterGraph):

@@ -10,7 +10,9 @@ The reference imports packages that are not installed in this image
 path needs:
 
 * ``pysam.AlignmentFile(bam).lengths / .get_reference_name(tid)`` — the BAM
-  header dictionary (``cluster.py:173-175``), decoded by ``fslr_amd.bam_header``.
+  header dictionary (``cluster.py:173-175``), decoded by ``fslr_amd.bam_header``;
+  ``.fetch(until_eof=True)`` — records as ``_AlignedSegment`` stand-ins decoded in pure
+  Python here (for ``collect_mapping_info.py``; independent of the product's C++ decoder).
 * ``superintervals.IntervalMap`` — ``add(start, end, value)``, ``build()``,
   ``search_values(start, end)``: every stored interval with ``start <= qend and
   end >= qstart`` (end-inclusive).  Result ORDER is the library's undocumented
@@ -71,6 +73,100 @@ class _IntervalMap:
         return out
 
 
+class _AlignedSegment:
+    """pysam.AlignedSegment stand-in for collect_mapping_info.py: the attributes it reads, decoded
+    here in pure Python (struct) from SAMv1 §4.2, following pysam's documented semantics:
+    infer_read_length = M I S = X H lengths, infer_query_length = M I S = X lengths,
+    reference_end = reference_start + M D N = X lengths, get_forward_sequence = SEQ
+    reverse-complemented (A<->T, C<->G) when flag & 16."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+    @property
+    def rname(self):
+        return self.reference_id
+
+    def infer_read_length(self):
+        return sum(n for op, n in self.cigartuples if op in (0, 1, 4, 7, 8, 5))
+
+    def infer_query_length(self):
+        return sum(n for op, n in self.cigartuples if op in (0, 1, 4, 7, 8))
+
+    @property
+    def reference_end(self):
+        return self.reference_start + sum(n for op, n in self.cigartuples if op in (0, 2, 3, 7, 8))
+
+    def get_tag(self, name):
+        if name not in self.tags:
+            raise KeyError(f"tag '{name}' not present")
+        return self.tags[name]
+
+    def get_forward_sequence(self):
+        s = self.seq
+        if s is None:
+            return None
+        if self.flag & 16:
+            s = s[::-1].translate(str.maketrans('ACGT', 'TGCA'))
+        return s
+
+
+def _read_records(path):
+    import gzip
+    import struct
+    data = gzip.open(path, 'rb').read()
+    (l_text,) = struct.unpack_from('<i', data, 4)
+    p = 8 + l_text
+    (n_ref,) = struct.unpack_from('<i', data, p)
+    p += 4
+    for _ in range(n_ref):
+        (l_name,) = struct.unpack_from('<i', data, p)
+        p += 8 + l_name
+    out = []
+    code = '=ACMGRSVTWYHKDBN'
+    while p < len(data):
+        (bs,) = struct.unpack_from('<i', data, p)
+        (tid, pos, l_rn, mapq, _bin, n_cig, flag, l_seq, _nt, _np, _tl) = struct.unpack_from('<iiBBHHHiiii', data, p + 4)
+        q = p + 36
+        name = data[q:q + l_rn - 1].decode()
+        q += l_rn
+        cig = []
+        for c in range(n_cig):
+            (v,) = struct.unpack_from('<I', data, q + 4 * c)
+            cig.append((v & 15, v >> 4))
+        q += 4 * n_cig
+        sb = data[q:q + (l_seq + 1) // 2]
+        seq = ''.join(code[(sb[i // 2] >> (4 if i % 2 == 0 else 0)) & 15] for i in range(l_seq)) if l_seq else None
+        q += (l_seq + 1) // 2 + l_seq
+        end = p + 4 + bs
+        tags = {}
+        while q < end:
+            tn = data[q:q + 2].decode()
+            ty = chr(data[q + 2])
+            q += 3
+            if ty in 'cCsSiI':
+                fmt = {'c': '<b', 'C': '<B', 's': '<h', 'S': '<H', 'i': '<i', 'I': '<I'}[ty]
+                (v,) = struct.unpack_from(fmt, data, q)
+                q += struct.calcsize(fmt)
+            elif ty == 'f':
+                (v,) = struct.unpack_from('<f', data, q)
+                q += 4
+            elif ty == 'A':
+                v = chr(data[q])
+                q += 1
+            elif ty in 'ZH':
+                z = data.index(b'\0', q)
+                v = data[q:z].decode()
+                q = z + 1
+            else:
+                raise ValueError(f'tag type {ty}')
+            tags[tn] = v
+        out.append(_AlignedSegment(qname=name, flag=flag, reference_id=tid, reference_start=pos, mapq=mapq,
+                                   cigartuples=cig, seq=seq, tags=tags))
+        p = end
+    return out
+
+
 def _install_stubs():
     from fslr_amd import bam_header
 
@@ -79,12 +175,16 @@ def _install_stubs():
     class AlignmentFile:
         def __init__(self, path, mode='rb', *a, **k):
             refs = bam_header.read_bam_references(path)
+            self._path = path
             self._names = [n for n, _ in refs]
             self.lengths = tuple(l for _, l in refs)
             self.references = tuple(self._names)
 
         def get_reference_name(self, tid):
             return self._names[tid]
+
+        def fetch(self, until_eof=False, **k):
+            return iter(_read_records(self._path))
 
         def close(self):
             pass
