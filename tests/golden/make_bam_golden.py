@@ -122,7 +122,7 @@ def main():
             cmi.mapping_info(os.path.join(OUT, 'flag_problem.bam'), os.path.join(OUT, 'unused.bed'), None, PRIMERS)
         except SystemExit as e:
             code = e.code
-    with open(os.path.join(OUT, 'meta.json'), 'w') as fh:
+    with open(os.path.join(OUT, 'producer.json'), 'w') as fh:
         json.dump({'primers': PRIMERS, 'flag_problem_stdout': out.getvalue().replace(OUT, '{DIR}'),
                    'flag_problem_exit': code,
                    'fslr_version': '0.3.10'}, fh, indent=1)

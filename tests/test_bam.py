@@ -20,7 +20,7 @@ GOLD = os.path.join(os.path.dirname(__file__), 'golden', 'bam')
 
 
 def _meta():
-    with open(os.path.join(GOLD, 'meta.json')) as fh:
+    with open(os.path.join(GOLD, 'producer.json')) as fh:
         return json.load(fh)
 
 
