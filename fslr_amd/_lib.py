@@ -13,7 +13,7 @@ import numpy as np
 
 LIB_PATH = os.environ.get('FSLR_LIB') or os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libfslr_hip.so')
 
-ABI_VERSION = 5          # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
+ABI_VERSION = 6          # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
 FSLR_OK, FSLR_ERR_ZERO_DIVISION, FSLR_ERR_INVALID, FSLR_ERR_HIP, FSLR_ERR_NOMEM, FSLR_ERR_STATE = range(6)
 FSLR_MAX_L = 64
 FSLR_MAX_READS = 1 << 25
@@ -32,7 +32,8 @@ EXPORTED = ['fslr_abi_version', 'fslr_last_error', 'fslr_ctx_create', 'fslr_ctx_
             'fslr_get_fwd_degree', 'fslr_get_edges', 'fslr_labels_device_ptr', 'fslr_copy_labels_device',
             'fslr_copy_fwd_device', 'fslr_union_pairs', 'fslr_finalize_labels', 'fslr_apply_edge_cap',
             'fslr_get_pair_kernel_times', 'fslr_set_chrom_filter', 'fslr_sweep_partition', 'fslr_sweep_evaluate',
-            'fslr_copy_edges_device', 'fslr_components_from_pairs']
+            'fslr_copy_edges_device', 'fslr_components_from_pairs', 'fslr_set_long_reads', 'fslr_long_query',
+            'fslr_get_long_edges']
 
 
 class HipUnavailable(RuntimeError):
@@ -137,6 +138,9 @@ def load(path: str = LIB_PATH):
         'fslr_sweep_evaluate': (ctypes.c_int, [vp, ctypes.POINTER(Params), vp, i64]),
         'fslr_copy_edges_device': (ctypes.c_int, [vp, vp, i64]),
         'fslr_components_from_pairs': (ctypes.c_int, [vp, vp, i64]),
+        'fslr_set_long_reads': (ctypes.c_int, [vp, i64, vp, vp, vp, vp, i32]),
+        'fslr_long_query': (ctypes.c_int, [vp, ctypes.POINTER(Params), ctypes.POINTER(ctypes.c_int64)]),
+        'fslr_get_long_edges': (ctypes.c_int, [vp, vp, vp, vp, vp, i64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -405,6 +409,23 @@ class Context:
             s = None if src is None else np.ascontiguousarray(src, np.int32)
             d = np.ascontiguousarray(dst, np.int32)
             self._check(self._L.fslr_union_pairs(self._h, _ptr(s) if s is not None else None, _ptr(d), int(n), 0))
+
+    # -- reads of more than FSLR_MAX_L intervals (fslr_hip.h fslr_set_long_reads / fslr_long_query) --
+    def set_long_reads(self, n_real, vreal, vbase, rlen, umax):
+        arrs = [np.ascontiguousarray(x, dtype=np.int32) for x in (vreal, vbase, rlen, umax)]
+        self._check(self._L.fslr_set_long_reads(self._h, int(n_real), *(_ptr(a) for a in arrs), int(arrs[3].size)))
+
+    def long_query(self, qlen_cut, nal_cut, pass_table, edge_threshold=10) -> int:
+        """Sweep the virtual index and decide every pair (fslr_long_query); returns the long-pair edge count."""
+        p = self._params(qlen_cut, nal_cut, pass_table, edge_threshold)
+        ne = ctypes.c_int64(0)
+        self._check(self._L.fslr_long_query(self._h, ctypes.byref(p), ctypes.byref(ne)))
+        return int(ne.value)
+
+    def long_edges(self, n_edges: int):
+        out = [np.empty(n_edges, np.int32) for _ in range(4)]
+        self._check(self._L.fslr_get_long_edges(self._h, *(_ptr(a) for a in out), int(n_edges)))
+        return tuple(out)
 
     def finalize_labels(self):
         self._check(self._L.fslr_finalize_labels(self._h))

@@ -30,9 +30,9 @@ import numpy as np
 import pandas as pd
 
 from . import bam_header, ingest, multi
-from ._lib import FSLR_THR_ZERO_ALN, Context
+from ._lib import FSLR_MAX_L, FSLR_THR_ZERO_ALN, Context
 from .prep import (IntervalData, IntervalItem, build_csr, data_order, first_last_masks, fold_overlap_threshold,
-                   group_span, mask_keep, pass_table)
+                   group_span, has_long_reads, mask_keep, pass_table, split_long_reads, umax_table)
 
 __all__ = ['IntervalItem', 'keep_fillings', 'rename_chromosomes', 'chrom_to_str', 'calc_coverage',
            'filter_high_coverage', 'delete_false', 'mask_sequences2', 'prepare_data', 'build_interval_trees',
@@ -190,8 +190,11 @@ class DeviceIntervalIndex:
         self.csr = data.csr()
         self.ctx = ctx or Context(_default_device() if device is None else device)
         c = self.csr
-        thr0 = np.where(c.iv_aln == 0, FSLR_THR_ZERO_ALN, 0).astype(np.int32)
-        self.ctx.load_csr(c, thr0)
+        # reads of more than FSLR_MAX_L intervals: the virtual CSR of the long-read stage
+        self.long = split_long_reads(c) if has_long_reads(c) else None
+        up = self.long[0] if self.long is not None else c
+        thr0 = np.where(up.iv_aln == 0, FSLR_THR_ZERO_ALN, 0).astype(np.int32)
+        self.ctx.load_csr(up, thr0)
         self.ctx.build_index()
 
 
@@ -295,9 +298,9 @@ def query_interval_trees(interval_trees, data, overlap_cutoff, jaccard_threshold
     if isinstance(interval_trees, MultiGpuIndex) and (interval_trees.source is data or interval_trees.data is data):
         mg = interval_trees
         thr = fold_overlap_threshold(mg.csr.iv_aln, overlap_cutoff)
-        if multi.sweep_applies(mg.csr, thr):
+        if multi.sweep_applies(mg.csr, thr) and not has_long_reads(mg.csr):
             return _query_multi_gpu(mg, thr, jaccard_threshold, edge_threshold, qlen_diff, diff)
-        # overlap <= 0 or an aln_size == 0 interval: the walk engine on one GPU
+        # overlap <= 0, an aln_size == 0 interval or a read of more than 64 intervals: one GPU
         interval_trees = DeviceIntervalIndex(mg.data, mg.first_device)
     if not isinstance(interval_trees, DeviceIntervalIndex) or (interval_trees.source is not data and
                                                                interval_trees.data is not data):
@@ -310,6 +313,8 @@ def query_interval_trees(interval_trees, data, overlap_cutoff, jaccard_threshold
     if csr.nal_varies:
         warnings.warn('n_alignments differs between rows of one read; the reference then uses the row its '
                       'search reaches first (order-dependent); the first row in data order is used', EdgeCapWarning)
+    if idx.long is not None:
+        return _query_long(idx, qnames_by_rank, overlap_cutoff, jaccard_threshold, edge_threshold, qlen_diff, diff)
     ctx.set_thresholds(fold_overlap_threshold(csr.iv_aln, overlap_cutoff))
     pt = pass_table(jaccard_threshold)
     qcut = 1 - qlen_diff
@@ -335,6 +340,53 @@ def _graph_outputs(qnames_by_rank, labels, a, b, I, U, fwd, st):
                              'query2': qnames_by_rank[b] if ne else np.zeros(0, object),
                              'jaccard_similarity': I / U if ne else np.zeros(0)})
     return match_df, ClusterGraph(qnames_by_rank, labels, (a, b), fwd, st)
+
+
+def _query_long(idx, qnames_by_rank, overlap_cutoff, jaccard_threshold, edge_threshold, qlen_diff, diff):
+    """query_interval_trees with reads of more than FSLR_MAX_L intervals: the sweep over
+    the virtual CSR writes every match entry; pairs of two short reads are decided by the sweep's pair
+    stage, pairs with a long read by the first-fit over their whole lists (fslr_long_query)."""
+    csr, ctx = idx.csr, idx.ctx
+    vcsr, vreal, vbase, rlen = idx.long
+    n = csr.n_reads
+    thr = fold_overlap_threshold(vcsr.iv_aln, overlap_cutoff)
+    if not multi.sweep_applies(vcsr, thr):
+        raise NotImplementedError('reads of more than 64 intervals need overlap > 0 and no aln_size == 0 '
+                                  'interval on the device path (DESIGN.md §13)')
+    lg = rlen > FSLR_MAX_L
+    if (csr.read_qlen2[lg] == 0).any() or (csr.read_nal[lg] == 0).any():
+        raise NotImplementedError('a read of more than 64 intervals with qlen2 or n_alignments 0 (DESIGN.md §13)')
+    ctx.set_thresholds(thr)
+    ctx.set_long_reads(n, vreal, vbase, rlen, umax_table(jaccard_threshold, int(rlen.max())))
+    pt = pass_table(jaccard_threshold)
+    qcut, ncut = 1 - qlen_diff, 1 - diff
+    ctx.reserve_edges(max(1 << 16, 12 * n))
+    while True:
+        n_long = ctx.long_query(qcut, ncut, pt, int(edge_threshold))
+        st = ctx.stats(check=False)
+        if st['n_edges'] <= st['edge_capacity']:
+            break
+        ctx.reserve_edges(int(st['n_edges'] * 1.25) + 4096)
+    st = ctx.stats()
+    ctx.components()
+    la, lb, lI, lU = ctx.long_edges(n_long)
+    if n_long:
+        ctx.union_pairs(la, lb, n_long, on_device=False)
+        ctx.finalize_labels()
+    labels = ctx.labels()[:n]
+    a, b, I, U = ctx.edges(st['n_edges'])
+    fwd = ctx.fwd_degree()[:n] + np.bincount(la, minlength=n).astype(np.int32)
+    max_fwd = int(fwd.max()) if n else 0
+    if max_fwd > int(edge_threshold):
+        raise NotImplementedError(f'the edge cap binds (a read has {max_fwd} > {int(edge_threshold)} forward '
+                                  'edges) with reads of more than 64 intervals: its replay is not built for '
+                                  'them (DESIGN.md §13)')
+    a, b = np.concatenate([a, la]), np.concatenate([b, lb])
+    I, U = np.concatenate([I, lI]), np.concatenate([U, lU])
+    st = dict(st, engine='sweep+long', n_edges=int(a.shape[0]), max_fwd=max_fwd, long_reads=int(lg.sum()),
+              long_pair_edges=int(n_long),
+              cap={'applied': 0, 'max_fwd': max_fwd})
+    return _graph_outputs(qnames_by_rank, labels, a, b, I, U, fwd, st)
 
 
 def _query_multi_gpu(mg, thr, jaccard_threshold, edge_threshold, qlen_diff, diff):

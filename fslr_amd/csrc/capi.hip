@@ -134,6 +134,7 @@ void fslr_ctx_destroy(fslr_ctx* c) {
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->sw_total) (void)hipHostFree(c->sw_total);
+  fslr_long_free(c);
   if (c->ev_ok) {
     for (auto& e : c->ev) (void)hipEventDestroy(e);
     for (auto& e : c->kev) (void)hipEventDestroy(e);

@@ -96,6 +96,29 @@ struct fslr_ctx {
   bool last_full = false;                // covered every read [0, n) with one shard
   double last_qcut = 0.0, last_ncut = 0.0;
   fslr_cap_stats cap_stats = {};
+  // reads of more than FSLR_MAX_L intervals (long.hip): the virtual-read map and the long-pair stage
+  bool lg_set = false;
+  int64_t lg_n_real = 0, lg_n_edges = 0;
+  int lg_n_umax = 0;
+  int* lg_vreal = nullptr;                  // [virtual reads] real read
+  int* lg_vbase = nullptr;                  // [virtual reads] index of its first interval in the real read
+  int* lg_rlen = nullptr;                   // [real reads] interval count
+  int* lg_umax = nullptr;                   // [n_umax] largest passing U per I (cluster.py:216-219)
+  unsigned long long *lg_pk = nullptr, *lg_ij = nullptr, *lg_pk2 = nullptr, *lg_ij2 = nullptr;
+  int64_t lg_cap = 0;
+  unsigned long long* lg_cnt = nullptr;     // [4] short entries, long entries, long edges, run count
+  unsigned long long* lg_uniq = nullptr;    // per pair run: (ra << 25 | rb)
+  int *lg_rlen_run = nullptr, *lg_roff = nullptr;
+  long long *lg_words = nullptr, *lg_woff = nullptr;
+  int64_t lg_run_cap = 0;
+  unsigned* lg_bits = nullptr;              // used-column bitmaps of the first-fit
+  int64_t lg_bits_cap = 0;
+  int4* lg_edges = nullptr;                 // (ra, rb, I, U)
+  int64_t lg_edge_cap = 0;
+  unsigned char* lg_temp = nullptr;
+  unsigned long long *lg_ent = nullptr, *lg_short = nullptr;   // the sweep's entries; the short-pair ones
+  int64_t lg_ent_cap = 0, lg_short_cap = 0;
+  size_t lg_temp_bytes = 0;
   // profiling
   bool profiling = false;
   hipEvent_t ev[8] = {};
@@ -106,6 +129,9 @@ struct fslr_ctx {
   bool ev_ok = false;
   bool t_index_rec = false, t_query_rec = false, t_comp_rec = false, t_kernel_rec = false;
 };
+
+// frees the long-read stage's buffers (long.hip)
+void fslr_long_free(fslr_ctx* c);
 
 namespace fslr {
 

@@ -238,8 +238,7 @@ def build_csr(data: IntervalData) -> CSR:
     n = counts.size
     if n >= FSLR_MAX_READS:
         raise ValueError(f'{n} reads exceed the device limit of {FSLR_MAX_READS}')
-    if n and counts.max() > FSLR_MAX_L:
-        raise ValueError(f'a read has {int(counts.max())} intervals; the device path supports at most {FSLR_MAX_L}')
+    # reads of more than FSLR_MAX_L intervals are uploaded split into chunks (split_long_reads)
     off = np.zeros(n + 1, dtype=np.int64)
     np.cumsum(counts, out=off[1:])
     start, end, chrom_raw, aln_p, nal_p = ingest.gather_columns(
@@ -270,6 +269,65 @@ def build_csr(data: IntervalData) -> CSR:
                iv_aln=aln_p, n_chroms=max(1, int(len(cids))),
                read_qcode=read_qcode, data_pos=perm.astype(np.int64), nal_varies=nal_varies,
                start_sorted=bool(n_iv < 2 or np.all(np.diff(np.asarray(data.start, np.int64)) >= 0)))
+
+
+def has_long_reads(csr: CSR) -> bool:
+    return bool(csr.n_reads and np.diff(csr.read_off).max() > FSLR_MAX_L)
+
+
+def split_long_reads(csr: CSR):
+    """The virtual CSR of fslr_set_long_reads (include/fslr_hip.h): virtual read r < n
+    is real read r with its first FSLR_MAX_L intervals; the further FSLR_MAX_L-interval chunks of the
+    long reads follow as reads n, n+1, ... (in real-rank, then chunk order).  Returns
+    (virtual CSR, vreal, vbase, rlen)."""
+    L = np.diff(csr.read_off.astype(np.int64))
+    n, ni = L.size, int(csr.read_off[-1])
+    extra = np.maximum((L + FSLR_MAX_L - 1) // FSLR_MAX_L - 1, 0)
+    n_extra = int(extra.sum())
+    extra_off = np.zeros(n, np.int64)
+    np.cumsum(extra[:-1], out=extra_off[1:])
+    r_of = np.repeat(np.arange(n, dtype=np.int64), L)
+    t = np.arange(ni, dtype=np.int64) - np.repeat(csr.read_off[:-1].astype(np.int64), L)
+    chunk = t // FSLR_MAX_L
+    v = np.where(chunk == 0, r_of, n + extra_off[r_of] + chunk - 1)
+    perm = np.argsort(v, kind='stable')
+    nv = n + n_extra
+    voff = np.zeros(nv + 1, np.int64)
+    np.cumsum(np.bincount(v, minlength=nv), out=voff[1:])
+    xr = np.repeat(np.arange(n, dtype=np.int64), extra)
+    vreal = np.concatenate([np.arange(n, dtype=np.int64), xr])
+    xk = np.arange(n_extra, dtype=np.int64) - np.repeat(extra_off, extra) + 1
+    vbase = np.concatenate([np.zeros(n, np.int64), xk * FSLR_MAX_L])
+    vcsr = dataclasses.replace(
+        csr, read_off=voff.astype(np.int32), read_qlen2=csr.read_qlen2[vreal], read_nal=csr.read_nal[vreal],
+        iv_chrom=csr.iv_chrom[perm], iv_start=csr.iv_start[perm], iv_end=csr.iv_end[perm], iv_aln=csr.iv_aln[perm],
+        read_qcode=csr.read_qcode[vreal], data_pos=csr.data_pos[perm])
+    return vcsr, vreal.astype(np.int32), vbase.astype(np.int32), L.astype(np.int32)
+
+
+def umax_table(cutoffs, max_i: int) -> np.ndarray:
+    """``umax[I-1]`` = the largest U (I <= U <= 2 max_i) with ``I/U >= cutoff(I)`` in Python floats
+    (cluster.py:216-219), or I - 1 when none passes: pass_table's rule for any I."""
+    cut = list(cutoffs)
+    if not cut:
+        raise ValueError('min() arg is an empty sequence')
+    hi = 2 * int(max_i)
+    out = np.zeros(int(max_i), np.int64)
+    for I in range(1, int(max_i) + 1):
+        target = cut[I - 1] if I - 1 < len(cut) else cut[-1]
+        if not I / I >= target:
+            out[I - 1] = I - 1
+            continue
+        if I / hi >= target:
+            out[I - 1] = hi
+            continue
+        u = max(I, min(hi, int(I / target)))       # I/U is decreasing in U: step to the boundary exactly
+        while u > I and not I / u >= target:
+            u -= 1
+        while u < hi and I / (u + 1) >= target:
+            u += 1
+        out[I - 1] = u
+    return out.astype(np.int32)
 
 
 # ------------------------------------------------------------------------------------------

@@ -27,6 +27,11 @@
  *   fslr_copy_edges_device, fslr_components_from_pairs
  *                         (multi-GPU merge of the ranks' gathered edge lists: get_subgraphs,
  *                         cluster.py:230-234, over the union of the ranks' edges)
+ *   fslr_set_long_reads,
+ *   fslr_long_query,
+ *   fslr_get_long_edges   cluster.py:140-170 overall_jaccard_similarity for reads of more than
+ *                         FSLR_MAX_L intervals (the reference has no limit; its l2_comparisons
+ *                         scratch holds 100000 columns, :195)
  *
  * Conventions: plain C types, caller-owned host arrays, library-owned device
  * memory behind an opaque context.  Every function returns FSLR_OK (0) or an
@@ -57,7 +62,7 @@
 extern "C" {
 #endif
 
-#define FSLR_ABI_VERSION 5
+#define FSLR_ABI_VERSION 6
 #define FSLR_MAX_L 64                /* max intervals per read (bitmask width) */
 #define FSLR_MAX_READS (1 << 25)     /* read rank packs into bits 6..30 of the index record */
 #define FSLR_THR_ZERO_ALN INT32_MIN
@@ -230,6 +235,24 @@ int  fslr_set_chrom_filter(fslr_ctx *ctx, const uint8_t *owned);
 int  fslr_sweep_partition(fslr_ctx *ctx, const fslr_params *params, int32_t n_dest, int32_t block_shift,
                           void *dst, int64_t dst_cap, int64_t *counts);
 int  fslr_sweep_evaluate(fslr_ctx *ctx, const fslr_params *params, const void *entries, int64_t n);
+
+/* Reads of more than FSLR_MAX_L intervals.  The caller uploads a *virtual* CSR with
+ * fslr_set_reads: virtual read v < n_real is real read v (its first <= FSLR_MAX_L intervals), reads
+ * v >= n_real are the further <= FSLR_MAX_L-interval chunks of the long reads; vreal[v] = its real
+ * read, vbase[v] = the index of its first interval in the real read's list, rlen[r] = the real
+ * read's interval count, umax[I-1] = the largest U with I/U >= cutoff(I) (cluster.py:216-219, Python
+ * floats), for I = 1 .. n_umax >= max(rlen).  Syncs.
+ * fslr_long_query (after fslr_build_index): sweep the virtual index (every match entry), decide the
+ * pairs with a long read with the reference's first-fit over their real interval lists (list1 = the
+ * lower-rank read) into a list of (a, b, I, U) edges (*n_long_edges), and the pairs of two short
+ * reads with the sweep's pair stage into the context's edges and forward degrees (as fslr_query:
+ * fslr_read_stats, reserve and rerun on overflow; then fslr_components).  Syncs.
+ * fslr_get_long_edges: D2H of the long-pair edges (sync); union them into the labels with
+ * fslr_union_pairs + fslr_finalize_labels after fslr_components. */
+int  fslr_set_long_reads(fslr_ctx *ctx, int64_t n_real, const int32_t *vreal, const int32_t *vbase,
+                         const int32_t *rlen, const int32_t *umax, int32_t n_umax);
+int  fslr_long_query(fslr_ctx *ctx, const fslr_params *params, int64_t *n_long_edges);
+int  fslr_get_long_edges(fslr_ctx *ctx, int32_t *a, int32_t *b, int32_t *I, int32_t *U, int64_t capacity);
 
 /* build_index + query(all reads) + components, enqueued back to back.  Async. */
 int  fslr_run(fslr_ctx *ctx, const fslr_params *params);

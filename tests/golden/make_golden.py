@@ -278,9 +278,18 @@ def make_vector(name, n, lmax, seed, **kw):
     print('vector', name, 'edges', len(md), 'components', len(st['subgraphs']), 'max_fwd', int(fwd.max()))
 
 
+def make_longreads():
+    # reads of more than 64 fillings: the device splits them into chunks
+    df, hdr = synth_df(400, 150, 21, lmin=1)
+    make_fixture('longreads_400', df, hdr, note='1-150 fillings: reads beyond the 64-interval chunk width')
+
+
 def main():
     sys.stdout.reconfigure(line_buffering=True)
     refharness.load()
+    if sys.argv[1:] == ['--only', 'longreads_400']:
+        make_longreads()
+        return
     df, hdr = synth_df(1000, 3, 0, lmin=3)
     make_fixture('cfg1_1k_x3', df, hdr, note='BASELINE config 1: 1k reads x 3 fillings, defaults')
     df, hdr = synth_df(2000, 8, 7)
@@ -308,6 +317,7 @@ def main():
     make_fixture('noclusters', df, hdr, note='no edges: "No clusters were found." and no output files')
     df, hdr = synth_df(1500, 6, 19, cluster_cap=40, size_p=1.0 / 14)
     make_fixture('capbind_1500', df, hdr, note='clusters up to 40 reads: edge cap binds (stub-order)')
+    make_longreads()
     make_kats()
     make_vector('v10k_l8_s7', 10_000, 8, 7)
     make_vector('v20k_l16_s11', 20_000, 16, 11)

@@ -141,7 +141,7 @@ def test_cli_matches_reference_outputs(name, io_flag):
         assert ('fslr finished' in res.output) == ('fslr finished' in meta['stdout'])
 
 
-@pytest.mark.parametrize('name', ['cfg1_1k_x3', 'capbind_1500', 'zerodiv', 'noclusters', 'params_a',
+@pytest.mark.parametrize('name', ['cfg1_1k_x3', 'capbind_1500', 'zerodiv', 'noclusters', 'longreads_400', 'params_a',
                                   'edge_cases_p0', 'zipf_800_l64'])
 def test_cli_multi_gpu_matches_reference_outputs(name):
     """``fslr --gpus 2``: two rank processes (sharing this box's one GPU over gloo) run the

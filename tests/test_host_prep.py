@@ -101,3 +101,40 @@ def test_interval_data_from_reference_items_round_trips():
     for f in ('read_off', 'read_qlen2', 'read_nal', 'iv_chrom', 'iv_start', 'iv_end', 'iv_aln', 'data_pos'):
         np.testing.assert_array_equal(getattr(a, f), getattr(b, f))
     assert list(back.qnames[a.read_qcode]) == list(data.qnames[b.read_qcode])
+
+
+def test_split_long_reads_layout():
+    """The virtual CSR of the long-read stage: reads < n keep their first 64
+    intervals, the further chunks follow in rank order, and every interval appears once."""
+    from fslr_amd import synth
+    from fslr_amd.prep import split_long_reads, has_long_reads
+    csr = synth.generate(500, 200, 9, lmin=1).interval_data().csr()
+    assert has_long_reads(csr)
+    v, vreal, vbase, rlen = split_long_reads(csr)
+    n = csr.n_reads
+    np.testing.assert_array_equal(rlen, np.diff(csr.read_off))
+    np.testing.assert_array_equal(vreal[:n], np.arange(n))
+    vl = np.diff(v.read_off)
+    assert vl.min() >= 1 and vl.max() <= 64
+    assert np.all(np.diff(vreal[n:]) >= 0)
+    # every virtual interval maps back to (real read, index) of the real CSR, each exactly once
+    seen = np.zeros(csr.n_intervals, bool)
+    for r in range(v.n_reads):
+        for t in range(vl[r]):
+            k = csr.read_off[vreal[r]] + vbase[r] + t
+            assert not seen[k]
+            seen[k] = True
+            kv = v.read_off[r] + t
+            assert (v.iv_start[kv], v.iv_end[kv], v.data_pos[kv]) == (csr.iv_start[k], csr.iv_end[k], csr.data_pos[k])
+    assert seen.all()
+    np.testing.assert_array_equal(v.read_qlen2, csr.read_qlen2[vreal])
+
+
+def test_umax_table_matches_pass_table():
+    from fslr_amd.prep import pass_table, umax_table
+    for cut in ([1, 1, .66, .66, .66, .5], [0.3], [1.2], [0.0], [0.7, 0.2]):
+        u = umax_table(cut, 64)
+        pt = pass_table(cut).reshape(64, 128)
+        for I in range(1, 65):
+            ok = [U for U in range(I, 129) if pt[I - 1, U - 1]]
+            assert u[I - 1] == min(max(ok) if ok else I - 1, 128)
