@@ -175,6 +175,10 @@ class Context:
         if profiling:
             self._check(self._L.fslr_set_profiling(self._h, 1))
 
+    def set_profiling(self, level: int):
+        """1: per-phase events and the pair-kernel events; 2: the pair-kernel events only; 0: off."""
+        self._check(self._L.fslr_set_profiling(self._h, int(level)))
+
     def close(self):
         if getattr(self, '_h', None):
             self._L.fslr_ctx_destroy(self._h)
@@ -340,6 +344,8 @@ class Context:
             grow = False
             if st['overflow_flags'] & 4:
                 engine = 'walk'
+                grow = True
+            if st['overflow_flags'] & 24:         # sweep entry buffers (a sync-free repeat query): rerun
                 grow = True
             if st['n_edges'] > st['edge_capacity']:
                 self.reserve_edges(int(st['n_edges'] * 1.25) + 4096)

@@ -190,6 +190,26 @@ void parallel_for(int n, F&& f) {
   for (auto& x : th) x.join();
 }
 
+// f(tid, begin, end) over [0, n) in `nth` contiguous ranges, one thread each (range k = thread k)
+template <typename F>
+void parallel_ranges(int64_t n, int nth, F&& f) {
+  if (nth <= 1) {
+    f(0, int64_t(0), n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int k = 0; k < nth; ++k) {
+    const int64_t b = n * k / nth, e = n * (k + 1) / nth;
+    th.emplace_back([&f, k, b, e] { f(k, b, e); });
+  }
+  for (auto& x : th) x.join();
+}
+
+int host_threads(int64_t work) {
+  const int hw = static_cast<int>(std::max(1u, std::thread::hardware_concurrency()));
+  return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>({hw, 16, work / (1 << 16)})));
+}
+
 }  // namespace
 
 extern "C" int fslr_apply_edge_cap(fslr_ctx* c, int32_t thr, fslr_cap_stats* out) {
@@ -241,17 +261,31 @@ extern "C" int fslr_apply_edge_cap(fslr_ctx* c, int32_t thr, fslr_cap_stats* out
   }
   HIP_TRY(c, hipStreamSynchronize(c->stream));
 
-  // forward adjacency of E* (edges are (a, b), a < b, from the pair kernels)
+  // forward adjacency of E* (edges are (a, b), a < b, from the pair kernels); rows are filled by
+  // several threads, so a row's order is arbitrary (the closure below only counts over rows)
+  const int nth_e = host_threads(ne);
   std::vector<int64_t> aoff(static_cast<size_t>(n) + 1, 0);
-  for (const int2& e : edges) {
-    if (e.x >= e.y || e.x < 0 || e.y >= n) return fail(c, FSLR_ERR_STATE, "edge list is not E* (a < b)");
-    ++aoff[e.x + 1];
-  }
+  std::vector<char> bad(static_cast<size_t>(nth_e), 0);
+  parallel_ranges(ne, nth_e, [&](int tid, int64_t b, int64_t e) {
+    for (int64_t k = b; k < e; ++k) {
+      const int2 ed = edges[k];
+      if (ed.x >= ed.y || ed.x < 0 || ed.y >= n) {
+        bad[tid] = 1;
+        return;
+      }
+      __atomic_fetch_add(&aoff[ed.x + 1], 1, __ATOMIC_RELAXED);
+    }
+  });
+  for (char b : bad)
+    if (b) return fail(c, FSLR_ERR_STATE, "edge list is not E* (a < b)");
   for (int64_t x = 0; x < n; ++x) aoff[x + 1] += aoff[x];
   std::vector<int> adj(static_cast<size_t>(ne));
   {
     std::vector<int64_t> fill(aoff.begin(), aoff.end() - 1);
-    for (const int2& e : edges) adj[fill[e.x]++] = e.y;
+    parallel_ranges(ne, nth_e, [&](int, int64_t b, int64_t e) {
+      for (int64_t k = b; k < e; ++k)
+        adj[__atomic_fetch_add(&fill[edges[k].x], 1, __ATOMIC_RELAXED)] = edges[k].y;
+    });
   }
   stage("D2H fwd + edges, adjacency");
   // 1. candidate readers T (closure bound, rank order)
@@ -427,25 +461,48 @@ extern "C" int fslr_apply_edge_cap(fslr_ctx* c, int32_t thr, fslr_cap_stats* out
 
   stage("replay loops");
   // E* pair (a, b) is an edge iff a's loop or, failing that, b's loop reaches it
-  std::vector<int2> kept;
-  std::vector<unsigned short> kept_iu;
-  kept.reserve(edges.size());
-  kept_iu.reserve(edges.size());
+  // (in parallel: per-range codes and counts, then each range compacts at its scanned offset, so the
+  // kept edges stay in E* order)
+  std::vector<unsigned char> who(static_cast<size_t>(ne));          // 0 a's loop, 1 b's loop, 2 none
+  std::vector<int64_t> rkept(static_cast<size_t>(nth_e) + 1, 0), rdrop(static_cast<size_t>(nth_e), 0),
+      rback(static_cast<size_t>(nth_e), 0);
   std::vector<int> formed(static_cast<size_t>(n), 0);
-  for (int64_t k = 0; k < ne; ++k) {
-    const int a = edges[k].x, b = edges[k].y;
-    int former = -1;
-    if (!broke[a] || reached_by(a, b)) former = a;
-    else if (!broke[b] || reached_by(b, a)) former = b;
-    if (former < 0) {
-      ++cs.dropped;
-      continue;
+  parallel_ranges(ne, nth_e, [&](int tid, int64_t b0, int64_t e0) {
+    int64_t kc = 0, dc = 0, bc = 0;
+    for (int64_t k = b0; k < e0; ++k) {
+      const int a = edges[k].x, b = edges[k].y;
+      unsigned char w = 2;
+      if (!broke[a] || reached_by(a, b)) w = 0;
+      else if (!broke[b] || reached_by(b, a)) w = 1;
+      who[k] = w;
+      if (w == 2) {
+        ++dc;
+        continue;
+      }
+      ++kc;
+      bc += w;
+      __atomic_fetch_add(&formed[w == 0 ? a : b], 1, __ATOMIC_RELAXED);
     }
-    if (former == b) ++cs.backward;
-    ++formed[former];
-    kept.push_back(former == a ? make_int2(a, b) : make_int2(b, a));
-    kept_iu.push_back(iu[k]);
+    rkept[tid + 1] = kc;
+    rdrop[tid] = dc;
+    rback[tid] = bc;
+  });
+  for (int k = 0; k < nth_e; ++k) {
+    rkept[k + 1] += rkept[k];
+    cs.dropped += rdrop[k];
+    cs.backward += rback[k];
   }
+  std::vector<int2> kept(static_cast<size_t>(rkept[nth_e]));
+  std::vector<unsigned short> kept_iu(kept.size());
+  parallel_ranges(ne, nth_e, [&](int tid, int64_t b0, int64_t e0) {
+    int64_t w = rkept[tid];
+    for (int64_t k = b0; k < e0; ++k) {
+      if (who[k] == 2) continue;
+      const int a = edges[k].x, b = edges[k].y;
+      kept[w] = who[k] == 0 ? make_int2(a, b) : make_int2(b, a);
+      kept_iu[w++] = iu[k];
+    }
+  });
   int max_fwd = 0;
   for (int64_t x = 0; x < n; ++x) {
     if (in_t[x] && formed[x] != own_edges[t_of[x]])

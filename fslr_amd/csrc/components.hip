@@ -10,6 +10,8 @@
 // older ancestor.  Only the hook is a coherent agent-scope CAS; when it fails, its returned value
 // (the fresh parent of the would-be root) continues the walk, so every retry moves strictly up
 // the tree and the loop ends.  Kernel boundaries make the final forest visible to finalize.
+#include <algorithm>
+
 #include "kernels.hpp"
 
 namespace fslr {
@@ -105,6 +107,21 @@ __global__ void k_uf_finalize(int* p, int n) {
 }
 
 }  // namespace
+
+// one launch instead of three fills per query: counters, error words and forward degrees to 0
+__global__ void k_query_reset(unsigned long long* __restrict__ counters, int nc, int* __restrict__ err, int ne,
+                              int* __restrict__ fwd, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nc) counters[i] = 0ull;
+  if (i < ne) err[i] = 0;
+  for (int k = i; k < n; k += gridDim.x * blockDim.x) fwd[k] = 0;
+}
+
+hipError_t launch_query_reset(unsigned long long* counters, int nc, int* err, int ne, int* fwd, int n, hipStream_t s) {
+  const long long work = std::max<long long>(std::max(nc, ne), n);
+  k_query_reset<<<grid_for(work), 256, 0, s>>>(counters, nc, err, ne, fwd, n);
+  return hipGetLastError();
+}
 
 hipError_t launch_uf_init(int* parent, int n, hipStream_t s) {
   if (n > 0) k_uf_init<<<grid_for(n), 256, 0, s>>>(parent, n);

@@ -86,6 +86,14 @@ struct fslr_ctx {
   void* sweep_temp = nullptr;
   size_t sweep_temp_bytes = 0;
   bool any_zero_aln = false;                // an aln_size == 0 interval: the walk engine replays it
+  // sync-free repeat query: a full one-pass sweep query on unchanged input (same reads, thresholds,
+  // filter, parameters) has the previous query's entry count, so the host need not read it back
+  uint64_t input_gen = 1;                   // bumped by set_reads / set_thresholds / set_chrom_filter / set_shard
+  uint64_t sw_prev_gen = 0;                 // input_gen of the last synchronous sweep query (0: none)
+  double sw_prev_q = 0, sw_prev_nc = 0;
+  std::vector<int> sw_prev_umax;
+  int64_t sw_prev_a0 = -1, sw_prev_a1 = -1, sw_prev_n = 0;
+  bool sw_fast_used = false;                // the last query ran sync-free
   int last_engine = FSLR_ENGINE_WALK;
   int* thr_tmp = nullptr;
   int64_t cap_n = 0, cap_ni = 0, cap_chroms = 0;
@@ -120,7 +128,8 @@ struct fslr_ctx {
   int64_t lg_ent_cap = 0, lg_short_cap = 0;
   size_t lg_temp_bytes = 0;
   // profiling
-  bool profiling = false;
+  bool profiling = false;                  // the pair-kernel event ring (fslr_set_profiling 1 or 2)
+  bool prof_phases = false;                // per-phase events too (fslr_set_profiling 1)
   hipEvent_t ev[8] = {};
   // (profiling) a ring of event pairs around the main pair-kernel launch of the last kKernRing queries
   static constexpr int kKernRing = 256;

@@ -44,6 +44,7 @@ enum Counter { kEdgeCount = 0,          // atomic (own 128-B line)
                kQueueStride = 16,
                kQueueBase2 = kQueueBase + 8 * kQueueStride,   // the partitioned launch's queues
                kSwTests = kQueueBase2 + 8 * kQueueStride,     // sweep: interval pairs tested
+               kSwNdev = kSwTests + 8,                        // sweep: entry count for the kernels (sync-free query)
                kNumCounters = kSwTests + 16 };
 // per-wave statistics of query_kernel: fields 0..8 (sum, except kWsMaxFwd: max; kWsWalked: index
 // records walked, every pass counted), then (section-
@@ -169,7 +170,9 @@ struct SweepArgs {
   unsigned long long* ent_sorted;     // [n_ent] grouped by A
   unsigned long long* ent_mid;        // (mode 3) [n_ent] grouping scratch
   int* grp;                           // [grp_ints()] grouping-sort bucket counts / offsets (null: radix sort)
-  long long n_ent;                    // (emit / pairs) entries of the count pass
+  long long n_ent;                    // (emit / pairs) entries of the count pass (host; with n_dev: an estimate)
+  const long long* n_dev;             // null, or the device word holding the count (sync-free repeat query)
+  long long ent_cap;                  // capacity of ent / ent_sorted (grouping-sort scatter bound)
   void* temp;                         // hipcub scratch (tile scan, grouping sort)
   size_t temp_bytes;
   int2* edges;
@@ -189,7 +192,8 @@ int sweep_max_waves();
 hipError_t launch_sweep_plan(const SweepArgs& a, hipStream_t s);
 // mode 2: the one-pass sweep (entries to ent_ub); mode 0: the count pass of the two-pass fallback.
 // Then the tile scan; total_dev[0..2] = entries, upper-bound total, overflow flags (read after a sync)
-hipError_t launch_sweep_count(const SweepArgs& a, int mode, long long* total_dev, hipStream_t s);
+hipError_t launch_sweep_count(const SweepArgs& a, int mode, long long* total_dev, hipStream_t s,
+                              long long* n_dev = nullptr, long long cap = -1);
 // packs (mode 2) or writes (mode 0: emit pass) the entries to `ent` (mode 3: they are there), groups
 // them by A, evaluates the pairs
 hipError_t launch_sweep_pairs(const SweepArgs& a, int mode, hipStream_t s);
@@ -223,6 +227,8 @@ hipError_t launch_eval_pairs(const int2* pairs, long long n, const int4* rmeta, 
 
 // ---- components (components.hip) ---------------------------------------------------------
 hipError_t launch_uf_init(int* parent, int n, hipStream_t s);
+// counters[0, nc), err[0, ne) and fwd[0, n) to zero in one launch (start of a query)
+hipError_t launch_query_reset(unsigned long long* counters, int nc, int* err, int ne, int* fwd, int n, hipStream_t s);
 // count > cap (edges were lost) sets err[kErrOverflow]
 hipError_t launch_uf_edges(int* parent, const int2* edges, const unsigned long long* count, long long cap, int* err,
                            hipStream_t s);

@@ -258,13 +258,20 @@ __global__ __launch_bounds__(256) void k_sum_slots(const unsigned long long* __r
 }
 
 // entries of the count pass: last tile offset + last tile count; (one-pass) also the upper-bound
-// total and the overflow flag, for the host
+// total and the overflow flag, for the host.  n_dev (sync-free repeat query): the count for the
+// grouping and pair kernels, clamped to the entry capacity cap (flag 16 when it did not fit: the
+// query is then refused and rerun with a sync)
 __global__ void k_total(const long long* __restrict__ off, const long long* __restrict__ cnt,
-                        const long long* __restrict__ ub, const long long* __restrict__ tests, const int* err, int nt,
-                        long long* total) {
+                        const long long* __restrict__ ub, const long long* __restrict__ tests, int* err, int nt,
+                        long long* total, long long* n_dev, long long cap) {
   if (threadIdx.x == 0) {
-    total[0] = off[nt - 1] + cnt[nt - 1];
+    const long long t = off[nt - 1] + cnt[nt - 1];
+    total[0] = t;
     total[1] = ub ? ub[nt - 1] + tests[nt - 1] : 0;
+    if (n_dev) {
+      n_dev[0] = t < cap ? t : cap;
+      if (t > cap) atomicOr(&err[kErrOverflow], 16);
+    }
     total[2] = err ? err[kErrOverflow] : 0;
   }
 }
@@ -332,7 +339,7 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
   EdgeStageN<kEdgeStage> es{es_all[wv], 0};
   const EdgeOut eo{g.edges, g.edge_iu, g.edge_cap, &g.counters[kEdgeCount]};
   const int umax_v = g.umax[lane];
-  const long long n = g.n_ent;
+  const long long n = g.n_dev ? *g.n_dev : g.n_ent;
   const unsigned long long* E = g.ent_sorted;
   const long long nchunks = (n + kChunk2 - 1) / kChunk2;
   const long long nw = static_cast<long long>(gridDim.x) * kSwWaves;
@@ -776,17 +783,19 @@ __global__ __launch_bounds__(kMsdThreads) void k_msd_pass1(const unsigned long l
 }
 
 // one workgroup per bucket: group [off[b P], off[(b + 1) P]) by A >> hb into dst
-__global__ __launch_bounds__(256) void k_msd_pass2(const unsigned long long* __restrict__ src, long long n,
+__global__ __launch_bounds__(256) void k_msd_pass2(const unsigned long long* __restrict__ src, long long n_host,
+                                                   const long long* __restrict__ n_dev,
                                                    const int* __restrict__ off, int P, int H, int hb, int lo_bits,
                                                    unsigned long long* __restrict__ dst) {
+  const long long n = n_dev ? *n_dev : n_host;
   __shared__ int hist[kMsdMaxLo];
   __shared__ int wsum[4];
   const int tid = threadIdx.x;
   const int lane = tid & (kWave - 1), w = tid >> 6;
   const int nb = 1 << lo_bits;
   const int b = blockIdx.x;
-  const long long s = off[static_cast<long long>(b) * P];
-  const long long e = b + 1 < H ? off[static_cast<long long>(b + 1) * P] : n;
+  const long long s = min(static_cast<long long>(off[static_cast<long long>(b) * P]), n);
+  const long long e = b + 1 < H ? min(static_cast<long long>(off[static_cast<long long>(b + 1) * P]), n) : n;
   if (e - s <= 1) {
     if (tid == 0 && e > s) dst[s] = src[s];
     return;
@@ -898,7 +907,8 @@ hipError_t launch_sweep_plan(const SweepArgs& a, hipStream_t s) {
   return hipcub::DeviceScan::ExclusiveSum(a.temp, tb, a.tile_tests, a.tile_ub, nt, s);
 }
 
-hipError_t launch_sweep_count(const SweepArgs& a, int mode, long long* total_dev, hipStream_t s) {
+hipError_t launch_sweep_count(const SweepArgs& a, int mode, long long* total_dev, hipStream_t s, long long* n_dev,
+                              long long cap) {
   const int nt = tiles_of(a);
   if (nt == 0) return hipMemsetAsync(total_dev, 0, 3 * sizeof(long long), s);
   const int blocks = std::min(blocks_mode(mode), (nt + kSwWaves - 1) / kSwWaves);
@@ -915,7 +925,8 @@ hipError_t launch_sweep_count(const SweepArgs& a, int mode, long long* total_dev
   size_t tb = a.temp_bytes;
   hipError_t e = hipcub::DeviceScan::ExclusiveSum(a.temp, tb, a.tile_cnt, a.tile_off, nt, s);
   if (e != hipSuccess) return e;
-  k_total<<<1, 64, 0, s>>>(a.tile_off, a.tile_cnt, mode == 2 ? a.tile_ub : nullptr, a.tile_tests, a.err, nt, total_dev);
+  k_total<<<1, 64, 0, s>>>(a.tile_off, a.tile_cnt, mode == 2 ? a.tile_ub : nullptr, a.tile_tests, a.err, nt, total_dev,
+                           n_dev, cap);
   return hipGetLastError();
 }
 
@@ -959,11 +970,12 @@ static hipError_t group_by_a(const SweepArgs& a, int mode, const unsigned long l
   hipError_t e = hipcub::DeviceScan::ExclusiveSum(a.temp, tb, mat, off, H * P, s);
   if (e != hipSuccess) return e;
   if (mode == 2) {
-    k_msd_pass1<true, true><<<P, kMsdThreads, 0, s>>>(a.ent_ub, a.ub_cap, a.tile_ub, a.tile_cnt, nt, lo, H, off, mid);
+    k_msd_pass1<true, true><<<P, kMsdThreads, 0, s>>>(a.ent_ub, a.ub_cap, a.tile_ub, a.tile_cnt, nt, lo, H, off, mid,
+                                                      a.n_dev ? a.ent_cap : 0x7FFFFFFFFFFFFFFFll);
   } else {
     k_msd_pass1<false, true><<<P, kMsdThreads, 0, s>>>(src, n, nullptr, nullptr, 0, lo, H, off, mid);
   }
-  k_msd_pass2<<<H, 256, 0, s>>>(mid, n, off, P, H, hb, lo, out);
+  k_msd_pass2<<<H, 256, 0, s>>>(mid, n, mode == 2 ? a.n_dev : nullptr, off, P, H, hb, lo, out);
   return hipGetLastError();
 }
 

@@ -139,7 +139,8 @@ typedef struct {
     int64_t edge_capacity;         /* edge buffer capacity; n_edges > capacity ⇒ reserve + rerun */
     int64_t walked_records;        /* index records the pair kernels walked (every partner-partition pass) */
     int32_t engine;                /* FSLR_ENGINE_WALK or FSLR_ENGINE_SWEEP: the engine that ran */
-    int32_t overflow_flags;        /* 1 deferred list, 2 edge buffer, 4 sweep partner table (rerun with WALK) */
+    int32_t overflow_flags;        /* 1 deferred list, 2 edge buffer, 4 sweep partner table (rerun with WALK),
+                                      8 | 16 sweep entry buffers (rerun) */
     int64_t pair_tests;            /* SWEEP: overlapping interval pairs tested (each pair once) */
     int64_t entry_capacity;        /* SWEEP: match-entry buffer (grown automatically) */
 } fslr_query_stats;
@@ -174,7 +175,9 @@ const char *fslr_last_error(const fslr_ctx *ctx);
 /* device: HIP ordinal; stream: hipStream_t to launch on (NULL = the library creates one). */
 int  fslr_ctx_create(int device, void *stream, fslr_ctx **out);
 void fslr_ctx_destroy(fslr_ctx *ctx);
-int  fslr_set_profiling(fslr_ctx *ctx, int enable);     /* hipEvent timing per phase */
+int  fslr_set_profiling(fslr_ctx *ctx, int enable);     /* 1: hipEvents per phase + around the pair kernel;
+                                                           2: around the pair kernel only (fewer stream
+                                                           markers in a timed loop); 0: off */
 
 /* Copy the CSR (host pointers) into context-owned HBM buffers (H2D). */
 int  fslr_set_reads(fslr_ctx *ctx, const fslr_reads *reads);

@@ -89,9 +89,9 @@ def main():
     st = ctx.stats()
     tm = ctx.timings()
     log(f'device step {ms:.2f} ms, {st["evaluated_pairs"]} evaluated pairs, {st["n_edges"]} edges')
-    log(json.dumps({'stats': {k: int(v) for k, v in st.items()}, 'timings': tm}))
+    log(json.dumps({'stats': {k: (v if isinstance(v, str) else int(v)) for k, v in st.items()}, 'timings': tm}))
     if args.sample <= 0:
-        print(json.dumps({'ms_per_step': ms, 'stats': {k: int(v) for k, v in st.items()}, 'timings': tm}))
+        print(json.dumps({'ms_per_step': ms, 'stats': {k: (v if isinstance(v, str) else int(v)) for k, v in st.items()}, 'timings': tm}))
         return 0
 
     # the reference's edge cap on the full query (it binds at this density): replay cost
