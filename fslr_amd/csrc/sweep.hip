@@ -641,11 +641,20 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
 // its locality); inside a run the order is free (k_sweep_pairs hashes the partners).
 // Two reads and one write per pass; pass 1 reads the sweep's upper-bound tile slots (no packing).
 constexpr int kMsdMaxBlocks = 1024;       // pass-1 workgroups (at most)
-constexpr int kMsdThreads = 1024;
+#ifndef FSLR_MSD_THREADS
+#define FSLR_MSD_THREADS 1024
+#endif
+#ifndef FSLR_MSD_HBMAX
+#define FSLR_MSD_HBMAX 13
+#endif
+#ifndef FSLR_MSD_UNROLL
+#define FSLR_MSD_UNROLL 8
+#endif
+constexpr int kMsdThreads = FSLR_MSD_THREADS;
 constexpr int kMsdMaxH = 8192;             // buckets (LDS histogram of pass 1)
 constexpr int kMsdMaxLo = 4096;            // in-bucket bins (LDS histogram of pass 2)
 constexpr int kGrpInts = 2 * (1 << 21);    // [bucket][block] counts and their scan (H P <= 2^21)
-constexpr int kMsdUnroll = 8;              // entries loaded per lane before their atomics
+constexpr int kMsdUnroll = FSLR_MSD_UNROLL;  // entries loaded per lane before their atomics
 
 // One wave-instruction of keys (lanes with `act`, a contiguous prefix): equal keys on adjacent lanes
 // form runs; the run's first lane adds its length to bin[key] (returning the base when `ret`), every
@@ -953,7 +962,7 @@ static hipError_t group_by_a(const SweepArgs& a, int mode, const unsigned long l
   // H = 2^hb buckets of ~4096 entries; P pass-1 workgroups with H P <= kGrpInts / 2 (pass 1 is
   // latency bound, so it wants waves in flight more than wide per-block histograms)
   int hb = 0;
-  while (hb < 13 && (n >> (12 + hb)) > 0) ++hb;
+  while (hb < FSLR_MSD_HBMAX && (n >> (12 + hb)) > 0) ++hb;
   hb = std::max(hb, nbits - 12);                            // low digit <= 12 bits (LDS bins)
   hb = std::min(hb, nbits);
   const int H = 1 << hb, lo = nbits - hb;

@@ -239,10 +239,11 @@ class SweepShard:
             ctx.sweep_evaluate(qlen_cut, nal_cut, pass_table, entries, n_recv, edge_threshold)
             st = ctx.stats(check=False)
         err = None
-        try:
-            ctx.stats()                                 # raises on a device-side error (ZeroDivisionError)
-        except Exception as e:                          # noqa: BLE001 - re-raised on every rank below
-            err = e
+        if st.get('error', 1) or st.get('overflow_flags', 1):   # only then read the stats again for the error
+            try:
+                ctx.stats()                             # raises on a device-side error (ZeroDivisionError)
+            except Exception as e:                      # noqa: BLE001 - re-raised on every rank below
+                err = e
         mf = int(st['max_fwd'])
         max_ne = int(st['n_edges'])
         if W > 1:

@@ -8,6 +8,6 @@ O=$R/gpurun_out/$TAG
 mkdir -p $O
 for v in "$@"; do
   lib=$R/fslr_amd/libfslr_hip${v:+_$v}.so
-  FSLR_LIB=$lib timeout -k 10 200 python $R/bench.py --cpu-sample-reads 0 > $O/bench_${v:-default}.json 2> $O/bench_${v:-default}.log
-  python -c "import json,sys; d=json.load(open('$O/bench_${v:-default}.json')); print('%-14s ms/step %.4f  query %.4f  index %.4f' % ('${v:-default}', d['ms_per_step'], d['roofline']['kernel_ms'], d['roofline']['phase_ms_last_step']['index_ms']))"
+  FSLR_LIB=$lib timeout -k 10 200 python $R/bench.py --cpu-sample-stride 0 --steps 20 > $O/bench_${v:-default}.json 2> $O/bench_${v:-default}.log
+  python -c "import json,sys; d=json.load(open('$O/bench_${v:-default}.json')); p=d['roofline']['phase_ms_last_step']; print('%-8s ms/step %.4f sweep %.4f sort %.4f pairs %.4f' % ('${v:-default}', d['ms_per_step'], d['roofline']['kernel_ms'], p['sweep_sort_ms'], p['sweep_pairs_ms']))"
 done
