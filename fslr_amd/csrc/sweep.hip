@@ -38,7 +38,10 @@ constexpr int kSwWaves = 4;
 constexpr int kSwBlock = kSwWaves * kWave;
 constexpr int kPairLimit = 160;            // long runs: insert while partners < limit (+64 per step < 256)
 constexpr int kPerPass = 80;               // entries per partner partition of a long run
-constexpr int kEdgeStage = 256;            // staged edges per wave
+#ifndef FSLR_EDGE_STAGE
+#define FSLR_EDGE_STAGE 256
+#endif
+constexpr int kEdgeStage = FSLR_EDGE_STAGE;  // staged edges per wave
 constexpr int kWsFields = 4;               // per-wave statistics slots
 
 __device__ __forceinline__ int entry_a(unsigned long long e) { return static_cast<int>(e >> 39); }
