@@ -353,6 +353,22 @@ def main():
             },
             'cpu_baseline': cpu,
         }
+        if world == 1 and st['engine'] == 'sweep' and lib_t and lib_t.get('sweep_pairs_ms'):
+            # the pair stage is the longest kernel at cfg3 (rocprof: k_sweep_pairs ~0.31 ms vs k_sweep<2>
+            # ~0.245 ms): its roofline too, from the untimed phase step's events (k_sweep_pairs + the
+            # 5-us statistics reduction after it); bytes: every grouped entry read once + each edge
+            # written (8 + 2 B) — a lower bound (per-read headers and forward degrees left out)
+            pb = B_ENT * sw['match_entries'] + 10 * st['n_edges']
+            pms = float(lib_t['sweep_pairs_ms'])
+            out['roofline_pair_stage'] = {
+                'bound': 'hbm', 'kernel': 'k_sweep_pairs', 'kernel_ms': pms,
+                'achieved': pb / (pms / 1000.0) / 1e9, 'peak': HBM_PEAK / 1e9, 'unit': 'GB/s',
+                'frac': pb / (pms / 1000.0) / HBM_PEAK, 'algo_bytes_per_launch': int(pb),
+                'algo_bytes_model': f'{B_ENT} B x grouped match entries read ({sw["match_entries"]}) + 10 B x edges '
+                                    f'written ({st["n_edges"]}); a lower bound',
+                'note': 'LDS- and latency-bound (an LDS hash per 128-entry stage, 3 waves/SIMD by LDS, one '
+                        'edge counter): DESIGN.md §3.6',
+            }
         if verified is not None:
             out['verified_labels_vs_single_context'] = verified
         print(json.dumps(out), flush=True)
