@@ -156,6 +156,14 @@ def _ptr(a: np.ndarray):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
+_contexts_created = False
+
+
+def contexts_created() -> bool:
+    """True once this process created a Context (the library's HIP runtime is initialised)."""
+    return _contexts_created
+
+
 class Context:
     """One HIP device context (library-owned HBM buffers + a stream)."""
 
@@ -168,6 +176,8 @@ class Context:
         if rc != FSLR_OK:
             raise HipUnavailable(f'fslr_ctx_create(device={device}) failed (rc={rc}): no usable HIP device')
         self._h = h
+        global _contexts_created
+        _contexts_created = True
         self.device = device
         self.n_reads = 0
         self.edge_capacity = 0

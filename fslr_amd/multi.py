@@ -124,7 +124,22 @@ def _child(d: str, rank: int, world: int, port: int) -> int:
     a, b, I, U = out['edges']
     np.save(os.path.join(d, f'edges{rank}.npy'), np.stack([a, b, I, U]).astype(np.int32))
     np.save(os.path.join(d, f'fwd{rank}.npy'), out['fwd'])
+    if rank == 0:                                  # rank 0 run as a child: the caller's view too
+        np.save(os.path.join(d, 'labels0.npy'), np.asarray(out['labels'], np.int32))
+        with open(os.path.join(d, 'rank0.json'), 'w') as fh:
+            json.dump({k: out[k] for k in out if k not in ('edges', 'fwd', 'labels')}, fh, default=int)
     return 0
+
+
+def _rank0_in_process() -> bool:
+    """Rank 0 runs in the calling process unless this library's HIP runtime is already up in it while
+    torch's is not: torch bundles its own HIP runtime, which then finds no device (the reverse order
+    works), so rank 0 becomes a child process like the others."""
+    from . import _lib
+    if not _lib.contexts_created():
+        return True
+    t = sys.modules.get('torch')
+    return bool(t is not None and t.cuda.is_initialized())
 
 
 def query(csr, iv_thr, qlen_cut, nal_cut, pass_table, edge_threshold, n_gpus, first_device=0,
@@ -145,15 +160,24 @@ def query(csr, iv_thr, qlen_cut, nal_cut, pass_table, edge_threshold, n_gpus, fi
         env = dict(os.environ, MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
         pkg_root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
         env['PYTHONPATH'] = pkg_root + (os.pathsep + env['PYTHONPATH'] if env.get('PYTHONPATH') else '')
-        for r in range(1, world):
+        in_proc = _rank0_in_process()
+        for r in range(0 if not in_proc else 1, world):
             procs.append(subprocess.Popen([sys.executable, '-m', 'fslr_amd.multi', d, str(r), str(world), str(port)],
                                           env=env))
-        out = _rank_main(d, 0, world, port)
+        out = _rank_main(d, 0, world, port) if in_proc else None
         deadline = time.monotonic() + timeout_s
-        for r, p in enumerate(procs, start=1):
+        for k, p in enumerate(procs):
+            r = k + (1 if in_proc else 0)
             rc = p.wait(timeout=max(1.0, deadline - time.monotonic()))
             if rc != 0:
                 raise RuntimeError(f'multi-GPU rank {r} exited with status {rc}')
+        if out is None:
+            with open(os.path.join(d, 'rank0.json')) as fh:
+                out = json.load(fh)
+            out['labels'] = np.load(os.path.join(d, 'labels0.npy'))
+            e = np.load(os.path.join(d, 'edges0.npy'))
+            out['edges'] = tuple(e[k] for k in range(4))
+            out['fwd'] = np.load(os.path.join(d, 'fwd0.npy'))
         parts = [out['edges']]
         fwd = out['fwd'].astype(np.int64)
         for r in range(1, world):
