@@ -13,7 +13,7 @@ import numpy as np
 
 LIB_PATH = os.environ.get('FSLR_LIB') or os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libfslr_hip.so')
 
-ABI_VERSION = 6          # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
+ABI_VERSION = 7          # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
 FSLR_OK, FSLR_ERR_ZERO_DIVISION, FSLR_ERR_INVALID, FSLR_ERR_HIP, FSLR_ERR_NOMEM, FSLR_ERR_STATE = range(6)
 FSLR_MAX_L = 64
 FSLR_MAX_READS = 1 << 25
@@ -33,7 +33,8 @@ EXPORTED = ['fslr_abi_version', 'fslr_last_error', 'fslr_ctx_create', 'fslr_ctx_
             'fslr_copy_fwd_device', 'fslr_union_pairs', 'fslr_finalize_labels', 'fslr_apply_edge_cap',
             'fslr_get_pair_kernel_times', 'fslr_set_chrom_filter', 'fslr_sweep_partition', 'fslr_sweep_evaluate',
             'fslr_copy_edges_device', 'fslr_components_from_pairs', 'fslr_set_long_reads', 'fslr_long_query',
-            'fslr_get_long_edges']
+            'fslr_get_long_edges', 'fslr_copy_edges_iu_device', 'fslr_cap_install_edges', 'fslr_cap_local',
+            'fslr_cap_copy_local', 'fslr_cap_replay']
 
 
 class HipUnavailable(RuntimeError):
@@ -141,6 +142,11 @@ def load(path: str = LIB_PATH):
         'fslr_set_long_reads': (ctypes.c_int, [vp, i64, vp, vp, vp, vp, i32]),
         'fslr_long_query': (ctypes.c_int, [vp, ctypes.POINTER(Params), ctypes.POINTER(ctypes.c_int64)]),
         'fslr_get_long_edges': (ctypes.c_int, [vp, vp, vp, vp, vp, i64]),
+        'fslr_copy_edges_iu_device': (ctypes.c_int, [vp, vp, i64]),
+        'fslr_cap_install_edges': (ctypes.c_int, [vp, vp, i64]),
+        'fslr_cap_local': (ctypes.c_int, [vp, i32, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
+        'fslr_cap_copy_local': (ctypes.c_int, [vp, vp, vp]),
+        'fslr_cap_replay': (ctypes.c_int, [vp, vp, vp, i64, i32, ctypes.POINTER(CapStats)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -318,6 +324,36 @@ class Context:
         """Replay the reference's per-read edge cap (cluster.py:223-224) on the last full query."""
         cs = CapStats()
         self._check(self._L.fslr_apply_edge_cap(self._h, int(edge_threshold), ctypes.byref(cs)))
+        return cs.as_dict()
+
+    # -- multi-GPU edge cap (fslr_hip.h fslr_cap_*) ------------------------------------------------
+    def edges_iu_into(self, t, n_pad: int):
+        """This context's edges as int32 rows {a, b, I | U << 8, 0} into the device tensor ``t`` (at least
+        4 * n_pad int32), padded with a = -1 (async)."""
+        assert t.numel() * t.element_size() >= 16 * n_pad
+        self._check(self._L.fslr_copy_edges_iu_device(self._h, ctypes.c_void_p(t.data_ptr()), int(n_pad)))
+
+    def cap_install_edges(self, t, n_rows: int):
+        """The gathered E* rows (device tensor, a < 0 = padding) become this context's edges."""
+        self._check(self._L.fslr_cap_install_edges(self._h, ctypes.c_void_p(t.data_ptr()) if n_rows else None,
+                                                   int(n_rows)))
+
+    def cap_local(self, edge_threshold=10):
+        """Candidates and the search-ordered hits of the candidate intervals this index holds:
+        returns (n_ti, n_hits)."""
+        nti, nh = ctypes.c_int64(0), ctypes.c_int64(0)
+        self._check(self._L.fslr_cap_local(self._h, int(edge_threshold), ctypes.byref(nti), ctypes.byref(nh)))
+        return int(nti.value), int(nh.value)
+
+    def cap_copy_local(self, counts, hits):
+        self._check(self._L.fslr_cap_copy_local(self._h, ctypes.c_void_p(counts.data_ptr()),
+                                                ctypes.c_void_p(hits.data_ptr())))
+
+    def cap_replay(self, counts, hits, pad: int, world: int) -> dict:
+        cs = CapStats()
+        self._check(self._L.fslr_cap_replay(self._h, ctypes.c_void_p(counts.data_ptr()),
+                                            ctypes.c_void_p(hits.data_ptr()), int(pad), int(world),
+                                            ctypes.byref(cs)))
         return cs.as_dict()
 
     def components(self):

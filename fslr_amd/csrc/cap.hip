@@ -1,4 +1,4 @@
-// cap.hip — the reference's per-query-read edge cap, replayed exactly (cluster.py:197-224).
+// cap.hip — the reference's per-query-read edge cap, replayed exactly on the device (cluster.py:197-224).
 //
 // The reference's driver walks the reads in rank order; read x's loop visits, interval by
 // interval (its `data` order), the superintervals hits of that interval (cluster.py:201) and
@@ -9,101 +9,307 @@
 //   interval still visits hits up to the next pair that passes the gate with I > 0.
 // The pair kernels compute E* (every candidate pair evaluated).  E* is the reference's graph
 // whenever no read has more than edge_threshold forward E* partners.  When one
-// does, fslr_apply_edge_cap replays the reference's loops on the host for the reads that can
-// reach the cap and rewrites the device edge list:
-//   1. candidates T: in rank order, x joins T when fwd(x) + #{y in T, y < x, (y, x) in E*} >=
-//      edge_threshold.  A read's loop breaks only if its edge count reaches the cap; the edges it
-//      can form are its forward E* pairs plus E* pairs (y, x) that an earlier *breaking* read y
-//      left unseen, so T contains every read that breaks.
-//   2. k_hit_emit lists every hit of every interval of the reads in T from the device index (the
-//      same end-inclusive overlaps the pair kernel walks); the host orders each interval's hits
-//      the way the search returns them (descending (start, -end, data position) — the order of
-//      the superintervals stand-in the golden fixtures were generated with; the library's own
-//      order is undocumented, SURVEY.md §8c: parity is pinned to that stand-in order).
-//   3. k_eval_pairs evaluates every distinct pair of those hit lists with the full predicate.
-//   4. the host replays the loops of T in rank order; a pair (y, x), y < x, is unseen at x's loop
-//      iff y broke before reaching it.  An E* pair is an edge iff the loop of its lower-rank read
-//      or, failing that, of its higher-rank read reaches it.
-// Edges are re-oriented as (the read whose loop formed it, the partner), like the reference's
-// match set (:220); forward degrees become the edges formed in each read's own loop.
+// does, the loops of the reads that can reach the cap are replayed:
+//   1. candidates T: x joins T when fwd(x) + #{y in T, y < x, (y, x) in E*} >= edge_threshold (a
+//      read's loop breaks only if its edge count reaches the cap; the edges it can form are its
+//      forward E* pairs plus E* pairs (y, x) an earlier breaking read y left unseen).  Kleene
+//      iteration from {fwd >= cap}: the rank-ordered definition has exactly one fixed point.
+//   2. the visit sequence of every read of T: per interval, its hits in the search's order
+//      (descending (start, -end, data position): the order of the superintervals stand-in the
+//      golden fixtures were made with — the library's own order is undocumented),
+//      the read's own intervals dropped (:203-204).  One wavefront per interval counts, then
+//      writes its hits top-down; runs of equal start are re-ranked on (end, position).
+//   3. slots: the distinct partners of each read of T (a radix sort of (t, partner) keys), with the
+//      sequence position of each partner's first occurrence, and the full pair predicate of each
+//      slot (k_cap_eval: length gate, first-fit, cut).
+//   4. x's loop depends on an earlier read y of T only through (did y break, did y's loop reach x),
+//      and only if y is one of x's partners: the loops are replayed per component of that
+//      dependency graph (union-find over the slots), one wavefront per component, reads in rank
+//      order.  Inside a loop, up to the break everything is visited, so the break is where the
+//      prefix count of first-occurrence edges reaches the cap (a wave-wide scan); after it, each
+//      later interval is walked to its first new counted pair.
+//   5. an E* pair (a, b) is an edge iff a's loop or, failing that, b's loop reaches it; edges are
+//      re-oriented as (the read whose loop formed it, partner) like the reference's match set
+//      (:220); forward degrees become the edges formed per loop; each replayed loop's own count
+//      must equal them (a consistency check).
+// Multi-GPU: each rank holds the full E* list (fslr_cap_install_edges) but indexes
+// only its chromosomes, so it writes the visit lists of the T intervals it owns (fslr_cap_local);
+// the caller all-gathers them and every rank replays (fslr_cap_replay).
+#include <hipcub/hipcub.hpp>
+
 #include <algorithm>
-#include <chrono>
 #include <cstdio>
-#include <cstdlib>
 #include <cstring>
-#include <memory>
-#include <thread>
+#include <string>
 #include <vector>
 
 #include "ctx.hpp"
 #include "kernels.hpp"
+#include "wave.hpp"
 
 namespace fslr {
 namespace {
 
-__device__ __forceinline__ int mbcnt64(unsigned long long m) {
-  return __builtin_amdgcn_mbcnt_hi(static_cast<unsigned>(m >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<unsigned>(m), 0u));
+constexpr int kInf = 0x7fffffff;
+constexpr unsigned long long kKeyMask = (1ull << 25) - 1;   // read ranks < FSLR_MAX_READS
+// per visit-sequence element (rec.y)
+enum RecBits { kRFirst = 1, kRNonTBack = 2, kRBackT = 4, kREdge = 8, kRCounted = 16, kRZd = 32 };
+// device error word
+enum CapErr { kCapErrZd = 1, kCapErrState = 2 };
+// device statistics words
+enum CapStat { kStCapped = 0, kStDropped, kStBackward, kStMaxFwd, kStKept, kStWords = 8 };
+// pinned host words (written by tiny kernels; one sync each)
+enum CapHost { kHNt = 0, kHNti, kHNloc, kHNslots, kHNseq, kHErr, kHStat = 8, kHWords = 16 };
+
+__device__ __forceinline__ unsigned long long lanes_le(int lane) {
+  return lane == 63 ? ~0ull : (2ull << lane) - 1ull;
 }
 
-__global__ void k_hit_counts(const int* __restrict__ reads, int n, const int4* __restrict__ rmeta,
-                             const int* __restrict__ qpos, const int2* __restrict__ rng_s,
-                             long long* __restrict__ counts) {
-  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < n; t += gridDim.x * blockDim.x) {
-    const int4 m = rmeta[reads[t]];
-    const int len = m.y & 0xffff;
-    long long c = 0;
-    for (int i = 0; i < len; ++i) {
-      const int q = qpos[m.x + i];
-      const int2 rs = rng_s[q];
-      c += static_cast<long long>(rs.x) + (q - rs.y) + 1;
-    }
-    counts[t] = c;
+// ---- 1. closure T ------------------------------------------------------------------------------
+// state: 0 not in T, 1 joined in the last round (its forward edges not yet counted), 2 counted
+__global__ void k_cap_init(const int* __restrict__ fwd, int n, int thr, int* __restrict__ state,
+                           int* __restrict__ back) {
+  for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < n; x += gridDim.x * blockDim.x) {
+    state[x] = fwd[x] >= thr ? 1 : 0;
+    back[x] = 0;
   }
 }
 
-// one wavefront per listed read; positions bwd_begin .. q + n_fwd of each interval, 64 per step
-__global__ __launch_bounds__(256) void k_hit_emit(const int* __restrict__ reads, int n, const long long* __restrict__ off,
-                                                  const int4* __restrict__ rmeta, const int* __restrict__ qpos,
-                                                  const int2* __restrict__ rng_s, const int4* __restrict__ idx4,
-                                                  int4* __restrict__ hits, int* __restrict__ nout) {
+__global__ void k_cap_back(const int2* __restrict__ edges, long long ne, const int* __restrict__ state,
+                           int* __restrict__ back, const int* __restrict__ prev_chg) {
+  if (!*prev_chg) return;                                         // converged in an earlier round
+  for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < ne;
+       k += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const int2 e = edges[k];
+    if (state[e.x] == 1) atomicAdd(back + e.y, 1);
+  }
+}
+
+__global__ void k_cap_join(const int* __restrict__ fwd, int n, int thr, int* __restrict__ state,
+                           const int* __restrict__ back, const int* __restrict__ prev_chg, int* __restrict__ chg) {
+  if (!*prev_chg) return;
+  bool any = false;
+  for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < n; x += gridDim.x * blockDim.x) {
+    const int s = state[x];
+    if (s == 1) {
+      state[x] = 2;
+    } else if (s == 0 && fwd[x] + back[x] >= thr) {
+      state[x] = 1;
+      any = true;
+    }
+  }
+  if (__ballot(any) && (threadIdx.x & 63) == 0) atomicOr(chg, 1);
+}
+
+// T in rank order: one scan of (1 << 32 | L) gives each member its index t and its first T-interval
+__global__ void k_cap_tpack(const int* __restrict__ state, const int4* __restrict__ rmeta, int n,
+                            unsigned long long* __restrict__ v) {
+  for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < n; x += gridDim.x * blockDim.x)
+    v[x] = state[x] ? ((1ull << 32) | static_cast<unsigned>(rmeta[x].y & 0xffff)) : 0ull;
+}
+
+__global__ void k_cap_tlist(const int* __restrict__ state, const unsigned long long* __restrict__ v,
+                            const unsigned long long* __restrict__ vs, int n, int* __restrict__ T,
+                            int* __restrict__ toff, int* __restrict__ t_of, long long* __restrict__ host) {
+  for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < n; x += gridDim.x * blockDim.x) {
+    const unsigned long long s = vs[x];
+    if (state[x]) {
+      const int t = static_cast<int>(s >> 32);
+      T[t] = x;
+      toff[t] = static_cast<int>(s & 0xffffffffu);
+      t_of[x] = t;
+    } else {
+      t_of[x] = -1;
+    }
+    if (x == n - 1) {
+      const unsigned long long tot = s + v[x];
+      toff[tot >> 32] = static_cast<int>(tot & 0xffffffffu);
+      host[kHNt] = static_cast<long long>(tot >> 32);
+      host[kHNti] = static_cast<long long>(tot & 0xffffffffu);
+    }
+  }
+}
+
+// T-interval -> its read's index t
+__global__ void k_cap_tread(const int* __restrict__ toff, int nt, int* __restrict__ tread) {
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += gridDim.x * blockDim.x)
+    for (int j = toff[t]; j < toff[t + 1]; ++j) tread[j] = t;
+}
+
+// T-interval -> its position in this context's index (-1: a chromosome another rank indexes)
+__global__ void k_cap_tq(const int4* __restrict__ idx4, int ni, const int* __restrict__ t_of,
+                         const int* __restrict__ toff, int* __restrict__ tq) {
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < ni; q += gridDim.x * blockDim.x) {
+    const int tag = idx4[q].w;
+    const int t = t_of[tag >> 6];
+    if (t >= 0) tq[toff[t] + (tag & 63)] = q;
+  }
+}
+
+// ---- 2. visit sequences ------------------------------------------------------------------------
+// One wavefront per T-interval (sorted position q): the hits are q + 1 .. q + n_fwd and those p in
+// [bwd_begin, q) with end_p >= start_q (kernels.hpp rng_s), minus the read's own intervals.
+// kEmit = false: icnt[ti] = their count; kEmit = true: their positions, highest first, at ioff[ti].
+template <bool kEmit>
+__global__ __launch_bounds__(256) void k_cap_hits(const int* __restrict__ tq, const int* __restrict__ tread,
+                                                  const int* __restrict__ T, const int4* __restrict__ idx4,
+                                                  const int2* __restrict__ rng_s, int nti, int* __restrict__ icnt,
+                                                  const int* __restrict__ ioff, int* __restrict__ seqp) {
   const int lane = threadIdx.x & 63;
   const int nw = gridDim.x * (blockDim.x >> 6);
-  for (int t = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); t < n; t += nw) {
-    const int4 m = rmeta[reads[t]];
-    const int len = m.y & 0xffff;
-    const long long base = off[t];
+  for (int ti = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); ti < nti; ti += nw) {
+    const int q = tq[ti];
+    if (q < 0) {
+      if (!kEmit && lane == 0) icnt[ti] = 0;
+      continue;
+    }
+    const int x = T[tread[ti]];
+    const int s = idx4[q].x;
+    const int2 rg = rng_s[q];
+    const int lo = rg.y, hi = q + rg.x;
     int w = 0;
-    for (int i = 0; i < len; ++i) {
-      const int q = qpos[m.x + i];
-      const int2 rs = rng_s[q];
-      const int s = idx4[q].x;
-      const int hi = q + rs.x;
-      for (int p0 = rs.y; p0 <= hi; p0 += 64) {
-        const int p = p0 + lane;
-        int4 rec = make_int4(0, -1, 0, 0);
-        if (p <= hi) rec = idx4[p];
-        const bool hit = p <= hi && (p >= q || rec.y >= s);
+    if (kEmit) {
+      const int base = ioff[ti];
+      for (int p0 = hi; p0 >= lo; p0 -= 64) {
+        const int p = p0 - lane;
+        bool hit = false;
+        if (p >= lo) {
+          const int4 r = idx4[p];
+          hit = (p >= q || r.y >= s) && (r.w >> 6) != x;
+        }
         const unsigned long long hm = __ballot(hit);
-        if (hit) hits[base + w + mbcnt64(hm)] = make_int4(rec.w >> 6, i, rec.x, rec.y);
+        if (hit) seqp[base + w + mbcnt(hm)] = p;
         w += __popcll(hm);
       }
+    } else {
+      for (int p0 = lo; p0 <= hi; p0 += 64) {
+        const int p = p0 + lane;
+        bool hit = false;
+        if (p <= hi) {
+          const int4 r = idx4[p];
+          hit = (p >= q || r.y >= s) && (r.w >> 6) != x;
+        }
+        w += __popcll(__ballot(hit));
+      }
+      if (lane == 0) icnt[ti] = w;
     }
-    if (lane == 0) nout[t] = w;
   }
 }
 
-// one wavefront per pair: B's intervals in lanes, A's rows broadcast (the deferred kernel's gather
-// evaluation, query.hip), reporting the predicate's parts instead of appending an edge
-__global__ __launch_bounds__(256) void k_eval_pairs(const int2* __restrict__ pairs, long long n,
-                                                    const int4* __restrict__ rmeta, const int4* __restrict__ iv,
-                                                    double qcut, double ncut, const int* __restrict__ umax,
-                                                    int* __restrict__ flags) {
+// Positions -> partner reads in the search's order.  Inside a segment starts descend; a run of
+// equal start holds exactly the hits of that run (its elements with end >= start_q, a prefix of the
+// stand-in's (end desc, position asc) order), so each run's hits are re-ranked by (end asc,
+// position desc).  One wavefront per T-interval.
+__global__ __launch_bounds__(256) void k_cap_seq(const int* __restrict__ seqp, const int4* __restrict__ idx4,
+                                                 const int* __restrict__ ioff, int nti, int* __restrict__ seq) {
   const int lane = threadIdx.x & 63;
-  const long long nw = static_cast<long long>(gridDim.x) * (blockDim.x >> 6);
+  const int nw = gridDim.x * (blockDim.x >> 6);
+  for (int ti = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); ti < nti; ti += nw) {
+    const int b0 = ioff[ti], b1 = ioff[ti + 1];
+    for (int k0 = b0; k0 < b1; k0 += 64) {
+      const int k = k0 + lane;
+      if (k >= b1) continue;
+      const int p = seqp[k];
+      const int4 r = idx4[p];
+      const bool tied = (k > b0 && idx4[seqp[k - 1]].x == r.x) || (k + 1 < b1 && idx4[seqp[k + 1]].x == r.x);
+      int dst = k;
+      if (tied) {
+        int bb = k;
+        while (bb > b0 && idx4[seqp[bb - 1]].x == r.x) --bb;
+        int rank = 0;
+        for (int f = bb; f < b1; ++f) {
+          const int pf = seqp[f];
+          const int4 rf = idx4[pf];
+          if (rf.x != r.x) break;
+          rank += rf.y < r.y || (rf.y == r.y && pf > p);
+        }
+        dst = bb + rank;
+      }
+      seq[dst] = r.w >> 6;
+    }
+  }
+}
+
+// Multi-GPU: the ranks' gathered lists (rank w's list holds its T-intervals' segments in T-interval
+// order) into one sequence.  loff = exclusive scan of the gathered counts (rank-major).
+__global__ __launch_bounds__(256) void k_cap_assemble(const int* __restrict__ cnt_all, const int* __restrict__ loff,
+                                                      const int* __restrict__ lists, long long pad, int world,
+                                                      int nti, const int* __restrict__ ioff, int* __restrict__ seq) {
+  const int lane = threadIdx.x & 63;
+  const int nw = gridDim.x * (blockDim.x >> 6);
+  for (int ti = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); ti < nti; ti += nw) {
+    int dst = ioff[ti];
+    for (int w = 0; w < world; ++w) {
+      const long long i = static_cast<long long>(w) * nti + ti;
+      const int cnt = cnt_all[i];
+      if (!cnt) continue;
+      const int* src = lists + w * pad + (loff[i] - loff[static_cast<long long>(w) * nti]);
+      for (int k = lane; k < cnt; k += 64) seq[dst + k] = src[k];
+      dst += cnt;
+    }
+  }
+}
+
+__global__ void k_cap_sum_counts(const int* __restrict__ cnt_all, int world, int nti, int* __restrict__ tot) {
+  for (int ti = blockIdx.x * blockDim.x + threadIdx.x; ti <= nti; ti += gridDim.x * blockDim.x) {
+    int s = 0;
+    if (ti < nti)
+      for (int w = 0; w < world; ++w) s += cnt_all[static_cast<long long>(w) * nti + ti];
+    tot[ti] = s;
+  }
+}
+
+// ---- 3. slots ----------------------------------------------------------------------------------
+// sort keys (t << 25 | partner), values = sequence position; one wavefront per T-interval
+__global__ __launch_bounds__(256) void k_cap_keys(const int* __restrict__ seq, const int* __restrict__ ioff,
+                                                  const int* __restrict__ tread, int nti,
+                                                  unsigned long long* __restrict__ key, int* __restrict__ val) {
+  const int lane = threadIdx.x & 63;
+  const int nw = gridDim.x * (blockDim.x >> 6);
+  for (int ti = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); ti < nti; ti += nw) {
+    const unsigned long long hi = static_cast<unsigned long long>(tread[ti]) << 25;
+    for (int k = ioff[ti] + lane; k < ioff[ti + 1]; k += 64) {
+      key[k] = hi | static_cast<unsigned>(seq[k]);
+      val[k] = k;
+    }
+  }
+}
+
+__global__ void k_cap_heads(const unsigned long long* __restrict__ key, int m, int* __restrict__ head) {
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < m; k += gridDim.x * blockDim.x)
+    head[k] = k == 0 || key[k] != key[k - 1];
+}
+
+// stable sort: a run's first value is the partner's first occurrence in the read's sequence
+__global__ void k_cap_slots(const unsigned long long* __restrict__ key, const int* __restrict__ val,
+                            const int* __restrict__ head, const int* __restrict__ hs, int m,
+                            int* __restrict__ slot_of, unsigned long long* __restrict__ ukey, int* __restrict__ fpos,
+                            long long* __restrict__ host) {
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < m; k += gridDim.x * blockDim.x) {
+    const int s = hs[k] + head[k] - 1;
+    slot_of[val[k]] = s;
+    if (head[k]) {
+      ukey[s] = key[k];
+      fpos[s] = val[k];
+    }
+    if (k == m - 1) host[kHNslots] = s + 1;
+  }
+}
+
+// the full predicate of each slot's pair — one wavefront per pair: B's intervals in lanes, A's rows
+// broadcast (first-fit in the reference's order, rows ascending, lowest unused column,
+// cluster.py:152-161); flags = zd | lenok << 1 | edge << 2 | I << 8 | U << 20
+__global__ __launch_bounds__(256) void k_cap_eval(const unsigned long long* __restrict__ ukey, int ns,
+                                                  const int* __restrict__ T, const int4* __restrict__ rmeta,
+                                                  const int4* __restrict__ iv, double qcut, double ncut,
+                                                  const int* __restrict__ umax, int* __restrict__ flags) {
+  const int lane = threadIdx.x & 63;
+  const int nw = gridDim.x * (blockDim.x >> 6);
   const int umax_v = umax[lane];
-  for (long long t = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); t < n; t += nw) {
-    const int2 pr = pairs[t];
-    const int4 am = rmeta[pr.x], bm = rmeta[pr.y];
+  for (int sl = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); sl < ns; sl += nw) {
+    const unsigned long long key = ukey[sl];
+    const int x = T[key >> 25], y = static_cast<int>(key & kKeyMask);
+    const int4 am = rmeta[min(x, y)], bm = rmeta[max(x, y)];
     const int LA = am.y & 0xffff, LB = bm.y & 0xffff;
     int4 ai = make_int4(-1, 0, 0, 0), bj = make_int4(-2, 0, 0, 0);
     if (lane < LA) ai = iv[am.x + lane];
@@ -114,15 +320,17 @@ __global__ __launch_bounds__(256) void k_eval_pairs(const int2* __restrict__ pai
     if (lenok && !zd) {
       bool used = false;
       for (int i = 0; i < LA; ++i) {
-        const int c = __builtin_amdgcn_readlane(ai.x, i), si = __builtin_amdgcn_readlane(ai.y, i);
-        const int ei = __builtin_amdgcn_readlane(ai.z, i), ti = __builtin_amdgcn_readlane(ai.w, i);
+        const int c = rdl(ai.x, i), si = rdl(ai.y, i), ei = rdl(ai.z, i), ti = rdl(ai.w, i);
         const bool cand = lane < LB && !used && bj.x == c;
         const bool zero = cand && (ti == FSLR_THR_ZERO_ALN || bj.w == FSLR_THR_ZERO_ALN);
         const bool hit = cand && (zero || iv_match_general(si, ei, ti, bj.y, bj.z, bj.w));
         const unsigned long long hm = __ballot(hit);
         if (!hm) continue;
         const int j = __builtin_ctzll(hm);
-        if (__shfl(static_cast<int>(zero), j)) { zd = true; break; }
+        if (__shfl(static_cast<int>(zero), j)) {
+          zd = true;
+          break;
+        }
         if (lane == j) used = true;
         ++I;
       }
@@ -130,85 +338,690 @@ __global__ __launch_bounds__(256) void k_eval_pairs(const int2* __restrict__ pai
     const int U = LA + LB - I;
     const bool edge = lenok && !zd && I > 0 && U <= __shfl(umax_v, max(I, 1) - 1);
     if (lane == 0)
-      flags[t] = static_cast<int>(zd) | (static_cast<int>(lenok && !zd) << 1) | (static_cast<int>(edge) << 2) |
-                 (I << 8) | (U << 20);
+      flags[sl] = static_cast<int>(zd) | (static_cast<int>(lenok && !zd) << 1) | (static_cast<int>(edge) << 2) |
+                  (I << 8) | (U << 20);
   }
 }
 
+__device__ __forceinline__ int find_slot(const unsigned long long* __restrict__ ukey, int ns, unsigned long long k) {
+  int lo = 0, hi = ns;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (ukey[mid] < k) lo = mid + 1; else hi = mid;
+  }
+  return lo < ns && ukey[lo] == k ? lo : -1;
+}
+
+// per slot (x, y): for an earlier partner y of T, the slot of (y, x) (where y's loop records
+// whether it reached x) and the union of x and y in the dependency graph
+__global__ void k_cap_mirror(const unsigned long long* __restrict__ ukey, int ns, const int* __restrict__ T,
+                             const int* __restrict__ t_of, int* __restrict__ mslot, int2* __restrict__ upairs,
+                             int* __restrict__ err) {
+  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < ns; s += gridDim.x * blockDim.x) {
+    const unsigned long long key = ukey[s];
+    const int t = static_cast<int>(key >> 25), y = static_cast<int>(key & kKeyMask);
+    const int x = T[t];
+    const int ty = y < x ? t_of[y] : -1;
+    int ms = -1;
+    int2 up = make_int2(-1, -1);
+    if (ty >= 0) {
+      ms = find_slot(ukey, ns, (static_cast<unsigned long long>(ty) << 25) | static_cast<unsigned>(x));
+      if (ms < 0) atomicOr(err, kCapErrState);          // hits are symmetric: cannot happen
+      up = make_int2(t, ty);
+    }
+    mslot[s] = ms;
+    upairs[s] = up;
+  }
+}
+
+__global__ void k_cap_ckeys(const int* __restrict__ tpar, int nt, unsigned long long* __restrict__ ck) {
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += gridDim.x * blockDim.x)
+    ck[t] = (static_cast<unsigned long long>(tpar[t]) << 25) | static_cast<unsigned>(t);
+}
+
+// the replay's static view of each sequence element: {slot, bits, mirror slot, T index of partner}
+__global__ void k_cap_recs(const int* __restrict__ slot_of, const unsigned long long* __restrict__ ukey,
+                           const int* __restrict__ fpos, const int* __restrict__ flags, const int* __restrict__ mslot,
+                           const int* __restrict__ T, const int* __restrict__ t_of, int m, int4* __restrict__ rec) {
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < m; k += gridDim.x * blockDim.x) {
+    const int s = slot_of[k];
+    const unsigned long long key = ukey[s];
+    const int x = T[key >> 25], y = static_cast<int>(key & kKeyMask);
+    const int f = flags[s];
+    int bits = fpos[s] == k ? kRFirst : 0;
+    int ty = -1;
+    if (y < x) {
+      ty = t_of[y];
+      bits |= ty >= 0 ? kRBackT : kRNonTBack;     // a non-T earlier read never breaks: pair seen
+    }
+    if (f & 1) bits |= kRZd;
+    if (f & 4) bits |= kREdge;
+    if ((f & 2) && ((f >> 8) & 0xfff) > 0) bits |= kRCounted;
+    rec[k] = make_int4(s, bits, ty >= 0 ? mslot[s] : -1, ty);
+  }
+}
+
+// ---- 4. the loops ------------------------------------------------------------------------------
+// did the (finished) loop of T read ty reach its slot ms?  Everything up to its break position, plus
+// what its post-break interval walks visited
+__device__ __forceinline__ bool reached(const int* __restrict__ fpos, const unsigned char* vis2,
+                                        const int* pbrk, int ms, int ty) {
+  return fpos[ms] <= pbrk[ty] || vis2[ms];
+}
+
+__device__ bool replay_read(int t, int lane, int thr, const int* __restrict__ toff, const int* __restrict__ ioff,
+                            const int4* __restrict__ rec, const int* __restrict__ fpos, unsigned char* vis2,
+                            int* pbrk, int* own, int* err) {
+  const int ti0 = toff[t], ti1 = toff[t + 1];
+  const int sb = ioff[ti0], se = ioff[ti1];
+  int edges = 0, P = kInf;
+  // before the break every hit is visited: the first occurrence of each partner is its visit
+  for (int k0 = sb; k0 < se; k0 += 64) {
+    const int k = k0 + lane;
+    bool e = false, cnt = false, zd = false;
+    if (k < se) {
+      const int4 r = rec[k];
+      bool proc = (r.y & kRFirst) && !(r.y & kRNonTBack);
+      if (proc && (r.y & kRBackT)) proc = !reached(fpos, vis2, pbrk, r.z, r.w);
+      e = proc && (r.y & kREdge);
+      cnt = proc && (r.y & kRCounted);
+      zd = proc && (r.y & kRZd);
+    }
+    const unsigned long long em = __ballot(e);
+    const int incl = edges + __popcll(em & lanes_le(lane));
+    const unsigned long long bm = __ballot(cnt && incl >= thr);   // the check after a counted pair (:223)
+    const unsigned long long zm = __ballot(zd);
+    const int fb = bm ? __builtin_ctzll(bm) : 64;
+    if (zm && __builtin_ctzll(zm) < fb) {
+      if (lane == 0) atomicOr(err, kCapErrZd);
+      return false;
+    }
+    if (bm) {
+      P = k0 + fb;
+      edges += __popcll(em & lanes_le(fb));
+      break;
+    }
+    edges += __popcll(em);
+  }
+  if (P != kInf) {
+    // the rest of the break's interval is left; each later interval is walked up to its first new
+    // pair that passes the gate with I > 0 (:216-217 skip the check, :223 then breaks again)
+    int ti = ti0;
+    while (ioff[ti + 1] <= P) ++ti;
+    for (++ti; ti < ti1; ++ti) {
+      const int b0 = ioff[ti], b1 = ioff[ti + 1];
+      for (int k0 = b0; k0 < b1; k0 += 64) {
+        const int k = k0 + lane;
+        bool proc = false, e = false, cnt = false, zd = false;
+        int s = 0;
+        if (k < b1) {
+          const int4 r = rec[k];
+          s = r.x;
+          proc = !(r.y & kRNonTBack);
+          if (proc && (r.y & kRBackT)) proc = !reached(fpos, vis2, pbrk, r.z, r.w);
+          if (proc) proc = fpos[s] > P && !vis2[s];
+          e = proc && (r.y & kREdge);
+          cnt = proc && (r.y & kRCounted);
+          zd = proc && (r.y & kRZd);
+        }
+        const unsigned long long cm = __ballot(cnt);
+        const unsigned long long zm = __ballot(zd);
+        const int stop = cm ? __builtin_ctzll(cm) : 64;
+        if (zm && __builtin_ctzll(zm) < stop) {
+          if (lane == 0) atomicOr(err, kCapErrZd);
+          return false;
+        }
+        if (proc && lane <= stop) vis2[s] = 1;
+        if (cm) {
+          edges += static_cast<int>((__ballot(e) >> stop) & 1ull);
+          break;
+        }
+      }
+      __threadfence();                     // this walk's marks before the next interval's loads
+    }
+  }
+  if (lane == 0) {
+    pbrk[t] = P;
+    own[t] = edges;
+  }
+  return true;
+}
+
+// one wavefront per component of the dependency graph (its head = its smallest t), reads in rank order
+__global__ __launch_bounds__(256) void k_cap_replay(const unsigned long long* __restrict__ ck, int nt, int thr,
+                                                    const int* __restrict__ toff, const int* __restrict__ ioff,
+                                                    const int4* __restrict__ rec, const int* __restrict__ fpos,
+                                                    unsigned char* vis2, int* pbrk, int* own, int* err) {
+  const int lane = threadIdx.x & 63;
+  const int nw = gridDim.x * (blockDim.x >> 6);
+  for (int h = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); h < nt; h += nw) {
+    const unsigned long long hk = ck[h];
+    const int root = static_cast<int>(hk >> 25);
+    if (static_cast<int>(hk & kKeyMask) != root) continue;
+    for (int k = h; k < nt; ++k) {
+      const unsigned long long kk = ck[k];
+      if (static_cast<int>(kk >> 25) != root) break;
+      if (!replay_read(static_cast<int>(kk & kKeyMask), lane, thr, toff, ioff, rec, fpos, vis2, pbrk, own, err))
+        return;
+      __threadfence();                     // this loop's results before a later read's loads
+    }
+  }
+}
+
+// ---- 5. the capped graph -----------------------------------------------------------------------
+__device__ __forceinline__ bool loop_reaches(int x, int y, const int* __restrict__ t_of,
+                                             const int* __restrict__ pbrk, const unsigned long long* __restrict__ ukey,
+                                             int ns, const int* __restrict__ fpos, const unsigned char* __restrict__ vis2,
+                                             int* err) {
+  const int t = t_of[x];
+  if (t < 0 || pbrk[t] == kInf) return true;       // the loop never broke: it visited every hit
+  const int s = find_slot(ukey, ns, (static_cast<unsigned long long>(t) << 25) | static_cast<unsigned>(y));
+  if (s < 0) {
+    atomicOr(err, kCapErrState);
+    return false;
+  }
+  return fpos[s] <= pbrk[t] || vis2[s];
+}
+
+// who: 0 formed in a's loop, 1 in b's, 2 in neither (dropped)
+__global__ void k_cap_classify(const int2* __restrict__ edges, long long ne, const int* __restrict__ t_of,
+                               const int* __restrict__ pbrk, const unsigned long long* __restrict__ ukey, int ns,
+                               const int* __restrict__ fpos, const unsigned char* __restrict__ vis2,
+                               int* __restrict__ kflag, unsigned char* __restrict__ who, int* __restrict__ formed,
+                               long long* __restrict__ stats, int* __restrict__ err) {
+  long long drop = 0, bwd = 0;
+  for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < ne;
+       k += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const int2 e = edges[k];
+    int w = 2;
+    if (loop_reaches(e.x, e.y, t_of, pbrk, ukey, ns, fpos, vis2, err)) w = 0;
+    else if (loop_reaches(e.y, e.x, t_of, pbrk, ukey, ns, fpos, vis2, err)) w = 1;
+    who[k] = static_cast<unsigned char>(w);
+    kflag[k] = w != 2;
+    if (w != 2) atomicAdd(formed + (w == 0 ? e.x : e.y), 1);
+    drop += w == 2;
+    bwd += w == 1;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    drop += __shfl_xor(drop, o);
+    bwd += __shfl_xor(bwd, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (drop) atomicAdd(reinterpret_cast<unsigned long long*>(stats + kStDropped), static_cast<unsigned long long>(drop));
+    if (bwd) atomicAdd(reinterpret_cast<unsigned long long*>(stats + kStBackward), static_cast<unsigned long long>(bwd));
+  }
+}
+
+__global__ void k_cap_compact(const int2* __restrict__ edges, const unsigned short* __restrict__ iu, long long ne,
+                              const unsigned char* __restrict__ who, const int* __restrict__ koff,
+                              int2* __restrict__ oe, unsigned short* __restrict__ oiu) {
+  for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < ne;
+       k += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const int w = who[k];
+    if (w == 2) continue;
+    const int2 e = edges[k];
+    const int o = koff[k];
+    oe[o] = w == 0 ? e : make_int2(e.y, e.x);
+    oiu[o] = iu[k];
+  }
+}
+
+// each replayed loop's own edge count must equal the edges classified as formed by it
+__global__ void k_cap_check(const int* __restrict__ T, int nt, const int* __restrict__ own, const int* __restrict__ pbrk,
+                            const int* __restrict__ formed, int n, long long* __restrict__ stats, int* __restrict__ err) {
+  int capped = 0, mx = 0;
+  const int m = max(n, nt);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
+    if (i < nt) {
+      if (formed[T[i]] != own[i]) atomicOr(err, kCapErrState);
+      capped += pbrk[i] != kInf;
+    }
+    if (i < n) mx = max(mx, formed[i]);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    capped += __shfl_xor(capped, o);
+    mx = max(mx, __shfl_xor(mx, o));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (capped) atomicAdd(reinterpret_cast<unsigned long long*>(stats + kStCapped), static_cast<unsigned long long>(capped));
+    atomicMax(reinterpret_cast<long long*>(stats + kStMaxFwd), static_cast<long long>(mx));
+  }
+}
+
+// the capped graph into the context: edge count, max forward degree; stats + error to pinned memory
+__global__ void k_cap_commit(const int* __restrict__ koff, const int* __restrict__ kflag, long long ne,
+                             unsigned long long* __restrict__ counters, int* __restrict__ errw,
+                             long long* __restrict__ stats, const int* __restrict__ err, long long* __restrict__ host) {
+  if (threadIdx.x != 0) return;
+  const long long kept = ne ? static_cast<long long>(koff[ne - 1]) + kflag[ne - 1] : 0;
+  stats[kStKept] = kept;
+  counters[kEdgeCount] = static_cast<unsigned long long>(kept);
+  errw[3] = static_cast<int>(stats[kStMaxFwd]);
+  for (int k = 0; k < kStWords; ++k) host[kHStat + k] = stats[k];
+  host[kHErr] = *err;
+}
+
+__global__ void k_cap_total(const int* __restrict__ off, long long i, long long* __restrict__ host, int slot) {
+  if (threadIdx.x == 0) host[slot] = off[i];
+}
+
+// multi-GPU: install a gathered E* list {a, b, iu, -} (rows with a < 0 are padding), stable
+__global__ void k_cap_flag_rows(const int4* __restrict__ rows, long long n, int* __restrict__ f) {
+  for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < n;
+       k += static_cast<long long>(gridDim.x) * blockDim.x)
+    f[k] = rows[k].x >= 0;
+}
+
+__global__ void k_cap_install(const int4* __restrict__ rows, long long n, const int* __restrict__ f,
+                              const int* __restrict__ off, int2* __restrict__ edges, unsigned short* __restrict__ iu,
+                              long long cap, int* __restrict__ fwd) {
+  for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < n;
+       k += static_cast<long long>(gridDim.x) * blockDim.x) {
+    if (!f[k]) continue;
+    const int4 r = rows[k];
+    const long long o = off[k];
+    if (o < cap) {
+      edges[o] = make_int2(r.x, r.y);
+      iu[o] = static_cast<unsigned short>(r.z);
+    }
+    atomicAdd(fwd + r.x, 1);
+  }
+}
+
+__global__ void k_cap_install_commit(const int* __restrict__ off, const int* __restrict__ f, long long n,
+                                     const int* __restrict__ fwd, int nr, unsigned long long* __restrict__ counters,
+                                     int* __restrict__ errw) {
+  int mx = 0;
+  for (int i = threadIdx.x; i < nr; i += blockDim.x) mx = max(mx, fwd[i]);
+  for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+  __shared__ int wm[16];
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < static_cast<int>(blockDim.x >> 6); ++w) mx = max(mx, wm[w]);
+    counters[kEdgeCount] = n ? static_cast<unsigned long long>(off[n - 1] + f[n - 1]) : 0ull;
+    errw[0] = 0;
+    errw[3] = max(mx, wm[0]);
+    errw[kErrOverflow] = 0;
+  }
+}
+
+__global__ void k_copy_edges_iu(const int2* __restrict__ edges, const unsigned short* __restrict__ iu,
+                                const unsigned long long* __restrict__ count, long long cap, int4* __restrict__ out,
+                                long long n_pad) {
+  const long long ne = min(min(static_cast<long long>(*count), cap), n_pad);
+  for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < n_pad;
+       k += static_cast<long long>(gridDim.x) * blockDim.x)
+    out[k] = k < ne ? make_int4(edges[k].x, edges[k].y, iu[k], 0) : make_int4(-1, -1, 0, 0);
+}
+
+__global__ void k_fill(int* __restrict__ p, int n, int v) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = v;
+}
+
+int bits_for(long long v) {
+  int b = 1;
+  while ((1ll << b) <= v) ++b;
+  return b;
+}
+
+int wave_grid(long long items) {
+  return static_cast<int>(std::max<long long>(1, std::min<long long>(8192, (items + 3) / 4)));
+}
+
 }  // namespace
-
-hipError_t launch_cap_hit_counts(const int* reads, int n, const int4* rmeta, const int* qpos, const int2* rng_s,
-                                 long long* counts, hipStream_t s) {
-  if (n > 0) k_hit_counts<<<grid_for(n), 256, 0, s>>>(reads, n, rmeta, qpos, rng_s, counts);
-  return hipGetLastError();
-}
-
-hipError_t launch_cap_hit_emit(const int* reads, int n, const long long* off, const int4* rmeta, const int* qpos,
-                               const int2* rng_s, const int4* idx4, int4* hits, int* nout, hipStream_t s) {
-  if (n > 0) k_hit_emit<<<std::min(4096, (n + 3) / 4), 256, 0, s>>>(reads, n, off, rmeta, qpos, rng_s, idx4, hits, nout);
-  return hipGetLastError();
-}
-
-hipError_t launch_eval_pairs(const int2* pairs, long long n, const int4* rmeta, const int4* iv, double qcut,
-                             double ncut, const int* umax, int* flags, hipStream_t s) {
-  if (n > 0)
-    k_eval_pairs<<<static_cast<int>(std::min<long long>(8192, (n + 3) / 4)), 256, 0, s>>>(pairs, n, rmeta, iv, qcut,
-                                                                                          ncut, umax, flags);
-  return hipGetLastError();
-}
-
 }  // namespace fslr
 
 using namespace fslr;
 
+// ---- host side: buffers -----------------------------------------------------------------------
+// Grow-only device arenas, one per phase (their sizes are known at the phase's start).
+struct CapArena {
+  char* base = nullptr;
+  size_t cap = 0;
+};
+
+struct CapWork {
+  CapArena ar[5];                     // 0: per read / per edge, 1: per T read / T-interval, 2: per hit (scratch),
+                                      // 3: multi-GPU offsets, 4: the visit sequence
+  void* temp = nullptr;
+  size_t temp_bytes = 0;
+  long long* host = nullptr;          // pinned, device-mapped
+  long long* host_dev = nullptr;
+  int thr = 0;
+  int64_t n = 0, ne = 0, nt = 0, nti = 0, nloc = 0, nseq = 0, ns = 0;
+  // phase 0
+  int *state = nullptr, *back = nullptr, *t_of = nullptr, *T = nullptr, *toff = nullptr, *formed = nullptr;
+  unsigned long long *tv = nullptr, *tvs = nullptr;
+  int *chg = nullptr, *err = nullptr, *kflag = nullptr, *koff = nullptr;
+  long long* stats = nullptr;
+  unsigned char* who = nullptr;
+  int2* oedges = nullptr;
+  unsigned short* oiu = nullptr;
+  // phase 1
+  int *tread = nullptr, *tq = nullptr, *icnt = nullptr, *ioff = nullptr, *pbrk = nullptr, *own = nullptr,
+      *tpar = nullptr;
+  unsigned long long *ck = nullptr, *ck2 = nullptr;
+  // phase 2 (local lists: seqp, seq; then the sequence)
+  int *seqp = nullptr, *seq = nullptr, *sval = nullptr, *sval2 = nullptr, *head = nullptr, *hs = nullptr,
+      *slot_of = nullptr, *fpos = nullptr, *flags = nullptr, *mslot = nullptr;
+  unsigned long long *skey = nullptr, *skey2 = nullptr, *ukey = nullptr;
+  int2* upairs = nullptr;
+  unsigned char* vis2 = nullptr;
+  int4* rec = nullptr;
+  // multi-GPU assembly
+  int *gsum = nullptr, *loff = nullptr;
+  bool prepared = false;              // fslr_cap_local ran on the current edges
+};
+
+void fslr_cap_free(fslr_ctx* c) {
+  CapWork* w = c->capw;
+  if (!w) return;
+  for (auto& a : w->ar)
+    if (a.base) (void)hipFree(a.base);
+  if (w->temp) (void)hipFree(w->temp);
+  if (w->host) (void)hipHostFree(w->host);
+  delete w;
+  c->capw = nullptr;
+}
+
 namespace {
 
-// device scratch freed on every exit path
-struct DevBuf {
-  void* p = nullptr;
-  ~DevBuf() {
-    if (p) (void)hipFree(p);
+// carve typed sub-arrays out of one arena (256-B aligned); grow it first if needed
+struct Carve {
+  struct Req {
+    void** p;
+    size_t bytes;
+  };
+  Req reqs[32];
+  int nreq = 0;
+  template <typename T>
+  void add(T** p, int64_t count) {
+    reqs[nreq++] = {reinterpret_cast<void**>(p), static_cast<size_t>(std::max<int64_t>(count, 1)) * sizeof(T)};
+  }
+  int commit(fslr_ctx* c, CapArena& a) {
+    size_t total = 0;
+    for (int i = 0; i < nreq; ++i) total += (reqs[i].bytes + 255) & ~size_t(255);
+    if (total > a.cap) {
+      if (a.base) (void)hipFree(a.base);
+      a.base = nullptr;
+      a.cap = 0;
+      const size_t want = total + total / 8;
+      hipError_t e = hipMalloc(reinterpret_cast<void**>(&a.base), want);
+      if (e != hipSuccess) return fail(c, FSLR_ERR_NOMEM, std::string("cap replay hipMalloc: ") + hipGetErrorString(e));
+      a.cap = want;
+    }
+    size_t off = 0;
+    for (int i = 0; i < nreq; ++i) {
+      *reqs[i].p = a.base + off;
+      off += (reqs[i].bytes + 255) & ~size_t(255);
+    }
+    return FSLR_OK;
   }
 };
 
-constexpr int kFlagZd = 1, kFlagLenOk = 2, kFlagEdge = 4;
-
-// f(begin, end) over [0, n) split across the host's cores
-template <typename F>
-void parallel_for(int n, F&& f) {
-  const int hw = static_cast<int>(std::max(1u, std::thread::hardware_concurrency()));
-  const int nth = std::max(1, std::min({hw, 16, n / 256}));
-  if (nth == 1) {
-    f(0, n);
-    return;
-  }
-  std::vector<std::thread> th;
-  for (int k = 0; k < nth; ++k) {
-    const int b = static_cast<int>(static_cast<long long>(n) * k / nth);
-    const int e = static_cast<int>(static_cast<long long>(n) * (k + 1) / nth);
-    th.emplace_back([&f, b, e] { f(b, e); });
-  }
-  for (auto& x : th) x.join();
+int ensure_temp(fslr_ctx* c, CapWork* w, size_t need) {
+  if (need <= w->temp_bytes) return FSLR_OK;
+  if (w->temp) (void)hipFree(w->temp);
+  w->temp = nullptr;
+  w->temp_bytes = 0;
+  HIP_TRY(c, hipMalloc(&w->temp, need + need / 8 + 4096));
+  w->temp_bytes = need + need / 8 + 4096;
+  return FSLR_OK;
 }
 
-// f(tid, begin, end) over [0, n) in `nth` contiguous ranges, one thread each (range k = thread k)
-template <typename F>
-void parallel_ranges(int64_t n, int nth, F&& f) {
-  if (nth <= 1) {
-    f(0, int64_t(0), n);
-    return;
+int cap_work(fslr_ctx* c, CapWork** out) {
+  if (!c->capw) {
+    c->capw = new CapWork();
+    HIP_TRY(c, hipHostMalloc(reinterpret_cast<void**>(&c->capw->host), kHWords * sizeof(long long), hipHostMallocMapped));
+    HIP_TRY(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->capw->host_dev), c->capw->host, 0));
   }
-  std::vector<std::thread> th;
-  for (int k = 0; k < nth; ++k) {
-    const int64_t b = n * k / nth, e = n * (k + 1) / nth;
-    th.emplace_back([&f, k, b, e] { f(k, b, e); });
-  }
-  for (auto& x : th) x.join();
+  *out = c->capw;
+  return FSLR_OK;
 }
 
-int host_threads(int64_t work) {
-  const int hw = static_cast<int>(std::max(1u, std::thread::hardware_concurrency()));
-  return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>({hw, 16, work / (1 << 16)})));
+long long host_word(CapWork* w, int k) {
+  return static_cast<const volatile long long*>(w->host)[k];
+}
+
+// Phase A: the closure T, the T-intervals and their local hit counts; the local visit lists
+// (partner reads, search order) at w->seq[0 .. nloc), segments at w->ioff (local counts).
+int cap_local(fslr_ctx* c, int thr, CapWork* w, int64_t ne) {
+  hipStream_t s = c->stream;
+  const int64_t n = c->n;
+  w->thr = thr;
+  w->n = n;
+  w->ne = ne;
+  w->prepared = false;
+  {
+    Carve cv;
+    cv.add(&w->state, n);
+    cv.add(&w->back, n);
+    cv.add(&w->t_of, n);
+    cv.add(&w->T, n);
+    cv.add(&w->toff, n + 1);
+    cv.add(&w->formed, n);
+    cv.add(&w->tv, n);
+    cv.add(&w->tvs, n);
+    cv.add(&w->chg, 16);
+    cv.add(&w->err, 4);
+    cv.add(&w->stats, kStWords);
+    cv.add(&w->kflag, ne);
+    cv.add(&w->koff, ne);
+    cv.add(&w->who, ne);
+    cv.add(&w->oedges, ne);
+    cv.add(&w->oiu, ne);
+    if (int rc = cv.commit(c, w->ar[0])) return rc;
+  }
+  HIP_TRY(c, hipMemsetAsync(w->err, 0, 4 * sizeof(int), s));
+  HIP_TRY(c, hipMemsetAsync(w->stats, 0, kStWords * sizeof(long long), s));
+  // 1. closure: rounds in batches of 8, one sync per batch (chg[0] = 1 starts each batch)
+  k_cap_init<<<grid_for(n), 256, 0, s>>>(c->fwd, static_cast<int>(n), thr, w->state, w->back);
+  HIP_TRY(c, hipGetLastError());
+  for (int batch = 0;; ++batch) {
+    HIP_TRY(c, hipMemsetAsync(w->chg, 0, 16 * sizeof(int), s));
+    HIP_TRY(c, hipMemsetAsync(w->chg, 0xff, sizeof(int), s));
+    for (int r = 1; r <= 8; ++r) {
+      k_cap_back<<<grid_for(ne), 256, 0, s>>>(c->edges, ne, w->state, w->back, w->chg + r - 1);
+      k_cap_join<<<grid_for(n), 256, 0, s>>>(c->fwd, static_cast<int>(n), thr, w->state, w->back, w->chg + r - 1,
+                                             w->chg + r);
+    }
+    HIP_TRY(c, hipGetLastError());
+    int last = 0;
+    HIP_TRY(c, hipMemcpyAsync(&last, w->chg + 8, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    if (!last) break;
+    if (batch > (n >> 3) + 2) return fail(c, FSLR_ERR_STATE, "edge cap closure does not converge");
+  }
+  // T in rank order, T-intervals
+  k_cap_tpack<<<grid_for(n), 256, 0, s>>>(w->state, c->rmeta, static_cast<int>(n), w->tv);
+  size_t tb = 0;
+  HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tb, w->tv, w->tvs, static_cast<int>(n), s));
+  if (int rc = ensure_temp(c, w, tb)) return rc;
+  tb = w->temp_bytes;
+  HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(w->temp, tb, w->tv, w->tvs, static_cast<int>(n), s));
+  k_cap_tlist<<<grid_for(n), 256, 0, s>>>(w->state, w->tv, w->tvs, static_cast<int>(n), w->T, w->toff, w->t_of,
+                                          w->host_dev);
+  HIP_TRY(c, hipGetLastError());
+  HIP_TRY(c, hipStreamSynchronize(s));
+  w->nt = host_word(w, kHNt);
+  w->nti = host_word(w, kHNti);
+  const int nt = static_cast<int>(w->nt), nti = static_cast<int>(w->nti);
+  {
+    Carve cv;
+    cv.add(&w->tread, nti);
+    cv.add(&w->tq, nti);
+    cv.add(&w->icnt, nti + 1);
+    cv.add(&w->ioff, nti + 1);
+    cv.add(&w->gsum, nti + 1);
+    cv.add(&w->pbrk, nt);
+    cv.add(&w->own, nt);
+    cv.add(&w->tpar, nt);
+    cv.add(&w->ck, nt);
+    cv.add(&w->ck2, nt);
+    if (int rc = cv.commit(c, w->ar[1])) return rc;
+  }
+  if (nt > 0) {
+    k_cap_tread<<<grid_for(nt), 256, 0, s>>>(w->toff, nt, w->tread);
+    HIP_TRY(c, hipMemsetAsync(w->tq, 0xff, static_cast<size_t>(nti) * sizeof(int), s));
+    k_cap_tq<<<grid_for(c->ni_idx), 256, 0, s>>>(c->idx4, static_cast<int>(c->ni_idx), w->t_of, w->toff, w->tq);
+    // 2. hits of the T-intervals this index holds: count, scan, emit top-down, ties, partner reads
+    k_cap_hits<false><<<wave_grid(nti), 256, 0, s>>>(w->tq, w->tread, w->T, c->idx4, c->rng_s, nti, w->icnt, nullptr,
+                                                      nullptr);
+    HIP_TRY(c, hipGetLastError());
+  }
+  HIP_TRY(c, hipMemsetAsync(w->icnt + nti, 0, sizeof(int), s));
+  tb = 0;
+  HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tb, w->icnt, w->ioff, nti + 1, s));
+  if (int rc = ensure_temp(c, w, tb)) return rc;
+  tb = w->temp_bytes;
+  HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(w->temp, tb, w->icnt, w->ioff, nti + 1, s));
+  k_cap_total<<<1, 64, 0, s>>>(w->ioff, nti, w->host_dev, kHNloc);
+  HIP_TRY(c, hipGetLastError());
+  HIP_TRY(c, hipStreamSynchronize(s));
+  w->nloc = host_word(w, kHNloc);
+  if (w->nloc >= (int64_t(1) << 31)) return fail(c, FSLR_ERR_NOMEM, "edge cap replay: more than 2^31 hits");
+  {
+    Carve c2, c4;
+    c2.add(&w->seqp, w->nloc);
+    c4.add(&w->seq, w->nloc);
+    if (int rc = c2.commit(c, w->ar[2])) return rc;
+    if (int rc = c4.commit(c, w->ar[4])) return rc;
+  }
+  if (nti > 0 && w->nloc > 0) {
+    k_cap_hits<true><<<wave_grid(nti), 256, 0, s>>>(w->tq, w->tread, w->T, c->idx4, c->rng_s, nti, nullptr, w->ioff,
+                                                     w->seqp);
+    k_cap_seq<<<wave_grid(nti), 256, 0, s>>>(w->seqp, c->idx4, w->ioff, nti, w->seq);
+    HIP_TRY(c, hipGetLastError());
+  }
+  w->prepared = true;
+  return FSLR_OK;
+}
+
+// Phase B: the sequence (w->seq, segments w->ioff, w->nseq elements) -> slots, predicates, loops,
+// the capped graph written back into the context.
+int cap_core(fslr_ctx* c, CapWork* w, fslr_cap_stats* cs) {
+  hipStream_t s = c->stream;
+  const int thr = w->thr;
+  const int64_t n = w->n, ne = w->ne;
+  const int nt = static_cast<int>(w->nt), nti = static_cast<int>(w->nti);
+  const int m = static_cast<int>(w->nseq);
+  {
+    Carve cv;                          // the sequence itself lives in arena 4
+    cv.add(&w->sval, m);
+    cv.add(&w->sval2, m);
+    cv.add(&w->head, m);
+    cv.add(&w->hs, m);
+    cv.add(&w->slot_of, m);
+    cv.add(&w->fpos, m);
+    cv.add(&w->flags, m);
+    cv.add(&w->mslot, m);
+    cv.add(&w->skey, m);
+    cv.add(&w->skey2, m);
+    cv.add(&w->ukey, m);
+    cv.add(&w->upairs, m);
+    cv.add(&w->vis2, m);
+    cv.add(&w->rec, m);
+    if (int rc = cv.commit(c, w->ar[2])) return rc;
+  }
+  int ns = 0;
+  if (m > 0) {
+    // 3. slots: sort (t, partner) keys stably by sequence position, unique
+    k_cap_keys<<<wave_grid(nti), 256, 0, s>>>(w->seq, w->ioff, w->tread, nti, w->skey, w->sval);
+    size_t b1 = 0, b2 = 0, b3 = 0;
+    const int kbits = 25 + bits_for(nt);
+    HIP_TRY(c, hipcub::DeviceRadixSort::SortPairs(nullptr, b1, w->skey, w->skey2, w->sval, w->sval2, m, 0, kbits, s));
+    HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(nullptr, b2, w->head, w->hs, m, s));
+    HIP_TRY(c, hipcub::DeviceRadixSort::SortKeys(nullptr, b3, w->ck, w->ck2, std::max(nt, 1), 0, 50, s));
+    if (int rc = ensure_temp(c, w, std::max({b1, b2, b3}))) return rc;
+    size_t tb = w->temp_bytes;
+    HIP_TRY(c, hipcub::DeviceRadixSort::SortPairs(w->temp, tb, w->skey, w->skey2, w->sval, w->sval2, m, 0, kbits, s));
+    k_cap_heads<<<grid_for(m), 256, 0, s>>>(w->skey2, m, w->head);
+    tb = w->temp_bytes;
+    HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(w->temp, tb, w->head, w->hs, m, s));
+    k_cap_slots<<<grid_for(m), 256, 0, s>>>(w->skey2, w->sval2, w->head, w->hs, m, w->slot_of, w->ukey, w->fpos,
+                                            w->host_dev);
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipStreamSynchronize(s));
+    ns = static_cast<int>(host_word(w, kHNslots));
+    // predicates, mirror slots, the dependency components
+    k_cap_eval<<<wave_grid(ns), 256, 0, s>>>(w->ukey, ns, w->T, c->rmeta, c->iv, c->last_qcut, c->last_ncut, c->umax,
+                                             w->flags);
+    k_cap_mirror<<<grid_for(ns), 256, 0, s>>>(w->ukey, ns, w->T, w->t_of, w->mslot, w->upairs, w->err);
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, launch_uf_init(w->tpar, nt, s));
+    HIP_TRY(c, launch_uf_pair_list(w->tpar, w->upairs, ns, s));
+    HIP_TRY(c, launch_uf_finalize(w->tpar, nt, s));
+    k_cap_ckeys<<<grid_for(nt), 256, 0, s>>>(w->tpar, nt, w->ck);
+    tb = w->temp_bytes;
+    HIP_TRY(c, hipcub::DeviceRadixSort::SortKeys(w->temp, tb, w->ck, w->ck2, nt, 0, 50, s));
+    k_cap_recs<<<grid_for(m), 256, 0, s>>>(w->slot_of, w->ukey, w->fpos, w->flags, w->mslot, w->T, w->t_of, m, w->rec);
+    HIP_TRY(c, hipMemsetAsync(w->vis2, 0, static_cast<size_t>(ns), s));
+    // 4. the loops
+    k_cap_replay<<<wave_grid(nt), 256, 0, s>>>(w->ck2, nt, thr, w->toff, w->ioff, w->rec, w->fpos, w->vis2, w->pbrk,
+                                               w->own, w->err);
+    HIP_TRY(c, hipGetLastError());
+  } else if (nt > 0) {
+    // no T read has a hit: no loop breaks
+    k_fill<<<grid_for(nt), 256, 0, s>>>(w->pbrk, nt, kInf);
+    k_fill<<<grid_for(nt), 256, 0, s>>>(w->own, nt, 0);
+    HIP_TRY(c, hipGetLastError());
+  }
+  w->ns = ns;
+  // 5. the capped graph
+  HIP_TRY(c, hipMemsetAsync(w->formed, 0, static_cast<size_t>(n) * sizeof(int), s));
+  if (ne > 0) {
+    k_cap_classify<<<grid_for(ne), 256, 0, s>>>(c->edges, ne, w->t_of, w->pbrk, w->ukey, ns, w->fpos, w->vis2,
+                                                w->kflag, w->who, w->formed, w->stats, w->err);
+    size_t tb = 0;
+    HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tb, w->kflag, w->koff, static_cast<int>(ne), s));
+    if (int rc = ensure_temp(c, w, tb)) return rc;
+    tb = w->temp_bytes;
+    HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(w->temp, tb, w->kflag, w->koff, static_cast<int>(ne), s));
+    k_cap_compact<<<grid_for(ne), 256, 0, s>>>(c->edges, c->edge_iu, ne, w->who, w->koff, w->oedges, w->oiu);
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipMemcpyAsync(c->edges, w->oedges, static_cast<size_t>(ne) * sizeof(int2), hipMemcpyDeviceToDevice, s));
+    HIP_TRY(c, hipMemcpyAsync(c->edge_iu, w->oiu, static_cast<size_t>(ne) * sizeof(unsigned short),
+                              hipMemcpyDeviceToDevice, s));
+  }
+  k_cap_check<<<grid_for(std::max<int64_t>(n, nt)), 256, 0, s>>>(w->T, nt, w->own, w->pbrk, w->formed,
+                                                                 static_cast<int>(n), w->stats, w->err);
+  HIP_TRY(c, hipMemcpyAsync(c->fwd, w->formed, static_cast<size_t>(n) * sizeof(int), hipMemcpyDeviceToDevice, s));
+  k_cap_commit<<<1, 64, 0, s>>>(w->koff, w->kflag, ne, c->counters, c->errw, w->stats, w->err, w->host_dev);
+  HIP_TRY(c, hipGetLastError());
+  HIP_TRY(c, hipStreamSynchronize(s));
+  const long long err = host_word(w, kHErr);
+  if (err & kCapErrZd) return fail(c, FSLR_ERR_ZERO_DIVISION, "division by zero");
+  if (err & kCapErrState) return fail(c, FSLR_ERR_STATE, "edge cap replay: inconsistent loop replay");
+  cs->applied = 1;
+  cs->max_fwd = static_cast<int32_t>(host_word(w, kHStat + kStMaxFwd));
+  cs->candidates = w->nt;
+  cs->capped = host_word(w, kHStat + kStCapped);
+  cs->hits = w->nseq;
+  cs->pairs = ns;
+  cs->dropped = host_word(w, kHStat + kStDropped);
+  cs->backward = host_word(w, kHStat + kStBackward);
+  w->prepared = false;
+  return FSLR_OK;
+}
+
+// edge count, max forward degree; FSLR_OK and *binds = false when E* is the reference's graph
+int cap_peek(fslr_ctx* c, int thr, int64_t* ne, bool* binds) {
+  long long pk[3] = {0, 0, 0};
+  if (c->counters) {
+    if (int rc = peek_counts(c, pk)) return rc;
+  } else {
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+  }
+  if (pk[1] == FSLR_ERR_ZERO_DIVISION) return fail(c, FSLR_ERR_ZERO_DIVISION, "division by zero");
+  *ne = pk[0];
+  if (*ne > c->edge_cap) return fail(c, FSLR_ERR_STATE, "edge buffer overflowed; reserve and rerun the query");
+  *binds = !c->cap_stats.applied && pk[2] > thr;
+  if (!*binds && !c->cap_stats.applied) {
+    std::memset(&c->cap_stats, 0, sizeof(c->cap_stats));
+    c->cap_stats.max_fwd = static_cast<int32_t>(pk[2]);
+  }
+  return FSLR_OK;
 }
 
 }  // namespace
@@ -216,320 +1029,155 @@ int host_threads(int64_t work) {
 extern "C" int fslr_apply_edge_cap(fslr_ctx* c, int32_t thr, fslr_cap_stats* out) {
   if (!c) return FSLR_ERR_INVALID;
   HIP_TRY(c, hipSetDevice(c->device));
-  fslr_cap_stats cs;
-  std::memset(&cs, 0, sizeof(cs));
-  unsigned long long ne_u = 0;
-  int ew[4] = {};
-  if (c->counters) {
-    long long pk[3];
-    if (int rc = peek_counts(c, pk)) return rc;
-    ne_u = static_cast<unsigned long long>(pk[0]);
-    ew[0] = static_cast<int>(pk[1]);
-    ew[3] = static_cast<int>(pk[2]);
-  } else {
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-  }
-  if (ew[0] == FSLR_ERR_ZERO_DIVISION) return fail(c, FSLR_ERR_ZERO_DIVISION, "division by zero");
-  const int64_t ne = static_cast<int64_t>(ne_u);
-  if (ne > c->edge_cap) return fail(c, FSLR_ERR_STATE, "edge buffer overflowed; reserve and rerun the query");
-  cs.max_fwd = ew[3];
-  if (c->cap_stats.applied || ew[3] <= thr) {   // E* is the reference's graph (or already replayed)
-    if (!c->cap_stats.applied) c->cap_stats = cs;
+  int64_t ne = 0;
+  bool binds = false;
+  if (int rc = cap_peek(c, thr, &ne, &binds)) return rc;
+  if (!binds) {
     if (out) *out = c->cap_stats;
     return FSLR_OK;
   }
-  if (!c->last_full)
+  if (!c->last_full && !c->edges_global)
     return fail(c, FSLR_ERR_STATE, "the edge cap binds: its replay needs the last query to cover every read on "
-                                   "one context (fslr_query over [0, n_reads))");
-  if (int rc = ensure_walk_index(c)) return rc;       // the replayed loops walk qpos and the scan ranges
-  const int64_t n = c->n;
-  // FSLR_CAP_TIMING=1: host wall time per stage on stderr (diagnostics)
-  const bool timing = std::getenv("FSLR_CAP_TIMING") != nullptr;
-  auto t_last = std::chrono::steady_clock::now();
-  auto stage = [&](const char* what) {
-    if (!timing) return;
-    const auto now = std::chrono::steady_clock::now();
-    std::fprintf(stderr, "[cap] %-28s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(now - t_last).count());
-    t_last = now;
-  };
-  // uninitialised host arrays (the D2H copies fill them; zero-filling 0.2 GB at cfg5 cost ~40 ms)
-  std::unique_ptr<int[]> fwd_buf(new int[static_cast<size_t>(std::max<int64_t>(n, 1))]);
-  std::unique_ptr<int2[]> edges_buf(new int2[static_cast<size_t>(std::max<int64_t>(ne, 1))]);
-  std::unique_ptr<unsigned short[]> iu_buf(new unsigned short[static_cast<size_t>(std::max<int64_t>(ne, 1))]);
-  int* const fwd = fwd_buf.get();
-  int2* const edges = edges_buf.get();
-  unsigned short* const iu = iu_buf.get();
-  HIP_TRY(c, hipMemcpyAsync(fwd, c->fwd, n * sizeof(int), hipMemcpyDeviceToHost, c->stream));
-  if (ne) {
-    HIP_TRY(c, hipMemcpyAsync(edges, c->edges, ne * sizeof(int2), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipMemcpyAsync(iu, c->edge_iu, ne * sizeof(unsigned short), hipMemcpyDeviceToHost, c->stream));
-  }
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
+                                   "one context (fslr_query over [0, n_reads)) or fslr_cap_install_edges");
+  if (c->filter_active)
+    return fail(c, FSLR_ERR_STATE, "the index covers a chromosome subset: use fslr_cap_local / fslr_cap_replay");
+  if (int rc = ensure_bwd_ranges(c)) return rc;
+  CapWork* w = nullptr;
+  if (int rc = cap_work(c, &w)) return rc;
+  if (int rc = cap_local(c, thr, w, ne)) return rc;
+  w->nseq = w->nloc;
+  fslr_cap_stats cs;
+  std::memset(&cs, 0, sizeof(cs));
+  if (int rc = cap_core(c, w, &cs)) return rc;
+  c->cap_stats = cs;
+  if (out) *out = cs;
+  return FSLR_OK;
+}
 
-  // forward adjacency of E* (edges are (a, b), a < b, from the pair kernels); rows are filled by
-  // several threads, so a row's order is arbitrary (the closure below only counts over rows)
-  const int nth_e = host_threads(ne);
-  std::vector<int64_t> aoff(static_cast<size_t>(n) + 1, 0);
-  std::vector<char> bad(static_cast<size_t>(nth_e), 0);
-  parallel_ranges(ne, nth_e, [&](int tid, int64_t b, int64_t e) {
-    for (int64_t k = b; k < e; ++k) {
-      const int2 ed = edges[k];
-      if (ed.x >= ed.y || ed.x < 0 || ed.y >= n) {
-        bad[tid] = 1;
-        return;
-      }
-      __atomic_fetch_add(&aoff[ed.x + 1], 1, __ATOMIC_RELAXED);
-    }
-  });
-  for (char b : bad)
-    if (b) return fail(c, FSLR_ERR_STATE, "edge list is not E* (a < b)");
-  for (int64_t x = 0; x < n; ++x) aoff[x + 1] += aoff[x];
-  std::vector<int> adj(static_cast<size_t>(ne));
-  {
-    std::vector<int64_t> fill(aoff.begin(), aoff.end() - 1);
-    parallel_ranges(ne, nth_e, [&](int, int64_t b, int64_t e) {
-      for (int64_t k = b; k < e; ++k)
-        adj[__atomic_fetch_add(&fill[edges[k].x], 1, __ATOMIC_RELAXED)] = edges[k].y;
-    });
-  }
-  stage("D2H fwd + edges, adjacency");
-  // 1. candidate readers T (closure bound, rank order)
-  std::vector<int> back(static_cast<size_t>(n), 0);
-  std::vector<char> in_t(static_cast<size_t>(n), 0);
-  std::vector<int> T;
-  for (int64_t x = 0; x < n; ++x) {
-    if (fwd[x] + back[x] < thr) continue;
-    in_t[x] = 1;
-    T.push_back(static_cast<int>(x));
-    for (int64_t k = aoff[x]; k < aoff[x + 1]; ++k) ++back[adj[k]];
-  }
-  cs.candidates = static_cast<int64_t>(T.size());
-  const int nt = static_cast<int>(T.size());
+extern "C" int fslr_copy_edges_iu_device(fslr_ctx* c, int32_t* dst, int64_t n_pad) {
+  if (!c || (!dst && n_pad) || n_pad < 0) return FSLR_ERR_INVALID;
+  if (!c->reads_set) return fail(c, FSLR_ERR_STATE, "fslr_set_reads first");
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (n_pad == 0) return FSLR_OK;
+  if (!c->edge_cap) return fail(c, FSLR_ERR_STATE, "no query has run");
+  k_copy_edges_iu<<<grid_for(n_pad), 256, 0, c->stream>>>(c->edges, c->edge_iu, c->counters + kEdgeCount, c->edge_cap,
+                                                          reinterpret_cast<int4*>(dst), n_pad);
+  HIP_TRY(c, hipGetLastError());
+  return FSLR_OK;
+}
 
-  stage("closure T");
-  // 2. hit lists of the candidates from the device index
-  DevBuf d_reads, d_cnt, d_hits, d_nout;
-  HIP_TRY(c, hipMalloc(&d_reads.p, std::max(1, nt) * sizeof(int)));
-  HIP_TRY(c, hipMalloc(&d_cnt.p, std::max(1, nt) * sizeof(long long)));
-  HIP_TRY(c, hipMemcpyAsync(d_reads.p, T.data(), nt * sizeof(int), hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(c, launch_cap_hit_counts(static_cast<int*>(d_reads.p), nt, c->rmeta, c->qpos, c->rng_s,
-                                   static_cast<long long*>(d_cnt.p), c->stream));
-  std::vector<long long> hoff(static_cast<size_t>(nt) + 1, 0);
-  HIP_TRY(c, hipMemcpyAsync(hoff.data() + 1, d_cnt.p, nt * sizeof(long long), hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
-  for (int t = 0; t < nt; ++t) hoff[t + 1] += hoff[t];
-  const long long cap_hits = hoff[nt];
-  HIP_TRY(c, hipMemcpyAsync(d_cnt.p, hoff.data(), nt * sizeof(long long), hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(c, hipMalloc(&d_hits.p, std::max(1ll, cap_hits) * sizeof(int4)));
-  HIP_TRY(c, hipMalloc(&d_nout.p, std::max(1, nt) * sizeof(int)));
-  HIP_TRY(c, launch_cap_hit_emit(static_cast<int*>(d_reads.p), nt, static_cast<long long*>(d_cnt.p), c->rmeta,
-                                 c->qpos, c->rng_s, c->idx4, static_cast<int4*>(d_hits.p),
-                                 static_cast<int*>(d_nout.p), c->stream));
-  std::vector<int4> hits(static_cast<size_t>(cap_hits));
-  std::vector<int> nout(static_cast<size_t>(nt));
-  if (cap_hits) HIP_TRY(c, hipMemcpyAsync(hits.data(), d_hits.p, cap_hits * sizeof(int4), hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(c, hipMemcpyAsync(nout.data(), d_nout.p, nt * sizeof(int), hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
+extern "C" int fslr_cap_install_edges(fslr_ctx* c, const int32_t* rows, int64_t n_rows) {
+  if (!c || (!rows && n_rows) || n_rows < 0 || n_rows >= (int64_t(1) << 31)) return FSLR_ERR_INVALID;
+  if (!c->reads_set) return fail(c, FSLR_ERR_STATE, "fslr_set_reads first");
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  if (c->edge_cap < n_rows) {
+    if (int rc = fslr_reserve_edges(c, n_rows)) return rc;
+  }
+  if (!c->counters) return fail(c, FSLR_ERR_STATE, "no query has run");
+  CapWork* w = nullptr;
+  if (int rc = cap_work(c, &w)) return rc;
+  int *f = nullptr, *off = nullptr;
+  Carve cv;
+  cv.add(&f, n_rows);
+  cv.add(&off, n_rows);
+  if (int rc = cv.commit(c, w->ar[3])) return rc;
+  const int4* r4 = reinterpret_cast<const int4*>(rows);
+  HIP_TRY(c, hipMemsetAsync(c->fwd, 0, static_cast<size_t>(c->n) * sizeof(int), s));
+  if (n_rows > 0) {
+    k_cap_flag_rows<<<grid_for(n_rows), 256, 0, s>>>(r4, n_rows, f);
+    size_t tb = 0;
+    HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tb, f, off, static_cast<int>(n_rows), s));
+    if (int rc = ensure_temp(c, w, tb)) return rc;
+    tb = w->temp_bytes;
+    HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(w->temp, tb, f, off, static_cast<int>(n_rows), s));
+    k_cap_install<<<grid_for(n_rows), 256, 0, s>>>(r4, n_rows, f, off, c->edges, c->edge_iu, c->edge_cap, c->fwd);
+  }
+  k_cap_install_commit<<<1, 1024, 0, s>>>(off, f, n_rows, c->fwd, static_cast<int>(c->n), c->counters, c->errw);
+  HIP_TRY(c, hipGetLastError());
+  HIP_TRY(c, hipStreamSynchronize(s));
+  c->edges_global = true;
+  std::memset(&c->cap_stats, 0, sizeof(c->cap_stats));
+  return FSLR_OK;
+}
 
-  stage("hit lists (device) + D2H");
-  // search order of each interval: the stand-in sorts by (start asc, end desc, data position asc)
-  // and returns hits from the highest sorted position down.  Device positions of equal start are
-  // in data order, so reading an interval's hits backwards is that order except inside runs of
-  // equal start, which are stably re-sorted on (start asc, end desc) first.  seq: per read,
-  // partners in visit order, -1 after each interval; own intervals dropped (cluster.py:203-204).
-  // uq: per read, its distinct partners (sorted) — the pairs evaluated in step 3, flags aligned.
-  std::vector<int64_t> soff(static_cast<size_t>(nt) + 1, 0), uoff(static_cast<size_t>(nt) + 1, 0);
-  for (int t = 0; t < nt; ++t) {
-    soff[t + 1] = soff[t] + nout[t] + 64;            // hits + one separator per interval (<= 64)
-    uoff[t + 1] = uoff[t] + nout[t];
-  }
-  std::vector<int> seq(static_cast<size_t>(soff[nt]), -2);   // -2: unused tail of a read's slot
-  std::vector<int> uq(static_cast<size_t>(uoff[nt]));
-  std::vector<int> nuq(static_cast<size_t>(nt), 0);
-  parallel_for(nt, [&](int t0, int t1) {
-    std::vector<int> tmp;
-    for (int t = t0; t < t1; ++t) {
-      const int x = T[t];
-      int4* h = hits.data() + hoff[t];
-      const int cnt = nout[t];
-      int64_t w = soff[t];
-      tmp.clear();
-      int g0 = 0;
-      while (g0 < cnt) {
-        int g1 = g0 + 1;
-        bool ties = false;
-        while (g1 < cnt && h[g1].y == h[g0].y) {
-          ties |= h[g1].z == h[g1 - 1].z;
-          ++g1;
-        }
-        if (ties)
-          std::stable_sort(h + g0, h + g1, [](const int4& u, const int4& v) {
-            return u.z != v.z ? u.z < v.z : u.w > v.w;
-          });
-        for (int k = g1 - 1; k >= g0; --k)
-          if (h[k].x != x) {
-            seq[w++] = h[k].x;
-            tmp.push_back(h[k].x);
-          }
-        seq[w++] = -1;
-        g0 = g1;
-      }
-      std::sort(tmp.begin(), tmp.end());
-      tmp.erase(std::unique(tmp.begin(), tmp.end()), tmp.end());
-      std::copy(tmp.begin(), tmp.end(), uq.begin() + uoff[t]);
-      nuq[t] = static_cast<int>(tmp.size());
-    }
-  });
-  for (int t = 0; t < nt; ++t) cs.hits += nout[t];
-  std::vector<int4>().swap(hits);
-  // compact the distinct partner lists (pairs of step 3, one per (read of T, partner))
-  {
-    int64_t w = 0;
-    for (int t = 0; t < nt; ++t) {
-      std::copy(uq.begin() + uoff[t], uq.begin() + uoff[t] + nuq[t], uq.begin() + w);
-      uoff[t] = w;
-      w += nuq[t];
-    }
-    uoff[nt] = w;
-    uq.resize(static_cast<size_t>(w));
-  }
-  cs.pairs = static_cast<int64_t>(uq.size());
+extern "C" int fslr_cap_local(fslr_ctx* c, int32_t thr, int64_t* n_ti, int64_t* n_hits) {
+  if (!c || !n_ti || !n_hits) return FSLR_ERR_INVALID;
+  HIP_TRY(c, hipSetDevice(c->device));
+  *n_ti = *n_hits = 0;
+  if (!c->edges_global && !c->last_full)
+    return fail(c, FSLR_ERR_STATE, "fslr_cap_local needs every E* edge on this context (fslr_cap_install_edges)");
+  int64_t ne = 0;
+  bool binds = false;
+  if (int rc = cap_peek(c, thr, &ne, &binds)) return rc;
+  if (!binds) return fail(c, FSLR_ERR_STATE, "the edge cap does not bind");
+  if (int rc = ensure_bwd_ranges(c)) return rc;
+  CapWork* w = nullptr;
+  if (int rc = cap_work(c, &w)) return rc;
+  if (int rc = cap_local(c, thr, w, ne)) return rc;
+  *n_ti = w->nti;
+  *n_hits = w->nloc;
+  return FSLR_OK;
+}
 
-  stage("visit order + partner lists");
-  // 3. the full predicate of every (read of T, partner) pair
-  std::vector<int> flags(uq.size());
-  if (!uq.empty()) {
-    std::vector<int2> pv(uq.size());
-    parallel_for(nt, [&](int t0, int t1) {
-      for (int t = t0; t < t1; ++t)
-        for (int64_t k = uoff[t]; k < uoff[t + 1]; ++k) pv[k] = make_int2(std::min(T[t], uq[k]), std::max(T[t], uq[k]));
-    });
-    DevBuf d_pairs, d_flags;
-    HIP_TRY(c, hipMalloc(&d_pairs.p, pv.size() * sizeof(int2)));
-    HIP_TRY(c, hipMalloc(&d_flags.p, pv.size() * sizeof(int)));
-    HIP_TRY(c, hipMemcpyAsync(d_pairs.p, pv.data(), pv.size() * sizeof(int2), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(c, launch_eval_pairs(static_cast<int2*>(d_pairs.p), static_cast<long long>(pv.size()), c->rmeta, c->iv,
-                                 c->last_qcut, c->last_ncut, c->umax, static_cast<int*>(d_flags.p), c->stream));
-    HIP_TRY(c, hipMemcpyAsync(flags.data(), d_flags.p, flags.size() * sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-  }
-  std::vector<int> t_of(static_cast<size_t>(n), -1);
-  for (int t = 0; t < nt; ++t) t_of[T[t]] = t;
-  auto flag_of = [&](int x, int y) {   // x in T
-    const int t = t_of[x];
-    return flags[std::lower_bound(uq.begin() + uoff[t], uq.begin() + uoff[t + 1], y) - uq.begin()];
-  };
-
-  stage("pair predicates (device)");
-  // 4. the loops of T in rank order
-  std::vector<char> broke(static_cast<size_t>(n), 0);
-  std::vector<int64_t> roff(static_cast<size_t>(nt) + 1, 0);   // reached partners of read T[t] (sorted)
-  std::vector<int> reached;
-  std::vector<int> stamp(static_cast<size_t>(n), -1);
-  std::vector<int> own_edges(static_cast<size_t>(nt), 0);
-  auto reached_by = [&](int y, int x) {   // did broken read y's loop reach x?
-    const int t = t_of[y];
-    return std::binary_search(reached.begin() + roff[t], reached.begin() + roff[t + 1], x);
-  };
-  for (int t = 0; t < nt; ++t) {
-    const int x = T[t];
-    int edges_x = 0;
-    bool br = false;
-    const size_t r0 = reached.size();
-    for (int64_t k = soff[t]; k < soff[t + 1]; ++k) {
-      const int y = seq[k];
-      if (y == -2) break;                                      // end of this read's hits
-      if (y < 0) continue;                                     // next interval
-      if (stamp[y] == x) continue;                             // seen in this loop
-      if (y < x && (!broke[y] || reached_by(y, x))) continue;  // seen in y's loop
-      stamp[y] = x;
-      reached.push_back(y);
-      const int f = flag_of(x, y);
-      if (f & kFlagZd) return fail(c, FSLR_ERR_ZERO_DIVISION, "division by zero");
-      if (!(f & kFlagLenOk) || ((f >> 8) & 0xfff) == 0) continue;
-      if (f & kFlagEdge) ++edges_x;
-      if (edges_x >= thr) {
-        br = true;
-        while (k + 1 < soff[t + 1] && seq[k + 1] >= 0) ++k;   // leave this interval's hits
-      }
-    }
-    own_edges[t] = edges_x;
-    if (br) {
-      broke[x] = 1;
-      ++cs.capped;
-      std::sort(reached.begin() + static_cast<int64_t>(r0), reached.end());
-    } else {
-      reached.resize(r0);                                      // reached everything: not stored
-    }
-    roff[t + 1] = static_cast<int64_t>(reached.size());
-  }
-
-  stage("replay loops");
-  // E* pair (a, b) is an edge iff a's loop or, failing that, b's loop reaches it
-  // (in parallel: per-range codes and counts, then each range compacts at its scanned offset, so the
-  // kept edges stay in E* order)
-  std::vector<unsigned char> who(static_cast<size_t>(ne));          // 0 a's loop, 1 b's loop, 2 none
-  std::vector<int64_t> rkept(static_cast<size_t>(nth_e) + 1, 0), rdrop(static_cast<size_t>(nth_e), 0),
-      rback(static_cast<size_t>(nth_e), 0);
-  std::vector<int> formed(static_cast<size_t>(n), 0);
-  parallel_ranges(ne, nth_e, [&](int tid, int64_t b0, int64_t e0) {
-    int64_t kc = 0, dc = 0, bc = 0;
-    for (int64_t k = b0; k < e0; ++k) {
-      const int a = edges[k].x, b = edges[k].y;
-      unsigned char w = 2;
-      if (!broke[a] || reached_by(a, b)) w = 0;
-      else if (!broke[b] || reached_by(b, a)) w = 1;
-      who[k] = w;
-      if (w == 2) {
-        ++dc;
-        continue;
-      }
-      ++kc;
-      bc += w;
-      __atomic_fetch_add(&formed[w == 0 ? a : b], 1, __ATOMIC_RELAXED);
-    }
-    rkept[tid + 1] = kc;
-    rdrop[tid] = dc;
-    rback[tid] = bc;
-  });
-  for (int k = 0; k < nth_e; ++k) {
-    rkept[k + 1] += rkept[k];
-    cs.dropped += rdrop[k];
-    cs.backward += rback[k];
-  }
-  std::vector<int2> kept(static_cast<size_t>(rkept[nth_e]));
-  std::vector<unsigned short> kept_iu(kept.size());
-  parallel_ranges(ne, nth_e, [&](int tid, int64_t b0, int64_t e0) {
-    int64_t w = rkept[tid];
-    for (int64_t k = b0; k < e0; ++k) {
-      if (who[k] == 2) continue;
-      const int a = edges[k].x, b = edges[k].y;
-      kept[w] = who[k] == 0 ? make_int2(a, b) : make_int2(b, a);
-      kept_iu[w++] = iu[k];
-    }
-  });
-  int max_fwd = 0;
-  for (int64_t x = 0; x < n; ++x) {
-    if (in_t[x] && formed[x] != own_edges[t_of[x]])
-      return fail(c, FSLR_ERR_STATE, "edge cap replay: inconsistent edge count for read " + std::to_string(x));
-    max_fwd = std::max(max_fwd, formed[x]);
-  }
-  cs.applied = 1;
-  cs.max_fwd = max_fwd;
-
-  stage("classify edges");
-  // write the capped graph back: edges (former, partner), forward degree = edges formed per loop
-  const unsigned long long nk = kept.size();
-  if (nk) {
-    HIP_TRY(c, hipMemcpyAsync(c->edges, kept.data(), nk * sizeof(int2), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(c, hipMemcpyAsync(c->edge_iu, kept_iu.data(), nk * sizeof(unsigned short), hipMemcpyHostToDevice,
+extern "C" int fslr_cap_copy_local(fslr_ctx* c, int32_t* counts, int32_t* hits) {
+  if (!c || !c->capw || !c->capw->prepared) return c ? fail(c, FSLR_ERR_STATE, "fslr_cap_local first") : FSLR_ERR_INVALID;
+  CapWork* w = c->capw;
+  if ((!counts && w->nti) || (!hits && w->nloc)) return FSLR_ERR_INVALID;
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (w->nti)
+    HIP_TRY(c, hipMemcpyAsync(counts, w->icnt, static_cast<size_t>(w->nti) * sizeof(int), hipMemcpyDeviceToDevice,
                               c->stream));
+  if (w->nloc)
+    HIP_TRY(c, hipMemcpyAsync(hits, w->seq, static_cast<size_t>(w->nloc) * sizeof(int), hipMemcpyDeviceToDevice,
+                              c->stream));
+  return FSLR_OK;
+}
+
+extern "C" int fslr_cap_replay(fslr_ctx* c, const int32_t* counts, const int32_t* lists, int64_t pad, int32_t world,
+                               fslr_cap_stats* out) {
+  if (!c || world < 1 || pad < 0) return FSLR_ERR_INVALID;
+  if (!c->capw || !c->capw->prepared) return fail(c, FSLR_ERR_STATE, "fslr_cap_local first");
+  CapWork* w = c->capw;
+  if ((!counts && w->nti) || (!lists && pad)) return FSLR_ERR_INVALID;
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const int nti = static_cast<int>(w->nti);
+  const int64_t nall = static_cast<int64_t>(world) * nti;
+  if (nall >= (int64_t(1) << 31)) return fail(c, FSLR_ERR_INVALID, "too many T-intervals");
+  {
+    Carve cv;
+    cv.add(&w->loff, nall + 1);
+    if (int rc = cv.commit(c, w->ar[3])) return rc;
   }
-  HIP_TRY(c, hipMemcpyAsync(c->counters + kEdgeCount, &nk, sizeof(nk), hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(c, hipMemcpyAsync(c->fwd, formed.data(), n * sizeof(int), hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(c, hipMemcpyAsync(c->errw + 3, &max_fwd, sizeof(int), hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
-  stage("H2D capped graph");
+  // global counts and offsets, then each rank's segments into the sequence
+  k_cap_sum_counts<<<grid_for(nti + 1), 256, 0, s>>>(counts, world, nti, w->gsum);
+  size_t b1 = 0, b2 = 0;
+  HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(nullptr, b1, w->gsum, w->ioff, nti + 1, s));
+  HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(nullptr, b2, counts, w->loff, static_cast<int>(std::max<int64_t>(nall, 1)), s));
+  if (int rc = ensure_temp(c, w, std::max(b1, b2))) return rc;
+  size_t tb = w->temp_bytes;
+  HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(w->temp, tb, w->gsum, w->ioff, nti + 1, s));
+  if (nall > 0) {
+    tb = w->temp_bytes;
+    HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(w->temp, tb, counts, w->loff, static_cast<int>(nall), s));
+  }
+  k_cap_total<<<1, 64, 0, s>>>(w->ioff, nti, w->host_dev, kHNseq);
+  HIP_TRY(c, hipGetLastError());
+  HIP_TRY(c, hipStreamSynchronize(s));
+  w->nseq = host_word(w, kHNseq);
+  if (w->nseq >= (int64_t(1) << 31)) return fail(c, FSLR_ERR_NOMEM, "edge cap replay: more than 2^31 hits");
+  {
+    Carve cv;                          // the local list was copied out (fslr_cap_copy_local)
+    cv.add(&w->seq, w->nseq);
+    if (int rc = cv.commit(c, w->ar[4])) return rc;
+  }
+  if (nti > 0 && w->nseq > 0)
+    k_cap_assemble<<<wave_grid(nti), 256, 0, s>>>(counts, w->loff, lists, pad, world, nti, w->ioff, w->seq);
+  HIP_TRY(c, hipGetLastError());
+  fslr_cap_stats cs;
+  std::memset(&cs, 0, sizeof(cs));
+  if (int rc = cap_core(c, w, &cs)) return rc;
   c->cap_stats = cs;
   if (out) *out = cs;
   return FSLR_OK;

@@ -130,11 +130,12 @@ void fslr_ctx_destroy(fslr_ctx* c) {
                   c->temp,   c->umax,   c->edges,   c->edge_iu, c->fwd,     c->parent,  c->counters,
                   c->errw,   c->thr_tmp, c->defer,   c->dchrom,  c->drec,    c->lbounds, c->diag, c->wstat,
                   c->dgate,  c->chist,  c->heavy, c->ent, c->ent_sorted, c->sweep_temp, c->sw_tile, c->sw_wstat, c->ent_ub,
-                  c->fdchrom, c->fdrec, c->fdgate, c->crange_f, c->part_cnt, c->grp};
+                  c->fdchrom, c->fdrec, c->fdgate, c->crange_f, c->part_cnt, c->grp, c->fmap};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->sw_total) (void)hipHostFree(c->sw_total);
   fslr_long_free(c);
+  fslr_cap_free(c);
   if (c->ev_ok) {
     for (auto& e : c->ev) (void)hipEventDestroy(e);
     for (auto& e : c->kev) (void)hipEventDestroy(e);
@@ -285,9 +286,8 @@ int fslr_set_thresholds(fslr_ctx* c, const int32_t* thr) {
     HIP_TRY(c, launch_set_thr(c->thr_tmp, c->iv, c->qpos, c->index_built ? c->idx4 : nullptr, c->data_pos,
                               c->have_data_pos ? c->drec : nullptr, static_cast<int>(c->ni), c->stream));
     if (c->filter_active)                                                    // refresh the filtered records
-      HIP_TRY(c, launch_chrom_filter(c->dchrom, c->drec, c->dgate, c->filter_mask, static_cast<int>(c->ni),
-                                     c->fdchrom, c->fdrec, c->fdgate, c->vals2, c->vals, c->temp, c->temp_bytes,
-                                     c->stream));
+      HIP_TRY(c, launch_chrom_filter(c->dchrom, c->drec, c->dgate, c->fmap, static_cast<int>(c->ni), c->fdchrom,
+                                     c->fdrec, c->fdgate, c->vals2, c->vals, c->temp, c->temp_bytes, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
   }
   c->thr_mode = thr_mode_of(thr, c->ni);
@@ -378,6 +378,14 @@ int fslr::peek_counts(fslr_ctx* c, long long out[3]) {
   return FSLR_OK;
 }
 
+int fslr::ensure_bwd_ranges(fslr_ctx* c) {
+  if (!c->index_built) return fail(c, FSLR_ERR_STATE, "fslr_build_index first");
+  if (c->index_full || c->bwd_ranges) return FSLR_OK;
+  HIP_TRY(c, launch_index_bwd_ranges(index_bufs(c), static_cast<int>(c->ni_idx), c->stream));
+  c->bwd_ranges = true;
+  return FSLR_OK;
+}
+
 int fslr::ensure_walk_index(fslr_ctx* c) {
   if (!c->index_built || c->index_full) return FSLR_OK;
   if (c->filter_active) return fail(c, FSLR_ERR_STATE, "the walk engine needs every chromosome's index");
@@ -396,12 +404,13 @@ int fslr_build_index(fslr_ctx* c) {
   // the sweep engine's index only (the walk engine's parts follow on demand, ensure_walk_index)
   // where the data-order path applies and one context covers every query read
   const bool full = !c->filter_active && !(c->have_data_pos && c->n_chroms <= 64 && c->n_shards == 1);
-  HIP_TRY(c, launch_build_index(index_bufs(c), static_cast<int>(c->n), static_cast<int>(c->ni_idx), c->n_chroms, full,
-                                c->stream));
+  HIP_TRY(c, launch_build_index(index_bufs(c), static_cast<int>(c->n), static_cast<int>(c->ni_idx),
+                                c->filter_active ? c->n_chroms_f : c->n_chroms, full, c->stream));
   if (c->prof_phases) HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));
   c->t_index_rec = c->prof_phases;
   c->index_built = true;
   c->index_full = full;
+  c->bwd_ranges = full;
   c->built_shard = c->shard;
   c->built_n_shards = c->n_shards;
   return FSLR_OK;
@@ -607,6 +616,9 @@ static int prepare_query(fslr_ctx* c, const fslr_params* p) {
   HIP_TRY(c, launch_query_reset(c->counters, kNumCounters, c->errw, kErrWords, c->fwd, static_cast<int>(c->n),
                                 c->stream));
   std::memset(&c->cap_stats, 0, sizeof(c->cap_stats));
+  c->edges_global = false;
+  c->last_qcut = p->qlen_cut;                       // the cap replay's pair predicate
+  c->last_ncut = p->nal_cut;
   return FSLR_OK;
 }
 
@@ -689,16 +701,18 @@ int fslr_set_chrom_filter(fslr_ctx* c, const uint8_t* owned) {
     c->ni_idx = c->ni;
     return FSLR_OK;
   }
-  if (!c->have_data_pos || c->n_chroms > 64)
-    return fail(c, FSLR_ERR_INVALID, "a chromosome filter needs the start-sorted data order (iv_data_pos) and at "
-                                     "most 64 chromosomes");
-  std::vector<int2> cr(static_cast<size_t>(c->n_chroms));
-  unsigned long long mask = 0;
+  if (!c->have_data_pos)
+    return fail(c, FSLR_ERR_INVALID, "a chromosome filter needs the start-sorted data order (iv_data_pos)");
+  // the owned chromosomes are renumbered 0 .. k-1 (chromosome order) in the filtered index: the
+  // counting-sort build applies whenever a rank owns at most 64 of them, however many there are
+  std::vector<int2> cr;
+  std::vector<int> lmap(static_cast<size_t>(c->n_chroms), -1);
   int64_t acc = 0;
   for (int ch = 0; ch < c->n_chroms; ++ch) {
-    const int64_t k = owned[ch] ? c->chrom_counts[ch] : 0;
-    if (owned[ch]) mask |= 1ull << ch;
-    cr[ch] = make_int2(static_cast<int>(acc), static_cast<int>(acc + k));
+    if (!owned[ch]) continue;
+    lmap[ch] = static_cast<int>(cr.size());
+    const int64_t k = c->chrom_counts[ch];
+    cr.push_back(make_int2(static_cast<int>(acc), static_cast<int>(acc + k)));
     acc += k;
   }
   const int64_t nf = acc;
@@ -708,13 +722,22 @@ int fslr_set_chrom_filter(fslr_ctx* c, const uint8_t* owned) {
       return rc;
     c->f_cap = nf;
   }
-  if (!c->crange_f && (rc = dalloc(c, &c->crange_f, 64))) return rc;
-  HIP_TRY(c, hipMemcpyAsync(c->crange_f, cr.data(), cr.size() * sizeof(int2), hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(c, launch_chrom_filter(c->dchrom, c->drec, c->dgate, mask, static_cast<int>(c->ni), c->fdchrom, c->fdrec,
+  if (static_cast<int64_t>(std::max<size_t>(cr.size(), 1)) > c->crange_f_cap) {
+    if ((rc = dalloc(c, &c->crange_f, std::max<size_t>(cr.size(), 1)))) return rc;
+    c->crange_f_cap = static_cast<int64_t>(std::max<size_t>(cr.size(), 1));
+  }
+  if (c->n_chroms > c->fmap_cap) {
+    if ((rc = dalloc(c, &c->fmap, static_cast<size_t>(c->n_chroms)))) return rc;
+    c->fmap_cap = c->n_chroms;
+  }
+  if (!cr.empty())
+    HIP_TRY(c, hipMemcpyAsync(c->crange_f, cr.data(), cr.size() * sizeof(int2), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(c->fmap, lmap.data(), lmap.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, launch_chrom_filter(c->dchrom, c->drec, c->dgate, c->fmap, static_cast<int>(c->ni), c->fdchrom, c->fdrec,
                                  c->fdgate, c->vals2, c->vals, c->temp, c->temp_bytes, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   c->filter_active = true;
-  c->filter_mask = mask;
+  c->n_chroms_f = static_cast<int>(cr.size());
   c->ni_idx = nf;
   return FSLR_OK;
 }

@@ -18,16 +18,20 @@ struct fslr_ctx {
   int thr_mode = 0;
   bool reads_set = false, index_built = false, have_data_pos = false;
   bool index_full = false;                 // the walk engine's index parts exist (qpos, backward ranges)
+  bool bwd_ranges = false;                 // backward scan ranges exist (the cap replay's hits; no qpos)
   // multi-GPU sweep: the index covers the chromosomes of a filter (fslr_set_chrom_filter)
   bool filter_active = false;
-  unsigned long long filter_mask = 0;
+  int n_chroms_f = 0;                       // chromosomes the filter keeps (numbered 0 .. n_chroms_f - 1)
+  int* fmap = nullptr;                      // [n_chroms] its local number, -1 = another rank's
+  int fmap_cap = 0;
   int64_t ni_idx = 0;                       // positions of the index (ni, or the filtered count)
   std::vector<int64_t> chrom_counts;        // intervals per chromosome (set_reads)
   unsigned* fdchrom = nullptr;              // the filtered data-order arrays
   int4* fdrec = nullptr;
   int2* fdgate = nullptr;
   int64_t f_cap = 0;
-  int2* crange_f = nullptr;                 // [64] chromosome ranges of the filtered index
+  int2* crange_f = nullptr;                 // [n_chroms_f] chromosome ranges of the filtered index
+  int64_t crange_f_cap = 0;
   int* grp = nullptr;                       // [grp_ints()] grouping sort: bucket counts / offsets
   long long* part_cnt = nullptr;            // partition scratch: per (destination, block) counts + offsets
   int shard = 0, n_shards = 1;             // fslr_set_shard: A-side index data for this shard only
@@ -104,6 +108,8 @@ struct fslr_ctx {
   bool last_full = false;                // covered every read [0, n) with one shard
   double last_qcut = 0.0, last_ncut = 0.0;
   fslr_cap_stats cap_stats = {};
+  bool edges_global = false;             // every E* edge is on this context (fslr_cap_install_edges)
+  struct CapWork* capw = nullptr;        // the device cap replay's buffers (cap.hip)
   // reads of more than FSLR_MAX_L intervals (long.hip): the virtual-read map and the long-pair stage
   bool lg_set = false;
   int64_t lg_n_real = 0, lg_n_edges = 0;
@@ -141,6 +147,8 @@ struct fslr_ctx {
 
 // frees the long-read stage's buffers (long.hip)
 void fslr_long_free(fslr_ctx* c);
+// frees the cap replay's buffers (cap.hip)
+void fslr_cap_free(fslr_ctx* c);
 
 namespace fslr {
 
@@ -148,6 +156,8 @@ namespace fslr {
 int ensure_walk_index(fslr_ctx* c);
 // {edge count, error code, max forward degree} of the last query through pinned memory; syncs
 int peek_counts(fslr_ctx* c, long long out[3]);
+// the backward scan ranges of the (possibly chromosome-filtered) index, without the CSR map (capi.hip)
+int ensure_bwd_ranges(fslr_ctx* c);
 
 
 inline int fail(fslr_ctx* c, int code, const std::string& msg) {

@@ -506,6 +506,12 @@ static hipError_t launch_walk_parts(const IndexBufs& b, int n, int ni, hipStream
   return hipGetLastError();
 }
 
+hipError_t launch_index_bwd_ranges(const IndexBufs& b, int ni, hipStream_t s) {
+  if (ni <= 0) return hipSuccess;
+  k_tile_max<<<grid_for(ni, kTile), kTile, 0, s>>>(b.endkey, ni, b.pmaxkey);
+  return launch_walk_parts(b, 0, ni, s, false);
+}
+
 hipError_t launch_index_walk_parts(const IndexBufs& b, int n, int ni, hipStream_t s) {
   if (ni <= 0) return hipSuccess;
   return launch_walk_parts(b, n, ni, s, true);

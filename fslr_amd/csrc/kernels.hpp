@@ -107,6 +107,9 @@ hipError_t index_temp_bytes(int ni, size_t* bytes, hipStream_t s);
 hipError_t launch_build_index(const IndexBufs& b, int n_reads, int ni, int n_chroms, bool full, hipStream_t s);
 // the walk engine's parts of a sweep-only index (qpos, tile prefix, backward ranges)
 hipError_t launch_index_walk_parts(const IndexBufs& b, int n_reads, int ni, hipStream_t s);
+// the backward scan ranges alone (tile prefix of end + k_ranges<true>): no CSR map, so it also
+// serves a chromosome-filtered index
+hipError_t launch_index_bwd_ranges(const IndexBufs& b, int ni, hipStream_t s);
 // thresholds into iv[k].w and (when the index exists) idx4[qpos[k]].z
 hipError_t launch_set_thr(const int* thr, int4* iv, const int* qpos, int4* idx4, const int* data_pos,
                           int4* drec, int ni, hipStream_t s);
@@ -207,23 +210,12 @@ hipError_t launch_sweep_partition(const SweepArgs& a, int mode, int shift, int n
 
 // ---- multi-GPU sweep (shard.hip) -------------------------------------------------------------
 constexpr int kMaxDest = 64;          // destination ranks of one partition
-// the data-order records of the owned chromosomes, compacted in data order (stable)
-hipError_t launch_chrom_filter(const unsigned* dchrom, const int4* drec, const int2* dgate, unsigned long long owned,
-                               int ni, unsigned* fdchrom, int4* fdrec, int2* fdgate, int* flags, int* offs,
-                               void* temp, size_t temp_bytes, hipStream_t s);
+// the data-order records of the owned chromosomes (lmap[c] >= 0: its local number), compacted in
+// data order (stable), their chromosome renumbered lmap[c]
+hipError_t launch_chrom_filter(const unsigned* dchrom, const int4* drec, const int2* dgate, const int* lmap, int ni,
+                               unsigned* fdchrom, int4* fdrec, int2* fdgate, int* flags, int* offs, void* temp,
+                               size_t temp_bytes, hipStream_t s);
 
-
-// ---- edge-cap replay (cap.hip) --------------------------------------------------------------
-// per listed read: upper bound of its interval hits (sum over its intervals of the scan range)
-hipError_t launch_cap_hit_counts(const int* reads, int n, const int4* rmeta, const int* qpos, const int2* rng_s,
-                                 long long* counts, hipStream_t s);
-// per listed read, into hits[off[t] ..]: {partner, interval i, start, end} of every end-inclusive
-// overlap of its intervals (CSR order), each interval's hits in ascending index position; nout[t] = count
-hipError_t launch_cap_hit_emit(const int* reads, int n, const long long* off, const int4* rmeta, const int* qpos,
-                               const int2* rng_s, const int4* idx4, int4* hits, int* nout, hipStream_t s);
-// per pair (a, b): zd | lenok << 1 | edge << 2 | I << 8 | U << 20 (the reference's predicates in full)
-hipError_t launch_eval_pairs(const int2* pairs, long long n, const int4* rmeta, const int4* iv, double qcut,
-                             double ncut, const int* umax, int* flags, hipStream_t s);
 
 // ---- components (components.hip) ---------------------------------------------------------
 hipError_t launch_uf_init(int* parent, int n, hipStream_t s);

@@ -135,8 +135,9 @@ class SweepShard:
     step() leaves this rank's edges / forward degrees (pairs whose first read it owns) in ``ctx``
     and the global min-rank labels in ``ctx`` (labels()).  When the reference's edge cap binds
     (some read has more than ``edge_threshold`` forward edges) the graph depends on the sequential
-    order of the reference's loops: rank 0 then reruns the whole query on all chromosomes, replays
-    the cap (fslr_apply_edge_cap) and broadcasts the labels (``capped`` in the step's result).
+    order of the reference's loops: the ranks exchange the E* edges and the candidate reads' hit
+    lists and every rank replays the loops on its device (``capped`` in the step's result; ``ctx``
+    then holds the whole capped graph on every rank).
     """
 
     def __init__(self, ctx, n_reads: int, chrom_counts, world: int, rank: int, device, block_shift: int = 6,
@@ -232,18 +233,23 @@ class SweepShard:
         else:
             n_recv = sent_total
             entries = self.send
-        ctx.sweep_evaluate(qlen_cut, nal_cut, pass_table, entries, n_recv, edge_threshold)
-        st = ctx.stats(check=False)
-        while st['n_edges'] > st['edge_capacity']:
-            ctx.reserve_edges(int(st['n_edges'] * 1.25) + 4096)
+        err = None
+        st = {'max_fwd': 0, 'n_edges': 0}
+        try:
+            # a failure here (NOMEM growing a buffer, a HIP error) rides in the all_reduce below, so
+            # every rank raises instead of the others waiting in the next collective
             ctx.sweep_evaluate(qlen_cut, nal_cut, pass_table, entries, n_recv, edge_threshold)
             st = ctx.stats(check=False)
-        err = None
-        if st.get('error', 1) or st.get('overflow_flags', 1):   # only then read the stats again for the error
-            try:
+            while st['n_edges'] > st['edge_capacity']:
+                ctx.reserve_edges(int(st['n_edges'] * 1.25) + 4096)
+                ctx.sweep_evaluate(qlen_cut, nal_cut, pass_table, entries, n_recv, edge_threshold)
+                st = ctx.stats(check=False)
+            if st.get('error', 1) or st.get('overflow_flags', 1):   # only then read the stats again
                 ctx.stats()                             # raises on a device-side error (ZeroDivisionError)
-            except Exception as e:                      # noqa: BLE001 - re-raised on every rank below
-                err = e
+        except Exception as e:                          # noqa: BLE001 - re-raised on every rank below
+            if W == 1:
+                raise
+            err = e
         mf = int(st['max_fwd'])
         max_ne = int(st['n_edges'])
         if W > 1:
@@ -263,7 +269,7 @@ class SweepShard:
                'max_fwd': mf, 'capped': False, 'sweep_stats': sweep_stats}
         if mf > edge_threshold:
             out['capped'] = True
-            out['cap'] = self._capped_labels(qlen_cut, nal_cut, pass_table, edge_threshold)
+            out['cap'] = self._capped_labels(edge_threshold, max_ne)
             return out
         if W == 1:
             ctx.components()
@@ -279,32 +285,83 @@ class SweepShard:
         ctx.components_from_pairs(self.egath, W * m)
         return out
 
-    def _capped_labels(self, qlen_cut, nal_cut, pass_table, edge_threshold):
-        """The cap binds: the reference's graph is order dependent, so rank 0 replays it on the
-        whole input (one context, every chromosome) and broadcasts the labels."""
+    def _grow32(self, t, need):
+        import torch
+        if t is not None and t.numel() >= need:
+            return t
+        return torch.empty(int(need * 1.125) + 4096, dtype=torch.int32, device=self.device)
+
+    def _agree(self, err):
+        """MAX over ranks of an error code (0 none, 1 ZeroDivisionError, 2 other): every rank raises
+        together instead of leaving the others in the next collective."""
+        import torch
+        import torch.distributed as dist
+        code = 0 if err is None else (1 if isinstance(err, ZeroDivisionError) else 2)
+        if self.world > 1:
+            t = torch.tensor([code], dtype=torch.int64, device='cpu' if self._gloo() else self.device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            code = int(t.item())
+        if err is not None:
+            raise err
+        if code:
+            from ._lib import FslrError
+            raise ZeroDivisionError('division by zero') if code == 1 else FslrError('error on another rank')
+
+    def _capped_labels(self, edge_threshold, max_ne):
+        """The cap binds: the reference's graph depends on the sequential order of its loops
+        (cluster.py:197-224).  Every rank gathers the whole E* list and the search-ordered hits of the
+        candidate reads' intervals (each rank lists those of its chromosomes), then replays the loops
+        on its device (fslr_cap_replay) and takes the components: the same capped graph on every rank,
+        with no rank re-running the query."""
         import torch
         import torch.distributed as dist
         ctx, W = self.ctx, self.world
-        cap = {}
-        if self.rank == 0:
-            if W > 1:
-                ctx.set_chrom_filter(None)
-            ctx.build_index()
-            ctx.run_query(qlen_cut, nal_cut, pass_table, edge_threshold)
-            cap = ctx.apply_edge_cap(edge_threshold)
-            ctx.components()
-            if W > 1:
-                ctx.labels_into(self.local)
-                ctx.set_chrom_filter(self.owned)
+        m = max(1, int(max_ne))
+        err = None
+        try:
+            self.rsend = self._grow32(getattr(self, 'rsend', None), 4 * m)
+            ctx.edges_iu_into(self.rsend, m)
+        except Exception as e:                          # noqa: BLE001 - re-raised on every rank
+            err = e
+        self._agree(err)
+        self.rgath = self._grow32(getattr(self, 'rgath', None), 4 * W * m)
         if W > 1:
-            if self._gloo() and self.local.device.type != 'cpu':
-                h = self.local.cpu()
-                dist.broadcast(h, 0)
-                self.local.copy_(h)
-            else:
-                dist.broadcast(self.local, 0)
-            if self.rank != 0:
-                self._labels = self.local.cpu().numpy().astype(np.int32)
+            self._all_gather(self.rgath[:4 * W * m], self.rsend[:4 * m])
+            rows = self.rgath
+        else:
+            rows = self.rsend
+        nti = nh = 0
+        try:
+            ctx.cap_install_edges(rows, W * m)
+            nti, nh = ctx.cap_local(edge_threshold)
+        except Exception as e:                          # noqa: BLE001
+            err = e
+        self._agree(err)
+        pad = nh
+        if W > 1:
+            t = torch.tensor([nh], dtype=torch.int64, device='cpu' if self._gloo() else self.device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            pad = int(t.item())
+        pad = max(1, pad)
+        self.csend = self._grow32(getattr(self, 'csend', None), max(1, nti))
+        self.hsend = self._grow32(getattr(self, 'hsend', None), pad)
+        ctx.cap_copy_local(self.csend, self.hsend)
+        if W > 1:
+            self.cgath = self._grow32(getattr(self, 'cgath', None), max(1, W * nti))
+            self.hgath = self._grow32(getattr(self, 'hgath', None), W * pad)
+            if nti:
+                self._all_gather(self.cgath[:W * nti], self.csend[:nti])
+            self._all_gather(self.hgath[:W * pad], self.hsend[:pad])
+            counts, hits = self.cgath, self.hgath
+        else:
+            counts, hits = self.csend, self.hsend
+        cap = {}
+        try:
+            cap = ctx.cap_replay(counts, hits, pad, W)
+            ctx.components()
+        except Exception as e:                          # noqa: BLE001
+            err = e
+        self._agree(err)
         return cap
 
     def labels(self) -> np.ndarray:

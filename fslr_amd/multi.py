@@ -34,10 +34,12 @@ _CSR_FIELDS = ('read_off', 'read_qlen2', 'read_nal', 'iv_chrom', 'iv_start', 'iv
 
 
 def sweep_applies(csr, iv_thr) -> bool:
-    """The chromosome split runs the sweep engine: every folded overlap threshold >= 1 (overlap > 0)
-    and no aln_size == 0 interval.  Otherwise the query runs on one GPU."""
+    """The chromosome split runs the sweep engine over each rank's chromosome filter: every folded
+    overlap threshold >= 1 (overlap > 0), no aln_size == 0 interval and the intervals
+    in the start-sorted data order the filter compacts (fslr_set_chrom_filter; any number of
+    chromosomes).  Otherwise the query runs on one GPU."""
     t = np.asarray(iv_thr)
-    return bool(t.size == 0 or t.min() >= 1)
+    return bool((t.size == 0 or t.min() >= 1) and getattr(csr, 'start_sorted', True))
 
 
 def _free_port() -> int:

@@ -27,6 +27,12 @@
  *   fslr_copy_edges_device, fslr_components_from_pairs
  *                         (multi-GPU merge of the ranks' gathered edge lists: get_subgraphs,
  *                         cluster.py:230-234, over the union of the ranks' edges)
+ *   fslr_copy_edges_iu_device,
+ *   fslr_cap_install_edges,
+ *   fslr_cap_local,
+ *   fslr_cap_copy_local,
+ *   fslr_cap_replay      cluster.py:197-224 the edge cap (:223-224) replayed on a rank that holds every
+ *                         E* edge but indexes only its chromosomes (multi-GPU)
  *   fslr_set_long_reads,
  *   fslr_long_query,
  *   fslr_get_long_edges   cluster.py:140-170 overall_jaccard_similarity for reads of more than
@@ -62,7 +68,7 @@
 extern "C" {
 #endif
 
-#define FSLR_ABI_VERSION 6
+#define FSLR_ABI_VERSION 7
 #define FSLR_MAX_L 64                /* max intervals per read (bitmask width) */
 #define FSLR_MAX_READS (1 << 25)     /* read rank packs into bits 6..30 of the index record */
 #define FSLR_THR_ZERO_ALN INT32_MIN
@@ -210,7 +216,9 @@ int  fslr_query_shard(fslr_ctx *ctx, const fslr_params *params, int32_t shard, i
  * golden fixtures were made with: descending (start, -end, data position)) for the reads that can
  * reach the cap, drops the E* edges no loop reaches, re-orients edges as (read whose loop formed
  * it, partner) and sets forward degrees to the edges formed per loop.  No-op (no sync beyond one
- * counter read) when the cap does not bind.  Needs the last query to be fslr_query over all reads.
+ * counter read) when the cap does not bind.  Needs the last query to be fslr_query over all reads
+ * (or fslr_cap_install_edges on an unfiltered index).  The replay runs on the device: loops of
+ * different components of the candidates' partner graph are independent.
  * Call between fslr_query and fslr_components.  Syncs; out may be NULL. */
 int  fslr_apply_edge_cap(fslr_ctx *ctx, int32_t edge_threshold, fslr_cap_stats *out);
 /* cluster.py:230-234 — union-find over the edges: label = min rank in component.  Async. */
@@ -235,6 +243,25 @@ int  fslr_components(fslr_ctx *ctx);
  * fslr_set_reads.  Async; fslr_read_stats / fslr_components / fslr_get_edges follow as after
  * fslr_query. */
 int  fslr_set_chrom_filter(fslr_ctx *ctx, const uint8_t *owned);
+/* Multi-GPU edge cap (cluster.py:197-224).  The replayed loops need every E* edge
+ * and every hit of the reads that can reach the cap; a rank's index holds its chromosomes' hits.
+ * fslr_copy_edges_iu_device: this context's edges as int32 rows {a, b, I | U << 8, 0} into a device
+ *   buffer of n_pad rows, padded with a = -1 (async).  The ranks all-gather them.
+ * fslr_cap_install_edges: the n_rows gathered rows (device; a < 0 = padding) become this context's
+ *   edge list and forward degrees (as after a full query).  Syncs.
+ * fslr_cap_local: the replay's candidates, their intervals (*n_ti, the same on every rank) and the
+ *   search-ordered hits of the intervals this rank's index holds (*n_hits).  Syncs.
+ * fslr_cap_copy_local: counts[n_ti] (int32, 0 for other ranks' intervals) and hits[n_hits] (the
+ *   partner reads, interval after interval) into device buffers (async).  The ranks all-gather both:
+ *   counts as world x n_ti, hits padded to `pad` per rank.
+ * fslr_cap_replay: replay the loops from the gathered lists and write the capped graph into this
+ *   context as fslr_apply_edge_cap does (every rank gets the same graph).  Syncs; out may be NULL. */
+int  fslr_copy_edges_iu_device(fslr_ctx *ctx, int32_t *dst, int64_t n_pad);
+int  fslr_cap_install_edges(fslr_ctx *ctx, const int32_t *rows, int64_t n_rows);
+int  fslr_cap_local(fslr_ctx *ctx, int32_t edge_threshold, int64_t *n_ti, int64_t *n_hits);
+int  fslr_cap_copy_local(fslr_ctx *ctx, int32_t *counts, int32_t *hits);
+int  fslr_cap_replay(fslr_ctx *ctx, const int32_t *counts, const int32_t *hits, int64_t pad, int32_t world,
+                     fslr_cap_stats *out);
 int  fslr_sweep_partition(fslr_ctx *ctx, const fslr_params *params, int32_t n_dest, int32_t block_shift,
                           void *dst, int64_t dst_cap, int64_t *counts);
 int  fslr_sweep_evaluate(fslr_ctx *ctx, const fslr_params *params, const void *entries, int64_t n);

@@ -24,7 +24,7 @@ from fslr_amd.prep import FSLR_MAX_L, PASS_STRIDE
 class EmuSweepContext:
     def __init__(self, csr, iv_thr, qlen_diff=0.04, n_aln_diff=0.25, overlap=0.8):
         self.csr = csr
-        self.diffs = (qlen_diff, n_aln_diff, overlap)     # the cap fallback hands these to the oracle
+        self.diffs = (qlen_diff, n_aln_diff, overlap)     # the cap replay hands these to the oracle
         self.thr = np.asarray(iv_thr, dtype=np.int64)
         assert (self.thr >= 1).all(), 'the sweep split needs overlap thresholds >= 1'
         self.n_reads = csr.n_reads
@@ -183,10 +183,85 @@ class EmuSweepContext:
         for k in range(lab.size):
             self._union(k % n, int(lab[k]))
 
-    # -- the cap fallback (rank 0 reruns the whole query and replays the cap): the oracle's loops --
-    def run_query(self, qlen_cut, nal_cut, pass_table, edge_threshold=10, *a, **k):
-        self._full = (qlen_cut, nal_cut, edge_threshold)
-        return {}
+    # -- the multi-GPU edge cap (fslr_cap_*): E* rows, candidates, search-ordered hit lists --------
+    def edges_iu_into(self, t, n_pad):
+        e = self._edges[:n_pad]
+        rows = np.zeros((n_pad, 4), np.int32)
+        rows[:, :2] = -1
+        rows[:len(e), 0] = e[:, 0]
+        rows[:len(e), 1] = e[:, 1]
+        rows[:len(e), 2] = e[:, 2] | (e[:, 3] << 8)
+        t.numpy()[:4 * n_pad] = rows.reshape(-1)
+
+    def cap_install_edges(self, t, n_rows):
+        rows = t.numpy()[:4 * n_rows].reshape(-1, 4).astype(np.int64)
+        rows = rows[rows[:, 0] >= 0]
+        self._edges = np.stack([rows[:, 0], rows[:, 1], rows[:, 2] & 0xff, rows[:, 2] >> 8], axis=1)
+        self._fwd = np.bincount(rows[:, 0], minlength=self.n_reads)
+
+    def _candidates(self, thr):
+        """T: x joins when fwd(x) + #{y in T, y < x, (y, x) in E*} >= thr (rank order)."""
+        back = np.zeros(self.n_reads, np.int64)
+        adj = {}
+        for a, b in self._edges[:, :2].tolist():
+            adj.setdefault(a, []).append(b)
+        T = []
+        for x in range(self.n_reads):
+            if self._fwd[x] + back[x] >= thr:
+                T.append(x)
+                for y in adj.get(x, ()):
+                    back[y] += 1
+        return T
+
+    def _hit_lists(self, T, owned):
+        """Per interval of each read of T (CSR order): the partner reads of its end-inclusive hits in
+        the stand-in's search order (descending (start, -end, data position)), own read dropped."""
+        c = self.csr
+        chrom = np.asarray(c.iv_chrom)
+        st, en = np.asarray(c.iv_start, np.int64), np.asarray(c.iv_end, np.int64)
+        dp = np.asarray(c.data_pos, np.int64)
+        off = np.asarray(c.read_off, np.int64)
+        out = []
+        for x in T:
+            for k in range(off[x], off[x + 1]):
+                if owned is not None and not owned[chrom[k]]:
+                    out.append([])
+                    continue
+                h = np.flatnonzero((chrom == chrom[k]) & (st <= en[k]) & (en >= st[k]) & (self.read_of != x))
+                order = sorted(h.tolist(), key=lambda p: (st[p], -en[p], dp[p]), reverse=True)
+                out.append([int(self.read_of[p]) for p in order])
+        return out
+
+    def cap_local(self, edge_threshold=10):
+        self._cap_thr = edge_threshold
+        self._T = self._candidates(edge_threshold)
+        lists = self._hit_lists(self._T, self.owned)
+        self._cap_counts = np.array([len(x) for x in lists], np.int32)
+        self._cap_hits = np.array([y for x in lists for y in x], np.int32)
+        return int(self._cap_counts.size), int(self._cap_hits.size)
+
+    def cap_copy_local(self, counts, hits):
+        counts.numpy()[:self._cap_counts.size] = self._cap_counts
+        hits.numpy()[:self._cap_hits.size] = self._cap_hits
+
+    def cap_replay(self, counts, hits, pad, world):
+        """Assemble the ranks' lists (each rank: its intervals' segments in interval order) and check
+        them against the lists of an unfiltered index; then the capped graph is the oracle's loop."""
+        nti = self._cap_counts.size
+        cnt = counts.numpy()[:world * nti].reshape(world, nti)
+        assert ((cnt > 0).sum(axis=0) <= 1).all(), 'an interval listed by two ranks'
+        hv = hits.numpy()[:world * pad].reshape(world, pad)
+        pos = [0] * world
+        got = []
+        for ti in range(nti):
+            seg = []
+            for w in range(world):
+                m = int(cnt[w, ti])
+                seg += hv[w, pos[w]:pos[w] + m].tolist()
+                pos[w] += m
+            got.append(seg)
+        assert got == self._hit_lists(self._T, None)
+        return self.apply_edge_cap(self._cap_thr)
 
     def apply_edge_cap(self, edge_threshold=10):
         from oracle import oracle as O
@@ -197,4 +272,7 @@ class EmuSweepContext:
         qd, nd, ov = self.diffs
         o = O.run_core(oc, overlap=ov, use_cap=True, qlen_diff=qd, n_aln_diff=nd, edge_threshold=edge_threshold)
         self._edges = np.stack([o['edge_a'], o['edge_b'], o['edge_I'], o['edge_U']], axis=1).astype(np.int64)
+        self._fwd = np.asarray(o['fwd'], np.int64)
+        self._st = {'n_edges': len(self._edges), 'edge_capacity': self.edge_capacity,
+                    'max_fwd': int(self._fwd.max()) if self._fwd.size else 0}
         return {'applied': 1}

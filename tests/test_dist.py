@@ -239,7 +239,7 @@ def _sweep_worker(rank, world, port, csr, thr, out_dir, edge_threshold):
     sh = SweepShard(ctx, csr.n_reads, chrom_counts_of(csr), world, rank, 'cpu')
     info = sh.step(1 - 0.04, 1 - 0.25, pass_table([1, 1, 0.66, 0.66, 0.66, 0.5]), edge_threshold)
     np.save(os.path.join(out_dir, f'labels{rank}.npy'), sh.labels())
-    a, b, I, U = ctx.edges(ctx.stats().get('n_edges', 0)) if not info['capped'] else (np.zeros(0),) * 4
+    a, b, I, U = ctx.edges(ctx.stats().get('n_edges', 0))
     np.save(os.path.join(out_dir, f'edges{rank}.npy'), np.stack([a, b, I, U], axis=1) if len(a) else np.zeros((0, 4)))
     np.save(os.path.join(out_dir, f'info{rank}.npy'), np.array([info['capped'], info['max_fwd']]))
     dist.barrier()
@@ -250,8 +250,10 @@ def _sweep_worker(rank, world, port, csr, thr, out_dir, edge_threshold):
 def test_gloo_world2_sweep_shard_equals_oracle(world_case, tmp_path, edge_threshold):
     """dist.SweepShard over gloo with world_size 2 (real all_to_all of entries, all-reduce of the
     forward degree, all-gather of labels) on the emulated device: both ranks end with the oracle's
-    components; the ranks' edges partition the oracle's edges.  edge_threshold 2 makes the cap bind,
-    which takes the rank-0 replay and label broadcast."""
+    components; the ranks' edges partition the oracle's edges.  edge_threshold 2 makes the cap bind:
+    the ranks all-gather E* and the candidates' hit lists (each rank lists its chromosomes' hits; the
+    emulator checks the assembled lists against an unfiltered index) and every rank holds the
+    oracle's capped graph."""
     import torch.multiprocessing as mp
     from fslr_amd.prep import fold_overlap_threshold
     csr, o = world_case
@@ -271,6 +273,22 @@ def test_gloo_world2_sweep_shard_equals_oracle(world_case, tmp_path, edge_thresh
         got = sorted(map(tuple, e.tolist()))
         want = sorted(zip(o['edge_a'].tolist(), o['edge_b'].tolist(), o['edge_I'].tolist(), o['edge_U'].tolist()))
         assert got == want
+    else:
+        want = sorted(zip(ref['edge_a'].tolist(), ref['edge_b'].tolist(), ref['edge_I'].tolist(),
+                          ref['edge_U'].tolist()))
+        for r in range(2):                              # every rank holds the whole capped graph
+            got = sorted(map(tuple, np.load(tmp_path / f'edges{r}.npy').astype(np.int64).tolist()))
+            assert got == want
+
+
+def _one_stream():
+    """One non-default torch stream, made current and shared with every context of a test: the
+    in-process 'collectives' (torch.cat of device buffers) then run in order with the kernels that
+    write and read those buffers (each context otherwise owns a stream of its own)."""
+    import torch
+    s = torch.cuda.Stream(torch.device('cuda', 0))
+    torch.cuda.set_stream(s)
+    return s
 
 
 def _sweep_split_on_device(csr, thr, pt, W, edge_threshold=10, block_shift=6):
@@ -281,11 +299,12 @@ def _sweep_split_on_device(csr, thr, pt, W, edge_threshold=10, block_shift=6):
     from fslr_amd import _lib
     from fslr_amd.dist import chrom_counts_of, chrom_owner
     dev = torch.device('cuda', 0)
+    stream = _one_stream()                         # torch's copies and the contexts' kernels in order
     owner = chrom_owner(chrom_counts_of(csr), W)
     segs = [[] for _ in range(W)]
     sent = []
     for r in range(W):
-        c = _lib.Context(0)
+        c = _lib.Context(0, stream=stream.cuda_stream)
         c.load_csr(csr, thr)
         c.set_chrom_filter(owner == r)
         c.build_index()
@@ -302,7 +321,7 @@ def _sweep_split_on_device(csr, thr, pt, W, edge_threshold=10, block_shift=6):
         c.close()
     ctxs = []
     for d in range(W):
-        c = _lib.Context(0)
+        c = _lib.Context(0, stream=stream.cuda_stream)
         c.load_csr(csr, thr)
         c.reserve_edges(12 * csr.n_reads)
         ent = torch.cat(segs[d]) if segs[d] else torch.empty(0, dtype=torch.int64, device=dev)
@@ -355,6 +374,100 @@ def test_sweep_split_contexts_one_gpu_equals_oracle(W):
     # every rank sent something and the chromosome split is roughly balanced
     per_rank = sent.sum(axis=1)
     assert per_rank.min() > 0 and per_rank.max() < 2.0 * per_rank.mean()
+
+
+def _sweep_split_capped_on_device(csr, thr, pt, W, edge_threshold, block_shift=6):
+    """The chromosome split with a binding cap, W contexts on cuda:0, every exchange done in-process
+    as the collectives would (torch.cat of the ranks' buffers): partition, evaluate, then the cap
+    exchange of SweepShard._capped_labels — E* rows, candidates' hit lists of each rank's
+    chromosomes, a replay on every rank.  No context runs fslr_query.  Returns the contexts."""
+    import torch
+    from fslr_amd import _lib
+    from fslr_amd.dist import chrom_counts_of, chrom_owner
+    dev = torch.device('cuda', 0)
+    stream = _one_stream()
+    owner = chrom_owner(chrom_counts_of(csr), W)
+    ctxs, segs = [], [[] for _ in range(W)]
+    for r in range(W):
+        c = _lib.Context(0, stream=stream.cuda_stream)
+        c.load_csr(csr, thr)
+        c.reserve_edges(12 * csr.n_reads)
+        c.set_chrom_filter(owner == r if W > 1 else None)
+        c.build_index()
+        buf = torch.empty(1 << 16, dtype=torch.int64, device=dev)
+        ok, counts = c.sweep_partition(1 - 0.04, 1 - 0.25, pt, W, block_shift, buf, edge_threshold)
+        if not ok:
+            buf = torch.empty(int(counts.sum()) + 16, dtype=torch.int64, device=dev)
+            ok, counts = c.sweep_partition(1 - 0.04, 1 - 0.25, pt, W, block_shift, buf, edge_threshold)
+        assert ok
+        pos = np.concatenate([[0], np.cumsum(counts)])
+        for d in range(W):
+            segs[d].append(buf[pos[d]:pos[d + 1]].clone())
+        ctxs.append(c)
+    for d, c in enumerate(ctxs):
+        ent = torch.cat(segs[d])
+        c.sweep_evaluate(1 - 0.04, 1 - 0.25, pt, ent, ent.numel(), edge_threshold)
+    torch.cuda.synchronize()
+    ne = [c.stats()['n_edges'] for c in ctxs]
+    assert max(c.stats()['max_fwd'] for c in ctxs) > edge_threshold          # the cap binds
+    m = max(1, max(ne))
+    rows = []
+    for c in ctxs:
+        t = torch.empty(4 * m, dtype=torch.int32, device=dev)
+        c.edges_iu_into(t, m)
+        rows.append(t)
+    torch.cuda.synchronize()
+    gathered = torch.cat(rows)
+    loc = []
+    for c in ctxs:
+        c.cap_install_edges(gathered, W * m)
+        loc.append(c.cap_local(edge_threshold))
+    nti = loc[0][0]
+    assert all(x[0] == nti for x in loc)
+    pad = max(1, max(x[1] for x in loc))
+    cnts, hits = [], []
+    for c in ctxs:
+        cnts.append(torch.zeros(max(1, nti), dtype=torch.int32, device=dev))
+        hits.append(torch.full((pad,), -7, dtype=torch.int32, device=dev))
+        c.cap_copy_local(cnts[-1], hits[-1])
+    torch.cuda.synchronize()
+    cg = torch.cat([x[:nti] for x in cnts]) if nti else cnts[0]
+    hg = torch.cat(hits)
+    caps = []
+    for c in ctxs:
+        caps.append(c.cap_replay(cg, hg, pad, W))
+        c.components()
+    torch.cuda.synchronize()
+    assert all(cp['applied'] == 1 for cp in caps) and all(cp == caps[0] for cp in caps)
+    return ctxs, caps[0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('W', [1, 2, 8])
+@pytest.mark.parametrize('thr', [3, 10])
+def test_sweep_split_capped_one_gpu_equals_oracle(W, thr):
+    """The cap replay of the multi-GPU split (each rank lists the hits of its chromosomes, every rank
+    replays): on a dense input where the cap binds for many reads, every rank's capped graph (edges
+    as (former, partner, I, U), edges per loop, components) equals the oracle's reference loop."""
+    import dataclasses
+    from fslr_amd.prep import fold_overlap_threshold, pass_table
+    s = synth.generate(20_000, 16, 47, cluster_cap=30, size_p=0.05)
+    csr = s.interval_data().csr()
+    st = csr.iv_start.astype(np.int64) // 100
+    en = st + (csr.iv_end.astype(np.int64) - csr.iv_start)
+    csr = dataclasses.replace(csr, iv_start=st.astype(np.int32), iv_end=en.astype(np.int32))
+    thr_iv = fold_overlap_threshold(csr.iv_aln, 0.8)
+    pt = pass_table([1, 1, 0.66, 0.66, 0.66, 0.5])
+    o = O.run_core(_oracle_csr(csr), edge_threshold=thr, use_cap=True)
+    ctxs, cap = _sweep_split_capped_on_device(csr, thr_iv, pt, W, thr)
+    assert cap['capped'] > 0 and cap['dropped'] > 0
+    want = sorted(zip(o['edge_a'].tolist(), o['edge_b'].tolist(), o['edge_I'].tolist(), o['edge_U'].tolist()))
+    for c in ctxs:
+        a, b, I, U = c.edges(c.stats()['n_edges'])
+        assert sorted(zip(a.tolist(), b.tolist(), I.tolist(), U.tolist())) == want
+        np.testing.assert_array_equal(c.fwd_degree(), o['fwd'])
+        np.testing.assert_array_equal(_components_from_labels(c.labels()), o['comp'])
+        c.close()
 
 
 def _sweep_gpu_worker(rank, world, port, out_dir):
