@@ -34,7 +34,7 @@ EXPORTED = ['fslr_abi_version', 'fslr_last_error', 'fslr_ctx_create', 'fslr_ctx_
             'fslr_get_pair_kernel_times', 'fslr_set_chrom_filter', 'fslr_sweep_partition', 'fslr_sweep_evaluate',
             'fslr_copy_edges_device', 'fslr_components_from_pairs', 'fslr_set_long_reads', 'fslr_long_query',
             'fslr_get_long_edges', 'fslr_copy_edges_iu_device', 'fslr_cap_install_edges', 'fslr_cap_local',
-            'fslr_cap_copy_local', 'fslr_cap_replay']
+            'fslr_cap_copy_local', 'fslr_cap_replay', 'fslr_get_stage_kernel_times']
 
 
 class HipUnavailable(RuntimeError):
@@ -133,6 +133,7 @@ def load(path: str = LIB_PATH):
         'fslr_finalize_labels': (ctypes.c_int, [vp]),
         'fslr_apply_edge_cap': (ctypes.c_int, [vp, i32, ctypes.POINTER(CapStats)]),
         'fslr_get_pair_kernel_times': (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_float), i32]),
+        'fslr_get_stage_kernel_times': (ctypes.c_int, [vp, i32, ctypes.POINTER(ctypes.c_float), i32]),
         'fslr_set_chrom_filter': (ctypes.c_int, [vp, vp]),
         'fslr_sweep_partition': (ctypes.c_int, [vp, ctypes.POINTER(Params), i32, i32, vp, i64,
                                                 ctypes.POINTER(ctypes.c_int64)]),
@@ -412,6 +413,16 @@ class Context:
         """Durations (ms) of the main pair-kernel launch of the last ``n`` queries (profiling contexts)."""
         out = np.zeros(n, np.float32)
         got = self._L.fslr_get_pair_kernel_times(self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), n)
+        if got < 0:
+            self._check(-got)
+        return out[:got]
+
+    def stage_kernel_times(self, stage: int, n: int = 256) -> np.ndarray:
+        """Durations (ms) of one stage kernel of the last ``n`` queries: 0 the main pair kernel, 1 the sweep
+        engine's pair-stage kernel (profiling contexts)."""
+        out = np.zeros(n, np.float32)
+        got = self._L.fslr_get_stage_kernel_times(self._h, int(stage),
+                                                  out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), n)
         if got < 0:
             self._check(-got)
         return out[:got]

@@ -17,7 +17,8 @@ namespace {
 int ensure_capacity(fslr_ctx* c, int64_t n, int64_t ni, int n_chroms) {
   int rc;
   if (n > c->cap_n) {
-    if ((rc = dalloc(c, &c->rmeta, n)) || (rc = dalloc(c, &c->fwd, n)) || (rc = dalloc(c, &c->parent, n)) ||
+    if ((rc = dalloc(c, &c->rmeta, n)) || (rc = dalloc(c, &c->rlen8, n)) || (rc = dalloc(c, &c->fwd, n)) ||
+        (rc = dalloc(c, &c->parent, n)) ||
         (rc = dalloc(c, &c->heavy, n)) ||
         (rc = dalloc(c, &c->lbounds, n)))
       return rc;
@@ -125,7 +126,7 @@ void fslr_ctx_destroy(fslr_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* bufs[] = {c->rmeta,  c->iv,     c->qpos,    c->rng_s,  c->idx4,    c->idx_gate, c->data_pos, c->s_start,
+  void* bufs[] = {c->rmeta,  c->rlen8, c->iv,     c->qpos,    c->rng_s,  c->idx4,    c->idx_gate, c->data_pos, c->s_start,
                   c->crange, c->keys,   c->keys2,   c->vals,    c->vals2,   c->endkey,  c->pmaxkey,
                   c->temp,   c->umax,   c->edges,   c->edge_iu, c->fwd,     c->parent,  c->counters,
                   c->errw,   c->thr_tmp, c->defer,   c->dchrom,  c->drec,    c->lbounds, c->diag, c->wstat,
@@ -139,6 +140,7 @@ void fslr_ctx_destroy(fslr_ctx* c) {
   if (c->ev_ok) {
     for (auto& e : c->ev) (void)hipEventDestroy(e);
     for (auto& e : c->kev) (void)hipEventDestroy(e);
+    for (auto& e : c->kev2) (void)hipEventDestroy(e);
     for (auto& e : c->sw_ev) (void)hipEventDestroy(e);
   }
   if (c->own_stream) (void)hipStreamDestroy(c->stream);
@@ -152,6 +154,8 @@ int fslr_set_profiling(fslr_ctx* c, int enable) {
     for (auto& e : c->ev) HIP_TRY(c, hipEventCreate(&e));
     c->kev.assign(2 * fslr_ctx::kKernRing, nullptr);
     for (auto& e : c->kev) HIP_TRY(c, hipEventCreate(&e));
+    c->kev2.assign(2 * fslr_ctx::kKernRing, nullptr);
+    for (auto& e : c->kev2) HIP_TRY(c, hipEventCreate(&e));
     for (auto& e : c->sw_ev) HIP_TRY(c, hipEventCreate(&e));
     c->ev_ok = true;
   }
@@ -172,6 +176,7 @@ int fslr_set_reads(fslr_ctx* c, const fslr_reads* r) {
   if (r->read_off[0] != 0 || r->read_off[n] != ni)
     return fail(c, FSLR_ERR_INVALID, "read_off does not span intervals");
   std::vector<int4> rm(static_cast<size_t>(n));
+  std::vector<unsigned char> rl(static_cast<size_t>(n));
   std::vector<int4> iv(static_cast<size_t>(ni));
   std::vector<unsigned char> zero(static_cast<size_t>(ni), 0);
   for (int64_t k = 0; k < ni; ++k) {
@@ -194,6 +199,7 @@ int fslr_set_reads(fslr_ctx* c, const fslr_reads* r) {
     for (int k = o; k < o + len; ++k)
       if (zero[k]) flags |= 1;
     rm[i] = make_int4(o, len | (flags << 16), r->read_qlen2[i], r->read_nal[i]);
+    rl[i] = static_cast<unsigned char>(len);
   }
   // chromosome ranges of the (chrom, start)-sorted index: chromosome ids ascending (host counts)
   std::vector<int2> cr(static_cast<size_t>(r->n_chroms), make_int2(0, 0));
@@ -261,6 +267,7 @@ int fslr_set_reads(fslr_ctx* c, const fslr_reads* r) {
   c->any_zero_aln = std::find(zero.begin(), zero.end(), 1) != zero.end();
   c->aln_zero_host.swap(zero);
   if (n) HIP_TRY(c, hipMemcpyAsync(c->rmeta, rm.data(), n * sizeof(int4), hipMemcpyHostToDevice, c->stream));
+  if (n) HIP_TRY(c, hipMemcpyAsync(c->rlen8, rl.data(), n, hipMemcpyHostToDevice, c->stream));
   if (ni) HIP_TRY(c, hipMemcpyAsync(c->iv, iv.data(), ni * sizeof(int4), hipMemcpyHostToDevice, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   c->reads_set = true;
@@ -473,6 +480,7 @@ static int sweep_front(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64
   if ((rc = ensure_grp(c))) return rc;
   s.grp = c->grp;
   s.rmeta = c->rmeta;
+  s.rlen8 = c->rlen8;
   s.idx4 = c->idx4;
   s.idx_gate = c->idx_gate;
   s.rng_s = c->rng_s;
@@ -513,6 +521,7 @@ static int sweep_front(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64
     if (mode == 2) HIP_TRY(c, launch_sweep_plan(s, c->stream));
     s.k0 = e0;                                       // the pair-kernel ring: the sweep kernel alone
     s.k1 = e1;
+    s.p0 = s.p1 = nullptr;
     if (c->prof_phases) HIP_TRY(c, hipEventRecord(c->sw_ev[0], c->stream));
     // a repeat of the last synchronous query on unchanged input: same entry count, no readback
     const bool fast = !defer && mode == 2 && attempt == 0 && c->sw_prev_gen == c->input_gen &&
@@ -574,6 +583,11 @@ static int sweep_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_
   int mode = 2;
   int rc = sweep_front(c, p, a_begin, a_end, e0, e1, s, mode);
   if (rc) return rc;
+  if (e0) {                                          // profiling: the pair-stage kernel's ring too
+    const int slot = static_cast<int>(c->n_kern2++ % fslr_ctx::kKernRing);
+    s.p0 = c->kev2[2 * slot];
+    s.p1 = c->kev2[2 * slot + 1];
+  }
   HIP_TRY(c, launch_sweep_pairs(s, mode, c->stream));
   c->sw_ev_rec = c->prof_phases;
   return FSLR_OK;
@@ -811,8 +825,10 @@ int fslr_sweep_evaluate(fslr_ctx* c, const fslr_params* p, const void* entries, 
   c->last_engine = FSLR_ENGINE_SWEEP;
   if (int rc = ensure_grp(c)) return rc;
   SweepArgs s{};
+  s.p0 = s.p1 = nullptr;
   s.grp = c->grp;
   s.rmeta = c->rmeta;
+  s.rlen8 = c->rlen8;
   s.umax = c->umax;
   s.ni = 0;
   s.n_reads = static_cast<int>(c->n);
@@ -957,20 +973,24 @@ int fslr_get_timings(fslr_ctx* c, fslr_timings* out) {
   return FSLR_OK;
 }
 
-int fslr_get_pair_kernel_times(fslr_ctx* c, float* ms, int32_t n) {
-  if (!c || (!ms && n > 0) || n < 0) return -FSLR_ERR_INVALID;
+int fslr_get_stage_kernel_times(fslr_ctx* c, int32_t stage, float* ms, int32_t n) {
+  if (!c || (!ms && n > 0) || n < 0 || stage < 0 || stage > 1) return -FSLR_ERR_INVALID;
   if (!c->ev_ok) return 0;
   if (hipSetDevice(c->device) != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess)
     return -fail(c, FSLR_ERR_HIP, "sync");
-  const int64_t have = std::min<int64_t>(c->n_kern, fslr_ctx::kKernRing);
+  const std::vector<hipEvent_t>& ring = stage == 0 ? c->kev : c->kev2;
+  const int64_t cnt = stage == 0 ? c->n_kern : c->n_kern2;
+  const int64_t have = std::min<int64_t>(cnt, fslr_ctx::kKernRing);
   const int k = static_cast<int>(std::min<int64_t>(have, n));
   for (int i = 0; i < k; ++i) {
-    const int slot = static_cast<int>((c->n_kern - k + i) % fslr_ctx::kKernRing);
-    if (hipEventElapsedTime(&ms[i], c->kev[2 * slot], c->kev[2 * slot + 1]) != hipSuccess)
+    const int slot = static_cast<int>((cnt - k + i) % fslr_ctx::kKernRing);
+    if (hipEventElapsedTime(&ms[i], ring[2 * slot], ring[2 * slot + 1]) != hipSuccess)
       return -fail(c, FSLR_ERR_HIP, "hipEventElapsedTime");
   }
   return k;
 }
+
+int fslr_get_pair_kernel_times(fslr_ctx* c, float* ms, int32_t n) { return fslr_get_stage_kernel_times(c, 0, ms, n); }
 
 int fslr_get_labels(fslr_ctx* c, int32_t* labels) {
   if (!c || (!labels && c->n)) return FSLR_ERR_INVALID;

@@ -38,6 +38,7 @@ struct fslr_ctx {
   int built_shard = 0, built_n_shards = 1;
   // device buffers
   int4* rmeta = nullptr;
+  unsigned char* rlen8 = nullptr;  // [N] interval count per read (the pair stage's L lookups)
   int4* iv = nullptr;
   int* qpos = nullptr;       // [NI] CSR interval -> its position in the sorted index
   int2* rng_s = nullptr;     // [NI] sorted position -> {n_fwd, bwd_begin}
@@ -141,6 +142,8 @@ struct fslr_ctx {
   static constexpr int kKernRing = 256;
   std::vector<hipEvent_t> kev;
   int64_t n_kern = 0;
+  std::vector<hipEvent_t> kev2;            // the same ring around the sweep's pair-stage kernel
+  int64_t n_kern2 = 0;
   bool ev_ok = false;
   bool t_index_rec = false, t_query_rec = false, t_comp_rec = false, t_kernel_rec = false;
 };

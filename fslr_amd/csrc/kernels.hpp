@@ -155,6 +155,7 @@ int query_max_waves();
 // ---- position sweep (sweep.hip) ------------------------------------------------------------
 struct SweepArgs {
   const int4* rmeta;
+  const unsigned char* rlen8;         // [n_reads] interval count of each read (1 B: stays in L2)
   const int4* idx4;
   const int2* idx_gate;
   const int2* rng_s;
@@ -188,6 +189,7 @@ struct SweepArgs {
   int wstat_waves;
   hipEvent_t ev[5];                   // (profiling) count | scan | emit | sort | pairs boundaries, or null
   hipEvent_t k0, k1;                  // (profiling) around the sweep kernel launch alone, or null
+  hipEvent_t p0, p1;                  // (profiling) around the pair-stage kernel (k_sweep_pairs) alone, or null
 };
 size_t sweep_temp_bytes(long long ent_cap, long long ni, hipStream_t s);
 int sweep_max_waves();

@@ -36,12 +36,8 @@ namespace {
 
 constexpr int kSwWaves = 4;
 constexpr int kSwBlock = kSwWaves * kWave;
-constexpr int kPairLimit = 160;            // long runs: insert while partners < limit (+64 per step < 256)
-constexpr int kPerPass = 80;               // entries per partner partition of a long run
-#ifndef FSLR_EDGE_STAGE
-#define FSLR_EDGE_STAGE 256
-#endif
-constexpr int kEdgeStage = FSLR_EDGE_STAGE;  // staged edges per wave
+constexpr int kPairLimit = 64;             // long runs: insert while partners < limit (+64 per step <= 128)
+constexpr int kPerPass = 40;               // entries per partner partition of a long run
 constexpr int kWsFields = 4;               // per-wave statistics slots
 
 __device__ __forceinline__ int entry_a(unsigned long long e) { return static_cast<int>(e >> 39); }
@@ -305,49 +301,130 @@ __global__ __launch_bounds__(256) void k_compact(const unsigned long long* __res
 
 // ---- 3. pairs from the entries grouped by A ------------------------------------------------------
 // Work item: a chunk of kChunk2 sorted entries; the runs (reads A) that start in it.  Whole runs are
-// staged in LDS a group of at most kStageE entries at a time and evaluated together: one LDS hash
-// over (run, B) collects every pair's entry count and row / column masks, then one lane per pair
-// decides it (I = count unless two entries share a row or a column, then first-fit in the reference's
-// order from the staged entries).  A run longer than the stage is evaluated alone, streamed from HBM,
-// in partner partitions (pass k takes the partners with part(B) == k).
-constexpr int kChunk2 = 128;
+// taken a group of at most kStageE entries at a time (two per lane, in registers) and sorted by
+// (run, B, i, j) with a wave-wide bitonic network: each read pair's entries become one segment, in
+// the reference's row order.  Per segment (one lane each): I = its entry count unless two entries
+// share a row (adjacent equal i) or a column (the segment's OR of column bits has fewer bits than
+// entries) — then first-fit in the reference's order over the sorted segment (rows ascending, the
+// lowest unused column, cluster.py:152-161).  A run longer than the stage is evaluated alone,
+// streamed from HBM, through an LDS hash over its partners in partner partitions (pass k takes the
+// partners with part(B) == k).
+constexpr int kChunk2 = 512;               // a wave's work item: whole runs starting in it
 constexpr int kStageE = 128;
-constexpr int kHash2 = 256;
+constexpr int kHash2 = 128;
 constexpr unsigned kEmpty = 0xFFFFFFFFu;
+#ifndef FSLR_PAIR_EDGE_STAGE
+#define FSLR_PAIR_EDGE_STAGE 256
+#endif
+constexpr int kPairEdgeStage = FSLR_PAIR_EDGE_STAGE;   // staged edges per wave (one atomic per flush)
+// per-wave LDS shared by the two paths: the long-run hash (KEY, CNT: 4 B, RM, CM: 8 B per slot, the
+// slot list) or the group's sorted keys, segment keys, column masks and heads
+constexpr int kLongScr = kHash2 * (4 + 4 + 8 + 8) + 2 * (kPairLimit + kWave);
+constexpr int kGroupScr = kStageE * (8 + 8 + 8) + 4 * (kStageE + 1);
+constexpr int kScrWords = ((kLongScr > kGroupScr ? kLongScr : kGroupScr) + 7) / 8;
+
+// lane ^ ST's value: DPP for strides 1 .. 8 (inside a 16-lane row: quad permutes, row shifts),
+// ds_swizzle for 16 (inside 32 lanes), ds_bpermute for 32 — the short strides cost a VALU op, not an
+// LDS round trip
+template <int ST>
+__device__ __forceinline__ unsigned xor_lane32(unsigned v, int lane) {
+  if constexpr (ST == 1) {
+    return static_cast<unsigned>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0xB1, 0xF, 0xF, false));
+  } else if constexpr (ST == 2) {
+    return static_cast<unsigned>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x4E, 0xF, 0xF, false));
+  } else if constexpr (ST == 4 || ST == 8) {
+    const int up = __builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x100 + ST, 0xF, 0xF, true);   // lane + ST
+    const int dn = __builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x110 + ST, 0xF, 0xF, true);   // lane - ST
+    return static_cast<unsigned>((lane & ST) ? dn : up);
+  } else if constexpr (ST == 16) {
+    return static_cast<unsigned>(__builtin_amdgcn_ds_swizzle(static_cast<int>(v), 0x401F));            // xor 16
+  } else {
+    return static_cast<unsigned>(__shfl_xor(static_cast<int>(v), ST));
+  }
+}
+
+template <int ST>
+__device__ __forceinline__ unsigned long long xor_lane(unsigned long long v, int lane) {
+  const unsigned lo = xor_lane32<ST>(static_cast<unsigned>(v), lane);
+  const unsigned hi = xor_lane32<ST>(static_cast<unsigned>(v >> 32), lane);
+  return (static_cast<unsigned long long>(hi) << 32) | lo;
+}
+
+// one compare-exchange step of the bitonic network: keep the min (keep_min) or the max of the
+// pair (lane, lane ^ ST)
+template <int ST>
+__device__ __forceinline__ unsigned long long bitonic_cx(unsigned long long v, bool keep_min, int lane) {
+  const unsigned long long o = xor_lane<ST>(v, lane);
+  return keep_min == (v < o) ? v : o;
+}
+
+// merge steps of one bitonic stage, strides ST .. 1 (size = the stage's sequence length; size 128 =
+// the final merge, all ascending)
+template <int SIZE, int ST>
+__device__ __forceinline__ void bitonic_steps(unsigned long long& a, unsigned long long& b, int lane) {
+  if constexpr (ST >= 1) {
+    const bool lower = (lane & ST) == 0;
+    const bool asc_a = SIZE == 2 * kWave || (lane & SIZE) == 0;
+    const bool asc_b = SIZE == 2 * kWave || ((lane + kWave) & SIZE) == 0;
+    a = bitonic_cx<ST>(a, lower == asc_a, lane);
+    b = bitonic_cx<ST>(b, lower == asc_b, lane);
+    bitonic_steps<SIZE, ST / 2>(a, b, lane);
+  }
+}
+
+// ascending sort of the 128 keys {a at element lane, b at element lane + 64}
+__device__ __forceinline__ void bitonic128(unsigned long long& a, unsigned long long& b, int lane) {
+  bitonic_steps<2, 1>(a, b, lane);
+  bitonic_steps<4, 2>(a, b, lane);
+  bitonic_steps<8, 4>(a, b, lane);
+  bitonic_steps<16, 8>(a, b, lane);
+  bitonic_steps<32, 16>(a, b, lane);
+  bitonic_steps<64, 32>(a, b, lane);
+  const unsigned long long lo = a < b ? a : b, hi = a < b ? b : a;   // the 128-merge: stride 64 in-lane
+  a = lo;
+  b = hi;
+  bitonic_steps<2 * kWave, 32>(a, b, lane);
+}
+
+// group sort key: run (7 bits) << 39 | B << 14 | i << 7 | j; the segment key (run, B) is key >> 14
+__device__ __forceinline__ unsigned long long group_key(unsigned long long e, int r) {
+  return (static_cast<unsigned long long>(r) << 39) | (e & ((1ull << 39) - 1));
+}
 
 __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
-  __shared__ unsigned long long ste_all[kSwWaves][kStageE];   // staged entries of the group
-  __shared__ unsigned key_all[kSwWaves][kHash2];              // run << 24 | B (group) or B (long run)
-  __shared__ unsigned cnt_all[kSwWaves][kHash2];              // entry count | conflict << 31
-  __shared__ uint2 rm_all[kSwWaves][kHash2];                  // rows i of A used by the pair's entries
-  __shared__ uint2 cm_all[kSwWaves][kHash2];                  // columns j of B
-  __shared__ unsigned short mp_all[kSwWaves][kPairLimit + kWave];
+  __shared__ unsigned long long scr_all[kSwWaves][kScrWords];
   __shared__ int runa_all[kSwWaves][kStageE];                 // per run of the group: A, L_A, edges formed
   __shared__ int runl_all[kSwWaves][kStageE];
   __shared__ int runf_all[kSwWaves][kStageE];
-  __shared__ uint2 rr_all[kSwWaves][kWave];                   // ordered path: row masks of one partner
-  __shared__ unsigned long long es_all[kSwWaves][kEdgeStage];
+  __shared__ uint2 rr_all[kSwWaves][kWave];                   // long runs' ordered path: row masks of one partner
+  __shared__ unsigned long long es_all[kSwWaves][kPairEdgeStage];
   const int lane = lane_id();
   const int wv = threadIdx.x >> 6;
-  unsigned long long* STE = ste_all[wv];
-  unsigned* KEY = key_all[wv];
-  unsigned* CNT = cnt_all[wv];
-  uint2* RM = rm_all[wv];
-  uint2* CM = cm_all[wv];
-  unsigned short* MP = mp_all[wv];
+  unsigned long long* scr = scr_all[wv];
+  // long-run path views
+  unsigned* KEY = reinterpret_cast<unsigned*>(scr);           // B
+  unsigned* CNT = KEY + kHash2;                               // entry count | L_B << 16 | conflict << 31
+  uint2* RM = reinterpret_cast<uint2*>(CNT + kHash2);          // rows i of A used by the pair's entries
+  uint2* CM = RM + kHash2;                                    // columns j of B
+  unsigned short* MP = reinterpret_cast<unsigned short*>(CM + kHash2);
+  // group path views
+  unsigned long long* SK = scr;                               // the sorted keys
+  unsigned long long* PK = SK + kStageE;                      // per segment: (run, B)
+  unsigned long long* PJ = PK + kStageE;                      // per segment: OR of column bits
+  int* PH = reinterpret_cast<int*>(PJ + kStageE);             // per segment: first position | row dup << 30
   int* RUNA = runa_all[wv];
   int* RUNL = runl_all[wv];
   int* RUNF = runf_all[wv];
   uint2* RR = rr_all[wv];
-  EdgeStageN<kEdgeStage> es{es_all[wv], 0};
+  EdgeStageN<kPairEdgeStage> es{es_all[wv], 0};
   const EdgeOut eo{g.edges, g.edge_iu, g.edge_cap, &g.counters[kEdgeCount]};
   const int umax_v = g.umax[lane];
   const long long n = g.n_dev ? *g.n_dev : g.n_ent;
   const unsigned long long* E = g.ent_sorted;
+  const unsigned char* RL = g.rlen8;
   const long long nchunks = (n + kChunk2 - 1) / kChunk2;
   const long long nw = static_cast<long long>(gridDim.x) * kSwWaves;
   const int wid = blockIdx.x * kSwWaves + wv;
-  const bool group_keys = g.n_reads < (1 << 24) - 1;     // run << 24 | B fits 32 bits
   int w_maxfwd = 0;
   unsigned long long w_pairs = 0;
   auto a_at = [&](long long k) -> int {   // A of sorted entry k (wave-uniform, scalar cache)
@@ -370,7 +447,7 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
   };
   // insert `key` (lanes with `mine`); returns the slot; isnew for the lane that created it
   auto insert = [&](bool mine, unsigned key, unsigned hseed, bool& isnew) -> int {
-    unsigned h = (hseed * 2654435761u) >> 24;       // 8 bits: kHash2
+    unsigned h = (hseed * 2654435761u) >> 25;       // 7 bits: kHash2
     isnew = false;
     if (mine) {
       while (true) {
@@ -414,7 +491,7 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
   // ---- a run longer than the stage: alone, streamed, in partner partitions ----
   auto long_run = [&](long long rs, long long re) {
     const int A = a_at(rs);
-    const int LA = sload4(g.rmeta, A).y & 0xffff;
+    const int LA = RL[A];
     const long long len = re - rs;
     const int npass = len <= kPairLimit ? 1 : static_cast<int>((len + kPerPass - 1) / kPerPass);
     int fwdA = 0;
@@ -429,7 +506,7 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
         const int B = static_cast<int>((e >> 14) & kRankMask);
         const int i = static_cast<int>((e >> 7) & 127u), j = static_cast<int>(e & 127u);
         bool mine = act && (npass == 1 || part_of(B, npass) == pass);
-        // insert while fewer than kPairLimit partners (+ 64 per step < 256 slots)
+        // insert while fewer than kPairLimit partners (+ 64 per step: at most kHash2 slots)
         const bool full = mine && uniq >= kPairLimit;
         full_any |= __ballot(full) != 0ull;
         mine = mine && !full;
@@ -440,7 +517,7 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
           CNT[h] = 0u;
           RM[h] = make_uint2(0u, 0u);
           CM[h] = make_uint2(0u, 0u);
-          lbn = g.rmeta[B].y & 0xffff;
+          lbn = RL[B];
         }
         const unsigned long long nm = __ballot(isnew);
         if (isnew) MP[uniq + mbcnt(nm)] = static_cast<unsigned short>(h);
@@ -490,23 +567,32 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
     w_maxfwd = max(w_maxfwd, fwdA);
   };
 
+  // the window of (up to) kStageE entries at s, and (lane 0) the entry after it (~0: none).  Vector
+  // loads only: a scalar load in flight would hold every LDS wait (lgkmcnt) of the group behind it
+  auto load_window = [&](long long s, unsigned long long& w0, unsigned long long& w1, unsigned long long& wn) {
+    const int lim = static_cast<int>(min(static_cast<long long>(kStageE), n - s));
+    w0 = lane < lim ? E[s + lane] : ~0ull;
+    w1 = lane + kWave < lim ? E[s + kWave + lane] : ~0ull;
+    wn = lane == 0 && s + lim < n ? E[s + lim] : ~0ull;
+  };
   for (long long c = wid; c < nchunks; c += nw) {
     const long long c0 = c * kChunk2, c1 = min(c0 + kChunk2, n);
     long long s = c0;
     if (s > 0) s = next_run(s, c1, a_at(s - 1));       // the run in progress belongs to the previous chunk
+    unsigned long long e0 = ~0ull, e1 = ~0ull, en = ~0ull;
+    if (s < c1) load_window(s, e0, e1, en);
     while (s < c1) {
-      // stage [s, s + lim): two entries per lane
+      // the window [s, s + lim): two entries per lane, neighbours by shuffles
       const int lim = static_cast<int>(min(static_cast<long long>(kStageE), n - s));
-      wave_lds_sync();
-      unsigned long long e0 = lane < lim ? E[s + lane] : ~0ull;
-      unsigned long long e1 = lane + kWave < lim ? E[s + kWave + lane] : ~0ull;
-      STE[lane] = e0;
-      STE[lane + kWave] = e1;
-      const bool last_done = s + lim >= n || a_at(s + lim) != entry_a(lim <= kWave ? __shfl(e0, lim - 1)
-                                                                                  : __shfl(e1, lim - 1 - kWave));
-      wave_lds_sync();
-      const unsigned long long p0 = lane > 0 ? STE[lane - 1] : ~0ull;
-      const unsigned long long p1 = STE[lane + kWave - 1];
+      const unsigned long long en0 = static_cast<unsigned long long>(
+          static_cast<unsigned>(__builtin_amdgcn_readfirstlane(static_cast<int>(en >> 32)))) << 32;
+      const bool last_done = s + lim >= n ||
+                             entry_a(en0) != entry_a(lim <= kWave ? __shfl(e0, lim - 1) : __shfl(e1, lim - 1 - kWave));
+      // every lane shuffles (a source lane outside EXEC would read as 0), then selects
+      const unsigned long long p0 = __shfl_up(e0, 1);
+      const unsigned long long e0_63 = __shfl(e0, kWave - 1);
+      const unsigned long long u1 = __shfl_up(e1, 1);
+      const unsigned long long p1 = lane > 0 ? u1 : e0_63;
       const bool h0 = lane < lim && (lane == 0 || entry_a(e0) != entry_a(p0));
       const bool h1 = lane + kWave < lim && entry_a(e1) != entry_a(p1);
       const unsigned long long H0 = __ballot(h0), H1 = __ballot(h1);
@@ -523,90 +609,106 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
       if (A0) gend = __builtin_ctzll(A0);
       else if (A1) gend = kWave + __builtin_ctzll(A1);
       else gend = last_done ? lim : h_top;
-      if (gend == 0 || !group_keys) {
-        // the run at s does not fit the stage (or ranks need 25 bits): alone
-        const long long re = gend == 0 ? next_run(s + lim, n, entry_a(__shfl(e0, 0))) : next_run(s + 1, n, entry_a(__shfl(e0, 0)));
+      if (gend == 0) {
+        // the run at s does not fit the stage: alone
+        const long long re = next_run(s + lim, n, entry_a(__shfl(e0, 0)));
         long_run(s, re);
         s = re;
+        if (s < c1) load_window(s, e0, e1, en);
         continue;
       }
-      // ---- the group [s, s + gend): whole runs, evaluated together ----
+      // ---- the group [s, s + gend): whole runs, sorted by (run, B, i, j) ----
       const int r0 = __popcll(H0 & upto(lane)) - 1;                 // run (in the group) of entry lane
       const int r1 = __popcll(H0) + __popcll(H1 & upto(lane)) - 1;
       const bool v0 = lane < gend, v1 = lane + kWave < gend;
+      const bool hv0 = h0 && v0, hv1 = h1 && v1;
       int la0 = 0, la1 = 0;
-      if (h0 && v0) la0 = g.rmeta[entry_a(e0)].y & 0xffff;      // gathered now, stored after the hash
-      if (h1 && v1) la1 = g.rmeta[entry_a(e1)].y & 0xffff;
-      clear_hash();
-      int uniq = 0;
-      for (int half = 0; half < 2; ++half) {
-        const unsigned long long e = half ? e1 : e0;
-        const bool act = half ? v1 : v0;
-        const int r = half ? r1 : r0;
-        const int B = static_cast<int>((e >> 14) & kRankMask);
-        const int i = static_cast<int>((e >> 7) & 127u), j = static_cast<int>(e & 127u);
-        const unsigned key = (static_cast<unsigned>(r) << 24) | static_cast<unsigned>(B);
-        bool isnew;
-        const int h = insert(act, key, key, isnew);
-        int lbn = 0;
-        if (isnew) {
-          CNT[h] = 0u;
-          RM[h] = make_uint2(0u, 0u);
-          CM[h] = make_uint2(0u, 0u);
-          lbn = g.rmeta[B].y & 0xffff;             // L_B, in flight while the masks are recorded
-        }
-        const unsigned long long nm = __ballot(isnew);
-        if (isnew) MP[uniq + mbcnt(nm)] = static_cast<unsigned short>(h);
-        uniq += __popcll(nm);
-        wave_lds_sync();
-        record(act, h, i, j);
-        if (isnew) atomicOr(&CNT[h], static_cast<unsigned>(lbn) << 16);   // bits 16..22: L_B
-      }
-      if (h0 && v0) {
+      if (hv0) la0 = RL[entry_a(e0)];                              // in flight during the sort
+      if (hv1) la1 = RL[entry_a(e1)];
+      unsigned long long k0 = v0 ? group_key(e0, r0) : ~0ull;
+      unsigned long long k1 = v1 ? group_key(e1, r1) : ~0ull;
+      bitonic128(k0, k1, lane);                                    // positions [0, gend) hold the group
+      const unsigned long long q0 = __shfl_up(k0, 1);
+      const unsigned long long k0_63 = __shfl(k0, kWave - 1);
+      const unsigned long long w1 = __shfl_up(k1, 1);
+      const unsigned long long q1 = lane > 0 ? w1 : k0_63;
+      // segments = read pairs (run, B); a row repeated inside a segment sits next to itself
+      const bool s0 = v0 && (lane == 0 || (k0 >> 14) != (q0 >> 14));
+      const bool s1 = v1 && (k1 >> 14) != (q1 >> 14);
+      const bool d0 = v0 && !s0 && (k0 >> 7) == (q0 >> 7);
+      const bool d1 = v1 && !s1 && (k1 >> 7) == (q1 >> 7);
+      int lb0 = 0, lb1 = 0;                                        // L_B of each segment, gathered by its head
+      if (s0) lb0 = RL[(k0 >> 14) & kRankMask];
+      if (s1) lb1 = RL[(k1 >> 14) & kRankMask];
+      // the next window, in flight while this group is evaluated
+      const long long sn = s + gend;
+      unsigned long long n0 = ~0ull, n1 = ~0ull, nn = ~0ull;
+      if (sn < c1) load_window(sn, n0, n1, nn);
+      const unsigned long long S0 = __ballot(s0), S1 = __ballot(s1);
+      const int ns0 = __popcll(S0), nseg = ns0 + __popcll(S1);
+      const int g0 = __popcll(S0 & upto(lane)) - 1;
+      const int g1 = ns0 + __popcll(S1 & upto(lane)) - 1;
+      wave_lds_sync();                                             // the previous group's reads are done
+      if (hv0) {
         RUNA[r0] = entry_a(e0);
         RUNL[r0] = la0;
         RUNF[r0] = 0;
       }
-      if (h1 && v1) {
+      if (hv1) {
         RUNA[r1] = entry_a(e1);
         RUNL[r1] = la1;
         RUNF[r1] = 0;
       }
+      SK[lane] = k0;
+      SK[lane + kWave] = k1;
+      if (s0) {
+        PK[g0] = (k0 >> 14) | (static_cast<unsigned long long>(lb0) << 32);
+        PJ[g0] = 0ull;
+        PH[g0] = lane;
+      }
+      if (s1) {
+        PK[g1] = (k1 >> 14) | (static_cast<unsigned long long>(lb1) << 32);
+        PJ[g1] = 0ull;
+        PH[g1] = lane + kWave;
+      }
+      if (lane == 0) PH[nseg] = gend;
       wave_lds_sync();
-      for (int k0 = 0; k0 < uniq; k0 += kWave) {
-        const bool act = k0 + lane < uniq;
-        const int h = act ? static_cast<int>(MP[k0 + lane]) : 0;
-        const unsigned key = KEY[h];
-        const int r = static_cast<int>(key >> 24);
-        const int B = static_cast<int>(key & 0xFFFFFFu);
-        const unsigned st = act ? CNT[h] : 0u;
-        int I = static_cast<int>(st & 0xFFFFu);
-        const int LB = static_cast<int>((st >> 16) & 127u);
-        const int A = RUNA[r], LA = RUNL[r];
-        unsigned long long cm = __ballot(act && (st >> 31));
-        while (cm) {
-          const int c = __builtin_ctzll(cm);
-          cm &= cm - 1;
-          const unsigned kc = static_cast<unsigned>(rdl(static_cast<int>(key), c));
-          RR[lane] = make_uint2(0u, 0u);
-          wave_lds_sync();
-          for (int half = 0; half < 2; ++half) {
-            const unsigned long long e = half ? e1 : e0;
-            const bool in = half ? v1 : v0;
-            const int re_ = half ? r1 : r0;
-            const unsigned ke = (static_cast<unsigned>(re_) << 24) | static_cast<unsigned>((e >> 14) & kRankMask);
-            if (in && ke == kc) {
-              const int ii = static_cast<int>((e >> 7) & 127u), jj = static_cast<int>(e & 127u);
-              if (jj < 32) atomicOr(&RR[ii].x, 1u << jj);
-              else atomicOr(&RR[ii].y, 1u << (jj - 32));
+      if (v0) atomicOr(&PJ[g0], 1ull << (k0 & 63u));
+      if (v1) atomicOr(&PJ[g1], 1ull << (k1 & 63u));
+      if (d0) atomicOr(&PH[g0], 1 << 30);
+      if (d1) atomicOr(&PH[g1], 1 << 30);
+      wave_lds_sync();
+      for (int k0s = 0; k0s < nseg; k0s += kWave) {
+        const int p = k0s + lane;
+        const bool act = p < nseg;
+        int I = 0, r = 0, B = 0, LB = 0;
+        if (act) {
+          const int hp = PH[p];
+          const int h = hp & 0x3FFFFFFF, he = PH[p + 1] & 0x3FFFFFFF;
+          const unsigned long long pk = PK[p];
+          r = static_cast<int>((pk >> 25) & 127u);
+          B = static_cast<int>(pk & kRankMask);
+          LB = static_cast<int>(pk >> 32);
+          I = he - h;
+          if ((hp >> 30) || __popcll(PJ[p]) < I) {
+            // a shared row or column: first-fit over the segment, rows ascending, lowest free column
+            unsigned long long used = 0ull;
+            int row = -1, Ic = 0;
+            for (int k = h; k < he; ++k) {
+              const unsigned long long key = SK[k];
+              const int i = static_cast<int>((key >> 7) & 127u), j = static_cast<int>(key & 63u);
+              if (i == row) continue;                              // this row already matched
+              if (!((used >> j) & 1ull)) {
+                used |= 1ull << j;
+                ++Ic;
+                row = i;
+              }
             }
+            I = Ic;
           }
-          wave_lds_sync();
-          const int Ic = ordered_I(rdl(LA, c));
-          if (lane == c) I = Ic;
-          wave_lds_sync();
         }
-        const int U = LA + LB - I;
+        const int A = act ? RUNA[r] : 0;
+        const int U = (act ? RUNL[r] : 0) + LB - I;
         const int um = __shfl(umax_v, max(I, 1) - 1);     // every lane reads (no && in front)
         const bool edge = act && I > 0 && U <= um;
         es.put(eo, edge, A, B, I, U, lane);
@@ -614,17 +716,20 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
         w_pairs += __popcll(__ballot(act));
       }
       wave_lds_sync();
-      if (h0 && v0) {
+      if (hv0) {
         const int f = RUNF[r0];
         g.fwd[entry_a(e0)] = f;
         w_maxfwd = max(w_maxfwd, f);
       }
-      if (h1 && v1) {
+      if (hv1) {
         const int f = RUNF[r1];
         g.fwd[entry_a(e1)] = f;
         w_maxfwd = max(w_maxfwd, f);
       }
-      s += gend;
+      s = sn;
+      e0 = n0;
+      e1 = n1;
+      en = nn;
     }
   }
   if (es.n > 0) es.flush(eo, lane);
@@ -1060,7 +1165,9 @@ hipError_t launch_sweep_pairs(const SweepArgs& a0, int mode, hipStream_t s) {
   const long long chunks = (a.n_ent + kChunk2 - 1) / kChunk2;
   const int blocks = static_cast<int>(std::max(1ll, std::min<long long>(blocks_pairs(), (chunks + kSwWaves - 1) / kSwWaves)));
   if (blocks * kSwWaves > a.wstat_waves) return hipErrorInvalidValue;
+  if (a.p0) (void)hipEventRecord(a.p0, s);
   k_sweep_pairs<<<blocks, kSwBlock, 0, s>>>(a);
+  if (a.p1) (void)hipEventRecord(a.p1, s);
   k_sum_slots<<<kSumBlocks, 256, 0, s>>>(a.wstat, blocks * kSwWaves, 2, 4, -1, -1, kMatchedPairs, a.counters,
                                          a.err + 3);
   return hipGetLastError();

@@ -296,6 +296,9 @@ int  fslr_get_timings(fslr_ctx *ctx, fslr_timings *out);        /* syncs */
  * profiling was enabled, oldest first (hipEvents recorded on the context's stream around that one
  * launch).  Syncs; returns the count or -error. */
 int  fslr_get_pair_kernel_times(fslr_ctx *ctx, float *ms, int32_t n);
+/* The same for one stage kernel: stage 0 = the main pair kernel (as above), 1 = the sweep engine's
+ * pair-stage kernel (the evaluation of the grouped match entries).  Syncs; count or -error. */
+int  fslr_get_stage_kernel_times(fslr_ctx *ctx, int32_t stage, float *ms, int32_t n);
 /* Raw device counters of the last query (diagnostics; layout is internal, kernels.hpp:
  * Counter).  Copies min(n, 32) words, syncs, returns the count or -error. */
 int  fslr_read_counters(fslr_ctx *ctx, uint64_t *out, int n);
