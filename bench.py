@@ -16,16 +16,18 @@ overall_jaccard_similarity runs: the unit SURVEY.md §8d defines and the referen
 measured 2.27e4 pairs/s counts) of the whole job per second.  Candidate
 pairs (gate-rejected ones included) and the dense-equivalent rate are secondary fields.
 
-``roofline``: the dominant kernel of the engine that ran.  Sweep engine (default): the
-position sweep k_sweep<2>; its algorithmic bytes per launch are every
-sorted position's index record, gate word and forward count and its read's gate ranges
-read once (48 B), plus each match entry written (8 B).  Walk engine: query_kernel, every
+``roofline``: the longest kernel of the step (HIP-event means over the timed steps), the
+others in ``roofline_other_kernels``.  Sweep engine (default): the position sweep
+k_sweep<2> — every sorted position's index record, gate word and forward
+count and its read's gate ranges read once (48 B), plus each match entry written (8 B) —
+and the pair stage k_sweep_pairs — each grouped entry read (8 B), each edge written (10 B),
+each read's forward degree written (4 B).  Walk engine: query_kernel, every
 walked index record (16-B record + 8-B gate word) read once, each query read's header,
 gate bounds and forward degree, each of its intervals' sorted position, row and scan
 range, and the edge / deferred-list output.  ``achieved`` = those bytes ÷ the mean
 duration of the timed launches, measured with hipEvents the library records around
-that one launch on its stream (fslr_get_pair_kernel_times).  ``traffic`` = HBM bytes
-per launch from rocprofv3 PMC counters (tools/pmc_traffic.py), used only when that
+each of those launches on its stream (fslr_get_stage_kernel_times).  ``traffic`` = HBM
+bytes per launch from rocprofv3 PMC counters (tools/pmc_traffic.py), used only when that
 summary was measured on the current sources of that kernel.
 
 Prints ONE JSON line on rank 0.
@@ -84,7 +86,7 @@ def parse():
                     help='single-thread CPU baseline: query reads of every k-th 64-rank block (0 = skip the '
                          'CPU baseline)')
     ap.add_argument('--cpu-threads', type=int, default=0,
-                    help='threads of the all-core CPU baseline (0 = the process CPU share, at most 16)')
+                    help='threads of the all-core CPU baseline (0 = the affinity set, limited by OMP_NUM_THREADS)')
     ap.add_argument('--verify', action='store_true',
                     help='after timing, rank 0 checks its labels against a single-context run of all reads')
     ap.add_argument('--traffic-json', default=TRAFFIC_JSON,
@@ -98,11 +100,19 @@ def log(*a):
 
 
 def cpu_share():
+    """Threads of the all-core CPU baseline: every CPU in this process's affinity set, limited only by
+    OMP_NUM_THREADS when it is set (the GPU box sets it to its CPU share per GPU, 16)."""
     n = len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else (os.cpu_count() or 1)
     env = os.environ.get('OMP_NUM_THREADS')
     if env and env.isdigit():
         n = min(n, int(env))
-    return max(1, min(n, 16))
+    return max(1, n)
+
+
+def cpu_policy():
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else None
+    return (f'threads = min(affinity set {aff} CPUs, OMP_NUM_THREADS={os.environ.get("OMP_NUM_THREADS", "unset")}); '
+            f'{os.cpu_count()} CPUs visible on the host')
 
 
 def main():
@@ -208,13 +218,23 @@ def main():
     elapsed = time.perf_counter() - t_start
     st = ctx.stats()
     kern = ctx.pair_kernel_times(args.steps)       # the timed steps' main pair-kernel launches
-    kernel_ms = float(np.mean(kern)) if kern.size else float('nan')
+    kern2 = ctx.stage_kernel_times(1, args.steps) if st['engine'] == 'sweep' else np.zeros(0)   # pair stage
     lib_t = None
+    cold_ms = None
     if world == 1:
         ctx.set_profiling(1)
         step()
         torch.cuda.synchronize()
         lib_t = ctx.timings()                         # hipEvents of one untimed step (library side)
+        # one cold step: a new input generation, so the query reads its entry count back mid-step
+        # (what the CLI's single query does; the timed steps repeat a query on unchanged input)
+        ctx.set_profiling(0)
+        ctx.set_thresholds(thr)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        step()
+        torch.cuda.synchronize()
+        cold_ms = 1000.0 * (time.perf_counter() - t)
 
     sw = info['sweep_stats'] if info is not None else st          # this rank's sweep counters
     if world > 1:
@@ -253,17 +273,40 @@ def main():
         max_fwd = int(st['max_fwd'])
     ms_per_step = 1000.0 * elapsed / args.steps
     value = jacc / (elapsed / args.steps)
-    achieved = algo_bytes / (kernel_ms / 1000.0)
-    traffic = None
-    traffic_src = None
-    # the committed PMC summary is of the single-GPU launch (all query reads); a shard's launch moves less
+    # the committed PMC summaries (profiles/pmc_traffic_latest.json, keyed by kernel) are of the
+    # single-GPU launch on these sources; a shard's launch moves less
+    tj = {}
     if world == 1 and args.traffic_json and os.path.exists(args.traffic_json):
         with open(args.traffic_json) as fh:
             tj = json.load(fh)
-        if tj.get('source_hash') == kernel_source_hash(st['engine']) and tj.get('kernel') == KERNEL_NAME[st['engine']]:
-            traffic = tj.get('hbm_bytes_per_launch', tj.get('query_kernel_hbm_bytes_per_launch'))
-            traffic_src = os.path.relpath(args.traffic_json, REPO)
+        if 'kernel' in tj:
+            tj = {tj['kernel']: tj}
+    src_hash = kernel_source_hash(st['engine'])
 
+    def roofline(name, times, algo, model):
+        kms = float(np.mean(times)) if times.size else float('nan')
+        ach = algo / (kms / 1000.0)
+        e = tj.get(name, {})
+        traffic = e.get('hbm_bytes_per_launch') if e.get('source_hash') == src_hash else None
+        return {'bound': 'hbm', 'kernel': name, 'achieved': ach / 1e9, 'peak': HBM_PEAK / 1e9, 'unit': 'GB/s',
+                'frac': ach / HBM_PEAK, 'traffic': traffic,
+                'traffic_source': os.path.relpath(args.traffic_json, REPO) if traffic else None,
+                'waste_ratio': (traffic / algo) if traffic else None, 'kernel_ms': kms,
+                'kernel_launches_timed': int(times.size), 'algo_bytes_per_launch': int(algo),
+                'algo_bytes_model': model}
+
+    roofs = [roofline(KERNEL_NAME[st['engine']], kern, algo_bytes, algo_model)]
+    if kern2.size:
+        # the pair stage: every grouped match entry read once (8 B), each edge written (a, b + I | U:
+        # 10 B), each read's forward degree written (4 B); the 1-byte read lengths it looks up stay in L2
+        pb = B_ENT * sw['match_entries'] + 10 * st['n_edges'] + 4 * csr.n_reads
+        roofs.append(roofline('k_sweep_pairs', kern2, pb,
+                              f'{B_ENT} B x grouped match entries read ({sw["match_entries"]}) + 10 B x edges '
+                              f'written ({st["n_edges"]}) + 4 B x forward degrees ({csr.n_reads})'))
+    # the headline roofline is the longest kernel's (HIP events over the timed steps)
+    roofs.sort(key=lambda r: -r['kernel_ms'] if r['kernel_ms'] == r['kernel_ms'] else 0.0)
+    head_roof = dict(roofs[0], phase_ms_last_step=lib_t,
+                     selection='the longest kernel of the step by its HIP-event mean over the timed steps')
     # transfers around the device path (not in `value`): CSR upload before, labels / edges after
     t = time.perf_counter()
     labels = shard.labels() if shard is not None else ctx.labels()
@@ -334,41 +377,15 @@ def main():
                                'round robin), evaluation there, RCCL label all_gather + union'
                 if world > 1 else 'single GPU',
                 'transfer': transfer,
+                'cold_step_ms': cold_ms,
+                'cold_step_note': 'one step after a new input generation (fslr_set_thresholds): the query reads '
+                                  'its entry count back mid-step, as the CLI\'s single query does; ms_per_step '
+                                  'repeats the query on unchanged input (the count stays on the device)',
             },
-            'roofline': {
-                'bound': 'hbm',
-                'kernel': KERNEL_NAME[st['engine']],
-                'achieved': achieved / 1e9,
-                'peak': HBM_PEAK / 1e9,
-                'unit': 'GB/s',
-                'frac': achieved / HBM_PEAK,
-                'traffic': traffic,
-                'traffic_source': traffic_src,
-                'waste_ratio': (traffic / algo_bytes) if traffic else None,
-                'kernel_ms': kernel_ms,
-                'kernel_launches_timed': int(kern.size),
-                'algo_bytes_per_launch': int(algo_bytes),
-                'algo_bytes_model': algo_model,
-                'phase_ms_last_step': lib_t,
-            },
+            'roofline': head_roof,
+            'roofline_other_kernels': roofs[1:],
             'cpu_baseline': cpu,
         }
-        if world == 1 and st['engine'] == 'sweep' and lib_t and lib_t.get('sweep_pairs_ms'):
-            # the pair stage is the longest kernel at cfg3 (rocprof: k_sweep_pairs ~0.31 ms vs k_sweep<2>
-            # ~0.245 ms): its roofline too, from the untimed phase step's events (k_sweep_pairs + the
-            # 5-us statistics reduction after it); bytes: every grouped entry read once + each edge
-            # written (8 + 2 B) — a lower bound (per-read headers and forward degrees left out)
-            pb = B_ENT * sw['match_entries'] + 10 * st['n_edges']
-            pms = float(lib_t['sweep_pairs_ms'])
-            out['roofline_pair_stage'] = {
-                'bound': 'hbm', 'kernel': 'k_sweep_pairs', 'kernel_ms': pms,
-                'achieved': pb / (pms / 1000.0) / 1e9, 'peak': HBM_PEAK / 1e9, 'unit': 'GB/s',
-                'frac': pb / (pms / 1000.0) / HBM_PEAK, 'algo_bytes_per_launch': int(pb),
-                'algo_bytes_model': f'{B_ENT} B x grouped match entries read ({sw["match_entries"]}) + 10 B x edges '
-                                    f'written ({st["n_edges"]}); a lower bound',
-                'note': 'LDS- and latency-bound (an LDS hash per 128-entry stage, 3 waves/SIMD by LDS, one '
-                        'edge counter): DESIGN.md §3.6',
-            }
         if verified is not None:
             out['verified_labels_vs_single_context'] = verified
         print(json.dumps(out), flush=True)
@@ -400,6 +417,7 @@ def cpu_baseline(csr, stride, threads, gpu_jacc):
                       f'{threads} threads sharing one index (index build included); {allc["jaccard_evals"]} '
                       f'Jaccard-evaluated pairs (GPU: {gpu_jacc})',
             'host_cpus_visible': os.cpu_count(),
+            'cores_policy': cpu_policy(),
             'single_thread': {'value': one['jaccard_evals'] / dt1, 'cores': 1, 'seconds': dt1,
                               'sample': f'query reads of every {stride}th 64-rank block '
                                         f'({one["jaccard_evals"]} pairs, index build included)'},

@@ -13,7 +13,7 @@ import numpy as np
 
 LIB_PATH = os.environ.get('FSLR_LIB') or os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libfslr_hip.so')
 
-ABI_VERSION = 7          # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
+ABI_VERSION = 8          # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
 FSLR_OK, FSLR_ERR_ZERO_DIVISION, FSLR_ERR_INVALID, FSLR_ERR_HIP, FSLR_ERR_NOMEM, FSLR_ERR_STATE = range(6)
 FSLR_MAX_L = 64
 FSLR_MAX_READS = 1 << 25
@@ -34,7 +34,8 @@ EXPORTED = ['fslr_abi_version', 'fslr_last_error', 'fslr_ctx_create', 'fslr_ctx_
             'fslr_get_pair_kernel_times', 'fslr_set_chrom_filter', 'fslr_sweep_partition', 'fslr_sweep_evaluate',
             'fslr_copy_edges_device', 'fslr_components_from_pairs', 'fslr_set_long_reads', 'fslr_long_query',
             'fslr_get_long_edges', 'fslr_copy_edges_iu_device', 'fslr_cap_install_edges', 'fslr_cap_local',
-            'fslr_cap_copy_local', 'fslr_cap_replay', 'fslr_get_stage_kernel_times']
+            'fslr_cap_copy_local', 'fslr_cap_replay', 'fslr_get_stage_kernel_times', 'fslr_long_pairs',
+            'fslr_cap_replay_pairs']
 
 
 class HipUnavailable(RuntimeError):
@@ -143,6 +144,8 @@ def load(path: str = LIB_PATH):
         'fslr_set_long_reads': (ctypes.c_int, [vp, i64, vp, vp, vp, vp, i32]),
         'fslr_long_query': (ctypes.c_int, [vp, ctypes.POINTER(Params), ctypes.POINTER(ctypes.c_int64)]),
         'fslr_get_long_edges': (ctypes.c_int, [vp, vp, vp, vp, vp, i64]),
+        'fslr_long_pairs': (ctypes.c_int, [vp, ctypes.POINTER(Params), ctypes.POINTER(ctypes.c_int64)]),
+        'fslr_cap_replay_pairs': (ctypes.c_int, [vp, i32, vp, vp, i64, vp, vp, ctypes.POINTER(CapStats)]),
         'fslr_copy_edges_iu_device': (ctypes.c_int, [vp, vp, i64]),
         'fslr_cap_install_edges': (ctypes.c_int, [vp, vp, i64]),
         'fslr_cap_local': (ctypes.c_int, [vp, i32, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
@@ -484,6 +487,24 @@ class Context:
         ne = ctypes.c_int64(0)
         self._check(self._L.fslr_long_query(self._h, ctypes.byref(p), ctypes.byref(ne)))
         return int(ne.value)
+
+    def long_pairs(self, qlen_cut, nal_cut, pass_table, edge_threshold=10) -> int:
+        """Decide every distinct pair with the general evaluator (fslr_long_pairs); returns the edge count."""
+        p = self._params(qlen_cut, nal_cut, pass_table, edge_threshold)
+        ne = ctypes.c_int64(0)
+        self._check(self._L.fslr_long_pairs(self._h, ctypes.byref(p), ctypes.byref(ne)))
+        return int(ne.value)
+
+    def cap_replay_pairs(self, edge_threshold, a, b, n_reads: int):
+        """The edge cap over the E* pairs (a < b): returns (who, fwd, cap stats) — fslr_cap_replay_pairs."""
+        a = np.ascontiguousarray(a, np.int32)
+        b = np.ascontiguousarray(b, np.int32)
+        who = np.empty(a.shape[0], np.uint8)
+        fwd = np.empty(int(n_reads), np.int32)
+        cs = CapStats()
+        self._check(self._L.fslr_cap_replay_pairs(self._h, int(edge_threshold), _ptr(a), _ptr(b), int(a.shape[0]),
+                                                  _ptr(who), _ptr(fwd), ctypes.byref(cs)))
+        return who, fwd, cs.as_dict()
 
     def long_edges(self, n_edges: int):
         out = [np.empty(n_edges, np.int32) for _ in range(4)]

@@ -343,49 +343,67 @@ def _graph_outputs(qnames_by_rank, labels, a, b, I, U, fwd, st):
 
 
 def _query_long(idx, qnames_by_rank, overlap_cutoff, jaccard_threshold, edge_threshold, qlen_diff, diff):
-    """query_interval_trees with reads of more than FSLR_MAX_L intervals: the sweep over
-    the virtual CSR writes every match entry; pairs of two short reads are decided by the sweep's pair
-    stage, pairs with a long read by the first-fit over their whole lists (fslr_long_query)."""
+    """query_interval_trees with reads of more than FSLR_MAX_L intervals.
+
+    E*: where the sweep's gates apply (overlap > 0, no aln_size == 0 interval, no long read with qlen2
+    or n_alignments 0), the sweep over the virtual CSR writes every match entry; pairs of two short
+    reads are decided by its pair stage, pairs with a long read by the first-fit over their whole
+    lists (fslr_long_query).  Otherwise every distinct pair goes through the general evaluator
+    (fslr_long_pairs).  When a read has more than ``edge_threshold`` forward edges, the reference's
+    per-read cap (cluster.py:223-224) is replayed over E* in the real-read space
+    (fslr_cap_replay_pairs)."""
     csr, ctx = idx.csr, idx.ctx
     vcsr, vreal, vbase, rlen = idx.long
     n = csr.n_reads
     thr = fold_overlap_threshold(vcsr.iv_aln, overlap_cutoff)
-    if not multi.sweep_applies(vcsr, thr):
-        raise NotImplementedError('reads of more than 64 intervals need overlap > 0 and no aln_size == 0 '
-                                  'interval on the device path (DESIGN.md §13)')
     lg = rlen > FSLR_MAX_L
-    if (csr.read_qlen2[lg] == 0).any() or (csr.read_nal[lg] == 0).any():
-        raise NotImplementedError('a read of more than 64 intervals with qlen2 or n_alignments 0 (DESIGN.md §13)')
+    fast = (multi.sweep_applies(vcsr, thr) and not (csr.read_qlen2[lg] == 0).any()
+            and not (csr.read_nal[lg] == 0).any())
     ctx.set_thresholds(thr)
     ctx.set_long_reads(n, vreal, vbase, rlen, umax_table(jaccard_threshold, int(rlen.max())))
     pt = pass_table(jaccard_threshold)
     qcut, ncut = 1 - qlen_diff, 1 - diff
     ctx.reserve_edges(max(1 << 16, 12 * n))
-    while True:
-        n_long = ctx.long_query(qcut, ncut, pt, int(edge_threshold))
-        st = ctx.stats(check=False)
-        if st['n_edges'] <= st['edge_capacity']:
-            break
-        ctx.reserve_edges(int(st['n_edges'] * 1.25) + 4096)
-    st = ctx.stats()
-    ctx.components()
-    la, lb, lI, lU = ctx.long_edges(n_long)
-    if n_long:
-        ctx.union_pairs(la, lb, n_long, on_device=False)
-        ctx.finalize_labels()
-    labels = ctx.labels()[:n]
-    a, b, I, U = ctx.edges(st['n_edges'])
-    fwd = ctx.fwd_degree()[:n] + np.bincount(la, minlength=n).astype(np.int32)
+    if fast:
+        while True:
+            n_long = ctx.long_query(qcut, ncut, pt, int(edge_threshold))
+            st = ctx.stats(check=False)
+            if st['n_edges'] <= st['edge_capacity']:
+                break
+            ctx.reserve_edges(int(st['n_edges'] * 1.25) + 4096)
+        st = ctx.stats()
+        la, lb, lI, lU = ctx.long_edges(n_long)
+        a, b, I, U = ctx.edges(st['n_edges'])
+        a, b = np.concatenate([a, la]), np.concatenate([b, lb])
+        I, U = np.concatenate([I, lI]), np.concatenate([U, lU])
+        engine = 'sweep+long'
+    else:
+        n_long = ctx.long_pairs(qcut, ncut, pt, int(edge_threshold))
+        st = ctx.stats()
+        a, b, I, U = ctx.long_edges(n_long)
+        engine = 'pairs'
+    fwd = np.bincount(a, minlength=n).astype(np.int32)
     max_fwd = int(fwd.max()) if n else 0
+    cap = {'applied': 0, 'max_fwd': max_fwd}
     if max_fwd > int(edge_threshold):
-        raise NotImplementedError(f'the edge cap binds (a read has {max_fwd} > {int(edge_threshold)} forward '
-                                  'edges) with reads of more than 64 intervals: its replay is not built for '
-                                  'them (DESIGN.md §13)')
-    a, b = np.concatenate([a, la]), np.concatenate([b, lb])
-    I, U = np.concatenate([I, lI]), np.concatenate([U, lU])
-    st = dict(st, engine='sweep+long', n_edges=int(a.shape[0]), max_fwd=max_fwd, long_reads=int(lg.sum()),
-              long_pair_edges=int(n_long),
-              cap={'applied': 0, 'max_fwd': max_fwd})
+        # the capped graph: edge k kept when formed in a loop, re-oriented as (former, partner)
+        who, fwd, cap = ctx.cap_replay_pairs(int(edge_threshold), a, b, n)
+        keep = who != 2
+        a, b = np.where(who == 0, a, b)[keep], np.where(who == 0, b, a)[keep]
+        I, U = I[keep], U[keep]
+        ctx.components()
+        labels = ctx.labels()[:n]
+    elif fast:
+        ctx.components()
+        if n_long:
+            ctx.union_pairs(la, lb, n_long, on_device=False)
+            ctx.finalize_labels()
+        labels = ctx.labels()[:n]
+    else:
+        ctx.components()
+        labels = ctx.labels()[:n]
+    st = dict(st, engine=engine, n_edges=int(a.shape[0]), max_fwd=max_fwd, long_reads=int(lg.sum()),
+              long_pair_edges=int(n_long), cap=cap)
     return _graph_outputs(qnames_by_rank, labels, a, b, I, U, fwd, st)
 
 

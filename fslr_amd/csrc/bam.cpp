@@ -50,14 +50,18 @@ bool inflate_all(const std::string &raw, int n_threads, std::string &out, std::s
     const unsigned char *h = reinterpret_cast<const unsigned char *>(raw.data() + p);
     if (h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || !(h[3] & 4)) { msg = "not a BGZF file"; return false; }
     const int xlen = h[10] | (h[11] << 8);
+    if (p + 12 + xlen > n) { msg = "truncated BGZF extra field"; return false; }
     int64_t bsize = -1;
     for (int64_t q = 12; q + 4 <= 12 + xlen;) {                 // extra subfields: find BC
       const int slen = h[q + 2] | (h[q + 3] << 8);
+      if (q + 4 + slen > 12 + xlen) { msg = "BGZF extra subfield past XLEN"; return false; }
       if (h[q] == 'B' && h[q + 1] == 'C' && slen == 2) bsize = (h[q + 4] | (h[q + 5] << 8)) + 1;
       q += 4 + slen;
     }
-    if (bsize < 0 || p + bsize > n) { msg = "BGZF block without a valid BSIZE"; return false; }
+    // the block holds its header, the extra field, the deflate data and the 8-byte CRC32 / ISIZE trailer
+    if (bsize < 20 + xlen || p + bsize > n) { msg = "BGZF block without a valid BSIZE"; return false; }
     const int64_t isize = rd<uint32_t>(raw.data() + p + bsize - 4);
+    if (isize > (int64_t(1) << 16)) { msg = "BGZF block with ISIZE above 64 KiB"; return false; }
     blocks.push_back({p + 12 + xlen, bsize - 12 - xlen - 8, isize, total});
     total += isize;
     p += bsize;
@@ -145,6 +149,11 @@ int fslr_bam_open(const char *path, int n_threads, FslrBam **out, char *err, siz
     const int32_t bs = rd<int32_t>(d.data() + p);
     if (bs < 32 || p + 4 + bs > n) return fail("bad alignment record size");
     const int l_name = static_cast<unsigned char>(d[p + 12]);
+    const int64_t nc = rd<uint16_t>(d.data() + p + 16);
+    const int64_t ls = rd<int32_t>(d.data() + p + 20);
+    // the fixed fields, read name, CIGAR, packed sequence and qualities lie inside the record
+    if (l_name < 1 || ls < 0 || 36 + l_name + 4 * nc + (ls + 1) / 2 + ls > 4 + static_cast<int64_t>(bs))
+      return fail("alignment record fields past its end");
     b->qname_bytes += std::max(0, l_name - 1);
     b->rec.push_back(p);
     p += 4 + bs;
@@ -209,35 +218,40 @@ int fslr_bam_columns(const FslrBam *b, int32_t *flag, int32_t *tid, int64_t *pos
     while (t + 3 <= end) {
       const char t0 = t[0], t1 = t[1], ty = t[2];
       const char *v = t + 3;
+      const int64_t room = end - v;
       int64_t ival = 0;
       int isint = 1, size = 0;
       switch (ty) {
         case 'A': size = 1; isint = 0; break;
-        case 'c': ival = rd<int8_t>(v); size = 1; break;
-        case 'C': ival = rd<uint8_t>(v); size = 1; break;
-        case 's': ival = rd<int16_t>(v); size = 2; break;
-        case 'S': ival = rd<uint16_t>(v); size = 2; break;
-        case 'i': ival = rd<int32_t>(v); size = 4; break;
-        case 'I': ival = rd<uint32_t>(v); size = 4; break;
+        case 'c': if (room < 1) return FSLR_BAM_ERROR; ival = rd<int8_t>(v); size = 1; break;
+        case 'C': if (room < 1) return FSLR_BAM_ERROR; ival = rd<uint8_t>(v); size = 1; break;
+        case 's': if (room < 2) return FSLR_BAM_ERROR; ival = rd<int16_t>(v); size = 2; break;
+        case 'S': if (room < 2) return FSLR_BAM_ERROR; ival = rd<uint16_t>(v); size = 2; break;
+        case 'i': if (room < 4) return FSLR_BAM_ERROR; ival = rd<int32_t>(v); size = 4; break;
+        case 'I': if (room < 4) return FSLR_BAM_ERROR; ival = rd<uint32_t>(v); size = 4; break;
         case 'f': size = 4; isint = 0; break;
         case 'Z': case 'H': {
-          const void *z = std::memchr(v, 0, static_cast<size_t>(end - v));
+          if (room <= 0) return FSLR_BAM_ERROR;
+          const void *z = std::memchr(v, 0, static_cast<size_t>(room));
           if (!z) return FSLR_BAM_ERROR;
           size = static_cast<int>(static_cast<const char *>(z) - v) + 1;
           isint = 0;
           break;
         }
         case 'B': {
-          if (v + 5 > end) return FSLR_BAM_ERROR;
+          if (room < 5) return FSLR_BAM_ERROR;
           const char sub = v[0];
           const int32_t cnt = rd<int32_t>(v + 1);
-          const int es = (sub == 'c' || sub == 'C') ? 1 : (sub == 's' || sub == 'S') ? 2 : 4;
+          const int es = (sub == 'c' || sub == 'C') ? 1 : (sub == 's' || sub == 'S') ? 2
+                       : (sub == 'i' || sub == 'I' || sub == 'f') ? 4 : 0;
+          if (!es || cnt < 0 || 5 + static_cast<int64_t>(es) * cnt > room) return FSLR_BAM_ERROR;
           size = 5 + es * cnt;
           isint = 0;
           break;
         }
         default: return FSLR_BAM_ERROR;
       }
+      if (size > room) return FSLR_BAM_ERROR;         // a fixed-size value cut off by the record end
       if (t0 == 'A' && t1 == 'S' && as_kind[k] == 0) {
         as_kind[k] = isint ? 1 : 2;
         as_tag[k] = ival;

@@ -102,10 +102,20 @@ __global__ void k_cap_join(const int* __restrict__ fwd, int n, int thr, int* __r
 }
 
 // T in rank order: one scan of (1 << 32 | L) gives each member its index t and its first T-interval
-__global__ void k_cap_tpack(const int* __restrict__ state, const int4* __restrict__ rmeta, int n,
-                            unsigned long long* __restrict__ v) {
+// read x's interval count: rlen (reads of more than FSLR_MAX_L intervals, real-read space) or rmeta
+__device__ __forceinline__ int read_len(const int4* __restrict__ rmeta, const int* __restrict__ rlen, int x) {
+  return rlen ? rlen[x] : (rmeta[x].y & 0xffff);
+}
+
+__global__ void k_cap_tpack(const int* __restrict__ state, const int4* __restrict__ rmeta,
+                            const int* __restrict__ rlen, int n, unsigned long long* __restrict__ v) {
   for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < n; x += gridDim.x * blockDim.x)
-    v[x] = state[x] ? ((1ull << 32) | static_cast<unsigned>(rmeta[x].y & 0xffff)) : 0ull;
+    v[x] = state[x] ? ((1ull << 32) | static_cast<unsigned>(read_len(rmeta, rlen, x))) : 0ull;
+}
+
+// every read is a candidate (fslr_long_pairs: the pairs of every read's hits)
+__global__ void k_cap_all(int* __restrict__ state, int n) {
+  for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < n; x += gridDim.x * blockDim.x) state[x] = 1;
 }
 
 __global__ void k_cap_tlist(const int* __restrict__ state, const unsigned long long* __restrict__ v,
@@ -136,13 +146,20 @@ __global__ void k_cap_tread(const int* __restrict__ toff, int nt, int* __restric
     for (int j = toff[t]; j < toff[t + 1]; ++j) tread[j] = t;
 }
 
+// The index is over the uploaded reads; with reads of more than FSLR_MAX_L intervals those are
+// virtual reads (fslr_set_long_reads): vreal / vbase map a virtual read and its interval j to the
+// real read and its interval vbase + j.  Null maps: the identity.
+__device__ __forceinline__ int real_of(const int* __restrict__ vreal, int v) { return vreal ? vreal[v] : v; }
+
 // T-interval -> its position in this context's index (-1: a chromosome another rank indexes)
 __global__ void k_cap_tq(const int4* __restrict__ idx4, int ni, const int* __restrict__ t_of,
-                         const int* __restrict__ toff, int* __restrict__ tq) {
+                         const int* __restrict__ toff, const int* __restrict__ vreal, const int* __restrict__ vbase,
+                         int* __restrict__ tq) {
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < ni; q += gridDim.x * blockDim.x) {
     const int tag = idx4[q].w;
-    const int t = t_of[tag >> 6];
-    if (t >= 0) tq[toff[t] + (tag & 63)] = q;
+    const int v = tag >> 6;
+    const int t = t_of[real_of(vreal, v)];
+    if (t >= 0) tq[toff[t] + (vbase ? vbase[v] : 0) + (tag & 63)] = q;
   }
 }
 
@@ -153,8 +170,9 @@ __global__ void k_cap_tq(const int4* __restrict__ idx4, int ni, const int* __res
 template <bool kEmit>
 __global__ __launch_bounds__(256) void k_cap_hits(const int* __restrict__ tq, const int* __restrict__ tread,
                                                   const int* __restrict__ T, const int4* __restrict__ idx4,
-                                                  const int2* __restrict__ rng_s, int nti, int* __restrict__ icnt,
-                                                  const int* __restrict__ ioff, int* __restrict__ seqp) {
+                                                  const int2* __restrict__ rng_s, const int* __restrict__ vreal,
+                                                  int nti, int* __restrict__ icnt, const int* __restrict__ ioff,
+                                                  int* __restrict__ seqp) {
   const int lane = threadIdx.x & 63;
   const int nw = gridDim.x * (blockDim.x >> 6);
   for (int ti = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); ti < nti; ti += nw) {
@@ -175,7 +193,7 @@ __global__ __launch_bounds__(256) void k_cap_hits(const int* __restrict__ tq, co
         bool hit = false;
         if (p >= lo) {
           const int4 r = idx4[p];
-          hit = (p >= q || r.y >= s) && (r.w >> 6) != x;
+          hit = (p >= q || r.y >= s) && real_of(vreal, r.w >> 6) != x;
         }
         const unsigned long long hm = __ballot(hit);
         if (hit) seqp[base + w + mbcnt(hm)] = p;
@@ -187,7 +205,7 @@ __global__ __launch_bounds__(256) void k_cap_hits(const int* __restrict__ tq, co
         bool hit = false;
         if (p <= hi) {
           const int4 r = idx4[p];
-          hit = (p >= q || r.y >= s) && (r.w >> 6) != x;
+          hit = (p >= q || r.y >= s) && real_of(vreal, r.w >> 6) != x;
         }
         w += __popcll(__ballot(hit));
       }
@@ -201,7 +219,8 @@ __global__ __launch_bounds__(256) void k_cap_hits(const int* __restrict__ tq, co
 // stand-in's (end desc, position asc) order), so each run's hits are re-ranked by (end asc,
 // position desc).  One wavefront per T-interval.
 __global__ __launch_bounds__(256) void k_cap_seq(const int* __restrict__ seqp, const int4* __restrict__ idx4,
-                                                 const int* __restrict__ ioff, int nti, int* __restrict__ seq) {
+                                                 const int* __restrict__ ioff, const int* __restrict__ vreal, int nti,
+                                                 int* __restrict__ seq) {
   const int lane = threadIdx.x & 63;
   const int nw = gridDim.x * (blockDim.x >> 6);
   for (int ti = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); ti < nti; ti += nw) {
@@ -225,7 +244,7 @@ __global__ __launch_bounds__(256) void k_cap_seq(const int* __restrict__ seqp, c
         }
         dst = bb + rank;
       }
-      seq[dst] = r.w >> 6;
+      seq[dst] = real_of(vreal, r.w >> 6);
     }
   }
 }
@@ -296,50 +315,69 @@ __global__ void k_cap_slots(const unsigned long long* __restrict__ key, const in
   }
 }
 
-// the full predicate of each slot's pair — one wavefront per pair: B's intervals in lanes, A's rows
-// broadcast (first-fit in the reference's order, rows ascending, lowest unused column,
-// cluster.py:152-161); flags = zd | lenok << 1 | edge << 2 | I << 8 | U << 20
+// the full predicate of each slot's pair — one wavefront per pair: B's intervals in lanes (64 at a
+// time), A's rows broadcast; first-fit in the reference's order (rows ascending, the lowest unused
+// column, cluster.py:152-161), ZeroDivisionError where the reference meets an aln_size == 0 interval
+// (:133-136) or both reads' qlen2 / n_alignments are 0 (:178-183).  Any read length up to
+// kMaxLongL: lane l keeps bit c of `used` for column 64 c + l.  A real read's intervals are its
+// first virtual read's and, beyond FSLR_MAX_L, the consecutive chunks starting at off2.
+// flags: {zd | lenok << 1 | edge << 2, I | U << 16}
+constexpr int kMaxLongL = 64 * 64;
+
+__device__ __forceinline__ int row_at(const int4* __restrict__ rmeta, const int* __restrict__ off2, int r, int i) {
+  return i < FSLR_MAX_L ? rmeta[r].x + i : off2[r] + (i - FSLR_MAX_L);
+}
+
 __global__ __launch_bounds__(256) void k_cap_eval(const unsigned long long* __restrict__ ukey, int ns,
                                                   const int* __restrict__ T, const int4* __restrict__ rmeta,
-                                                  const int4* __restrict__ iv, double qcut, double ncut,
-                                                  const int* __restrict__ umax, int* __restrict__ flags) {
+                                                  const int4* __restrict__ iv, const int* __restrict__ rlen,
+                                                  const int* __restrict__ off2, double qcut, double ncut,
+                                                  const int* __restrict__ umax, int n_umax, int2* __restrict__ flags) {
   const int lane = threadIdx.x & 63;
   const int nw = gridDim.x * (blockDim.x >> 6);
-  const int umax_v = umax[lane];
   for (int sl = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); sl < ns; sl += nw) {
     const unsigned long long key = ukey[sl];
     const int x = T[key >> 25], y = static_cast<int>(key & kKeyMask);
-    const int4 am = rmeta[min(x, y)], bm = rmeta[max(x, y)];
-    const int LA = am.y & 0xffff, LB = bm.y & 0xffff;
-    int4 ai = make_int4(-1, 0, 0, 0), bj = make_int4(-2, 0, 0, 0);
-    if (lane < LA) ai = iv[am.x + lane];
-    if (lane < LB) bj = iv[bm.x + lane];
+    const int a = min(x, y), b = max(x, y);
+    const int4 am = rmeta[a], bm = rmeta[b];
+    const int LA = read_len(rmeta, rlen, a), LB = read_len(rmeta, rlen, b);
     bool zd = false;
     const bool lenok = lengths_pass(am.z, bm.z, am.w, bm.w, qcut, ncut, &zd);
     int I = 0;
     if (lenok && !zd) {
-      bool used = false;
-      for (int i = 0; i < LA; ++i) {
-        const int c = rdl(ai.x, i), si = rdl(ai.y, i), ei = rdl(ai.z, i), ti = rdl(ai.w, i);
-        const bool cand = lane < LB && !used && bj.x == c;
-        const bool zero = cand && (ti == FSLR_THR_ZERO_ALN || bj.w == FSLR_THR_ZERO_ALN);
-        const bool hit = cand && (zero || iv_match_general(si, ei, ti, bj.y, bj.z, bj.w));
-        const unsigned long long hm = __ballot(hit);
-        if (!hm) continue;
-        const int j = __builtin_ctzll(hm);
-        if (__shfl(static_cast<int>(zero), j)) {
-          zd = true;
+      const int nb = (LB + 63) >> 6;
+      unsigned long long used = 0ull;
+      int4 b0 = make_int4(-2, 0, 0, 0);                          // the first 64 columns stay in registers
+      if (lane < LB) b0 = iv[bm.x + lane];
+      int4 ai = make_int4(-1, 0, 0, 0);
+      for (int i = 0; i < LA && !zd; ++i) {
+        if ((i & 63) == 0) ai = i + lane < LA ? iv[row_at(rmeta, off2, a, i + lane)] : make_int4(-1, 0, 0, 0);
+        const int c = rdl(ai.x, i & 63), si = rdl(ai.y, i & 63), ei = rdl(ai.z, i & 63), ti = rdl(ai.w, i & 63);
+        for (int cc = 0; cc < nb; ++cc) {
+          const int jj = (cc << 6) + lane;
+          int4 bj = b0;
+          if (cc > 0) bj = jj < LB ? iv[row_at(rmeta, off2, b, jj)] : make_int4(-2, 0, 0, 0);
+          const bool cand = jj < LB && !((used >> cc) & 1ull) && bj.x == c;
+          const bool zero = cand && (ti == FSLR_THR_ZERO_ALN || bj.w == FSLR_THR_ZERO_ALN);
+          const bool hit = cand && (zero || iv_match_general(si, ei, ti, bj.y, bj.z, bj.w));
+          const unsigned long long hm = __ballot(hit);
+          if (!hm) continue;
+          const int j = __builtin_ctzll(hm);
+          if (__shfl(static_cast<int>(zero), j)) {
+            zd = true;
+            break;
+          }
+          if (lane == j) used |= 1ull << cc;
+          ++I;
           break;
         }
-        if (lane == j) used = true;
-        ++I;
       }
     }
     const int U = LA + LB - I;
-    const bool edge = lenok && !zd && I > 0 && U <= __shfl(umax_v, max(I, 1) - 1);
+    const bool edge = lenok && !zd && I > 0 && I <= n_umax && U <= umax[min(max(I, 1), n_umax) - 1];
     if (lane == 0)
-      flags[sl] = static_cast<int>(zd) | (static_cast<int>(lenok && !zd) << 1) | (static_cast<int>(edge) << 2) |
-                  (I << 8) | (U << 20);
+      flags[sl] = make_int2(static_cast<int>(zd) | (static_cast<int>(lenok && !zd) << 1) | (static_cast<int>(edge) << 2),
+                            I | (U << 16));
   }
 }
 
@@ -381,13 +419,14 @@ __global__ void k_cap_ckeys(const int* __restrict__ tpar, int nt, unsigned long 
 
 // the replay's static view of each sequence element: {slot, bits, mirror slot, T index of partner}
 __global__ void k_cap_recs(const int* __restrict__ slot_of, const unsigned long long* __restrict__ ukey,
-                           const int* __restrict__ fpos, const int* __restrict__ flags, const int* __restrict__ mslot,
+                           const int* __restrict__ fpos, const int2* __restrict__ flags, const int* __restrict__ mslot,
                            const int* __restrict__ T, const int* __restrict__ t_of, int m, int4* __restrict__ rec) {
   for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < m; k += gridDim.x * blockDim.x) {
     const int s = slot_of[k];
     const unsigned long long key = ukey[s];
     const int x = T[key >> 25], y = static_cast<int>(key & kKeyMask);
-    const int f = flags[s];
+    const int2 fl = flags[s];
+    const int f = fl.x;
     int bits = fpos[s] == k ? kRFirst : 0;
     int ty = -1;
     if (y < x) {
@@ -396,7 +435,7 @@ __global__ void k_cap_recs(const int* __restrict__ slot_of, const unsigned long 
     }
     if (f & 1) bits |= kRZd;
     if (f & 4) bits |= kREdge;
-    if ((f & 2) && ((f >> 8) & 0xfff) > 0) bits |= kRCounted;
+    if ((f & 2) && (fl.y & 0xffff) > 0) bits |= kRCounted;
     rec[k] = make_int4(s, bits, ty >= 0 ? mslot[s] : -1, ty);
   }
 }
@@ -655,6 +694,30 @@ __global__ void k_copy_edges_iu(const int2* __restrict__ edges, const unsigned s
     out[k] = k < ne ? make_int4(edges[k].x, edges[k].y, iu[k], 0) : make_int4(-1, -1, 0, 0);
 }
 
+// fslr_long_pairs: each unordered pair once (the slot of its lower-rank read), its edge (a, b, I, U)
+// appended to the long-edge list and to the context's edges; a ZeroDivisionError flag stops the query
+__global__ void k_cap_pairs_out(const unsigned long long* __restrict__ ukey, int ns, const int* __restrict__ T,
+                                const int2* __restrict__ flags, int4* __restrict__ out4, long long cap4,
+                                int2* __restrict__ edges, unsigned short* __restrict__ edge_iu, long long edge_cap,
+                                unsigned long long* __restrict__ cnt, int* __restrict__ fwd, int* __restrict__ err) {
+  for (int sl = blockIdx.x * blockDim.x + threadIdx.x; sl < ns; sl += gridDim.x * blockDim.x) {
+    const unsigned long long key = ukey[sl];
+    const int x = T[key >> 25], y = static_cast<int>(key & kKeyMask);
+    if (y < x) continue;
+    const int2 f = flags[sl];
+    if (f.x & 1) atomicOr(err, kCapErrZd);
+    if (!(f.x & 4)) continue;
+    const int I = f.y & 0xffff, U = f.y >> 16;
+    const unsigned long long k = atomicAdd(cnt, 1ull);
+    if (static_cast<long long>(k) < cap4) out4[k] = make_int4(x, y, I, U);
+    if (static_cast<long long>(k) < edge_cap) {
+      edges[k] = make_int2(x, y);
+      edge_iu[k] = static_cast<unsigned short>(min(I, 255) | (min(U, 255) << 8));
+    }
+    atomicAdd(fwd + x, 1);
+  }
+}
+
 __global__ void k_fill(int* __restrict__ p, int n, int v) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = v;
 }
@@ -690,6 +753,10 @@ struct CapWork {
   long long* host_dev = nullptr;
   int thr = 0;
   int64_t n = 0, ne = 0, nt = 0, nti = 0, nloc = 0, nseq = 0, ns = 0;
+  // the read space of the replay: the uploaded reads, or with reads of more than FSLR_MAX_L
+  // intervals (fslr_set_long_reads) the real reads behind the virtual ones
+  const int *vreal = nullptr, *vbase = nullptr, *rlen = nullptr, *off2 = nullptr, *umax = nullptr;
+  int n_umax = FSLR_MAX_L;
   // phase 0
   int *state = nullptr, *back = nullptr, *t_of = nullptr, *T = nullptr, *toff = nullptr, *formed = nullptr;
   unsigned long long *tv = nullptr, *tvs = nullptr;
@@ -704,7 +771,8 @@ struct CapWork {
   unsigned long long *ck = nullptr, *ck2 = nullptr;
   // phase 2 (local lists: seqp, seq; then the sequence)
   int *seqp = nullptr, *seq = nullptr, *sval = nullptr, *sval2 = nullptr, *head = nullptr, *hs = nullptr,
-      *slot_of = nullptr, *fpos = nullptr, *flags = nullptr, *mslot = nullptr;
+      *slot_of = nullptr, *fpos = nullptr, *mslot = nullptr;
+  int2* flags = nullptr;
   unsigned long long *skey = nullptr, *skey2 = nullptr, *ukey = nullptr;
   int2* upairs = nullptr;
   unsigned char* vis2 = nullptr;
@@ -784,13 +852,31 @@ long long host_word(CapWork* w, int k) {
   return static_cast<const volatile long long*>(w->host)[k];
 }
 
-// Phase A: the closure T, the T-intervals and their local hit counts; the local visit lists
-// (partner reads, search order) at w->seq[0 .. nloc), segments at w->ioff (local counts).
-int cap_local(fslr_ctx* c, int thr, CapWork* w, int64_t ne) {
+void set_space(fslr_ctx* c, CapWork* w) {
+  if (c->lg_set) {
+    w->n = c->lg_n_real;
+    w->vreal = c->lg_vreal;
+    w->vbase = c->lg_vbase;
+    w->rlen = c->lg_rlen;
+    w->off2 = c->lg_off2;
+    w->umax = c->lg_umax;
+    w->n_umax = c->lg_n_umax;
+  } else {
+    w->n = c->n;
+    w->vreal = w->vbase = w->rlen = w->off2 = nullptr;
+    w->umax = c->umax;
+    w->n_umax = FSLR_MAX_L;
+  }
+}
+
+// Phase A: the closure T (all_reads: every read, fslr_long_pairs), the T-intervals and their
+// local hit counts; the local visit lists (partner reads, search order) at w->seq[0 .. nloc),
+// segments at w->ioff (local counts).
+int cap_local(fslr_ctx* c, int thr, CapWork* w, int64_t ne, bool all_reads = false) {
   hipStream_t s = c->stream;
-  const int64_t n = c->n;
+  set_space(c, w);
+  const int64_t n = w->n;
   w->thr = thr;
-  w->n = n;
   w->ne = ne;
   w->prepared = false;
   {
@@ -816,9 +902,10 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, int64_t ne) {
   HIP_TRY(c, hipMemsetAsync(w->err, 0, 4 * sizeof(int), s));
   HIP_TRY(c, hipMemsetAsync(w->stats, 0, kStWords * sizeof(long long), s));
   // 1. closure: rounds in batches of 8, one sync per batch (chg[0] = 1 starts each batch)
-  k_cap_init<<<grid_for(n), 256, 0, s>>>(c->fwd, static_cast<int>(n), thr, w->state, w->back);
+  if (all_reads) k_cap_all<<<grid_for(n), 256, 0, s>>>(w->state, static_cast<int>(n));
+  else k_cap_init<<<grid_for(n), 256, 0, s>>>(c->fwd, static_cast<int>(n), thr, w->state, w->back);
   HIP_TRY(c, hipGetLastError());
-  for (int batch = 0;; ++batch) {
+  for (int batch = 0; !all_reads; ++batch) {
     HIP_TRY(c, hipMemsetAsync(w->chg, 0, 16 * sizeof(int), s));
     HIP_TRY(c, hipMemsetAsync(w->chg, 0xff, sizeof(int), s));
     for (int r = 1; r <= 8; ++r) {
@@ -834,7 +921,7 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, int64_t ne) {
     if (batch > (n >> 3) + 2) return fail(c, FSLR_ERR_STATE, "edge cap closure does not converge");
   }
   // T in rank order, T-intervals
-  k_cap_tpack<<<grid_for(n), 256, 0, s>>>(w->state, c->rmeta, static_cast<int>(n), w->tv);
+  k_cap_tpack<<<grid_for(n), 256, 0, s>>>(w->state, c->rmeta, w->rlen, static_cast<int>(n), w->tv);
   size_t tb = 0;
   HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tb, w->tv, w->tvs, static_cast<int>(n), s));
   if (int rc = ensure_temp(c, w, tb)) return rc;
@@ -864,10 +951,11 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, int64_t ne) {
   if (nt > 0) {
     k_cap_tread<<<grid_for(nt), 256, 0, s>>>(w->toff, nt, w->tread);
     HIP_TRY(c, hipMemsetAsync(w->tq, 0xff, static_cast<size_t>(nti) * sizeof(int), s));
-    k_cap_tq<<<grid_for(c->ni_idx), 256, 0, s>>>(c->idx4, static_cast<int>(c->ni_idx), w->t_of, w->toff, w->tq);
+    k_cap_tq<<<grid_for(c->ni_idx), 256, 0, s>>>(c->idx4, static_cast<int>(c->ni_idx), w->t_of, w->toff, w->vreal,
+                                                 w->vbase, w->tq);
     // 2. hits of the T-intervals this index holds: count, scan, emit top-down, ties, partner reads
-    k_cap_hits<false><<<wave_grid(nti), 256, 0, s>>>(w->tq, w->tread, w->T, c->idx4, c->rng_s, nti, w->icnt, nullptr,
-                                                      nullptr);
+    k_cap_hits<false><<<wave_grid(nti), 256, 0, s>>>(w->tq, w->tread, w->T, c->idx4, c->rng_s, w->vreal, nti,
+                                                      w->icnt, nullptr, nullptr);
     HIP_TRY(c, hipGetLastError());
   }
   HIP_TRY(c, hipMemsetAsync(w->icnt + nti, 0, sizeof(int), s));
@@ -889,9 +977,9 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, int64_t ne) {
     if (int rc = c4.commit(c, w->ar[4])) return rc;
   }
   if (nti > 0 && w->nloc > 0) {
-    k_cap_hits<true><<<wave_grid(nti), 256, 0, s>>>(w->tq, w->tread, w->T, c->idx4, c->rng_s, nti, nullptr, w->ioff,
-                                                     w->seqp);
-    k_cap_seq<<<wave_grid(nti), 256, 0, s>>>(w->seqp, c->idx4, w->ioff, nti, w->seq);
+    k_cap_hits<true><<<wave_grid(nti), 256, 0, s>>>(w->tq, w->tread, w->T, c->idx4, c->rng_s, w->vreal, nti, nullptr,
+                                                     w->ioff, w->seqp);
+    k_cap_seq<<<wave_grid(nti), 256, 0, s>>>(w->seqp, c->idx4, w->ioff, w->vreal, nti, w->seq);
     HIP_TRY(c, hipGetLastError());
   }
   w->prepared = true;
@@ -900,10 +988,10 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, int64_t ne) {
 
 // Phase B: the sequence (w->seq, segments w->ioff, w->nseq elements) -> slots, predicates, loops,
 // the capped graph written back into the context.
-int cap_core(fslr_ctx* c, CapWork* w, fslr_cap_stats* cs) {
+// 3. slots: the distinct partners of each read of T — a stable radix sort of (t, partner) keys by
+// sequence position, unique — and each slot's pair predicate.  Returns the slot count in w->ns.
+int cap_slots(fslr_ctx* c, CapWork* w) {
   hipStream_t s = c->stream;
-  const int thr = w->thr;
-  const int64_t n = w->n, ne = w->ne;
   const int nt = static_cast<int>(w->nt), nti = static_cast<int>(w->nti);
   const int m = static_cast<int>(w->nseq);
   {
@@ -924,36 +1012,49 @@ int cap_core(fslr_ctx* c, CapWork* w, fslr_cap_stats* cs) {
     cv.add(&w->rec, m);
     if (int rc = cv.commit(c, w->ar[2])) return rc;
   }
-  int ns = 0;
+  w->ns = 0;
+  if (m == 0) return FSLR_OK;
+  k_cap_keys<<<wave_grid(nti), 256, 0, s>>>(w->seq, w->ioff, w->tread, nti, w->skey, w->sval);
+  size_t b1 = 0, b2 = 0, b3 = 0;
+  const int kbits = 25 + bits_for(nt);
+  HIP_TRY(c, hipcub::DeviceRadixSort::SortPairs(nullptr, b1, w->skey, w->skey2, w->sval, w->sval2, m, 0, kbits, s));
+  HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(nullptr, b2, w->head, w->hs, m, s));
+  HIP_TRY(c, hipcub::DeviceRadixSort::SortKeys(nullptr, b3, w->ck, w->ck2, std::max(nt, 1), 0, 50, s));
+  if (int rc = ensure_temp(c, w, std::max({b1, b2, b3}))) return rc;
+  size_t tb = w->temp_bytes;
+  HIP_TRY(c, hipcub::DeviceRadixSort::SortPairs(w->temp, tb, w->skey, w->skey2, w->sval, w->sval2, m, 0, kbits, s));
+  k_cap_heads<<<grid_for(m), 256, 0, s>>>(w->skey2, m, w->head);
+  tb = w->temp_bytes;
+  HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(w->temp, tb, w->head, w->hs, m, s));
+  k_cap_slots<<<grid_for(m), 256, 0, s>>>(w->skey2, w->sval2, w->head, w->hs, m, w->slot_of, w->ukey, w->fpos,
+                                          w->host_dev);
+  HIP_TRY(c, hipGetLastError());
+  HIP_TRY(c, hipStreamSynchronize(s));
+  const int ns = static_cast<int>(host_word(w, kHNslots));
+  w->ns = ns;
+  k_cap_eval<<<wave_grid(ns), 256, 0, s>>>(w->ukey, ns, w->T, c->rmeta, c->iv, w->rlen, w->off2, c->last_qcut,
+                                           c->last_ncut, w->umax, w->n_umax, w->flags);
+  HIP_TRY(c, hipGetLastError());
+  return FSLR_OK;
+}
+
+int cap_core(fslr_ctx* c, CapWork* w, fslr_cap_stats* cs) {
+  hipStream_t s = c->stream;
+  const int thr = w->thr;
+  const int64_t n = w->n, ne = w->ne;
+  const int nt = static_cast<int>(w->nt);
+  const int m = static_cast<int>(w->nseq);
+  if (int rc = cap_slots(c, w)) return rc;
+  const int ns = static_cast<int>(w->ns);
   if (m > 0) {
-    // 3. slots: sort (t, partner) keys stably by sequence position, unique
-    k_cap_keys<<<wave_grid(nti), 256, 0, s>>>(w->seq, w->ioff, w->tread, nti, w->skey, w->sval);
-    size_t b1 = 0, b2 = 0, b3 = 0;
-    const int kbits = 25 + bits_for(nt);
-    HIP_TRY(c, hipcub::DeviceRadixSort::SortPairs(nullptr, b1, w->skey, w->skey2, w->sval, w->sval2, m, 0, kbits, s));
-    HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(nullptr, b2, w->head, w->hs, m, s));
-    HIP_TRY(c, hipcub::DeviceRadixSort::SortKeys(nullptr, b3, w->ck, w->ck2, std::max(nt, 1), 0, 50, s));
-    if (int rc = ensure_temp(c, w, std::max({b1, b2, b3}))) return rc;
-    size_t tb = w->temp_bytes;
-    HIP_TRY(c, hipcub::DeviceRadixSort::SortPairs(w->temp, tb, w->skey, w->skey2, w->sval, w->sval2, m, 0, kbits, s));
-    k_cap_heads<<<grid_for(m), 256, 0, s>>>(w->skey2, m, w->head);
-    tb = w->temp_bytes;
-    HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(w->temp, tb, w->head, w->hs, m, s));
-    k_cap_slots<<<grid_for(m), 256, 0, s>>>(w->skey2, w->sval2, w->head, w->hs, m, w->slot_of, w->ukey, w->fpos,
-                                            w->host_dev);
-    HIP_TRY(c, hipGetLastError());
-    HIP_TRY(c, hipStreamSynchronize(s));
-    ns = static_cast<int>(host_word(w, kHNslots));
-    // predicates, mirror slots, the dependency components
-    k_cap_eval<<<wave_grid(ns), 256, 0, s>>>(w->ukey, ns, w->T, c->rmeta, c->iv, c->last_qcut, c->last_ncut, c->umax,
-                                             w->flags);
+    // mirror slots, the dependency components
     k_cap_mirror<<<grid_for(ns), 256, 0, s>>>(w->ukey, ns, w->T, w->t_of, w->mslot, w->upairs, w->err);
     HIP_TRY(c, hipGetLastError());
     HIP_TRY(c, launch_uf_init(w->tpar, nt, s));
     HIP_TRY(c, launch_uf_pair_list(w->tpar, w->upairs, ns, s));
     HIP_TRY(c, launch_uf_finalize(w->tpar, nt, s));
     k_cap_ckeys<<<grid_for(nt), 256, 0, s>>>(w->tpar, nt, w->ck);
-    tb = w->temp_bytes;
+    size_t tb = w->temp_bytes;
     HIP_TRY(c, hipcub::DeviceRadixSort::SortKeys(w->temp, tb, w->ck, w->ck2, nt, 0, 50, s));
     k_cap_recs<<<grid_for(m), 256, 0, s>>>(w->slot_of, w->ukey, w->fpos, w->flags, w->mslot, w->T, w->t_of, m, w->rec);
     HIP_TRY(c, hipMemsetAsync(w->vis2, 0, static_cast<size_t>(ns), s));
@@ -1178,6 +1279,108 @@ extern "C" int fslr_cap_replay(fslr_ctx* c, const int32_t* counts, const int32_t
   fslr_cap_stats cs;
   std::memset(&cs, 0, sizeof(cs));
   if (int rc = cap_core(c, w, &cs)) return rc;
+  c->cap_stats = cs;
+  if (out) *out = cs;
+  return FSLR_OK;
+}
+
+extern "C" int fslr_long_pairs(fslr_ctx* c, const fslr_params* p, int64_t* n_edges) {
+  if (!c || !p || !n_edges) return FSLR_ERR_INVALID;
+  *n_edges = 0;
+  if (!c->lg_set) return fail(c, FSLR_ERR_STATE, "fslr_set_long_reads first");
+  if (!c->index_built || c->filter_active) return fail(c, FSLR_ERR_STATE, "fslr_build_index (every chromosome) first");
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  if (int rc = ensure_bwd_ranges(c)) return rc;
+  c->last_qcut = p->qlen_cut;
+  c->last_ncut = p->nal_cut;
+  c->last_full = false;
+  c->edges_global = false;
+  std::memset(&c->cap_stats, 0, sizeof(c->cap_stats));
+  CapWork* w = nullptr;
+  if (int rc = cap_work(c, &w)) return rc;
+  if (int rc = cap_local(c, 0, w, 0, true)) return rc;          // every read's hits, any thresholds
+  w->nseq = w->nloc;
+  if (int rc = cap_slots(c, w)) return rc;
+  const int ns = static_cast<int>(w->ns);
+  // every pair is in both reads' slots: at most ns / 2 edges
+  const int64_t need = std::max<int64_t>(ns / 2 + 1, 1024);
+  if (need > c->lg_edge_cap) {
+    if (dalloc(c, &c->lg_edges, need)) return FSLR_ERR_NOMEM;
+    c->lg_edge_cap = need;
+  }
+  if (need > c->edge_cap)
+    if (int rc = fslr_reserve_edges(c, need)) return rc;
+  if (!c->lg_cnt && dalloc(c, &c->lg_cnt, 4)) return FSLR_ERR_NOMEM;
+  HIP_TRY(c, hipMemsetAsync(c->lg_cnt, 0, 4 * sizeof(unsigned long long), s));
+  HIP_TRY(c, hipMemsetAsync(c->fwd, 0, static_cast<size_t>(c->n) * sizeof(int), s));
+  HIP_TRY(c, hipMemsetAsync(c->errw, 0, kErrWords * sizeof(int), s));
+  if (ns > 0)
+    k_cap_pairs_out<<<grid_for(ns), 256, 0, s>>>(w->ukey, ns, w->T, w->flags, c->lg_edges, c->lg_edge_cap, c->edges,
+                                                  c->edge_iu, c->edge_cap, c->lg_cnt, c->fwd, w->err);
+  HIP_TRY(c, hipGetLastError());
+  unsigned long long cnt = 0;
+  int err = 0;
+  HIP_TRY(c, hipMemcpyAsync(&cnt, c->lg_cnt, sizeof(cnt), hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipMemcpyAsync(&err, w->err, sizeof(int), hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipMemcpyAsync(c->counters + kEdgeCount, &cnt, sizeof(cnt), hipMemcpyHostToDevice, s));
+  HIP_TRY(c, hipStreamSynchronize(s));
+  w->prepared = false;
+  if (err & kCapErrZd) return fail(c, FSLR_ERR_ZERO_DIVISION, "division by zero");
+  c->lg_n_edges = static_cast<int64_t>(cnt);
+  c->last_engine = FSLR_ENGINE_WALK;
+  *n_edges = c->lg_n_edges;
+  return FSLR_OK;
+}
+
+extern "C" int fslr_cap_replay_pairs(fslr_ctx* c, int32_t thr, const int32_t* a, const int32_t* b, int64_t ne,
+                                     uint8_t* who, int32_t* fwd, fslr_cap_stats* out) {
+  if (!c || ne < 0 || ((!a || !b || !who) && ne) || ne >= (int64_t(1) << 31)) return FSLR_ERR_INVALID;
+  if (!c->reads_set || !c->index_built || c->filter_active)
+    return fail(c, FSLR_ERR_STATE, "fslr_build_index (every chromosome) first");
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const int64_t n = c->lg_set ? c->lg_n_real : c->n;
+  // the edge list (read ranks of the replay's read space, a < b) becomes this context's E*
+  std::vector<int2> ab(static_cast<size_t>(ne));
+  std::vector<int> deg(static_cast<size_t>(n), 0);
+  int max_fwd = 0;
+  for (int64_t k = 0; k < ne; ++k) {
+    if (a[k] < 0 || a[k] >= b[k] || b[k] >= n) return fail(c, FSLR_ERR_INVALID, "edges must be (a < b) read ranks");
+    ab[k] = make_int2(a[k], b[k]);
+    max_fwd = std::max(max_fwd, ++deg[a[k]]);
+  }
+  if (ne > c->edge_cap)
+    if (int rc = fslr_reserve_edges(c, ne)) return rc;
+  if (!c->counters) return fail(c, FSLR_ERR_STATE, "no query has run");
+  if (ne) HIP_TRY(c, hipMemcpyAsync(c->edges, ab.data(), ab.size() * sizeof(int2), hipMemcpyHostToDevice, s));
+  HIP_TRY(c, hipMemsetAsync(c->edge_iu, 0, std::max<int64_t>(ne, 1) * sizeof(unsigned short), s));
+  HIP_TRY(c, hipMemcpyAsync(c->fwd, deg.data(), deg.size() * sizeof(int), hipMemcpyHostToDevice, s));
+  const unsigned long long ne_u = static_cast<unsigned long long>(ne);
+  HIP_TRY(c, hipMemcpyAsync(c->counters + kEdgeCount, &ne_u, sizeof(ne_u), hipMemcpyHostToDevice, s));
+  int ew[kErrWords] = {};
+  ew[3] = max_fwd;
+  HIP_TRY(c, hipMemcpyAsync(c->errw, ew, sizeof(ew), hipMemcpyHostToDevice, s));
+  HIP_TRY(c, hipStreamSynchronize(s));
+  c->edges_global = true;
+  std::memset(&c->cap_stats, 0, sizeof(c->cap_stats));
+  fslr_cap_stats cs;
+  std::memset(&cs, 0, sizeof(cs));
+  cs.max_fwd = max_fwd;
+  if (max_fwd > thr) {
+    if (int rc = ensure_bwd_ranges(c)) return rc;
+    CapWork* w = nullptr;
+    if (int rc = cap_work(c, &w)) return rc;
+    if (int rc = cap_local(c, thr, w, ne)) return rc;
+    w->nseq = w->nloc;
+    if (int rc = cap_core(c, w, &cs)) return rc;
+    if (ne) HIP_TRY(c, hipMemcpyAsync(who, w->who, static_cast<size_t>(ne), hipMemcpyDeviceToHost, s));
+    if (fwd) HIP_TRY(c, hipMemcpyAsync(fwd, c->fwd, static_cast<size_t>(n) * sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+  } else {
+    if (ne) std::memset(who, 0, static_cast<size_t>(ne));
+    if (fwd) std::copy(deg.begin(), deg.end(), fwd);
+  }
   c->cap_stats = cs;
   if (out) *out = cs;
   return FSLR_OK;

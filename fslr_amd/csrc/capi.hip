@@ -272,6 +272,8 @@ int fslr_set_reads(fslr_ctx* c, const fslr_reads* r) {
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   c->reads_set = true;
   c->index_built = false;
+  c->lg_set = false;                        // a virtual-read map belongs to the reads it was set for
+  c->edges_global = false;
   ++c->input_gen;
   return FSLR_OK;
 }

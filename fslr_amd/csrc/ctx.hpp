@@ -119,6 +119,7 @@ struct fslr_ctx {
   int* lg_vbase = nullptr;                  // [virtual reads] index of its first interval in the real read
   int* lg_rlen = nullptr;                   // [real reads] interval count
   int* lg_umax = nullptr;                   // [n_umax] largest passing U per I (cluster.py:216-219)
+  int* lg_off2 = nullptr;                   // [real reads] CSR offset of a long read's intervals beyond FSLR_MAX_L
   unsigned long long *lg_pk = nullptr, *lg_ij = nullptr, *lg_pk2 = nullptr, *lg_ij2 = nullptr;
   int64_t lg_cap = 0;
   unsigned long long* lg_cnt = nullptr;     // [4] short entries, long entries, long edges, run count

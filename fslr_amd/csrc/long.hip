@@ -141,6 +141,16 @@ k_long_greedy(const unsigned long long* __restrict__ uniq, const int* __restrict
   }
 }
 
+constexpr int kMaxRealL = 4096;           // the cap replay's general pair evaluator (cap.hip kMaxLongL)
+
+// the CSR offset of each long real read's second chunk: its intervals beyond FSLR_MAX_L are the
+// consecutive chunks from there (prep.split_long_reads lays a read's chunks out in order)
+__global__ void k_long_off2(const int4* __restrict__ rmeta, const int* __restrict__ vreal,
+                            const int* __restrict__ vbase, int n_real, int nv, int* __restrict__ off2) {
+  for (int v = n_real + blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += gridDim.x * blockDim.x)
+    if (vbase[v] == FSLR_MAX_L) off2[vreal[v]] = rmeta[v].x;
+}
+
 template <typename T>
 int grow(fslr_ctx* c, T** p, int64_t* cap, int64_t need) {
   if (need <= *cap) return FSLR_OK;
@@ -156,7 +166,7 @@ int grow(fslr_ctx* c, T** p, int64_t* cap, int64_t need) {
 using namespace fslr;
 
 void fslr_long_free(fslr_ctx* c) {
-  void* bufs[] = {c->lg_vreal, c->lg_vbase, c->lg_rlen, c->lg_umax, c->lg_pk, c->lg_ij, c->lg_pk2, c->lg_ij2,
+  void* bufs[] = {c->lg_vreal, c->lg_vbase, c->lg_rlen, c->lg_umax, c->lg_off2, c->lg_pk, c->lg_ij, c->lg_pk2, c->lg_ij2,
                   c->lg_edges, c->lg_cnt,   c->lg_uniq, c->lg_rlen_run, c->lg_roff, c->lg_words, c->lg_woff,
                   c->lg_bits,  c->lg_temp, c->lg_ent, c->lg_short};
   for (void* b : bufs)
@@ -185,13 +195,18 @@ extern "C" int fslr_set_long_reads(fslr_ctx* c, int64_t n_real, const int32_t* v
       return fail(c, FSLR_ERR_INVALID, "virtual read map out of range");
   }
   if (n_umax < maxl) return fail(c, FSLR_ERR_INVALID, "umax must cover I up to the longest read");
+  if (maxl > kMaxRealL) return fail(c, FSLR_ERR_INVALID, "reads of more than 4096 intervals are not supported");
   if (dalloc(c, &c->lg_vreal, nv) || dalloc(c, &c->lg_vbase, nv) || dalloc(c, &c->lg_rlen, n_real) ||
-      dalloc(c, &c->lg_umax, n_umax) || (!c->lg_cnt && dalloc(c, &c->lg_cnt, 4)))
+      dalloc(c, &c->lg_umax, n_umax) || dalloc(c, &c->lg_off2, std::max<int64_t>(n_real, 1)) ||
+      (!c->lg_cnt && dalloc(c, &c->lg_cnt, 4)))
     return FSLR_ERR_NOMEM;
   HIP_TRY(c, hipMemcpyAsync(c->lg_vreal, vreal, nv * sizeof(int), hipMemcpyHostToDevice, c->stream));
   HIP_TRY(c, hipMemcpyAsync(c->lg_vbase, vbase, nv * sizeof(int), hipMemcpyHostToDevice, c->stream));
   if (n_real) HIP_TRY(c, hipMemcpyAsync(c->lg_rlen, rlen, n_real * sizeof(int), hipMemcpyHostToDevice, c->stream));
   if (n_umax) HIP_TRY(c, hipMemcpyAsync(c->lg_umax, umax, n_umax * sizeof(int), hipMemcpyHostToDevice, c->stream));
+  if (nv > n_real)
+    k_long_off2<<<grid_for(nv - n_real), 256, 0, c->stream>>>(c->rmeta, c->lg_vreal, c->lg_vbase, n_real, nv, c->lg_off2);
+  HIP_TRY(c, hipGetLastError());
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   c->lg_n_real = n_real;
   c->lg_n_umax = n_umax;

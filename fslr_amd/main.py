@@ -123,6 +123,11 @@ def run_clustering(args, basename):
     t = {}
     t0 = time.perf_counter()
     print('Making clusters')
+    if (args.get('gpus') or 1) > 1:
+        # the other ranks start now: their interpreter, torch import and process-group rendezvous run
+        # while this process reads and prepares the input (fslr_amd.multi.RankPool)
+        from . import multi
+        multi.pool(args['gpus'], first_device=args.get('device') or 0)
     tsv, bed_file = _native_open(f'{basename}.mappings.bed') if args.get('native_io', True) else (None, None)
     if bed_file is None:
         bed_file = pd.read_csv(f'{basename}.mappings.bed', sep='\t')

@@ -68,7 +68,7 @@
 extern "C" {
 #endif
 
-#define FSLR_ABI_VERSION 7
+#define FSLR_ABI_VERSION 8
 #define FSLR_MAX_L 64                /* max intervals per read (bitmask width) */
 #define FSLR_MAX_READS (1 << 25)     /* read rank packs into bits 6..30 of the index record */
 #define FSLR_THR_ZERO_ALN INT32_MIN
@@ -283,6 +283,21 @@ int  fslr_set_long_reads(fslr_ctx *ctx, int64_t n_real, const int32_t *vreal, co
                          const int32_t *rlen, const int32_t *umax, int32_t n_umax);
 int  fslr_long_query(fslr_ctx *ctx, const fslr_params *params, int64_t *n_long_edges);
 int  fslr_get_long_edges(fslr_ctx *ctx, int32_t *a, int32_t *b, int32_t *I, int32_t *U, int64_t capacity);
+/* The general pair path (any overlap, aln_size == 0 intervals, qlen2 / n_alignments
+ * 0, reads of up to 4096 intervals), replacing cluster.py:197-222 where the sweep's gates do not
+ * apply.  fslr_long_pairs (after fslr_set_reads [+ fslr_set_long_reads] and fslr_build_index):
+ * every read's search-ordered hits, each distinct pair decided once by the reference's first-fit
+ * (list1 = the lower-rank read) into the long-edge list (fslr_get_long_edges, I and U unclamped) and
+ * the context's edges and forward degrees (then fslr_components); FSLR_ERR_ZERO_DIVISION when a pair
+ * raises.  Syncs.
+ * fslr_cap_replay_pairs: the edge cap (cluster.py:223-224) replayed over the given E* — ne pairs of
+ * real read ranks a < b, host arrays — in the read space of the last fslr_set_reads (+
+ * fslr_set_long_reads).  who[k] = 0 when edge k is formed in a's loop, 1 in b's, 2 when the capped
+ * graph drops it; fwd[n_reads] (may be NULL) = edges formed in each read's own loop.  The capped
+ * graph also becomes the context's edges (fslr_components).  Syncs; out may be NULL. */
+int  fslr_long_pairs(fslr_ctx *ctx, const fslr_params *params, int64_t *n_edges);
+int  fslr_cap_replay_pairs(fslr_ctx *ctx, int32_t edge_threshold, const int32_t *a, const int32_t *b, int64_t ne,
+                           uint8_t *who, int32_t *fwd, fslr_cap_stats *out);
 
 /* build_index + query(all reads) + components, enqueued back to back.  Async. */
 int  fslr_run(fslr_ctx *ctx, const fslr_params *params);

@@ -247,9 +247,55 @@ static int index_build(const oracle_input *in, oracle_index *ix) {
     return ORACLE_OK;
 }
 
+/* Reached lists for the lean seen-set (oracle_query_lean): the partners > r that read r's own
+ * query inserted into `seen` before its first edge-cap break, for reads whose query broke. */
+typedef struct { int64_t *off; int32_t *pool; int64_t n, cap; unsigned char *broke; } reached_lists;
+
+static int rl_push(reached_lists *rl, int32_t v) {
+    if (rl->n == rl->cap) {
+        int64_t nc = rl->cap ? rl->cap * 2 : (1 << 20);
+        int32_t *np = (int32_t *)realloc(rl->pool, (size_t)nc * sizeof(int32_t));
+        if (!np) return -1;
+        rl->pool = np; rl->cap = nc;
+    }
+    rl->pool[rl->n++] = v;
+    return 0;
+}
+
+static int cmp_i32(const void *x, const void *y) {
+    int32_t a = *(const int32_t *)x, b = *(const int32_t *)y;
+    return (a > b) - (a < b);
+}
+
+static int query_impl(const oracle_input *in, const oracle_params *p,
+                      int64_t *edge_a, int64_t *edge_b, int32_t *edge_I, int32_t *edge_U, int64_t edge_capacity,
+                      int32_t *fwd_count, int32_t *comp, oracle_stats *st, int lean);
+
 int oracle_query(const oracle_input *in, const oracle_params *p,
                  int64_t *edge_a, int64_t *edge_b, int32_t *edge_I, int32_t *edge_U, int64_t edge_capacity,
                  int32_t *fwd_count, int32_t *comp, oracle_stats *st) {
+    return query_impl(in, p, edge_a, edge_b, edge_I, edge_U, edge_capacity, fwd_count, comp, st, 0);
+}
+
+/* oracle_query with the seen-set (cluster.py:205-207) held per read instead of as one set of
+ * pairs — the same answer in O(reads + reached pairs of broken reads) memory, for full-size runs
+ * (config 5: ~1e10 distinct pairs would not fit a pair hash set).  Why it is the same set: when
+ * read a meets partner b,
+ *   - b > a: {a, b} can only have been inserted earlier in a's own query -> a per-query stamp;
+ *   - b < a: {a, b} was inserted in b's query iff b's query visited a before it stopped.  A query
+ *     that never met the edge-cap break visited every hit partner, and hits are symmetric (a's
+ *     interval overlaps b's), so it visited a; a query that broke visited exactly the partners it
+ *     recorded in its reached list (partners > b only: the others are never queried again).
+ * tests/test_oracle.py checks both forms equal on every capped fixture. */
+int oracle_query_lean(const oracle_input *in, const oracle_params *p,
+                      int64_t *edge_a, int64_t *edge_b, int32_t *edge_I, int32_t *edge_U, int64_t edge_capacity,
+                      int32_t *fwd_count, int32_t *comp, oracle_stats *st) {
+    return query_impl(in, p, edge_a, edge_b, edge_I, edge_U, edge_capacity, fwd_count, comp, st, 1);
+}
+
+static int query_impl(const oracle_input *in, const oracle_params *p,
+                      int64_t *edge_a, int64_t *edge_b, int32_t *edge_I, int32_t *edge_U, int64_t edge_capacity,
+                      int32_t *fwd_count, int32_t *comp, oracle_stats *st, int lean) {
     memset(st, 0, sizeof(*st));
     st->err_a = st->err_b = -1;
     const int64_t N = in->n_reads;
@@ -263,6 +309,9 @@ int oracle_query(const oracle_input *in, const oracle_params *p,
 
     pairset seen;
     if (ps_init(&seen, 1 << 16) != 0) { index_free(&ix); free(used); return ORACLE_NOMEM; }
+    reached_lists rl;
+    memset(&rl, 0, sizeof(rl));
+    int64_t *stamp = NULL;                         /* lean: last query read that met each read */
     int rc = ORACLE_OK;
     int64_t ne = 0;
     /* graph node insertion order (networkx dict order) */
@@ -271,11 +320,20 @@ int oracle_query(const oracle_input *in, const oracle_params *p,
     int64_t *ins_pos = (int64_t *)malloc((size_t)(N > 0 ? N : 1) * sizeof(int64_t));
     int64_t *uf = (int64_t *)malloc((size_t)(N > 0 ? N : 1) * sizeof(int64_t));
     if (!ins_order || !ins_pos || !uf) { rc = ORACLE_NOMEM; goto done; }
+    if (lean) {
+        rl.off = (int64_t *)malloc((size_t)(N + 1) * sizeof(int64_t));
+        rl.broke = (unsigned char *)calloc((size_t)(N > 0 ? N : 1), 1);
+        stamp = (int64_t *)malloc((size_t)(N > 0 ? N : 1) * sizeof(int64_t));
+        if (!rl.off || !rl.broke || !stamp) { rc = ORACLE_NOMEM; goto done; }
+        for (int64_t r = 0; r < N; r++) stamp[r] = -1;
+        rl.off[0] = 0;
+    }
     for (int64_t r = 0; r < N; r++) { ins_pos[r] = -1; uf[r] = r; fwd_count[r] = 0; }
 
     const int64_t qend = (p->query_end >= 0 && p->query_end < N) ? p->query_end : N;
     for (int64_t a = 0; a < qend && rc == ORACLE_OK; a++) {
         int64_t edges = 0;
+        const int64_t rl_begin = rl.n;
         const int64_t a0 = in->read_off[a], la = in->read_off[a + 1] - a0;
         for (int64_t i = 0; i < la && rc == ORACLE_OK; i++) {
             const int64_t itv = a0 + i;
@@ -290,8 +348,25 @@ int oracle_query(const oracle_input *in, const oracle_params *p,
                 st->interval_hits++;
                 const int64_t b = read_of[o];
                 if (b == a) continue;                     /* cluster.py:203-204 */
-                const uint64_t lo_r = (uint64_t)(a < b ? a : b), hi_r = (uint64_t)(a < b ? b : a);
-                int ins = ps_insert(&seen, lo_r * (uint64_t)N + hi_r);
+                int ins;
+                if (!lean) {
+                    const uint64_t lo_r = (uint64_t)(a < b ? a : b), hi_r = (uint64_t)(a < b ? b : a);
+                    ins = ps_insert(&seen, lo_r * (uint64_t)N + hi_r);
+                } else if (stamp[b] == a) {
+                    ins = 0;                              /* met earlier in this query */
+                } else {
+                    stamp[b] = a;
+                    if (b > a) {
+                        ins = 1;
+                        if (rl_push(&rl, (int32_t)b) != 0) ins = -1;
+                    } else if (!rl.broke[b]) {
+                        ins = 0;                          /* b's unbroken query visited a */
+                    } else {
+                        const int32_t key = (int32_t)a;
+                        ins = bsearch(&key, rl.pool + rl.off[b], (size_t)(rl.off[b + 1] - rl.off[b]),
+                                      sizeof(int32_t), cmp_i32) ? 0 : 1;
+                    }
+                }
                 if (ins < 0) { rc = ORACLE_NOMEM; break; }
                 if (ins == 0) continue;                   /* cluster.py:205-207 */
                 st->evaluated_pairs++;
@@ -322,8 +397,17 @@ int oracle_query(const oracle_input *in, const oracle_params *p,
                     edges++;
                     fwd_count[a]++;
                 }
-                if (p->use_cap && edges >= p->edge_threshold) break;   /* cluster.py:223-224 */
+                if (p->use_cap && edges >= p->edge_threshold) {         /* cluster.py:223-224 */
+                    if (lean) rl.broke[a] = 1;
+                    break;
+                }
             }
+        }
+        if (lean) {
+            /* keep the reached list only for a broken query; sorted for the lookups above */
+            if (!rl.broke[a]) rl.n = rl_begin;
+            else qsort(rl.pool + rl_begin, (size_t)(rl.n - rl_begin), sizeof(int32_t), cmp_i32);
+            rl.off[a + 1] = rl.n;
         }
         if (fwd_count[a] > st->max_fwd) st->max_fwd = fwd_count[a];
     }
@@ -344,6 +428,7 @@ int oracle_query(const oracle_input *in, const oracle_params *p,
         free(root_comp);
     }
 done:
+    free(rl.off); free(rl.pool); free(rl.broke); free(stamp);
     free(seen.slot); index_free(&ix); free(used);
     free(ins_order); free(ins_pos); free(uf);
     return rc;

@@ -58,9 +58,10 @@ def lib():
         if not os.path.exists(LIB_PATH):
             build()
         L = ctypes.CDLL(LIB_PATH)
-        L.oracle_query.restype = ctypes.c_int
-        L.oracle_query.argtypes = [ctypes.POINTER(_Input), ctypes.POINTER(_Params)] + [ctypes.c_void_p] * 4 + [
-            ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(_Stats)]
+        for fn in (L.oracle_query, L.oracle_query_lean):
+            fn.restype = ctypes.c_int
+            fn.argtypes = [ctypes.POINTER(_Input), ctypes.POINTER(_Params)] + [ctypes.c_void_p] * 4 + [
+                ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(_Stats)]
         L.oracle_jaccard_lists.restype = ctypes.c_int
         L.oracle_jaccard_lists.argtypes = [ctypes.c_int64] + [ctypes.c_void_p] * 4 + [ctypes.c_int64] + \
             [ctypes.c_void_p] * 4 + [ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p]
@@ -101,8 +102,10 @@ class OracleZeroDivision(ZeroDivisionError):
 
 
 def run_core(csr: OracleCSR, overlap=0.8, cutoffs=(1, 1, 0.66, 0.66, 0.66, 0.5), qlen_diff=0.04,
-             n_aln_diff=0.25, edge_threshold=10, use_cap=True, query_end=-1):
+             n_aln_diff=0.25, edge_threshold=10, use_cap=True, query_end=-1, lean=False):
     """Run ``oracle_query``; returns dict with edges, fwd counts, component per read, stats.
+
+    ``lean`` runs ``oracle_query_lean`` (the same seen-set held per read: full-size inputs).
 
     ``query_end`` >= 0 restricts the driver to query reads [0, query_end) (a bounded
     sample for the CPU baseline; components are then those of the sampled edges).
@@ -123,7 +126,7 @@ def run_core(csr: OracleCSR, overlap=0.8, cutoffs=(1, 1, 0.66, 0.66, 0.66, 0.5),
         fwd = np.zeros(max(N, 1), np.int32)
         comp = np.full(max(N, 1), -1, np.int32)
         st = _Stats()
-        rc = L.oracle_query(ctypes.byref(inp), ctypes.byref(prm), _p(ea), _p(eb), _p(eI), _p(eU), cap, _p(fwd),
+        rc = (L.oracle_query_lean if lean else L.oracle_query)(ctypes.byref(inp), ctypes.byref(prm), _p(ea), _p(eb), _p(eI), _p(eU), cap, _p(fwd),
                             _p(comp), ctypes.byref(st))
         if rc == ORACLE_EDGE_CAPACITY:
             cap *= 4

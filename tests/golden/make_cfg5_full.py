@@ -79,7 +79,7 @@ def main():
                      np.repeat(csr.read_qlen2, cnt), np.repeat(csr.read_nal, cnt), csr.data_pos)
     del csr
     t = time.perf_counter()
-    o = O.run_core(oc, use_cap=True)
+    o = O.run_core(oc, use_cap=True, lean=True)
     el = time.perf_counter() - t
     print(f'oracle full run in {el:.0f}s: {o["stats"]}', flush=True)
     d = digests(o['edge_a'], o['edge_b'], o['edge_I'], o['edge_U'], o['fwd'], labels_from_comp(o['comp']))

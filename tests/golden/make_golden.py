@@ -155,6 +155,36 @@ def noclusters_df():
     return df, hdr
 
 
+def chroms115_df():
+    """115 chromosome names (chr1..chr22, chrX and 92 unplaced-contig-style names): the multi-GPU
+    chromosome filter beyond 64 chromosomes (fslr --gpus N), and the radix-pass index build."""
+    df, hdr = synth_df(1500, 8, 31)
+    names = [f'chr{i}' for i in range(1, 23)] + ['chrX'] + [f'chrUn_KI2707{k:02d}v1' for k in range(92)]
+    # every row keeps its coordinates; its chromosome becomes one of 115 by (chromosome, 30-Mb bin)
+    base = pd.factorize(df['chrom'], sort=True)[0]
+    slot = (base * 5 + (df['rstart'].to_numpy() // 30_000_000) % 5) % len(names)
+    df['chrom'] = np.asarray(names, dtype=object)[slot]
+    length = dict(hdr)[hdr[0][0]]
+    return df, [(c, length) for c in names]
+
+
+def longcap_df():
+    """Dense long reads: events of up to 30 reads with 60-150 fillings, so reads of more than 64
+    intervals have more than edge_threshold forward partners and the cap binds with them."""
+    return synth_df(240, 150, 23, lmin=60, cluster_cap=30, size_p=0.06)
+
+
+def longzero_df():
+    """Long reads (65-120 fillings) where one read's qlen2 is 0 for a pair of such reads: the
+    reference raises ZeroDivisionError in different_lengths_or_alignments (cluster.py:178-183)."""
+    df, hdr = synth_df(60, 120, 29, lmin=65)
+    q = df['qname'].to_numpy()
+    rows = np.flatnonzero(np.isin(q, pd.unique(q)[:6]))     # the first reads (events are consecutive)
+    df.loc[rows, 'qstart'] = 0                               # fillings span nothing: qlen2 = 0
+    df.loc[rows, 'qend'] = 0
+    return df, hdr
+
+
 def make_kats(n_random=3000, seed=17):
     """Known answers of the reference predicates on random + boundary inputs."""
     cluster, _ = refharness.load()
@@ -284,11 +314,25 @@ def make_longreads():
     make_fixture('longreads_400', df, hdr, note='1-150 fillings: reads beyond the 64-interval chunk width')
 
 
+def make_round3():
+    df, hdr = chroms115_df()
+    make_fixture('chroms_115', df, hdr, note='115 chromosome names: --gpus N beyond 64 chromosomes')
+    df, hdr = longcap_df()
+    make_fixture('longcap_240', df, hdr, note='dense reads of 60-150 fillings: the edge cap binds with long reads')
+    make_fixture('longreads_p0', *synth_df(160, 110, 37, lmin=50), args=['--overlap', '0', '--jaccard-cutoffs', '0.2'],
+                 note='long reads with overlap 0 (matches need not overlap; the walk engine)')
+    df, hdr = longzero_df()
+    make_fixture('longzero_60', df, hdr, note='a long read with qlen2 0 raises ZeroDivisionError')
+
+
 def main():
     sys.stdout.reconfigure(line_buffering=True)
     refharness.load()
     if sys.argv[1:] == ['--only', 'longreads_400']:
         make_longreads()
+        return
+    if sys.argv[1:2] == ['--round3']:
+        make_round3()
         return
     df, hdr = synth_df(1000, 3, 0, lmin=3)
     make_fixture('cfg1_1k_x3', df, hdr, note='BASELINE config 1: 1k reads x 3 fillings, defaults')
@@ -318,6 +362,7 @@ def main():
     df, hdr = synth_df(1500, 6, 19, cluster_cap=40, size_p=1.0 / 14)
     make_fixture('capbind_1500', df, hdr, note='clusters up to 40 reads: edge cap binds (stub-order)')
     make_longreads()
+    make_round3()
     make_kats()
     make_vector('v10k_l8_s7', 10_000, 8, 7)
     make_vector('v20k_l16_s11', 20_000, 16, 11)

@@ -82,3 +82,93 @@ def test_library_exports_every_declared_symbol():
     names = set(re.findall(r'\b(fslr_bam_\w+)\s*\(', hdr))
     L = B.load()
     assert names and all(hasattr(L, n) for n in names)
+
+
+def _asan_driver(tmp_path):
+    """tests/native/bam_asan_driver.cpp + bam.cpp built with -fsanitize=address (host code only)."""
+    import shutil
+    import subprocess
+    if shutil.which('g++') is None:
+        pytest.skip('no g++')
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = tmp_path / 'bam_asan'
+    subprocess.run(['g++', '-O1', '-g', '-std=c++17', '-fsanitize=address,undefined', '-fno-omit-frame-pointer',
+                    '-pthread', '-I' + os.path.join(root, 'include'), '-o', str(exe),
+                    os.path.join(root, 'tests', 'native', 'bam_asan_driver.cpp'),
+                    os.path.join(root, 'fslr_amd', 'csrc', 'bam.cpp'), '-lz'], check=True)
+    return exe
+
+
+def _corrupt_bams(tmp_path):
+    """A valid BAM, then truncations of its BGZF file and of its decompressed stream, and records whose
+    name / CIGAR / sequence / tag lengths point past their end."""
+    import struct
+    recs = [dict(qname=f'r{i}', flag=0, tid=i % 2, pos=10 * i, mapq=60, cigar=[('S', 3), ('M', 20), ('I', 2), ('M', 5)],
+                 seq='ACGT' * 7 + 'A' * 3, tags=[('XA', 'Z', 'chr1,+5,10M,0'), ('AS', 'i', -i)]) for i in range(40)]
+    good = tmp_path / 'good.bam'
+    B.write_bam(str(good), [('chrA', 100000), ('chrB', 200000)], recs)
+    raw = good.read_bytes()
+    body = gzip.decompress(raw)
+    files = [good]
+
+    def put(name, data, compressed=False):
+        p = tmp_path / name
+        p.write_bytes(data if compressed else B._bgzf_block(bytes(data)) + B._BGZF_EOF)
+        files.append(p)
+
+    for cut in (5, 17, 18, 30, len(raw) // 2, len(raw) - 29, len(raw) - 1):
+        put(f'ctrunc{cut}.bam', raw[:cut], compressed=True)
+    blk = bytearray(raw)
+    blk[10:12] = struct.pack('<H', 60000)            # XLEN past the file
+    put('xlen.bam', blk, compressed=True)
+    blk = bytearray(raw)
+    blk[14:16] = struct.pack('<H', 400)              # the BC subfield's SLEN past XLEN
+    put('slen.bam', blk, compressed=True)
+    blk = bytearray(raw)
+    blk[16:18] = struct.pack('<H', 3)                # BSIZE below header + trailer
+    put('bsize.bam', blk, compressed=True)
+    # the first record: its block_size field offset
+    l_text = struct.unpack_from('<i', body, 4)[0]
+    p = 8 + l_text
+    n_ref = struct.unpack_from('<i', body, p)[0]
+    p += 4
+    for _ in range(n_ref):
+        p += 8 + struct.unpack_from('<i', body, p)[0]
+    r0 = p
+    bs = struct.unpack_from('<i', body, r0)[0]
+    for cut in (r0 + 20, r0 + 40, r0 + 4 + bs - 3, len(body) - 5):
+        put(f'btrunc{cut}.bam', body[:cut])
+    for name, off, fmt, val in [('lname0', 12, '<B', 0), ('ncig', 16, '<H', 4000), ('lseq', 20, '<i', 1 << 20),
+                                ('lseqneg', 20, '<i', -7), ('bsneg', 0, '<i', -4), ('bsbig', 0, '<i', 1 << 30)]:
+        b = bytearray(body)
+        struct.pack_into(fmt, b, r0 + off, val)
+        put(f'{name}.bam', b)
+    # tags: the record's tag area starts after qual; corrupt the AS tag type and a B array count
+    rec = body[r0:r0 + 4 + bs]
+    t = rec.find(b'ASi')
+    for name, patch in [('tagB', b'ASBi' + struct.pack('<i', -3)), ('tagBbig', b'ASBc' + struct.pack('<i', 1 << 28)),
+                        ('tagtype', b'ASq'), ('tagZ', b'AS' + b'Z' + b'x' * 3)]:
+        b = bytearray(body)
+        seg = bytearray(rec)
+        seg[t:t + len(patch)] = patch[:len(seg) - t]
+        b[r0:r0 + 4 + bs] = seg[:4 + bs]
+        put(f'{name}.bam', b)
+    return files
+
+
+def test_corrupt_bam_returns_an_error_under_asan(tmp_path):
+    """Truncated or corrupt BAM / BGZF input: the decoder returns FSLR_BAM_ERROR instead of reading
+    past its buffers (AddressSanitizer + UBSan build of bam.cpp)."""
+    import subprocess
+    exe = _asan_driver(tmp_path)
+    files = _corrupt_bams(tmp_path)
+    env = dict(os.environ, ASAN_OPTIONS='detect_leaks=0:abort_on_error=1', UBSAN_OPTIONS='halt_on_error=1')
+    res = subprocess.run([str(exe)] + [str(f) for f in files], capture_output=True, text=True, env=env, timeout=120)
+    assert res.returncode == 0, res.stderr[-3000:]
+    lines = res.stdout.splitlines()
+    assert len(lines) == len(files)
+    assert lines[0] == 'ok 40'
+    bad = dict(zip([f.name for f in files], lines))
+    for name in ('xlen.bam', 'slen.bam', 'bsize.bam', 'lname0.bam', 'ncig.bam', 'lseq.bam', 'lseqneg.bam', 'bsneg.bam',
+                 'bsbig.bam', 'tagB.bam', 'tagBbig.bam', 'tagtype.bam'):
+        assert bad[name].startswith('error'), (name, bad[name])

@@ -142,12 +142,14 @@ def test_cli_matches_reference_outputs(name, io_flag):
 
 
 @pytest.mark.parametrize('name', ['cfg1_1k_x3', 'capbind_1500', 'zerodiv', 'noclusters', 'longreads_400', 'params_a',
-                                  'edge_cases_p0', 'zipf_800_l64'])
+                                  'edge_cases_p0', 'zipf_800_l64', 'chroms_115', 'longcap_240'])
 def test_cli_multi_gpu_matches_reference_outputs(name):
     """``fslr --gpus 2``: two rank processes (sharing this box's one GPU over gloo) run the
     chromosome-split sweep (fslr_amd.multi); outputs byte-identical to the reference's.  Covers the
     cap replay on rank 0 (capbind_1500), a ZeroDivisionError raised on every rank (zerodiv), the
-    empty graph and the one-GPU fallback for overlap <= 0 (edge_cases_p0)."""
+    empty graph and the one-GPU fallback for overlap <= 0 (edge_cases_p0), 115 chromosomes (more than
+    the device chromosome filter's 64-bit mask held before round 3), long reads with the cap binding
+    (longcap_240, one GPU)."""
     meta = fx.meta(name)
     with tempfile.TemporaryDirectory() as tmp:
         res = run_product_cli(name, tmp, '--gpus=2')
@@ -698,3 +700,57 @@ def test_shard_built_index_matches_full_index():
             c.query(1 - 0.04, 1 - 0.25, pt)
         c.close()
     full.close()
+
+
+def _multi_inputs(name):
+    from fslr_amd.prep import fold_overlap_threshold, pass_table
+    data, _, kw = host_prepare(name)
+    csr = data.csr()
+    cut = [float(x) for x in kw['jaccard_cutoffs'].split(',')]
+    return csr, fold_overlap_threshold(csr.iv_aln, kw['overlap']), kw, pass_table(cut)
+
+
+def test_rank_pool_is_reused_across_queries():
+    """The CLI's persistent ranks (fslr_amd.multi.RankPool): two queries on the same children (same
+    PIDs), each equal to the single-GPU oracle's graph (edges, forward degrees)."""
+    from fslr_amd import multi
+    pool = multi.pool(2)
+    pids = sorted(p.pid for p in pool.procs.values())
+    for name in ('capbind_1500', 'mixed_2k_l8'):
+        csr, thr, kw, pt = _multi_inputs(name)
+        r = multi.query(csr, thr, 1 - kw['qlen_diff'], 1 - kw['n_alignment_diff'], pt, 10, 2)
+        o = O.run_core(oracle_from_csr(csr), kw['overlap'], [float(x) for x in kw['jaccard_cutoffs'].split(',')],
+                       kw['qlen_diff'], kw['n_alignment_diff'], 10, use_cap=True)
+        a, b, I, U = r['edges']
+        assert sorted(zip(a.tolist(), b.tolist(), I.tolist(), U.tolist())) == sorted(
+            zip(o['edge_a'].tolist(), o['edge_b'].tolist(), o['edge_I'].tolist(), o['edge_U'].tolist()))
+        np.testing.assert_array_equal(r['fwd'], o['fwd'])
+        assert multi.pool(2) is pool and sorted(p.pid for p in pool.procs.values()) == pids
+
+
+def test_rank_pool_child_rank0_raises_zero_division(monkeypatch):
+    """Rank 0 as a child process (the caller's HIP runtime already up without torch's): its
+    ZeroDivisionError reaches the caller with its type, and the pool stays usable."""
+    from fslr_amd import multi
+    monkeypatch.setattr(multi, '_rank0_in_process', lambda: False)
+    pool = multi.RankPool(2)
+    try:
+        assert 0 in pool.procs
+        import dataclasses
+        csr, thr, kw, pt = _multi_inputs('cfg1_1k_x3')
+        q2 = csr.read_qlen2.copy()
+        q2[::3] = 0                                  # pairs of two qlen2-0 reads raise (cluster.py:178-183)
+        csr = dataclasses.replace(csr, read_qlen2=q2)
+        assert multi.sweep_applies(csr, thr)
+        with pytest.raises(ZeroDivisionError):
+            O.run_core(oracle_from_csr(csr), use_cap=True)
+        with pytest.raises(ZeroDivisionError):
+            pool.query(csr, thr, 1 - kw['qlen_diff'], 1 - kw['n_alignment_diff'], pt, 10)
+        assert pool.alive()
+        csr, thr, kw, pt = _multi_inputs('cfg1_1k_x3')
+        r = pool.query(csr, thr, 1 - kw['qlen_diff'], 1 - kw['n_alignment_diff'], pt, 10)
+        o = O.run_core(oracle_from_csr(csr), use_cap=True)
+        assert sorted(zip(r['edges'][0].tolist(), r['edges'][1].tolist())) == sorted(
+            zip(o['edge_a'].tolist(), o['edge_b'].tolist()))
+    finally:
+        pool.close()

@@ -141,3 +141,48 @@ def test_threaded_cpu_baseline_counts_equal_the_oracle(nthreads):
     part = O.count_threads(oc, nthreads=nthreads, stride=4)
     own = (np.arange(csr.n_reads) // 64) % 4 == 0
     assert part['n_edges'] == int(full['fwd'][own].sum())
+
+
+def _dense_oracle_csr(n, lmax, seed, squeeze, ccap):
+    import dataclasses
+    s = synth.generate(n, lmax, seed, cluster_cap=ccap, size_p=0.05)
+    c = s.interval_data().csr()
+    st = c.iv_start.astype(np.int64) // squeeze
+    en = st + (c.iv_end.astype(np.int64) - c.iv_start)
+    c = dataclasses.replace(c, iv_start=st.astype(np.int32), iv_end=en.astype(np.int32))
+    cnt = np.diff(c.read_off)
+    return O.OracleCSR(c.read_off, c.iv_chrom, c.iv_start, c.iv_end, c.iv_aln, np.repeat(c.read_qlen2, cnt),
+                       np.repeat(c.read_nal, cnt), c.data_pos)
+
+
+@pytest.mark.parametrize('n,lmax,seed,squeeze,ccap,thr', [
+    (6_000, 16, 47, 100, 30, 3),
+    (4_000, 8, 53, 2000, 10, 1),
+    (4_000, 8, 59, 50, 200, 10),
+    (3_000, 64, 13, 300, 40, 10),
+])
+def test_lean_seen_set_equals_pair_set(n, lmax, seed, squeeze, ccap, thr):
+    """oracle_query_lean (the seen-set held as per-read reached lists, for the full config-5 pin) gives
+    the pair-set oracle's result exactly where the cap binds for many reads."""
+    oc = _dense_oracle_csr(n, lmax, seed, squeeze, ccap)
+    a = O.run_core(oc, edge_threshold=thr, use_cap=True)
+    b = O.run_core(oc, edge_threshold=thr, use_cap=True, lean=True)
+    assert a['stats']['max_fwd'] >= thr and a['stats'] == b['stats']
+    for k in ('edge_a', 'edge_b', 'edge_I', 'edge_U', 'fwd', 'comp'):
+        np.testing.assert_array_equal(a[k], b[k])
+
+
+@pytest.mark.parametrize('name', CLUSTER_FIXTURES)
+def test_lean_seen_set_on_reference_fixtures(name):
+    kw = fx.cli_options(name)
+    if fx.meta(name).get('exception'):
+        return
+    bed = fx.input_bed(name)
+    lens = bam_header.get_chromosome_lengths(fx.input_bam(name))
+    csr, _ = O.restate_prep(bed, lens, kw['cluster_mask'], kw['filter_false'])
+    cut = [float(x) for x in kw['jaccard_cutoffs'].split(',')]
+    args = (csr, kw['overlap'], cut, kw['qlen_diff'], kw['n_alignment_diff'], 10)
+    a, b = O.run_core(*args, use_cap=True), O.run_core(*args, use_cap=True, lean=True)
+    assert a['stats'] == b['stats']
+    for k in ('edge_a', 'edge_b', 'fwd', 'comp'):
+        np.testing.assert_array_equal(a[k], b[k])

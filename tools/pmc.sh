@@ -4,7 +4,7 @@
 set -e
 OUT=${OUT:-gpurun_out/pmc}
 ENGINE=${ENGINE:-sweep}
-if [ "$ENGINE" = walk ]; then KREGEX="query_kernel"; KNAME="query_kernel<0, false>"; else KREGEX="k_sweep<2>"; KNAME="k_sweep<2>"; fi
+if [ "$ENGINE" = walk ]; then KREGEX="query_kernel"; KNAMES="query_kernel<0, false>"; else KREGEX="k_sweep<2>|k_sweep_pairs"; KNAMES="k_sweep<2>;k_sweep_pairs"; fi
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $ROOT/$OUT
 cd /tmp && export TMPDIR=/tmp
@@ -18,5 +18,9 @@ for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_
 done
 cd $ROOT
 H=$(python3 -c "import bench; print(bench.kernel_source_hash('$ENGINE'))")
-python3 tools/pmc_traffic.py $ROOT/$OUT --kernel "$KNAME" --source-hash $H -o $ROOT/$OUT/traffic.json > /dev/null
-echo "traffic summary: $OUT/traffic.json (source $H)"
+rm -f $ROOT/$OUT/traffic.json
+IFS=';' read -ra KS <<< "$KNAMES"
+for K in "${KS[@]}"; do
+  python3 tools/pmc_traffic.py $ROOT/$OUT --kernel "$K" --source-hash $H --merge-into $ROOT/$OUT/traffic.json > /dev/null
+done
+echo "traffic summary: $OUT/traffic.json (source $H; kernels: $KNAMES)"

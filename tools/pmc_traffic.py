@@ -41,6 +41,8 @@ def main():
     ap.add_argument('--kernel', default='k_sweep<2>')
     ap.add_argument('-o', '--out', default=None)
     ap.add_argument('--source-hash', default=None, help='hash of the kernel sources the counters were taken on')
+    ap.add_argument('--merge-into', default=None,
+                    help='a JSON object keyed by kernel name (bench.py --traffic-json): set this kernel\'s entry')
     args = ap.parse_args()
     c, dur = collect(args.root, args.kernel)
     if 'FETCH_SIZE' not in c:
@@ -65,6 +67,16 @@ def main():
         out['wave_cycle_split'] = {k: c.get(k, 0.0) / wc for k in ('SQ_WAIT_ANY', 'SQ_WAIT_INST_ANY',
                                                                   'SQ_ACTIVE_INST_ANY')}
     text = json.dumps(out, indent=1)
+    if args.merge_into:
+        allk = {}
+        if os.path.exists(args.merge_into):
+            with open(args.merge_into) as fh:
+                allk = json.load(fh)
+            if 'kernel' in allk:                        # an older single-kernel summary
+                allk = {allk['kernel']: allk}
+        allk[args.kernel] = out
+        with open(args.merge_into, 'w') as fh:
+            fh.write(json.dumps(allk, indent=1) + '\n')
     if args.out:
         with open(args.out, 'w') as fh:
             fh.write(text + '\n')
