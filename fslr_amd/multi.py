@@ -170,8 +170,12 @@ def _raise_error(d, rank):
 
 def _child_loop(rank, world, port, first_device, force_gloo, timeout_s):
     """A pool rank: join the group once, then run each query named on stdin ('RUN dir'), answering
-    'DONE' on stdout once its results (or its error) are in the directory; 'EXIT' ends it."""
-    out = sys.stdout
+    'DONE' on stdout once its results (or its error) are in the directory; 'EXIT' ends it.  The
+    protocol keeps the process's original stdout to itself: fd 1 is pointed at stderr, so what the
+    libraries print (gloo's connection lines, warnings) cannot be read as an answer."""
+    out = os.fdopen(os.dup(1), 'w', buffering=1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
     r = None
     try:
         r = _Rank(rank, world, port, first_device, force_gloo, timeout_s)
