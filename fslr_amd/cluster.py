@@ -294,6 +294,22 @@ def query_interval_trees(interval_trees, data, overlap_cutoff, jaccard_threshold
     float) — sorted by (query1 rank, query2 rank); the reference's row order is
     set order (arbitrary).
     """
+    g = query_graph(interval_trees, data, overlap_cutoff, jaccard_threshold, edge_threshold, qlen_diff, diff)
+    return _graph_outputs(g.data.qnames[g.csr.read_qcode], g.labels, g.a, g.b, g.I, g.U, g.fwd, g.stats)
+
+
+class RawGraph:
+    """query_graph's result: the graph over read ranks without qname strings (the CLI's columnar
+    path maps ranks to qname codes itself).  Edges sorted by (a, b)."""
+
+    def __init__(self, data, csr, labels, a, b, I, U, fwd, st):
+        order = np.lexsort((b, a))
+        self.data, self.csr, self.labels, self.fwd, self.stats = data, csr, labels, fwd, st
+        self.a, self.b, self.I, self.U = a[order], b[order], I[order], U[order]
+
+
+def query_graph(interval_trees, data, overlap_cutoff, jaccard_threshold, edge_threshold, qlen_diff, diff):
+    """query_interval_trees without the match_df / qname outputs: a RawGraph."""
     min(jaccard_threshold)                              # cluster.py:188 raises on an empty list
     if isinstance(interval_trees, MultiGpuIndex) and (interval_trees.source is data or interval_trees.data is data):
         mg = interval_trees
@@ -309,12 +325,11 @@ def query_interval_trees(interval_trees, data, overlap_cutoff, jaccard_threshold
     data = idx.data
     csr = idx.csr
     ctx = idx.ctx
-    qnames_by_rank = data.qnames[csr.read_qcode]
     if csr.nal_varies:
         warnings.warn('n_alignments differs between rows of one read; the reference then uses the row its '
                       'search reaches first (order-dependent); the first row in data order is used', EdgeCapWarning)
     if idx.long is not None:
-        return _query_long(idx, qnames_by_rank, overlap_cutoff, jaccard_threshold, edge_threshold, qlen_diff, diff)
+        return _query_long(idx, overlap_cutoff, jaccard_threshold, edge_threshold, qlen_diff, diff)
     ctx.set_thresholds(fold_overlap_threshold(csr.iv_aln, overlap_cutoff))
     pt = pass_table(jaccard_threshold)
     qcut = 1 - qlen_diff
@@ -329,7 +344,7 @@ def query_interval_trees(interval_trees, data, overlap_cutoff, jaccard_threshold
     ne = st['n_edges']
     a, b, I, U = ctx.edges(ne)
     fwd = ctx.fwd_degree()
-    return _graph_outputs(qnames_by_rank, labels, a, b, I, U, fwd, st)
+    return RawGraph(data, csr, labels, a, b, I, U, fwd, st)
 
 
 def _graph_outputs(qnames_by_rank, labels, a, b, I, U, fwd, st):
@@ -342,7 +357,7 @@ def _graph_outputs(qnames_by_rank, labels, a, b, I, U, fwd, st):
     return match_df, ClusterGraph(qnames_by_rank, labels, (a, b), fwd, st)
 
 
-def _query_long(idx, qnames_by_rank, overlap_cutoff, jaccard_threshold, edge_threshold, qlen_diff, diff):
+def _query_long(idx, overlap_cutoff, jaccard_threshold, edge_threshold, qlen_diff, diff):
     """query_interval_trees with reads of more than FSLR_MAX_L intervals.
 
     E*: where the sweep's gates apply (overlap > 0, no aln_size == 0 interval, no long read with qlen2
@@ -404,14 +419,13 @@ def _query_long(idx, qnames_by_rank, overlap_cutoff, jaccard_threshold, edge_thr
         labels = ctx.labels()[:n]
     st = dict(st, engine=engine, n_edges=int(a.shape[0]), max_fwd=max_fwd, long_reads=int(lg.sum()),
               long_pair_edges=int(n_long), cap=cap)
-    return _graph_outputs(qnames_by_rank, labels, a, b, I, U, fwd, st)
+    return RawGraph(idx.data, csr, labels, a, b, I, U, fwd, st)
 
 
 def _query_multi_gpu(mg, thr, jaccard_threshold, edge_threshold, qlen_diff, diff):
     """query_interval_trees over ``mg.n_gpus`` ranks (fslr_amd.multi): same edges, forward degrees and
     labels as one GPU (union of per-chromosome matchings, label union; the cap replayed on rank 0)."""
     data, csr = mg.data, mg.csr
-    qnames_by_rank = data.qnames[csr.read_qcode]
     if csr.nal_varies:
         warnings.warn('n_alignments differs between rows of one read; the reference then uses the row its '
                       'search reaches first (order-dependent); the first row in data order is used', EdgeCapWarning)
@@ -420,7 +434,7 @@ def _query_multi_gpu(mg, thr, jaccard_threshold, edge_threshold, qlen_diff, diff
     a, b, I, U = r['edges']
     st = {'engine': 'sweep', 'n_gpus': mg.n_gpus, 'backend': r['backend'], 'evaluated_pairs': -1,
           'n_edges': int(a.shape[0]), 'max_fwd': r['max_fwd'], 'cap': r['cap'], 'capped': r['capped']}
-    return _graph_outputs(qnames_by_rank, np.asarray(r['labels']), a, b, I, U, r['fwd'], st)
+    return RawGraph(data, csr, np.asarray(r['labels']), a, b, I, U, r['fwd'], st)
 
 
 def get_subgraphs(G):

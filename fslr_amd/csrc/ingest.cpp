@@ -1,13 +1,15 @@
 // ingest.cpp — threaded reader for `{name}.mappings.bed` (include/fslr_ingest.h).
 // Host-only C++17; built with g++ into fslr_amd/libfslr_ingest.so.
 //
-// Layout: the file is read whole into one buffer; line starts are found by a
+// Layout: the file is mapped read-only (threads fault its pages in parallel); line starts are found by a
 // per-thread newline count + prefix sum; a column is produced by re-walking each
 // line to its k-th tab (the file stays hot in the CPU caches per chunk, and only
 // the requested columns are ever materialised).
 #include "fslr_ingest.h"
 
 #include <algorithm>
+#include <cctype>
+#include <emmintrin.h>
 #include <charconv>
 #include <cmath>
 #include <atomic>
@@ -20,9 +22,28 @@
 #include <unordered_map>
 #include <vector>
 
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+// A vector allocator that leaves new int64 elements uninitialised (the line index is filled by
+// threads; zero-filling 1+ GB first on one thread costs more than the scan).
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+    template <class U> struct rebind { using other = NoInitAlloc<U>; };
+    NoInitAlloc() = default;
+    template <class U> NoInitAlloc(const NoInitAlloc<U> &) {}
+    template <class U> void construct(U *p) noexcept { ::new (static_cast<void *>(p)) U; }
+    template <class U, class... A> void construct(U *p, A &&...a) { ::new (static_cast<void *>(p)) U(std::forward<A>(a)...); }
+};
+
 struct FslrTsv {
-    std::string buf;                      // file contents
-    std::vector<int64_t> line;            // [rows starts | file size | rows ends] (header excluded)
+    const char *data = nullptr;           // the mapped file (size bytes)
+    size_t size = 0;
+    void *map = nullptr;                  // mmap base (nullptr for an empty file)
+    ~FslrTsv() { if (map) munmap(map, size); }
+    std::vector<int64_t, NoInitAlloc<int64_t>> line;   // [rows starts | file size | rows ends] (header excluded)
     std::vector<std::string> names;       // header
     int n_threads = 1;
     // last factorize result per column
@@ -83,11 +104,15 @@ inline bool canon_int(std::string_view f, int64_t *v) {
 
 // pandas' default na_values (read_csv keep_default_na=True).
 bool is_na(std::string_view f) {
-    static const char *na[] = {"", "#N/A", "#N/A N/A", "#NA", "-1.#IND", "-1.#QNAN", "-NaN", "-nan",
-                               "1.#IND", "1.#QNAN", "<NA>", "N/A", "NA", "NULL", "NaN", "None",
-                               "n/a", "nan", "null"};
-    if (!f.data()) return true;
-    for (const char *s : na)
+    static const std::string_view na[] = {"", "#N/A", "#N/A N/A", "#NA", "-1.#IND", "-1.#QNAN", "-NaN", "-nan",
+                                          "1.#IND", "1.#QNAN", "<NA>", "N/A", "NA", "NULL", "NaN", "None",
+                                          "n/a", "nan", "null"};
+    if (!f.data() || f.empty()) return true;
+    // every NA spelling is at most 8 bytes and starts with one of these
+    if (f.size() > 8) return false;
+    const char c0 = f[0];
+    if (c0 != '#' && c0 != '-' && c0 != '1' && c0 != '<' && c0 != 'N' && c0 != 'n') return false;
+    for (const std::string_view &s : na)
         if (f == s) return true;
     return false;
 }
@@ -98,25 +123,47 @@ extern "C" {
 
 int fslr_tsv_open(const char *path, int n_threads, FslrTsv **out, char *err, size_t errlen) {
     *out = nullptr;
-    FILE *fp = std::fopen(path, "rb");
-    if (!fp) { set_err(err, errlen, std::string("cannot open ") + path); return FSLR_INGEST_ERROR; }
+    const int fd = ::open(path, O_RDONLY);
+    if (fd < 0) { set_err(err, errlen, std::string("cannot open ") + path); return FSLR_INGEST_ERROR; }
+    struct stat sb;
+    if (fstat(fd, &sb) != 0) { ::close(fd); set_err(err, errlen, std::string("cannot stat ") + path); return FSLR_INGEST_ERROR; }
     auto *t = new FslrTsv();
-    std::fseek(fp, 0, SEEK_END);
-    long sz = std::ftell(fp);
-    std::fseek(fp, 0, SEEK_SET);
-    t->buf.resize((size_t)std::max(0L, sz));
-    size_t got = sz > 0 ? std::fread(&t->buf[0], 1, (size_t)sz, fp) : 0;
-    std::fclose(fp);
-    if ((long)got != sz) { delete t; set_err(err, errlen, "short read"); return FSLR_INGEST_ERROR; }
+    t->size = (size_t)std::max<off_t>(0, sb.st_size);
+    if (t->size) {
+        t->map = mmap(nullptr, t->size, PROT_READ, MAP_PRIVATE, fd, 0);
+        if (t->map == MAP_FAILED) {
+            t->map = nullptr;
+            ::close(fd);
+            delete t;
+            set_err(err, errlen, "mmap failed");
+            return FSLR_INGEST_ERROR;
+        }
+        madvise(t->map, t->size, MADV_WILLNEED);
+        t->data = static_cast<const char *>(t->map);
+    } else {
+        t->data = "";
+    }
+    ::close(fd);
     if (n_threads <= 0) {   // the CPU share, not the whole machine: OMP_NUM_THREADS, else min(cores, 16)
         const char *env = std::getenv("OMP_NUM_THREADS");
         n_threads = env ? std::atoi(env) : 0;
         if (n_threads <= 0) n_threads = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
     }
     t->n_threads = std::min(n_threads, 256);
-    const char *b = t->buf.data();
-    const int64_t n = (int64_t)t->buf.size();
-    if (std::memchr(b, '"', (size_t)n)) { delete t; set_err(err, errlen, "quoted fields"); return FSLR_INGEST_DECLINE; }
+    const char *b = t->data;
+    const int64_t n = (int64_t)t->size;
+    {
+        std::atomic<bool> quoted{false};
+        const int Tq = (int)std::max<int64_t>(1, std::min<int64_t>(t->n_threads, n >> 20));
+        std::vector<std::thread> qp;
+        for (int i = 0; i < Tq; ++i)
+            qp.emplace_back([&, i] {
+                const int64_t a = n * i / Tq, e = n * (i + 1) / Tq;
+                if (a < e && std::memchr(b + a, '"', (size_t)(e - a))) quoted = true;
+            });
+        for (auto &th : qp) th.join();
+        if (quoted) { delete t; set_err(err, errlen, "quoted fields"); return FSLR_INGEST_DECLINE; }
+    }
     // header
     const char *nl = (const char *)std::memchr(b, '\n', (size_t)n);
     int64_t h_end = nl ? (int64_t)(nl - b) : n;
@@ -132,60 +179,62 @@ int fslr_tsv_open(const char *path, int n_threads, FslrTsv **out, char *err, siz
             p = q + 1;
         }
     }
-    // line starts: count per chunk, prefix, fill. Blank lines are skipped (skip_blank_lines=True).
+    // Lines: each chunk counts the non-blank line starts in it (newline scan), then fills its
+    // slice of the index with them and with the end (one past its first newline) of each such
+    // line; a chunk's last line may end in a later chunk and is completed by one memchr.  Blank
+    // lines are skipped (skip_blank_lines=True).  Layout: line[0..rows) starts, line[rows] = n,
+    // line[rows+1 ..] ends.
     const int T = t->n_threads;
     const int64_t len = n - body;
-    std::vector<int64_t> cnt(T + 1, 0);
     auto chunk = [&](int i) { return std::make_pair(body + len * i / T, body + len * (i + 1) / T); };
     auto nonblank = [&](int64_t p) {   // p (a line start) begins a non-blank line
         return p < n && !(b[p] == '\n' || (b[p] == '\r' && (p + 1 >= n || b[p + 1] == '\n')));
     };
-    // f(p) for every non-blank line start p in [a, e): body itself, and one past each '\n' (memchr scan).
-    auto for_starts = [&](int64_t a, int64_t e, auto &&f) {
+    // f(p) for every non-blank line start p in [a, e) and g(y) for every newline y in [a - 1, e - 1)
+    auto walk = [&](int64_t a, int64_t e, auto &&f, auto &&g) {
         if (a >= e) return;
         if (a == body && nonblank(a)) f(a);
         int64_t x = a == body ? a : a - 1;   // a newline at a-1 makes a a start
         while (x < e - 1) {
             const void *q = std::memchr(b + x, '\n', (size_t)(e - 1 - x));
             if (!q) break;
-            int64_t p = (int64_t)((const char *)q - b) + 1;
-            if (nonblank(p)) f(p);
-            x = p;
+            const int64_t y = (int64_t)((const char *)q - b);
+            g(y);
+            if (nonblank(y + 1)) f(y + 1);
+            x = y + 1;
         }
     };
+    std::vector<int64_t> base((size_t)T + 1, 0);
     std::vector<std::thread> pool;
     for (int i = 0; i < T; ++i)
         pool.emplace_back([&, i] {
             auto [a, e] = chunk(i);
             int64_t c = 0;
-            for_starts(a, e, [&](int64_t) { ++c; });
-            cnt[i + 1] = c;
+            walk(a, e, [&](int64_t) { ++c; }, [](int64_t) {});
+            base[(size_t)i + 1] = c;
         });
     for (auto &th : pool) th.join();
     pool.clear();
-    for (int i = 0; i < T; ++i) cnt[i + 1] += cnt[i];
-    t->line.resize((size_t)cnt[T] + 1);
+    for (int i = 0; i < T; ++i) base[(size_t)i + 1] += base[(size_t)i];
+    const int64_t rows = base[(size_t)T];
+    t->line.resize((size_t)rows * 2 + 1);
+    if (rows) madvise(t->line.data(), t->line.size() * sizeof(int64_t), MADV_HUGEPAGE);
+    t->line[(size_t)rows] = n;
+    int64_t *S = t->line.data(), *E = t->line.data() + rows + 1;
     for (int i = 0; i < T; ++i)
         pool.emplace_back([&, i] {
             auto [a, e] = chunk(i);
-            int64_t k = cnt[i];
-            for_starts(a, e, [&](int64_t p) { t->line[k++] = p; });
+            int64_t k = base[(size_t)i];
+            bool open = false;                       // S[k - 1] has no end yet
+            walk(a, e, [&](int64_t p) { S[k++] = p; open = true; },
+                 [&](int64_t y) { if (open) { E[k - 1] = y + 1; open = false; } });
+            if (open) {                              // ends in a later chunk (or at the end of the file)
+                const int64_t s0 = S[k - 1];
+                const void *q = std::memchr(b + s0, '\n', (size_t)(n - s0));
+                E[k - 1] = q ? (int64_t)((const char *)q - b) + 1 : n;
+            }
         });
     for (auto &th : pool) th.join();
-    // Each line ends at its own first newline (blank lines between data lines are skipped,
-    // so the next start is not the end). Layout: line[0..rows) starts, line[rows] = n,
-    // line[rows+1 .. 2*rows] ends.
-    const int64_t rows = cnt[T];
-    std::vector<int64_t> ends((size_t)rows);
-    parallel_for(rows, T, [&](int64_t a, int64_t e, int) {
-        for (int64_t i = a; i < e; ++i) {
-            const void *q = std::memchr(b + t->line[i], '\n', (size_t)(n - t->line[i]));
-            ends[i] = q ? (int64_t)((const char *)q - b) + 1 : n;
-        }
-    });
-    t->line.resize((size_t)rows * 2 + 1);
-    std::copy(ends.begin(), ends.end(), t->line.begin() + rows + 1);
-    t->line[rows] = n;
     t->uniq.assign(t->names.size(), {});
     *out = t;
     return FSLR_INGEST_OK;
@@ -210,9 +259,171 @@ int fslr_tsv_find(const FslrTsv *t, const char *name) {
 }  // extern "C"
 
 namespace {
+// 64-bit hash of a short string: 8-byte words folded with a multiply-xorshift mix.
+inline uint64_t str_hash(std::string_view f) {
+    const uint64_t k = 0x9E3779B97F4A7C15ull;
+    uint64_t h = (uint64_t)f.size() * k;
+    size_t i = 0;
+    for (; i + 8 <= f.size(); i += 8) {
+        uint64_t w;
+        std::memcpy(&w, f.data() + i, 8);
+        h = (h ^ w) * k;
+        h ^= h >> 29;
+    }
+    if (i < f.size()) {
+        uint64_t w = 0;
+        std::memcpy(&w, f.data() + i, f.size() - i);
+        h = (h ^ w) * k;
+        h ^= h >> 29;
+    }
+    h *= 0xBF58476D1CE4E5B9ull;
+    return h ^ (h >> 31);
+}
+
+// Open-addressing map string_view -> int32 id (linear probing, grown at half load).
+struct StrTable {
+    struct Slot { uint64_t h; const char *p; uint32_t n; int32_t id; };
+    std::vector<Slot> s;
+    size_t used = 0, mask = 0;
+    StrTable() { s.assign(1024, Slot{0, nullptr, 0, -1}); mask = 1023; }
+    void grow() {
+        std::vector<Slot> o;
+        o.swap(s);
+        s.assign(o.size() * 2, Slot{0, nullptr, 0, -1});
+        mask = s.size() - 1;
+        for (const Slot &x : o)
+            if (x.id >= 0) {
+                size_t j = (size_t)(x.h >> 7) & mask;        // the low bits choose the merge shard
+                while (s[j].id >= 0) j = (j + 1) & mask;
+                s[j] = x;
+            }
+    }
+    // the id of key f, inserting `fresh` when absent
+    int32_t *find_or_insert(std::string_view f, uint64_t h, int32_t fresh) {
+        if (2 * (used + 1) > s.size()) grow();
+        size_t j = (size_t)(h >> 7) & mask;
+        while (s[j].id >= 0) {
+            if (s[j].h == h && s[j].n == f.size() && std::memcmp(s[j].p, f.data(), f.size()) == 0) return &s[j].id;
+            j = (j + 1) & mask;
+        }
+        s[j] = Slot{h, f.data(), (uint32_t)f.size(), fresh};
+        ++used;
+        return &s[j].id;
+    }
+};
+
+// First-appearance dictionary of one column over one chunk of rows (local ids in local order).
+struct ChunkDict {
+    StrTable m;
+    std::vector<std::string_view> ord;
+    std::vector<uint64_t> oh;
+    std::string_view prev;
+    int32_t prev_id = -1;
+    bool have_prev = false, all_int = true, na = false;
+    int32_t add(std::string_view f) {
+        if (have_prev && f == prev) return prev_id;     // rows of one read are adjacent: no lookup
+        if (is_na(f)) { na = true; return 0; }
+        int64_t d;
+        if (all_int && !canon_int(f, &d)) all_int = false;
+        const uint64_t h = str_hash(f);
+        const int32_t id = *m.find_or_insert(f, h, (int32_t)ord.size());
+        if (id == (int32_t)ord.size()) { ord.push_back(f); oh.push_back(h); }
+        prev = f;
+        prev_id = id;
+        have_prev = true;
+        return id;
+    }
+};
+
+// The chunks' dictionaries (chunk c = rows [rows c / T, rows (c+1) / T), codes holding local ids)
+// merged into pd.factorize codes: sharded by hash, shard s walks the chunks in order, so the first
+// chunk holding a key is its global first appearance; global ids are dense in (chunk, local order)
+// of first appearances.  The uniques go to t->uniq[col].
+void merge_dicts(FslrTsv *t, int col, std::vector<ChunkDict> &D, int64_t rows, int32_t *codes, int64_t *n_uniq,
+                 int64_t *uniq_bytes) {
+    const int T = (int)D.size();
+    std::vector<std::thread> pool;
+    auto run = [&](auto &&f) {
+        for (int c = 0; c < T; ++c) pool.emplace_back([&, c] { f(c); });
+        for (auto &th : pool) th.join();
+        pool.clear();
+    };
+    std::vector<std::vector<int64_t>> first((size_t)T);   // -1: first appearance; else (chunk << 32 | k)
+    std::vector<std::vector<int32_t>> remap((size_t)T);
+    run([&](int c) {
+        D[(size_t)c].m = StrTable();                      // the local tables are done
+        first[(size_t)c].resize(D[(size_t)c].ord.size());
+        remap[(size_t)c].resize(D[(size_t)c].ord.size());
+    });
+    run([&](int sh) {
+        StrTable m;
+        std::vector<int64_t> where;
+        for (int c = 0; c < T; ++c) {
+            const auto &ord = D[(size_t)c].ord;
+            const auto &oh = D[(size_t)c].oh;
+            for (size_t k = 0; k < ord.size(); ++k) {
+                if ((int)(oh[k] % (uint64_t)T) != sh) continue;
+                const int32_t id = *m.find_or_insert(ord[k], oh[k], (int32_t)where.size());
+                if (id == (int32_t)where.size()) {
+                    where.push_back(((int64_t)c << 32) | (int64_t)k);
+                    first[(size_t)c][k] = -1;
+                } else {
+                    first[(size_t)c][k] = where[(size_t)id];
+                }
+            }
+        }
+    });
+    std::vector<int64_t> base((size_t)T + 1, 0);
+    for (int c = 0; c < T; ++c)
+        base[(size_t)c + 1] = base[(size_t)c] + std::count(first[(size_t)c].begin(), first[(size_t)c].end(), (int64_t)-1);
+    std::vector<std::string_view> &order = t->uniq[(size_t)col];
+    order.assign((size_t)base[(size_t)T], std::string_view());
+    run([&](int c) {
+        int64_t id = base[(size_t)c];
+        for (size_t k = 0; k < first[(size_t)c].size(); ++k)
+            if (first[(size_t)c][k] < 0) { remap[(size_t)c][k] = (int32_t)id; order[(size_t)id++] = D[(size_t)c].ord[k]; }
+    });
+    run([&](int c) {
+        for (size_t k = 0; k < first[(size_t)c].size(); ++k)
+            if (first[(size_t)c][k] >= 0) remap[(size_t)c][k] = remap[first[(size_t)c][k] >> 32][first[(size_t)c][k] & 0xffffffff];
+        const int64_t a = rows * c / T, e = rows * (c + 1) / T;
+        const int32_t *r = remap[(size_t)c].data();
+        for (int64_t i = a; i < e; ++i) codes[i] = r[codes[i]];
+    });
+    int64_t bytes = 0;
+    for (auto &sv : order) bytes += (int64_t)sv.size();
+    *n_uniq = (int64_t)order.size();
+    *uniq_bytes = bytes;
+}
+
+// Field starts of the line [s, le): fs[k] = start of field k, fs[count] = le + 1 (so field k is
+// [fs[k], fs[k+1] - 1)).  Tabs are found 16 bytes at a time (loads stay inside the line).  Returns
+// the field count, or -1 past maxf fields.
+inline int split_fields(const char *s, const char *le, const char **fs, int maxf) {
+    int k = 0;
+    fs[k++] = s;
+    const char *p = s;
+    const __m128i tab = _mm_set1_epi8('\t');
+    for (; p + 16 <= le; p += 16) {
+        unsigned m = (unsigned)_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_loadu_si128((const __m128i *)p), tab));
+        while (m) {
+            if (k > maxf) return -1;
+            fs[k++] = p + __builtin_ctz(m) + 1;
+            m &= m - 1;
+        }
+    }
+    for (; p < le; ++p)
+        if (*p == '\t') {
+            if (k > maxf) return -1;
+            fs[k++] = p + 1;
+        }
+    fs[k] = le + 1;
+    return k;
+}
+
 inline std::string_view row_field(const FslrTsv *t, int64_t i, int col) {
     const int64_t rows = fslr_tsv_rows(t);
-    const char *b = t->buf.data();
+    const char *b = t->data;
     const char *s = b + t->line[i];
     const char *e = b + t->line[rows + 1 + i];
     if (e > s && e[-1] == '\n') --e;
@@ -233,95 +444,57 @@ int fslr_tsv_int_column(const FslrTsv *t, int col, int64_t *out) {
     return ok ? FSLR_INGEST_OK : FSLR_INGEST_DECLINE;
 }
 
+int fslr_tsv_int_columns(const FslrTsv *t, int n, const int32_t *cols, int64_t *const *outs) {
+    const int ncol = (int)t->names.size();
+    int maxc = -1;
+    for (int k = 0; k < n; ++k) {
+        if (cols[k] < 0 || cols[k] >= ncol) return FSLR_INGEST_ERROR;
+        maxc = std::max(maxc, (int)cols[k]);
+    }
+    if (n == 0) return FSLR_INGEST_OK;
+    std::vector<int> slot((size_t)maxc + 1, -1);          // column -> output (one output per column)
+    for (int k = 0; k < n; ++k) slot[(size_t)cols[k]] = k;
+    const int64_t rows = fslr_tsv_rows(t);
+    std::atomic<bool> ok{true};
+    const char *b = t->data;
+    parallel_for(rows, t->n_threads, [&](int64_t a, int64_t e, int) {
+        for (int64_t i = a; i < e && ok.load(std::memory_order_relaxed); ++i) {
+            const char *s = b + t->line[i];
+            const char *le = b + t->line[rows + 1 + i];
+            if (le > s && le[-1] == '\n') --le;
+            if (le > s && le[-1] == '\r') --le;
+            const char *p = s;
+            for (int c = 0; c <= maxc; ++c) {
+                const char *q = p ? static_cast<const char *>(std::memchr(p, '\t', (size_t)(le - p))) : nullptr;
+                const char *fe = q ? q : le;
+                if (slot[(size_t)c] >= 0) {
+                    int64_t v;
+                    if (!p || !canon_int(std::string_view(p, (size_t)(fe - p)), &v)) { ok = false; break; }
+                    outs[slot[(size_t)c]][i] = v;
+                }
+                p = q ? q + 1 : nullptr;                    // a missing field: NaN in pandas
+            }
+        }
+    });
+    return ok ? FSLR_INGEST_OK : FSLR_INGEST_DECLINE;
+}
+
 int fslr_tsv_factorize(FslrTsv *t, int col, int32_t *codes, int64_t *n_uniq, int64_t *uniq_bytes) {
     if (col < 0 || col >= (int)t->names.size()) return FSLR_INGEST_ERROR;
     const int64_t rows = fslr_tsv_rows(t);
     const int T = (int)std::min<int64_t>(t->n_threads, std::max<int64_t>(1, rows / 4096));
-    // pass 1: per-chunk first-appearance dictionaries (local ids in local order)
-    std::vector<std::unordered_map<std::string_view, int32_t>> loc((size_t)T);
-    std::vector<std::vector<std::string_view>> loc_order((size_t)T);
-    std::atomic<bool> ok{true}, all_int{true};
-    std::vector<std::thread> pool;
-    for (int c = 0; c < T; ++c)
-        pool.emplace_back([&, c] {
-            const int64_t a = rows * c / T, e = rows * (c + 1) / T;
-            auto &m = loc[c];
-            auto &ord = loc_order[c];
-            bool local_int = true;
-            std::string_view prev;
-            int32_t prev_id = -1;
-            for (int64_t i = a; i < e; ++i) {
-                std::string_view f = row_field(t, i, col);
-                if (is_na(f)) { ok = false; return; }
-                int64_t dummy;
-                if (local_int && !canon_int(f, &dummy)) local_int = false;
-                int32_t id;
-                if (i > a && f == prev) {
-                    id = prev_id;   // rows of one read are adjacent: skip the hash lookup
-                } else {
-                    auto it = m.find(f);
-                    if (it == m.end()) { id = (int32_t)ord.size(); m.emplace(f, id); ord.push_back(f); }
-                    else id = it->second;
-                }
-                prev = f;
-                prev_id = id;
-                codes[i] = id;   // local id for now
-            }
-            if (!local_int) all_int = false;
-        });
-    for (auto &th : pool) th.join();
-    pool.clear();
-    if (!ok) return FSLR_INGEST_DECLINE;
-    if (all_int && rows > 0) return FSLR_INGEST_DECLINE;   // pandas would type the column as int64
-    // Merge, sharded by hash: shard s owns the keys with hash % T == s and walks the chunks
-    // in order, so the first chunk holding a key is its global first appearance. Global ids
-    // are then dense in (chunk, local order) of first appearances = pd.factorize order.
-    auto run = [&](auto &&f) {
-        for (int c = 0; c < T; ++c) pool.emplace_back([&, c] { f(c); });
-        for (auto &th : pool) th.join();
-        pool.clear();
-    };
-    std::vector<std::vector<uint32_t>> hs((size_t)T);
-    std::vector<std::vector<int64_t>> first((size_t)T);   // -1: first appearance; else (chunk << 32 | k)
-    std::vector<std::vector<int32_t>> remap((size_t)T);
-    run([&](int c) {
-        const auto &ord = loc_order[c];
-        hs[c].resize(ord.size());
-        first[c].resize(ord.size());
-        remap[c].resize(ord.size());
-        for (size_t k = 0; k < ord.size(); ++k) hs[c][k] = (uint32_t)(std::hash<std::string_view>{}(ord[k]) % T);
-        loc[c] = {};   // local maps are no longer needed
+    std::vector<ChunkDict> D((size_t)T);
+    parallel_for(rows, T, [&](int64_t a, int64_t e, int c) {
+        ChunkDict &d = D[(size_t)c];
+        for (int64_t i = a; i < e && !d.na; ++i) codes[i] = d.add(row_field(t, i, col));
     });
-    run([&](int s) {
-        std::unordered_map<std::string_view, int64_t> m;
-        for (int c = 0; c < T; ++c)
-            for (size_t k = 0; k < loc_order[c].size(); ++k) {
-                if ((int)hs[c][k] != s) continue;
-                auto r = m.try_emplace(loc_order[c][k], ((int64_t)c << 32) | (int64_t)k);
-                first[c][k] = r.second ? -1 : r.first->second;
-            }
-    });
-    std::vector<int64_t> base((size_t)T + 1, 0);
-    for (int c = 0; c < T; ++c)
-        base[c + 1] = base[c] + std::count(first[c].begin(), first[c].end(), (int64_t)-1);
-    std::vector<std::string_view> &order = t->uniq[col];
-    order.assign((size_t)base[T], std::string_view());
-    run([&](int c) {
-        int64_t id = base[c];
-        for (size_t k = 0; k < first[c].size(); ++k)
-            if (first[c][k] < 0) { remap[c][k] = (int32_t)id; order[(size_t)id++] = loc_order[c][k]; }
-    });
-    run([&](int c) {
-        for (size_t k = 0; k < first[c].size(); ++k)
-            if (first[c][k] >= 0) remap[c][k] = remap[first[c][k] >> 32][first[c][k] & 0xffffffff];
-        const int64_t a = rows * c / T, e = rows * (c + 1) / T;
-        const int32_t *r = remap[c].data();
-        for (int64_t i = a; i < e; ++i) codes[i] = r[codes[i]];
-    });
-    int64_t bytes = 0;
-    for (auto &s : order) bytes += (int64_t)s.size();
-    *n_uniq = (int64_t)order.size();
-    *uniq_bytes = bytes;
+    bool all_int = rows > 0;
+    for (auto &d : D) {
+        if (d.na) return FSLR_INGEST_DECLINE;
+        all_int = all_int && d.all_int;
+    }
+    if (all_int) return FSLR_INGEST_DECLINE;   // pandas would type the column as int64
+    merge_dicts(t, col, D, rows, codes, n_uniq, uniq_bytes);
     return FSLR_INGEST_OK;
 }
 
@@ -351,22 +524,54 @@ bool boolish(std::string_view f) {
     };
     return eq("true") || eq("false");
 }
-// Any field pandas' C parser could turn into a number.
+// Any field pandas' C parser could turn into a number (strtod consumes all of it).  strtod reads
+// nothing from a field that starts with a letter other than i / n (inf, infinity, nan) or with
+// another character that cannot begin a number, so those fields skip the call.
 bool numeric(std::string_view f) {
     if (f.empty()) return false;
-    std::string s(f);
+    const unsigned char c0 = (unsigned char)f[0];
+    const bool may = (c0 >= '0' && c0 <= '9') || c0 == '+' || c0 == '-' || c0 == '.' || c0 == 'i' || c0 == 'I' ||
+                     c0 == 'n' || c0 == 'N' || std::isspace(c0);
+    if (!may) return false;
+    char small[96];
+    std::string big;
+    const char *z;
+    if (f.size() < sizeof(small)) {
+        std::memcpy(small, f.data(), f.size());
+        small[f.size()] = '\0';
+        z = small;
+    } else {
+        big.assign(f);
+        z = big.c_str();
+    }
     char *end = nullptr;
-    std::strtod(s.c_str(), &end);
-    return end == s.c_str() + s.size();
+    std::strtod(z, &end);
+    return end == z + f.size();
 }
 }  // namespace
 
 extern "C" {
 
-int fslr_tsv_verbatim(const FslrTsv *t) {
+int fslr_tsv_verbatim(const FslrTsv *t) { return fslr_tsv_scan(t, 0, nullptr, nullptr); }
+
+int fslr_tsv_scan(const FslrTsv *t, int n_int, const int32_t *int_cols, int64_t *const *outs) {
+    return fslr_tsv_scan_all(const_cast<FslrTsv *>(t), n_int, int_cols, outs, 0, nullptr, nullptr, nullptr);
+}
+
+int fslr_tsv_scan_all(FslrTsv *t, int n_int, const int32_t *int_cols, int64_t *const *outs, int n_str,
+                      const int32_t *str_cols, int32_t *const *str_codes, int64_t *str_counts) {
     const int ncol = (int)t->names.size();
     const int64_t rows = fslr_tsv_rows(t);
     if (rows == 0) return FSLR_INGEST_DECLINE;
+    std::vector<int> slot((size_t)ncol, -1), sslot((size_t)ncol, -1);   // column -> int / string output
+    for (int k = 0; k < n_int; ++k) {
+        if (int_cols[k] < 0 || int_cols[k] >= ncol) return FSLR_INGEST_ERROR;
+        slot[(size_t)int_cols[k]] = k;
+    }
+    for (int k = 0; k < n_str; ++k) {
+        if (str_cols[k] < 0 || str_cols[k] >= ncol || slot[(size_t)str_cols[k]] >= 0) return FSLR_INGEST_ERROR;
+        sslot[(size_t)str_cols[k]] = k;
+    }
     // pandas renames empty header names ('Unnamed: N') and repeated ones ('x.1'): the input's own
     // header line would then not be what to_csv writes
     {
@@ -376,92 +581,173 @@ int fslr_tsv_verbatim(const FslrTsv *t) {
         std::sort(nm.begin(), nm.end());
         if (std::adjacent_find(nm.begin(), nm.end()) != nm.end()) return FSLR_INGEST_DECLINE;
     }
-    // every row exactly ncol fields: a longer row makes pandas raise (or index by the first
-    // column), a shorter one NaN-fills — either way the row bytes are not what to_csv writes
-    {
-        std::atomic<int> ragged{0};
-        const char *b = t->buf.data();
-        parallel_for(rows, t->n_threads, [&](int64_t a, int64_t e, int) {
-            for (int64_t i = a; i < e && !ragged.load(std::memory_order_relaxed); ++i) {
-                const char *s = b + t->line[i];
-                const char *le = b + t->line[rows + 1 + i];
-                if (le > s && le[-1] == '\n') --le;
-                if (le > s && le[-1] == '\r') --le;
-                int tabs = 0;
-                for (const char *q = s; (q = static_cast<const char *>(std::memchr(q, '\t', (size_t)(le - q)))) != nullptr; ++q)
-                    ++tabs;
-                if (tabs != ncol - 1) ragged = 1;
+    // One row-major pass, each line split once.  Every row must hold exactly ncol fields: a longer
+    // row makes pandas raise (or index by the first column), a shorter one NaN-fills — either way
+    // the row bytes are not what to_csv writes.  Per column: all fields canonical ints (pandas
+    // types it int64, the text round-trips), or text with no numeric-looking, bool-looking or
+    // non-empty NA field and at least one text field (empty fields come back as '' either way).
+    // Requested int columns are parsed, requested string columns factorized, in the same pass.
+    std::atomic<int> bad{0};
+    const int T = (int)std::min<int64_t>(t->n_threads, std::max<int64_t>(1, rows / 4096));
+    std::vector<std::vector<unsigned char>> st((size_t)T, std::vector<unsigned char>((size_t)ncol * 3, 0));
+    std::vector<std::vector<ChunkDict>> D((size_t)n_str, std::vector<ChunkDict>((size_t)T));
+    const char *b = t->data;
+    parallel_for(rows, T, [&](int64_t a, int64_t e, int w) {
+        // per column: ai = every field so far a canonical int, tk = no field rules text out, at = a text field
+        std::vector<unsigned char> ai((size_t)ncol, 1), tk((size_t)ncol, 1), at((size_t)ncol, 0);
+        // the previous row's field per column and its class (bit 0: canonical int, bit 1: rules text
+        // out): columns such as strand or version repeat one value, which is classified once
+        std::vector<std::string_view> prev((size_t)ncol);
+        std::vector<unsigned char> pcls((size_t)ncol, 0);
+        std::vector<int64_t> pval((size_t)ncol, 0);
+        std::vector<const char *> fs((size_t)ncol + 2);
+        for (int64_t i = a; i < e && !bad.load(std::memory_order_relaxed); ++i) {
+            const char *s = b + t->line[i];
+            const char *le = b + t->line[rows + 1 + i];
+            if (le > s && le[-1] == '\n') --le;
+            if (le > s && le[-1] == '\r') --le;
+            if (split_fields(s, le, fs.data(), ncol) != ncol) { bad = 1; break; }   // ragged row
+            for (int c = 0; c < ncol; ++c) {
+                const std::string_view f(fs[(size_t)c], (size_t)(fs[(size_t)c + 1] - 1 - fs[(size_t)c]));
+                unsigned char cls;
+                // (int fields are parsed afresh: canon_int costs about what the compare does)
+                if (i > a && !(pcls[(size_t)c] & 1) && f == prev[(size_t)c]) {
+                    cls = pcls[(size_t)c];
+                } else {
+                    int64_t v = 0;
+                    cls = canon_int(f, &v) ? 1 : 0;
+                    if (!cls && !f.empty() && (is_na(f) || boolish(f) || numeric(f))) cls |= 2;
+                    prev[(size_t)c] = f;
+                    pcls[(size_t)c] = cls;
+                    pval[(size_t)c] = v;
+                }
+                if (slot[(size_t)c] >= 0) {
+                    if (!(cls & 1)) { bad = 1; break; }                  // a requested int column is not one
+                    outs[slot[(size_t)c]][i] = pval[(size_t)c];
+                } else if (sslot[(size_t)c] >= 0) {
+                    ChunkDict &d = D[(size_t)sslot[(size_t)c]][(size_t)w];
+                    str_codes[sslot[(size_t)c]][i] = d.add(f);
+                    if (d.na) { bad = 1; break; }
+                }
+                if (ai[(size_t)c] && !(cls & 1)) {
+                    ai[(size_t)c] = 0;
+                    if (i > a) tk[(size_t)c] = 0;          // the earlier fields were canonical ints: numeric text
+                }
+                if (!ai[(size_t)c] && !f.empty() && tk[(size_t)c]) {
+                    if (cls & 2) tk[(size_t)c] = 0;
+                    else at[(size_t)c] = 1;
+                }
+                if (!ai[(size_t)c] && !tk[(size_t)c]) { bad = 1; break; }    // neither int nor text: decline
             }
-        });
-        if (ragged) return FSLR_INGEST_DECLINE;
-    }
+        }
+        auto &o = st[(size_t)w];
+        for (int c = 0; c < ncol; ++c) { o[(size_t)c] = ai[(size_t)c]; o[(size_t)(ncol + c)] = tk[(size_t)c]; o[(size_t)(2 * ncol + c)] = at[(size_t)c]; }
+    });
+    if (bad) return FSLR_INGEST_DECLINE;
     for (int c = 0; c < ncol; ++c) {
-        // 0: every field a canonical int; else the column must be text with no numeric-looking,
-        // bool-looking or non-empty NA field (empty fields come back as '' either way).
-        std::atomic<int> all_int{1}, text_ok{1}, any_text{0};
-        parallel_for(rows, t->n_threads, [&](int64_t a, int64_t e, int) {
-            bool ai = true, tk = true, at = false;
-            for (int64_t i = a; i < e; ++i) {
-                std::string_view f = row_field(t, i, c);
-                int64_t v;
-                if (ai && !canon_int(f, &v)) ai = false;
-                if (!f.data()) { tk = false; continue; }   // missing field
-                if (f.empty()) continue;
-                if (is_na(f) || boolish(f) || numeric(f)) tk = false;
-                else at = true;
-            }
-            if (!ai) all_int = 0;
-            if (!tk) text_ok = 0;
-            if (at) any_text = 1;
-        });
-        if (all_int) continue;
+        bool all_int = true, text_ok = true, any_text = false;
+        for (int w = 0; w < T; ++w) {
+            all_int = all_int && st[(size_t)w][(size_t)c];
+            text_ok = text_ok && !st[(size_t)w][(size_t)c] && st[(size_t)w][(size_t)(ncol + c)];   // an all-int chunk is numeric
+            any_text = any_text || st[(size_t)w][(size_t)(2 * ncol + c)];
+        }
+        if (all_int) {
+            if (sslot[(size_t)c] >= 0) return FSLR_INGEST_DECLINE;      // pandas types it int64, not text
+            continue;
+        }
         if (!(text_ok && any_text)) return FSLR_INGEST_DECLINE;
     }
+    for (int k = 0; k < n_str; ++k)
+        merge_dicts(t, str_cols[k], D[(size_t)k], rows, str_codes[k], &str_counts[2 * k], &str_counts[2 * k + 1]);
     return FSLR_INGEST_OK;
 }
 
 int fslr_tsv_write(const FslrTsv *t, const char *path, const char *header_suffix, const int64_t *rows_out,
                    int64_t n_out, const int32_t *suffix_id, const char *suffix_buf, const int64_t *suffix_ends,
                    char *err, size_t errlen) {
-    FILE *fp = std::fopen(path, "wb");
-    if (!fp) { set_err(err, errlen, std::string("cannot write ") + path); return FSLR_INGEST_ERROR; }
+    // Each thread owns a contiguous range of output rows: their byte lengths are summed first, so
+    // every range knows its file offset and is formatted and written (pwrite) independently.
+    const int fd = ::open(path, O_WRONLY | O_CREAT | O_TRUNC, 0666);
+    if (fd < 0) { set_err(err, errlen, std::string("cannot write ") + path); return FSLR_INGEST_ERROR; }
     std::string head;
     for (size_t c = 0; c < t->names.size(); ++c) { if (c) head += '\t'; head += t->names[c]; }
     head += header_suffix;
     head += '\n';
-    std::fwrite(head.data(), 1, head.size(), fp);
     const int64_t rows = fslr_tsv_rows(t);
-    const char *b = t->buf.data();
-    const int T = std::max(1, t->n_threads);
-    const int64_t block = 1 << 18;   // rows per formatting round (bounded memory)
-    std::vector<std::string> part((size_t)T);
-    bool bad = false;
-    for (int64_t r0 = 0; r0 < n_out && !bad; r0 += block) {
-        const int64_t r1 = std::min(n_out, r0 + block);
-        std::atomic<bool> oob{false};
-        parallel_for(r1 - r0, T, [&](int64_t a, int64_t e, int w) {
-            std::string &o = part[(size_t)w];
-            o.clear();
-            for (int64_t k = r0 + a; k < r0 + e; ++k) {
-                const int64_t i = rows_out[k];
-                if (i < 0 || i >= rows) { oob = true; return; }
-                const char *s = b + t->line[i];
-                const char *le = b + t->line[rows + 1 + i];
-                if (le > s && le[-1] == '\n') --le;
-                if (le > s && le[-1] == '\r') --le;
-                o.append(s, (size_t)(le - s));
-                const int32_t u = suffix_id[k];
-                const int64_t ss = u ? suffix_ends[u - 1] : 0;
-                o.append(suffix_buf + ss, (size_t)(suffix_ends[u] - ss));
-                o += '\n';
-            }
-        });
-        if (oob) { bad = true; break; }
-        const int used = (int)std::min<int64_t>(T, std::max<int64_t>(1, (r1 - r0) / 4096));
-        for (int w = 0; w < used; ++w) std::fwrite(part[(size_t)w].data(), 1, part[(size_t)w].size(), fp);
+    const char *b = t->data;
+    auto span = [&](int64_t i, const char **s) {
+        *s = b + t->line[i];
+        const char *le = b + t->line[rows + 1 + i];
+        if (le > *s && le[-1] == '\n') --le;
+        if (le > *s && le[-1] == '\r') --le;
+        return (int64_t)(le - *s);
+    };
+    auto sfx = [&](int64_t k, int64_t *ss) {
+        const int32_t u = suffix_id[k];
+        *ss = u ? suffix_ends[u - 1] : 0;
+        return suffix_ends[u] - *ss;
+    };
+    const int T = (int)std::min<int64_t>(std::max(1, t->n_threads), std::max<int64_t>(1, n_out / 4096));
+    std::vector<int64_t> bytes((size_t)T + 1, 0);
+    std::atomic<bool> oob{false}, werr{false};
+    auto range = [&](int w) { return std::make_pair(n_out * w / T, n_out * (w + 1) / T); };
+    {
+        std::vector<std::thread> pool;
+        for (int w = 0; w < T; ++w)
+            pool.emplace_back([&, w] {
+                auto [a, e] = range(w);
+                int64_t tot = 0;
+                for (int64_t k = a; k < e; ++k) {
+                    const int64_t i = rows_out[k];
+                    if (i < 0 || i >= rows) { oob = true; return; }
+                    const char *s;
+                    int64_t ss;
+                    tot += span(i, &s) + sfx(k, &ss) + 1;
+                }
+                bytes[(size_t)w + 1] = tot;
+            });
+        for (auto &th : pool) th.join();
     }
-    if (std::fclose(fp) != 0 || bad) {
-        set_err(err, errlen, bad ? "row index out of range" : "write failed");
+    if (oob) { ::close(fd); set_err(err, errlen, "row index out of range"); return FSLR_INGEST_ERROR; }
+    bytes[0] = (int64_t)head.size();
+    for (int w = 0; w < T; ++w) bytes[(size_t)w + 1] += bytes[(size_t)w];
+    auto put = [&](const char *p, size_t len, int64_t off) {
+        while (len) {
+            const ssize_t r = ::pwrite(fd, p, len, off);
+            if (r <= 0) { werr = true; return; }
+            p += r;
+            len -= (size_t)r;
+            off += r;
+        }
+    };
+    put(head.data(), head.size(), 0);
+    {
+        std::vector<std::thread> pool;
+        for (int w = 0; w < T; ++w)
+            pool.emplace_back([&, w] {
+                auto [a, e] = range(w);
+                int64_t off = bytes[(size_t)w];
+                std::string o;
+                o.reserve(8 << 20);
+                for (int64_t k = a; k < e && !werr; ++k) {
+                    const char *s;
+                    int64_t ss;
+                    const int64_t ln = span(rows_out[k], &s);
+                    o.append(s, (size_t)ln);
+                    const int64_t sl = sfx(k, &ss);
+                    o.append(suffix_buf + ss, (size_t)sl);
+                    o += '\n';
+                    if (o.size() >= (8u << 20) || k + 1 == e) {
+                        put(o.data(), o.size(), off);
+                        off += (int64_t)o.size();
+                        o.clear();
+                    }
+                }
+            });
+        for (auto &th : pool) th.join();
+    }
+    if (::close(fd) != 0 || werr) {
+        set_err(err, errlen, "write failed");
         return FSLR_INGEST_ERROR;
     }
     return FSLR_INGEST_OK;
@@ -534,26 +820,42 @@ int fslr_format_suffix(int n_cols, const int32_t *kinds, const void *const *cols
   if (n_cols < 0 || n_keys < 0 || (!out && cap) || (n_keys && !ends)) return FSLR_INGEST_ERROR;
   for (int c = 0; c < n_cols; ++c)
     if (kinds[c] != 0 && kinds[c] != 1) return FSLR_INGEST_ERROR;
-  int64_t pos = 0;
-  char tmp[64];
-  for (int64_t k = 0; k < n_keys; ++k) {
-    for (int c = 0; c < n_cols; ++c) {
-      int len;
-      if (kinds[c] == 0) {
-        len = std::sprintf(tmp, "%lld", static_cast<long long>(static_cast<const int64_t *>(cols[c])[k]));
-      } else {
-        const double v = static_cast<const double *>(cols[c])[k];
-        if (!std::isfinite(v)) return FSLR_INGEST_DECLINE;                // NaN / inf: pandas' own text
-        len = repr_double(v, tmp);
-        if (len < 0) return FSLR_INGEST_ERROR;
+  // key ranges formatted by threads into their own buffers, then placed by a prefix sum
+  const char *env = std::getenv("OMP_NUM_THREADS");
+  int T = env ? std::atoi(env) : 0;
+  if (T <= 0) T = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+  T = (int)std::min<int64_t>(T, std::max<int64_t>(1, n_keys / 8192));
+  std::vector<std::string> part((size_t)T);
+  std::atomic<int> rc{FSLR_INGEST_OK};
+  parallel_for(n_keys, T, [&](int64_t a, int64_t e, int w) {
+    std::string &o = part[(size_t)w];
+    o.reserve((size_t)(e - a) * (size_t)n_cols * 12);
+    char tmp[64];
+    for (int64_t k = a; k < e; ++k) {
+      for (int c = 0; c < n_cols; ++c) {
+        int len;
+        if (kinds[c] == 0) {
+          len = std::sprintf(tmp, "%lld", static_cast<long long>(static_cast<const int64_t *>(cols[c])[k]));
+        } else {
+          const double v = static_cast<const double *>(cols[c])[k];
+          if (!std::isfinite(v)) { rc = FSLR_INGEST_DECLINE; return; }     // NaN / inf: pandas' own text
+          len = repr_double(v, tmp);
+          if (len < 0) { rc = FSLR_INGEST_ERROR; return; }
+        }
+        o += '\t';
+        o.append(tmp, (size_t)len);
       }
-      if (pos + len + 1 > cap) return FSLR_INGEST_ERROR;
-      out[pos++] = '\t';
-      std::memcpy(out + pos, tmp, static_cast<size_t>(len));
-      pos += len;
+      ends[k] = (int64_t)o.size();                 // local for now
     }
-    ends[k] = pos;
-  }
+  });
+  if (rc != FSLR_INGEST_OK) return rc;
+  std::vector<int64_t> base((size_t)T + 1, 0);
+  for (int w = 0; w < T; ++w) base[(size_t)w + 1] = base[(size_t)w] + (int64_t)part[(size_t)w].size();
+  if (base[(size_t)T] > cap) return FSLR_INGEST_ERROR;
+  parallel_for(n_keys, T, [&](int64_t a, int64_t e, int w) {
+    std::memcpy(out + base[(size_t)w], part[(size_t)w].data(), part[(size_t)w].size());
+    for (int64_t k = a; k < e; ++k) ends[k] += base[(size_t)w];
+  });
   return FSLR_INGEST_OK;
 }
 

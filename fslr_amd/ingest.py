@@ -42,9 +42,12 @@ def load(path: str = LIB_PATH):
         'fslr_tsv_colname': (cp, [vp, i32]),
         'fslr_tsv_find': (i32, [vp, cp]),
         'fslr_tsv_int_column': (i32, [vp, i32, vp]),
+        'fslr_tsv_int_columns': (i32, [vp, i32, vp, vp]),
         'fslr_tsv_factorize': (i32, [vp, i32, vp, ctypes.POINTER(i64), ctypes.POINTER(i64)]),
         'fslr_tsv_uniques': (i32, [vp, i32, vp, vp]),
         'fslr_tsv_verbatim': (i32, [vp]),
+        'fslr_tsv_scan': (i32, [vp, i32, vp, vp]),
+        'fslr_tsv_scan_all': (i32, [vp, i32, vp, vp, i32, vp, vp, vp]),
         'fslr_tsv_write': (i32, [vp, cp, cp, vp, i64, vp, vp, vp, cp, ctypes.c_size_t]),
         'fslr_format_suffix': (i32, [i32, vp, vp, i64, vp, i64, vp]),
         'fslr_group_by_first_appearance': (i32, [vp, i64, i64, vp, vp, vp, vp]),
@@ -101,22 +104,77 @@ class TsvFile:
         rc = self._L.fslr_tsv_int_column(self._h, self._col(name), out.ctypes.data)
         return out if rc == OK else None
 
-    def factorize(self, name: str):
-        """(codes int32[rows], uniques object[k]) as ``pd.factorize(col, sort=False)``, or None."""
+    def int_columns(self, names):
+        """{name: int64[rows]} for several columns in one pass over the rows, or None."""
+        names = list(dict.fromkeys(names))
+        cols = np.asarray([self._col(n) for n in names], dtype=np.int32)
+        outs = [np.empty(self.rows, dtype=np.int64) for _ in names]
+        ptrs = (ctypes.c_void_p * len(outs))(*[o.ctypes.data for o in outs])
+        rc = self._L.fslr_tsv_int_columns(self._h, len(names), cols.ctypes.data, ctypes.cast(ptrs, ctypes.c_void_p))
+        return dict(zip(names, outs)) if rc == OK else None
+
+    def factorize_codes(self, name: str):
+        """(codes int32[rows], number of uniques) of ``pd.factorize(col, sort=False)``, or None; the
+        uniques stay in the library until :meth:`uniques`."""
         c = self._col(name)
         codes = np.empty(self.rows, dtype=np.int32)
         nu, nb = ctypes.c_int64(), ctypes.c_int64()
         rc = self._L.fslr_tsv_factorize(self._h, c, codes.ctypes.data, ctypes.byref(nu), ctypes.byref(nb))
         if rc != OK:
             return None
-        buf = np.empty(max(nb.value, 1), dtype=np.uint8)
-        ends = np.empty(max(nu.value, 1), dtype=np.int64)
-        self._L.fslr_tsv_uniques(self._h, c, buf.ctypes.data, ends.ctypes.data)
+        self._fact = getattr(self, '_fact', {})
+        self._fact[name] = (int(nu.value), int(nb.value))
+        return codes, int(nu.value)
+
+    def uniques(self, name: str):
+        """The uniques of the last :meth:`factorize_codes` of ``name`` (object array of str)."""
+        nu, nb = self._fact[name]
+        buf = np.empty(max(nb, 1), dtype=np.uint8)
+        ends = np.empty(max(nu, 1), dtype=np.int64)
+        self._L.fslr_tsv_uniques(self._h, self._col(name), buf.ctypes.data, ends.ctypes.data)
         raw = buf.tobytes()
-        starts = np.concatenate(([0], ends[:nu.value - 1])) if nu.value else ends[:0]
-        uniq = np.array([raw[s:e].decode() for s, e in zip(starts.tolist(), ends[:nu.value].tolist())],
-                        dtype=object)
-        return codes, uniq
+        starts = np.concatenate(([0], ends[:nu - 1])) if nu else ends[:0]
+        return np.array([raw[s:e].decode() for s, e in zip(starts.tolist(), ends[:nu].tolist())], dtype=object)
+
+    def factorize(self, name: str):
+        """(codes int32[rows], uniques object[k]) as ``pd.factorize(col, sort=False)``, or None."""
+        f = self.factorize_codes(name)
+        if f is None:
+            return None
+        return f[0], self.uniques(name)
+
+    def scan(self, int_names):
+        """verbatim() and int_columns(int_names) in one pass: the columns, or None when either fails."""
+        names = list(dict.fromkeys(int_names))
+        cols = np.asarray([self._col(n) for n in names], dtype=np.int32)
+        outs = [np.empty(self.rows, dtype=np.int64) for _ in names]
+        ptrs = (ctypes.c_void_p * len(outs))(*[o.ctypes.data for o in outs])
+        rc = self._L.fslr_tsv_scan(self._h, len(names), cols.ctypes.data, ctypes.cast(ptrs, ctypes.c_void_p))
+        return dict(zip(names, outs)) if rc == OK else None
+
+    def scan_all(self, int_names, str_names):
+        """scan() that also factorizes ``str_names`` in the same pass: ({name: int64[rows]},
+        {name: (codes int32[rows], number of uniques)}), or None.  :meth:`uniques` gives the values."""
+        names = list(dict.fromkeys(int_names))
+        snames = list(dict.fromkeys(str_names))
+        cols = np.asarray([self._col(n) for n in names], dtype=np.int32)
+        scols = np.asarray([self._col(n) for n in snames], dtype=np.int32)
+        outs = [np.empty(self.rows, dtype=np.int64) for _ in names]
+        codes = [np.empty(self.rows, dtype=np.int32) for _ in snames]
+        counts = np.zeros(2 * max(1, len(snames)), dtype=np.int64)
+        ptrs = (ctypes.c_void_p * max(1, len(outs)))(*[o.ctypes.data for o in outs])
+        sptrs = (ctypes.c_void_p * max(1, len(codes)))(*[o.ctypes.data for o in codes])
+        rc = self._L.fslr_tsv_scan_all(self._h, len(names), cols.ctypes.data, ctypes.cast(ptrs, ctypes.c_void_p),
+                                       len(snames), scols.ctypes.data, ctypes.cast(sptrs, ctypes.c_void_p),
+                                       counts.ctypes.data)
+        if rc != OK:
+            return None
+        self._fact = getattr(self, '_fact', {})
+        strs = {}
+        for k, n in enumerate(snames):
+            self._fact[n] = (int(counts[2 * k]), int(counts[2 * k + 1]))
+            strs[n] = (codes[k], int(counts[2 * k]))
+        return dict(zip(names, outs)), strs
 
     def verbatim(self) -> bool:
         return self._L.fslr_tsv_verbatim(self._h) == OK
@@ -272,21 +330,17 @@ def frame_from(t: 'TsvFile', int_columns=INT_COLUMNS, str_columns=STR_COLUMNS):
     in ``attrs`` (:class:`QnameCodes`)."""
     if t.declined or not (set(int_columns) | set(str_columns)) <= set(t.columns):
         return None
-    cols = {}
+    cols = t.int_columns([c for c in int_columns if c not in str_columns])
+    if cols is None:
+        return None
     qcodes = None
-    for name in set(int_columns) | set(str_columns):
-        if name in str_columns:
-            f = t.factorize(name)
-            if f is None:
-                return None
-            cols[name] = f[1][f[0]]
-            if name == 'qname':
-                qcodes = QnameCodes(f[0], f[1])
-        else:
-            v = t.int_column(name)
-            if v is None:
-                return None
-            cols[name] = v
+    for name in str_columns:
+        f = t.factorize(name)
+        if f is None:
+            return None
+        cols[name] = f[1][f[0]]
+        if name == 'qname':
+            qcodes = QnameCodes(f[0], f[1])
     df = pd.DataFrame({c: cols[c] for c in t.columns if c in cols})
     if qcodes is not None:
         df.attrs[ATTR] = qcodes

@@ -21,7 +21,7 @@ import click
 import numpy as np
 import pandas as pd
 
-from . import __version__, cluster, ingest
+from . import __version__, cluster, fastcli, ingest
 
 # primer names of the reference's primers.csv (fslr/primers.csv:2-7); main.py:59-67 validates
 # --primers against them even under --skip-alignment
@@ -128,30 +128,69 @@ def run_clustering(args, basename):
         # while this process reads and prepares the input (fslr_amd.multi.RankPool)
         from . import multi
         multi.pool(args['gpus'], first_device=args.get('device') or 0)
-    tsv, bed_file = _native_open(f'{basename}.mappings.bed') if args.get('native_io', True) else (None, None)
-    if bed_file is None:
-        bed_file = pd.read_csv(f'{basename}.mappings.bed', sep='\t')
-    t['read_csv'] = time.perf_counter() - t0
+    path = f'{basename}.mappings.bed'
+    tsv = _open_tsv(path) if args.get('native_io', True) else None
     try:
+        if tsv is not None and not args['filter_high_coverage']:
+            # the columnar path (fastcli): codes and int columns, no frame of rows; the scan checks
+            # that every column round-trips through pandas (verbatim) while parsing the int columns
+            try:
+                cols = tsv.scan_all(fastcli.INT_COLS, fastcli.STR_COLS)
+            except KeyError:
+                cols = None
+            if cols is not None:
+                t['read_csv'] = time.perf_counter() - t0
+                try:
+                    return fastcli.run(args, basename, tsv, cols[0], cols[1], t)
+                except fastcli.Fallback:
+                    pass
+        if tsv is not None and not tsv.verbatim():
+            tsv.close()
+            tsv = None
+        bed_file = None
+        if tsv is not None:
+            bed_file = ingest.frame_from(tsv, int_columns=ingest.INT_COLUMNS + ('alignment_score',))
+            if bed_file is None:
+                tsv.close()
+                tsv = None
+        if bed_file is None:
+            bed_file = pd.read_csv(path, sep='\t')
+        t['read_csv'] = time.perf_counter() - t0
         return _cluster_and_write(args, basename, bed_file, tsv, t)
     finally:
         if tsv is not None:
             tsv.close()
 
 
-def _native_open(path):
-    """(TsvFile, frame of the columns clustering and the writers read) or (None, None).
-
-    Only when every input column would round-trip through pandas unchanged, so that writing the
-    input's own row bytes equals ``to_csv`` of the pandas frame (reference main.py:349,352).
-    """
+def _open_tsv(path):
+    """The native reader's TsvFile, or None when it declines the file (pandas reads it)."""
     try:
         tsv = ingest.TsvFile(path)
     except (FileNotFoundError, OSError):
+        return None
+    if tsv.declined:
+        tsv.close()
+        return None
+    return tsv
+
+
+def _native_tsv(path):
+    """The native reader's TsvFile when every input column would round-trip through pandas unchanged,
+    so that writing the input's own row bytes equals ``to_csv`` of the pandas frame (reference
+    main.py:349,352); else None (pandas reads the file)."""
+    tsv = _open_tsv(path)
+    if tsv is not None and not tsv.verbatim():
+        tsv.close()
+        return None
+    return tsv
+
+
+def _native_open(path):
+    """(TsvFile, frame of the columns clustering and the writers read) or (None, None)."""
+    tsv = _native_tsv(path)
+    if tsv is None:
         return None, None
-    bed = None
-    if not tsv.declined and tsv.verbatim():
-        bed = ingest.frame_from(tsv, int_columns=ingest.INT_COLUMNS + ('alignment_score',))
+    bed = ingest.frame_from(tsv, int_columns=ingest.INT_COLUMNS + ('alignment_score',))
     if bed is None:
         tsv.close()
         return None, None

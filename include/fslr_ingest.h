@@ -42,6 +42,8 @@ int fslr_tsv_find(const FslrTsv *t, const char *name);
 
 /* out[rows]: the column as int64 if every field is a canonical integer, else DECLINE. */
 int fslr_tsv_int_column(const FslrTsv *t, int col, int64_t *out);
+/* fslr_tsv_int_column for n columns in one pass over the rows (cols distinct): outs[k][rows]. */
+int fslr_tsv_int_columns(const FslrTsv *t, int n, const int32_t *cols, int64_t *const *outs);
 
 /* codes[rows] (int32, first-appearance order like pd.factorize(sort=False)).
  * Returns the number of unique values in *n_uniq and their total byte length in
@@ -57,6 +59,15 @@ int fslr_tsv_uniques(const FslrTsv *t, int col, char *buf, int64_t *ends);
  * column back byte-identically (canonical int64 columns, or text columns with no numeric,
  * bool or NA spelling besides empty); otherwise DECLINE and the caller writes with pandas. */
 int fslr_tsv_verbatim(const FslrTsv *t);
+/* fslr_tsv_verbatim and the canonical-int columns int_cols (outs[k][rows]) in the same pass over
+ * the rows: OK only when both hold (DECLINE otherwise: the pandas path reads the file). */
+int fslr_tsv_scan(const FslrTsv *t, int n_int, const int32_t *int_cols, int64_t *const *outs);
+/* fslr_tsv_scan that also factorizes the string columns str_cols in the same pass (codes
+ * str_codes[k][rows] as fslr_tsv_factorize; str_counts[2k] = uniques, str_counts[2k+1] = their
+ * bytes, fetched with fslr_tsv_uniques); DECLINE as fslr_tsv_scan, or when a string column holds an
+ * NA field or only canonical ints. */
+int fslr_tsv_scan_all(FslrTsv *t, int n_int, const int32_t *int_cols, int64_t *const *outs, int n_str,
+                      const int32_t *str_cols, int32_t *const *str_codes, int64_t *str_counts);
 /* Header = input header + header_suffix.  Row k of the output = input row rows_out[k] (LF line
  * end) + suffix suffix_id[k], where suffix u is suffix_buf[suffix_ends[u-1] .. suffix_ends[u]). */
 int fslr_tsv_write(const FslrTsv *t, const char *path, const char *header_suffix, const int64_t *rows_out,

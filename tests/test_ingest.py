@@ -81,7 +81,10 @@ def test_inputs_pandas_types_differently_are_declined(tmp_path, mutate):
     HEADER + _rows(30).replace('\t+\tAC\n', '\t+\n', 2),                             # rows narrower than it
     HEADER.replace('strand', 'seq') + _rows(30),                                    # repeated name -> 'seq.1'
     HEADER.replace('strand', '') + _rows(30),                                       # empty name -> 'Unnamed: 8'
-], ids=['wide_row', 'short_rows', 'dup_name', 'empty_name'])
+    HEADER + _rows(30).replace('\tAC\n', '\tACx\n').replace('\tACx\n', '\t12\n', 3),   # ints, then text
+    HEADER + _rows(30).replace('\tAC\n', '\t7\n', 29),                               # text after 29 ints
+    HEADER + _rows(30).replace('\tAC\n', '\t1.5\n', 1),                              # a float among text
+], ids=['wide_row', 'short_rows', 'dup_name', 'empty_name', 'int_then_text', 'text_last', 'float_in_text'])
 def test_verbatim_declines_rows_pandas_would_rewrite(tmp_path, text):
     """The writer copies input row bytes only when to_csv would write them unchanged: ragged rows
     and header names pandas renames send the CLI to the pandas path."""
