@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Digests of the oracle's graph for BASELINE config 3/4's input (1M reads, 1-16 fillings, uniform,
-seed 11): E* (no cap) and the reference loop with the per-read edge cap (cluster.py:197-224), as
+seed 11): E* (no cap; the cap at 10 does not bind on this input, max forward degree 9) and the
+reference loop with the per-read edge cap at 3 (cluster.py:197-224, binding), as
 tests/golden/make_cfg5_full.py defines them.  tests/test_gpu_configs.py checks the product's W = 8
 chromosome split on one GPU against both.
 
@@ -31,9 +32,9 @@ def main():
                      np.repeat(csr.read_qlen2, cnt), np.repeat(csr.read_nal, cnt), csr.data_pos)
     out = dict(reads=READS, lmax=LMAX, seed=SEED, dist='uniform', n_intervals=int(csr.n_intervals),
                generator='tests/golden/make_cfg4_1m.py')
-    for key, cap in (('estar', False), ('capped', True)):
+    for key, cap, thr in (('estar', False, 10), ('capped10', True, 10), ('capped3', True, 3)):
         t = time.perf_counter()
-        o = O.run_core(oc, use_cap=cap, lean=True)
+        o = O.run_core(oc, edge_threshold=thr, use_cap=cap, lean=True)
         d = digests(o['edge_a'], o['edge_b'], o['edge_I'], o['edge_U'], o['fwd'], labels_from_comp(o['comp']))
         out[key] = dict(d, n_components=int(o['stats']['n_components']),
                         evaluated_pairs=int(o['stats']['evaluated_pairs']),

@@ -8,10 +8,15 @@
 * cfg5: 10M reads, 1-64 fillings (truncated Zipf 1.5): the edge cap binds (forward
   degrees up to 28); the capped graph of the full run, restricted to the loops of query
   reads [0, 50000), equals the oracle's reference loop over those reads
-  (tests/golden/cfg5/sample50k_capped.npz, made by tests/golden/make_cfg5_sample.py).
+  (tests/golden/cfg5/sample50k_capped.npz, made by tests/golden/make_cfg5_sample.py), and the
+  whole capped graph (every edge with I, U, the forward degrees and the labels of all 10M reads)
+  has the digests of the oracle's full run (tests/golden/cfg5/full_capped.json).
+* cfg4 input through the product's chromosome split: W = 8 ranks on one GPU, each rank's capped
+  graph and labels against the oracle's full 1M-read digests (tests/golden/cfg5/cfg4_1m.json).
 """
 import json
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -22,6 +27,7 @@ from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(__file__), 'golden')
+sys.path.insert(0, GOLDEN)
 CUTS = [1, 1, 0.66, 0.66, 0.66, 0.5]
 
 
@@ -86,7 +92,7 @@ def test_config4_1m_eight_shards_merge_to_the_full_run():
 
 
 @pytest.mark.slow
-def test_config5_10m_capped_sample_vs_oracle():
+def test_config5_10m_capped_vs_oracle():
     with open(os.path.join(GOLDEN, 'cfg5', 'sample50k_capped.json')) as fh:
         meta = json.load(fh)
     z = np.load(os.path.join(GOLDEN, 'cfg5', 'sample50k_capped.npz'))
@@ -101,6 +107,10 @@ def test_config5_10m_capped_sample_vs_oracle():
     ctx.reserve_deferred(64 << 20)
     ctx.build_index()
     want = sorted(zip(z['a'].tolist(), z['b'].tolist(), z['I'].tolist(), z['U'].tolist()))
+    from make_cfg5_full import digests
+    with open(os.path.join(GOLDEN, 'cfg5', 'full_capped.json')) as fh:
+        ref = json.load(fh)
+    full = {k: ref[k] for k in ('edges_sha256', 'fwd_sha256', 'labels_sha256', 'n_edges', 'max_fwd')}
     labels = {}
     for engine in ('sweep', 'walk'):
         st = ctx.run_query(1 - 0.04, 1 - 0.25, pass_table(CUTS), engine=engine)
@@ -114,9 +124,49 @@ def test_config5_10m_capped_sample_vs_oracle():
         got = sorted(zip(a[own].tolist(), b[own].tolist(), I[own].tolist(), U[own].tolist()))
         assert len(got) == len(want) == meta['n_edges']
         assert got == want
-        np.testing.assert_array_equal(ctx.fwd_degree()[:S], z['fwd'])
+        fwd = ctx.fwd_degree()
+        np.testing.assert_array_equal(fwd[:S], z['fwd'])
         ctx.components()
         labels[engine] = lab = ctx.labels()
         assert lab.shape == (csr.n_reads,) and np.all(lab <= np.arange(csr.n_reads))
+        d = digests(a, b, I, U, fwd, lab)
+        assert {k: d[k] for k in full} == full, engine           # the whole 10M-read graph
     np.testing.assert_array_equal(labels['sweep'], labels['walk'])
     ctx.close()
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize('thr', [10, 3])
+def test_config4_1m_product_split_w8_vs_oracle(thr):
+    """The product's chromosome split (fslr_sweep_partition -> exchange -> fslr_sweep_evaluate on
+    each of W = 8 contexts; with a binding cap also the cap exchange and replay of
+    dist.SweepShard's capped path) on the 1M-read input: every rank's graph and labels have the
+    oracle's digests (thr 10: the cap does not bind, E*; thr 3: it binds)."""
+    from make_cfg5_full import digests
+    from test_dist import _sweep_split_capped_on_device, _sweep_split_on_device
+    with open(os.path.join(GOLDEN, 'cfg5', 'cfg4_1m.json')) as fh:
+        ref = json.load(fh)
+    csr = synth.generate(ref['reads'], ref['lmax'], ref['seed']).interval_data().csr()
+    assert csr.n_intervals == ref['n_intervals']
+    thr_iv, pt = fold_overlap_threshold(csr.iv_aln, 0.8), pass_table(CUTS)
+    key = 'capped3' if thr == 3 else 'estar'
+    want = {k: ref[key][k] for k in ('edges_sha256', 'fwd_sha256', 'labels_sha256', 'n_edges', 'max_fwd')}
+    if thr == 3:
+        ctxs, cap = _sweep_split_capped_on_device(csr, thr_iv, pt, 8, thr)
+        assert cap['capped'] > 0
+        views = []
+        for c in ctxs:
+            a, b, I, U = c.edges(c.stats()['n_edges'])
+            views.append(digests(a, b, I, U, c.fwd_degree(), c.labels()))
+    else:
+        ctxs, _ = _sweep_split_on_device(csr, thr_iv, pt, 8, thr)
+        parts = [c.edges(c.stats()['n_edges']) for c in ctxs]      # each destination's edges
+        a, b, I, U = (np.concatenate([p[k] for p in parts]) for k in range(4))
+        fwd = np.sum([c.fwd_degree().astype(np.int64) for c in ctxs], axis=0)
+        views = [digests(a, b, I, U, fwd, c.labels()) for c in ctxs]
+    try:
+        for d in views:
+            assert {k: d[k] for k in want} == want
+    finally:
+        for c in ctxs:
+            c.close()
