@@ -867,22 +867,75 @@ extern "C" {
 int fslr_group_by_first_appearance(const int64_t *codes, int64_t n, int64_t n_codes, int64_t *read_code,
                                    int64_t *n_reads, int64_t *off, int64_t *perm) {
   if (n < 0 || n_codes < 0 || (n && (!codes || !perm)) || !n_reads || !off) return FSLR_INGEST_ERROR;
-  std::vector<int64_t> rank_of(static_cast<size_t>(n_codes), -1);
-  int64_t nr = 0;
-  for (int64_t k = 0; k < n; ++k) {                 // rank = order of first appearance (cluster.py:189-191)
-    const int64_t c = codes[k];
-    if (c < 0 || c >= n_codes) return FSLR_INGEST_ERROR;
-    if (rank_of[c] < 0) {
-      rank_of[c] = nr;
-      read_code[nr] = c;
-      ++nr;
+  const char *env = std::getenv("OMP_NUM_THREADS");
+  int T = env ? std::atoi(env) : 0;
+  if (T <= 0) T = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+  T = (int)std::min<int64_t>(T, std::max<int64_t>(1, n / 65536));
+  // 1. each code's first position (rank = order of first appearance, cluster.py:189-191)
+  std::vector<std::atomic<int64_t>> first_at(static_cast<size_t>(n_codes));
+  parallel_for(n_codes, T, [&](int64_t a, int64_t e, int) {
+    for (int64_t c = a; c < e; ++c) first_at[(size_t)c].store(n, std::memory_order_relaxed);
+  });
+  std::atomic<bool> bad{false};
+  parallel_for(n, T, [&](int64_t a, int64_t e, int) {
+    for (int64_t k = a; k < e; ++k) {
+      const int64_t c = codes[k];
+      if (c < 0 || c >= n_codes) { bad = true; return; }
+      int64_t cur = first_at[(size_t)c].load(std::memory_order_relaxed);
+      while (k < cur && !first_at[(size_t)c].compare_exchange_weak(cur, k, std::memory_order_relaxed)) {}
     }
-  }
-  std::vector<int64_t> cur(static_cast<size_t>(nr) + 1, 0);
-  for (int64_t k = 0; k < n; ++k) ++cur[rank_of[codes[k]] + 1];
-  for (int64_t r = 0; r < nr; ++r) cur[r + 1] += cur[r];
-  for (int64_t r = 0; r <= nr; ++r) off[r] = cur[r];
-  for (int64_t k = 0; k < n; ++k) perm[cur[rank_of[codes[k]]]++] = k;   // stable: data order inside a read
+  });
+  if (bad) return FSLR_INGEST_ERROR;
+  // 2. ranks: a position is a rank start when it is its code's first; prefix over positions
+  std::vector<int64_t> rk(static_cast<size_t>(n));            // first-position flags, then the rank per position
+  std::vector<int64_t> base((size_t)T + 1, 0);
+  parallel_for(n, T, [&](int64_t a, int64_t e, int w) {
+    int64_t cnt = 0;
+    for (int64_t k = a; k < e; ++k) cnt += first_at[(size_t)codes[k]].load(std::memory_order_relaxed) == k;
+    base[(size_t)w + 1] = cnt;
+  });
+  for (int w = 0; w < T; ++w) base[(size_t)w + 1] += base[(size_t)w];
+  const int64_t nr = base[(size_t)T];
+  std::vector<int64_t> rank_of(static_cast<size_t>(n_codes), -1);
+  parallel_for(n, T, [&](int64_t a, int64_t e, int w) {
+    int64_t r = base[(size_t)w];
+    for (int64_t k = a; k < e; ++k) {
+      const int64_t c = codes[k];
+      if (first_at[(size_t)c].load(std::memory_order_relaxed) == k) { rank_of[(size_t)c] = r; read_code[r] = c; ++r; }
+    }
+  });
+  // 3. rank per position and counts per rank
+  std::vector<std::atomic<int64_t>> cnt(static_cast<size_t>(nr) + 1);
+  parallel_for(nr + 1, T, [&](int64_t a, int64_t e, int) {
+    for (int64_t r = a; r < e; ++r) cnt[(size_t)r].store(0, std::memory_order_relaxed);
+  });
+  parallel_for(n, T, [&](int64_t a, int64_t e, int) {
+    for (int64_t k = a; k < e; ++k) {
+      const int64_t r = rank_of[(size_t)codes[k]];
+      rk[(size_t)k] = r;
+      cnt[(size_t)r + 1].fetch_add(1, std::memory_order_relaxed);
+    }
+  });
+  off[0] = 0;
+  for (int64_t r = 0; r < nr; ++r) off[r + 1] = off[r] + cnt[(size_t)r + 1].load(std::memory_order_relaxed);
+  // 4. stable scatter (data order inside a read): thread w owns a contiguous range of ranks holding
+  // about n / T positions and walks every position, keeping its own
+  std::vector<int64_t> rb((size_t)T + 1, nr);
+  rb[0] = 0;
+  for (int w = 1; w < T; ++w) rb[(size_t)w] = std::upper_bound(off, off + nr + 1, n * w / T) - off - 1;
+  for (int w = 1; w <= T; ++w) rb[(size_t)w] = std::max(rb[(size_t)w], rb[(size_t)w - 1]);
+  std::vector<std::thread> pool;
+  for (int w = 0; w < T; ++w)
+    pool.emplace_back([&, w] {
+      const int64_t r0 = rb[(size_t)w], r1 = rb[(size_t)w + 1];
+      if (r0 >= r1) return;
+      std::vector<int64_t> cur(off + r0, off + r1);
+      for (int64_t k = 0; k < n; ++k) {
+        const int64_t r = rk[(size_t)k];
+        if (r >= r0 && r < r1) perm[cur[(size_t)(r - r0)]++] = k;
+      }
+    });
+  for (auto &th : pool) th.join();
   *n_reads = nr;
   return FSLR_INGEST_OK;
 }
@@ -918,3 +971,67 @@ int fslr_gather_i64(int n_arrays, const int64_t *const *src, int64_t *const *dst
 }
 
 }  // extern "C"
+
+// ---- keep_fillings + prepare_data's per-row columns (fastcli) ----
+extern "C" {
+
+int fslr_fillings(int64_t n_rows, const int32_t *qcode, int64_t n_q, const uint8_t *row_keep, const int64_t *rstart,
+                  const int64_t *rend, const int64_t *aln, const int64_t *qstart, const int64_t *qend,
+                  const int64_t *nal, const int32_t *ccode, const int64_t *chrom_lut, int64_t *n_out, int64_t *frow,
+                  int64_t *start, int64_t *end, int64_t *aln_o, int64_t *qc_o, int64_t *nal_o, int64_t *qlen2_o,
+                  int64_t *chrom_o, int n_threads) {
+    if (n_rows < 0 || n_q < 0 || !qcode || !n_out) return FSLR_INGEST_ERROR;
+    // 1. first and last row (file order, rows kept by row_keep) of every qname
+    std::vector<int64_t> first((size_t)n_q, -1), last((size_t)n_q, -1);
+    for (int64_t i = 0; i < n_rows; ++i) {
+        if (row_keep && !row_keep[i]) continue;
+        const int32_t q = qcode[i];
+        if (q < 0 || q >= n_q) return FSLR_INGEST_ERROR;
+        if (first[(size_t)q] < 0) first[(size_t)q] = i;
+        last[(size_t)q] = i;
+    }
+    auto kept = [&](int64_t i) {
+        if (row_keep && !row_keep[i]) return false;
+        const int32_t q = qcode[i];
+        return first[(size_t)q] != i && last[(size_t)q] != i;
+    };
+    // 2. qlen2 = max(qend) - min(qstart) over each qname's fillings (cluster.py:14-31)
+    std::vector<int64_t> lo((size_t)n_q, INT64_MAX), hi((size_t)n_q, INT64_MIN);
+    for (int64_t i = 0; i < n_rows; ++i) {
+        if (!kept(i)) continue;
+        const int32_t q = qcode[i];
+        lo[(size_t)q] = std::min(lo[(size_t)q], qstart[i]);
+        hi[(size_t)q] = std::max(hi[(size_t)q], qend[i]);
+    }
+    // 3. the fillings' columns, compacted in file order
+    int T = n_threads > 0 ? n_threads : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    T = (int)std::min<int64_t>(T, std::max<int64_t>(1, n_rows / 65536));
+    std::vector<int64_t> base((size_t)T + 1, 0);
+    parallel_for(n_rows, T, [&](int64_t a, int64_t e, int w) {
+        int64_t c = 0;
+        for (int64_t i = a; i < e; ++i) c += kept(i);
+        base[(size_t)w + 1] = c;
+    });
+    for (int w = 0; w < T; ++w) base[(size_t)w + 1] += base[(size_t)w];
+    parallel_for(n_rows, T, [&](int64_t a, int64_t e, int w) {
+        int64_t k = base[(size_t)w];
+        for (int64_t i = a; i < e; ++i) {
+            if (!kept(i)) continue;
+            const int32_t q = qcode[i];
+            frow[k] = i;
+            start[k] = std::min(rstart[i], rend[i]);
+            end[k] = std::max(rstart[i], rend[i]);
+            aln_o[k] = aln[i];
+            qc_o[k] = q;
+            nal_o[k] = nal[i];
+            qlen2_o[k] = hi[(size_t)q] - lo[(size_t)q];
+            chrom_o[k] = chrom_lut[ccode[i]];
+            ++k;
+        }
+    });
+    *n_out = base[(size_t)T];
+    return FSLR_INGEST_OK;
+}
+
+}  // extern "C"
+

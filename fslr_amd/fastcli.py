@@ -101,45 +101,26 @@ def run(args, basename, tsv, ints, strs, t):
     mask = [cmap.get(x) if x != 'subtelomere' else x for x in mask_names]
     chrom_num = np.asarray([cmap[c] for c in chrom_names], dtype=np.int64)
     # cluster.py:80-86 delete_false: whole qnames go
+    row_keep = None
     if args['filter_false']:
         bad_q = np.fromiter(('False' in q for q in tsv.uniques('qname')), dtype=bool, count=n_q)
-        rows = np.flatnonzero(~bad_q[qcode])
+        row_keep = ~bad_q[qcode]
+        rows = np.flatnonzero(row_keep)
     else:
         rows = np.arange(n_rows, dtype=np.int64)
-    qc = qcode[rows].astype(np.int64)
-    # cluster.py:14-31 keep_fillings: drop each qname's first and last row, qlen2 = its fillings' span
-    first, last = first_last_masks(qc)
-    keep = ~(first | last)
-    frows = rows[keep]
-    fq_ = qc[keep]
-    qs, qe = ints['qstart'][frows], ints['qend'][frows]
-    lo = np.zeros(n_q, np.int64)
-    hi = np.zeros(n_q, np.int64)
-    if fq_.size:
-        st = _run_starts(fq_)
-        if st is not None:                                 # qname-grouped rows: one reduceat per run
-            lo[fq_[st]] = np.minimum.reduceat(qs, st)
-            hi[fq_[st]] = np.maximum.reduceat(qe, st)
-        else:
-            lo[:] = np.iinfo(np.int64).max
-            hi[:] = np.iinfo(np.int64).min
-            np.minimum.at(lo, fq_, qs)
-            np.maximum.at(hi, fq_, qe)
-    qlen2 = (hi - lo)[fq_]
-    # cluster.py:109-121 prepare_data: min/max of rstart/rend, sort by start (pandas' quicksort
-    # argsort, ties included), mask_sequences2
-    rs, re_ = ints['rstart'][frows], ints['rend'][frows]
-    start = np.minimum(rs, re_)
-    end = np.maximum(rs, re_)
-    aln = ints['aln_size'][frows]
-    chrom = chrom_num[ccode[frows]]
+    # cluster.py:14-31 keep_fillings (each qname's first and last row dropped, qlen2 = its fillings'
+    # span) and cluster.py:109-121 prepare_data's columns (min/max of rstart/rend), natively
+    f = ingest.fillings(qcode, n_q, row_keep, ints, ccode, chrom_num)
+    start = f['start']
+    # prepare_data's sort_values('start') (pandas' quicksort argsort, ties included), mask_sequences2
     order = data_order(start)
     if mask:
-        keepm = mask_keep(chrom, start, end, mask, chr_lengths, 500_000)
+        keepm = mask_keep(f['chrom'], start, f['end'], mask, chr_lengths, 500_000)
         order = order[keepm[order]]
-    cols = ingest.gather_columns([chrom, start, end, aln, fq_, ints['n_alignments'][frows], qlen2,
-                                  aln // 2 + start, frows], order)
-    c, s, e, a, q, nal, ql2, mid, ix = cols
+    c, s, e, a, q, nal, ql2, ix = ingest.gather_columns([f['chrom'], start, f['end'], f['aln'], f['qcode'], f['nal'],
+                                                         f['qlen2'], f['frow']], order)
+    mid = a // 2 + s
+    qc = qcode[rows].astype(np.int64)
     data = IntervalData(chrom=c, start=s, end=e, aln_size=a, qcode=q, qnames=_LazyQnames(tsv, n_q),
                         n_alignments=nal, qlen2=ql2, middle=mid, index=ix)
     t['prepare'] = time.perf_counter() - t1

@@ -52,6 +52,7 @@ def load(path: str = LIB_PATH):
         'fslr_format_suffix': (i32, [i32, vp, vp, i64, vp, i64, vp]),
         'fslr_group_by_first_appearance': (i32, [vp, i64, i64, vp, vp, vp, vp]),
         'fslr_gather_i64': (i32, [i32, vp, vp, vp, i64, i32]),
+        'fslr_fillings': (i32, [i64, vp, i64, vp] + [vp] * 8 + [vp] + [vp] * 8 + [i32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -351,3 +352,27 @@ def read_hot_columns(path: str, n_threads: int = 0):
     """``pd.read_csv(path, sep='\\t', usecols=HOT_COLUMNS)`` natively, or None (read with pandas)."""
     with TsvFile(path, n_threads) as t:
         return frame_from(t)
+
+
+def fillings(qcode, n_q, row_keep, ints, ccode, chrom_lut, n_threads: int = 0):
+    """keep_fillings + prepare_data's per-row columns natively (fslr_fillings): a dict of int64 columns
+    frow, start, end, aln, qcode, nal, qlen2, chrom over the fillings in file order."""
+    L = load()
+    n = int(qcode.shape[0])
+    qcode = np.ascontiguousarray(qcode, np.int32)
+    ccode = np.ascontiguousarray(ccode, np.int32)
+    lut = np.ascontiguousarray(chrom_lut, np.int64)
+    keep = None if row_keep is None else np.ascontiguousarray(row_keep, np.uint8)
+    src = [np.ascontiguousarray(ints[k], np.int64) for k in ('rstart', 'rend', 'aln_size', 'qstart', 'qend',
+                                                                'n_alignments')]
+    names = ('frow', 'start', 'end', 'aln', 'qcode', 'nal', 'qlen2', 'chrom')
+    out = {k: np.empty(n, np.int64) for k in names}
+    n_out = ctypes.c_int64()
+    rc = L.fslr_fillings(n, qcode.ctypes.data, int(n_q), keep.ctypes.data if keep is not None else None,
+                         *(a.ctypes.data for a in src), ccode.ctypes.data, lut.ctypes.data, ctypes.byref(n_out),
+                         *(out[k].ctypes.data for k in names), int(n_threads))
+    if rc != OK:
+        raise RuntimeError('fslr_fillings failed')
+    m = int(n_out.value)
+    return {k: v[:m] for k, v in out.items()}
+

@@ -90,6 +90,16 @@ int fslr_group_by_first_appearance(const int64_t *codes, int64_t n, int64_t n_co
 
 /* dst[a][k] = src[a][idx[k]] for k < n and each of the n_arrays int64 columns (n_threads <= 0: all
  * cores).  prepare_data's start sort + mask as one threaded pass. */
+/* keep_fillings (cluster.py:14-31) and prepare_data's per-row columns (cluster.py:109-121) over the
+ * rows with row_keep[i] != 0 (NULL: all): each qname's first and last row dropped, the fillings'
+ * start = min(rstart, rend), end = max(...), aln_size, qname code, n_alignments, qlen2 = max(qend) -
+ * min(qstart) over the qname's fillings, chrom = chrom_lut[ccode]; outputs hold n_rows elements,
+ * *n_out of them written, in file order. */
+int fslr_fillings(int64_t n_rows, const int32_t *qcode, int64_t n_q, const uint8_t *row_keep, const int64_t *rstart,
+                  const int64_t *rend, const int64_t *aln, const int64_t *qstart, const int64_t *qend,
+                  const int64_t *nal, const int32_t *ccode, const int64_t *chrom_lut, int64_t *n_out, int64_t *frow,
+                  int64_t *start, int64_t *end, int64_t *aln_o, int64_t *qc_o, int64_t *nal_o, int64_t *qlen2_o,
+                  int64_t *chrom_o, int n_threads);
 int fslr_gather_i64(int n_arrays, const int64_t *const *src, int64_t *const *dst, const int64_t *idx, int64_t n,
                     int n_threads);
 
