@@ -213,7 +213,12 @@ class MultiGpuIndex:
         self.first_device = 0 if device is None else int(device)
 
 
-def build_interval_trees(data, device: int | None = None, n_gpus: int = 1):
+def _open_context(device: int | None = None) -> Context:
+    """A library context on ``device`` (default $FSLR_DEVICE / $LOCAL_RANK / 0)."""
+    return Context(_default_device() if device is None else int(device))
+
+
+def build_interval_trees(data, device: int | None = None, n_gpus: int = 1, ctx: Context | None = None):
     """cluster.py:124-130: upload the prepared intervals and build the (chrom, start) index on the GPU.
 
     ``data`` is this module's ``prepare_data`` result or the reference's (a list of IntervalItem).
@@ -221,7 +226,7 @@ def build_interval_trees(data, device: int | None = None, n_gpus: int = 1):
     per-GPU processes that query_interval_trees starts."""
     if int(n_gpus) > 1:
         return MultiGpuIndex(data, n_gpus, device)
-    return DeviceIntervalIndex(data, device)
+    return DeviceIntervalIndex(data, device, ctx=ctx)
 
 
 class ClusterGraph:
@@ -303,9 +308,23 @@ class RawGraph:
     path maps ranks to qname codes itself).  Edges sorted by (a, b)."""
 
     def __init__(self, data, csr, labels, a, b, I, U, fwd, st):
-        order = np.lexsort((b, a))
         self.data, self.csr, self.labels, self.fwd, self.stats = data, csr, labels, fwd, st
-        self.a, self.b, self.I, self.U = a[order], b[order], I[order], U[order]
+        self._raw = (a, b, I, U)
+        self._sorted = None
+        self.n_edges = int(a.shape[0])
+
+    def _edges(self):
+        if self._sorted is None:                    # sorted on first use (the CLI needs only labels)
+            a, b, I, U = self._raw
+            order = np.lexsort((b, a))
+            self._sorted = (a[order], b[order], I[order], U[order])
+            self._raw = None
+        return self._sorted
+
+    a = property(lambda self: self._edges()[0])
+    b = property(lambda self: self._edges()[1])
+    I = property(lambda self: self._edges()[2])
+    U = property(lambda self: self._edges()[3])
 
 
 def query_graph(interval_trees, data, overlap_cutoff, jaccard_threshold, edge_threshold, qlen_diff, diff):

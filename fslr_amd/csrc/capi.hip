@@ -1,9 +1,11 @@
 // capi.hip — the C ABI (include/fslr_hip.h): context, HBM buffers, launch sequencing, timing.
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "fslr_hip.h"
@@ -83,6 +85,27 @@ int reserve_entries(fslr_ctx* c, int64_t capacity) {
 static int ensure_grp(fslr_ctx* c) {
   if (c->grp) return FSLR_OK;
   return dalloc(c, &c->grp, grp_ints());
+}
+
+// f(a, e, w) over [0, n) in contiguous slices on up to 16 host threads ($OMP_NUM_THREADS); the input
+// packing of fslr_set_reads touches every interval a few times (62M at cfg5)
+int host_threads(int64_t n) {
+  const char* env = std::getenv("OMP_NUM_THREADS");
+  int t = env ? std::atoi(env) : 0;
+  if (t <= 0) t = static_cast<int>(std::min(16u, std::max(1u, std::thread::hardware_concurrency())));
+  return static_cast<int>(std::min<int64_t>(std::min(t, 256), std::max<int64_t>(1, n / 65536)));
+}
+
+template <class F>
+void host_for(int64_t n, F f) {
+  const int t = host_threads(n);
+  if (t <= 1) {
+    f(int64_t(0), n, 0);
+    return;
+  }
+  std::vector<std::thread> pool;
+  for (int i = 0; i < t; ++i) pool.emplace_back([=, &f] { f(n * i / t, n * (i + 1) / t, i); });
+  for (auto& th : pool) th.join();
 }
 
 int thr_mode_of(const int32_t* thr, int64_t ni) {
@@ -179,52 +202,77 @@ int fslr_set_reads(fslr_ctx* c, const fslr_reads* r) {
   std::vector<unsigned char> rl(static_cast<size_t>(n));
   std::vector<int4> iv(static_cast<size_t>(ni));
   std::vector<unsigned char> zero(static_cast<size_t>(ni), 0);
-  for (int64_t k = 0; k < ni; ++k) {
-    const int ch = r->iv_chrom[k], s = r->iv_start[k], e = r->iv_end[k], t = r->iv_thr[k];
-    if (ch < 0 || ch >= r->n_chroms) return fail(c, FSLR_ERR_INVALID, "chrom id out of range");
-    if (s < 0 || e < s || e >= kMaxCoord)
-      return fail(c, FSLR_ERR_INVALID, "interval coordinates out of [0, 2^30)");
-    if (t == FSLR_THR_ZERO_ALN) zero[k] = 1;
-    iv[k] = make_int4(ch, s, e, t);
-  }
-  for (int64_t i = 0; i < n; ++i) {
-    const int o = r->read_off[i], len = r->read_off[i + 1] - o;
-    if (len < 1 || len > FSLR_MAX_L)
-      return fail(c, FSLR_ERR_INVALID, "every read needs 1.." + std::to_string(FSLR_MAX_L) + " intervals");
-    if (r->read_nal[i] < 0 || r->read_nal[i] >= (1 << 24))
-      return fail(c, FSLR_ERR_INVALID, "n_alignments outside [0, 2^24)");
-    if (r->read_qlen2[i] < 0)   // max(qend) - min(qstart) over a read's fillings (cluster.py:26-29)
-      return fail(c, FSLR_ERR_INVALID, "qlen2 < 0");
-    int flags = 0;
-    for (int k = o; k < o + len; ++k)
-      if (zero[k]) flags |= 1;
-    rm[i] = make_int4(o, len | (flags << 16), r->read_qlen2[i], r->read_nal[i]);
-    rl[i] = static_cast<unsigned char>(len);
-  }
+  // 0 ok, 1 chrom id, 2 coordinates, 3 read length, 4 n_alignments, 5 qlen2 (the first slice's first
+  // failure in index order is reported)
+  std::atomic<int> bad{0};
+  host_for(ni, [&](int64_t a, int64_t e, int) {
+    for (int64_t k = a; k < e; ++k) {
+      const int ch = r->iv_chrom[k], s = r->iv_start[k], en = r->iv_end[k], t = r->iv_thr[k];
+      if (ch < 0 || ch >= r->n_chroms) { bad = 1; return; }
+      if (s < 0 || en < s || en >= kMaxCoord) { bad = 2; return; }
+      if (t == FSLR_THR_ZERO_ALN) zero[k] = 1;
+      iv[k] = make_int4(ch, s, en, t);
+    }
+  });
+  if (bad == 1) return fail(c, FSLR_ERR_INVALID, "chrom id out of range");
+  if (bad == 2) return fail(c, FSLR_ERR_INVALID, "interval coordinates out of [0, 2^30)");
+  host_for(n, [&](int64_t a, int64_t e, int) {
+    for (int64_t i = a; i < e; ++i) {
+      const int o = r->read_off[i], len = r->read_off[i + 1] - o;
+      if (len < 1 || len > FSLR_MAX_L) { bad = 3; return; }
+      if (r->read_nal[i] < 0 || r->read_nal[i] >= (1 << 24)) { bad = 4; return; }
+      if (r->read_qlen2[i] < 0) { bad = 5; return; }   // max(qend) - min(qstart) over a read's fillings (cluster.py:26-29)
+      int flags = 0;
+      for (int k = o; k < o + len; ++k)
+        if (zero[k]) flags |= 1;
+      rm[i] = make_int4(o, len | (flags << 16), r->read_qlen2[i], r->read_nal[i]);
+      rl[i] = static_cast<unsigned char>(len);
+    }
+  });
+  if (bad == 3) return fail(c, FSLR_ERR_INVALID, "every read needs 1.." + std::to_string(FSLR_MAX_L) + " intervals");
+  if (bad == 4) return fail(c, FSLR_ERR_INVALID, "n_alignments outside [0, 2^24)");
+  if (bad == 5) return fail(c, FSLR_ERR_INVALID, "qlen2 < 0");
   // chromosome ranges of the (chrom, start)-sorted index: chromosome ids ascending (host counts)
   std::vector<int2> cr(static_cast<size_t>(r->n_chroms), make_int2(0, 0));
   std::vector<int64_t> chrom_counts(static_cast<size_t>(r->n_chroms), 0);
   {
-    std::vector<int64_t>& cnt = chrom_counts;
-    for (int64_t k = 0; k < ni; ++k) cnt[r->iv_chrom[k]]++;
+    std::vector<std::vector<int64_t>> part(static_cast<size_t>(host_threads(ni)),
+                                           std::vector<int64_t>(static_cast<size_t>(r->n_chroms), 0));
+    host_for(ni, [&](int64_t a, int64_t e, int w) {
+      std::vector<int64_t>& cnt = part[static_cast<size_t>(w)];
+      for (int64_t k = a; k < e; ++k) cnt[r->iv_chrom[k]]++;
+    });
+    for (const auto& p : part)
+      for (int ch = 0; ch < r->n_chroms; ++ch) chrom_counts[ch] += p[ch];
     int64_t acc = 0;
     for (int ch = 0; ch < r->n_chroms; ++ch) {
-      cr[ch] = make_int2(static_cast<int>(acc), static_cast<int>(acc + cnt[ch]));
-      acc += cnt[ch];
+      cr[ch] = make_int2(static_cast<int>(acc), static_cast<int>(acc + chrom_counts[ch]));
+      acc += chrom_counts[ch];
     }
   }
   // optional start-sorted data order: must be a permutation with non-decreasing start
   bool use_dp = false;
+  std::vector<int> inv;
   if (r->iv_data_pos) {
-    std::vector<int> inv(static_cast<size_t>(ni), -1);
-    use_dp = true;
-    for (int64_t k = 0; k < ni && use_dp; ++k) {
-      const int d = r->iv_data_pos[k];
-      if (d < 0 || d >= ni || inv[d] >= 0) use_dp = false;
-      else inv[d] = static_cast<int>(k);
-    }
-    for (int64_t d = 1; d < ni && use_dp; ++d)
-      if (r->iv_start[inv[d]] < r->iv_start[inv[d - 1]]) use_dp = false;
+    inv.assign(static_cast<size_t>(ni), -1);
+    std::atomic<bool> ok{true};
+    host_for(ni, [&](int64_t a, int64_t e, int) {
+      for (int64_t k = a; k < e; ++k) {
+        const int d = r->iv_data_pos[k];
+        if (d < 0 || d >= ni) { ok = false; return; }
+        inv[d] = static_cast<int>(k);      // a repeated d leaves a hole: the -1 check below finds it
+      }
+    });
+    if (ok)
+      host_for(ni, [&](int64_t a, int64_t e, int) {
+        for (int64_t d = a; d < e; ++d) {
+          if (inv[d] < 0 || (d > 0 && (inv[d - 1] < 0 || r->iv_start[inv[d]] < r->iv_start[inv[d - 1]]))) {
+            ok = false;
+            return;
+          }
+        }
+      });
+    use_dp = ok;
     if (!use_dp) return fail(c, FSLR_ERR_INVALID, "iv_data_pos is not a start-sorted permutation");
   }
   int rc = ensure_capacity(c, n, ni, r->n_chroms);
@@ -238,19 +286,21 @@ int fslr_set_reads(fslr_ctx* c, const fslr_reads* r) {
     dch.resize(static_cast<size_t>(ni));
     drc.resize(static_cast<size_t>(ni));
     dgt.resize(static_cast<size_t>(ni));
-    for (int64_t i = 0; i < n; ++i) {
-      // the gate word of kernels.hpp idx_gate, per interval like the reference's IntervalItem
-      // (which carries qlen2 and n_alignments, cluster.py:10-11)
-      const int4 m = rm[i];
-      const int2 gate = make_int2(m.z, (m.w & 0xFFFFFF) | ((m.y & 0x7F) << 24) | (((m.y >> 16) & 1) << 31));
-      for (int k = r->read_off[i]; k < r->read_off[i + 1]; ++k) {
-        const int d = r->iv_data_pos[k];
-        dch[d] = static_cast<unsigned>(r->iv_chrom[k]);
-        drc[d] = make_int4(r->iv_start[k], r->iv_end[k], r->iv_thr[k],
-                           static_cast<int>((i << 6) | (k - r->read_off[i])));
-        dgt[d] = gate;
+    host_for(n, [&](int64_t a, int64_t e, int) {
+      for (int64_t i = a; i < e; ++i) {
+        // the gate word of kernels.hpp idx_gate, per interval like the reference's IntervalItem
+        // (which carries qlen2 and n_alignments, cluster.py:10-11)
+        const int4 m = rm[i];
+        const int2 gate = make_int2(m.z, (m.w & 0xFFFFFF) | ((m.y & 0x7F) << 24) | (((m.y >> 16) & 1) << 31));
+        for (int k = r->read_off[i]; k < r->read_off[i + 1]; ++k) {
+          const int d = r->iv_data_pos[k];
+          dch[d] = static_cast<unsigned>(r->iv_chrom[k]);
+          drc[d] = make_int4(r->iv_start[k], r->iv_end[k], r->iv_thr[k],
+                             static_cast<int>((i << 6) | (k - r->read_off[i])));
+          dgt[d] = gate;
+        }
       }
-    }
+    });
     HIP_TRY(c, hipMemcpyAsync(c->data_pos, r->iv_data_pos, ni * sizeof(int), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(c, hipMemcpyAsync(c->dchrom, dch.data(), ni * sizeof(unsigned), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(c, hipMemcpyAsync(c->drec, drc.data(), ni * sizeof(int4), hipMemcpyHostToDevice, c->stream));

@@ -627,7 +627,9 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
       if (hv1) la1 = RL[entry_a(e1)];
       unsigned long long k0 = v0 ? group_key(e0, r0) : ~0ull;
       unsigned long long k1 = v1 ? group_key(e1, r1) : ~0ull;
+#if !defined(FSLR_PAIRS_ABLATE) || (FSLR_PAIRS_ABLATE & 1) == 0
       bitonic128(k0, k1, lane);                                    // positions [0, gend) hold the group
+#endif
       const unsigned long long q0 = __shfl_up(k0, 1);
       const unsigned long long k0_63 = __shfl(k0, kWave - 1);
       const unsigned long long w1 = __shfl_up(k1, 1);
@@ -678,7 +680,11 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
       if (d0) atomicOr(&PH[g0], 1 << 30);
       if (d1) atomicOr(&PH[g1], 1 << 30);
       wave_lds_sync();
+#if defined(FSLR_PAIRS_ABLATE) && (FSLR_PAIRS_ABLATE & 2)
+      for (int k0s = 0; k0s < 0; k0s += kWave) {                  // profiling ablation: no segment pass
+#else
       for (int k0s = 0; k0s < nseg; k0s += kWave) {
+#endif
         const int p = k0s + lane;
         const bool act = p < nseg;
         int I = 0, r = 0, B = 0, LB = 0;

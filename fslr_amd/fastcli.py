@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import ctypes
 import time
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
@@ -78,6 +79,10 @@ def run(args, basename, tsv, ints, strs, t):
     after writing both outputs.  Raises Fallback before writing anything when a step needs the
     pandas path."""
     t1 = time.perf_counter()
+    # the HIP context comes up while the host prepares the input (one GPU; the multi-GPU ranks make
+    # their own)
+    pool = ThreadPoolExecutor(2)
+    ctx_f = pool.submit(cluster._open_context, args.get('device')) if (args.get('gpus') or 1) == 1 else None
     n_rows = tsv.rows
     qcode, n_q = strs['qname']
     ccode, _ = strs['chrom']
@@ -112,15 +117,20 @@ def run(args, basename, tsv, ints, strs, t):
     # span) and cluster.py:109-121 prepare_data's columns (min/max of rstart/rend), natively
     f = ingest.fillings(qcode, n_q, row_keep, ints, ccode, chrom_num)
     start = f['start']
-    # prepare_data's sort_values('start') (pandas' quicksort argsort, ties included), mask_sequences2
-    order = data_order(start)
-    if mask:
-        keepm = mask_keep(f['chrom'], start, f['end'], mask, chr_lengths, 500_000)
+    t['prepare.fill'] = time.perf_counter() - t1
+    # prepare_data's sort_values('start') (pandas' quicksort argsort, ties included; numpy sorts
+    # without the GIL, so mask_sequences2 and the writers' per-qname sums run beside it)
+    order_f = pool.submit(data_order, start)
+    keepm = mask_keep(f['chrom'], start, f['end'], mask, chr_lengths, 500_000) if mask else None
+    qc = qcode[rows].astype(np.int64)
+    w = _writer_prep(qc, n_q, score[rows])
+    order = order_f.result()
+    t['prepare.sort'] = time.perf_counter() - t1 - t['prepare.fill']
+    if keepm is not None:
         order = order[keepm[order]]
     c, s, e, a, q, nal, ql2, ix = ingest.gather_columns([f['chrom'], start, f['end'], f['aln'], f['qcode'], f['nal'],
                                                          f['qlen2'], f['frow']], order)
     mid = a // 2 + s
-    qc = qcode[rows].astype(np.int64)
     data = IntervalData(chrom=c, start=s, end=e, aln_size=a, qcode=q, qnames=_LazyQnames(tsv, n_q),
                         n_alignments=nal, qlen2=ql2, middle=mid, index=ix)
     t['prepare'] = time.perf_counter() - t1
@@ -129,13 +139,15 @@ def run(args, basename, tsv, ints, strs, t):
     t['csr'] = time.perf_counter() - t1
 
     t2 = time.perf_counter()
-    trees = cluster.build_interval_trees(data, device=args.get('device'), n_gpus=args.get('gpus') or 1)
+    trees = cluster.build_interval_trees(data, device=args.get('device'), n_gpus=args.get('gpus') or 1,
+                                         ctx=ctx_f.result() if ctx_f is not None else None)
+    pool.shutdown()
     t['upload'] = time.perf_counter() - t2
     t2 = time.perf_counter()
     g = cluster.query_graph(trees, data, args['overlap'], [float(i) for i in args['jaccard_cutoffs'].split(',')], 10,
                             args['qlen_diff'], args['n_alignment_diff'])
     t['query'] = time.perf_counter() - t2
-    if g.a.shape[0] == 0:
+    if g.n_edges == 0:
         print('No clusters were found.')
         return False
 
@@ -154,31 +166,17 @@ def run(args, basename, tsv, ints, strs, t):
     rq = csr.read_qcode[node]
     q_cid[rq] = rid[lab[node]]
     q_size[rq] = sizes[lab[node]]
-    present = np.zeros(n_q, bool)
-    present[qc] = True
+    present, keys, key_of_code, avg, first_row = w
     single = present & (q_cid < 0)
     k = int(single.sum())
     q_cid[single] = roots.size + np.arange(k)
     q_size[single] = 1
-    keys = np.flatnonzero(present)                       # ascending code = first-appearance order
-    key_of_code = np.full(n_q, -1, np.int64)
-    key_of_code[keys] = np.arange(keys.size)
     cl_k, nr_k = q_cid[keys], q_size[keys]
     if k:
         cl_k, nr_k = cl_k.astype(np.float64), nr_k.astype(np.float64)
     _write(tsv, f'{basename}.mappings.cluster.bed', rows, key_of_code[qc], ['cluster', 'n_reads'], [cl_k, nr_k])
     # cluster.py:237-254 choose_alignment: per cluster the qname with the highest mean score, the
     # first in file order on ties; its rows
-    sums = np.bincount(qc, weights=score[rows].astype(np.float64), minlength=n_q)
-    cnt = np.bincount(qc, minlength=n_q)
-    with np.errstate(invalid='ignore', divide='ignore'):
-        avg = sums / cnt
-    first_row = np.full(n_q, rows.size, np.int64)
-    st = _run_starts(qc)
-    if st is not None:
-        first_row[qc[st]] = st
-    else:
-        np.minimum.at(first_row, qc, np.arange(rows.size))
     cid_k = q_cid[keys]
     best = np.full(int(cid_k.max()) + 1, -np.inf)
     np.maximum.at(best, cid_k, avg[keys])
@@ -195,9 +193,32 @@ def run(args, basename, tsv, ints, strs, t):
         st = g.stats
         import sys
         print('timings_s ' + ' '.join(f'{k}={v:.3f}' for k, v in t.items()) +
-              f' evaluated_pairs={st.get("evaluated_pairs", -1)} edges={g.a.shape[0]} max_fwd={st.get("max_fwd", -1)}'
+              f' evaluated_pairs={st.get("evaluated_pairs", -1)} edges={g.n_edges} max_fwd={st.get("max_fwd", -1)}'
               ' path=columns', file=sys.stderr)
     return True
+
+
+def _writer_prep(qc, n_q, score):
+    """What the writers need that does not depend on the graph: the qnames present (ascending code =
+    first-appearance order) and their key numbers, each qname's mean alignment_score
+    (choose_alignment's groupby mean: a float64 sum of int64 values below 2**53 is exact in any
+    order) and its first row."""
+    present = np.zeros(n_q, bool)
+    present[qc] = True
+    keys = np.flatnonzero(present)
+    key_of_code = np.full(n_q, -1, np.int64)
+    key_of_code[keys] = np.arange(keys.size)
+    sums = np.bincount(qc, weights=score.astype(np.float64), minlength=n_q)
+    cnt = np.bincount(qc, minlength=n_q)
+    with np.errstate(invalid='ignore', divide='ignore'):
+        avg = sums / cnt
+    first_row = np.full(n_q, qc.size, np.int64)
+    st = _run_starts(qc)
+    if st is not None:
+        first_row[qc[st]] = st
+    else:
+        np.minimum.at(first_row, qc, np.arange(qc.size))
+    return present, keys, key_of_code, avg, first_row
 
 
 def _run_starts(codes):

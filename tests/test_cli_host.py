@@ -40,7 +40,8 @@ def _oracle_graph(trees, data, overlap, cuts, thr, qlen_diff, diff):
 
 @pytest.fixture
 def oracle_query(monkeypatch):
-    monkeypatch.setattr(cluster, 'build_interval_trees', lambda data, device=None, n_gpus=1: None)
+    monkeypatch.setattr(cluster, 'build_interval_trees', lambda data, device=None, n_gpus=1, ctx=None: None)
+    monkeypatch.setattr(cluster, '_open_context', lambda device=None: None)
     monkeypatch.setattr(cluster, 'query_graph', _oracle_graph)
 
 
