@@ -34,6 +34,7 @@ import socket
 import subprocess
 import sys
 import tempfile
+import threading
 import time
 
 import numpy as np
@@ -105,6 +106,7 @@ class _Rank:
             kw['device_id'] = self.dev
         dist.init_process_group(self.backend, **kw)
         self.stream = torch.cuda.Stream(self.dev)
+        self.ctx = None                               # the rank's library context, kept across queries
 
     def step(self, d):
         """One query on the CSR in directory d; rank 0: the labels, its edges and forward degrees (all
@@ -119,7 +121,9 @@ class _Rank:
         torch.cuda.set_device(self.dev_index)
         torch.cuda.set_stream(self.stream)
         try:
-            ctx = _lib.Context(self.dev_index, stream=self.stream.cuda_stream)
+            if self.ctx is None:
+                self.ctx = _lib.Context(self.dev_index, stream=self.stream.cuda_stream)
+            ctx = self.ctx
             try:
                 ctx.load_csr(csr, thr)
                 ctx.reserve_edges(max(1 << 16, 12 * csr.n_reads // self.world))
@@ -136,14 +140,19 @@ class _Rank:
                     fwd = ctx.fwd_degree()
                 return {'labels': labels, 'edges': (a, b, I, U), 'fwd': fwd, 'capped': bool(info['capped']),
                         'max_fwd': int(info['max_fwd']), 'cap': info.get('cap', {}), 'backend': self.backend}
-            finally:
-                ctx.close()
+            except BaseException:
+                self.ctx.close()                      # a failed query leaves no half-set context behind
+                self.ctx = None
+                raise
         finally:
             torch.cuda.set_device(prev_dev)
             torch.cuda.set_stream(prev_stream)
 
     def close(self):
         import torch.distributed as dist
+        if self.ctx is not None:
+            self.ctx.close()
+            self.ctx = None
         if dist.is_initialized():
             dist.destroy_process_group()
 
@@ -235,11 +244,23 @@ class RankPool:
         pkg_root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
         env['PYTHONPATH'] = pkg_root + (os.pathsep + env['PYTHONPATH'] if env.get('PYTHONPATH') else '')
         self.procs = {}
+        self._warm, self._warm_err = None, None
         for r in range(1 if self.in_proc else 0, self.world):
             self.procs[r] = subprocess.Popen(
                 [sys.executable, '-m', 'fslr_amd.multi', str(r), str(self.world), str(self.port),
                  str(self.first_device), str(int(self.force_gloo)), str(self.timeout_s)],
                 env=env, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, bufsize=1)
+        if self.in_proc:
+            # rank 0 joins on a worker thread (torch import, device, rendezvous) while the caller
+            # reads and prepares its input; the first query waits for it
+            self._warm = threading.Thread(target=self._make_rank0, daemon=True)
+            self._warm.start()
+
+    def _make_rank0(self):
+        try:
+            self.rank0 = _Rank(0, self.world, self.port, self.first_device, self.force_gloo, self.timeout_s)
+        except BaseException as e:                   # noqa: BLE001 - raised by the first query
+            self._warm_err = e
 
     def _wait_done(self, limit=None):
         """Every child's 'DONE' for the current query; RuntimeError when one died or, with ``limit``
@@ -274,6 +295,11 @@ class RankPool:
             err0 = None
             if self.in_proc:
                 try:
+                    if self._warm is not None:
+                        self._warm.join()
+                        self._warm = None
+                        if self._warm_err is not None:
+                            raise self._warm_err
                     if self.rank0 is None:
                         self.rank0 = _Rank(0, self.world, self.port, self.first_device, self.force_gloo,
                                            self.timeout_s)
@@ -329,6 +355,8 @@ class RankPool:
                 p.kill()
                 p.wait()
         self.procs = {}
+        if self._warm is not None and self._warm.is_alive():
+            self._warm.join(timeout=5)               # its rendezvous fails once the other ranks are gone
         if self.rank0 is not None:
             self.rank0.close()
             self.rank0 = None
