@@ -323,9 +323,9 @@ constexpr int kLongScr = kHash2 * (4 + 4 + 8 + 8) + 2 * (kPairLimit + kWave);
 constexpr int kGroupScr = kStageE * (8 + 8 + 8) + 4 * (kStageE + 1);
 constexpr int kScrWords = ((kLongScr > kGroupScr ? kLongScr : kGroupScr) + 7) / 8;
 
-// lane ^ ST's value without an LDS round trip: DPP for strides 1 .. 8 (inside a 16-lane row: quad
-// permutes, row shifts), gfx950's v_permlane16_swap / v_permlane32_swap for 16 and 32 (swap(v, v)
-// exchanges the odd rows / upper half of one copy with the even rows / lower half of the other)
+// lane ^ ST's value: DPP for strides 1 .. 8 (inside a 16-lane row: quad permutes, row shifts),
+// ds_swizzle for 16 (inside 32 lanes), ds_bpermute for 32 — the short strides cost a VALU op, not an
+// LDS round trip
 template <int ST>
 __device__ __forceinline__ unsigned xor_lane32(unsigned v, int lane) {
   if constexpr (ST == 1) {
@@ -337,12 +337,9 @@ __device__ __forceinline__ unsigned xor_lane32(unsigned v, int lane) {
     const int dn = __builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x110 + ST, 0xF, 0xF, true);   // lane - ST
     return static_cast<unsigned>((lane & ST) ? dn : up);
   } else if constexpr (ST == 16) {
-    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);   // [0]: rows 1, 3 <- rows 0, 2
-    return (lane & 16) ? r[0] : r[1];
+    return static_cast<unsigned>(__builtin_amdgcn_ds_swizzle(static_cast<int>(v), 0x401F));            // xor 16
   } else {
-    static_assert(ST == 32, "strides 1 .. 32");
-    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);   // [0]: lanes 32.. <- lanes 0..
-    return (lane & 32) ? r[0] : r[1];
+    return static_cast<unsigned>(__shfl_xor(static_cast<int>(v), ST));
   }
 }
 
