@@ -114,7 +114,10 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
     if constexpr (kMode == 2) {
       out = g.tile_ub[tile];
       if (out + T > g.ub_cap) {                  // the upper-bound buffer is too small: grow + rerun
-        if (lane == 0) atomicOr(g.err + kErrOverflow, 8);
+        if (lane == 0) {
+          atomicOr(g.err + kErrOverflow, 8);
+          g.tile_cnt[tile] = 0;                  // the passes after the sweep read every tile's count
+        }
         continue;
       }
     }
@@ -875,7 +878,7 @@ __global__ __launch_bounds__(kMsdThreads) void k_msd_pass1(const unsigned long l
             j = lo;
           }
           const long long at = __shfl(u0, j) + (k - __shfl(exc, j));
-          v[q] = k < T && at < n ? src[at] : 0ull;              // n: the slot buffer's size
+          v[q] = k < T && at >= 0 && at < n ? src[at] : 0ull;   // n: the slot buffer's size
         }
 #pragma unroll
         for (int q = 0; q < kMsdUnroll; ++q) {
