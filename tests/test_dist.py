@@ -580,3 +580,36 @@ def test_gloo_world2_zero_division_raises_on_every_rank(world_case, tmp_path):
                        join=True, start_method='spawn')
     for r in range(2):
         assert (tmp_path / f'raised{r}.txt').read_text().startswith('ZeroDivisionError')
+
+
+@pytest.mark.gpu
+def test_sweep_partition_first_call_in_reused_memory():
+    """The first fslr_sweep_partition on a fresh context overflows its upper-bound slots (sized for
+    4 pair tests per interval) and reruns; the grouping pass that runs before the overflow check must
+    see every tile's count defined even when the context's buffers come from freed, dirty device
+    memory (round-3 fix: a skipped tile's count was left unwritten)."""
+    import torch
+    from fslr_amd import _lib
+    from fslr_amd.dist import chrom_counts_of, chrom_owner
+    from fslr_amd.prep import fold_overlap_threshold, pass_table
+    dirty = torch.full((1 << 28,), -1, dtype=torch.int32, device='cuda')      # 1 GiB of 0xFF bytes
+    torch.cuda.synchronize()
+    del dirty
+    torch.cuda.empty_cache()                         # back to the HIP allocator, contents kept
+    import dataclasses
+    s = synth.generate(40_000, 16, 29)
+    csr = s.interval_data().csr()
+    st = csr.iv_start.astype(np.int64) // 50             # squeezed: ~2.8M pair tests per rank > 1M slots
+    en = st + (csr.iv_end.astype(np.int64) - csr.iv_start)
+    csr = dataclasses.replace(csr, iv_start=st.astype(np.int32), iv_end=en.astype(np.int32))
+    thr = fold_overlap_threshold(csr.iv_aln, 0.8)
+    pt = pass_table([1, 1, 0.66, 0.66, 0.66, 0.5])
+    o = O.run_core(_oracle_csr(csr), use_cap=False)
+    ctxs, _ = _sweep_split_on_device(csr, thr, pt, 2)
+    got = []
+    for c in ctxs:
+        a, b, I, U = c.edges(c.stats()['n_edges'])
+        got += list(zip(a.tolist(), b.tolist(), I.tolist(), U.tolist()))
+        c.close()
+    assert sorted(got) == sorted(zip(o['edge_a'].tolist(), o['edge_b'].tolist(), o['edge_I'].tolist(),
+                                     o['edge_U'].tolist()))
