@@ -342,6 +342,11 @@ def fold_overlap_threshold(aln, overlap) -> np.ndarray:
     """
     a = np.asarray(aln, dtype=np.int64)
     p = float(overlap)
+    if a.size > (1 << 16):
+        lo, hi = int(a.min()), int(a.max())
+        if lo >= 0 and hi < (1 << 22) and hi < a.size:
+            # the fold is a function of the value: fold each value 0 .. max once, then one gather
+            return fold_overlap_threshold(np.arange(hi + 1, dtype=np.int64), p)[a]
     out = np.full(a.shape, THR_NEVER, dtype=np.int64)
     out[a == 0] = FSLR_THR_ZERO_ALN
     pos = a > 0

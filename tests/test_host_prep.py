@@ -138,3 +138,16 @@ def test_umax_table_matches_pass_table():
         for I in range(1, 65):
             ok = [U for U in range(I, 129) if pt[I - 1, U - 1]]
             assert u[I - 1] == min(max(ok) if ok else I - 1, 128)
+
+
+@pytest.mark.parametrize('overlap', [0.8, 0.0, -0.5, 1.0, 0.33, 1.5])
+def test_fold_lookup_table_path_equals_direct(overlap):
+    """Large inputs fold each distinct value once (a lookup table gathered by value); the result equals
+    the direct per-element fold, zeros included."""
+    rng = np.random.default_rng(5)
+    x = rng.integers(0, 6000, 300_000)
+    x[::97] = 0
+    big = fold_overlap_threshold(x, overlap)
+    small = np.concatenate([fold_overlap_threshold(x[i:i + 50_000], overlap) for i in range(0, x.size, 50_000)])
+    assert big.dtype == small.dtype
+    np.testing.assert_array_equal(big, small)
