@@ -305,17 +305,29 @@ def query_interval_trees(interval_trees, data, overlap_cutoff, jaccard_threshold
 
 class RawGraph:
     """query_graph's result: the graph over read ranks without qname strings (the CLI's columnar
-    path maps ranks to qname codes itself).  Edges sorted by (a, b)."""
+    path maps ranks to qname codes itself).  Edges sorted by (a, b).
 
-    def __init__(self, data, csr, labels, a, b, I, U, fwd, st):
-        self.data, self.csr, self.labels, self.fwd, self.stats = data, csr, labels, fwd, st
-        self._raw = (a, b, I, U)
+    ``a, b, I, U`` and ``fwd`` are arrays, or — from a single-GPU query — ``edges`` / ``fwd`` loaders
+    that copy them off the device on first use (the CLI needs only the labels and the edge count)."""
+
+    def __init__(self, data, csr, labels, a=None, b=None, I=None, U=None, fwd=None, st=None, *, edges=None,
+                 n_edges=None):
+        self.data, self.csr, self.labels, self.stats = data, csr, labels, st
+        self._raw = (a, b, I, U) if edges is None else edges
+        self._fwd = fwd
         self._sorted = None
-        self.n_edges = int(a.shape[0])
+        self.n_edges = int(a.shape[0]) if n_edges is None else int(n_edges)
+
+    @property
+    def fwd(self):
+        if callable(self._fwd):
+            self._fwd = self._fwd()
+        return self._fwd
 
     def _edges(self):
-        if self._sorted is None:                    # sorted on first use (the CLI needs only labels)
-            a, b, I, U = self._raw
+        if self._sorted is None:                    # fetched and sorted on first use
+            raw = self._raw() if callable(self._raw) else self._raw
+            a, b, I, U = raw
             order = np.lexsort((b, a))
             self._sorted = (a[order], b[order], I[order], U[order])
             self._raw = None
@@ -361,9 +373,15 @@ def query_graph(interval_trees, data, overlap_cutoff, jaccard_threshold, edge_th
     ctx.components()
     labels = ctx.labels()
     ne = st['n_edges']
-    a, b, I, U = ctx.edges(ne)
-    fwd = ctx.fwd_degree()
-    return RawGraph(data, csr, labels, a, b, I, U, fwd, st)
+    # the edges and forward degrees stay in HBM until asked for (query_interval_trees does at once;
+    # the CLI never does); this context's next query would replace them
+    gen = ctx.query_gen = getattr(ctx, 'query_gen', 0) + 1
+
+    def fetch(what):
+        if getattr(ctx, 'query_gen', 0) != gen:
+            raise RuntimeError('the graph\'s context has run another query since')
+        return ctx.edges(ne) if what == 'edges' else ctx.fwd_degree()
+    return RawGraph(data, csr, labels, fwd=lambda: fetch('fwd'), st=st, edges=lambda: fetch('edges'), n_edges=ne)
 
 
 def _graph_outputs(qnames_by_rank, labels, a, b, I, U, fwd, st):
