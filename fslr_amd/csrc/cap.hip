@@ -315,67 +315,131 @@ __global__ void k_cap_slots(const unsigned long long* __restrict__ key, const in
   }
 }
 
-// the full predicate of each slot's pair — one wavefront per pair: B's intervals in lanes (64 at a
-// time), A's rows broadcast; first-fit in the reference's order (rows ascending, the lowest unused
-// column, cluster.py:152-161), ZeroDivisionError where the reference meets an aln_size == 0 interval
-// (:133-136) or both reads' qlen2 / n_alignments are 0 (:178-183).  Any read length up to
-// kMaxLongL: lane l keeps bit c of `used` for column 64 c + l.  A real read's intervals are its
-// first virtual read's and, beyond FSLR_MAX_L, the consecutive chunks starting at off2.
-// flags: {zd | lenok << 1 | edge << 2, I | U << 16}
-constexpr int kMaxLongL = 64 * 64;
 
 __device__ __forceinline__ int row_at(const int4* __restrict__ rmeta, const int* __restrict__ off2, int r, int i) {
   return i < FSLR_MAX_L ? rmeta[r].x + i : off2[r] + (i - FSLR_MAX_L);
 }
 
+// one slot's first-fit on a wavefront (any lengths): B's intervals in lanes, 64 columns at a time
+__device__ __forceinline__ void eval_wave(const int4* __restrict__ rmeta, const int4* __restrict__ iv,
+                                          const int* __restrict__ off2, int a, int b, int LA, int LB, int lane,
+                                          int* I_out, bool* zd_out) {
+  const int4 bm = rmeta[b];
+  const int nb = (LB + 63) >> 6;
+  unsigned long long used = 0ull;
+  int4 b0 = make_int4(-2, 0, 0, 0);                          // the first 64 columns stay in registers
+  if (lane < LB) b0 = iv[bm.x + lane];
+  int4 ai = make_int4(-1, 0, 0, 0);
+  int I = 0;
+  bool zd = false;
+  for (int i = 0; i < LA && !zd; ++i) {
+    if ((i & 63) == 0) ai = i + lane < LA ? iv[row_at(rmeta, off2, a, i + lane)] : make_int4(-1, 0, 0, 0);
+    const int c = rdl(ai.x, i & 63), si = rdl(ai.y, i & 63), ei = rdl(ai.z, i & 63), ti = rdl(ai.w, i & 63);
+    for (int cc = 0; cc < nb; ++cc) {
+      const int jj = (cc << 6) + lane;
+      int4 bj = b0;
+      if (cc > 0) bj = jj < LB ? iv[row_at(rmeta, off2, b, jj)] : make_int4(-2, 0, 0, 0);
+      const bool cand = jj < LB && !((used >> cc) & 1ull) && bj.x == c;
+      const bool zero = cand && (ti == FSLR_THR_ZERO_ALN || bj.w == FSLR_THR_ZERO_ALN);
+      const bool hit = cand && (zero || iv_match_general(si, ei, ti, bj.y, bj.z, bj.w));
+      const unsigned long long hm = __ballot(hit);
+      if (!hm) continue;
+      const int j = __builtin_ctzll(hm);
+      if (__shfl(static_cast<int>(zero), j)) {
+        zd = true;
+        break;
+      }
+      if (lane == j) used |= 1ull << cc;
+      ++I;
+      break;
+    }
+  }
+  *I_out = I;
+  *zd_out = zd;
+}
+
+// the same first-fit by one lane, for two reads of at most kLaneL intervals: rows ascending, the
+// lowest unused column of the row's chromosome that matches (or raises)
+constexpr int kLaneL = 16;
+__device__ __forceinline__ void eval_lane(const int4* __restrict__ iv, int oa, int ob, int LA, int LB, int* I_out,
+                                          bool* zd_out) {
+  unsigned used = 0u;
+  int I = 0;
+  bool zd = false;
+  for (int i = 0; i < LA && !zd; ++i) {
+    const int4 ai = iv[oa + i];
+    for (int j = 0; j < LB; ++j) {
+      if ((used >> j) & 1u) continue;
+      const int4 bj = iv[ob + j];
+      if (bj.x != ai.x) continue;
+      if (ai.w == FSLR_THR_ZERO_ALN || bj.w == FSLR_THR_ZERO_ALN) {
+        zd = true;
+        break;
+      }
+      if (iv_match_general(ai.y, ai.z, ai.w, bj.y, bj.z, bj.w)) {
+        used |= 1u << j;
+        ++I;
+        break;
+      }
+    }
+  }
+  *I_out = I;
+  *zd_out = zd;
+}
+
+// the full predicate of each slot's pair: the length gate, first-fit in the reference's order
+// (rows ascending, the lowest unused column, cluster.py:152-161), the cut; ZeroDivisionError where
+// the reference meets an aln_size == 0 interval (:133-136) or both reads' qlen2 / n_alignments are 0
+// (:178-183).  A wavefront takes 64 consecutive slots, one per lane: pairs of two reads of at most
+// kLaneL intervals are decided by their lane; the others one after the other by the whole wavefront
+// (B's intervals in lanes, A's rows broadcast; any read length up to 4096 (long.hip checks it at
+// upload): lane l keeps bit c
+// of `used` for column 64 c + l; a real read's intervals are its first virtual read's and, beyond
+// FSLR_MAX_L, the consecutive chunks starting at off2).
+// flags: {zd | lenok << 1 | edge << 2, I | U << 16}
 __global__ __launch_bounds__(256) void k_cap_eval(const unsigned long long* __restrict__ ukey, int ns,
                                                   const int* __restrict__ T, const int4* __restrict__ rmeta,
                                                   const int4* __restrict__ iv, const int* __restrict__ rlen,
                                                   const int* __restrict__ off2, double qcut, double ncut,
                                                   const int* __restrict__ umax, int n_umax, int2* __restrict__ flags) {
   const int lane = threadIdx.x & 63;
-  const int nw = gridDim.x * (blockDim.x >> 6);
-  for (int sl = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); sl < ns; sl += nw) {
-    const unsigned long long key = ukey[sl];
-    const int x = T[key >> 25], y = static_cast<int>(key & kKeyMask);
-    const int a = min(x, y), b = max(x, y);
-    const int4 am = rmeta[a], bm = rmeta[b];
-    const int LA = read_len(rmeta, rlen, a), LB = read_len(rmeta, rlen, b);
-    bool zd = false;
-    const bool lenok = lengths_pass(am.z, bm.z, am.w, bm.w, qcut, ncut, &zd);
+  const long long nw = static_cast<long long>(gridDim.x) * (blockDim.x >> 6);
+  for (long long base = (static_cast<long long>(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64; base < ns;
+       base += nw * 64) {
+    const long long sl = base + lane;
+    const bool valid = sl < ns;
+    int a = 0, b = 0, LA = 0, LB = 0;
+    bool zd = false, lenok = false;
+    if (valid) {
+      const unsigned long long key = ukey[sl];
+      const int x = T[key >> 25], y = static_cast<int>(key & kKeyMask);
+      a = min(x, y);
+      b = max(x, y);
+      const int4 am = rmeta[a], bm = rmeta[b];
+      LA = read_len(rmeta, rlen, a);
+      LB = read_len(rmeta, rlen, b);
+      lenok = lengths_pass(am.z, bm.z, am.w, bm.w, qcut, ncut, &zd);
+    }
+    const bool need = valid && lenok && !zd;
+    const bool small = need && LA <= kLaneL && LB <= kLaneL;
     int I = 0;
-    if (lenok && !zd) {
-      const int nb = (LB + 63) >> 6;
-      unsigned long long used = 0ull;
-      int4 b0 = make_int4(-2, 0, 0, 0);                          // the first 64 columns stay in registers
-      if (lane < LB) b0 = iv[bm.x + lane];
-      int4 ai = make_int4(-1, 0, 0, 0);
-      for (int i = 0; i < LA && !zd; ++i) {
-        if ((i & 63) == 0) ai = i + lane < LA ? iv[row_at(rmeta, off2, a, i + lane)] : make_int4(-1, 0, 0, 0);
-        const int c = rdl(ai.x, i & 63), si = rdl(ai.y, i & 63), ei = rdl(ai.z, i & 63), ti = rdl(ai.w, i & 63);
-        for (int cc = 0; cc < nb; ++cc) {
-          const int jj = (cc << 6) + lane;
-          int4 bj = b0;
-          if (cc > 0) bj = jj < LB ? iv[row_at(rmeta, off2, b, jj)] : make_int4(-2, 0, 0, 0);
-          const bool cand = jj < LB && !((used >> cc) & 1ull) && bj.x == c;
-          const bool zero = cand && (ti == FSLR_THR_ZERO_ALN || bj.w == FSLR_THR_ZERO_ALN);
-          const bool hit = cand && (zero || iv_match_general(si, ei, ti, bj.y, bj.z, bj.w));
-          const unsigned long long hm = __ballot(hit);
-          if (!hm) continue;
-          const int j = __builtin_ctzll(hm);
-          if (__shfl(static_cast<int>(zero), j)) {
-            zd = true;
-            break;
-          }
-          if (lane == j) used |= 1ull << cc;
-          ++I;
-          break;
-        }
+    bool fzd = false;
+    if (small) eval_lane(iv, rmeta[a].x, rmeta[b].x, LA, LB, &I, &fzd);
+    // the larger pairs of these 64 slots: the whole wavefront, one pair after the other
+    for (unsigned long long big = __ballot(need && !small); big; big &= big - 1) {
+      const int c = __builtin_ctzll(big);
+      int Ic = 0;
+      bool zc = false;
+      eval_wave(rmeta, iv, off2, rdl(a, c), rdl(b, c), rdl(LA, c), rdl(LB, c), lane, &Ic, &zc);
+      if (lane == c) {
+        I = Ic;
+        fzd = zc;
       }
     }
+    zd = zd || fzd;
     const int U = LA + LB - I;
     const bool edge = lenok && !zd && I > 0 && I <= n_umax && U <= umax[min(max(I, 1), n_umax) - 1];
-    if (lane == 0)
+    if (valid)
       flags[sl] = make_int2(static_cast<int>(zd) | (static_cast<int>(lenok && !zd) << 1) | (static_cast<int>(edge) << 2),
                             I | (U << 16));
   }
@@ -1032,7 +1096,7 @@ int cap_slots(fslr_ctx* c, CapWork* w) {
   HIP_TRY(c, hipStreamSynchronize(s));
   const int ns = static_cast<int>(host_word(w, kHNslots));
   w->ns = ns;
-  k_cap_eval<<<wave_grid(ns), 256, 0, s>>>(w->ukey, ns, w->T, c->rmeta, c->iv, w->rlen, w->off2, c->last_qcut,
+  k_cap_eval<<<wave_grid((ns + 63) / 64), 256, 0, s>>>(w->ukey, ns, w->T, c->rmeta, c->iv, w->rlen, w->off2, c->last_qcut,
                                            c->last_ncut, w->umax, w->n_umax, w->flags);
   HIP_TRY(c, hipGetLastError());
   return FSLR_OK;
