@@ -561,7 +561,13 @@ static int sweep_front(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64
   s.ent_cap = c->ent_cap;
   for (int k = 0; k < 5; ++k) s.ev[k] = c->prof_phases ? c->sw_ev[k] : nullptr;
   s.ev[0] = nullptr;                                // recorded here, around the sweep pass
-  HIP_TRY(c, launch_len_bounds(c->rmeta, 0, static_cast<int>(c->n), p->qlen_cut, p->nal_cut, c->lbounds, c->stream));
+  // the gate ranges depend on the reads and the two cuts only: a repeat query keeps them
+  if (c->lb_gen != c->input_gen || c->lb_q != p->qlen_cut || c->lb_n != p->nal_cut) {
+    HIP_TRY(c, launch_len_bounds(c->rmeta, 0, static_cast<int>(c->n), p->qlen_cut, p->nal_cut, c->lbounds, c->stream));
+    c->lb_gen = c->input_gen;
+    c->lb_q = p->qlen_cut;
+    c->lb_n = p->nal_cut;
+  }
   mode = 2;
   for (int attempt = 0; attempt < 3; ++attempt) {
     s.ent = c->ent;
@@ -705,6 +711,7 @@ static int query_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_
   g.defer_cap = c->defer_cap;
   g.umax = c->umax;
   g.lb = c->lbounds;
+  c->lb_gen = -1;                                    // the walk engine writes its own range of lbounds
   g.qlen_cut = p->qlen_cut;
   g.nal_cut = p->nal_cut;
   g.a_begin = static_cast<int>(a_begin);

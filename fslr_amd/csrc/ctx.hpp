@@ -63,6 +63,8 @@ struct fslr_ctx {
   size_t temp_bytes = 0;
   int* umax = nullptr;     // [FSLR_MAX_L] derived from the pass table
   int4* lbounds = nullptr; // [N] per query read: exact integer ranges of the length gate
+  int64_t lb_gen = -1;     // lbounds hold every read's ranges for this input generation and cuts
+  double lb_q = 0.0, lb_n = 0.0;
   int2* edges = nullptr;
   unsigned short* edge_iu = nullptr;
   int64_t edge_cap = 0;
