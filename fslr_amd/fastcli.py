@@ -23,8 +23,8 @@ from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
-from . import cluster, ingest, multi
-from .prep import IntervalData, data_order, first_last_masks, mask_keep
+from . import cluster, ingest
+from .prep import IntervalData, data_order, mask_keep
 
 INT_COLS = ('rstart', 'rend', 'n_alignments', 'aln_size', 'qstart', 'qend', 'alignment_score')
 STR_COLS = ('qname', 'chrom')
@@ -246,4 +246,4 @@ class _LazyQnames:
         return self._u[k]
 
 
-__all__ = ['run', 'Fallback', 'chrom_map', 'multi']
+__all__ = ['run', 'Fallback', 'chrom_map']
