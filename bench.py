@@ -172,9 +172,9 @@ def main():
         # the match entries to the first read's owner (RCCL all_to_all), evaluates, merges labels
         shard = SweepShard(ctx, csr.n_reads, chrom_counts_of(csr), world, rank, dev)
 
-    def step(collect=False):
+    def step(collect=False, repeat=False):
         if shard is not None:
-            return shard.step(qcut, ncut, pt, 10, collect=collect)
+            return shard.step(qcut, ncut, pt, 10, collect=collect, repeat=repeat)
         ctx.build_index()
         ctx.query(qcut, ncut, pt, 10, engine=args.engine)
         ctx.components()
@@ -211,11 +211,15 @@ def main():
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        step(repeat=True)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
+    if shard is not None:
+        # the timed steps repeated the last warmup step without host syncs (SweepShard.step repeat):
+        # every rank's device checks and edge counts must agree with it
+        shard.verify_repeat()
     st = ctx.stats()
     kern = ctx.pair_kernel_times(args.steps)       # the timed steps' main pair-kernel launches
     kern2 = ctx.stage_kernel_times(1, args.steps) if st['engine'] == 'sweep' else np.zeros(0)   # pair stage

@@ -13,7 +13,7 @@ import numpy as np
 
 LIB_PATH = os.environ.get('FSLR_LIB') or os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libfslr_hip.so')
 
-ABI_VERSION = 8          # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
+ABI_VERSION = 9          # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
 FSLR_OK, FSLR_ERR_ZERO_DIVISION, FSLR_ERR_INVALID, FSLR_ERR_HIP, FSLR_ERR_NOMEM, FSLR_ERR_STATE = range(6)
 FSLR_MAX_L = 64
 FSLR_MAX_READS = 1 << 25
@@ -32,6 +32,7 @@ EXPORTED = ['fslr_abi_version', 'fslr_last_error', 'fslr_ctx_create', 'fslr_ctx_
             'fslr_get_fwd_degree', 'fslr_get_edges', 'fslr_labels_device_ptr', 'fslr_copy_labels_device',
             'fslr_copy_fwd_device', 'fslr_union_pairs', 'fslr_finalize_labels', 'fslr_apply_edge_cap',
             'fslr_get_pair_kernel_times', 'fslr_set_chrom_filter', 'fslr_sweep_partition', 'fslr_sweep_evaluate',
+            'fslr_sweep_partition_repeat',
             'fslr_copy_edges_device', 'fslr_components_from_pairs', 'fslr_set_long_reads', 'fslr_long_query',
             'fslr_get_long_edges', 'fslr_copy_edges_iu_device', 'fslr_cap_install_edges', 'fslr_cap_local',
             'fslr_cap_copy_local', 'fslr_cap_replay', 'fslr_get_stage_kernel_times', 'fslr_long_pairs',
@@ -138,6 +139,7 @@ def load(path: str = LIB_PATH):
         'fslr_set_chrom_filter': (ctypes.c_int, [vp, vp]),
         'fslr_sweep_partition': (ctypes.c_int, [vp, ctypes.POINTER(Params), i32, i32, vp, i64,
                                                 ctypes.POINTER(ctypes.c_int64)]),
+        'fslr_sweep_partition_repeat': (ctypes.c_int, [vp, ctypes.POINTER(Params), i32, i32, vp, i64]),
         'fslr_sweep_evaluate': (ctypes.c_int, [vp, ctypes.POINTER(Params), vp, i64]),
         'fslr_copy_edges_device': (ctypes.c_int, [vp, vp, i64]),
         'fslr_components_from_pairs': (ctypes.c_int, [vp, vp, i64]),
@@ -296,6 +298,14 @@ class Context:
             return False, counts
         self._check(rc)
         return True, counts
+
+    def sweep_partition_repeat(self, qlen_cut, nal_cut, pass_table, n_dest, block_shift, dst, edge_threshold=10):
+        """sweep_partition again on unchanged input, parameters and split, without the readback: the
+        entries land where the last synchronous call put them (async).  A difference is flagged on
+        the device and raised by the next stats() (fslr_sweep_partition_repeat)."""
+        p = self._params(qlen_cut, nal_cut, pass_table, edge_threshold)
+        self._check(self._L.fslr_sweep_partition_repeat(self._h, ctypes.byref(p), int(n_dest), int(block_shift),
+                                                        ctypes.c_void_p(dst.data_ptr()), int(dst.numel())))
 
     def sweep_evaluate(self, qlen_cut, nal_cut, pass_table, entries, n, edge_threshold=10):
         """Evaluate the pairs of the first ``n`` entries of the int64 device tensor ``entries`` (async)."""

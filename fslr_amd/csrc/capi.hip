@@ -437,9 +437,18 @@ int fslr::peek_counts(fslr_ctx* c, long long out[3]) {
   return FSLR_OK;
 }
 
+// a lean index (fslr_build_index for the sweep) gets its (chrom, end) keys and data -> sorted map
+static int ensure_keys(fslr_ctx* c) {
+  if (!c->index_lean) return FSLR_OK;
+  HIP_TRY(c, launch_index_rescatter(index_bufs(c), static_cast<int>(c->ni_idx), c->built_n_chroms, c->stream));
+  c->index_lean = false;
+  return FSLR_OK;
+}
+
 int fslr::ensure_bwd_ranges(fslr_ctx* c) {
   if (!c->index_built) return fail(c, FSLR_ERR_STATE, "fslr_build_index first");
   if (c->index_full || c->bwd_ranges) return FSLR_OK;
+  if (int rc = ensure_keys(c)) return rc;
   HIP_TRY(c, launch_index_bwd_ranges(index_bufs(c), static_cast<int>(c->ni_idx), c->stream));
   c->bwd_ranges = true;
   return FSLR_OK;
@@ -448,6 +457,7 @@ int fslr::ensure_bwd_ranges(fslr_ctx* c) {
 int fslr::ensure_walk_index(fslr_ctx* c) {
   if (!c->index_built || c->index_full) return FSLR_OK;
   if (c->filter_active) return fail(c, FSLR_ERR_STATE, "the walk engine needs every chromosome's index");
+  if (int rc = ensure_keys(c)) return rc;
   HIP_TRY(c, launch_index_walk_parts(index_bufs(c), static_cast<int>(c->n), static_cast<int>(c->ni), c->stream));
   c->index_full = true;
   return FSLR_OK;
@@ -463,8 +473,11 @@ int fslr_build_index(fslr_ctx* c) {
   // the sweep engine's index only (the walk engine's parts follow on demand, ensure_walk_index)
   // where the data-order path applies and one context covers every query read
   const bool full = !c->filter_active && !(c->have_data_pos && c->n_chroms <= 64 && c->n_shards == 1);
-  HIP_TRY(c, launch_build_index(index_bufs(c), static_cast<int>(c->n), static_cast<int>(c->ni_idx),
-                                c->filter_active ? c->n_chroms_f : c->n_chroms, full, c->stream));
+  const int nch = c->filter_active ? c->n_chroms_f : c->n_chroms;
+  HIP_TRY(c, launch_build_index(index_bufs(c), static_cast<int>(c->n), static_cast<int>(c->ni_idx), nch, full,
+                                c->stream));
+  c->index_lean = !full && index_bufs(c).dchrom && nch <= 64;
+  c->built_n_chroms = nch;
   if (c->prof_phases) HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));
   c->t_index_rec = c->prof_phases;
   c->index_built = true;
@@ -866,7 +879,57 @@ int fslr_sweep_partition(fslr_ctx* c, const fslr_params* p, int32_t n_dest, int3
   }
   int64_t sum = 0;
   for (int k = 0; k < n_dest; ++k) sum += (counts[k] = tot[k]);
+  c->pt_gen = 0;
   if (sum > dst_cap) return fail(c, FSLR_ERR_STATE, "destination buffer too small for the entries (see counts)");
+  if (ew[kErrOverflow] == 0) {                      // clean: a repeat may replay this partition
+    c->pt_gen = c->input_gen;
+    c->pt_q = p->qlen_cut;
+    c->pt_nc = p->nal_cut;
+    c->pt_umax = c->umax_host;
+    c->pt_ndest = n_dest;
+    c->pt_shift = block_shift;
+    c->pt_sum = sum;
+    c->pt_counts.assign(tot, tot + n_dest);
+  }
+  return FSLR_OK;
+}
+
+// a repeat partition's destination totals against the last synchronous one's: a difference flags
+// the query (overflow_flags 32), whose results are then refused by fslr_read_stats
+struct PartExpect {
+  long long n[kMaxDest];
+};
+__global__ void k_part_check(const long long* __restrict__ totals, PartExpect expect, int n_dest, int* err) {
+  const int k = threadIdx.x;
+  if (k < n_dest && totals[k] != expect.n[k]) atomicOr(&err[kErrOverflow], 32);
+}
+
+int fslr_sweep_partition_repeat(fslr_ctx* c, const fslr_params* p, int32_t n_dest, int32_t block_shift, void* dst,
+                                int64_t dst_cap) {
+  if (!c || !p || !p->pass_table || n_dest < 1 || n_dest > kMaxDest || !dst) return FSLR_ERR_INVALID;
+  if (!c->index_built) return fail(c, FSLR_ERR_STATE, "fslr_build_index first");
+  if (int rc = prepare_query(c, p)) return rc;           // folds the cut table into umax_host
+  if (c->pt_gen != c->input_gen || c->pt_q != p->qlen_cut || c->pt_nc != p->nal_cut || c->pt_umax != c->umax_host ||
+      c->pt_ndest != n_dest || c->pt_shift != block_shift || c->pt_sum > dst_cap)
+    return fail(c, FSLR_ERR_STATE, "no synchronous fslr_sweep_partition of this input, parameters and split");
+  c->last_full = false;
+  c->last_engine = FSLR_ENGINE_SWEEP;
+  hipEvent_t k0 = nullptr, k1 = nullptr;
+  if (c->profiling && c->n > 0) {
+    const int slot = static_cast<int>(c->n_kern++ % fslr_ctx::kKernRing);
+    k0 = c->kev[2 * slot];
+    k1 = c->kev[2 * slot + 1];
+  }
+  SweepArgs s;
+  int mode = 2;
+  if (int rc = sweep_front(c, p, 0, c->n, k0, k1, s, mode, true)) return rc;
+  HIP_TRY(c, launch_sweep_partition(s, 2, block_shift, n_dest, static_cast<unsigned long long*>(dst), dst_cap,
+                                    c->part_cnt, c->stream));
+  PartExpect ex{};
+  for (int k = 0; k < n_dest; ++k) ex.n[k] = c->pt_counts[k];
+  k_part_check<<<1, kMaxDest, 0, c->stream>>>(c->part_cnt, ex, n_dest, c->errw);
+  HIP_TRY(c, hipGetLastError());
+  c->t_kernel_rec = k0 != nullptr;
   return FSLR_OK;
 }
 
@@ -1005,6 +1068,10 @@ int fslr_read_stats(fslr_ctx* c, fslr_query_stats* out) {
   if (ew[kErrOverflow] & 24) {                       // a sync-free repeat query did not fit: rerun (with a sync)
     c->sw_prev_gen = 0;
     return fail(c, FSLR_ERR_STATE, "sweep entry buffers overflowed; rerun the query");
+  }
+  if (ew[kErrOverflow] & 32) {                       // a repeat partition differed from the synchronous one
+    c->pt_gen = 0;
+    return fail(c, FSLR_ERR_STATE, "repeat partition differs from the last synchronous one; rerun it synchronously");
   }
   return FSLR_OK;
 }

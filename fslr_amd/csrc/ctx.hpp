@@ -19,6 +19,8 @@ struct fslr_ctx {
   bool reads_set = false, index_built = false, have_data_pos = false;
   bool index_full = false;                 // the walk engine's index parts exist (qpos, backward ranges)
   bool bwd_ranges = false;                 // backward scan ranges exist (the cap replay's hits; no qpos)
+  bool index_lean = false;                 // lean scatter (no (chrom, end) keys, no data -> sorted map)
+  int built_n_chroms = 0;                  // chromosomes of the built index (filtered: the owned ones)
   // multi-GPU sweep: the index covers the chromosomes of a filter (fslr_set_chrom_filter)
   bool filter_active = false;
   int n_chroms_f = 0;                       // chromosomes the filter keeps (numbered 0 .. n_chroms_f - 1)
@@ -34,6 +36,13 @@ struct fslr_ctx {
   int64_t crange_f_cap = 0;
   int* grp = nullptr;                       // [grp_ints()] grouping sort: bucket counts / offsets
   long long* part_cnt = nullptr;            // partition scratch: per (destination, block) counts + offsets
+  // the last synchronous fslr_sweep_partition (fslr_sweep_partition_repeat replays it without a readback)
+  uint64_t pt_gen = 0;
+  double pt_q = 0, pt_nc = 0;
+  std::vector<int> pt_umax;
+  int pt_ndest = 0, pt_shift = 0;
+  int64_t pt_sum = 0;
+  std::vector<long long> pt_counts;
   int shard = 0, n_shards = 1;             // fslr_set_shard: A-side index data for this shard only
   int built_shard = 0, built_n_shards = 1;
   // device buffers

@@ -97,7 +97,7 @@ __global__ __launch_bounds__(kTile) void k_finish(const int4* __restrict__ idx4,
 }
 
 // ---- fused data-order path (n_chroms <= 64) --------------------------------------------------
-// A stable counting sort on the chromosome, one block per tile of kChromTile data positions.
+// A stable counting sort on the chromosome, one block per tile of rounds x 1024 data positions.
 // Within a round of 64 lanes, six ballots of the chromosome bits give every lane the mask of lanes
 // sharing its chromosome (its rank among them) and lane l the count of chromosome l.
 //   k_chrom_count    counts per (chromosome, tile)                      reads 4 B / interval
@@ -109,7 +109,20 @@ __global__ __launch_bounds__(kTile) void k_finish(const int4* __restrict__ idx4,
 // same (chrom, start) order, ties included, as the radix pass it replaces.
 constexpr int kTileThreads = 1024;
 constexpr int kTileWaves = kTileThreads / 64;
-constexpr int kChromTile = 16 * kTileThreads;     // data positions per block tile
+// a block tile is `rounds` rounds of kTileThreads data positions, sized so the grid fits the chip in
+// one pass (two 16-wave blocks per CU): 519 tiles of 16 rounds at cfg3 left 7 blocks for a second pass
+int chrom_rounds(int ni) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                hipSuccess || cus < 1)
+      cus = 256;
+  }
+  const long long subs = (static_cast<long long>(ni) + kTileThreads - 1) / kTileThreads;
+  const long long slots = 2ll * cus;
+  return static_cast<int>(std::max(4ll, (subs + slots - 1) / slots));
+}
 constexpr int kChromBits = 6;
 constexpr int kMaxFusedChroms = 1 << kChromBits;
 
@@ -118,14 +131,14 @@ __device__ __forceinline__ unsigned long long lane_mask_lt() {
 }
 
 __global__ __launch_bounds__(kTileThreads) void k_chrom_count(const unsigned* __restrict__ dchrom, int ni,
-                                                              int ntl, int* __restrict__ chist) {
+                                                              int ntl, int rounds, int* __restrict__ chist) {
   __shared__ int wc[kTileWaves][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int tl = blockIdx.x;
-  const int e0 = tl * kChromTile;
+  const int e0 = tl * rounds * kTileThreads;
   int cnt = 0;
 #pragma unroll 4
-  for (int r = 0; r < kChromTile / kTileThreads; ++r) {
+  for (int r = 0; r < rounds; ++r) {
     const int e = e0 + r * kTileThreads + threadIdx.x;
     const unsigned c = e < ni ? dchrom[e] : 0u;
     unsigned long long m = __ballot(e < ni);
@@ -169,18 +182,21 @@ __global__ __launch_bounds__(1024) void k_chrom_scan(int* __restrict__ chist, in
   }
 }
 
-// One block of 16 waves per tile of kChromTile data positions, 16 rounds of 1024 in data order.
+// One block of 16 waves per tile of `rounds` x 1024 data positions, rounds of 1024 in data order.
 // Per round each wave ranks its lanes within their chromosome (ballots), the waves' per-chromosome
 // counts are prefixed in LDS, and every element lands at q = run[c] + (earlier waves' count of c)
 // + rank.  A chromosome's run in a tile (~700 positions at 23 chromosomes) is written by one block,
 // so its cache lines fill up in one L2; with 1024-position tiles per wave the runs were ~45 long,
 // most lines were shared by waves on different XCDs and the stores cost 155 of 215 us.
 // qd[e] = q is written in data order for the CSR -> sorted position gather.
+// kFull = false (the sweep engine's lean index): the (chrom, end) key and the data -> sorted map are
+// not written, only each position's end (s_end, in the endkey buffer): 56 instead of 68 B / interval
+template <bool kFull>
 __global__ __launch_bounds__(kTileThreads) void k_chrom_scatter(const unsigned* __restrict__ dchrom,
                                                               const int4* __restrict__ drec,
                                                               const int2* __restrict__ dgate,
                                                               const int* __restrict__ chist, int ni, int ntl,
-                                                              int4* __restrict__ idx4, int2* __restrict__ idx_gate,
+                                                              int rounds, int4* __restrict__ idx4, int2* __restrict__ idx_gate,
                                                               int* __restrict__ s_start,
                                                               unsigned long long* __restrict__ endkey,
                                                               int* __restrict__ qd) {
@@ -189,7 +205,7 @@ __global__ __launch_bounds__(kTileThreads) void k_chrom_scatter(const unsigned* 
   __shared__ int runs[2][64];             // next sorted position of chromosome l (double buffered)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int tl = blockIdx.x;
-  const int e0 = tl * kChromTile;
+  const int e0 = tl * rounds * kTileThreads;
   const unsigned long long lt = lane_mask_lt();
   if (threadIdx.x < 64) runs[0][threadIdx.x] = chist[threadIdx.x * ntl + tl];
   auto load = [&](int r, unsigned& c, int4& rec, int2& gate) {
@@ -207,13 +223,13 @@ __global__ __launch_bounds__(kTileThreads) void k_chrom_scatter(const unsigned* 
   int4 rec_n;
   int2 gate_n;
   load(0, c_n, rec_n, gate_n);
-  for (int r = 0; r < kChromTile / kTileThreads; ++r) {
+  for (int r = 0; r < rounds; ++r) {
     const unsigned c = c_n;
     const int4 rec = rec_n;
     const int2 gate = gate_n;
     const int e = e0 + r * kTileThreads + threadIdx.x;
     const bool valid = e < ni;
-    if (r + 1 < kChromTile / kTileThreads) load(r + 1, c_n, rec_n, gate_n);
+    if (r + 1 < rounds) load(r + 1, c_n, rec_n, gate_n);
     const unsigned long long v = __ballot(valid);
     unsigned long long mine = v, mylane = v;
 #pragma unroll
@@ -237,8 +253,12 @@ __global__ __launch_bounds__(kTileThreads) void k_chrom_scatter(const unsigned* 
       idx4[q] = rec;
       idx_gate[q] = gate;
       s_start[q] = rec.x;
-      endkey[q] = (static_cast<unsigned long long>(c) << 32) | static_cast<unsigned>(rec.y);
-      qd[e] = q;
+      if constexpr (kFull) {
+        endkey[q] = (static_cast<unsigned long long>(c) << 32) | static_cast<unsigned>(rec.y);
+        qd[e] = q;
+      } else {
+        reinterpret_cast<int*>(endkey)[q] = rec.y;
+      }
     }
   }
 }
@@ -345,18 +365,22 @@ struct TilePrefix {
   __device__ __forceinline__ unsigned long long incl(int t) const { return max_u64(group_excl[t / kGroup], loc[t]); }
 };
 
-// kBwd = false (the sweep engine): forward counts only, no pmax window (rng_s[q].y = -1)
+// kBwd = false (the sweep engine, lean index): forward counts only, no pmax window (rng_s[q].y = -1);
+// ends from the s_end column (endkey's buffer), the chromosome from its begin in crange (n_chroms <= 64)
 template <bool kBwd>
 __global__ __launch_bounds__(kRangeBlock) void k_ranges(const int4* __restrict__ idx4, int shard, int n_shards,
                                                         const int* __restrict__ s_start,
                                                         const unsigned long long* __restrict__ endkey,
                                                         TilePrefix tile_incl,
                                                         const int2* __restrict__ crange, int ni,
-                                                        int2* __restrict__ rng_s) {
+                                                        int2* __restrict__ rng_s, int n_chroms = 0) {
   __shared__ int w_st[kRangeSpan + 2 * kWin];    // starts of [w0, w1)
-  __shared__ int w_pm[kRangeSpan + kWin];        // pmax (end part) of [w0, q0 + kRangeSpan)
-  __shared__ unsigned long long t_part[kRangeBlock];
+  __shared__ int w_pm[kBwd ? kRangeSpan + kWin : 1];   // pmax (end part) of [w0, q0 + kRangeSpan)
+  __shared__ unsigned long long t_part[kBwd ? kRangeBlock : 1];
+  __shared__ int c_beg[kBwd ? 1 : 64];
   const int q0 = blockIdx.x * kRangeSpan;
+  if constexpr (!kBwd)
+    if (threadIdx.x < 64) c_beg[threadIdx.x] = threadIdx.x < n_chroms ? crange[threadIdx.x].x : 0x7FFFFFFF;
   const int w0 = max(q0 - kWin, 0);              // tile-aligned
   const int w1 = min(q0 + kRangeSpan + kWin, ni);
   const int wp1 = min(q0 + kRangeSpan, ni);
@@ -389,10 +413,20 @@ __global__ __launch_bounds__(kRangeBlock) void k_ranges(const int4* __restrict__
   __syncthreads();
   for (int q = q0 + threadIdx.x; q < wp1; q += kRangeBlock) {
     if (n_shards > 1 && !shard_owns(idx4[q].w >> 6, shard, n_shards)) continue;   // another shard's A side
-    const unsigned long long ek = endkey[q];
-    const int c = static_cast<int>(ek >> 32);
+    int c, e;
+    if constexpr (kBwd) {
+      const unsigned long long ek = endkey[q];
+      c = static_cast<int>(ek >> 32);
+      e = static_cast<int>(static_cast<unsigned>(ek));
+    } else {
+      e = reinterpret_cast<const int*>(endkey)[q];
+      c = 0;                                     // the last chromosome beginning at or before q
+#pragma unroll
+      for (int b = 32; b > 0; b >>= 1)
+        if (c + b < 64 && c_beg[c + b] <= q) c += b;
+    }
     const int2 cr = crange[c];
-    const int s = w_st[q - w0], e = static_cast<int>(static_cast<unsigned>(ek));
+    const int s = w_st[q - w0];
     // forward: first p in (q, cr.y) with start_p > e
     const int hi_lim = min(cr.y, w1);
     int lo = q + 1, hi = hi_lim;
@@ -522,17 +556,21 @@ hipError_t launch_build_index(const IndexBufs& b, int n, int ni, int n_chroms, b
   hipError_t e;
   size_t tb = b.temp_bytes;
   if (b.dchrom && n_chroms <= kMaxFusedChroms) {
-    const int ntl = (ni + kChromTile - 1) / kChromTile;
-    k_chrom_count<<<ntl, kTileThreads, 0, s>>>(b.dchrom, ni, ntl, b.chist);
+    const int rounds = chrom_rounds(ni);
+    const int ntl = static_cast<int>((static_cast<long long>(ni) + rounds * kTileThreads - 1) / (rounds * kTileThreads));
+    k_chrom_count<<<ntl, kTileThreads, 0, s>>>(b.dchrom, ni, ntl, rounds, b.chist);
     k_chrom_scan<<<n_chroms, 1024, 0, s>>>(b.chist, ntl, b.crange);
-    k_chrom_scatter<<<ntl, kTileThreads, 0, s>>>(b.dchrom, b.drec, b.dgate, b.chist, ni, ntl, b.idx4, b.idx_gate,
-                                                 b.s_start, b.endkey, b.vals);
     if (!full) {
-      // the sweep engine's index: records, gate words and forward counts
+      // the sweep engine's lean index: records, gate words, starts and ends, forward counts
+      k_chrom_scatter<false><<<ntl, kTileThreads, 0, s>>>(b.dchrom, b.drec, b.dgate, b.chist, ni, ntl, rounds, b.idx4,
+                                                          b.idx_gate, b.s_start, b.endkey, b.vals);
       k_ranges<false><<<(ni + kRangeSpan - 1) / kRangeSpan, kRangeBlock, 0, s>>>(
-          b.idx4, b.shard, b.n_shards, b.s_start, b.endkey, TilePrefix{nullptr, nullptr}, b.crange, ni, b.rng_s);
+          b.idx4, b.shard, b.n_shards, b.s_start, b.endkey, TilePrefix{nullptr, nullptr}, b.crange, ni, b.rng_s,
+          n_chroms);
       return hipGetLastError();
     }
+    k_chrom_scatter<true><<<ntl, kTileThreads, 0, s>>>(b.dchrom, b.drec, b.dgate, b.chist, ni, ntl, rounds, b.idx4, b.idx_gate,
+                                                       b.s_start, b.endkey, b.vals);
     return launch_walk_parts(b, n, ni, s, true);
   } else if (b.dchrom) {
     unsigned* k32 = reinterpret_cast<unsigned*>(b.keys2);
@@ -550,6 +588,18 @@ hipError_t launch_build_index(const IndexBufs& b, int n, int ni, int n_chroms, b
                                                          b.pmaxkey, b.qpos, b.shard, b.n_shards);
   }
   return launch_walk_parts(b, n, ni, s, false);
+}
+
+hipError_t launch_index_rescatter(const IndexBufs& b, int ni, int n_chroms, hipStream_t s) {
+  if (ni <= 0) return hipSuccess;
+  if (!b.dchrom || n_chroms > kMaxFusedChroms) return hipErrorInvalidValue;
+  const int rounds = chrom_rounds(ni);
+  const int ntl = static_cast<int>((static_cast<long long>(ni) + rounds * kTileThreads - 1) / (rounds * kTileThreads));
+  k_chrom_count<<<ntl, kTileThreads, 0, s>>>(b.dchrom, ni, ntl, rounds, b.chist);
+  k_chrom_scan<<<n_chroms, 1024, 0, s>>>(b.chist, ntl, b.crange);
+  k_chrom_scatter<true><<<ntl, kTileThreads, 0, s>>>(b.dchrom, b.drec, b.dgate, b.chist, ni, ntl, rounds, b.idx4, b.idx_gate,
+                                                     b.s_start, b.endkey, b.vals);
+  return hipGetLastError();
 }
 
 hipError_t launch_set_thr(const int* thr, int4* iv, const int* qpos, int4* idx4, const int* data_pos,

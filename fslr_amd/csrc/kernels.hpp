@@ -105,6 +105,9 @@ hipError_t index_temp_bytes(int ni, size_t* bytes, hipStream_t s);
 // full = false: only what the sweep engine reads (records, gate words, forward counts); applies to
 // the data-order path with <= 64 chromosomes (the other paths always build everything)
 hipError_t launch_build_index(const IndexBufs& b, int n_reads, int ni, int n_chroms, bool full, hipStream_t s);
+// a lean (sweep-only) index's full scatter again: the (chrom, end) keys and the data -> sorted map the
+// walk parts and the backward ranges read (same records, same order)
+hipError_t launch_index_rescatter(const IndexBufs& b, int ni, int n_chroms, hipStream_t s);
 // the walk engine's parts of a sweep-only index (qpos, tile prefix, backward ranges)
 hipError_t launch_index_walk_parts(const IndexBufs& b, int n_reads, int ni, hipStream_t s);
 // the backward scan ranges alone (tile prefix of end + k_ranges<true>): no CSR map, so it also

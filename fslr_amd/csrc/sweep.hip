@@ -91,6 +91,8 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
   // rank's share of the multi-GPU split), so every wave gets work: the sweep is latency bound
   const int run = max(1, min(kTileRun, nt / nw));
   const int nchunks = (nt + run - 1) / run;
+  // chunks dealt grid-stride (per-XCD work queues were tried: 0.241 -> 0.260 ms at cfg3, the
+  // tickets' latency and the lost neighbour order cost more than the balance gained)
   for (int chunk = wid; chunk < nchunks; chunk += nw)
   for (int tile = chunk * run; tile < min(nt, (chunk + 1) * run); ++tile) {
     const int q0 = tile * kWave;
@@ -275,6 +277,53 @@ __global__ void k_total(const long long* __restrict__ off, const long long* __re
       if (t > cap) atomicOr(&err[kErrOverflow], 16);
     }
     total[2] = err ? err[kErrOverflow] : 0;
+  }
+}
+
+// one-pass sweep (kMode 2): the per-wave statistics summed into the counters (tests, hits, entries),
+// the entry total and upper-bound total for the host, the clamped count for a sync-free query —
+// one block in place of k_sum_slots, a scan of the tile counts and k_total
+__global__ __launch_bounds__(1024) void k_sweep_total(const unsigned long long* __restrict__ ws, int nwaves,
+                                                      const long long* __restrict__ ub,
+                                                      const long long* __restrict__ tests, int nt,
+                                                      unsigned long long* counters, int* err, long long* total,
+                                                      long long* n_dev, long long cap) {
+  __shared__ unsigned long long part[16][3];
+  unsigned long long a0 = 0, a1 = 0, a2 = 0;
+  for (int w = threadIdx.x; w < nwaves; w += 1024) {
+    a0 += ws[static_cast<long long>(w) * kWsFields];
+    a1 += ws[static_cast<long long>(w) * kWsFields + 1];
+    a2 += ws[static_cast<long long>(w) * kWsFields + 2];
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    a0 += __shfl_xor(a0, o);
+    a1 += __shfl_xor(a1, o);
+    a2 += __shfl_xor(a2, o);
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+    part[w][0] = a0;
+    part[w][1] = a1;
+    part[w][2] = a2;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < 16; ++k) {
+      a0 += part[k][0];
+      a1 += part[k][1];
+      a2 += part[k][2];
+    }
+    counters[kSwTests] += a0;
+    counters[kCand] += a1;
+    counters[kMatchEntries] += a2;
+    const long long t = static_cast<long long>(a2);
+    total[0] = t;
+    total[1] = ub[nt - 1] + tests[nt - 1];
+    if (n_dev) {
+      n_dev[0] = t < cap ? t : cap;
+      if (t > cap) atomicOr(&err[kErrOverflow], 16);
+    }
+    total[2] = err[kErrOverflow];
   }
 }
 
@@ -1045,6 +1094,12 @@ hipError_t launch_sweep_count(const SweepArgs& a, int mode, long long* total_dev
   else
     k_sweep<0><<<blocks, kSwBlock, 0, s>>>(a);
   if (a.k1) (void)hipEventRecord(a.k1, s);
+  if (mode == 2) {
+    k_sweep_total<<<1, 1024, 0, s>>>(a.wstat, blocks * kSwWaves, a.tile_ub, a.tile_tests, nt, a.counters, a.err,
+                                     total_dev, n_dev, cap);
+    if (a.ev[1]) (void)hipEventRecord(a.ev[1], s);
+    return hipGetLastError();
+  }
   k_sum_slots<<<kSumBlocks, 256, 0, s>>>(a.wstat, blocks * kSwWaves, 0, 3, kSwTests, kCand, kMatchEntries,
                                          a.counters, nullptr);
   if (a.ev[1]) (void)hipEventRecord(a.ev[1], s);
@@ -1060,6 +1115,10 @@ hipError_t launch_sweep_dense(const SweepArgs& a, int mode, hipStream_t s) {
   const int nt = tiles_of(a);
   if (a.n_ent <= 0 || nt == 0) return hipSuccess;
   if (mode == 2) {
+    // the tiles' places in `ent` (the one-pass sweep does not scan its tile counts)
+    size_t tb = a.temp_bytes;
+    hipError_t e = hipcub::DeviceScan::ExclusiveSum(a.temp, tb, a.tile_cnt, a.tile_off, nt, s);
+    if (e != hipSuccess) return e;
     k_compact<<<grid_for(static_cast<long long>(nt) * kWave, 256, 8192), 256, 0, s>>>(a.ent_ub, a.tile_ub, a.tile_off,
                                                                                     a.tile_cnt, nt, a.ent);
   } else {

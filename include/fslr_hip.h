@@ -68,7 +68,7 @@
 extern "C" {
 #endif
 
-#define FSLR_ABI_VERSION 8
+#define FSLR_ABI_VERSION 9
 #define FSLR_MAX_L 64                /* max intervals per read (bitmask width) */
 #define FSLR_MAX_READS (1 << 25)     /* read rank packs into bits 6..30 of the index record */
 #define FSLR_THR_ZERO_ALN INT32_MIN
@@ -265,6 +265,14 @@ int  fslr_cap_replay(fslr_ctx *ctx, const int32_t *counts, const int32_t *hits, 
 int  fslr_sweep_partition(fslr_ctx *ctx, const fslr_params *params, int32_t n_dest, int32_t block_shift,
                           void *dst, int64_t dst_cap, int64_t *counts);
 int  fslr_sweep_evaluate(fslr_ctx *ctx, const fslr_params *params, const void *entries, int64_t n);
+/* fslr_sweep_partition_repeat: fslr_sweep_partition again on unchanged input (no fslr_set_* since),
+ * parameters and split, without the readback: the entries land where the last synchronous call put
+ * them (its counts), and a device check flags any difference (fslr_read_stats then returns
+ * FSLR_ERR_STATE with overflow_flags & 32: rerun synchronously).  Async.  FSLR_ERR_STATE when the last
+ * synchronous call was for another input, parameters or split.  The repeated steps of a benchmark
+ * or of a service querying one resident input use it. */
+int  fslr_sweep_partition_repeat(fslr_ctx *ctx, const fslr_params *params, int32_t n_dest, int32_t block_shift,
+                                 void *dst, int64_t dst_cap);
 
 /* Reads of more than FSLR_MAX_L intervals.  The caller uploads a *virtual* CSR with
  * fslr_set_reads: virtual read v < n_real is real read v (its first <= FSLR_MAX_L intervals), reads

@@ -94,6 +94,11 @@ class EmuSweepContext:
         self._st = {'match_entries': int(ent.size)}
         return True, counts
 
+    def sweep_partition_repeat(self, qlen_cut, nal_cut, pass_table, n_dest, block_shift, dst, edge_threshold=10):
+        ok, counts = self.sweep_partition(qlen_cut, nal_cut, pass_table, n_dest, block_shift, dst, edge_threshold)
+        assert ok, 'a repeat partition must fit where the synchronous one did'
+        self.repeat_partitions = getattr(self, 'repeat_partitions', 0) + 1
+
     # -- evaluation -----------------------------------------------------------------------------
     def sweep_evaluate(self, qlen_cut, nal_cut, pass_table, entries, n, edge_threshold=10):
         ent = entries.numpy()[:n].astype(np.int64)

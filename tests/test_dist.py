@@ -237,7 +237,15 @@ def _sweep_worker(rank, world, port, csr, thr, out_dir, edge_threshold):
     dist.init_process_group('gloo', rank=rank, world_size=world)
     ctx = EmuSweepContext(csr, thr)
     sh = SweepShard(ctx, csr.n_reads, chrom_counts_of(csr), world, rank, 'cpu')
-    info = sh.step(1 - 0.04, 1 - 0.25, pass_table([1, 1, 0.66, 0.66, 0.66, 0.5]), edge_threshold)
+    pt = pass_table([1, 1, 0.66, 0.66, 0.66, 0.5])
+    info = sh.step(1 - 0.04, 1 - 0.25, pt, edge_threshold)
+    # a repeat step (no host syncs: the synchronous step's counts) gives the same result; with the
+    # cap binding it runs synchronously again
+    info2 = sh.step(1 - 0.04, 1 - 0.25, pt, edge_threshold, repeat=True)
+    assert info2.get('repeat', False) == (not info['capped'])
+    if info2.get('repeat'):
+        assert ctx.repeat_partitions == 1
+        sh.verify_repeat()
     np.save(os.path.join(out_dir, f'labels{rank}.npy'), sh.labels())
     a, b, I, U = ctx.edges(ctx.stats().get('n_edges', 0))
     np.save(os.path.join(out_dir, f'edges{rank}.npy'), np.stack([a, b, I, U], axis=1) if len(a) else np.zeros((0, 4)))
@@ -489,6 +497,9 @@ def _sweep_gpu_worker(rank, world, port, out_dir):
     pt = pass_table([1, 1, 0.66, 0.66, 0.66, 0.5])
     for _ in range(2):                               # the second step reuses the grown buffers
         info = sh.step(1 - 0.04, 1 - 0.25, pt, 10)
+    info = sh.step(1 - 0.04, 1 - 0.25, pt, 10, repeat=True)     # as bench.py's timed steps
+    assert info.get('repeat')
+    sh.verify_repeat()
     np.save(os.path.join(out_dir, f'labels{rank}.npy'), sh.labels())
     st = ctx.stats()
     a, b, I, U = ctx.edges(st['n_edges'])
@@ -613,3 +624,50 @@ def test_sweep_partition_first_call_in_reused_memory():
         c.close()
     assert sorted(got) == sorted(zip(o['edge_a'].tolist(), o['edge_b'].tolist(), o['edge_I'].tolist(),
                                      o['edge_U'].tolist()))
+
+
+@pytest.mark.gpu
+def test_sweep_partition_repeat_equals_sync():
+    """fslr_sweep_partition_repeat (the timed multi-GPU steps of bench.py): on unchanged input it
+    writes each destination's segment with the same entries as the synchronous partition, with no
+    flag raised; another split or a new input generation is refused."""
+    import torch
+    from fslr_amd import _lib
+    from fslr_amd.dist import chrom_counts_of, chrom_owner
+    from fslr_amd.prep import fold_overlap_threshold, pass_table
+    s = synth.generate(20_000, 16, 5)
+    csr = s.interval_data().csr()
+    thr = fold_overlap_threshold(csr.iv_aln, 0.8)
+    pt = pass_table([1, 1, 0.66, 0.66, 0.66, 0.5])
+    qc, nc = 1 - 0.04, 1 - 0.25
+    ctx = _lib.Context(0)
+    ctx.load_csr(csr, thr)
+    ctx.set_chrom_filter(chrom_owner(chrom_counts_of(csr), 2) == 0)
+    ctx.build_index()
+    dst = torch.empty(1 << 16, dtype=torch.int64, device='cuda')
+    ok, counts = ctx.sweep_partition(qc, nc, pt, 3, 6, dst)
+    if not ok:
+        dst = torch.empty(int(counts.sum()) + 4096, dtype=torch.int64, device='cuda')
+        ok, counts = ctx.sweep_partition(qc, nc, pt, 3, 6, dst)
+    assert ok and counts.sum() > 0
+    pos = np.concatenate([[0], np.cumsum(counts)])
+    ref = dst[:pos[-1]].cpu().numpy()
+    dst.fill_(0)
+    torch.cuda.synchronize()
+    for _ in range(2):
+        ctx.build_index()
+        ctx.sweep_partition_repeat(qc, nc, pt, 3, 6, dst)
+        ctx.sync()
+        got = dst[:pos[-1]].cpu().numpy()
+        for d in range(3):                       # order inside a segment is free (LDS atomics)
+            np.testing.assert_array_equal(np.sort(got[pos[d]:pos[d + 1]]), np.sort(ref[pos[d]:pos[d + 1]]))
+        st = ctx.stats()
+        assert not st['overflow_flags'] & 32
+    with pytest.raises(_lib.FslrError):
+        ctx.sweep_partition_repeat(qc, nc, pt, 2, 6, dst)          # another split
+    ctx.set_thresholds(thr)                                        # a new input generation
+    ctx.set_chrom_filter(chrom_owner(chrom_counts_of(csr), 2) == 0)
+    ctx.build_index()
+    with pytest.raises(_lib.FslrError):
+        ctx.sweep_partition_repeat(qc, nc, pt, 3, 6, dst)
+    ctx.close()
