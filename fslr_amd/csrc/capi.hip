@@ -437,9 +437,16 @@ int fslr::peek_counts(fslr_ctx* c, long long out[3]) {
   return FSLR_OK;
 }
 
-// a lean index (fslr_build_index for the sweep) gets its (chrom, end) keys and data -> sorted map
-static int ensure_keys(fslr_ctx* c) {
+// a lean index (fslr_build_index for the sweep) gets its (chrom, end) keys (keys_only: what the
+// backward ranges read, from its end column) or also its data -> sorted map (a full scatter again)
+static int ensure_keys(fslr_ctx* c, bool keys_only) {
   if (!c->index_lean) return FSLR_OK;
+  if (keys_only) {
+    if (c->lean_keys) return FSLR_OK;
+    HIP_TRY(c, launch_index_endkeys(index_bufs(c), static_cast<int>(c->ni_idx), c->built_n_chroms, c->stream));
+    c->lean_keys = true;
+    return FSLR_OK;
+  }
   HIP_TRY(c, launch_index_rescatter(index_bufs(c), static_cast<int>(c->ni_idx), c->built_n_chroms, c->stream));
   c->index_lean = false;
   return FSLR_OK;
@@ -448,7 +455,7 @@ static int ensure_keys(fslr_ctx* c) {
 int fslr::ensure_bwd_ranges(fslr_ctx* c) {
   if (!c->index_built) return fail(c, FSLR_ERR_STATE, "fslr_build_index first");
   if (c->index_full || c->bwd_ranges) return FSLR_OK;
-  if (int rc = ensure_keys(c)) return rc;
+  if (int rc = ensure_keys(c, true)) return rc;
   HIP_TRY(c, launch_index_bwd_ranges(index_bufs(c), static_cast<int>(c->ni_idx), c->stream));
   c->bwd_ranges = true;
   return FSLR_OK;
@@ -457,7 +464,7 @@ int fslr::ensure_bwd_ranges(fslr_ctx* c) {
 int fslr::ensure_walk_index(fslr_ctx* c) {
   if (!c->index_built || c->index_full) return FSLR_OK;
   if (c->filter_active) return fail(c, FSLR_ERR_STATE, "the walk engine needs every chromosome's index");
-  if (int rc = ensure_keys(c)) return rc;
+  if (int rc = ensure_keys(c, false)) return rc;
   HIP_TRY(c, launch_index_walk_parts(index_bufs(c), static_cast<int>(c->n), static_cast<int>(c->ni), c->stream));
   c->index_full = true;
   return FSLR_OK;
@@ -477,6 +484,7 @@ int fslr_build_index(fslr_ctx* c) {
   HIP_TRY(c, launch_build_index(index_bufs(c), static_cast<int>(c->n), static_cast<int>(c->ni_idx), nch, full,
                                 c->stream));
   c->index_lean = !full && index_bufs(c).dchrom && nch <= 64;
+  c->lean_keys = false;
   c->built_n_chroms = nch;
   if (c->prof_phases) HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));
   c->t_index_rec = c->prof_phases;

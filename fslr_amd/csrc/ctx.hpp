@@ -19,7 +19,8 @@ struct fslr_ctx {
   bool reads_set = false, index_built = false, have_data_pos = false;
   bool index_full = false;                 // the walk engine's index parts exist (qpos, backward ranges)
   bool bwd_ranges = false;                 // backward scan ranges exist (the cap replay's hits; no qpos)
-  bool index_lean = false;                 // lean scatter (no (chrom, end) keys, no data -> sorted map)
+  bool index_lean = false;                 // lean scatter (no data -> sorted map; `vals` holds the ends)
+  bool lean_keys = false;                  // a lean index's (chrom, end) keys were made (k_endkey)
   int built_n_chroms = 0;                  // chromosomes of the built index (filtered: the owned ones)
   // multi-GPU sweep: the index covers the chromosomes of a filter (fslr_set_chrom_filter)
   bool filter_active = false;

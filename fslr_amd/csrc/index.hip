@@ -137,7 +137,6 @@ __global__ __launch_bounds__(kTileThreads) void k_chrom_count(const unsigned* __
   const int tl = blockIdx.x;
   const int e0 = tl * rounds * kTileThreads;
   int cnt = 0;
-#pragma unroll 4
   for (int r = 0; r < rounds; ++r) {
     const int e = e0 + r * kTileThreads + threadIdx.x;
     const unsigned c = e < ni ? dchrom[e] : 0u;
@@ -190,7 +189,7 @@ __global__ __launch_bounds__(1024) void k_chrom_scan(int* __restrict__ chist, in
 // most lines were shared by waves on different XCDs and the stores cost 155 of 215 us.
 // qd[e] = q is written in data order for the CSR -> sorted position gather.
 // kFull = false (the sweep engine's lean index): the (chrom, end) key and the data -> sorted map are
-// not written, only each position's end (s_end, in the endkey buffer): 56 instead of 68 B / interval
+// not written, only each position's end (in the map's buffer `qd`): 56 instead of 68 B / interval
 template <bool kFull>
 __global__ __launch_bounds__(kTileThreads) void k_chrom_scatter(const unsigned* __restrict__ dchrom,
                                                               const int4* __restrict__ drec,
@@ -257,7 +256,7 @@ __global__ __launch_bounds__(kTileThreads) void k_chrom_scatter(const unsigned* 
         endkey[q] = (static_cast<unsigned long long>(c) << 32) | static_cast<unsigned>(rec.y);
         qd[e] = q;
       } else {
-        reinterpret_cast<int*>(endkey)[q] = rec.y;
+        qd[q] = rec.y;                           // lean: the end column in the map's buffer
       }
     }
   }
@@ -366,7 +365,8 @@ struct TilePrefix {
 };
 
 // kBwd = false (the sweep engine, lean index): forward counts only, no pmax window (rng_s[q].y = -1);
-// ends from the s_end column (endkey's buffer), the chromosome from its begin in crange (n_chroms <= 64)
+// ends from the lean scatter's end column (passed as endkey), the chromosome from its begin in crange
+// (n_chroms <= 64)
 template <bool kBwd>
 __global__ __launch_bounds__(kRangeBlock) void k_ranges(const int4* __restrict__ idx4, int shard, int n_shards,
                                                         const int* __restrict__ s_start,
@@ -565,8 +565,8 @@ hipError_t launch_build_index(const IndexBufs& b, int n, int ni, int n_chroms, b
       k_chrom_scatter<false><<<ntl, kTileThreads, 0, s>>>(b.dchrom, b.drec, b.dgate, b.chist, ni, ntl, rounds, b.idx4,
                                                           b.idx_gate, b.s_start, b.endkey, b.vals);
       k_ranges<false><<<(ni + kRangeSpan - 1) / kRangeSpan, kRangeBlock, 0, s>>>(
-          b.idx4, b.shard, b.n_shards, b.s_start, b.endkey, TilePrefix{nullptr, nullptr}, b.crange, ni, b.rng_s,
-          n_chroms);
+          b.idx4, b.shard, b.n_shards, b.s_start, reinterpret_cast<const unsigned long long*>(b.vals),
+          TilePrefix{nullptr, nullptr}, b.crange, ni, b.rng_s, n_chroms);
       return hipGetLastError();
     }
     k_chrom_scatter<true><<<ntl, kTileThreads, 0, s>>>(b.dchrom, b.drec, b.dgate, b.chist, ni, ntl, rounds, b.idx4, b.idx_gate,
@@ -588,6 +588,28 @@ hipError_t launch_build_index(const IndexBufs& b, int n, int ni, int n_chroms, b
                                                          b.pmaxkey, b.qpos, b.shard, b.n_shards);
   }
   return launch_walk_parts(b, n, ni, s, false);
+}
+
+// a lean index's (chrom, end) keys from its end column (the backward ranges need them, not the map)
+__global__ __launch_bounds__(256) void k_endkey(const int* __restrict__ s_end, const int2* __restrict__ crange,
+                                                int n_chroms, int ni, unsigned long long* __restrict__ endkey) {
+  __shared__ int c_beg[64];
+  if (threadIdx.x < 64) c_beg[threadIdx.x] = threadIdx.x < n_chroms ? crange[threadIdx.x].x : 0x7FFFFFFF;
+  __syncthreads();
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < ni; q += gridDim.x * blockDim.x) {
+    int c = 0;
+#pragma unroll
+    for (int b = 32; b > 0; b >>= 1)
+      if (c + b < 64 && c_beg[c + b] <= q) c += b;
+    endkey[q] = (static_cast<unsigned long long>(c) << 32) | static_cast<unsigned>(s_end[q]);
+  }
+}
+
+hipError_t launch_index_endkeys(const IndexBufs& b, int ni, int n_chroms, hipStream_t s) {
+  if (ni <= 0) return hipSuccess;
+  if (n_chroms > kMaxFusedChroms) return hipErrorInvalidValue;
+  k_endkey<<<grid_for(ni), 256, 0, s>>>(b.vals, b.crange, n_chroms, ni, b.endkey);
+  return hipGetLastError();
 }
 
 hipError_t launch_index_rescatter(const IndexBufs& b, int ni, int n_chroms, hipStream_t s) {

@@ -108,6 +108,8 @@ hipError_t launch_build_index(const IndexBufs& b, int n_reads, int ni, int n_chr
 // a lean (sweep-only) index's full scatter again: the (chrom, end) keys and the data -> sorted map the
 // walk parts and the backward ranges read (same records, same order)
 hipError_t launch_index_rescatter(const IndexBufs& b, int ni, int n_chroms, hipStream_t s);
+// a lean index's (chrom, end) keys alone (its end column stays in b.vals): what the backward ranges read
+hipError_t launch_index_endkeys(const IndexBufs& b, int ni, int n_chroms, hipStream_t s);
 // the walk engine's parts of a sweep-only index (qpos, tile prefix, backward ranges)
 hipError_t launch_index_walk_parts(const IndexBufs& b, int n_reads, int ni, hipStream_t s);
 // the backward scan ranges alone (tile prefix of end + k_ranges<true>): no CSR map, so it also

@@ -675,8 +675,13 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
       const bool v0 = lane < gend, v1 = lane + kWave < gend;
       const bool hv0 = h0 && v0, hv1 = h1 && v1;
       int la0 = 0, la1 = 0;
+#if defined(FSLR_PAIRS_ABLATE) && (FSLR_PAIRS_ABLATE & 4)
+      if (hv0) la0 = 8;                                            // profiling ablation: no L gathers
+      if (hv1) la1 = 8;
+#else
       if (hv0) la0 = RL[entry_a(e0)];                              // in flight during the sort
       if (hv1) la1 = RL[entry_a(e1)];
+#endif
       unsigned long long k0 = v0 ? group_key(e0, r0) : ~0ull;
       unsigned long long k1 = v1 ? group_key(e1, r1) : ~0ull;
 #if !defined(FSLR_PAIRS_ABLATE) || (FSLR_PAIRS_ABLATE & 1) == 0
@@ -692,8 +697,13 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
       const bool d0 = v0 && !s0 && (k0 >> 7) == (q0 >> 7);
       const bool d1 = v1 && !s1 && (k1 >> 7) == (q1 >> 7);
       int lb0 = 0, lb1 = 0;                                        // L_B of each segment, gathered by its head
+#if defined(FSLR_PAIRS_ABLATE) && (FSLR_PAIRS_ABLATE & 4)
+      if (s0) lb0 = 8;
+      if (s1) lb1 = 8;
+#else
       if (s0) lb0 = RL[(k0 >> 14) & kRankMask];
       if (s1) lb1 = RL[(k1 >> 14) & kRankMask];
+#endif
       // the next window, in flight while this group is evaluated
       const long long sn = s + gend;
       unsigned long long n0 = ~0ull, n1 = ~0ull, nn = ~0ull;
