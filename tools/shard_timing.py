@@ -99,7 +99,7 @@ def main():
     counts = chrom_counts_of(csr)
     for W in [int(x) for x in args.worlds.split(',')]:
         owner = chrom_owner(counts, W)
-        part, segs, sent = [], [[] for _ in range(W)], []
+        part, part_rep, segs, sent = [], [], [[] for _ in range(W)], []
         buf = torch.empty(max(1 << 16, int(1.2 * st1['match_entries'] / W) + 4096), dtype=torch.int64, device=dev)
         for r in range(W):
             cp.set_chrom_filter(owner == r if W > 1 else None)
@@ -115,6 +115,13 @@ def main():
                 res['cnt'] = cnt
             part.append(timed(p, args.reps))
             cnt = res['cnt']
+            if W > 1:
+                # the repeat step's partition (SweepShard.step(repeat=True)): no readback inside
+                def pr():
+                    cp.build_index()
+                    cp.sweep_partition_repeat(qc, nc, pt, W, 6, buf)
+                part_rep.append(timed(pr, args.reps))
+                assert not cp.stats()['overflow_flags'] & 32
             pos = np.concatenate([[0], np.cumsum(cnt)])
             for d in range(W):
                 segs[d].append(buf[pos[d]:pos[d + 1]].clone())
@@ -154,12 +161,17 @@ def main():
         gather_ms = 0.0 if W == 1 else 8 * m * (W - 1) / (args.xgmi_gbs * 1e6) + args.coll_us / 1000
         # + the all_reduce of (max forward degree, error flag, edge count) between evaluation and gather
         step = max(part) + a2a_ms + max(evl) + gather_ms + merge + (args.coll_us / 1000 if W > 1 else 0.0)
-        row = {'W': W, 'part_ms': part, 'eval_ms': evl, 'merge_ms': merge, 'a2a_ms_model': a2a_ms,
+        # repeat steps: no count exchange and no all_reduce (one collective latency less in the a2a
+        # model, none for the reduce), the partition without its readback
+        step_rep = (max(part_rep) + a2a_ms - args.coll_us / 1000 + max(evl) + gather_ms + merge) if W > 1 else step
+        row = {'W': W, 'part_ms': part, 'part_repeat_ms': part_rep, 'eval_ms': evl, 'merge_ms': merge,
+               'a2a_ms_model': a2a_ms, 'projected_step_repeat_ms': step_rep, 'projected_speedup_repeat': t1 / step_rep,
                'gather_ms_model': gather_ms, 'entries_sent_per_rank': sent.sum(axis=1).tolist(),
                'entries_recv_per_rank': recv.tolist(), 'edges_per_rank': nedges, 'projected_step_ms': step,
                'projected_speedup': t1 / step}
         log(f'W={W}: part max {max(part):.3f} ms, eval max {max(evl):.3f} ms, merge {merge:.3f} ms, '
-            f'a2a {a2a_ms:.3f} ms, gather {gather_ms:.3f} ms -> {step:.3f} ms ({t1 / step:.2f}x)')
+            f'a2a {a2a_ms:.3f} ms, gather {gather_ms:.3f} ms -> {step:.3f} ms ({t1 / step:.2f}x); repeat steps '
+            f'{step_rep:.3f} ms ({t1 / step_rep:.2f}x)')
         out['worlds'].append(row)
         print(json.dumps(row), flush=True)
     print(json.dumps(out), flush=True)
