@@ -373,7 +373,7 @@ constexpr int kPairEdgeStage = FSLR_PAIR_EDGE_STAGE;   // staged edges per wave 
 // slot list) or the group's sorted keys, segment keys, column masks and heads
 constexpr int kLongScr = kHash2 * (4 + 4 + 8 + 8) + 2 * (kPairLimit + kWave);
 constexpr int kGroupScr = kStageE * (8 + 8 + 8) + 4 * (kStageE + 1);
-constexpr int kScrWords = ((kLongScr > kGroupScr ? kLongScr : kGroupScr) + 7) / 8;
+constexpr int kScrWords = ((kLongScr > kGroupScr ? kLongScr : kGroupScr) + 15) / 16 * 2;   // 16-B rows
 
 // lane ^ ST's value: DPP for strides 1 .. 8 (inside a 16-lane row: quad permutes, row shifts),
 // ds_swizzle for 16 (inside 32 lanes), ds_bpermute for 32 — the short strides cost a VALU op, not an
@@ -438,13 +438,44 @@ __device__ __forceinline__ void bitonic128(unsigned long long& a, unsigned long 
   bitonic_steps<2 * kWave, 32>(a, b, lane);
 }
 
+// The same sort with element e = lane << 1 | slot (a: slot 0, b: slot 1): index bit 0 is in-lane (7
+// of the 28 stages exchange nothing), bits 1-4 are DPP lane exchanges and only bits 5 and 6 cross 16
+// lanes (3 LDS-permute stages instead of 5).  The network is a chain of 28 dependent stages, and a
+// permute through LDS is its slowest link.  Sorted element e ends at lane e >> 1, slot e & 1.
+template <int SIZE, int D>
+__device__ __forceinline__ void bitonic_il_steps(unsigned long long& a, unsigned long long& b, int lane) {
+  if constexpr (D >= 1) {
+    const bool asc = ((lane << 1) & SIZE) == 0;
+    if constexpr (D == 1) {
+      const unsigned long long lo = a < b ? a : b, hi = a < b ? b : a;
+      a = asc ? lo : hi;
+      b = asc ? hi : lo;
+    } else {
+      const bool lower = (lane & (D >> 1)) == 0;
+      a = bitonic_cx<D / 2>(a, lower == asc, lane);
+      b = bitonic_cx<D / 2>(b, lower == asc, lane);
+    }
+    bitonic_il_steps<SIZE, D / 2>(a, b, lane);
+  }
+}
+
+__device__ __forceinline__ void bitonic128_il(unsigned long long& a, unsigned long long& b, int lane) {
+  bitonic_il_steps<2, 1>(a, b, lane);
+  bitonic_il_steps<4, 2>(a, b, lane);
+  bitonic_il_steps<8, 4>(a, b, lane);
+  bitonic_il_steps<16, 8>(a, b, lane);
+  bitonic_il_steps<32, 16>(a, b, lane);
+  bitonic_il_steps<64, 32>(a, b, lane);
+  bitonic_il_steps<128, 64>(a, b, lane);
+}
+
 // group sort key: run (7 bits) << 39 | B << 14 | i << 7 | j; the segment key (run, B) is key >> 14
 __device__ __forceinline__ unsigned long long group_key(unsigned long long e, int r) {
   return (static_cast<unsigned long long>(r) << 39) | (e & ((1ull << 39) - 1));
 }
 
 __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
-  __shared__ unsigned long long scr_all[kSwWaves][kScrWords];
+  __shared__ __attribute__((aligned(16))) unsigned long long scr_all[kSwWaves][kScrWords];
   __shared__ int runa_all[kSwWaves][kStageE];                 // per run of the group: A, L_A, edges formed
   __shared__ int runl_all[kSwWaves][kStageE];
   __shared__ int runf_all[kSwWaves][kStageE];
@@ -685,8 +716,14 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
       unsigned long long k0 = v0 ? group_key(e0, r0) : ~0ull;
       unsigned long long k1 = v1 ? group_key(e1, r1) : ~0ull;
 #if !defined(FSLR_PAIRS_ABLATE) || (FSLR_PAIRS_ABLATE & 1) == 0
-      bitonic128(k0, k1, lane);                                    // positions [0, gend) hold the group
+      bitonic128_il(k0, k1, lane);
 #endif
+      // back to position p at lane p (k0) / p - 64 (k1) through the group's key array
+      wave_lds_sync();                                             // the previous group's reads are done
+      reinterpret_cast<ulonglong2*>(SK)[lane] = make_ulonglong2(k0, k1);
+      wave_lds_sync();
+      k0 = SK[lane];                                               // positions [0, gend) hold the group
+      k1 = SK[lane + kWave];
       const unsigned long long q0 = __shfl_up(k0, 1);
       const unsigned long long k0_63 = __shfl(k0, kWave - 1);
       const unsigned long long w1 = __shfl_up(k1, 1);
@@ -723,8 +760,6 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
         RUNL[r1] = la1;
         RUNF[r1] = 0;
       }
-      SK[lane] = k0;
-      SK[lane + kWave] = k1;
       if (s0) {
         PK[g0] = (k0 >> 14) | (static_cast<unsigned long long>(lb0) << 32);
         PJ[g0] = 0ull;
