@@ -522,12 +522,15 @@ int fslr_query_shard(fslr_ctx* c, const fslr_params* p, int32_t shard, int32_t n
 // fallback (count, then emit: the sweep runs twice).
 static int sweep_front(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_t a_end, hipEvent_t e0,
                        hipEvent_t e1, SweepArgs& s, int& mode, bool defer = false) {
-  int64_t ub_budget = int64_t(1) << 30;              // upper-bound slots (8 B each)
-  {
+  // upper-bound slots (8 B each) the one-pass sweep may use: half the free HBM, at least 2^30; asked
+  // only when the slot buffer has to grow (hipMemGetInfo is a driver round trip, kept off repeat queries)
+  auto ub_budget = []() {
+    int64_t b = int64_t(1) << 30;
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) == hipSuccess)
-      ub_budget = std::max<int64_t>(ub_budget, static_cast<int64_t>(fr / 2 / sizeof(unsigned long long)));
-  }
+      b = std::max<int64_t>(b, static_cast<int64_t>(fr / 2 / sizeof(unsigned long long)));
+    return b;
+  };
   const int64_t nix = c->ni_idx;                      // positions of the (possibly chromosome-filtered) index
   const int64_t tiles = (nix + 63) / 64 + 1;
   int rc;
@@ -625,7 +628,7 @@ static int sweep_front(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64
     if (mode == 2 && (tot[2] & 8)) {
       // upper-bound buffer too small (or beyond the budget: two passes); clear the flag and counters
       const int64_t need = tot[1];
-      if (need > ub_budget) {
+      if (need > ub_budget()) {
         mode = 0;
       } else {
         if ((rc = dalloc(c, &c->ent_ub, need + (need >> 3) + 4096))) return rc;
