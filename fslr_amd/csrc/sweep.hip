@@ -1187,7 +1187,9 @@ static hipError_t group_by_a(const SweepArgs& a, int mode, const unsigned long l
   hb = std::max(hb, nbits - 12);                            // low digit <= 12 bits (LDS bins)
   hb = std::min(hb, nbits);
   const int H = 1 << hb, lo = nbits - hb;
-  const int P = std::max(64, std::min(kMsdMaxBlocks, (kGrpInts / 2) / H));
+  // (a small entry set, e.g. one rank's share of the multi-GPU split, takes fewer blocks: about 8K
+  // entries per block, so the [bucket][block] counts and their scan stay small)
+  const int P = std::max(64, std::min({kMsdMaxBlocks, (kGrpInts / 2) / H, static_cast<int>((n + 8191) / 8192)}));
   int* mat = a.grp;
   int* off = a.grp + kGrpInts / 2;
   const int nt = tiles_of(a);
