@@ -474,7 +474,10 @@ __device__ __forceinline__ unsigned long long group_key(unsigned long long e, in
   return (static_cast<unsigned long long>(r) << 39) | (e & ((1ull << 39) - 1));
 }
 
-__global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
+#ifndef FSLR_PAIRS_WPE
+#define FSLR_PAIRS_WPE 5
+#endif
+__global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(FSLR_PAIRS_WPE))) void k_sweep_pairs(SweepArgs g) {
   __shared__ __attribute__((aligned(16))) unsigned long long scr_all[kSwWaves][kScrWords];
   __shared__ int runa_all[kSwWaves][kStageE];                 // per run of the group: A, L_A, edges formed
   __shared__ int runl_all[kSwWaves][kStageE];
