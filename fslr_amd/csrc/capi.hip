@@ -970,7 +970,6 @@ int fslr_sweep_evaluate(fslr_ctx* c, const fslr_params* p, const void* entries, 
   s.ent = static_cast<unsigned long long*>(const_cast<void*>(entries));
   s.ent_mid = c->ent;
   s.ent_sorted = c->ent_sorted;
-  s.ent_cap = c->ent_cap;
   s.n_ent = n;
   s.temp = c->sweep_temp;
   s.temp_bytes = c->sweep_temp_bytes;

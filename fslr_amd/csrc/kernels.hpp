@@ -195,10 +195,6 @@ struct SweepArgs {
   hipEvent_t ev[5];                   // (profiling) count | scan | emit | sort | pairs boundaries, or null
   hipEvent_t k0, k1;                  // (profiling) around the sweep kernel launch alone, or null
   hipEvent_t p0, p1;                  // (profiling) around the pair-stage kernel (k_sweep_pairs) alone, or null
-  unsigned long long* slot_buf;       // (pair stage, set by launch_sweep_pairs) counter-free edge slots, or null
-  long long* slot_start;              // per 512-entry chunk: its first run start (the chunk's slot base)
-  int* slot_cnt;                      // per chunk: edges written; then its exclusive offset (k_slot_scan)
-  long long* slot_off;
 };
 size_t sweep_temp_bytes(long long ent_cap, long long ni, hipStream_t s);
 int sweep_max_waves();

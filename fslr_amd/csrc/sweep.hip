@@ -474,10 +474,7 @@ __device__ __forceinline__ unsigned long long group_key(unsigned long long e, in
   return (static_cast<unsigned long long>(r) << 39) | (e & ((1ull << 39) - 1));
 }
 
-#ifndef FSLR_PAIRS_WPE
-#define FSLR_PAIRS_WPE 5
-#endif
-__global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(FSLR_PAIRS_WPE))) void k_sweep_pairs(SweepArgs g) {
+__global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
   __shared__ __attribute__((aligned(16))) unsigned long long scr_all[kSwWaves][kScrWords];
   __shared__ int runa_all[kSwWaves][kStageE];                 // per run of the group: A, L_A, edges formed
   __shared__ int runl_all[kSwWaves][kStageE];
@@ -504,22 +501,6 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(FSLR_P
   uint2* RR = rr_all[wv];
   EdgeStageN<kPairEdgeStage> es{es_all[wv], 0};
   const EdgeOut eo{g.edges, g.edge_iu, g.edge_cap, &g.counters[kEdgeCount]};
-  // counter-free edge output (g.slot_buf): the edges of the runs that start in chunk c are written
-  // from the chunk's first run start on (a run of m entries forms at most m edges, so chunks never
-  // overlap); k_slot_scan / k_slot_copy compact them afterwards in chunk order
-  unsigned long long* const SL = g.slot_buf;
-  long long cb = 0;
-  int cn = 0;
-  auto put = [&](bool edge, int A, int B, int I, int U) -> int {
-    if (!SL) return es.put(eo, edge, A, B, I, U, lane);
-    const unsigned long long em = __ballot(edge);
-    if (edge)
-      SL[cb + cn + mbcnt(em)] = (static_cast<unsigned long long>(A) << 39) | (static_cast<unsigned long long>(B) << 14) |
-                                (static_cast<unsigned long long>(I) << 7) | static_cast<unsigned long long>(U);
-    const int ne = __popcll(em);
-    cn += ne;
-    return ne;
-  };
   const int umax_v = g.umax[lane];
   const long long n = g.n_dev ? *g.n_dev : g.n_ent;
   const unsigned long long* E = g.ent_sorted;
@@ -661,7 +642,7 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(FSLR_P
         const int U = LA + LB - I;
         const int um = __shfl(umax_v, max(I, 1) - 1);     // every lane reads (no && in front)
         const bool edge = act && I > 0 && U <= um;
-        fwdA += put(edge, A, B, I, U);
+        fwdA += es.put(eo, edge, A, B, I, U, lane);
         w_pairs += __popcll(__ballot(act));
       }
     }
@@ -681,8 +662,6 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(FSLR_P
     const long long c0 = c * kChunk2, c1 = min(c0 + kChunk2, n);
     long long s = c0;
     if (s > 0) s = next_run(s, c1, a_at(s - 1));       // the run in progress belongs to the previous chunk
-    cb = s;
-    cn = 0;
     unsigned long long e0 = ~0ull, e1 = ~0ull, en = ~0ull;
     if (s < c1) load_window(s, e0, e1, en);
     while (s < c1) {
@@ -835,7 +814,7 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(FSLR_P
         const int U = (act ? RUNL[r] : 0) + LB - I;
         const int um = __shfl(umax_v, max(I, 1) - 1);     // every lane reads (no && in front)
         const bool edge = act && I > 0 && U <= um;
-        put(edge, A, B, I, U);
+        es.put(eo, edge, A, B, I, U, lane);
         if (edge) atomicAdd(&RUNF[r], 1);
         w_pairs += __popcll(__ballot(act));
       }
@@ -854,10 +833,6 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(FSLR_P
       e0 = n0;
       e1 = n1;
       en = nn;
-    }
-    if (SL && lane == 0) {
-      g.slot_start[c] = cb;
-      g.slot_cnt[c] = cn;
     }
   }
   if (es.n > 0) es.flush(eo, lane);
@@ -1272,68 +1247,10 @@ hipError_t launch_sweep_partition(const SweepArgs& a, int mode, int shift, int n
   return hipGetLastError();
 }
 
-#ifndef FSLR_PAIR_SLOTS
-#define FSLR_PAIR_SLOTS 0
-#endif
-// exclusive scan of the chunks' edge counts (one block), edge counter += total
-__global__ __launch_bounds__(1024) void k_slot_scan(const int* __restrict__ cnt, long long* __restrict__ off,
-                                                    const long long* __restrict__ n_dev, long long n_host,
-                                                    unsigned long long* __restrict__ counters) {
-  __shared__ long long part[1024];
-  const long long n = n_dev ? *n_dev : n_host;
-  const long long nch = (n + kChunk2 - 1) / kChunk2;
-  const long long per = (nch + 1023) / 1024;
-  const long long b = threadIdx.x * per, e = min(b + per, nch);
-  long long t = 0;
-  for (long long k = b; k < e; ++k) t += cnt[k];
-  part[threadIdx.x] = t;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {
-    const long long v = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
-    __syncthreads();
-    part[threadIdx.x] += v;
-    __syncthreads();
-  }
-  const long long base = static_cast<long long>(counters[kEdgeCount]);
-  long long run = base + part[threadIdx.x] - t;
-  for (long long k = b; k < e; ++k) {
-    off[k] = run;
-    run += cnt[k];
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) counters[kEdgeCount] = static_cast<unsigned long long>(base + part[1023]);
-}
-
-// one wave per chunk: its edges from its slots to their place in edges / edge_iu (below the cap)
-__global__ __launch_bounds__(256) void k_slot_copy(const unsigned long long* __restrict__ slots,
-                                                   const long long* __restrict__ start, const int* __restrict__ cnt,
-                                                   const long long* __restrict__ off, const long long* __restrict__ n_dev,
-                                                   long long n_host, int2* __restrict__ edges,
-                                                   unsigned short* __restrict__ edge_iu, long long cap) {
-  const long long n = n_dev ? *n_dev : n_host;
-  const long long nch = (n + kChunk2 - 1) / kChunk2;
-  const int lane = lane_id();
-  const long long nw = static_cast<long long>(gridDim.x) * (blockDim.x >> 6);
-  for (long long c = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); c < nch; c += nw) {
-    const int m = cnt[c];
-    const unsigned long long* src = slots + start[c];
-    const long long o = off[c];
-    for (int t = lane; t < m; t += kWave) {
-      const unsigned long long e = src[t];
-      const long long k = o + t;
-      if (k < cap) {
-        edges[k] = make_int2(static_cast<int>(e >> 39), static_cast<int>((e >> 14) & kRankMask));
-        edge_iu[k] = static_cast<unsigned short>(((e >> 7) & 127u) | ((e & 127u) << 8));
-      }
-    }
-  }
-}
-
 hipError_t launch_sweep_pairs(const SweepArgs& a0, int mode, hipStream_t s) {
   SweepArgs a = a0;
   if (a.ev[2]) (void)hipEventRecord(a.ev[2], s);
   const bool msd = a.grp && a.n_ent > 0 && a.n_ent < (1ll << 31);
-  unsigned long long* free_after_mode0 = nullptr;
   if (mode == 0 || (mode == 2 && !msd)) {
     hipError_t e = launch_sweep_dense(a, mode, s);          // dense entries in a.ent
     if (e != hipSuccess) return e;
@@ -1346,7 +1263,6 @@ hipError_t launch_sweep_pairs(const SweepArgs& a0, int mode, hipStream_t s) {
     if (mode == 2) {
       e = group_by_a(a, 2, nullptr, a.ent, a.ent_sorted, s);
     } else if (mode == 0) {
-      free_after_mode0 = a.ent_sorted;
       e = group_by_a(a, 0, a.ent, a.ent_sorted, a.ent, s);
       a.ent_sorted = a.ent;
     } else {
@@ -1362,26 +1278,10 @@ hipError_t launch_sweep_pairs(const SweepArgs& a0, int mode, hipStream_t s) {
   }
   if (a.ev[4]) (void)hipEventRecord(a.ev[4], s);
   const long long chunks = (a.n_ent + kChunk2 - 1) / kChunk2;
-  // counter-free edge output: slots in the entry buffer the grouping left free, per-chunk meta in the
-  // grouping's count buffer (also free now); beyond their capacity, the staged atomic output
-  const long long ch_cap = (a.ent_cap + kChunk2 - 1) / kChunk2;
-  a.slot_buf = nullptr;
-  if (FSLR_PAIR_SLOTS && a.grp && a.n_ent > 0 && a.ent_cap >= a.n_ent && ch_cap * 20 <= static_cast<long long>(kGrpInts) * 4) {
-    a.slot_buf = (mode == 3) ? a.ent_mid : (mode == 0 && msd) ? free_after_mode0 : a.ent;
-    a.slot_start = reinterpret_cast<long long*>(a.grp);
-    a.slot_off = a.slot_start + ch_cap;
-    a.slot_cnt = reinterpret_cast<int*>(a.slot_off + ch_cap);
-  }
   const int blocks = static_cast<int>(std::max(1ll, std::min<long long>(blocks_pairs(), (chunks + kSwWaves - 1) / kSwWaves)));
   if (blocks * kSwWaves > a.wstat_waves) return hipErrorInvalidValue;
   if (a.p0) (void)hipEventRecord(a.p0, s);
   k_sweep_pairs<<<blocks, kSwBlock, 0, s>>>(a);
-  if (a.slot_buf) {
-    k_slot_scan<<<1, 1024, 0, s>>>(a.slot_cnt, a.slot_off, a.n_dev, a.n_ent, a.counters);
-    const int cb = static_cast<int>(std::max(1ll, std::min<long long>(4096, (chunks + 3) / 4)));
-    k_slot_copy<<<cb, 256, 0, s>>>(a.slot_buf, a.slot_start, a.slot_cnt, a.slot_off, a.n_dev, a.n_ent, a.edges,
-                                   a.edge_iu, a.edge_cap);
-  }
   if (a.p1) (void)hipEventRecord(a.p1, s);
   k_sum_slots<<<kSumBlocks, 256, 0, s>>>(a.wstat, blocks * kSwWaves, 2, 4, -1, -1, kMatchedPairs, a.counters,
                                          a.err + 3);
