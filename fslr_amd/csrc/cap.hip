@@ -1378,7 +1378,7 @@ extern "C" int fslr_long_pairs(fslr_ctx* c, const fslr_params* p, int64_t* n_edg
   if (!c->lg_cnt && dalloc(c, &c->lg_cnt, 4)) return FSLR_ERR_NOMEM;
   HIP_TRY(c, hipMemsetAsync(c->lg_cnt, 0, 4 * sizeof(unsigned long long), s));
   HIP_TRY(c, hipMemsetAsync(c->fwd, 0, static_cast<size_t>(c->n) * sizeof(int), s));
-  HIP_TRY(c, hipMemsetAsync(c->errw, 0, kErrWords * sizeof(int), s));
+  HIP_TRY(c, hipMemsetAsync(c->errw, 0, kErrSticky * sizeof(int), s));
   if (ns > 0)
     k_cap_pairs_out<<<grid_for(ns), 256, 0, s>>>(w->ukey, ns, w->T, w->flags, c->lg_edges, c->lg_edge_cap, c->edges,
                                                   c->edge_iu, c->edge_cap, c->lg_cnt, c->fwd, w->err);

@@ -202,26 +202,33 @@ int fslr_set_reads(fslr_ctx* c, const fslr_reads* r) {
   std::vector<unsigned char> rl(static_cast<size_t>(n));
   std::vector<int4> iv(static_cast<size_t>(ni));
   std::vector<unsigned char> zero(static_cast<size_t>(ni), 0);
-  // 0 ok, 1 chrom id, 2 coordinates, 3 read length, 4 n_alignments, 5 qlen2 (the first slice's first
-  // failure in index order is reported)
-  std::atomic<int> bad{0};
-  host_for(ni, [&](int64_t a, int64_t e, int) {
+  // per slice the code of its first failure: 0 ok, 1 chrom id, 2 coordinates, 3 read length,
+  // 4 n_alignments, 5 qlen2.  Slices are contiguous in index order, so the lowest failing slice holds
+  // the input's first failure: the same error whatever the thread timing
+  std::vector<int> bad_slice(static_cast<size_t>(std::max(host_threads(ni), host_threads(n))), 0);
+  auto first_bad = [&]() {
+    for (int b : bad_slice)
+      if (b) return b;
+    return 0;
+  };
+  host_for(ni, [&](int64_t a, int64_t e, int w) {
     for (int64_t k = a; k < e; ++k) {
       const int ch = r->iv_chrom[k], s = r->iv_start[k], en = r->iv_end[k], t = r->iv_thr[k];
-      if (ch < 0 || ch >= r->n_chroms) { bad = 1; return; }
-      if (s < 0 || en < s || en >= kMaxCoord) { bad = 2; return; }
+      if (ch < 0 || ch >= r->n_chroms) { bad_slice[w] = 1; return; }
+      if (s < 0 || en < s || en >= kMaxCoord) { bad_slice[w] = 2; return; }
       if (t == FSLR_THR_ZERO_ALN) zero[k] = 1;
       iv[k] = make_int4(ch, s, en, t);
     }
   });
+  int bad = first_bad();
   if (bad == 1) return fail(c, FSLR_ERR_INVALID, "chrom id out of range");
   if (bad == 2) return fail(c, FSLR_ERR_INVALID, "interval coordinates out of [0, 2^30)");
-  host_for(n, [&](int64_t a, int64_t e, int) {
+  host_for(n, [&](int64_t a, int64_t e, int w) {
     for (int64_t i = a; i < e; ++i) {
       const int o = r->read_off[i], len = r->read_off[i + 1] - o;
-      if (len < 1 || len > FSLR_MAX_L) { bad = 3; return; }
-      if (r->read_nal[i] < 0 || r->read_nal[i] >= (1 << 24)) { bad = 4; return; }
-      if (r->read_qlen2[i] < 0) { bad = 5; return; }   // max(qend) - min(qstart) over a read's fillings (cluster.py:26-29)
+      if (len < 1 || len > FSLR_MAX_L) { bad_slice[w] = 3; return; }
+      if (r->read_nal[i] < 0 || r->read_nal[i] >= (1 << 24)) { bad_slice[w] = 4; return; }
+      if (r->read_qlen2[i] < 0) { bad_slice[w] = 5; return; }   // max(qend) - min(qstart) over a read's fillings (cluster.py:26-29)
       int flags = 0;
       for (int k = o; k < o + len; ++k)
         if (zero[k]) flags |= 1;
@@ -229,6 +236,7 @@ int fslr_set_reads(fslr_ctx* c, const fslr_reads* r) {
       rl[i] = static_cast<unsigned char>(len);
     }
   });
+  bad = first_bad();
   if (bad == 3) return fail(c, FSLR_ERR_INVALID, "every read needs 1.." + std::to_string(FSLR_MAX_L) + " intervals");
   if (bad == 4) return fail(c, FSLR_ERR_INVALID, "n_alignments outside [0, 2^24)");
   if (bad == 5) return fail(c, FSLR_ERR_INVALID, "qlen2 < 0");
@@ -260,7 +268,11 @@ int fslr_set_reads(fslr_ctx* c, const fslr_reads* r) {
       for (int64_t k = a; k < e; ++k) {
         const int d = r->iv_data_pos[k];
         if (d < 0 || d >= ni) { ok = false; return; }
-        inv[d] = static_cast<int>(k);      // a repeated d leaves a hole: the -1 check below finds it
+        // atomic: a repeated d is seen by whichever thread comes second (the message is the same)
+        if (__atomic_exchange_n(&inv[static_cast<size_t>(d)], static_cast<int>(k), __ATOMIC_RELAXED) != -1) {
+          ok = false;
+          return;
+        }
       }
     });
     if (ok)
@@ -635,7 +647,7 @@ static int sweep_front(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64
         c->ent_ub_cap = need + (need >> 3) + 4096;
       }
       HIP_TRY(c, hipMemsetAsync(c->counters, 0, kNumCounters * sizeof(unsigned long long), c->stream));
-      HIP_TRY(c, hipMemsetAsync(c->errw, 0, kErrWords * sizeof(int), c->stream));
+      HIP_TRY(c, hipMemsetAsync(c->errw, 0, kErrSticky * sizeof(int), c->stream));
       continue;
     }
     s.n_ent = tot[0];
@@ -676,7 +688,9 @@ static int sweep_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_
 }
 
 // buffers, the folded cut table and cleared counters / errors / forward degrees for one query
-static int prepare_query(fslr_ctx* c, const fslr_params* p) {
+// keep_sticky: the repeat-partition flags (kErrSticky) survive (a repeat partition and the
+// evaluations after it); any other query starts a new series and clears them
+static int prepare_query(fslr_ctx* c, const fslr_params* p, bool keep_sticky = false) {
   HIP_TRY(c, hipSetDevice(c->device));
   if (c->edge_cap == 0) {
     int rc = fslr_reserve_edges(c, std::max<int64_t>(1 << 16, 12 * c->n));
@@ -709,7 +723,8 @@ static int prepare_query(fslr_ctx* c, const fslr_params* p) {
     if (rc) return rc;
     c->wstat_waves = w;
   }
-  HIP_TRY(c, launch_query_reset(c->counters, kNumCounters, c->errw, kErrWords, c->fwd, static_cast<int>(c->n),
+  HIP_TRY(c, launch_query_reset(c->counters, kNumCounters, c->errw, keep_sticky ? kErrSticky : kErrWords, c->fwd,
+                                static_cast<int>(c->n),
                                 c->stream));
   std::memset(&c->cap_stats, 0, sizeof(c->cap_stats));
   c->edges_global = false;
@@ -749,7 +764,7 @@ static int query_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_
   g.heavy = c->heavy;
   g.counters = c->counters;
   g.err = c->errw;
-  g.mode = c->ablate;
+  g.mode = c->ablate & 3;                            // bits 0-1: the walk kernel's ablations
   g.diag = c->diag;
   g.wstat = c->wstat;
   g.wstat_waves = c->wstat_waves;
@@ -892,7 +907,9 @@ int fslr_sweep_partition(fslr_ctx* c, const fslr_params* p, int32_t n_dest, int3
   for (int k = 0; k < n_dest; ++k) sum += (counts[k] = tot[k]);
   c->pt_gen = 0;
   if (sum > dst_cap) return fail(c, FSLR_ERR_STATE, "destination buffer too small for the entries (see counts)");
-  if (ew[kErrOverflow] == 0) {                      // clean: a repeat may replay this partition
+  // clean, and one pass into the upper-bound slots (a two-pass rerun left them undersized): a repeat
+  // may replay this partition
+  if (ew[kErrOverflow] == 0 && mode == 2) {
     c->pt_gen = c->input_gen;
     c->pt_q = p->qlen_cut;
     c->pt_nc = p->nal_cut;
@@ -912,14 +929,14 @@ struct PartExpect {
 };
 __global__ void k_part_check(const long long* __restrict__ totals, PartExpect expect, int n_dest, int* err) {
   const int k = threadIdx.x;
-  if (k < n_dest && totals[k] != expect.n[k]) atomicOr(&err[kErrOverflow], 32);
+  if (k < n_dest && totals[k] != expect.n[k]) atomicOr(&err[kErrSticky], 32);
 }
 
 int fslr_sweep_partition_repeat(fslr_ctx* c, const fslr_params* p, int32_t n_dest, int32_t block_shift, void* dst,
                                 int64_t dst_cap) {
   if (!c || !p || !p->pass_table || n_dest < 1 || n_dest > kMaxDest || !dst) return FSLR_ERR_INVALID;
   if (!c->index_built) return fail(c, FSLR_ERR_STATE, "fslr_build_index first");
-  if (int rc = prepare_query(c, p)) return rc;           // folds the cut table into umax_host
+  if (int rc = prepare_query(c, p, true)) return rc;     // folds the cut table into umax_host
   if (c->pt_gen != c->input_gen || c->pt_q != p->qlen_cut || c->pt_nc != p->nal_cut || c->pt_umax != c->umax_host ||
       c->pt_ndest != n_dest || c->pt_shift != block_shift || c->pt_sum > dst_cap)
     return fail(c, FSLR_ERR_STATE, "no synchronous fslr_sweep_partition of this input, parameters and split");
@@ -938,6 +955,7 @@ int fslr_sweep_partition_repeat(fslr_ctx* c, const fslr_params* p, int32_t n_des
                                     c->part_cnt, c->stream));
   PartExpect ex{};
   for (int k = 0; k < n_dest; ++k) ex.n[k] = c->pt_counts[k];
+  if (c->ablate & 64) ex.n[0] += 1;                     // tests: a repeat whose totals differ
   k_part_check<<<1, kMaxDest, 0, c->stream>>>(c->part_cnt, ex, n_dest, c->errw);
   HIP_TRY(c, hipGetLastError());
   c->t_kernel_rec = k0 != nullptr;
@@ -947,7 +965,7 @@ int fslr_sweep_partition_repeat(fslr_ctx* c, const fslr_params* p, int32_t n_des
 int fslr_sweep_evaluate(fslr_ctx* c, const fslr_params* p, const void* entries, int64_t n) {
   if (!c || !p || !p->pass_table || (!entries && n) || n < 0) return FSLR_ERR_INVALID;
   if (!c->reads_set) return fail(c, FSLR_ERR_STATE, "fslr_set_reads first");
-  if (int rc = prepare_query(c, p)) return rc;
+  if (int rc = prepare_query(c, p, true)) return rc;
   if (n > c->ent_cap && reserve_entries(c, n + (n >> 3) + 4096)) return FSLR_ERR_NOMEM;
   if (!c->sw_wstat) {
     const int w = sweep_max_waves();
@@ -1059,6 +1077,7 @@ int fslr_read_stats(fslr_ctx* c, fslr_query_stats* out) {
   out->deferred_capacity = c->defer_cap;
   out->edge_capacity = c->edge_cap;
   out->engine = c->last_engine;
+  ew[kErrOverflow] |= ew[kErrSticky];               // a differing repeat partition stays flagged
   out->overflow_flags = ew[kErrOverflow];
   out->pair_tests = static_cast<int64_t>(cnt[kSwTests]);
   out->entry_capacity = c->ent_cap;

@@ -25,7 +25,11 @@ constexpr int kShardShift = 6;
 // error words (QueryArgs::err): [0] code, [1] a, [2] b, [3] max forward degree, [4] overflow flags
 // (1: deferred list, 2: edge buffer) — a query that lost pairs; its labels are refused
 constexpr int kErrWords = 8;
-constexpr int kErrOverflow = 4;        // query shards own blocks of 64 consecutive ranks, round robin
+constexpr int kErrOverflow = 4;
+// [7]: sticky flags of repeated multi-GPU partitions (32: totals differed), kept across queries and
+// cleared by the next synchronous fslr_sweep_partition / fslr_query; the per-query resets stop before it
+constexpr int kErrSticky = 7;
+// query shards own blocks of 64 consecutive ranks, round robin
 
 __host__ __device__ inline bool shard_owns(int read, int shard, int n_shards) {
   return n_shards == 1 || ((read >> kShardShift) % n_shards) == shard;
@@ -194,7 +198,11 @@ struct SweepArgs {
   int wstat_waves;
   hipEvent_t ev[5];                   // (profiling) count | scan | emit | sort | pairs boundaries, or null
   hipEvent_t k0, k1;                  // (profiling) around the sweep kernel launch alone, or null
-  hipEvent_t p0, p1;                  // (profiling) around the pair-stage kernel (k_sweep_pairs) alone, or null
+  hipEvent_t p0, p1;                  // (profiling) around the pair-stage kernel (k_bucket_pairs) alone, or null
+  // set by launch_sweep_pairs for k_sweep_pairs' list mode (the buckets k_bucket_pairs spilled)
+  const long long* spill;             // [2 x count] entry ranges [s, e) in ent_sorted, or null (whole array)
+  const unsigned* spill_n;
+  int wbase;                          // first per-wave statistics slot
 };
 size_t sweep_temp_bytes(long long ent_cap, long long ni, hipStream_t s);
 int sweep_max_waves();

@@ -126,6 +126,25 @@ def chrom_counts_of(csr) -> np.ndarray:
     return np.bincount(np.asarray(csr.iv_chrom), minlength=int(csr.n_chroms))
 
 
+def agree_error(err, world: int, device):
+    """MAX over ranks of an error code (0 none, 1 ZeroDivisionError, 2 other), one all_reduce: every
+    rank raises together (its own exception, or one naming the other rank's) instead of leaving the
+    others waiting in the next collective."""
+    import torch
+    import torch.distributed as dist
+    code = 0 if err is None else (1 if isinstance(err, ZeroDivisionError) else 2)
+    if world > 1:
+        gloo = dist.get_backend() == 'gloo'
+        t = torch.tensor([code], dtype=torch.int64, device='cpu' if gloo else device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        code = int(t.item())
+    if err is not None:
+        raise err
+    if code:
+        from ._lib import FslrError
+        raise ZeroDivisionError('division by zero') if code == 1 else FslrError('error on another rank')
+
+
 class SweepShard:
     """One rank of the chromosome-split sweep (fslr_set_chrom_filter / fslr_sweep_partition /
     fslr_sweep_evaluate, then the edge exchange).  ``ctx`` holds every read (set_reads); this
@@ -351,20 +370,7 @@ class SweepShard:
         return torch.empty(int(need * 1.125) + 4096, dtype=torch.int32, device=self.device)
 
     def _agree(self, err):
-        """MAX over ranks of an error code (0 none, 1 ZeroDivisionError, 2 other): every rank raises
-        together instead of leaving the others in the next collective."""
-        import torch
-        import torch.distributed as dist
-        code = 0 if err is None else (1 if isinstance(err, ZeroDivisionError) else 2)
-        if self.world > 1:
-            t = torch.tensor([code], dtype=torch.int64, device='cpu' if self._gloo() else self.device)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            code = int(t.item())
-        if err is not None:
-            raise err
-        if code:
-            from ._lib import FslrError
-            raise ZeroDivisionError('division by zero') if code == 1 else FslrError('error on another rank')
+        agree_error(err, self.world, self.device)
 
     def _capped_labels(self, edge_threshold, max_ne):
         """The cap binds: the reference's graph depends on the sequential order of its loops

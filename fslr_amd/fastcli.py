@@ -77,12 +77,26 @@ def run(args, basename, tsv, ints, strs, t):
     """main.py:190-352 on columns (``ints``: INT_COLS of every row, ``strs``: the STR_COLS codes, both
     from TsvFile.scan_all); returns False for "No clusters were found." (as the pandas path), True
     after writing both outputs.  Raises Fallback before writing anything when a step needs the
-    pandas path."""
-    t1 = time.perf_counter()
+    pandas path; the HIP context it opened is closed first, so the pandas path opens the only one."""
     # the HIP context comes up while the host prepares the input (one GPU; the multi-GPU ranks make
     # their own)
     pool = ThreadPoolExecutor(2)
     ctx_f = pool.submit(cluster._open_context, args.get('device')) if (args.get('gpus') or 1) == 1 else None
+    state = {'trees': None}
+    try:
+        return _run(args, basename, tsv, ints, strs, t, pool, ctx_f, state)
+    except BaseException:
+        pool.shutdown(wait=True)
+        ctx = state['trees'].ctx if state['trees'] is not None and hasattr(state['trees'], 'ctx') else None
+        if ctx is None and ctx_f is not None and ctx_f.done() and ctx_f.exception() is None:
+            ctx = ctx_f.result()
+        if ctx is not None:
+            ctx.close()
+        raise
+
+
+def _run(args, basename, tsv, ints, strs, t, pool, ctx_f, state):
+    t1 = time.perf_counter()
     n_rows = tsv.rows
     qcode, n_q = strs['qname']
     ccode, _ = strs['chrom']
@@ -139,8 +153,9 @@ def run(args, basename, tsv, ints, strs, t):
     t['csr'] = time.perf_counter() - t1
 
     t2 = time.perf_counter()
-    trees = cluster.build_interval_trees(data, device=args.get('device'), n_gpus=args.get('gpus') or 1,
-                                         ctx=ctx_f.result() if ctx_f is not None else None)
+    trees = state['trees'] = cluster.build_interval_trees(data, device=args.get('device'),
+                                                          n_gpus=args.get('gpus') or 1,
+                                                          ctx=ctx_f.result() if ctx_f is not None else None)
     pool.shutdown()
     t['upload'] = time.perf_counter() - t2
     t2 = time.perf_counter()

@@ -114,20 +114,34 @@ class _Rank:
         edges and forward degrees.  The caller's current device and stream are restored."""
         import torch
         from . import _lib
-        from .dist import SweepShard, chrom_counts_of
-        csr, thr, pt, meta = _load(d)
+        from .dist import SweepShard, agree_error, chrom_counts_of
         prev_dev = torch.cuda.current_device()
         prev_stream = torch.cuda.current_stream()
         torch.cuda.set_device(self.dev_index)
         torch.cuda.set_stream(self.stream)
         try:
-            if self.ctx is None:
-                self.ctx = _lib.Context(self.dev_index, stream=self.stream.cuda_stream)
+            # per-query setup, then one agreement collective: a rank that fails here (context, upload,
+            # chromosome filter) raises on every rank instead of leaving the others in the first
+            # collective of the step until the group's timeout
+            err = None
+            try:
+                csr, thr, pt, meta = _load(d)
+                if self.ctx is None:
+                    self.ctx = _lib.Context(self.dev_index, stream=self.stream.cuda_stream)
+                self.ctx.load_csr(csr, thr)
+                self.ctx.reserve_edges(max(1 << 16, 12 * csr.n_reads // self.world))
+                shard = SweepShard(self.ctx, csr.n_reads, chrom_counts_of(csr), self.world, self.rank, self.dev)
+            except Exception as e:                   # noqa: BLE001 - raised on every rank by agree_error
+                err = e
+            try:
+                agree_error(err, self.world, self.dev)
+            except BaseException:
+                if self.ctx is not None:
+                    self.ctx.close()
+                    self.ctx = None
+                raise
             ctx = self.ctx
             try:
-                ctx.load_csr(csr, thr)
-                ctx.reserve_edges(max(1 << 16, 12 * csr.n_reads // self.world))
-                shard = SweepShard(ctx, csr.n_reads, chrom_counts_of(csr), self.world, self.rank, self.dev)
                 info = shard.step(meta['qlen_cut'], meta['nal_cut'], pt, int(meta['edge_threshold']))
                 torch.cuda.synchronize(self.dev)
                 labels = shard.labels()
@@ -276,8 +290,11 @@ class RankPool:
                 raise RuntimeError('multi-GPU ranks did not finish the query')
             for r, p in list(pending.items()):
                 if p.stdout in ready:
-                    if p.stdout.readline().strip() != 'DONE':
-                        raise RuntimeError(f'multi-GPU rank {r} exited with status {p.poll()} during a query')
+                    line = p.stdout.readline().strip()
+                    if line != 'DONE':
+                        st = p.poll()
+                        raise RuntimeError(f'multi-GPU rank {r} exited with status {st} during a query' if st is not None
+                                           else f'multi-GPU rank {r} answered {line!r} instead of DONE')
                     del pending[r]
 
     def query(self, csr, iv_thr, qlen_cut, nal_cut, pass_table, edge_threshold) -> dict:

@@ -528,6 +528,55 @@ def test_sweep_shard_gloo_two_processes_one_gpu(tmp_path):
         assert not np.load(tmp_path / f'info{r}.npy')[0]
 
 
+def _sweep_gpu_tamper_worker(rank, world, port, out_dir):
+    import torch
+    import torch.distributed as dist
+    from fslr_amd import _lib
+    from fslr_amd.dist import SweepShard, chrom_counts_of
+    from fslr_amd.prep import fold_overlap_threshold, pass_table
+    # capi.hip: ablation bit 64 makes fslr_sweep_partition_repeat expect one entry more for
+    # destination 0 than the synchronous partition wrote, as a partition that landed differently would
+    os.environ['FSLR_ABLATE'] = '64' if rank == 1 else '0'
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    s = synth.generate(20_000, 16, 23)
+    csr = s.interval_data().csr()
+    dev = torch.device('cuda', 0)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    ctx = _lib.Context(0, stream=stream.cuda_stream)
+    ctx.load_csr(csr, fold_overlap_threshold(csr.iv_aln, 0.8))
+    sh = SweepShard(ctx, csr.n_reads, chrom_counts_of(csr), world, rank, dev)
+    pt = pass_table([1, 1, 0.66, 0.66, 0.66, 0.5])
+    sh.step(1 - 0.04, 1 - 0.25, pt, 10)
+    info = sh.step(1 - 0.04, 1 - 0.25, pt, 10, repeat=True)
+    assert info.get('repeat')
+    raised = 0
+    try:
+        sh.verify_repeat()
+    except _lib.FslrError:
+        raised = 1
+    np.save(os.path.join(out_dir, f'raised{rank}.npy'), np.array([raised]))
+    # a synchronous step starts a new series: clean again
+    sh.step(1 - 0.04, 1 - 0.25, pt, 10)
+    assert not ctx.stats()['overflow_flags'] & 32
+    dist.barrier()
+    ctx.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sweep_shard_repeat_mismatch_raises_on_every_rank(tmp_path):
+    """A repeat step whose device partition differs from the synchronous step's (forced on rank 1)
+    is caught by verify_repeat() on both ranks: the flag survives the evaluation that follows the
+    partition (round-3 advice: the per-query reset used to erase it)."""
+    import torch.multiprocessing as mp
+    mp.start_processes(_sweep_gpu_tamper_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True,
+                       start_method='spawn')
+    for r in range(2):
+        assert int(np.load(tmp_path / f'raised{r}.npy')[0]) == 1
+
+
 def test_multi_csr_handoff_roundtrip(tmp_path, world_case):
     """fslr_amd.multi hands the prepared CSR to the rank processes as .npy files: every field the
     ranks upload comes back unchanged, with the query parameters."""
