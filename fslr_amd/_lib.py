@@ -13,7 +13,7 @@ import numpy as np
 
 LIB_PATH = os.environ.get('FSLR_LIB') or os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libfslr_hip.so')
 
-ABI_VERSION = 9          # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
+ABI_VERSION = 10         # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
 FSLR_OK, FSLR_ERR_ZERO_DIVISION, FSLR_ERR_INVALID, FSLR_ERR_HIP, FSLR_ERR_NOMEM, FSLR_ERR_STATE = range(6)
 FSLR_MAX_L = 64
 FSLR_MAX_READS = 1 << 25
@@ -36,7 +36,7 @@ EXPORTED = ['fslr_abi_version', 'fslr_last_error', 'fslr_ctx_create', 'fslr_ctx_
             'fslr_copy_edges_device', 'fslr_components_from_pairs', 'fslr_set_long_reads', 'fslr_long_query',
             'fslr_get_long_edges', 'fslr_copy_edges_iu_device', 'fslr_cap_install_edges', 'fslr_cap_local',
             'fslr_cap_copy_local', 'fslr_cap_replay', 'fslr_get_stage_kernel_times', 'fslr_long_pairs',
-            'fslr_cap_replay_pairs']
+            'fslr_cap_replay_pairs', 'fslr_source_hash']
 
 
 class HipUnavailable(RuntimeError):
@@ -160,8 +160,36 @@ def load(path: str = LIB_PATH):
         fn.argtypes = args
     if L.fslr_abi_version() != ABI_VERSION:
         raise HipUnavailable(f'{path} has ABI {L.fslr_abi_version()}, this binding needs {ABI_VERSION}: rebuild it')
+    L.fslr_source_hash.restype = ctypes.c_char_p
+    L.fslr_source_hash.argtypes = []
+    want = source_hash()
+    if want is not None and os.environ.get('FSLR_ALLOW_STALE') != '1':
+        got = L.fslr_source_hash().decode()
+        if got != want:
+            raise HipUnavailable(f'{path} was built from other sources (hash {got}, the sources beside it hash to '
+                                 f'{want}): rebuild it (make -C fslr_amd/csrc)')
     _lib = L
     return L
+
+
+def source_hash():
+    """The hash the Makefile embeds (fslr_source_hash): sha256 of the sorted csrc/*.hip and *.hpp, then
+    include/fslr_hip.h, first 16 hex digits; None when the sources are not beside the package."""
+    import glob
+    import hashlib
+    here = os.path.dirname(os.path.abspath(__file__))
+    csrc = os.path.join(here, 'csrc')
+    hdr = os.path.join(os.path.dirname(here), 'include', 'fslr_hip.h')
+    files = sorted(os.path.basename(p) for p in glob.glob(os.path.join(csrc, '*.hip')) + glob.glob(os.path.join(csrc, '*.hpp')))
+    if not files or not os.path.exists(hdr):
+        return None
+    h = hashlib.sha256()
+    for f in files:
+        with open(os.path.join(csrc, f), 'rb') as fh:
+            h.update(fh.read())
+    with open(hdr, 'rb') as fh:
+        h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def _ptr(a: np.ndarray):

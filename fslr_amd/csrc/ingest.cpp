@@ -8,6 +8,7 @@
 #include "fslr_ingest.h"
 
 #include <algorithm>
+#include <memory>
 #include <cctype>
 #include <emmintrin.h>
 #include <charconv>
@@ -1031,6 +1032,85 @@ int fslr_fillings(int64_t n_rows, const int32_t *qcode, int64_t n_q, const uint8
     });
     *n_out = base[(size_t)T];
     return FSLR_INGEST_OK;
+}
+
+}  // extern "C"
+
+// ---- prepare_data's start order when every start is distinct (cluster.py:114) ----------------------
+// df.sort_values('start') is numpy's quicksort argsort (pandas nargsort): its order of tied starts is
+// the algorithm's own.  When no two starts tie every sort gives the one order, so a stable parallel
+// LSD radix sort of (start - min, row) stands in; a tie is reported and the caller sorts with numpy.
+extern "C" {
+
+int fslr_argsort_distinct(const int64_t *keys, int64_t n, int64_t *order, int n_threads) {
+    if (n < 0 || (n && (!keys || !order))) return -2;
+    if (n >= (int64_t(1) << 32)) return -1;
+    int T = n_threads;
+    if (T <= 0) T = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    T = (int)std::min<int64_t>(T, std::max<int64_t>(1, n / 65536));
+    if (n == 0) return 1;
+    std::vector<int64_t> lo((size_t)T, INT64_MAX), hi((size_t)T, INT64_MIN);
+    parallel_for(n, T, [&](int64_t a, int64_t e, int w) {
+        int64_t l = INT64_MAX, h = INT64_MIN;
+        for (int64_t i = a; i < e; ++i) {
+            l = std::min(l, keys[i]);
+            h = std::max(h, keys[i]);
+        }
+        lo[(size_t)w] = l;
+        hi[(size_t)w] = h;
+    });
+    const int64_t mn = *std::min_element(lo.begin(), lo.end()), mx = *std::max_element(hi.begin(), hi.end());
+    if ((uint64_t)mx - (uint64_t)mn >= (uint64_t(1) << 32)) return -1;
+    const uint64_t range = (uint64_t)mx - (uint64_t)mn;
+    int bits = 0;
+    while (bits < 32 && (range >> bits)) ++bits;
+    // (key - min) << 32 | row, sorted on bits 32 .. 32 + bits in digits of up to 11 bits
+    // uninitialised (a value-initialised vector zero-fills 2 x 8 B x n on one thread first)
+    std::unique_ptr<uint64_t[]> vb(new uint64_t[(size_t)n]), tb(new uint64_t[(size_t)n]);
+    uint64_t *v = vb.get(), *t = tb.get();
+    parallel_for(n, T, [&](int64_t a, int64_t e, int) {
+        for (int64_t i = a; i < e; ++i) v[i] = ((uint64_t)(keys[i] - mn) << 32) | (uint64_t)i;
+    });
+    constexpr int kD = 11, kB = 1 << kD;
+    const int passes = (bits + kD - 1) / kD;
+    std::vector<int64_t> cnt((size_t)T * kB);
+    for (int ps = 0; ps < passes; ++ps) {
+        const int sh = 32 + ps * kD;
+        std::fill(cnt.begin(), cnt.end(), 0);
+        parallel_for(n, T, [&](int64_t a, int64_t e, int w) {
+            int64_t *c = cnt.data() + (size_t)w * kB;
+            for (int64_t i = a; i < e; ++i) c[(v[i] >> sh) & (kB - 1)]++;
+        });
+        // digit-major, then slice order: stable
+        int64_t acc = 0;
+        for (int d = 0; d < kB; ++d)
+            for (int w = 0; w < T; ++w) {
+                const int64_t x = cnt[(size_t)w * kB + d];
+                cnt[(size_t)w * kB + d] = acc;
+                acc += x;
+            }
+        parallel_for(n, T, [&](int64_t a, int64_t e, int w) {
+            int64_t *c = cnt.data() + (size_t)w * kB;
+            for (int64_t i = a; i < e; ++i) {
+                const uint64_t x = v[i];
+                t[c[(x >> sh) & (kB - 1)]++] = x;
+            }
+        });
+        std::swap(v, t);
+    }
+    std::vector<char> tie((size_t)T, 0);
+    parallel_for(n, T, [&](int64_t a, int64_t e, int w) {
+        bool any = false;
+        for (int64_t i = a; i < e; ++i) {
+            const uint64_t x = v[i];
+            if (i > 0 && (x >> 32) == (v[i - 1] >> 32)) any = true;
+            order[i] = (int64_t)(x & 0xFFFFFFFFu);
+        }
+        tie[(size_t)w] = any;
+    });
+    for (char c : tie)
+        if (c) return 0;
+    return 1;
 }
 
 }  // extern "C"

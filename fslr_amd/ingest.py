@@ -52,6 +52,7 @@ def load(path: str = LIB_PATH):
         'fslr_format_suffix': (i32, [i32, vp, vp, i64, vp, i64, vp]),
         'fslr_group_by_first_appearance': (i32, [vp, i64, i64, vp, vp, vp, vp]),
         'fslr_gather_i64': (i32, [i32, vp, vp, vp, i64, i32]),
+        'fslr_argsort_distinct': (i32, [vp, i64, vp, i32]),
         'fslr_fillings': (i32, [i64, vp, i64, vp] + [vp] * 8 + [vp] + [vp] * 8 + [i32]),
     }
     for name, (res, args) in sig.items():
@@ -282,6 +283,20 @@ def gather_columns(columns, idx, n_threads: int = 0):
     if rc != OK:
         raise RuntimeError('fslr_gather_i64 failed')
     return out
+
+
+def argsort_distinct(keys, n_threads: int = 0):
+    """The argsort of ``keys`` when no two keys tie (then every sort agrees, numpy's quicksort
+    included), by a threaded native radix sort; None when two keys tie, the key range is wider
+    than 2^32 or the library is not built (the caller sorts with numpy)."""
+    keys = np.ascontiguousarray(keys, dtype=np.int64)
+    try:
+        L = load()
+    except FileNotFoundError:
+        return None
+    order = np.empty(keys.size, dtype=np.int64)
+    rc = L.fslr_argsort_distinct(keys.ctypes.data, keys.size, order.ctypes.data, int(n_threads))
+    return order if rc == 1 else None
 
 
 class QnameCodes:

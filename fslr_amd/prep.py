@@ -147,8 +147,16 @@ class IntervalData:
 
 
 def data_order(start: np.ndarray) -> np.ndarray:
-    """Row order of ``df.sort_values('start')`` (pandas nargsort: quicksort argsort, no NaN)."""
-    return np.asarray(start, dtype=np.int64).argsort(kind='quicksort')
+    """Row order of ``df.sort_values('start')`` (pandas nargsort: quicksort argsort, no NaN).  When
+    no two starts tie every sort gives that order, and a threaded radix sort makes it
+    (ingest.argsort_distinct); ties keep numpy's quicksort, whose tie order pandas' is."""
+    start = np.asarray(start, dtype=np.int64)
+    if start.size >= 1 << 16:
+        from . import ingest
+        order = ingest.argsort_distinct(start)
+        if order is not None:
+            return order
+    return start.argsort(kind='quicksort')
 
 
 def mask_keep(chrom, start, end, mask, chromosome_lengths, threshold=500_000) -> np.ndarray:

@@ -68,7 +68,7 @@
 extern "C" {
 #endif
 
-#define FSLR_ABI_VERSION 9
+#define FSLR_ABI_VERSION 10
 #define FSLR_MAX_L 64                /* max intervals per read (bitmask width) */
 #define FSLR_MAX_READS (1 << 25)     /* read rank packs into bits 6..30 of the index record */
 #define FSLR_THR_ZERO_ALN INT32_MIN
@@ -176,6 +176,9 @@ typedef struct {
 } fslr_cap_stats;
 
 int  fslr_abi_version(void);
+/* first 16 hex digits of the sha256 of the kernel sources the library was built from (the sorted
+ * fslr_amd/csrc/*.hip and *.hpp, then this header): a binding can refuse a stale build */
+const char *fslr_source_hash(void);
 const char *fslr_last_error(const fslr_ctx *ctx);
 
 /* device: HIP ordinal; stream: hipStream_t to launch on (NULL = the library creates one). */

@@ -102,6 +102,11 @@ int fslr_fillings(int64_t n_rows, const int32_t *qcode, int64_t n_q, const uint8
                   int64_t *chrom_o, int n_threads);
 int fslr_gather_i64(int n_arrays, const int64_t *const *src, int64_t *const *dst, const int64_t *idx, int64_t n,
                     int n_threads);
+/* prepare_data's start order (cluster.py:114, df.sort_values('start')) when no two keys tie: a
+ * stable radix argsort into order[n].  Returns 1 (every key distinct: the order any sort gives,
+ * pandas' quicksort included), 0 (a tie: order undefined, sort with numpy's quicksort for pandas'
+ * tie order), -1 (max - min >= 2^32 or n >= 2^32: not sorted), -2 bad arguments. */
+int fslr_argsort_distinct(const int64_t *keys, int64_t n, int64_t *order, int n_threads);
 
 #ifdef __cplusplus
 }

@@ -9,6 +9,7 @@ import glob
 import os
 
 import pandas as pd
+import numpy as np
 import pytest
 
 from fslr_amd import ingest
@@ -227,3 +228,22 @@ def test_native_suffix_text_equals_pandas_to_csv():
     assert ends[-1] == len(buf)
     assert ingest.format_suffix(pd.DataFrame({'x': [1.0, float('nan')]})) is None        # na_rep: pandas
     assert ingest.format_suffix(pd.DataFrame({'x': ['a', 'b']})) is None
+
+
+def test_argsort_distinct_radix_matches_numpy():
+    """prepare_data's start order (cluster.py:114): the native radix argsort stands in for numpy's
+    quicksort only when no two starts tie (then every sort agrees); a tie or a key range wider than
+    2^32 hands the sort back to numpy, whose tie order is pandas'."""
+    from fslr_amd import ingest
+    from fslr_amd.prep import data_order
+    rng = np.random.default_rng(5)
+    for n in (1, 2, 1000, 70_000, 400_000):
+        k = (rng.permutation(3 * n)[:n].astype(np.int64) - n) * 5
+        o = ingest.argsort_distinct(k, n_threads=3)
+        assert o is not None
+        np.testing.assert_array_equal(o, np.argsort(k, kind='stable'))
+        np.testing.assert_array_equal(data_order(k), np.argsort(k, kind='quicksort'))
+    tied = rng.integers(0, 5000, 100_000)
+    assert ingest.argsort_distinct(tied) is None
+    np.testing.assert_array_equal(data_order(tied), tied.astype(np.int64).argsort(kind='quicksort'))
+    assert ingest.argsort_distinct(np.array([0, 1 << 33], dtype=np.int64)) is None
