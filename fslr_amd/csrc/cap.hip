@@ -39,6 +39,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -611,6 +612,96 @@ __global__ __launch_bounds__(256) void k_cap_replay(const unsigned long long* __
   }
 }
 
+// ---- 4'. the loops in dependency order (k_cap_replay_dag) ------------------------------------------
+// x's loop needs only the finished loops of its earlier partners in T (replay_read reads their
+// pbrk and the visit marks of their slots for x).  Those form a DAG in rank order, so a loop can
+// run as soon as its last earlier T partner has finished: a ready queue instead of one wavefront
+// per component, which keeps a large component's chain of loops from running one after the other.
+// Slots of one t are contiguous in ukey (sorted by t, then partner): sbeg / send.
+__global__ void k_cap_dag_bounds(const unsigned long long* __restrict__ ukey, int ns, int* __restrict__ sbeg,
+                                 int* __restrict__ send) {
+  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < ns; s += gridDim.x * blockDim.x) {
+    const int t = static_cast<int>(ukey[s] >> 25);
+    if (s == 0 || static_cast<int>(ukey[s - 1] >> 25) != t) sbeg[t] = s;
+    if (s == ns - 1 || static_cast<int>(ukey[s + 1] >> 25) != t) send[t] = s + 1;
+  }
+}
+
+// earlier T partners per read (k_cap_mirror's upairs: (t, ty) for a partner ty of T before x)
+__global__ void k_cap_dag_indeg(const int2* __restrict__ upairs, int ns, int* __restrict__ indeg) {
+  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < ns; s += gridDim.x * blockDim.x) {
+    const int2 u = upairs[s];
+    if (u.x >= 0) atomicAdd(indeg + u.x, 1);
+  }
+}
+
+// the reads with no earlier T partner start the queue (rank order inside each wave)
+__global__ void k_cap_dag_seed(const int* __restrict__ indeg, int nt, int* __restrict__ ready,
+                               unsigned* __restrict__ qtail) {
+  const int lane = threadIdx.x & 63;
+  for (int t0 = (blockIdx.x * blockDim.x + threadIdx.x) & ~63; t0 < nt; t0 += gridDim.x * blockDim.x) {
+    const int t = t0 + lane;
+    const bool r = t < nt && indeg[t] == 0;
+    const unsigned long long m = __ballot(r);
+    if (!m) continue;
+    unsigned base = 0;
+    if (lane == 0) base = atomicAdd(qtail, static_cast<unsigned>(__popcll(m)));
+    base = static_cast<unsigned>(__shfl(static_cast<int>(base), 0));
+    if (r) ready[base + mbcnt(m)] = t;
+  }
+}
+
+constexpr long long kDagSpinTicks = 50000000;   // s_memrealtime at 100 MHz: 0.5 s without a ready loop
+
+// One wavefront per loop at a time: take the next queue position, wait for its read, replay it,
+// then release the later T partners whose last earlier partner it was.  Every position below nt
+// is filled exactly once (each read's in-degree reaches 0 once; the smallest unfinished rank always
+// has every earlier partner done), and a wave leaves when the positions run out; a wave that sees
+// no read arrive for kDagSpinTicks flags err[1] and leaves (the host then runs k_cap_replay).
+__global__ __launch_bounds__(256) void k_cap_replay_dag(int nt, int thr, const int* __restrict__ T,
+                                                        const int* __restrict__ t_of, const int* __restrict__ toff,
+                                                        const int* __restrict__ ioff, const int4* __restrict__ rec,
+                                                        const int* __restrict__ fpos,
+                                                        const unsigned long long* __restrict__ ukey,
+                                                        const int* __restrict__ sbeg, const int* __restrict__ send,
+                                                        int* indeg, int* ready, unsigned* queue, unsigned char* vis2,
+                                                        int* pbrk, int* own, int* err) {
+  const int lane = threadIdx.x & 63;
+  while (true) {
+    unsigned k = 0;
+    if (lane == 0) k = atomicAdd(queue, 1u);                     // queue[0]: next position to take
+    k = static_cast<unsigned>(__shfl(static_cast<int>(k), 0));
+    if (k >= static_cast<unsigned>(nt)) return;
+    int t = __hip_atomic_load(ready + k, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    if (t < 0) {
+      const long long t0 = wall_clock64();
+      while (t < 0) {
+        __builtin_amdgcn_s_sleep(4);
+        t = __hip_atomic_load(ready + k, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        if (t < 0 && wall_clock64() - t0 > kDagSpinTicks) {
+          if (lane == 0) atomicOr(err + 1, 1);
+          return;
+        }
+      }
+    }
+    replay_read(t, lane, thr, toff, ioff, rec, fpos, vis2, pbrk, own, err);   // a ZeroDivisionError is in err
+    __threadfence();                       // this loop's pbrk / own / visit marks before the releases
+    const int x = T[t];
+    for (int s0 = sbeg[t]; s0 < send[t]; s0 += 64) {
+      const int s = s0 + lane;
+      int t2 = -1;
+      if (s < send[t]) {
+        const int y = static_cast<int>(ukey[s] & kKeyMask);
+        if (y > x) t2 = t_of[y];
+      }
+      if (t2 >= 0 && __hip_atomic_fetch_add(indeg + t2, -1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == 1) {
+        const unsigned slot = atomicAdd(queue + 1, 1u);                // queue[1]: next position to fill
+        __hip_atomic_store(ready + slot, t2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
 // ---- 5. the capped graph -----------------------------------------------------------------------
 __device__ __forceinline__ bool loop_reaches(int x, int y, const int* __restrict__ t_of,
                                              const int* __restrict__ pbrk, const unsigned long long* __restrict__ ukey,
@@ -832,6 +923,8 @@ struct CapWork {
   // phase 1
   int *tread = nullptr, *tq = nullptr, *icnt = nullptr, *ioff = nullptr, *pbrk = nullptr, *own = nullptr,
       *tpar = nullptr;
+  int *sbeg = nullptr, *send = nullptr, *indeg = nullptr, *ready = nullptr;   // the loops' dependency DAG
+  unsigned* queue = nullptr;
   unsigned long long *ck = nullptr, *ck2 = nullptr;
   // phase 2 (local lists: seqp, seq; then the sequence)
   int *seqp = nullptr, *seq = nullptr, *sval = nullptr, *sval2 = nullptr, *head = nullptr, *hs = nullptr,
@@ -1010,6 +1103,11 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, int64_t ne, bool all_reads = fal
     cv.add(&w->tpar, nt);
     cv.add(&w->ck, nt);
     cv.add(&w->ck2, nt);
+    cv.add(&w->sbeg, nt);
+    cv.add(&w->send, nt);
+    cv.add(&w->indeg, nt);
+    cv.add(&w->ready, nt);
+    cv.add(&w->queue, 4);
     if (int rc = cv.commit(c, w->ar[1])) return rc;
   }
   if (nt > 0) {
@@ -1102,6 +1200,15 @@ int cap_slots(fslr_ctx* c, CapWork* w) {
   return FSLR_OK;
 }
 
+// FSLR_CAP_REPLAY=components: the round-3 replay (one wavefront per dependency component), for A/B
+bool cap_dag_disabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("FSLR_CAP_REPLAY");
+    return e && std::strcmp(e, "components") == 0;
+  }();
+  return v;
+}
+
 int cap_core(fslr_ctx* c, CapWork* w, fslr_cap_stats* cs) {
   hipStream_t s = c->stream;
   const int thr = w->thr;
@@ -1111,21 +1218,48 @@ int cap_core(fslr_ctx* c, CapWork* w, fslr_cap_stats* cs) {
   if (int rc = cap_slots(c, w)) return rc;
   const int ns = static_cast<int>(w->ns);
   if (m > 0) {
-    // mirror slots, the dependency components
+    // mirror slots; each read's earlier T partners (its in-degree in the loops' dependency DAG)
     k_cap_mirror<<<grid_for(ns), 256, 0, s>>>(w->ukey, ns, w->T, w->t_of, w->mslot, w->upairs, w->err);
-    HIP_TRY(c, hipGetLastError());
-    HIP_TRY(c, launch_uf_init(w->tpar, nt, s));
-    HIP_TRY(c, launch_uf_pair_list(w->tpar, w->upairs, ns, s));
-    HIP_TRY(c, launch_uf_finalize(w->tpar, nt, s));
-    k_cap_ckeys<<<grid_for(nt), 256, 0, s>>>(w->tpar, nt, w->ck);
-    size_t tb = w->temp_bytes;
-    HIP_TRY(c, hipcub::DeviceRadixSort::SortKeys(w->temp, tb, w->ck, w->ck2, nt, 0, 50, s));
     k_cap_recs<<<grid_for(m), 256, 0, s>>>(w->slot_of, w->ukey, w->fpos, w->flags, w->mslot, w->T, w->t_of, m, w->rec);
     HIP_TRY(c, hipMemsetAsync(w->vis2, 0, static_cast<size_t>(ns), s));
-    // 4. the loops
-    k_cap_replay<<<wave_grid(nt), 256, 0, s>>>(w->ck2, nt, thr, w->toff, w->ioff, w->rec, w->fpos, w->vis2, w->pbrk,
-                                               w->own, w->err);
-    HIP_TRY(c, hipGetLastError());
+    bool dag_ok = false;
+    if (!cap_dag_disabled()) {
+      HIP_TRY(c, hipMemsetAsync(w->sbeg, 0, static_cast<size_t>(nt) * sizeof(int), s));
+      HIP_TRY(c, hipMemsetAsync(w->send, 0, static_cast<size_t>(nt) * sizeof(int), s));
+      HIP_TRY(c, hipMemsetAsync(w->indeg, 0, static_cast<size_t>(nt) * sizeof(int), s));
+      HIP_TRY(c, hipMemsetAsync(w->ready, 0xff, static_cast<size_t>(nt) * sizeof(int), s));
+      HIP_TRY(c, hipMemsetAsync(w->queue, 0, 4 * sizeof(unsigned), s));
+      k_cap_dag_bounds<<<grid_for(ns), 256, 0, s>>>(w->ukey, ns, w->sbeg, w->send);
+      k_cap_dag_indeg<<<grid_for(ns), 256, 0, s>>>(w->upairs, ns, w->indeg);
+      k_cap_dag_seed<<<grid_for(nt), 256, 0, s>>>(w->indeg, nt, w->ready, w->queue + 1);
+      // 4. the loops, each as soon as its earlier T partners' loops are done
+      k_cap_replay_dag<<<std::min(wave_grid(nt), 2048), 256, 0, s>>>(nt, thr, w->T, w->t_of, w->toff, w->ioff, w->rec,
+                                                                    w->fpos, w->ukey, w->sbeg, w->send, w->indeg,
+                                                                    w->ready, w->queue, w->vis2, w->pbrk, w->own,
+                                                                    w->err);
+      HIP_TRY(c, hipGetLastError());
+      int derr[2] = {0, 0};
+      HIP_TRY(c, hipMemcpyAsync(derr, w->err, sizeof(derr), hipMemcpyDeviceToHost, s));
+      HIP_TRY(c, hipStreamSynchronize(s));
+      dag_ok = derr[1] == 0;
+      if (!dag_ok) {                     // a loop never became ready (cannot happen): replay per component
+        std::fprintf(stderr, "fslr: edge-cap DAG replay stalled; replaying per component\n");
+        HIP_TRY(c, hipMemsetAsync(w->err + 1, 0, sizeof(int), s));
+        HIP_TRY(c, hipMemsetAsync(w->vis2, 0, static_cast<size_t>(ns), s));
+      }
+    }
+    if (!dag_ok) {
+      // the dependency components, one wavefront per component, its reads in rank order
+      HIP_TRY(c, launch_uf_init(w->tpar, nt, s));
+      HIP_TRY(c, launch_uf_pair_list(w->tpar, w->upairs, ns, s));
+      HIP_TRY(c, launch_uf_finalize(w->tpar, nt, s));
+      k_cap_ckeys<<<grid_for(nt), 256, 0, s>>>(w->tpar, nt, w->ck);
+      size_t tb = w->temp_bytes;
+      HIP_TRY(c, hipcub::DeviceRadixSort::SortKeys(w->temp, tb, w->ck, w->ck2, nt, 0, 50, s));
+      k_cap_replay<<<wave_grid(nt), 256, 0, s>>>(w->ck2, nt, thr, w->toff, w->ioff, w->rec, w->fpos, w->vis2,
+                                                 w->pbrk, w->own, w->err);
+      HIP_TRY(c, hipGetLastError());
+    }
   } else if (nt > 0) {
     // no T read has a hit: no loop breaks
     k_fill<<<grid_for(nt), 256, 0, s>>>(w->pbrk, nt, kInf);

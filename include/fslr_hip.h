@@ -177,7 +177,7 @@ typedef struct {
 
 int  fslr_abi_version(void);
 /* first 16 hex digits of the sha256 of the kernel sources the library was built from (the sorted
- * fslr_amd/csrc/*.hip and *.hpp, then this header): a binding can refuse a stale build */
+ * .hip and .hpp files of fslr_amd/csrc, then this header): a binding can refuse a stale build */
 const char *fslr_source_hash(void);
 const char *fslr_last_error(const fslr_ctx *ctx);
 
