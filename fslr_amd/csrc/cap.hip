@@ -102,6 +102,68 @@ __global__ void k_cap_join(const int* __restrict__ fwd, int n, int thr, int* __r
   if (__ballot(any) && (threadIdx.x & 63) == 0) atomicOr(chg, 1);
 }
 
+// The same fixed point by frontiers (the operator is monotone, so adding reads in any order as soon
+// as they reach the cap ends at the same least fixed point): E* grouped by its lower read once, then
+// each round walks only the forward edges of the reads that joined in the previous round.
+__global__ void k_cap_adj_count(const int2* __restrict__ edges, long long ne, int* __restrict__ cnt) {
+  for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < ne;
+       k += static_cast<long long>(gridDim.x) * blockDim.x)
+    atomicAdd(cnt + edges[k].x, 1);
+}
+
+__global__ void k_cap_adj_fill(const int2* __restrict__ edges, long long ne, const int* __restrict__ aoff,
+                               int* __restrict__ cur, int* __restrict__ adj) {
+  for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < ne;
+       k += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const int2 e = edges[k];
+    adj[aoff[e.x] + atomicAdd(cur + e.x, 1)] = e.y;
+  }
+}
+
+// the seeds: reads whose own forward degree reaches the cap (frontier 0)
+__global__ void k_cap_seed(const int* __restrict__ fwd, int n, int thr, int* __restrict__ state,
+                           int* __restrict__ back, int* __restrict__ fl, unsigned* __restrict__ fn) {
+  const int lane = threadIdx.x & 63;
+  for (int x0 = (blockIdx.x * blockDim.x + threadIdx.x) & ~63; x0 < n; x0 += gridDim.x * blockDim.x) {
+    const int x = x0 + lane;
+    const bool j = x < n && fwd[x] >= thr;
+    if (x < n) {
+      state[x] = j ? 1 : 0;
+      back[x] = 0;
+    }
+    const unsigned long long m = __ballot(j);
+    if (!m) continue;
+    unsigned base = 0;
+    if (lane == 0) base = atomicAdd(fn, static_cast<unsigned>(__popcll(m)));
+    base = static_cast<unsigned>(__shfl(static_cast<int>(base), 0));
+    if (j) fl[base + mbcnt(m)] = x;
+  }
+}
+
+// one round: every forward edge (x, y) of a read x that joined last round counts for y; y joins (and
+// enters the next frontier) when its forward degree plus those counts reaches the cap
+__global__ void k_cap_frontier(const int* __restrict__ aoff, const int* __restrict__ adj, const int* __restrict__ fwd,
+                               int thr, int* __restrict__ state, int* __restrict__ back, const int* __restrict__ fin,
+                               const unsigned* __restrict__ fin_n, int* __restrict__ fout, unsigned* __restrict__ fout_n) {
+  const int nin = static_cast<int>(*fin_n);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nin; i += gridDim.x * blockDim.x) {
+    const int x = fin[i];
+    for (int k = aoff[x]; k < aoff[x + 1]; ++k) {
+      const int y = adj[k];
+      const int b = atomicAdd(back + y, 1) + 1;
+      if (fwd[y] + b >= thr && atomicCAS(state + y, 0, 1) == 0) fout[atomicAdd(fout_n, 1u)] = y;
+    }
+  }
+}
+
+__global__ void k_cap_fcnt_roll(unsigned* fcnt) {
+  if (threadIdx.x == 0) {
+    const unsigned v = fcnt[16];
+    for (int k = 1; k < 64; ++k) fcnt[k] = 0;
+    fcnt[0] = v;
+  }
+}
+
 // T in rank order: one scan of (1 << 32 | L) gives each member its index t and its first T-interval
 // read x's interval count: rlen (reads of more than FSLR_MAX_L intervals, real-read space) or rmeta
 __device__ __forceinline__ int read_len(const int4* __restrict__ rmeta, const int* __restrict__ rlen, int x) {
@@ -914,6 +976,8 @@ struct CapWork {
   int n_umax = FSLR_MAX_L;
   // phase 0
   int *state = nullptr, *back = nullptr, *t_of = nullptr, *T = nullptr, *toff = nullptr, *formed = nullptr;
+  int *aoff = nullptr, *acur = nullptr, *adj = nullptr, *fl0 = nullptr, *fl1 = nullptr;   // frontier closure
+  unsigned* fcnt = nullptr;
   unsigned long long *tv = nullptr, *tvs = nullptr;
   int *chg = nullptr, *err = nullptr, *kflag = nullptr, *koff = nullptr;
   long long* stats = nullptr;
@@ -1026,6 +1090,24 @@ void set_space(fslr_ctx* c, CapWork* w) {
   }
 }
 
+// FSLR_CAP_CLOSURE=rounds: the round-3 closure (every edge and read each round), for A/B
+bool cap_rounds_closure() {
+  static const bool v = [] {
+    const char* e = std::getenv("FSLR_CAP_CLOSURE");
+    return e && std::strcmp(e, "rounds") == 0;
+  }();
+  return v;
+}
+
+// FSLR_CAP_REPLAY=components: the round-3 replay (one wavefront per dependency component), for A/B
+bool cap_dag_disabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("FSLR_CAP_REPLAY");
+    return e && std::strcmp(e, "components") == 0;
+  }();
+  return v;
+}
+
 // Phase A: the closure T (all_reads: every read, fslr_long_pairs), the T-intervals and their
 // local hit counts; the local visit lists (partner reads, search order) at w->seq[0 .. nloc),
 // segments at w->ioff (local counts).
@@ -1054,15 +1136,55 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, int64_t ne, bool all_reads = fal
     cv.add(&w->who, ne);
     cv.add(&w->oedges, ne);
     cv.add(&w->oiu, ne);
+    cv.add(&w->aoff, n + 1);
+    cv.add(&w->acur, n);
+    cv.add(&w->adj, ne);
+    cv.add(&w->fl0, n);
+    cv.add(&w->fl1, n);
+    cv.add(&w->fcnt, 64);
     if (int rc = cv.commit(c, w->ar[0])) return rc;
   }
   HIP_TRY(c, hipMemsetAsync(w->err, 0, 4 * sizeof(int), s));
   HIP_TRY(c, hipMemsetAsync(w->stats, 0, kStWords * sizeof(long long), s));
-  // 1. closure: rounds in batches of 8, one sync per batch (chg[0] = 1 starts each batch)
+  // 1. closure.  Frontier rounds (batches of 16, one sync per batch), or FSLR_CAP_CLOSURE=rounds:
+  // rounds over every edge and read in batches of 8 (chg[0] = 1 starts each batch)
+  const bool frontier = !all_reads && !cap_rounds_closure();
   if (all_reads) k_cap_all<<<grid_for(n), 256, 0, s>>>(w->state, static_cast<int>(n));
-  else k_cap_init<<<grid_for(n), 256, 0, s>>>(c->fwd, static_cast<int>(n), thr, w->state, w->back);
+  else if (!frontier) k_cap_init<<<grid_for(n), 256, 0, s>>>(c->fwd, static_cast<int>(n), thr, w->state, w->back);
   HIP_TRY(c, hipGetLastError());
-  for (int batch = 0; !all_reads; ++batch) {
+  if (frontier) {
+    HIP_TRY(c, hipMemsetAsync(w->acur, 0, static_cast<size_t>(n) * sizeof(int), s));
+    HIP_TRY(c, hipMemsetAsync(w->fcnt, 0, 64 * sizeof(unsigned), s));
+    if (ne > 0) k_cap_adj_count<<<grid_for(ne), 256, 0, s>>>(c->edges, ne, w->acur);
+    // aoff[0] = 0, aoff[1 .. n] = the inclusive scan of the counts
+    size_t tb = 0;
+    HIP_TRY(c, hipcub::DeviceScan::InclusiveSum(nullptr, tb, w->acur, w->aoff + 1, static_cast<int>(n), s));
+    if (int rc = ensure_temp(c, w, tb)) return rc;
+    tb = w->temp_bytes;
+    HIP_TRY(c, hipcub::DeviceScan::InclusiveSum(w->temp, tb, w->acur, w->aoff + 1, static_cast<int>(n), s));
+    HIP_TRY(c, hipMemsetAsync(w->aoff, 0, sizeof(int), s));
+    HIP_TRY(c, hipMemsetAsync(w->acur, 0, static_cast<size_t>(n) * sizeof(int), s));
+    if (ne > 0) k_cap_adj_fill<<<grid_for(ne), 256, 0, s>>>(c->edges, ne, w->aoff, w->acur, w->adj);
+    k_cap_seed<<<grid_for(n), 256, 0, s>>>(c->fwd, static_cast<int>(n), thr, w->state, w->back, w->fl0, w->fcnt);
+    HIP_TRY(c, hipGetLastError());
+    int* fl[2] = {w->fl0, w->fl1};
+    for (int batch = 0;; ++batch) {
+      // rounds r = 0 .. 15 of the batch: frontier fl[r & 1] (count fcnt[r]) -> fl[(r + 1) & 1] (fcnt[r + 1])
+      for (int r = 0; r < 16; ++r)
+        k_cap_frontier<<<1024, 256, 0, s>>>(w->aoff, w->adj, c->fwd, thr, w->state, w->back, fl[r & 1], w->fcnt + r,
+                                            fl[(r + 1) & 1], w->fcnt + r + 1);
+      HIP_TRY(c, hipGetLastError());
+      unsigned last = 0;
+      HIP_TRY(c, hipMemcpyAsync(&last, w->fcnt + 16, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+      HIP_TRY(c, hipStreamSynchronize(s));
+      if (!last) break;
+      if (batch > (n >> 4) + 2) return fail(c, FSLR_ERR_STATE, "edge cap closure does not converge");
+      // the next batch starts from frontier fl[0] (16 rounds: an even count) with fcnt[0] = fcnt[16]
+      k_cap_fcnt_roll<<<1, 64, 0, s>>>(w->fcnt);
+      HIP_TRY(c, hipGetLastError());
+    }
+  }
+  for (int batch = 0; !all_reads && !frontier; ++batch) {
     HIP_TRY(c, hipMemsetAsync(w->chg, 0, 16 * sizeof(int), s));
     HIP_TRY(c, hipMemsetAsync(w->chg, 0xff, sizeof(int), s));
     for (int r = 1; r <= 8; ++r) {
@@ -1198,15 +1320,6 @@ int cap_slots(fslr_ctx* c, CapWork* w) {
                                            c->last_ncut, w->umax, w->n_umax, w->flags);
   HIP_TRY(c, hipGetLastError());
   return FSLR_OK;
-}
-
-// FSLR_CAP_REPLAY=components: the round-3 replay (one wavefront per dependency component), for A/B
-bool cap_dag_disabled() {
-  static const bool v = [] {
-    const char* e = std::getenv("FSLR_CAP_REPLAY");
-    return e && std::strcmp(e, "components") == 0;
-  }();
-  return v;
 }
 
 int cap_core(fslr_ctx* c, CapWork* w, fslr_cap_stats* cs) {
