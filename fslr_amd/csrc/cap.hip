@@ -794,7 +794,10 @@ __global__ void k_cap_classify(const int2* __restrict__ edges, long long ne, con
     else if (loop_reaches(e.y, e.x, t_of, pbrk, ukey, ns, fpos, vis2, err)) w = 1;
     who[k] = static_cast<unsigned char>(w);
     kflag[k] = w != 2;
-    if (w != 2) atomicAdd(formed + (w == 0 ? e.x : e.y), 1);
+    // formed starts as the E* forward degrees (every edge in its lower read's loop): only an edge
+    // formed in the higher read's loop, or dropped, moves a count (no atomic for the many others)
+    if (w != 0) atomicSub(formed + e.x, 1);
+    if (w == 1) atomicAdd(formed + e.y, 1);
     drop += w == 2;
     bwd += w == 1;
   }
@@ -1381,7 +1384,9 @@ int cap_core(fslr_ctx* c, CapWork* w, fslr_cap_stats* cs) {
   }
   w->ns = ns;
   // 5. the capped graph
-  HIP_TRY(c, hipMemsetAsync(w->formed, 0, static_cast<size_t>(n) * sizeof(int), s));
+  // edges formed per loop, from the E* forward degrees (fwd[x] = E* edges (x, .), as the query or the
+  // install left them)
+  HIP_TRY(c, hipMemcpyAsync(w->formed, c->fwd, static_cast<size_t>(n) * sizeof(int), hipMemcpyDeviceToDevice, s));
   if (ne > 0) {
     k_cap_classify<<<grid_for(ne), 256, 0, s>>>(c->edges, ne, w->t_of, w->pbrk, w->ukey, ns, w->fpos, w->vis2,
                                                 w->kflag, w->who, w->formed, w->stats, w->err);
