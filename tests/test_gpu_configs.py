@@ -170,3 +170,33 @@ def test_config4_1m_product_split_w8_vs_oracle(thr):
     finally:
         for c in ctxs:
             c.close()
+
+
+@pytest.mark.slow
+def test_config5_10m_product_split_w8_capped_vs_oracle():
+    """North star's config 5 (10M reads x 1-64 Zipf, the cap binding) through the product's
+    chromosome split on W = 8 contexts: partition, entry exchange, evaluation, then dist.SweepShard's
+    capped path (E* rows gathered, each rank's chromosomes' hit lists gathered, the replay) — every
+    rank's capped graph (edges with I, U; edges per loop) and labels have the digests of the
+    oracle's full run (tests/golden/cfg5/full_capped.json)."""
+    from make_cfg5_full import digests
+    from test_dist import _sweep_split_capped_on_device
+    with open(os.path.join(GOLDEN, 'cfg5', 'sample50k_capped.json')) as fh:
+        meta = json.load(fh)
+    with open(os.path.join(GOLDEN, 'cfg5', 'full_capped.json')) as fh:
+        ref = json.load(fh)
+    want = {k: ref[k] for k in ('edges_sha256', 'fwd_sha256', 'labels_sha256', 'n_edges', 'max_fwd')}
+    s = synth.generate(meta['reads'], meta['lmax'], meta['seed'], dist=meta['dist'])
+    csr = s.interval_data().csr()
+    del s
+    assert csr.n_intervals == meta['n_intervals']
+    ctxs, cap = _sweep_split_capped_on_device(csr, fold_overlap_threshold(csr.iv_aln, 0.8), pass_table(CUTS), 8, 10)
+    try:
+        assert cap['applied'] == 1 and cap['dropped'] > 0
+        for c in ctxs:
+            a, b, I, U = c.edges(c.stats()['n_edges'])
+            d = digests(a, b, I, U, c.fwd_degree(), c.labels())
+            assert {k: d[k] for k in want} == want
+    finally:
+        for c in ctxs:
+            c.close()
