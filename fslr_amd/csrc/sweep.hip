@@ -93,9 +93,19 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
   // rank's share of the multi-GPU split), so every wave gets work: the sweep is latency bound
   const int run = max(1, min(kTileRun, nt / nw));
   const int nchunks = (nt + run - 1) / run;
-  // chunks dealt grid-stride (per-XCD work queues were tried: 0.241 -> 0.260 ms at cfg3, the
-  // tickets' latency and the lost neighbour order cost more than the balance gained)
-  for (int chunk = wid; chunk < nchunks; chunk += nw)
+  // XCD-aware: workgroup b runs on XCD b % 8 (the usual dispatch; it only affects speed), and each
+  // XCD takes one contiguous eighth of the chunks, dealt to its waves in order — a chunk's forward
+  // window runs into the next chunk's positions, which a neighbouring wave of the same XCD (often of
+  // the same workgroup) reads at about the same time, so the overlap is served by that XCD's L2
+  // instead of being fetched again by another XCD.  (Per-XCD work queues were tried in round 3:
+  // 0.241 -> 0.260 ms at cfg3, the tickets' latency cost more than the balance gained.)
+  const int nx = min(8, static_cast<int>(gridDim.x));                    // XCDs in use
+  const int xcd = static_cast<int>(blockIdx.x) % nx;
+  const int bpx = (static_cast<int>(gridDim.x) - xcd + nx - 1) / nx;      // workgroups on this XCD
+  const int wx = static_cast<int>(blockIdx.x) / nx * kSwWaves + wv;        // wave index inside the XCD
+  const int c_lo = static_cast<int>((static_cast<long long>(nchunks) * xcd) / nx);
+  const int c_hi = static_cast<int>((static_cast<long long>(nchunks) * (xcd + 1)) / nx);
+  for (int chunk = c_lo + wx; chunk < c_hi; chunk += bpx * kSwWaves)
   for (int tile = chunk * run; tile < min(nt, (chunk + 1) * run); ++tile) {
     const int q0 = tile * kWave;
     const int q = q0 + lane;
