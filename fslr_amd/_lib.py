@@ -36,7 +36,7 @@ EXPORTED = ['fslr_abi_version', 'fslr_last_error', 'fslr_ctx_create', 'fslr_ctx_
             'fslr_copy_edges_device', 'fslr_components_from_pairs', 'fslr_set_long_reads', 'fslr_long_query',
             'fslr_get_long_edges', 'fslr_copy_edges_iu_device', 'fslr_cap_install_edges', 'fslr_cap_local',
             'fslr_cap_copy_local', 'fslr_cap_replay', 'fslr_get_stage_kernel_times', 'fslr_long_pairs',
-            'fslr_cap_replay_pairs', 'fslr_source_hash']
+            'fslr_cap_replay_pairs', 'fslr_source_hash', 'fslr_set_reads_any', 'fslr_set_long_cutoffs']
 
 
 class HipUnavailable(RuntimeError):
@@ -144,6 +144,8 @@ def load(path: str = LIB_PATH):
         'fslr_copy_edges_device': (ctypes.c_int, [vp, vp, i64]),
         'fslr_components_from_pairs': (ctypes.c_int, [vp, vp, i64]),
         'fslr_set_long_reads': (ctypes.c_int, [vp, i64, vp, vp, vp, vp, i32]),
+        'fslr_set_reads_any': (ctypes.c_int, [vp, ctypes.POINTER(Reads)]),
+        'fslr_set_long_cutoffs': (ctypes.c_int, [vp, vp, i32]),
         'fslr_long_query': (ctypes.c_int, [vp, ctypes.POINTER(Params), ctypes.POINTER(ctypes.c_int64)]),
         'fslr_get_long_edges': (ctypes.c_int, [vp, vp, vp, vp, vp, i64]),
         'fslr_long_pairs': (ctypes.c_int, [vp, ctypes.POINTER(Params), ctypes.POINTER(ctypes.c_int64)]),
@@ -260,6 +262,24 @@ class Context:
         if arrs[2].size and (arrs[2].min() < 0 or arrs[2].max() >= (1 << 24)):
             raise ValueError('n_alignments must lie in [0, 2**24) for the device path')
         self.n_reads = len(arrs[1])
+
+    def load_csr_any(self, csr, iv_thr):
+        """Upload a CSR whose reads may have more than FSLR_MAX_L intervals (fslr_set_reads_any: the
+        library splits them into chunks); thresholds here and in set_thresholds are in
+        the CSR's own interval order.  Labels and forward degrees then cover the virtual reads (the
+        real reads first)."""
+        arrs = [np.ascontiguousarray(x, dtype=np.int32) for x in
+                (csr.read_off, csr.read_qlen2, csr.read_nal, csr.iv_chrom, csr.iv_start, csr.iv_end, iv_thr)]
+        dp = np.ascontiguousarray(csr.data_pos, dtype=np.int32) if getattr(csr, 'start_sorted', True) else None
+        r = Reads(len(arrs[1]), len(arrs[3]), int(csr.n_chroms), *(_ptr(a) for a in arrs),
+                  _ptr(dp) if dp is not None else None)
+        self._check(self._L.fslr_set_reads_any(self._h, ctypes.byref(r)))
+        L = np.diff(arrs[0].astype(np.int64))
+        self.n_reads = int(len(arrs[1]) + np.maximum((L + FSLR_MAX_L - 1) // FSLR_MAX_L - 1, 0).sum())
+
+    def set_long_cutoffs(self, umax):
+        u = np.ascontiguousarray(umax, dtype=np.int32)
+        self._check(self._L.fslr_set_long_cutoffs(self._h, _ptr(u), int(u.size)))
 
     def load_csr(self, csr, iv_thr):
         """Upload a ``fslr_amd.prep.CSR`` (with its start-sorted data order) and thresholds."""

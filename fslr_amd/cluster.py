@@ -32,7 +32,7 @@ import pandas as pd
 from . import bam_header, ingest, multi
 from ._lib import FSLR_MAX_L, FSLR_THR_ZERO_ALN, Context
 from .prep import (IntervalData, IntervalItem, build_csr, data_order, first_last_masks, fold_overlap_threshold,
-                   group_span, has_long_reads, mask_keep, pass_table, split_long_reads, umax_table)
+                   group_span, has_long_reads, mask_keep, pass_table, umax_table)
 
 __all__ = ['IntervalItem', 'keep_fillings', 'rename_chromosomes', 'chrom_to_str', 'calc_coverage',
            'filter_high_coverage', 'delete_false', 'mask_sequences2', 'prepare_data', 'build_interval_trees',
@@ -190,11 +190,14 @@ class DeviceIntervalIndex:
         self.csr = data.csr()
         self.ctx = ctx or Context(_default_device() if device is None else device)
         c = self.csr
-        # reads of more than FSLR_MAX_L intervals: the virtual CSR of the long-read stage
-        self.long = split_long_reads(c) if has_long_reads(c) else None
-        up = self.long[0] if self.long is not None else c
-        thr0 = np.where(up.iv_aln == 0, FSLR_THR_ZERO_ALN, 0).astype(np.int32)
-        self.ctx.load_csr(up, thr0)
+        thr0 = np.where(c.iv_aln == 0, FSLR_THR_ZERO_ALN, 0).astype(np.int32)
+        # reads of more than FSLR_MAX_L intervals: the library uploads them as FSLR_MAX_L-interval
+        # chunks (fslr_set_reads_any); self.long = the real reads' lengths
+        self.long = np.diff(np.asarray(c.read_off, np.int64)).astype(np.int32) if has_long_reads(c) else None
+        if self.long is not None:
+            self.ctx.load_csr_any(c, thr0)
+        else:
+            self.ctx.load_csr(c, thr0)
         self.ctx.build_index()
 
 
@@ -405,14 +408,14 @@ def _query_long(idx, overlap_cutoff, jaccard_threshold, edge_threshold, qlen_dif
     per-read cap (cluster.py:223-224) is replayed over E* in the real-read space
     (fslr_cap_replay_pairs)."""
     csr, ctx = idx.csr, idx.ctx
-    vcsr, vreal, vbase, rlen = idx.long
+    rlen = idx.long
     n = csr.n_reads
-    thr = fold_overlap_threshold(vcsr.iv_aln, overlap_cutoff)
+    thr = fold_overlap_threshold(csr.iv_aln, overlap_cutoff)           # the real CSR's order
     lg = rlen > FSLR_MAX_L
-    fast = (multi.sweep_applies(vcsr, thr) and not (csr.read_qlen2[lg] == 0).any()
+    fast = (multi.sweep_applies(csr, thr) and not (csr.read_qlen2[lg] == 0).any()
             and not (csr.read_nal[lg] == 0).any())
     ctx.set_thresholds(thr)
-    ctx.set_long_reads(n, vreal, vbase, rlen, umax_table(jaccard_threshold, int(rlen.max())))
+    ctx.set_long_cutoffs(umax_table(jaccard_threshold, int(rlen.max())))
     pt = pass_table(jaccard_threshold)
     qcut, ncut = 1 - qlen_diff, 1 - diff
     ctx.reserve_edges(max(1 << 16, 12 * n))

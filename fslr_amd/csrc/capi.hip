@@ -335,15 +335,24 @@ int fslr_set_reads(fslr_ctx* c, const fslr_reads* r) {
   c->reads_set = true;
   c->index_built = false;
   c->lg_set = false;                        // a virtual-read map belongs to the reads it was set for
+  c->lg_perm.clear();
   c->edges_global = false;
   ++c->input_gen;
   return FSLR_OK;
 }
 
-int fslr_set_thresholds(fslr_ctx* c, const int32_t* thr) {
-  if (!c || (!thr && c->ni)) return FSLR_ERR_INVALID;
+int fslr_set_thresholds(fslr_ctx* c, const int32_t* thr_in) {
+  if (!c || (!thr_in && c->ni)) return FSLR_ERR_INVALID;
   if (!c->reads_set) return fail(c, FSLR_ERR_STATE, "fslr_set_reads first");
   ++c->input_gen;
+  // reads uploaded by fslr_set_reads_any: the thresholds come in the real CSR's interval order
+  std::vector<int32_t> permuted;
+  const int32_t* thr = thr_in;
+  if (!c->lg_perm.empty()) {
+    permuted.resize(c->lg_perm.size());
+    for (size_t k = 0; k < permuted.size(); ++k) permuted[k] = thr_in[c->lg_perm[k]];
+    thr = permuted.data();
+  }
   HIP_TRY(c, hipSetDevice(c->device));
   for (int64_t k = 0; k < c->ni; ++k)
     if ((thr[k] == FSLR_THR_ZERO_ALN) != (c->aln_zero_host[k] != 0))

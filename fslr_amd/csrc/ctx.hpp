@@ -125,6 +125,9 @@ struct fslr_ctx {
   struct CapWork* capw = nullptr;        // the device cap replay's buffers (cap.hip)
   // reads of more than FSLR_MAX_L intervals (long.hip): the virtual-read map and the long-pair stage
   bool lg_set = false;
+  // fslr_set_reads_any: virtual interval k is real interval lg_perm[k] (thresholds arrive in the real
+  // CSR's order and are permuted); empty when the reads were uploaded as they are
+  std::vector<int> lg_perm;
   int64_t lg_n_real = 0, lg_n_edges = 0;
   int lg_n_umax = 0;
   int* lg_vreal = nullptr;                  // [virtual reads] real read

@@ -24,6 +24,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <string>
 #include <vector>
 
 #include "ctx.hpp"
@@ -171,6 +172,99 @@ void fslr_long_free(fslr_ctx* c) {
                   c->lg_bits,  c->lg_temp, c->lg_ent, c->lg_short};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
+}
+
+// The virtual CSR of a real one (the layout fslr_set_long_reads describes): virtual
+// read r < n is real read r with its first FSLR_MAX_L intervals, the further FSLR_MAX_L-interval
+// chunks of the long reads follow as reads n, n + 1, ... in real-rank, then chunk order; a chunk
+// keeps its real read's qlen2 and n_alignments (the pair gate, cluster.py:178-183, and
+// calculate_overlap, :133-136, see only those and the two intervals).  Uploaded with
+// fslr_set_reads, the maps with fslr_set_long_reads (umax later: fslr_set_long_cutoffs).
+extern "C" int fslr_set_reads_any(fslr_ctx* c, const fslr_reads* r) {
+  if (!c || !r || r->n_reads < 0 || r->n_intervals < 0 || !r->read_off) return FSLR_ERR_INVALID;
+  const int64_t n = r->n_reads, ni = r->n_intervals;
+  if (r->read_off[0] != 0 || r->read_off[n] != ni) return fail(c, FSLR_ERR_INVALID, "read_off does not span intervals");
+  std::vector<int> extra(static_cast<size_t>(n)), rlen(static_cast<size_t>(n));
+  int64_t n_extra = 0;
+  bool any_long = false;
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t L = static_cast<int64_t>(r->read_off[i + 1]) - r->read_off[i];
+    if (L < 1 || L > kMaxRealL)
+      return fail(c, FSLR_ERR_INVALID, "every read needs 1.." + std::to_string(kMaxRealL) + " intervals");
+    rlen[i] = static_cast<int>(L);
+    extra[i] = static_cast<int>((L + FSLR_MAX_L - 1) / FSLR_MAX_L - 1);
+    n_extra += extra[i];
+    any_long |= L > FSLR_MAX_L;
+  }
+  if (!any_long) return fslr_set_reads(c, r);
+  const int64_t nv = n + n_extra;
+  if (nv >= FSLR_MAX_READS) return fail(c, FSLR_ERR_INVALID, "too many reads after the split into chunks");
+  std::vector<int32_t> voff(static_cast<size_t>(nv) + 1), vreal(static_cast<size_t>(nv)), vbase(static_cast<size_t>(nv));
+  std::vector<int32_t> vq(static_cast<size_t>(nv)), vn(static_cast<size_t>(nv));
+  std::vector<int> perm(static_cast<size_t>(ni));
+  // virtual read lengths: first chunks (ranks 0 .. n-1), then the further chunks in order
+  int64_t v = n;
+  for (int64_t i = 0; i < n; ++i) {
+    vreal[i] = static_cast<int32_t>(i);
+    vbase[i] = 0;
+    voff[i + 1] = std::min(rlen[i], FSLR_MAX_L);
+    for (int k = 1; k <= extra[i]; ++k, ++v) {
+      vreal[v] = static_cast<int32_t>(i);
+      vbase[v] = k * FSLR_MAX_L;
+      voff[v + 1] = std::min(rlen[i] - k * FSLR_MAX_L, FSLR_MAX_L);
+    }
+  }
+  voff[0] = 0;
+  for (int64_t u = 0; u < nv; ++u) voff[u + 1] += voff[u];
+  for (int64_t u = 0; u < nv; ++u) {
+    const int64_t src = static_cast<int64_t>(r->read_off[vreal[u]]) + vbase[u];
+    for (int64_t k = voff[u]; k < voff[u + 1]; ++k) perm[k] = static_cast<int>(src + (k - voff[u]));
+    vq[u] = r->read_qlen2 ? r->read_qlen2[vreal[u]] : 0;
+    vn[u] = r->read_nal ? r->read_nal[vreal[u]] : 0;
+  }
+  auto take = [&](const int32_t* a) {
+    std::vector<int32_t> out;
+    if (!a) return out;
+    out.resize(static_cast<size_t>(ni));
+    for (int64_t k = 0; k < ni; ++k) out[k] = a[perm[k]];
+    return out;
+  };
+  const std::vector<int32_t> ch = take(r->iv_chrom), st = take(r->iv_start), en = take(r->iv_end),
+                             th = take(r->iv_thr), dp = take(r->iv_data_pos);
+  fslr_reads vr = *r;
+  vr.n_reads = nv;
+  vr.read_off = voff.data();
+  vr.read_qlen2 = r->read_qlen2 ? vq.data() : nullptr;
+  vr.read_nal = r->read_nal ? vn.data() : nullptr;
+  vr.iv_chrom = r->iv_chrom ? ch.data() : nullptr;
+  vr.iv_start = r->iv_start ? st.data() : nullptr;
+  vr.iv_end = r->iv_end ? en.data() : nullptr;
+  vr.iv_thr = r->iv_thr ? th.data() : nullptr;
+  vr.iv_data_pos = r->iv_data_pos ? dp.data() : nullptr;
+  if (int rc = fslr_set_reads(c, &vr)) return rc;
+  // the cutoff table comes per query (fslr_set_long_cutoffs); a placeholder covers the longest read
+  int maxl = 0;
+  for (int L : rlen) maxl = std::max(maxl, L);
+  std::vector<int32_t> um(static_cast<size_t>(maxl), 0);
+  if (int rc = fslr_set_long_reads(c, n, vreal.data(), vbase.data(), rlen.data(), um.data(), maxl)) return rc;
+  c->lg_perm.swap(perm);
+  return FSLR_OK;
+}
+
+extern "C" int fslr_set_long_cutoffs(fslr_ctx* c, const int32_t* umax, int32_t n_umax) {
+  if (!c || n_umax < 0 || (!umax && n_umax)) return FSLR_ERR_INVALID;
+  if (!c->lg_set) return fail(c, FSLR_ERR_STATE, "fslr_set_reads_any (reads of more than FSLR_MAX_L intervals) first");
+  HIP_TRY(c, hipSetDevice(c->device));
+  int maxl = 0;
+  std::vector<int> rl(static_cast<size_t>(c->lg_n_real));
+  if (c->lg_n_real) HIP_TRY(c, hipMemcpy(rl.data(), c->lg_rlen, rl.size() * sizeof(int), hipMemcpyDeviceToHost));
+  for (int L : rl) maxl = std::max(maxl, L);
+  if (n_umax < maxl) return fail(c, FSLR_ERR_INVALID, "umax must cover I up to the longest read");
+  if (n_umax > c->lg_n_umax && dalloc(c, &c->lg_umax, n_umax)) return FSLR_ERR_NOMEM;
+  if (n_umax) HIP_TRY(c, hipMemcpyAsync(c->lg_umax, umax, n_umax * sizeof(int), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->lg_n_umax = n_umax;
+  return FSLR_OK;
 }
 
 extern "C" int fslr_set_long_reads(fslr_ctx* c, int64_t n_real, const int32_t* vreal, const int32_t* vbase,

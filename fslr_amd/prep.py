@@ -246,7 +246,8 @@ def build_csr(data: IntervalData) -> CSR:
     n = counts.size
     if n >= FSLR_MAX_READS:
         raise ValueError(f'{n} reads exceed the device limit of {FSLR_MAX_READS}')
-    # reads of more than FSLR_MAX_L intervals are uploaded split into chunks (split_long_reads)
+    # reads of more than FSLR_MAX_L intervals are uploaded split into chunks (fslr_set_reads_any;
+    # split_long_reads below is the same layout on the host)
     off = np.zeros(n + 1, dtype=np.int64)
     np.cumsum(counts, out=off[1:])
     start, end, chrom_raw, aln_p, nal_p = ingest.gather_columns(

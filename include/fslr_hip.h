@@ -292,6 +292,14 @@ int  fslr_sweep_partition_repeat(fslr_ctx *ctx, const fslr_params *params, int32
  * fslr_union_pairs + fslr_finalize_labels after fslr_components. */
 int  fslr_set_long_reads(fslr_ctx *ctx, int64_t n_real, const int32_t *vreal, const int32_t *vbase,
                          const int32_t *rlen, const int32_t *umax, int32_t n_umax);
+/* The same without a caller-made split: fslr_set_reads_any takes the REAL CSR (reads of 1..4096
+ * intervals), makes the virtual CSR and maps above and uploads them (as fslr_set_reads when no read
+ * exceeds FSLR_MAX_L).  Later fslr_set_thresholds calls take iv_thr in the real CSR's interval order
+ * too.  fslr_set_long_cutoffs sets umax (as above) before fslr_long_query / fslr_long_pairs /
+ * fslr_cap_replay_pairs.  Replaces the host-side split a binding would otherwise re-implement
+ * (reference: overall_jaccard_similarity takes lists of any length, cluster.py:140-170). */
+int  fslr_set_reads_any(fslr_ctx *ctx, const fslr_reads *reads);
+int  fslr_set_long_cutoffs(fslr_ctx *ctx, const int32_t *umax, int32_t n_umax);
 int  fslr_long_query(fslr_ctx *ctx, const fslr_params *params, int64_t *n_long_edges);
 int  fslr_get_long_edges(fslr_ctx *ctx, int32_t *a, int32_t *b, int32_t *I, int32_t *U, int64_t capacity);
 /* The general pair path (any overlap, aln_size == 0 intervals, qlen2 / n_alignments
