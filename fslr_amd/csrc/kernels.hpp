@@ -200,8 +200,8 @@ struct SweepArgs {
   hipEvent_t k0, k1;                  // (profiling) around the sweep kernel launch alone, or null
   hipEvent_t p0, p1;                  // (profiling) around the pair-stage kernel (k_bucket_pairs) alone, or null
   // set by launch_sweep_pairs for k_sweep_pairs' list mode (the buckets k_bucket_pairs spilled)
-  const long long* spill;             // [2 x count] entry ranges [s, e) in ent_sorted, or null (whole array)
-  const unsigned* spill_n;
+  const long long* spill;             // [3 x count] {s, e, first chunk}: spilled buckets in ent_sorted, or null
+  const unsigned long long* spill_n;  // count << 40 | total chunks of kChunk2 entries
   int wbase;                          // first per-wave statistics slot
 };
 size_t sweep_temp_bytes(long long ent_cap, long long ni, hipStream_t s);

@@ -25,6 +25,7 @@
 // Scope: thresholds >= 1 (overlap > 0) and no aln_size == 0 interval; other inputs take the walk
 // engine (capi.hip picks).
 #include <hipcub/hipcub.hpp>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
@@ -514,12 +515,15 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
   EdgeStageN<kPairEdgeStage> es{es_all[wv], 0};
   const EdgeOut eo{g.edges, g.edge_iu, g.edge_cap, &g.counters[kEdgeCount]};
   const int umax_v = g.umax[lane];
-  // list mode (g.spill): the items are whole buckets [s, e) of runs that k_bucket_pairs spilled, and
-  // n is the current bucket's end (no run crosses it)
+  // list mode (g.spill): the items are the kChunk2-entry chunks of the buckets k_bucket_pairs spilled
+  // (runs grouped by A inside each), and n is the current bucket's end (no run crosses it)
   long long n = g.n_dev ? *g.n_dev : g.n_ent;
   const unsigned long long* E = g.ent_sorted;
   const unsigned char* RL = g.rlen8;
-  const long long nchunks = g.spill ? static_cast<long long>(*g.spill_n) : (n + kChunk2 - 1) / kChunk2;
+  // list mode: the spilled buckets' chunks of kChunk2 entries (count << 40 | chunk total)
+  const unsigned long long spill_w = g.spill ? *g.spill_n : 0ull;
+  const int n_spill = static_cast<int>(spill_w >> 40);
+  const long long nchunks = g.spill ? static_cast<long long>(spill_w & ((1ull << 40) - 1)) : (n + kChunk2 - 1) / kChunk2;
   const long long nw = static_cast<long long>(gridDim.x) * kSwWaves;
   const int wid = blockIdx.x * kSwWaves + wv;
   int w_maxfwd = 0;
@@ -674,15 +678,23 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
   };
   for (long long c = wid; c < nchunks; c += nw) {
     long long c0, c1;
+    long long sb = 0;                                   // start of the array or of the spilled bucket
     if (g.spill) {
-      c0 = g.spill[2 * c];
-      c1 = n = g.spill[2 * c + 1];
+      int lo_k = 0, hi_k = n_spill - 1;                 // the bucket holding chunk c: largest first chunk <= c
+      while (lo_k < hi_k) {
+        const int mid_k = (lo_k + hi_k + 1) >> 1;
+        if (g.spill[3 * mid_k + 2] <= c) lo_k = mid_k; else hi_k = mid_k - 1;
+      }
+      sb = g.spill[3 * lo_k];
+      n = g.spill[3 * lo_k + 1];
+      c0 = sb + (c - g.spill[3 * lo_k + 2]) * kChunk2;
+      c1 = min(c0 + kChunk2, n);
     } else {
       c0 = c * kChunk2;
       c1 = min(c0 + kChunk2, n);
     }
     long long s = c0;
-    if (s > 0 && !g.spill) s = next_run(s, c1, a_at(s - 1));   // the run in progress belongs to the previous chunk
+    if (s > sb) s = next_run(s, c1, a_at(s - 1));      // the run in progress belongs to the previous chunk
     unsigned long long e0 = ~0ull, e1 = ~0ull, en = ~0ull;
     if (s < c1) load_window(s, e0, e1, en);
     while (s < c1) {
@@ -887,7 +899,7 @@ constexpr int kMsdMaxH = 16384;            // buckets (LDS histogram of pass 1)
 constexpr int kMsdMaxLo = 4096;            // in-bucket bins (LDS histogram of pass 2)
 constexpr int kGrpInts = 2 * (1 << 22);    // [bucket][block] counts and their scan (H P <= 2^22)
 // after them: the spill list of k_bucket_pairs (2 x kMsdMaxH entry ranges) and its count
-constexpr int kGrpSpillInts = 4 * kMsdMaxH + 64;
+constexpr int kGrpSpillInts = 6 * kMsdMaxH + 64;    // {s, e, first chunk} per bucket, then the count
 constexpr int kMsdUnroll = FSLR_MSD_UNROLL;  // entries loaded per lane before their atomics
 
 // One wave-instruction of keys (lanes with `act`, a contiguous prefix): equal keys on adjacent lanes
@@ -924,10 +936,10 @@ __global__ __launch_bounds__(kMsdThreads) void k_msd_pass1(const unsigned long l
                                                            int lo_bits, int H, int* __restrict__ mat,
                                                            unsigned long long* __restrict__ dst,
                                                            long long cap = 0x7FFFFFFFFFFFFFFFll,
-                                                           unsigned* zero = nullptr) {
+                                                           unsigned long long* zero = nullptr) {
   __shared__ int hist[kMsdMaxH];
   const int tid = threadIdx.x;
-  if (zero && blockIdx.x == 0 && tid == 0) *zero = 0u;   // (count pass) the spill list of k_bucket_pairs
+  if (zero && blockIdx.x == 0 && tid == 0) *zero = 0ull;   // (count pass) the spill list of k_bucket_pairs
   const int lane = tid & (kWave - 1), w = tid >> 6;
   const int P = gridDim.x;
   for (int i = tid; i < H; i += kMsdThreads) hist[i] = kScatter ? mat[i * P + blockIdx.x] : 0;
@@ -1130,11 +1142,15 @@ template <int CAP, int NT>
 __global__ __launch_bounds__(NT) void k_bucket_pairs(SweepArgs g, const unsigned long long* __restrict__ mid,
                                                      const int* __restrict__ off, int P, int H, int lo, int hbB,
                                                      unsigned long long* __restrict__ out,
-                                                     long long* __restrict__ spill, unsigned* __restrict__ spill_n) {
+                                                     long long* __restrict__ spill,
+                                                     unsigned long long* __restrict__ spill_n) {
   constexpr int K = CAP / NT;                  // entries per thread
   constexpr int NW = NT / kWave;
+  constexpr int KR = (kFuseMaxReads + NT - 1) / NT;   // reads of the bucket per thread
   static_assert(CAP % NT == 0 && kFuseBins % NT == 0, "shape");
   constexpr int PER = kFuseBins / NT;          // digits per thread in the scan
+  // LDS entry: L_B << 50 | A's low bits << 39 | B << 14 | i << 7 | j (A's high bits are the bucket's,
+  // and L_B, a function of B, rides where they were: bits >> 14 still name the pair)
   __shared__ __attribute__((aligned(16))) unsigned long long E[CAP];
   __shared__ __attribute__((aligned(16))) int HIST[kFuseBins];
   __shared__ unsigned long long ES[kFuseEs];
@@ -1154,6 +1170,7 @@ __global__ __launch_bounds__(NT) void k_bucket_pairs(SweepArgs g, const unsigned
   if (tid == 0) s_esn = 0;
   int w_maxfwd = 0;
   unsigned long long w_pairs = 0;
+  // digit of a global entry (A << 39 ...) or an LDS entry (A's low bits << 39 ...): the same bits
   auto digit = [&](unsigned long long x) -> int {
     const unsigned A = static_cast<unsigned>(x >> 39), B = static_cast<unsigned>(x >> 14) & kRankMask;
     return static_cast<int>(((A & lmask) << hbB) | ((B * 0x9E3779B1u) >> (32 - hbB)));   // hbB >= 1
@@ -1223,18 +1240,27 @@ __global__ __launch_bounds__(NT) void k_bucket_pairs(SweepArgs g, const unsigned
     long long sn = 0, en = 0;
     if (bn < H) range_of(bn, sn, en);
     __syncthreads();                                   // the previous bucket is done with the LDS
-    if (s_esn > kFuseEs - CAP / 4) flush();            // room for this bucket's edges (rarely short: see put)
+    if (s_esn > kFuseEs / 2) flush();                  // room for this bucket's edges (past it: see below)
     if (c == 0) {
       load(sn, en);
       b = bn; s = sn; e = en;
       continue;
     }
-    for (int i = tid; i < kFuseBins; i += NT) HIST[i] = 0;
-    for (int i = tid; i < nr; i += NT) {
-      FD[i] = 0;
-      const long long A = (static_cast<long long>(b) << lo) + i;
-      RLA[i] = A < g.n_reads ? RL[A] : 0;
+    // the read lengths this bucket needs, in flight under the histogram and its scan: L_B of each
+    // entry (packed into its LDS copy) and L_A of the bucket's reads
+    unsigned lbv[K];
+    int lav[KR];
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      lbv[k] = c <= CAP && tid + k * NT < c ? RL[static_cast<unsigned>(v[k] >> 14) & kRankMask] : 0u;
+#pragma unroll
+    for (int k = 0; k < KR; ++k) {
+      const int a = tid + k * NT;
+      const long long A = (static_cast<long long>(b) << lo) + a;
+      lav[k] = a < nr && A < g.n_reads ? RL[A] : 0;
     }
+    for (int i = tid; i < kFuseBins; i += NT) HIST[i] = 0;
+    for (int i = tid; i < nr; i += NT) FD[i] = 0;
     if (tid == 0) s_spill = c > CAP;
     __syncthreads();
     // digit histogram (entries of one read arrive in runs: run_add folds equal neighbours)
@@ -1262,7 +1288,8 @@ __global__ __launch_bounds__(NT) void k_bucket_pairs(SweepArgs g, const unsigned
       }
     __syncthreads();
     if (s_spill) {
-      // runs grouped by digit into out[s, e) (runs of one A contiguous), evaluated by the list pass
+      // runs grouped by digit into out[s, e) (runs of one A contiguous), listed with the count of
+      // their 512-entry chunks; k_sweep_pairs' list mode takes those chunks
       if (c <= CAP) {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -1282,14 +1309,20 @@ __global__ __launch_bounds__(NT) void k_bucket_pairs(SweepArgs g, const unsigned
         }
       }
       if (tid == 0) {
-        const unsigned k = atomicAdd(spill_n, 1u);
-        spill[2 * k] = s;
-        spill[2 * k + 1] = e;
+        const unsigned long long chunks = static_cast<unsigned long long>((c + kChunk2 - 1) / kChunk2);
+        const unsigned long long old = atomicAdd(spill_n, (1ull << 40) | chunks);
+        const unsigned k = static_cast<unsigned>(old >> 40);
+        spill[3 * k] = s;
+        spill[3 * k + 1] = e;
+        spill[3 * k + 2] = static_cast<long long>(old & ((1ull << 40) - 1));
       }
       load(sn, en);
       b = bn; s = sn; e = en;
       continue;
     }
+#pragma unroll
+    for (int k = 0; k < KR; ++k)
+      if (tid + k * NT < nr) RLA[tid + k * NT] = static_cast<unsigned char>(lav[k]);
     // scatter into LDS grouped by digit; afterwards HIST[d] = the end of bin d
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -1297,18 +1330,20 @@ __global__ __launch_bounds__(NT) void k_bucket_pairs(SweepArgs g, const unsigned
       if (k * NT >= c) break;
       const bool act = i < c;
       const int p = run_add<true>(HIST, act ? digit(v[k]) : 0, act, lane);
-      if (act) E[p] = v[k];
+      if (act)
+        E[p] = (v[k] & ((1ull << 39) - 1)) | (static_cast<unsigned long long>((v[k] >> 39) & lmask) << 39) |
+               (static_cast<unsigned long long>(lbv[k]) << 50);
     }
-    load(sn, en);                                      // the next bucket's entries, in flight
+    load(sn, en);                                      // the next bucket's entries, in flight (no more loads here)
     __syncthreads();
-    // pairs: lane per entry; the head of each (A, B) decides it
+    // pairs: lane per entry; the head of each (A, B) decides it (LDS only)
     for (int p0 = 0; p0 < c; p0 += NT) {
       const int p = p0 + tid;
       bool head = false, edge = false;
       int A = 0, B = 0, I = 0, U = 0;
       if (p < c) {
         const unsigned long long x = E[p];
-        const unsigned long long key = x >> 14;        // (A, B)
+        const unsigned long long key = x >> 14;        // (L_B, A, B)
         const int d = digit(x);
         const int bs = d > 0 ? HIST[d - 1] : 0, be = HIST[d];
         head = true;
@@ -1350,11 +1385,12 @@ __global__ __launch_bounds__(NT) void k_bucket_pairs(SweepArgs g, const unsigned
               }
             }
           }
-          A = static_cast<int>(x >> 39);
+          const unsigned al = static_cast<unsigned>(x >> 39) & lmask;
+          A = (b << lo) | static_cast<int>(al);
           B = static_cast<int>(key & kRankMask);
-          U = RLA[static_cast<unsigned>(A) & lmask] + RL[B] - I;
+          U = RLA[al] + static_cast<int>((x >> 50) & 127u) - I;
           edge = I > 0 && U <= UM[max(I, 1) - 1];
-          if (edge) atomicAdd(&FD[static_cast<unsigned>(A) & lmask], 1);
+          if (edge) atomicAdd(&FD[al], 1);
         }
       }
       w_pairs += __popcll(__ballot(head));
@@ -1609,7 +1645,7 @@ static hipError_t fused_pairs(const SweepArgs& a, int mode, const unsigned long 
   int* mat = a.grp;
   int* off = a.grp + kGrpInts / 2;
   long long* spill = reinterpret_cast<long long*>(a.grp + kGrpInts);
-  unsigned* spill_n = reinterpret_cast<unsigned*>(spill + 2 * kMsdMaxH);
+  auto* spill_n = reinterpret_cast<unsigned long long*>(spill + 3 * kMsdMaxH);   // count << 40 | chunks
   const int nt = tiles_of(a);
   if (mode == 2)
     k_msd_pass1<true, false><<<P, kMsdThreads, 0, s>>>(a.ent_ub, a.ub_cap, a.tile_ub, a.tile_cnt, nt, lo, H, mat, nullptr,
@@ -1654,6 +1690,13 @@ static hipError_t fused_pairs(const SweepArgs& a, int mode, const unsigned long 
   if (fw + lb * kSwWaves > a.wstat_waves) return hipErrorInvalidValue;
   k_sweep_pairs<<<lb, kSwBlock, 0, s>>>(l);
   *waves = fw + lb * kSwWaves;
+  if (std::getenv("FSLR_DEBUG_SPILL")) {                // diagnostics: how much took the list pass
+    unsigned long long sw = 0;
+    (void)hipMemcpyAsync(&sw, spill_n, sizeof(sw), hipMemcpyDeviceToHost, s);
+    (void)hipStreamSynchronize(s);
+    std::fprintf(stderr, "fslr: pair stage H=%d lo=%d hbB=%d %s, %llu of %d buckets spilled (%llu chunks), n=%lld\n", H,
+                 lo, hbB, big ? "12288/1024" : "4096/512", sw >> 40, H, sw & ((1ull << 40) - 1), n);
+  }
   return hipGetLastError();
 }
 
