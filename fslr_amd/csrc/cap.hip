@@ -643,7 +643,11 @@ __device__ bool replay_read(int t, int lane, int thr, const int* __restrict__ to
           break;
         }
       }
-      __threadfence();                     // this walk's marks before the next interval's loads
+      // this walk's marks before the next interval's loads: the same wave reads them back, so the
+      // stores only need to have landed (workgroup scope; an agent-scope fence per interval costs
+      // microseconds, MI355X_MICROARCH.md)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
   }
   if (lane == 0) {
@@ -669,7 +673,9 @@ __global__ __launch_bounds__(256) void k_cap_replay(const unsigned long long* __
       if (static_cast<int>(kk >> 25) != root) break;
       if (!replay_read(static_cast<int>(kk & kKeyMask), lane, thr, toff, ioff, rec, fpos, vis2, pbrk, own, err))
         return;
-      __threadfence();                     // this loop's results before a later read's loads
+      // this loop's results before a later read's loads (the same wave: workgroup scope)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
   }
 }
@@ -756,7 +762,10 @@ __global__ __launch_bounds__(256) void k_cap_replay_dag(int nt, int thr, const i
         const int y = static_cast<int>(ukey[s] & kKeyMask);
         if (y > x) t2 = t_of[y];
       }
-      if (t2 >= 0 && __hip_atomic_fetch_add(indeg + t2, -1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == 1) {
+      // the release fence above orders this loop's results before the decrement; the lane that
+      // takes the count to 0 acquires (every earlier partner's results) before it publishes t2
+      if (t2 >= 0 && __hip_atomic_fetch_add(indeg + t2, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         const unsigned slot = atomicAdd(queue + 1, 1u);                // queue[1]: next position to fill
         __hip_atomic_store(ready + slot, t2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       }
