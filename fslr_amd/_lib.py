@@ -13,7 +13,7 @@ import numpy as np
 
 LIB_PATH = os.environ.get('FSLR_LIB') or os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libfslr_hip.so')
 
-ABI_VERSION = 10         # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
+ABI_VERSION = 11         # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
 FSLR_OK, FSLR_ERR_ZERO_DIVISION, FSLR_ERR_INVALID, FSLR_ERR_HIP, FSLR_ERR_NOMEM, FSLR_ERR_STATE = range(6)
 FSLR_MAX_L = 64
 FSLR_MAX_READS = 1 << 25
@@ -36,7 +36,9 @@ EXPORTED = ['fslr_abi_version', 'fslr_last_error', 'fslr_ctx_create', 'fslr_ctx_
             'fslr_copy_edges_device', 'fslr_components_from_pairs', 'fslr_set_long_reads', 'fslr_long_query',
             'fslr_get_long_edges', 'fslr_copy_edges_iu_device', 'fslr_cap_install_edges', 'fslr_cap_local',
             'fslr_cap_copy_local', 'fslr_cap_replay', 'fslr_get_stage_kernel_times', 'fslr_long_pairs',
-            'fslr_cap_replay_pairs', 'fslr_source_hash', 'fslr_set_reads_any', 'fslr_set_long_cutoffs']
+            'fslr_cap_replay_pairs', 'fslr_source_hash', 'fslr_set_reads_any', 'fslr_set_long_cutoffs',
+            'fslr_cap_install_pairs', 'fslr_cap_sizes', 'fslr_cap_dep_local', 'fslr_cap_shard_plan',
+            'fslr_cap_shard_pack', 'fslr_cap_replay_shard', 'fslr_cap_copy_changes', 'fslr_cap_apply_changes']
 
 
 class HipUnavailable(RuntimeError):
@@ -155,6 +157,14 @@ def load(path: str = LIB_PATH):
         'fslr_cap_local': (ctypes.c_int, [vp, i32, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
         'fslr_cap_copy_local': (ctypes.c_int, [vp, vp, vp]),
         'fslr_cap_replay': (ctypes.c_int, [vp, vp, vp, i64, i32, ctypes.POINTER(CapStats)]),
+        'fslr_cap_install_pairs': (ctypes.c_int, [vp, vp, i64, i32, i32]),
+        'fslr_cap_sizes': (ctypes.c_int, [vp] + [ctypes.POINTER(ctypes.c_int64)] * 3),
+        'fslr_cap_dep_local': (ctypes.c_int, [vp, vp]),
+        'fslr_cap_shard_plan': (ctypes.c_int, [vp, vp, i32, i32, vp]),
+        'fslr_cap_shard_pack': (ctypes.c_int, [vp, vp, vp]),
+        'fslr_cap_replay_shard': (ctypes.c_int, [vp, vp, vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(CapStats)]),
+        'fslr_cap_copy_changes': (ctypes.c_int, [vp, vp, i64]),
+        'fslr_cap_apply_changes': (ctypes.c_int, [vp, vp, i64, ctypes.POINTER(CapStats)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -416,6 +426,52 @@ class Context:
         self._check(self._L.fslr_cap_replay(self._h, ctypes.c_void_p(counts.data_ptr()),
                                             ctypes.c_void_p(hits.data_ptr()), int(pad), int(world),
                                             ctypes.byref(cs)))
+        return cs.as_dict()
+
+    # -- multi-GPU edge cap sharded by the candidates' hit components (fslr_hip.h) ----------------
+    @staticmethod
+    def _dp(t, n):
+        return ctypes.c_void_p(t.data_ptr()) if n else None
+
+    def cap_install_pairs(self, t, n_rows: int, world: int, rank: int):
+        """The gathered E* (a, b) int32 rows (device tensor; a < 0 = padding), rank w's block at w m."""
+        self._check(self._L.fslr_cap_install_pairs(self._h, self._dp(t, n_rows), int(n_rows), int(world), int(rank)))
+
+    def cap_sizes(self):
+        """(|T|, T-intervals, local hits) after cap_local."""
+        v = [ctypes.c_int64() for _ in range(3)]
+        self._check(self._L.fslr_cap_sizes(self._h, *[ctypes.byref(x) for x in v]))
+        return tuple(int(x.value) for x in v)
+
+    def cap_dep_local(self, t):
+        """t[0 .. 2|T|) (int32 device): local forest roots of T reads, then their local hit counts."""
+        self._check(self._L.fslr_cap_dep_local(self._h, ctypes.c_void_p(t.data_ptr())))
+
+    def cap_shard_plan(self, gathered, world: int, rank: int):
+        """The components' ranks; returns (T-intervals per destination, local hits per destination)."""
+        sizes = np.zeros(2 * world, np.int64)
+        self._check(self._L.fslr_cap_shard_plan(self._h, ctypes.c_void_p(gathered.data_ptr()), int(world), int(rank),
+                                                _ptr(sizes)))
+        return sizes[:world].copy(), sizes[world:].copy()
+
+    def cap_shard_pack(self, counts, hits):
+        self._check(self._L.fslr_cap_shard_pack(self._h, ctypes.c_void_p(counts.data_ptr()),
+                                                ctypes.c_void_p(hits.data_ptr())))
+
+    def cap_replay_shard(self, counts, hits):
+        """Replay this rank's components from the received lists; returns (changes, partial cap stats)."""
+        nch = ctypes.c_int64()
+        cs = CapStats()
+        self._check(self._L.fslr_cap_replay_shard(self._h, ctypes.c_void_p(counts.data_ptr()),
+                                                  ctypes.c_void_p(hits.data_ptr()), ctypes.byref(nch), ctypes.byref(cs)))
+        return int(nch.value), cs.as_dict()
+
+    def cap_copy_changes(self, t, n_pad: int):
+        self._check(self._L.fslr_cap_copy_changes(self._h, self._dp(t, n_pad), int(n_pad)))
+
+    def cap_apply_changes(self, t, n: int) -> dict:
+        cs = CapStats()
+        self._check(self._L.fslr_cap_apply_changes(self._h, self._dp(t, n), int(n), ctypes.byref(cs)))
         return cs.as_dict()
 
     def components(self):

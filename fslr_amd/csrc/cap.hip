@@ -82,7 +82,7 @@ __global__ void k_cap_back(const int2* __restrict__ edges, long long ne, const i
   for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < ne;
        k += static_cast<long long>(gridDim.x) * blockDim.x) {
     const int2 e = edges[k];
-    if (state[e.x] == 1) atomicAdd(back + e.y, 1);
+    if (e.x >= 0 && state[e.x] == 1) atomicAdd(back + e.y, 1);     // a < 0: gathered padding
   }
 }
 
@@ -107,8 +107,10 @@ __global__ void k_cap_join(const int* __restrict__ fwd, int n, int thr, int* __r
 // each round walks only the forward edges of the reads that joined in the previous round.
 __global__ void k_cap_adj_count(const int2* __restrict__ edges, long long ne, int* __restrict__ cnt) {
   for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < ne;
-       k += static_cast<long long>(gridDim.x) * blockDim.x)
-    atomicAdd(cnt + edges[k].x, 1);
+       k += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const int a = edges[k].x;
+    if (a >= 0) atomicAdd(cnt + a, 1);                              // a < 0: gathered padding
+  }
 }
 
 __global__ void k_cap_adj_fill(const int2* __restrict__ edges, long long ne, const int* __restrict__ aoff,
@@ -116,7 +118,7 @@ __global__ void k_cap_adj_fill(const int2* __restrict__ edges, long long ne, con
   for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < ne;
        k += static_cast<long long>(gridDim.x) * blockDim.x) {
     const int2 e = edges[k];
-    adj[aoff[e.x] + atomicAdd(cur + e.x, 1)] = e.y;
+    if (e.x >= 0) adj[aoff[e.x] + atomicAdd(cur + e.x, 1)] = e.y;
   }
 }
 
@@ -947,6 +949,253 @@ __global__ void k_cap_pairs_out(const unsigned long long* __restrict__ ukey, int
   }
 }
 
+// ---- 6. the replay sharded over ranks (multi-GPU) -------------------------------
+// A loop of T depends on another T read's loop only when one's intervals hit the other's
+// (k_cap_mirror's pairs), so the components of the T-T hit graph replay independently: each rank
+// replays the components assigned to it and reports only the E* rows its loops do not form in the
+// lower read's loop.  Every rank holds the gathered E* (a, b) rows (row w * m + i = rank w's i-th
+// edge, a < 0 = padding) and computes the closure T itself.
+
+// the gathered rows' forward degrees
+__global__ void k_cap_gfwd(const int2* __restrict__ rows, long long n, int* __restrict__ fwd) {
+  for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < n;
+       k += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const int a = rows[k].x;
+    if (a >= 0) atomicAdd(fwd + a, 1);
+  }
+}
+
+// the T-T pairs of this rank's visit lists, one per list element ((-1, -1): a partner outside T), and
+// each T read's local hit count.  One wavefront per T-interval.
+__global__ __launch_bounds__(256) void k_cap_tdeps(const int* __restrict__ seq, const int* __restrict__ ioff,
+                                                   const int* __restrict__ tread, const int* __restrict__ t_of, int nti,
+                                                   int2* __restrict__ pairs, int* __restrict__ thits) {
+  const int lane = threadIdx.x & 63;
+  const int nw = gridDim.x * (blockDim.x >> 6);
+  for (int ti = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); ti < nti; ti += nw) {
+    const int t = tread[ti];
+    const int b0 = ioff[ti], b1 = ioff[ti + 1];
+    for (int k = b0 + lane; k < b1; k += 64) {
+      const int ty = t_of[seq[k]];
+      pairs[k] = ty >= 0 ? make_int2(t, ty) : make_int2(-1, -1);
+    }
+    if (lane == 0 && b1 > b0) atomicAdd(thits + t, b1 - b0);
+  }
+}
+
+// per T read: its hits summed over the ranks' gathered counts (the cost of its loop)
+__global__ void k_cap_tcost(const int* __restrict__ gath, int world, int nt, int* __restrict__ cost) {
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += gridDim.x * blockDim.x) {
+    int s = 0;
+    for (int w = 0; w < world; ++w) s += gath[static_cast<long long>(w) * 2 * nt + nt + t];
+    cost[t] = s;
+  }
+}
+
+// per T-interval: the rank replaying its read's component (sort key), and its index
+__global__ void k_cap_tikey(const int* __restrict__ tread, const int* __restrict__ tdest, int nti,
+                            unsigned* __restrict__ key, int* __restrict__ val) {
+  for (int ti = blockIdx.x * blockDim.x + threadIdx.x; ti < nti; ti += gridDim.x * blockDim.x) {
+    key[ti] = static_cast<unsigned>(tdest[tread[ti]]);
+    val[ti] = ti;
+  }
+}
+
+// the local counts in destination order, and per destination its T-intervals and hits (block
+// histograms in LDS, then one atomic per bin and block)
+__global__ __launch_bounds__(256) void k_cap_sendcnt(const int* __restrict__ tsorted, const unsigned* __restrict__ skey,
+                                                     const int* __restrict__ icnt, int nti, int* __restrict__ scnt,
+                                                     long long* __restrict__ totals) {
+  __shared__ long long h[2 * kMaxDest];
+  for (int i = threadIdx.x; i < 2 * kMaxDest; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nti; i += gridDim.x * blockDim.x) {
+    const int d = static_cast<int>(skey[i]);
+    const int cnt = icnt[tsorted[i]];
+    scnt[i] = cnt;
+    atomicAdd(reinterpret_cast<unsigned long long*>(h + d), 1ull);
+    atomicAdd(reinterpret_cast<unsigned long long*>(h + kMaxDest + d), static_cast<unsigned long long>(cnt));
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * kMaxDest; i += blockDim.x)
+    if (h[i]) atomicAdd(reinterpret_cast<unsigned long long*>(totals + i), static_cast<unsigned long long>(h[i]));
+}
+
+// the local hit lists in destination order; one wavefront per T-interval
+__global__ __launch_bounds__(256) void k_cap_pack(const int* __restrict__ tsorted, const int* __restrict__ scnt,
+                                                  const int* __restrict__ shoff, const int* __restrict__ seq,
+                                                  const int* __restrict__ ioff, int nti, int* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int nw = gridDim.x * (blockDim.x >> 6);
+  for (int i = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < nti; i += nw) {
+    const int cnt = scnt[i];
+    if (!cnt) continue;
+    const int* src = seq + ioff[tsorted[i]];
+    int* dst = out + shoff[i];
+    for (int k = lane; k < cnt; k += 64) dst[k] = src[k];
+  }
+}
+
+// receiving rank: its T-intervals' counts summed over the W sources (an interval's hits come from the
+// one rank indexing its chromosome), at the interval's place in T order (others stay 0)
+__global__ void k_cap_recv_sum(const int* __restrict__ rcnt, int world, int nmine, const int* __restrict__ mine,
+                               int* __restrict__ icnt) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nmine; i += gridDim.x * blockDim.x) {
+    int s = 0;
+    for (int w = 0; w < world; ++w) s += rcnt[static_cast<long long>(w) * nmine + i];
+    icnt[mine[i]] = s;
+  }
+}
+
+// the received lists into the visit sequence; roff = exclusive scan of rcnt (source-major, the
+// layout of the received hits).  One wavefront per received T-interval.
+__global__ __launch_bounds__(256) void k_cap_recv_assemble(const int* __restrict__ rcnt, const int* __restrict__ roff,
+                                                           const int* __restrict__ rhits, int world, int nmine,
+                                                           const int* __restrict__ mine, const int* __restrict__ ioff,
+                                                           int* __restrict__ seq) {
+  const int lane = threadIdx.x & 63;
+  const int nw = gridDim.x * (blockDim.x >> 6);
+  for (int i = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < nmine; i += nw) {
+    int dst = ioff[mine[i]];
+    for (int w = 0; w < world; ++w) {
+      const long long j = static_cast<long long>(w) * nmine + i;
+      const int cnt = rcnt[j];
+      if (!cnt) continue;
+      const int* src = rhits + roff[j];
+      for (int k = lane; k < cnt; k += 64) seq[dst + k] = src[k];
+      dst += cnt;
+    }
+  }
+}
+
+// the gathered rows this rank decides (a T endpoint in one of its components): who = 0 when a's loop
+// forms the edge, 1 when b's does, 2 when neither; changes k << 2 | who for who != 0
+__global__ void k_cap_classify_shard(const int2* __restrict__ rows, long long n, const int* __restrict__ t_of,
+                                     const int* __restrict__ tdest, const int* __restrict__ comp, int rank,
+                                     const int* __restrict__ pbrk, const unsigned long long* __restrict__ ukey, int ns,
+                                     const int* __restrict__ fpos, const unsigned char* __restrict__ vis2,
+                                     int* __restrict__ chg, unsigned* __restrict__ nchg, int* __restrict__ err) {
+  const int lane = threadIdx.x & 63;
+  for (long long k0 = (blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x) & ~63ll; k0 < n;
+       k0 += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const long long k = k0 + lane;
+    int w = 0;
+    if (k < n) {
+      const int2 e = rows[k];
+      const int ta = e.x >= 0 ? t_of[e.x] : -1, tb = e.x >= 0 ? t_of[e.y] : -1;
+      const int t = ta >= 0 ? ta : tb;
+      if (t >= 0 && tdest[t] == rank) {
+        if (ta >= 0 && tb >= 0 && comp[ta] != comp[tb]) {
+          atomicOr(err, kCapErrState);                // E* partners hit each other: one component
+        } else if (!loop_reaches(e.x, e.y, t_of, pbrk, ukey, ns, fpos, vis2, err)) {
+          w = loop_reaches(e.y, e.x, t_of, pbrk, ukey, ns, fpos, vis2, err) ? 1 : 2;
+        }
+      }
+    }
+    const unsigned long long m = __ballot(w != 0);
+    if (!m) continue;
+    unsigned base = 0;
+    if (lane == 0) base = atomicAdd(nchg, static_cast<unsigned>(__popcll(m)));
+    base = static_cast<unsigned>(__shfl(static_cast<int>(base), 0));
+    if (w) chg[base + mbcnt(m)] = static_cast<int>((k << 2) | w);
+  }
+}
+
+// T reads (of this rank's components) whose loop reached the cap
+__global__ void k_cap_count_capped(const int* __restrict__ pbrk, int nt, long long* __restrict__ stats) {
+  int capped = 0;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nt; i += gridDim.x * blockDim.x) capped += pbrk[i] != kInf;
+  for (int o = 32; o > 0; o >>= 1) capped += __shfl_xor(capped, o);
+  if ((threadIdx.x & 63) == 0 && capped)
+    atomicAdd(reinterpret_cast<unsigned long long*>(stats + kStCapped), static_cast<unsigned long long>(capped));
+}
+
+// every rank's changes (-1 = padding): who per gathered row, edges formed per loop
+__global__ void k_cap_apply(const int* __restrict__ chg, long long n, const int2* __restrict__ rows,
+                            unsigned char* __restrict__ who, int* __restrict__ formed, long long* __restrict__ stats) {
+  long long drop = 0, bwd = 0;
+  for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < n;
+       k += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const int v = chg[k];
+    if (v < 0) continue;
+    const int r = v >> 2, w = v & 3;
+    const int2 e = rows[r];
+    who[r] = static_cast<unsigned char>(w);
+    atomicSub(formed + e.x, 1);
+    if (w == 1) atomicAdd(formed + e.y, 1);
+    drop += w == 2;
+    bwd += w == 1;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    drop += __shfl_xor(drop, o);
+    bwd += __shfl_xor(bwd, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (drop) atomicAdd(reinterpret_cast<unsigned long long*>(stats + kStDropped), static_cast<unsigned long long>(drop));
+    if (bwd) atomicAdd(reinterpret_cast<unsigned long long*>(stats + kStBackward), static_cast<unsigned long long>(bwd));
+  }
+}
+
+// this rank's block of rows (its own edges, in its edge order): kept flags
+__global__ void k_cap_local_flags(const int2* __restrict__ rows, const unsigned char* __restrict__ who, long long m,
+                                  int* __restrict__ kflag) {
+  for (long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; i < m;
+       i += static_cast<long long>(gridDim.x) * blockDim.x)
+    kflag[i] = rows[i].x >= 0 && who[i] != 2;
+}
+
+// its kept edges compacted, as (the read whose loop forms it, partner), and edges per former read
+__global__ void k_cap_local_compact(const int2* __restrict__ edges, const unsigned short* __restrict__ iu, long long m,
+                                    const int* __restrict__ kflag, const int* __restrict__ koff,
+                                    const unsigned char* __restrict__ who, int2* __restrict__ oe,
+                                    unsigned short* __restrict__ oiu, int* __restrict__ lfwd) {
+  for (long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; i < m;
+       i += static_cast<long long>(gridDim.x) * blockDim.x) {
+    if (!kflag[i]) continue;
+    const int2 e = edges[i];
+    const bool fl = who[i] == 1;
+    oe[koff[i]] = fl ? make_int2(e.y, e.x) : e;
+    oiu[koff[i]] = iu[i];
+    atomicAdd(lfwd + (fl ? e.y : e.x), 1);
+  }
+}
+
+// dropped rows become padding (the capped graph's components)
+__global__ void k_cap_drop_rows(int2* __restrict__ rows, const unsigned char* __restrict__ who, long long n) {
+  for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < n;
+       k += static_cast<long long>(gridDim.x) * blockDim.x)
+    if (who[k] == 2) rows[k] = make_int2(-1, -1);
+}
+
+// each loop this rank replayed formed exactly the edges the changes give it; the largest count
+__global__ void k_cap_check_shard(const int* __restrict__ T, int nt, const int* __restrict__ tdest, int rank,
+                                  const int* __restrict__ own, const int* __restrict__ formed, int n,
+                                  long long* __restrict__ stats, int* __restrict__ err) {
+  int mx = 0;
+  const int m = max(n, nt);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
+    if (i < nt && tdest[i] == rank && formed[T[i]] != own[i]) atomicOr(err, kCapErrState);
+    if (i < n) mx = max(mx, formed[i]);
+  }
+  for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+  if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<long long*>(stats + kStMaxFwd), static_cast<long long>(mx));
+}
+
+__global__ void k_cap_commit_shard(const int* __restrict__ koff, const int* __restrict__ kflag, long long m,
+                                   unsigned long long* __restrict__ counters, int* __restrict__ errw,
+                                   long long* __restrict__ stats, const int* __restrict__ err,
+                                   long long* __restrict__ host) {
+  if (threadIdx.x != 0) return;
+  const long long kept = m ? static_cast<long long>(koff[m - 1]) + kflag[m - 1] : 0;
+  stats[kStKept] = kept;
+  counters[kEdgeCount] = static_cast<unsigned long long>(kept);
+  errw[0] = 0;
+  errw[3] = static_cast<int>(stats[kStMaxFwd]);
+  errw[kErrOverflow] = 0;
+  for (int k = 0; k < kStWords; ++k) host[kHStat + k] = stats[k];
+  host[kHErr] = *err;
+}
+
 __global__ void k_fill(int* __restrict__ p, int n, int v) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = v;
 }
@@ -974,8 +1223,10 @@ struct CapArena {
 };
 
 struct CapWork {
-  CapArena ar[5];                     // 0: per read / per edge, 1: per T read / T-interval, 2: per hit (scratch),
-                                      // 3: multi-GPU offsets, 4: the visit sequence
+  CapArena ar[9];                     // 0: per read / per edge, 1: per T read / T-interval, 2: per hit (scratch),
+                                      // 3: multi-GPU offsets, 4: the visit sequence; the sharded replay:
+                                      // 5: gathered rows, 6: plan (per T read / T-interval), 7: T-T pairs,
+                                      // 8: received offsets and changes
   void* temp = nullptr;
   size_t temp_bytes = 0;
   long long* host = nullptr;          // pinned, device-mapped
@@ -1013,6 +1264,23 @@ struct CapWork {
   // multi-GPU assembly
   int *gsum = nullptr, *loff = nullptr;
   bool prepared = false;              // fslr_cap_local ran on the current edges
+  // the sharded replay (fslr_cap_install_pairs ... fslr_cap_apply_changes)
+  bool gmode = false;                 // the closure runs over the gathered rows
+  int2* grows = nullptr;              // gathered E* (a, b) rows, a < 0 = padding
+  int* gfwd = nullptr;                // their forward degrees
+  unsigned char* gwho = nullptr;      // per row: 0 formed in a's loop, 1 in b's, 2 dropped
+  int64_t g_rows = 0, g_m = 0;
+  int g_world = 1, g_rank = 0;
+  int *comp = nullptr, *tcost = nullptr, *tdest = nullptr, *tival = nullptr, *tsorted = nullptr, *scnt = nullptr,
+      *shoff = nullptr;
+  unsigned *tikey = nullptr, *tikey2 = nullptr;
+  long long* totals = nullptr;        // [2 kMaxDest]: T-intervals and hits per destination
+  int64_t nmine = 0, mine_off = 0, planned = 0;
+  int2* tdeps = nullptr;
+  int *roff = nullptr, *chgl = nullptr;
+  unsigned* nchg = nullptr;
+  int64_t n_chg = 0;
+  bool replayed = false;              // fslr_cap_replay_shard ran (changes ready)
 };
 
 void fslr_cap_free(fslr_ctx* c) {
@@ -1120,10 +1388,11 @@ bool cap_dag_disabled() {
   return v;
 }
 
-// Phase A: the closure T (all_reads: every read, fslr_long_pairs), the T-intervals and their
+// Phase A: the closure T over E* = E[0 .. ne) with forward degrees F (all_reads: every read,
+// fslr_long_pairs), the T-intervals and their
 // local hit counts; the local visit lists (partner reads, search order) at w->seq[0 .. nloc),
 // segments at w->ioff (local counts).
-int cap_local(fslr_ctx* c, int thr, CapWork* w, int64_t ne, bool all_reads = false) {
+int cap_local(fslr_ctx* c, int thr, CapWork* w, const int2* E, const int* F, int64_t ne, bool all_reads = false) {
   hipStream_t s = c->stream;
   set_space(c, w);
   const int64_t n = w->n;
@@ -1162,12 +1431,12 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, int64_t ne, bool all_reads = fal
   // rounds over every edge and read in batches of 8 (chg[0] = 1 starts each batch)
   const bool frontier = !all_reads && !cap_rounds_closure();
   if (all_reads) k_cap_all<<<grid_for(n), 256, 0, s>>>(w->state, static_cast<int>(n));
-  else if (!frontier) k_cap_init<<<grid_for(n), 256, 0, s>>>(c->fwd, static_cast<int>(n), thr, w->state, w->back);
+  else if (!frontier) k_cap_init<<<grid_for(n), 256, 0, s>>>(F, static_cast<int>(n), thr, w->state, w->back);
   HIP_TRY(c, hipGetLastError());
   if (frontier) {
     HIP_TRY(c, hipMemsetAsync(w->acur, 0, static_cast<size_t>(n) * sizeof(int), s));
     HIP_TRY(c, hipMemsetAsync(w->fcnt, 0, 64 * sizeof(unsigned), s));
-    if (ne > 0) k_cap_adj_count<<<grid_for(ne), 256, 0, s>>>(c->edges, ne, w->acur);
+    if (ne > 0) k_cap_adj_count<<<grid_for(ne), 256, 0, s>>>(E, ne, w->acur);
     // aoff[0] = 0, aoff[1 .. n] = the inclusive scan of the counts
     size_t tb = 0;
     HIP_TRY(c, hipcub::DeviceScan::InclusiveSum(nullptr, tb, w->acur, w->aoff + 1, static_cast<int>(n), s));
@@ -1176,14 +1445,14 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, int64_t ne, bool all_reads = fal
     HIP_TRY(c, hipcub::DeviceScan::InclusiveSum(w->temp, tb, w->acur, w->aoff + 1, static_cast<int>(n), s));
     HIP_TRY(c, hipMemsetAsync(w->aoff, 0, sizeof(int), s));
     HIP_TRY(c, hipMemsetAsync(w->acur, 0, static_cast<size_t>(n) * sizeof(int), s));
-    if (ne > 0) k_cap_adj_fill<<<grid_for(ne), 256, 0, s>>>(c->edges, ne, w->aoff, w->acur, w->adj);
-    k_cap_seed<<<grid_for(n), 256, 0, s>>>(c->fwd, static_cast<int>(n), thr, w->state, w->back, w->fl0, w->fcnt);
+    if (ne > 0) k_cap_adj_fill<<<grid_for(ne), 256, 0, s>>>(E, ne, w->aoff, w->acur, w->adj);
+    k_cap_seed<<<grid_for(n), 256, 0, s>>>(F, static_cast<int>(n), thr, w->state, w->back, w->fl0, w->fcnt);
     HIP_TRY(c, hipGetLastError());
     int* fl[2] = {w->fl0, w->fl1};
     for (int batch = 0;; ++batch) {
       // rounds r = 0 .. 15 of the batch: frontier fl[r & 1] (count fcnt[r]) -> fl[(r + 1) & 1] (fcnt[r + 1])
       for (int r = 0; r < 16; ++r)
-        k_cap_frontier<<<1024, 256, 0, s>>>(w->aoff, w->adj, c->fwd, thr, w->state, w->back, fl[r & 1], w->fcnt + r,
+        k_cap_frontier<<<1024, 256, 0, s>>>(w->aoff, w->adj, F, thr, w->state, w->back, fl[r & 1], w->fcnt + r,
                                             fl[(r + 1) & 1], w->fcnt + r + 1);
       HIP_TRY(c, hipGetLastError());
       unsigned last = 0;
@@ -1200,8 +1469,8 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, int64_t ne, bool all_reads = fal
     HIP_TRY(c, hipMemsetAsync(w->chg, 0, 16 * sizeof(int), s));
     HIP_TRY(c, hipMemsetAsync(w->chg, 0xff, sizeof(int), s));
     for (int r = 1; r <= 8; ++r) {
-      k_cap_back<<<grid_for(ne), 256, 0, s>>>(c->edges, ne, w->state, w->back, w->chg + r - 1);
-      k_cap_join<<<grid_for(n), 256, 0, s>>>(c->fwd, static_cast<int>(n), thr, w->state, w->back, w->chg + r - 1,
+      k_cap_back<<<grid_for(ne), 256, 0, s>>>(E, ne, w->state, w->back, w->chg + r - 1);
+      k_cap_join<<<grid_for(n), 256, 0, s>>>(F, static_cast<int>(n), thr, w->state, w->back, w->chg + r - 1,
                                              w->chg + r);
     }
     HIP_TRY(c, hipGetLastError());
@@ -1334,10 +1603,10 @@ int cap_slots(fslr_ctx* c, CapWork* w) {
   return FSLR_OK;
 }
 
-int cap_core(fslr_ctx* c, CapWork* w, fslr_cap_stats* cs) {
+// 3 + 4: slots, predicates and every read of T's loop (pbrk, own, visit marks)
+int cap_loops(fslr_ctx* c, CapWork* w) {
   hipStream_t s = c->stream;
   const int thr = w->thr;
-  const int64_t n = w->n, ne = w->ne;
   const int nt = static_cast<int>(w->nt);
   const int m = static_cast<int>(w->nseq);
   if (int rc = cap_slots(c, w)) return rc;
@@ -1392,6 +1661,15 @@ int cap_core(fslr_ctx* c, CapWork* w, fslr_cap_stats* cs) {
     HIP_TRY(c, hipGetLastError());
   }
   w->ns = ns;
+  return FSLR_OK;
+}
+
+int cap_core(fslr_ctx* c, CapWork* w, fslr_cap_stats* cs) {
+  hipStream_t s = c->stream;
+  const int64_t n = w->n, ne = w->ne;
+  const int nt = static_cast<int>(w->nt);
+  if (int rc = cap_loops(c, w)) return rc;
+  const int ns = static_cast<int>(w->ns);
   // 5. the capped graph
   // edges formed per loop, from the E* forward degrees (fwd[x] = E* edges (x, .), as the query or the
   // install left them)
@@ -1470,7 +1748,7 @@ extern "C" int fslr_apply_edge_cap(fslr_ctx* c, int32_t thr, fslr_cap_stats* out
   if (int rc = ensure_bwd_ranges(c)) return rc;
   CapWork* w = nullptr;
   if (int rc = cap_work(c, &w)) return rc;
-  if (int rc = cap_local(c, thr, w, ne)) return rc;
+  if (int rc = cap_local(c, thr, w, c->edges, c->fwd, ne)) return rc;
   w->nseq = w->nloc;
   fslr_cap_stats cs;
   std::memset(&cs, 0, sizeof(cs));
@@ -1523,6 +1801,7 @@ extern "C" int fslr_cap_install_edges(fslr_ctx* c, const int32_t* rows, int64_t 
   HIP_TRY(c, hipGetLastError());
   HIP_TRY(c, hipStreamSynchronize(s));
   c->edges_global = true;
+  c->cap_gmode = false;
   std::memset(&c->cap_stats, 0, sizeof(c->cap_stats));
   return FSLR_OK;
 }
@@ -1531,6 +1810,16 @@ extern "C" int fslr_cap_local(fslr_ctx* c, int32_t thr, int64_t* n_ti, int64_t* 
   if (!c || !n_ti || !n_hits) return FSLR_ERR_INVALID;
   HIP_TRY(c, hipSetDevice(c->device));
   *n_ti = *n_hits = 0;
+  if (c->cap_gmode) {                  // the sharded replay: the closure over the gathered rows
+    CapWork* w = c->capw;
+    if (int rc = ensure_bwd_ranges(c)) return rc;
+    if (int rc = cap_local(c, thr, w, w->grows, w->gfwd, w->g_rows)) return rc;
+    w->planned = 0;
+    w->replayed = false;
+    *n_ti = w->nti;
+    *n_hits = w->nloc;
+    return FSLR_OK;
+  }
   if (!c->edges_global && !c->last_full)
     return fail(c, FSLR_ERR_STATE, "fslr_cap_local needs every E* edge on this context (fslr_cap_install_edges)");
   int64_t ne = 0;
@@ -1540,7 +1829,7 @@ extern "C" int fslr_cap_local(fslr_ctx* c, int32_t thr, int64_t* n_ti, int64_t* 
   if (int rc = ensure_bwd_ranges(c)) return rc;
   CapWork* w = nullptr;
   if (int rc = cap_work(c, &w)) return rc;
-  if (int rc = cap_local(c, thr, w, ne)) return rc;
+  if (int rc = cap_local(c, thr, w, c->edges, c->fwd, ne)) return rc;
   *n_ti = w->nti;
   *n_hits = w->nloc;
   return FSLR_OK;
@@ -1624,7 +1913,7 @@ extern "C" int fslr_long_pairs(fslr_ctx* c, const fslr_params* p, int64_t* n_edg
   std::memset(&c->cap_stats, 0, sizeof(c->cap_stats));
   CapWork* w = nullptr;
   if (int rc = cap_work(c, &w)) return rc;
-  if (int rc = cap_local(c, 0, w, 0, true)) return rc;          // every read's hits, any thresholds
+  if (int rc = cap_local(c, 0, w, c->edges, c->fwd, 0, true)) return rc;          // every read's hits, any thresholds
   w->nseq = w->nloc;
   if (int rc = cap_slots(c, w)) return rc;
   const int ns = static_cast<int>(w->ns);
@@ -1696,7 +1985,7 @@ extern "C" int fslr_cap_replay_pairs(fslr_ctx* c, int32_t thr, const int32_t* a,
     if (int rc = ensure_bwd_ranges(c)) return rc;
     CapWork* w = nullptr;
     if (int rc = cap_work(c, &w)) return rc;
-    if (int rc = cap_local(c, thr, w, ne)) return rc;
+    if (int rc = cap_local(c, thr, w, c->edges, c->fwd, ne)) return rc;
     w->nseq = w->nloc;
     if (int rc = cap_core(c, w, &cs)) return rc;
     if (ne) HIP_TRY(c, hipMemcpyAsync(who, w->who, static_cast<size_t>(ne), hipMemcpyDeviceToHost, s));
@@ -1706,6 +1995,357 @@ extern "C" int fslr_cap_replay_pairs(fslr_ctx* c, int32_t thr, const int32_t* a,
     if (ne) std::memset(who, 0, static_cast<size_t>(ne));
     if (fwd) std::copy(deg.begin(), deg.end(), fwd);
   }
+  c->cap_stats = cs;
+  if (out) *out = cs;
+  return FSLR_OK;
+}
+
+// ---- the sharded replay (multi-GPU): host side ---------------------------------------------------
+extern "C" int fslr_cap_install_pairs(fslr_ctx* c, const int32_t* pairs, int64_t n_rows, int32_t world, int32_t rank) {
+  if (!c || (!pairs && n_rows) || n_rows < 0 || world < 1 || world > kMaxDest || rank < 0 || rank >= world ||
+      n_rows % world)
+    return FSLR_ERR_INVALID;
+  if (n_rows >= (int64_t(1) << 29)) return fail(c, FSLR_ERR_INVALID, "sharded edge cap: at most 2^29 gathered rows");
+  if (!c->reads_set) return fail(c, FSLR_ERR_STATE, "fslr_set_reads first");
+  if (c->lg_set) return fail(c, FSLR_ERR_STATE, "the sharded edge cap takes reads of at most FSLR_MAX_L intervals");
+  if (!c->counters) return fail(c, FSLR_ERR_STATE, "no query has run");
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  CapWork* w = nullptr;
+  if (int rc = cap_work(c, &w)) return rc;
+  {
+    Carve cv;
+    cv.add(&w->grows, n_rows);
+    cv.add(&w->gfwd, c->n);
+    cv.add(&w->gwho, n_rows);
+    if (int rc = cv.commit(c, w->ar[5])) return rc;
+  }
+  if (n_rows) HIP_TRY(c, hipMemcpyAsync(w->grows, pairs, static_cast<size_t>(n_rows) * sizeof(int2),
+                                        hipMemcpyDeviceToDevice, s));
+  HIP_TRY(c, hipMemsetAsync(w->gfwd, 0, static_cast<size_t>(std::max<int64_t>(c->n, 1)) * sizeof(int), s));
+  if (n_rows) k_cap_gfwd<<<grid_for(n_rows), 256, 0, s>>>(w->grows, n_rows, w->gfwd);
+  HIP_TRY(c, hipGetLastError());
+  w->g_rows = n_rows;
+  w->g_m = n_rows / world;
+  w->g_world = world;
+  w->g_rank = rank;
+  w->prepared = false;
+  w->planned = 0;
+  w->replayed = false;
+  c->cap_gmode = true;
+  c->edges_global = false;
+  std::memset(&c->cap_stats, 0, sizeof(c->cap_stats));
+  return FSLR_OK;
+}
+
+extern "C" int fslr_cap_sizes(fslr_ctx* c, int64_t* n_t, int64_t* n_ti, int64_t* n_hits) {
+  if (!c || !n_t || !n_ti || !n_hits) return FSLR_ERR_INVALID;
+  if (!c->capw || !c->capw->prepared) return fail(c, FSLR_ERR_STATE, "fslr_cap_local first");
+  *n_t = c->capw->nt;
+  *n_ti = c->capw->nti;
+  *n_hits = c->capw->nloc;
+  return FSLR_OK;
+}
+
+extern "C" int fslr_cap_dep_local(fslr_ctx* c, int32_t* out) {
+  if (!c) return FSLR_ERR_INVALID;
+  CapWork* w = c->capw;
+  if (!c->cap_gmode || !w || !w->prepared) return fail(c, FSLR_ERR_STATE, "fslr_cap_install_pairs, fslr_cap_local first");
+  const int nt = static_cast<int>(w->nt), nti = static_cast<int>(w->nti);
+  if (!out && nt) return FSLR_ERR_INVALID;
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  if (nt == 0) return FSLR_OK;
+  {
+    Carve cv;
+    cv.add(&w->tdeps, w->nloc);
+    if (int rc = cv.commit(c, w->ar[7])) return rc;
+  }
+  int* par = out;
+  int* thits = out + nt;
+  HIP_TRY(c, hipMemsetAsync(thits, 0, static_cast<size_t>(nt) * sizeof(int), s));
+  HIP_TRY(c, launch_uf_init(par, nt, s));
+  if (w->nloc > 0) {
+    k_cap_tdeps<<<wave_grid(nti), 256, 0, s>>>(w->seq, w->ioff, w->tread, w->t_of, nti, w->tdeps, thits);
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, launch_uf_pair_list(par, w->tdeps, w->nloc, s));
+  }
+  HIP_TRY(c, launch_uf_finalize(par, nt, s));
+  return FSLR_OK;
+}
+
+extern "C" int fslr_cap_shard_plan(fslr_ctx* c, const int32_t* gathered, int32_t world, int32_t rank, int64_t* sizes) {
+  if (!c || !sizes) return FSLR_ERR_INVALID;
+  CapWork* w = c->capw;
+  if (!c->cap_gmode || !w || !w->prepared) return fail(c, FSLR_ERR_STATE, "fslr_cap_install_pairs, fslr_cap_local first");
+  if (world != w->g_world || rank != w->g_rank) return fail(c, FSLR_ERR_INVALID, "world / rank differ from fslr_cap_install_pairs");
+  const int nt = static_cast<int>(w->nt), nti = static_cast<int>(w->nti);
+  if (!gathered && nt) return FSLR_ERR_INVALID;
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  {
+    Carve cv;
+    cv.add(&w->comp, nt);
+    cv.add(&w->tcost, nt);
+    cv.add(&w->tdest, nt);
+    cv.add(&w->tikey, nti);
+    cv.add(&w->tikey2, nti);
+    cv.add(&w->tival, nti);
+    cv.add(&w->tsorted, nti);
+    cv.add(&w->scnt, nti + 1);
+    cv.add(&w->shoff, nti + 1);
+    cv.add(&w->totals, 2 * kMaxDest);
+    if (int rc = cv.commit(c, w->ar[6])) return rc;
+  }
+  // the components of the T-T hit graph: the union of the ranks' local forests
+  std::vector<int> comp(nt), cost(nt), dest(nt);
+  if (nt > 0) {
+    HIP_TRY(c, launch_uf_init(w->comp, nt, s));
+    HIP_TRY(c, launch_uf_strided(w->comp, gathered, world, nt, 2ll * nt, s));
+    HIP_TRY(c, launch_uf_finalize(w->comp, nt, s));
+    k_cap_tcost<<<grid_for(nt), 256, 0, s>>>(gathered, world, nt, w->tcost);
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipMemcpyAsync(comp.data(), w->comp, static_cast<size_t>(nt) * sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipMemcpyAsync(cost.data(), w->tcost, static_cast<size_t>(nt) * sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+  }
+  // components by cost (its reads' hits, plus one per read), largest first onto the least-loaded
+  // rank (ties: the lower rank) — the same assignment on every rank
+  std::vector<int64_t> ccost(nt, 0);
+  std::vector<int> roots;
+  for (int t = 0; t < nt; ++t) {
+    ccost[comp[t]] += static_cast<int64_t>(cost[t]) + 1;
+    if (comp[t] == t) roots.push_back(t);
+  }
+  std::sort(roots.begin(), roots.end(), [&](int a, int b) { return ccost[a] != ccost[b] ? ccost[a] > ccost[b] : a < b; });
+  std::vector<int64_t> load(world, 0);
+  std::vector<int> droot(nt, 0);
+  for (int r : roots) {
+    int d = 0;
+    for (int k = 1; k < world; ++k)
+      if (load[k] < load[d]) d = k;
+    droot[r] = d;
+    load[d] += ccost[r];
+  }
+  for (int t = 0; t < nt; ++t) dest[t] = droot[comp[t]];
+  if (nt > 0)
+    HIP_TRY(c, hipMemcpyAsync(w->tdest, dest.data(), static_cast<size_t>(nt) * sizeof(int), hipMemcpyHostToDevice, s));
+  // the T-intervals grouped by destination (stable: T order inside a group), their counts and hits
+  HIP_TRY(c, hipMemsetAsync(w->totals, 0, 2 * kMaxDest * sizeof(long long), s));
+  HIP_TRY(c, hipMemsetAsync(w->scnt + nti, 0, sizeof(int), s));
+  if (nti > 0) {
+    k_cap_tikey<<<grid_for(nti), 256, 0, s>>>(w->tread, w->tdest, nti, w->tikey, w->tival);
+    size_t tb = 0;
+    const int kb = bits_for(world);
+    HIP_TRY(c, hipcub::DeviceRadixSort::SortPairs(nullptr, tb, w->tikey, w->tikey2, w->tival, w->tsorted, nti, 0, kb, s));
+    if (int rc = ensure_temp(c, w, tb)) return rc;
+    tb = w->temp_bytes;
+    HIP_TRY(c, hipcub::DeviceRadixSort::SortPairs(w->temp, tb, w->tikey, w->tikey2, w->tival, w->tsorted, nti, 0, kb, s));
+    k_cap_sendcnt<<<std::min(grid_for(nti), 1024), 256, 0, s>>>(w->tsorted, w->tikey2, w->icnt, nti, w->scnt, w->totals);
+    HIP_TRY(c, hipGetLastError());
+  }
+  size_t tb = 0;
+  HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tb, w->scnt, w->shoff, nti + 1, s));
+  if (int rc = ensure_temp(c, w, tb)) return rc;
+  tb = w->temp_bytes;
+  HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(w->temp, tb, w->scnt, w->shoff, nti + 1, s));
+  long long tot[2 * kMaxDest];
+  HIP_TRY(c, hipMemcpyAsync(tot, w->totals, sizeof(tot), hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipStreamSynchronize(s));
+  int64_t off = 0, hits = 0;
+  for (int d = 0; d < world; ++d) {
+    sizes[d] = tot[d];
+    sizes[world + d] = tot[kMaxDest + d];
+    if (d < rank) off += tot[d];
+    hits += tot[kMaxDest + d];
+  }
+  if (hits != w->nloc) return fail(c, FSLR_ERR_STATE, "sharded edge cap: hit totals differ from the local lists");
+  w->nmine = tot[rank];
+  w->mine_off = off;
+  w->planned = 1;
+  return FSLR_OK;
+}
+
+extern "C" int fslr_cap_shard_pack(fslr_ctx* c, int32_t* counts, int32_t* hits) {
+  if (!c) return FSLR_ERR_INVALID;
+  CapWork* w = c->capw;
+  if (!c->cap_gmode || !w || !w->planned) return fail(c, FSLR_ERR_STATE, "fslr_cap_shard_plan first");
+  if ((!counts && w->nti) || (!hits && w->nloc)) return FSLR_ERR_INVALID;
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const int nti = static_cast<int>(w->nti);
+  if (nti) HIP_TRY(c, hipMemcpyAsync(counts, w->scnt, static_cast<size_t>(nti) * sizeof(int), hipMemcpyDeviceToDevice, s));
+  if (nti && w->nloc) {
+    k_cap_pack<<<wave_grid(nti), 256, 0, s>>>(w->tsorted, w->scnt, w->shoff, w->seq, w->ioff, nti, hits);
+    HIP_TRY(c, hipGetLastError());
+  }
+  return FSLR_OK;
+}
+
+extern "C" int fslr_cap_replay_shard(fslr_ctx* c, const int32_t* rcounts, const int32_t* rhits, int64_t* n_changes,
+                                     fslr_cap_stats* part) {
+  if (!c || !n_changes) return FSLR_ERR_INVALID;
+  *n_changes = 0;
+  CapWork* w = c->capw;
+  if (!c->cap_gmode || !w || !w->planned) return fail(c, FSLR_ERR_STATE, "fslr_cap_shard_plan first");
+  const int world = w->g_world, nti = static_cast<int>(w->nti), nt = static_cast<int>(w->nt);
+  const int nmine = static_cast<int>(w->nmine);
+  const int64_t nrc = static_cast<int64_t>(world) * nmine;
+  if (!rcounts && nrc) return FSLR_ERR_INVALID;
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  {
+    Carve cv;
+    cv.add(&w->roff, nrc + 1);
+    cv.add(&w->chgl, w->g_rows);
+    cv.add(&w->nchg, 4);
+    if (int rc = cv.commit(c, w->ar[8])) return rc;
+  }
+  HIP_TRY(c, hipMemsetAsync(w->err, 0, 4 * sizeof(int), s));
+  HIP_TRY(c, hipMemsetAsync(w->stats, 0, kStWords * sizeof(long long), s));
+  HIP_TRY(c, hipMemsetAsync(w->nchg, 0, 4 * sizeof(unsigned), s));
+  // this rank's T-intervals get the received counts, every other one none; the sequence offsets
+  HIP_TRY(c, hipMemsetAsync(w->icnt, 0, static_cast<size_t>(nti + 1) * sizeof(int), s));
+  const int* mine = w->tsorted + w->mine_off;
+  if (nmine > 0) {
+    k_cap_recv_sum<<<grid_for(nmine), 256, 0, s>>>(rcounts, world, nmine, mine, w->icnt);
+    HIP_TRY(c, hipGetLastError());
+  }
+  size_t b1 = 0, b2 = 0;
+  HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(nullptr, b1, w->icnt, w->ioff, nti + 1, s));
+  if (nrc > 0) HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(nullptr, b2, rcounts, w->roff, static_cast<int>(nrc), s));
+  if (int rc = ensure_temp(c, w, std::max(b1, b2))) return rc;
+  size_t tb = w->temp_bytes;
+  HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(w->temp, tb, w->icnt, w->ioff, nti + 1, s));
+  if (nrc > 0) {
+    tb = w->temp_bytes;
+    HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(w->temp, tb, rcounts, w->roff, static_cast<int>(nrc), s));
+  }
+  k_cap_total<<<1, 64, 0, s>>>(w->ioff, nti, w->host_dev, kHNseq);
+  HIP_TRY(c, hipGetLastError());
+  HIP_TRY(c, hipStreamSynchronize(s));
+  w->nseq = host_word(w, kHNseq);
+  if (w->nseq >= (int64_t(1) << 31)) return fail(c, FSLR_ERR_NOMEM, "edge cap replay: more than 2^31 hits");
+  if (w->nseq && !rhits) return FSLR_ERR_INVALID;
+  {
+    Carve cv;
+    cv.add(&w->seq, w->nseq);
+    if (int rc = cv.commit(c, w->ar[4])) return rc;
+  }
+  if (nmine > 0 && w->nseq > 0) {
+    k_cap_recv_assemble<<<wave_grid(nmine), 256, 0, s>>>(rcounts, w->roff, rhits, world, nmine, mine, w->ioff, w->seq);
+    HIP_TRY(c, hipGetLastError());
+  }
+  // slots, predicates and loops of this rank's components (every other T read has no hit: no break)
+  if (int rc = cap_loops(c, w)) return rc;
+  const int ns = static_cast<int>(w->ns);
+  if (w->g_rows > 0) {
+    k_cap_classify_shard<<<grid_for(w->g_rows), 256, 0, s>>>(w->grows, w->g_rows, w->t_of, w->tdest, w->comp, w->g_rank,
+                                                             w->pbrk, w->ukey, ns, w->fpos, w->vis2, w->chgl, w->nchg,
+                                                             w->err);
+    HIP_TRY(c, hipGetLastError());
+  }
+  if (nt > 0) {
+    k_cap_count_capped<<<grid_for(nt), 256, 0, s>>>(w->pbrk, nt, w->stats);
+    HIP_TRY(c, hipGetLastError());
+  }
+  unsigned nch = 0;
+  int err = 0;
+  long long capped = 0;
+  HIP_TRY(c, hipMemcpyAsync(&nch, w->nchg, sizeof(nch), hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipMemcpyAsync(&err, w->err, sizeof(err), hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipMemcpyAsync(&capped, w->stats + kStCapped, sizeof(capped), hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipStreamSynchronize(s));
+  if (err & kCapErrZd) return fail(c, FSLR_ERR_ZERO_DIVISION, "division by zero");
+  if (err & kCapErrState) return fail(c, FSLR_ERR_STATE, "sharded edge cap: inconsistent loop replay");
+  w->n_chg = nch;
+  w->replayed = true;
+  *n_changes = nch;
+  if (part) {
+    std::memset(part, 0, sizeof(*part));
+    part->applied = 1;
+    part->candidates = w->nt;
+    part->capped = capped;
+    part->hits = w->nseq;
+    part->pairs = ns;
+  }
+  return FSLR_OK;
+}
+
+extern "C" int fslr_cap_copy_changes(fslr_ctx* c, int32_t* dst, int64_t n_pad) {
+  if (!c || n_pad < 0 || (!dst && n_pad)) return FSLR_ERR_INVALID;
+  CapWork* w = c->capw;
+  if (!c->cap_gmode || !w || !w->replayed) return fail(c, FSLR_ERR_STATE, "fslr_cap_replay_shard first");
+  if (n_pad < w->n_chg) return fail(c, FSLR_ERR_INVALID, "n_pad below this rank's change count");
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  if (w->n_chg) HIP_TRY(c, hipMemcpyAsync(dst, w->chgl, static_cast<size_t>(w->n_chg) * sizeof(int), hipMemcpyDeviceToDevice, s));
+  if (n_pad > w->n_chg) {
+    k_fill<<<grid_for(n_pad - w->n_chg), 256, 0, s>>>(dst + w->n_chg, static_cast<int>(n_pad - w->n_chg), -1);
+    HIP_TRY(c, hipGetLastError());
+  }
+  return FSLR_OK;
+}
+
+extern "C" int fslr_cap_apply_changes(fslr_ctx* c, const int32_t* changes, int64_t n, fslr_cap_stats* out) {
+  if (!c || n < 0 || (!changes && n)) return FSLR_ERR_INVALID;
+  CapWork* w = c->capw;
+  if (!c->cap_gmode || !w || !w->replayed) return fail(c, FSLR_ERR_STATE, "fslr_cap_replay_shard first");
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const int64_t nr = c->n, rows = w->g_rows, m = w->g_m;
+  const int nt = static_cast<int>(w->nt);
+  const int64_t mloc = std::min(m, c->edge_cap);
+  HIP_TRY(c, hipMemsetAsync(w->err, 0, 4 * sizeof(int), s));
+  HIP_TRY(c, hipMemsetAsync(w->stats, 0, kStWords * sizeof(long long), s));
+  if (rows) HIP_TRY(c, hipMemsetAsync(w->gwho, 0, static_cast<size_t>(rows), s));
+  HIP_TRY(c, hipMemcpyAsync(w->formed, w->gfwd, static_cast<size_t>(nr) * sizeof(int), hipMemcpyDeviceToDevice, s));
+  if (n > 0) {
+    k_cap_apply<<<grid_for(n), 256, 0, s>>>(changes, n, w->grows, w->gwho, w->formed, w->stats);
+    HIP_TRY(c, hipGetLastError());
+  }
+  // this rank's own edges (block g_rank of the rows): kept ones compacted and re-oriented, their formers
+  const int2* blk = w->grows + w->g_rank * m;
+  const unsigned char* wblk = w->gwho + w->g_rank * m;
+  HIP_TRY(c, hipMemsetAsync(c->fwd, 0, static_cast<size_t>(nr) * sizeof(int), s));
+  if (mloc > 0) {
+    k_cap_local_flags<<<grid_for(mloc), 256, 0, s>>>(blk, wblk, mloc, w->kflag);
+    size_t tb = 0;
+    HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tb, w->kflag, w->koff, static_cast<int>(mloc), s));
+    if (int rc = ensure_temp(c, w, tb)) return rc;
+    tb = w->temp_bytes;
+    HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(w->temp, tb, w->kflag, w->koff, static_cast<int>(mloc), s));
+    k_cap_local_compact<<<grid_for(mloc), 256, 0, s>>>(c->edges, c->edge_iu, mloc, w->kflag, w->koff, wblk, w->oedges,
+                                                       w->oiu, c->fwd);
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipMemcpyAsync(c->edges, w->oedges, static_cast<size_t>(mloc) * sizeof(int2), hipMemcpyDeviceToDevice, s));
+    HIP_TRY(c, hipMemcpyAsync(c->edge_iu, w->oiu, static_cast<size_t>(mloc) * sizeof(unsigned short),
+                              hipMemcpyDeviceToDevice, s));
+  }
+  k_cap_check_shard<<<grid_for(std::max<int64_t>(nr, nt)), 256, 0, s>>>(w->T, nt, w->tdest, w->g_rank, w->own, w->formed,
+                                                                       static_cast<int>(nr), w->stats, w->err);
+  // the capped graph's components: every row that some loop forms
+  if (rows > 0) k_cap_drop_rows<<<grid_for(rows), 256, 0, s>>>(w->grows, w->gwho, rows);
+  HIP_TRY(c, hipGetLastError());
+  HIP_TRY(c, launch_uf_init(c->parent, static_cast<int>(nr), s));
+  HIP_TRY(c, launch_uf_pair_list(c->parent, w->grows, rows, s));
+  HIP_TRY(c, launch_uf_finalize(c->parent, static_cast<int>(nr), s));
+  k_cap_commit_shard<<<1, 64, 0, s>>>(w->koff, w->kflag, mloc, c->counters, c->errw, w->stats, w->err, w->host_dev);
+  HIP_TRY(c, hipGetLastError());
+  HIP_TRY(c, hipStreamSynchronize(s));
+  const long long err = host_word(w, kHErr);
+  w->prepared = false;
+  w->planned = 0;
+  w->replayed = false;
+  c->cap_gmode = false;
+  if (err & kCapErrState) return fail(c, FSLR_ERR_STATE, "sharded edge cap: a replayed loop's edge count differs");
+  fslr_cap_stats cs;
+  std::memset(&cs, 0, sizeof(cs));
+  cs.applied = 1;
+  cs.max_fwd = static_cast<int32_t>(host_word(w, kHStat + kStMaxFwd));
+  cs.candidates = w->nt;
+  cs.dropped = host_word(w, kHStat + kStDropped);
+  cs.backward = host_word(w, kHStat + kStBackward);
   c->cap_stats = cs;
   if (out) *out = cs;
   return FSLR_OK;

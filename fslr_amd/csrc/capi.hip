@@ -337,6 +337,7 @@ int fslr_set_reads(fslr_ctx* c, const fslr_reads* r) {
   c->lg_set = false;                        // a virtual-read map belongs to the reads it was set for
   c->lg_perm.clear();
   c->edges_global = false;
+  c->cap_gmode = false;
   ++c->input_gen;
   return FSLR_OK;
 }
@@ -737,6 +738,7 @@ static int prepare_query(fslr_ctx* c, const fslr_params* p, bool keep_sticky = f
                                 c->stream));
   std::memset(&c->cap_stats, 0, sizeof(c->cap_stats));
   c->edges_global = false;
+  c->cap_gmode = false;
   c->last_qcut = p->qlen_cut;                       // the cap replay's pair predicate
   c->last_ncut = p->nal_cut;
   return FSLR_OK;

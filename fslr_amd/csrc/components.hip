@@ -81,6 +81,17 @@ __global__ void k_uf_pair_list(int* p, const int2* __restrict__ pairs, long long
   }
 }
 
+// W label blocks of n values at vals + w * stride (the multi-GPU cap's gathered forests): union of
+// k and vals[w * stride + k] for every block w
+__global__ void k_uf_strided(int* p, const int* __restrict__ vals, long long blocks, int n, long long stride) {
+  for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < blocks * n;
+       k += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const long long w = k / n;
+    const int i = static_cast<int>(k - w * n);
+    uf_union(p, i, vals[w * stride + i]);
+  }
+}
+
 // this context's edges as (a, b) pairs, padded with (-1, -1) to n_pad (count read on the device)
 __global__ void k_copy_edges(const int2* __restrict__ edges, const unsigned long long* __restrict__ count,
                              long long cap, int2* __restrict__ out, long long n_pad) {
@@ -141,6 +152,11 @@ hipError_t launch_uf_pairs(int* parent, const int* src, const int* dst, long lon
 
 hipError_t launch_uf_pair_list(int* parent, const int2* pairs, long long n, hipStream_t s) {
   if (n > 0) k_uf_pair_list<<<grid_for(n), 256, 0, s>>>(parent, pairs, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_uf_strided(int* parent, const int* vals, long long blocks, int n, long long stride, hipStream_t s) {
+  if (blocks > 0 && n > 0) k_uf_strided<<<grid_for(blocks * n), 256, 0, s>>>(parent, vals, blocks, n, stride);
   return hipGetLastError();
 }
 

@@ -122,6 +122,7 @@ struct fslr_ctx {
   double last_qcut = 0.0, last_ncut = 0.0;
   fslr_cap_stats cap_stats = {};
   bool edges_global = false;             // every E* edge is on this context (fslr_cap_install_edges)
+  bool cap_gmode = false;                // gathered E* rows installed for the sharded replay (fslr_cap_install_pairs)
   struct CapWork* capw = nullptr;        // the device cap replay's buffers (cap.hip)
   // reads of more than FSLR_MAX_L intervals (long.hip): the virtual-read map and the long-pair stage
   bool lg_set = false;

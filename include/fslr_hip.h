@@ -33,6 +33,11 @@
  *   fslr_cap_copy_local,
  *   fslr_cap_replay      cluster.py:197-224 the edge cap (:223-224) replayed on a rank that holds every
  *                         E* edge but indexes only its chromosomes (multi-GPU)
+ *   fslr_cap_install_pairs, fslr_cap_sizes, fslr_cap_dep_local, fslr_cap_shard_plan,
+ *   fslr_cap_shard_pack, fslr_cap_replay_shard, fslr_cap_copy_changes,
+ *   fslr_cap_apply_changes
+ *                         cluster.py:197-224 the same loops sharded over the ranks by the components of
+ *                         the candidates' hit graph (multi-GPU)
  *   fslr_set_long_reads,
  *   fslr_long_query,
  *   fslr_get_long_edges   cluster.py:140-170 overall_jaccard_similarity for reads of more than
@@ -68,7 +73,7 @@
 extern "C" {
 #endif
 
-#define FSLR_ABI_VERSION 10
+#define FSLR_ABI_VERSION 11
 #define FSLR_MAX_L 64                /* max intervals per read (bitmask width) */
 #define FSLR_MAX_READS (1 << 25)     /* read rank packs into bits 6..30 of the index record */
 #define FSLR_THR_ZERO_ALN INT32_MIN
@@ -265,6 +270,40 @@ int  fslr_cap_local(fslr_ctx *ctx, int32_t edge_threshold, int64_t *n_ti, int64_
 int  fslr_cap_copy_local(fslr_ctx *ctx, int32_t *counts, int32_t *hits);
 int  fslr_cap_replay(fslr_ctx *ctx, const int32_t *counts, const int32_t *hits, int64_t pad, int32_t world,
                      fslr_cap_stats *out);
+/* The multi-GPU edge cap sharded over the ranks (cluster.py:197-224).  Two loops of the
+ * replay depend on each other only when an interval of one read hits an interval of the other, so the
+ * components of that graph over the candidates T replay independently, each on one rank.
+ * fslr_cap_install_pairs: n_rows gathered E* rows as int32 (a, b) pairs (device; a < 0 = padding;
+ *   rank w's block is rows [w m, (w + 1) m), m = n_rows / world, in its fslr_copy_edges_device order).
+ *   This context's own edges stay its edge list; fslr_cap_local then computes the closure T over the
+ *   gathered rows and lists the hits of T's intervals on this rank's chromosomes (async + syncs).
+ * fslr_cap_sizes: |T|, its intervals, the local hits (after fslr_cap_local).
+ * fslr_cap_dep_local: out[2 |T|] (device): out[t] = the root (smallest index) of T read t in the forest
+ *   of the T-T hits on this rank's chromosomes, out[|T| + t] = its local hit count (async).
+ * fslr_cap_shard_plan: gathered = the ranks' out arrays (world x 2 |T|).  Unions the forests, assigns the
+ *   components to ranks by cost (hits; largest first onto the least-loaded rank: the same on every
+ *   rank) and groups the local lists by destination.  sizes[d] = T-intervals sent to rank d (the same on
+ *   every rank), sizes[world + d] = local hits sent to rank d.  Syncs.
+ * fslr_cap_shard_pack: counts (sum sizes[0 .. world) int32) and hits (sum sizes[world ..)) for one
+ *   all_to_all each, destination-major (async).  The rank receives world x sizes[rank] counts.
+ * fslr_cap_replay_shard: replays the loops of this rank's components from the received counts and hits
+ *   (source-major) and lists the gathered rows it decides that the lower read's loop does not form:
+ *   *n_changes of them; part (may be NULL): its candidates, capped loops, hits and slots.  Syncs.
+ * fslr_cap_copy_changes: the changes (int32 row << 2 | who, who 1 = formed in b's loop, 2 = dropped)
+ *   padded with -1 to n_pad (device, async).  The ranks all-gather them.
+ * fslr_cap_apply_changes: every rank's changes: this context keeps its own capped edges (re-oriented as
+ *   (former, partner)) and their formers' counts (fwd), the components of the whole capped graph
+ *   (fslr_get_labels), errw max_fwd = the largest edges-per-loop.  Syncs; out: applied, max_fwd,
+ *   candidates, dropped, backward (capped / hits / pairs: the sum of the ranks' parts). */
+int  fslr_cap_install_pairs(fslr_ctx *ctx, const int32_t *pairs, int64_t n_rows, int32_t world, int32_t rank);
+int  fslr_cap_sizes(fslr_ctx *ctx, int64_t *n_t, int64_t *n_ti, int64_t *n_hits);
+int  fslr_cap_dep_local(fslr_ctx *ctx, int32_t *out);
+int  fslr_cap_shard_plan(fslr_ctx *ctx, const int32_t *gathered, int32_t world, int32_t rank, int64_t *sizes);
+int  fslr_cap_shard_pack(fslr_ctx *ctx, int32_t *counts, int32_t *hits);
+int  fslr_cap_replay_shard(fslr_ctx *ctx, const int32_t *counts, const int32_t *hits, int64_t *n_changes,
+                           fslr_cap_stats *part);
+int  fslr_cap_copy_changes(fslr_ctx *ctx, int32_t *dst, int64_t n_pad);
+int  fslr_cap_apply_changes(fslr_ctx *ctx, const int32_t *changes, int64_t n, fslr_cap_stats *out);
 int  fslr_sweep_partition(fslr_ctx *ctx, const fslr_params *params, int32_t n_dest, int32_t block_shift,
                           void *dst, int64_t dst_cap, int64_t *counts);
 int  fslr_sweep_evaluate(fslr_ctx *ctx, const fslr_params *params, const void *entries, int64_t n);
