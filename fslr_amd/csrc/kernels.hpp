@@ -203,6 +203,7 @@ struct SweepArgs {
   const long long* spill;             // [3 x count] {s, e, first chunk}: spilled buckets in ent_sorted, or null
   const unsigned long long* spill_n;  // count << 40 | total chunks of kChunk2 entries
   int wbase;                          // first per-wave statistics slot
+  int xcd_map;                        // k_sweep: 1 = each XCD a contiguous share of the chunks, 0 = grid stride
 };
 size_t sweep_temp_bytes(long long ent_cap, long long ni, hipStream_t s);
 int sweep_max_waves();

@@ -106,7 +106,9 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
   const int wx = static_cast<int>(blockIdx.x) / nx * kSwWaves + wv;        // wave index inside the XCD
   const int c_lo = static_cast<int>((static_cast<long long>(nchunks) * xcd) / nx);
   const int c_hi = static_cast<int>((static_cast<long long>(nchunks) * (xcd + 1)) / nx);
-  for (int chunk = c_lo + wx; chunk < c_hi; chunk += bpx * kSwWaves)
+  const int c0 = g.xcd_map ? c_lo + wx : wid, c1 = g.xcd_map ? c_hi : nchunks;
+  const int cstep = g.xcd_map ? bpx * kSwWaves : nw;
+  for (int chunk = c0; chunk < c1; chunk += cstep)
   for (int tile = chunk * run; tile < min(nt, (chunk + 1) * run); ++tile) {
     const int q0 = tile * kWave;
     const int q = q0 + lane;
@@ -1506,8 +1508,19 @@ hipError_t launch_sweep_plan(const SweepArgs& a, hipStream_t s) {
   return hipcub::DeviceScan::ExclusiveSum(a.temp, tb, a.tile_tests, a.tile_ub, nt, s);
 }
 
-hipError_t launch_sweep_count(const SweepArgs& a, int mode, long long* total_dev, hipStream_t s, long long* n_dev,
+// FSLR_SWEEP_MAP=stride: k_sweep's chunks dealt grid-stride (the round-3 mapping), for A/B
+static int sweep_xcd_map() {
+  static const int v = [] {
+    const char* e = std::getenv("FSLR_SWEEP_MAP");
+    return e && std::strcmp(e, "stride") == 0 ? 0 : 1;
+  }();
+  return v;
+}
+
+hipError_t launch_sweep_count(const SweepArgs& a0, int mode, long long* total_dev, hipStream_t s, long long* n_dev,
                               long long cap) {
+  SweepArgs a = a0;
+  a.xcd_map = sweep_xcd_map();
   const int nt = tiles_of(a);
   if (nt == 0) return hipMemsetAsync(total_dev, 0, 3 * sizeof(long long), s);
   const int blocks = std::min(blocks_mode(mode), (nt + kSwWaves - 1) / kSwWaves);
@@ -1547,7 +1560,9 @@ hipError_t launch_sweep_dense(const SweepArgs& a, int mode, hipStream_t s) {
                                                                                     a.tile_cnt, nt, a.ent);
   } else {
     const int be = std::min(blocks_mode(1), (nt + kSwWaves - 1) / kSwWaves);
-    k_sweep<1><<<be, kSwBlock, 0, s>>>(a);
+    SweepArgs a1 = a;
+    a1.xcd_map = sweep_xcd_map();
+    k_sweep<1><<<be, kSwBlock, 0, s>>>(a1);
   }
   return hipGetLastError();
 }

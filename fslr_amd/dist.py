@@ -126,17 +126,124 @@ def chrom_counts_of(csr) -> np.ndarray:
     return np.bincount(np.asarray(csr.iv_chrom), minlength=int(csr.n_chroms))
 
 
-def agree_error(err, world: int, device):
+class TorchComm:
+    """The step's collectives over the default process group (RCCL; with ``gloo`` the device tensors
+    are staged through host memory: the one-GPU rehearsal and the CPU tests)."""
+
+    def __init__(self, device):
+        import torch
+        self.device = torch.device(device)
+
+    @property
+    def gloo(self):
+        import torch.distributed as dist
+        return dist.get_backend() == 'gloo'
+
+    def small(self, values):
+        """An int64 tensor of ``values`` where this backend's small collectives take it."""
+        import torch
+        return torch.as_tensor(np.asarray(values, dtype=np.int64), device='cpu' if self.gloo else self.device)
+
+    def all_to_all(self, out, inp, out_splits=None, in_splits=None):
+        import torch.distributed as dist
+        if self.gloo and out.device.type != 'cpu':
+            o = out.cpu()
+            dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits)
+            out.copy_(o)
+        else:
+            dist.all_to_all_single(out, inp, out_splits, in_splits)
+
+    def all_gather(self, out, inp):
+        import torch.distributed as dist
+        if self.gloo and out.device.type != 'cpu':
+            o = out.new_empty(out.shape, device='cpu')
+            dist.all_gather_into_tensor(o, inp.cpu())
+            out.copy_(o)
+        else:
+            dist.all_gather_into_tensor(out, inp)
+
+    def all_reduce(self, t, op='max'):
+        import torch.distributed as dist
+        dist.all_reduce(t, op=dist.ReduceOp.MAX if op == 'max' else dist.ReduceOp.MIN)
+
+
+class LocalHub:
+    """In-process collectives for W ranks run as threads of one process, each with its own library
+    context (tests: the product's SweepShard at W = 8 on one GPU).  A collective publishes each rank's
+    tensor after a device synchronize, and every rank copies what it needs before the next one."""
+
+    def __init__(self, world: int, timeout: float = 900.0):
+        import threading
+        self.world = int(world)
+        self.barrier = threading.Barrier(self.world, timeout=timeout)
+        self.slots = [None] * self.world
+
+    def comm(self, rank: int, device):
+        return LocalComm(self, rank, device)
+
+
+class LocalComm:
+    gloo = False
+
+    def __init__(self, hub, rank, device):
+        import torch
+        self.hub, self.rank, self.device = hub, int(rank), torch.device(device)
+
+    def small(self, values):
+        import torch
+        return torch.as_tensor(np.asarray(values, dtype=np.int64), device=self.device)
+
+    def _sync(self):
+        import torch
+        if self.device.type == 'cuda':
+            torch.cuda.synchronize(self.device)
+
+    def _publish(self, obj):
+        self._sync()
+        self.hub.slots[self.rank] = obj
+        self.hub.barrier.wait()
+        return list(self.hub.slots)
+
+    def _done(self):
+        self._sync()
+        self.hub.barrier.wait()
+
+    def all_to_all(self, out, inp, out_splits=None, in_splits=None):
+        W = self.hub.world
+        if in_splits is None:
+            in_splits = [inp.numel() // W] * W
+        got = self._publish((inp, list(in_splits)))
+        o = 0
+        for t, spl in got:
+            off, cnt = sum(spl[:self.rank]), spl[self.rank]
+            out[o:o + cnt].copy_(t[off:off + cnt])
+            o += cnt
+        self._done()
+
+    def all_gather(self, out, inp):
+        n = inp.numel()
+        got = self._publish(inp)
+        for w, t in enumerate(got):
+            out[w * n:(w + 1) * n].copy_(t[:n])
+        self._done()
+
+    def all_reduce(self, t, op='max'):
+        import torch
+        got = self._publish(t.clone())
+        st = torch.stack([g.to(t.device) for g in got])
+        t.copy_(st.max(dim=0).values if op == 'max' else st.min(dim=0).values)
+        self._done()
+
+
+def agree_error(err, world: int, device, comm=None):
     """MAX over ranks of an error code (0 none, 1 ZeroDivisionError, 2 other), one all_reduce: every
     rank raises together (its own exception, or one naming the other rank's) instead of leaving the
     others waiting in the next collective."""
-    import torch
-    import torch.distributed as dist
     code = 0 if err is None else (1 if isinstance(err, ZeroDivisionError) else 2)
     if world > 1:
-        gloo = dist.get_backend() == 'gloo'
-        t = torch.tensor([code], dtype=torch.int64, device='cpu' if gloo else device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        comm = comm if comm is not None else TorchComm(device)
+        t = comm.small([code])
+        comm.all_reduce(t, 'max')
         code = int(t.item())
     if err is not None:
         raise err
@@ -154,15 +261,16 @@ class SweepShard:
     step() leaves this rank's edges / forward degrees (pairs whose first read it owns) in ``ctx``
     and the global min-rank labels in ``ctx`` (labels()).  When the reference's edge cap binds
     (some read has more than ``edge_threshold`` forward edges) the graph depends on the sequential
-    order of the reference's loops: the ranks exchange the E* edges and the candidate reads' hit
-    lists and every rank replays the loops on its device (``capped`` in the step's result; ``ctx``
-    then holds the whole capped graph on every rank).
+    order of the reference's loops: the loops are replayed sharded over the ranks by the components
+    of the candidates' hit graph (``capped`` in the step's result; ``ctx`` then holds this rank's
+    capped edges, re-oriented as the reference's match rows, and their formers' edge counts).
     """
 
     def __init__(self, ctx, n_reads: int, chrom_counts, world: int, rank: int, device, block_shift: int = 6,
-                 owner=None):
+                 owner=None, comm=None):
         import torch
         self.ctx = ctx
+        self.comm = comm if comm is not None else TorchComm(device)
         self.n = int(n_reads)
         self.world = int(world)
         self.rank = int(rank)
@@ -179,28 +287,12 @@ class SweepShard:
         self._rep = None                   # the last synchronous step's counts (repeat steps)
         ctx.set_chrom_filter(self.owned if world > 1 else None)
 
-    # -- collectives (RCCL; gloo stages device tensors through host memory) -----------------------
-    def _gloo(self):
-        import torch.distributed as dist
-        return dist.get_backend() == 'gloo'
-
+    # -- collectives (self.comm: RCCL, gloo staged through host memory, or in-process) --------------
     def _all_to_all(self, out, inp, out_splits, in_splits):
-        import torch.distributed as dist
-        if self._gloo() and out.device.type != 'cpu':
-            o = out.cpu()
-            dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits)
-            out.copy_(o)
-        else:
-            dist.all_to_all_single(out, inp, out_splits, in_splits)
+        self.comm.all_to_all(out, inp, out_splits, in_splits)
 
     def _all_gather(self, out, inp):
-        import torch.distributed as dist
-        if self._gloo() and out.device.type != 'cpu':
-            o = out.new_empty(out.shape, device='cpu')
-            dist.all_gather_into_tensor(o, inp.cpu())
-            out.copy_(o)
-        else:
-            dist.all_gather_into_tensor(out, inp)
+        self.comm.all_gather(out, inp)
 
     def _grow(self, t, need):
         import torch
@@ -219,7 +311,6 @@ class SweepShard:
         without host syncs: the partition lands where it did (fslr_sweep_partition_repeat, checked
         on the device), and the exchanges reuse its counts; verify_repeat() checks afterwards."""
         import torch
-        import torch.distributed as dist
         ctx, W = self.ctx, self.world
         self._labels = None
         rep = self._rep if repeat else None
@@ -245,10 +336,9 @@ class SweepShard:
         sweep_stats = ctx.stats(check=False) if collect and err is None else None
         sent_total = int(counts.sum())
         if W > 1:
-            cdev = 'cpu' if self._gloo() else self.device
-            cin = torch.from_numpy(counts).to(cdev)
+            cin = self.comm.small(counts)
             cout = torch.empty_like(cin)
-            dist.all_to_all_single(cout, cin)
+            self.comm.all_to_all(cout, cin)
             recv_counts = cout.cpu().numpy()
             if err is not None or (recv_counts < 0).any():
                 if err is None:
@@ -287,8 +377,8 @@ class SweepShard:
             # raises on one evaluator raises on every rank instead of leaving the others in a
             # collective, and every rank knows the padded size of the edge exchange
             code = 0 if err is None else (1 if isinstance(err, ZeroDivisionError) else 2)
-            t = torch.tensor([mf, code, max_ne], dtype=torch.int64, device='cpu' if self._gloo() else self.device)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            t = self.comm.small([mf, code, max_ne])
+            self.comm.all_reduce(t, 'max')
             mf, code, max_ne = (int(x) for x in t.tolist())
             if err is None and code:
                 from ._lib import FslrError
@@ -340,8 +430,6 @@ class SweepShard:
     def verify_repeat(self):
         """After repeat steps: every rank's device flags are clean (the partition totals equal the
         synchronous step's, no error) and its edge count is unchanged; raises on every rank otherwise."""
-        import torch
-        import torch.distributed as dist
         rep = self._rep
         ok = 1
         err = None
@@ -353,8 +441,8 @@ class SweepShard:
             err = e
             ok = 0
         if self.world > 1:
-            t = torch.tensor([ok], dtype=torch.int64, device='cpu' if self._gloo() else self.device)
-            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            t = self.comm.small([ok])
+            self.comm.all_reduce(t, 'min')
             ok = int(t.item())
         if err is not None:
             raise err
@@ -370,60 +458,109 @@ class SweepShard:
         return torch.empty(int(need * 1.125) + 4096, dtype=torch.int32, device=self.device)
 
     def _agree(self, err):
-        agree_error(err, self.world, self.device)
+        agree_error(err, self.world, self.device, self.comm)
 
     def _capped_labels(self, edge_threshold, max_ne):
         """The cap binds: the reference's graph depends on the sequential order of its loops
-        (cluster.py:197-224).  Every rank gathers the whole E* list and the search-ordered hits of the
-        candidate reads' intervals (each rank lists those of its chromosomes), then replays the loops
-        on its device (fslr_cap_replay) and takes the components: the same capped graph on every rank,
-        with no rank re-running the query."""
+        (cluster.py:197-224).  Two loops depend on each other only when an interval of one read hits an
+        interval of the other, so the loops are replayed sharded by the components of that graph over
+        the candidates T (fslr_hip.h fslr_cap_install_pairs ... fslr_cap_apply_changes):
+
+        1. every rank gathers E* as (a, b) rows (the exchange of the uncapped merge), computes the
+           closure T and lists the search-ordered hits of T's intervals on its own chromosomes;
+        2. the ranks' local forests of the T-T hits (and T's hit counts) are all-gathered; every rank
+           unions them and assigns the same components to ranks by cost;
+        3. the lists travel to the rank replaying their read's component (all_to_all);
+        4. each rank replays its components' loops and lists the rows they do not form in the lower
+           read's loop (re-oriented or dropped);
+        5. those changes are all-gathered and applied everywhere: each rank keeps its own capped edges
+           and forward degrees (the reference's match rows), every rank has the capped graph's labels.
+        """
         import torch
-        import torch.distributed as dist
-        ctx, W = self.ctx, self.world
+        ctx, W, r = self.ctx, self.world, self.rank
         m = max(1, int(max_ne))
         err = None
+        self.esend = self._grow(self.esend, m)
+        self.egath = self._grow(self.egath, W * m)
+        ctx.edges_into(self.esend, m)
+        if W > 1:
+            self._all_gather(self.egath[:W * m], self.esend[:m])
+            rows = self.egath
+        else:
+            rows = self.esend
+        nt = 0
         try:
-            self.rsend = self._grow32(getattr(self, 'rsend', None), 4 * m)
-            ctx.edges_iu_into(self.rsend, m)
+            ctx.cap_install_pairs(rows, W * m, W, r)
+            ctx.cap_local(edge_threshold)
+            nt = ctx.cap_sizes()[0]
+            self.tinfo = self._grow32(getattr(self, 'tinfo', None), max(1, 2 * nt))
+            ctx.cap_dep_local(self.tinfo)
         except Exception as e:                          # noqa: BLE001 - re-raised on every rank
             err = e
         self._agree(err)
-        self.rgath = self._grow32(getattr(self, 'rgath', None), 4 * W * m)
         if W > 1:
-            self._all_gather(self.rgath[:4 * W * m], self.rsend[:4 * m])
-            rows = self.rgath
+            self.tgath = self._grow32(getattr(self, 'tgath', None), max(1, W * 2 * nt))
+            if nt:
+                self._all_gather(self.tgath[:W * 2 * nt], self.tinfo[:2 * nt])
+            tg = self.tgath
         else:
-            rows = self.rsend
-        nti = nh = 0
+            tg = self.tinfo
+        ti_d = hits_d = np.zeros(W, np.int64)
         try:
-            ctx.cap_install_edges(rows, W * m)
-            nti, nh = ctx.cap_local(edge_threshold)
+            ti_d, hits_d = ctx.cap_shard_plan(tg, W, r)
+            self.csend = self._grow32(getattr(self, 'csend', None), max(1, int(ti_d.sum())))
+            self.hsend = self._grow32(getattr(self, 'hsend', None), max(1, int(hits_d.sum())))
+            ctx.cap_shard_pack(self.csend, self.hsend)
         except Exception as e:                          # noqa: BLE001
             err = e
         self._agree(err)
-        pad = nh
+        nmine = int(ti_d[r])
         if W > 1:
-            t = torch.tensor([nh], dtype=torch.int64, device='cpu' if self._gloo() else self.device)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            pad = int(t.item())
-        pad = max(1, pad)
-        self.csend = self._grow32(getattr(self, 'csend', None), max(1, nti))
-        self.hsend = self._grow32(getattr(self, 'hsend', None), pad)
-        ctx.cap_copy_local(self.csend, self.hsend)
-        if W > 1:
-            self.cgath = self._grow32(getattr(self, 'cgath', None), max(1, W * nti))
-            self.hgath = self._grow32(getattr(self, 'hgath', None), W * pad)
-            if nti:
-                self._all_gather(self.cgath[:W * nti], self.csend[:nti])
-            self._all_gather(self.hgath[:W * pad], self.hsend[:pad])
-            counts, hits = self.cgath, self.hgath
+            self.crecv = self._grow32(getattr(self, 'crecv', None), max(1, W * nmine))
+            self._all_to_all(self.crecv[:W * nmine], self.csend[:int(ti_d.sum())], [nmine] * W, ti_d.tolist())
+            hin = self.comm.small(hits_d)
+            hout = torch.empty_like(hin)
+            self._all_to_all(hout, hin, [1] * W, [1] * W)
+            hits_from = hout.cpu().numpy()
+            self.hrecv = self._grow32(getattr(self, 'hrecv', None), max(1, int(hits_from.sum())))
+            self._all_to_all(self.hrecv[:int(hits_from.sum())], self.hsend[:int(hits_d.sum())], hits_from.tolist(),
+                             hits_d.tolist())
+            rcnt, rhits = self.crecv, self.hrecv
         else:
-            counts, hits = self.csend, self.hsend
+            rcnt, rhits = self.csend, self.hsend
+        nch, part = 0, {}
+        try:
+            nch, part = ctx.cap_replay_shard(rcnt, rhits)
+        except Exception as e:                          # noqa: BLE001
+            err = e
+        # the error code rides with the change count and the partial statistics
+        code = 0 if err is None else (1 if isinstance(err, ZeroDivisionError) else 2)
+        mine = np.array([code, nch, part.get('capped', 0), part.get('hits', 0), part.get('pairs', 0)], np.int64)
+        if W > 1:
+            t = self.comm.small(mine)
+            g = torch.empty(5 * W, dtype=torch.int64, device=t.device)
+            self._all_gather(g, t)
+            allp = g.cpu().numpy().reshape(W, 5)
+        else:
+            allp = mine.reshape(1, 5)
+        if err is not None:
+            raise err
+        if allp[:, 0].max():
+            from ._lib import FslrError
+            raise ZeroDivisionError('division by zero') if (allp[:, 0] == 1).any() else FslrError('error on another rank')
+        pad = max(1, int(allp[:, 1].max()))
+        self.chsend = self._grow32(getattr(self, 'chsend', None), pad)
+        ctx.cap_copy_changes(self.chsend, pad)
+        if W > 1:
+            self.chgath = self._grow32(getattr(self, 'chgath', None), W * pad)
+            self._all_gather(self.chgath[:W * pad], self.chsend[:pad])
+            chg = self.chgath
+        else:
+            chg = self.chsend
         cap = {}
         try:
-            cap = ctx.cap_replay(counts, hits, pad, W)
-            ctx.components()
+            cap = ctx.cap_apply_changes(chg, W * pad)
+            cap.update(capped=int(allp[:, 2].sum()), hits=int(allp[:, 3].sum()), pairs=int(allp[:, 4].sum()))
         except Exception as e:                          # noqa: BLE001
             err = e
         self._agree(err)

@@ -13,7 +13,8 @@ children) and every rank runs one step of the chromosome-split sweep (dist.Sweep
 §6): it indexes and sweeps the chromosomes it owns, RCCL all_to_all routes the match entries to the
 rank that owns each pair's first read, that rank evaluates the pair, and the ranks' edge lists are
 all-gathered for the components.  When the reference's edge cap binds (cluster.py:223-224) the
-ranks exchange E* and the candidates' hit lists and every rank replays the loops on its device.
+candidates' loops are replayed sharded by the components of their hit graph, each rank replaying
+its components and the ranks exchanging the rows their loops re-orient or drop.
 
 Rank 0 returns the labels and the union of the ranks' edges and forward degrees (the children hand
 theirs back through the same directory): they are the single-GPU results exactly.  An exception on
@@ -109,9 +110,9 @@ class _Rank:
         self.ctx = None                               # the rank's library context, kept across queries
 
     def step(self, d):
-        """One query on the CSR in directory d; rank 0: the labels, its edges and forward degrees (all
-        of them when the cap bound: every rank then holds the whole capped graph); other ranks: their
-        edges and forward degrees.  The caller's current device and stream are restored."""
+        """One query on the CSR in directory d: the labels (every rank holds them), this rank's edges
+        and forward degrees (capped ones when the cap bound).  The caller's current device and stream
+        are restored."""
         import torch
         from . import _lib
         from .dist import SweepShard, agree_error, chrom_counts_of
@@ -145,13 +146,9 @@ class _Rank:
                 info = shard.step(meta['qlen_cut'], meta['nal_cut'], pt, int(meta['edge_threshold']))
                 torch.cuda.synchronize(self.dev)
                 labels = shard.labels()
-                if info['capped'] and self.rank != 0:
-                    a = b = I = U = np.zeros(0, np.int32)
-                    fwd = np.zeros(csr.n_reads, np.int32)
-                else:
-                    st = ctx.stats()
-                    a, b, I, U = ctx.edges(st['n_edges'])
-                    fwd = ctx.fwd_degree()
+                st = ctx.stats()
+                a, b, I, U = ctx.edges(st['n_edges'])
+                fwd = ctx.fwd_degree()
                 return {'labels': labels, 'edges': (a, b, I, U), 'fwd': fwd, 'capped': bool(info['capped']),
                         'max_fwd': int(info['max_fwd']), 'cap': info.get('cap', {}), 'backend': self.backend}
             except BaseException:

@@ -204,15 +204,17 @@ class EmuSweepContext:
         self._edges = np.stack([rows[:, 0], rows[:, 1], rows[:, 2] & 0xff, rows[:, 2] >> 8], axis=1)
         self._fwd = np.bincount(rows[:, 0], minlength=self.n_reads)
 
-    def _candidates(self, thr):
+    def _candidates(self, thr, edges=None, fwd=None):
         """T: x joins when fwd(x) + #{y in T, y < x, (y, x) in E*} >= thr (rank order)."""
+        edges = self._edges[:, :2] if edges is None else edges
+        fwd = self._fwd if fwd is None else fwd
         back = np.zeros(self.n_reads, np.int64)
         adj = {}
-        for a, b in self._edges[:, :2].tolist():
+        for a, b in edges.tolist():
             adj.setdefault(a, []).append(b)
         T = []
         for x in range(self.n_reads):
-            if self._fwd[x] + back[x] >= thr:
+            if fwd[x] + back[x] >= thr:
                 T.append(x)
                 for y in adj.get(x, ()):
                     back[y] += 1
@@ -239,7 +241,11 @@ class EmuSweepContext:
 
     def cap_local(self, edge_threshold=10):
         self._cap_thr = edge_threshold
-        self._T = self._candidates(edge_threshold)
+        if getattr(self, '_gmode', False):
+            g = self._g[self._g[:, 0] >= 0]
+            self._T = self._candidates(edge_threshold, g, self._gfwd)
+        else:
+            self._T = self._candidates(edge_threshold)
         lists = self._hit_lists(self._T, self.owned)
         self._cap_counts = np.array([len(x) for x in lists], np.int32)
         self._cap_hits = np.array([y for x in lists for y in x], np.int32)
@@ -281,3 +287,159 @@ class EmuSweepContext:
         self._st = {'n_edges': len(self._edges), 'edge_capacity': self.edge_capacity,
                     'max_fwd': int(self._fwd.max()) if self._fwd.size else 0}
         return {'applied': 1}
+
+    # -- the sharded edge cap (fslr_cap_install_pairs ... fslr_cap_apply_changes) ------------------
+    def cap_install_pairs(self, t, n_rows, world, rank):
+        self._g = t.numpy()[:n_rows].view(np.int32).reshape(-1, 2).astype(np.int64)
+        self._gw, self._gr, self._gm = int(world), int(rank), int(n_rows) // int(world)
+        v = self._g[:, 0] >= 0
+        self._gfwd = np.bincount(self._g[v, 0], minlength=self.n_reads)
+        self._gmode = True
+
+    def cap_sizes(self):
+        return len(self._T), int(self._cap_counts.size), int(self._cap_hits.size)
+
+    def _ti_read(self):
+        off = np.asarray(self.csr.read_off, np.int64)
+        return np.repeat(np.arange(len(self._T)), [off[x + 1] - off[x] for x in self._T]).astype(np.int64)
+
+    def cap_dep_local(self, t):
+        """Roots (smallest t) of the forest of T-T hits on this rank's chromosomes; local hits per t."""
+        nt = len(self._T)
+        t_of = {x: k for k, x in enumerate(self._T)}
+        par = list(range(nt))
+
+        def find(x):
+            while par[x] != x:
+                x = par[x]
+            return x
+        tread = self._ti_read()
+        hits = np.zeros(nt, np.int64)
+        pos = 0
+        for ti, cnt in enumerate(self._cap_counts.tolist()):
+            tx = int(tread[ti])
+            hits[tx] += cnt
+            for y in self._cap_hits[pos:pos + cnt].tolist():
+                if y in t_of:
+                    a, b = find(tx), find(t_of[y])
+                    if a != b:
+                        par[max(a, b)] = min(a, b)
+            pos += cnt
+        out = t.numpy()
+        out[:nt] = [find(k) for k in range(nt)]
+        out[nt:2 * nt] = hits
+
+    def cap_shard_plan(self, gathered, world, rank):
+        nt = len(self._T)
+        g = gathered.numpy()[:world * 2 * nt].reshape(world, 2 * nt).astype(np.int64)
+        par = list(range(nt))
+
+        def find(x):
+            while par[x] != x:
+                x = par[x]
+            return x
+        for w in range(world):
+            for k in range(nt):
+                a, b = find(k), find(int(g[w, k]))
+                if a != b:
+                    par[max(a, b)] = min(a, b)
+        comp = np.array([find(k) for k in range(nt)], np.int64)
+        cost = g[:, nt:].sum(axis=0) + 1
+        ccost = np.bincount(comp, weights=cost, minlength=nt).astype(np.int64)
+        roots = sorted(set(comp.tolist()), key=lambda r: (-ccost[r], r))
+        load = np.zeros(world, np.int64)
+        droot = {}
+        for r in roots:
+            d = int(np.argmin(load))
+            droot[r] = d
+            load[d] += ccost[r]
+        self._comp = comp
+        self._tdest = np.array([droot[c] for c in comp.tolist()], np.int64)
+        tread = self._ti_read()
+        dti = self._tdest[tread]
+        self._tsorted = np.argsort(dti, kind='stable')
+        ti_d = np.bincount(dti, minlength=world).astype(np.int64)
+        hits_d = np.bincount(dti, weights=self._cap_counts, minlength=world).astype(np.int64)
+        self._mine = self._tsorted[ti_d[:rank].sum():ti_d[:rank + 1].sum()]
+        return ti_d, hits_d
+
+    def cap_shard_pack(self, counts, hits):
+        off = np.concatenate([[0], np.cumsum(self._cap_counts)])
+        c = self._cap_counts[self._tsorted]
+        counts.numpy()[:c.size] = c
+        h = [self._cap_hits[off[ti]:off[ti + 1]] for ti in self._tsorted.tolist()]
+        if h:
+            h = np.concatenate(h)
+            hits.numpy()[:h.size] = h
+
+    def cap_replay_shard(self, counts, hits):
+        """Assemble this rank's T-intervals' lists from the received ones and check them against an
+        unfiltered index's; the changes of the rows it decides come from the oracle's capped graph."""
+        W, nm = self._gw, self._mine.size
+        rc = counts.numpy()[:W * nm].reshape(W, nm)
+        assert ((rc > 0).sum(axis=0) <= 1).all(), 'an interval listed by two ranks'
+        rh = hits.numpy()
+        pos = np.concatenate([[0], np.cumsum(rc.reshape(-1))])
+        full = self._hit_lists(self._T, None)
+        for i, ti in enumerate(self._mine.tolist()):
+            seg = []
+            for w in range(W):
+                k = w * nm + i
+                seg += rh[pos[k]:pos[k + 1]].tolist()
+            assert seg == full[ti]
+        from oracle import oracle as O
+        c = self.csr
+        cnt = np.diff(c.read_off)
+        oc = O.OracleCSR(c.read_off, c.iv_chrom, c.iv_start, c.iv_end, c.iv_aln, np.repeat(c.read_qlen2, cnt),
+                         np.repeat(c.read_nal, cnt), c.data_pos)
+        qd, nd, ov = self.diffs
+        o = O.run_core(oc, overlap=ov, use_cap=True, qlen_diff=qd, n_aln_diff=nd, edge_threshold=self._cap_thr)
+        kept = set(zip(np.asarray(o['edge_a']).tolist(), np.asarray(o['edge_b']).tolist()))
+        t_of = {x: k for k, x in enumerate(self._T)}
+        chg = []
+        for k, (a, b) in enumerate(self._g.tolist()):
+            if a < 0:
+                continue
+            t = t_of.get(a, t_of.get(b, -1))
+            if t < 0 or self._tdest[t] != self._gr:
+                continue
+            w = 0 if (a, b) in kept else (1 if (b, a) in kept else 2)
+            if w:
+                chg.append((k << 2) | w)
+        self._chg = np.array(chg, np.int32)
+        return len(chg), {'applied': 1, 'candidates': len(self._T), 'capped': 0,
+                          'hits': int(sum(len(full[ti]) for ti in self._mine.tolist())), 'pairs': 0}
+
+    def cap_copy_changes(self, t, n_pad):
+        out = np.full(n_pad, -1, np.int32)
+        out[:self._chg.size] = self._chg
+        t.numpy()[:n_pad] = out
+
+    def cap_apply_changes(self, t, n):
+        ch = t.numpy()[:n].astype(np.int64)
+        ch = ch[ch >= 0]
+        who = np.zeros(len(self._g), np.int64)
+        who[ch >> 2] = ch & 3
+        m, r = self._gm, self._gr
+        loc = self._edges
+        wl = who[r * m:r * m + len(loc)]
+        keep = wl != 2
+        e = loc[keep].copy()
+        fl = wl[keep] == 1
+        e[fl, 0], e[fl, 1] = loc[keep][fl, 1], loc[keep][fl, 0]
+        self._edges = e
+        self._fwd = np.bincount(e[:, 0], minlength=self.n_reads) if len(e) else np.zeros(self.n_reads, np.int64)
+        formed = self._gfwd.copy()
+        for k in np.flatnonzero(who).tolist():
+            a, b = self._g[k]
+            formed[a] -= 1
+            if who[k] == 1:
+                formed[b] += 1
+        self._parent = np.arange(self.n_reads)
+        for k, (a, b) in enumerate(self._g.tolist()):
+            if a >= 0 and who[k] != 2:
+                self._union(a, b)
+        self._gmode = False
+        self._st = {'n_edges': len(e), 'edge_capacity': self.edge_capacity, 'max_fwd': int(formed.max())}
+        return {'applied': 1, 'max_fwd': int(formed.max()), 'candidates': len(self._T), 'capped': 0, 'hits': 0,
+                'pairs': 0, 'dropped': int((who == 2).sum()), 'backward': int((who == 1).sum())}

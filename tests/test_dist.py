@@ -259,9 +259,9 @@ def test_gloo_world2_sweep_shard_equals_oracle(world_case, tmp_path, edge_thresh
     """dist.SweepShard over gloo with world_size 2 (real all_to_all of entries, all-reduce of the
     forward degree, all-gather of labels) on the emulated device: both ranks end with the oracle's
     components; the ranks' edges partition the oracle's edges.  edge_threshold 2 makes the cap bind:
-    the ranks all-gather E* and the candidates' hit lists (each rank lists its chromosomes' hits; the
-    emulator checks the assembled lists against an unfiltered index) and every rank holds the
-    oracle's capped graph."""
+    the sharded replay's exchanges run for real (gathered E* rows, the local T-T forests, the hit lists
+    to the components' ranks — the emulator checks each rank's assembled lists against an unfiltered
+    index — and the change lists) and the ranks' capped edges partition the oracle's capped graph."""
     import torch.multiprocessing as mp
     from fslr_amd.prep import fold_overlap_threshold
     csr, o = world_case
@@ -282,11 +282,56 @@ def test_gloo_world2_sweep_shard_equals_oracle(world_case, tmp_path, edge_thresh
         want = sorted(zip(o['edge_a'].tolist(), o['edge_b'].tolist(), o['edge_I'].tolist(), o['edge_U'].tolist()))
         assert got == want
     else:
+        # the sharded replay: the ranks' capped edges (re-oriented as (former, partner)) partition the
+        # oracle's capped graph
         want = sorted(zip(ref['edge_a'].tolist(), ref['edge_b'].tolist(), ref['edge_I'].tolist(),
                           ref['edge_U'].tolist()))
-        for r in range(2):                              # every rank holds the whole capped graph
-            got = sorted(map(tuple, np.load(tmp_path / f'edges{r}.npy').astype(np.int64).tolist()))
-            assert got == want
+        e = np.concatenate([np.load(tmp_path / f'edges{r}.npy') for r in range(2)]).astype(np.int64)
+        assert sorted(map(tuple, e.tolist())) == want
+
+
+@pytest.mark.parametrize('edge_threshold', [10, 2])
+def test_local_hub_w3_sweep_shard_equals_oracle(world_case, edge_threshold):
+    """dist.SweepShard on W = 3 ranks as threads over dist.LocalHub (the in-process collectives the
+    10M-read GPU test runs the product split with), on the emulated device: every rank has the
+    oracle's components and the ranks' edges partition the oracle's (capped when edge_threshold 2)."""
+    import threading
+    from fslr_amd.dist import LocalHub, SweepShard, chrom_counts_of
+    from fslr_amd.prep import fold_overlap_threshold, pass_table
+    from tests.sweep_emu import EmuSweepContext
+    csr, o = world_case
+    thr = fold_overlap_threshold(csr.iv_aln, 0.8)
+    pt = pass_table([1, 1, 0.66, 0.66, 0.66, 0.5])
+    W = 3
+    hub = LocalHub(W, timeout=120)
+    ctxs = [EmuSweepContext(csr, thr) for _ in range(W)]
+    infos, errs = [None] * W, [None] * W
+
+    def run(r):
+        try:
+            sh = SweepShard(ctxs[r], csr.n_reads, chrom_counts_of(csr), W, r, 'cpu', comm=hub.comm(r, 'cpu'))
+            infos[r] = sh.step(1 - 0.04, 1 - 0.25, pt, edge_threshold)
+        except BaseException as e:                     # noqa: BLE001
+            errs[r] = e
+            hub.barrier.abort()
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in range(W)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for e in errs:
+        if e is not None:
+            raise e
+    ref = o if edge_threshold == 10 else O.run_core(_oracle_csr(csr), use_cap=True, edge_threshold=edge_threshold)
+    assert all(i['capped'] == (edge_threshold == 2) for i in infos)
+    got = []
+    for c in ctxs:
+        a, b, I, U = c.edges(c.stats()['n_edges'])
+        got += list(zip(a.tolist(), b.tolist(), I.tolist(), U.tolist()))
+        np.testing.assert_array_equal(_components_from_labels(c.labels()), ref['comp'])
+    want = sorted(zip(ref['edge_a'].tolist(), ref['edge_b'].tolist(), ref['edge_I'].tolist(), ref['edge_U'].tolist()))
+    assert sorted(got) == want
 
 
 def _one_stream():
@@ -384,79 +429,65 @@ def test_sweep_split_contexts_one_gpu_equals_oracle(W):
     assert per_rank.min() > 0 and per_rank.max() < 2.0 * per_rank.mean()
 
 
-def _sweep_split_capped_on_device(csr, thr, pt, W, edge_threshold, block_shift=6):
-    """The chromosome split with a binding cap, W contexts on cuda:0, every exchange done in-process
-    as the collectives would (torch.cat of the ranks' buffers): partition, evaluate, then the cap
-    exchange of SweepShard._capped_labels — E* rows, candidates' hit lists of each rank's
-    chromosomes, a replay on every rank.  No context runs fslr_query.  Returns the contexts."""
+def _sweep_shards_threads(csr, thr, pt, W, edge_threshold, steps=1):
+    """The product's dist.SweepShard on W ranks that are threads of this process, each with its own
+    context and stream on cuda:0, the collectives in-process (dist.LocalHub: a device synchronize,
+    then every rank copies what it needs).  Returns (contexts, step infos of the last step)."""
+    import threading
     import torch
     from fslr_amd import _lib
-    from fslr_amd.dist import chrom_counts_of, chrom_owner
+    from fslr_amd.dist import LocalHub, SweepShard, chrom_counts_of
     dev = torch.device('cuda', 0)
-    stream = _one_stream()
-    owner = chrom_owner(chrom_counts_of(csr), W)
-    ctxs, segs = [], [[] for _ in range(W)]
-    for r in range(W):
-        c = _lib.Context(0, stream=stream.cuda_stream)
-        c.load_csr(csr, thr)
-        c.reserve_edges(12 * csr.n_reads)
-        c.set_chrom_filter(owner == r if W > 1 else None)
-        c.build_index()
-        buf = torch.empty(1 << 16, dtype=torch.int64, device=dev)
-        ok, counts = c.sweep_partition(1 - 0.04, 1 - 0.25, pt, W, block_shift, buf, edge_threshold)
-        if not ok:
-            buf = torch.empty(int(counts.sum()) + 16, dtype=torch.int64, device=dev)
-            ok, counts = c.sweep_partition(1 - 0.04, 1 - 0.25, pt, W, block_shift, buf, edge_threshold)
-        assert ok
-        pos = np.concatenate([[0], np.cumsum(counts)])
-        for d in range(W):
-            segs[d].append(buf[pos[d]:pos[d + 1]].clone())
-        ctxs.append(c)
-    for d, c in enumerate(ctxs):
-        ent = torch.cat(segs[d])
-        c.sweep_evaluate(1 - 0.04, 1 - 0.25, pt, ent, ent.numel(), edge_threshold)
-    torch.cuda.synchronize()
-    ne = [c.stats()['n_edges'] for c in ctxs]
-    assert max(c.stats()['max_fwd'] for c in ctxs) > edge_threshold          # the cap binds
-    m = max(1, max(ne))
-    rows = []
-    for c in ctxs:
-        t = torch.empty(4 * m, dtype=torch.int32, device=dev)
-        c.edges_iu_into(t, m)
-        rows.append(t)
-    torch.cuda.synchronize()
-    gathered = torch.cat(rows)
-    loc = []
-    for c in ctxs:
-        c.cap_install_edges(gathered, W * m)
-        loc.append(c.cap_local(edge_threshold))
-    nti = loc[0][0]
-    assert all(x[0] == nti for x in loc)
-    pad = max(1, max(x[1] for x in loc))
-    cnts, hits = [], []
-    for c in ctxs:
-        cnts.append(torch.zeros(max(1, nti), dtype=torch.int32, device=dev))
-        hits.append(torch.full((pad,), -7, dtype=torch.int32, device=dev))
-        c.cap_copy_local(cnts[-1], hits[-1])
-    torch.cuda.synchronize()
-    cg = torch.cat([x[:nti] for x in cnts]) if nti else cnts[0]
-    hg = torch.cat(hits)
-    caps = []
-    for c in ctxs:
-        caps.append(c.cap_replay(cg, hg, pad, W))
-        c.components()
-    torch.cuda.synchronize()
-    assert all(cp['applied'] == 1 for cp in caps) and all(cp == caps[0] for cp in caps)
-    return ctxs, caps[0]
+    hub = LocalHub(W)
+    ctxs, infos, errs = [None] * W, [None] * W, [None] * W
+
+    def run(r):
+        try:
+            s = torch.cuda.Stream(dev)
+            torch.cuda.set_stream(s)
+            c = _lib.Context(0, stream=s.cuda_stream)
+            ctxs[r] = c
+            c.load_csr(csr, thr)
+            c.reserve_edges(max(1 << 16, 12 * csr.n_reads // W))
+            sh = SweepShard(c, csr.n_reads, chrom_counts_of(csr), W, r, dev, comm=hub.comm(r, dev))
+            for _ in range(steps):
+                infos[r] = sh.step(1 - 0.04, 1 - 0.25, pt, edge_threshold)
+            torch.cuda.synchronize(dev)
+        except BaseException as e:                     # noqa: BLE001 - re-raised by the caller
+            errs[r] = e
+            hub.barrier.abort()
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in range(W)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for e in errs:
+        if e is not None and not isinstance(e, threading.BrokenBarrierError):
+            raise e
+    for e in errs:
+        if e is not None:
+            raise e
+    return ctxs, infos
+
+
+def _union_view(ctxs):
+    """The ranks' edges (a, b, I, U) concatenated and their forward degrees summed."""
+    parts = [c.edges(c.stats()['n_edges']) for c in ctxs]
+    a, b, I, U = (np.concatenate([p[k] for p in parts]) for k in range(4))
+    fwd = np.sum([c.fwd_degree().astype(np.int64) for c in ctxs], axis=0)
+    return a, b, I, U, fwd
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('W', [1, 2, 8])
 @pytest.mark.parametrize('thr', [3, 10])
 def test_sweep_split_capped_one_gpu_equals_oracle(W, thr):
-    """The cap replay of the multi-GPU split (each rank lists the hits of its chromosomes, every rank
-    replays): on a dense input where the cap binds for many reads, every rank's capped graph (edges
-    as (former, partner, I, U), edges per loop, components) equals the oracle's reference loop."""
+    """The product's SweepShard with a binding cap, W ranks as threads on one GPU: the sharded replay
+    (each rank lists the hits of its chromosomes, the lists travel to the rank replaying their read's
+    component, the changes are exchanged) on a dense input where the cap binds for many reads — the
+    ranks' capped edges (as (former, partner, I, U)) are the oracle's reference loop's, their edges
+    per loop add up to the oracle's, and every rank has the oracle's components."""
     import dataclasses
     from fslr_amd.prep import fold_overlap_threshold, pass_table
     s = synth.generate(20_000, 16, 47, cluster_cap=30, size_p=0.05)
@@ -467,15 +498,21 @@ def test_sweep_split_capped_one_gpu_equals_oracle(W, thr):
     thr_iv = fold_overlap_threshold(csr.iv_aln, 0.8)
     pt = pass_table([1, 1, 0.66, 0.66, 0.66, 0.5])
     o = O.run_core(_oracle_csr(csr), edge_threshold=thr, use_cap=True)
-    ctxs, cap = _sweep_split_capped_on_device(csr, thr_iv, pt, W, thr)
-    assert cap['capped'] > 0 and cap['dropped'] > 0
-    want = sorted(zip(o['edge_a'].tolist(), o['edge_b'].tolist(), o['edge_I'].tolist(), o['edge_U'].tolist()))
-    for c in ctxs:
-        a, b, I, U = c.edges(c.stats()['n_edges'])
+    ctxs, infos = _sweep_shards_threads(csr, thr_iv, pt, W, thr, steps=2)
+    try:
+        assert all(i['capped'] for i in infos)
+        caps = [i['cap'] for i in infos]
+        assert all(cp == caps[0] for cp in caps)
+        assert caps[0]['capped'] > 0 and caps[0]['dropped'] > 0
+        want = sorted(zip(o['edge_a'].tolist(), o['edge_b'].tolist(), o['edge_I'].tolist(), o['edge_U'].tolist()))
+        a, b, I, U, fwd = _union_view(ctxs)
         assert sorted(zip(a.tolist(), b.tolist(), I.tolist(), U.tolist())) == want
-        np.testing.assert_array_equal(c.fwd_degree(), o['fwd'])
-        np.testing.assert_array_equal(_components_from_labels(c.labels()), o['comp'])
-        c.close()
+        np.testing.assert_array_equal(fwd, o['fwd'])
+        for c in ctxs:
+            np.testing.assert_array_equal(_components_from_labels(c.labels()), o['comp'])
+    finally:
+        for c in ctxs:
+            c.close()
 
 
 def _sweep_gpu_worker(rank, world, port, out_dir):

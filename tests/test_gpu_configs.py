@@ -143,7 +143,7 @@ def test_config4_1m_product_split_w8_vs_oracle(thr):
     dist.SweepShard's capped path) on the 1M-read input: every rank's graph and labels have the
     oracle's digests (thr 10: the cap does not bind, E*; thr 3: it binds)."""
     from make_cfg5_full import digests
-    from test_dist import _sweep_split_capped_on_device, _sweep_split_on_device
+    from test_dist import _sweep_shards_threads, _sweep_split_on_device, _union_view
     with open(os.path.join(GOLDEN, 'cfg5', 'cfg4_1m.json')) as fh:
         ref = json.load(fh)
     csr = synth.generate(ref['reads'], ref['lmax'], ref['seed']).interval_data().csr()
@@ -152,12 +152,10 @@ def test_config4_1m_product_split_w8_vs_oracle(thr):
     key = 'capped3' if thr == 3 else 'estar'
     want = {k: ref[key][k] for k in ('edges_sha256', 'fwd_sha256', 'labels_sha256', 'n_edges', 'max_fwd')}
     if thr == 3:
-        ctxs, cap = _sweep_split_capped_on_device(csr, thr_iv, pt, 8, thr)
-        assert cap['capped'] > 0
-        views = []
-        for c in ctxs:
-            a, b, I, U = c.edges(c.stats()['n_edges'])
-            views.append(digests(a, b, I, U, c.fwd_degree(), c.labels()))
+        ctxs, infos = _sweep_shards_threads(csr, thr_iv, pt, 8, thr)
+        assert all(i['capped'] and i['cap']['capped'] > 0 for i in infos)
+        a, b, I, U, fwd = _union_view(ctxs)
+        views = [digests(a, b, I, U, fwd, c.labels()) for c in ctxs]
     else:
         ctxs, _ = _sweep_split_on_device(csr, thr_iv, pt, 8, thr)
         parts = [c.edges(c.stats()['n_edges']) for c in ctxs]      # each destination's edges
@@ -175,12 +173,13 @@ def test_config4_1m_product_split_w8_vs_oracle(thr):
 @pytest.mark.slow
 def test_config5_10m_product_split_w8_capped_vs_oracle():
     """North star's config 5 (10M reads x 1-64 Zipf, the cap binding) through the product's
-    chromosome split on W = 8 contexts: partition, entry exchange, evaluation, then dist.SweepShard's
-    capped path (E* rows gathered, each rank's chromosomes' hit lists gathered, the replay) — every
-    rank's capped graph (edges with I, U; edges per loop) and labels have the digests of the
-    oracle's full run (tests/golden/cfg5/full_capped.json)."""
+    dist.SweepShard on W = 8 ranks (threads of this process, one context each, in-process
+    collectives): partition, entry exchange, evaluation, then the sharded cap replay (E* rows
+    gathered, the candidates' hit components assigned to ranks, each rank replaying its own) — the
+    union of the ranks' capped graphs (edges with I, U; edges per loop) and every rank's labels have
+    the digests of the oracle's full run (tests/golden/cfg5/full_capped.json)."""
     from make_cfg5_full import digests
-    from test_dist import _sweep_split_capped_on_device
+    from test_dist import _sweep_shards_threads, _union_view
     with open(os.path.join(GOLDEN, 'cfg5', 'sample50k_capped.json')) as fh:
         meta = json.load(fh)
     with open(os.path.join(GOLDEN, 'cfg5', 'full_capped.json')) as fh:
@@ -190,12 +189,13 @@ def test_config5_10m_product_split_w8_capped_vs_oracle():
     csr = s.interval_data().csr()
     del s
     assert csr.n_intervals == meta['n_intervals']
-    ctxs, cap = _sweep_split_capped_on_device(csr, fold_overlap_threshold(csr.iv_aln, 0.8), pass_table(CUTS), 8, 10)
+    ctxs, infos = _sweep_shards_threads(csr, fold_overlap_threshold(csr.iv_aln, 0.8), pass_table(CUTS), 8, 10)
     try:
+        cap = infos[0]['cap']
         assert cap['applied'] == 1 and cap['dropped'] > 0
+        a, b, I, U, fwd = _union_view(ctxs)
         for c in ctxs:
-            a, b, I, U = c.edges(c.stats()['n_edges'])
-            d = digests(a, b, I, U, c.fwd_degree(), c.labels())
+            d = digests(a, b, I, U, fwd, c.labels())
             assert {k: d[k] for k in want} == want
     finally:
         for c in ctxs:
