@@ -13,7 +13,7 @@ import numpy as np
 
 LIB_PATH = os.environ.get('FSLR_LIB') or os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libfslr_hip.so')
 
-ABI_VERSION = 11         # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
+ABI_VERSION = 12         # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
 FSLR_OK, FSLR_ERR_ZERO_DIVISION, FSLR_ERR_INVALID, FSLR_ERR_HIP, FSLR_ERR_NOMEM, FSLR_ERR_STATE = range(6)
 FSLR_MAX_L = 64
 FSLR_MAX_READS = 1 << 25
@@ -38,7 +38,8 @@ EXPORTED = ['fslr_abi_version', 'fslr_last_error', 'fslr_ctx_create', 'fslr_ctx_
             'fslr_cap_copy_local', 'fslr_cap_replay', 'fslr_get_stage_kernel_times', 'fslr_long_pairs',
             'fslr_cap_replay_pairs', 'fslr_source_hash', 'fslr_set_reads_any', 'fslr_set_long_cutoffs',
             'fslr_cap_install_pairs', 'fslr_cap_sizes', 'fslr_cap_dep_local', 'fslr_cap_shard_plan',
-            'fslr_cap_shard_pack', 'fslr_cap_replay_shard', 'fslr_cap_copy_changes', 'fslr_cap_apply_changes']
+            'fslr_cap_shard_pack', 'fslr_cap_replay_shard', 'fslr_cap_copy_changes', 'fslr_cap_apply_changes',
+            'fslr_local_forest', 'fslr_copy_forest_pairs']
 
 
 class HipUnavailable(RuntimeError):
@@ -158,6 +159,8 @@ def load(path: str = LIB_PATH):
         'fslr_cap_copy_local': (ctypes.c_int, [vp, vp, vp]),
         'fslr_cap_replay': (ctypes.c_int, [vp, vp, vp, i64, i32, ctypes.POINTER(CapStats)]),
         'fslr_cap_install_pairs': (ctypes.c_int, [vp, vp, i64, i32, i32]),
+        'fslr_local_forest': (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int64)]),
+        'fslr_copy_forest_pairs': (ctypes.c_int, [vp, vp, i64]),
         'fslr_cap_sizes': (ctypes.c_int, [vp] + [ctypes.POINTER(ctypes.c_int64)] * 3),
         'fslr_cap_dep_local': (ctypes.c_int, [vp, vp]),
         'fslr_cap_shard_plan': (ctypes.c_int, [vp, vp, i32, i32, vp]),
@@ -380,6 +383,21 @@ class Context:
         2 * n_pad int32), padded with (-1, -1) to n_pad pairs (async, context stream)."""
         assert t.numel() * t.element_size() >= 8 * n_pad
         self._check(self._L.fslr_copy_edges_device(self._h, ctypes.c_void_p(t.data_ptr()), int(n_pad)))
+
+    def local_forest(self, count: bool = True):
+        """Union-find over this context's edges, keeping the (read, root) pairs of non-root reads; their
+        count (one sync) or None (async)."""
+        if not count:
+            self._check(self._L.fslr_local_forest(self._h, None))
+            return None
+        k = ctypes.c_int64()
+        self._check(self._L.fslr_local_forest(self._h, ctypes.byref(k)))
+        return int(k.value)
+
+    def forest_pairs_into(self, t, n_pad: int):
+        """The local forest's (read, root) int32 pairs into device tensor ``t`` (int64 view), padded."""
+        self._check(self._L.fslr_copy_forest_pairs(self._h, ctypes.c_void_p(t.data_ptr()) if n_pad else None,
+                                                   int(n_pad)))
 
     def components_from_pairs(self, t, n_pairs: int):
         """Labels = components of the n_pairs (a, b) int32 pairs in the device tensor ``t``

@@ -20,7 +20,7 @@ int ensure_capacity(fslr_ctx* c, int64_t n, int64_t ni, int n_chroms) {
   int rc;
   if (n > c->cap_n) {
     if ((rc = dalloc(c, &c->rmeta, n)) || (rc = dalloc(c, &c->rlen8, n)) || (rc = dalloc(c, &c->fwd, n)) ||
-        (rc = dalloc(c, &c->parent, n)) ||
+        (rc = dalloc(c, &c->parent, n)) || (rc = dalloc(c, &c->forest, n)) ||
         (rc = dalloc(c, &c->heavy, n)) ||
         (rc = dalloc(c, &c->lbounds, n)))
       return rc;
@@ -56,6 +56,7 @@ int ensure_capacity(fslr_ctx* c, int64_t n, int64_t ni, int n_chroms) {
     if ((rc = dalloc(c, &c->umax, FSLR_MAX_L))) return rc;
     if ((rc = dalloc(c, &c->counters, kNumCounters))) return rc;
     if ((rc = dalloc(c, &c->errw, kErrWords))) return rc;
+    if ((rc = dalloc(c, &c->forest_cnt, 1))) return rc;
     // no query yet: no edges, no errors (fslr_components before any query gives singleton labels)
     HIP_TRY(c, hipMemsetAsync(c->counters, 0, kNumCounters * sizeof(unsigned long long), c->stream));
     HIP_TRY(c, hipMemsetAsync(c->errw, 0, kErrWords * sizeof(int), c->stream));
@@ -151,7 +152,7 @@ void fslr_ctx_destroy(fslr_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void* bufs[] = {c->rmeta,  c->rlen8, c->iv,     c->qpos,    c->rng_s,  c->idx4,    c->idx_gate, c->data_pos, c->s_start,
                   c->crange, c->keys,   c->keys2,   c->vals,    c->vals2,   c->endkey,  c->pmaxkey,
-                  c->temp,   c->umax,   c->edges,   c->edge_iu, c->fwd,     c->parent,  c->counters,
+                  c->temp,   c->umax,   c->edges,   c->edge_iu, c->fwd,     c->parent,  c->counters, c->forest, c->forest_cnt,
                   c->errw,   c->thr_tmp, c->defer,   c->dchrom,  c->drec,    c->lbounds, c->diag, c->wstat,
                   c->dgate,  c->chist,  c->heavy, c->ent, c->ent_sorted, c->sweep_temp, c->sw_tile, c->sw_wstat, c->ent_ub,
                   c->fdchrom, c->fdrec, c->fdgate, c->crange_f, c->part_cnt, c->grp, c->fmap};
@@ -1255,6 +1256,35 @@ int fslr_copy_edges_device(fslr_ctx* c, int32_t* dst, int64_t n_pad) {
   if (!c->edge_cap) return fail(c, FSLR_ERR_STATE, "no query has run");
   HIP_TRY(c, launch_copy_edges(c->edges, &c->counters[kEdgeCount], c->edge_cap, reinterpret_cast<int2*>(dst), n_pad,
                                c->stream));
+  return FSLR_OK;
+}
+
+int fslr_local_forest(fslr_ctx* c, int64_t* n_pairs) {
+  if (!c) return FSLR_ERR_INVALID;
+  if (!c->reads_set) return fail(c, FSLR_ERR_STATE, "fslr_set_reads first");
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const int nr = static_cast<int>(c->n);
+  HIP_TRY(c, launch_uf_init(c->parent, nr, s));
+  if (c->edge_cap) HIP_TRY(c, launch_uf_edges(c->parent, c->edges, c->counters, c->edge_cap, c->errw, s));
+  HIP_TRY(c, launch_uf_finalize(c->parent, nr, s));
+  HIP_TRY(c, hipMemsetAsync(c->forest_cnt, 0, sizeof(unsigned long long), s));
+  HIP_TRY(c, launch_forest_pairs(c->parent, nr, c->forest, c->forest_cnt, s));
+  if (n_pairs) {
+    unsigned long long k = 0;
+    HIP_TRY(c, hipMemcpyAsync(&k, c->forest_cnt, sizeof(k), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    *n_pairs = static_cast<int64_t>(k);
+  }
+  return FSLR_OK;
+}
+
+int fslr_copy_forest_pairs(fslr_ctx* c, int32_t* dst, int64_t n_pad) {
+  if (!c || (!dst && n_pad) || n_pad < 0) return FSLR_ERR_INVALID;
+  if (!c->forest || !c->forest_cnt) return fail(c, FSLR_ERR_STATE, "fslr_set_reads first");
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (n_pad == 0) return FSLR_OK;
+  HIP_TRY(c, launch_copy_edges(c->forest, c->forest_cnt, c->n, reinterpret_cast<int2*>(dst), n_pad, c->stream));
   return FSLR_OK;
 }
 

@@ -101,6 +101,24 @@ __global__ void k_copy_edges(const int2* __restrict__ edges, const unsigned long
     out[k] = k < ne ? edges[k] : make_int2(-1, -1);
 }
 
+// a finalized forest's (read, root) pairs of the reads that are not their own root (the multi-GPU
+// merge exchanges these instead of the raw edges: unions of the same partition)
+__global__ void k_forest_pairs(const int* __restrict__ p, int n, int2* __restrict__ out,
+                               unsigned long long* __restrict__ cnt) {
+  const int lane = threadIdx.x & 63;
+  for (int x0 = (blockIdx.x * blockDim.x + threadIdx.x) & ~63; x0 < n; x0 += gridDim.x * blockDim.x) {
+    const int x = x0 + lane;
+    const int r = x < n ? p[x] : x;
+    const bool t = r != x;
+    const unsigned long long m = __ballot(t);
+    if (!m) continue;
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(cnt, static_cast<unsigned long long>(__popcll(m)));
+    base = __shfl(base, 0);
+    if (t) out[base + __popcll(m & ((1ull << lane) - 1ull))] = make_int2(x, r);
+  }
+}
+
 // find without path halving: the finalize pass's only store is each node's own root.  (With
 // halving here, another thread's late halving store into p[x] — an ancestor that is not the root —
 // could land after x's own root store and leave x labelled with a non-root.)
@@ -163,6 +181,11 @@ hipError_t launch_uf_strided(int* parent, const int* vals, long long blocks, int
 hipError_t launch_copy_edges(const int2* edges, const unsigned long long* count, long long cap, int2* out,
                              long long n_pad, hipStream_t s) {
   if (n_pad > 0) k_copy_edges<<<grid_for(n_pad), 256, 0, s>>>(edges, count, cap, out, n_pad);
+  return hipGetLastError();
+}
+
+hipError_t launch_forest_pairs(const int* parent, int n, int2* out, unsigned long long* cnt, hipStream_t s) {
+  if (n > 0) k_forest_pairs<<<grid_for(n), 256, 0, s>>>(parent, n, out, cnt);
   return hipGetLastError();
 }
 

@@ -81,6 +81,8 @@ struct fslr_ctx {
   int* fwd = nullptr;
   int* heavy = nullptr;      // [N] reads handed to the partitioned pair-kernel launch
   int* parent = nullptr;
+  int2* forest = nullptr;                    // [n] the local forest's (read, root) pairs (fslr_local_forest)
+  unsigned long long* forest_cnt = nullptr;  // [1] their count (device)
   unsigned long long* counters = nullptr;
   unsigned long long* wstat = nullptr;       // [wstat_waves x kWStride] per-wave statistics of the pair kernel
   int wstat_waves = 0;

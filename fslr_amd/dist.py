@@ -372,14 +372,20 @@ class SweepShard:
             err = e
         mf = int(st['max_fwd'])
         max_ne = int(st['n_edges'])
+        max_fp = 0
+        if W > 1 and err is None:
+            try:
+                max_fp = ctx.local_forest()         # this rank's forest: the merge exchanges its pairs
+            except Exception as e:                  # noqa: BLE001 - re-raised on every rank below
+                err = e
         if W > 1:
-            # the error flag and the edge count ride with the forward-degree maximum, so a pair that
-            # raises on one evaluator raises on every rank instead of leaving the others in a
-            # collective, and every rank knows the padded size of the edge exchange
+            # the error flag, the edge count and the forest's pair count ride with the forward-degree
+            # maximum, so a pair that raises on one evaluator raises on every rank instead of leaving
+            # the others in a collective, and every rank knows the padded sizes of the exchanges
             code = 0 if err is None else (1 if isinstance(err, ZeroDivisionError) else 2)
-            t = self.comm.small([mf, code, max_ne])
+            t = self.comm.small([mf, code, max_ne, max_fp])
             self.comm.all_reduce(t, 'max')
-            mf, code, max_ne = (int(x) for x in t.tolist())
+            mf, code, max_ne, max_fp = (int(x) for x in t.tolist())
             if err is None and code:
                 from ._lib import FslrError
                 err = ZeroDivisionError('division by zero') if code == 1 else FslrError('error on another rank')
@@ -395,20 +401,22 @@ class SweepShard:
             ctx.components()
             return out
         self._rep = {'key': self._key(qlen_cut, nal_cut, pass_table, edge_threshold), 'counts': counts.copy(),
-                     'recv_counts': recv_counts.copy(), 'max_ne': max_ne, 'n_edges_local': int(st['n_edges']),
+                     'recv_counts': recv_counts.copy(), 'max_fp': max_fp, 'n_edges_local': int(st['n_edges']),
                      'out': dict(out, sweep_stats=None)}
-        self._merge(max_ne)
+        self._merge(max_fp)
         return out
 
-    def _merge(self, max_ne):
-        """Components of the union of the ranks' edges: all_gather of the edge lists, padded to the
-        largest count (8 B per edge: 1.8M edges at 1M reads, against 4 B per read per rank for a
-        label exchange), then one union-find over all of them on every rank."""
+    def _merge(self, max_fp):
+        """Components of the union of the ranks' edges from their local forests: each rank's (read,
+        root) pairs of the reads that are not their own root (fslr_local_forest; a partition is the
+        union of the partitions of its parts, and a forest has fewer pairs than the edges it unions:
+        about 0.37 of them at 1M reads) are all-gathered, padded to the largest count, and every rank
+        unions them (8 B per pair)."""
         ctx, W = self.ctx, self.world
-        m = max(1, max_ne)
+        m = max(1, max_fp)
         self.esend = self._grow(self.esend, m)
         self.egath = self._grow(self.egath, W * m)
-        ctx.edges_into(self.esend, m)
+        ctx.forest_pairs_into(self.esend, m)
         self._all_gather(self.egath[:W * m], self.esend[:m])
         ctx.components_from_pairs(self.egath, W * m)
 
@@ -423,7 +431,8 @@ class SweepShard:
         ctx.sweep_partition_repeat(qlen_cut, nal_cut, pass_table, W, self.block_shift, self.send, edge_threshold)
         self._all_to_all(self.recv[:n_recv], self.send[:sent_total], recv_counts.tolist(), counts.tolist())
         ctx.sweep_evaluate(qlen_cut, nal_cut, pass_table, self.recv, n_recv, edge_threshold)
-        self._merge(rep['max_ne'])
+        ctx.local_forest(count=False)
+        self._merge(rep['max_fp'])
         self._rep_steps = getattr(self, '_rep_steps', 0) + 1
         return dict(rep['out'], repeat=True)
 

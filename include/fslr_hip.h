@@ -24,8 +24,9 @@
  *                         multi-GPU path)
  *   fslr_union_pairs      (multi-GPU merge of per-shard component labels; no
  *                         reference counterpart — the reference is single-process)
- *   fslr_copy_edges_device, fslr_components_from_pairs
- *                         (multi-GPU merge of the ranks' gathered edge lists: get_subgraphs,
+ *   fslr_copy_edges_device, fslr_components_from_pairs, fslr_local_forest,
+ *   fslr_copy_forest_pairs
+ *                         (multi-GPU merge of the ranks' gathered local forests: get_subgraphs,
  *                         cluster.py:230-234, over the union of the ranks' edges)
  *   fslr_copy_edges_iu_device,
  *   fslr_cap_install_edges,
@@ -73,7 +74,7 @@
 extern "C" {
 #endif
 
-#define FSLR_ABI_VERSION 11
+#define FSLR_ABI_VERSION 12
 #define FSLR_MAX_L 64                /* max intervals per read (bitmask width) */
 #define FSLR_MAX_READS (1 << 25)     /* read rank packs into bits 6..30 of the index record */
 #define FSLR_THR_ZERO_ALN INT32_MIN
@@ -295,6 +296,14 @@ int  fslr_cap_replay(fslr_ctx *ctx, const int32_t *counts, const int32_t *hits, 
  *   (former, partner)) and their formers' counts (fwd), the components of the whole capped graph
  *   (fslr_get_labels), errw max_fwd = the largest edges-per-loop.  Syncs; out: applied, max_fwd,
  *   candidates, dropped, backward (capped / hits / pairs: the sum of the ranks' parts). */
+/* The multi-GPU merge by local forests (get_subgraphs, cluster.py:230-234, over the union of the ranks'
+ * edges).  fslr_local_forest: union-find over this context's edges; the (read, root) pairs of the
+ * reads that are not their own root are kept (the same partition as the edges, in fewer pairs);
+ * *n_pairs (may be NULL: no sync) gets their count.  fslr_copy_forest_pairs: those pairs as int32
+ * (read, root) into a device buffer of n_pad pairs, padded with -1 (async).  The ranks all-gather
+ * them and fslr_components_from_pairs takes the union. */
+int  fslr_local_forest(fslr_ctx *ctx, int64_t *n_pairs);
+int  fslr_copy_forest_pairs(fslr_ctx *ctx, int32_t *dst, int64_t n_pad);
 int  fslr_cap_install_pairs(fslr_ctx *ctx, const int32_t *pairs, int64_t n_rows, int32_t world, int32_t rank);
 int  fslr_cap_sizes(fslr_ctx *ctx, int64_t *n_t, int64_t *n_ti, int64_t *n_hits);
 int  fslr_cap_dep_local(fslr_ctx *ctx, int32_t *out);

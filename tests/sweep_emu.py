@@ -175,6 +175,18 @@ class EmuSweepContext:
         pairs[:len(e)] = e[:, :2]
         t.numpy()[:n_pad] = pairs.view(np.int64)[:, 0]
 
+    def local_forest(self, count=True):
+        self.components()
+        lab = self.labels().astype(np.int64)
+        x = np.flatnonzero(lab != np.arange(self.n_reads))
+        self._forest = np.stack([x, lab[x]], axis=1)
+        return int(x.size) if count else None
+
+    def forest_pairs_into(self, t, n_pad):
+        pairs = np.full((n_pad, 2), -1, dtype=np.int32)
+        pairs[:len(self._forest)] = self._forest
+        t.numpy()[:n_pad] = pairs.view(np.int64)[:, 0]
+
     def components_from_pairs(self, t, n):
         pairs = t.numpy()[:n].view(np.int32).reshape(-1, 2)
         self._parent = np.arange(self.n_reads)

@@ -4,13 +4,13 @@
 For each world size W the ranks' work is run one rank at a time on cuda:0 with the data a rank
 would hold (every read; the index of its own chromosomes):
   part[r]  = build_index (filtered) + fslr_sweep_partition (sweep, pack, route; ends in a sync)
-  eval[d]  = fslr_sweep_evaluate (sort + pair kernel) over the entries destined to d, + the copy of
-             its edges into the padded exchange buffer
-  merge    = union-find over the W gathered edge lists (the replicated step)
+  eval[d]  = fslr_sweep_evaluate (sort + pair kernel) over the entries destined to d, + its local
+             forest (fslr_local_forest) and the copy of its (read, root) pairs for the exchange
+  merge    = union-find over the W gathered forests' pairs (the replicated step)
 and the single-context step (build_index + sweep query + components) as the W = 1 baseline.
 The exchange itself cannot run on one GPU; it is priced from the bytes each rank moves
-(entries all_to_all: the off-rank share of its entries; edges all_gather: 8 B x the largest
-rank's edge count x (W - 1)) at an
+(entries all_to_all: the off-rank share of its entries; forest all_gather: 8 B x the largest
+rank's pair count x (W - 1)) at an
 assumed per-GPU xGMI rate (--xgmi-gbs, default 300 GB/s of the 7 x ~153 GB/s links, both
 directions shared) plus a fixed per-collective latency (--coll-us).
 
@@ -126,7 +126,7 @@ def main():
             for d in range(W):
                 segs[d].append(buf[pos[d]:pos[d + 1]].clone())
             sent.append(cnt)
-        evl, nedges, elists = [], [], []
+        evl, nedges, elists, npairs = [], [], [], []
         for d in range(W):
             ent = torch.cat(segs[d])
             ebuf = torch.empty(max(1, int(1.5 * st1['n_edges'] / W) + 4096), dtype=torch.int64, device=dev)
@@ -136,18 +136,21 @@ def main():
                 if W == 1:
                     ce.components()
                 else:
-                    ce.edges_into(ebuf, ebuf.numel())
+                    ce.local_forest(count=False)               # the merge's (read, root) pairs
+                    ce.forest_pairs_into(ebuf, ebuf.numel())
             evl.append(timed(e, args.reps))
             ne = ce.stats()['n_edges']
             nedges.append(ne)
-            elists.append(ebuf[:ne].clone())
+            fp = ce.local_forest() if W > 1 else 0
+            npairs.append(fp)
+            elists.append(ebuf[:fp].clone())
             segs[d] = None
             del ent
         assert sum(nedges) == st1['n_edges'], (nedges, st1['n_edges'])
-        m = max(nedges)
+        m = max(1, max(npairs))
         gathered = torch.full((W * m,), -1, dtype=torch.int64, device=dev)
         for d in range(W):
-            gathered[d * m:d * m + nedges[d]] = elists[d]
+            gathered[d * m:d * m + npairs[d]] = elists[d]
         merge = timed(lambda: ce.components_from_pairs(gathered, W * m), args.reps) if W > 1 else 0.0
         if W > 1:
             ref = c1_labels
@@ -167,7 +170,8 @@ def main():
         row = {'W': W, 'part_ms': part, 'part_repeat_ms': part_rep, 'eval_ms': evl, 'merge_ms': merge,
                'a2a_ms_model': a2a_ms, 'projected_step_repeat_ms': step_rep, 'projected_speedup_repeat': t1 / step_rep,
                'gather_ms_model': gather_ms, 'entries_sent_per_rank': sent.sum(axis=1).tolist(),
-               'entries_recv_per_rank': recv.tolist(), 'edges_per_rank': nedges, 'projected_step_ms': step,
+               'entries_recv_per_rank': recv.tolist(), 'edges_per_rank': nedges, 'forest_pairs_per_rank': npairs,
+               'projected_step_ms': step,
                'projected_speedup': t1 / step}
         log(f'W={W}: part max {max(part):.3f} ms, eval max {max(evl):.3f} ms, merge {merge:.3f} ms, '
             f'a2a {a2a_ms:.3f} ms, gather {gather_ms:.3f} ms -> {step:.3f} ms ({t1 / step:.2f}x); repeat steps '
