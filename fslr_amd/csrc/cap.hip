@@ -1379,12 +1379,21 @@ bool cap_rounds_closure() {
   return v;
 }
 
-// FSLR_CAP_REPLAY=components: the round-3 replay (one wavefront per dependency component), for A/B
-bool cap_dag_disabled() {
+// The loops' replay: one wavefront per dependency component (default), or FSLR_CAP_REPLAY=dag, a ready
+// queue over the loops' DAG (k_cap_replay_dag).  Measured at cfg5 (profiles/r04/cap/): the DAG
+// replay's cross-wave hand-offs (agent-scope release / acquire through memory, a few microseconds
+// each along the longest dependency chain) made it 7.2 ms against 2.5 ms per component.
+bool cap_dag_enabled() {
   static const bool v = [] {
     const char* e = std::getenv("FSLR_CAP_REPLAY");
-    return e && std::strcmp(e, "components") == 0;
+    return e && std::strcmp(e, "dag") == 0;
   }();
+  return v;
+}
+
+// FSLR_DEBUG_CAP=1: the dependency components' sizes on stderr (diagnostics)
+bool cap_debug() {
+  static const bool v = std::getenv("FSLR_DEBUG_CAP") != nullptr;
   return v;
 }
 
@@ -1617,7 +1626,7 @@ int cap_loops(fslr_ctx* c, CapWork* w) {
     k_cap_recs<<<grid_for(m), 256, 0, s>>>(w->slot_of, w->ukey, w->fpos, w->flags, w->mslot, w->T, w->t_of, m, w->rec);
     HIP_TRY(c, hipMemsetAsync(w->vis2, 0, static_cast<size_t>(ns), s));
     bool dag_ok = false;
-    if (!cap_dag_disabled()) {
+    if (cap_dag_enabled()) {
       HIP_TRY(c, hipMemsetAsync(w->sbeg, 0, static_cast<size_t>(nt) * sizeof(int), s));
       HIP_TRY(c, hipMemsetAsync(w->send, 0, static_cast<size_t>(nt) * sizeof(int), s));
       HIP_TRY(c, hipMemsetAsync(w->indeg, 0, static_cast<size_t>(nt) * sizeof(int), s));
@@ -1650,6 +1659,26 @@ int cap_loops(fslr_ctx* c, CapWork* w) {
       k_cap_ckeys<<<grid_for(nt), 256, 0, s>>>(w->tpar, nt, w->ck);
       size_t tb = w->temp_bytes;
       HIP_TRY(c, hipcub::DeviceRadixSort::SortKeys(w->temp, tb, w->ck, w->ck2, nt, 0, 50, s));
+      if (cap_debug()) {
+        std::vector<int> par(nt), toff(nt + 1), ioff(static_cast<size_t>(w->nti) + 1);
+        HIP_TRY(c, hipMemcpyAsync(par.data(), w->tpar, nt * sizeof(int), hipMemcpyDeviceToHost, s));
+        HIP_TRY(c, hipMemcpyAsync(toff.data(), w->toff, (nt + 1) * sizeof(int), hipMemcpyDeviceToHost, s));
+        HIP_TRY(c, hipMemcpyAsync(ioff.data(), w->ioff, ioff.size() * sizeof(int), hipMemcpyDeviceToHost, s));
+        HIP_TRY(c, hipStreamSynchronize(s));
+        std::vector<long long> sz(nt, 0), hits(nt, 0);
+        for (int t = 0; t < nt; ++t) {
+          ++sz[par[t]];
+          hits[par[t]] += ioff[toff[t + 1]] - ioff[toff[t]];
+        }
+        long long ncomp = 0, big = 0, bighits = 0, maxhits = 0;
+        for (int t = 0; t < nt; ++t) {
+          ncomp += sz[t] > 0;
+          if (sz[t] > big) { big = sz[t]; bighits = hits[t]; }
+          maxhits = std::max(maxhits, hits[t]);
+        }
+        std::fprintf(stderr, "fslr: cap replay %d loops in %lld components; largest %lld loops (%lld hits); most hits %lld; %lld hits\n",
+                     nt, ncomp, big, bighits, maxhits, static_cast<long long>(w->nseq));
+      }
       k_cap_replay<<<wave_grid(nt), 256, 0, s>>>(w->ck2, nt, thr, w->toff, w->ioff, w->rec, w->fpos, w->vis2,
                                                  w->pbrk, w->own, w->err);
       HIP_TRY(c, hipGetLastError());

@@ -1133,15 +1133,32 @@ __global__ __launch_bounds__(256) void k_msd_pass2(const unsigned long long* __r
 // spilled: grouped by digit into `out` (runs contiguous, as k_msd_pass2 would) and listed; the list
 // is then evaluated by k_sweep_pairs in list mode (its long-run path handles reads with thousands
 // of entries in partner partitions).
-constexpr int kFuseBinsLog = 12;
+#ifndef FSLR_FUSE_BINS_LOG
+#define FSLR_FUSE_BINS_LOG 12
+#endif
+#ifndef FSLR_FUSE_READS_LOG
+#define FSLR_FUSE_READS_LOG 11
+#endif
+#ifndef FSLR_FUSE_ES
+#define FSLR_FUSE_ES 2048
+#endif
+constexpr int kFuseBinsLog = FSLR_FUSE_BINS_LOG;
 constexpr int kFuseBins = 1 << kFuseBinsLog;   // digits of a bucket (A's low bits, then B's hash)
-constexpr int kFuseMaxReadsLog = 11;
+constexpr int kFuseMaxReadsLog = FSLR_FUSE_READS_LOG;
 constexpr int kFuseMaxReads = 1 << kFuseMaxReadsLog;   // reads per bucket at most (2^lo)
-constexpr int kFuseEs = 2048;                  // staged edges per workgroup (one atomic per flush)
+constexpr int kFuseEs = FSLR_FUSE_ES;          // staged edges per workgroup (one atomic per flush)
+static_assert(kFuseMaxReadsLog < kFuseBinsLog, "at least one bit of B's hash per digit");
 constexpr int kFuseLong = 512;                 // a longer run sends its bucket to the spill path
 
+#ifndef FSLR_FUSE_WAVES
+#define FSLR_FUSE_WAVES 0
+#endif
 template <int CAP, int NT>
-__global__ __launch_bounds__(NT) void k_bucket_pairs(SweepArgs g, const unsigned long long* __restrict__ mid,
+__global__ __launch_bounds__(NT)
+#if FSLR_FUSE_WAVES
+__attribute__((amdgpu_waves_per_eu(FSLR_FUSE_WAVES)))
+#endif
+void k_bucket_pairs(SweepArgs g, const unsigned long long* __restrict__ mid,
                                                      const int* __restrict__ off, int P, int H, int lo, int hbB,
                                                      unsigned long long* __restrict__ out,
                                                      long long* __restrict__ spill,
@@ -1508,11 +1525,12 @@ hipError_t launch_sweep_plan(const SweepArgs& a, hipStream_t s) {
   return hipcub::DeviceScan::ExclusiveSum(a.temp, tb, a.tile_tests, a.tile_ub, nt, s);
 }
 
-// FSLR_SWEEP_MAP=stride: k_sweep's chunks dealt grid-stride (the round-3 mapping), for A/B
+// k_sweep's chunks dealt grid-stride (default), or FSLR_SWEEP_MAP=xcd: each XCD a contiguous share.
+// Measured at cfg3 (profiles/r04/ab/): the XCD mapping 0.2485 ms against 0.2447 ms grid-stride.
 static int sweep_xcd_map() {
   static const int v = [] {
     const char* e = std::getenv("FSLR_SWEEP_MAP");
-    return e && std::strcmp(e, "stride") == 0 ? 0 : 1;
+    return e && std::strcmp(e, "xcd") == 0 ? 1 : 0;
   }();
   return v;
 }
@@ -1715,12 +1733,14 @@ static hipError_t fused_pairs(const SweepArgs& a, int mode, const unsigned long 
   return hipGetLastError();
 }
 
-// FSLR_PAIR_STAGE=legacy: the round-3 pair stage (k_msd_pass2 grouping + k_sweep_pairs over every
-// entry), kept for A/B measurements
+// The pair stage: the two-level grouping (k_msd_pass1 + k_msd_pass2) and k_sweep_pairs (default), or
+// FSLR_PAIR_STAGE=fused: pass 2 fused with the evaluation (k_bucket_pairs).  Measured at cfg3
+// (profiles/r04/ab/): fused 0.374 ms of grouping pass 2 + pairs against 0.271 + 0.09 ms, step 1.176
+// against 1.146 ms.
 static bool legacy_pair_stage() {
   static const bool v = [] {
     const char* e = std::getenv("FSLR_PAIR_STAGE");
-    return e && std::strcmp(e, "legacy") == 0;
+    return !(e && std::strcmp(e, "fused") == 0);
   }();
   return v;
 }
