@@ -25,5 +25,5 @@ python3 -c "import json; d=json.load(open('$O/cfg5_cap_frontier.json')); print('
 FSLR_CAP_CLOSURE=rounds timeout -k 10 300 python3 tools/cfg5_cap.py --reps 3 > $O/cfg5_cap_rounds.json 2> $O/cfg5_cap_rounds.log || { tail -20 $O/cfg5_cap_rounds.log; exit 1; }
 python3 -c "import json; d=json.load(open('$O/cfg5_cap_rounds.json')); print('cfg5 rounds+components rep_ms', d['rep_ms'], d.get('full_equal'))"
 timeout -k 10 400 python3 tools/shard_cap_timing.py --worlds 8 --reps 3 > $O/shard_cap_w8.jsonl 2> $O/shard_cap_w8.log || { tail -20 $O/shard_cap_w8.log; exit 1; }
-tail -2 $O/shard_cap_w8.log
+tail -3 $O/shard_cap_w8.log
 echo done

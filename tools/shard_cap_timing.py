@@ -115,6 +115,7 @@ def main():
             ctx.append(c)
         ph = {k: [[] for _ in range(W)] for k in ('part', 'eval', 'cap_local', 'cap_plan', 'cap_replay', 'cap_apply')}
         model = []
+        sub = {}
         for rep in range(args.reps + 1):
             segs, sent = [[] for _ in range(W)], []
             for r in range(W):
@@ -149,15 +150,15 @@ def main():
             nts = []
             tinfo = []
             for r in range(W):
-                def cl_():
-                    ctx[r].cap_install_pairs(rows, W * m, W, r)
-                    ctx[r].cap_local(et)
-                    nt = ctx[r].cap_sizes()[0]
-                    ti = torch.empty(max(1, 2 * nt), dtype=torch.int32, device=dev)
-                    ctx[r].cap_dep_local(ti)
-                    return nt, ti
-                ms, (nt, ti) = timed_once(cl_)
-                ph['cap_local'][r].append(ms)
+                m1, _ = timed_once(lambda: ctx[r].cap_install_pairs(rows, W * m, W, r))
+                m2, _ = timed_once(lambda: ctx[r].cap_local(et))
+                nt = ctx[r].cap_sizes()[0]
+                ti = torch.empty(max(1, 2 * nt), dtype=torch.int32, device=dev)
+                m3, _ = timed_once(lambda: ctx[r].cap_dep_local(ti))
+                ph['cap_local'][r].append(m1 + m2 + m3)
+                sub.setdefault('install', [[] for _ in range(W)])[r].append(m1)
+                sub.setdefault('closure_hits', [[] for _ in range(W)])[r].append(m2)
+                sub.setdefault('dep_local', [[] for _ in range(W)])[r].append(m3)
                 nts.append(nt)
                 tinfo.append(ti[:2 * nt])
             nt = nts[0]
@@ -225,7 +226,10 @@ def main():
         cap_ms = (max(med['cap_local']) + mdl['tinfo_gather_ms'] + max(med['cap_plan']) + mdl['counts_a2a_ms']
                   + mdl['hits_a2a_ms'] + max(med['cap_replay']) + mdl['changes_gather_ms'] + max(med['cap_apply']))
         step = (max(med['part']) + mdl['a2a_ms'] + max(med['eval']) + cl + mdl['gather_ms'] + cap_ms)
-        row = {'W': W, 'phase_ms_per_rank': med, 'model': mdl, 'cap_ms_per_rank_projected': cap_ms,
+        smed = {k: [float(np.median(v[r][1:])) for r in range(W)] for k, v in sub.items()}
+        log('cap_local parts (max over ranks):', {k: round(max(v), 3) for k, v in smed.items()})
+        row = {'W': W, 'phase_ms_per_rank': med, 'cap_local_parts_ms': smed, 'model': mdl,
+               'cap_ms_per_rank_projected': cap_ms,
                'projected_step_ms': step, 'projected_speedup': one[2] / step,
                'single_cap_ms': one[1], 'cap_speedup': one[1] / cap_ms}
         log(f'W={W}: part {max(med["part"]):.3f}, eval {max(med["eval"]):.3f}, cap local {max(med["cap_local"]):.3f} '
