@@ -13,7 +13,7 @@ import numpy as np
 
 LIB_PATH = os.environ.get('FSLR_LIB') or os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libfslr_hip.so')
 
-ABI_VERSION = 12         # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
+ABI_VERSION = 13         # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
 FSLR_OK, FSLR_ERR_ZERO_DIVISION, FSLR_ERR_INVALID, FSLR_ERR_HIP, FSLR_ERR_NOMEM, FSLR_ERR_STATE = range(6)
 FSLR_MAX_L = 64
 FSLR_MAX_READS = 1 << 25
@@ -39,7 +39,7 @@ EXPORTED = ['fslr_abi_version', 'fslr_last_error', 'fslr_ctx_create', 'fslr_ctx_
             'fslr_cap_replay_pairs', 'fslr_source_hash', 'fslr_set_reads_any', 'fslr_set_long_cutoffs',
             'fslr_cap_install_pairs', 'fslr_cap_sizes', 'fslr_cap_dep_local', 'fslr_cap_shard_plan',
             'fslr_cap_shard_pack', 'fslr_cap_replay_shard', 'fslr_cap_copy_changes', 'fslr_cap_apply_changes',
-            'fslr_local_forest', 'fslr_copy_forest_pairs']
+            'fslr_local_forest', 'fslr_copy_forest_pairs', 'fslr_sort_edges']
 
 
 class HipUnavailable(RuntimeError):
@@ -160,6 +160,7 @@ def load(path: str = LIB_PATH):
         'fslr_cap_replay': (ctypes.c_int, [vp, vp, vp, i64, i32, ctypes.POINTER(CapStats)]),
         'fslr_cap_install_pairs': (ctypes.c_int, [vp, vp, i64, i32, i32]),
         'fslr_local_forest': (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int64)]),
+        'fslr_sort_edges': (ctypes.c_int, [vp]),
         'fslr_copy_forest_pairs': (ctypes.c_int, [vp, vp, i64]),
         'fslr_cap_sizes': (ctypes.c_int, [vp] + [ctypes.POINTER(ctypes.c_int64)] * 3),
         'fslr_cap_dep_local': (ctypes.c_int, [vp, vp]),
@@ -383,6 +384,10 @@ class Context:
         2 * n_pad int32), padded with (-1, -1) to n_pad pairs (async, context stream)."""
         assert t.numel() * t.element_size() >= 8 * n_pad
         self._check(self._L.fslr_copy_edges_device(self._h, ctypes.c_void_p(t.data_ptr()), int(n_pad)))
+
+    def sort_edges(self):
+        """This context's edges (with I, U) in (a, b) order, in place."""
+        self._check(self._L.fslr_sort_edges(self._h))
 
     def local_forest(self, count: bool = True):
         """Union-find over this context's edges, keeping the (read, root) pairs of non-root reads; their

@@ -965,6 +965,79 @@ __global__ void k_cap_gfwd(const int2* __restrict__ rows, long long n, int* __re
   }
 }
 
+// Every rank sorts its edges by (a, b) before the gather (fslr_sort_edges), so each read's forward edges
+// are one run of the gathered rows (in its owner's block): the closure walks those runs instead of an
+// adjacency built with per-edge atomics.  [gstart[a], gend[a]) = the run of a; flag: a block not sorted.
+__global__ void k_cap_runs(const int2* __restrict__ rows, long long n, long long m, int* __restrict__ gstart,
+                           int* __restrict__ gend, int* __restrict__ flag, unsigned long long* __restrict__ valid) {
+  unsigned long long cnt = 0;
+  for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < n;
+       k += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const int a = rows[k].x;
+    if (a < 0) continue;
+    ++cnt;
+    const long long kb = k % m;
+    const int prev = kb ? rows[k - 1].x : -1;
+    if (prev > a || (kb && prev < 0)) atomicOr(flag, 1);          // unsorted, or a row after the padding
+    if (prev != a) gstart[a] = static_cast<int>(k);
+    const int next = kb + 1 < m && k + 1 < n ? rows[k + 1].x : -1;
+    if (next != a) gend[a] = static_cast<int>(k + 1);
+  }
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+  if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(valid, cnt);
+}
+
+// forward degrees from the runs and their total (equal to the valid rows when every read has one run)
+__global__ void k_cap_runfwd(const int* __restrict__ gstart, const int* __restrict__ gend, int n, int* __restrict__ fwd,
+                             unsigned long long* __restrict__ tot) {
+  unsigned long long s = 0;
+  for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < n; x += gridDim.x * blockDim.x) {
+    const int f = gend[x] - gstart[x];
+    fwd[x] = f;
+    s += static_cast<unsigned long long>(f);
+  }
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if ((threadIdx.x & 63) == 0 && s) atomicAdd(tot, s);
+}
+
+// one closure round over the runs: every forward edge (x, y) of a read x that joined last round
+__global__ void k_cap_frontier_rows(const int* __restrict__ gstart, const int* __restrict__ gend,
+                                    const int2* __restrict__ rows, const int* __restrict__ fwd, int thr,
+                                    int* __restrict__ state, int* __restrict__ back, const int* __restrict__ fin,
+                                    const unsigned* __restrict__ fin_n, int* __restrict__ fout,
+                                    unsigned* __restrict__ fout_n) {
+  const int nin = static_cast<int>(*fin_n);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nin; i += gridDim.x * blockDim.x) {
+    const int x = fin[i];
+    for (int k = gstart[x]; k < gend[x]; ++k) {
+      const int y = rows[k].y;
+      const int b = atomicAdd(back + y, 1) + 1;
+      if (fwd[y] + b >= thr && atomicCAS(state + y, 0, 1) == 0) fout[atomicAdd(fout_n, 1u)] = y;
+    }
+  }
+}
+
+// this context's edges by (a, b): keys and their positions, then the permutation
+__global__ void k_edge_keys(const int2* __restrict__ e, long long n, unsigned long long* __restrict__ key,
+                            int* __restrict__ val) {
+  for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < n;
+       k += static_cast<long long>(gridDim.x) * blockDim.x) {
+    key[k] = (static_cast<unsigned long long>(static_cast<unsigned>(e[k].x)) << 32) | static_cast<unsigned>(e[k].y);
+    val[k] = static_cast<int>(k);
+  }
+}
+
+__global__ void k_edge_permute(const int2* __restrict__ e, const unsigned short* __restrict__ iu,
+                               const int* __restrict__ idx, long long n, int2* __restrict__ oe,
+                               unsigned short* __restrict__ oiu) {
+  for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < n;
+       k += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const int i = idx[k];
+    oe[k] = e[i];
+    oiu[k] = iu[i];
+  }
+}
+
 // the T-T pairs of this rank's visit lists, one per list element ((-1, -1): a partner outside T), and
 // each T read's local hit count.  One wavefront per T-interval.
 __global__ __launch_bounds__(256) void k_cap_tdeps(const int* __restrict__ seq, const int* __restrict__ ioff,
@@ -1160,13 +1233,6 @@ __global__ void k_cap_local_compact(const int2* __restrict__ edges, const unsign
   }
 }
 
-// dropped rows become padding (the capped graph's components)
-__global__ void k_cap_drop_rows(int2* __restrict__ rows, const unsigned char* __restrict__ who, long long n) {
-  for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < n;
-       k += static_cast<long long>(gridDim.x) * blockDim.x)
-    if (who[k] == 2) rows[k] = make_int2(-1, -1);
-}
-
 // each loop this rank replayed formed exactly the edges the changes give it; the largest count
 __global__ void k_cap_check_shard(const int* __restrict__ T, int nt, const int* __restrict__ tdest, int rank,
                                   const int* __restrict__ own, const int* __restrict__ formed, int n,
@@ -1223,10 +1289,10 @@ struct CapArena {
 };
 
 struct CapWork {
-  CapArena ar[9];                     // 0: per read / per edge, 1: per T read / T-interval, 2: per hit (scratch),
+  CapArena ar[10];                     // 0: per read / per edge, 1: per T read / T-interval, 2: per hit (scratch),
                                       // 3: multi-GPU offsets, 4: the visit sequence; the sharded replay:
                                       // 5: gathered rows, 6: plan (per T read / T-interval), 7: T-T pairs,
-                                      // 8: received offsets and changes
+                                      // 8: received offsets and changes, 9: edge sort scratch
   void* temp = nullptr;
   size_t temp_bytes = 0;
   long long* host = nullptr;          // pinned, device-mapped
@@ -1266,7 +1332,11 @@ struct CapWork {
   bool prepared = false;              // fslr_cap_local ran on the current edges
   // the sharded replay (fslr_cap_install_pairs ... fslr_cap_apply_changes)
   bool gmode = false;                 // the closure runs over the gathered rows
-  int2* grows = nullptr;              // gathered E* (a, b) rows, a < 0 = padding
+  const int2* grows = nullptr;        // gathered E* (a, b) rows, a < 0 = padding (the caller's buffer)
+  int *gstart = nullptr, *gend = nullptr;   // each read's run of forward rows (sorted blocks)
+  int* gflag = nullptr;
+  unsigned long long* gtot = nullptr;       // [2]: valid rows, the runs' total
+  bool g_sorted = false;
   int* gfwd = nullptr;                // their forward degrees
   unsigned char* gwho = nullptr;      // per row: 0 formed in a's loop, 1 in b's, 2 dropped
   int64_t g_rows = 0, g_m = 0;
@@ -1401,7 +1471,8 @@ bool cap_debug() {
 // fslr_long_pairs), the T-intervals and their
 // local hit counts; the local visit lists (partner reads, search order) at w->seq[0 .. nloc),
 // segments at w->ioff (local counts).
-int cap_local(fslr_ctx* c, int thr, CapWork* w, const int2* E, const int* F, int64_t ne, bool all_reads = false) {
+int cap_local(fslr_ctx* c, int thr, CapWork* w, const int2* E, const int* F, int64_t ne, bool all_reads = false,
+              const int* rstart = nullptr, const int* rend = nullptr) {
   hipStream_t s = c->stream;
   set_space(c, w);
   const int64_t n = w->n;
@@ -1443,8 +1514,11 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, const int2* E, const int* F, int
   else if (!frontier) k_cap_init<<<grid_for(n), 256, 0, s>>>(F, static_cast<int>(n), thr, w->state, w->back);
   HIP_TRY(c, hipGetLastError());
   if (frontier) {
-    HIP_TRY(c, hipMemsetAsync(w->acur, 0, static_cast<size_t>(n) * sizeof(int), s));
     HIP_TRY(c, hipMemsetAsync(w->fcnt, 0, 64 * sizeof(unsigned), s));
+  }
+  if (frontier && !rstart) {
+    // the adjacency of E grouped by its lower read (rows sorted by lower read come with their runs)
+    HIP_TRY(c, hipMemsetAsync(w->acur, 0, static_cast<size_t>(n) * sizeof(int), s));
     if (ne > 0) k_cap_adj_count<<<grid_for(ne), 256, 0, s>>>(E, ne, w->acur);
     // aoff[0] = 0, aoff[1 .. n] = the inclusive scan of the counts
     size_t tb = 0;
@@ -1455,14 +1529,21 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, const int2* E, const int* F, int
     HIP_TRY(c, hipMemsetAsync(w->aoff, 0, sizeof(int), s));
     HIP_TRY(c, hipMemsetAsync(w->acur, 0, static_cast<size_t>(n) * sizeof(int), s));
     if (ne > 0) k_cap_adj_fill<<<grid_for(ne), 256, 0, s>>>(E, ne, w->aoff, w->acur, w->adj);
+  }
+  if (frontier) {
     k_cap_seed<<<grid_for(n), 256, 0, s>>>(F, static_cast<int>(n), thr, w->state, w->back, w->fl0, w->fcnt);
     HIP_TRY(c, hipGetLastError());
     int* fl[2] = {w->fl0, w->fl1};
     for (int batch = 0;; ++batch) {
       // rounds r = 0 .. 15 of the batch: frontier fl[r & 1] (count fcnt[r]) -> fl[(r + 1) & 1] (fcnt[r + 1])
-      for (int r = 0; r < 16; ++r)
-        k_cap_frontier<<<1024, 256, 0, s>>>(w->aoff, w->adj, F, thr, w->state, w->back, fl[r & 1], w->fcnt + r,
-                                            fl[(r + 1) & 1], w->fcnt + r + 1);
+      for (int r = 0; r < 16; ++r) {
+        if (rstart)
+          k_cap_frontier_rows<<<1024, 256, 0, s>>>(rstart, rend, E, F, thr, w->state, w->back, fl[r & 1], w->fcnt + r,
+                                                   fl[(r + 1) & 1], w->fcnt + r + 1);
+        else
+          k_cap_frontier<<<1024, 256, 0, s>>>(w->aoff, w->adj, F, thr, w->state, w->back, fl[r & 1], w->fcnt + r,
+                                              fl[(r + 1) & 1], w->fcnt + r + 1);
+      }
       HIP_TRY(c, hipGetLastError());
       unsigned last = 0;
       HIP_TRY(c, hipMemcpyAsync(&last, w->fcnt + 16, sizeof(unsigned), hipMemcpyDeviceToHost, s));
@@ -1842,7 +1923,9 @@ extern "C" int fslr_cap_local(fslr_ctx* c, int32_t thr, int64_t* n_ti, int64_t* 
   if (c->cap_gmode) {                  // the sharded replay: the closure over the gathered rows
     CapWork* w = c->capw;
     if (int rc = ensure_bwd_ranges(c)) return rc;
-    if (int rc = cap_local(c, thr, w, w->grows, w->gfwd, w->g_rows)) return rc;
+    if (int rc = cap_local(c, thr, w, w->grows, w->gfwd, w->g_rows, false, w->g_sorted ? w->gstart : nullptr,
+                           w->g_sorted ? w->gend : nullptr))
+      return rc;
     w->planned = 0;
     w->replayed = false;
     *n_ti = w->nti;
@@ -2044,16 +2127,36 @@ extern "C" int fslr_cap_install_pairs(fslr_ctx* c, const int32_t* pairs, int64_t
   if (int rc = cap_work(c, &w)) return rc;
   {
     Carve cv;
-    cv.add(&w->grows, n_rows);
     cv.add(&w->gfwd, c->n);
+    cv.add(&w->gstart, c->n);
+    cv.add(&w->gend, c->n);
     cv.add(&w->gwho, n_rows);
+    cv.add(&w->gflag, 4);
+    cv.add(&w->gtot, 2);
     if (int rc = cv.commit(c, w->ar[5])) return rc;
   }
-  if (n_rows) HIP_TRY(c, hipMemcpyAsync(w->grows, pairs, static_cast<size_t>(n_rows) * sizeof(int2),
-                                        hipMemcpyDeviceToDevice, s));
-  HIP_TRY(c, hipMemsetAsync(w->gfwd, 0, static_cast<size_t>(std::max<int64_t>(c->n, 1)) * sizeof(int), s));
-  if (n_rows) k_cap_gfwd<<<grid_for(n_rows), 256, 0, s>>>(w->grows, n_rows, w->gfwd);
+  w->grows = reinterpret_cast<const int2*>(pairs);
+  const size_t nb = static_cast<size_t>(std::max<int64_t>(c->n, 1)) * sizeof(int);
+  HIP_TRY(c, hipMemsetAsync(w->gstart, 0, nb, s));
+  HIP_TRY(c, hipMemsetAsync(w->gend, 0, nb, s));
+  HIP_TRY(c, hipMemsetAsync(w->gflag, 0, 4 * sizeof(int), s));
+  HIP_TRY(c, hipMemsetAsync(w->gtot, 0, 2 * sizeof(unsigned long long), s));
+  // each read's run of forward rows (every block sorted by a: fslr_sort_edges before the gather)
+  const int64_t m = n_rows / world;
+  if (n_rows) k_cap_runs<<<grid_for(n_rows), 256, 0, s>>>(w->grows, n_rows, m, w->gstart, w->gend, w->gflag, w->gtot);
+  k_cap_runfwd<<<grid_for(c->n), 256, 0, s>>>(w->gstart, w->gend, static_cast<int>(c->n), w->gfwd, w->gtot + 1);
   HIP_TRY(c, hipGetLastError());
+  unsigned long long tot[2] = {0, 0};
+  int flag = 0;
+  HIP_TRY(c, hipMemcpyAsync(tot, w->gtot, sizeof(tot), hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipMemcpyAsync(&flag, w->gflag, sizeof(flag), hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipStreamSynchronize(s));
+  w->g_sorted = !flag && tot[0] == tot[1];
+  if (!w->g_sorted) {                 // unsorted blocks: forward degrees by atomics, the closure by adjacency
+    HIP_TRY(c, hipMemsetAsync(w->gfwd, 0, nb, s));
+    if (n_rows) k_cap_gfwd<<<grid_for(n_rows), 256, 0, s>>>(w->grows, n_rows, w->gfwd);
+    HIP_TRY(c, hipGetLastError());
+  }
   w->g_rows = n_rows;
   w->g_m = n_rows / world;
   w->g_world = world;
@@ -2353,12 +2456,7 @@ extern "C" int fslr_cap_apply_changes(fslr_ctx* c, const int32_t* changes, int64
   }
   k_cap_check_shard<<<grid_for(std::max<int64_t>(nr, nt)), 256, 0, s>>>(w->T, nt, w->tdest, w->g_rank, w->own, w->formed,
                                                                        static_cast<int>(nr), w->stats, w->err);
-  // the capped graph's components: every row that some loop forms
-  if (rows > 0) k_cap_drop_rows<<<grid_for(rows), 256, 0, s>>>(w->grows, w->gwho, rows);
   HIP_TRY(c, hipGetLastError());
-  HIP_TRY(c, launch_uf_init(c->parent, static_cast<int>(nr), s));
-  HIP_TRY(c, launch_uf_pair_list(c->parent, w->grows, rows, s));
-  HIP_TRY(c, launch_uf_finalize(c->parent, static_cast<int>(nr), s));
   k_cap_commit_shard<<<1, 64, 0, s>>>(w->koff, w->kflag, mloc, c->counters, c->errw, w->stats, w->err, w->host_dev);
   HIP_TRY(c, hipGetLastError());
   HIP_TRY(c, hipStreamSynchronize(s));
@@ -2377,5 +2475,46 @@ extern "C" int fslr_cap_apply_changes(fslr_ctx* c, const int32_t* changes, int64
   cs.backward = host_word(w, kHStat + kStBackward);
   c->cap_stats = cs;
   if (out) *out = cs;
+  return FSLR_OK;
+}
+
+extern "C" int fslr_sort_edges(fslr_ctx* c) {
+  if (!c) return FSLR_ERR_INVALID;
+  if (!c->reads_set) return fail(c, FSLR_ERR_STATE, "fslr_set_reads first");
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (!c->counters || !c->edge_cap) return FSLR_OK;
+  hipStream_t s = c->stream;
+  long long pk[3] = {0, 0, 0};
+  if (int rc = peek_counts(c, pk)) return rc;
+  const int64_t ne = std::min<int64_t>(pk[0], c->edge_cap);
+  if (ne < 2) return FSLR_OK;
+  if (ne >= (int64_t(1) << 31)) return fail(c, FSLR_ERR_INVALID, "too many edges to sort");
+  CapWork* w = nullptr;
+  if (int rc = cap_work(c, &w)) return rc;
+  unsigned long long *k1 = nullptr, *k2 = nullptr;
+  int *v1 = nullptr, *v2 = nullptr;
+  int2* oe = nullptr;
+  unsigned short* oiu = nullptr;
+  {
+    Carve cv;
+    cv.add(&k1, ne);
+    cv.add(&k2, ne);
+    cv.add(&v1, ne);
+    cv.add(&v2, ne);
+    cv.add(&oe, ne);
+    cv.add(&oiu, ne);
+    if (int rc = cv.commit(c, w->ar[9])) return rc;
+  }
+  const int n = static_cast<int>(ne);
+  k_edge_keys<<<grid_for(ne), 256, 0, s>>>(c->edges, ne, k1, v1);
+  size_t tb = 0;
+  HIP_TRY(c, hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k1, k2, v1, v2, n, 0, 32 + bits_for(c->n), s));
+  if (int rc = ensure_temp(c, w, tb)) return rc;
+  tb = w->temp_bytes;
+  HIP_TRY(c, hipcub::DeviceRadixSort::SortPairs(w->temp, tb, k1, k2, v1, v2, n, 0, 32 + bits_for(c->n), s));
+  k_edge_permute<<<grid_for(ne), 256, 0, s>>>(c->edges, c->edge_iu, v2, ne, oe, oiu);
+  HIP_TRY(c, hipGetLastError());
+  HIP_TRY(c, hipMemcpyAsync(c->edges, oe, static_cast<size_t>(ne) * sizeof(int2), hipMemcpyDeviceToDevice, s));
+  HIP_TRY(c, hipMemcpyAsync(c->edge_iu, oiu, static_cast<size_t>(ne) * sizeof(unsigned short), hipMemcpyDeviceToDevice, s));
   return FSLR_OK;
 }

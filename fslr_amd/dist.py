@@ -475,15 +475,17 @@ class SweepShard:
         interval of the other, so the loops are replayed sharded by the components of that graph over
         the candidates T (fslr_hip.h fslr_cap_install_pairs ... fslr_cap_apply_changes):
 
-        1. every rank gathers E* as (a, b) rows (the exchange of the uncapped merge), computes the
-           closure T and lists the search-ordered hits of T's intervals on its own chromosomes;
+        1. every rank sorts its edges by lower read and gathers E* as (a, b) rows, computes the closure
+           T over the rows' runs and lists the search-ordered hits of T's intervals on its own
+           chromosomes;
         2. the ranks' local forests of the T-T hits (and T's hit counts) are all-gathered; every rank
            unions them and assigns the same components to ranks by cost;
         3. the lists travel to the rank replaying their read's component (all_to_all);
         4. each rank replays its components' loops and lists the rows they do not form in the lower
            read's loop (re-oriented or dropped);
         5. those changes are all-gathered and applied everywhere: each rank keeps its own capped edges
-           and forward degrees (the reference's match rows), every rank has the capped graph's labels.
+           and forward degrees (the reference's match rows); the ranks' local forests of those edges
+           are merged as in the uncapped step, so every rank has the capped graph's labels.
         """
         import torch
         ctx, W, r = self.ctx, self.world, self.rank
@@ -491,6 +493,11 @@ class SweepShard:
         err = None
         self.esend = self._grow(self.esend, m)
         self.egath = self._grow(self.egath, W * m)
+        try:
+            ctx.sort_edges()                     # each read's forward rows one run of the gathered rows
+        except Exception as e:                   # noqa: BLE001 - re-raised on every rank
+            err = e
+        self._agree(err)
         ctx.edges_into(self.esend, m)
         if W > 1:
             self._all_gather(self.egath[:W * m], self.esend[:m])
@@ -567,12 +574,28 @@ class SweepShard:
         else:
             chg = self.chsend
         cap = {}
+        fp = 0
         try:
             cap = ctx.cap_apply_changes(chg, W * pad)
             cap.update(capped=int(allp[:, 2].sum()), hits=int(allp[:, 3].sum()), pairs=int(allp[:, 4].sum()))
+            if W == 1:
+                ctx.components()
+            else:
+                fp = ctx.local_forest()             # the capped graph's components: the forest merge
         except Exception as e:                          # noqa: BLE001
             err = e
-        self._agree(err)
+        if W > 1:
+            code = 0 if err is None else (1 if isinstance(err, ZeroDivisionError) else 2)
+            t = self.comm.small([code, fp])
+            self.comm.all_reduce(t, 'max')
+            code, fp = (int(x) for x in t.tolist())
+            if err is None and code:
+                from ._lib import FslrError
+                err = ZeroDivisionError('division by zero') if code == 1 else FslrError('error on another rank')
+            if err is None:
+                self._merge(fp)
+        if err is not None:
+            raise err
         return cap
 
     def labels(self) -> np.ndarray:

@@ -74,7 +74,7 @@
 extern "C" {
 #endif
 
-#define FSLR_ABI_VERSION 12
+#define FSLR_ABI_VERSION 13
 #define FSLR_MAX_L 64                /* max intervals per read (bitmask width) */
 #define FSLR_MAX_READS (1 << 25)     /* read rank packs into bits 6..30 of the index record */
 #define FSLR_THR_ZERO_ALN INT32_MIN
@@ -275,7 +275,9 @@ int  fslr_cap_replay(fslr_ctx *ctx, const int32_t *counts, const int32_t *hits, 
  * replay depend on each other only when an interval of one read hits an interval of the other, so the
  * components of that graph over the candidates T replay independently, each on one rank.
  * fslr_cap_install_pairs: n_rows gathered E* rows as int32 (a, b) pairs (device; a < 0 = padding;
- *   rank w's block is rows [w m, (w + 1) m), m = n_rows / world, in its fslr_copy_edges_device order).
+ *   rank w's block is rows [w m, (w + 1) m), m = n_rows / world, in its fslr_copy_edges_device order,
+ *   after fslr_sort_edges).  The rows are read in place: keep them unchanged until
+ *   fslr_cap_apply_changes.
  *   This context's own edges stay its edge list; fslr_cap_local then computes the closure T over the
  *   gathered rows and lists the hits of T's intervals on this rank's chromosomes (async + syncs).
  * fslr_cap_sizes: |T|, its intervals, the local hits (after fslr_cap_local).
@@ -293,9 +295,10 @@ int  fslr_cap_replay(fslr_ctx *ctx, const int32_t *counts, const int32_t *hits, 
  * fslr_cap_copy_changes: the changes (int32 row << 2 | who, who 1 = formed in b's loop, 2 = dropped)
  *   padded with -1 to n_pad (device, async).  The ranks all-gather them.
  * fslr_cap_apply_changes: every rank's changes: this context keeps its own capped edges (re-oriented as
- *   (former, partner)) and their formers' counts (fwd), the components of the whole capped graph
- *   (fslr_get_labels), errw max_fwd = the largest edges-per-loop.  Syncs; out: applied, max_fwd,
- *   candidates, dropped, backward (capped / hits / pairs: the sum of the ranks' parts). */
+ *   (former, partner)) and their formers' counts (fwd), errw max_fwd = the largest edges-per-loop;
+ *   the components of the capped graph then come from the ranks' local forests (fslr_local_forest).
+ *   Syncs; out: applied, max_fwd, candidates, dropped, backward (capped / hits / pairs: the sum of the
+ *   ranks' parts). */
 /* The multi-GPU merge by local forests (get_subgraphs, cluster.py:230-234, over the union of the ranks'
  * edges).  fslr_local_forest: union-find over this context's edges; the (read, root) pairs of the
  * reads that are not their own root are kept (the same partition as the edges, in fewer pairs);
@@ -304,6 +307,10 @@ int  fslr_cap_replay(fslr_ctx *ctx, const int32_t *counts, const int32_t *hits, 
  * them and fslr_components_from_pairs takes the union. */
 int  fslr_local_forest(fslr_ctx *ctx, int64_t *n_pairs);
 int  fslr_copy_forest_pairs(fslr_ctx *ctx, int32_t *dst, int64_t n_pad);
+/* fslr_sort_edges: this context's edge list (with I, U) in (a, b) order, in place (syncs once for the
+ * count).  The sharded cap's ranks sort before the gather, so each read's forward edges are one run of
+ * the gathered rows (the closure walks the runs; unsorted blocks still work, through an adjacency). */
+int  fslr_sort_edges(fslr_ctx *ctx);
 int  fslr_cap_install_pairs(fslr_ctx *ctx, const int32_t *pairs, int64_t n_rows, int32_t world, int32_t rank);
 int  fslr_cap_sizes(fslr_ctx *ctx, int64_t *n_t, int64_t *n_ti, int64_t *n_hits);
 int  fslr_cap_dep_local(fslr_ctx *ctx, int32_t *out);

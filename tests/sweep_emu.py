@@ -301,6 +301,10 @@ class EmuSweepContext:
         return {'applied': 1}
 
     # -- the sharded edge cap (fslr_cap_install_pairs ... fslr_cap_apply_changes) ------------------
+    def sort_edges(self):
+        if len(self._edges):
+            self._edges = self._edges[np.lexsort((self._edges[:, 1], self._edges[:, 0]))]
+
     def cap_install_pairs(self, t, n_rows, world, rank):
         self._g = t.numpy()[:n_rows].view(np.int32).reshape(-1, 2).astype(np.int64)
         self._gw, self._gr, self._gm = int(world), int(rank), int(n_rows) // int(world)
@@ -447,10 +451,6 @@ class EmuSweepContext:
             formed[a] -= 1
             if who[k] == 1:
                 formed[b] += 1
-        self._parent = np.arange(self.n_reads)
-        for k, (a, b) in enumerate(self._g.tolist()):
-            if a >= 0 and who[k] != 2:
-                self._union(a, b)
         self._gmode = False
         self._st = {'n_edges': len(e), 'edge_capacity': self.edge_capacity, 'max_fwd': int(formed.max())}
         return {'applied': 1, 'max_fwd': int(formed.max()), 'candidates': len(self._T), 'capped': 0, 'hits': 0,

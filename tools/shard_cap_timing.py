@@ -9,7 +9,9 @@ Every phase runs rank after rank (a synchronize around each), so each rank's tim
                 rows, T's local hit lists, the local T-T forest)
   cap_plan[r]   fslr_cap_shard_plan + fslr_cap_shard_pack
   cap_replay[r] fslr_cap_replay_shard (this rank's components)
-  cap_apply[r]  fslr_cap_copy_changes + fslr_cap_apply_changes (+ the capped graph's union-find)
+  cap_apply[r]  fslr_cap_apply_changes + fslr_local_forest (its capped edges' forest)
+  cap_merge[r]  fslr_components_from_pairs over the gathered forests (the capped graph's labels)
+  (the edge sort before the gather, fslr_sort_edges, is reported as a cap_local part)
 The exchanges cannot run on one GPU; they are priced from the bytes each rank moves at an assumed
 per-GPU xGMI rate (--xgmi-gbs) plus a fixed latency per collective (--coll-us), as
 tools/shard_timing.py does.  The single-context step (index + sweep query + fslr_apply_edge_cap +
@@ -113,7 +115,8 @@ def main():
             c.reserve_edges(max(1 << 16, int(2.5 * st1['n_edges'] / W) + 4096))
             c.set_chrom_filter(owner == r if W > 1 else None)
             ctx.append(c)
-        ph = {k: [[] for _ in range(W)] for k in ('part', 'eval', 'cap_local', 'cap_plan', 'cap_replay', 'cap_apply')}
+        ph = {k: [[] for _ in range(W)] for k in ('part', 'eval', 'cap_local', 'cap_plan', 'cap_replay', 'cap_apply',
+                                                     'cap_merge')}
         model = []
         sub = {}
         for rep in range(args.reps + 1):
@@ -146,6 +149,8 @@ def main():
             m = max(1, max(ne))
             rows = torch.empty(W * m, dtype=torch.int64, device=dev)
             for d in range(W):
+                ms, _ = timed_once(lambda: ctx[d].sort_edges())
+                sub.setdefault('sort', [[] for _ in range(W)])[d].append(ms)
                 ctx[d].edges_into(rows[d * m:(d + 1) * m], m)
             nts = []
             tinfo = []
@@ -195,11 +200,20 @@ def main():
             cg = torch.empty(W * pad, dtype=torch.int32, device=dev)
             for r in range(W):
                 ctx[r].cap_copy_changes(cg[r * pad:(r + 1) * pad], pad)
-            caps = []
+            caps, fps = [], []
             for r in range(W):
                 ms, cp = timed_once(lambda: ctx[r].cap_apply_changes(cg, W * pad))
-                ph['cap_apply'][r].append(ms)
+                m4, fp = timed_once(lambda: ctx[r].local_forest())
+                ph['cap_apply'][r].append(ms + m4)
                 caps.append(cp)
+                fps.append(fp)
+            mf = max(1, max(fps))
+            fg = torch.empty(W * mf, dtype=torch.int64, device=dev)
+            for r in range(W):
+                ctx[r].forest_pairs_into(fg[r * mf:(r + 1) * mf], mf)
+            for r in range(W):
+                ms, _ = timed_once(lambda: ctx[r].components_from_pairs(fg, W * mf))
+                ph['cap_merge'][r].append(ms)
             if rep == 0:
                 for r in range(W):
                     assert np.array_equal(ctx[r].labels(), ref_labels), f'rank {r}: labels differ from one context'
@@ -217,14 +231,17 @@ def main():
             hin = np.array([hits_mat[:, w_].sum() - hits_mat[w_, w_] for w_ in range(W)])
             hits_ms = 0.0 if W == 1 else 4 * max(hoff.max(), hin.max()) / gbs + 2 * cl
             chg_ms = 0.0 if W == 1 else 4 * pad * (W - 1) / gbs + 2 * cl     # + the counts' all_gather
+            fgath_ms = 0.0 if W == 1 else 8 * mf * (W - 1) / gbs + 2 * cl    # + the count's all_reduce
             model.append({'a2a_ms': a2a, 'gather_ms': gath, 'tinfo_gather_ms': tg_ms, 'counts_a2a_ms': cnt_ms,
-                          'hits_a2a_ms': hits_ms, 'changes_gather_ms': chg_ms, 'nt': nt, 'changes': chg_n,
+                          'hits_a2a_ms': hits_ms, 'changes_gather_ms': chg_ms, 'forest_gather_ms': fgath_ms,
+                          'forest_pairs': fps, 'nt': nt, 'changes': chg_n,
                           'hits_to': hits_mat.sum(axis=0).tolist(), 'entries_sent': sent.sum(axis=1).tolist(),
                           'edges_per_rank': ne})
         med = {k: [float(np.median(v[r][1:])) for r in range(W)] for k, v in ph.items()}
         mdl = model[-1]
-        cap_ms = (max(med['cap_local']) + mdl['tinfo_gather_ms'] + max(med['cap_plan']) + mdl['counts_a2a_ms']
-                  + mdl['hits_a2a_ms'] + max(med['cap_replay']) + mdl['changes_gather_ms'] + max(med['cap_apply']))
+        cap_ms = (max(sub['sort'][r][-1] for r in range(W)) + max(med['cap_local']) + mdl['tinfo_gather_ms']
+                  + max(med['cap_plan']) + mdl['counts_a2a_ms'] + mdl['hits_a2a_ms'] + max(med['cap_replay'])
+                  + mdl['changes_gather_ms'] + max(med['cap_apply']) + mdl['forest_gather_ms'] + max(med['cap_merge']))
         step = (max(med['part']) + mdl['a2a_ms'] + max(med['eval']) + cl + mdl['gather_ms'] + cap_ms)
         smed = {k: [float(np.median(v[r][1:])) for r in range(W)] for k, v in sub.items()}
         log('cap_local parts (max over ranks):', {k: round(max(v), 3) for k, v in smed.items()})
@@ -234,6 +251,7 @@ def main():
                'single_cap_ms': one[1], 'cap_speedup': one[1] / cap_ms}
         log(f'W={W}: part {max(med["part"]):.3f}, eval {max(med["eval"]):.3f}, cap local {max(med["cap_local"]):.3f} '
             f'plan {max(med["cap_plan"]):.3f} replay {max(med["cap_replay"]):.3f} apply {max(med["cap_apply"]):.3f} '
+            f'merge {max(med["cap_merge"]):.3f} '
             f'ms; cap per rank {cap_ms:.3f} ms (one GPU {one[1]:.3f}); step {step:.3f} ms ({one[2] / step:.2f}x)')
         out['worlds'].append(row)
         print(json.dumps(row), flush=True)
