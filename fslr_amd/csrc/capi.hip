@@ -153,6 +153,7 @@ void fslr_ctx_destroy(fslr_ctx* c) {
   void* bufs[] = {c->rmeta,  c->rlen8, c->iv,     c->qpos,    c->rng_s,  c->idx4,    c->idx_gate, c->data_pos, c->s_start,
                   c->crange, c->keys,   c->keys2,   c->vals,    c->vals2,   c->endkey,  c->pmaxkey,
                   c->temp,   c->umax,   c->edges,   c->edge_iu, c->fwd,     c->parent,  c->counters, c->forest, c->forest_cnt,
+                  c->upl,    c->upl64,
                   c->errw,   c->thr_tmp, c->defer,   c->dchrom,  c->drec,    c->lbounds, c->diag, c->wstat,
                   c->dgate,  c->chist,  c->heavy, c->ent, c->ent_sorted, c->sweep_temp, c->sw_tile, c->sw_wstat, c->ent_ub,
                   c->fdchrom, c->fdrec, c->fdgate, c->crange_f, c->part_cnt, c->grp, c->fmap};
@@ -199,140 +200,127 @@ int fslr_set_reads(fslr_ctx* c, const fslr_reads* r) {
     return fail(c, FSLR_ERR_INVALID, "null array");
   if (r->read_off[0] != 0 || r->read_off[n] != ni)
     return fail(c, FSLR_ERR_INVALID, "read_off does not span intervals");
-  std::vector<int4> rm(static_cast<size_t>(n));
-  std::vector<unsigned char> rl(static_cast<size_t>(n));
-  std::vector<int4> iv(static_cast<size_t>(ni));
-  std::vector<unsigned char> zero(static_cast<size_t>(ni), 0);
-  // per slice the code of its first failure: 0 ok, 1 chrom id, 2 coordinates, 3 read length,
-  // 4 n_alignments, 5 qlen2.  Slices are contiguous in index order, so the lowest failing slice holds
-  // the input's first failure: the same error whatever the thread timing
+  hipStream_t st = c->stream;
+  int rc = ensure_capacity(c, n, ni, r->n_chroms);
+  if (rc) return rc;
+  const int64_t upl_need = 3 * n + 1 + 4 * ni;
+  if (upl_need > c->upl_cap) {
+    if ((rc = dalloc(c, &c->upl, static_cast<size_t>(upl_need)))) return rc;
+    c->upl_cap = upl_need;
+  }
+  if (r->n_chroms + 2 > c->upl64_cap) {
+    if ((rc = dalloc(c, &c->upl64, static_cast<size_t>(r->n_chroms + 2)))) return rc;
+    c->upl64_cap = r->n_chroms + 2;
+  }
+  // the caller's columns to the device as they are; validation and packing run there (upload.hip)
+  int* d_off = c->upl;
+  int* d_q2 = d_off + n + 1;
+  int* d_nal = d_q2 + n;
+  int* d_ch = d_nal + n;
+  int* d_st = d_ch + ni;
+  int* d_en = d_st + ni;
+  int* d_th = d_en + ni;
+  unsigned long long* d_cnt = c->upl64;
+  unsigned long long* d_err = c->upl64 + r->n_chroms;
+  const size_t nb = static_cast<size_t>(n) * sizeof(int), ib = static_cast<size_t>(ni) * sizeof(int);
+  HIP_TRY(c, hipMemsetAsync(d_cnt, 0, static_cast<size_t>(r->n_chroms) * sizeof(unsigned long long), st));
+  HIP_TRY(c, hipMemsetAsync(d_err, 0xff, 2 * sizeof(unsigned long long), st));
+  HIP_TRY(c, hipMemcpyAsync(d_off, r->read_off, nb + sizeof(int), hipMemcpyHostToDevice, st));
+  if (n) {
+    HIP_TRY(c, hipMemcpyAsync(d_q2, r->read_qlen2, nb, hipMemcpyHostToDevice, st));
+    HIP_TRY(c, hipMemcpyAsync(d_nal, r->read_nal, nb, hipMemcpyHostToDevice, st));
+  }
+  if (ni) {
+    HIP_TRY(c, hipMemcpyAsync(d_ch, r->iv_chrom, ib, hipMemcpyHostToDevice, st));
+    HIP_TRY(c, hipMemcpyAsync(d_st, r->iv_start, ib, hipMemcpyHostToDevice, st));
+    HIP_TRY(c, hipMemcpyAsync(d_en, r->iv_end, ib, hipMemcpyHostToDevice, st));
+    HIP_TRY(c, hipMemcpyAsync(d_th, r->iv_thr, ib, hipMemcpyHostToDevice, st));
+    if (r->iv_data_pos) HIP_TRY(c, hipMemcpyAsync(c->data_pos, r->iv_data_pos, ib, hipMemcpyHostToDevice, st));
+  }
+  // the reads' own checks on the host (a read's intervals must lie in [0, ni) before the device reads
+  // them); per slice the code of its first failure: 3 read length, 4 n_alignments, 5 qlen2 — slices are
+  // contiguous in index order, so the lowest failing slice holds the input's first failure
   std::vector<int> bad_slice(static_cast<size_t>(std::max(host_threads(ni), host_threads(n))), 0);
-  auto first_bad = [&]() {
-    for (int b : bad_slice)
-      if (b) return b;
-    return 0;
-  };
-  host_for(ni, [&](int64_t a, int64_t e, int w) {
-    for (int64_t k = a; k < e; ++k) {
-      const int ch = r->iv_chrom[k], s = r->iv_start[k], en = r->iv_end[k], t = r->iv_thr[k];
-      if (ch < 0 || ch >= r->n_chroms) { bad_slice[w] = 1; return; }
-      if (s < 0 || en < s || en >= kMaxCoord) { bad_slice[w] = 2; return; }
-      if (t == FSLR_THR_ZERO_ALN) zero[k] = 1;
-      iv[k] = make_int4(ch, s, en, t);
-    }
-  });
-  int bad = first_bad();
-  if (bad == 1) return fail(c, FSLR_ERR_INVALID, "chrom id out of range");
-  if (bad == 2) return fail(c, FSLR_ERR_INVALID, "interval coordinates out of [0, 2^30)");
   host_for(n, [&](int64_t a, int64_t e, int w) {
     for (int64_t i = a; i < e; ++i) {
-      const int o = r->read_off[i], len = r->read_off[i + 1] - o;
+      const int len = r->read_off[i + 1] - r->read_off[i];
       if (len < 1 || len > FSLR_MAX_L) { bad_slice[w] = 3; return; }
       if (r->read_nal[i] < 0 || r->read_nal[i] >= (1 << 24)) { bad_slice[w] = 4; return; }
       if (r->read_qlen2[i] < 0) { bad_slice[w] = 5; return; }   // max(qend) - min(qstart) over a read's fillings (cluster.py:26-29)
-      int flags = 0;
-      for (int k = o; k < o + len; ++k)
-        if (zero[k]) flags |= 1;
-      rm[i] = make_int4(o, len | (flags << 16), r->read_qlen2[i], r->read_nal[i]);
-      rl[i] = static_cast<unsigned char>(len);
     }
   });
-  bad = first_bad();
+  int bad = 0;
+  for (int b : bad_slice)
+    if (b) { bad = b; break; }
+  UploadArgs ua{};
+  ua.off = d_off;
+  ua.qlen2 = d_q2;
+  ua.nal = d_nal;
+  ua.chrom = d_ch;
+  ua.start = d_st;
+  ua.end = d_en;
+  ua.thr = d_th;
+  ua.dp = r->iv_data_pos ? c->data_pos : nullptr;
+  ua.n = static_cast<int>(n);
+  ua.ni = static_cast<int>(ni);
+  ua.n_chroms = r->n_chroms;
+  ua.reads_ok = bad == 0;
+  ua.iv = c->iv;
+  ua.rmeta = c->rmeta;
+  ua.rlen8 = c->rlen8;
+  ua.dch = c->dchrom;
+  ua.drc = c->drec;
+  ua.dgt = c->dgate;
+  ua.inv = c->vals2;
+  ua.chrom_cnt = d_cnt;
+  ua.err = d_err;
+  HIP_TRY(c, launch_upload_pack(ua, st));
+  // beside the device: the aln_size == 0 marks (fslr_set_thresholds checks them) and the threshold mode
+  std::vector<unsigned char> zero(static_cast<size_t>(ni), 0);
+  std::vector<int> any_zero(static_cast<size_t>(host_threads(ni)), 0);
+  host_for(ni, [&](int64_t a, int64_t e, int w) {
+    int z = 0;
+    for (int64_t k = a; k < e; ++k) {
+      const unsigned char f = r->iv_thr[k] == FSLR_THR_ZERO_ALN;
+      zero[k] = f;
+      z |= f;
+    }
+    any_zero[w] = z;
+  });
+  const int tmode = thr_mode_of(r->iv_thr, ni);
+  std::vector<int64_t> chrom_counts(static_cast<size_t>(r->n_chroms), 0);
+  unsigned long long err[2] = {0, 0};
+  HIP_TRY(c, hipMemcpyAsync(chrom_counts.data(), d_cnt, chrom_counts.size() * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipMemcpyAsync(err, d_err, sizeof(err), hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipStreamSynchronize(st));
+  c->reads_set = false;
+  if (err[0] != ~0ull) {
+    if ((err[0] & 7) == kUpErrChrom) return fail(c, FSLR_ERR_INVALID, "chrom id out of range");
+    return fail(c, FSLR_ERR_INVALID, "interval coordinates out of [0, 2^30)");
+  }
   if (bad == 3) return fail(c, FSLR_ERR_INVALID, "every read needs 1.." + std::to_string(FSLR_MAX_L) + " intervals");
   if (bad == 4) return fail(c, FSLR_ERR_INVALID, "n_alignments outside [0, 2^24)");
   if (bad == 5) return fail(c, FSLR_ERR_INVALID, "qlen2 < 0");
-  // chromosome ranges of the (chrom, start)-sorted index: chromosome ids ascending (host counts)
+  if (err[1] != ~0ull) return fail(c, FSLR_ERR_INVALID, "iv_data_pos is not a start-sorted permutation");
+  // chromosome ranges of the (chrom, start)-sorted index: chromosome ids ascending
   std::vector<int2> cr(static_cast<size_t>(r->n_chroms), make_int2(0, 0));
-  std::vector<int64_t> chrom_counts(static_cast<size_t>(r->n_chroms), 0);
-  {
-    std::vector<std::vector<int64_t>> part(static_cast<size_t>(host_threads(ni)),
-                                           std::vector<int64_t>(static_cast<size_t>(r->n_chroms), 0));
-    host_for(ni, [&](int64_t a, int64_t e, int w) {
-      std::vector<int64_t>& cnt = part[static_cast<size_t>(w)];
-      for (int64_t k = a; k < e; ++k) cnt[r->iv_chrom[k]]++;
-    });
-    for (const auto& p : part)
-      for (int ch = 0; ch < r->n_chroms; ++ch) chrom_counts[ch] += p[ch];
-    int64_t acc = 0;
-    for (int ch = 0; ch < r->n_chroms; ++ch) {
-      cr[ch] = make_int2(static_cast<int>(acc), static_cast<int>(acc + chrom_counts[ch]));
-      acc += chrom_counts[ch];
-    }
+  int64_t acc = 0;
+  for (int ch = 0; ch < r->n_chroms; ++ch) {
+    cr[ch] = make_int2(static_cast<int>(acc), static_cast<int>(acc + chrom_counts[ch]));
+    acc += chrom_counts[ch];
   }
-  // optional start-sorted data order: must be a permutation with non-decreasing start
-  bool use_dp = false;
-  std::vector<int> inv;
-  if (r->iv_data_pos) {
-    inv.assign(static_cast<size_t>(ni), -1);
-    std::atomic<bool> ok{true};
-    host_for(ni, [&](int64_t a, int64_t e, int) {
-      for (int64_t k = a; k < e; ++k) {
-        const int d = r->iv_data_pos[k];
-        if (d < 0 || d >= ni) { ok = false; return; }
-        // atomic: a repeated d is seen by whichever thread comes second (the message is the same)
-        if (__atomic_exchange_n(&inv[static_cast<size_t>(d)], static_cast<int>(k), __ATOMIC_RELAXED) != -1) {
-          ok = false;
-          return;
-        }
-      }
-    });
-    if (ok)
-      host_for(ni, [&](int64_t a, int64_t e, int) {
-        for (int64_t d = a; d < e; ++d) {
-          if (inv[d] < 0 || (d > 0 && (inv[d - 1] < 0 || r->iv_start[inv[d]] < r->iv_start[inv[d - 1]]))) {
-            ok = false;
-            return;
-          }
-        }
-      });
-    use_dp = ok;
-    if (!use_dp) return fail(c, FSLR_ERR_INVALID, "iv_data_pos is not a start-sorted permutation");
-  }
-  int rc = ensure_capacity(c, n, ni, r->n_chroms);
-  if (rc) return rc;
-  HIP_TRY(c, hipMemcpyAsync(c->crange, cr.data(), cr.size() * sizeof(int2), hipMemcpyHostToDevice, c->stream));
-  std::vector<unsigned> dch;
-  std::vector<int4> drc;
-  std::vector<int2> dgt;
-  if (use_dp && ni) {
-    // the `data` list itself (cluster.py:116-121) in its start-sorted order
-    dch.resize(static_cast<size_t>(ni));
-    drc.resize(static_cast<size_t>(ni));
-    dgt.resize(static_cast<size_t>(ni));
-    host_for(n, [&](int64_t a, int64_t e, int) {
-      for (int64_t i = a; i < e; ++i) {
-        // the gate word of kernels.hpp idx_gate, per interval like the reference's IntervalItem
-        // (which carries qlen2 and n_alignments, cluster.py:10-11)
-        const int4 m = rm[i];
-        const int2 gate = make_int2(m.z, (m.w & 0xFFFFFF) | ((m.y & 0x7F) << 24) | (((m.y >> 16) & 1) << 31));
-        for (int k = r->read_off[i]; k < r->read_off[i + 1]; ++k) {
-          const int d = r->iv_data_pos[k];
-          dch[d] = static_cast<unsigned>(r->iv_chrom[k]);
-          drc[d] = make_int4(r->iv_start[k], r->iv_end[k], r->iv_thr[k],
-                             static_cast<int>((i << 6) | (k - r->read_off[i])));
-          dgt[d] = gate;
-        }
-      }
-    });
-    HIP_TRY(c, hipMemcpyAsync(c->data_pos, r->iv_data_pos, ni * sizeof(int), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(c, hipMemcpyAsync(c->dchrom, dch.data(), ni * sizeof(unsigned), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(c, hipMemcpyAsync(c->drec, drc.data(), ni * sizeof(int4), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(c, hipMemcpyAsync(c->dgate, dgt.data(), ni * sizeof(int2), hipMemcpyHostToDevice, c->stream));
-  }
-  c->have_data_pos = use_dp;
+  HIP_TRY(c, hipMemcpyAsync(c->crange, cr.data(), cr.size() * sizeof(int2), hipMemcpyHostToDevice, st));
+  HIP_TRY(c, hipStreamSynchronize(st));
+  c->have_data_pos = r->iv_data_pos != nullptr;
   c->n = n;
   c->ni = ni;
   c->ni_idx = ni;
   c->filter_active = false;
   c->chrom_counts.swap(chrom_counts);
   c->n_chroms = r->n_chroms;
-  c->thr_mode = thr_mode_of(r->iv_thr, ni);
-  c->any_zero_aln = std::find(zero.begin(), zero.end(), 1) != zero.end();
+  c->thr_mode = tmode;
+  c->any_zero_aln = std::find(any_zero.begin(), any_zero.end(), 1) != any_zero.end();
   c->aln_zero_host.swap(zero);
-  if (n) HIP_TRY(c, hipMemcpyAsync(c->rmeta, rm.data(), n * sizeof(int4), hipMemcpyHostToDevice, c->stream));
-  if (n) HIP_TRY(c, hipMemcpyAsync(c->rlen8, rl.data(), n, hipMemcpyHostToDevice, c->stream));
-  if (ni) HIP_TRY(c, hipMemcpyAsync(c->iv, iv.data(), ni * sizeof(int4), hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
   c->reads_set = true;
   c->index_built = false;
   c->lg_set = false;                        // a virtual-read map belongs to the reads it was set for

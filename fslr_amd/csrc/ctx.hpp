@@ -81,6 +81,10 @@ struct fslr_ctx {
   int* fwd = nullptr;
   int* heavy = nullptr;      // [N] reads handed to the partitioned pair-kernel launch
   int* parent = nullptr;
+  int* upl = nullptr;                        // fslr_set_reads: the caller's columns as copied (upload.hip)
+  int64_t upl_cap = 0;
+  unsigned long long* upl64 = nullptr;       // [n_chroms + 2]: intervals per chromosome, first failures
+  int64_t upl64_cap = 0;
   int2* forest = nullptr;                    // [n] the local forest's (read, root) pairs (fslr_local_forest)
   unsigned long long* forest_cnt = nullptr;  // [1] their count (device)
   unsigned long long* counters = nullptr;

@@ -233,6 +233,27 @@ hipError_t launch_chrom_filter(const unsigned* dchrom, const int4* drec, const i
                                size_t temp_bytes, hipStream_t s);
 
 
+// ---- upload (upload.hip): fslr_set_reads' validation and packing on the device ----------------
+enum UploadErr { kUpErrChrom = 1, kUpErrCoord = 2, kUpErrDataPos = 6 };
+constexpr int kUpHistLds = 4096;      // chromosomes counted in LDS (more: global atomics)
+struct UploadArgs {
+  // the caller's columns, copied as they are
+  const int *off, *qlen2, *nal, *chrom, *start, *end, *thr, *dp;   // dp null: no data order
+  int n, ni, n_chroms;
+  bool reads_ok;                      // read_off passed the host checks (k_up_reads / k_up_data may run)
+  // outputs
+  int4* iv;
+  int4* rmeta;
+  unsigned char* rlen8;
+  unsigned* dch;
+  int4* drc;
+  int2* dgt;
+  int* inv;                           // [ni] scratch
+  unsigned long long* chrom_cnt;      // [n_chroms], zeroed by the caller
+  unsigned long long* err;            // [2] first failure (index << 3 | code): columns, data order; ~0 by the caller
+};
+hipError_t launch_upload_pack(const UploadArgs& a, hipStream_t s);
+
 // ---- components (components.hip) ---------------------------------------------------------
 hipError_t launch_uf_init(int* parent, int n, hipStream_t s);
 // counters[0, nc), err[0, ne) and fwd[0, n) to zero in one launch (start of a query)
