@@ -20,8 +20,9 @@ pairs (gate-rejected ones included) and the dense-equivalent rate are secondary 
 others in ``roofline_other_kernels``.  Sweep engine (default): the position sweep
 k_sweep<2> — every sorted position's index record, gate word and forward
 count and its read's gate ranges read once (48 B), plus each match entry written (8 B) —
-and the pair stage k_bucket_pairs — each match entry read once from the grouping's pass-1
-buckets (8 B), each edge written (10 B), each read's forward degree written (4 B).  Walk engine: query_kernel, every
+and the pair stage k_sweep_pairs — each grouped match entry read once (8 B), each edge written
+(10 B), each read's forward degree written (4 B) (the same bytes for the fused variant
+k_bucket_pairs, FSLR_PAIR_STAGE=fused, which reads the entries from the grouping's pass-1 buckets).  Walk engine: query_kernel, every
 walked index record (16-B record + 8-B gate word) read once, each query read's header,
 gate bounds and forward degree, each of its intervals' sorted position, row and scan
 range, and the edge / deferred-list output.  ``achieved`` = those bytes ÷ the mean
@@ -53,9 +54,9 @@ B_WALK, B_READ, B_IVL, B_EDGE, B_DEFER = 24, 8 + 16 + 4, 4 + 12 + 8, 8 + 2, 8
 B_POS, B_ENT = 16 + 8 + 8 + 16, 8
 KERNEL_SOURCES = {'sweep': ('sweep.hip', 'wave.hpp', 'kernels.hpp'), 'walk': ('query.hip', 'kernels.hpp')}
 KERNEL_NAME = {'sweep': 'k_sweep<2>', 'walk': 'query_kernel<0, false>'}
-# the sweep's pair-stage kernel (the one fslr_get_stage_kernel_times(1) times): the bucket kernel,
-# or with FSLR_PAIR_STAGE=legacy the round-3 k_sweep_pairs over the grouped entries
-PAIR_STAGE = 'k_sweep_pairs' if os.environ.get('FSLR_PAIR_STAGE') == 'legacy' else 'k_bucket_pairs'
+# the sweep's pair-stage kernel (the one fslr_get_stage_kernel_times(1) times): k_sweep_pairs over the
+# grouped entries, or with FSLR_PAIR_STAGE=fused the bucket kernel fused with the grouping's pass 2
+PAIR_STAGE = 'k_bucket_pairs' if os.environ.get('FSLR_PAIR_STAGE') == 'fused' else 'k_sweep_pairs'
 # the reference's own rate on this config: 33,020,021 Jaccard-evaluated
 # pairs in 1454.0 s of query_interval_trees, 1 core of the survey container, pure Python
 REFERENCE_PY = {'value': 33_020_021 / 1454.0, 'unit': 'Jaccard-evaluated read pairs/s', 'cores': 1,
@@ -299,6 +300,10 @@ def main():
         split = e.get('wave_cycle_split') if e.get('source_hash') == src_hash else None
         return {'bound': 'hbm', 'kernel': name, 'achieved': ach / 1e9, 'peak': HBM_PEAK / 1e9, 'unit': 'GB/s',
                 'frac': ach / HBM_PEAK, 'traffic': traffic,
+                # the roofline is HBM's (integer work, no MFMA); what limits these kernels is latency and
+                # issue, not bytes: valu_issue_frac and wave_cycle_split say how far from the issue side
+                'limiter': 'latency / issue (dependent LDS and gather chains), not HBM bytes: see valu_issue_frac, '
+                           'wave_cycle_split',
                 # the issue side beside the HBM side: 2 cycles per wave64 VALU instruction over the
                 # launch's cycles on 1024 SIMDs (PMC), and where the wave-cycles went
                 'valu_issue_frac': valu, 'wave_cycle_split': split,
@@ -313,7 +318,7 @@ def main():
         # 10 B), each read's forward degree written (4 B); the 1-byte read lengths it looks up stay in L2
         pb = B_ENT * sw['match_entries'] + 10 * st['n_edges'] + 4 * csr.n_reads
         roofs.append(roofline(PAIR_STAGE, kern2, pb,
-                              f'{B_ENT} B x match entries read from the grouping\'s buckets ({sw["match_entries"]}) '
+                              f'{B_ENT} B x grouped match entries read ({sw["match_entries"]}) '
                               f'+ 10 B x edges written ({st["n_edges"]}) + 4 B x forward degrees ({csr.n_reads})'))
     # the headline roofline is the longest kernel's (HIP events over the timed steps)
     roofs.sort(key=lambda r: -r['kernel_ms'] if r['kernel_ms'] == r['kernel_ms'] else 0.0)

@@ -386,7 +386,7 @@ class Context:
         self._check(self._L.fslr_copy_edges_device(self._h, ctypes.c_void_p(t.data_ptr()), int(n_pad)))
 
     def sort_edges(self):
-        """This context's edges (with I, U) in (a, b) order, in place."""
+        """This context's edges (with I, U) grouped by lower read, stably, in place."""
         self._check(self._L.fslr_sort_edges(self._h))
 
     def local_forest(self, count: bool = True):

@@ -38,6 +38,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -1017,12 +1018,12 @@ __global__ void k_cap_frontier_rows(const int* __restrict__ gstart, const int* _
   }
 }
 
-// this context's edges by (a, b): keys and their positions, then the permutation
-__global__ void k_edge_keys(const int2* __restrict__ e, long long n, unsigned long long* __restrict__ key,
+// this context's edges by lower read (stable): keys and their positions, then the permutation
+__global__ void k_edge_keys(const int2* __restrict__ e, long long n, unsigned* __restrict__ key,
                             int* __restrict__ val) {
   for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < n;
        k += static_cast<long long>(gridDim.x) * blockDim.x) {
-    key[k] = (static_cast<unsigned long long>(static_cast<unsigned>(e[k].x)) << 32) | static_cast<unsigned>(e[k].y);
+    key[k] = static_cast<unsigned>(e[k].x);
     val[k] = static_cast<int>(k);
   }
 }
@@ -1440,11 +1441,15 @@ void set_space(fslr_ctx* c, CapWork* w) {
   }
 }
 
-// FSLR_CAP_CLOSURE=rounds: the round-3 closure (every edge and read each round), for A/B
+// The closure over an edge list: rounds over every edge and read (default), or FSLR_CAP_CLOSURE=frontier,
+// rounds over the joined reads' forward edges only, through an adjacency built with per-edge atomics.
+// Measured at cfg5 (profiles/r04/r4e/): the whole replay 5.15 ms with rounds, 5.9 ms with the frontier
+// (its adjacency build, 1.2 ms, costs more than the rounds it saves).  Gathered rows sorted by lower
+// read (the sharded replay) have their adjacency for free and always take the frontier.
 bool cap_rounds_closure() {
   static const bool v = [] {
     const char* e = std::getenv("FSLR_CAP_CLOSURE");
-    return e && std::strcmp(e, "rounds") == 0;
+    return !(e && std::strcmp(e, "frontier") == 0);
   }();
   return v;
 }
@@ -1461,11 +1466,30 @@ bool cap_dag_enabled() {
   return v;
 }
 
-// FSLR_DEBUG_CAP=1: the dependency components' sizes on stderr (diagnostics)
+// FSLR_DEBUG_CAP=1: the dependency components' sizes and per-stage times on stderr (diagnostics; the
+// stage times synchronize the stream)
 bool cap_debug() {
   static const bool v = std::getenv("FSLR_DEBUG_CAP") != nullptr;
   return v;
 }
+
+struct CapTimer {
+  bool on;
+  hipStream_t s;
+  std::chrono::steady_clock::time_point t;
+  explicit CapTimer(hipStream_t st) : on(cap_debug()), s(st), t(std::chrono::steady_clock::now()) {
+    if (on) (void)hipStreamSynchronize(s);
+    t = std::chrono::steady_clock::now();
+  }
+  void lap(const char* what) {
+    if (!on) return;
+    (void)hipStreamSynchronize(s);
+    const auto now = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "fslr: cap stage %-14s %8.3f ms\n", what,
+                 std::chrono::duration<double, std::milli>(now - t).count());
+    t = now;
+  }
+};
 
 // Phase A: the closure T over E* = E[0 .. ne) with forward degrees F (all_reads: every read,
 // fslr_long_pairs), the T-intervals and their
@@ -1474,6 +1498,7 @@ bool cap_debug() {
 int cap_local(fslr_ctx* c, int thr, CapWork* w, const int2* E, const int* F, int64_t ne, bool all_reads = false,
               const int* rstart = nullptr, const int* rend = nullptr) {
   hipStream_t s = c->stream;
+  CapTimer tm(s);
   set_space(c, w);
   const int64_t n = w->n;
   w->thr = thr;
@@ -1509,7 +1534,7 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, const int2* E, const int* F, int
   HIP_TRY(c, hipMemsetAsync(w->stats, 0, kStWords * sizeof(long long), s));
   // 1. closure.  Frontier rounds (batches of 16, one sync per batch), or FSLR_CAP_CLOSURE=rounds:
   // rounds over every edge and read in batches of 8 (chg[0] = 1 starts each batch)
-  const bool frontier = !all_reads && !cap_rounds_closure();
+  const bool frontier = !all_reads && (rstart || !cap_rounds_closure());
   if (all_reads) k_cap_all<<<grid_for(n), 256, 0, s>>>(w->state, static_cast<int>(n));
   else if (!frontier) k_cap_init<<<grid_for(n), 256, 0, s>>>(F, static_cast<int>(n), thr, w->state, w->back);
   HIP_TRY(c, hipGetLastError());
@@ -1570,6 +1595,7 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, const int2* E, const int* F, int
     if (!last) break;
     if (batch > (n >> 3) + 2) return fail(c, FSLR_ERR_STATE, "edge cap closure does not converge");
   }
+  tm.lap("closure");
   // T in rank order, T-intervals
   k_cap_tpack<<<grid_for(n), 256, 0, s>>>(w->state, c->rmeta, w->rlen, static_cast<int>(n), w->tv);
   size_t tb = 0;
@@ -1623,6 +1649,7 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, const int2* E, const int* F, int
   HIP_TRY(c, hipGetLastError());
   HIP_TRY(c, hipStreamSynchronize(s));
   w->nloc = host_word(w, kHNloc);
+  tm.lap("T, hit counts");
   if (w->nloc >= (int64_t(1) << 31)) return fail(c, FSLR_ERR_NOMEM, "edge cap replay: more than 2^31 hits");
   {
     Carve c2, c4;
@@ -1637,6 +1664,7 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, const int2* E, const int* F, int
     k_cap_seq<<<wave_grid(nti), 256, 0, s>>>(w->seqp, c->idx4, w->ioff, w->vreal, nti, w->seq);
     HIP_TRY(c, hipGetLastError());
   }
+  tm.lap("hit lists");
   w->prepared = true;
   return FSLR_OK;
 }
@@ -1696,10 +1724,12 @@ int cap_slots(fslr_ctx* c, CapWork* w) {
 // 3 + 4: slots, predicates and every read of T's loop (pbrk, own, visit marks)
 int cap_loops(fslr_ctx* c, CapWork* w) {
   hipStream_t s = c->stream;
+  CapTimer tm(s);
   const int thr = w->thr;
   const int nt = static_cast<int>(w->nt);
   const int m = static_cast<int>(w->nseq);
   if (int rc = cap_slots(c, w)) return rc;
+  tm.lap("slots, eval");
   const int ns = static_cast<int>(w->ns);
   if (m > 0) {
     // mirror slots; each read's earlier T partners (its in-degree in the loops' dependency DAG)
@@ -1771,6 +1801,7 @@ int cap_loops(fslr_ctx* c, CapWork* w) {
     HIP_TRY(c, hipGetLastError());
   }
   w->ns = ns;
+  tm.lap("loops");
   return FSLR_OK;
 }
 
@@ -1780,6 +1811,7 @@ int cap_core(fslr_ctx* c, CapWork* w, fslr_cap_stats* cs) {
   const int nt = static_cast<int>(w->nt);
   if (int rc = cap_loops(c, w)) return rc;
   const int ns = static_cast<int>(w->ns);
+  CapTimer tm(s);
   // 5. the capped graph
   // edges formed per loop, from the E* forward degrees (fwd[x] = E* edges (x, .), as the query or the
   // install left them)
@@ -1804,6 +1836,7 @@ int cap_core(fslr_ctx* c, CapWork* w, fslr_cap_stats* cs) {
   k_cap_commit<<<1, 64, 0, s>>>(w->koff, w->kflag, ne, c->counters, c->errw, w->stats, w->err, w->host_dev);
   HIP_TRY(c, hipGetLastError());
   HIP_TRY(c, hipStreamSynchronize(s));
+  tm.lap("classify");
   const long long err = host_word(w, kHErr);
   if (err & kCapErrZd) return fail(c, FSLR_ERR_ZERO_DIVISION, "division by zero");
   if (err & kCapErrState) return fail(c, FSLR_ERR_STATE, "edge cap replay: inconsistent loop replay");
@@ -2152,6 +2185,7 @@ extern "C" int fslr_cap_install_pairs(fslr_ctx* c, const int32_t* pairs, int64_t
   HIP_TRY(c, hipMemcpyAsync(&flag, w->gflag, sizeof(flag), hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipStreamSynchronize(s));
   w->g_sorted = !flag && tot[0] == tot[1];
+  if (cap_debug()) std::fprintf(stderr, "fslr: cap install %lld rows, sorted %d\n", static_cast<long long>(n_rows), w->g_sorted);
   if (!w->g_sorted) {                 // unsorted blocks: forward degrees by atomics, the closure by adjacency
     HIP_TRY(c, hipMemsetAsync(w->gfwd, 0, nb, s));
     if (n_rows) k_cap_gfwd<<<grid_for(n_rows), 256, 0, s>>>(w->grows, n_rows, w->gfwd);
@@ -2229,6 +2263,7 @@ extern "C" int fslr_cap_shard_plan(fslr_ctx* c, const int32_t* gathered, int32_t
     cv.add(&w->totals, 2 * kMaxDest);
     if (int rc = cv.commit(c, w->ar[6])) return rc;
   }
+  CapTimer tm(s);
   // the components of the T-T hit graph: the union of the ranks' local forests
   std::vector<int> comp(nt), cost(nt), dest(nt);
   if (nt > 0) {
@@ -2260,6 +2295,7 @@ extern "C" int fslr_cap_shard_plan(fslr_ctx* c, const int32_t* gathered, int32_t
     load[d] += ccost[r];
   }
   for (int t = 0; t < nt; ++t) dest[t] = droot[comp[t]];
+  tm.lap("plan: assign");
   if (nt > 0)
     HIP_TRY(c, hipMemcpyAsync(w->tdest, dest.data(), static_cast<size_t>(nt) * sizeof(int), hipMemcpyHostToDevice, s));
   // the T-intervals grouped by destination (stable: T order inside a group), their counts and hits
@@ -2291,6 +2327,7 @@ extern "C" int fslr_cap_shard_plan(fslr_ctx* c, const int32_t* gathered, int32_t
     if (d < rank) off += tot[d];
     hits += tot[kMaxDest + d];
   }
+  tm.lap("plan: group");
   if (hits != w->nloc) return fail(c, FSLR_ERR_STATE, "sharded edge cap: hit totals differ from the local lists");
   w->nmine = tot[rank];
   w->mine_off = off;
@@ -2368,6 +2405,7 @@ extern "C" int fslr_cap_replay_shard(fslr_ctx* c, const int32_t* rcounts, const 
     k_cap_recv_assemble<<<wave_grid(nmine), 256, 0, s>>>(rcounts, w->roff, rhits, world, nmine, mine, w->ioff, w->seq);
     HIP_TRY(c, hipGetLastError());
   }
+  CapTimer tm(s);
   // slots, predicates and loops of this rank's components (every other T read has no hit: no break)
   if (int rc = cap_loops(c, w)) return rc;
   const int ns = static_cast<int>(w->ns);
@@ -2381,6 +2419,7 @@ extern "C" int fslr_cap_replay_shard(fslr_ctx* c, const int32_t* rcounts, const 
     k_cap_count_capped<<<grid_for(nt), 256, 0, s>>>(w->pbrk, nt, w->stats);
     HIP_TRY(c, hipGetLastError());
   }
+  tm.lap("classify");
   unsigned nch = 0;
   int err = 0;
   long long capped = 0;
@@ -2428,6 +2467,7 @@ extern "C" int fslr_cap_apply_changes(fslr_ctx* c, const int32_t* changes, int64
   const int64_t nr = c->n, rows = w->g_rows, m = w->g_m;
   const int nt = static_cast<int>(w->nt);
   const int64_t mloc = std::min(m, c->edge_cap);
+  CapTimer tm(s);
   HIP_TRY(c, hipMemsetAsync(w->err, 0, 4 * sizeof(int), s));
   HIP_TRY(c, hipMemsetAsync(w->stats, 0, kStWords * sizeof(long long), s));
   if (rows) HIP_TRY(c, hipMemsetAsync(w->gwho, 0, static_cast<size_t>(rows), s));
@@ -2436,6 +2476,7 @@ extern "C" int fslr_cap_apply_changes(fslr_ctx* c, const int32_t* changes, int64
     k_cap_apply<<<grid_for(n), 256, 0, s>>>(changes, n, w->grows, w->gwho, w->formed, w->stats);
     HIP_TRY(c, hipGetLastError());
   }
+  tm.lap("apply: changes");
   // this rank's own edges (block g_rank of the rows): kept ones compacted and re-oriented, their formers
   const int2* blk = w->grows + w->g_rank * m;
   const unsigned char* wblk = w->gwho + w->g_rank * m;
@@ -2454,6 +2495,7 @@ extern "C" int fslr_cap_apply_changes(fslr_ctx* c, const int32_t* changes, int64
     HIP_TRY(c, hipMemcpyAsync(c->edge_iu, w->oiu, static_cast<size_t>(mloc) * sizeof(unsigned short),
                               hipMemcpyDeviceToDevice, s));
   }
+  tm.lap("apply: local");
   k_cap_check_shard<<<grid_for(std::max<int64_t>(nr, nt)), 256, 0, s>>>(w->T, nt, w->tdest, w->g_rank, w->own, w->formed,
                                                                        static_cast<int>(nr), w->stats, w->err);
   HIP_TRY(c, hipGetLastError());
@@ -2491,7 +2533,7 @@ extern "C" int fslr_sort_edges(fslr_ctx* c) {
   if (ne >= (int64_t(1) << 31)) return fail(c, FSLR_ERR_INVALID, "too many edges to sort");
   CapWork* w = nullptr;
   if (int rc = cap_work(c, &w)) return rc;
-  unsigned long long *k1 = nullptr, *k2 = nullptr;
+  unsigned *k1 = nullptr, *k2 = nullptr;
   int *v1 = nullptr, *v2 = nullptr;
   int2* oe = nullptr;
   unsigned short* oiu = nullptr;
@@ -2508,10 +2550,10 @@ extern "C" int fslr_sort_edges(fslr_ctx* c) {
   const int n = static_cast<int>(ne);
   k_edge_keys<<<grid_for(ne), 256, 0, s>>>(c->edges, ne, k1, v1);
   size_t tb = 0;
-  HIP_TRY(c, hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k1, k2, v1, v2, n, 0, 32 + bits_for(c->n), s));
+  HIP_TRY(c, hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k1, k2, v1, v2, n, 0, bits_for(c->n), s));
   if (int rc = ensure_temp(c, w, tb)) return rc;
   tb = w->temp_bytes;
-  HIP_TRY(c, hipcub::DeviceRadixSort::SortPairs(w->temp, tb, k1, k2, v1, v2, n, 0, 32 + bits_for(c->n), s));
+  HIP_TRY(c, hipcub::DeviceRadixSort::SortPairs(w->temp, tb, k1, k2, v1, v2, n, 0, bits_for(c->n), s));
   k_edge_permute<<<grid_for(ne), 256, 0, s>>>(c->edges, c->edge_iu, v2, ne, oe, oiu);
   HIP_TRY(c, hipGetLastError());
   HIP_TRY(c, hipMemcpyAsync(c->edges, oe, static_cast<size_t>(ne) * sizeof(int2), hipMemcpyDeviceToDevice, s));

@@ -307,8 +307,8 @@ int  fslr_cap_replay(fslr_ctx *ctx, const int32_t *counts, const int32_t *hits, 
  * them and fslr_components_from_pairs takes the union. */
 int  fslr_local_forest(fslr_ctx *ctx, int64_t *n_pairs);
 int  fslr_copy_forest_pairs(fslr_ctx *ctx, int32_t *dst, int64_t n_pad);
-/* fslr_sort_edges: this context's edge list (with I, U) in (a, b) order, in place (syncs once for the
- * count).  The sharded cap's ranks sort before the gather, so each read's forward edges are one run of
+/* fslr_sort_edges: this context's edge list (with I, U) grouped by a, stably, in place (syncs once for
+ * the count).  The sharded cap's ranks sort before the gather, so each read's forward edges are one run of
  * the gathered rows (the closure walks the runs; unsorted blocks still work, through an adjacency). */
 int  fslr_sort_edges(fslr_ctx *ctx);
 int  fslr_cap_install_pairs(fslr_ctx *ctx, const int32_t *pairs, int64_t n_rows, int32_t world, int32_t rank);
