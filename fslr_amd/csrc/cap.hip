@@ -63,6 +63,19 @@ enum CapStat { kStCapped = 0, kStDropped, kStBackward, kStMaxFwd, kStKept, kStWo
 // pinned host words (written by tiny kernels; one sync each)
 enum CapHost { kHNt = 0, kHNti, kHNloc, kHNslots, kHNseq, kHErr, kHStat = 8, kHWords = 16 };
 
+// one value per block: the wavefronts' values combined in LDS, valid in thread 0 (call from every thread
+// of the block; 256 threads).  A per-block atomic instead of one per wavefront: one hot word takes
+// ~90 returning atomics per microsecond, so 150k wave atomics over a 10M-read pass cost ~0.2 ms
+template <typename T, typename Op>
+__device__ __forceinline__ T block_reduce256(T v, Op op) {
+  __shared__ T ws[4];
+  for (int o = 32; o > 0; o >>= 1) v = op(v, __shfl_xor(v, o));
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) v = op(op(ws[0], ws[1]), op(ws[2], ws[3]));
+  return v;
+}
+
 __device__ __forceinline__ unsigned long long lanes_le(int lane) {
   return lane == 63 ? ~0ull : (2ull << lane) - 1ull;
 }
@@ -849,11 +862,9 @@ __global__ void k_cap_check(const int* __restrict__ T, int nt, const int* __rest
     }
     if (i < n) mx = max(mx, formed[i]);
   }
-  for (int o = 32; o > 0; o >>= 1) {
-    capped += __shfl_xor(capped, o);
-    mx = max(mx, __shfl_xor(mx, o));
-  }
-  if ((threadIdx.x & 63) == 0) {
+  capped = block_reduce256(capped, [](int x, int y) { return x + y; });
+  mx = block_reduce256(mx, [](int x, int y) { return max(x, y); });
+  if (threadIdx.x == 0) {
     if (capped) atomicAdd(reinterpret_cast<unsigned long long*>(stats + kStCapped), static_cast<unsigned long long>(capped));
     atomicMax(reinterpret_cast<long long*>(stats + kStMaxFwd), static_cast<long long>(mx));
   }
@@ -984,8 +995,8 @@ __global__ void k_cap_runs(const int2* __restrict__ rows, long long n, long long
     const int next = kb + 1 < m && k + 1 < n ? rows[k + 1].x : -1;
     if (next != a) gend[a] = static_cast<int>(k + 1);
   }
-  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
-  if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(valid, cnt);
+  cnt = block_reduce256(cnt, [](unsigned long long x, unsigned long long y) { return x + y; });
+  if (threadIdx.x == 0 && cnt) atomicAdd(valid, cnt);
 }
 
 // forward degrees from the runs and their total (equal to the valid rows when every read has one run)
@@ -997,8 +1008,8 @@ __global__ void k_cap_runfwd(const int* __restrict__ gstart, const int* __restri
     fwd[x] = f;
     s += static_cast<unsigned long long>(f);
   }
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-  if ((threadIdx.x & 63) == 0 && s) atomicAdd(tot, s);
+  s = block_reduce256(s, [](unsigned long long x, unsigned long long y) { return x + y; });
+  if (threadIdx.x == 0 && s) atomicAdd(tot, s);
 }
 
 // one closure round over the runs: every forward edge (x, y) of a read x that joined last round
@@ -1244,8 +1255,8 @@ __global__ void k_cap_check_shard(const int* __restrict__ T, int nt, const int* 
     if (i < nt && tdest[i] == rank && formed[T[i]] != own[i]) atomicOr(err, kCapErrState);
     if (i < n) mx = max(mx, formed[i]);
   }
-  for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
-  if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<long long*>(stats + kStMaxFwd), static_cast<long long>(mx));
+  mx = block_reduce256(mx, [](int x, int y) { return max(x, y); });
+  if (threadIdx.x == 0) atomicMax(reinterpret_cast<long long*>(stats + kStMaxFwd), static_cast<long long>(mx));
 }
 
 __global__ void k_cap_commit_shard(const int* __restrict__ koff, const int* __restrict__ kflag, long long m,
@@ -1352,6 +1363,8 @@ struct CapWork {
   unsigned* nchg = nullptr;
   int64_t n_chg = 0;
   bool replayed = false;              // fslr_cap_replay_shard ran (changes ready)
+  int* hpin = nullptr;                // pinned host scratch (the plan's per-T arrays)
+  size_t hpin_cap = 0;
 };
 
 void fslr_cap_free(fslr_ctx* c) {
@@ -1361,6 +1374,7 @@ void fslr_cap_free(fslr_ctx* c) {
     if (a.base) (void)hipFree(a.base);
   if (w->temp) (void)hipFree(w->temp);
   if (w->host) (void)hipHostFree(w->host);
+  if (w->hpin) (void)hipHostFree(w->hpin);
   delete w;
   c->capw = nullptr;
 }
@@ -2264,16 +2278,27 @@ extern "C" int fslr_cap_shard_plan(fslr_ctx* c, const int32_t* gathered, int32_t
     if (int rc = cv.commit(c, w->ar[6])) return rc;
   }
   CapTimer tm(s);
+  // pinned host copies of the per-T arrays (pageable copies go through the driver's staging)
+  if (static_cast<size_t>(3 * nt + 3) > w->hpin_cap) {
+    if (w->hpin) (void)hipHostFree(w->hpin);
+    w->hpin = nullptr;
+    w->hpin_cap = 0;
+    const size_t want = static_cast<size_t>(3 * nt + 3) + static_cast<size_t>(nt) / 4 + 1024;
+    HIP_TRY(c, hipHostMalloc(reinterpret_cast<void**>(&w->hpin), want * sizeof(int), hipHostMallocDefault));
+    w->hpin_cap = want;
+  }
+  int* comp = w->hpin;
+  int* cost = comp + nt + 1;
+  int* dest = cost + nt + 1;
   // the components of the T-T hit graph: the union of the ranks' local forests
-  std::vector<int> comp(nt), cost(nt), dest(nt);
   if (nt > 0) {
     HIP_TRY(c, launch_uf_init(w->comp, nt, s));
     HIP_TRY(c, launch_uf_strided(w->comp, gathered, world, nt, 2ll * nt, s));
     HIP_TRY(c, launch_uf_finalize(w->comp, nt, s));
     k_cap_tcost<<<grid_for(nt), 256, 0, s>>>(gathered, world, nt, w->tcost);
     HIP_TRY(c, hipGetLastError());
-    HIP_TRY(c, hipMemcpyAsync(comp.data(), w->comp, static_cast<size_t>(nt) * sizeof(int), hipMemcpyDeviceToHost, s));
-    HIP_TRY(c, hipMemcpyAsync(cost.data(), w->tcost, static_cast<size_t>(nt) * sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipMemcpyAsync(comp, w->comp, static_cast<size_t>(nt) * sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipMemcpyAsync(cost, w->tcost, static_cast<size_t>(nt) * sizeof(int), hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
   }
   // components by cost (its reads' hits, plus one per read), largest first onto the least-loaded
@@ -2297,7 +2322,7 @@ extern "C" int fslr_cap_shard_plan(fslr_ctx* c, const int32_t* gathered, int32_t
   for (int t = 0; t < nt; ++t) dest[t] = droot[comp[t]];
   tm.lap("plan: assign");
   if (nt > 0)
-    HIP_TRY(c, hipMemcpyAsync(w->tdest, dest.data(), static_cast<size_t>(nt) * sizeof(int), hipMemcpyHostToDevice, s));
+    HIP_TRY(c, hipMemcpyAsync(w->tdest, dest, static_cast<size_t>(nt) * sizeof(int), hipMemcpyHostToDevice, s));
   // the T-intervals grouped by destination (stable: T order inside a group), their counts and hits
   HIP_TRY(c, hipMemsetAsync(w->totals, 0, 2 * kMaxDest * sizeof(long long), s));
   HIP_TRY(c, hipMemsetAsync(w->scnt + nti, 0, sizeof(int), s));

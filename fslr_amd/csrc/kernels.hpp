@@ -265,8 +265,9 @@ hipError_t launch_uf_edges(int* parent, const int2* edges, const unsigned long l
 hipError_t launch_uf_pairs(int* parent, const int* src, const int* dst, long long n, int period, hipStream_t s);
 hipError_t launch_uf_finalize(int* parent, int n, hipStream_t s);
 hipError_t launch_uf_pair_list(int* parent, const int2* pairs, long long n, hipStream_t s);
-// (x, parent[x]) for every x of a finalized forest with parent[x] != x, appended at *cnt
-hipError_t launch_forest_pairs(const int* parent, int n, int2* out, unsigned long long* cnt, hipStream_t s);
+// (x, parent[x]) for every x of a finalized forest with parent[x] != x, in x order; *cnt = their count;
+// bcnt: [1024] scratch
+hipError_t launch_forest_pairs(const int* parent, int n, int2* out, unsigned long long* cnt, int* bcnt, hipStream_t s);
 // union of k and vals[w * stride + k] for k < n, w < blocks
 hipError_t launch_uf_strided(int* parent, const int* vals, long long blocks, int n, long long stride, hipStream_t s);
 hipError_t launch_copy_edges(const int2* edges, const unsigned long long* count, long long cap, int2* out,
