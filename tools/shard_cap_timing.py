@@ -152,6 +152,16 @@ def main():
                 ms, _ = timed_once(lambda: ctx[d].sort_edges())
                 sub.setdefault('sort', [[] for _ in range(W)])[d].append(ms)
                 ctx[d].edges_into(rows[d * m:(d + 1) * m], m)
+            if rep == 0 and W > 1:
+                # diagnostics: the rows whose lower read can join the candidates (total E* degree >= the cap)
+                rw = rows.cpu().numpy().view(np.int32).reshape(-1, 2)
+                rw = rw[rw[:, 0] >= 0]
+                deg = np.bincount(rw[:, 0], minlength=n) + np.bincount(rw[:, 1], minlength=n)
+                S = deg >= et
+                out.setdefault('restrict', {})[W] = {'rows': int(rw.shape[0]), 'S': int(S.sum()),
+                                                     'rows_lower_in_S': int(S[rw[:, 0]].sum())}
+                log('restricted gather:', out['restrict'][W])
+                del rw, deg, S
             nts = []
             tinfo = []
             for r in range(W):
