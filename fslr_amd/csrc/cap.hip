@@ -2297,10 +2297,12 @@ extern "C" int fslr_cap_shard_plan(fslr_ctx* c, const int32_t* gathered, int32_t
     HIP_TRY(c, launch_uf_finalize(w->comp, nt, s));
     k_cap_tcost<<<grid_for(nt), 256, 0, s>>>(gathered, world, nt, w->tcost);
     HIP_TRY(c, hipGetLastError());
+    tm.lap("plan: unions");
     HIP_TRY(c, hipMemcpyAsync(comp, w->comp, static_cast<size_t>(nt) * sizeof(int), hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipMemcpyAsync(cost, w->tcost, static_cast<size_t>(nt) * sizeof(int), hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
   }
+  tm.lap("plan: d2h");
   // components by cost (its reads' hits, plus one per read), largest first onto the least-loaded
   // rank (ties: the lower rank) — the same assignment on every rank
   std::vector<int64_t> ccost(nt, 0);
