@@ -4,7 +4,7 @@
 set -e
 OUT=${OUT:-gpurun_out/pmc}
 ENGINE=${ENGINE:-sweep}
-if [ "$ENGINE" = walk ]; then KREGEX="query_kernel"; KNAMES="query_kernel<0, false>"; else KREGEX="k_sweep<2>|k_sweep_pairs|k_bucket_pairs"; KNAMES="k_sweep<2>;k_sweep_pairs;k_bucket_pairs"; fi
+if [ "$ENGINE" = walk ]; then KREGEX="query_kernel"; KNAMES="query_kernel<0, false>"; else KREGEX="k_sweep<2>|k_sweep_pairs|k_bucket_pairs"; KNAMES="k_sweep<2>;k_sweep_pairs"; fi
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $ROOT/$OUT
 cd /tmp && export TMPDIR=/tmp
@@ -21,6 +21,7 @@ H=$(python3 -c "import bench; print(bench.kernel_source_hash('$ENGINE'))")
 rm -f $ROOT/$OUT/traffic.json
 IFS=';' read -ra KS <<< "$KNAMES"
 for K in "${KS[@]}"; do
-  python3 tools/pmc_traffic.py $ROOT/$OUT --kernel "$K" --source-hash $H --merge-into $ROOT/$OUT/traffic.json > /dev/null
+  python3 tools/pmc_traffic.py $ROOT/$OUT --kernel "$K" --source-hash $H --merge-into $ROOT/$OUT/traffic.json > /dev/null \
+    || echo "no rows for $K (not launched by this configuration)"
 done
 echo "traffic summary: $OUT/traffic.json (source $H; kernels: $KNAMES)"
