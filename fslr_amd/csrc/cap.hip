@@ -1077,6 +1077,38 @@ __global__ void k_cap_tcost(const int* __restrict__ gath, int world, int nt, int
   }
 }
 
+// per component (its root = smallest t): its cost (the hits of its reads, plus one per read), and the
+// list of roots with their costs (the host orders them and assigns ranks)
+__global__ void k_cap_ccost(const int* __restrict__ comp, const int* __restrict__ cost, int nt,
+                            unsigned long long* __restrict__ ccost) {
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += gridDim.x * blockDim.x)
+    atomicAdd(ccost + comp[t], static_cast<unsigned long long>(cost[t]) + 1ull);
+}
+
+__global__ void k_cap_roots(const int* __restrict__ comp, const unsigned long long* __restrict__ ccost, int nt,
+                            int2* __restrict__ roots, unsigned* __restrict__ nroots) {
+  const int lane = threadIdx.x & 63;
+  for (int t0 = (blockIdx.x * blockDim.x + threadIdx.x) & ~63; t0 < nt; t0 += gridDim.x * blockDim.x) {
+    const int t = t0 + lane;
+    const bool r = t < nt && comp[t] == t;
+    const unsigned long long m = __ballot(r);
+    if (!m) continue;
+    unsigned base = 0;
+    if (lane == 0) base = atomicAdd(nroots, static_cast<unsigned>(__popcll(m)));
+    base = static_cast<unsigned>(__shfl(static_cast<int>(base), 0));
+    if (r) roots[base + mbcnt(m)] = make_int2(t, static_cast<int>(min(ccost[t], 0x7fffffffull)));
+  }
+}
+
+// every T read's rank: its component root's (dmap holds the roots' ranks)
+__global__ void k_cap_tdest(const int* __restrict__ comp, const int* __restrict__ dmap, int nt, int* __restrict__ tdest) {
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += gridDim.x * blockDim.x) tdest[t] = dmap[comp[t]];
+}
+
+__global__ void k_cap_dmap(const int2* __restrict__ rd, int nr, int* __restrict__ dmap) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nr; i += gridDim.x * blockDim.x) dmap[rd[i].x] = rd[i].y;
+}
+
 // per T-interval: the rank replaying its read's component (sort key), and its index
 __global__ void k_cap_tikey(const int* __restrict__ tread, const int* __restrict__ tdest, int nti,
                             unsigned* __restrict__ key, int* __restrict__ val) {
@@ -1357,6 +1389,10 @@ struct CapWork {
       *shoff = nullptr;
   unsigned *tikey = nullptr, *tikey2 = nullptr;
   long long* totals = nullptr;        // [2 kMaxDest]: T-intervals and hits per destination
+  unsigned long long* ccost = nullptr;
+  int2* roots = nullptr;
+  int* dmap = nullptr;
+  unsigned* nroots = nullptr;
   int64_t nmine = 0, mine_off = 0, planned = 0;
   int2* tdeps = nullptr;
   int *roff = nullptr, *chgl = nullptr;
@@ -2275,56 +2311,63 @@ extern "C" int fslr_cap_shard_plan(fslr_ctx* c, const int32_t* gathered, int32_t
     cv.add(&w->scnt, nti + 1);
     cv.add(&w->shoff, nti + 1);
     cv.add(&w->totals, 2 * kMaxDest);
+    cv.add(&w->ccost, nt);
+    cv.add(&w->roots, nt);
+    cv.add(&w->dmap, nt);
+    cv.add(&w->nroots, 4);
     if (int rc = cv.commit(c, w->ar[6])) return rc;
   }
   CapTimer tm(s);
-  // pinned host copies of the per-T arrays (pageable copies go through the driver's staging)
-  if (static_cast<size_t>(3 * nt + 3) > w->hpin_cap) {
-    if (w->hpin) (void)hipHostFree(w->hpin);
-    w->hpin = nullptr;
-    w->hpin_cap = 0;
-    const size_t want = static_cast<size_t>(3 * nt + 3) + static_cast<size_t>(nt) / 4 + 1024;
-    HIP_TRY(c, hipHostMalloc(reinterpret_cast<void**>(&w->hpin), want * sizeof(int), hipHostMallocDefault));
-    w->hpin_cap = want;
-  }
-  int* comp = w->hpin;
-  int* cost = comp + nt + 1;
-  int* dest = cost + nt + 1;
-  // the components of the T-T hit graph: the union of the ranks' local forests
+  // the components of the T-T hit graph: the union of the ranks' local forests; each component's cost
+  // and the list of roots, on the device
+  unsigned nr = 0;
   if (nt > 0) {
     HIP_TRY(c, launch_uf_init(w->comp, nt, s));
     HIP_TRY(c, launch_uf_strided(w->comp, gathered, world, nt, 2ll * nt, s));
     HIP_TRY(c, launch_uf_finalize(w->comp, nt, s));
     k_cap_tcost<<<grid_for(nt), 256, 0, s>>>(gathered, world, nt, w->tcost);
+    HIP_TRY(c, hipMemsetAsync(w->ccost, 0, static_cast<size_t>(nt) * sizeof(unsigned long long), s));
+    HIP_TRY(c, hipMemsetAsync(w->nroots, 0, sizeof(unsigned), s));
+    k_cap_ccost<<<grid_for(nt), 256, 0, s>>>(w->comp, w->tcost, nt, w->ccost);
+    k_cap_roots<<<grid_for(nt), 256, 0, s>>>(w->comp, w->ccost, nt, w->roots, w->nroots);
     HIP_TRY(c, hipGetLastError());
-    tm.lap("plan: unions");
-    HIP_TRY(c, hipMemcpyAsync(comp, w->comp, static_cast<size_t>(nt) * sizeof(int), hipMemcpyDeviceToHost, s));
-    HIP_TRY(c, hipMemcpyAsync(cost, w->tcost, static_cast<size_t>(nt) * sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipMemcpyAsync(&nr, w->nroots, sizeof(nr), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+  }
+  tm.lap("plan: unions");
+  // pinned host copy of the roots (pageable copies go through the driver's staging)
+  if (static_cast<size_t>(2 * nr + 2) > w->hpin_cap) {
+    if (w->hpin) (void)hipHostFree(w->hpin);
+    w->hpin = nullptr;
+    w->hpin_cap = 0;
+    const size_t want = static_cast<size_t>(2 * nr + 2) + nr / 4 + 1024;
+    HIP_TRY(c, hipHostMalloc(reinterpret_cast<void**>(&w->hpin), want * sizeof(int), hipHostMallocDefault));
+    w->hpin_cap = want;
+  }
+  int2* rh = reinterpret_cast<int2*>(w->hpin);
+  if (nr) {
+    HIP_TRY(c, hipMemcpyAsync(rh, w->roots, static_cast<size_t>(nr) * sizeof(int2), hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
   }
   tm.lap("plan: d2h");
-  // components by cost (its reads' hits, plus one per read), largest first onto the least-loaded
-  // rank (ties: the lower rank) — the same assignment on every rank
-  std::vector<int64_t> ccost(nt, 0);
-  std::vector<int> roots;
-  for (int t = 0; t < nt; ++t) {
-    ccost[comp[t]] += static_cast<int64_t>(cost[t]) + 1;
-    if (comp[t] == t) roots.push_back(t);
-  }
-  std::sort(roots.begin(), roots.end(), [&](int a, int b) { return ccost[a] != ccost[b] ? ccost[a] > ccost[b] : a < b; });
-  std::vector<int64_t> load(world, 0);
-  std::vector<int> droot(nt, 0);
-  for (int r : roots) {
+  // components largest first (ties: the smaller root) onto the least-loaded rank (ties: the lower
+  // rank) — the same assignment on every rank
+  std::sort(rh, rh + nr, [](const int2& a, const int2& b) { return a.y != b.y ? a.y > b.y : a.x < b.x; });
+  int64_t load[kMaxDest] = {};
+  for (unsigned k = 0; k < nr; ++k) {
     int d = 0;
-    for (int k = 1; k < world; ++k)
-      if (load[k] < load[d]) d = k;
-    droot[r] = d;
-    load[d] += ccost[r];
+    for (int q = 1; q < world; ++q)
+      if (load[q] < load[d]) d = q;
+    load[d] += rh[k].y;
+    rh[k].y = d;
   }
-  for (int t = 0; t < nt; ++t) dest[t] = droot[comp[t]];
   tm.lap("plan: assign");
-  if (nt > 0)
-    HIP_TRY(c, hipMemcpyAsync(w->tdest, dest, static_cast<size_t>(nt) * sizeof(int), hipMemcpyHostToDevice, s));
+  if (nr) {
+    HIP_TRY(c, hipMemcpyAsync(w->roots, rh, static_cast<size_t>(nr) * sizeof(int2), hipMemcpyHostToDevice, s));
+    k_cap_dmap<<<grid_for(nr), 256, 0, s>>>(w->roots, static_cast<int>(nr), w->dmap);
+    k_cap_tdest<<<grid_for(nt), 256, 0, s>>>(w->comp, w->dmap, nt, w->tdest);
+    HIP_TRY(c, hipGetLastError());
+  }
   // the T-intervals grouped by destination (stable: T order inside a group), their counts and hits
   HIP_TRY(c, hipMemsetAsync(w->totals, 0, 2 * kMaxDest * sizeof(long long), s));
   HIP_TRY(c, hipMemsetAsync(w->scnt + nti, 0, sizeof(int), s));
