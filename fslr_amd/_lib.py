@@ -13,7 +13,7 @@ import numpy as np
 
 LIB_PATH = os.environ.get('FSLR_LIB') or os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libfslr_hip.so')
 
-ABI_VERSION = 13         # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
+ABI_VERSION = 14         # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
 FSLR_OK, FSLR_ERR_ZERO_DIVISION, FSLR_ERR_INVALID, FSLR_ERR_HIP, FSLR_ERR_NOMEM, FSLR_ERR_STATE = range(6)
 FSLR_MAX_L = 64
 FSLR_MAX_READS = 1 << 25
@@ -39,7 +39,8 @@ EXPORTED = ['fslr_abi_version', 'fslr_last_error', 'fslr_ctx_create', 'fslr_ctx_
             'fslr_cap_replay_pairs', 'fslr_source_hash', 'fslr_set_reads_any', 'fslr_set_long_cutoffs',
             'fslr_cap_install_pairs', 'fslr_cap_sizes', 'fslr_cap_dep_local', 'fslr_cap_shard_plan',
             'fslr_cap_shard_pack', 'fslr_cap_replay_shard', 'fslr_cap_copy_changes', 'fslr_cap_apply_changes',
-            'fslr_local_forest', 'fslr_copy_forest_pairs', 'fslr_sort_edges']
+            'fslr_local_forest', 'fslr_copy_forest_pairs', 'fslr_sort_edges', 'fslr_cap_bwd_counts',
+            'fslr_cap_restrict', 'fslr_cap_copy_restricted', 'fslr_cap_install_restricted']
 
 
 class HipUnavailable(RuntimeError):
@@ -169,6 +170,10 @@ def load(path: str = LIB_PATH):
         'fslr_cap_replay_shard': (ctypes.c_int, [vp, vp, vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(CapStats)]),
         'fslr_cap_copy_changes': (ctypes.c_int, [vp, vp, i64]),
         'fslr_cap_apply_changes': (ctypes.c_int, [vp, vp, i64, ctypes.POINTER(CapStats)]),
+        'fslr_cap_bwd_counts': (ctypes.c_int, [vp, i32, vp, i32]),
+        'fslr_cap_restrict': (ctypes.c_int, [vp, vp, i32, ctypes.POINTER(ctypes.c_int64)]),
+        'fslr_cap_copy_restricted': (ctypes.c_int, [vp, vp, i64]),
+        'fslr_cap_install_restricted': (ctypes.c_int, [vp, vp, i64, i32, i32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -459,6 +464,26 @@ class Context:
     def cap_install_pairs(self, t, n_rows: int, world: int, rank: int):
         """The gathered E* (a, b) int32 rows (device tensor; a < 0 = padding), rank w's block at w m."""
         self._check(self._L.fslr_cap_install_pairs(self._h, self._dp(t, n_rows), int(n_rows), int(world), int(rank)))
+
+    def cap_bwd_counts(self, edge_threshold: int, t):
+        """This rank's edge counts per upper read into device tensor ``t`` (uint8: clipped at the
+        threshold, or int32), for the sum over ranks."""
+        eb = t.element_size()
+        self._check(self._L.fslr_cap_bwd_counts(self._h, int(edge_threshold), ctypes.c_void_p(t.data_ptr()), eb))
+
+    def cap_restrict(self, t) -> int:
+        """The rows of S from the summed counts ``t``; their count (one sync)."""
+        k = ctypes.c_int64()
+        self._check(self._L.fslr_cap_restrict(self._h, ctypes.c_void_p(t.data_ptr()), t.element_size(),
+                                              ctypes.byref(k)))
+        return int(k.value)
+
+    def cap_copy_restricted(self, t, n_pad: int):
+        self._check(self._L.fslr_cap_copy_restricted(self._h, self._dp(t, n_pad), int(n_pad)))
+
+    def cap_install_restricted(self, t, n_rows: int, world: int, rank: int):
+        self._check(self._L.fslr_cap_install_restricted(self._h, self._dp(t, n_rows), int(n_rows), int(world),
+                                                        int(rank)))
 
     def cap_sizes(self):
         """(|T|, T-intervals, local hits) after cap_local."""

@@ -1306,6 +1306,61 @@ __global__ void k_cap_commit_shard(const int* __restrict__ koff, const int* __re
   host[kHErr] = *err;
 }
 
+// ---- the restricted gather -----------------------------------------------------------------------
+// A read x joins the closure T only when fwd(x) + back(x) >= thr with back(x) <= bwd(x) over E*, and
+// only rows whose lower read is in T are walked by the closure, break a loop or change: the rows
+// of S = {x : fwd(x) + bwd(x) >= thr} suffice (3% of E* at cfg5).  Each rank holds every forward row
+// of the reads it owns (the partition routes a pair to its lower read's owner); bwd is a sum over
+// ranks of counts clipped at thr (the test fwd + sum >= thr is unchanged by the clip).
+__global__ void k_cap_degs(const int2* __restrict__ e, long long ne, int* __restrict__ fwd, int* __restrict__ bwd) {
+  for (long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; i < ne;
+       i += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const int2 v = e[i];
+    atomicAdd(fwd + v.x, 1);
+    atomicAdd(bwd + v.y, 1);
+  }
+}
+
+__global__ void k_cap_clip8(const int* __restrict__ cnt, int n, int thr, unsigned char* __restrict__ out) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    out[i] = static_cast<unsigned char>(min(cnt[i], thr));
+}
+
+__global__ void k_cap_rflags(const int2* __restrict__ e, long long ne, const int* __restrict__ fwd,
+                             const void* __restrict__ bwd, int eb, int thr, int* __restrict__ flag) {
+  for (long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; i < ne;
+       i += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const int a = e[i].x;
+    const int b = eb == 1 ? static_cast<int>(static_cast<const unsigned char*>(bwd)[a]) : static_cast<const int*>(bwd)[a];
+    flag[i] = fwd[a] + b >= thr;
+  }
+}
+
+__global__ void k_cap_rcompact(const int2* __restrict__ e, long long ne, const int* __restrict__ flag,
+                               const int* __restrict__ off, int2* __restrict__ rows, int* __restrict__ rmap) {
+  for (long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; i < ne;
+       i += static_cast<long long>(gridDim.x) * blockDim.x) {
+    if (!flag[i]) continue;
+    rows[off[i]] = e[i];
+    rmap[off[i]] = static_cast<int>(i);
+  }
+}
+
+// this rank's block of the restricted rows: who back onto its local edges
+__global__ void k_cap_rwho(const unsigned char* __restrict__ gwho, const int* __restrict__ rmap, long long nr,
+                           unsigned char* __restrict__ lwho) {
+  for (long long j = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; j < nr;
+       j += static_cast<long long>(gridDim.x) * blockDim.x)
+    lwho[rmap[j]] = gwho[j];
+}
+
+// reads with no gathered forward row (outside S, or none at all): their own forward edges, held here
+__global__ void k_cap_addfwd(int* __restrict__ formed, const int* __restrict__ gfwd, const int* __restrict__ rfwd,
+                             int n) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    if (gfwd[i] == 0) formed[i] += rfwd[i];
+}
+
 __global__ void k_fill(int* __restrict__ p, int n, int v) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) p[i] = v;
 }
@@ -1333,10 +1388,11 @@ struct CapArena {
 };
 
 struct CapWork {
-  CapArena ar[10];                     // 0: per read / per edge, 1: per T read / T-interval, 2: per hit (scratch),
+  CapArena ar[11];                     // 0: per read / per edge, 1: per T read / T-interval, 2: per hit (scratch),
                                       // 3: multi-GPU offsets, 4: the visit sequence; the sharded replay:
                                       // 5: gathered rows, 6: plan (per T read / T-interval), 7: T-T pairs,
-                                      // 8: received offsets and changes, 9: edge sort scratch
+                                      // 8: received offsets and changes, 9: edge sort scratch,
+                                      // 10: the restricted gather (per local edge / read)
   void* temp = nullptr;
   size_t temp_bytes = 0;
   long long* host = nullptr;          // pinned, device-mapped
@@ -1401,6 +1457,16 @@ struct CapWork {
   bool replayed = false;              // fslr_cap_replay_shard ran (changes ready)
   int* hpin = nullptr;                // pinned host scratch (the plan's per-T arrays)
   size_t hpin_cap = 0;
+  // the restricted gather (fslr_cap_bwd_counts, fslr_cap_restrict, fslr_cap_install_restricted):
+  // local forward counts, the local backward counts (before the sum over ranks), kept flags and
+  // offsets of the local edges, the kept rows and their local edge index, local who
+  int *rfwd = nullptr, *rcnt = nullptr, *rflag = nullptr, *rkoff = nullptr, *rmap = nullptr;
+  int2* rrows = nullptr;
+  unsigned short* roiu = nullptr;
+  unsigned char* lwho = nullptr;
+  int64_t r_ne = 0, r_n = 0;
+  int r_thr = 0;
+  bool r_counted = false, r_ready = false, g_restricted = false;
 };
 
 void fslr_cap_free(fslr_ctx* c) {
@@ -2196,7 +2262,8 @@ extern "C" int fslr_cap_replay_pairs(fslr_ctx* c, int32_t thr, const int32_t* a,
 }
 
 // ---- the sharded replay (multi-GPU): host side ---------------------------------------------------
-extern "C" int fslr_cap_install_pairs(fslr_ctx* c, const int32_t* pairs, int64_t n_rows, int32_t world, int32_t rank) {
+namespace {
+int cap_install(fslr_ctx* c, const int32_t* pairs, int64_t n_rows, int32_t world, int32_t rank, bool restricted) {
   if (!c || (!pairs && n_rows) || n_rows < 0 || world < 1 || world > kMaxDest || rank < 0 || rank >= world ||
       n_rows % world)
     return FSLR_ERR_INVALID;
@@ -2248,10 +2315,112 @@ extern "C" int fslr_cap_install_pairs(fslr_ctx* c, const int32_t* pairs, int64_t
   w->prepared = false;
   w->planned = 0;
   w->replayed = false;
+  w->g_restricted = restricted;
   c->cap_gmode = true;
   c->edges_global = false;
   std::memset(&c->cap_stats, 0, sizeof(c->cap_stats));
   return FSLR_OK;
+}
+}  // namespace
+
+extern "C" int fslr_cap_install_pairs(fslr_ctx* c, const int32_t* pairs, int64_t n_rows, int32_t world, int32_t rank) {
+  if (c && c->capw) c->capw->r_ready = c->capw->r_counted = false;
+  return cap_install(c, pairs, n_rows, world, rank, false);
+}
+
+extern "C" int fslr_cap_bwd_counts(fslr_ctx* c, int32_t thr, void* out, int32_t elem_bytes) {
+  if (!c || !out || (elem_bytes != 1 && elem_bytes != 4) || thr < 1 || (elem_bytes == 1 && thr > 255))
+    return FSLR_ERR_INVALID;
+  if (!c->reads_set) return fail(c, FSLR_ERR_STATE, "fslr_set_reads first");
+  if (c->lg_set) return fail(c, FSLR_ERR_STATE, "the sharded edge cap takes reads of at most FSLR_MAX_L intervals");
+  if (!c->counters) return fail(c, FSLR_ERR_STATE, "no query has run");
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  long long pk[3] = {0, 0, 0};
+  if (int rc = peek_counts(c, pk)) return rc;
+  const int64_t ne = std::min<int64_t>(pk[0], c->edge_cap), n = c->n;
+  if (ne >= (int64_t(1) << 31)) return fail(c, FSLR_ERR_INVALID, "too many edges for the restricted gather");
+  CapWork* w = nullptr;
+  if (int rc = cap_work(c, &w)) return rc;
+  {
+    Carve cv;
+    cv.add(&w->rfwd, n);
+    cv.add(&w->rcnt, n);
+    cv.add(&w->rflag, ne);
+    cv.add(&w->rkoff, ne);
+    cv.add(&w->rmap, ne);
+    cv.add(&w->rrows, ne);
+    cv.add(&w->roiu, ne);
+    cv.add(&w->lwho, ne);
+    if (int rc = cv.commit(c, w->ar[10])) return rc;
+  }
+  int* bcnt = elem_bytes == 4 ? static_cast<int*>(out) : w->rcnt;
+  HIP_TRY(c, hipMemsetAsync(w->rfwd, 0, static_cast<size_t>(std::max<int64_t>(n, 1)) * sizeof(int), s));
+  HIP_TRY(c, hipMemsetAsync(bcnt, 0, static_cast<size_t>(std::max<int64_t>(n, 1)) * sizeof(int), s));
+  if (ne > 0) k_cap_degs<<<grid_for(ne), 256, 0, s>>>(c->edges, ne, w->rfwd, bcnt);
+  if (elem_bytes == 1 && n > 0)
+    k_cap_clip8<<<grid_for(n), 256, 0, s>>>(w->rcnt, static_cast<int>(n), thr, static_cast<unsigned char*>(out));
+  HIP_TRY(c, hipGetLastError());
+  w->r_ne = ne;
+  w->r_thr = thr;
+  w->r_counted = true;
+  w->r_ready = false;
+  return FSLR_OK;
+}
+
+extern "C" int fslr_cap_restrict(fslr_ctx* c, const void* bwd, int32_t elem_bytes, int64_t* n_rows) {
+  if (!c || !bwd || !n_rows || (elem_bytes != 1 && elem_bytes != 4)) return FSLR_ERR_INVALID;
+  *n_rows = 0;
+  CapWork* w = c->capw;
+  if (!w || !w->r_counted) return fail(c, FSLR_ERR_STATE, "fslr_cap_bwd_counts first");
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  const int64_t ne = w->r_ne;
+  int64_t kept = 0;
+  if (ne > 0) {
+    k_cap_rflags<<<grid_for(ne), 256, 0, s>>>(c->edges, ne, w->rfwd, bwd, elem_bytes, w->r_thr, w->rflag);
+    size_t tb = 0;
+    HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tb, w->rflag, w->rkoff, static_cast<int>(ne), s));
+    if (int rc = ensure_temp(c, w, tb)) return rc;
+    tb = w->temp_bytes;
+    HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(w->temp, tb, w->rflag, w->rkoff, static_cast<int>(ne), s));
+    k_cap_rcompact<<<grid_for(ne), 256, 0, s>>>(c->edges, ne, w->rflag, w->rkoff, w->rrows, w->rmap);
+    HIP_TRY(c, hipGetLastError());
+    int last[2] = {0, 0};
+    HIP_TRY(c, hipMemcpyAsync(last, w->rkoff + ne - 1, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipMemcpyAsync(last + 1, w->rflag + ne - 1, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    kept = static_cast<int64_t>(last[0]) + last[1];
+  }
+  w->r_n = kept;
+  w->r_ready = true;
+  *n_rows = kept;
+  return FSLR_OK;
+}
+
+extern "C" int fslr_cap_copy_restricted(fslr_ctx* c, int32_t* dst, int64_t n_pad) {
+  if (!c || n_pad < 0 || (!dst && n_pad)) return FSLR_ERR_INVALID;
+  CapWork* w = c->capw;
+  if (!w || !w->r_ready) return fail(c, FSLR_ERR_STATE, "fslr_cap_restrict first");
+  if (n_pad < w->r_n) return fail(c, FSLR_ERR_INVALID, "n_pad below this rank's restricted row count");
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  if (w->r_n)
+    HIP_TRY(c, hipMemcpyAsync(dst, w->rrows, static_cast<size_t>(w->r_n) * sizeof(int2), hipMemcpyDeviceToDevice, s));
+  if (n_pad > w->r_n) {
+    k_fill<<<grid_for(2 * (n_pad - w->r_n)), 256, 0, s>>>(dst + 2 * w->r_n, static_cast<int>(2 * (n_pad - w->r_n)), -1);
+    HIP_TRY(c, hipGetLastError());
+  }
+  return FSLR_OK;
+}
+
+extern "C" int fslr_cap_install_restricted(fslr_ctx* c, const int32_t* pairs, int64_t n_rows, int32_t world,
+                                           int32_t rank) {
+  if (!c || world < 1 || n_rows < 0 || n_rows % world) return FSLR_ERR_INVALID;
+  CapWork* w = c->capw;
+  if (!w || !w->r_ready) return fail(c, FSLR_ERR_STATE, "fslr_cap_restrict first");
+  if (n_rows / world < w->r_n) return fail(c, FSLR_ERR_INVALID, "the blocks are smaller than this rank's restricted rows");
+  return cap_install(c, pairs, n_rows, world, rank, true);
 }
 
 extern "C" int fslr_cap_sizes(fslr_ctx* c, int64_t* n_t, int64_t* n_ti, int64_t* n_hits) {
@@ -2547,35 +2716,49 @@ extern "C" int fslr_cap_apply_changes(fslr_ctx* c, const int32_t* changes, int64
     HIP_TRY(c, hipGetLastError());
   }
   tm.lap("apply: changes");
-  // this rank's own edges (block g_rank of the rows): kept ones compacted and re-oriented, their formers
-  const int2* blk = w->grows + w->g_rank * m;
-  const unsigned char* wblk = w->gwho + w->g_rank * m;
+  // this rank's own edges (block g_rank of the rows: all of them, or with the restricted gather its
+  // rows of S mapped back onto its edges): kept ones compacted and re-oriented, their formers
+  const bool rs = w->g_restricted;
+  const int2* blk = rs ? c->edges : w->grows + w->g_rank * m;
+  const unsigned char* wblk = rs ? w->lwho : w->gwho + w->g_rank * m;
+  int *kflag = rs ? w->rflag : w->kflag, *koff = rs ? w->rkoff : w->koff;
+  int2* oedges = rs ? w->rrows : w->oedges;
+  unsigned short* oiu = rs ? w->roiu : w->oiu;
+  const int64_t mown = rs ? w->r_ne : mloc;
+  if (rs) {
+    // the maximum then covers S and this rank's reads outside S (the caller's MAX over ranks)
+    if (mown) HIP_TRY(c, hipMemsetAsync(w->lwho, 0, static_cast<size_t>(mown), s));
+    if (w->r_n) k_cap_rwho<<<grid_for(w->r_n), 256, 0, s>>>(w->gwho + w->g_rank * m, w->rmap, w->r_n, w->lwho);
+    if (nr) k_cap_addfwd<<<grid_for(nr), 256, 0, s>>>(w->formed, w->gfwd, w->rfwd, static_cast<int>(nr));
+    HIP_TRY(c, hipGetLastError());
+  }
   HIP_TRY(c, hipMemsetAsync(c->fwd, 0, static_cast<size_t>(nr) * sizeof(int), s));
-  if (mloc > 0) {
-    k_cap_local_flags<<<grid_for(mloc), 256, 0, s>>>(blk, wblk, mloc, w->kflag);
+  if (mown > 0) {
+    k_cap_local_flags<<<grid_for(mown), 256, 0, s>>>(blk, wblk, mown, kflag);
     size_t tb = 0;
-    HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tb, w->kflag, w->koff, static_cast<int>(mloc), s));
+    HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tb, kflag, koff, static_cast<int>(mown), s));
     if (int rc = ensure_temp(c, w, tb)) return rc;
     tb = w->temp_bytes;
-    HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(w->temp, tb, w->kflag, w->koff, static_cast<int>(mloc), s));
-    k_cap_local_compact<<<grid_for(mloc), 256, 0, s>>>(c->edges, c->edge_iu, mloc, w->kflag, w->koff, wblk, w->oedges,
-                                                       w->oiu, c->fwd);
+    HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(w->temp, tb, kflag, koff, static_cast<int>(mown), s));
+    k_cap_local_compact<<<grid_for(mown), 256, 0, s>>>(c->edges, c->edge_iu, mown, kflag, koff, wblk, oedges, oiu,
+                                                       c->fwd);
     HIP_TRY(c, hipGetLastError());
-    HIP_TRY(c, hipMemcpyAsync(c->edges, w->oedges, static_cast<size_t>(mloc) * sizeof(int2), hipMemcpyDeviceToDevice, s));
-    HIP_TRY(c, hipMemcpyAsync(c->edge_iu, w->oiu, static_cast<size_t>(mloc) * sizeof(unsigned short),
+    HIP_TRY(c, hipMemcpyAsync(c->edges, oedges, static_cast<size_t>(mown) * sizeof(int2), hipMemcpyDeviceToDevice, s));
+    HIP_TRY(c, hipMemcpyAsync(c->edge_iu, oiu, static_cast<size_t>(mown) * sizeof(unsigned short),
                               hipMemcpyDeviceToDevice, s));
   }
   tm.lap("apply: local");
   k_cap_check_shard<<<grid_for(std::max<int64_t>(nr, nt)), 256, 0, s>>>(w->T, nt, w->tdest, w->g_rank, w->own, w->formed,
                                                                        static_cast<int>(nr), w->stats, w->err);
   HIP_TRY(c, hipGetLastError());
-  k_cap_commit_shard<<<1, 64, 0, s>>>(w->koff, w->kflag, mloc, c->counters, c->errw, w->stats, w->err, w->host_dev);
+  k_cap_commit_shard<<<1, 64, 0, s>>>(koff, kflag, mown, c->counters, c->errw, w->stats, w->err, w->host_dev);
   HIP_TRY(c, hipGetLastError());
   HIP_TRY(c, hipStreamSynchronize(s));
   const long long err = host_word(w, kHErr);
   w->prepared = false;
   w->planned = 0;
   w->replayed = false;
+  w->g_restricted = w->r_ready = w->r_counted = false;
   c->cap_gmode = false;
   if (err & kCapErrState) return fail(c, FSLR_ERR_STATE, "sharded edge cap: a replayed loop's edge count differs");
   fslr_cap_stats cs;

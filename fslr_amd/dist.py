@@ -29,6 +29,8 @@ all found by the shard that owns it); they are summed only for reporting.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 
 
@@ -164,7 +166,13 @@ class TorchComm:
 
     def all_reduce(self, t, op='max'):
         import torch.distributed as dist
-        dist.all_reduce(t, op=dist.ReduceOp.MAX if op == 'max' else dist.ReduceOp.MIN)
+        rop = {'max': dist.ReduceOp.MAX, 'min': dist.ReduceOp.MIN, 'sum': dist.ReduceOp.SUM}[op]
+        if self.gloo and t.device.type != 'cpu':
+            o = t.cpu()
+            dist.all_reduce(o, op=rop)
+            t.copy_(o)
+        else:
+            dist.all_reduce(t, op=rop)
 
 
 class LocalHub:
@@ -231,7 +239,10 @@ class LocalComm:
         import torch
         got = self._publish(t.clone())
         st = torch.stack([g.to(t.device) for g in got])
-        t.copy_(st.max(dim=0).values if op == 'max' else st.min(dim=0).values)
+        if op == 'sum':
+            t.copy_(st.sum(dim=0).to(t.dtype))
+        else:
+            t.copy_(st.max(dim=0).values if op == 'max' else st.min(dim=0).values)
         self._done()
 
 
@@ -493,12 +504,45 @@ class SweepShard:
         err = None
         self.esend = self._grow(self.esend, m)
         self.egath = self._grow(self.egath, W * m)
+        restricted = os.environ.get('FSLR_CAP_GATHER', 'restricted') != 'full'
         try:
             ctx.sort_edges()                     # each read's forward rows one run of the gathered rows
+            if restricted:
+                # only the rows of S = {x : fwd(x) + bwd(x) >= threshold} travel (bwd summed over ranks)
+                dt = (torch.uint8 if W * edge_threshold <= 255 and os.environ.get('FSLR_CAP_BWD') != 'i32'
+                      else torch.int32)
+                if getattr(self, 'bwd', None) is None or self.bwd.dtype != dt or self.bwd.numel() < self.n:
+                    self.bwd = torch.empty(max(1, self.n), dtype=dt, device=self.device)
+                ctx.cap_bwd_counts(edge_threshold, self.bwd)
         except Exception as e:                   # noqa: BLE001 - re-raised on every rank
             err = e
         self._agree(err)
-        ctx.edges_into(self.esend, m)
+        if restricted:
+            if W > 1:
+                self.comm.all_reduce(self.bwd[:self.n], 'sum')
+            nr = 0
+            try:
+                nr = ctx.cap_restrict(self.bwd)
+            except Exception as e:               # noqa: BLE001
+                err = e
+            code = 0 if err is None else (1 if isinstance(err, ZeroDivisionError) else 2)
+            if W > 1:
+                t = self.comm.small([code, nr])
+                self.comm.all_reduce(t, 'max')
+                code, m = (int(x) for x in t.tolist())
+            else:
+                m = nr
+            if err is not None:
+                raise err
+            if code:
+                from ._lib import FslrError
+                raise FslrError('error on another rank')
+            m = max(1, m)
+            self.esend = self._grow(self.esend, m)
+            self.egath = self._grow(self.egath, W * m)
+            ctx.cap_copy_restricted(self.esend, m)
+        else:
+            ctx.edges_into(self.esend, m)
         if W > 1:
             self._all_gather(self.egath[:W * m], self.esend[:m])
             rows = self.egath
@@ -506,7 +550,10 @@ class SweepShard:
             rows = self.esend
         nt = 0
         try:
-            ctx.cap_install_pairs(rows, W * m, W, r)
+            if restricted:
+                ctx.cap_install_restricted(rows, W * m, W, r)
+            else:
+                ctx.cap_install_pairs(rows, W * m, W, r)
             ctx.cap_local(edge_threshold)
             nt = ctx.cap_sizes()[0]
             self.tinfo = self._grow32(getattr(self, 'tinfo', None), max(1, 2 * nt))
@@ -586,9 +633,12 @@ class SweepShard:
             err = e
         if W > 1:
             code = 0 if err is None else (1 if isinstance(err, ZeroDivisionError) else 2)
-            t = self.comm.small([code, fp])
+            # the restricted gather's max_fwd is this rank's part (S and its own reads outside S)
+            t = self.comm.small([code, fp, int(cap.get('max_fwd', 0))])
             self.comm.all_reduce(t, 'max')
-            code, fp = (int(x) for x in t.tolist())
+            code, fp, mf = (int(x) for x in t.tolist())
+            if cap:
+                cap['max_fwd'] = mf
             if err is None and code:
                 from ._lib import FslrError
                 err = ZeroDivisionError('division by zero') if code == 1 else FslrError('error on another rank')

@@ -36,7 +36,8 @@
  *                         E* edge but indexes only its chromosomes (multi-GPU)
  *   fslr_cap_install_pairs, fslr_cap_sizes, fslr_cap_dep_local, fslr_cap_shard_plan,
  *   fslr_cap_shard_pack, fslr_cap_replay_shard, fslr_cap_copy_changes,
- *   fslr_cap_apply_changes
+ *   fslr_cap_apply_changes, fslr_cap_bwd_counts, fslr_cap_restrict, fslr_cap_copy_restricted,
+ *   fslr_cap_install_restricted
  *                         cluster.py:197-224 the same loops sharded over the ranks by the components of
  *                         the candidates' hit graph (multi-GPU)
  *   fslr_set_long_reads,
@@ -74,7 +75,7 @@
 extern "C" {
 #endif
 
-#define FSLR_ABI_VERSION 13
+#define FSLR_ABI_VERSION 14
 #define FSLR_MAX_L 64                /* max intervals per read (bitmask width) */
 #define FSLR_MAX_READS (1 << 25)     /* read rank packs into bits 6..30 of the index record */
 #define FSLR_THR_ZERO_ALN INT32_MIN
@@ -298,7 +299,19 @@ int  fslr_cap_replay(fslr_ctx *ctx, const int32_t *counts, const int32_t *hits, 
  *   (former, partner)) and their formers' counts (fwd), errw max_fwd = the largest edges-per-loop;
  *   the components of the capped graph then come from the ranks' local forests (fslr_local_forest).
  *   Syncs; out: applied, max_fwd, candidates, dropped, backward (capped / hits / pairs: the sum of the
- *   ranks' parts). */
+ *   ranks' parts).
+ * The restricted gather: only rows whose lower read x has fwd(x) + bwd(x) >= edge_threshold over E* can
+ * take part (the closure's join test, cluster.py:210-213 via DESIGN.md §11), about 3% of E* at cfg5.
+ * fslr_cap_bwd_counts: after fslr_sort_edges, this rank's counts of its edges per upper read b into out
+ *   (device, n_reads elements of elem_bytes: 1 = uint8 clipped at edge_threshold <= 255, 4 = int32;
+ *   async); the caller sums them over the ranks (all_reduce; uint8 needs world x threshold <= 255).
+ * fslr_cap_restrict: from the summed counts, this rank's rows of S (its edges whose lower read has
+ *   fwd + bwd >= threshold, in edge order); *n_rows = their count (syncs).
+ * fslr_cap_copy_restricted: those rows as int32 (a, b) pairs padded with -1 to n_pad (device, async).
+ * fslr_cap_install_restricted: the ranks' gathered restricted rows, as fslr_cap_install_pairs (the rest
+ *   of the sequence is unchanged); fslr_cap_apply_changes then maps this rank's block back onto its
+ *   edges and its max_fwd covers S and this rank's reads outside S: the MAX over ranks is the capped
+ *   graph's. */
 /* The multi-GPU merge by local forests (get_subgraphs, cluster.py:230-234, over the union of the ranks'
  * edges).  fslr_local_forest: union-find over this context's edges; the (read, root) pairs of the
  * reads that are not their own root are kept (the same partition as the edges, in fewer pairs);
@@ -320,6 +333,10 @@ int  fslr_cap_replay_shard(fslr_ctx *ctx, const int32_t *counts, const int32_t *
                            fslr_cap_stats *part);
 int  fslr_cap_copy_changes(fslr_ctx *ctx, int32_t *dst, int64_t n_pad);
 int  fslr_cap_apply_changes(fslr_ctx *ctx, const int32_t *changes, int64_t n, fslr_cap_stats *out);
+int  fslr_cap_bwd_counts(fslr_ctx *ctx, int32_t edge_threshold, void *out, int32_t elem_bytes);
+int  fslr_cap_restrict(fslr_ctx *ctx, const void *bwd, int32_t elem_bytes, int64_t *n_rows);
+int  fslr_cap_copy_restricted(fslr_ctx *ctx, int32_t *dst, int64_t n_pad);
+int  fslr_cap_install_restricted(fslr_ctx *ctx, const int32_t *pairs, int64_t n_rows, int32_t world, int32_t rank);
 int  fslr_sweep_partition(fslr_ctx *ctx, const fslr_params *params, int32_t n_dest, int32_t block_shift,
                           void *dst, int64_t dst_cap, int64_t *counts);
 int  fslr_sweep_evaluate(fslr_ctx *ctx, const fslr_params *params, const void *entries, int64_t n);

@@ -305,7 +305,34 @@ class EmuSweepContext:
         if len(self._edges):
             self._edges = self._edges[np.lexsort((self._edges[:, 1], self._edges[:, 0]))]
 
+    def cap_bwd_counts(self, edge_threshold, t):
+        import torch
+        e = self._edges
+        self._r_thr = int(edge_threshold)
+        self._rfwd = np.bincount(e[:, 0], minlength=self.n_reads) if len(e) else np.zeros(self.n_reads, np.int64)
+        b = np.bincount(e[:, 1], minlength=self.n_reads) if len(e) else np.zeros(self.n_reads, np.int64)
+        if t.dtype == torch.uint8:
+            b = np.minimum(b, edge_threshold)
+        t.numpy()[:self.n_reads] = b
+
+    def cap_restrict(self, t):
+        bwd = t.numpy()[:self.n_reads].astype(np.int64)
+        e = self._edges
+        keep = (self._rfwd[e[:, 0]] + bwd[e[:, 0]] >= self._r_thr) if len(e) else np.zeros(0, bool)
+        self._rmap = np.flatnonzero(keep)
+        return int(self._rmap.size)
+
+    def cap_copy_restricted(self, t, n_pad):
+        pairs = np.full((n_pad, 2), -1, dtype=np.int32)
+        pairs[:self._rmap.size] = self._edges[self._rmap, :2]
+        t.numpy()[:n_pad] = pairs.view(np.int64)[:, 0]
+
+    def cap_install_restricted(self, t, n_rows, world, rank):
+        self.cap_install_pairs(t, n_rows, world, rank)
+        self._restricted = True
+
     def cap_install_pairs(self, t, n_rows, world, rank):
+        self._restricted = False
         self._g = t.numpy()[:n_rows].view(np.int32).reshape(-1, 2).astype(np.int64)
         self._gw, self._gr, self._gm = int(world), int(rank), int(n_rows) // int(world)
         v = self._g[:, 0] >= 0
@@ -438,7 +465,12 @@ class EmuSweepContext:
         who[ch >> 2] = ch & 3
         m, r = self._gm, self._gr
         loc = self._edges
-        wl = who[r * m:r * m + len(loc)]
+        if self._restricted:                     # this rank's block of S rows back onto its edges
+            wl = np.zeros(len(loc), np.int64)
+            wl[self._rmap] = who[r * m:r * m + self._rmap.size]
+            lf = self._rfwd
+        else:
+            wl = who[r * m:r * m + len(loc)]
         keep = wl != 2
         e = loc[keep].copy()
         fl = wl[keep] == 1
@@ -451,6 +483,8 @@ class EmuSweepContext:
             formed[a] -= 1
             if who[k] == 1:
                 formed[b] += 1
+        if self._restricted:                     # reads with no gathered row: their own edges
+            formed += np.where(self._gfwd == 0, lf, 0)
         self._gmode = False
         self._st = {'n_edges': len(e), 'edge_capacity': self.edge_capacity, 'max_fwd': int(formed.max())}
         return {'applied': 1, 'max_fwd': int(formed.max()), 'candidates': len(self._T), 'capped': 0, 'hits': 0,

@@ -290,8 +290,8 @@ def test_gloo_world2_sweep_shard_equals_oracle(world_case, tmp_path, edge_thresh
         assert sorted(map(tuple, e.tolist())) == want
 
 
-@pytest.mark.parametrize('edge_threshold', [10, 2])
-def test_local_hub_w3_sweep_shard_equals_oracle(world_case, edge_threshold):
+@pytest.mark.parametrize('edge_threshold,gather', [(10, 'restricted'), (2, 'restricted'), (2, 'full'), (2, 'i32')])
+def test_local_hub_w3_sweep_shard_equals_oracle(world_case, edge_threshold, gather, monkeypatch):
     """dist.SweepShard on W = 3 ranks as threads over dist.LocalHub (the in-process collectives the
     10M-read GPU test runs the product split with), on the emulated device: every rank has the
     oracle's components and the ranks' edges partition the oracle's (capped when edge_threshold 2)."""
@@ -299,6 +299,9 @@ def test_local_hub_w3_sweep_shard_equals_oracle(world_case, edge_threshold):
     from fslr_amd.dist import LocalHub, SweepShard, chrom_counts_of
     from fslr_amd.prep import fold_overlap_threshold, pass_table
     from tests.sweep_emu import EmuSweepContext
+    monkeypatch.setenv('FSLR_CAP_GATHER', 'full' if gather == 'full' else 'restricted')
+    if gather == 'i32':
+        monkeypatch.setenv('FSLR_CAP_BWD', 'i32')
     csr, o = world_case
     thr = fold_overlap_threshold(csr.iv_aln, 0.8)
     pt = pass_table([1, 1, 0.66, 0.66, 0.66, 0.5])
@@ -325,6 +328,8 @@ def test_local_hub_w3_sweep_shard_equals_oracle(world_case, edge_threshold):
             raise e
     ref = o if edge_threshold == 10 else O.run_core(_oracle_csr(csr), use_cap=True, edge_threshold=edge_threshold)
     assert all(i['capped'] == (edge_threshold == 2) for i in infos)
+    if edge_threshold == 2:
+        assert all(i['cap']['max_fwd'] == int(ref['fwd'].max()) for i in infos)
     got = []
     for c in ctxs:
         a, b, I, U = c.edges(c.stats()['n_edges'])
@@ -480,15 +485,20 @@ def _union_view(ctxs):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('W', [1, 2, 8])
-@pytest.mark.parametrize('thr', [3, 10])
-def test_sweep_split_capped_one_gpu_equals_oracle(W, thr):
+@pytest.mark.parametrize('W,thr,gather', [(1, 3, 'restricted'), (2, 3, 'restricted'), (8, 3, 'restricted'),
+                                          (1, 10, 'restricted'), (2, 10, 'restricted'), (8, 10, 'restricted'),
+                                          (2, 3, 'full'), (8, 10, 'full'), (2, 3, 'i32'), (8, 3, 'i32')])
+def test_sweep_split_capped_one_gpu_equals_oracle(W, thr, gather, monkeypatch):
     """The product's SweepShard with a binding cap, W ranks as threads on one GPU: the sharded replay
     (each rank lists the hits of its chromosomes, the lists travel to the rank replaying their read's
     component, the changes are exchanged) on a dense input where the cap binds for many reads — the
     ranks' capped edges (as (former, partner, I, U)) are the oracle's reference loop's, their edges
-    per loop add up to the oracle's, and every rank has the oracle's components."""
+    per loop add up to the oracle's, and every rank has the oracle's components.  ``gather``: the
+    rows of S only (uint8 or int32 backward counts summed over the ranks), or every E* row."""
     import dataclasses
+    monkeypatch.setenv('FSLR_CAP_GATHER', 'full' if gather == 'full' else 'restricted')
+    if gather == 'i32':
+        monkeypatch.setenv('FSLR_CAP_BWD', 'i32')
     from fslr_amd.prep import fold_overlap_threshold, pass_table
     s = synth.generate(20_000, 16, 47, cluster_cap=30, size_p=0.05)
     csr = s.interval_data().csr()
@@ -504,6 +514,7 @@ def test_sweep_split_capped_one_gpu_equals_oracle(W, thr):
         caps = [i['cap'] for i in infos]
         assert all(cp == caps[0] for cp in caps)
         assert caps[0]['capped'] > 0 and caps[0]['dropped'] > 0
+        assert caps[0]['max_fwd'] == int(o['fwd'].max())
         want = sorted(zip(o['edge_a'].tolist(), o['edge_b'].tolist(), o['edge_I'].tolist(), o['edge_U'].tolist()))
         a, b, I, U, fwd = _union_view(ctxs)
         assert sorted(zip(a.tolist(), b.tolist(), I.tolist(), U.tolist())) == want

@@ -5,13 +5,15 @@ measured on ONE GPU with W contexts (one per rank, each indexing its own chromos
 Every phase runs rank after rank (a synchronize around each), so each rank's time is its own:
   part[r]   build_index (filtered) + fslr_sweep_partition
   eval[d]   fslr_sweep_evaluate of the entries destined to d + the copy of its edges for the gather
-  cap_local[r]  fslr_cap_install_pairs + fslr_cap_local + fslr_cap_dep_local (closure over the gathered
-                rows, T's local hit lists, the local T-T forest)
+  cap_local[r]  fslr_cap_install_restricted (or _pairs) + fslr_cap_local + fslr_cap_dep_local (closure
+                over the gathered rows, T's local hit lists, the local T-T forest)
   cap_plan[r]   fslr_cap_shard_plan + fslr_cap_shard_pack
   cap_replay[r] fslr_cap_replay_shard (this rank's components)
   cap_apply[r]  fslr_cap_apply_changes + fslr_local_forest (its capped edges' forest)
   cap_merge[r]  fslr_components_from_pairs over the gathered forests (the capped graph's labels)
-  (the edge sort before the gather, fslr_sort_edges, is reported as a cap_local part)
+  (the edge sort before the gather, fslr_sort_edges, and with the restricted gather (--gather, default)
+  fslr_cap_bwd_counts + fslr_cap_restrict are reported as parts before cap_local; the counts' sum over
+  ranks is priced as a ring all_reduce)
 The exchanges cannot run on one GPU; they are priced from the bytes each rank moves at an assumed
 per-GPU xGMI rate (--xgmi-gbs) plus a fixed latency per collective (--coll-us), as
 tools/shard_timing.py does.  The single-context step (index + sweep query + fslr_apply_edge_cap +
@@ -46,7 +48,10 @@ def main():
     ap.add_argument('--edge-threshold', type=int, default=10)
     ap.add_argument('--xgmi-gbs', type=float, default=300.0)
     ap.add_argument('--coll-us', type=float, default=30.0)
+    ap.add_argument('--gather', choices=['restricted', 'full'], default='restricted',
+                    help='gather the rows of S only (the default of dist.SweepShard) or every E* row')
     args = ap.parse_args()
+    restricted = args.gather == 'restricted'
     import torch
     from fslr_amd import _lib, synth
     from fslr_amd.dist import chrom_counts_of, chrom_owner
@@ -101,7 +106,7 @@ def main():
     st1 = c1.stats()
     log(f'W=1: query {one[0]:.3f} ms, cap {one[1]:.3f} ms, step {one[2]:.3f} ms; cap {cap1}')
     c1.close()
-    out = {'workload': f'{n} reads x 1-{args.lmax} ({args.dist}), seed {args.seed}', 'n_reads': n,
+    out = {'gather': args.gather, 'workload': f'{n} reads x 1-{args.lmax} ({args.dist}), seed {args.seed}', 'n_reads': n,
            'n_intervals': int(csr.n_intervals), 'single': {'query_ms': one[0], 'cap_ms': one[1], 'step_ms': one[2],
                                                            'cap': cap1, 'edges': int(st1['n_edges'])},
            'xgmi_gbs_assumed': args.xgmi_gbs, 'collective_latency_us': args.coll_us, 'worlds': []}
@@ -146,13 +151,40 @@ def main():
                 ne.append(ctx[d].stats()['n_edges'])
                 ph['eval'][d].append(ms)
                 del ent
-            m = max(1, max(ne))
-            rows = torch.empty(W * m, dtype=torch.int64, device=dev)
             for d in range(W):
                 ms, _ = timed_once(lambda: ctx[d].sort_edges())
                 sub.setdefault('sort', [[] for _ in range(W)])[d].append(ms)
-                ctx[d].edges_into(rows[d * m:(d + 1) * m], m)
-            if rep == 0 and W > 1:
+            bwd_ms = 0.0
+            if restricted:
+                # the rows of S only: backward counts per rank, summed (all_reduce), then each rank's rows
+                dt = torch.uint8 if W * et <= 255 else torch.int32
+                bl = [torch.empty(n, dtype=dt, device=dev) for _ in range(W)]
+                for d in range(W):
+                    ms, _ = timed_once(lambda: ctx[d].cap_bwd_counts(et, bl[d]))
+                    sub.setdefault('bwd_counts', [[] for _ in range(W)])[d].append(ms)
+                bsum = torch.stack([b.to(torch.int32) for b in bl]).sum(dim=0).to(dt)
+                del bl
+                nrs = []
+                for d in range(W):
+                    ms, nr = timed_once(lambda: ctx[d].cap_restrict(bsum))
+                    sub.setdefault('restrict', [[] for _ in range(W)])[d].append(ms)
+                    nrs.append(nr)
+                del bsum
+                esz = 1 if dt == torch.uint8 else 4
+                bwd_ms = 0.0 if W == 1 else 2 * (W - 1) / W * n * esz / gbs + 2 * cl   # + the counts' all_reduce
+                m = max(1, max(nrs))
+                rows = torch.empty(W * m, dtype=torch.int64, device=dev)
+                for d in range(W):
+                    ctx[d].cap_copy_restricted(rows[d * m:(d + 1) * m], m)
+                if rep == 0:
+                    out.setdefault('restrict', {})[W] = {'rows': int(sum(ne)), 'rows_in_S': int(sum(nrs))}
+                    log('restricted gather:', out['restrict'][W])
+            else:
+                m = max(1, max(ne))
+                rows = torch.empty(W * m, dtype=torch.int64, device=dev)
+                for d in range(W):
+                    ctx[d].edges_into(rows[d * m:(d + 1) * m], m)
+            if rep == 0 and W > 1 and not restricted:
                 # diagnostics: the rows whose lower read can join the candidates (total E* degree >= the cap)
                 rw = rows.cpu().numpy().view(np.int32).reshape(-1, 2)
                 rw = rw[rw[:, 0] >= 0]
@@ -165,7 +197,8 @@ def main():
             nts = []
             tinfo = []
             for r in range(W):
-                m1, _ = timed_once(lambda: ctx[r].cap_install_pairs(rows, W * m, W, r))
+                m1, _ = timed_once(lambda: (ctx[r].cap_install_restricted if restricted else ctx[r].cap_install_pairs)(
+                    rows, W * m, W, r))
                 m2, _ = timed_once(lambda: ctx[r].cap_local(et))
                 nt = ctx[r].cap_sizes()[0]
                 ti = torch.empty(max(1, 2 * nt), dtype=torch.int32, device=dev)
@@ -242,18 +275,21 @@ def main():
             hits_ms = 0.0 if W == 1 else 4 * max(hoff.max(), hin.max()) / gbs + 2 * cl
             chg_ms = 0.0 if W == 1 else 4 * pad * (W - 1) / gbs + 2 * cl     # + the counts' all_gather
             fgath_ms = 0.0 if W == 1 else 8 * mf * (W - 1) / gbs + 2 * cl    # + the count's all_reduce
-            model.append({'a2a_ms': a2a, 'gather_ms': gath, 'tinfo_gather_ms': tg_ms, 'counts_a2a_ms': cnt_ms,
+            model.append({'a2a_ms': a2a, 'gather_ms': gath, 'bwd_allreduce_ms': bwd_ms, 'gather_rows_per_rank': m, 'tinfo_gather_ms': tg_ms, 'counts_a2a_ms': cnt_ms,
                           'hits_a2a_ms': hits_ms, 'changes_gather_ms': chg_ms, 'forest_gather_ms': fgath_ms,
                           'forest_pairs': fps, 'nt': nt, 'changes': chg_n,
                           'hits_to': hits_mat.sum(axis=0).tolist(), 'entries_sent': sent.sum(axis=1).tolist(),
                           'edges_per_rank': ne})
         med = {k: [float(np.median(v[r][1:])) for r in range(W)] for k, v in ph.items()}
         mdl = model[-1]
-        cap_ms = (max(sub['sort'][r][-1] for r in range(W)) + max(med['cap_local']) + mdl['tinfo_gather_ms']
+        smed = {k: [float(np.median(v[r][1:])) for r in range(W)] for k, v in sub.items()}
+        pre = max(smed['sort'])
+        if restricted:
+            pre += max(smed['bwd_counts']) + mdl['bwd_allreduce_ms'] + max(smed['restrict'])
+        cap_ms = (pre + max(med['cap_local']) + mdl['tinfo_gather_ms']
                   + max(med['cap_plan']) + mdl['counts_a2a_ms'] + mdl['hits_a2a_ms'] + max(med['cap_replay'])
                   + mdl['changes_gather_ms'] + max(med['cap_apply']) + mdl['forest_gather_ms'] + max(med['cap_merge']))
         step = (max(med['part']) + mdl['a2a_ms'] + max(med['eval']) + cl + mdl['gather_ms'] + cap_ms)
-        smed = {k: [float(np.median(v[r][1:])) for r in range(W)] for k, v in sub.items()}
         log('cap_local parts (max over ranks):', {k: round(max(v), 3) for k, v in smed.items()})
         row = {'W': W, 'phase_ms_per_rank': med, 'cap_local_parts_ms': smed, 'model': mdl,
                'cap_ms_per_rank_projected': cap_ms,
