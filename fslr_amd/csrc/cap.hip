@@ -836,6 +836,147 @@ __global__ void k_cap_classify(const int2* __restrict__ edges, long long ne, con
   }
 }
 
+// ---- 5'. one GPU, the edge list grouped by lower read (the sweep engine writes each read's forward
+// edges as one run: its edge stage never splits a read).  The closure walks the runs (frontier), and
+// only the rows of T's runs can change: they are classified in place, the dropped ones marked and
+// the list closed up by moving the few surviving rows behind the new end into the holes before it.
+// A read with two runs (another engine's order) flags the list: the full-list path runs instead.
+__global__ void k_cap_runs1(const int2* __restrict__ e, long long ne, int* __restrict__ gstart, int* __restrict__ gend,
+                            int* __restrict__ flag) {
+  for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < ne;
+       k += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const int a = e[k].x;
+    const int prev = k ? e[k - 1].x : -1;
+    const int next = k + 1 < ne ? e[k + 1].x : -1;
+    if (prev != a && atomicCAS(gstart + a, -1, static_cast<int>(k)) != -1) atomicOr(flag, 1);
+    if (next != a) gend[a] = static_cast<int>(k + 1);
+  }
+}
+
+__global__ void k_cap_runfix(int* __restrict__ gstart, int* __restrict__ gend, int n) {
+  for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < n; x += gridDim.x * blockDim.x)
+    if (gstart[x] < 0) gstart[x] = gend[x] = 0;
+}
+
+// one wavefront per read of T: its run's rows; re-oriented rows flipped in place, dropped rows marked
+// (a = -1) and listed
+__global__ __launch_bounds__(256) void k_cap_classify_runs(int2* __restrict__ edges, const int* __restrict__ gstart,
+                                                           const int* __restrict__ gend, const int* __restrict__ T,
+                                                           int nt, const int* __restrict__ t_of,
+                                                           const int* __restrict__ pbrk,
+                                                           const unsigned long long* __restrict__ ukey, int ns,
+                                                           const int* __restrict__ fpos,
+                                                           const unsigned char* __restrict__ vis2,
+                                                           int* __restrict__ formed, int* __restrict__ drops,
+                                                           unsigned* __restrict__ ndrop, long long* __restrict__ stats,
+                                                           int* __restrict__ err) {
+  const int lane = threadIdx.x & 63;
+  long long drop = 0, bwd = 0;
+  for (int t = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; t < nt; t += (gridDim.x * blockDim.x) >> 6) {
+    const int a = T[t];
+    if (pbrk[t] == kInf) continue;                   // the loop never broke: it formed all its edges
+    const int k0 = gstart[a], k1 = gend[a];
+    for (int kb = k0; kb < k1; kb += 64) {
+      const int k = kb + lane;
+      int w = 0;
+      int2 e = make_int2(0, 0);
+      if (k < k1) {
+        e = edges[k];
+        if (!loop_reaches(e.x, e.y, t_of, pbrk, ukey, ns, fpos, vis2, err))
+          w = loop_reaches(e.y, e.x, t_of, pbrk, ukey, ns, fpos, vis2, err) ? 1 : 2;
+      }
+      if (w == 1) {
+        edges[k] = make_int2(e.y, e.x);
+        atomicAdd(formed + e.y, 1);
+      }
+      if (w) atomicSub(formed + e.x, 1);
+      const unsigned long long dm = __ballot(w == 2);
+      if (dm) {
+        unsigned base = 0;
+        if (lane == 0) base = atomicAdd(ndrop, static_cast<unsigned>(__popcll(dm)));
+        base = static_cast<unsigned>(__shfl(static_cast<int>(base), 0));
+        if (w == 2) {
+          edges[k].x = -1;
+          drops[base + mbcnt(dm)] = k;
+        }
+      }
+      drop += w == 2;
+      bwd += w == 1;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    drop += __shfl_xor(drop, o);
+    bwd += __shfl_xor(bwd, o);
+  }
+  if (lane == 0) {
+    if (drop) atomicAdd(reinterpret_cast<unsigned long long*>(stats + kStDropped), static_cast<unsigned long long>(drop));
+    if (bwd) atomicAdd(reinterpret_cast<unsigned long long*>(stats + kStBackward), static_cast<unsigned long long>(bwd));
+  }
+}
+
+// the holes: dropped rows before the new end ne - d; the survivors: unmarked rows from there on
+__global__ void k_cap_holes(const int* __restrict__ drops, const unsigned* __restrict__ ndrop, long long ne,
+                            int* __restrict__ holes, unsigned* __restrict__ nh) {
+  const long long d = *ndrop;
+  const long long keep = ne - d;
+  const int lane = threadIdx.x & 63;
+  for (long long i0 = (blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x) & ~63ll; i0 < d;
+       i0 += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const long long i = i0 + lane;
+    const int k = i < d ? drops[i] : 0;
+    const bool h = i < d && k < keep;
+    const unsigned long long m = __ballot(h);
+    if (!m) continue;
+    unsigned base = 0;
+    if (lane == 0) base = atomicAdd(nh, static_cast<unsigned>(__popcll(m)));
+    base = static_cast<unsigned>(__shfl(static_cast<int>(base), 0));
+    if (h) holes[base + mbcnt(m)] = k;
+  }
+}
+
+__global__ void k_cap_survivors(const int2* __restrict__ edges, const unsigned* __restrict__ ndrop, long long ne,
+                                int* __restrict__ surv, unsigned* __restrict__ ns) {
+  const long long keep = ne - static_cast<long long>(*ndrop);
+  const int lane = threadIdx.x & 63;
+  for (long long k0 = keep + ((blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x) & ~63ll); k0 < ne;
+       k0 += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const long long k = k0 + lane;
+    const bool v = k < ne && edges[k].x >= 0;
+    const unsigned long long m = __ballot(v);
+    if (!m) continue;
+    unsigned base = 0;
+    if (lane == 0) base = atomicAdd(ns, static_cast<unsigned>(__popcll(m)));
+    base = static_cast<unsigned>(__shfl(static_cast<int>(base), 0));
+    if (v) surv[base + mbcnt(m)] = static_cast<int>(k);
+  }
+}
+
+// survivor i into hole i (as many of each); the edge count and the statistics for the host
+__global__ void k_cap_fill(int2* __restrict__ edges, unsigned short* __restrict__ iu, const int* __restrict__ holes,
+                           const int* __restrict__ surv, const unsigned* __restrict__ cnt, int* __restrict__ err) {
+  const unsigned nh = cnt[0], nsv = cnt[1];
+  if (blockIdx.x == 0 && threadIdx.x == 0 && nh != nsv) atomicOr(err, kCapErrState);
+  const unsigned m = min(nh, nsv);
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
+    const int h = holes[i], v = surv[i];
+    edges[h] = edges[v];
+    iu[h] = iu[v];
+  }
+}
+
+__global__ void k_cap_commit_runs(const unsigned* __restrict__ ndrop, long long ne,
+                                  unsigned long long* __restrict__ counters, int* __restrict__ errw,
+                                  long long* __restrict__ stats, const int* __restrict__ err,
+                                  long long* __restrict__ host) {
+  if (threadIdx.x != 0) return;
+  const long long kept = ne - static_cast<long long>(*ndrop);
+  stats[kStKept] = kept;
+  counters[kEdgeCount] = static_cast<unsigned long long>(kept);
+  errw[3] = static_cast<int>(stats[kStMaxFwd]);
+  for (int k = 0; k < kStWords; ++k) host[kHStat + k] = stats[k];
+  host[kHErr] = *err;
+}
+
 __global__ void k_cap_compact(const int2* __restrict__ edges, const unsigned short* __restrict__ iu, long long ne,
                               const unsigned char* __restrict__ who, const int* __restrict__ koff,
                               int2* __restrict__ oe, unsigned short* __restrict__ oiu) {
@@ -1457,6 +1598,7 @@ struct CapWork {
   bool replayed = false;              // fslr_cap_replay_shard ran (changes ready)
   int* hpin = nullptr;                // pinned host scratch (the plan's per-T arrays)
   size_t hpin_cap = 0;
+  bool runs1 = false;                 // one GPU: the edge list is grouped by lower read (gstart / gend)
   // the restricted gather (fslr_cap_bwd_counts, fslr_cap_restrict, fslr_cap_install_restricted):
   // local forward counts, the local backward counts (before the sum over ranks), kept flags and
   // offsets of the local edges, the kept rows and their local edge index, local who
@@ -1574,6 +1716,16 @@ bool cap_rounds_closure() {
 // queue over the loops' DAG (k_cap_replay_dag).  Measured at cfg5 (profiles/r04/cap/): the DAG
 // replay's cross-wave hand-offs (agent-scope release / acquire through memory, a few microseconds
 // each along the longest dependency chain) made it 7.2 ms against 2.5 ms per component.
+// one GPU: the closure over the edge list's runs and the classification of T's runs only, when every
+// read's forward edges are one run of the list (default; FSLR_CAP_RUNS=0: always the full-list path)
+bool cap_runs_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("FSLR_CAP_RUNS");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  return v;
+}
+
 bool cap_dag_enabled() {
   static const bool v = [] {
     const char* e = std::getenv("FSLR_CAP_REPLAY");
@@ -1932,7 +2084,24 @@ int cap_core(fslr_ctx* c, CapWork* w, fslr_cap_stats* cs) {
   // edges formed per loop, from the E* forward degrees (fwd[x] = E* edges (x, .), as the query or the
   // install left them)
   HIP_TRY(c, hipMemcpyAsync(w->formed, c->fwd, static_cast<size_t>(n) * sizeof(int), hipMemcpyDeviceToDevice, s));
-  if (ne > 0) {
+  if (w->runs1) {
+    // only T's runs can change: classified in place, then the dropped rows' holes filled
+    unsigned* cnt = reinterpret_cast<unsigned*>(w->chg);          // [0] dropped, [1] holes, [2] survivors
+    HIP_TRY(c, hipMemsetAsync(cnt, 0, 4 * sizeof(unsigned), s));
+    if (nt > 0)
+      k_cap_classify_runs<<<std::min(wave_grid(nt), 4096), 256, 0, s>>>(
+          c->edges, w->gstart, w->gend, w->T, nt, w->t_of, w->pbrk, w->ukey, ns, w->fpos, w->vis2, w->formed,
+          w->kflag, cnt, w->stats, w->err);
+    k_cap_holes<<<256, 256, 0, s>>>(w->kflag, cnt, ne, w->koff, cnt + 1);
+    k_cap_survivors<<<256, 256, 0, s>>>(c->edges, cnt, ne, w->adj, cnt + 2);
+    k_cap_fill<<<256, 256, 0, s>>>(c->edges, c->edge_iu, w->koff, w->adj, cnt + 1, w->err);
+    k_cap_check<<<grid_for(std::max<int64_t>(n, nt)), 256, 0, s>>>(w->T, nt, w->own, w->pbrk, w->formed,
+                                                                   static_cast<int>(n), w->stats, w->err);
+    HIP_TRY(c, hipMemcpyAsync(c->fwd, w->formed, static_cast<size_t>(n) * sizeof(int), hipMemcpyDeviceToDevice, s));
+    k_cap_commit_runs<<<1, 64, 0, s>>>(cnt, ne, c->counters, c->errw, w->stats, w->err, w->host_dev);
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipStreamSynchronize(s));
+  } else if (ne > 0) {
     k_cap_classify<<<grid_for(ne), 256, 0, s>>>(c->edges, ne, w->t_of, w->pbrk, w->ukey, ns, w->fpos, w->vis2,
                                                 w->kflag, w->who, w->formed, w->stats, w->err);
     size_t tb = 0;
@@ -1946,12 +2115,15 @@ int cap_core(fslr_ctx* c, CapWork* w, fslr_cap_stats* cs) {
     HIP_TRY(c, hipMemcpyAsync(c->edge_iu, w->oiu, static_cast<size_t>(ne) * sizeof(unsigned short),
                               hipMemcpyDeviceToDevice, s));
   }
-  k_cap_check<<<grid_for(std::max<int64_t>(n, nt)), 256, 0, s>>>(w->T, nt, w->own, w->pbrk, w->formed,
-                                                                 static_cast<int>(n), w->stats, w->err);
-  HIP_TRY(c, hipMemcpyAsync(c->fwd, w->formed, static_cast<size_t>(n) * sizeof(int), hipMemcpyDeviceToDevice, s));
-  k_cap_commit<<<1, 64, 0, s>>>(w->koff, w->kflag, ne, c->counters, c->errw, w->stats, w->err, w->host_dev);
-  HIP_TRY(c, hipGetLastError());
-  HIP_TRY(c, hipStreamSynchronize(s));
+  if (!w->runs1) {
+    k_cap_check<<<grid_for(std::max<int64_t>(n, nt)), 256, 0, s>>>(w->T, nt, w->own, w->pbrk, w->formed,
+                                                                   static_cast<int>(n), w->stats, w->err);
+    HIP_TRY(c, hipMemcpyAsync(c->fwd, w->formed, static_cast<size_t>(n) * sizeof(int), hipMemcpyDeviceToDevice, s));
+    k_cap_commit<<<1, 64, 0, s>>>(w->koff, w->kflag, ne, c->counters, c->errw, w->stats, w->err, w->host_dev);
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipStreamSynchronize(s));
+  }
+  w->runs1 = false;
   tm.lap("classify");
   const long long err = host_word(w, kHErr);
   if (err & kCapErrZd) return fail(c, FSLR_ERR_ZERO_DIVISION, "division by zero");
@@ -2007,7 +2179,33 @@ extern "C" int fslr_apply_edge_cap(fslr_ctx* c, int32_t thr, fslr_cap_stats* out
   if (int rc = ensure_bwd_ranges(c)) return rc;
   CapWork* w = nullptr;
   if (int rc = cap_work(c, &w)) return rc;
-  if (int rc = cap_local(c, thr, w, c->edges, c->fwd, ne)) return rc;
+  // each read's forward edges one run of the list (the sweep engine's order)?  Then the closure walks
+  // the runs and only T's runs are classified (FSLR_CAP_RUNS=0: the full-list path)
+  w->runs1 = false;
+  if (!c->lg_set && ne > 0 && cap_runs_enabled()) {
+    const int n = static_cast<int>(c->n);
+    {
+      Carve cv;
+      cv.add(&w->gstart, n);
+      cv.add(&w->gend, n);
+      cv.add(&w->gflag, 4);
+      if (int rc = cv.commit(c, w->ar[5])) return rc;
+    }
+    hipStream_t s = c->stream;
+    HIP_TRY(c, hipMemsetAsync(w->gstart, 0xff, static_cast<size_t>(n) * sizeof(int), s));
+    HIP_TRY(c, hipMemsetAsync(w->gflag, 0, 4 * sizeof(int), s));
+    k_cap_runs1<<<grid_for(ne), 256, 0, s>>>(c->edges, ne, w->gstart, w->gend, w->gflag);
+    k_cap_runfix<<<grid_for(n), 256, 0, s>>>(w->gstart, w->gend, n);
+    HIP_TRY(c, hipGetLastError());
+    int flag = 0;
+    HIP_TRY(c, hipMemcpyAsync(&flag, w->gflag, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    w->runs1 = flag == 0;
+    if (cap_debug()) std::fprintf(stderr, "fslr: cap edge list grouped by lower read: %d\n", w->runs1);
+  }
+  if (int rc = cap_local(c, thr, w, c->edges, c->fwd, ne, false, w->runs1 ? w->gstart : nullptr,
+                         w->runs1 ? w->gend : nullptr))
+    return rc;
   w->nseq = w->nloc;
   fslr_cap_stats cs;
   std::memset(&cs, 0, sizeof(cs));
@@ -2153,6 +2351,7 @@ extern "C" int fslr_cap_replay(fslr_ctx* c, const int32_t* counts, const int32_t
   HIP_TRY(c, hipGetLastError());
   fslr_cap_stats cs;
   std::memset(&cs, 0, sizeof(cs));
+  w->runs1 = false;                 // the full-list classification
   if (int rc = cap_core(c, w, &cs)) return rc;
   c->cap_stats = cs;
   if (out) *out = cs;
@@ -2248,6 +2447,7 @@ extern "C" int fslr_cap_replay_pairs(fslr_ctx* c, int32_t thr, const int32_t* a,
     if (int rc = cap_work(c, &w)) return rc;
     if (int rc = cap_local(c, thr, w, c->edges, c->fwd, ne)) return rc;
     w->nseq = w->nloc;
+    w->runs1 = false;                 // the full-list classification
     if (int rc = cap_core(c, w, &cs)) return rc;
     if (ne) HIP_TRY(c, hipMemcpyAsync(who, w->who, static_cast<size_t>(ne), hipMemcpyDeviceToHost, s));
     if (fwd) HIP_TRY(c, hipMemcpyAsync(fwd, c->fwd, static_cast<size_t>(n) * sizeof(int), hipMemcpyDeviceToHost, s));
@@ -2644,9 +2844,9 @@ extern "C" int fslr_cap_replay_shard(fslr_ctx* c, const int32_t* rcounts, const 
     k_cap_recv_assemble<<<wave_grid(nmine), 256, 0, s>>>(rcounts, w->roff, rhits, world, nmine, mine, w->ioff, w->seq);
     HIP_TRY(c, hipGetLastError());
   }
-  CapTimer tm(s);
   // slots, predicates and loops of this rank's components (every other T read has no hit: no break)
   if (int rc = cap_loops(c, w)) return rc;
+  CapTimer tm(s);
   const int ns = static_cast<int>(w->ns);
   if (w->g_rows > 0) {
     k_cap_classify_shard<<<grid_for(w->g_rows), 256, 0, s>>>(w->grows, w->g_rows, w->t_of, w->tdest, w->comp, w->g_rank,

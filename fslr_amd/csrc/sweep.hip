@@ -62,26 +62,13 @@ __device__ __forceinline__ int part_of(int B, int npass) {
 // window is a few hundred consecutive positions, so these loads hit L1 / L2).  kEmit = false counts
 // the tile's entries (and the statistics); kEmit = true writes them at the tile's scanned offset.
 constexpr int kMapCap = 2048;              // items per map segment (a longer tile takes several)
-#ifndef FSLR_SWEEP_PREFETCH
-#define FSLR_SWEEP_PREFETCH 0
-#endif
-constexpr bool kSweepPrefetch = FSLR_SWEEP_PREFETCH != 0;
-constexpr bool kSweepPrefetchGateEarly = FSLR_SWEEP_PREFETCH == 1;   // 2: the gate after the sweep
-constexpr bool kSweepPrefetchGate = FSLR_SWEEP_PREFETCH != 3;        // 3: the record only
-#ifndef FSLR_SWEEP_WAVES
-#define FSLR_SWEEP_WAVES 0
-#endif
 constexpr int kTileRun = 8;                // consecutive tiles per work item
 
 // kMode 0: count the tile's entries (two-pass fallback), 1: write them at the tile's scanned offset
 // (two-pass fallback), 2: one pass — write them at the tile's upper-bound slot (its forward-range
 // total, the pair tests) and count them; k_compact then packs the tiles.
 template <int kMode>
-__global__ __launch_bounds__(kSwBlock)
-#if FSLR_SWEEP_WAVES
-__attribute__((amdgpu_waves_per_eu(FSLR_SWEEP_WAVES)))
-#endif
-void k_sweep(SweepArgs g) {
+__global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
   constexpr bool kEmit = kMode != 0;
   constexpr bool kCount = kMode != 1;
   __shared__ int4 qa_all[kSwWaves][kWave];     // {end, thr, tag, qlo}
@@ -121,47 +108,15 @@ void k_sweep(SweepArgs g) {
   const int c_hi = static_cast<int>((static_cast<long long>(nchunks) * (xcd + 1)) / nx);
   const int c0 = g.xcd_map ? c_lo + wx : wid, c1 = g.xcd_map ? c_hi : nchunks;
   const int cstep = g.xcd_map ? bpx * kSwWaves : nw;
-  // Each tile's header (q's record and forward count, then its read's gate ranges: a dependent
-  // pair of loads) is loaded while the previous tile is swept (FSLR_SWEEP_PREFETCH): the record and
-  // count at the previous tile's start, the gate once its map is built.
-  struct Hdr {
-    int4 rq;
-    int nf;
-    int4 lbq;
-  };
-  auto hdr_rec = [&](int t, Hdr& h) {
-    const int qh = t * kWave + lane;
-    const int qhc = qh < g.ni ? qh : t * kWave;
-    h.rq = g.idx4[qhc];
-    h.nf = qh < g.ni ? g.rng_s[qhc].x : 0;
-  };
-  auto hdr_gate = [&](Hdr& h) { h.lbq = g.lb[h.rq.w >> 6]; };
-  // tiles in order: chunk by chunk (grid-stride or per XCD), consecutive tiles inside a chunk
-  auto advance = [&](int& ch, int& t) {
-    if (t + 1 < min(nt, (ch + 1) * run)) {
-      ++t;
-      return;
-    }
-    ch += cstep;
-    t = ch < c1 ? ch * run : -1;
-  };
-  int chunk = c0, tile = c0 < c1 ? c0 * run : -1;
-  Hdr cur, nxt;
-  if (tile >= 0) {
-    hdr_rec(tile, cur);
-    hdr_gate(cur);
-  }
-  while (tile >= 0) {
-    int nchunk = chunk, ntile = tile;
-    advance(nchunk, ntile);
-    if (kSweepPrefetch && ntile >= 0) hdr_rec(ntile, nxt);
-  {
+  for (int chunk = c0; chunk < c1; chunk += cstep)
+  for (int tile = chunk * run; tile < min(nt, (chunk + 1) * run); ++tile) {
     const int q0 = tile * kWave;
     const int q = q0 + lane;
     const bool qv = q < g.ni;
-    const int4 rq = cur.rq;
-    const int nf = cur.nf;
-    const int4 lbq = cur.lbq;                    // the gate of q's read as integer ranges
+    const int qc = qv ? q : q0;
+    int4 rq = g.idx4[qc];
+    const int nf = qv ? g.rng_s[qc].x : 0;
+    const int4 lbq = g.lb[rq.w >> 6];            // the gate of q's read as integer ranges
     const bool any_zero = __ballot(qv && (lbq.x < 0 || lbq.z < 0)) != 0ull;   // v == 0 (ZeroDivision)
     const int pre = wave_incl_scan(nf);
     const int ex = pre - nf;
@@ -180,10 +135,9 @@ void k_sweep(SweepArgs g) {
           atomicOr(g.err + kErrOverflow, 8);
           g.tile_cnt[tile] = 0;                  // the passes after the sweep read every tile's count
         }
-        goto tile_done;
+        continue;
       }
     }
-    if (kSweepPrefetch && kSweepPrefetchGate && kSweepPrefetchGateEarly && ntile >= 0) hdr_gate(nxt);
     int sn = 0, cnt = 0;                         // staged entries (kEmit) / entries of the tile
     if constexpr (kCount) w_tests += static_cast<unsigned long long>(T);
     for (int seg = 0; seg < T; seg += kMapCap) {
@@ -279,19 +233,6 @@ void k_sweep(SweepArgs g) {
     if constexpr (kCount) {
       if (lane == 0) g.tile_cnt[tile] = cnt;
       w_ent += static_cast<unsigned long long>(cnt);
-    }
-  }
-  tile_done:
-    chunk = nchunk;
-    tile = ntile;
-    if (tile >= 0) {
-      if (kSweepPrefetch) {
-        if (!kSweepPrefetchGate || !kSweepPrefetchGateEarly) hdr_gate(nxt);
-        cur = nxt;
-      } else {
-        hdr_rec(tile, cur);
-        hdr_gate(cur);
-      }
     }
   }
   if constexpr (kCount) {
@@ -436,21 +377,6 @@ __global__ __launch_bounds__(256) void k_compact(const unsigned long long* __res
 // streamed from HBM, through an LDS hash over its partners in partner partitions (pass k takes the
 // partners with part(B) == k).
 constexpr int kChunk2 = 512;               // a wave's work item: whole runs starting in it
-#ifndef FSLR_PAIRS_EARLY
-#define FSLR_PAIRS_EARLY 0
-#endif
-constexpr bool kPairsEarlyNext = FSLR_PAIRS_EARLY != 0;   // the next window's loads before the sort
-// FSLR_PAIRS_LBPOS: the sort key carries each entry's position in the group, and every entry's L_B
-// is gathered before the sort (in flight during it); a segment's head then takes its L_B from the
-// entry's original lane, instead of a dependent gather after the sort.  Key layouts:
-//   0: run << 39 | B << 14 | i << 7 | j            1: run << 46 | B << 21 | i << 14 | j << 7 | pos
-#ifndef FSLR_PAIRS_LBPOS
-#define FSLR_PAIRS_LBPOS 0
-#endif
-constexpr bool kPairsLbPos = FSLR_PAIRS_LBPOS != 0;
-constexpr int kSegShift = kPairsLbPos ? 21 : 14;        // key >> kSegShift = (run, B)
-constexpr int kRowShift = kPairsLbPos ? 14 : 7;         // key >> kRowShift = (run, B, i)
-constexpr int kColShift = kPairsLbPos ? 7 : 0;          // (key >> kColShift) & 63 = j
 constexpr int kStageE = 128;
 constexpr int kHash2 = 128;
 constexpr unsigned kEmpty = 0xFFFFFFFFu;
@@ -458,6 +384,7 @@ constexpr unsigned kEmpty = 0xFFFFFFFFu;
 #define FSLR_PAIR_EDGE_STAGE 256
 #endif
 constexpr int kPairEdgeStage = FSLR_PAIR_EDGE_STAGE;   // staged edges per wave (one atomic per flush)
+static_assert(kPairEdgeStage >= kStageE, "a group's edges fit one flush");
 // per-wave LDS shared by the two paths: the long-run hash (KEY, CNT: 4 B, RM, CM: 8 B per slot, the
 // slot list) or the group's sorted keys, segment keys, column masks and heads
 constexpr int kLongScr = kHash2 * (4 + 4 + 8 + 8) + 2 * (kPairLimit + kWave);
@@ -559,9 +486,7 @@ __device__ __forceinline__ void bitonic128_il(unsigned long long& a, unsigned lo
 }
 
 // group sort key: run (7 bits) << 39 | B << 14 | i << 7 | j; the segment key (run, B) is key >> 14
-__device__ __forceinline__ unsigned long long group_key(unsigned long long e, int r, int pos) {
-  if constexpr (kPairsLbPos)
-    return (static_cast<unsigned long long>(r) << 46) | ((e & ((1ull << 39) - 1)) << 7) | static_cast<unsigned>(pos);
+__device__ __forceinline__ unsigned long long group_key(unsigned long long e, int r) {
   return (static_cast<unsigned long long>(r) << 39) | (e & ((1ull << 39) - 1));
 }
 
@@ -674,6 +599,7 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
     const long long len = re - rs;
     const int npass = len <= kPairLimit ? 1 : static_cast<int>((len + kPerPass - 1) / kPerPass);
     int fwdA = 0;
+    if (es.n > 0) es.flush(eo, lane);               // A's edges from an empty stage: one run (<= the stage)
     for (int pass = 0; pass < npass; ++pass) {
       clear_hash();
       int uniq = 0;
@@ -812,9 +738,6 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
         continue;
       }
       // ---- the group [s, s + gend): whole runs, sorted by (run, B, i, j) ----
-      const long long sn = s + gend;
-      unsigned long long n0 = ~0ull, n1 = ~0ull, nn = ~0ull;
-      if (kPairsEarlyNext && sn < c1) load_window(sn, n0, n1, nn);   // in flight during the sort
       const int r0 = __popcll(H0 & upto(lane)) - 1;                 // run (in the group) of entry lane
       const int r1 = __popcll(H0) + __popcll(H1 & upto(lane)) - 1;
       const bool v0 = lane < gend, v1 = lane + kWave < gend;
@@ -827,13 +750,8 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
       if (hv0) la0 = RL[entry_a(e0)];                              // in flight during the sort
       if (hv1) la1 = RL[entry_a(e1)];
 #endif
-      unsigned long long k0 = v0 ? group_key(e0, r0, lane) : ~0ull;
-      unsigned long long k1 = v1 ? group_key(e1, r1, lane + kWave) : ~0ull;
-      int lbe0 = 0, lbe1 = 0;                                      // L_B of every entry (kPairsLbPos)
-      if constexpr (kPairsLbPos) {
-        if (v0) lbe0 = RL[(e0 >> 14) & kRankMask];
-        if (v1) lbe1 = RL[(e1 >> 14) & kRankMask];
-      }
+      unsigned long long k0 = v0 ? group_key(e0, r0) : ~0ull;
+      unsigned long long k1 = v1 ? group_key(e1, r1) : ~0ull;
 #if !defined(FSLR_PAIRS_ABLATE) || (FSLR_PAIRS_ABLATE & 1) == 0
       bitonic128_il(k0, k1, lane);
 #endif
@@ -848,29 +766,22 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
       const unsigned long long w1 = __shfl_up(k1, 1);
       const unsigned long long q1 = lane > 0 ? w1 : k0_63;
       // segments = read pairs (run, B); a row repeated inside a segment sits next to itself
-      const bool s0 = v0 && (lane == 0 || (k0 >> kSegShift) != (q0 >> kSegShift));
-      const bool s1 = v1 && (k1 >> kSegShift) != (q1 >> kSegShift);
-      const bool d0 = v0 && !s0 && (k0 >> kRowShift) == (q0 >> kRowShift);
-      const bool d1 = v1 && !s1 && (k1 >> kRowShift) == (q1 >> kRowShift);
+      const bool s0 = v0 && (lane == 0 || (k0 >> 14) != (q0 >> 14));
+      const bool s1 = v1 && (k1 >> 14) != (q1 >> 14);
+      const bool d0 = v0 && !s0 && (k0 >> 7) == (q0 >> 7);
+      const bool d1 = v1 && !s1 && (k1 >> 7) == (q1 >> 7);
       int lb0 = 0, lb1 = 0;                                        // L_B of each segment, gathered by its head
 #if defined(FSLR_PAIRS_ABLATE) && (FSLR_PAIRS_ABLATE & 4)
       if (s0) lb0 = 8;
       if (s1) lb1 = 8;
 #else
-      if constexpr (kPairsLbPos) {
-        // from the entry's lane before the sort (every lane shuffles, then selects)
-        const int p0 = static_cast<int>(k0 & 127u), p1 = static_cast<int>(k1 & 127u);
-        const int x0 = __shfl(lbe0, p0 & 63), y0 = __shfl(lbe1, p0 & 63);
-        const int x1 = __shfl(lbe0, p1 & 63), y1 = __shfl(lbe1, p1 & 63);
-        if (s0) lb0 = p0 < kWave ? x0 : y0;
-        if (s1) lb1 = p1 < kWave ? x1 : y1;
-      } else {
-        if (s0) lb0 = RL[(k0 >> 14) & kRankMask];
-        if (s1) lb1 = RL[(k1 >> 14) & kRankMask];
-      }
+      if (s0) lb0 = RL[(k0 >> 14) & kRankMask];
+      if (s1) lb1 = RL[(k1 >> 14) & kRankMask];
 #endif
       // the next window, in flight while this group is evaluated
-      if (!kPairsEarlyNext && sn < c1) load_window(sn, n0, n1, nn);
+      const long long sn = s + gend;
+      unsigned long long n0 = ~0ull, n1 = ~0ull, nn = ~0ull;
+      if (sn < c1) load_window(sn, n0, n1, nn);
       const unsigned long long S0 = __ballot(s0), S1 = __ballot(s1);
       const int ns0 = __popcll(S0), nseg = ns0 + __popcll(S1);
       const int g0 = __popcll(S0 & upto(lane)) - 1;
@@ -887,22 +798,25 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
         RUNF[r1] = 0;
       }
       if (s0) {
-        PK[g0] = (k0 >> kSegShift) | (static_cast<unsigned long long>(lb0) << 32);
+        PK[g0] = (k0 >> 14) | (static_cast<unsigned long long>(lb0) << 32);
         PJ[g0] = 0ull;
         PH[g0] = lane;
       }
       if (s1) {
-        PK[g1] = (k1 >> kSegShift) | (static_cast<unsigned long long>(lb1) << 32);
+        PK[g1] = (k1 >> 14) | (static_cast<unsigned long long>(lb1) << 32);
         PJ[g1] = 0ull;
         PH[g1] = lane + kWave;
       }
       if (lane == 0) PH[nseg] = gend;
       wave_lds_sync();
-      if (v0) atomicOr(&PJ[g0], 1ull << ((k0 >> kColShift) & 63u));
-      if (v1) atomicOr(&PJ[g1], 1ull << ((k1 >> kColShift) & 63u));
+      if (v0) atomicOr(&PJ[g0], 1ull << (k0 & 63u));
+      if (v1) atomicOr(&PJ[g1], 1ull << (k1 & 63u));
       if (d0) atomicOr(&PH[g0], 1 << 30);
       if (d1) atomicOr(&PH[g1], 1 << 30);
       wave_lds_sync();
+      // the group's edges (at most one per segment) go out in one flush: each read's forward edges stay
+      // one run of the edge list (the edge cap's replay walks those runs)
+      if (es.n + nseg > kPairEdgeStage) es.flush(eo, lane);
 #if defined(FSLR_PAIRS_ABLATE) && (FSLR_PAIRS_ABLATE & 2)
       for (int k0s = 0; k0s < 0; k0s += kWave) {                  // profiling ablation: no segment pass
 #else
@@ -925,7 +839,7 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
             int row = -1, Ic = 0;
             for (int k = h; k < he; ++k) {
               const unsigned long long key = SK[k];
-              const int i = static_cast<int>((key >> kRowShift) & 127u), j = static_cast<int>((key >> kColShift) & 63u);
+              const int i = static_cast<int>((key >> 7) & 127u), j = static_cast<int>(key & 63u);
               if (i == row) continue;                              // this row already matched
               if (!((used >> j) & 1ull)) {
                 used |= 1ull << j;

@@ -277,6 +277,23 @@ def test_one_locus_capped_vs_oracle(ctx, thr, engine):
     compare_capped_with_oracle(g, o, n)
 
 
+@pytest.mark.parametrize('n,lmax,seed,squeeze,dist,ccap', [
+    (30_000, 16, 41, 400, 'uniform', 60),
+    (20_000, 64, 13, 300, 'zipf', 40),
+    (8_000, 8, 59, 50, 'uniform', 200),
+])
+def test_sweep_edges_one_run_per_lower_read(ctx, n, lmax, seed, squeeze, dist, ccap):
+    """The sweep engine writes each read's forward edges E* as one run of the edge list (its edge
+    stage never splits a read, reads of up to 256 forward edges), which the one-GPU cap replay walks
+    (cap.hip k_cap_runs1; a split list falls back to the full-list path)."""
+    csr = _squeezed(n, lmax, seed, squeeze, dist, cluster_cap=ccap, size_p=0.05)
+    g = gpu_run(ctx, csr, engine='sweep')
+    a = g['a']
+    heads = a[np.r_[True, a[1:] != a[:-1]]]
+    assert g['fwd'].max() <= 256
+    assert np.unique(heads).size == heads.size          # no read starts two runs
+
+
 @pytest.mark.parametrize('engine', ENGINES)
 def test_cap_not_binding_is_identity(ctx, engine):
     s = synth.generate(30_000, 16, 2)
