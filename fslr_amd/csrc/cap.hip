@@ -242,6 +242,35 @@ __global__ void k_cap_tq(const int4* __restrict__ idx4, int ni, const int* __res
   }
 }
 
+// ... on one GPU's full index, without reading the index: a binary search for the interval's start in
+// its chromosome's range of the start column, then the run of equal starts (data order) for its record
+__global__ void k_cap_tq_bs(const int* __restrict__ tread, const int* __restrict__ T, const int* __restrict__ toff,
+                            int nti, const int4* __restrict__ rmeta, const int4* __restrict__ iv,
+                            const int2* __restrict__ crange, const int* __restrict__ s_start,
+                            const int4* __restrict__ idx4, int* __restrict__ tq, int* __restrict__ err) {
+  for (int ti = blockIdx.x * blockDim.x + threadIdx.x; ti < nti; ti += gridDim.x * blockDim.x) {
+    const int t = tread[ti];
+    const int x = T[t];
+    const int j = ti - toff[t];
+    const int4 v = iv[rmeta[x].x + j];
+    const int2 cr = crange[v.x];
+    int lo = cr.x, hi = cr.y;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (s_start[mid] < v.y) lo = mid + 1; else hi = mid;
+    }
+    const int tag = (x << 6) | j;
+    int q = -1;
+    for (int p = lo; p < cr.y && s_start[p] == v.y; ++p)
+      if (idx4[p].w == tag) {
+        q = p;
+        break;
+      }
+    tq[ti] = q;
+    if (q < 0) atomicOr(err, kCapErrState);
+  }
+}
+
 // ---- 2. visit sequences ------------------------------------------------------------------------
 // One wavefront per T-interval (sorted position q): the hits are q + 1 .. q + n_fwd and those p in
 // [bwd_begin, q) with end_p >= start_q (kernels.hpp rng_s), minus the read's own intervals.
@@ -370,6 +399,39 @@ __global__ __launch_bounds__(256) void k_cap_keys(const int* __restrict__ seq, c
       key[k] = hi | static_cast<unsigned>(seq[k]);
       val[k] = k;
     }
+  }
+}
+
+// the segmented form: partners (32-bit) sorted inside each read's segment of the sequence (a few
+// hundred hits) instead of (read, partner) keys over the whole sequence; then the keys rebuilt
+__global__ __launch_bounds__(256) void k_cap_pkeys(const int* __restrict__ seq, int m, unsigned* __restrict__ key,
+                                                   int* __restrict__ val) {
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < m; k += gridDim.x * blockDim.x) {
+    key[k] = static_cast<unsigned>(seq[k]);
+    val[k] = k;
+  }
+}
+
+__global__ void k_cap_segb(const int* __restrict__ ioff, const int* __restrict__ toff, int nt, int* __restrict__ segb) {
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t <= nt; t += gridDim.x * blockDim.x) segb[t] = ioff[toff[t]];
+}
+
+__global__ __launch_bounds__(256) void k_cap_rekey(const unsigned* __restrict__ pkey, const int* __restrict__ segb,
+                                                   int nt, unsigned long long* __restrict__ key) {
+  const int lane = threadIdx.x & 63;
+  const int nw = gridDim.x * (blockDim.x >> 6);
+  for (int t = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); t < nt; t += nw) {
+    const unsigned long long hi = static_cast<unsigned long long>(t) << 25;
+    for (int k = segb[t] + lane; k < segb[t + 1]; k += 64) key[k] = hi | pkey[k];
+  }
+}
+
+// each read of T's first slot (its sequence segment's first head; an empty segment: the next one's)
+__global__ void k_cap_tsb(const int* __restrict__ hs, const int* __restrict__ head, const int* __restrict__ segb,
+                          int nt, int m, int* __restrict__ tsb) {
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t <= nt; t += gridDim.x * blockDim.x) {
+    const int k = segb[t];
+    tsb[t] = k < m ? hs[k] : hs[m - 1] + head[m - 1];
   }
 }
 
@@ -524,8 +586,11 @@ __global__ __launch_bounds__(256) void k_cap_eval(const unsigned long long* __re
   }
 }
 
-__device__ __forceinline__ int find_slot(const unsigned long long* __restrict__ ukey, int ns, unsigned long long k) {
-  int lo = 0, hi = ns;
+// slot of key k = t << 25 | partner among read t's slots [tsb[t], tsb[t + 1]) (ukey sorted; -1: none)
+__device__ __forceinline__ int find_slot(const unsigned long long* __restrict__ ukey, const int* __restrict__ tsb,
+                                         int t, unsigned long long k) {
+  const int ns = tsb[t + 1];
+  int lo = tsb[t], hi = ns;
   while (lo < hi) {
     const int mid = (lo + hi) >> 1;
     if (ukey[mid] < k) lo = mid + 1; else hi = mid;
@@ -535,7 +600,8 @@ __device__ __forceinline__ int find_slot(const unsigned long long* __restrict__ 
 
 // per slot (x, y): for an earlier partner y of T, the slot of (y, x) (where y's loop records
 // whether it reached x) and the union of x and y in the dependency graph
-__global__ void k_cap_mirror(const unsigned long long* __restrict__ ukey, int ns, const int* __restrict__ T,
+__global__ void k_cap_mirror(const unsigned long long* __restrict__ ukey, int ns, const int* __restrict__ tsb,
+                             const int* __restrict__ T,
                              const int* __restrict__ t_of, int* __restrict__ mslot, int2* __restrict__ upairs,
                              int* __restrict__ err) {
   for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < ns; s += gridDim.x * blockDim.x) {
@@ -546,7 +612,7 @@ __global__ void k_cap_mirror(const unsigned long long* __restrict__ ukey, int ns
     int ms = -1;
     int2 up = make_int2(-1, -1);
     if (ty >= 0) {
-      ms = find_slot(ukey, ns, (static_cast<unsigned long long>(ty) << 25) | static_cast<unsigned>(x));
+      ms = find_slot(ukey, tsb, ty, (static_cast<unsigned long long>(ty) << 25) | static_cast<unsigned>(x));
       if (ms < 0) atomicOr(err, kCapErrState);          // hits are symmetric: cannot happen
       up = make_int2(t, ty);
     }
@@ -792,11 +858,11 @@ __global__ __launch_bounds__(256) void k_cap_replay_dag(int nt, int thr, const i
 // ---- 5. the capped graph -----------------------------------------------------------------------
 __device__ __forceinline__ bool loop_reaches(int x, int y, const int* __restrict__ t_of,
                                              const int* __restrict__ pbrk, const unsigned long long* __restrict__ ukey,
-                                             int ns, const int* __restrict__ fpos, const unsigned char* __restrict__ vis2,
+                                             const int* __restrict__ tsb, const int* __restrict__ fpos, const unsigned char* __restrict__ vis2,
                                              int* err) {
   const int t = t_of[x];
   if (t < 0 || pbrk[t] == kInf) return true;       // the loop never broke: it visited every hit
-  const int s = find_slot(ukey, ns, (static_cast<unsigned long long>(t) << 25) | static_cast<unsigned>(y));
+  const int s = find_slot(ukey, tsb, t, (static_cast<unsigned long long>(t) << 25) | static_cast<unsigned>(y));
   if (s < 0) {
     atomicOr(err, kCapErrState);
     return false;
@@ -806,7 +872,7 @@ __device__ __forceinline__ bool loop_reaches(int x, int y, const int* __restrict
 
 // who: 0 formed in a's loop, 1 in b's, 2 in neither (dropped)
 __global__ void k_cap_classify(const int2* __restrict__ edges, long long ne, const int* __restrict__ t_of,
-                               const int* __restrict__ pbrk, const unsigned long long* __restrict__ ukey, int ns,
+                               const int* __restrict__ pbrk, const unsigned long long* __restrict__ ukey, const int* __restrict__ tsb,
                                const int* __restrict__ fpos, const unsigned char* __restrict__ vis2,
                                int* __restrict__ kflag, unsigned char* __restrict__ who, int* __restrict__ formed,
                                long long* __restrict__ stats, int* __restrict__ err) {
@@ -815,8 +881,8 @@ __global__ void k_cap_classify(const int2* __restrict__ edges, long long ne, con
        k += static_cast<long long>(gridDim.x) * blockDim.x) {
     const int2 e = edges[k];
     int w = 2;
-    if (loop_reaches(e.x, e.y, t_of, pbrk, ukey, ns, fpos, vis2, err)) w = 0;
-    else if (loop_reaches(e.y, e.x, t_of, pbrk, ukey, ns, fpos, vis2, err)) w = 1;
+    if (loop_reaches(e.x, e.y, t_of, pbrk, ukey, tsb, fpos, vis2, err)) w = 0;
+    else if (loop_reaches(e.y, e.x, t_of, pbrk, ukey, tsb, fpos, vis2, err)) w = 1;
     who[k] = static_cast<unsigned char>(w);
     kflag[k] = w != 2;
     // formed starts as the E* forward degrees (every edge in its lower read's loop): only an edge
@@ -864,7 +930,7 @@ __global__ __launch_bounds__(256) void k_cap_classify_runs(int2* __restrict__ ed
                                                            const int* __restrict__ gend, const int* __restrict__ T,
                                                            int nt, const int* __restrict__ t_of,
                                                            const int* __restrict__ pbrk,
-                                                           const unsigned long long* __restrict__ ukey, int ns,
+                                                           const unsigned long long* __restrict__ ukey, const int* __restrict__ tsb,
                                                            const int* __restrict__ fpos,
                                                            const unsigned char* __restrict__ vis2,
                                                            int* __restrict__ formed, int* __restrict__ drops,
@@ -882,8 +948,8 @@ __global__ __launch_bounds__(256) void k_cap_classify_runs(int2* __restrict__ ed
       int2 e = make_int2(0, 0);
       if (k < k1) {
         e = edges[k];
-        if (!loop_reaches(e.x, e.y, t_of, pbrk, ukey, ns, fpos, vis2, err))
-          w = loop_reaches(e.y, e.x, t_of, pbrk, ukey, ns, fpos, vis2, err) ? 1 : 2;
+        if (!loop_reaches(e.x, e.y, t_of, pbrk, ukey, tsb, fpos, vis2, err))
+          w = loop_reaches(e.y, e.x, t_of, pbrk, ukey, tsb, fpos, vis2, err) ? 1 : 2;
       }
       if (w == 1) {
         edges[k] = make_int2(e.y, e.x);
@@ -1330,7 +1396,7 @@ __global__ __launch_bounds__(256) void k_cap_recv_assemble(const int* __restrict
 // forms the edge, 1 when b's does, 2 when neither; changes k << 2 | who for who != 0
 __global__ void k_cap_classify_shard(const int2* __restrict__ rows, long long n, const int* __restrict__ t_of,
                                      const int* __restrict__ tdest, const int* __restrict__ comp, int rank,
-                                     const int* __restrict__ pbrk, const unsigned long long* __restrict__ ukey, int ns,
+                                     const int* __restrict__ pbrk, const unsigned long long* __restrict__ ukey, const int* __restrict__ tsb,
                                      const int* __restrict__ fpos, const unsigned char* __restrict__ vis2,
                                      int* __restrict__ chg, unsigned* __restrict__ nchg, int* __restrict__ err) {
   const int lane = threadIdx.x & 63;
@@ -1345,8 +1411,8 @@ __global__ void k_cap_classify_shard(const int2* __restrict__ rows, long long n,
       if (t >= 0 && tdest[t] == rank) {
         if (ta >= 0 && tb >= 0 && comp[ta] != comp[tb]) {
           atomicOr(err, kCapErrState);                // E* partners hit each other: one component
-        } else if (!loop_reaches(e.x, e.y, t_of, pbrk, ukey, ns, fpos, vis2, err)) {
-          w = loop_reaches(e.y, e.x, t_of, pbrk, ukey, ns, fpos, vis2, err) ? 1 : 2;
+        } else if (!loop_reaches(e.x, e.y, t_of, pbrk, ukey, tsb, fpos, vis2, err)) {
+          w = loop_reaches(e.y, e.x, t_of, pbrk, ukey, tsb, fpos, vis2, err) ? 1 : 2;
         }
       }
     }
@@ -1557,6 +1623,7 @@ struct CapWork {
   // phase 1
   int *tread = nullptr, *tq = nullptr, *icnt = nullptr, *ioff = nullptr, *pbrk = nullptr, *own = nullptr,
       *tpar = nullptr;
+  int* tsb = nullptr;                 // each read of T's first slot (tsb[nt] = the slot count)
   int *sbeg = nullptr, *send = nullptr, *indeg = nullptr, *ready = nullptr;   // the loops' dependency DAG
   unsigned* queue = nullptr;
   unsigned long long *ck = nullptr, *ck2 = nullptr;
@@ -1726,6 +1793,16 @@ bool cap_runs_enabled() {
   return v;
 }
 
+// the slots' sort: segmented by read of T (default) or FSLR_CAP_SLOTSORT=global, one radix sort of
+// (read, partner) keys over the whole sequence
+bool cap_slot_segmented() {
+  static const bool v = [] {
+    const char* e = std::getenv("FSLR_CAP_SLOTSORT");
+    return !(e && std::strcmp(e, "global") == 0);
+  }();
+  return v;
+}
+
 bool cap_dag_enabled() {
   static const bool v = [] {
     const char* e = std::getenv("FSLR_CAP_REPLAY");
@@ -1887,6 +1964,7 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, const int2* E, const int* F, int
     cv.add(&w->gsum, nti + 1);
     cv.add(&w->pbrk, nt);
     cv.add(&w->own, nt);
+    cv.add(&w->tsb, nt + 1);
     cv.add(&w->tpar, nt);
     cv.add(&w->ck, nt);
     cv.add(&w->ck2, nt);
@@ -1900,8 +1978,12 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, const int2* E, const int* F, int
   if (nt > 0) {
     k_cap_tread<<<grid_for(nt), 256, 0, s>>>(w->toff, nt, w->tread);
     HIP_TRY(c, hipMemsetAsync(w->tq, 0xff, static_cast<size_t>(nti) * sizeof(int), s));
-    k_cap_tq<<<grid_for(c->ni_idx), 256, 0, s>>>(c->idx4, static_cast<int>(c->ni_idx), w->t_of, w->toff, w->vreal,
-                                                 w->vbase, w->tq);
+    if (!c->filter_active && !c->lg_set && !w->vreal)
+      k_cap_tq_bs<<<grid_for(nti), 256, 0, s>>>(w->tread, w->T, w->toff, nti, c->rmeta, c->iv, c->crange, c->s_start,
+                                                c->idx4, w->tq, w->err);
+    else
+      k_cap_tq<<<grid_for(c->ni_idx), 256, 0, s>>>(c->idx4, static_cast<int>(c->ni_idx), w->t_of, w->toff, w->vreal,
+                                                   w->vbase, w->tq);
     // 2. hits of the T-intervals this index holds: count, scan, emit top-down, ties, partner reads
     k_cap_hits<false><<<wave_grid(nti), 256, 0, s>>>(w->tq, w->tread, w->T, c->idx4, c->rng_s, w->vreal, nti,
                                                       w->icnt, nullptr, nullptr);
@@ -1964,21 +2046,43 @@ int cap_slots(fslr_ctx* c, CapWork* w) {
     if (int rc = cv.commit(c, w->ar[2])) return rc;
   }
   w->ns = 0;
-  if (m == 0) return FSLR_OK;
-  k_cap_keys<<<wave_grid(nti), 256, 0, s>>>(w->seq, w->ioff, w->tread, nti, w->skey, w->sval);
+  if (m == 0) {
+    HIP_TRY(c, hipMemsetAsync(w->tsb, 0, static_cast<size_t>(nt + 1) * sizeof(int), s));
+    return FSLR_OK;
+  }
   size_t b1 = 0, b2 = 0, b3 = 0;
   const int kbits = 25 + bits_for(nt);
-  HIP_TRY(c, hipcub::DeviceRadixSort::SortPairs(nullptr, b1, w->skey, w->skey2, w->sval, w->sval2, m, 0, kbits, s));
+  const bool seg = cap_slot_segmented();
+  unsigned* pkey = reinterpret_cast<unsigned*>(w->skey);           // segmented: 32-bit partners
+  unsigned* pkey2 = pkey + m;
+  int* segb = reinterpret_cast<int*>(w->ck);                       // nt + 1 segment offsets (ck: 2 nt ints)
+  const int pbits = bits_for(std::max<int64_t>(w->n, 1));
+  k_cap_segb<<<grid_for(nt + 1), 256, 0, s>>>(w->ioff, w->toff, nt, segb);
+  if (seg) {
+    k_cap_pkeys<<<grid_for(m), 256, 0, s>>>(w->seq, m, pkey, w->sval);
+    HIP_TRY(c, hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, b1, pkey, pkey2, w->sval, w->sval2, m, nt, segb,
+                                                           segb + 1, 0, pbits, s));
+  } else {
+    k_cap_keys<<<wave_grid(nti), 256, 0, s>>>(w->seq, w->ioff, w->tread, nti, w->skey, w->sval);
+    HIP_TRY(c, hipcub::DeviceRadixSort::SortPairs(nullptr, b1, w->skey, w->skey2, w->sval, w->sval2, m, 0, kbits, s));
+  }
   HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(nullptr, b2, w->head, w->hs, m, s));
   HIP_TRY(c, hipcub::DeviceRadixSort::SortKeys(nullptr, b3, w->ck, w->ck2, std::max(nt, 1), 0, 50, s));
   if (int rc = ensure_temp(c, w, std::max({b1, b2, b3}))) return rc;
   size_t tb = w->temp_bytes;
-  HIP_TRY(c, hipcub::DeviceRadixSort::SortPairs(w->temp, tb, w->skey, w->skey2, w->sval, w->sval2, m, 0, kbits, s));
+  if (seg) {
+    HIP_TRY(c, hipcub::DeviceSegmentedRadixSort::SortPairs(w->temp, tb, pkey, pkey2, w->sval, w->sval2, m, nt, segb,
+                                                           segb + 1, 0, pbits, s));
+    k_cap_rekey<<<wave_grid(nt), 256, 0, s>>>(pkey2, segb, nt, w->skey2);
+  } else {
+    HIP_TRY(c, hipcub::DeviceRadixSort::SortPairs(w->temp, tb, w->skey, w->skey2, w->sval, w->sval2, m, 0, kbits, s));
+  }
   k_cap_heads<<<grid_for(m), 256, 0, s>>>(w->skey2, m, w->head);
   tb = w->temp_bytes;
   HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(w->temp, tb, w->head, w->hs, m, s));
   k_cap_slots<<<grid_for(m), 256, 0, s>>>(w->skey2, w->sval2, w->head, w->hs, m, w->slot_of, w->ukey, w->fpos,
                                           w->host_dev);
+  k_cap_tsb<<<grid_for(nt + 1), 256, 0, s>>>(w->hs, w->head, segb, nt, m, w->tsb);
   HIP_TRY(c, hipGetLastError());
   HIP_TRY(c, hipStreamSynchronize(s));
   const int ns = static_cast<int>(host_word(w, kHNslots));
@@ -2001,7 +2105,7 @@ int cap_loops(fslr_ctx* c, CapWork* w) {
   const int ns = static_cast<int>(w->ns);
   if (m > 0) {
     // mirror slots; each read's earlier T partners (its in-degree in the loops' dependency DAG)
-    k_cap_mirror<<<grid_for(ns), 256, 0, s>>>(w->ukey, ns, w->T, w->t_of, w->mslot, w->upairs, w->err);
+    k_cap_mirror<<<grid_for(ns), 256, 0, s>>>(w->ukey, ns, w->tsb, w->T, w->t_of, w->mslot, w->upairs, w->err);
     k_cap_recs<<<grid_for(m), 256, 0, s>>>(w->slot_of, w->ukey, w->fpos, w->flags, w->mslot, w->T, w->t_of, m, w->rec);
     HIP_TRY(c, hipMemsetAsync(w->vis2, 0, static_cast<size_t>(ns), s));
     bool dag_ok = false;
@@ -2090,7 +2194,7 @@ int cap_core(fslr_ctx* c, CapWork* w, fslr_cap_stats* cs) {
     HIP_TRY(c, hipMemsetAsync(cnt, 0, 4 * sizeof(unsigned), s));
     if (nt > 0)
       k_cap_classify_runs<<<std::min(wave_grid(nt), 4096), 256, 0, s>>>(
-          c->edges, w->gstart, w->gend, w->T, nt, w->t_of, w->pbrk, w->ukey, ns, w->fpos, w->vis2, w->formed,
+          c->edges, w->gstart, w->gend, w->T, nt, w->t_of, w->pbrk, w->ukey, w->tsb, w->fpos, w->vis2, w->formed,
           w->kflag, cnt, w->stats, w->err);
     k_cap_holes<<<256, 256, 0, s>>>(w->kflag, cnt, ne, w->koff, cnt + 1);
     k_cap_survivors<<<256, 256, 0, s>>>(c->edges, cnt, ne, w->adj, cnt + 2);
@@ -2102,7 +2206,7 @@ int cap_core(fslr_ctx* c, CapWork* w, fslr_cap_stats* cs) {
     HIP_TRY(c, hipGetLastError());
     HIP_TRY(c, hipStreamSynchronize(s));
   } else if (ne > 0) {
-    k_cap_classify<<<grid_for(ne), 256, 0, s>>>(c->edges, ne, w->t_of, w->pbrk, w->ukey, ns, w->fpos, w->vis2,
+    k_cap_classify<<<grid_for(ne), 256, 0, s>>>(c->edges, ne, w->t_of, w->pbrk, w->ukey, w->tsb, w->fpos, w->vis2,
                                                 w->kflag, w->who, w->formed, w->stats, w->err);
     size_t tb = 0;
     HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tb, w->kflag, w->koff, static_cast<int>(ne), s));
@@ -2850,7 +2954,7 @@ extern "C" int fslr_cap_replay_shard(fslr_ctx* c, const int32_t* rcounts, const 
   const int ns = static_cast<int>(w->ns);
   if (w->g_rows > 0) {
     k_cap_classify_shard<<<grid_for(w->g_rows), 256, 0, s>>>(w->grows, w->g_rows, w->t_of, w->tdest, w->comp, w->g_rank,
-                                                             w->pbrk, w->ukey, ns, w->fpos, w->vis2, w->chgl, w->nchg,
+                                                             w->pbrk, w->ukey, w->tsb, w->fpos, w->vis2, w->chgl, w->nchg,
                                                              w->err);
     HIP_TRY(c, hipGetLastError());
   }
