@@ -242,18 +242,24 @@ __global__ void k_cap_tq(const int4* __restrict__ idx4, int ni, const int* __res
   }
 }
 
-// ... on one GPU's full index, without reading the index: a binary search for the interval's start in
-// its chromosome's range of the start column, then the run of equal starts (data order) for its record
+// ... without reading the index: a binary search for the interval's start in its chromosome's range of
+// the start column, then the run of equal starts (data order) for its record
 __global__ void k_cap_tq_bs(const int* __restrict__ tread, const int* __restrict__ T, const int* __restrict__ toff,
                             int nti, const int4* __restrict__ rmeta, const int4* __restrict__ iv,
-                            const int2* __restrict__ crange, const int* __restrict__ s_start,
-                            const int4* __restrict__ idx4, int* __restrict__ tq, int* __restrict__ err) {
+                            const int* __restrict__ fmap, const int2* __restrict__ crange,
+                            const int* __restrict__ s_start, const int4* __restrict__ idx4, int* __restrict__ tq,
+                            int* __restrict__ err) {
   for (int ti = blockIdx.x * blockDim.x + threadIdx.x; ti < nti; ti += gridDim.x * blockDim.x) {
     const int t = tread[ti];
     const int x = T[t];
     const int j = ti - toff[t];
     const int4 v = iv[rmeta[x].x + j];
-    const int2 cr = crange[v.x];
+    const int ch = fmap ? fmap[v.x] : v.x;         // a chromosome subset: its local number, -1 = not here
+    if (ch < 0) {
+      tq[ti] = -1;
+      continue;
+    }
+    const int2 cr = crange[ch];
     int lo = cr.x, hi = cr.y;
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
@@ -1978,9 +1984,11 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, const int2* E, const int* F, int
   if (nt > 0) {
     k_cap_tread<<<grid_for(nt), 256, 0, s>>>(w->toff, nt, w->tread);
     HIP_TRY(c, hipMemsetAsync(w->tq, 0xff, static_cast<size_t>(nti) * sizeof(int), s));
-    if (!c->filter_active && !c->lg_set && !w->vreal)
-      k_cap_tq_bs<<<grid_for(nti), 256, 0, s>>>(w->tread, w->T, w->toff, nti, c->rmeta, c->iv, c->crange, c->s_start,
-                                                c->idx4, w->tq, w->err);
+    if (!c->lg_set && !w->vreal)
+      k_cap_tq_bs<<<grid_for(nti), 256, 0, s>>>(w->tread, w->T, w->toff, nti, c->rmeta, c->iv,
+                                                c->filter_active ? c->fmap : nullptr,
+                                                c->filter_active ? c->crange_f : c->crange, c->s_start, c->idx4,
+                                                w->tq, w->err);
     else
       k_cap_tq<<<grid_for(c->ni_idx), 256, 0, s>>>(c->idx4, static_cast<int>(c->ni_idx), w->t_of, w->toff, w->vreal,
                                                    w->vbase, w->tq);
@@ -2050,6 +2058,7 @@ int cap_slots(fslr_ctx* c, CapWork* w) {
     HIP_TRY(c, hipMemsetAsync(w->tsb, 0, static_cast<size_t>(nt + 1) * sizeof(int), s));
     return FSLR_OK;
   }
+  CapTimer tm(s);
   size_t b1 = 0, b2 = 0, b3 = 0;
   const int kbits = 25 + bits_for(nt);
   const bool seg = cap_slot_segmented();
@@ -2087,27 +2096,29 @@ int cap_slots(fslr_ctx* c, CapWork* w) {
   HIP_TRY(c, hipStreamSynchronize(s));
   const int ns = static_cast<int>(host_word(w, kHNslots));
   w->ns = ns;
+  tm.lap("slots: sort");
   k_cap_eval<<<wave_grid((ns + 63) / 64), 256, 0, s>>>(w->ukey, ns, w->T, c->rmeta, c->iv, w->rlen, w->off2, c->last_qcut,
                                            c->last_ncut, w->umax, w->n_umax, w->flags);
   HIP_TRY(c, hipGetLastError());
+  tm.lap("slots: eval");
   return FSLR_OK;
 }
 
 // 3 + 4: slots, predicates and every read of T's loop (pbrk, own, visit marks)
 int cap_loops(fslr_ctx* c, CapWork* w) {
   hipStream_t s = c->stream;
-  CapTimer tm(s);
   const int thr = w->thr;
   const int nt = static_cast<int>(w->nt);
   const int m = static_cast<int>(w->nseq);
   if (int rc = cap_slots(c, w)) return rc;
-  tm.lap("slots, eval");
+  CapTimer tm(s);
   const int ns = static_cast<int>(w->ns);
   if (m > 0) {
     // mirror slots; each read's earlier T partners (its in-degree in the loops' dependency DAG)
     k_cap_mirror<<<grid_for(ns), 256, 0, s>>>(w->ukey, ns, w->tsb, w->T, w->t_of, w->mslot, w->upairs, w->err);
     k_cap_recs<<<grid_for(m), 256, 0, s>>>(w->slot_of, w->ukey, w->fpos, w->flags, w->mslot, w->T, w->t_of, m, w->rec);
     HIP_TRY(c, hipMemsetAsync(w->vis2, 0, static_cast<size_t>(ns), s));
+    tm.lap("loops: mirror");
     bool dag_ok = false;
     if (cap_dag_enabled()) {
       HIP_TRY(c, hipMemsetAsync(w->sbeg, 0, static_cast<size_t>(nt) * sizeof(int), s));
@@ -2142,6 +2153,7 @@ int cap_loops(fslr_ctx* c, CapWork* w) {
       k_cap_ckeys<<<grid_for(nt), 256, 0, s>>>(w->tpar, nt, w->ck);
       size_t tb = w->temp_bytes;
       HIP_TRY(c, hipcub::DeviceRadixSort::SortKeys(w->temp, tb, w->ck, w->ck2, nt, 0, 50, s));
+      tm.lap("loops: comps");
       if (cap_debug()) {
         std::vector<int> par(nt), toff(nt + 1), ioff(static_cast<size_t>(w->nti) + 1);
         HIP_TRY(c, hipMemcpyAsync(par.data(), w->tpar, nt * sizeof(int), hipMemcpyDeviceToHost, s));
@@ -2173,7 +2185,7 @@ int cap_loops(fslr_ctx* c, CapWork* w) {
     HIP_TRY(c, hipGetLastError());
   }
   w->ns = ns;
-  tm.lap("loops");
+  tm.lap("loops: replay");
   return FSLR_OK;
 }
 
