@@ -1298,8 +1298,9 @@ __global__ void k_cap_ccost(const int* __restrict__ comp, const int* __restrict_
     atomicAdd(ccost + comp[t], static_cast<unsigned long long>(cost[t]) + 1ull);
 }
 
+// the components' roots as sort keys: cost descending, then root ascending
 __global__ void k_cap_roots(const int* __restrict__ comp, const unsigned long long* __restrict__ ccost, int nt,
-                            int2* __restrict__ roots, unsigned* __restrict__ nroots) {
+                            unsigned long long* __restrict__ roots, unsigned* __restrict__ nroots) {
   const int lane = threadIdx.x & 63;
   for (int t0 = (blockIdx.x * blockDim.x + threadIdx.x) & ~63; t0 < nt; t0 += gridDim.x * blockDim.x) {
     const int t = t0 + lane;
@@ -1309,7 +1310,7 @@ __global__ void k_cap_roots(const int* __restrict__ comp, const unsigned long lo
     unsigned base = 0;
     if (lane == 0) base = atomicAdd(nroots, static_cast<unsigned>(__popcll(m)));
     base = static_cast<unsigned>(__shfl(static_cast<int>(base), 0));
-    if (r) roots[base + mbcnt(m)] = make_int2(t, static_cast<int>(min(ccost[t], 0x7fffffffull)));
+    if (r) roots[base + mbcnt(m)] = ((0x7fffffffull - min(ccost[t], 0x7fffffffull)) << 32) | static_cast<unsigned>(t);
   }
 }
 
@@ -2806,6 +2807,7 @@ extern "C" int fslr_cap_shard_plan(fslr_ctx* c, const int32_t* gathered, int32_t
   // the components of the T-T hit graph: the union of the ranks' local forests; each component's cost
   // and the list of roots, on the device
   unsigned nr = 0;
+  unsigned long long* rkeys = reinterpret_cast<unsigned long long*>(w->roots);   // then sorted into ccost
   if (nt > 0) {
     HIP_TRY(c, launch_uf_init(w->comp, nt, s));
     HIP_TRY(c, launch_uf_strided(w->comp, gathered, world, nt, 2ll * nt, s));
@@ -2814,10 +2816,19 @@ extern "C" int fslr_cap_shard_plan(fslr_ctx* c, const int32_t* gathered, int32_t
     HIP_TRY(c, hipMemsetAsync(w->ccost, 0, static_cast<size_t>(nt) * sizeof(unsigned long long), s));
     HIP_TRY(c, hipMemsetAsync(w->nroots, 0, sizeof(unsigned), s));
     k_cap_ccost<<<grid_for(nt), 256, 0, s>>>(w->comp, w->tcost, nt, w->ccost);
-    k_cap_roots<<<grid_for(nt), 256, 0, s>>>(w->comp, w->ccost, nt, w->roots, w->nroots);
+    k_cap_roots<<<grid_for(nt), 256, 0, s>>>(w->comp, w->ccost, nt, rkeys, w->nroots);
     HIP_TRY(c, hipGetLastError());
     HIP_TRY(c, hipMemcpyAsync(&nr, w->nroots, sizeof(nr), hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
+    if (nr > 1) {                      // largest first (ties: the smaller root), on the device
+      size_t tb = 0;
+      HIP_TRY(c, hipcub::DeviceRadixSort::SortKeys(nullptr, tb, rkeys, w->ccost, static_cast<int>(nr), 0, 63, s));
+      if (int rc = ensure_temp(c, w, tb)) return rc;
+      tb = w->temp_bytes;
+      HIP_TRY(c, hipcub::DeviceRadixSort::SortKeys(w->temp, tb, rkeys, w->ccost, static_cast<int>(nr), 0, 63, s));
+    } else if (nr == 1) {
+      HIP_TRY(c, hipMemcpyAsync(w->ccost, rkeys, sizeof(unsigned long long), hipMemcpyDeviceToDevice, s));
+    }
   }
   tm.lap("plan: unions");
   // pinned host copy of the roots (pageable copies go through the driver's staging)
@@ -2830,21 +2841,25 @@ extern "C" int fslr_cap_shard_plan(fslr_ctx* c, const int32_t* gathered, int32_t
     w->hpin_cap = want;
   }
   int2* rh = reinterpret_cast<int2*>(w->hpin);
+  const unsigned long long* rk = reinterpret_cast<const unsigned long long*>(w->hpin);
   if (nr) {
-    HIP_TRY(c, hipMemcpyAsync(rh, w->roots, static_cast<size_t>(nr) * sizeof(int2), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipMemcpyAsync(w->hpin, w->ccost, static_cast<size_t>(nr) * sizeof(unsigned long long),
+                              hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
   }
   tm.lap("plan: d2h");
   // components largest first (ties: the smaller root) onto the least-loaded rank (ties: the lower
   // rank) — the same assignment on every rank
-  std::sort(rh, rh + nr, [](const int2& a, const int2& b) { return a.y != b.y ? a.y > b.y : a.x < b.x; });
   int64_t load[kMaxDest] = {};
   for (unsigned k = 0; k < nr; ++k) {
+    const unsigned long long key = rk[k];
+    const int root = static_cast<int>(key & 0xffffffffull);
+    const int64_t cost = static_cast<int64_t>(0x7fffffffull - (key >> 32));
     int d = 0;
     for (int q = 1; q < world; ++q)
       if (load[q] < load[d]) d = q;
-    load[d] += rh[k].y;
-    rh[k].y = d;
+    load[d] += cost;
+    rh[k] = make_int2(root, d);        // (in place: the key just read)
   }
   tm.lap("plan: assign");
   if (nr) {
