@@ -1039,11 +1039,15 @@ __global__ void k_cap_fill(int2* __restrict__ edges, unsigned short* __restrict_
 __global__ void k_cap_commit_runs(const unsigned* __restrict__ ndrop, long long ne,
                                   unsigned long long* __restrict__ counters, int* __restrict__ errw,
                                   long long* __restrict__ stats, const int* __restrict__ err,
-                                  long long* __restrict__ host) {
+                                  long long* __restrict__ host, bool clear) {
   if (threadIdx.x != 0) return;
   const long long kept = ne - static_cast<long long>(*ndrop);
   stats[kStKept] = kept;
   counters[kEdgeCount] = static_cast<unsigned long long>(kept);
+  if (clear) {                                       // the sharded replay: the query's flags are settled
+    errw[0] = 0;
+    errw[kErrOverflow] = 0;
+  }
   errw[3] = static_cast<int>(stats[kStMaxFwd]);
   for (int k = 0; k < kStWords; ++k) host[kHStat + k] = stats[k];
   host[kHErr] = *err;
@@ -1524,15 +1528,13 @@ __global__ void k_cap_commit_shard(const int* __restrict__ koff, const int* __re
 // A read x joins the closure T only when fwd(x) + back(x) >= thr with back(x) <= bwd(x) over E*, and
 // only rows whose lower read is in T are walked by the closure, break a loop or change: the rows
 // of S = {x : fwd(x) + bwd(x) >= thr} suffice (3% of E* at cfg5).  Each rank holds every forward row
-// of the reads it owns (the partition routes a pair to its lower read's owner); bwd is a sum over
-// ranks of counts clipped at thr (the test fwd + sum >= thr is unchanged by the clip).
-__global__ void k_cap_degs(const int2* __restrict__ e, long long ne, int* __restrict__ fwd, int* __restrict__ bwd) {
+// of the reads it owns (the partition routes a pair to its lower read's owner: fwd, the context's
+// forward degrees, is the whole of it); bwd is a sum over ranks of counts clipped at thr (the test
+// fwd + sum >= thr is unchanged by the clip).
+__global__ void k_cap_bwdc(const int2* __restrict__ e, long long ne, int* __restrict__ bwd) {
   for (long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; i < ne;
-       i += static_cast<long long>(gridDim.x) * blockDim.x) {
-    const int2 v = e[i];
-    atomicAdd(fwd + v.x, 1);
-    atomicAdd(bwd + v.y, 1);
-  }
+       i += static_cast<long long>(gridDim.x) * blockDim.x)
+    atomicAdd(bwd + e[i].y, 1);
 }
 
 __global__ void k_cap_clip8(const int* __restrict__ cnt, int n, int thr, unsigned char* __restrict__ out) {
@@ -1560,12 +1562,35 @@ __global__ void k_cap_rcompact(const int2* __restrict__ e, long long ne, const i
   }
 }
 
-// this rank's block of the restricted rows: who back onto its local edges
-__global__ void k_cap_rwho(const unsigned char* __restrict__ gwho, const int* __restrict__ rmap, long long nr,
-                           unsigned char* __restrict__ lwho) {
-  for (long long j = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; j < nr;
-       j += static_cast<long long>(gridDim.x) * blockDim.x)
-    lwho[rmap[j]] = gwho[j];
+// this rank's block of the restricted rows, applied in place on its edges: formers' counts moved,
+// re-oriented rows flipped, dropped rows marked (a = -1) and listed for the hole fill
+__global__ void k_cap_rapply(const unsigned char* __restrict__ gwho, const int* __restrict__ rmap, long long nr,
+                             int2* __restrict__ edges, int* __restrict__ fwd, int* __restrict__ drops,
+                             unsigned* __restrict__ ndrop) {
+  const int lane = threadIdx.x & 63;
+  for (long long j0 = (blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x) & ~63ll; j0 < nr;
+       j0 += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const long long j = j0 + lane;
+    const int w = j < nr ? gwho[j] : 0;
+    int k = 0;
+    if (w) {
+      k = rmap[j];
+      const int2 e = edges[k];
+      atomicSub(fwd + e.x, 1);
+      if (w == 1) {
+        edges[k] = make_int2(e.y, e.x);
+        atomicAdd(fwd + e.y, 1);
+      } else {
+        edges[k].x = -1;
+      }
+    }
+    const unsigned long long dm = __ballot(w == 2);
+    if (!dm) continue;
+    unsigned base = 0;
+    if (lane == 0) base = atomicAdd(ndrop, static_cast<unsigned>(__popcll(dm)));
+    base = static_cast<unsigned>(__shfl(static_cast<int>(base), 0));
+    if (w == 2) drops[base + mbcnt(dm)] = k;
+  }
 }
 
 // reads with no gathered forward row (outside S, or none at all): their own forward edges, held here
@@ -1676,10 +1701,8 @@ struct CapWork {
   // the restricted gather (fslr_cap_bwd_counts, fslr_cap_restrict, fslr_cap_install_restricted):
   // local forward counts, the local backward counts (before the sum over ranks), kept flags and
   // offsets of the local edges, the kept rows and their local edge index, local who
-  int *rfwd = nullptr, *rcnt = nullptr, *rflag = nullptr, *rkoff = nullptr, *rmap = nullptr;
+  int *rcnt = nullptr, *rflag = nullptr, *rkoff = nullptr, *rmap = nullptr;
   int2* rrows = nullptr;
-  unsigned short* roiu = nullptr;
-  unsigned char* lwho = nullptr;
   int64_t r_ne = 0, r_n = 0;
   int r_thr = 0;
   bool r_counted = false, r_ready = false, g_restricted = false;
@@ -2215,7 +2238,7 @@ int cap_core(fslr_ctx* c, CapWork* w, fslr_cap_stats* cs) {
     k_cap_check<<<grid_for(std::max<int64_t>(n, nt)), 256, 0, s>>>(w->T, nt, w->own, w->pbrk, w->formed,
                                                                    static_cast<int>(n), w->stats, w->err);
     HIP_TRY(c, hipMemcpyAsync(c->fwd, w->formed, static_cast<size_t>(n) * sizeof(int), hipMemcpyDeviceToDevice, s));
-    k_cap_commit_runs<<<1, 64, 0, s>>>(cnt, ne, c->counters, c->errw, w->stats, w->err, w->host_dev);
+    k_cap_commit_runs<<<1, 64, 0, s>>>(cnt, ne, c->counters, c->errw, w->stats, w->err, w->host_dev, false);
     HIP_TRY(c, hipGetLastError());
     HIP_TRY(c, hipStreamSynchronize(s));
   } else if (ne > 0) {
@@ -2661,20 +2684,16 @@ extern "C" int fslr_cap_bwd_counts(fslr_ctx* c, int32_t thr, void* out, int32_t 
   if (int rc = cap_work(c, &w)) return rc;
   {
     Carve cv;
-    cv.add(&w->rfwd, n);
     cv.add(&w->rcnt, n);
     cv.add(&w->rflag, ne);
     cv.add(&w->rkoff, ne);
     cv.add(&w->rmap, ne);
     cv.add(&w->rrows, ne);
-    cv.add(&w->roiu, ne);
-    cv.add(&w->lwho, ne);
     if (int rc = cv.commit(c, w->ar[10])) return rc;
   }
   int* bcnt = elem_bytes == 4 ? static_cast<int*>(out) : w->rcnt;
-  HIP_TRY(c, hipMemsetAsync(w->rfwd, 0, static_cast<size_t>(std::max<int64_t>(n, 1)) * sizeof(int), s));
   HIP_TRY(c, hipMemsetAsync(bcnt, 0, static_cast<size_t>(std::max<int64_t>(n, 1)) * sizeof(int), s));
-  if (ne > 0) k_cap_degs<<<grid_for(ne), 256, 0, s>>>(c->edges, ne, w->rfwd, bcnt);
+  if (ne > 0) k_cap_bwdc<<<grid_for(ne), 256, 0, s>>>(c->edges, ne, bcnt);
   if (elem_bytes == 1 && n > 0)
     k_cap_clip8<<<grid_for(n), 256, 0, s>>>(w->rcnt, static_cast<int>(n), thr, static_cast<unsigned char*>(out));
   HIP_TRY(c, hipGetLastError());
@@ -2695,7 +2714,7 @@ extern "C" int fslr_cap_restrict(fslr_ctx* c, const void* bwd, int32_t elem_byte
   const int64_t ne = w->r_ne;
   int64_t kept = 0;
   if (ne > 0) {
-    k_cap_rflags<<<grid_for(ne), 256, 0, s>>>(c->edges, ne, w->rfwd, bwd, elem_bytes, w->r_thr, w->rflag);
+    k_cap_rflags<<<grid_for(ne), 256, 0, s>>>(c->edges, ne, c->fwd, bwd, elem_bytes, w->r_thr, w->rflag);
     size_t tb = 0;
     HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tb, w->rflag, w->rkoff, static_cast<int>(ne), s));
     if (int rc = ensure_temp(c, w, tb)) return rc;
@@ -3047,42 +3066,50 @@ extern "C" int fslr_cap_apply_changes(fslr_ctx* c, const int32_t* changes, int64
     HIP_TRY(c, hipGetLastError());
   }
   tm.lap("apply: changes");
-  // this rank's own edges (block g_rank of the rows: all of them, or with the restricted gather its
-  // rows of S mapped back onto its edges): kept ones compacted and re-oriented, their formers
+  // this rank's own edges (block g_rank of the rows): kept ones compacted and re-oriented, their formers;
+  // with the restricted gather its rows of S are applied in place through their local edge index and
+  // the dropped rows' holes filled from the tail
   const bool rs = w->g_restricted;
-  const int2* blk = rs ? c->edges : w->grows + w->g_rank * m;
-  const unsigned char* wblk = rs ? w->lwho : w->gwho + w->g_rank * m;
-  int *kflag = rs ? w->rflag : w->kflag, *koff = rs ? w->rkoff : w->koff;
-  int2* oedges = rs ? w->rrows : w->oedges;
-  unsigned short* oiu = rs ? w->roiu : w->oiu;
-  const int64_t mown = rs ? w->r_ne : mloc;
+  unsigned* rcnt3 = reinterpret_cast<unsigned*>(w->chg);          // [0] dropped, [1] holes, [2] survivors
   if (rs) {
     // the maximum then covers S and this rank's reads outside S (the caller's MAX over ranks)
-    if (mown) HIP_TRY(c, hipMemsetAsync(w->lwho, 0, static_cast<size_t>(mown), s));
-    if (w->r_n) k_cap_rwho<<<grid_for(w->r_n), 256, 0, s>>>(w->gwho + w->g_rank * m, w->rmap, w->r_n, w->lwho);
-    if (nr) k_cap_addfwd<<<grid_for(nr), 256, 0, s>>>(w->formed, w->gfwd, w->rfwd, static_cast<int>(nr));
+    if (nr) k_cap_addfwd<<<grid_for(nr), 256, 0, s>>>(w->formed, w->gfwd, c->fwd, static_cast<int>(nr));
+    HIP_TRY(c, hipMemsetAsync(rcnt3, 0, 4 * sizeof(unsigned), s));
+    if (w->r_n)
+      k_cap_rapply<<<grid_for(w->r_n), 256, 0, s>>>(w->gwho + w->g_rank * m, w->rmap, w->r_n, c->edges, c->fwd,
+                                                    w->rflag, rcnt3);
+    k_cap_holes<<<256, 256, 0, s>>>(w->rflag, rcnt3, w->r_ne, w->rkoff, rcnt3 + 1);
+    k_cap_survivors<<<256, 256, 0, s>>>(c->edges, rcnt3, w->r_ne, w->rmap, rcnt3 + 2);
+    k_cap_fill<<<256, 256, 0, s>>>(c->edges, c->edge_iu, w->rkoff, w->rmap, rcnt3 + 1, w->err);
     HIP_TRY(c, hipGetLastError());
-  }
-  HIP_TRY(c, hipMemsetAsync(c->fwd, 0, static_cast<size_t>(nr) * sizeof(int), s));
-  if (mown > 0) {
-    k_cap_local_flags<<<grid_for(mown), 256, 0, s>>>(blk, wblk, mown, kflag);
-    size_t tb = 0;
-    HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tb, kflag, koff, static_cast<int>(mown), s));
-    if (int rc = ensure_temp(c, w, tb)) return rc;
-    tb = w->temp_bytes;
-    HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(w->temp, tb, kflag, koff, static_cast<int>(mown), s));
-    k_cap_local_compact<<<grid_for(mown), 256, 0, s>>>(c->edges, c->edge_iu, mown, kflag, koff, wblk, oedges, oiu,
-                                                       c->fwd);
-    HIP_TRY(c, hipGetLastError());
-    HIP_TRY(c, hipMemcpyAsync(c->edges, oedges, static_cast<size_t>(mown) * sizeof(int2), hipMemcpyDeviceToDevice, s));
-    HIP_TRY(c, hipMemcpyAsync(c->edge_iu, oiu, static_cast<size_t>(mown) * sizeof(unsigned short),
-                              hipMemcpyDeviceToDevice, s));
+  } else {
+    const int2* blk = w->grows + w->g_rank * m;
+    const unsigned char* wblk = w->gwho + w->g_rank * m;
+    HIP_TRY(c, hipMemsetAsync(c->fwd, 0, static_cast<size_t>(nr) * sizeof(int), s));
+    if (mloc > 0) {
+      k_cap_local_flags<<<grid_for(mloc), 256, 0, s>>>(blk, wblk, mloc, w->kflag);
+      size_t tb = 0;
+      HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tb, w->kflag, w->koff, static_cast<int>(mloc), s));
+      if (int rc = ensure_temp(c, w, tb)) return rc;
+      tb = w->temp_bytes;
+      HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(w->temp, tb, w->kflag, w->koff, static_cast<int>(mloc), s));
+      k_cap_local_compact<<<grid_for(mloc), 256, 0, s>>>(c->edges, c->edge_iu, mloc, w->kflag, w->koff, wblk,
+                                                         w->oedges, w->oiu, c->fwd);
+      HIP_TRY(c, hipGetLastError());
+      HIP_TRY(c, hipMemcpyAsync(c->edges, w->oedges, static_cast<size_t>(mloc) * sizeof(int2), hipMemcpyDeviceToDevice,
+                                s));
+      HIP_TRY(c, hipMemcpyAsync(c->edge_iu, w->oiu, static_cast<size_t>(mloc) * sizeof(unsigned short),
+                                hipMemcpyDeviceToDevice, s));
+    }
   }
   tm.lap("apply: local");
   k_cap_check_shard<<<grid_for(std::max<int64_t>(nr, nt)), 256, 0, s>>>(w->T, nt, w->tdest, w->g_rank, w->own, w->formed,
                                                                        static_cast<int>(nr), w->stats, w->err);
   HIP_TRY(c, hipGetLastError());
-  k_cap_commit_shard<<<1, 64, 0, s>>>(koff, kflag, mown, c->counters, c->errw, w->stats, w->err, w->host_dev);
+  if (rs)
+    k_cap_commit_runs<<<1, 64, 0, s>>>(rcnt3, w->r_ne, c->counters, c->errw, w->stats, w->err, w->host_dev, true);
+  else
+    k_cap_commit_shard<<<1, 64, 0, s>>>(w->koff, w->kflag, mloc, c->counters, c->errw, w->stats, w->err, w->host_dev);
   HIP_TRY(c, hipGetLastError());
   HIP_TRY(c, hipStreamSynchronize(s));
   const long long err = host_word(w, kHErr);
