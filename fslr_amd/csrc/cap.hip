@@ -1562,6 +1562,17 @@ __global__ void k_cap_rcompact(const int2* __restrict__ e, long long ne, const i
   }
 }
 
+// the restricted rows by lower read (stable): a sorted (row, local edge) pair list
+__global__ void k_cap_rpermute(const int2* __restrict__ rows, const int* __restrict__ rmap, const int* __restrict__ idx,
+                               long long n, int2* __restrict__ orows, int* __restrict__ ormap) {
+  for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < n;
+       k += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const int i = idx[k];
+    orows[k] = rows[i];
+    ormap[k] = rmap[i];
+  }
+}
+
 // this rank's block of the restricted rows, applied in place on its edges: formers' counts moved,
 // re-oriented rows flipped, dropped rows marked (a = -1) and listed for the hole fill
 __global__ void k_cap_rapply(const unsigned char* __restrict__ gwho, const int* __restrict__ rmap, long long nr,
@@ -2727,6 +2738,33 @@ extern "C" int fslr_cap_restrict(fslr_ctx* c, const void* bwd, int32_t elem_byte
     HIP_TRY(c, hipMemcpyAsync(last + 1, w->rflag + ne - 1, sizeof(int), hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
     kept = static_cast<int64_t>(last[0]) + last[1];
+  }
+  if (kept > 1) {
+    // sorted by lower read (each read's rows one run of the gathered blocks); only these rows need it
+    unsigned *k1 = nullptr, *k2 = nullptr;
+    int *v1 = nullptr, *v2 = nullptr, *ormap = nullptr;
+    int2* orows = nullptr;
+    {
+      Carve cv;
+      cv.add(&k1, kept);
+      cv.add(&k2, kept);
+      cv.add(&v1, kept);
+      cv.add(&v2, kept);
+      cv.add(&orows, kept);
+      cv.add(&ormap, kept);
+      if (int rc = cv.commit(c, w->ar[9])) return rc;
+    }
+    const int nk = static_cast<int>(kept);
+    k_edge_keys<<<grid_for(kept), 256, 0, s>>>(w->rrows, kept, k1, v1);
+    size_t tb = 0;
+    HIP_TRY(c, hipcub::DeviceRadixSort::SortPairs(nullptr, tb, k1, k2, v1, v2, nk, 0, bits_for(c->n), s));
+    if (int rc = ensure_temp(c, w, tb)) return rc;
+    tb = w->temp_bytes;
+    HIP_TRY(c, hipcub::DeviceRadixSort::SortPairs(w->temp, tb, k1, k2, v1, v2, nk, 0, bits_for(c->n), s));
+    k_cap_rpermute<<<grid_for(kept), 256, 0, s>>>(w->rrows, w->rmap, v2, kept, orows, ormap);
+    HIP_TRY(c, hipGetLastError());
+    HIP_TRY(c, hipMemcpyAsync(w->rrows, orows, static_cast<size_t>(kept) * sizeof(int2), hipMemcpyDeviceToDevice, s));
+    HIP_TRY(c, hipMemcpyAsync(w->rmap, ormap, static_cast<size_t>(kept) * sizeof(int), hipMemcpyDeviceToDevice, s));
   }
   w->r_n = kept;
   w->r_ready = true;

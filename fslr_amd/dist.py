@@ -506,8 +506,9 @@ class SweepShard:
         self.egath = self._grow(self.egath, W * m)
         restricted = os.environ.get('FSLR_CAP_GATHER', 'restricted') != 'full'
         try:
-            ctx.sort_edges()                     # each read's forward rows one run of the gathered rows
-            if restricted:
+            if not restricted:
+                ctx.sort_edges()                 # each read's forward rows one run of the gathered rows
+            else:
                 # only the rows of S = {x : fwd(x) + bwd(x) >= threshold} travel (bwd summed over ranks)
                 dt = (torch.uint8 if W * edge_threshold <= 255 and os.environ.get('FSLR_CAP_BWD') != 'i32'
                       else torch.int32)

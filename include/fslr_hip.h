@@ -302,11 +302,12 @@ int  fslr_cap_replay(fslr_ctx *ctx, const int32_t *counts, const int32_t *hits, 
  *   ranks' parts).
  * The restricted gather: only rows whose lower read x has fwd(x) + bwd(x) >= edge_threshold over E* can
  * take part (the closure's join test, cluster.py:210-213 via DESIGN.md §11), about 3% of E* at cfg5.
- * fslr_cap_bwd_counts: after fslr_sort_edges, this rank's counts of its edges per upper read b into out
+ * fslr_cap_bwd_counts: this rank's counts of its edges per upper read b into out
  *   (device, n_reads elements of elem_bytes: 1 = uint8 clipped at edge_threshold <= 255, 4 = int32;
  *   async); the caller sums them over the ranks (all_reduce; uint8 needs world x threshold <= 255).
  * fslr_cap_restrict: from the summed counts, this rank's rows of S (its edges whose lower read has
- *   fwd + bwd >= threshold, in edge order); *n_rows = their count (syncs).
+ *   fwd + bwd >= threshold, sorted by lower read: no fslr_sort_edges of the whole list is needed);
+ *   *n_rows = their count (syncs).
  * fslr_cap_copy_restricted: those rows as int32 (a, b) pairs padded with -1 to n_pad (device, async).
  * fslr_cap_install_restricted: the ranks' gathered restricted rows, as fslr_cap_install_pairs (the rest
  *   of the sequence is unchanged); fslr_cap_apply_changes then maps this rank's block back onto its

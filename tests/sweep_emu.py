@@ -319,7 +319,8 @@ class EmuSweepContext:
         bwd = t.numpy()[:self.n_reads].astype(np.int64)
         e = self._edges
         keep = (self._rfwd[e[:, 0]] + bwd[e[:, 0]] >= self._r_thr) if len(e) else np.zeros(0, bool)
-        self._rmap = np.flatnonzero(keep)
+        rm = np.flatnonzero(keep)
+        self._rmap = rm[np.argsort(e[rm, 0], kind='stable')]      # by lower read (one run per read)
         return int(self._rmap.size)
 
     def cap_copy_restricted(self, t, n_pad):
