@@ -138,7 +138,8 @@ __global__ void k_cap_adj_fill(const int2* __restrict__ edges, long long ne, con
 
 // the seeds: reads whose own forward degree reaches the cap (frontier 0)
 __global__ void k_cap_seed(const int* __restrict__ fwd, int n, int thr, int* __restrict__ state,
-                           int* __restrict__ back, int* __restrict__ fl, unsigned* __restrict__ fn) {
+                           int* __restrict__ back, int* __restrict__ fl, unsigned* __restrict__ fn,
+                           int* __restrict__ tl, unsigned* __restrict__ tn) {
   const int lane = threadIdx.x & 63;
   for (int x0 = (blockIdx.x * blockDim.x + threadIdx.x) & ~63; x0 < n; x0 += gridDim.x * blockDim.x) {
     const int x = x0 + lane;
@@ -149,10 +150,17 @@ __global__ void k_cap_seed(const int* __restrict__ fwd, int n, int thr, int* __r
     }
     const unsigned long long m = __ballot(j);
     if (!m) continue;
-    unsigned base = 0;
-    if (lane == 0) base = atomicAdd(fn, static_cast<unsigned>(__popcll(m)));
+    unsigned base = 0, tbase = 0;
+    if (lane == 0) {
+      base = atomicAdd(fn, static_cast<unsigned>(__popcll(m)));
+      tbase = atomicAdd(tn, static_cast<unsigned>(__popcll(m)));
+    }
     base = static_cast<unsigned>(__shfl(static_cast<int>(base), 0));
-    if (j) fl[base + mbcnt(m)] = x;
+    tbase = static_cast<unsigned>(__shfl(static_cast<int>(tbase), 0));
+    if (j) {
+      fl[base + mbcnt(m)] = x;
+      tl[tbase + mbcnt(m)] = x;                    // every member of T, in joining order
+    }
   }
 }
 
@@ -160,14 +168,18 @@ __global__ void k_cap_seed(const int* __restrict__ fwd, int n, int thr, int* __r
 // enters the next frontier) when its forward degree plus those counts reaches the cap
 __global__ void k_cap_frontier(const int* __restrict__ aoff, const int* __restrict__ adj, const int* __restrict__ fwd,
                                int thr, int* __restrict__ state, int* __restrict__ back, const int* __restrict__ fin,
-                               const unsigned* __restrict__ fin_n, int* __restrict__ fout, unsigned* __restrict__ fout_n) {
+                               const unsigned* __restrict__ fin_n, int* __restrict__ fout, unsigned* __restrict__ fout_n,
+                               int* __restrict__ tl, unsigned* __restrict__ tn) {
   const int nin = static_cast<int>(*fin_n);
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nin; i += gridDim.x * blockDim.x) {
     const int x = fin[i];
     for (int k = aoff[x]; k < aoff[x + 1]; ++k) {
       const int y = adj[k];
       const int b = atomicAdd(back + y, 1) + 1;
-      if (fwd[y] + b >= thr && atomicCAS(state + y, 0, 1) == 0) fout[atomicAdd(fout_n, 1u)] = y;
+      if (fwd[y] + b >= thr && atomicCAS(state + y, 0, 1) == 0) {
+        fout[atomicAdd(fout_n, 1u)] = y;
+        tl[atomicAdd(tn, 1u)] = y;
+      }
     }
   }
 }
@@ -175,7 +187,7 @@ __global__ void k_cap_frontier(const int* __restrict__ aoff, const int* __restri
 __global__ void k_cap_fcnt_roll(unsigned* fcnt) {
   if (threadIdx.x == 0) {
     const unsigned v = fcnt[16];
-    for (int k = 1; k < 64; ++k) fcnt[k] = 0;
+    for (int k = 1; k < 32; ++k) fcnt[k] = 0;        // fcnt[32]: the T list's length
     fcnt[0] = v;
   }
 }
@@ -190,6 +202,20 @@ __global__ void k_cap_tpack(const int* __restrict__ state, const int4* __restric
                             const int* __restrict__ rlen, int n, unsigned long long* __restrict__ v) {
   for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < n; x += gridDim.x * blockDim.x)
     v[x] = state[x] ? ((1ull << 32) | static_cast<unsigned>(read_len(rmeta, rlen, x))) : 0ull;
+}
+
+// T from the frontier closure's list (sorted by rank): the read of each t, its interval count
+__global__ void k_cap_tfin(const int* __restrict__ T, int nt, const int4* __restrict__ rmeta,
+                           const int* __restrict__ rlen, int* __restrict__ t_of, int* __restrict__ tlen) {
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t <= nt; t += gridDim.x * blockDim.x) {
+    if (t == nt) {
+      tlen[t] = 0;
+      continue;
+    }
+    const int x = T[t];
+    t_of[x] = t;
+    tlen[t] = read_len(rmeta, rlen, x);
+  }
 }
 
 // every read is a candidate (fslr_long_pairs: the pairs of every read's hits)
@@ -1234,14 +1260,17 @@ __global__ void k_cap_frontier_rows(const int* __restrict__ gstart, const int* _
                                     const int2* __restrict__ rows, const int* __restrict__ fwd, int thr,
                                     int* __restrict__ state, int* __restrict__ back, const int* __restrict__ fin,
                                     const unsigned* __restrict__ fin_n, int* __restrict__ fout,
-                                    unsigned* __restrict__ fout_n) {
+                                    unsigned* __restrict__ fout_n, int* __restrict__ tl, unsigned* __restrict__ tn) {
   const int nin = static_cast<int>(*fin_n);
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nin; i += gridDim.x * blockDim.x) {
     const int x = fin[i];
     for (int k = gstart[x]; k < gend[x]; ++k) {
       const int y = rows[k].y;
       const int b = atomicAdd(back + y, 1) + 1;
-      if (fwd[y] + b >= thr && atomicCAS(state + y, 0, 1) == 0) fout[atomicAdd(fout_n, 1u)] = y;
+      if (fwd[y] + b >= thr && atomicCAS(state + y, 0, 1) == 0) {
+        fout[atomicAdd(fout_n, 1u)] = y;
+        tl[atomicAdd(tn, 1u)] = y;
+      }
     }
   }
 }
@@ -1656,6 +1685,7 @@ struct CapWork {
   // phase 0
   int *state = nullptr, *back = nullptr, *t_of = nullptr, *T = nullptr, *toff = nullptr, *formed = nullptr;
   int *aoff = nullptr, *acur = nullptr, *adj = nullptr, *fl0 = nullptr, *fl1 = nullptr;   // frontier closure
+  int* tl = nullptr;                  // the frontier closure's members of T (joining order; fcnt[32] of them)
   unsigned* fcnt = nullptr;
   unsigned long long *tv = nullptr, *tvs = nullptr;
   int *chg = nullptr, *err = nullptr, *kflag = nullptr, *koff = nullptr;
@@ -1913,6 +1943,7 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, const int2* E, const int* F, int
     cv.add(&w->adj, ne);
     cv.add(&w->fl0, n);
     cv.add(&w->fl1, n);
+    cv.add(&w->tl, n);
     cv.add(&w->fcnt, 64);
     if (int rc = cv.commit(c, w->ar[0])) return rc;
   }
@@ -1941,8 +1972,10 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, const int2* E, const int* F, int
     HIP_TRY(c, hipMemsetAsync(w->acur, 0, static_cast<size_t>(n) * sizeof(int), s));
     if (ne > 0) k_cap_adj_fill<<<grid_for(ne), 256, 0, s>>>(E, ne, w->aoff, w->acur, w->adj);
   }
+  unsigned ntl = 0;                    // the frontier closure: |T|
   if (frontier) {
-    k_cap_seed<<<grid_for(n), 256, 0, s>>>(F, static_cast<int>(n), thr, w->state, w->back, w->fl0, w->fcnt);
+    k_cap_seed<<<grid_for(n), 256, 0, s>>>(F, static_cast<int>(n), thr, w->state, w->back, w->fl0, w->fcnt, w->tl,
+                                           w->fcnt + 32);
     HIP_TRY(c, hipGetLastError());
     int* fl[2] = {w->fl0, w->fl1};
     for (int batch = 0;; ++batch) {
@@ -1950,14 +1983,15 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, const int2* E, const int* F, int
       for (int r = 0; r < 16; ++r) {
         if (rstart)
           k_cap_frontier_rows<<<1024, 256, 0, s>>>(rstart, rend, E, F, thr, w->state, w->back, fl[r & 1], w->fcnt + r,
-                                                   fl[(r + 1) & 1], w->fcnt + r + 1);
+                                                   fl[(r + 1) & 1], w->fcnt + r + 1, w->tl, w->fcnt + 32);
         else
           k_cap_frontier<<<1024, 256, 0, s>>>(w->aoff, w->adj, F, thr, w->state, w->back, fl[r & 1], w->fcnt + r,
-                                              fl[(r + 1) & 1], w->fcnt + r + 1);
+                                              fl[(r + 1) & 1], w->fcnt + r + 1, w->tl, w->fcnt + 32);
       }
       HIP_TRY(c, hipGetLastError());
       unsigned last = 0;
       HIP_TRY(c, hipMemcpyAsync(&last, w->fcnt + 16, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+      HIP_TRY(c, hipMemcpyAsync(&ntl, w->fcnt + 32, sizeof(unsigned), hipMemcpyDeviceToHost, s));
       HIP_TRY(c, hipStreamSynchronize(s));
       if (!last) break;
       if (batch > (n >> 4) + 2) return fail(c, FSLR_ERR_STATE, "edge cap closure does not converge");
@@ -1982,15 +2016,38 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, const int2* E, const int* F, int
     if (batch > (n >> 3) + 2) return fail(c, FSLR_ERR_STATE, "edge cap closure does not converge");
   }
   tm.lap("closure");
-  // T in rank order, T-intervals
-  k_cap_tpack<<<grid_for(n), 256, 0, s>>>(w->state, c->rmeta, w->rlen, static_cast<int>(n), w->tv);
+  // T in rank order, T-intervals.  The frontier closure listed T's members: sorted, their interval
+  // counts scanned (no pass over every read but t_of's reset); the rounds closure: a scan of all reads
   size_t tb = 0;
-  HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tb, w->tv, w->tvs, static_cast<int>(n), s));
-  if (int rc = ensure_temp(c, w, tb)) return rc;
-  tb = w->temp_bytes;
-  HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(w->temp, tb, w->tv, w->tvs, static_cast<int>(n), s));
-  k_cap_tlist<<<grid_for(n), 256, 0, s>>>(w->state, w->tv, w->tvs, static_cast<int>(n), w->T, w->toff, w->t_of,
-                                          w->host_dev);
+  if (frontier) {
+    const int ntt = static_cast<int>(ntl);
+    int* tlen = reinterpret_cast<int*>(w->tv);
+    if (ntt > 1) {
+      HIP_TRY(c, hipcub::DeviceRadixSort::SortKeys(nullptr, tb, w->tl, w->T, ntt, 0, bits_for(n), s));
+      if (int rc = ensure_temp(c, w, tb)) return rc;
+      tb = w->temp_bytes;
+      HIP_TRY(c, hipcub::DeviceRadixSort::SortKeys(w->temp, tb, w->tl, w->T, ntt, 0, bits_for(n), s));
+    } else if (ntt == 1) {
+      HIP_TRY(c, hipMemcpyAsync(w->T, w->tl, sizeof(int), hipMemcpyDeviceToDevice, s));
+    }
+    HIP_TRY(c, hipMemsetAsync(w->t_of, 0xff, static_cast<size_t>(n) * sizeof(int), s));
+    k_cap_tfin<<<grid_for(ntt + 1), 256, 0, s>>>(w->T, ntt, c->rmeta, w->rlen, w->t_of, tlen);
+    tb = 0;
+    HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tb, tlen, w->toff, ntt + 1, s));
+    if (int rc = ensure_temp(c, w, tb)) return rc;
+    tb = w->temp_bytes;
+    HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(w->temp, tb, tlen, w->toff, ntt + 1, s));
+    k_cap_total<<<1, 64, 0, s>>>(w->toff, ntt, w->host_dev, kHNti);
+    w->host[kHNt] = ntt;
+  } else {
+    k_cap_tpack<<<grid_for(n), 256, 0, s>>>(w->state, c->rmeta, w->rlen, static_cast<int>(n), w->tv);
+    HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tb, w->tv, w->tvs, static_cast<int>(n), s));
+    if (int rc = ensure_temp(c, w, tb)) return rc;
+    tb = w->temp_bytes;
+    HIP_TRY(c, hipcub::DeviceScan::ExclusiveSum(w->temp, tb, w->tv, w->tvs, static_cast<int>(n), s));
+    k_cap_tlist<<<grid_for(n), 256, 0, s>>>(w->state, w->tv, w->tvs, static_cast<int>(n), w->T, w->toff, w->t_of,
+                                            w->host_dev);
+  }
   HIP_TRY(c, hipGetLastError());
   HIP_TRY(c, hipStreamSynchronize(s));
   w->nt = host_word(w, kHNt);
