@@ -444,9 +444,56 @@ __global__ __launch_bounds__(256) void k_cap_pkeys(const int* __restrict__ seq, 
   }
 }
 
-__global__ void k_cap_segb(const int* __restrict__ ioff, const int* __restrict__ toff, int nt, int* __restrict__ segb) {
-  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t <= nt; t += gridDim.x * blockDim.x) segb[t] = ioff[toff[t]];
+__global__ void k_cap_segb(const int* __restrict__ ioff, const int* __restrict__ toff, int nt, int* __restrict__ segb,
+                           unsigned* __restrict__ segmax) {
+  unsigned mx = 0;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t <= nt; t += gridDim.x * blockDim.x) {
+    segb[t] = ioff[toff[t]];
+    if (t < nt) mx = max(mx, static_cast<unsigned>(ioff[toff[t + 1]] - ioff[toff[t]]));
+  }
+  mx = block_reduce256(mx, [](unsigned x, unsigned y) { return max(x, y); });
+  if (threadIdx.x == 0 && mx) atomicMax(segmax, mx);
 }
+
+// ... in LDS: one workgroup per read of T whose segment has (lo, CAP] hits, a bitonic sort of
+// (partner << 32 | position) keys (positions ascending among equal partners, as the stable sorts)
+template <int CAP>
+__global__ __launch_bounds__(256) void k_cap_segsort(const int* __restrict__ seq, const int* __restrict__ segb, int nt,
+                                                     int lo, unsigned* __restrict__ pkey2, int* __restrict__ sval2) {
+  __shared__ unsigned long long buf[CAP];
+  for (int t = blockIdx.x; t < nt; t += gridDim.x) {
+    const int b = segb[t], n = segb[t + 1] - b;
+    if (n <= lo || n > CAP) continue;                // another size class (workgroup-uniform)
+    int P = 1;
+    while (P < n) P <<= 1;
+    for (int i = threadIdx.x; i < P; i += blockDim.x)
+      buf[i] = i < n ? (static_cast<unsigned long long>(static_cast<unsigned>(seq[b + i])) << 32) |
+                           static_cast<unsigned>(b + i)
+                     : ~0ull;
+    __syncthreads();
+    for (int k = 2; k <= P; k <<= 1)
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = threadIdx.x; i < P; i += blockDim.x) {
+          const int l = i ^ j;
+          if (l > i) {
+            const unsigned long long x = buf[i], y = buf[l];
+            if ((x > y) == ((i & k) == 0)) {
+              buf[i] = y;
+              buf[l] = x;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      const unsigned long long v = buf[i];
+      pkey2[b + i] = static_cast<unsigned>(v >> 32);
+      sval2[b + i] = static_cast<int>(static_cast<unsigned>(v));
+    }
+    __syncthreads();
+  }
+}
+constexpr int kSegSmall = 1024, kSegBig = 8192;
 
 __global__ __launch_bounds__(256) void k_cap_rekey(const unsigned* __restrict__ pkey, const int* __restrict__ segb,
                                                    int nt, unsigned long long* __restrict__ key) {
@@ -1864,12 +1911,15 @@ bool cap_runs_enabled() {
   return v;
 }
 
-// the slots' sort: segmented by read of T (default) or FSLR_CAP_SLOTSORT=global, one radix sort of
+// the slots' sort: per read of T in LDS (default; a segment of more than 8192 hits: the segmented
+// radix sort), FSLR_CAP_SLOTSORT=seg the segmented radix sort (hipcub), =global one radix sort of
 // (read, partner) keys over the whole sequence
-bool cap_slot_segmented() {
-  static const bool v = [] {
+int cap_slot_sort() {
+  static const int v = [] {
     const char* e = std::getenv("FSLR_CAP_SLOTSORT");
-    return !(e && std::strcmp(e, "global") == 0);
+    if (e && std::strcmp(e, "global") == 0) return 0;
+    if (e && std::strcmp(e, "seg") == 0) return 1;
+    return 2;
   }();
   return v;
 }
@@ -2153,13 +2203,26 @@ int cap_slots(fslr_ctx* c, CapWork* w) {
   CapTimer tm(s);
   size_t b1 = 0, b2 = 0, b3 = 0;
   const int kbits = 25 + bits_for(nt);
-  const bool seg = cap_slot_segmented();
+  int mode = cap_slot_sort();                                      // 0 global, 1 segmented radix, 2 LDS
   unsigned* pkey = reinterpret_cast<unsigned*>(w->skey);           // segmented: 32-bit partners
   unsigned* pkey2 = pkey + m;
   int* segb = reinterpret_cast<int*>(w->ck);                       // nt + 1 segment offsets (ck: 2 nt ints)
   const int pbits = bits_for(std::max<int64_t>(w->n, 1));
-  k_cap_segb<<<grid_for(nt + 1), 256, 0, s>>>(w->ioff, w->toff, nt, segb);
-  if (seg) {
+  unsigned* segmax = reinterpret_cast<unsigned*>(w->chg) + 8;
+  HIP_TRY(c, hipMemsetAsync(segmax, 0, sizeof(unsigned), s));
+  k_cap_segb<<<grid_for(nt + 1), 256, 0, s>>>(w->ioff, w->toff, nt, segb, segmax);
+  if (mode == 2) {
+    unsigned smax = 0;
+    HIP_TRY(c, hipMemcpyAsync(&smax, segmax, sizeof(smax), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    if (smax > static_cast<unsigned>(kSegBig)) mode = 1;          // a segment beyond the LDS sort
+  }
+  const bool seg = mode != 0;
+  if (mode == 2) {
+    k_cap_segsort<kSegSmall><<<std::min(nt, 8192), 256, 0, s>>>(w->seq, segb, nt, 0, pkey2, w->sval2);
+    k_cap_segsort<kSegBig><<<std::min(nt, 512), 256, 0, s>>>(w->seq, segb, nt, kSegSmall, pkey2, w->sval2);
+    HIP_TRY(c, hipGetLastError());
+  } else if (seg) {
     k_cap_pkeys<<<grid_for(m), 256, 0, s>>>(w->seq, m, pkey, w->sval);
     HIP_TRY(c, hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, b1, pkey, pkey2, w->sval, w->sval2, m, nt, segb,
                                                            segb + 1, 0, pbits, s));
@@ -2172,8 +2235,9 @@ int cap_slots(fslr_ctx* c, CapWork* w) {
   if (int rc = ensure_temp(c, w, std::max({b1, b2, b3}))) return rc;
   size_t tb = w->temp_bytes;
   if (seg) {
-    HIP_TRY(c, hipcub::DeviceSegmentedRadixSort::SortPairs(w->temp, tb, pkey, pkey2, w->sval, w->sval2, m, nt, segb,
-                                                           segb + 1, 0, pbits, s));
+    if (mode == 1)
+      HIP_TRY(c, hipcub::DeviceSegmentedRadixSort::SortPairs(w->temp, tb, pkey, pkey2, w->sval, w->sval2, m, nt, segb,
+                                                             segb + 1, 0, pbits, s));
     k_cap_rekey<<<wave_grid(nt), 256, 0, s>>>(pkey2, segb, nt, w->skey2);
   } else {
     HIP_TRY(c, hipcub::DeviceRadixSort::SortPairs(w->temp, tb, w->skey, w->skey2, w->sval, w->sval2, m, 0, kbits, s));
@@ -2291,21 +2355,22 @@ int cap_core(fslr_ctx* c, CapWork* w, fslr_cap_stats* cs) {
   // 5. the capped graph
   // edges formed per loop, from the E* forward degrees (fwd[x] = E* edges (x, .), as the query or the
   // install left them)
-  HIP_TRY(c, hipMemcpyAsync(w->formed, c->fwd, static_cast<size_t>(n) * sizeof(int), hipMemcpyDeviceToDevice, s));
+  if (!w->runs1)
+    HIP_TRY(c, hipMemcpyAsync(w->formed, c->fwd, static_cast<size_t>(n) * sizeof(int), hipMemcpyDeviceToDevice, s));
   if (w->runs1) {
+    // the forward degrees become the edges formed per loop in place (the changes move a few)
     // only T's runs can change: classified in place, then the dropped rows' holes filled
     unsigned* cnt = reinterpret_cast<unsigned*>(w->chg);          // [0] dropped, [1] holes, [2] survivors
     HIP_TRY(c, hipMemsetAsync(cnt, 0, 4 * sizeof(unsigned), s));
     if (nt > 0)
       k_cap_classify_runs<<<std::min(wave_grid(nt), 4096), 256, 0, s>>>(
-          c->edges, w->gstart, w->gend, w->T, nt, w->t_of, w->pbrk, w->ukey, w->tsb, w->fpos, w->vis2, w->formed,
+          c->edges, w->gstart, w->gend, w->T, nt, w->t_of, w->pbrk, w->ukey, w->tsb, w->fpos, w->vis2, c->fwd,
           w->kflag, cnt, w->stats, w->err);
     k_cap_holes<<<256, 256, 0, s>>>(w->kflag, cnt, ne, w->koff, cnt + 1);
     k_cap_survivors<<<256, 256, 0, s>>>(c->edges, cnt, ne, w->adj, cnt + 2);
     k_cap_fill<<<256, 256, 0, s>>>(c->edges, c->edge_iu, w->koff, w->adj, cnt + 1, w->err);
-    k_cap_check<<<grid_for(std::max<int64_t>(n, nt)), 256, 0, s>>>(w->T, nt, w->own, w->pbrk, w->formed,
+    k_cap_check<<<grid_for(std::max<int64_t>(n, nt)), 256, 0, s>>>(w->T, nt, w->own, w->pbrk, c->fwd,
                                                                    static_cast<int>(n), w->stats, w->err);
-    HIP_TRY(c, hipMemcpyAsync(c->fwd, w->formed, static_cast<size_t>(n) * sizeof(int), hipMemcpyDeviceToDevice, s));
     k_cap_commit_runs<<<1, 64, 0, s>>>(cnt, ne, c->counters, c->errw, w->stats, w->err, w->host_dev, false);
     HIP_TRY(c, hipGetLastError());
     HIP_TRY(c, hipStreamSynchronize(s));
