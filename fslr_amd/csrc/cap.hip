@@ -1911,15 +1911,16 @@ bool cap_runs_enabled() {
   return v;
 }
 
-// the slots' sort: per read of T in LDS (default; a segment of more than 8192 hits: the segmented
-// radix sort), FSLR_CAP_SLOTSORT=seg the segmented radix sort (hipcub), =global one radix sort of
-// (read, partner) keys over the whole sequence
+// the slots' sort: the segmented radix sort per read of T (hipcub, default), FSLR_CAP_SLOTSORT=lds a
+// bitonic sort per read in LDS (a segment of more than 8192 hits: the segmented sort; measured slower:
+// 3.32 vs 3.17 ms for the cfg5 replay), =global one radix sort of (read, partner) keys over the whole
+// sequence (3.57 ms)
 int cap_slot_sort() {
   static const int v = [] {
     const char* e = std::getenv("FSLR_CAP_SLOTSORT");
     if (e && std::strcmp(e, "global") == 0) return 0;
-    if (e && std::strcmp(e, "seg") == 0) return 1;
-    return 2;
+    if (e && std::strcmp(e, "lds") == 0) return 2;
+    return 1;
   }();
   return v;
 }
