@@ -679,24 +679,36 @@ __device__ __forceinline__ int find_slot(const unsigned long long* __restrict__ 
 
 // per slot (x, y): for an earlier partner y of T, the slot of (y, x) (where y's loop records
 // whether it reached x) and the union of x and y in the dependency graph
+// compact: the T-T pairs listed (nup of them), else one entry per slot ((-1, -1): none; the DAG replay)
 __global__ void k_cap_mirror(const unsigned long long* __restrict__ ukey, int ns, const int* __restrict__ tsb,
                              const int* __restrict__ T,
                              const int* __restrict__ t_of, int* __restrict__ mslot, int2* __restrict__ upairs,
-                             int* __restrict__ err) {
-  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < ns; s += gridDim.x * blockDim.x) {
-    const unsigned long long key = ukey[s];
-    const int t = static_cast<int>(key >> 25), y = static_cast<int>(key & kKeyMask);
-    const int x = T[t];
-    const int ty = y < x ? t_of[y] : -1;
-    int ms = -1;
-    int2 up = make_int2(-1, -1);
-    if (ty >= 0) {
-      ms = find_slot(ukey, tsb, ty, (static_cast<unsigned long long>(ty) << 25) | static_cast<unsigned>(x));
-      if (ms < 0) atomicOr(err, kCapErrState);          // hits are symmetric: cannot happen
-      up = make_int2(t, ty);
+                             unsigned* __restrict__ nup, bool compact, int* __restrict__ err) {
+  const int lane = threadIdx.x & 63;
+  for (int s0 = (blockIdx.x * blockDim.x + threadIdx.x) & ~63; s0 < ns; s0 += gridDim.x * blockDim.x) {
+    const int s = s0 + lane;
+    int ms = -1, t = 0, ty = -1;
+    if (s < ns) {
+      const unsigned long long key = ukey[s];
+      t = static_cast<int>(key >> 25);
+      const int y = static_cast<int>(key & kKeyMask);
+      const int x = T[t];
+      ty = y < x ? t_of[y] : -1;
+      if (ty >= 0) {
+        ms = find_slot(ukey, tsb, ty, (static_cast<unsigned long long>(ty) << 25) | static_cast<unsigned>(x));
+        if (ms < 0) atomicOr(err, kCapErrState);        // hits are symmetric: cannot happen
+      }
+      mslot[s] = ms;
+      if (!compact) upairs[s] = ty >= 0 ? make_int2(t, ty) : make_int2(-1, -1);
     }
-    mslot[s] = ms;
-    upairs[s] = up;
+    if (compact) {
+      const unsigned long long m = __ballot(ty >= 0);
+      if (!m) continue;
+      unsigned base = 0;
+      if (lane == 0) base = atomicAdd(nup, static_cast<unsigned>(__popcll(m)));
+      base = static_cast<unsigned>(__shfl(static_cast<int>(base), 0));
+      if (ty >= 0) upairs[base + mbcnt(m)] = make_int2(t, ty);
+    }
   }
 }
 
@@ -986,6 +998,8 @@ __global__ void k_cap_classify(const int2* __restrict__ edges, long long ne, con
 // only the rows of T's runs can change: they are classified in place, the dropped ones marked and
 // the list closed up by moving the few surviving rows behind the new end into the holes before it.
 // A read with two runs (another engine's order) flags the list: the full-list path runs instead.
+// (gstart, gend zeroed: a read without edges has the empty run [0, 0); a run's end is never 0, so a
+// second run of a read finds its end taken)
 __global__ void k_cap_runs1(const int2* __restrict__ e, long long ne, int* __restrict__ gstart, int* __restrict__ gend,
                             int* __restrict__ flag) {
   for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < ne;
@@ -993,14 +1007,9 @@ __global__ void k_cap_runs1(const int2* __restrict__ e, long long ne, int* __res
     const int a = e[k].x;
     const int prev = k ? e[k - 1].x : -1;
     const int next = k + 1 < ne ? e[k + 1].x : -1;
-    if (prev != a && atomicCAS(gstart + a, -1, static_cast<int>(k)) != -1) atomicOr(flag, 1);
-    if (next != a) gend[a] = static_cast<int>(k + 1);
+    if (prev != a) gstart[a] = static_cast<int>(k);
+    if (next != a && atomicCAS(gend + a, 0, static_cast<int>(k + 1)) != 0) atomicOr(flag, 1);
   }
-}
-
-__global__ void k_cap_runfix(int* __restrict__ gstart, int* __restrict__ gend, int n) {
-  for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < n; x += gridDim.x * blockDim.x)
-    if (gstart[x] < 0) gstart[x] = gend[x] = 0;
 }
 
 // one wavefront per read of T: its run's rows; re-oriented rows flipped in place, dropped rows marked
@@ -1808,6 +1817,11 @@ void fslr_cap_free(fslr_ctx* c) {
   c->capw = nullptr;
 }
 
+namespace fslr {
+hipError_t launch_uf_pair_list_dev(int* parent, const int2* pairs, const unsigned* n_dev, long long cap, int grid,
+                                   hipStream_t s);   // components.hip
+}  // namespace fslr
+
 namespace {
 
 // carve typed sub-arrays out of one arena (256-B aligned); grow it first if needed
@@ -2272,7 +2286,11 @@ int cap_loops(fslr_ctx* c, CapWork* w) {
   const int ns = static_cast<int>(w->ns);
   if (m > 0) {
     // mirror slots; each read's earlier T partners (its in-degree in the loops' dependency DAG)
-    k_cap_mirror<<<grid_for(ns), 256, 0, s>>>(w->ukey, ns, w->tsb, w->T, w->t_of, w->mslot, w->upairs, w->err);
+    unsigned* nup = reinterpret_cast<unsigned*>(w->chg) + 9;
+    const bool dag = cap_dag_enabled();
+    HIP_TRY(c, hipMemsetAsync(nup, 0, sizeof(unsigned), s));
+    k_cap_mirror<<<grid_for(ns), 256, 0, s>>>(w->ukey, ns, w->tsb, w->T, w->t_of, w->mslot, w->upairs, nup, !dag,
+                                              w->err);
     k_cap_recs<<<grid_for(m), 256, 0, s>>>(w->slot_of, w->ukey, w->fpos, w->flags, w->mslot, w->T, w->t_of, m, w->rec);
     HIP_TRY(c, hipMemsetAsync(w->vis2, 0, static_cast<size_t>(ns), s));
     tm.lap("loops: mirror");
@@ -2305,11 +2323,14 @@ int cap_loops(fslr_ctx* c, CapWork* w) {
     if (!dag_ok) {
       // the dependency components, one wavefront per component, its reads in rank order
       HIP_TRY(c, launch_uf_init(w->tpar, nt, s));
-      HIP_TRY(c, launch_uf_pair_list(w->tpar, w->upairs, ns, s));
+      if (dag)                                               // a stalled DAG replay: per-slot pairs
+        HIP_TRY(c, launch_uf_pair_list(w->tpar, w->upairs, ns, s));
+      else
+        HIP_TRY(c, launch_uf_pair_list_dev(w->tpar, w->upairs, nup, ns, std::min(grid_for(ns), 2048), s));
       HIP_TRY(c, launch_uf_finalize(w->tpar, nt, s));
       k_cap_ckeys<<<grid_for(nt), 256, 0, s>>>(w->tpar, nt, w->ck);
       size_t tb = w->temp_bytes;
-      HIP_TRY(c, hipcub::DeviceRadixSort::SortKeys(w->temp, tb, w->ck, w->ck2, nt, 0, 50, s));
+      HIP_TRY(c, hipcub::DeviceRadixSort::SortKeys(w->temp, tb, w->ck, w->ck2, nt, 0, 25 + bits_for(nt), s));
       tm.lap("loops: comps");
       if (cap_debug()) {
         std::vector<int> par(nt), toff(nt + 1), ioff(static_cast<size_t>(w->nti) + 1);
@@ -2466,10 +2487,10 @@ extern "C" int fslr_apply_edge_cap(fslr_ctx* c, int32_t thr, fslr_cap_stats* out
       if (int rc = cv.commit(c, w->ar[5])) return rc;
     }
     hipStream_t s = c->stream;
-    HIP_TRY(c, hipMemsetAsync(w->gstart, 0xff, static_cast<size_t>(n) * sizeof(int), s));
+    HIP_TRY(c, hipMemsetAsync(w->gstart, 0, static_cast<size_t>(n) * sizeof(int), s));
+    HIP_TRY(c, hipMemsetAsync(w->gend, 0, static_cast<size_t>(n) * sizeof(int), s));
     HIP_TRY(c, hipMemsetAsync(w->gflag, 0, 4 * sizeof(int), s));
     k_cap_runs1<<<grid_for(ne), 256, 0, s>>>(c->edges, ne, w->gstart, w->gend, w->gflag);
-    k_cap_runfix<<<grid_for(n), 256, 0, s>>>(w->gstart, w->gend, n);
     HIP_TRY(c, hipGetLastError());
     int flag = 0;
     HIP_TRY(c, hipMemcpyAsync(&flag, w->gflag, sizeof(int), hipMemcpyDeviceToHost, s));
