@@ -679,36 +679,24 @@ __device__ __forceinline__ int find_slot(const unsigned long long* __restrict__ 
 
 // per slot (x, y): for an earlier partner y of T, the slot of (y, x) (where y's loop records
 // whether it reached x) and the union of x and y in the dependency graph
-// compact: the T-T pairs listed (nup of them), else one entry per slot ((-1, -1): none; the DAG replay)
 __global__ void k_cap_mirror(const unsigned long long* __restrict__ ukey, int ns, const int* __restrict__ tsb,
                              const int* __restrict__ T,
                              const int* __restrict__ t_of, int* __restrict__ mslot, int2* __restrict__ upairs,
-                             unsigned* __restrict__ nup, bool compact, int* __restrict__ err) {
-  const int lane = threadIdx.x & 63;
-  for (int s0 = (blockIdx.x * blockDim.x + threadIdx.x) & ~63; s0 < ns; s0 += gridDim.x * blockDim.x) {
-    const int s = s0 + lane;
-    int ms = -1, t = 0, ty = -1;
-    if (s < ns) {
-      const unsigned long long key = ukey[s];
-      t = static_cast<int>(key >> 25);
-      const int y = static_cast<int>(key & kKeyMask);
-      const int x = T[t];
-      ty = y < x ? t_of[y] : -1;
-      if (ty >= 0) {
-        ms = find_slot(ukey, tsb, ty, (static_cast<unsigned long long>(ty) << 25) | static_cast<unsigned>(x));
-        if (ms < 0) atomicOr(err, kCapErrState);        // hits are symmetric: cannot happen
-      }
-      mslot[s] = ms;
-      if (!compact) upairs[s] = ty >= 0 ? make_int2(t, ty) : make_int2(-1, -1);
+                             int* __restrict__ err) {
+  for (int s = blockIdx.x * blockDim.x + threadIdx.x; s < ns; s += gridDim.x * blockDim.x) {
+    const unsigned long long key = ukey[s];
+    const int t = static_cast<int>(key >> 25), y = static_cast<int>(key & kKeyMask);
+    const int x = T[t];
+    const int ty = y < x ? t_of[y] : -1;
+    int ms = -1;
+    int2 up = make_int2(-1, -1);
+    if (ty >= 0) {
+      ms = find_slot(ukey, tsb, ty, (static_cast<unsigned long long>(ty) << 25) | static_cast<unsigned>(x));
+      if (ms < 0) atomicOr(err, kCapErrState);          // hits are symmetric: cannot happen
+      up = make_int2(t, ty);
     }
-    if (compact) {
-      const unsigned long long m = __ballot(ty >= 0);
-      if (!m) continue;
-      unsigned base = 0;
-      if (lane == 0) base = atomicAdd(nup, static_cast<unsigned>(__popcll(m)));
-      base = static_cast<unsigned>(__shfl(static_cast<int>(base), 0));
-      if (ty >= 0) upairs[base + mbcnt(m)] = make_int2(t, ty);
-    }
+    mslot[s] = ms;
+    upairs[s] = up;
   }
 }
 
@@ -1817,10 +1805,6 @@ void fslr_cap_free(fslr_ctx* c) {
   c->capw = nullptr;
 }
 
-namespace fslr {
-hipError_t launch_uf_pair_list_dev(int* parent, const int2* pairs, const unsigned* n_dev, long long cap, int grid,
-                                   hipStream_t s);   // components.hip
-}  // namespace fslr
 
 namespace {
 
@@ -2286,11 +2270,8 @@ int cap_loops(fslr_ctx* c, CapWork* w) {
   const int ns = static_cast<int>(w->ns);
   if (m > 0) {
     // mirror slots; each read's earlier T partners (its in-degree in the loops' dependency DAG)
-    unsigned* nup = reinterpret_cast<unsigned*>(w->chg) + 9;
-    const bool dag = cap_dag_enabled();
-    HIP_TRY(c, hipMemsetAsync(nup, 0, sizeof(unsigned), s));
-    k_cap_mirror<<<grid_for(ns), 256, 0, s>>>(w->ukey, ns, w->tsb, w->T, w->t_of, w->mslot, w->upairs, nup, !dag,
-                                              w->err);
+    // (one pair per slot, (-1, -1) for none: compacting the T-T pairs through one counter cost 0.9 ms)
+    k_cap_mirror<<<grid_for(ns), 256, 0, s>>>(w->ukey, ns, w->tsb, w->T, w->t_of, w->mslot, w->upairs, w->err);
     k_cap_recs<<<grid_for(m), 256, 0, s>>>(w->slot_of, w->ukey, w->fpos, w->flags, w->mslot, w->T, w->t_of, m, w->rec);
     HIP_TRY(c, hipMemsetAsync(w->vis2, 0, static_cast<size_t>(ns), s));
     tm.lap("loops: mirror");
@@ -2323,10 +2304,7 @@ int cap_loops(fslr_ctx* c, CapWork* w) {
     if (!dag_ok) {
       // the dependency components, one wavefront per component, its reads in rank order
       HIP_TRY(c, launch_uf_init(w->tpar, nt, s));
-      if (dag)                                               // a stalled DAG replay: per-slot pairs
-        HIP_TRY(c, launch_uf_pair_list(w->tpar, w->upairs, ns, s));
-      else
-        HIP_TRY(c, launch_uf_pair_list_dev(w->tpar, w->upairs, nup, ns, std::min(grid_for(ns), 2048), s));
+      HIP_TRY(c, launch_uf_pair_list(w->tpar, w->upairs, ns, s));
       HIP_TRY(c, launch_uf_finalize(w->tpar, nt, s));
       k_cap_ckeys<<<grid_for(nt), 256, 0, s>>>(w->tpar, nt, w->ck);
       size_t tb = w->temp_bytes;

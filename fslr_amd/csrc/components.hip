@@ -81,17 +81,6 @@ __global__ void k_uf_pair_list(int* p, const int2* __restrict__ pairs, long long
   }
 }
 
-// ... with the count on the device (a compacted list; at most cap pairs)
-__global__ void k_uf_pair_list_dev(int* p, const int2* __restrict__ pairs, const unsigned* __restrict__ n_dev,
-                                   long long cap) {
-  const long long n = min(static_cast<long long>(*n_dev), cap);
-  for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < n;
-       k += static_cast<long long>(gridDim.x) * blockDim.x) {
-    const int2 e = pairs[k];
-    if (e.x >= 0) uf_union(p, e.x, e.y);
-  }
-}
-
 // W label blocks of n values at vals + w * stride (the multi-GPU cap's gathered forests): union of
 // k and vals[w * stride + k] for every block w
 __global__ void k_uf_strided(int* p, const int* __restrict__ vals, long long blocks, int n, long long stride) {
@@ -221,12 +210,6 @@ hipError_t launch_uf_pairs(int* parent, const int* src, const int* dst, long lon
 
 hipError_t launch_uf_pair_list(int* parent, const int2* pairs, long long n, hipStream_t s) {
   if (n > 0) k_uf_pair_list<<<grid_for(n), 256, 0, s>>>(parent, pairs, n);
-  return hipGetLastError();
-}
-
-hipError_t launch_uf_pair_list_dev(int* parent, const int2* pairs, const unsigned* n_dev, long long cap, int grid,
-                                   hipStream_t s) {
-  if (cap > 0) k_uf_pair_list_dev<<<grid, 256, 0, s>>>(parent, pairs, n_dev, cap);
   return hipGetLastError();
 }
 

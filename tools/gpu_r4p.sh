@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round-4: compacted T-T pairs, narrower component keys, run detection without the fix-up pass: suite,
+# Round-4: narrower component keys, run detection without the fix-up pass (and, measured slower and
+# reverted, compacted T-T pairs): suite,
 # cfg5 cap (stage times, clean), sharded model at W=8.
 set -o pipefail
 TAG=${1:-r4p}
