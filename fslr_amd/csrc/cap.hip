@@ -1923,6 +1923,17 @@ int cap_slot_sort() {
   return v;
 }
 
+// workgroups of a frontier round (grid-stride over the frontier; most rounds' frontiers are a few
+// thousand reads, and a round's launch cost grows with its workgroups): FSLR_CAP_FGRID, default 256
+int cap_frontier_grid() {
+  static const int v = [] {
+    const char* e = std::getenv("FSLR_CAP_FGRID");
+    const int g = e ? std::atoi(e) : 256;
+    return g >= 1 && g <= 65536 ? g : 256;
+  }();
+  return v;
+}
+
 bool cap_dag_enabled() {
   static const bool v = [] {
     const char* e = std::getenv("FSLR_CAP_REPLAY");
@@ -2029,12 +2040,13 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, const int2* E, const int* F, int
     int* fl[2] = {w->fl0, w->fl1};
     for (int batch = 0;; ++batch) {
       // rounds r = 0 .. 15 of the batch: frontier fl[r & 1] (count fcnt[r]) -> fl[(r + 1) & 1] (fcnt[r + 1])
+      const int fg = cap_frontier_grid();
       for (int r = 0; r < 16; ++r) {
         if (rstart)
-          k_cap_frontier_rows<<<1024, 256, 0, s>>>(rstart, rend, E, F, thr, w->state, w->back, fl[r & 1], w->fcnt + r,
+          k_cap_frontier_rows<<<fg, 256, 0, s>>>(rstart, rend, E, F, thr, w->state, w->back, fl[r & 1], w->fcnt + r,
                                                    fl[(r + 1) & 1], w->fcnt + r + 1, w->tl, w->fcnt + 32);
         else
-          k_cap_frontier<<<1024, 256, 0, s>>>(w->aoff, w->adj, F, thr, w->state, w->back, fl[r & 1], w->fcnt + r,
+          k_cap_frontier<<<fg, 256, 0, s>>>(w->aoff, w->adj, F, thr, w->state, w->back, fl[r & 1], w->fcnt + r,
                                               fl[(r + 1) & 1], w->fcnt + r + 1, w->tl, w->fcnt + 32);
       }
       HIP_TRY(c, hipGetLastError());
