@@ -1923,13 +1923,13 @@ int cap_slot_sort() {
   return v;
 }
 
-// workgroups of a frontier round (grid-stride over the frontier; most rounds' frontiers are a few
-// thousand reads, and a round's launch cost grows with its workgroups): FSLR_CAP_FGRID, default 256
+// workgroups of a frontier round (grid-stride over the frontier): FSLR_CAP_FGRID, default 1024 (256 and
+// 128 measured the same on the cfg5 replay, profiles/r04/r4r/)
 int cap_frontier_grid() {
   static const int v = [] {
     const char* e = std::getenv("FSLR_CAP_FGRID");
-    const int g = e ? std::atoi(e) : 256;
-    return g >= 1 && g <= 65536 ? g : 256;
+    const int g = e ? std::atoi(e) : 1024;
+    return g >= 1 && g <= 65536 ? g : 1024;
   }();
   return v;
 }
