@@ -181,10 +181,13 @@ def load(path: str = LIB_PATH):
         fn.argtypes = args
     if L.fslr_abi_version() != ABI_VERSION:
         raise HipUnavailable(f'{path} has ABI {L.fslr_abi_version()}, this binding needs {ABI_VERSION}: rebuild it')
-    L.fslr_source_hash.restype = ctypes.c_char_p
-    L.fslr_source_hash.argtypes = []
     want = source_hash()
     if want is not None and os.environ.get('FSLR_ALLOW_STALE') != '1':
+        if not hasattr(L, 'fslr_source_hash'):
+            raise HipUnavailable(f'{path} carries no source hash (fslr_source_hash): rebuild it (make -C fslr_amd/csrc), '
+                                 f'or set FSLR_ALLOW_STALE=1 to load it anyway')
+        L.fslr_source_hash.restype = ctypes.c_char_p
+        L.fslr_source_hash.argtypes = []
         got = L.fslr_source_hash().decode()
         if got != want:
             raise HipUnavailable(f'{path} was built from other sources (hash {got}, the sources beside it hash to '

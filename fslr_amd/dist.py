@@ -384,9 +384,11 @@ class SweepShard:
         mf = int(st['max_fwd'])
         max_ne = int(st['n_edges'])
         max_fp = 0
-        if W > 1 and err is None:
+        if W > 1 and err is None and mf <= edge_threshold:
+            # this rank's forest: the merge exchanges its pairs (not built when this rank already knows
+            # the cap binds: the capped graph's forest replaces it)
             try:
-                max_fp = ctx.local_forest()         # this rank's forest: the merge exchanges its pairs
+                max_fp = ctx.local_forest()
             except Exception as e:                  # noqa: BLE001 - re-raised on every rank below
                 err = e
         if W > 1:
@@ -502,11 +504,12 @@ class SweepShard:
         ctx, W, r = self.ctx, self.world, self.rank
         m = max(1, int(max_ne))
         err = None
-        self.esend = self._grow(self.esend, m)
-        self.egath = self._grow(self.egath, W * m)
         restricted = os.environ.get('FSLR_CAP_GATHER', 'restricted') != 'full'
         try:
             if not restricted:
+                # every E* row travels: only this branch sizes the buffers for W * max_ne rows
+                self.esend = self._grow(self.esend, m)
+                self.egath = self._grow(self.egath, W * m)
                 ctx.sort_edges()                 # each read's forward rows one run of the gathered rows
             else:
                 # only the rows of S = {x : fwd(x) + bwd(x) >= threshold} travel (bwd summed over ranks)

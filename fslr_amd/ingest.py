@@ -26,6 +26,10 @@ HOT_COLUMNS = ('chrom', 'rstart', 'rend', 'qname', 'n_alignments', 'aln_size', '
 _lib = None
 
 
+class StaleLibrary(FileNotFoundError):
+    """The reader library exists but was built from sources without an entry point this binding needs."""
+
+
 def load(path: str = LIB_PATH):
     global _lib
     if _lib is not None:
@@ -55,6 +59,10 @@ def load(path: str = LIB_PATH):
         'fslr_argsort_distinct': (i32, [vp, i64, vp, i32]),
         'fslr_fillings': (i32, [i64, vp, i64, vp] + [vp] * 8 + [vp] + [vp] * 8 + [i32]),
     }
+    missing = [name for name in sig if not hasattr(L, name)]
+    if missing:
+        # a library built from older sources: every caller treats it as not built (pandas / numpy)
+        raise StaleLibrary(f'{path} lacks {", ".join(missing)}: rebuild it (make -C fslr_amd/csrc)')
     for name, (res, args) in sig.items():
         f = getattr(L, name)
         f.restype, f.argtypes = res, args
