@@ -13,7 +13,7 @@ import numpy as np
 
 LIB_PATH = os.environ.get('FSLR_LIB') or os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libfslr_hip.so')
 
-ABI_VERSION = 14         # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
+ABI_VERSION = 15         # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
 FSLR_OK, FSLR_ERR_ZERO_DIVISION, FSLR_ERR_INVALID, FSLR_ERR_HIP, FSLR_ERR_NOMEM, FSLR_ERR_STATE = range(6)
 FSLR_MAX_L = 64
 FSLR_MAX_READS = 1 << 25
@@ -71,7 +71,7 @@ class QueryStats(ctypes.Structure):
                 ('matched_pairs', ctypes.c_int64), ('deferred', ctypes.c_int64),
                 ('deferred_capacity', ctypes.c_int64), ('edge_capacity', ctypes.c_int64),
                 ('walked_records', ctypes.c_int64), ('engine', ctypes.c_int32), ('overflow_flags', ctypes.c_int32),
-                ('pair_tests', ctypes.c_int64), ('entry_capacity', ctypes.c_int64)]
+                ('pair_tests', ctypes.c_int64), ('entry_capacity', ctypes.c_int64), ('zd_pairs', ctypes.c_int64)]
 
     def as_dict(self):
         d = {f: getattr(self, f) for f, _ in self._fields_}
@@ -561,6 +561,8 @@ class Context:
                 engine = 'walk'
                 grow = True
             if st['overflow_flags'] & 24:         # sweep entry buffers (a sync-free repeat query): rerun
+                grow = True
+            if st['overflow_flags'] & 64:         # the ZeroDivisionError pair list (the cap binds): rerun
                 grow = True
             if st['n_edges'] > st['edge_capacity']:
                 self.reserve_edges(int(st['n_edges'] * 1.25) + 4096)

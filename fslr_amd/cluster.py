@@ -439,6 +439,10 @@ def _query_long(idx, overlap_cutoff, jaccard_threshold, edge_threshold, qlen_dif
         engine = 'pairs'
     fwd = np.bincount(a, minlength=n).astype(np.int32)
     max_fwd = int(fwd.max()) if n else 0
+    if st.get('zd_pairs', 0) and max_fwd <= int(edge_threshold):
+        # every loop runs to its end, so each listed pair is visited (cluster.py:178-183, 133-136); with
+        # the cap binding the replay decides (fslr_cap_replay_pairs raises where a loop reaches one)
+        raise ZeroDivisionError('division by zero')
     cap = {'applied': 0, 'max_fwd': max_fwd}
     if max_fwd > int(edge_threshold):
         # the capped graph: edge k kept when formed in a loop, re-oriented as (former, partner)

@@ -61,7 +61,7 @@ enum CapErr { kCapErrZd = 1, kCapErrState = 2 };
 // device statistics words
 enum CapStat { kStCapped = 0, kStDropped, kStBackward, kStMaxFwd, kStKept, kStWords = 8 };
 // pinned host words (written by tiny kernels; one sync each)
-enum CapHost { kHNt = 0, kHNti, kHNloc, kHNslots, kHNseq, kHErr, kHStat = 8, kHWords = 16 };
+enum CapHost { kHNt = 0, kHNti, kHNloc, kHNslots, kHNseq, kHErr, kHZd, kHStat = 8, kHWords = 16 };
 
 // one value per block: the wavefronts' values combined in LDS, valid in thread 0 (call from every thread
 // of the block; 256 threads).  A per-block atomic instead of one per wavefront: one hot word takes
@@ -1224,18 +1224,37 @@ __global__ void k_copy_edges_iu(const int2* __restrict__ edges, const unsigned s
     out[k] = k < ne ? make_int4(edges[k].x, edges[k].y, iu[k], 0) : make_int4(-1, -1, 0, 0);
 }
 
+// The query's ZeroDivisionError pairs (kernels.hpp kErrZdCount) against the candidates T: a pair with a
+// read outside T is visited by that read's loop, which never breaks (or earlier by the other read's), so
+// the reference raises (cluster.py:205-209, 179-181); pairs of two T reads are left to the replay, which
+// raises where a replayed loop reaches one.  host[0]: 1 raise, 2 the list overflowed (undecidable), 0.
+__global__ __launch_bounds__(256) void k_cap_zd_outside(const int* __restrict__ errw, const int* __restrict__ t_of,
+                                                         long long* __restrict__ host) {
+  const int cnt = errw[kErrZdCount], cap = errw[kErrZdCap];
+  const int m = min(cnt, cap);
+  const int2* L = reinterpret_cast<const int2*>(errw + kErrZdList);
+  bool out = false;
+  for (int k = threadIdx.x; k < m; k += blockDim.x) {
+    const int2 p = L[k];
+    out = out || t_of[p.x] < 0 || t_of[p.y] < 0;
+  }
+  out = __syncthreads_or(out);
+  if (threadIdx.x == 0) host[0] = out ? 1 : (cnt > cap ? 2 : 0);
+}
+
 // fslr_long_pairs: each unordered pair once (the slot of its lower-rank read), its edge (a, b, I, U)
-// appended to the long-edge list and to the context's edges; a ZeroDivisionError flag stops the query
+// appended to the long-edge list and to the context's edges; a pair that raises ZeroDivisionError is
+// listed in the error words (the caller decides once the edge cap's binding is known)
 __global__ void k_cap_pairs_out(const unsigned long long* __restrict__ ukey, int ns, const int* __restrict__ T,
                                 const int2* __restrict__ flags, int4* __restrict__ out4, long long cap4,
                                 int2* __restrict__ edges, unsigned short* __restrict__ edge_iu, long long edge_cap,
-                                unsigned long long* __restrict__ cnt, int* __restrict__ fwd, int* __restrict__ err) {
+                                unsigned long long* __restrict__ cnt, int* __restrict__ fwd, int* __restrict__ errw) {
   for (int sl = blockIdx.x * blockDim.x + threadIdx.x; sl < ns; sl += gridDim.x * blockDim.x) {
     const unsigned long long key = ukey[sl];
     const int x = T[key >> 25], y = static_cast<int>(key & kKeyMask);
     if (y < x) continue;
     const int2 f = flags[sl];
-    if (f.x & 1) atomicOr(err, kCapErrZd);
+    raise_zd(errw, f.x & 1, x, y);
     if (!(f.x & 4)) continue;
     const int I = f.y & 0xffff, U = f.y >> 16;
     const unsigned long long k = atomicAdd(cnt, 1ull);
@@ -1244,7 +1263,7 @@ __global__ void k_cap_pairs_out(const unsigned long long* __restrict__ ukey, int
       edges[k] = make_int2(x, y);
       edge_iu[k] = static_cast<unsigned short>(min(I, 255) | (min(U, 255) << 8));
     }
-    atomicAdd(fwd + x, 1);
+    atomicMax(errw + 3, atomicAdd(fwd + x, 1) + 1);     // the forward-degree maximum (cap binding)
   }
 }
 
@@ -2109,10 +2128,14 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, const int2* E, const int* F, int
     k_cap_tlist<<<grid_for(n), 256, 0, s>>>(w->state, w->tv, w->tvs, static_cast<int>(n), w->T, w->toff, w->t_of,
                                             w->host_dev);
   }
+  if (!all_reads) k_cap_zd_outside<<<1, 256, 0, s>>>(c->errw, w->t_of, w->host_dev + kHZd);
   HIP_TRY(c, hipGetLastError());
   HIP_TRY(c, hipStreamSynchronize(s));
   w->nt = host_word(w, kHNt);
   w->nti = host_word(w, kHNti);
+  if (!all_reads && host_word(w, kHZd) == 1) return fail(c, FSLR_ERR_ZERO_DIVISION, "division by zero");
+  if (!all_reads && host_word(w, kHZd) == 2)
+    return fail(c, FSLR_ERR_STATE, "too many ZeroDivisionError pairs to replay the edge cap; rerun the query");
   const int nt = static_cast<int>(w->nt), nti = static_cast<int>(w->nti);
   {
     Carve cv;
@@ -2427,7 +2450,7 @@ int cap_core(fslr_ctx* c, CapWork* w, fslr_cap_stats* cs) {
 
 // edge count, max forward degree; FSLR_OK and *binds = false when E* is the reference's graph
 int cap_peek(fslr_ctx* c, int thr, int64_t* ne, bool* binds) {
-  long long pk[3] = {0, 0, 0};
+  long long pk[4] = {0, 0, 0, 0};
   if (c->counters) {
     if (int rc = peek_counts(c, pk)) return rc;
   } else {
@@ -2435,6 +2458,9 @@ int cap_peek(fslr_ctx* c, int thr, int64_t* ne, bool* binds) {
   }
   if (pk[1] == FSLR_ERR_ZERO_DIVISION) return fail(c, FSLR_ERR_ZERO_DIVISION, "division by zero");
   *ne = pk[0];
+  // a listed ZeroDivisionError pair raises when every loop runs to its end (the cap does not bind);
+  // otherwise only where a loop reaches it (cap_local: a pair with a read outside T; the replay)
+  if (pk[3] > 0 && !c->cap_stats.applied && pk[2] <= thr) return fail(c, FSLR_ERR_ZERO_DIVISION, "division by zero");
   if (*ne > c->edge_cap) return fail(c, FSLR_ERR_STATE, "edge buffer overflowed; reserve and rerun the query");
   *binds = !c->cap_stats.applied && pk[2] > thr;
   if (!*binds && !c->cap_stats.applied) {
@@ -2673,19 +2699,18 @@ extern "C" int fslr_long_pairs(fslr_ctx* c, const fslr_params* p, int64_t* n_edg
   if (!c->lg_cnt && dalloc(c, &c->lg_cnt, 4)) return FSLR_ERR_NOMEM;
   HIP_TRY(c, hipMemsetAsync(c->lg_cnt, 0, 4 * sizeof(unsigned long long), s));
   HIP_TRY(c, hipMemsetAsync(c->fwd, 0, static_cast<size_t>(c->n) * sizeof(int), s));
-  HIP_TRY(c, hipMemsetAsync(c->errw, 0, kErrSticky * sizeof(int), s));
+  HIP_TRY(c, hipMemsetAsync(c->errw, 0, kErrSticky * sizeof(int), s));   // ZeroDivisionError pairs included
+  c->q_thr = p->edge_threshold;
+  c->zd_host = true;
   if (ns > 0)
     k_cap_pairs_out<<<grid_for(ns), 256, 0, s>>>(w->ukey, ns, w->T, w->flags, c->lg_edges, c->lg_edge_cap, c->edges,
-                                                  c->edge_iu, c->edge_cap, c->lg_cnt, c->fwd, w->err);
+                                                  c->edge_iu, c->edge_cap, c->lg_cnt, c->fwd, c->errw);
   HIP_TRY(c, hipGetLastError());
   unsigned long long cnt = 0;
-  int err = 0;
   HIP_TRY(c, hipMemcpyAsync(&cnt, c->lg_cnt, sizeof(cnt), hipMemcpyDeviceToHost, s));
-  HIP_TRY(c, hipMemcpyAsync(&err, w->err, sizeof(int), hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipMemcpyAsync(c->counters + kEdgeCount, &cnt, sizeof(cnt), hipMemcpyHostToDevice, s));
   HIP_TRY(c, hipStreamSynchronize(s));
   w->prepared = false;
-  if (err & kCapErrZd) return fail(c, FSLR_ERR_ZERO_DIVISION, "division by zero");
   c->lg_n_edges = static_cast<int64_t>(cnt);
   c->last_engine = FSLR_ENGINE_WALK;
   *n_edges = c->lg_n_edges;
@@ -2717,7 +2742,7 @@ extern "C" int fslr_cap_replay_pairs(fslr_ctx* c, int32_t thr, const int32_t* a,
   HIP_TRY(c, hipMemcpyAsync(c->fwd, deg.data(), deg.size() * sizeof(int), hipMemcpyHostToDevice, s));
   const unsigned long long ne_u = static_cast<unsigned long long>(ne);
   HIP_TRY(c, hipMemcpyAsync(c->counters + kEdgeCount, &ne_u, sizeof(ne_u), hipMemcpyHostToDevice, s));
-  int ew[kErrWords] = {};
+  int ew[kErrZdCount] = {};                 // the query's ZeroDivisionError pairs stay listed (cap_local)
   ew[3] = max_fwd;
   HIP_TRY(c, hipMemcpyAsync(c->errw, ew, sizeof(ew), hipMemcpyHostToDevice, s));
   HIP_TRY(c, hipStreamSynchronize(s));
@@ -2821,7 +2846,7 @@ extern "C" int fslr_cap_bwd_counts(fslr_ctx* c, int32_t thr, void* out, int32_t 
   if (!c->counters) return fail(c, FSLR_ERR_STATE, "no query has run");
   HIP_TRY(c, hipSetDevice(c->device));
   hipStream_t s = c->stream;
-  long long pk[3] = {0, 0, 0};
+  long long pk[4] = {0, 0, 0, 0};
   if (int rc = peek_counts(c, pk)) return rc;
   const int64_t ne = std::min<int64_t>(pk[0], c->edge_cap), n = c->n;
   if (ne >= (int64_t(1) << 31)) return fail(c, FSLR_ERR_INVALID, "too many edges for the restricted gather");
@@ -3309,7 +3334,7 @@ extern "C" int fslr_sort_edges(fslr_ctx* c) {
   HIP_TRY(c, hipSetDevice(c->device));
   if (!c->counters || !c->edge_cap) return FSLR_OK;
   hipStream_t s = c->stream;
-  long long pk[3] = {0, 0, 0};
+  long long pk[4] = {0, 0, 0, 0};
   if (int rc = peek_counts(c, pk)) return rc;
   const int64_t ne = std::min<int64_t>(pk[0], c->edge_cap);
   if (ne < 2) return FSLR_OK;

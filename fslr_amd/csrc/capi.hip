@@ -16,6 +16,8 @@ using namespace fslr;
 
 namespace {
 
+int alloc_errw(fslr_ctx* c, int cap);
+
 int ensure_capacity(fslr_ctx* c, int64_t n, int64_t ni, int n_chroms) {
   int rc;
   if (n > c->cap_n) {
@@ -55,13 +57,23 @@ int ensure_capacity(fslr_ctx* c, int64_t n, int64_t ni, int n_chroms) {
   if (!c->umax) {
     if ((rc = dalloc(c, &c->umax, FSLR_MAX_L))) return rc;
     if ((rc = dalloc(c, &c->counters, kNumCounters))) return rc;
-    if ((rc = dalloc(c, &c->errw, kErrWords))) return rc;
+    if ((rc = alloc_errw(c, kZdListInit))) return rc;
     if ((rc = dalloc(c, &c->forest_cnt, 1))) return rc;
     if ((rc = dalloc(c, &c->forest_blk, 1024))) return rc;
     // no query yet: no edges, no errors (fslr_components before any query gives singleton labels)
     HIP_TRY(c, hipMemsetAsync(c->counters, 0, kNumCounters * sizeof(unsigned long long), c->stream));
-    HIP_TRY(c, hipMemsetAsync(c->errw, 0, kErrWords * sizeof(int), c->stream));
   }
+  return FSLR_OK;
+}
+
+// the error words and the ZeroDivisionError pair list after them (kernels.hpp kErrZdList), zeroed, with
+// the list's capacity in word kErrZdCap
+int alloc_errw(fslr_ctx* c, int cap) {
+  if (int rc = dalloc(c, &c->errw, kErrZdList + 2 * static_cast<size_t>(cap))) return rc;
+  c->zd_cap = cap;
+  HIP_TRY(c, hipMemsetAsync(c->errw, 0, kErrZdList * sizeof(int), c->stream));
+  HIP_TRY(c, hipMemcpyAsync(c->errw + kErrZdCap, &c->zd_cap, sizeof(int), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
   return FSLR_OK;
 }
 
@@ -433,10 +445,11 @@ __global__ void k_peek(const unsigned long long* counters, const int* err, long 
     out[0] = static_cast<long long>(counters[kEdgeCount]);
     out[1] = err[0];
     out[2] = err[3];
+    out[3] = err[kErrZdCount];
   }
 }
 
-int fslr::peek_counts(fslr_ctx* c, long long out[3]) {
+int fslr::peek_counts(fslr_ctx* c, long long out[4]) {
   if (!c->sw_total) {
     HIP_TRY(c, hipHostMalloc(reinterpret_cast<void**>(&c->sw_total), 8 * sizeof(long long), hipHostMallocMapped));
     HIP_TRY(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->sw_total_dev), c->sw_total, 0));
@@ -445,7 +458,7 @@ int fslr::peek_counts(fslr_ctx* c, long long out[3]) {
   HIP_TRY(c, hipGetLastError());
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   const volatile long long* v = c->sw_total + 4;
-  for (int k = 0; k < 3; ++k) out[k] = v[k];
+  for (int k = 0; k < 4; ++k) out[k] = v[k];
   return FSLR_OK;
 }
 
@@ -688,7 +701,8 @@ static int sweep_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_
 }
 
 // buffers, the folded cut table and cleared counters / errors / forward degrees for one query
-// keep_sticky: the repeat-partition flags (kErrSticky) survive (a repeat partition and the
+// keep_sticky: the repeat-partition flags (kErrSticky) and the ZeroDivisionError pairs of the partition
+// (kErrZdCount) survive (a repeat partition and the
 // evaluations after it); any other query starts a new series and clears them
 static int prepare_query(fslr_ctx* c, const fslr_params* p, bool keep_sticky = false) {
   HIP_TRY(c, hipSetDevice(c->device));
@@ -723,7 +737,7 @@ static int prepare_query(fslr_ctx* c, const fslr_params* p, bool keep_sticky = f
     if (rc) return rc;
     c->wstat_waves = w;
   }
-  HIP_TRY(c, launch_query_reset(c->counters, kNumCounters, c->errw, keep_sticky ? kErrSticky : kErrWords, c->fwd,
+  HIP_TRY(c, launch_query_reset(c->counters, kNumCounters, c->errw, keep_sticky ? kErrKeep : kErrWords, c->fwd,
                                 static_cast<int>(c->n),
                                 c->stream));
   std::memset(&c->cap_stats, 0, sizeof(c->cap_stats));
@@ -731,6 +745,8 @@ static int prepare_query(fslr_ctx* c, const fslr_params* p, bool keep_sticky = f
   c->cap_gmode = false;
   c->last_qcut = p->qlen_cut;                       // the cap replay's pair predicate
   c->last_ncut = p->nal_cut;
+  c->q_thr = p->edge_threshold;
+  c->zd_host = true;                                // fslr_query clears it: there the library decides
   return FSLR_OK;
 }
 
@@ -740,6 +756,7 @@ static int query_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_
     return fail(c, FSLR_ERR_STATE, "the index covers a chromosome subset (fslr_set_chrom_filter): use "
                                    "fslr_sweep_partition / fslr_sweep_evaluate");
   if (int rc = prepare_query(c, p)) return rc;
+  c->zd_host = false;
   QueryArgs g;
   g.rmeta = c->rmeta;
   g.iv = c->iv;
@@ -900,10 +917,8 @@ int fslr_sweep_partition(fslr_ctx* c, const fslr_params* p, int32_t n_dest, int3
     if (int rc = read_back()) return rc;
   }
   c->t_kernel_rec = k0 != nullptr;
-  if (ew[0] == FSLR_ERR_ZERO_DIVISION) {
-    c->err = "division by zero";
-    return FSLR_ERR_ZERO_DIVISION;
-  }
+  // ZeroDivisionError pairs are listed (ew[kErrZdCount]), not raised: the caller decides once the edge
+  // cap's binding is known over every rank (fslr_read_stats zd_pairs)
   int64_t sum = 0;
   for (int k = 0; k < n_dest; ++k) sum += (counts[k] = tot[k]);
   c->pt_gen = 0;
@@ -1088,9 +1103,27 @@ int fslr_read_stats(fslr_ctx* c, fslr_query_stats* out) {
   out->err_a = ew[1];
   out->err_b = ew[2];
   out->max_fwd = ew[3];
-  if (ew[0] == FSLR_ERR_ZERO_DIVISION) {
-    c->err = "division by zero";
-    return FSLR_ERR_ZERO_DIVISION;
+  out->zd_pairs = ew[kErrZdCount];
+  if (ew[kErrZdCount] > 0) {
+    // the first listed pair; whether the reference raises: every pair is visited when the cap does not
+    // bind (max_fwd <= edge_threshold), otherwise fslr_apply_edge_cap decides (the loops that break)
+    int2 first = make_int2(0, 0);
+    HIP_TRY(c, hipMemcpyAsync(&first, c->errw + kErrZdList, sizeof(first), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    out->err_a = first.x;
+    out->err_b = first.y;
+    const bool binds = ew[3] > c->q_thr;
+    if (!c->zd_host && !binds) {
+      out->error = FSLR_ERR_ZERO_DIVISION;
+      c->err = "division by zero";
+      return FSLR_ERR_ZERO_DIVISION;
+    }
+    if (!c->zd_host && ew[kErrZdCount] > c->zd_cap) {
+      // the cap's replay needs every pair: a longer list, and the query again
+      if (int rc = alloc_errw(c, std::max(2 * c->zd_cap, ew[kErrZdCount] + (ew[kErrZdCount] >> 2)))) return rc;
+      out->overflow_flags |= 64;
+      return fail(c, FSLR_ERR_STATE, "ZeroDivisionError pair list overflowed; rerun the query");
+    }
   }
   if (out->deferred > c->defer_cap) return fail(c, FSLR_ERR_STATE, "deferred list overflowed; reserve and rerun");
   if (out->n_edges > c->edge_cap) return fail(c, FSLR_ERR_STATE, "edge buffer overflowed; reserve and rerun");

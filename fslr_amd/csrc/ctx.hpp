@@ -92,7 +92,11 @@ struct fslr_ctx {
   unsigned long long* wstat = nullptr;       // [wstat_waves x kWStride] per-wave statistics of the pair kernel
   int wstat_waves = 0;
   unsigned long long* diag = nullptr;        // FSLR_SECTION_PROF builds: per-read timing of the pair kernel
-  int* errw = nullptr;     // [0..2] error, [3] max_fwd
+  int* errw = nullptr;     // [0..2] error, [3] max_fwd, ... then the ZeroDivisionError pair list (kernels.hpp)
+  int zd_cap = 0;          // capacity of that list (pairs)
+  bool zd_host = false;    // the last query's ZeroDivisionError pairs are decided by the caller (a partition,
+                           // an evaluation or a long-read query: the edge cap's binding is known there)
+  int q_thr = 0;           // the last query's edge_threshold (fslr_read_stats: does the cap bind?)
   // position-sweep engine (sweep.hip)
   long long* sw_tile = nullptr;             // [4 x tiles]: entries, their scan, pair tests, their scan
   long long* sw_total = nullptr;            // [4] pinned host memory, device-mapped: entries, bound, flags
@@ -182,7 +186,7 @@ namespace fslr {
 // builds the walk engine's index parts of a sweep-only index (capi.hip); no-op when present
 int ensure_walk_index(fslr_ctx* c);
 // {edge count, error code, max forward degree} of the last query through pinned memory; syncs
-int peek_counts(fslr_ctx* c, long long out[3]);
+int peek_counts(fslr_ctx* c, long long out[4]);   // edges, err code, max_fwd, ZeroDivisionError pairs
 // the backward scan ranges of the (possibly chromosome-filtered) index, without the CSR map (capi.hip)
 int ensure_bwd_ranges(fslr_ctx* c);
 

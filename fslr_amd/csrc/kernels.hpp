@@ -26,9 +26,18 @@ constexpr int kShardShift = 6;
 // (1: deferred list, 2: edge buffer) — a query that lost pairs; its labels are refused
 constexpr int kErrWords = 8;
 constexpr int kErrOverflow = 4;
+// [6]: pairs whose evaluation raises ZeroDivisionError (cluster.py:135, 179, 181), listed as int2
+// (a, b) from word kErrZdList (capacity at word kErrZdCap).  The engines only list them: whether the
+// reference raises depends on whether a loop reaches the pair, which the edge cap decides
+// (fslr_read_stats, fslr_apply_edge_cap).  A repeated partition and its evaluation keep the count.
+constexpr int kErrZdCount = 6;
 // [7]: sticky flags of repeated multi-GPU partitions (32: totals differed), kept across queries and
-// cleared by the next synchronous fslr_sweep_partition / fslr_query; the per-query resets stop before it
+// cleared by the next synchronous fslr_sweep_partition / fslr_query
 constexpr int kErrSticky = 7;
+constexpr int kErrKeep = 6;           // a repeat's reset clears [0, kErrKeep); a query's all kErrWords
+constexpr int kErrZdCap = 8;          // never reset: the list's capacity in pairs
+constexpr int kErrZdList = 16;
+constexpr int kZdListInit = 1 << 16;
 // query shards own blocks of 64 consecutive ranks, round robin
 
 __host__ __device__ inline bool shard_owns(int read, int shard, int n_shards) {

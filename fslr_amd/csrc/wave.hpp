@@ -75,10 +75,12 @@ __device__ inline int2 ratio_range(int v, double cut) {
   return make_int2(lo, hi);
 }
 
+// a pair (a, b) whose evaluation raises ZeroDivisionError: listed in the error words (kernels.hpp
+// kErrZdCount); the reference raises only if a loop reaches it, which the edge cap decides
 __device__ __forceinline__ void raise_zd(int* err, bool zd, int a, int b) {
-  if (zd && atomicCAS(err, 0, FSLR_ERR_ZERO_DIVISION) == 0) {
-    err[1] = a;
-    err[2] = b;
+  if (zd) {
+    const int k = atomicAdd(&err[kErrZdCount], 1);
+    if (k < err[kErrZdCap]) reinterpret_cast<int2*>(err + kErrZdList)[k] = make_int2(a, b);
   }
 }
 

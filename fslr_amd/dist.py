@@ -383,6 +383,10 @@ class SweepShard:
             err = e
         mf = int(st['max_fwd'])
         max_ne = int(st['n_edges'])
+        # pairs whose evaluation raises ZeroDivisionError, listed by this rank's partition sweep: the
+        # reference raises when every loop runs to its end (the cap does not bind anywhere); otherwise
+        # only where a capped loop reaches one (fslr_cap_local, the replay)
+        zd = int(st.get('zd_pairs', 0))
         max_fp = 0
         if W > 1 and err is None and mf <= edge_threshold:
             # this rank's forest: the merge exchanges its pairs (not built when this rank already knows
@@ -396,12 +400,14 @@ class SweepShard:
             # maximum, so a pair that raises on one evaluator raises on every rank instead of leaving
             # the others in a collective, and every rank knows the padded sizes of the exchanges
             code = 0 if err is None else (1 if isinstance(err, ZeroDivisionError) else 2)
-            t = self.comm.small([mf, code, max_ne, max_fp])
+            t = self.comm.small([mf, code, max_ne, max_fp, zd])
             self.comm.all_reduce(t, 'max')
-            mf, code, max_ne, max_fp = (int(x) for x in t.tolist())
+            mf, code, max_ne, max_fp, zd = (int(x) for x in t.tolist())
             if err is None and code:
                 from ._lib import FslrError
                 err = ZeroDivisionError('division by zero') if code == 1 else FslrError('error on another rank')
+        if err is None and zd > 0 and mf <= edge_threshold:
+            err = ZeroDivisionError('division by zero')
         if err is not None:
             raise err
         out = {'entries_sent': sent_total, 'entries_received': n_recv, 'n_edges_local': int(st['n_edges']),

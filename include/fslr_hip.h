@@ -75,7 +75,7 @@
 extern "C" {
 #endif
 
-#define FSLR_ABI_VERSION 14
+#define FSLR_ABI_VERSION 15
 #define FSLR_MAX_L 64                /* max intervals per read (bitmask width) */
 #define FSLR_MAX_READS (1 << 25)     /* read rank packs into bits 6..30 of the index record */
 #define FSLR_THR_ZERO_ALN INT32_MIN
@@ -156,6 +156,15 @@ typedef struct {
                                       8 | 16 sweep entry buffers (rerun) */
     int64_t pair_tests;            /* SWEEP: overlapping interval pairs tested (each pair once) */
     int64_t entry_capacity;        /* SWEEP: match-entry buffer (grown automatically) */
+    int64_t zd_pairs;              /* read pairs whose evaluation raises ZeroDivisionError (both qlen2 or both
+                                      n_alignments 0 at the length gate, cluster.py:178-183; an aln_size == 0
+                                      interval met by first-fit, :133-136).  The reference raises only if a loop
+                                      reaches one: always when the edge cap does not bind (max_fwd <=
+                                      edge_threshold: fslr_read_stats returns FSLR_ERR_ZERO_DIVISION after
+                                      fslr_query), otherwise fslr_apply_edge_cap decides.  After
+                                      fslr_sweep_partition / fslr_sweep_evaluate / fslr_long_query /
+                                      fslr_long_pairs the caller decides (the binding may be known only over
+                                      every rank); overflow_flags 64: the list grew, rerun the query */
 } fslr_query_stats;
 
 typedef struct {
@@ -245,8 +254,9 @@ int  fslr_components(fslr_ctx *ctx);
  * write its match entries (8 bytes each, layout internal to the library) to the device buffer dst
  * grouped by destination k = (a >> block_shift) % n_dest, a = the pair's first (lower-rank) read:
  * rank blocks dealt round robin, n_dest <= 64; counts[k] = entries for k.  Syncs; FSLR_ERR_STATE if
- * sum(counts) > dst_cap (counts are still filled: grow dst and call again), FSLR_ERR_ZERO_DIVISION
- * as fslr_read_stats.
+ * sum(counts) > dst_cap (counts are still filled: grow dst and call again).  Pairs that raise
+ * ZeroDivisionError are listed, not raised (fslr_query_stats zd_pairs; fslr_cap_local raises for those
+ * the capped loops reach).
  * fslr_sweep_evaluate: evaluate the pairs of the n entries (a device buffer: every rank's segment
  * for this rank, concatenated in any order) into this context's edges and forward degrees.  Every
  * entry of a pair must be present, so each pair's first read belongs to one destination.  Needs only

@@ -185,6 +185,80 @@ def longzero_df():
     return df, hdr
 
 
+ZDCAP_ARGS = ['--n-alignment-diff', '1']
+
+
+def _zero_qlen(df, qnames):
+    """qlen2 = max(qend) - min(qstart) over a read's fillings (cluster.py:26-29): 0 for these reads."""
+    rows = df['qname'].isin(list(qnames))
+    df.loc[rows, 'qstart'] = 0
+    df.loc[rows, 'qend'] = 0
+    return df
+
+
+def zdcap_search(limit=400):
+    """Inputs where the edge cap binds and two overlapping reads both have qlen2 0, so their pair raises
+    ZeroDivisionError in different_lengths_or_alignments (cluster.py:179) — but only if a loop reaches
+    it (:205-209, 223-224).  With --n-alignment-diff 1 every other pair passes the gate on n_alignments,
+    so zeroing the two reads' qlen2 changes nothing else.  Candidates: E* edges (a, b) whose reads both
+    have more forward edges than the cap (both in the replay's T), in rank order; the oracle's reference
+    loop (pinned to the reference by every other fixture) says whether it raises.  Returns the first
+    pair that does not raise (both loops break before it) and the first that does."""
+    sys.path.insert(0, REPO)
+    from oracle import oracle as O
+    base, hdr = synth_df(1500, 6, 19, cluster_cap=40, size_p=1.0 / 14)
+    lens = dict(hdr)
+    cut = (1, 1, 0.66, 0.66, 0.66, 0.5)
+    csr, _ = O.restate_prep(base.copy(), lens, 'subtelomere', False)
+    e = O.run_core(csr, 0.8, cut, 0.04, 1.0, 10, use_cap=False)
+    fwd = e['fwd']
+    cands = [(int(a), int(b)) for a, b in zip(e['edge_a'], e['edge_b']) if fwd[a] >= 12 and fwd[b] >= 12]
+    found = {}
+    for a, b in sorted(cands)[:limit]:
+        qa, qb = csr.qnames[a], csr.qnames[b]
+        df = _zero_qlen(base.copy(), (qa, qb))
+        c2, _ = O.restate_prep(df.copy(), lens, 'subtelomere', False)
+        try:
+            O.run_core(c2, 0.8, cut, 0.04, 1.0, 10, use_cap=True)
+            kind = 'skip'
+        except ZeroDivisionError:
+            kind = 'raise'
+        found.setdefault(kind, (df, (qa, qb)))
+        if len(found) == 2:
+            break
+    return found, hdr
+
+
+def add_isolated_long_read(df, hdr, n_fill=70):
+    """One read of n_fill fillings (more than the 64-interval chunk) far from every other interval, one
+    filling with aln_size 0: the input then takes the long-read general path (no pair is evaluated with
+    it: its intervals only hit its own)."""
+    chrom, length = hdr[0]
+    lo, hi = 600_000, 600_000 + 3000 * (n_fill + 2)
+    on = df['chrom'] == chrom
+    assert not ((df.loc[on, 'rend'] >= lo) & (df.loc[on, 'rstart'] <= hi)).any()
+    rows = []
+    tmpl = df.iloc[1].to_dict()
+    for k in range(n_fill + 2):
+        r = dict(tmpl)
+        r.update(chrom=chrom, rstart=lo + 3000 * k, rend=lo + 3000 * k + 1000, qname='zz_isolated_long_read',
+                 n_alignments=n_fill + 2, aln_size=0 if k == 5 else 1000, qstart=100 * k, qend=100 * k + 90,
+                 alignment_score=1000, qlen=100 * (n_fill + 2))
+        rows.append(r)
+    return pd.concat([df, pd.DataFrame(rows, columns=df.columns)], ignore_index=True)
+
+
+def make_round5():
+    found, hdr = zdcap_search()
+    for kind in ('skip', 'raise'):
+        df, pair = found[kind]
+        note = (f'edge cap binds; reads {pair[0]} and {pair[1]} both have qlen2 0 and overlap: their pair raises '
+                f'ZeroDivisionError only if a loop reaches it ({"both loops break before it" if kind == "skip" else "a loop reaches it"})')
+        make_fixture(f'zdcap_{kind}', df, hdr, args=ZDCAP_ARGS, note=note)
+        make_fixture(f'zdcap_{kind}_long', add_isolated_long_read(df, hdr), hdr, args=ZDCAP_ARGS,
+                     note=note + '; plus an isolated long read with an aln_size 0 filling (the general path)')
+
+
 def make_kats(n_random=3000, seed=17):
     """Known answers of the reference predicates on random + boundary inputs."""
     cluster, _ = refharness.load()
@@ -334,6 +408,9 @@ def main():
     if sys.argv[1:2] == ['--round3']:
         make_round3()
         return
+    if sys.argv[1:2] == ['--round5']:
+        make_round5()
+        return
     df, hdr = synth_df(1000, 3, 0, lmin=3)
     make_fixture('cfg1_1k_x3', df, hdr, note='BASELINE config 1: 1k reads x 3 fillings, defaults')
     df, hdr = synth_df(2000, 8, 7)
@@ -363,6 +440,7 @@ def main():
     make_fixture('capbind_1500', df, hdr, note='clusters up to 40 reads: edge cap binds (stub-order)')
     make_longreads()
     make_round3()
+    make_round5()
     make_kats()
     make_vector('v10k_l8_s7', 10_000, 8, 7)
     make_vector('v20k_l16_s11', 20_000, 16, 11)

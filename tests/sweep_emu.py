@@ -50,17 +50,18 @@ class EmuSweepContext:
 
     # -- partition ------------------------------------------------------------------------------
     def _gate(self, a, b, qcut, ncut):
+        """(passes, raises ZeroDivisionError) of the length gate (cluster.py:178-183)."""
         q1, q2 = int(self.csr.read_qlen2[a]), int(self.csr.read_qlen2[b])
         mn, mx = min(q1, q2), max(q1, q2)
         if mx == 0:
-            raise ZeroDivisionError('division by zero')
+            return False, True
         if mn / mx >= qcut:
-            return True
+            return True, False
         n1, n2 = int(self.csr.read_nal[a]), int(self.csr.read_nal[b])
         mn, mx = min(n1, n2), max(n1, n2)
         if mx == 0:
-            raise ZeroDivisionError('division by zero')
-        return mn / mx >= ncut
+            return False, True
+        return mn / mx >= ncut, False
 
     def _entries(self, qcut, ncut):
         c = self.csr
@@ -73,17 +74,21 @@ class EmuSweepContext:
             ks = np.flatnonzero(chrom == ch)
             s, e = start[ks], end[ks]
             o = np.minimum(e[:, None], e[None, :]) - np.maximum(s[:, None], s[None, :])
-            ok = (o >= self.thr[ks][:, None]) & (o >= self.thr[ks][None, :])
             ra, rb = self.read_of[ks][:, None], self.read_of[ks][None, :]
-            ok &= ra < rb
-            x, y = np.nonzero(ok)
-            for p, q in zip(ks[x].tolist(), ks[y].tolist()):
+            hit = (o >= 0) & (ra < rb)              # end-inclusive overlap of two different reads (:201)
+            ok = hit & (o >= self.thr[ks][:, None]) & (o >= self.thr[ks][None, :])
+            x, y = np.nonzero(hit)
+            for p, q, m in zip(ks[x].tolist(), ks[y].tolist(), ok[x, y].tolist()):
                 a, b = int(self.read_of[p]), int(self.read_of[q])
-                if self._gate(a, b, qcut, ncut):
+                passes, zd = self._gate(a, b, qcut, ncut)
+                if zd:
+                    self._zd.add((a, b))            # listed, not raised (the edge cap decides)
+                elif passes and m:
                     out.append((a << 39) | (b << 14) | (int(self.slot[p]) << 7) | int(self.slot[q]))
         return np.array(out, dtype=np.int64)
 
     def sweep_partition(self, qlen_cut, nal_cut, pass_table, n_dest, block_shift, dst, edge_threshold=10):
+        self._zd = set()
         ent = self._entries(qlen_cut, nal_cut)
         dest = (ent >> (39 + block_shift)) % n_dest
         order = np.argsort(dest, kind='stable')
@@ -91,7 +96,7 @@ class EmuSweepContext:
         if counts.sum() > dst.numel():
             return False, counts
         dst.numpy()[:ent.size] = ent[order]
-        self._st = {'match_entries': int(ent.size)}
+        self._st = {'match_entries': int(ent.size), 'zd_pairs': len(self._zd)}
         return True, counts
 
     def sweep_partition_repeat(self, qlen_cut, nal_cut, pass_table, n_dest, block_shift, dst, edge_threshold=10):
@@ -131,7 +136,7 @@ class EmuSweepContext:
         self._edges = np.array(edges, dtype=np.int64).reshape(-1, 4)
         self._fwd = fwd
         self._st = {'n_edges': len(edges), 'edge_capacity': self.edge_capacity,
-                    'max_fwd': int(fwd.max()) if fwd.size else 0}
+                    'max_fwd': int(fwd.max()) if fwd.size else 0, 'zd_pairs': len(getattr(self, '_zd', ()))}
 
     def stats(self, check=True):
         return dict(self._st)
@@ -258,6 +263,10 @@ class EmuSweepContext:
             self._T = self._candidates(edge_threshold, g, self._gfwd)
         else:
             self._T = self._candidates(edge_threshold)
+        inT = set(self._T)
+        if any(a not in inT or b not in inT for a, b in getattr(self, '_zd', ())):
+            # a listed pair with a read outside T: that read's loop never breaks and visits it
+            raise ZeroDivisionError('division by zero')
         lists = self._hit_lists(self._T, self.owned)
         self._cap_counts = np.array([len(x) for x in lists], np.int32)
         self._cap_hits = np.array([y for x in lists for y in x], np.int32)

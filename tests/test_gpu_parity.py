@@ -142,7 +142,8 @@ def test_cli_matches_reference_outputs(name, io_flag):
 
 
 @pytest.mark.parametrize('name', ['cfg1_1k_x3', 'capbind_1500', 'zerodiv', 'noclusters', 'longreads_400', 'params_a',
-                                  'edge_cases_p0', 'zipf_800_l64', 'chroms_115', 'longcap_240'])
+                                  'edge_cases_p0', 'zipf_800_l64', 'chroms_115', 'longcap_240', 'zdcap_skip',
+                                  'zdcap_raise', 'zdcap_skip_long', 'zdcap_raise_long'])
 def test_cli_multi_gpu_matches_reference_outputs(name):
     """``fslr --gpus 2``: two rank processes (sharing this box's one GPU over gloo) run the
     chromosome-split sweep (fslr_amd.multi); outputs byte-identical to the reference's.  Covers the
@@ -165,6 +166,35 @@ def test_cli_multi_gpu_matches_reference_outputs(name):
                 assert 'No clusters were found.' in res.output
             else:
                 assert open(path).read() == want, f'{name}: {which} output differs'
+
+
+@pytest.mark.parametrize('engine', ENGINES)
+@pytest.mark.parametrize('name', ['zdcap_skip', 'zdcap_raise'])
+def test_zero_division_under_binding_cap(ctx, name, engine):
+    """Two overlapping reads with qlen2 0 (their pair raises ZeroDivisionError in
+    different_lengths_or_alignments, cluster.py:179) inside a locus where the edge cap binds: the
+    reference raises only if a loop reaches the pair (cluster.py:205-209, 223-224).  zdcap_skip: both
+    reads' loops break before it, no raise, the capped graph is the reference's; zdcap_raise: a loop
+    reaches it.  The engines list such pairs instead of raising (zd_pairs); the cap replay decides."""
+    data, _, kw = host_prepare(name)
+    csr = data.csr()
+    cut = [float(x) for x in kw['jaccard_cutoffs'].split(',')]
+    args = dict(overlap=kw['overlap'], cutoffs=cut, qlen_diff=kw['qlen_diff'], nal_diff=kw['n_alignment_diff'])
+    oc = oracle_from_csr(csr)
+    oargs = (kw['overlap'], cut, kw['qlen_diff'], kw['n_alignment_diff'], 10)
+    if fx.meta(name)['exception']:
+        with pytest.raises(ZeroDivisionError):
+            O.run_core(oc, *oargs, use_cap=True)
+        with pytest.raises(ZeroDivisionError):
+            gpu_run(ctx, csr, cap=10, engine=engine, **args)
+        return
+    o = O.run_core(oc, *oargs, use_cap=True)
+    g = gpu_run(ctx, csr, cap=10, engine=engine, **args)
+    assert g['stats']['zd_pairs'] >= 1 and g['stats']['cap']['applied'] == 1
+    compare_capped_with_oracle(g, o, csr.n_reads)
+    # without the cap (every loop runs to its end) the same input raises
+    with pytest.raises(ZeroDivisionError):
+        gpu_run(ctx, csr, cap=10 ** 6, engine=engine, **args)
 
 
 @pytest.mark.parametrize('name', [f for f in fx.FIXTURES if fx.stage(f) is not None])
