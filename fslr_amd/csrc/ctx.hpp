@@ -93,6 +93,19 @@ struct fslr_ctx {
   int wstat_waves = 0;
   unsigned long long* diag = nullptr;        // FSLR_SECTION_PROF builds: per-read timing of the pair kernel
   int* errw = nullptr;     // [0..2] error, [3] max_fwd, ... then the ZeroDivisionError pair list (kernels.hpp)
+  // fslr_rows_upload / fslr_set_reads_rows (rows.hip): the uploaded rows and the CSR the device made
+  long long* rows_col = nullptr;    // [7 x rows_cap] chrom, start, end, aln, qcode, nal, qlen2
+  int64_t rows_cap = 0, rows_n = 0, rows_codes = 0, rows_cids = 0;
+  long long* rows_ord = nullptr;    // [rows_cap] the start order
+  unsigned char* rows_keep = nullptr;
+  int* rows_int = nullptr;          // [16 x rows_cap + ...] the build's int scratch and CSR columns
+  int64_t rows_int_cap = 0;
+  long long* rows_l = nullptr;      // [2 x rows_cap] aln in CSR order, qname code of each rank
+  void* rows_temp = nullptr;
+  size_t rows_temp_bytes = 0;
+  bool rows_set = false;            // the reads came from fslr_set_reads_rows (fslr_get_csr, fold)
+  std::vector<int> rows_dmap;       // chromosome number -> dense id, and its inverse
+  std::vector<int64_t> rows_cid;
   int zd_cap = 0;          // capacity of that list (pairs)
   bool zd_host = false;    // the last query's ZeroDivisionError pairs are decided by the caller (a partition,
                            // an evaluation or a long-read query: the edge cap's binding is known there)

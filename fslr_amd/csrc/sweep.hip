@@ -54,14 +54,27 @@ __device__ __forceinline__ int part_of(int B, int npass) {
 }
 
 // ---- 1. the sweep -------------------------------------------------------------------------------
-// One wavefront per tile of 64 consecutive sorted positions (lane l holds q = q0 + l), tiles dealt
-// grid-stride over a resident grid.  The tile's forward ranges are flattened into an LDS map (item
-// r -> the lane whose range holds it), then walked 64 interval pairs per step, one per lane, the
-// next step's index records loaded while the current step is tested.  The q side of a pair comes
-// from LDS (written once per tile), the p side is the index record and gate word at p (a tile's
-// window is a few hundred consecutive positions, so these loads hit L1 / L2).  kEmit = false counts
-// the tile's entries (and the statistics); kEmit = true writes them at the tile's scanned offset.
-constexpr int kMapCap = 2048;              // items per map segment (a longer tile takes several)
+// One wavefront per tile of 64 consecutive sorted positions (lane l holds q = q0 + l), tiles dealt in
+// chunks of consecutive tiles, grid-stride over a resident grid.  The tile's forward ranges are
+// flattened into an LDS map (item r -> its lane and p - q0), then walked 64 interval pairs per step,
+// one per lane, the next step's operands read while the current step is tested.
+// The index records and gate words of positions [q0, q0 + kRing) sit in a per-wave LDS ring (slot
+// p mod kRing): a tile's pairs have p in q0 + 1 .. q + n_fwd(q), so the p side of almost every pair
+// test — and the q side — is an LDS read instead of a dependent gather through L1 / L2.  Moving to the
+// next tile of a chunk loads only the 64 positions entering the ring (one coalesced record and gate
+// load per lane: every position's 24 B cross HBM once per chunk); a pair beyond the ring (a tile whose
+// forward window is longer) reads the index in global memory.
+// kEmit = false counts the tile's entries (and the statistics); kEmit = true writes them.
+#ifndef FSLR_SWEEP_RING
+#define FSLR_SWEEP_RING 128
+#endif
+#ifndef FSLR_SWEEP_DB
+#define FSLR_SWEEP_DB 0
+#endif
+constexpr int kRing = FSLR_SWEEP_RING;     // positions per wave in the LDS ring (a power of two >= 64)
+static_assert(kRing >= kWave && (kRing & (kRing - 1)) == 0 && kRing < 1024, "ring size");
+constexpr int kRingMask = kRing - 1;
+constexpr int kMapCap = 1024;              // items per map segment (a longer tile takes several)
 constexpr int kTileRun = 8;                // consecutive tiles per work item
 
 // kMode 0: count the tile's entries (two-pass fallback), 1: write them at the tile's scanned offset
@@ -71,60 +84,69 @@ template <int kMode>
 __global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
   constexpr bool kEmit = kMode != 0;
   constexpr bool kCount = kMode != 1;
-  __shared__ int4 qa_all[kSwWaves][kWave];     // {end, thr, tag, qlo}
-  __shared__ int4 qb_all[kSwWaves][kWave];     // {qhi, nlo, nhi, offv}
+  __shared__ int4 rr_all[kSwWaves][kRing];     // ring: index records {start, end, thr, read << 6 | j}
+  __shared__ int2 rg_all[kSwWaves][kRing];     // ring: gate words {qlen2, nal | L << 24 | zero-aln << 31}
+  __shared__ int4 qb_all[kSwWaves][kWave];     // lane's read's gate as integer ranges {qlo, qhi, nlo, nhi}
+  __shared__ int off_all[kSwWaves][kWave];     // item r of lane k is position r + offv_k
   __shared__ unsigned char zf_all[kSwWaves][kWave];   // q's read has qlen2 == 0 (1) / n_alignments == 0 (2)
-  __shared__ unsigned char map_all[kSwWaves][kMapCap];          // item -> its lane (position q0 + mi)
+  __shared__ unsigned short map_all[kSwWaves][kMapCap];   // item -> lane | min(p - q0, kRing) << 6
   __shared__ unsigned long long st_all[kSwWaves][kEmit ? kWave : 1];
   unsigned long long* const dst = kMode == 2 ? g.ent_ub : g.ent;
   const int lane = lane_id();
   const int wv = threadIdx.x >> 6;
-  int4* QA = qa_all[wv];
+  int4* RR = rr_all[wv];
+  int2* RG = rg_all[wv];
   int4* QB = qb_all[wv];
+  int* OFF = off_all[wv];
   unsigned char* ZF = zf_all[wv];
-  unsigned char* MAP = map_all[wv];
+  unsigned short* MAP = map_all[wv];
   unsigned long long* ST = st_all[wv];
   unsigned long long w_tests = 0, w_hits = 0, w_ent = 0;
   const int nt = (g.ni + kWave - 1) / kWave;
   const int nw = gridDim.x * kSwWaves;
   const int wid = blockIdx.x * kSwWaves + wv;
   // tiles in chunks of up to kTileRun consecutive tiles per wave (a tile's forward window reaches
-  // into the next tile, whose records the same wave then finds in its caches), chunks dealt
-  // grid-stride; shorter chunks when there are fewer than kTileRun tiles per wave of the grid (a
-  // rank's share of the multi-GPU split), so every wave gets work: the sweep is latency bound
+  // into the next tile, whose records the ring already holds), chunks dealt grid-stride; shorter
+  // chunks when there are fewer than kTileRun tiles per wave of the grid (a rank's share of the
+  // multi-GPU split), so every wave gets work: the sweep is latency bound
   const int run = max(1, min(kTileRun, nt / nw));
   const int nchunks = (nt + run - 1) / run;
-  // XCD-aware: workgroup b runs on XCD b % 8 (the usual dispatch; it only affects speed), and each
-  // XCD takes one contiguous eighth of the chunks, dealt to its waves in order — a chunk's forward
-  // window runs into the next chunk's positions, which a neighbouring wave of the same XCD (often of
-  // the same workgroup) reads at about the same time, so the overlap is served by that XCD's L2
-  // instead of being fetched again by another XCD.  (Per-XCD work queues were tried in round 3:
-  // 0.241 -> 0.260 ms at cfg3, the tickets' latency cost more than the balance gained.)
-  const int nx = min(8, static_cast<int>(gridDim.x));                    // XCDs in use
-  const int xcd = static_cast<int>(blockIdx.x) % nx;
-  const int bpx = (static_cast<int>(gridDim.x) - xcd + nx - 1) / nx;      // workgroups on this XCD
-  const int wx = static_cast<int>(blockIdx.x) / nx * kSwWaves + wv;        // wave index inside the XCD
-  const int c_lo = static_cast<int>((static_cast<long long>(nchunks) * xcd) / nx);
-  const int c_hi = static_cast<int>((static_cast<long long>(nchunks) * (xcd + 1)) / nx);
-  const int c0 = g.xcd_map ? c_lo + wx : wid, c1 = g.xcd_map ? c_hi : nchunks;
-  const int cstep = g.xcd_map ? bpx * kSwWaves : nw;
-  for (int chunk = c0; chunk < c1; chunk += cstep)
+  for (int chunk = wid; chunk < nchunks; chunk += nw)
   for (int tile = chunk * run; tile < min(nt, (chunk + 1) * run); ++tile) {
     const int q0 = tile * kWave;
     const int q = q0 + lane;
     const bool qv = q < g.ni;
     const int qc = qv ? q : q0;
-    int4 rq = g.idx4[qc];
     const int nf = qv ? g.rng_s[qc].x : 0;
+    wave_lds_sync();                             // the previous tile's ring and map reads are done
+    if (tile == chunk * run) {
+      // the chunk's first tile: positions [q0, q0 + kRing)
+#pragma unroll
+      for (int k = 0; k < kRing / kWave; ++k) {
+        const int p = q0 + k * kWave + lane;
+        if (p < g.ni) {
+          RR[p & kRingMask] = g.idx4[p];
+          RG[p & kRingMask] = g.idx_gate[p];
+        }
+      }
+    } else {
+      // the ring held [q0 - 64, q0 - 64 + kRing): the 64 positions entering it replace the last tile's
+      const int p = q0 + kRing - kWave + lane;
+      if (p < g.ni) {
+        RR[p & kRingMask] = g.idx4[p];
+        RG[p & kRingMask] = g.idx_gate[p];
+      }
+    }
+    wave_lds_sync();
+    const int4 rq = RR[qc & kRingMask];
     const int4 lbq = g.lb[rq.w >> 6];            // the gate of q's read as integer ranges
     const bool any_zero = __ballot(qv && (lbq.x < 0 || lbq.z < 0)) != 0ull;   // v == 0 (ZeroDivision)
     const int pre = wave_incl_scan(nf);
     const int ex = pre - nf;
     const int T = rdl(pre, kWave - 1);
-    wave_lds_sync();
     // lower bounds with v == 0 (lo < 0: partner 0 raises, [1, hi] passes) folded to 1
-    QA[lane] = make_int4(rq.y, rq.z, rq.w, lbq.x < 0 ? 1 : lbq.x);
-    QB[lane] = make_int4(lbq.y, lbq.z < 0 ? 1 : lbq.z, lbq.w, q + 1 - ex);   // item r of lane k: position r + offv_k
+    QB[lane] = make_int4(lbq.x < 0 ? 1 : lbq.x, lbq.y, lbq.z < 0 ? 1 : lbq.z, lbq.w);
+    OFF[lane] = q + 1 - ex;
     ZF[lane] = static_cast<unsigned char>((lbq.x < 0 ? 1 : 0) | (lbq.z < 0 ? 2 : 0));
     long long out = 0;                           // kEmit: next entry slot of this tile
     if constexpr (kMode == 1) out = g.tile_off[tile];
@@ -143,36 +165,46 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
     for (int seg = 0; seg < T; seg += kMapCap) {
       const int se = min(T, seg + kMapCap);
       wave_lds_sync();
-      for (int r = max(ex, seg); r < min(pre, se); ++r) MAP[r - seg] = static_cast<unsigned char>(lane);
+      for (int r = max(ex, seg); r < min(pre, se); ++r)
+        MAP[r - seg] = static_cast<unsigned short>(lane | min(r - ex + lane + 1, kRing) << 6);
       wave_lds_sync();
-      // step loads: the mapped lane's offset, then the p-side record and gate word
+      // step operands: the mapped lane's gate ranges, q's record (ring), p's record and gate word
+      // (ring; global beyond it)
       struct Step {
         int mi;
-        int4 b4, rp;
+        int4 b4, a4, rp;
         int2 gp;
       };
       auto step_load = [&](int base, Step& t) {
         const int r = base + lane;
-        t.mi = r < se ? MAP[r - seg] : 0;
+        const unsigned md = r < se ? MAP[r - seg] : 0u;
+        t.mi = static_cast<int>(md & 63u);
+        const int d = static_cast<int>(md >> 6);
         t.b4 = QB[t.mi];
-        const int p = r < se ? r + t.b4.w : q0;
-        t.rp = g.idx4[p];
-        t.gp = g.idx_gate[p];
+        t.a4 = RR[(q0 + t.mi) & kRingMask];
+        if (d < kRing) {
+          t.rp = RR[(q0 + d) & kRingMask];
+          t.gp = RG[(q0 + d) & kRingMask];
+        } else {
+          const int p = r + OFF[t.mi];
+          t.rp = g.idx4[p];
+          t.gp = g.idx_gate[p];
+        }
       };
       // one step of 64 interval pairs; kZero: some q of the tile has qlen2 or n_alignments == 0
       // (only then can a pair raise ZeroDivisionError)
       auto step = [&](auto zero_tag, int base, const Step& t) __attribute__((always_inline)) {
         constexpr bool kZero = decltype(zero_tag)::value;
         const bool valid = base + lane < se;
-        const int4 a4 = QA[t.mi];
-        const int X = a4.z >> 6, Y = t.rp.w >> 6;
+        const int4 a4 = t.a4;
+        const int X = a4.w >> 6, Y = t.rp.w >> 6;
         const bool hit = valid & (X != Y);
         // calculate_overlap >= overlap for both intervals: start_p >= start_q, start_p <= end_q
-        const int o = min(a4.x, t.rp.y) - t.rp.x;
-        const bool match = o >= max(a4.y, t.rp.z);
+        const int o = min(a4.y, t.rp.y) - t.rp.x;
+        const bool match = o >= max(a4.z, t.rp.z);
         // different_lengths_or_alignments: passes when either ratio is close (idx_gate word of p)
         const int q2 = t.gp.x, n2 = t.gp.y & 0xFFFFFF;
-        const int qlo = a4.w, qhi = t.b4.x, nlo = t.b4.y, nhi = t.b4.z;
+        const int qlo = t.b4.x, qhi = t.b4.y, nlo = t.b4.z, nhi = t.b4.w;
         const bool pq = (q2 >= qlo) & (q2 <= qhi);
         const bool lenok = pq | ((n2 >= nlo) & (n2 <= nhi));
         bool emit = hit & lenok & match;
@@ -199,7 +231,7 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
           if (emit) {
             // A << 39 | B << 14 | i << 7 | j as two dwords
             const int A = min(X, Y), B = max(X, Y);
-            const int iq = a4.z & 63, jp = t.rp.w & 63;
+            const int iq = a4.w & 63, jp = t.rp.w & 63;
             const unsigned ij = X < Y ? static_cast<unsigned>(iq << 7 | jp) : static_cast<unsigned>(jp << 7 | iq);
             const unsigned lo = (static_cast<unsigned>(B) << 14) | ij;
             const unsigned hi = (static_cast<unsigned>(A) << 7) | (static_cast<unsigned>(B) >> 18);
@@ -209,7 +241,8 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
         }
       };
       auto run_steps = [&](auto zero_tag) __attribute__((always_inline)) {
-        // double buffer unrolled by two: the loads of the next step are in flight while one is tested
+#if FSLR_SWEEP_DB
+        // double buffer unrolled by two: the operands of the next step are in flight while one is tested
         Step s0, s1;
         step_load(seg, s0);
         for (int base = seg; base < se; base += 2 * kWave) {
@@ -220,6 +253,14 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
           if (base + 2 * kWave < se) step_load(base + 2 * kWave, s0);
           step(zero_tag, base + kWave, s1);
         }
+#else
+        // LDS operands: other waves cover their latency
+        for (int base = seg; base < se; base += kWave) {
+          Step s0;
+          step_load(base, s0);
+          step(zero_tag, base, s0);
+        }
+#endif
       };
       if (any_zero) run_steps(std::true_type{});
       else run_steps(std::false_type{});
@@ -236,7 +277,7 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
     }
   }
   if constexpr (kCount) {
-    // statistics: plain stores into this wave's slots, summed by k_sum_slots
+    // statistics: plain stores into this wave's slots, summed by k_sweep_total / k_sum_slots
     const unsigned long long f = lane == 0 ? w_tests : lane == 1 ? w_hits : w_ent;
     if (lane < 3) g.wstat[static_cast<long long>(wid) * kWsFields + lane] = f;
   }
@@ -1530,20 +1571,9 @@ hipError_t launch_sweep_plan(const SweepArgs& a, hipStream_t s) {
   return hipcub::DeviceScan::ExclusiveSum(a.temp, tb, a.tile_tests, a.tile_ub, nt, s);
 }
 
-// k_sweep's chunks dealt grid-stride (default), or FSLR_SWEEP_MAP=xcd: each XCD a contiguous share.
-// Measured at cfg3 (profiles/r04/ab/): the XCD mapping 0.2485 ms against 0.2447 ms grid-stride.
-static int sweep_xcd_map() {
-  static const int v = [] {
-    const char* e = std::getenv("FSLR_SWEEP_MAP");
-    return e && std::strcmp(e, "xcd") == 0 ? 1 : 0;
-  }();
-  return v;
-}
-
 hipError_t launch_sweep_count(const SweepArgs& a0, int mode, long long* total_dev, hipStream_t s, long long* n_dev,
                               long long cap) {
-  SweepArgs a = a0;
-  a.xcd_map = sweep_xcd_map();
+  const SweepArgs& a = a0;
   const int nt = tiles_of(a);
   if (nt == 0) return hipMemsetAsync(total_dev, 0, 3 * sizeof(long long), s);
   const int blocks = std::min(blocks_mode(mode), (nt + kSwWaves - 1) / kSwWaves);
@@ -1583,9 +1613,7 @@ hipError_t launch_sweep_dense(const SweepArgs& a, int mode, hipStream_t s) {
                                                                                     a.tile_cnt, nt, a.ent);
   } else {
     const int be = std::min(blocks_mode(1), (nt + kSwWaves - 1) / kSwWaves);
-    SweepArgs a1 = a;
-    a1.xcd_map = sweep_xcd_map();
-    k_sweep<1><<<be, kSwBlock, 0, s>>>(a1);
+    k_sweep<1><<<be, kSwBlock, 0, s>>>(a);
   }
   return hipGetLastError();
 }

@@ -93,7 +93,19 @@ class SynthBed:
         return df[BED_COLUMNS]
 
     def write_tsv(self, path: str) -> None:
-        self.to_dataframe().to_csv(path, sep='\t', index=False)
+        """``to_dataframe().to_csv(path, sep='\\t', index=False)``; the same bytes through pyarrow's
+        threaded CSV writer when it is importable (10M reads: minutes with pandas)."""
+        df = self.to_dataframe()
+        try:
+            import pyarrow as pa
+            import pyarrow.csv as pcsv
+        except ImportError:                      # pragma: no cover - pyarrow ships in this image
+            df.to_csv(path, sep='\t', index=False)
+            return
+        with open(path, 'wb') as fh:
+            fh.write(('\t'.join(df.columns) + '\n').encode())
+            pcsv.write_csv(pa.Table.from_pandas(df, preserve_index=False), fh,
+                           pcsv.WriteOptions(include_header=False, delimiter='\t', quoting_style='none'))
 
     def interval_data(self, cluster_mask=('subtelomere',), threshold: int = 500_000):
         """The prepared ``data`` (fslr_amd.prep.IntervalData) straight from the columns.
