@@ -13,7 +13,7 @@ import numpy as np
 
 LIB_PATH = os.environ.get('FSLR_LIB') or os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libfslr_hip.so')
 
-ABI_VERSION = 16         # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
+ABI_VERSION = 18         # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
 FSLR_OK, FSLR_ERR_ZERO_DIVISION, FSLR_ERR_INVALID, FSLR_ERR_HIP, FSLR_ERR_NOMEM, FSLR_ERR_STATE = range(6)
 FSLR_MAX_L = 64
 FSLR_MAX_READS = 1 << 25
@@ -41,7 +41,8 @@ EXPORTED = ['fslr_abi_version', 'fslr_last_error', 'fslr_ctx_create', 'fslr_ctx_
             'fslr_cap_shard_pack', 'fslr_cap_replay_shard', 'fslr_cap_copy_changes', 'fslr_cap_apply_changes',
             'fslr_local_forest', 'fslr_copy_forest_pairs', 'fslr_sort_edges', 'fslr_cap_bwd_counts',
             'fslr_cap_restrict', 'fslr_cap_copy_restricted', 'fslr_cap_install_restricted', 'fslr_rows_upload',
-            'fslr_set_reads_rows', 'fslr_get_read_codes', 'fslr_get_csr', 'fslr_fold_thresholds']
+            'fslr_set_reads_rows', 'fslr_get_read_codes', 'fslr_get_csr', 'fslr_fold_thresholds',
+            'fslr_position_costs', 'fslr_set_position_filter', 'fslr_use_position_filter', 'fslr_long_pairs_shard']
 
 
 class HipUnavailable(RuntimeError):
@@ -194,6 +195,10 @@ def load(path: str = LIB_PATH):
         'fslr_get_read_codes': (ctypes.c_int, [vp, vp]),
         'fslr_get_csr': (ctypes.c_int, [vp] + [vp] * 10),
         'fslr_fold_thresholds': (ctypes.c_int, [vp, ctypes.c_double]),
+        'fslr_position_costs': (ctypes.c_int, [vp, vp, vp, i64]),
+        'fslr_set_position_filter': (ctypes.c_int, [vp, i64, i64, i64]),
+        'fslr_use_position_filter': (ctypes.c_int, [vp]),
+        'fslr_long_pairs_shard': (ctypes.c_int, [vp, ctypes.POINTER(Params), i32, i32, ctypes.POINTER(ctypes.c_int64)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -304,6 +309,7 @@ class Context:
         if arrs[2].size and (arrs[2].min() < 0 or arrs[2].max() >= (1 << 24)):
             raise ValueError('n_alignments must lie in [0, 2**24) for the device path')
         self.n_reads = len(arrs[1])
+        self.n_intervals = len(arrs[3])
 
     def load_csr_any(self, csr, iv_thr):
         """Upload a CSR whose reads may have more than FSLR_MAX_L intervals (fslr_set_reads_any: the
@@ -318,6 +324,7 @@ class Context:
         self._check(self._L.fslr_set_reads_any(self._h, ctypes.byref(r)))
         L = np.diff(arrs[0].astype(np.int64))
         self.n_reads = int(len(arrs[1]) + np.maximum((L + FSLR_MAX_L - 1) // FSLR_MAX_L - 1, 0).sum())
+        self.n_intervals = len(arrs[3])
 
     def rows_upload(self, cols, n_codes, n_chrom_ids):
         """fslr_rows_upload: keep_fillings' rows (``cols``: int64 columns chrom, start, end, aln, qcode,
@@ -346,6 +353,7 @@ class Context:
                 e.info = d
                 raise
         self.n_reads = d['n_reads']
+        self.n_intervals = d['n_intervals']
         return d
 
     def read_codes(self) -> np.ndarray:
@@ -421,6 +429,19 @@ class Context:
             return
         o = np.ascontiguousarray(np.asarray(owned, dtype=bool).astype(np.uint8))
         self._check(self._L.fslr_set_chrom_filter(self._h, _ptr(o)))
+
+    def position_costs(self):
+        """(pair tests, forward-window end) per 64-position tile of the full index (fslr_position_costs)."""
+        nt = (self.n_intervals + 63) // 64
+        tests, reach = np.zeros(nt, np.int64), np.zeros(nt, np.int64)
+        self._check(self._L.fslr_position_costs(self._h, _ptr(tests), _ptr(reach), nt))
+        return tests, reach
+
+    def set_position_filter(self, lo, hi, end):
+        self._check(self._L.fslr_set_position_filter(self._h, int(lo), int(hi), int(end)))
+
+    def use_position_filter(self):
+        self._check(self._L.fslr_use_position_filter(self._h))
 
     def sweep_partition(self, qlen_cut, nal_cut, pass_table, n_dest, block_shift, dst, edge_threshold=10):
         """Sweep the (filtered) index and write the match entries grouped by destination
@@ -729,6 +750,14 @@ class Context:
         p = self._params(qlen_cut, nal_cut, pass_table, edge_threshold)
         ne = ctypes.c_int64(0)
         self._check(self._L.fslr_long_pairs(self._h, ctypes.byref(p), ctypes.byref(ne)))
+        return int(ne.value)
+
+    def long_pairs_shard(self, qlen_cut, nal_cut, pass_table, shard, n_shards, edge_threshold=10) -> int:
+        """fslr_long_pairs for the pairs whose lower read lies in query shard ``shard`` of ``n_shards``."""
+        p = self._params(qlen_cut, nal_cut, pass_table, edge_threshold)
+        ne = ctypes.c_int64(0)
+        self._check(self._L.fslr_long_pairs_shard(self._h, ctypes.byref(p), int(shard), int(n_shards),
+                                                  ctypes.byref(ne)))
         return int(ne.value)
 
     def cap_replay_pairs(self, edge_threshold, a, b, n_reads: int):

@@ -390,10 +390,9 @@ def query_graph(interval_trees, data, overlap_cutoff, jaccard_threshold, edge_th
     if isinstance(interval_trees, MultiGpuIndex) and (interval_trees.source is data or interval_trees.data is data):
         mg = interval_trees
         thr = fold_overlap_threshold(mg.csr.iv_aln, overlap_cutoff)
-        if multi.sweep_applies(mg.csr, thr) and not has_long_reads(mg.csr):
-            return _query_multi_gpu(mg, thr, jaccard_threshold, edge_threshold, qlen_diff, diff)
-        # overlap <= 0, an aln_size == 0 interval or a read of more than 64 intervals: one GPU
-        interval_trees = DeviceIntervalIndex(mg.data, mg.first_device)
+        # the sweep split, or for overlap <= 0, an aln_size == 0 interval or reads of more than 64
+        # intervals the query-shard split
+        return _query_multi_gpu(mg, thr, jaccard_threshold, edge_threshold, qlen_diff, diff)
     if not isinstance(interval_trees, DeviceIntervalIndex) or (interval_trees.source is not data and
                                                                interval_trees.data is not data):
         interval_trees = DeviceIntervalIndex(data)
@@ -521,9 +520,9 @@ def _query_multi_gpu(mg, thr, jaccard_threshold, edge_threshold, qlen_diff, diff
         warnings.warn('n_alignments differs between rows of one read; the reference then uses the row its '
                       'search reaches first (order-dependent); the first row in data order is used', EdgeCapWarning)
     r = multi.query(csr, thr, 1 - qlen_diff, 1 - diff, pass_table(jaccard_threshold), int(edge_threshold),
-                    mg.n_gpus, first_device=mg.first_device)
+                    mg.n_gpus, first_device=mg.first_device, cutoffs=list(jaccard_threshold))
     a, b, I, U = r['edges']
-    st = {'engine': 'sweep', 'n_gpus': mg.n_gpus, 'backend': r['backend'], 'evaluated_pairs': -1,
+    st = {'engine': r.get('path', 'sweep'), 'n_gpus': mg.n_gpus, 'backend': r['backend'], 'evaluated_pairs': -1,
           'n_edges': int(a.shape[0]), 'max_fwd': r['max_fwd'], 'cap': r['cap'], 'capped': r['capped']}
     return RawGraph(data, csr, np.asarray(r['labels']), a, b, I, U, r['fwd'], st)
 

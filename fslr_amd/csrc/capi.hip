@@ -170,7 +170,8 @@ void fslr_ctx_destroy(fslr_ctx* c) {
                   c->errw,   c->thr_tmp, c->defer,   c->dchrom,  c->drec,    c->lbounds, c->diag, c->wstat,
                   c->dgate,  c->chist,  c->heavy, c->ent, c->ent_sorted, c->sweep_temp, c->sw_tile, c->sw_wstat, c->ent_ub,
                   c->fdchrom, c->fdrec, c->fdgate, c->crange_f, c->part_cnt, c->grp, c->fmap,
-                  c->rows_col, c->rows_ord, c->rows_keep, c->rows_int, c->rows_l, c->rows_temp};
+                  c->rows_col, c->rows_ord, c->rows_keep, c->rows_int, c->rows_l, c->rows_temp,
+                  c->pf_sel, c->pf_lmap, c->pf_cost};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->sw_total) (void)hipHostFree(c->sw_total);
@@ -337,6 +338,8 @@ int fslr_set_reads(fslr_ctx* c, const fslr_reads* r) {
   c->any_zero_aln = std::find(any_zero.begin(), any_zero.end(), 1) != any_zero.end();
   c->aln_zero_host.swap(zero);
   c->reads_set = true;
+  ++c->reads_gen;
+  c->pf_set = c->pf_on = false;
   c->index_built = false;
   c->lg_set = false;                        // a virtual-read map belongs to the reads it was set for
   c->lg_perm.clear();
@@ -370,7 +373,10 @@ int fslr_set_thresholds(fslr_ctx* c, const int32_t* thr_in) {
     if (rc) return rc;
     HIP_TRY(c, launch_set_thr(c->thr_tmp, c->iv, c->qpos, c->index_built ? c->idx4 : nullptr, c->data_pos,
                               c->have_data_pos ? c->drec : nullptr, static_cast<int>(c->ni), c->stream));
-    if (c->filter_active)                                                    // refresh the filtered records
+    if (c->filter_active && c->pf_on)                                        // refresh the filtered records
+      HIP_TRY(c, launch_pos_gather(c->pf_sel, static_cast<int>(c->pf_end - c->pf_lo), c->dchrom, c->drec, c->dgate,
+                                   c->pf_lmap, c->fdchrom, c->fdrec, c->fdgate, c->stream));
+    else if (c->filter_active)
       HIP_TRY(c, launch_chrom_filter(c->dchrom, c->drec, c->dgate, c->fmap, static_cast<int>(c->ni), c->fdchrom,
                                      c->fdrec, c->fdgate, c->vals2, c->vals, c->temp, c->temp_bytes, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -597,6 +603,8 @@ int fslr_set_reads_rows(fslr_ctx* c, const int64_t* order, const uint8_t* keep, 
   c->rows_cid.swap(cid);
   c->rows_set = true;
   c->reads_set = true;
+  ++c->reads_gen;
+  c->pf_set = c->pf_on = false;
   c->index_built = false;
   c->lg_set = false;
   c->lg_perm.clear();
@@ -877,6 +885,7 @@ static int sweep_front(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64
   s.rng_s = c->rng_s;
   s.umax = c->umax;
   s.ni = static_cast<int>(nix);
+  s.nq = c->filter_active && c->pf_on ? static_cast<int>(c->pf_hi - c->pf_lo) : static_cast<int>(nix);
   s.n_reads = static_cast<int>(c->n);
   s.a_begin = static_cast<int>(a_begin);
   s.a_end = static_cast<int>(a_end);
@@ -1046,7 +1055,7 @@ static int query_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_
     return fail(c, FSLR_ERR_STATE, "the index covers a chromosome subset (fslr_set_chrom_filter): use "
                                    "fslr_sweep_partition / fslr_sweep_evaluate");
   if (int rc = prepare_query(c, p)) return rc;
-  c->zd_host = false;
+  c->zd_host = n_shards > 1;                        // a query shard: the caller decides over every shard
   QueryArgs g;
   g.rmeta = c->rmeta;
   g.iv = c->iv;
@@ -1111,6 +1120,7 @@ static int query_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_
 
 // ---- multi-GPU sweep: chromosome-filtered index, entry partition by owner, owner evaluation ----
 int fslr_set_chrom_filter(fslr_ctx* c, const uint8_t* owned) {
+  if (c) c->pf_on = false;
   if (c) ++c->input_gen;
   if (!c) return FSLR_ERR_INVALID;
   if (!c->reads_set) return fail(c, FSLR_ERR_STATE, "fslr_set_reads first");
@@ -1160,6 +1170,107 @@ int fslr_set_chrom_filter(fslr_ctx* c, const uint8_t* owned) {
   c->n_chroms_f = static_cast<int>(cr.size());
   c->ni_idx = nf;
   return FSLR_OK;
+}
+
+// ---- the position split (multi-GPU) ----------------------------------------------------
+int fslr_position_costs(fslr_ctx* c, int64_t* tests, int64_t* reach, int64_t n_tiles) {
+  if (!c || !tests || !reach) return FSLR_ERR_INVALID;
+  if (!c->index_built || c->filter_active) return fail(c, FSLR_ERR_STATE, "fslr_build_index over every chromosome first");
+  const int64_t nt = (c->ni + 63) / 64;
+  if (n_tiles != nt) return fail(c, FSLR_ERR_INVALID, "n_tiles must be ceil(n_intervals / 64)");
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (2 * std::max<int64_t>(nt, 1) > c->pf_cost_cap) {
+    if (int rc = dalloc(c, &c->pf_cost, 2 * std::max<int64_t>(nt, 1))) return rc;
+    c->pf_cost_cap = 2 * std::max<int64_t>(nt, 1);
+  }
+  HIP_TRY(c, launch_tile_costs(c->rng_s, static_cast<int>(c->ni), c->pf_cost, c->pf_cost + nt, c->stream));
+  if (nt) {
+    HIP_TRY(c, hipMemcpyAsync(tests, c->pf_cost, nt * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(reach, c->pf_cost + nt, nt * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+  }
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FSLR_OK;
+}
+
+namespace {
+// activate the kept selection: its records in data order, renumbered, as the filtered index's input
+int pos_activate(fslr_ctx* c) {
+  const int64_t m = c->pf_end - c->pf_lo;
+  const int nch = static_cast<int>(c->pf_cr.size());
+  if (std::max<int64_t>(nch, 1) > c->crange_f_cap) {
+    if (int rc = dalloc(c, &c->crange_f, std::max<int64_t>(nch, 1))) return rc;
+    c->crange_f_cap = std::max<int64_t>(nch, 1);
+  }
+  if (m > c->f_cap) {
+    int rc;
+    if ((rc = dalloc(c, &c->fdchrom, m)) || (rc = dalloc(c, &c->fdrec, m)) || (rc = dalloc(c, &c->fdgate, m))) return rc;
+    c->f_cap = m;
+  }
+  if (nch) HIP_TRY(c, hipMemcpyAsync(c->crange_f, c->pf_cr.data(), nch * sizeof(int2), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, launch_pos_gather(c->pf_sel, static_cast<int>(m), c->dchrom, c->drec, c->dgate, c->pf_lmap, c->fdchrom,
+                               c->fdrec, c->fdgate, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->filter_active = true;
+  c->pf_on = true;
+  c->n_chroms_f = nch;
+  c->ni_idx = m;
+  c->index_built = false;
+  ++c->input_gen;
+  return FSLR_OK;
+}
+}  // namespace
+
+int fslr_set_position_filter(fslr_ctx* c, int64_t lo, int64_t hi, int64_t end) {
+  if (!c || lo < 0 || hi < lo || end < hi) return FSLR_ERR_INVALID;
+  if (!c->reads_set) return fail(c, FSLR_ERR_STATE, "fslr_set_reads first");
+  if (end > c->ni) return fail(c, FSLR_ERR_INVALID, "position range beyond the index");
+  if (!c->have_data_pos || c->n_chroms > 64 || c->n_shards != 1)
+    return fail(c, FSLR_ERR_STATE, "the position split needs the data-order index build (iv_data_pos, <= 64 chromosomes)");
+  HIP_TRY(c, hipSetDevice(c->device));
+  // the full index once more, with its data -> sorted map (vals)
+  c->filter_active = c->pf_on = false;
+  c->ni_idx = c->ni;
+  if (int rc = fslr_build_index(c)) return rc;
+  if (int rc = ensure_keys(c, false)) return rc;
+  const int64_t m = end - lo;
+  if (std::max<int64_t>(m, 1) > c->pf_sel_cap) {
+    if (int rc = dalloc(c, &c->pf_sel, std::max<int64_t>(m, 1))) return rc;
+    c->pf_sel_cap = std::max<int64_t>(m, 1);
+  }
+  if (c->n_chroms > c->pf_lmap_cap) {
+    if (int rc = dalloc(c, &c->pf_lmap, c->n_chroms)) return rc;
+    c->pf_lmap_cap = c->n_chroms;
+  }
+  // the chromosomes the range meets, numbered in order, and their ranges inside it
+  std::vector<int> lmap(static_cast<size_t>(c->n_chroms), -1);
+  std::vector<int2> cr;
+  int64_t acc = 0;
+  for (int ch = 0; ch < c->n_chroms; ++ch) {
+    const int64_t a = acc, b = acc + c->chrom_counts[ch];
+    acc = b;
+    const int64_t x = std::max(a, lo), y = std::min(b, end);
+    if (x >= y) continue;
+    lmap[ch] = static_cast<int>(cr.size());
+    cr.push_back(make_int2(static_cast<int>(x - lo), static_cast<int>(y - lo)));
+  }
+  HIP_TRY(c, hipMemcpyAsync(c->pf_lmap, lmap.data(), lmap.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, launch_pos_select(c->vals, static_cast<int>(c->ni), static_cast<int>(lo), static_cast<int>(end), c->vals2,
+                               c->qpos, c->pf_sel, c->temp, c->temp_bytes, c->stream));
+  c->index_full = false;                                          // qpos was scratch: the walk parts are gone
+  c->pf_lo = lo;
+  c->pf_hi = hi;
+  c->pf_end = end;
+  c->pf_cr.swap(cr);
+  c->pf_set = true;
+  c->pf_gen = c->reads_gen;
+  return pos_activate(c);
+}
+
+int fslr_use_position_filter(fslr_ctx* c) {
+  if (!c) return FSLR_ERR_INVALID;
+  if (!c->pf_set || c->pf_gen != c->reads_gen) return fail(c, FSLR_ERR_STATE, "no position filter for these reads");
+  HIP_TRY(c, hipSetDevice(c->device));
+  return pos_activate(c);
 }
 
 int fslr_sweep_partition(fslr_ctx* c, const fslr_params* p, int32_t n_dest, int32_t block_shift, void* dst,
@@ -1288,6 +1399,7 @@ int fslr_sweep_evaluate(fslr_ctx* c, const fslr_params* p, const void* entries, 
   s.rlen8 = c->rlen8;
   s.umax = c->umax;
   s.ni = 0;
+  s.nq = 0;
   s.n_reads = static_cast<int>(c->n);
   s.a_begin = 0;
   s.a_end = static_cast<int>(c->n);

@@ -35,6 +35,20 @@ struct fslr_ctx {
   int64_t f_cap = 0;
   int2* crange_f = nullptr;                 // [n_chroms_f] chromosome ranges of the filtered index
   int64_t crange_f_cap = 0;
+  // the position split (fslr_set_position_filter): the index holds the sorted positions [pf_lo, pf_end)
+  // of the full index (pf_on), the sweep queries [pf_lo, pf_hi); the selection is kept (pf_set) so
+  // fslr_use_position_filter re-activates it after a chromosome filter
+  bool pf_set = false, pf_on = false;
+  int64_t pf_lo = 0, pf_hi = 0, pf_end = 0;
+  uint64_t pf_gen = 0;                      // reads_gen of the selection
+  int* pf_sel = nullptr;                    // [pf_end - pf_lo] their data positions, ascending
+  int64_t pf_sel_cap = 0;
+  int* pf_lmap = nullptr;                   // [n_chroms] chromosome -> the range's own numbering, -1
+  int64_t pf_lmap_cap = 0;
+  std::vector<int2> pf_cr;                  // the range's chromosome ranges (local positions)
+  long long* pf_cost = nullptr;             // [2 x tiles] fslr_position_costs scratch
+  int64_t pf_cost_cap = 0;
+  uint64_t reads_gen = 0;                   // bumped by every set_reads
   int* grp = nullptr;                       // [grp_ints()] grouping sort: bucket counts / offsets
   long long* part_cnt = nullptr;            // partition scratch: per (destination, block) counts + offsets
   // the last synchronous fslr_sweep_partition (fslr_sweep_partition_repeat replays it without a readback)

@@ -179,6 +179,7 @@ struct SweepArgs {
   const int2* rng_s;
   const int* umax;
   int ni, n_reads;
+  int nq;                             // query positions [0, nq) of the index (the rest: a forward halo)
   int a_begin, a_end;                 // reads whose pairs (as the lower rank A) are evaluated
   double qlen_cut, nal_cut;
   int4* lb;                           // [n_reads] length-gate ranges (launch_len_bounds)
@@ -207,11 +208,7 @@ struct SweepArgs {
   int wstat_waves;
   hipEvent_t ev[5];                   // (profiling) count | scan | emit | sort | pairs boundaries, or null
   hipEvent_t k0, k1;                  // (profiling) around the sweep kernel launch alone, or null
-  hipEvent_t p0, p1;                  // (profiling) around the pair-stage kernel (k_bucket_pairs) alone, or null
-  // set by launch_sweep_pairs for k_sweep_pairs' list mode (the buckets k_bucket_pairs spilled)
-  const long long* spill;             // [3 x count] {s, e, first chunk}: spilled buckets in ent_sorted, or null
-  const unsigned long long* spill_n;  // count << 40 | total chunks of kChunk2 entries
-  int wbase;                          // first per-wave statistics slot
+  hipEvent_t p0, p1;                  // (profiling) around the pair-stage kernel (k_sweep_pairs) alone, or null
 };
 size_t sweep_temp_bytes(long long ent_cap, long long ni, hipStream_t s);
 int sweep_max_waves();
@@ -236,6 +233,13 @@ hipError_t launch_sweep_partition(const SweepArgs& a, int mode, int shift, int n
 constexpr int kMaxDest = 64;          // destination ranks of one partition
 // the data-order records of the owned chromosomes (lmap[c] >= 0: its local number), compacted in
 // data order (stable), their chromosome renumbered lmap[c]
+// the position split (shard.hip): per 64-position tile its pair tests and forward-window end; the
+// data positions of a sorted-position range and their records in data order
+hipError_t launch_tile_costs(const int2* rng_s, int ni, long long* tests, long long* reach, hipStream_t s);
+hipError_t launch_pos_select(const int* qd, int ni, int lo, int end, int* flags, int* offs, int* sel,
+                             void* temp, size_t temp_bytes, hipStream_t s);
+hipError_t launch_pos_gather(const int* sel, int m, const unsigned* dchrom, const int4* drec, const int2* dgate,
+                             const int* lmap, unsigned* fdchrom, int4* fdrec, int2* fdgate, hipStream_t s);
 hipError_t launch_chrom_filter(const unsigned* dchrom, const int4* drec, const int2* dgate, const int* lmap, int ni,
                                unsigned* fdchrom, int4* fdrec, int2* fdgate, int* flags, int* offs, void* temp,
                                size_t temp_bytes, hipStream_t s);

@@ -181,7 +181,7 @@ def _member(sorted_arr: np.ndarray, x: np.ndarray) -> np.ndarray:
 
 
 def generate(n_reads: int, lmax: int, seed: int, dist: str = 'uniform', cluster_cap: int = 10,
-             lmin: int = 1, size_p: float = 1.0 / 3.0) -> SynthBed:
+             lmin: int = 1, size_p: float = 1.0 / 3.0, chrom_weights=None) -> SynthBed:
     """Generate ``n_reads`` reads (SURVEY §8d model).  Deterministic in ``seed``.
 
     ``cluster_cap``/``size_p`` set the event size ``min(cluster_cap, Geometric(size_p))``;
@@ -204,7 +204,11 @@ def generate(n_reads: int, lmax: int, seed: int, dist: str = 'uniform', cluster_
     ev_off = np.zeros(n_ev + 1, dtype=np.int64)
     np.cumsum(ev_L, out=ev_off[1:])
     n_ev_fill = int(ev_off[-1])
-    ev_chrom = rng.integers(0, len(CHROMS), size=n_ev_fill).astype(np.int32)
+    if chrom_weights is None:
+        ev_chrom = rng.integers(0, len(CHROMS), size=n_ev_fill).astype(np.int32)
+    else:                                        # a skewed genome (e.g. a targeted panel): chromosome weights
+        w = np.asarray(chrom_weights, np.float64)
+        ev_chrom = rng.choice(len(CHROMS), size=n_ev_fill, p=w / w.sum()).astype(np.int32)
     ev_start = rng.integers(1_000_000, 140_000_000, size=n_ev_fill).astype(np.int64)
     ev_len = rng.integers(300, 5001, size=n_ev_fill).astype(np.int64)
 

@@ -75,7 +75,7 @@
 extern "C" {
 #endif
 
-#define FSLR_ABI_VERSION 16
+#define FSLR_ABI_VERSION 18
 #define FSLR_MAX_L 64                /* max intervals per read (bitmask width) */
 #define FSLR_MAX_READS (1 << 25)     /* read rank packs into bits 6..30 of the index record */
 #define FSLR_THR_ZERO_ALN INT32_MIN
@@ -304,6 +304,20 @@ int  fslr_components(fslr_ctx *ctx);
  * fslr_set_reads.  Async; fslr_read_stats / fslr_components / fslr_get_edges follow as after
  * fslr_query. */
 int  fslr_set_chrom_filter(fslr_ctx *ctx, const uint8_t *owned);
+/* The position split: a rank sweeps a contiguous range of the (chrom, start)-sorted
+ * positions, cut where the pair tests balance, whatever the chromosomes.
+ * fslr_position_costs: after fslr_build_index over every chromosome, per tile of 64 sorted positions
+ *   its pair tests (the sum of its forward counts) and the end of its forward window (max q + n_fwd(q)
+ *   + 1); n_tiles = ceil(n_intervals / 64).  Syncs.
+ * fslr_set_position_filter: the next fslr_build_index indexes the sorted positions [lo, end) only and
+ *   fslr_sweep_partition sweeps the pairs whose lower position lies in [lo, hi); end must cover the
+ *   forward windows of [lo, hi) (fslr_position_costs).  Every pair of overlapping intervals is met by
+ *   the rank holding its lower position.  Needs iv_data_pos and <= 64 chromosomes.  Syncs.
+ * fslr_use_position_filter: make the last position filter of these reads active again (after
+ *   fslr_set_chrom_filter, which the edge cap's sharded replay lists its hits with). */
+int  fslr_position_costs(fslr_ctx *ctx, int64_t *tile_tests, int64_t *tile_reach, int64_t n_tiles);
+int  fslr_set_position_filter(fslr_ctx *ctx, int64_t lo, int64_t hi, int64_t end);
+int  fslr_use_position_filter(fslr_ctx *ctx);
 /* Multi-GPU edge cap (cluster.py:197-224).  The replayed loops need every E* edge
  * and every hit of the reads that can reach the cap; a rank's index holds its chromosomes' hits.
  * fslr_copy_edges_iu_device: this context's edges as int32 rows {a, b, I | U << 8, 0} into a device
@@ -439,6 +453,11 @@ int  fslr_get_long_edges(fslr_ctx *ctx, int32_t *a, int32_t *b, int32_t *I, int3
  * graph drops it; fwd[n_reads] (may be NULL) = edges formed in each read's own loop.  The capped
  * graph also becomes the context's edges (fslr_components).  Syncs; out may be NULL. */
 int  fslr_long_pairs(fslr_ctx *ctx, const fslr_params *params, int64_t *n_edges);
+/* fslr_long_pairs for the pairs whose lower-rank read lies in query shard `shard` of `n_shards` (read
+ * blocks of 64 dealt round robin, as fslr_query_shard): the shards together give fslr_long_pairs'
+ * edges, each pair once (the multi-GPU split of the inputs the sweep does not take). */
+int  fslr_long_pairs_shard(fslr_ctx *ctx, const fslr_params *params, int32_t shard, int32_t n_shards,
+                           int64_t *n_edges);
 int  fslr_cap_replay_pairs(fslr_ctx *ctx, int32_t edge_threshold, const int32_t *a, const int32_t *b, int64_t ne,
                            uint8_t *who, int32_t *fwd, fslr_cap_stats *out);
 
