@@ -13,7 +13,7 @@ import numpy as np
 
 LIB_PATH = os.environ.get('FSLR_LIB') or os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libfslr_hip.so')
 
-ABI_VERSION = 15         # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
+ABI_VERSION = 18         # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
 FSLR_OK, FSLR_ERR_ZERO_DIVISION, FSLR_ERR_INVALID, FSLR_ERR_HIP, FSLR_ERR_NOMEM, FSLR_ERR_STATE = range(6)
 FSLR_MAX_L = 64
 FSLR_MAX_READS = 1 << 25
@@ -40,7 +40,9 @@ EXPORTED = ['fslr_abi_version', 'fslr_last_error', 'fslr_ctx_create', 'fslr_ctx_
             'fslr_cap_install_pairs', 'fslr_cap_sizes', 'fslr_cap_dep_local', 'fslr_cap_shard_plan',
             'fslr_cap_shard_pack', 'fslr_cap_replay_shard', 'fslr_cap_copy_changes', 'fslr_cap_apply_changes',
             'fslr_local_forest', 'fslr_copy_forest_pairs', 'fslr_sort_edges', 'fslr_cap_bwd_counts',
-            'fslr_cap_restrict', 'fslr_cap_copy_restricted', 'fslr_cap_install_restricted']
+            'fslr_cap_restrict', 'fslr_cap_copy_restricted', 'fslr_cap_install_restricted', 'fslr_rows_upload',
+            'fslr_set_reads_rows', 'fslr_get_read_codes', 'fslr_get_csr', 'fslr_fold_thresholds',
+            'fslr_position_costs', 'fslr_set_position_filter', 'fslr_use_position_filter', 'fslr_long_pairs_shard']
 
 
 class HipUnavailable(RuntimeError):
@@ -55,6 +57,20 @@ class Reads(ctypes.Structure):
     _fields_ = [('n_reads', ctypes.c_int64), ('n_intervals', ctypes.c_int64), ('n_chroms', ctypes.c_int32)] + [
         (f, ctypes.c_void_p) for f in ('read_off', 'read_qlen2', 'read_nal', 'iv_chrom', 'iv_start', 'iv_end',
                                        'iv_thr', 'iv_data_pos')]
+
+
+class Rows(ctypes.Structure):
+    _fields_ = [('n_rows', ctypes.c_int64), ('n_codes', ctypes.c_int64), ('n_chrom_ids', ctypes.c_int64)] + [
+        (f, ctypes.c_void_p) for f in ('chrom', 'start', 'end', 'aln', 'qcode', 'nal', 'qlen2')]
+
+
+class RowsInfo(ctypes.Structure):
+    _fields_ = [('n_reads', ctypes.c_int64), ('n_intervals', ctypes.c_int64)] + [
+        (f, ctypes.c_int32) for f in ('n_chroms', 'max_len', 'nal_varies', 'general_thresholds', 'any_zero_aln',
+                                      'pad')]
+
+    def as_dict(self):
+        return {f: int(getattr(self, f)) for f, _ in self._fields_ if f != 'pad'}
 
 
 class Params(ctypes.Structure):
@@ -174,6 +190,15 @@ def load(path: str = LIB_PATH):
         'fslr_cap_restrict': (ctypes.c_int, [vp, vp, i32, ctypes.POINTER(ctypes.c_int64)]),
         'fslr_cap_copy_restricted': (ctypes.c_int, [vp, vp, i64]),
         'fslr_cap_install_restricted': (ctypes.c_int, [vp, vp, i64, i32, i32]),
+        'fslr_rows_upload': (ctypes.c_int, [vp, ctypes.POINTER(Rows)]),
+        'fslr_set_reads_rows': (ctypes.c_int, [vp, vp, vp, ctypes.c_double, ctypes.POINTER(RowsInfo)]),
+        'fslr_get_read_codes': (ctypes.c_int, [vp, vp]),
+        'fslr_get_csr': (ctypes.c_int, [vp] + [vp] * 10),
+        'fslr_fold_thresholds': (ctypes.c_int, [vp, ctypes.c_double]),
+        'fslr_position_costs': (ctypes.c_int, [vp, vp, vp, i64]),
+        'fslr_set_position_filter': (ctypes.c_int, [vp, i64, i64, i64]),
+        'fslr_use_position_filter': (ctypes.c_int, [vp]),
+        'fslr_long_pairs_shard': (ctypes.c_int, [vp, ctypes.POINTER(Params), i32, i32, ctypes.POINTER(ctypes.c_int64)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -284,6 +309,7 @@ class Context:
         if arrs[2].size and (arrs[2].min() < 0 or arrs[2].max() >= (1 << 24)):
             raise ValueError('n_alignments must lie in [0, 2**24) for the device path')
         self.n_reads = len(arrs[1])
+        self.n_intervals = len(arrs[3])
 
     def load_csr_any(self, csr, iv_thr):
         """Upload a CSR whose reads may have more than FSLR_MAX_L intervals (fslr_set_reads_any: the
@@ -298,6 +324,57 @@ class Context:
         self._check(self._L.fslr_set_reads_any(self._h, ctypes.byref(r)))
         L = np.diff(arrs[0].astype(np.int64))
         self.n_reads = int(len(arrs[1]) + np.maximum((L + FSLR_MAX_L - 1) // FSLR_MAX_L - 1, 0).sum())
+        self.n_intervals = len(arrs[3])
+
+    def rows_upload(self, cols, n_codes, n_chrom_ids):
+        """fslr_rows_upload: keep_fillings' rows (``cols``: int64 columns chrom, start, end, aln, qcode,
+        nal, qlen2 in file order).  Releases the GIL while it copies (a caller sorts beside it)."""
+        names = ('chrom', 'start', 'end', 'aln', 'qcode', 'nal', 'qlen2')
+        arrs = [np.ascontiguousarray(cols[k], dtype=np.int64) for k in names]
+        self._rows_keep = arrs
+        r = Rows(int(arrs[0].size), int(n_codes), int(n_chrom_ids), *(_ptr(a) for a in arrs))
+        self._check(self._L.fslr_rows_upload(self._h, ctypes.byref(r)))
+
+    def set_reads_rows(self, order, keep, overlap) -> dict:
+        """fslr_set_reads_rows: the reads from the uploaded rows, their start order and mask keep flags
+        (None: all); thresholds folded for ``overlap``.  Returns the info dict; raises FslrError (with
+        ``info``) when the rows do not fit (a read of more than FSLR_MAX_L intervals)."""
+        o = np.ascontiguousarray(order, dtype=np.int64)
+        k = None if keep is None else np.ascontiguousarray(keep).view(np.uint8)
+        info = RowsInfo()
+        rc = self._L.fslr_set_reads_rows(self._h, _ptr(o), _ptr(k) if k is not None else None, float(overlap),
+                                         ctypes.byref(info))
+        self._rows_keep = None
+        d = info.as_dict()
+        if rc != FSLR_OK:
+            try:
+                self._check(rc)
+            except FslrError as e:
+                e.info = d
+                raise
+        self.n_reads = d['n_reads']
+        self.n_intervals = d['n_intervals']
+        return d
+
+    def read_codes(self) -> np.ndarray:
+        out = np.empty(self.n_reads, np.int64)
+        self._check(self._L.fslr_get_read_codes(self._h, _ptr(out)))
+        return out
+
+    def device_csr(self, n_intervals: int, n_chroms: int):
+        """The CSR a fslr_set_reads_rows context holds, as host arrays (fslr_get_csr)."""
+        n, ni = self.n_reads, int(n_intervals)
+        out = dict(read_off=np.empty(n + 1, np.int32), read_qlen2=np.empty(n, np.int32), read_nal=np.empty(n, np.int32),
+                   iv_chrom=np.empty(ni, np.int32), iv_start=np.empty(ni, np.int32), iv_end=np.empty(ni, np.int32),
+                   iv_aln=np.empty(ni, np.int64), iv_thr=np.empty(ni, np.int32), data_pos=np.empty(ni, np.int64))
+        out['chrom_ids'] = np.empty(max(1, int(n_chroms)), np.int64)
+        self._check(self._L.fslr_get_csr(self._h, *(_ptr(out[k]) for k in ('read_off', 'read_qlen2', 'read_nal',
+                                                                        'iv_chrom', 'iv_start', 'iv_end', 'iv_aln',
+                                                                        'iv_thr', 'data_pos', 'chrom_ids'))))
+        return out
+
+    def fold_thresholds(self, overlap):
+        self._check(self._L.fslr_fold_thresholds(self._h, float(overlap)))
 
     def set_long_cutoffs(self, umax):
         u = np.ascontiguousarray(umax, dtype=np.int32)
@@ -352,6 +429,19 @@ class Context:
             return
         o = np.ascontiguousarray(np.asarray(owned, dtype=bool).astype(np.uint8))
         self._check(self._L.fslr_set_chrom_filter(self._h, _ptr(o)))
+
+    def position_costs(self):
+        """(pair tests, forward-window end) per 64-position tile of the full index (fslr_position_costs)."""
+        nt = (self.n_intervals + 63) // 64
+        tests, reach = np.zeros(nt, np.int64), np.zeros(nt, np.int64)
+        self._check(self._L.fslr_position_costs(self._h, _ptr(tests), _ptr(reach), nt))
+        return tests, reach
+
+    def set_position_filter(self, lo, hi, end):
+        self._check(self._L.fslr_set_position_filter(self._h, int(lo), int(hi), int(end)))
+
+    def use_position_filter(self):
+        self._check(self._L.fslr_use_position_filter(self._h))
 
     def sweep_partition(self, qlen_cut, nal_cut, pass_table, n_dest, block_shift, dst, edge_threshold=10):
         """Sweep the (filtered) index and write the match entries grouped by destination
@@ -660,6 +750,14 @@ class Context:
         p = self._params(qlen_cut, nal_cut, pass_table, edge_threshold)
         ne = ctypes.c_int64(0)
         self._check(self._L.fslr_long_pairs(self._h, ctypes.byref(p), ctypes.byref(ne)))
+        return int(ne.value)
+
+    def long_pairs_shard(self, qlen_cut, nal_cut, pass_table, shard, n_shards, edge_threshold=10) -> int:
+        """fslr_long_pairs for the pairs whose lower read lies in query shard ``shard`` of ``n_shards``."""
+        p = self._params(qlen_cut, nal_cut, pass_table, edge_threshold)
+        ne = ctypes.c_int64(0)
+        self._check(self._L.fslr_long_pairs_shard(self._h, ctypes.byref(p), int(shard), int(n_shards),
+                                                  ctypes.byref(ne)))
         return int(ne.value)
 
     def cap_replay_pairs(self, edge_threshold, a, b, n_reads: int):

@@ -31,7 +31,7 @@ import pandas as pd
 
 from . import bam_header, ingest, multi
 from ._lib import FSLR_MAX_L, FSLR_THR_ZERO_ALN, Context
-from .prep import (IntervalData, IntervalItem, build_csr, data_order, first_last_masks, fold_overlap_threshold,
+from .prep import (CSR, IntervalData, IntervalItem, build_csr, data_order, first_last_masks, fold_overlap_threshold,
                    group_span, has_long_reads, mask_keep, pass_table, umax_table)
 
 __all__ = ['IntervalItem', 'keep_fillings', 'rename_chromosomes', 'chrom_to_str', 'calc_coverage',
@@ -201,6 +201,48 @@ class DeviceIntervalIndex:
         self.ctx.build_index()
 
 
+class RowsCSR:
+    """The CSR fslr_set_reads_rows made on the device: the host holds what the CLI reads
+    of it (the qname code of each read rank, the counts and flags); the columns are copied off the
+    device on first use (fslr_get_csr) and then read as a ``prep.CSR``."""
+    start_sorted = True
+
+    def __init__(self, ctx, info):
+        self._ctx, self._host = ctx, None
+        self._n, self._ni = int(info['n_reads']), int(info['n_intervals'])
+        self.n_chroms = int(info['n_chroms'])
+        self.nal_varies = bool(info['nal_varies'])
+        self.read_qcode = ctx.read_codes()
+
+    n_reads = property(lambda self: self._n)
+    n_intervals = property(lambda self: self._ni)
+
+    def host(self) -> CSR:
+        if self._host is None:
+            d = self._ctx.device_csr(self._ni, self.n_chroms)
+            self._host = CSR(read_off=d['read_off'], read_qlen2=d['read_qlen2'], read_nal=d['read_nal'],
+                             iv_chrom=d['iv_chrom'], iv_start=d['iv_start'], iv_end=d['iv_end'], iv_aln=d['iv_aln'],
+                             n_chroms=self.n_chroms, read_qcode=self.read_qcode, data_pos=d['data_pos'],
+                             nal_varies=self.nal_varies, start_sorted=True)
+        return self._host
+
+    def __getattr__(self, name):                 # read_off, iv_*, data_pos: the host copy
+        if name.startswith('_'):
+            raise AttributeError(name)
+        return getattr(self.host(), name)
+
+
+class RowsIndex(DeviceIntervalIndex):
+    """build_interval_trees' result for the columnar CLI: the reads set on the device from rows
+    (fslr_set_reads_rows, thresholds folded there for ``overlap``) and the index built."""
+
+    def __init__(self, data, csr: RowsCSR, ctx: Context, overlap: float):
+        self.source = self.data = data
+        self.csr, self.ctx, self.long = csr, ctx, None
+        self.overlap = float(overlap)
+        ctx.build_index()
+
+
 class MultiGpuIndex:
     """What build_interval_trees returns for ``n_gpus > 1``: the prepared CSR on the host.  The ranks
     (one process per GPU, fslr_amd.multi) upload it and build their chromosomes' index inside
@@ -348,10 +390,9 @@ def query_graph(interval_trees, data, overlap_cutoff, jaccard_threshold, edge_th
     if isinstance(interval_trees, MultiGpuIndex) and (interval_trees.source is data or interval_trees.data is data):
         mg = interval_trees
         thr = fold_overlap_threshold(mg.csr.iv_aln, overlap_cutoff)
-        if multi.sweep_applies(mg.csr, thr) and not has_long_reads(mg.csr):
-            return _query_multi_gpu(mg, thr, jaccard_threshold, edge_threshold, qlen_diff, diff)
-        # overlap <= 0, an aln_size == 0 interval or a read of more than 64 intervals: one GPU
-        interval_trees = DeviceIntervalIndex(mg.data, mg.first_device)
+        # the sweep split, or for overlap <= 0, an aln_size == 0 interval or reads of more than 64
+        # intervals the query-shard split
+        return _query_multi_gpu(mg, thr, jaccard_threshold, edge_threshold, qlen_diff, diff)
     if not isinstance(interval_trees, DeviceIntervalIndex) or (interval_trees.source is not data and
                                                                interval_trees.data is not data):
         interval_trees = DeviceIntervalIndex(data)
@@ -364,7 +405,12 @@ def query_graph(interval_trees, data, overlap_cutoff, jaccard_threshold, edge_th
                       'search reaches first (order-dependent); the first row in data order is used', EdgeCapWarning)
     if idx.long is not None:
         return _query_long(idx, overlap_cutoff, jaccard_threshold, edge_threshold, qlen_diff, diff)
-    ctx.set_thresholds(fold_overlap_threshold(csr.iv_aln, overlap_cutoff))
+    if isinstance(idx, RowsIndex):
+        if idx.overlap != float(overlap_cutoff):             # folded on the device at the upload
+            ctx.fold_thresholds(overlap_cutoff)
+            idx.overlap = float(overlap_cutoff)
+    else:
+        ctx.set_thresholds(fold_overlap_threshold(csr.iv_aln, overlap_cutoff))
     pt = pass_table(jaccard_threshold)
     qcut = 1 - qlen_diff
     ncut = 1 - diff
@@ -474,9 +520,9 @@ def _query_multi_gpu(mg, thr, jaccard_threshold, edge_threshold, qlen_diff, diff
         warnings.warn('n_alignments differs between rows of one read; the reference then uses the row its '
                       'search reaches first (order-dependent); the first row in data order is used', EdgeCapWarning)
     r = multi.query(csr, thr, 1 - qlen_diff, 1 - diff, pass_table(jaccard_threshold), int(edge_threshold),
-                    mg.n_gpus, first_device=mg.first_device)
+                    mg.n_gpus, first_device=mg.first_device, cutoffs=list(jaccard_threshold))
     a, b, I, U = r['edges']
-    st = {'engine': 'sweep', 'n_gpus': mg.n_gpus, 'backend': r['backend'], 'evaluated_pairs': -1,
+    st = {'engine': r.get('path', 'sweep'), 'n_gpus': mg.n_gpus, 'backend': r['backend'], 'evaluated_pairs': -1,
           'n_edges': int(a.shape[0]), 'max_fwd': r['max_fwd'], 'cap': r['cap'], 'capped': r['capped']}
     return RawGraph(data, csr, np.asarray(r['labels']), a, b, I, U, r['fwd'], st)
 

@@ -219,8 +219,10 @@ __global__ void k_cap_tfin(const int* __restrict__ T, int nt, const int4* __rest
 }
 
 // every read is a candidate (fslr_long_pairs: the pairs of every read's hits)
-__global__ void k_cap_all(int* __restrict__ state, int n) {
-  for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < n; x += gridDim.x * blockDim.x) state[x] = 1;
+// every read (fslr_long_pairs), or a query shard's reads (blocks of 64 ranks dealt round robin)
+__global__ void k_cap_all(int* __restrict__ state, int n, int shard, int n_shards) {
+  for (int x = blockIdx.x * blockDim.x + threadIdx.x; x < n; x += gridDim.x * blockDim.x)
+    state[x] = shard_owns(x, shard, n_shards) ? 1 : 0;
 }
 
 __global__ void k_cap_tlist(const int* __restrict__ state, const unsigned long long* __restrict__ v,
@@ -1740,6 +1742,7 @@ struct CapWork {
   long long* host = nullptr;          // pinned, device-mapped
   long long* host_dev = nullptr;
   int thr = 0;
+  int all_shard = 0, all_n_shards = 1;  // cap_local(all_reads): the query shard whose reads form T
   int64_t n = 0, ne = 0, nt = 0, nti = 0, nloc = 0, nseq = 0, ns = 0;
   // the read space of the replay: the uploaded reads, or with reads of more than FSLR_MAX_L
   // intervals (fslr_set_long_reads) the real reads behind the virtual ones
@@ -2031,7 +2034,7 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, const int2* E, const int* F, int
   // 1. closure.  Frontier rounds (batches of 16, one sync per batch), or FSLR_CAP_CLOSURE=rounds:
   // rounds over every edge and read in batches of 8 (chg[0] = 1 starts each batch)
   const bool frontier = !all_reads && (rstart || !cap_rounds_closure());
-  if (all_reads) k_cap_all<<<grid_for(n), 256, 0, s>>>(w->state, static_cast<int>(n));
+  if (all_reads) k_cap_all<<<grid_for(n), 256, 0, s>>>(w->state, static_cast<int>(n), w->all_shard, w->all_n_shards);
   else if (!frontier) k_cap_init<<<grid_for(n), 256, 0, s>>>(F, static_cast<int>(n), thr, w->state, w->back);
   HIP_TRY(c, hipGetLastError());
   if (frontier) {
@@ -2670,7 +2673,12 @@ extern "C" int fslr_cap_replay(fslr_ctx* c, const int32_t* counts, const int32_t
 }
 
 extern "C" int fslr_long_pairs(fslr_ctx* c, const fslr_params* p, int64_t* n_edges) {
-  if (!c || !p || !n_edges) return FSLR_ERR_INVALID;
+  return fslr_long_pairs_shard(c, p, 0, 1, n_edges);
+}
+
+extern "C" int fslr_long_pairs_shard(fslr_ctx* c, const fslr_params* p, int32_t shard, int32_t n_shards,
+                                     int64_t* n_edges) {
+  if (!c || !p || !n_edges || n_shards < 1 || shard < 0 || shard >= n_shards) return FSLR_ERR_INVALID;
   *n_edges = 0;
   if (!c->lg_set) return fail(c, FSLR_ERR_STATE, "fslr_set_long_reads first");
   if (!c->index_built || c->filter_active) return fail(c, FSLR_ERR_STATE, "fslr_build_index (every chromosome) first");
@@ -2684,7 +2692,13 @@ extern "C" int fslr_long_pairs(fslr_ctx* c, const fslr_params* p, int64_t* n_edg
   std::memset(&c->cap_stats, 0, sizeof(c->cap_stats));
   CapWork* w = nullptr;
   if (int rc = cap_work(c, &w)) return rc;
-  if (int rc = cap_local(c, 0, w, c->edges, c->fwd, 0, true)) return rc;          // every read's hits, any thresholds
+  // the shard's reads' hits (every read: n_shards 1), any thresholds; each pair from its lower read's slot
+  w->all_shard = shard;
+  w->all_n_shards = n_shards;
+  const int rc_local = cap_local(c, 0, w, c->edges, c->fwd, 0, true);
+  w->all_shard = 0;
+  w->all_n_shards = 1;
+  if (rc_local) return rc_local;
   w->nseq = w->nloc;
   if (int rc = cap_slots(c, w)) return rc;
   const int ns = static_cast<int>(w->ns);

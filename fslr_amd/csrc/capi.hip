@@ -169,7 +169,9 @@ void fslr_ctx_destroy(fslr_ctx* c) {
                   c->upl,    c->upl64,
                   c->errw,   c->thr_tmp, c->defer,   c->dchrom,  c->drec,    c->lbounds, c->diag, c->wstat,
                   c->dgate,  c->chist,  c->heavy, c->ent, c->ent_sorted, c->sweep_temp, c->sw_tile, c->sw_wstat, c->ent_ub,
-                  c->fdchrom, c->fdrec, c->fdgate, c->crange_f, c->part_cnt, c->grp, c->fmap};
+                  c->fdchrom, c->fdrec, c->fdgate, c->crange_f, c->part_cnt, c->grp, c->fmap,
+                  c->rows_col, c->rows_ord, c->rows_keep, c->rows_int, c->rows_l, c->rows_temp,
+                  c->pf_sel, c->pf_lmap, c->pf_cost};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->sw_total) (void)hipHostFree(c->sw_total);
@@ -325,6 +327,7 @@ int fslr_set_reads(fslr_ctx* c, const fslr_reads* r) {
   HIP_TRY(c, hipMemcpyAsync(c->crange, cr.data(), cr.size() * sizeof(int2), hipMemcpyHostToDevice, st));
   HIP_TRY(c, hipStreamSynchronize(st));
   c->have_data_pos = r->iv_data_pos != nullptr;
+  c->rows_set = false;
   c->n = n;
   c->ni = ni;
   c->ni_idx = ni;
@@ -335,6 +338,8 @@ int fslr_set_reads(fslr_ctx* c, const fslr_reads* r) {
   c->any_zero_aln = std::find(any_zero.begin(), any_zero.end(), 1) != any_zero.end();
   c->aln_zero_host.swap(zero);
   c->reads_set = true;
+  ++c->reads_gen;
+  c->pf_set = c->pf_on = false;
   c->index_built = false;
   c->lg_set = false;                        // a virtual-read map belongs to the reads it was set for
   c->lg_perm.clear();
@@ -368,12 +373,305 @@ int fslr_set_thresholds(fslr_ctx* c, const int32_t* thr_in) {
     if (rc) return rc;
     HIP_TRY(c, launch_set_thr(c->thr_tmp, c->iv, c->qpos, c->index_built ? c->idx4 : nullptr, c->data_pos,
                               c->have_data_pos ? c->drec : nullptr, static_cast<int>(c->ni), c->stream));
-    if (c->filter_active)                                                    // refresh the filtered records
+    if (c->filter_active && c->pf_on)                                        // refresh the filtered records
+      HIP_TRY(c, launch_pos_gather(c->pf_sel, static_cast<int>(c->pf_end - c->pf_lo), c->dchrom, c->drec, c->dgate,
+                                   c->pf_lmap, c->fdchrom, c->fdrec, c->fdgate, c->stream));
+    else if (c->filter_active)
       HIP_TRY(c, launch_chrom_filter(c->dchrom, c->drec, c->dgate, c->fmap, static_cast<int>(c->ni), c->fdchrom,
                                      c->fdrec, c->fdgate, c->vals2, c->vals, c->temp, c->temp_bytes, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
   }
   c->thr_mode = thr_mode_of(thr, c->ni);
+  return FSLR_OK;
+}
+
+// ---- the clustering input from rows (rows.hip) ------------------------------------------------------
+int fslr_rows_upload(fslr_ctx* c, const fslr_rows* r) {
+  if (!c || !r || r->n_rows < 1 || r->n_rows >= (int64_t(1) << 31) - 1 || r->n_codes < 1 ||
+      r->n_codes >= (int64_t(1) << 31) || r->n_chrom_ids < 1 || r->n_chrom_ids >= (1 << 24))
+    return FSLR_ERR_INVALID;
+  if (!r->chrom || !r->start || !r->end || !r->aln || !r->qcode || !r->nal || !r->qlen2)
+    return fail(c, FSLR_ERR_INVALID, "null array");
+  HIP_TRY(c, hipSetDevice(c->device));
+  const int64_t n = r->n_rows;
+  c->rows_n = 0;
+  if (n > c->rows_cap) {
+    int rc;
+    if ((rc = dalloc(c, &c->rows_col, 7 * static_cast<size_t>(n))) || (rc = dalloc(c, &c->rows_ord, n)) ||
+        (rc = dalloc(c, &c->rows_keep, n)) || (rc = dalloc(c, &c->rows_l, 2 * static_cast<size_t>(n))))
+      return rc;
+    c->rows_cap = n;
+  }
+  const int64_t* src[7] = {r->chrom, r->start, r->end, r->aln, r->qcode, r->nal, r->qlen2};
+  for (int k = 0; k < 7; ++k)
+    HIP_TRY(c, hipMemcpyAsync(c->rows_col + k * n, src[k], static_cast<size_t>(n) * sizeof(long long),
+                              hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->rows_n = n;
+  c->rows_codes = r->n_codes;
+  c->rows_cids = r->n_chrom_ids;
+  return FSLR_OK;
+}
+
+namespace {
+// the build's views of the rows arenas (capacity rows_cap; the per-code and per-chromosome arrays last)
+RowsWork rows_views(fslr_ctx* c) {
+  const int64_t n = c->rows_cap;
+  RowsWork w{};
+  const long long* col = c->rows_col;
+  w.chrom = col;
+  w.start = col + n;
+  w.end = col + 2 * n;
+  w.aln = col + 3 * n;
+  w.qcode = col + 4 * n;
+  w.nal = col + 5 * n;
+  w.qlen2 = col + 6 * n;
+  int* p = c->rows_int;
+  auto take = [&](int64_t k) {
+    int* q = p;
+    p += (k + 63) / 64 * 64;
+    return q;
+  };
+  w.ord32 = take(n);
+  w.flag = reinterpret_cast<unsigned char*>(take(n / 4 + 1));
+  w.sel = take(n);
+  w.nsel = take(1);
+  w.f = take(n);
+  w.fscan = take(n);
+  w.key = take(n);
+  w.val = take(n);
+  w.key_s = take(n);
+  w.perm = take(n);
+  w.off = take(n + 1);
+  w.ch_raw = take(n);
+  w.st32 = take(n);
+  w.en32 = take(n);
+  w.dp = take(n);            // the index build reads the data order from c->data_pos (a copy below)
+  w.q2 = take(n);
+  w.nal32 = take(n);
+  w.present = take(c->rows_cids);
+  w.stat = take(4);
+  w.err = take(1);
+  w.first = take(c->rows_codes);
+  w.aln_k = c->rows_l;
+  w.code_of_rank = c->rows_l + n;
+  w.temp = c->rows_temp;
+  w.temp_bytes = c->rows_temp_bytes;
+  return w;
+}
+
+int64_t rows_int_need(int64_t n, int64_t codes, int64_t cids) {
+  return 20 * ((n + 64) / 64 * 64 + 64) + (codes + 63) / 64 * 64 + (cids + 63) / 64 * 64 + 4 * 64 + 4 * n;
+}
+}  // namespace
+
+int fslr_set_reads_rows(fslr_ctx* c, const int64_t* order, const uint8_t* keep, double overlap,
+                        fslr_rows_info* info) {
+  if (!c || !order || !info) return FSLR_ERR_INVALID;
+  std::memset(info, 0, sizeof(*info));
+  const int64_t n = c->rows_n;
+  if (n < 1) return fail(c, FSLR_ERR_STATE, "fslr_rows_upload first");
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t st = c->stream;
+  int rc;
+  const int64_t need = rows_int_need(c->rows_cap, c->rows_codes, c->rows_cids) + 2 * c->rows_cids;
+  if (need > c->rows_int_cap) {
+    if ((rc = dalloc(c, &c->rows_int, static_cast<size_t>(need)))) return rc;
+    c->rows_int_cap = need;
+  }
+  const size_t tb = rows_temp_bytes(c->rows_cap, st);
+  if (tb > c->rows_temp_bytes) {
+    if (c->rows_temp) (void)hipFree(c->rows_temp);
+    c->rows_temp = nullptr;
+    HIP_TRY(c, hipMalloc(&c->rows_temp, tb));
+    c->rows_temp_bytes = tb;
+  }
+  RowsWork w = rows_views(c);
+  int* dmap_d = c->rows_int + rows_int_need(c->rows_cap, c->rows_codes, c->rows_cids);
+  HIP_TRY(c, hipMemcpyAsync(c->rows_ord, order, static_cast<size_t>(n) * sizeof(long long), hipMemcpyHostToDevice, st));
+  if (keep) HIP_TRY(c, hipMemcpyAsync(c->rows_keep, keep, static_cast<size_t>(n), hipMemcpyHostToDevice, st));
+  HIP_TRY(c, hipMemsetAsync(w.stat, 0, 4 * sizeof(int), st));
+  HIP_TRY(c, hipMemsetAsync(w.err, 0, sizeof(int), st));
+  // 1. the data list (prepare_data + mask_sequences2) and the read ranks (first appearance)
+  long long mr[2] = {0, 0};
+  HIP_TRY(c, rows_rank(w, n, c->rows_codes, c->rows_ord, keep ? c->rows_keep : nullptr, mr, st));
+  const int64_t m = mr[0], n_reads = mr[1];
+  if (m < 1) return fail(c, FSLR_ERR_INVALID, "no interval is left after the mask");
+  if (n_reads >= FSLR_MAX_READS) return fail(c, FSLR_ERR_INVALID, "read count out of range");
+  // 2. grouping into the CSR; the read lengths, gate values and the chromosomes present
+  HIP_TRY(c, rows_csr(w, static_cast<int>(m), static_cast<int>(n_reads), c->rows_cids, st));
+  int stat[4] = {0, 0, 0, 0}, err = 0;
+  std::vector<int> present(static_cast<size_t>(c->rows_cids));
+  HIP_TRY(c, hipMemcpyAsync(stat, w.stat, sizeof(stat), hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipMemcpyAsync(&err, w.err, sizeof(err), hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipMemcpyAsync(present.data(), w.present, present.size() * sizeof(int), hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipStreamSynchronize(st));
+  info->n_reads = n_reads;
+  info->n_intervals = m;
+  info->max_len = stat[0];
+  info->nal_varies = stat[1];
+  if (err & kRowsErrOrder) return fail(c, FSLR_ERR_INVALID, "order holds a row out of range");
+  if (err & kRowsErrCode) return fail(c, FSLR_ERR_INVALID, "qname code out of range");
+  if (err & kRowsErrChrom) return fail(c, FSLR_ERR_INVALID, "chrom id out of range");
+  if (err & kRowsErrCoord) return fail(c, FSLR_ERR_INVALID, "interval coordinates out of [0, 2^30)");
+  if (err & kRowsErrNal) return fail(c, FSLR_ERR_INVALID, "n_alignments outside [0, 2^24)");
+  if (err & kRowsErrQlen) return fail(c, FSLR_ERR_INVALID, "qlen2 outside [0, 2^31)");
+  if (stat[0] > FSLR_MAX_L)
+    return fail(c, FSLR_ERR_INVALID, "a read of more than FSLR_MAX_L intervals: set the reads with fslr_set_reads_any");
+  // 3. dense chromosome ids (ascending numbers of the chromosomes present), thresholds, packing
+  std::vector<int> dmap(static_cast<size_t>(c->rows_cids), 0);
+  std::vector<int64_t> cid;
+  for (int64_t k = 0; k < c->rows_cids; ++k)
+    if (present[k]) {
+      dmap[k] = static_cast<int>(cid.size());
+      cid.push_back(k);
+    }
+  const int n_chroms = std::max<int>(1, static_cast<int>(cid.size()));
+  info->n_chroms = n_chroms;
+  if ((rc = ensure_capacity(c, n_reads, m, n_chroms))) return rc;
+  if (n_chroms + 2 > c->upl64_cap) {
+    if ((rc = dalloc(c, &c->upl64, static_cast<size_t>(n_chroms + 2)))) return rc;
+    c->upl64_cap = n_chroms + 2;
+  }
+  HIP_TRY(c, hipMemcpyAsync(dmap_d, dmap.data(), dmap.size() * sizeof(int), hipMemcpyHostToDevice, st));
+  // the dense ids go to w.val (the sort's input values, free after it) and the thresholds to thr_tmp
+  int* ch_dense = w.val;
+  HIP_TRY(c, rows_fold(w.aln_k, static_cast<int>(m), overlap, w.ch_raw, dmap_d, c->thr_tmp, ch_dense, w.stat, st));
+  HIP_TRY(c, hipMemcpyAsync(c->data_pos, w.dp, static_cast<size_t>(m) * sizeof(int), hipMemcpyDeviceToDevice, st));
+  unsigned long long* d_cnt = c->upl64;
+  unsigned long long* d_err = c->upl64 + n_chroms;
+  HIP_TRY(c, hipMemsetAsync(d_cnt, 0, static_cast<size_t>(n_chroms) * sizeof(unsigned long long), st));
+  HIP_TRY(c, hipMemsetAsync(d_err, 0xff, 2 * sizeof(unsigned long long), st));
+  UploadArgs ua{};
+  ua.off = w.off;
+  ua.qlen2 = w.q2;
+  ua.nal = w.nal32;
+  ua.chrom = ch_dense;
+  ua.start = w.st32;
+  ua.end = w.en32;
+  ua.thr = c->thr_tmp;
+  ua.dp = c->data_pos;
+  ua.n = static_cast<int>(n_reads);
+  ua.ni = static_cast<int>(m);
+  ua.n_chroms = n_chroms;
+  ua.reads_ok = true;
+  ua.iv = c->iv;
+  ua.rmeta = c->rmeta;
+  ua.rlen8 = c->rlen8;
+  ua.dch = c->dchrom;
+  ua.drc = c->drec;
+  ua.dgt = c->dgate;
+  ua.inv = c->vals2;
+  ua.chrom_cnt = d_cnt;
+  ua.err = d_err;
+  HIP_TRY(c, launch_upload_pack(ua, st));
+  std::vector<int64_t> chrom_counts(static_cast<size_t>(n_chroms), 0);
+  unsigned long long uerr[2] = {0, 0};
+  HIP_TRY(c, hipMemcpyAsync(chrom_counts.data(), d_cnt, chrom_counts.size() * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipMemcpyAsync(uerr, d_err, sizeof(uerr), hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipMemcpyAsync(stat, w.stat, sizeof(stat), hipMemcpyDeviceToHost, st));
+  HIP_TRY(c, hipStreamSynchronize(st));
+  c->reads_set = false;
+  if (uerr[0] != ~0ull || uerr[1] != ~0ull) return fail(c, FSLR_ERR_STATE, "rows upload: inconsistent packing");
+  info->general_thresholds = stat[2];
+  info->any_zero_aln = stat[3];
+  std::vector<unsigned char> zero(static_cast<size_t>(m), 0);
+  if (stat[3]) {
+    HIP_TRY(c, rows_zero_flags(c->thr_tmp, static_cast<int>(m), c->rows_keep, st));
+    HIP_TRY(c, hipMemcpyAsync(zero.data(), c->rows_keep, zero.size(), hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipStreamSynchronize(st));
+  }
+  std::vector<int2> cr(static_cast<size_t>(n_chroms), make_int2(0, 0));
+  int64_t acc = 0;
+  for (int k = 0; k < n_chroms; ++k) {
+    cr[k] = make_int2(static_cast<int>(acc), static_cast<int>(acc + chrom_counts[k]));
+    acc += chrom_counts[k];
+  }
+  HIP_TRY(c, hipMemcpyAsync(c->crange, cr.data(), cr.size() * sizeof(int2), hipMemcpyHostToDevice, st));
+  HIP_TRY(c, hipStreamSynchronize(st));
+  c->have_data_pos = true;
+  c->n = n_reads;
+  c->ni = m;
+  c->ni_idx = m;
+  c->filter_active = false;
+  c->chrom_counts.swap(chrom_counts);
+  c->n_chroms = n_chroms;
+  c->thr_mode = stat[2] ? 1 : 0;
+  c->any_zero_aln = stat[3] != 0;
+  c->aln_zero_host.swap(zero);
+  c->rows_dmap.swap(dmap);
+  c->rows_cid.swap(cid);
+  c->rows_set = true;
+  c->reads_set = true;
+  ++c->reads_gen;
+  c->pf_set = c->pf_on = false;
+  c->index_built = false;
+  c->lg_set = false;
+  c->lg_perm.clear();
+  c->edges_global = false;
+  c->cap_gmode = false;
+  ++c->input_gen;
+  return FSLR_OK;
+}
+
+int fslr_get_read_codes(fslr_ctx* c, int64_t* codes) {
+  if (!c || (!codes && c->n)) return FSLR_ERR_INVALID;
+  if (!c->rows_set) return fail(c, FSLR_ERR_STATE, "the reads were not set by fslr_set_reads_rows");
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (c->n)
+    HIP_TRY(c, hipMemcpyAsync(codes, c->rows_l + c->rows_cap, static_cast<size_t>(c->n) * sizeof(int64_t),
+                              hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FSLR_OK;
+}
+
+int fslr_get_csr(fslr_ctx* c, int32_t* read_off, int32_t* read_qlen2, int32_t* read_nal, int32_t* iv_chrom,
+                 int32_t* iv_start, int32_t* iv_end, int64_t* iv_aln, int32_t* iv_thr, int64_t* data_pos,
+                 int64_t* chrom_ids) {
+  if (!c) return FSLR_ERR_INVALID;
+  if (!c->rows_set) return fail(c, FSLR_ERR_STATE, "the reads were not set by fslr_set_reads_rows");
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipStream_t st = c->stream;
+  const RowsWork w = rows_views(c);
+  const size_t nb = static_cast<size_t>(c->n) * sizeof(int), ib = static_cast<size_t>(c->ni) * sizeof(int);
+  if (read_off) HIP_TRY(c, hipMemcpyAsync(read_off, w.off, nb + sizeof(int), hipMemcpyDeviceToHost, st));
+  if (read_qlen2) HIP_TRY(c, hipMemcpyAsync(read_qlen2, w.q2, nb, hipMemcpyDeviceToHost, st));
+  if (read_nal) HIP_TRY(c, hipMemcpyAsync(read_nal, w.nal32, nb, hipMemcpyDeviceToHost, st));
+  if (iv_chrom) HIP_TRY(c, hipMemcpyAsync(iv_chrom, w.val, ib, hipMemcpyDeviceToHost, st));
+  if (iv_start) HIP_TRY(c, hipMemcpyAsync(iv_start, w.st32, ib, hipMemcpyDeviceToHost, st));
+  if (iv_end) HIP_TRY(c, hipMemcpyAsync(iv_end, w.en32, ib, hipMemcpyDeviceToHost, st));
+  if (iv_thr) HIP_TRY(c, hipMemcpyAsync(iv_thr, c->thr_tmp, ib, hipMemcpyDeviceToHost, st));
+  if (iv_aln) HIP_TRY(c, hipMemcpyAsync(iv_aln, w.aln_k, static_cast<size_t>(c->ni) * sizeof(int64_t),
+                                        hipMemcpyDeviceToHost, st));
+  std::vector<int> dp;
+  if (data_pos) {
+    dp.resize(static_cast<size_t>(c->ni));
+    HIP_TRY(c, hipMemcpyAsync(dp.data(), w.dp, ib, hipMemcpyDeviceToHost, st));
+  }
+  HIP_TRY(c, hipStreamSynchronize(st));
+  if (data_pos)
+    for (int64_t k = 0; k < c->ni; ++k) data_pos[k] = dp[k];
+  if (chrom_ids) std::copy(c->rows_cid.begin(), c->rows_cid.end(), chrom_ids);
+  return FSLR_OK;
+}
+
+int fslr_fold_thresholds(fslr_ctx* c, double overlap) {
+  if (!c) return FSLR_ERR_INVALID;
+  if (!c->reads_set || !c->rows_set) return fail(c, FSLR_ERR_STATE, "the reads were not set by fslr_set_reads_rows");
+  HIP_TRY(c, hipSetDevice(c->device));
+  ++c->input_gen;
+  const RowsWork w = rows_views(c);
+  HIP_TRY(c, hipMemsetAsync(w.stat + 2, 0, 2 * sizeof(int), c->stream));
+  HIP_TRY(c, rows_fold(w.aln_k, static_cast<int>(c->ni), overlap, nullptr, nullptr, c->thr_tmp, nullptr, w.stat,
+                       c->stream));
+  if (c->index_built && (c->built_n_shards != 1 || c->filter_active)) c->index_built = false;
+  if (int rc = ensure_walk_index(c)) return rc;
+  HIP_TRY(c, launch_set_thr(c->thr_tmp, c->iv, c->qpos, c->index_built ? c->idx4 : nullptr, c->data_pos, c->drec,
+                            static_cast<int>(c->ni), c->stream));
+  int stat[2] = {0, 0};
+  HIP_TRY(c, hipMemcpyAsync(stat, w.stat + 2, sizeof(stat), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->thr_mode = stat[0] ? 1 : 0;
   return FSLR_OK;
 }
 
@@ -587,6 +885,7 @@ static int sweep_front(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64
   s.rng_s = c->rng_s;
   s.umax = c->umax;
   s.ni = static_cast<int>(nix);
+  s.nq = c->filter_active && c->pf_on ? static_cast<int>(c->pf_hi - c->pf_lo) : static_cast<int>(nix);
   s.n_reads = static_cast<int>(c->n);
   s.a_begin = static_cast<int>(a_begin);
   s.a_end = static_cast<int>(a_end);
@@ -756,7 +1055,7 @@ static int query_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_
     return fail(c, FSLR_ERR_STATE, "the index covers a chromosome subset (fslr_set_chrom_filter): use "
                                    "fslr_sweep_partition / fslr_sweep_evaluate");
   if (int rc = prepare_query(c, p)) return rc;
-  c->zd_host = false;
+  c->zd_host = n_shards > 1;                        // a query shard: the caller decides over every shard
   QueryArgs g;
   g.rmeta = c->rmeta;
   g.iv = c->iv;
@@ -821,6 +1120,7 @@ static int query_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_
 
 // ---- multi-GPU sweep: chromosome-filtered index, entry partition by owner, owner evaluation ----
 int fslr_set_chrom_filter(fslr_ctx* c, const uint8_t* owned) {
+  if (c) c->pf_on = false;
   if (c) ++c->input_gen;
   if (!c) return FSLR_ERR_INVALID;
   if (!c->reads_set) return fail(c, FSLR_ERR_STATE, "fslr_set_reads first");
@@ -870,6 +1170,107 @@ int fslr_set_chrom_filter(fslr_ctx* c, const uint8_t* owned) {
   c->n_chroms_f = static_cast<int>(cr.size());
   c->ni_idx = nf;
   return FSLR_OK;
+}
+
+// ---- the position split (multi-GPU) ----------------------------------------------------
+int fslr_position_costs(fslr_ctx* c, int64_t* tests, int64_t* reach, int64_t n_tiles) {
+  if (!c || !tests || !reach) return FSLR_ERR_INVALID;
+  if (!c->index_built || c->filter_active) return fail(c, FSLR_ERR_STATE, "fslr_build_index over every chromosome first");
+  const int64_t nt = (c->ni + 63) / 64;
+  if (n_tiles != nt) return fail(c, FSLR_ERR_INVALID, "n_tiles must be ceil(n_intervals / 64)");
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (2 * std::max<int64_t>(nt, 1) > c->pf_cost_cap) {
+    if (int rc = dalloc(c, &c->pf_cost, 2 * std::max<int64_t>(nt, 1))) return rc;
+    c->pf_cost_cap = 2 * std::max<int64_t>(nt, 1);
+  }
+  HIP_TRY(c, launch_tile_costs(c->rng_s, static_cast<int>(c->ni), c->pf_cost, c->pf_cost + nt, c->stream));
+  if (nt) {
+    HIP_TRY(c, hipMemcpyAsync(tests, c->pf_cost, nt * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(reach, c->pf_cost + nt, nt * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+  }
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FSLR_OK;
+}
+
+namespace {
+// activate the kept selection: its records in data order, renumbered, as the filtered index's input
+int pos_activate(fslr_ctx* c) {
+  const int64_t m = c->pf_end - c->pf_lo;
+  const int nch = static_cast<int>(c->pf_cr.size());
+  if (std::max<int64_t>(nch, 1) > c->crange_f_cap) {
+    if (int rc = dalloc(c, &c->crange_f, std::max<int64_t>(nch, 1))) return rc;
+    c->crange_f_cap = std::max<int64_t>(nch, 1);
+  }
+  if (m > c->f_cap) {
+    int rc;
+    if ((rc = dalloc(c, &c->fdchrom, m)) || (rc = dalloc(c, &c->fdrec, m)) || (rc = dalloc(c, &c->fdgate, m))) return rc;
+    c->f_cap = m;
+  }
+  if (nch) HIP_TRY(c, hipMemcpyAsync(c->crange_f, c->pf_cr.data(), nch * sizeof(int2), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, launch_pos_gather(c->pf_sel, static_cast<int>(m), c->dchrom, c->drec, c->dgate, c->pf_lmap, c->fdchrom,
+                               c->fdrec, c->fdgate, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->filter_active = true;
+  c->pf_on = true;
+  c->n_chroms_f = nch;
+  c->ni_idx = m;
+  c->index_built = false;
+  ++c->input_gen;
+  return FSLR_OK;
+}
+}  // namespace
+
+int fslr_set_position_filter(fslr_ctx* c, int64_t lo, int64_t hi, int64_t end) {
+  if (!c || lo < 0 || hi < lo || end < hi) return FSLR_ERR_INVALID;
+  if (!c->reads_set) return fail(c, FSLR_ERR_STATE, "fslr_set_reads first");
+  if (end > c->ni) return fail(c, FSLR_ERR_INVALID, "position range beyond the index");
+  if (!c->have_data_pos || c->n_chroms > 64 || c->n_shards != 1)
+    return fail(c, FSLR_ERR_STATE, "the position split needs the data-order index build (iv_data_pos, <= 64 chromosomes)");
+  HIP_TRY(c, hipSetDevice(c->device));
+  // the full index once more, with its data -> sorted map (vals)
+  c->filter_active = c->pf_on = false;
+  c->ni_idx = c->ni;
+  if (int rc = fslr_build_index(c)) return rc;
+  if (int rc = ensure_keys(c, false)) return rc;
+  const int64_t m = end - lo;
+  if (std::max<int64_t>(m, 1) > c->pf_sel_cap) {
+    if (int rc = dalloc(c, &c->pf_sel, std::max<int64_t>(m, 1))) return rc;
+    c->pf_sel_cap = std::max<int64_t>(m, 1);
+  }
+  if (c->n_chroms > c->pf_lmap_cap) {
+    if (int rc = dalloc(c, &c->pf_lmap, c->n_chroms)) return rc;
+    c->pf_lmap_cap = c->n_chroms;
+  }
+  // the chromosomes the range meets, numbered in order, and their ranges inside it
+  std::vector<int> lmap(static_cast<size_t>(c->n_chroms), -1);
+  std::vector<int2> cr;
+  int64_t acc = 0;
+  for (int ch = 0; ch < c->n_chroms; ++ch) {
+    const int64_t a = acc, b = acc + c->chrom_counts[ch];
+    acc = b;
+    const int64_t x = std::max(a, lo), y = std::min(b, end);
+    if (x >= y) continue;
+    lmap[ch] = static_cast<int>(cr.size());
+    cr.push_back(make_int2(static_cast<int>(x - lo), static_cast<int>(y - lo)));
+  }
+  HIP_TRY(c, hipMemcpyAsync(c->pf_lmap, lmap.data(), lmap.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, launch_pos_select(c->vals, static_cast<int>(c->ni), static_cast<int>(lo), static_cast<int>(end), c->vals2,
+                               c->qpos, c->pf_sel, c->temp, c->temp_bytes, c->stream));
+  c->index_full = false;                                          // qpos was scratch: the walk parts are gone
+  c->pf_lo = lo;
+  c->pf_hi = hi;
+  c->pf_end = end;
+  c->pf_cr.swap(cr);
+  c->pf_set = true;
+  c->pf_gen = c->reads_gen;
+  return pos_activate(c);
+}
+
+int fslr_use_position_filter(fslr_ctx* c) {
+  if (!c) return FSLR_ERR_INVALID;
+  if (!c->pf_set || c->pf_gen != c->reads_gen) return fail(c, FSLR_ERR_STATE, "no position filter for these reads");
+  HIP_TRY(c, hipSetDevice(c->device));
+  return pos_activate(c);
 }
 
 int fslr_sweep_partition(fslr_ctx* c, const fslr_params* p, int32_t n_dest, int32_t block_shift, void* dst,
@@ -998,6 +1399,7 @@ int fslr_sweep_evaluate(fslr_ctx* c, const fslr_params* p, const void* entries, 
   s.rlen8 = c->rlen8;
   s.umax = c->umax;
   s.ni = 0;
+  s.nq = 0;
   s.n_reads = static_cast<int>(c->n);
   s.a_begin = 0;
   s.a_end = static_cast<int>(c->n);

@@ -35,6 +35,20 @@ struct fslr_ctx {
   int64_t f_cap = 0;
   int2* crange_f = nullptr;                 // [n_chroms_f] chromosome ranges of the filtered index
   int64_t crange_f_cap = 0;
+  // the position split (fslr_set_position_filter): the index holds the sorted positions [pf_lo, pf_end)
+  // of the full index (pf_on), the sweep queries [pf_lo, pf_hi); the selection is kept (pf_set) so
+  // fslr_use_position_filter re-activates it after a chromosome filter
+  bool pf_set = false, pf_on = false;
+  int64_t pf_lo = 0, pf_hi = 0, pf_end = 0;
+  uint64_t pf_gen = 0;                      // reads_gen of the selection
+  int* pf_sel = nullptr;                    // [pf_end - pf_lo] their data positions, ascending
+  int64_t pf_sel_cap = 0;
+  int* pf_lmap = nullptr;                   // [n_chroms] chromosome -> the range's own numbering, -1
+  int64_t pf_lmap_cap = 0;
+  std::vector<int2> pf_cr;                  // the range's chromosome ranges (local positions)
+  long long* pf_cost = nullptr;             // [2 x tiles] fslr_position_costs scratch
+  int64_t pf_cost_cap = 0;
+  uint64_t reads_gen = 0;                   // bumped by every set_reads
   int* grp = nullptr;                       // [grp_ints()] grouping sort: bucket counts / offsets
   long long* part_cnt = nullptr;            // partition scratch: per (destination, block) counts + offsets
   // the last synchronous fslr_sweep_partition (fslr_sweep_partition_repeat replays it without a readback)
@@ -93,6 +107,19 @@ struct fslr_ctx {
   int wstat_waves = 0;
   unsigned long long* diag = nullptr;        // FSLR_SECTION_PROF builds: per-read timing of the pair kernel
   int* errw = nullptr;     // [0..2] error, [3] max_fwd, ... then the ZeroDivisionError pair list (kernels.hpp)
+  // fslr_rows_upload / fslr_set_reads_rows (rows.hip): the uploaded rows and the CSR the device made
+  long long* rows_col = nullptr;    // [7 x rows_cap] chrom, start, end, aln, qcode, nal, qlen2
+  int64_t rows_cap = 0, rows_n = 0, rows_codes = 0, rows_cids = 0;
+  long long* rows_ord = nullptr;    // [rows_cap] the start order
+  unsigned char* rows_keep = nullptr;
+  int* rows_int = nullptr;          // [16 x rows_cap + ...] the build's int scratch and CSR columns
+  int64_t rows_int_cap = 0;
+  long long* rows_l = nullptr;      // [2 x rows_cap] aln in CSR order, qname code of each rank
+  void* rows_temp = nullptr;
+  size_t rows_temp_bytes = 0;
+  bool rows_set = false;            // the reads came from fslr_set_reads_rows (fslr_get_csr, fold)
+  std::vector<int> rows_dmap;       // chromosome number -> dense id, and its inverse
+  std::vector<int64_t> rows_cid;
   int zd_cap = 0;          // capacity of that list (pairs)
   bool zd_host = false;    // the last query's ZeroDivisionError pairs are decided by the caller (a partition,
                            // an evaluation or a long-read query: the edge cap's binding is known there)

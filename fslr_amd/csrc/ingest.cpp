@@ -23,6 +23,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include <cerrno>
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -712,6 +713,49 @@ int fslr_tsv_write(const FslrTsv *t, const char *path, const char *header_suffix
     if (oob) { ::close(fd); set_err(err, errlen, "row index out of range"); return FSLR_INGEST_ERROR; }
     bytes[0] = (int64_t)head.size();
     for (int w = 0; w < T; ++w) bytes[(size_t)w + 1] += bytes[(size_t)w];
+    // The file is sized once and mapped: each thread copies its rows into its own byte range.  Page
+    // faults on a shared file mapping run in parallel, where buffered pwrite()s of one file serialise
+    // on its inode lock (a 16-thread writer ran at one thread's copy speed).  pwrite() stays the
+    // fallback when the mapping is refused.
+    const int64_t total = bytes[(size_t)T];
+    // the blocks are reserved first (a full disk is an error here, not a SIGBUS in a mapped store)
+    const int fa = total > 0 ? ::posix_fallocate(fd, 0, (off_t)total) : 0;
+    if (fa != 0 && fa != EOPNOTSUPP && fa != EINVAL) {
+        ::close(fd);
+        set_err(err, errlen, std::string("cannot write ") + path + ": " + std::strerror(fa));
+        return FSLR_INGEST_ERROR;
+    }
+    if (total > 0 && fa == 0 && ::ftruncate(fd, (off_t)total) == 0) {
+        void *m = ::mmap(nullptr, (size_t)total, PROT_WRITE, MAP_SHARED, fd, 0);
+        if (m != MAP_FAILED) {
+            char *out = static_cast<char *>(m);
+            std::memcpy(out, head.data(), head.size());
+            std::vector<std::thread> pool;
+            for (int w = 0; w < T; ++w)
+                pool.emplace_back([&, w] {
+                    auto [a, e] = range(w);
+                    char *o = out + bytes[(size_t)w];
+                    for (int64_t k = a; k < e; ++k) {
+                        const char *s;
+                        int64_t ss;
+                        const int64_t ln = span(rows_out[k], &s);
+                        std::memcpy(o, s, (size_t)ln);
+                        o += ln;
+                        const int64_t sl = sfx(k, &ss);
+                        std::memcpy(o, suffix_buf + ss, (size_t)sl);
+                        o += sl;
+                        *o++ = '\n';
+                    }
+                });
+            for (auto &th : pool) th.join();
+            const bool ok = ::munmap(m, (size_t)total) == 0;
+            if (::close(fd) != 0 || !ok) {
+                set_err(err, errlen, "write failed");
+                return FSLR_INGEST_ERROR;
+            }
+            return FSLR_INGEST_OK;
+        }
+    }
     auto put = [&](const char *p, size_t len, int64_t off) {
         while (len) {
             const ssize_t r = ::pwrite(fd, p, len, off);
@@ -982,31 +1026,75 @@ int fslr_fillings(int64_t n_rows, const int32_t *qcode, int64_t n_q, const uint8
                   int64_t *start, int64_t *end, int64_t *aln_o, int64_t *qc_o, int64_t *nal_o, int64_t *qlen2_o,
                   int64_t *chrom_o, int n_threads) {
     if (n_rows < 0 || n_q < 0 || !qcode || !n_out) return FSLR_INGEST_ERROR;
-    // 1. first and last row (file order, rows kept by row_keep) of every qname
+    int T = n_threads > 0 ? n_threads : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    T = (int)std::min<int64_t>(T, std::max<int64_t>(1, n_rows / 65536));
+    // 1. first and last row (file order, rows kept by row_keep) of every qname, and 2. qlen2 =
+    // max(qend) - min(qstart) over its fillings (cluster.py:14-31).  A file grouped by qname (the
+    // mapping step writes it so) has each qname's rows as one run: runs are found and measured in
+    // parallel; any other file takes the ordered pass
     std::vector<int64_t> first((size_t)n_q, -1), last((size_t)n_q, -1);
-    for (int64_t i = 0; i < n_rows; ++i) {
-        if (row_keep && !row_keep[i]) continue;
-        const int32_t q = qcode[i];
-        if (q < 0 || q >= n_q) return FSLR_INGEST_ERROR;
-        if (first[(size_t)q] < 0) first[(size_t)q] = i;
-        last[(size_t)q] = i;
+    std::vector<int64_t> lo((size_t)n_q, INT64_MAX), hi((size_t)n_q, INT64_MIN);
+    std::atomic<bool> bad{false}, grouped{true};
+    {
+        std::unique_ptr<std::atomic<int8_t>[]> seen(new std::atomic<int8_t>[(size_t)n_q]);
+        parallel_for(n_q, T, [&](int64_t a, int64_t e, int) {
+            for (int64_t q = a; q < e; ++q) seen[q].store(0, std::memory_order_relaxed);
+        });
+        parallel_for(n_rows, T, [&](int64_t a, int64_t e, int) {
+            for (int64_t i = a; i < e && !bad && grouped; ++i) {
+                const int32_t q = qcode[i];
+                if (q < 0 || q >= n_q) { bad = true; return; }
+                if (i > 0 && qcode[i - 1] == q) continue;             // not a run start
+                if (seen[q].exchange(1, std::memory_order_relaxed)) { grouped = false; return; }
+                int64_t j = i + 1;
+                while (j < n_rows && qcode[j] == q) ++j;
+                if (row_keep && !row_keep[i]) {                       // delete_false drops whole qnames
+                    for (int64_t k = i; k < j; ++k)
+                        if (row_keep[k]) { grouped = false; return; }
+                    continue;
+                }
+                for (int64_t k = i; k < j; ++k)
+                    if (row_keep && !row_keep[k]) { grouped = false; return; }
+                first[(size_t)q] = i;
+                last[(size_t)q] = j - 1;
+                int64_t l = INT64_MAX, h = INT64_MIN;
+                for (int64_t k = i + 1; k < j - 1; ++k) {
+                    l = std::min(l, qstart[k]);
+                    h = std::max(h, qend[k]);
+                }
+                lo[(size_t)q] = l;
+                hi[(size_t)q] = h;
+            }
+        });
+    }
+    if (bad) return FSLR_INGEST_ERROR;
+    if (!grouped) {
+        std::fill(first.begin(), first.end(), -1);
+        std::fill(last.begin(), last.end(), -1);
+        for (int64_t i = 0; i < n_rows; ++i) {
+            if (row_keep && !row_keep[i]) continue;
+            const int32_t q = qcode[i];
+            if (q < 0 || q >= n_q) return FSLR_INGEST_ERROR;
+            if (first[(size_t)q] < 0) first[(size_t)q] = i;
+            last[(size_t)q] = i;
+        }
     }
     auto kept = [&](int64_t i) {
         if (row_keep && !row_keep[i]) return false;
         const int32_t q = qcode[i];
         return first[(size_t)q] != i && last[(size_t)q] != i;
     };
-    // 2. qlen2 = max(qend) - min(qstart) over each qname's fillings (cluster.py:14-31)
-    std::vector<int64_t> lo((size_t)n_q, INT64_MAX), hi((size_t)n_q, INT64_MIN);
-    for (int64_t i = 0; i < n_rows; ++i) {
-        if (!kept(i)) continue;
-        const int32_t q = qcode[i];
-        lo[(size_t)q] = std::min(lo[(size_t)q], qstart[i]);
-        hi[(size_t)q] = std::max(hi[(size_t)q], qend[i]);
+    if (!grouped) {
+        std::fill(lo.begin(), lo.end(), INT64_MAX);
+        std::fill(hi.begin(), hi.end(), INT64_MIN);
+        for (int64_t i = 0; i < n_rows; ++i) {
+            if (!kept(i)) continue;
+            const int32_t q = qcode[i];
+            lo[(size_t)q] = std::min(lo[(size_t)q], qstart[i]);
+            hi[(size_t)q] = std::max(hi[(size_t)q], qend[i]);
+        }
     }
     // 3. the fillings' columns, compacted in file order
-    int T = n_threads > 0 ? n_threads : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
-    T = (int)std::min<int64_t>(T, std::max<int64_t>(1, n_rows / 65536));
     std::vector<int64_t> base((size_t)T + 1, 0);
     parallel_for(n_rows, T, [&](int64_t a, int64_t e, int w) {
         int64_t c = 0;

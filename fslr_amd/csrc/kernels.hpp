@@ -179,6 +179,7 @@ struct SweepArgs {
   const int2* rng_s;
   const int* umax;
   int ni, n_reads;
+  int nq;                             // query positions [0, nq) of the index (the rest: a forward halo)
   int a_begin, a_end;                 // reads whose pairs (as the lower rank A) are evaluated
   double qlen_cut, nal_cut;
   int4* lb;                           // [n_reads] length-gate ranges (launch_len_bounds)
@@ -207,12 +208,7 @@ struct SweepArgs {
   int wstat_waves;
   hipEvent_t ev[5];                   // (profiling) count | scan | emit | sort | pairs boundaries, or null
   hipEvent_t k0, k1;                  // (profiling) around the sweep kernel launch alone, or null
-  hipEvent_t p0, p1;                  // (profiling) around the pair-stage kernel (k_bucket_pairs) alone, or null
-  // set by launch_sweep_pairs for k_sweep_pairs' list mode (the buckets k_bucket_pairs spilled)
-  const long long* spill;             // [3 x count] {s, e, first chunk}: spilled buckets in ent_sorted, or null
-  const unsigned long long* spill_n;  // count << 40 | total chunks of kChunk2 entries
-  int wbase;                          // first per-wave statistics slot
-  int xcd_map;                        // k_sweep: 1 = each XCD a contiguous share of the chunks, 0 = grid stride
+  hipEvent_t p0, p1;                  // (profiling) around the pair-stage kernel (k_sweep_pairs) alone, or null
 };
 size_t sweep_temp_bytes(long long ent_cap, long long ni, hipStream_t s);
 int sweep_max_waves();
@@ -237,6 +233,13 @@ hipError_t launch_sweep_partition(const SweepArgs& a, int mode, int shift, int n
 constexpr int kMaxDest = 64;          // destination ranks of one partition
 // the data-order records of the owned chromosomes (lmap[c] >= 0: its local number), compacted in
 // data order (stable), their chromosome renumbered lmap[c]
+// the position split (shard.hip): per 64-position tile its pair tests and forward-window end; the
+// data positions of a sorted-position range and their records in data order
+hipError_t launch_tile_costs(const int2* rng_s, int ni, long long* tests, long long* reach, hipStream_t s);
+hipError_t launch_pos_select(const int* qd, int ni, int lo, int end, int* flags, int* offs, int* sel,
+                             void* temp, size_t temp_bytes, hipStream_t s);
+hipError_t launch_pos_gather(const int* sel, int m, const unsigned* dchrom, const int4* drec, const int2* dgate,
+                             const int* lmap, unsigned* fdchrom, int4* fdrec, int2* fdgate, hipStream_t s);
 hipError_t launch_chrom_filter(const unsigned* dchrom, const int4* drec, const int2* dgate, const int* lmap, int ni,
                                unsigned* fdchrom, int4* fdrec, int2* fdgate, int* flags, int* offs, void* temp,
                                size_t temp_bytes, hipStream_t s);
@@ -262,6 +265,41 @@ struct UploadArgs {
   unsigned long long* err;            // [2] first failure (index << 3 | code): columns, data order; ~0 by the caller
 };
 hipError_t launch_upload_pack(const UploadArgs& a, hipStream_t s);
+
+// ---- rows -> the clustering input (rows.hip): fslr_set_reads_rows ------------------------------
+enum RowsErr { kRowsErrOrder = 1, kRowsErrCode = 2, kRowsErrChrom = 4, kRowsErrCoord = 8, kRowsErrNal = 16,
+               kRowsErrQlen = 32 };
+struct RowsWork {
+  // the uploaded fillings' columns [n_rows] (file order)
+  const long long *chrom, *start, *end, *aln, *qcode, *nal, *qlen2;
+  // the data list and the ranks
+  int* ord32;                          // [n_rows] order as int32
+  unsigned char* flag;                 // [n_rows] keep flag of each data position
+  int* sel;                            // [n_rows] the data list: rows in data order
+  int* nsel;                           // [1] its length
+  int* first;                          // [n_codes] first data position of each qname code
+  int* f;                              // [m] 1 at a qname's first position
+  int* fscan;                          // [m] their exclusive scan: the read rank
+  int *key, *val, *key_s, *perm;       // [m] the grouping sort (rank, data position)
+  long long* code_of_rank;             // [m] qname code of each rank
+  // the CSR columns
+  int* off;                            // [m + 1] read offsets
+  int *ch_raw, *st32, *en32, *dp;      // [m] chromosome number, start, end, data position
+  long long* aln_k;                    // [m] aln_size (threshold folds)
+  int *q2, *nal32;                     // [m] per read
+  int* present;                        // [n_cids] chromosomes present
+  int* stat;                           // [4] max read length, n_alignments varies, general thresholds, aln 0
+  int* err;                            // [1] RowsErr bits
+  void* temp;
+  size_t temp_bytes;
+};
+hipError_t rows_rank(const RowsWork& w, long long n_rows, long long n_codes, const long long* order,
+                     const unsigned char* keep, long long out[2], hipStream_t s);
+size_t rows_temp_bytes(long long n, hipStream_t s);
+hipError_t rows_csr(const RowsWork& w, int m, int n_reads, long long n_cids, hipStream_t s);
+hipError_t rows_fold(const long long* aln_k, int ni, double p, const int* ch_raw, const int* dmap, int* thr, int* ch,
+                     int* stat, hipStream_t s);
+hipError_t rows_zero_flags(const int* thr, int ni, unsigned char* z, hipStream_t s);
 
 // ---- components (components.hip) ---------------------------------------------------------
 hipError_t launch_uf_init(int* parent, int n, hipStream_t s);

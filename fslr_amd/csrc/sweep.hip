@@ -54,14 +54,27 @@ __device__ __forceinline__ int part_of(int B, int npass) {
 }
 
 // ---- 1. the sweep -------------------------------------------------------------------------------
-// One wavefront per tile of 64 consecutive sorted positions (lane l holds q = q0 + l), tiles dealt
-// grid-stride over a resident grid.  The tile's forward ranges are flattened into an LDS map (item
-// r -> the lane whose range holds it), then walked 64 interval pairs per step, one per lane, the
-// next step's index records loaded while the current step is tested.  The q side of a pair comes
-// from LDS (written once per tile), the p side is the index record and gate word at p (a tile's
-// window is a few hundred consecutive positions, so these loads hit L1 / L2).  kEmit = false counts
-// the tile's entries (and the statistics); kEmit = true writes them at the tile's scanned offset.
-constexpr int kMapCap = 2048;              // items per map segment (a longer tile takes several)
+// One wavefront per tile of 64 consecutive sorted positions (lane l holds q = q0 + l), tiles dealt in
+// chunks of consecutive tiles, grid-stride over a resident grid.  The tile's forward ranges are
+// flattened into an LDS map (item r -> its lane and p - q0), then walked 64 interval pairs per step,
+// one per lane, the next step's operands read while the current step is tested.
+// The index records and gate words of positions [q0, q0 + kRing) sit in a per-wave LDS ring (slot
+// p mod kRing): a tile's pairs have p in q0 + 1 .. q + n_fwd(q), so the p side of almost every pair
+// test — and the q side — is an LDS read instead of a dependent gather through L1 / L2.  Moving to the
+// next tile of a chunk loads only the 64 positions entering the ring (one coalesced record and gate
+// load per lane: every position's 24 B cross HBM once per chunk); a pair beyond the ring (a tile whose
+// forward window is longer) reads the index in global memory.
+// kEmit = false counts the tile's entries (and the statistics); kEmit = true writes them.
+#ifndef FSLR_SWEEP_RING
+#define FSLR_SWEEP_RING 128
+#endif
+#ifndef FSLR_SWEEP_DB
+#define FSLR_SWEEP_DB 0
+#endif
+constexpr int kRing = FSLR_SWEEP_RING;     // positions per wave in the LDS ring (a power of two >= 64)
+static_assert(kRing >= kWave && (kRing & (kRing - 1)) == 0 && kRing < 1024, "ring size");
+constexpr int kRingMask = kRing - 1;
+constexpr int kMapCap = 1024;              // items per map segment (a longer tile takes several)
 constexpr int kTileRun = 8;                // consecutive tiles per work item
 
 // kMode 0: count the tile's entries (two-pass fallback), 1: write them at the tile's scanned offset
@@ -71,60 +84,69 @@ template <int kMode>
 __global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
   constexpr bool kEmit = kMode != 0;
   constexpr bool kCount = kMode != 1;
-  __shared__ int4 qa_all[kSwWaves][kWave];     // {end, thr, tag, qlo}
-  __shared__ int4 qb_all[kSwWaves][kWave];     // {qhi, nlo, nhi, offv}
+  __shared__ int4 rr_all[kSwWaves][kRing];     // ring: index records {start, end, thr, read << 6 | j}
+  __shared__ int2 rg_all[kSwWaves][kRing];     // ring: gate words {qlen2, nal | L << 24 | zero-aln << 31}
+  __shared__ int4 qb_all[kSwWaves][kWave];     // lane's read's gate as integer ranges {qlo, qhi, nlo, nhi}
+  __shared__ int off_all[kSwWaves][kWave];     // item r of lane k is position r + offv_k
   __shared__ unsigned char zf_all[kSwWaves][kWave];   // q's read has qlen2 == 0 (1) / n_alignments == 0 (2)
-  __shared__ unsigned char map_all[kSwWaves][kMapCap];          // item -> its lane (position q0 + mi)
+  __shared__ unsigned short map_all[kSwWaves][kMapCap];   // item -> lane | min(p - q0, kRing) << 6
   __shared__ unsigned long long st_all[kSwWaves][kEmit ? kWave : 1];
   unsigned long long* const dst = kMode == 2 ? g.ent_ub : g.ent;
   const int lane = lane_id();
   const int wv = threadIdx.x >> 6;
-  int4* QA = qa_all[wv];
+  int4* RR = rr_all[wv];
+  int2* RG = rg_all[wv];
   int4* QB = qb_all[wv];
+  int* OFF = off_all[wv];
   unsigned char* ZF = zf_all[wv];
-  unsigned char* MAP = map_all[wv];
+  unsigned short* MAP = map_all[wv];
   unsigned long long* ST = st_all[wv];
   unsigned long long w_tests = 0, w_hits = 0, w_ent = 0;
-  const int nt = (g.ni + kWave - 1) / kWave;
+  const int nt = (g.nq + kWave - 1) / kWave;      // query tiles (the index may hold a halo beyond them)
   const int nw = gridDim.x * kSwWaves;
   const int wid = blockIdx.x * kSwWaves + wv;
   // tiles in chunks of up to kTileRun consecutive tiles per wave (a tile's forward window reaches
-  // into the next tile, whose records the same wave then finds in its caches), chunks dealt
-  // grid-stride; shorter chunks when there are fewer than kTileRun tiles per wave of the grid (a
-  // rank's share of the multi-GPU split), so every wave gets work: the sweep is latency bound
+  // into the next tile, whose records the ring already holds), chunks dealt grid-stride; shorter
+  // chunks when there are fewer than kTileRun tiles per wave of the grid (a rank's share of the
+  // multi-GPU split), so every wave gets work: the sweep is latency bound
   const int run = max(1, min(kTileRun, nt / nw));
   const int nchunks = (nt + run - 1) / run;
-  // XCD-aware: workgroup b runs on XCD b % 8 (the usual dispatch; it only affects speed), and each
-  // XCD takes one contiguous eighth of the chunks, dealt to its waves in order — a chunk's forward
-  // window runs into the next chunk's positions, which a neighbouring wave of the same XCD (often of
-  // the same workgroup) reads at about the same time, so the overlap is served by that XCD's L2
-  // instead of being fetched again by another XCD.  (Per-XCD work queues were tried in round 3:
-  // 0.241 -> 0.260 ms at cfg3, the tickets' latency cost more than the balance gained.)
-  const int nx = min(8, static_cast<int>(gridDim.x));                    // XCDs in use
-  const int xcd = static_cast<int>(blockIdx.x) % nx;
-  const int bpx = (static_cast<int>(gridDim.x) - xcd + nx - 1) / nx;      // workgroups on this XCD
-  const int wx = static_cast<int>(blockIdx.x) / nx * kSwWaves + wv;        // wave index inside the XCD
-  const int c_lo = static_cast<int>((static_cast<long long>(nchunks) * xcd) / nx);
-  const int c_hi = static_cast<int>((static_cast<long long>(nchunks) * (xcd + 1)) / nx);
-  const int c0 = g.xcd_map ? c_lo + wx : wid, c1 = g.xcd_map ? c_hi : nchunks;
-  const int cstep = g.xcd_map ? bpx * kSwWaves : nw;
-  for (int chunk = c0; chunk < c1; chunk += cstep)
+  for (int chunk = wid; chunk < nchunks; chunk += nw)
   for (int tile = chunk * run; tile < min(nt, (chunk + 1) * run); ++tile) {
     const int q0 = tile * kWave;
     const int q = q0 + lane;
-    const bool qv = q < g.ni;
+    const bool qv = q < g.nq;
     const int qc = qv ? q : q0;
-    int4 rq = g.idx4[qc];
     const int nf = qv ? g.rng_s[qc].x : 0;
+    wave_lds_sync();                             // the previous tile's ring and map reads are done
+    if (tile == chunk * run) {
+      // the chunk's first tile: positions [q0, q0 + kRing)
+#pragma unroll
+      for (int k = 0; k < kRing / kWave; ++k) {
+        const int p = q0 + k * kWave + lane;
+        if (p < g.ni) {
+          RR[p & kRingMask] = g.idx4[p];
+          RG[p & kRingMask] = g.idx_gate[p];
+        }
+      }
+    } else {
+      // the ring held [q0 - 64, q0 - 64 + kRing): the 64 positions entering it replace the last tile's
+      const int p = q0 + kRing - kWave + lane;
+      if (p < g.ni) {
+        RR[p & kRingMask] = g.idx4[p];
+        RG[p & kRingMask] = g.idx_gate[p];
+      }
+    }
+    wave_lds_sync();
+    const int4 rq = RR[qc & kRingMask];
     const int4 lbq = g.lb[rq.w >> 6];            // the gate of q's read as integer ranges
     const bool any_zero = __ballot(qv && (lbq.x < 0 || lbq.z < 0)) != 0ull;   // v == 0 (ZeroDivision)
     const int pre = wave_incl_scan(nf);
     const int ex = pre - nf;
     const int T = rdl(pre, kWave - 1);
-    wave_lds_sync();
     // lower bounds with v == 0 (lo < 0: partner 0 raises, [1, hi] passes) folded to 1
-    QA[lane] = make_int4(rq.y, rq.z, rq.w, lbq.x < 0 ? 1 : lbq.x);
-    QB[lane] = make_int4(lbq.y, lbq.z < 0 ? 1 : lbq.z, lbq.w, q + 1 - ex);   // item r of lane k: position r + offv_k
+    QB[lane] = make_int4(lbq.x < 0 ? 1 : lbq.x, lbq.y, lbq.z < 0 ? 1 : lbq.z, lbq.w);
+    OFF[lane] = q + 1 - ex;
     ZF[lane] = static_cast<unsigned char>((lbq.x < 0 ? 1 : 0) | (lbq.z < 0 ? 2 : 0));
     long long out = 0;                           // kEmit: next entry slot of this tile
     if constexpr (kMode == 1) out = g.tile_off[tile];
@@ -143,36 +165,46 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
     for (int seg = 0; seg < T; seg += kMapCap) {
       const int se = min(T, seg + kMapCap);
       wave_lds_sync();
-      for (int r = max(ex, seg); r < min(pre, se); ++r) MAP[r - seg] = static_cast<unsigned char>(lane);
+      for (int r = max(ex, seg); r < min(pre, se); ++r)
+        MAP[r - seg] = static_cast<unsigned short>(lane | min(r - ex + lane + 1, kRing) << 6);
       wave_lds_sync();
-      // step loads: the mapped lane's offset, then the p-side record and gate word
+      // step operands: the mapped lane's gate ranges, q's record (ring), p's record and gate word
+      // (ring; global beyond it)
       struct Step {
         int mi;
-        int4 b4, rp;
+        int4 b4, a4, rp;
         int2 gp;
       };
       auto step_load = [&](int base, Step& t) {
         const int r = base + lane;
-        t.mi = r < se ? MAP[r - seg] : 0;
+        const unsigned md = r < se ? MAP[r - seg] : 0u;
+        t.mi = static_cast<int>(md & 63u);
+        const int d = static_cast<int>(md >> 6);
         t.b4 = QB[t.mi];
-        const int p = r < se ? r + t.b4.w : q0;
-        t.rp = g.idx4[p];
-        t.gp = g.idx_gate[p];
+        t.a4 = RR[(q0 + t.mi) & kRingMask];
+        if (d < kRing) {
+          t.rp = RR[(q0 + d) & kRingMask];
+          t.gp = RG[(q0 + d) & kRingMask];
+        } else {
+          const int p = r + OFF[t.mi];
+          t.rp = g.idx4[p];
+          t.gp = g.idx_gate[p];
+        }
       };
       // one step of 64 interval pairs; kZero: some q of the tile has qlen2 or n_alignments == 0
       // (only then can a pair raise ZeroDivisionError)
       auto step = [&](auto zero_tag, int base, const Step& t) __attribute__((always_inline)) {
         constexpr bool kZero = decltype(zero_tag)::value;
         const bool valid = base + lane < se;
-        const int4 a4 = QA[t.mi];
-        const int X = a4.z >> 6, Y = t.rp.w >> 6;
+        const int4 a4 = t.a4;
+        const int X = a4.w >> 6, Y = t.rp.w >> 6;
         const bool hit = valid & (X != Y);
         // calculate_overlap >= overlap for both intervals: start_p >= start_q, start_p <= end_q
-        const int o = min(a4.x, t.rp.y) - t.rp.x;
-        const bool match = o >= max(a4.y, t.rp.z);
+        const int o = min(a4.y, t.rp.y) - t.rp.x;
+        const bool match = o >= max(a4.z, t.rp.z);
         // different_lengths_or_alignments: passes when either ratio is close (idx_gate word of p)
         const int q2 = t.gp.x, n2 = t.gp.y & 0xFFFFFF;
-        const int qlo = a4.w, qhi = t.b4.x, nlo = t.b4.y, nhi = t.b4.z;
+        const int qlo = t.b4.x, qhi = t.b4.y, nlo = t.b4.z, nhi = t.b4.w;
         const bool pq = (q2 >= qlo) & (q2 <= qhi);
         const bool lenok = pq | ((n2 >= nlo) & (n2 <= nhi));
         bool emit = hit & lenok & match;
@@ -199,7 +231,7 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
           if (emit) {
             // A << 39 | B << 14 | i << 7 | j as two dwords
             const int A = min(X, Y), B = max(X, Y);
-            const int iq = a4.z & 63, jp = t.rp.w & 63;
+            const int iq = a4.w & 63, jp = t.rp.w & 63;
             const unsigned ij = X < Y ? static_cast<unsigned>(iq << 7 | jp) : static_cast<unsigned>(jp << 7 | iq);
             const unsigned lo = (static_cast<unsigned>(B) << 14) | ij;
             const unsigned hi = (static_cast<unsigned>(A) << 7) | (static_cast<unsigned>(B) >> 18);
@@ -209,7 +241,8 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
         }
       };
       auto run_steps = [&](auto zero_tag) __attribute__((always_inline)) {
-        // double buffer unrolled by two: the loads of the next step are in flight while one is tested
+#if FSLR_SWEEP_DB
+        // double buffer unrolled by two: the operands of the next step are in flight while one is tested
         Step s0, s1;
         step_load(seg, s0);
         for (int base = seg; base < se; base += 2 * kWave) {
@@ -220,6 +253,14 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
           if (base + 2 * kWave < se) step_load(base + 2 * kWave, s0);
           step(zero_tag, base + kWave, s1);
         }
+#else
+        // LDS operands: other waves cover their latency
+        for (int base = seg; base < se; base += kWave) {
+          Step s0;
+          step_load(base, s0);
+          step(zero_tag, base, s0);
+        }
+#endif
       };
       if (any_zero) run_steps(std::true_type{});
       else run_steps(std::false_type{});
@@ -236,7 +277,7 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
     }
   }
   if constexpr (kCount) {
-    // statistics: plain stores into this wave's slots, summed by k_sum_slots
+    // statistics: plain stores into this wave's slots, summed by k_sweep_total / k_sum_slots
     const unsigned long long f = lane == 0 ? w_tests : lane == 1 ? w_hits : w_ent;
     if (lane < 3) g.wstat[static_cast<long long>(wid) * kWsFields + lane] = f;
   }
@@ -518,15 +559,10 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
   EdgeStageN<kPairEdgeStage> es{es_all[wv], 0};
   const EdgeOut eo{g.edges, g.edge_iu, g.edge_cap, &g.counters[kEdgeCount]};
   const int umax_v = g.umax[lane];
-  // list mode (g.spill): the items are the kChunk2-entry chunks of the buckets k_bucket_pairs spilled
-  // (runs grouped by A inside each), and n is the current bucket's end (no run crosses it)
-  long long n = g.n_dev ? *g.n_dev : g.n_ent;
+  const long long n = g.n_dev ? *g.n_dev : g.n_ent;
   const unsigned long long* E = g.ent_sorted;
   const unsigned char* RL = g.rlen8;
-  // list mode: the spilled buckets' chunks of kChunk2 entries (count << 40 | chunk total)
-  const unsigned long long spill_w = g.spill ? *g.spill_n : 0ull;
-  const int n_spill = static_cast<int>(spill_w >> 40);
-  const long long nchunks = g.spill ? static_cast<long long>(spill_w & ((1ull << 40) - 1)) : (n + kChunk2 - 1) / kChunk2;
+  const long long nchunks = (n + kChunk2 - 1) / kChunk2;
   const long long nw = static_cast<long long>(gridDim.x) * kSwWaves;
   const int wid = blockIdx.x * kSwWaves + wv;
   int w_maxfwd = 0;
@@ -681,24 +717,9 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
     wn = lane == 0 && s + lim < n ? E[s + lim] : ~0ull;
   };
   for (long long c = wid; c < nchunks; c += nw) {
-    long long c0, c1;
-    long long sb = 0;                                   // start of the array or of the spilled bucket
-    if (g.spill) {
-      int lo_k = 0, hi_k = n_spill - 1;                 // the bucket holding chunk c: largest first chunk <= c
-      while (lo_k < hi_k) {
-        const int mid_k = (lo_k + hi_k + 1) >> 1;
-        if (g.spill[3 * mid_k + 2] <= c) lo_k = mid_k; else hi_k = mid_k - 1;
-      }
-      sb = g.spill[3 * lo_k];
-      n = g.spill[3 * lo_k + 1];
-      c0 = sb + (c - g.spill[3 * lo_k + 2]) * kChunk2;
-      c1 = min(c0 + kChunk2, n);
-    } else {
-      c0 = c * kChunk2;
-      c1 = min(c0 + kChunk2, n);
-    }
+    const long long c0 = c * kChunk2, c1 = min(c0 + kChunk2, n);
     long long s = c0;
-    if (s > sb) s = next_run(s, c1, a_at(s - 1));      // the run in progress belongs to the previous chunk
+    if (s > 0) s = next_run(s, c1, a_at(s - 1));       // the run in progress belongs to the previous chunk
     unsigned long long e0 = ~0ull, e1 = ~0ull, en = ~0ull;
     if (s < c1) load_window(s, e0, e1, en);
     while (s < c1) {
@@ -743,18 +764,11 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
       const bool v0 = lane < gend, v1 = lane + kWave < gend;
       const bool hv0 = h0 && v0, hv1 = h1 && v1;
       int la0 = 0, la1 = 0;
-#if defined(FSLR_PAIRS_ABLATE) && (FSLR_PAIRS_ABLATE & 4)
-      if (hv0) la0 = 8;                                            // profiling ablation: no L gathers
-      if (hv1) la1 = 8;
-#else
       if (hv0) la0 = RL[entry_a(e0)];                              // in flight during the sort
       if (hv1) la1 = RL[entry_a(e1)];
-#endif
       unsigned long long k0 = v0 ? group_key(e0, r0) : ~0ull;
       unsigned long long k1 = v1 ? group_key(e1, r1) : ~0ull;
-#if !defined(FSLR_PAIRS_ABLATE) || (FSLR_PAIRS_ABLATE & 1) == 0
       bitonic128_il(k0, k1, lane);
-#endif
       // back to position p at lane p (k0) / p - 64 (k1) through the group's key array
       wave_lds_sync();                                             // the previous group's reads are done
       reinterpret_cast<ulonglong2*>(SK)[lane] = make_ulonglong2(k0, k1);
@@ -771,13 +785,8 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
       const bool d0 = v0 && !s0 && (k0 >> 7) == (q0 >> 7);
       const bool d1 = v1 && !s1 && (k1 >> 7) == (q1 >> 7);
       int lb0 = 0, lb1 = 0;                                        // L_B of each segment, gathered by its head
-#if defined(FSLR_PAIRS_ABLATE) && (FSLR_PAIRS_ABLATE & 4)
-      if (s0) lb0 = 8;
-      if (s1) lb1 = 8;
-#else
       if (s0) lb0 = RL[(k0 >> 14) & kRankMask];
       if (s1) lb1 = RL[(k1 >> 14) & kRankMask];
-#endif
       // the next window, in flight while this group is evaluated
       const long long sn = s + gend;
       unsigned long long n0 = ~0ull, n1 = ~0ull, nn = ~0ull;
@@ -817,11 +826,7 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
       // the group's edges (at most one per segment) go out in one flush: each read's forward edges stay
       // one run of the edge list (the edge cap's replay walks those runs)
       if (es.n + nseg > kPairEdgeStage) es.flush(eo, lane);
-#if defined(FSLR_PAIRS_ABLATE) && (FSLR_PAIRS_ABLATE & 2)
-      for (int k0s = 0; k0s < 0; k0s += kWave) {                  // profiling ablation: no segment pass
-#else
       for (int k0s = 0; k0s < nseg; k0s += kWave) {
-#endif
         const int p = k0s + lane;
         const bool act = p < nseg;
         int I = 0, r = 0, B = 0, LB = 0;
@@ -879,7 +884,7 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
   // statistics: plain stores into this wave's slots (field 2: matched pairs, field 3: max fwd)
   for (int o = 32; o > 0; o >>= 1) w_maxfwd = max(w_maxfwd, __shfl_xor(w_maxfwd, o));
   const unsigned long long f = lane == 2 ? w_pairs : static_cast<unsigned long long>(w_maxfwd);
-  if (lane == 2 || lane == 3) g.wstat[static_cast<long long>(g.wbase + wid) * kWsFields + lane] = f;
+  if (lane == 2 || lane == 3) g.wstat[static_cast<long long>(wid) * kWsFields + lane] = f;
 }
 
 // ---- 2. grouping by A: a two-level counting sort ---------------------------------------------------
@@ -905,8 +910,7 @@ constexpr int kMsdThreads = FSLR_MSD_THREADS;
 constexpr int kMsdMaxH = 16384;            // buckets (LDS histogram of pass 1)
 constexpr int kMsdMaxLo = 4096;            // in-bucket bins (LDS histogram of pass 2)
 constexpr int kGrpInts = 2 * (1 << 22);    // [bucket][block] counts and their scan (H P <= 2^22)
-// after them: the spill list of k_bucket_pairs (2 x kMsdMaxH entry ranges) and its count
-constexpr int kGrpSpillInts = 6 * kMsdMaxH + 64;    // {s, e, first chunk} per bucket, then the count
+
 constexpr int kMsdUnroll = FSLR_MSD_UNROLL;  // entries loaded per lane before their atomics
 
 // One wave-instruction of keys (lanes with `act`, a contiguous prefix): equal keys on adjacent lanes
@@ -942,11 +946,9 @@ __global__ __launch_bounds__(kMsdThreads) void k_msd_pass1(const unsigned long l
                                                            const long long* __restrict__ cnt, int nt,
                                                            int lo_bits, int H, int* __restrict__ mat,
                                                            unsigned long long* __restrict__ dst,
-                                                           long long cap = 0x7FFFFFFFFFFFFFFFll,
-                                                           unsigned long long* zero = nullptr) {
+                                                           long long cap = 0x7FFFFFFFFFFFFFFFll) {
   __shared__ int hist[kMsdMaxH];
   const int tid = threadIdx.x;
-  if (zero && blockIdx.x == 0 && tid == 0) *zero = 0ull;   // (count pass) the spill list of k_bucket_pairs
   const int lane = tid & (kWave - 1), w = tid >> 6;
   const int P = gridDim.x;
   for (int i = tid; i < H; i += kMsdThreads) hist[i] = kScatter ? mat[i * P + blockIdx.x] : 0;
@@ -1122,352 +1124,6 @@ __global__ __launch_bounds__(256) void k_msd_pass2(const unsigned long long* __r
   }
 }
 
-// ---- 3'. the pair stage fused with the grouping's second pass (k_bucket_pairs) ---------------------
-// One workgroup per pass-1 bucket (the reads A with A >> lo == b; a resident grid walks the buckets
-// grid-stride).  The bucket's entries are loaded once into registers (the next bucket's loads are
-// issued before the current one is evaluated), counted in LDS by digit d = (A's low bits, a hash of
-// B's rank), and scattered into LDS grouped by digit.  Every entry of a read pair (A, B) then has the
-// same digit, so a pair is the entries of one bin with its B: the bin's first entry of that B is
-// the pair's head, and the head's lane collects the pair's rows i and columns j.  I is the entry
-// count unless two entries share a row or a column, where first-fit runs in the reference's order
-// (cluster.py:152-161: rows ascending, the lowest unused matching column).  Edge iff I > 0 and
-// U = L_A + L_B - I <= umax[I - 1] (cluster.py:216-219).  Nothing is written back but edges and
-// forward degrees: the grouped entries never leave LDS, and no per-run sort is needed (the first-fit
-// order is recovered inside the few pairs that conflict).
-// A bucket of more than CAP entries, or with a run (one read A) of more than kFuseLong entries, is
-// spilled: grouped by digit into `out` (runs contiguous, as k_msd_pass2 would) and listed; the list
-// is then evaluated by k_sweep_pairs in list mode (its long-run path handles reads with thousands
-// of entries in partner partitions).
-#ifndef FSLR_FUSE_BINS_LOG
-#define FSLR_FUSE_BINS_LOG 12
-#endif
-#ifndef FSLR_FUSE_READS_LOG
-#define FSLR_FUSE_READS_LOG 11
-#endif
-#ifndef FSLR_FUSE_ES
-#define FSLR_FUSE_ES 2048
-#endif
-constexpr int kFuseBinsLog = FSLR_FUSE_BINS_LOG;
-constexpr int kFuseBins = 1 << kFuseBinsLog;   // digits of a bucket (A's low bits, then B's hash)
-constexpr int kFuseMaxReadsLog = FSLR_FUSE_READS_LOG;
-constexpr int kFuseMaxReads = 1 << kFuseMaxReadsLog;   // reads per bucket at most (2^lo)
-constexpr int kFuseEs = FSLR_FUSE_ES;          // staged edges per workgroup (one atomic per flush)
-static_assert(kFuseMaxReadsLog < kFuseBinsLog, "at least one bit of B's hash per digit");
-constexpr int kFuseLong = 512;                 // a longer run sends its bucket to the spill path
-
-#ifndef FSLR_FUSE_WAVES
-#define FSLR_FUSE_WAVES 0
-#endif
-template <int CAP, int NT>
-__global__ __launch_bounds__(NT)
-#if FSLR_FUSE_WAVES
-__attribute__((amdgpu_waves_per_eu(FSLR_FUSE_WAVES)))
-#endif
-void k_bucket_pairs(SweepArgs g, const unsigned long long* __restrict__ mid,
-                                                     const int* __restrict__ off, int P, int H, int lo, int hbB,
-                                                     unsigned long long* __restrict__ out,
-                                                     long long* __restrict__ spill,
-                                                     unsigned long long* __restrict__ spill_n) {
-  constexpr int K = CAP / NT;                  // entries per thread
-  constexpr int NW = NT / kWave;
-  constexpr int KR = (kFuseMaxReads + NT - 1) / NT;   // reads of the bucket per thread
-  static_assert(CAP % NT == 0 && kFuseBins % NT == 0, "shape");
-  constexpr int PER = kFuseBins / NT;          // digits per thread in the scan
-  // LDS entry: L_B << 50 | A's low bits << 39 | B << 14 | i << 7 | j (A's high bits are the bucket's,
-  // and L_B, a function of B, rides where they were: bits >> 14 still name the pair)
-  __shared__ __attribute__((aligned(16))) unsigned long long E[CAP];
-  __shared__ __attribute__((aligned(16))) int HIST[kFuseBins];
-  __shared__ unsigned long long ES[kFuseEs];
-  __shared__ int FD[kFuseMaxReads];            // edges formed per read of the bucket
-  __shared__ unsigned char RLA[kFuseMaxReads]; // L_A of the bucket's reads
-  __shared__ int UM[kWave];
-  __shared__ int WS[NW];
-  __shared__ int s_esn, s_spill;
-  __shared__ unsigned long long s_base;
-  const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid >> 6;
-  const long long n = g.n_dev ? *g.n_dev : g.n_ent;
-  const int nr = 1 << lo;
-  const unsigned lmask = static_cast<unsigned>(nr - 1);
-  const unsigned char* RL = g.rlen8;
-  const EdgeOut eo{g.edges, g.edge_iu, g.edge_cap, &g.counters[kEdgeCount]};
-  if (tid < kWave) UM[tid] = g.umax[tid];
-  if (tid == 0) s_esn = 0;
-  int w_maxfwd = 0;
-  unsigned long long w_pairs = 0;
-  // digit of a global entry (A << 39 ...) or an LDS entry (A's low bits << 39 ...): the same bits
-  auto digit = [&](unsigned long long x) -> int {
-    const unsigned A = static_cast<unsigned>(x >> 39), B = static_cast<unsigned>(x >> 14) & kRankMask;
-    return static_cast<int>(((A & lmask) << hbB) | ((B * 0x9E3779B1u) >> (32 - hbB)));   // hbB >= 1
-  };
-  auto range_of = [&](int bb, long long& s_, long long& e_) {
-    s_ = min(static_cast<long long>(off[static_cast<long long>(bb) * P]), n);
-    e_ = bb + 1 < H ? min(static_cast<long long>(off[static_cast<long long>(bb + 1) * P]), n) : n;
-    if (e_ < s_) e_ = s_;
-  };
-  unsigned long long v[K];
-  auto load = [&](long long s_, long long e_) {
-    const bool fits = e_ - s_ <= CAP;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const long long i = s_ + tid + k * NT;
-      v[k] = fits && i < e_ ? mid[i] : 0ull;
-    }
-  };
-  // staged edges out with one global atomic (block-uniform call)
-  auto flush = [&]() {
-    const int ne = min(s_esn, kFuseEs);
-    if (tid == 0) s_base = atomicAdd(eo.count, static_cast<unsigned long long>(ne));
-    __syncthreads();
-    const long long base = static_cast<long long>(s_base);
-    for (int t = tid; t < ne; t += NT) {
-      const unsigned long long x = ES[t];
-      const long long k = base + t;
-      if (k < eo.cap) {
-        eo.edges[k] = make_int2(static_cast<int>(x >> 39), static_cast<int>((x >> 14) & kRankMask));
-        eo.edge_iu[k] = static_cast<unsigned short>(((x >> 7) & 127u) | ((x & 127u) << 8));
-      }
-    }
-    __syncthreads();
-    if (tid == 0) s_esn = 0;
-  };
-  // block exclusive scan of HIST in place (digits in contiguous runs of PER per thread)
-  auto scan_hist = [&]() {
-    int loc[PER];
-    int sum = 0;
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      loc[i] = HIST[tid * PER + i];
-      sum += loc[i];
-    }
-    const int inc = wave_incl_scan(sum);
-    if (lane == kWave - 1) WS[w] = inc;
-    __syncthreads();
-    int base = inc - sum;
-    for (int x = 0; x < w; ++x) base += WS[x];
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      HIST[tid * PER + i] = base;
-      base += loc[i];
-    }
-    __syncthreads();
-  };
-
-  int b = blockIdx.x;
-  long long s = 0, e = 0;
-  if (b < H) {
-    range_of(b, s, e);
-    load(s, e);
-  }
-  while (b < H) {
-    const long long c = e - s;
-    const int bn = b + static_cast<int>(gridDim.x);
-    long long sn = 0, en = 0;
-    if (bn < H) range_of(bn, sn, en);
-    __syncthreads();                                   // the previous bucket is done with the LDS
-    if (s_esn > kFuseEs / 2) flush();                  // room for this bucket's edges (past it: see below)
-    if (c == 0) {
-      load(sn, en);
-      b = bn; s = sn; e = en;
-      continue;
-    }
-    // the read lengths this bucket needs, in flight under the histogram and its scan: L_B of each
-    // entry (packed into its LDS copy) and L_A of the bucket's reads
-    unsigned lbv[K];
-    int lav[KR];
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-      lbv[k] = c <= CAP && tid + k * NT < c ? RL[static_cast<unsigned>(v[k] >> 14) & kRankMask] : 0u;
-#pragma unroll
-    for (int k = 0; k < KR; ++k) {
-      const int a = tid + k * NT;
-      const long long A = (static_cast<long long>(b) << lo) + a;
-      lav[k] = a < nr && A < g.n_reads ? RL[A] : 0;
-    }
-    for (int i = tid; i < kFuseBins; i += NT) HIST[i] = 0;
-    for (int i = tid; i < nr; i += NT) FD[i] = 0;
-    if (tid == 0) s_spill = c > CAP;
-    __syncthreads();
-    // digit histogram (entries of one read arrive in runs: run_add folds equal neighbours)
-    if (c <= CAP) {
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const long long i = tid + k * NT;
-        if (k * NT >= c) break;                        // block-uniform
-        run_add<false>(HIST, i < c ? digit(v[k]) : 0, i < c, lane);
-      }
-    } else {
-      for (long long k0 = 0; k0 < c; k0 += NT) {
-        const long long i = k0 + tid;
-        run_add<false>(HIST, i < c ? digit(mid[s + i]) : 0, i < c, lane);
-      }
-    }
-    __syncthreads();
-    scan_hist();
-    // a run longer than kFuseLong spills the bucket (its pairs' bins would be long linear scans)
-    if (c <= CAP)
-      for (int a = tid; a < nr; a += NT) {
-        const int st = HIST[a << hbB];
-        const long long en_a = a + 1 < nr ? HIST[(a + 1) << hbB] : c;
-        if (en_a - st > kFuseLong) s_spill = 1;
-      }
-    __syncthreads();
-    if (s_spill) {
-      // runs grouped by digit into out[s, e) (runs of one A contiguous), listed with the count of
-      // their 512-entry chunks; k_sweep_pairs' list mode takes those chunks
-      if (c <= CAP) {
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          const long long i = tid + k * NT;
-          if (k * NT >= c) break;
-          const bool act = i < c;
-          const int p = run_add<true>(HIST, act ? digit(v[k]) : 0, act, lane);
-          if (act) out[s + p] = v[k];
-        }
-      } else {
-        for (long long k0 = 0; k0 < c; k0 += NT) {
-          const long long i = k0 + tid;
-          const bool act = i < c;
-          const unsigned long long x = act ? mid[s + i] : 0ull;
-          const int p = run_add<true>(HIST, act ? digit(x) : 0, act, lane);
-          if (act) out[s + p] = x;
-        }
-      }
-      if (tid == 0) {
-        const unsigned long long chunks = static_cast<unsigned long long>((c + kChunk2 - 1) / kChunk2);
-        const unsigned long long old = atomicAdd(spill_n, (1ull << 40) | chunks);
-        const unsigned k = static_cast<unsigned>(old >> 40);
-        spill[3 * k] = s;
-        spill[3 * k + 1] = e;
-        spill[3 * k + 2] = static_cast<long long>(old & ((1ull << 40) - 1));
-      }
-      load(sn, en);
-      b = bn; s = sn; e = en;
-      continue;
-    }
-#pragma unroll
-    for (int k = 0; k < KR; ++k)
-      if (tid + k * NT < nr) RLA[tid + k * NT] = static_cast<unsigned char>(lav[k]);
-    // scatter into LDS grouped by digit; afterwards HIST[d] = the end of bin d
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const long long i = tid + k * NT;
-      if (k * NT >= c) break;
-      const bool act = i < c;
-      const int p = run_add<true>(HIST, act ? digit(v[k]) : 0, act, lane);
-      if (act)
-        E[p] = (v[k] & ((1ull << 39) - 1)) | (static_cast<unsigned long long>((v[k] >> 39) & lmask) << 39) |
-               (static_cast<unsigned long long>(lbv[k]) << 50);
-    }
-    load(sn, en);                                      // the next bucket's entries, in flight (no more loads here)
-    __syncthreads();
-    // pairs: lane per entry; the head of each (A, B) decides it (LDS only)
-    for (int p0 = 0; p0 < c; p0 += NT) {
-      const int p = p0 + tid;
-      bool head = false, edge = false;
-      int A = 0, B = 0, I = 0, U = 0;
-      if (p < c) {
-        const unsigned long long x = E[p];
-        const unsigned long long key = x >> 14;        // (L_B, A, B)
-        const int d = digit(x);
-        const int bs = d > 0 ? HIST[d - 1] : 0, be = HIST[d];
-        head = true;
-        for (int k = bs; k < p; ++k)
-          if ((E[k] >> 14) == key) {
-            head = false;
-            break;
-          }
-        if (head) {
-          int cnt = 0;
-          unsigned long long rm = 0ull, cm = 0ull;
-          bool dup = false;
-          for (int k = p; k < be; ++k) {
-            const unsigned long long y = E[k];
-            if ((y >> 14) == key) {
-              const unsigned long long bi = 1ull << ((y >> 7) & 63u);
-              dup |= (rm & bi) != 0ull;
-              rm |= bi;
-              cm |= 1ull << (y & 63u);
-              ++cnt;
-            }
-          }
-          I = cnt;
-          if (dup || __popcll(cm) < cnt) {
-            // a shared row or column: first-fit, rows ascending, the lowest unused matching column
-            unsigned long long used = 0ull;
-            I = 0;
-            for (unsigned long long rr = rm; rr; rr &= rr - 1) {
-              const unsigned i = static_cast<unsigned>(__builtin_ctzll(rr));
-              unsigned long long cand = 0ull;
-              for (int k = p; k < be; ++k) {
-                const unsigned long long y = E[k];
-                if ((y >> 14) == key && ((y >> 7) & 63u) == i) cand |= 1ull << (y & 63u);
-              }
-              cand &= ~used;
-              if (cand) {
-                used |= cand & (0ull - cand);
-                ++I;
-              }
-            }
-          }
-          const unsigned al = static_cast<unsigned>(x >> 39) & lmask;
-          A = (b << lo) | static_cast<int>(al);
-          B = static_cast<int>(key & kRankMask);
-          U = RLA[al] + static_cast<int>((x >> 50) & 127u) - I;
-          edge = I > 0 && U <= UM[max(I, 1) - 1];
-          if (edge) atomicAdd(&FD[al], 1);
-        }
-      }
-      w_pairs += __popcll(__ballot(head));
-      // stage the edges: one LDS atomic per wave; past the stage, straight out with a global atomic
-      const unsigned long long em = __ballot(edge);
-      if (em) {
-        const int first = __builtin_ctzll(em);
-        int base = 0;
-        if (lane == first) base = atomicAdd(&s_esn, __popcll(em));
-        base = __shfl(base, first);
-        const int slot = base + mbcnt(em);
-        const unsigned long long rec = (static_cast<unsigned long long>(A) << 39) |
-                                       (static_cast<unsigned long long>(B) << 14) |
-                                       (static_cast<unsigned long long>(I) << 7) | static_cast<unsigned long long>(U);
-        if (edge && slot < kFuseEs) ES[slot] = rec;
-        const unsigned long long om = __ballot(edge && slot >= kFuseEs);
-        if (om) {
-          const int f2 = __builtin_ctzll(om);
-          unsigned long long gb = 0;
-          if (lane == f2) gb = atomicAdd(eo.count, static_cast<unsigned long long>(__popcll(om)));
-          gb = __shfl(gb, f2);
-          if (edge && slot >= kFuseEs) {
-            const long long k = static_cast<long long>(gb) + mbcnt(om);
-            if (k < eo.cap) {
-              eo.edges[k] = make_int2(A, B);
-              eo.edge_iu[k] = static_cast<unsigned short>(I | (U << 8));
-            }
-          }
-        }
-      }
-    }
-    __syncthreads();
-    // forward degrees of the bucket's reads that have entries
-    for (int a = tid; a < nr; a += NT) {
-      const int en_a = HIST[((a + 1) << hbB) - 1];
-      const int st_a = a > 0 ? HIST[(a << hbB) - 1] : 0;
-      if (en_a > st_a) {
-        const int f = FD[a];
-        g.fwd[(static_cast<long long>(b) << lo) + a] = f;
-        w_maxfwd = max(w_maxfwd, f);
-      }
-    }
-    b = bn; s = sn; e = en;
-  }
-  __syncthreads();
-  if (s_esn > 0) flush();
-  // statistics: plain stores into this wave's slots (field 2: matched pairs, field 3: max fwd)
-  for (int o = 32; o > 0; o >>= 1) w_maxfwd = max(w_maxfwd, __shfl_xor(w_maxfwd, o));
-  const long long wid = static_cast<long long>(blockIdx.x) * NW + w;
-  const unsigned long long f = lane == 2 ? w_pairs : static_cast<unsigned long long>(w_maxfwd);
-  if (lane == 2 || lane == 3) g.wstat[wid * kWsFields + lane] = f;
-}
-
 int bits_for(long long v) {
   int b = 1;
   while ((1ll << b) <= v) ++b;
@@ -1497,16 +1153,12 @@ int blocks_mode(int m) {
   return m == 0 ? b0 : m == 1 ? b1 : b2;
 }
 int blocks_pairs() { static const int b = resident_blocks(k_sweep_pairs); return b; }
-int tiles_of(const SweepArgs& a) { return static_cast<int>((static_cast<long long>(a.ni) + kWave - 1) / kWave); }
+int tiles_of(const SweepArgs& a) { return static_cast<int>((static_cast<long long>(a.nq) + kWave - 1) / kWave); }
 
 }  // namespace
 
 int sweep_max_waves() {
-  // the fused pair stage's waves plus the list pass's (their statistics slots are disjoint)
-  const int fused = std::max(resident_blocks_n(k_bucket_pairs<4096, 512>, 512) * 8,
-                             resident_blocks_n(k_bucket_pairs<12288, 1024>, 1024) * 16);
-  return std::max(std::max(std::max(blocks_mode(0), blocks_mode(1)), std::max(blocks_mode(2), blocks_pairs())) * kSwWaves,
-                  fused + blocks_pairs() * kSwWaves);
+  return std::max(std::max(blocks_mode(0), blocks_mode(1)), std::max(blocks_mode(2), blocks_pairs())) * kSwWaves;
 }
 
 size_t sweep_temp_bytes(long long ent_cap, long long ni, hipStream_t s) {
@@ -1525,25 +1177,14 @@ size_t sweep_temp_bytes(long long ent_cap, long long ni, hipStream_t s) {
 hipError_t launch_sweep_plan(const SweepArgs& a, hipStream_t s) {
   const int nt = tiles_of(a);
   if (nt == 0) return hipSuccess;
-  k_tile_tests<<<grid_for(static_cast<long long>(nt) * kWave, 256, 4096), 256, 0, s>>>(a.rng_s, a.ni, a.tile_tests);
+  k_tile_tests<<<grid_for(static_cast<long long>(nt) * kWave, 256, 4096), 256, 0, s>>>(a.rng_s, a.nq, a.tile_tests);
   size_t tb = a.temp_bytes;
   return hipcub::DeviceScan::ExclusiveSum(a.temp, tb, a.tile_tests, a.tile_ub, nt, s);
 }
 
-// k_sweep's chunks dealt grid-stride (default), or FSLR_SWEEP_MAP=xcd: each XCD a contiguous share.
-// Measured at cfg3 (profiles/r04/ab/): the XCD mapping 0.2485 ms against 0.2447 ms grid-stride.
-static int sweep_xcd_map() {
-  static const int v = [] {
-    const char* e = std::getenv("FSLR_SWEEP_MAP");
-    return e && std::strcmp(e, "xcd") == 0 ? 1 : 0;
-  }();
-  return v;
-}
-
 hipError_t launch_sweep_count(const SweepArgs& a0, int mode, long long* total_dev, hipStream_t s, long long* n_dev,
                               long long cap) {
-  SweepArgs a = a0;
-  a.xcd_map = sweep_xcd_map();
+  const SweepArgs& a = a0;
   const int nt = tiles_of(a);
   if (nt == 0) return hipMemsetAsync(total_dev, 0, 3 * sizeof(long long), s);
   const int blocks = std::min(blocks_mode(mode), (nt + kSwWaves - 1) / kSwWaves);
@@ -1583,14 +1224,12 @@ hipError_t launch_sweep_dense(const SweepArgs& a, int mode, hipStream_t s) {
                                                                                     a.tile_cnt, nt, a.ent);
   } else {
     const int be = std::min(blocks_mode(1), (nt + kSwWaves - 1) / kSwWaves);
-    SweepArgs a1 = a;
-    a1.xcd_map = sweep_xcd_map();
-    k_sweep<1><<<be, kSwBlock, 0, s>>>(a1);
+    k_sweep<1><<<be, kSwBlock, 0, s>>>(a);
   }
   return hipGetLastError();
 }
 
-int grp_ints() { return kGrpInts + kGrpSpillInts; }
+int grp_ints() { return kGrpInts; }
 
 // group the entries by A: from the tile slots (mode 2) or dense `src` into `mid`, then into `out`
 static hipError_t group_by_a(const SweepArgs& a, int mode, const unsigned long long* src, unsigned long long* mid,
@@ -1664,97 +1303,8 @@ hipError_t launch_sweep_partition(const SweepArgs& a, int mode, int shift, int n
   return hipGetLastError();
 }
 
-// the pair stage on the grouping's pass-1 buckets: pass 1 from the tile slots (mode 2) or dense `src`
-// into `mid`, k_bucket_pairs per bucket, then k_sweep_pairs in list mode over the buckets it spilled
-// into `out`.  Returns the per-wave statistics slots used (k_sum_slots sums them).
-static hipError_t fused_pairs(const SweepArgs& a, int mode, const unsigned long long* src, unsigned long long* mid,
-                              unsigned long long* out, hipStream_t s, int* waves) {
-  const long long n = a.n_ent;
-  const int nbits = bits_for(std::max(1, a.n_reads - 1));
-  // H = 2^hb buckets of about 2K entries, 2^lo reads each with lo <= kFuseMaxReadsLog; the digits
-  // of a bucket are (A's lo low bits, hbB = 12 - lo bits of B's hash)
-  int hb = 0;
-  while (hb < 14 && (n >> (12 + hb)) > 0) ++hb;
-  hb = std::max(hb, nbits - kFuseMaxReadsLog);
-  hb = std::min(hb, nbits);
-  const int H = 1 << hb, lo = nbits - hb, hbB = kFuseBinsLog - lo;
-  const int P = std::max(64, std::min({kMsdMaxBlocks, std::max((1 << 21) / H, 256), static_cast<int>((n + 8191) / 8192)}));
-  if (static_cast<long long>(H) * P > kGrpInts / 2 || H > kMsdMaxH) return hipErrorInvalidValue;
-  int* mat = a.grp;
-  int* off = a.grp + kGrpInts / 2;
-  long long* spill = reinterpret_cast<long long*>(a.grp + kGrpInts);
-  auto* spill_n = reinterpret_cast<unsigned long long*>(spill + 3 * kMsdMaxH);   // count << 40 | chunks
-  const int nt = tiles_of(a);
-  if (mode == 2)
-    k_msd_pass1<true, false><<<P, kMsdThreads, 0, s>>>(a.ent_ub, a.ub_cap, a.tile_ub, a.tile_cnt, nt, lo, H, mat, nullptr,
-                                                       0x7FFFFFFFFFFFFFFFll, spill_n);
-  else
-    k_msd_pass1<false, false><<<P, kMsdThreads, 0, s>>>(src, n, nullptr, nullptr, 0, lo, H, mat, nullptr,
-                                                        0x7FFFFFFFFFFFFFFFll, spill_n);
-  size_t tb = a.temp_bytes;
-  hipError_t e = hipcub::DeviceScan::ExclusiveSum(a.temp, tb, mat, off, H * P, s);
-  if (e != hipSuccess) return e;
-  if (mode == 2)
-    k_msd_pass1<true, true><<<P, kMsdThreads, 0, s>>>(a.ent_ub, a.ub_cap, a.tile_ub, a.tile_cnt, nt, lo, H, off, mid,
-                                                      a.n_dev ? a.ent_cap : 0x7FFFFFFFFFFFFFFFll);
-  else
-    k_msd_pass1<false, true><<<P, kMsdThreads, 0, s>>>(src, n, nullptr, nullptr, 0, lo, H, off, mid);
-  if (a.ev[4]) (void)hipEventRecord(a.ev[4], s);
-  // buckets of about 2K entries: 4096 in LDS, two workgroups per CU; beyond 2^14 buckets the
-  // buckets grow and take the one-workgroup-per-CU shape
-  const bool big = n > static_cast<long long>(H) * 2600;
-  int fw;
-  if (a.p0) (void)hipEventRecord(a.p0, s);
-  if (!big) {
-    constexpr int kCap = 4096, kNt = 512;
-    const int blocks = std::min(H, resident_blocks_n(k_bucket_pairs<kCap, kNt>, kNt));
-    fw = blocks * (kNt / kWave);
-    if (fw > a.wstat_waves) return hipErrorInvalidValue;
-    k_bucket_pairs<kCap, kNt><<<blocks, kNt, 0, s>>>(a, mid, off, P, H, lo, hbB, out, spill, spill_n);
-  } else {
-    constexpr int kCap = 12288, kNt = 1024;
-    const int blocks = std::min(H, resident_blocks_n(k_bucket_pairs<kCap, kNt>, kNt));
-    fw = blocks * (kNt / kWave);
-    if (fw > a.wstat_waves) return hipErrorInvalidValue;
-    k_bucket_pairs<kCap, kNt><<<blocks, kNt, 0, s>>>(a, mid, off, P, H, lo, hbB, out, spill, spill_n);
-  }
-  if (a.p1) (void)hipEventRecord(a.p1, s);
-  SweepArgs l = a;
-  l.ent_sorted = out;
-  l.spill = spill;
-  l.spill_n = spill_n;
-  l.wbase = fw;
-  const int lb = blocks_pairs();
-  if (fw + lb * kSwWaves > a.wstat_waves) return hipErrorInvalidValue;
-  k_sweep_pairs<<<lb, kSwBlock, 0, s>>>(l);
-  *waves = fw + lb * kSwWaves;
-  if (std::getenv("FSLR_DEBUG_SPILL")) {                // diagnostics: how much took the list pass
-    unsigned long long sw = 0;
-    (void)hipMemcpyAsync(&sw, spill_n, sizeof(sw), hipMemcpyDeviceToHost, s);
-    (void)hipStreamSynchronize(s);
-    std::fprintf(stderr, "fslr: pair stage H=%d lo=%d hbB=%d %s, %llu of %d buckets spilled (%llu chunks), n=%lld\n", H,
-                 lo, hbB, big ? "12288/1024" : "4096/512", sw >> 40, H, sw & ((1ull << 40) - 1), n);
-  }
-  return hipGetLastError();
-}
-
-// The pair stage: the two-level grouping (k_msd_pass1 + k_msd_pass2) and k_sweep_pairs (default), or
-// FSLR_PAIR_STAGE=fused: pass 2 fused with the evaluation (k_bucket_pairs).  Measured at cfg3
-// (profiles/r04/ab/): fused 0.374 ms of grouping pass 2 + pairs against 0.271 + 0.09 ms, step 1.176
-// against 1.146 ms.
-static bool legacy_pair_stage() {
-  static const bool v = [] {
-    const char* e = std::getenv("FSLR_PAIR_STAGE");
-    return !(e && std::strcmp(e, "fused") == 0);
-  }();
-  return v;
-}
-
 hipError_t launch_sweep_pairs(const SweepArgs& a0, int mode, hipStream_t s) {
   SweepArgs a = a0;
-  a.spill = nullptr;
-  a.spill_n = nullptr;
-  a.wbase = 0;
   if (a.ev[2]) (void)hipEventRecord(a.ev[2], s);
   const bool msd = a.grp && a.n_ent > 0 && a.n_ent < (1ll << 31);
   if (mode == 0 || (mode == 2 && !msd)) {
@@ -1762,18 +1312,6 @@ hipError_t launch_sweep_pairs(const SweepArgs& a0, int mode, hipStream_t s) {
     if (e != hipSuccess) return e;
   }
   if (a.ev[3]) (void)hipEventRecord(a.ev[3], s);
-  if (msd && !legacy_pair_stage()) {
-    // mode 2: tile slots -> ent (pass 1) -> pairs, spills in ent_sorted; mode 0: ent -> ent_sorted,
-    // spills in ent; mode 3: the caller's entries -> ent_mid, spills in ent_sorted
-    int waves = 0;
-    hipError_t e;
-    if (mode == 2) e = fused_pairs(a, 2, nullptr, a.ent, a.ent_sorted, s, &waves);
-    else if (mode == 0) e = fused_pairs(a, 0, a.ent, a.ent_sorted, a.ent, s, &waves);
-    else e = fused_pairs(a, 3, a.ent, a.ent_mid, a.ent_sorted, s, &waves);
-    if (e != hipSuccess) return e;
-    k_sum_slots<<<kSumBlocks, 256, 0, s>>>(a.wstat, waves, 2, 4, -1, -1, kMatchedPairs, a.counters, a.err + 3);
-    return hipGetLastError();
-  }
   if (msd) {
     // mode 2: tile slots -> ent -> ent_sorted; mode 0: ent -> ent_sorted -> ent (the pair kernel
     // then reads ent); mode 3: the caller's entries -> ent_mid -> ent_sorted

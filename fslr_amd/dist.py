@@ -124,6 +124,36 @@ def chrom_owner(chrom_counts, world: int) -> np.ndarray:
     return owner
 
 
+POSITION_COST = 4       # per sorted position, in pair tests: the sweep's per-position work beside its tests
+
+
+def position_plan(tile_tests, tile_reach, n_intervals: int, world: int, per_position: int = POSITION_COST):
+    """Contiguous ranges of the (chrom, start)-sorted positions, one per rank: cut at 64-position tile
+    boundaries where the running cost (the tile's pair tests, the sweep's work, plus ``per_position``
+    per position) reaches r / world of the total, whatever the chromosomes.  Returns (lo, hi, end) per
+    rank: the rank sweeps the pairs whose lower position lies in [lo, hi) and indexes [lo, end), end
+    covering the forward windows of its tiles (fslr_position_costs).  Deterministic: every rank makes the
+    same plan from its own full index."""
+    tests = np.asarray(tile_tests, np.int64)
+    reach = np.asarray(tile_reach, np.int64)
+    nt = tests.size
+    ni = int(n_intervals)
+    width = np.minimum(64, ni - 64 * np.arange(nt, dtype=np.int64))
+    cum = np.cumsum(tests + per_position * width)
+    total = int(cum[-1]) if nt else 0
+    cuts = [0]
+    for r in range(1, world):
+        cuts.append(max(cuts[-1], min(nt, int(np.searchsorted(cum, total * r / world, side='left')) + 1)))
+    cuts.append(nt)
+    out = []
+    for r in range(world):
+        t0, t1 = cuts[r], cuts[r + 1]
+        lo, hi = min(ni, 64 * t0), min(ni, 64 * t1)
+        end = max(hi, int(reach[t0:t1].max())) if t1 > t0 else hi
+        out.append((lo, hi, min(ni, end)))
+    return out
+
+
 def chrom_counts_of(csr) -> np.ndarray:
     return np.bincount(np.asarray(csr.iv_chrom), minlength=int(csr.n_chroms))
 
@@ -278,8 +308,18 @@ class SweepShard:
     """
 
     def __init__(self, ctx, n_reads: int, chrom_counts, world: int, rank: int, device, block_shift: int = 6,
-                 owner=None, comm=None):
+                 owner=None, comm=None, split: str = 'chrom'):
+        """``split``: 'chrom' — each rank indexes and sweeps whole chromosomes (largest first onto the
+        least-loaded rank); 'position' — each rank sweeps a contiguous range of sorted positions cut where
+        the pair tests balance (position_plan: one chromosome may span ranks), planned from one full
+        index build on the first step.  The edge cap's sharded replay lists its hits on whole
+        chromosomes in both (chrom_owner)."""
         import torch
+        if split not in ('chrom', 'position'):
+            raise ValueError(f'split must be chrom or position, not {split!r}')
+        self.split = split
+        self.pos = None                         # (lo, hi, end) of this rank once planned
+        self.n_intervals = int(np.asarray(chrom_counts, np.int64).sum())
         self.ctx = ctx
         self.comm = comm if comm is not None else TorchComm(device)
         self.n = int(n_reads)
@@ -296,7 +336,18 @@ class SweepShard:
         self.egath = torch.empty(1 << 12, dtype=torch.int64, device=self.device)
         self._labels = None
         self._rep = None                   # the last synchronous step's counts (repeat steps)
-        ctx.set_chrom_filter(self.owned if world > 1 else None)
+        if split == 'chrom':
+            ctx.set_chrom_filter(self.owned if world > 1 else None)
+
+    def _plan_positions(self):
+        """The position split's range of this rank (every rank makes the same plan from its full index)."""
+        ctx = self.ctx
+        ctx.set_chrom_filter(None)
+        ctx.build_index()
+        tests, reach = ctx.position_costs()
+        self.plan = position_plan(tests, reach, self.n_intervals, self.world)
+        self.pos = self.plan[self.rank]
+        ctx.set_position_filter(*self.pos)
 
     # -- collectives (self.comm: RCCL, gloo staged through host memory, or in-process) --------------
     def _all_to_all(self, out, inp, out_splits, in_splits):
@@ -330,6 +381,8 @@ class SweepShard:
         self._rep = None
         err = None
         try:
+            if self.split == 'position' and self.pos is None:
+                self._plan_positions()
             ctx.build_index()
             ok, counts = ctx.sweep_partition(qlen_cut, nal_cut, pass_table, W, self.block_shift, self.send,
                                              edge_threshold)
@@ -564,6 +617,12 @@ class SweepShard:
                 ctx.cap_install_restricted(rows, W * m, W, r)
             else:
                 ctx.cap_install_pairs(rows, W * m, W, r)
+            if self.split == 'position':
+                # the replay lists each interval's hits in search order from one index holding its whole
+                # chromosome: the chromosome split's index for this step (the next step's build restores
+                # the position range)
+                ctx.set_chrom_filter(self.owned if W > 1 else None)
+                ctx.build_index()
             ctx.cap_local(edge_threshold)
             nt = ctx.cap_sizes()[0]
             self.tinfo = self._grow32(getattr(self, 'tinfo', None), max(1, 2 * nt))
@@ -654,6 +713,8 @@ class SweepShard:
                 err = ZeroDivisionError('division by zero') if code == 1 else FslrError('error on another rank')
             if err is None:
                 self._merge(fp)
+        if self.split == 'position':
+            ctx.use_position_filter()
         if err is not None:
             raise err
         return cap
@@ -661,3 +722,163 @@ class SweepShard:
     def labels(self) -> np.ndarray:
         """Global min-rank labels after step() (every rank)."""
         return self._labels if self._labels is not None else self.ctx.labels()
+
+
+class PairShard(SweepShard):
+    """One rank of the query-shard split for the inputs the sweep split does not take:
+    overlap <= 0 (matches need not overlap), an aln_size == 0 interval, reads of more than FSLR_MAX_L
+    intervals.  Every rank holds every read and the full index and decides the pairs whose lower-rank
+    read lies in its blocks of 64 ranks (dealt round robin) — the walk engine's fslr_query_shard, or with
+    long reads the general evaluator's fslr_long_pairs_shard — so each pair is decided once
+    (cluster.py:197-208: a pair is first met from its lower-rank read's loop when no loop breaks).
+    Components merge by the ranks' local forests (as SweepShard).  ZeroDivisionError pairs are listed
+    per rank and raise on every rank when the cap does not bind anywhere.  When it binds, E* is gathered
+    and every rank replays the reference's loops over it (fslr_apply_edge_cap /
+    fslr_cap_replay_pairs); each rank then reports the capped edges and forward degrees of its own
+    read blocks, so the ranks' parts still add up to the one-GPU graph."""
+
+    def __init__(self, ctx, n_reads: int, world: int, rank: int, device, comm=None, long_reads: bool = False):
+        import torch
+        self.ctx = ctx
+        self.comm = comm if comm is not None else TorchComm(device)
+        self.n = int(n_reads)                   # real reads
+        self.world, self.rank = int(world), int(rank)
+        self.device = torch.device(device)
+        self.long = bool(long_reads)
+        self.esend = torch.empty(1 << 12, dtype=torch.int64, device=self.device)
+        self.egath = torch.empty(1 << 12, dtype=torch.int64, device=self.device)
+        self._labels = None
+        self._rep = None
+        self.edges_out = None                   # (a, b, I, U) of this rank's part (host)
+        self.fwd_out = None
+
+    def _mine(self, reads):
+        return (np.asarray(reads, np.int64) >> 6) % self.world == self.rank
+
+    def step(self, qlen_cut, nal_cut, pass_table, edge_threshold=10, **_) -> dict:
+        import torch
+        ctx, W, r = self.ctx, self.world, self.rank
+        thr = int(edge_threshold)
+        self._labels = None
+        err = None
+        mf = zd = ne = 0
+        part = None
+        try:
+            if self.long:
+                n_long = ctx.long_pairs_shard(qlen_cut, nal_cut, pass_table, r, W, thr)
+                st = ctx.stats(check=False)
+                part = ctx.long_edges(n_long)
+                ne = int(n_long)
+                mf = int(np.bincount(part[0], minlength=1).max()) if ne else 0
+            else:
+                while True:
+                    ctx.query_shard(qlen_cut, nal_cut, pass_table, r, W, thr)
+                    st = ctx.stats(check=False)
+                    grow = False
+                    if st['n_edges'] > st['edge_capacity']:
+                        ctx.reserve_edges(int(st['n_edges'] * 1.25) + 4096)
+                        grow = True
+                    if st['deferred'] > st['deferred_capacity']:
+                        ctx.reserve_deferred(int(st['deferred'] * 1.25) + 4096)
+                        grow = True
+                    if not grow:
+                        break
+                ne = int(st['n_edges'])
+                mf = int(st['max_fwd'])
+            zd = int(st.get('zd_pairs', 0))
+        except Exception as e:                         # noqa: BLE001 - re-raised on every rank below
+            if W == 1:
+                raise
+            err = e
+        code = 0 if err is None else (1 if isinstance(err, ZeroDivisionError) else 2)
+        if W > 1:
+            t = self.comm.small([mf, code, zd, ne])
+            self.comm.all_reduce(t, 'max')
+            mf, code, zd, ne_max = (int(x) for x in t.tolist())
+        else:
+            ne_max = ne
+        if err is None and code:
+            from ._lib import FslrError
+            err = ZeroDivisionError('division by zero') if code == 1 else FslrError('error on another rank')
+        if err is None and zd > 0 and mf <= thr:
+            err = ZeroDivisionError('division by zero')   # every loop runs to its end: each pair is visited
+        if err is not None:
+            raise err
+        out = {'capped': mf > thr, 'max_fwd': mf, 'n_edges_local': ne, 'path': 'long' if self.long else 'walk'}
+        if mf <= thr:
+            if self.long:
+                a, b, I, U = part
+                self.edges_out = (a, b, I, U)
+            else:
+                self.edges_out = ctx.edges(ne)
+            fwd = np.bincount(self.edges_out[0], minlength=self.n)[:self.n]
+            self.fwd_out = fwd.astype(np.int32)
+            if W > 1:
+                fp = ctx.local_forest()                # the merge unions the ranks' forests
+                t = self.comm.small([fp])
+                self.comm.all_reduce(t, 'max')
+                self._merge(int(t.item()))
+            else:
+                ctx.components()
+            self._labels = ctx.labels()[:self.n]
+            return out
+        cap, err = {}, None
+        try:
+            cap = self._capped(thr, part, ne_max)
+        except Exception as e:                         # noqa: BLE001 - a replayed loop raised on some rank
+            err = e
+        self._agree(err)
+        out['cap'] = cap
+        return out
+
+    def _capped(self, thr, part, ne_max):
+        """The cap binds: E* on every rank, the loops replayed on each (the same result everywhere)."""
+        import torch
+        ctx, W = self.ctx, self.world
+        m = max(1, int(ne_max))
+        if self.long:
+            a, b, I, U = part
+            rows = np.full((m, 4), -1, np.int32)
+            rows[:a.size] = np.stack([a, b, I, U], axis=1)
+            t = torch.from_numpy(rows.reshape(-1).view(np.int64).copy()).to(self.device)
+            g = torch.empty(W * t.numel(), dtype=torch.int64, device=self.device)
+            if W > 1:
+                self._all_gather(g, t)
+            else:
+                g = t
+            allr = g.cpu().numpy().view(np.int32).reshape(-1, 4)
+            allr = allr[allr[:, 0] >= 0]
+            order = np.lexsort((allr[:, 1], allr[:, 0]))
+            allr = allr[order]
+            a, b, I, U = (allr[:, k].copy() for k in range(4))
+            who, fwd, cap = ctx.cap_replay_pairs(thr, a, b, self.n)
+            keep = who != 2
+            a2, b2 = np.where(who == 0, a, b)[keep], np.where(who == 0, b, a)[keep]
+            I2, U2 = I[keep], U[keep]
+            ctx.components()
+            self._labels = ctx.labels()[:self.n]
+        else:
+            self.esend = self._grow(self.esend, 2 * m)            # rows of 16 B: two int64 per row
+            self.egath = self._grow(self.egath, 2 * W * m)
+            ctx.edges_iu_into(self.esend, m)
+            if W > 1:
+                self._all_gather(self.egath[:2 * W * m], self.esend[:2 * m])
+                rows = self.egath
+            else:
+                rows = self.esend
+            ctx.cap_install_edges(rows, W * m)
+            cap = ctx.apply_edge_cap(thr)
+            st = ctx.stats()
+            a2, b2, I2, U2 = ctx.edges(st['n_edges'])
+            fwd = ctx.fwd_degree()
+            ctx.components()
+            self._labels = ctx.labels()[:self.n]
+        mine = self._mine(a2)
+        self.edges_out = (a2[mine], b2[mine], I2[mine], U2[mine])
+        f = np.asarray(fwd, np.int64)[:self.n].copy()
+        f[~self._mine(np.arange(self.n))] = 0
+        self.fwd_out = f.astype(np.int32)
+        return cap
+
+    def labels(self) -> np.ndarray:
+        return self._labels

@@ -24,6 +24,7 @@ from concurrent.futures import ThreadPoolExecutor
 import numpy as np
 
 from . import cluster, ingest
+from ._lib import FSLR_MAX_L, FslrError
 from .prep import IntervalData, data_order, mask_keep
 
 INT_COLS = ('rstart', 'rend', 'n_alignments', 'aln_size', 'qstart', 'qend', 'alignment_score')
@@ -80,7 +81,7 @@ def run(args, basename, tsv, ints, strs, t):
     pandas path; the HIP context it opened is closed first, so the pandas path opens the only one."""
     # the HIP context comes up while the host prepares the input (one GPU; the multi-GPU ranks make
     # their own)
-    pool = ThreadPoolExecutor(2)
+    pool = ThreadPoolExecutor(3)
     ctx_f = pool.submit(cluster._open_context, args.get('device')) if (args.get('gpus') or 1) == 1 else None
     state = {'trees': None}
     try:
@@ -133,31 +134,56 @@ def _run(args, basename, tsv, ints, strs, t, pool, ctx_f, state):
     start = f['start']
     t['prepare.fill'] = time.perf_counter() - t1
     # prepare_data's sort_values('start') (pandas' quicksort argsort, ties included; numpy sorts
-    # without the GIL, so mask_sequences2 and the writers' per-qname sums run beside it)
+    # without the GIL, so mask_sequences2, the writers' per-qname sums and the rows' upload to the
+    # device run beside it)
     order_f = pool.submit(data_order, start)
+    rows_f = pool.submit(_rows_upload, ctx_f, f, n_q, int(chrom_num.max(initial=0)) + 1) \
+        if ctx_f is not None and start.size else None
     keepm = mask_keep(f['chrom'], start, f['end'], mask, chr_lengths, 500_000) if mask else None
     qc = qcode[rows].astype(np.int64)
     w = _writer_prep(qc, n_q, score[rows])
     order = order_f.result()
     t['prepare.sort'] = time.perf_counter() - t1 - t['prepare.fill']
-    if keepm is not None:
-        order = order[keepm[order]]
-    c, s, e, a, q, nal, ql2, ix = ingest.gather_columns([f['chrom'], start, f['end'], f['aln'], f['qcode'], f['nal'],
-                                                         f['qlen2'], f['frow']], order)
-    mid = a // 2 + s
-    data = IntervalData(chrom=c, start=s, end=e, aln_size=a, qcode=q, qnames=_LazyQnames(tsv, n_q),
-                        n_alignments=nal, qlen2=ql2, middle=mid, index=ix)
-    t['prepare'] = time.perf_counter() - t1
-    t1 = time.perf_counter()
-    csr = data.csr()
-    t['csr'] = time.perf_counter() - t1
 
-    t2 = time.perf_counter()
-    trees = state['trees'] = cluster.build_interval_trees(data, device=args.get('device'),
-                                                          n_gpus=args.get('gpus') or 1,
-                                                          ctx=ctx_f.result() if ctx_f is not None else None)
-    pool.shutdown()
-    t['upload'] = time.perf_counter() - t2
+    def host_data():
+        # the prepared `data` list as columns on the host (IntervalData): the masked order's gathers
+        o = order if keepm is None else order[keepm[order]]
+        c, s, e, a, q, nal, ql2, ix = ingest.gather_columns([f['chrom'], start, f['end'], f['aln'], f['qcode'],
+                                                             f['nal'], f['qlen2'], f['frow']], o)
+        return IntervalData(chrom=c, start=s, end=e, aln_size=a, qcode=q, qnames=_LazyQnames(tsv, n_q),
+                            n_alignments=nal, qlen2=ql2, middle=a // 2 + s, index=ix)
+    trees = None
+    if rows_f is not None and rows_f.result():
+        # the device makes the `data` list, the read ranks and the CSR from the rows (fslr_set_reads_rows)
+        ctx = ctx_f.result()
+        t['prepare'] = time.perf_counter() - t1
+        t1 = time.perf_counter()
+        try:
+            info = ctx.set_reads_rows(order, keepm, args['overlap'])
+        except FslrError as e:
+            if getattr(e, 'info', {}).get('max_len', 0) <= FSLR_MAX_L:
+                raise
+            info = None                          # reads of more than FSLR_MAX_L intervals: the host CSR
+        if info is not None:
+            data = _LazyData(host_data)
+            csr = cluster.RowsCSR(ctx, info)
+            t['csr'] = time.perf_counter() - t1
+            t2 = time.perf_counter()
+            trees = state['trees'] = cluster.RowsIndex(data, csr, ctx, args['overlap'])
+            pool.shutdown()
+            t['upload'] = time.perf_counter() - t2
+    if trees is None:
+        data = host_data()
+        t['prepare'] = time.perf_counter() - t1
+        t1 = time.perf_counter()
+        csr = data.csr()
+        t['csr'] = time.perf_counter() - t1
+        t2 = time.perf_counter()
+        trees = state['trees'] = cluster.build_interval_trees(data, device=args.get('device'),
+                                                              n_gpus=args.get('gpus') or 1,
+                                                              ctx=ctx_f.result() if ctx_f is not None else None)
+        pool.shutdown()
+        t['upload'] = time.perf_counter() - t2
     t2 = time.perf_counter()
     g = cluster.query_graph(trees, data, args['overlap'], [float(i) for i in args['jaccard_cutoffs'].split(',')], 10,
                             args['qlen_diff'], args['n_alignment_diff'])
@@ -244,6 +270,36 @@ def _run_starts(codes):
     st = np.concatenate(([0], np.flatnonzero(codes[1:] != codes[:-1]) + 1))
     distinct = np.count_nonzero(np.bincount(codes))
     return st if distinct == st.size else None
+
+
+def _rows_upload(ctx_f, f, n_q, n_chrom_ids):
+    """The fillings' columns to the device (fslr_rows_upload) while the host sorts; False when no
+    context came up (the CPU tests stand the oracle in for the device)."""
+    ctx = ctx_f.result()
+    if ctx is None:
+        return False
+    ctx.rows_upload(f, n_q, n_chrom_ids)
+    return True
+
+
+class _LazyData:
+    """IntervalData of the device path: built on the host only if something reads it."""
+
+    def __init__(self, build):
+        self._build, self._d = build, None
+
+    def _get(self):
+        if self._d is None:
+            self._d = self._build()
+        return self._d
+
+    def __len__(self):
+        return len(self._get())
+
+    def __getattr__(self, name):
+        if name.startswith('_'):
+            raise AttributeError(name)
+        return getattr(self._get(), name)
 
 
 class _LazyQnames:

@@ -47,7 +47,7 @@ def sweep_applies(csr, iv_thr) -> bool:
     """The chromosome split runs the sweep engine over each rank's chromosome filter: every folded
     overlap threshold >= 1 (overlap > 0), no aln_size == 0 interval and the intervals
     in the start-sorted data order the filter compacts (fslr_set_chrom_filter; any number of
-    chromosomes).  Otherwise the query runs on one GPU."""
+    chromosomes).  Otherwise the ranks split the queries instead (dist.PairShard)."""
     t = np.asarray(iv_thr)
     return bool((t.size == 0 or t.min() >= 1) and getattr(csr, 'start_sorted', True))
 
@@ -115,7 +115,8 @@ class _Rank:
         are restored."""
         import torch
         from . import _lib
-        from .dist import SweepShard, agree_error, chrom_counts_of
+        from .dist import PairShard, SweepShard, agree_error, chrom_counts_of
+        from .prep import FSLR_MAX_L, FSLR_THR_ZERO_ALN, umax_table
         prev_dev = torch.cuda.current_device()
         prev_stream = torch.cuda.current_stream()
         torch.cuda.set_device(self.dev_index)
@@ -129,9 +130,24 @@ class _Rank:
                 csr, thr, pt, meta = _load(d)
                 if self.ctx is None:
                     self.ctx = _lib.Context(self.dev_index, stream=self.stream.cuda_stream)
-                self.ctx.load_csr(csr, thr)
-                self.ctx.reserve_edges(max(1 << 16, 12 * csr.n_reads // self.world))
-                shard = SweepShard(self.ctx, csr.n_reads, chrom_counts_of(csr), self.world, self.rank, self.dev)
+                rlen = np.diff(np.asarray(csr.read_off, np.int64))
+                long_reads = bool(rlen.size and rlen.max() > FSLR_MAX_L)
+                if sweep_applies(csr, thr) and not long_reads:
+                    self.ctx.load_csr(csr, thr)
+                    self.ctx.reserve_edges(max(1 << 16, 12 * csr.n_reads // self.world))
+                    shard = SweepShard(self.ctx, csr.n_reads, chrom_counts_of(csr), self.world, self.rank, self.dev,
+                                       split=meta.get('split', 'chrom'))
+                else:
+                    # the query-shard split (dist.PairShard): every rank the full index
+                    if long_reads:
+                        self.ctx.load_csr_any(csr, np.where(np.asarray(csr.iv_aln) == 0, FSLR_THR_ZERO_ALN, 0))
+                        self.ctx.set_thresholds(thr)
+                        self.ctx.set_long_cutoffs(umax_table(meta['cutoffs'], int(rlen.max())))
+                    else:
+                        self.ctx.load_csr(csr, thr)
+                    self.ctx.reserve_edges(max(1 << 16, 12 * csr.n_reads))
+                    self.ctx.build_index()
+                    shard = PairShard(self.ctx, csr.n_reads, self.world, self.rank, self.dev, long_reads=long_reads)
             except Exception as e:                   # noqa: BLE001 - raised on every rank by agree_error
                 err = e
             try:
@@ -146,11 +162,15 @@ class _Rank:
                 info = shard.step(meta['qlen_cut'], meta['nal_cut'], pt, int(meta['edge_threshold']))
                 torch.cuda.synchronize(self.dev)
                 labels = shard.labels()
-                st = ctx.stats()
-                a, b, I, U = ctx.edges(st['n_edges'])
-                fwd = ctx.fwd_degree()
+                if isinstance(shard, PairShard):
+                    (a, b, I, U), fwd = shard.edges_out, shard.fwd_out
+                else:
+                    st = ctx.stats()
+                    a, b, I, U = ctx.edges(st['n_edges'])
+                    fwd = ctx.fwd_degree()
                 return {'labels': labels, 'edges': (a, b, I, U), 'fwd': fwd, 'capped': bool(info['capped']),
-                        'max_fwd': int(info['max_fwd']), 'cap': info.get('cap', {}), 'backend': self.backend}
+                        'max_fwd': int(info['max_fwd']), 'cap': info.get('cap', {}), 'backend': self.backend,
+                        'path': info.get('path', 'sweep-' + shard.split if isinstance(shard, SweepShard) else 'sweep')}
             except BaseException:
                 self.ctx.close()                      # a failed query leaves no half-set context behind
                 self.ctx = None
@@ -294,13 +314,14 @@ class RankPool:
                                            else f'multi-GPU rank {r} answered {line!r} instead of DONE')
                     del pending[r]
 
-    def query(self, csr, iv_thr, qlen_cut, nal_cut, pass_table, edge_threshold) -> dict:
+    def query(self, csr, iv_thr, qlen_cut, nal_cut, pass_table, edge_threshold, cutoffs=None, split='chrom') -> dict:
         """One chromosome-split query; returns rank 0's view (labels, edges, fwd, capped, max_fwd, cap,
         backend)."""
         d = os.path.join(self.dir, f'q{self.n_queries}')
         self.n_queries += 1
         _save(d, csr, iv_thr, dict(qlen_cut=float(qlen_cut), nal_cut=float(nal_cut), pass_table=pass_table,
-                                   edge_threshold=int(edge_threshold)))
+                                   edge_threshold=int(edge_threshold), split=split,
+                                   cutoffs=None if cutoffs is None else [float(x) for x in cutoffs]))
         try:
             for p in self.procs.values():
                 p.stdin.write(f'RUN {d}\n')
@@ -403,12 +424,20 @@ def close_pools():
 
 
 def query(csr, iv_thr, qlen_cut, nal_cut, pass_table, edge_threshold, n_gpus, first_device=0,
-          force_gloo=False) -> dict:
+          force_gloo=False, cutoffs=None, split='chrom') -> dict:
     """Run the chromosome-split query on ``n_gpus`` ranks of this process's pool; returns rank 0's view:
     ``labels`` (global min-rank labels), ``edges`` (a, b, I, U over all ranks), ``fwd`` (forward
     degrees), ``capped``, ``max_fwd``, ``backend``.  The pool's children start on the first call (or
     earlier, ``pool()``), before this process initialises the GPU."""
-    return pool(n_gpus, first_device, force_gloo).query(csr, iv_thr, qlen_cut, nal_cut, pass_table, edge_threshold)
+    global last_path
+    rlen = np.diff(np.asarray(csr.read_off, np.int64))
+    long_reads = bool(rlen.size and rlen.max() > 64)
+    last_path = 'sweep-' + split if sweep_applies(csr, iv_thr) and not long_reads else ('long' if long_reads else 'walk')
+    return pool(n_gpus, first_device, force_gloo).query(csr, iv_thr, qlen_cut, nal_cut, pass_table, edge_threshold,
+                                                        cutoffs=cutoffs, split=split)
+
+
+last_path = None           # the split the last multi-GPU query took (tests: no one-GPU fallback)
 
 
 if __name__ == '__main__':

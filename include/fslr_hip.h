@@ -75,7 +75,7 @@
 extern "C" {
 #endif
 
-#define FSLR_ABI_VERSION 15
+#define FSLR_ABI_VERSION 18
 #define FSLR_MAX_L 64                /* max intervals per read (bitmask width) */
 #define FSLR_MAX_READS (1 << 25)     /* read rank packs into bits 6..30 of the index record */
 #define FSLR_THR_ZERO_ALN INT32_MIN
@@ -206,6 +206,47 @@ int  fslr_set_profiling(fslr_ctx *ctx, int enable);     /* 1: hipEvents per phas
 
 /* Copy the CSR (host pointers) into context-owned HBM buffers (H2D). */
 int  fslr_set_reads(fslr_ctx *ctx, const fslr_reads *reads);
+/* The clustering input from rows (the columnar CLI path).  fslr_rows_upload copies
+ * keep_fillings' rows (cluster.py:14-31), file order, as int64 columns (syncs; a caller may run it while
+ * it sorts the starts).  fslr_set_reads_rows takes prepare_data's start order of those rows (the
+ * argsort of `start`, cluster.py:114) and, optionally, mask_sequences2's keep flag per row
+ * (cluster.py:89-106); on the device it forms the `data` list, ranks the reads by first appearance in
+ * it and groups each read's intervals in data order (cluster.py:189-191), numbers the chromosomes
+ * present densely in ascending order, folds the overlap thresholds for `overlap` (fslr_reads iv_thr)
+ * and sets the reads as fslr_set_reads with iv_data_pos would.  A read of more than FSLR_MAX_L
+ * intervals sets nothing: FSLR_ERR_INVALID with info->max_len > FSLR_MAX_L (use fslr_set_reads_any).
+ * fslr_get_read_codes: the qname code of each read rank.  fslr_get_csr: the CSR the device made (as
+ * fslr_reads with its folded thresholds, plus aln_size per interval, the data position of each interval and the chromosome
+ * number of each dense id; NULL outputs are skipped).  fslr_fold_thresholds: the thresholds of another
+ * overlap, folded on the device (as fslr_set_thresholds). */
+typedef struct {
+    int64_t n_rows;                /* fillings */
+    int64_t n_codes;               /* qcode values lie in [0, n_codes) */
+    int64_t n_chrom_ids;           /* chrom values lie in [0, n_chrom_ids) */
+    const int64_t *chrom;          /* rename_chromosomes' number (cluster.py:34-43) */
+    const int64_t *start, *end;    /* min / max of rstart, rend (cluster.py:111-112) */
+    const int64_t *aln;            /* aln_size */
+    const int64_t *qcode;          /* the row's qname code */
+    const int64_t *nal;            /* n_alignments */
+    const int64_t *qlen2;          /* the row's read's keep_fillings qlen2 */
+} fslr_rows;
+typedef struct {
+    int64_t n_reads, n_intervals;
+    int32_t n_chroms;              /* chromosomes present (dense ids) */
+    int32_t max_len;               /* longest read */
+    int32_t nal_varies;            /* n_alignments differs between intervals of a read */
+    int32_t general_thresholds;    /* a threshold below 1 (overlap <= 0): the sweep does not apply */
+    int32_t any_zero_aln;          /* an aln_size == 0 interval */
+    int32_t pad;
+} fslr_rows_info;
+int  fslr_rows_upload(fslr_ctx *ctx, const fslr_rows *rows);
+int  fslr_set_reads_rows(fslr_ctx *ctx, const int64_t *order, const uint8_t *keep, double overlap,
+                         fslr_rows_info *info);
+int  fslr_get_read_codes(fslr_ctx *ctx, int64_t *codes);
+int  fslr_get_csr(fslr_ctx *ctx, int32_t *read_off, int32_t *read_qlen2, int32_t *read_nal, int32_t *iv_chrom,
+                  int32_t *iv_start, int32_t *iv_end, int64_t *iv_aln, int32_t *iv_thr, int64_t *data_pos,
+                  int64_t *chrom_ids);
+int  fslr_fold_thresholds(fslr_ctx *ctx, double overlap);
 /* Replace the folded overlap thresholds (iv_thr, CSR order) without re-uploading
  * or re-indexing: the index does not depend on them (calculate_overlap's
  * `percentage`, cluster.py:157, is a query-time parameter). */
@@ -263,6 +304,20 @@ int  fslr_components(fslr_ctx *ctx);
  * fslr_set_reads.  Async; fslr_read_stats / fslr_components / fslr_get_edges follow as after
  * fslr_query. */
 int  fslr_set_chrom_filter(fslr_ctx *ctx, const uint8_t *owned);
+/* The position split: a rank sweeps a contiguous range of the (chrom, start)-sorted
+ * positions, cut where the pair tests balance, whatever the chromosomes.
+ * fslr_position_costs: after fslr_build_index over every chromosome, per tile of 64 sorted positions
+ *   its pair tests (the sum of its forward counts) and the end of its forward window (max q + n_fwd(q)
+ *   + 1); n_tiles = ceil(n_intervals / 64).  Syncs.
+ * fslr_set_position_filter: the next fslr_build_index indexes the sorted positions [lo, end) only and
+ *   fslr_sweep_partition sweeps the pairs whose lower position lies in [lo, hi); end must cover the
+ *   forward windows of [lo, hi) (fslr_position_costs).  Every pair of overlapping intervals is met by
+ *   the rank holding its lower position.  Needs iv_data_pos and <= 64 chromosomes.  Syncs.
+ * fslr_use_position_filter: make the last position filter of these reads active again (after
+ *   fslr_set_chrom_filter, which the edge cap's sharded replay lists its hits with). */
+int  fslr_position_costs(fslr_ctx *ctx, int64_t *tile_tests, int64_t *tile_reach, int64_t n_tiles);
+int  fslr_set_position_filter(fslr_ctx *ctx, int64_t lo, int64_t hi, int64_t end);
+int  fslr_use_position_filter(fslr_ctx *ctx);
 /* Multi-GPU edge cap (cluster.py:197-224).  The replayed loops need every E* edge
  * and every hit of the reads that can reach the cap; a rank's index holds its chromosomes' hits.
  * fslr_copy_edges_iu_device: this context's edges as int32 rows {a, b, I | U << 8, 0} into a device
@@ -398,6 +453,11 @@ int  fslr_get_long_edges(fslr_ctx *ctx, int32_t *a, int32_t *b, int32_t *I, int3
  * graph drops it; fwd[n_reads] (may be NULL) = edges formed in each read's own loop.  The capped
  * graph also becomes the context's edges (fslr_components).  Syncs; out may be NULL. */
 int  fslr_long_pairs(fslr_ctx *ctx, const fslr_params *params, int64_t *n_edges);
+/* fslr_long_pairs for the pairs whose lower-rank read lies in query shard `shard` of `n_shards` (read
+ * blocks of 64 dealt round robin, as fslr_query_shard): the shards together give fslr_long_pairs'
+ * edges, each pair once (the multi-GPU split of the inputs the sweep does not take). */
+int  fslr_long_pairs_shard(fslr_ctx *ctx, const fslr_params *params, int32_t shard, int32_t n_shards,
+                           int64_t *n_edges);
 int  fslr_cap_replay_pairs(fslr_ctx *ctx, int32_t edge_threshold, const int32_t *a, const int32_t *b, int64_t ne,
                            uint8_t *who, int32_t *fwd, fslr_cap_stats *out);
 

@@ -33,6 +33,13 @@ class EmuSweepContext:
         self.slot = np.arange(off[-1]) - off[self.read_of]
         self.L = np.diff(off)
         self.owned = None
+        self.prange = None                                 # the position split's (lo, hi, end)
+        self._pset = None
+        self.n_intervals = int(off[-1])
+        # each interval's position in the (chrom, start)-sorted index: chromosome, then data order
+        self.pos = np.empty(self.n_intervals, np.int64)
+        self.pos[np.lexsort((np.asarray(csr.data_pos, np.int64), np.asarray(csr.iv_chrom, np.int64)))] = \
+            np.arange(self.n_intervals)
         self.edge_capacity = 1 << 30
         self._edges = np.zeros((0, 4), np.int64)
         self._parent = np.arange(self.n_reads)
@@ -41,6 +48,41 @@ class EmuSweepContext:
     # -- filter / index ------------------------------------------------------------------------
     def set_chrom_filter(self, owned):
         self.owned = None if owned is None else np.asarray(owned, dtype=bool)
+        self.prange = None
+
+    def _n_fwd(self):
+        """Per sorted position q: #{p > q of its chromosome : start_p <= end_q} (end-inclusive hits)."""
+        c = self.csr
+        order = np.argsort(self.pos)
+        ch = np.asarray(c.iv_chrom, np.int64)[order]
+        st = np.asarray(c.iv_start, np.int64)[order]
+        en = np.asarray(c.iv_end, np.int64)[order]
+        nf = np.zeros(order.size, np.int64)
+        for x in np.unique(ch):
+            k = np.flatnonzero(ch == x)
+            nf[k] = np.searchsorted(st[k], en[k], side='right') - np.arange(k.size) - 1
+        return nf
+
+    def position_costs(self):
+        nf = self._n_fwd()
+        nt = (nf.size + 63) // 64
+        tests = np.array([nf[64 * t:64 * t + 64].sum() for t in range(nt)], np.int64)
+        reach = np.array([(np.arange(64 * t, min(nf.size, 64 * t + 64)) + nf[64 * t:64 * t + 64] + 1).max()
+                          for t in range(nt)], np.int64)
+        return tests, reach
+
+    def set_position_filter(self, lo, hi, end):
+        nf = self._n_fwd()
+        q = np.arange(nf.size)
+        sel = (q >= lo) & (q < hi)
+        assert (q[sel] + nf[sel] < end).all(), 'the position range does not hold its forward windows'
+        self.owned = None
+        self.prange = self._pset = (int(lo), int(hi), int(end))
+
+    def use_position_filter(self):
+        assert self._pset is not None
+        self.owned = None
+        self.prange = self._pset
 
     def build_index(self):
         pass
@@ -77,6 +119,10 @@ class EmuSweepContext:
             ra, rb = self.read_of[ks][:, None], self.read_of[ks][None, :]
             hit = (o >= 0) & (ra < rb)              # end-inclusive overlap of two different reads (:201)
             ok = hit & (o >= self.thr[ks][:, None]) & (o >= self.thr[ks][None, :])
+            if self.prange is not None:             # the position split: the pair's lower position in [lo, hi)
+                lower = np.minimum(self.pos[ks][:, None], self.pos[ks][None, :])
+                inr = (lower >= self.prange[0]) & (lower < self.prange[1])
+                hit &= inr
             x, y = np.nonzero(hit)
             for p, q, m in zip(ks[x].tolist(), ks[y].tolist(), ok[x, y].tolist()):
                 a, b = int(self.read_of[p]), int(self.read_of[q])

@@ -434,7 +434,7 @@ def test_sweep_split_contexts_one_gpu_equals_oracle(W):
     assert per_rank.min() > 0 and per_rank.max() < 2.0 * per_rank.mean()
 
 
-def _sweep_shards_threads(csr, thr, pt, W, edge_threshold, steps=1):
+def _sweep_shards_threads(csr, thr, pt, W, edge_threshold, steps=1, split='chrom'):
     """The product's dist.SweepShard on W ranks that are threads of this process, each with its own
     context and stream on cuda:0, the collectives in-process (dist.LocalHub: a device synchronize,
     then every rank copies what it needs).  Returns (contexts, step infos of the last step)."""
@@ -454,9 +454,10 @@ def _sweep_shards_threads(csr, thr, pt, W, edge_threshold, steps=1):
             ctxs[r] = c
             c.load_csr(csr, thr)
             c.reserve_edges(max(1 << 16, 12 * csr.n_reads // W))
-            sh = SweepShard(c, csr.n_reads, chrom_counts_of(csr), W, r, dev, comm=hub.comm(r, dev))
+            sh = SweepShard(c, csr.n_reads, chrom_counts_of(csr), W, r, dev, comm=hub.comm(r, dev), split=split)
             for _ in range(steps):
                 infos[r] = sh.step(1 - 0.04, 1 - 0.25, pt, edge_threshold)
+            infos[r]['pos'] = sh.pos
             torch.cuda.synchronize(dev)
         except BaseException as e:                     # noqa: BLE001 - re-raised by the caller
             errs[r] = e
@@ -768,3 +769,210 @@ def test_sweep_partition_repeat_equals_sync():
     with pytest.raises(_lib.FslrError):
         ctx.sweep_partition_repeat(qc, nc, pt, 3, 6, dst)
     ctx.close()
+
+
+def skewed_case(n=6000, seed=37):
+    """>= 50 % of the intervals on one chromosome (a targeted-panel genome): the chromosome split cannot
+    balance it, the position split can."""
+    w = np.ones(len(synth.CHROMS))
+    w[0] = len(synth.CHROMS) * 1.2
+    s = synth.generate(n, 8, seed, chrom_weights=w)
+    return s.interval_data().csr()
+
+
+def test_position_plan_balances_a_skewed_genome():
+    """position_plan cuts the sorted positions where the emulated pair tests balance; the ranges tile the
+    index, every range holds its forward windows, and the most loaded rank is within 1.2 of the mean
+    (the chromosome split: > 3 x at W = 8)."""
+    from fslr_amd.dist import chrom_owner, position_plan
+    from fslr_amd.prep import fold_overlap_threshold
+    from tests.sweep_emu import EmuSweepContext
+    csr = skewed_case(20000)
+    counts = np.bincount(csr.iv_chrom, minlength=csr.n_chroms)
+    assert counts.max() >= 0.5 * counts.sum()
+    ctx = EmuSweepContext(csr, fold_overlap_threshold(csr.iv_aln, 0.8))
+    tests, reach = ctx.position_costs()
+    nf = ctx._n_fwd()
+    cost = nf + 4
+    for W in (2, 4, 8):
+        plan = position_plan(tests, reach, csr.n_intervals, W)
+        assert plan[0][0] == 0 and plan[-1][1] == csr.n_intervals
+        for (a0, a1, e), (b0, _, _) in zip(plan, plan[1:]):
+            assert a1 == b0
+        for lo, hi, end in plan:
+            q = np.arange(lo, hi)
+            assert (q + nf[lo:hi] < end).all() and end <= csr.n_intervals
+        per = np.array([cost[lo:hi].sum() for lo, hi, _ in plan])
+        assert per.max() <= 1.2 * per.mean() + 64 * 40, (W, per)
+        own = chrom_owner(counts, W)
+        pos_c = np.asarray(csr.iv_chrom)[np.argsort(ctx.pos)]
+        per_c = np.array([cost[np.isin(pos_c, np.flatnonzero(own == r))].sum() for r in range(W)])
+        if W == 8:
+            assert per_c.max() > 3 * per_c.mean()
+
+
+def _pos_worker(rank, world, port, csr, thr, out_dir, edge_threshold):
+    import torch.distributed as dist
+    from fslr_amd.dist import SweepShard, chrom_counts_of
+    from fslr_amd.prep import pass_table
+    from tests.sweep_emu import EmuSweepContext
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    ctx = EmuSweepContext(csr, thr)
+    sh = SweepShard(ctx, csr.n_reads, chrom_counts_of(csr), world, rank, 'cpu', split='position')
+    pt = pass_table([1, 1, 0.66, 0.66, 0.66, 0.5])
+    info = sh.step(1 - 0.04, 1 - 0.25, pt, edge_threshold)
+    info2 = sh.step(1 - 0.04, 1 - 0.25, pt, edge_threshold, repeat=True)
+    assert info2.get('repeat', False) == (not info['capped'])
+    np.save(os.path.join(out_dir, f'labels{rank}.npy'), sh.labels())
+    a, b, I, U = ctx.edges(ctx.stats().get('n_edges', 0))
+    np.save(os.path.join(out_dir, f'edges{rank}.npy'), np.stack([a, b, I, U], axis=1) if len(a) else np.zeros((0, 4)))
+    np.save(os.path.join(out_dir, f'pos{rank}.npy'), np.array(sh.pos))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('edge_threshold', [10, 2])
+def test_gloo_world2_position_split_equals_oracle(tmp_path, edge_threshold):
+    """SweepShard(split='position') over gloo at world size 2 on a skewed genome: the ranks' ranges tile
+    the sorted positions (one chromosome spans both), the ranks' edges partition the oracle's (capped
+    with edge_threshold 2: the replay lists its hits on the chromosome split) and every rank has the
+    oracle's components."""
+    import torch.multiprocessing as mp
+    from fslr_amd.prep import fold_overlap_threshold
+    csr = skewed_case()
+    thr = fold_overlap_threshold(csr.iv_aln, 0.8)
+    mp.start_processes(_pos_worker, args=(2, _free_port(), csr, thr, str(tmp_path), edge_threshold), nprocs=2,
+                       join=True, start_method='spawn')
+    ref = O.run_core(_oracle_csr(csr), use_cap=True, edge_threshold=edge_threshold)
+    p0, p1 = np.load(tmp_path / 'pos0.npy'), np.load(tmp_path / 'pos1.npy')
+    assert p0[0] == 0 and p0[1] == p1[0] and p1[1] == csr.n_intervals
+    for r in range(2):
+        np.testing.assert_array_equal(_components_from_labels(np.load(tmp_path / f'labels{r}.npy')), ref['comp'])
+    e = np.concatenate([np.load(tmp_path / f'edges{r}.npy') for r in range(2)]).astype(np.int64)
+    want = sorted(zip(ref['edge_a'].tolist(), ref['edge_b'].tolist(), ref['edge_I'].tolist(), ref['edge_U'].tolist()))
+    assert sorted(map(tuple, e.tolist())) == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('W,edge_threshold', [(8, 10), (8, 3), (3, 10)])
+def test_position_split_skewed_genome_one_gpu_equals_oracle(W, edge_threshold):
+    """A genome with >= 50 % of the intervals on one chromosome through the product's
+    SweepShard(split='position') at W ranks (threads on one GPU): the ranges tile the sorted positions
+    and split that chromosome, the ranks' edges partition the oracle's (capped at 3: the replay's hit
+    lists come from the chromosome split), every rank has the oracle's components; two steps each."""
+    from fslr_amd.prep import fold_overlap_threshold, pass_table
+    w = np.ones(len(synth.CHROMS))
+    w[0] = len(synth.CHROMS) * 1.2
+    s = synth.generate(150_000, 16, 53, chrom_weights=w)
+    csr = s.interval_data().csr()
+    counts = np.bincount(csr.iv_chrom, minlength=csr.n_chroms)
+    assert counts.max() >= 0.5 * counts.sum()
+    thr_iv = fold_overlap_threshold(csr.iv_aln, 0.8)
+    pt = pass_table([1, 1, 0.66, 0.66, 0.66, 0.5])
+    o = O.run_core(_oracle_csr(csr), edge_threshold=edge_threshold, use_cap=True)
+    ctxs, infos = _sweep_shards_threads(csr, thr_iv, pt, W, edge_threshold, steps=2, split='position')
+    try:
+        pos = [i['pos'] for i in infos]
+        assert pos[0][0] == 0 and pos[-1][1] == csr.n_intervals
+        assert all(a[1] == b[0] for a, b in zip(pos, pos[1:]))
+        h = int(np.argmax(counts))                # the heavy chromosome's sorted positions [big0, big1)
+        big0 = int(counts[:h].sum())
+        big1 = big0 + int(counts[h])
+        assert sum(1 for lo, hi, _ in pos if lo < big1 and hi > big0) >= 2, pos
+        want = sorted(zip(o['edge_a'].tolist(), o['edge_b'].tolist(), o['edge_I'].tolist(), o['edge_U'].tolist()))
+        a, b, I, U, fwd = _union_view(ctxs)
+        assert sorted(zip(a.tolist(), b.tolist(), I.tolist(), U.tolist())) == want
+        np.testing.assert_array_equal(fwd, o['fwd'])
+        for c in ctxs:
+            np.testing.assert_array_equal(_components_from_labels(c.labels()), o['comp'])
+    finally:
+        for c in ctxs:
+            c.close()
+
+
+def _pair_shards_threads(csr, thr, pt, W, edge_threshold, long_reads=False, cutoffs=None):
+    """dist.PairShard (the query-shard split) on W ranks as threads of this process, each with its own
+    context and stream on cuda:0 and the full index."""
+    import threading
+    import torch
+    from fslr_amd import _lib
+    from fslr_amd.dist import LocalHub, PairShard
+    from fslr_amd.prep import FSLR_THR_ZERO_ALN, umax_table
+    dev = torch.device('cuda', 0)
+    hub = LocalHub(W)
+    ctxs, shards, infos, errs = [None] * W, [None] * W, [None] * W, [None] * W
+
+    def run(r):
+        try:
+            s = torch.cuda.Stream(dev)
+            torch.cuda.set_stream(s)
+            c = _lib.Context(0, stream=s.cuda_stream)
+            ctxs[r] = c
+            if long_reads:
+                c.load_csr_any(csr, np.where(np.asarray(csr.iv_aln) == 0, FSLR_THR_ZERO_ALN, 0))
+                c.set_thresholds(thr)
+                c.set_long_cutoffs(umax_table(cutoffs, int(np.diff(csr.read_off).max())))
+            else:
+                c.load_csr(csr, thr)
+            c.reserve_edges(max(1 << 16, 12 * csr.n_reads))
+            c.build_index()
+            sh = shards[r] = PairShard(c, csr.n_reads, W, r, dev, comm=hub.comm(r, dev), long_reads=long_reads)
+            infos[r] = sh.step(1 - 0.04, 1 - 0.25, pt, edge_threshold)
+            torch.cuda.synchronize(dev)
+        except BaseException as e:                     # noqa: BLE001 - re-raised by the caller
+            errs[r] = e
+            hub.barrier.abort()
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in range(W)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for e in errs:
+        if e is not None and not isinstance(e, threading.BrokenBarrierError):
+            raise e
+    for e in errs:
+        if e is not None:
+            raise e
+    return ctxs, shards, infos
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('case,W,edge_threshold', [('overlap0', 3, 10), ('overlap0', 2, 3), ('long', 3, 10),
+                                                   ('long', 2, 3)])
+def test_pair_shard_split_equals_oracle(case, W, edge_threshold):
+    """The query-shard split (dist.PairShard) for the inputs the sweep split does not take — overlap 0
+    (the walk engine's general thresholds) and reads of up to 150 intervals (the general evaluator,
+    fslr_long_pairs_shard) — at W ranks (threads on one GPU):
+    the ranks' parts of the edges and forward degrees add up to the oracle's graph (capped at 3: every
+    rank replays the loops over the gathered E*), every rank has the oracle's components."""
+    from fslr_amd.prep import fold_overlap_threshold, pass_table
+    cut = [1, 1, 0.66, 0.66, 0.66, 0.5]
+    overlap = 0.0 if case == 'overlap0' else 0.8
+    if case == 'long':
+        s = synth.generate(900, 150, 21, lmin=1)
+    else:
+        s = synth.generate(6000, 8, 29)
+    csr = s.interval_data().csr()
+    thr_iv = fold_overlap_threshold(csr.iv_aln, overlap)
+    o = O.run_core(_oracle_csr(csr), overlap=overlap, edge_threshold=edge_threshold, use_cap=True)
+    ctxs, shards, infos = _pair_shards_threads(csr, thr_iv, pass_table(cut), W, edge_threshold,
+                                               long_reads=case == 'long', cutoffs=cut)
+    try:
+        assert all(i['path'] == ('long' if case == 'long' else 'walk') for i in infos)
+        if edge_threshold == 3:
+            assert all(i['capped'] for i in infos)
+        a = np.concatenate([sh.edges_out[0] for sh in shards])
+        b = np.concatenate([sh.edges_out[1] for sh in shards])
+        I = np.concatenate([sh.edges_out[2] for sh in shards])
+        U = np.concatenate([sh.edges_out[3] for sh in shards])
+        want = sorted(zip(o['edge_a'].tolist(), o['edge_b'].tolist(), o['edge_I'].tolist(), o['edge_U'].tolist()))
+        assert sorted(zip(a.tolist(), b.tolist(), I.tolist(), U.tolist())) == want
+        np.testing.assert_array_equal(np.sum([sh.fwd_out.astype(np.int64) for sh in shards], axis=0), o['fwd'])
+        for sh in shards:
+            np.testing.assert_array_equal(_components_from_labels(sh.labels()), o['comp'])
+    finally:
+        for c in ctxs:
+            if c is not None:
+                c.close()

@@ -151,9 +151,16 @@ def test_cli_multi_gpu_matches_reference_outputs(name):
     empty graph and the one-GPU fallback for overlap <= 0 (edge_cases_p0), 115 chromosomes (more than
     the device chromosome filter's 64-bit mask held before round 3), long reads with the cap binding
     (longcap_240, one GPU)."""
+    from fslr_amd import multi
     meta = fx.meta(name)
+    multi.last_path = None
     with tempfile.TemporaryDirectory() as tmp:
         res = run_product_cli(name, tmp, '--gpus=2')
+        # every input takes a two-rank split (no one-GPU fallback): the sweep split, or the query-shard
+        # split for overlap <= 0 (edge_cases_p0), aln_size == 0 (zerodiv) and long reads
+        want_path = {'edge_cases_p0': 'walk', 'zerodiv': 'walk', 'longreads_400': 'long', 'longcap_240': 'long',
+                     'zdcap_skip_long': 'long', 'zdcap_raise_long': 'long'}.get(name, 'sweep-chrom')
+        assert multi.last_path == want_path, (name, multi.last_path)
         if meta['exception']:
             assert isinstance(res.exception, ZeroDivisionError), (res.output, res.exception)
             return
