@@ -1,0 +1,51 @@
+#!/bin/bash
+# One GPU call on the tree's sources (gpurun -- bash tools/gpu_check.sh TAG [STEPS]): STEPS is a comma list
+# of tests (the whole GPU suite), smoke, bench (the default bench line), prof (rocprofv3 kernel table of a
+# short bench), cli10m (the 10M-read cfg5 CLI, native I/O, stage table), pmc (HBM traffic passes).
+# Every step runs under its own time limit; the first failure ends the call.
+set -o pipefail
+TAG=${1:-chk}
+STEPS=${2:-tests,smoke,bench,prof}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+cd $R
+( while sleep 50; do echo "tick $(date +%T)"; done ) &
+TICK=$!
+trap "kill $TICK" EXIT
+has() { [[ ",$STEPS," == *",$1,"* ]]; }
+if has tests; then
+  timeout -k 10 900 python -u -m pytest tests/ -x -q --timeout 300 --timeout-method thread -m gpu > $O/pytest_gpu.log 2>&1 \
+      || { echo "gpu tests failed"; tail -40 $O/pytest_gpu.log; exit 1; }
+  tail -2 $O/pytest_gpu.log
+fi
+if has smoke; then
+  timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+  tail -1 $O/smoke.log
+fi
+if has bench; then
+  timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.log || { tail -20 $O/bench.log; exit 1; }
+  python3 -c "import json; d=json.load(open('$O/bench.json')); r=d['roofline']; print('value %.4e ms/step %.4f cold %s kernel %s %.4f ms frac %.3f' % (d['value'], d['ms_per_step'], d['config'].get('cold_step_ms'), r['kernel'], r['kernel_ms'], r['frac']), r.get('phase_ms_last_step'))"
+fi
+if has prof; then
+  ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv \
+      -- python3 $R/bench.py --steps 10 --warmup 2 --cpu-sample-stride 0 > $O/prof.log 2>&1 ) || { echo "rocprof failed"; tail -5 $O/prof.log; exit 1; }
+  f=$(find $O/prof -name 'run_kernel_stats.csv' | head -1); cp $f $O/kernel_stats.csv
+  python3 - $O/kernel_stats.csv <<'PY'
+import csv, re, sys
+for r in list(csv.DictReader(open(sys.argv[1])))[:14]:
+    n = re.sub(r'^void ', '', r['Name'].replace('(anonymous namespace)::', '')); i = n.find('('); n = n[:i] if i > 0 else n
+    print(f"   {float(r['AverageNs'])/1000:9.1f} us  x{r['Calls']:>4}  {n[:80]}")
+PY
+fi
+if has cli10m; then
+  export TMPDIR=${TMPDIR:-/tmp}
+  timeout -k 10 600 python3 -u tools/cli_io_timing.py 10000000 64 13 $O/cli_10m.json zipf --native-io > $O/cli_10m.log 2>&1 \
+      || { echo "cli10m failed"; tail -20 $O/cli_10m.log; exit 1; }
+  tail -3 $O/cli_10m.log
+fi
+if has pmc; then
+  OUT=gpurun_out/$TAG/pmc timeout -k 10 900 bash tools/pmc.sh > $O/pmc.log 2>&1 || { echo "pmc failed"; tail -20 $O/pmc.log; exit 1; }
+  tail -5 $O/pmc.log
+fi
+echo done

@@ -4,7 +4,7 @@
 set -e
 OUT=${OUT:-gpurun_out/pmc}
 ENGINE=${ENGINE:-sweep}
-if [ "$ENGINE" = walk ]; then KREGEX="query_kernel"; KNAMES="query_kernel<0, false>"; else KREGEX="k_sweep<2>|k_sweep_pairs|k_bucket_pairs"; KNAMES="k_sweep<2>;k_sweep_pairs"; fi
+if [ "$ENGINE" = walk ]; then KREGEX="query_kernel"; KNAMES="query_kernel<0, false>"; else KREGEX="k_sweep<2>|k_sweep_pairs"; KNAMES="k_sweep<2>;k_sweep_pairs"; fi
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $ROOT/$OUT
 cd /tmp && export TMPDIR=/tmp
