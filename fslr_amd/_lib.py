@@ -13,7 +13,7 @@ import numpy as np
 
 LIB_PATH = os.environ.get('FSLR_LIB') or os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libfslr_hip.so')
 
-ABI_VERSION = 18         # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
+ABI_VERSION = 19         # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
 FSLR_OK, FSLR_ERR_ZERO_DIVISION, FSLR_ERR_INVALID, FSLR_ERR_HIP, FSLR_ERR_NOMEM, FSLR_ERR_STATE = range(6)
 FSLR_MAX_L = 64
 FSLR_MAX_READS = 1 << 25
@@ -42,7 +42,8 @@ EXPORTED = ['fslr_abi_version', 'fslr_last_error', 'fslr_ctx_create', 'fslr_ctx_
             'fslr_local_forest', 'fslr_copy_forest_pairs', 'fslr_sort_edges', 'fslr_cap_bwd_counts',
             'fslr_cap_restrict', 'fslr_cap_copy_restricted', 'fslr_cap_install_restricted', 'fslr_rows_upload',
             'fslr_set_reads_rows', 'fslr_get_read_codes', 'fslr_get_csr', 'fslr_fold_thresholds',
-            'fslr_position_costs', 'fslr_set_position_filter', 'fslr_use_position_filter', 'fslr_long_pairs_shard']
+            'fslr_position_costs', 'fslr_set_position_filter', 'fslr_use_position_filter', 'fslr_long_pairs_shard',
+            'fslr_edge_cap_deferred', 'fslr_edge_cap_deferred_read']
 
 
 class HipUnavailable(RuntimeError):
@@ -199,6 +200,8 @@ def load(path: str = LIB_PATH):
         'fslr_set_position_filter': (ctypes.c_int, [vp, i64, i64, i64]),
         'fslr_use_position_filter': (ctypes.c_int, [vp]),
         'fslr_long_pairs_shard': (ctypes.c_int, [vp, ctypes.POINTER(Params), i32, i32, ctypes.POINTER(ctypes.c_int64)]),
+        'fslr_edge_cap_deferred': (ctypes.c_int, [vp, i32]),
+        'fslr_edge_cap_deferred_read': (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int32)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -518,6 +521,16 @@ class Context:
         cs = CapStats()
         self._check(self._L.fslr_apply_edge_cap(self._h, int(edge_threshold), ctypes.byref(cs)))
         return cs.as_dict()
+
+    def edge_cap_deferred(self, edge_threshold=10):
+        """The edge-cap check of a repeated query without a host round trip (fslr_edge_cap_deferred)."""
+        self._check(self._L.fslr_edge_cap_deferred(self._h, int(edge_threshold)))
+
+    def edge_cap_deferred_read(self) -> int:
+        """Sync; the deferred checks' sticky word (1: the cap bound, 2: a ZeroDivisionError pair), cleared."""
+        f = ctypes.c_int32()
+        self._check(self._L.fslr_edge_cap_deferred_read(self._h, ctypes.byref(f)))
+        return int(f.value)
 
     # -- multi-GPU edge cap (fslr_hip.h fslr_cap_*) ------------------------------------------------
     def edges_iu_into(self, t, n_pad: int):

@@ -675,6 +675,42 @@ int fslr_fold_thresholds(fslr_ctx* c, double overlap) {
   return FSLR_OK;
 }
 
+}  // extern "C"
+
+// the deferred edge-cap check: sticky host word 8 |= (max forward degree > thr) | (a listed
+// ZeroDivisionError pair) << 1 — a repeat step that must not wait for the host (fslr_edge_cap_deferred)
+__global__ void k_cap_sticky(const int* err, int thr, long long* sticky) {
+  if (threadIdx.x == 0) {
+    const long long f = (err[3] > thr ? 1 : 0) | (err[kErrZdCount] > 0 ? 2 : 0);
+    if (f) *sticky |= f;
+  }
+}
+
+extern "C" {
+
+int fslr_edge_cap_deferred(fslr_ctx* c, int32_t thr) {
+  if (!c) return FSLR_ERR_INVALID;
+  if (!c->counters) return fail(c, FSLR_ERR_STATE, "no query has run");
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (!c->sw_total) {
+    HIP_TRY(c, hipHostMalloc(reinterpret_cast<void**>(&c->sw_total), 16 * sizeof(long long), hipHostMallocMapped));
+    HIP_TRY(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->sw_total_dev), c->sw_total, 0));
+    c->sw_total[8] = 0;
+  }
+  k_cap_sticky<<<1, 64, 0, c->stream>>>(c->errw, thr, c->sw_total_dev + 8);
+  HIP_TRY(c, hipGetLastError());
+  return FSLR_OK;
+}
+
+int fslr_edge_cap_deferred_read(fslr_ctx* c, int32_t* flags) {
+  if (!c || !flags) return FSLR_ERR_INVALID;
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  *flags = c->sw_total ? static_cast<int32_t>(c->sw_total[8]) : 0;
+  if (c->sw_total) c->sw_total[8] = 0;
+  return FSLR_OK;
+}
+
 int fslr_reserve_edges(fslr_ctx* c, int64_t capacity) {
   if (!c || capacity < 0) return FSLR_ERR_INVALID;
   HIP_TRY(c, hipSetDevice(c->device));
@@ -749,7 +785,7 @@ __global__ void k_peek(const unsigned long long* counters, const int* err, long 
 
 int fslr::peek_counts(fslr_ctx* c, long long out[4]) {
   if (!c->sw_total) {
-    HIP_TRY(c, hipHostMalloc(reinterpret_cast<void**>(&c->sw_total), 8 * sizeof(long long), hipHostMallocMapped));
+    HIP_TRY(c, hipHostMalloc(reinterpret_cast<void**>(&c->sw_total), 16 * sizeof(long long), hipHostMallocMapped));
     HIP_TRY(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->sw_total_dev), c->sw_total, 0));
   }
   k_peek<<<1, 64, 0, c->stream>>>(c->counters, c->errw, c->sw_total_dev + 4);
@@ -863,7 +899,7 @@ static int sweep_front(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64
     c->ent_cap = 0;                                  // re-size the scan scratch with the entries
   }
   if (!c->sw_total) {
-    HIP_TRY(c, hipHostMalloc(reinterpret_cast<void**>(&c->sw_total), 8 * sizeof(long long), hipHostMallocMapped));
+    HIP_TRY(c, hipHostMalloc(reinterpret_cast<void**>(&c->sw_total), 16 * sizeof(long long), hipHostMallocMapped));
     HIP_TRY(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&c->sw_total_dev), c->sw_total, 0));
   }
   if (!c->sw_wstat) {

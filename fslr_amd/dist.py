@@ -745,6 +745,7 @@ class PairShard(SweepShard):
         self.world, self.rank = int(world), int(rank)
         self.device = torch.device(device)
         self.long = bool(long_reads)
+        self.split = 'query'
         self.esend = torch.empty(1 << 12, dtype=torch.int64, device=self.device)
         self.egath = torch.empty(1 << 12, dtype=torch.int64, device=self.device)
         self._labels = None

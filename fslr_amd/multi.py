@@ -170,7 +170,7 @@ class _Rank:
                     fwd = ctx.fwd_degree()
                 return {'labels': labels, 'edges': (a, b, I, U), 'fwd': fwd, 'capped': bool(info['capped']),
                         'max_fwd': int(info['max_fwd']), 'cap': info.get('cap', {}), 'backend': self.backend,
-                        'path': info.get('path', 'sweep-' + shard.split if isinstance(shard, SweepShard) else 'sweep')}
+                        'path': info['path'] if 'path' in info else 'sweep-' + shard.split}
             except BaseException:
                 self.ctx.close()                      # a failed query leaves no half-set context behind
                 self.ctx = None

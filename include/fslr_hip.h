@@ -75,7 +75,7 @@
 extern "C" {
 #endif
 
-#define FSLR_ABI_VERSION 18
+#define FSLR_ABI_VERSION 19
 #define FSLR_MAX_L 64                /* max intervals per read (bitmask width) */
 #define FSLR_MAX_READS (1 << 25)     /* read rank packs into bits 6..30 of the index record */
 #define FSLR_THR_ZERO_ALN INT32_MIN
@@ -281,6 +281,12 @@ int  fslr_query_shard(fslr_ctx *ctx, const fslr_params *params, int32_t shard, i
  * different components of the candidates' partner graph are independent.
  * Call between fslr_query and fslr_components.  Syncs; out may be NULL. */
 int  fslr_apply_edge_cap(fslr_ctx *ctx, int32_t edge_threshold, fslr_cap_stats *out);
+/* The same check without a host round trip, for a repeated query on unchanged input: the device ORs
+ * (max forward degree > edge_threshold) | (a listed ZeroDivisionError pair) << 1 into a sticky word (async);
+ * fslr_edge_cap_deferred_read syncs, returns the word and clears it.  A nonzero word means a step needed
+ * fslr_apply_edge_cap (or raised): its results are to be recomputed synchronously. */
+int  fslr_edge_cap_deferred(fslr_ctx *ctx, int32_t edge_threshold);
+int  fslr_edge_cap_deferred_read(fslr_ctx *ctx, int32_t *flags);
 /* cluster.py:230-234 — union-find over the edges: label = min rank in component.  Async. */
 int  fslr_components(fslr_ctx *ctx);
 /* Multi-GPU sweep.  A rank indexes only the chromosomes it owns, sweeps them and
