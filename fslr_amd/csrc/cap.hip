@@ -2702,8 +2702,9 @@ extern "C" int fslr_long_pairs_shard(fslr_ctx* c, const fslr_params* p, int32_t 
   w->nseq = w->nloc;
   if (int rc = cap_slots(c, w)) return rc;
   const int ns = static_cast<int>(w->ns);
-  // every pair is in both reads' slots: at most ns / 2 edges
-  const int64_t need = std::max<int64_t>(ns / 2 + 1, 1024);
+  // every pair is in both reads' slots: at most ns / 2 edges (a shard's slots: a pair's other read may
+  // lie outside it, at most ns)
+  const int64_t need = std::max<int64_t>((n_shards > 1 ? ns : ns / 2) + 1, 1024);
   if (need > c->lg_edge_cap) {
     if (dalloc(c, &c->lg_edges, need)) return FSLR_ERR_NOMEM;
     c->lg_edge_cap = need;
@@ -2725,6 +2726,8 @@ extern "C" int fslr_long_pairs_shard(fslr_ctx* c, const fslr_params* p, int32_t 
   HIP_TRY(c, hipMemcpyAsync(c->counters + kEdgeCount, &cnt, sizeof(cnt), hipMemcpyHostToDevice, s));
   HIP_TRY(c, hipStreamSynchronize(s));
   w->prepared = false;
+  if (static_cast<int64_t>(cnt) > c->lg_edge_cap || static_cast<int64_t>(cnt) > c->edge_cap)
+    return fail(c, FSLR_ERR_STATE, "long-pair edge list overflowed");
   c->lg_n_edges = static_cast<int64_t>(cnt);
   c->last_engine = FSLR_ENGINE_WALK;
   *n_edges = c->lg_n_edges;

@@ -750,6 +750,11 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
       if (A0) gend = __builtin_ctzll(A0);
       else if (A1) gend = kWave + __builtin_ctzll(A1);
       else gend = last_done ? lim : h_top;
+#ifdef FSLR_PAIRS_HIST
+      // measurement build: groups by size (8-entry bins, counters 48..63), long runs (42), the groups'
+      // read pairs (43) and runs (44)
+      if (lane == 0) atomicAdd(gend ? &g.counters[kSecBase + ((gend - 1) >> 3)] : &g.counters[42], 1ull);
+#endif
       if (gend == 0) {
         // the run at s does not fit the stage: alone
         const long long re = next_run(s + lim, n, entry_a(__shfl(e0, 0)));
@@ -793,6 +798,13 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
       if (sn < c1) load_window(sn, n0, n1, nn);
       const unsigned long long S0 = __ballot(s0), S1 = __ballot(s1);
       const int ns0 = __popcll(S0), nseg = ns0 + __popcll(S1);
+#ifdef FSLR_PAIRS_HIST
+      if (lane == 0) {
+        atomicAdd(&g.counters[43], static_cast<unsigned long long>(nseg));
+        atomicAdd(&g.counters[44], static_cast<unsigned long long>(__popcll(H0 & (gend >= kWave ? ~0ull : (1ull << gend) - 1)) +
+                                                                  __popcll(H1 & (gend <= kWave ? 0ull : gend >= 2 * kWave ? ~0ull : (1ull << (gend - kWave)) - 1))));
+      }
+#endif
       const int g0 = __popcll(S0 & upto(lane)) - 1;
       const int g1 = ns0 + __popcll(S1 & upto(lane)) - 1;
       wave_lds_sync();                                             // the previous group's reads are done
