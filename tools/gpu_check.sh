@@ -15,7 +15,7 @@ TICK=$!
 trap "kill $TICK" EXIT
 has() { [[ ",$STEPS," == *",$1,"* ]]; }
 if has tests; then
-  timeout -k 10 900 python -u -m pytest tests/ -x -q --timeout 300 --timeout-method thread -m gpu > $O/pytest_gpu.log 2>&1 \
+  timeout -k 10 900 python -u -m pytest tests/ --maxfail=5 -q --timeout 300 --timeout-method thread -m gpu > $O/pytest_gpu.log 2>&1 \
       || { echo "gpu tests failed"; tail -40 $O/pytest_gpu.log; exit 1; }
   tail -2 $O/pytest_gpu.log
 fi
@@ -43,6 +43,11 @@ if has cli10m; then
   timeout -k 10 600 python3 -u tools/cli_io_timing.py 10000000 64 13 $O/cli_10m.json zipf --native-io > $O/cli_10m.log 2>&1 \
       || { echo "cli10m failed"; tail -20 $O/cli_10m.log; exit 1; }
   tail -3 $O/cli_10m.log
+fi
+if has hist; then
+  FSLR_LIB=$R/fslr_amd/libfslr_hip_hist.so FSLR_ALLOW_STALE=1 timeout -k 10 300 python3 tools/pairs_hist.py $O/pairs_group_hist.json \
+      > $O/hist.log 2>&1 || { echo "hist failed"; tail -20 $O/hist.log; exit 1; }
+  tail -30 $O/hist.log
 fi
 if has pmc; then
   OUT=gpurun_out/$TAG/pmc timeout -k 10 900 bash tools/pmc.sh > $O/pmc.log 2>&1 || { echo "pmc failed"; tail -20 $O/pmc.log; exit 1; }
