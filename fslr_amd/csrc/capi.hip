@@ -880,7 +880,7 @@ int fslr_query_shard(fslr_ctx* c, const fslr_params* p, int32_t shard, int32_t n
 // input); an upper bound beyond the budget (half the free HBM, at least 8 GB) takes the two-pass
 // fallback (count, then emit: the sweep runs twice).
 static int sweep_front(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_t a_end, hipEvent_t e0,
-                       hipEvent_t e1, SweepArgs& s, int& mode, bool defer = false) {
+                       hipEvent_t e1, SweepArgs& s, int& mode, bool defer = false, bool coarse = false) {
   // upper-bound slots (8 B each) the one-pass sweep may use: half the free HBM, at least 2^30; asked
   // only when the slot buffer has to grow (hipMemGetInfo is a driver round trip, kept off repeat queries)
   auto ub_budget = []() {
@@ -945,6 +945,8 @@ static int sweep_front(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64
   s.ent_cap = c->ent_cap;
   for (int k = 0; k < 5; ++k) s.ev[k] = c->prof_phases ? c->sw_ev[k] : nullptr;
   s.ev[0] = nullptr;                                // recorded here, around the sweep pass
+  s.hist_mat = nullptr;
+  if (coarse) sweep_coarse_hist(s);                  // the sweep counts the grouping's coarse buckets
   // the gate ranges depend on the reads and the two cuts only: a repeat query keeps them
   if (c->lb_gen != c->input_gen || c->lb_q != p->qlen_cut || c->lb_n != p->nal_cut) {
     HIP_TRY(c, launch_len_bounds(c->rmeta, 0, static_cast<int>(c->n), p->qlen_cut, p->nal_cut, c->lbounds, c->stream));
@@ -1021,9 +1023,9 @@ static int sweep_front(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64
 
 static int sweep_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_t a_end, hipEvent_t e0,
                       hipEvent_t e1) {
-  SweepArgs s;
+  SweepArgs s{};
   int mode = 2;
-  int rc = sweep_front(c, p, a_begin, a_end, e0, e1, s, mode);
+  int rc = sweep_front(c, p, a_begin, a_end, e0, e1, s, mode, false, true);
   if (rc) return rc;
   if (e0) {                                          // profiling: the pair-stage kernel's ring too
     const int slot = static_cast<int>(c->n_kern2++ % fslr_ctx::kKernRing);
@@ -1339,7 +1341,7 @@ int fslr_sweep_partition(fslr_ctx* c, const fslr_params* p, int32_t n_dest, int3
     k0 = c->kev[2 * slot];
     k1 = c->kev[2 * slot + 1];
   }
-  SweepArgs s;
+  SweepArgs s{};
   int mode = 2;
   if (int rc = sweep_front(c, p, 0, c->n, k0, k1, s, mode, true)) return rc;
   HIP_TRY(c, launch_sweep_partition(s, 2, block_shift, n_dest, out, dst_cap, totals, c->stream));
@@ -1401,7 +1403,7 @@ int fslr_sweep_partition_repeat(fslr_ctx* c, const fslr_params* p, int32_t n_des
     k0 = c->kev[2 * slot];
     k1 = c->kev[2 * slot + 1];
   }
-  SweepArgs s;
+  SweepArgs s{};
   int mode = 2;
   if (int rc = sweep_front(c, p, 0, c->n, k0, k1, s, mode, true)) return rc;
   HIP_TRY(c, launch_sweep_partition(s, 2, block_shift, n_dest, static_cast<unsigned long long*>(dst), dst_cap,

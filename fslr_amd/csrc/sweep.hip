@@ -77,6 +77,30 @@ constexpr int kRingMask = kRing - 1;
 constexpr int kMapCap = 1024;              // items per map segment (a longer tile takes several)
 constexpr int kTileRun = 8;                // consecutive tiles per work item
 
+// One wave-instruction of keys (lanes with `act`, a contiguous prefix): equal keys on adjacent lanes
+// form runs; the run's first lane adds its length to bin[key] (returning the base when `ret`), every
+// lane gets base + its offset in the run.
+template <bool kRet>
+__device__ __forceinline__ int run_add(int* bin, int key, bool act, int lane) {
+  const int prev = __shfl_up(key, 1);
+  const bool head = act && (lane == 0 || prev != key);
+  const unsigned long long hm = __ballot(head);
+  const unsigned long long am = __ballot(act);
+  const int n_act = __popcll(am);
+  int base = 0;
+  if (head) {
+    const unsigned long long nx = hm & above(lane);
+    const int len = (nx ? __builtin_ctzll(nx) : n_act) - lane;
+    if (kRet) base = atomicAdd(&bin[key], len);
+    else atomicAdd(&bin[key], len);
+  }
+  if (!kRet) return 0;
+  const int my_head = 63 - __builtin_clzll(hm & upto(lane));   // lane 0 is a head when active
+  return __shfl(base, act ? my_head : 0) + (lane - my_head);
+}
+
+constexpr int kHistMax = 1024;             // coarse A buckets the one-pass sweep counts (LDS)
+
 // kMode 0: count the tile's entries (two-pass fallback), 1: write them at the tile's scanned offset
 // (two-pass fallback), 2: one pass — write them at the tile's upper-bound slot (its forward-range
 // total, the pair tests) and count them; k_compact then packs the tiles.
@@ -91,9 +115,15 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
   __shared__ unsigned char zf_all[kSwWaves][kWave];   // q's read has qlen2 == 0 (1) / n_alignments == 0 (2)
   __shared__ unsigned short map_all[kSwWaves][kMapCap];   // item -> lane | min(p - q0, kRing) << 6
   __shared__ unsigned long long st_all[kSwWaves][kEmit ? kWave : 1];
+  __shared__ int hist_s[kMode == 2 ? kHistMax : 1];   // the block's entries per coarse A bucket
   unsigned long long* const dst = kMode == 2 ? g.ent_ub : g.ent;
   const int lane = lane_id();
   const int wv = threadIdx.x >> 6;
+  const bool do_hist = kMode == 2 && g.hist_mat != nullptr;
+  if (do_hist) {
+    for (int i = threadIdx.x; i < g.hist_h; i += kSwBlock) hist_s[i] = 0;
+    __syncthreads();
+  }
   int4* RR = rr_all[wv];
   int2* RG = rg_all[wv];
   int4* QB = qb_all[wv];
@@ -161,6 +191,15 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
       }
     }
     int sn = 0, cnt = 0;                         // staged entries (kEmit) / entries of the tile
+    // the staged entries to their slots (and, counting coarse buckets, into the block's histogram:
+    // equal buckets on adjacent lanes take one LDS atomic)
+    auto flush = [&]() __attribute__((always_inline)) {
+      wave_lds_sync();
+      const bool act = lane < sn;
+      const unsigned long long v = act ? ST[lane] : 0ull;
+      if (act) dst[out + lane] = v;
+      if (do_hist) run_add<false>(hist_s, static_cast<int>(static_cast<unsigned>(v >> 39) >> g.hist_lo), act, lane);
+    };
     if constexpr (kCount) w_tests += static_cast<unsigned long long>(T);
     for (int seg = 0; seg < T; seg += kMapCap) {
       const int se = min(T, seg + kMapCap);
@@ -222,8 +261,7 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
         }
         if (kEmit && ne) {
           if (sn + ne > kWave) {
-            wave_lds_sync();
-            if (lane < sn) dst[out + lane] = ST[lane];
+            flush();
             out += sn;
             sn = 0;
             wave_lds_sync();
@@ -266,10 +304,7 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
       else run_steps(std::false_type{});
     }
     if constexpr (kEmit) {
-      if (sn > 0) {
-        wave_lds_sync();
-        if (lane < sn) dst[out + lane] = ST[lane];
-      }
+      if (sn > 0) flush();
     }
     if constexpr (kCount) {
       if (lane == 0) g.tile_cnt[tile] = cnt;
@@ -280,6 +315,11 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
     // statistics: plain stores into this wave's slots, summed by k_sweep_total / k_sum_slots
     const unsigned long long f = lane == 0 ? w_tests : lane == 1 ? w_hits : w_ent;
     if (lane < 3) g.wstat[static_cast<long long>(wid) * kWsFields + lane] = f;
+  }
+  if (do_hist) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < g.hist_h; i += kSwBlock)
+      g.hist_mat[static_cast<long long>(i) * gridDim.x + blockIdx.x] = hist_s[i];
   }
 }
 
@@ -467,37 +507,9 @@ __device__ __forceinline__ unsigned long long bitonic_cx(unsigned long long v, b
   return keep_min == (v < o) ? v : o;
 }
 
-// merge steps of one bitonic stage, strides ST .. 1 (size = the stage's sequence length; size 128 =
-// the final merge, all ascending)
-template <int SIZE, int ST>
-__device__ __forceinline__ void bitonic_steps(unsigned long long& a, unsigned long long& b, int lane) {
-  if constexpr (ST >= 1) {
-    const bool lower = (lane & ST) == 0;
-    const bool asc_a = SIZE == 2 * kWave || (lane & SIZE) == 0;
-    const bool asc_b = SIZE == 2 * kWave || ((lane + kWave) & SIZE) == 0;
-    a = bitonic_cx<ST>(a, lower == asc_a, lane);
-    b = bitonic_cx<ST>(b, lower == asc_b, lane);
-    bitonic_steps<SIZE, ST / 2>(a, b, lane);
-  }
-}
-
-// ascending sort of the 128 keys {a at element lane, b at element lane + 64}
-__device__ __forceinline__ void bitonic128(unsigned long long& a, unsigned long long& b, int lane) {
-  bitonic_steps<2, 1>(a, b, lane);
-  bitonic_steps<4, 2>(a, b, lane);
-  bitonic_steps<8, 4>(a, b, lane);
-  bitonic_steps<16, 8>(a, b, lane);
-  bitonic_steps<32, 16>(a, b, lane);
-  bitonic_steps<64, 32>(a, b, lane);
-  const unsigned long long lo = a < b ? a : b, hi = a < b ? b : a;   // the 128-merge: stride 64 in-lane
-  a = lo;
-  b = hi;
-  bitonic_steps<2 * kWave, 32>(a, b, lane);
-}
-
-// The same sort with element e = lane << 1 | slot (a: slot 0, b: slot 1): index bit 0 is in-lane (7
-// of the 28 stages exchange nothing), bits 1-4 are DPP lane exchanges and only bits 5 and 6 cross 16
-// lanes (3 LDS-permute stages instead of 5).  The network is a chain of 28 dependent stages, and a
+// Bitonic sort of up to 128 keys, two per lane, element e = lane << 1 | slot (a: slot 0, b: slot 1):
+// index bit 0 is in-lane (7 of the 28 stages exchange nothing), bits 1-4 are DPP lane exchanges and
+// only bits 5 and 6 cross 16 lanes (3 LDS-permute stages instead of 5 with e = lane | slot << 6).  The network is a chain of 28 dependent stages, and a
 // permute through LDS is its slowest link.  Sorted element e ends at lane e >> 1, slot e & 1.
 template <int SIZE, int D>
 __device__ __forceinline__ void bitonic_il_steps(unsigned long long& a, unsigned long long& b, int lane) {
@@ -516,14 +528,18 @@ __device__ __forceinline__ void bitonic_il_steps(unsigned long long& a, unsigned
   }
 }
 
-__device__ __forceinline__ void bitonic128_il(unsigned long long& a, unsigned long long& b, int lane) {
+// ascending sort of N = 32, 64 or 128 elements in lanes [0, N / 2) (N < 128: lanes N / 2 .. 63 sort
+// their own copies, which the caller discards): log2(N) (log2(N) + 1) / 2 dependent stages — 15 for
+// 32 (all DPP), 21 for 64 (one ds_swizzle stride), 28 for 128 (three LDS permutes)
+template <int N>
+__device__ __forceinline__ void bitonic_il(unsigned long long& a, unsigned long long& b, int lane) {
   bitonic_il_steps<2, 1>(a, b, lane);
   bitonic_il_steps<4, 2>(a, b, lane);
   bitonic_il_steps<8, 4>(a, b, lane);
   bitonic_il_steps<16, 8>(a, b, lane);
   bitonic_il_steps<32, 16>(a, b, lane);
-  bitonic_il_steps<64, 32>(a, b, lane);
-  bitonic_il_steps<128, 64>(a, b, lane);
+  if constexpr (N >= 64) bitonic_il_steps<64, 32>(a, b, lane);
+  if constexpr (N >= 128) bitonic_il_steps<128, 64>(a, b, lane);
 }
 
 // group sort key: run (7 bits) << 39 | B << 14 | i << 7 | j; the segment key (run, B) is key >> 14
@@ -716,6 +732,15 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
     w1 = lane + kWave < lim ? E[s + kWave + lane] : ~0ull;
     wn = lane == 0 && s + lim < n ? E[s + lim] : ~0ull;
   };
+#ifdef FSLR_PAIRS_HIST
+  // measurement build: wave-clock sums per phase (counters 68..73: window and heads, sort, segment
+  // setup, segment evaluation, tail, long runs)
+  unsigned long long ck[6] = {0, 0, 0, 0, 0, 0};
+  long long tck = clock64();
+#define FSLR_PCK(k) do { const long long t_ = clock64(); ck[k] += t_ - tck; tck = t_; } while (0)
+#else
+#define FSLR_PCK(k) do { } while (0)
+#endif
   for (long long c = wid; c < nchunks; c += nw) {
     const long long c0 = c * kChunk2, c1 = min(c0 + kChunk2, n);
     long long s = c0;
@@ -755,10 +780,12 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
       // read pairs (43) and runs (44)
       if (lane == 0) atomicAdd(gend ? &g.counters[kSecBase + ((gend - 1) >> 3)] : &g.counters[42], 1ull);
 #endif
+      FSLR_PCK(0);
       if (gend == 0) {
         // the run at s does not fit the stage: alone
         const long long re = next_run(s + lim, n, entry_a(__shfl(e0, 0)));
         long_run(s, re);
+        FSLR_PCK(5);
         s = re;
         if (s < c1) load_window(s, e0, e1, en);
         continue;
@@ -773,7 +800,24 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
       if (hv1) la1 = RL[entry_a(e1)];
       unsigned long long k0 = v0 ? group_key(e0, r0) : ~0ull;
       unsigned long long k1 = v1 ? group_key(e1, r1) : ~0ull;
-      bitonic128_il(k0, k1, lane);
+      // the group's network: the smallest of 32 / 64 / 128 elements that holds it (a group of <= 64
+      // entries sits in k0; its upper half moves to lanes [0, 32) as the second slot)
+#ifdef FSLR_SORT128
+      if (true) {
+#else
+      if (gend > kWave) {
+#endif
+        bitonic_il<128>(k0, k1, lane);
+      } else if (gend > kWave / 2) {
+        k1 = __shfl(k0, (lane + kWave / 2) & (kWave - 1));
+        bitonic_il<64>(k0, k1, lane);
+        if (lane >= kWave / 2) k0 = k1 = ~0ull;
+      } else {
+        k1 = __shfl(k0, (lane + kWave / 4) & (kWave - 1));
+        bitonic_il<32>(k0, k1, lane);
+        if (lane >= kWave / 4) k0 = k1 = ~0ull;
+      }
+      FSLR_PCK(1);
       // back to position p at lane p (k0) / p - 64 (k1) through the group's key array
       wave_lds_sync();                                             // the previous group's reads are done
       reinterpret_cast<ulonglong2*>(SK)[lane] = make_ulonglong2(k0, k1);
@@ -837,6 +881,7 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
       wave_lds_sync();
       // the group's edges (at most one per segment) go out in one flush: each read's forward edges stay
       // one run of the edge list (the edge cap's replay walks those runs)
+      FSLR_PCK(2);
       if (es.n + nseg > kPairEdgeStage) es.flush(eo, lane);
       for (int k0s = 0; k0s < nseg; k0s += kWave) {
         const int p = k0s + lane;
@@ -875,6 +920,7 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
         if (edge) atomicAdd(&RUNF[r], 1);
         w_pairs += __popcll(__ballot(act));
       }
+      FSLR_PCK(3);
       wave_lds_sync();
       if (hv0) {
         const int f = RUNF[r0];
@@ -890,8 +936,14 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
       e0 = n0;
       e1 = n1;
       en = nn;
+      FSLR_PCK(4);
     }
   }
+#ifdef FSLR_PAIRS_HIST
+  if (lane == 0)
+    for (int k = 0; k < 6; ++k) atomicAdd(&g.counters[68 + k], ck[k]);
+#endif
+#undef FSLR_PCK
   if (es.n > 0) es.flush(eo, lane);
   // statistics: plain stores into this wave's slots (field 2: matched pairs, field 3: max fwd)
   for (int o = 32; o > 0; o >>= 1) w_maxfwd = max(w_maxfwd, __shfl_xor(w_maxfwd, o));
@@ -924,28 +976,6 @@ constexpr int kMsdMaxLo = 4096;            // in-bucket bins (LDS histogram of p
 constexpr int kGrpInts = 2 * (1 << 22);    // [bucket][block] counts and their scan (H P <= 2^22)
 
 constexpr int kMsdUnroll = FSLR_MSD_UNROLL;  // entries loaded per lane before their atomics
-
-// One wave-instruction of keys (lanes with `act`, a contiguous prefix): equal keys on adjacent lanes
-// form runs; the run's first lane adds its length to bin[key] (returning the base when `ret`), every
-// lane gets base + its offset in the run.
-template <bool kRet>
-__device__ __forceinline__ int run_add(int* bin, int key, bool act, int lane) {
-  const int prev = __shfl_up(key, 1);
-  const bool head = act && (lane == 0 || prev != key);
-  const unsigned long long hm = __ballot(head);
-  const unsigned long long am = __ballot(act);
-  const int n_act = __popcll(am);
-  int base = 0;
-  if (head) {
-    const unsigned long long nx = hm & above(lane);
-    const int len = (nx ? __builtin_ctzll(nx) : n_act) - lane;
-    if (kRet) base = atomicAdd(&bin[key], len);
-    else atomicAdd(&bin[key], len);
-  }
-  if (!kRet) return 0;
-  const int my_head = 63 - __builtin_clzll(hm & upto(lane));   // lane 0 is a head when active
-  return __shfl(base, act ? my_head : 0) + (lane - my_head);
-}
 
 // kTiles: entries of tile t at src[ub[t] .. ub[t] + cnt[t]) (slots at or beyond n, the buffer's size,
 // are not read: an overflowed sweep's result is discarded by the caller); else dense src[0, n) in
@@ -1060,13 +1090,16 @@ __global__ __launch_bounds__(kMsdThreads) void k_msd_pass1(const unsigned long l
   }
 }
 
-// one workgroup per bucket: group [off[b P], off[(b + 1) P]) by A >> hb into dst
+// one workgroup per bucket: group [off[b P], off[(b + 1) P]) by the low lo_bits of A into dst
+// (kBins >= 2^lo_bits LDS bins: 4096 for the counted grouping, 16384 for the sweep's coarse buckets
+// of an input beyond 2^22 reads)
+template <int kBins>
 __global__ __launch_bounds__(256) void k_msd_pass2(const unsigned long long* __restrict__ src, long long n_host,
                                                    const long long* __restrict__ n_dev,
                                                    const int* __restrict__ off, int P, int H, int hb, int lo_bits,
                                                    unsigned long long* __restrict__ dst) {
   const long long n = n_dev ? *n_dev : n_host;
-  __shared__ int hist[kMsdMaxLo];
+  __shared__ int hist[kBins];
   __shared__ int wsum[4];
   const int tid = threadIdx.x;
   const int lane = tid & (kWave - 1), w = tid >> 6;
@@ -1132,6 +1165,134 @@ __global__ __launch_bounds__(256) void k_msd_pass2(const unsigned long long* __r
       const bool act = a + q * kWave + lane < e;
       const int p = run_add<true>(hist, act ? key_of(v[q]) : 0, act, lane);
       if (act) dst[p] = v[q];
+    }
+  }
+}
+
+// k_msd_pass2 for the sweep's coarse buckets (~16K entries at 1M reads): 1024 threads, the first
+// kR x 1024 entries of the bucket held in registers between the histogram and the scatter (one HBM
+// read instead of two); the rest, if any, read twice.
+constexpr int kP2Threads = 1024;
+template <int kBins, int kR>
+__global__ __launch_bounds__(kP2Threads) void k_msd_pass2r(const unsigned long long* __restrict__ src, long long n_host,
+                                                           const long long* __restrict__ n_dev,
+                                                           const int* __restrict__ off, int P, int H, int lo_bits,
+                                                           unsigned long long* __restrict__ dst) {
+  const long long n = n_dev ? *n_dev : n_host;
+  __shared__ int hist[kBins];
+  __shared__ int wsum[kP2Threads / kWave];
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1), w = tid >> 6;
+  const int nb = 1 << lo_bits;
+  const int b = blockIdx.x;
+  const long long s = min(static_cast<long long>(off[static_cast<long long>(b) * P]), n);
+  const long long e = b + 1 < H ? min(static_cast<long long>(off[static_cast<long long>(b + 1) * P]), n) : n;
+  if (e - s <= 1) {
+    if (tid == 0 && e > s) dst[s] = src[s];
+    return;
+  }
+  for (int i = tid; i < nb; i += kP2Threads) hist[i] = 0;
+  const unsigned mask = static_cast<unsigned>(nb - 1);
+  auto key_of = [&](unsigned long long v) { return static_cast<int>(static_cast<unsigned>(v >> 39) & mask); };
+  unsigned long long v[kR];
+#pragma unroll
+  for (int q = 0; q < kR; ++q) {
+    const long long k = s + static_cast<long long>(q) * kP2Threads + tid;
+    v[q] = k < e ? src[k] : 0ull;
+  }
+  __syncthreads();
+  // a wave's lanes hold consecutive entries: a run of one read adds with one atomic
+#pragma unroll
+  for (int q = 0; q < kR; ++q) {
+    const long long k0 = s + static_cast<long long>(q) * kP2Threads + w * kWave;
+    if (k0 >= e) break;                                   // wave-uniform
+    run_add<false>(hist, key_of(v[q]), k0 + lane < e, lane);
+  }
+  for (long long k0 = s + static_cast<long long>(kR) * kP2Threads + w * kWave; k0 < e; k0 += kP2Threads) {
+    const bool act = k0 + lane < e;
+    run_add<false>(hist, act ? key_of(src[k0 + lane]) : 0, act, lane);
+  }
+  __syncthreads();
+  // exclusive scan of hist: each thread owns a contiguous run of per = nb / 1024 bins (or one bin)
+  const int per = nb >= kP2Threads ? nb / kP2Threads : 1;
+  const int first = tid * per;
+  int loc = 0;
+  if (first < nb)
+    for (int i = 0; i < per; ++i) loc += hist[first + i];
+  const int inc = wave_incl_scan(loc);
+  if (lane == kWave - 1) wsum[w] = inc;
+  __syncthreads();
+  int base = inc - loc;
+  for (int x = 0; x < w; ++x) base += wsum[x];
+  if (first < nb) {
+    int run = static_cast<int>(s) + base;                 // positions fit 31 bits (n < 2^31)
+    for (int i = 0; i < per; ++i) {
+      const int c = hist[first + i];
+      hist[first + i] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < kR; ++q) {
+    const long long k0 = s + static_cast<long long>(q) * kP2Threads + w * kWave;
+    if (k0 >= e) break;
+    const bool act = k0 + lane < e;
+    const int p = run_add<true>(hist, act ? key_of(v[q]) : 0, act, lane);
+    if (act) dst[p] = v[q];
+  }
+  for (long long k0 = s + static_cast<long long>(kR) * kP2Threads + w * kWave; k0 < e; k0 += kP2Threads) {
+    const bool act = k0 + lane < e;
+    const unsigned long long x = act ? src[k0 + lane] : 0ull;
+    const int p = run_add<true>(hist, act ? key_of(x) : 0, act, lane);
+    if (act) dst[p] = x;
+  }
+}
+
+// The one-pass sweep's tile slots into their coarse A buckets (k_sweep<2> counted them per block in
+// hist_mat; off = the scan of those counts): block b walks the tiles its k_sweep<2> block swept (same
+// grid, same chunk -> wave deal), so its LDS cursors start at off[bucket][b].  A wave's chunk of <= 8
+// consecutive tiles is one dense range: lane l holds tile l's count and slot, each loaded entry finds
+// its tile among those lanes; 4 wave-loads are in flight before their cursor atomics.
+__global__ __launch_bounds__(kSwBlock) void k_sweep_scatter(SweepArgs g, const int* __restrict__ off,
+                                                            unsigned long long* __restrict__ dst, long long cap) {
+  __shared__ int cur[kHistMax];
+  for (int i = threadIdx.x; i < g.hist_h; i += kSwBlock) cur[i] = off[static_cast<long long>(i) * gridDim.x + blockIdx.x];
+  __syncthreads();
+  const int lane = lane_id();
+  const int nt = (g.nq + kWave - 1) / kWave;
+  const int nw = gridDim.x * kSwWaves;
+  const int wid = blockIdx.x * kSwWaves + (threadIdx.x >> 6);
+  const int run = max(1, min(kTileRun, nt / nw));   // as k_sweep
+  const int nchunks = (nt + run - 1) / run;
+  constexpr int kU = 4;
+  for (int chunk = wid; chunk < nchunks; chunk += nw) {
+    const int t = chunk * run + lane;
+    const bool tv = lane < run && t < nt;
+    const int c = tv ? g.tile_cnt[t] : 0;
+    const long long u0 = tv ? g.tile_ub[t] : 0;
+    const int inc = wave_incl_scan(c);
+    const int exc = inc - c;
+    const int T = rdl(inc, kWave - 1);
+    for (int k0 = 0; k0 < T; k0 += kU * kWave) {
+      unsigned long long v[kU];
+#pragma unroll
+      for (int q = 0; q < kU; ++q) {
+        const int k = k0 + q * kWave + lane;
+        int j = 0;                                    // the last tile (lane < run) starting at or before k
+#pragma unroll
+        for (int l = 1; l < kTileRun; ++l)
+          if (l < run && rdl(exc, l) <= k && rdl(c, l) > 0) j = l;
+        const long long at = __shfl(u0, j) + (k - __shfl(exc, j));
+        v[q] = k < T && at < g.ub_cap ? g.ent_ub[at] : 0ull;
+      }
+#pragma unroll
+      for (int q = 0; q < kU; ++q) {
+        if (k0 + q * kWave >= T) break;               // wave-uniform
+        const bool act = k0 + q * kWave + lane < T;
+        const int p = run_add<true>(cur, static_cast<int>(static_cast<unsigned>(v[q] >> 39) >> g.hist_lo), act, lane);
+        if (act && p < cap) dst[p] = v[q];
+      }
     }
   }
 }
@@ -1243,10 +1404,45 @@ hipError_t launch_sweep_dense(const SweepArgs& a, int mode, hipStream_t s) {
 
 int grp_ints() { return kGrpInts; }
 
+void sweep_coarse_hist(SweepArgs& a) {
+#ifdef FSLR_GROUP_COUNTED
+  a.hist_mat = nullptr;
+  return;
+#endif
+  // at most kHistMax buckets; the rest of A's bits (<= 14 for 2^24 reads) are pass 2's LDS bins
+  const int nbits = bits_for(std::max(1, a.n_reads - 1));
+  const int hb = std::min(nbits, 10);
+  const int nt = tiles_of(a);
+  const long long P = std::min(blocks_mode(2), (nt + kSwWaves - 1) / kSwWaves);
+  if (!a.grp || nbits - hb > 14 || (static_cast<long long>(1) << hb) * P > kGrpInts / 2) {
+    a.hist_mat = nullptr;
+    return;
+  }
+  a.hist_mat = a.grp;
+  a.hist_h = 1 << hb;
+  a.hist_lo = nbits - hb;
+}
+
 // group the entries by A: from the tile slots (mode 2) or dense `src` into `mid`, then into `out`
 static hipError_t group_by_a(const SweepArgs& a, int mode, const unsigned long long* src, unsigned long long* mid,
                              unsigned long long* out, hipStream_t s) {
   const long long n = a.n_ent;
+  const int nt = tiles_of(a);
+  if (mode == 2 && a.hist_mat) {
+    // the sweep counted its entries per coarse bucket: scan, scatter, then each bucket by its low bits
+    const int P = std::min(blocks_mode(2), (nt + kSwWaves - 1) / kSwWaves);   // the sweep's grid
+    const int H = a.hist_h, lo = a.hist_lo;
+    int* off = a.grp + kGrpInts / 2;
+    size_t tb = a.temp_bytes;
+    hipError_t e = hipcub::DeviceScan::ExclusiveSum(a.temp, tb, a.hist_mat, off, H * P, s);
+    if (e != hipSuccess) return e;
+    k_sweep_scatter<<<P, kSwBlock, 0, s>>>(a, off, mid, a.n_dev ? a.ent_cap : 0x7FFFFFFFFFFFFFFFll);
+    if (lo <= 12)
+      k_msd_pass2r<kMsdMaxLo, 16><<<H, kP2Threads, 0, s>>>(mid, n, a.n_dev, off, P, H, lo, out);
+    else
+      k_msd_pass2r<4 * kMsdMaxLo, 16><<<H, kP2Threads, 0, s>>>(mid, n, a.n_dev, off, P, H, lo, out);
+    return hipGetLastError();
+  }
   const int nbits = bits_for(std::max(1, a.n_reads - 1));
   // H = 2^hb buckets of ~4096 entries; P pass-1 workgroups with H P <= kGrpInts / 2 (pass 1 is
   // latency bound, so it wants waves in flight more than wide per-block histograms)
@@ -1260,7 +1456,6 @@ static hipError_t group_by_a(const SweepArgs& a, int mode, const unsigned long l
   const int P = std::max(64, std::min({kMsdMaxBlocks, (1 << 21) / H, static_cast<int>((n + 8191) / 8192)}));
   int* mat = a.grp;
   int* off = a.grp + kGrpInts / 2;
-  const int nt = tiles_of(a);
   if (mode == 2) {
     k_msd_pass1<true, false><<<P, kMsdThreads, 0, s>>>(a.ent_ub, a.ub_cap, a.tile_ub, a.tile_cnt, nt, lo, H, mat, nullptr);
   } else {
@@ -1275,7 +1470,7 @@ static hipError_t group_by_a(const SweepArgs& a, int mode, const unsigned long l
   } else {
     k_msd_pass1<false, true><<<P, kMsdThreads, 0, s>>>(src, n, nullptr, nullptr, 0, lo, H, off, mid);
   }
-  k_msd_pass2<<<H, 256, 0, s>>>(mid, n, mode == 2 ? a.n_dev : nullptr, off, P, H, hb, lo, out);
+  k_msd_pass2<kMsdMaxLo><<<H, 256, 0, s>>>(mid, n, mode == 2 ? a.n_dev : nullptr, off, P, H, hb, lo, out);
   return hipGetLastError();
 }
 

@@ -28,6 +28,12 @@ def main():
            'group_size_hist': {f'{8 * k + 1}-{8 * k + 8}': int(v) for k, v in enumerate(bins)},
            'mean_group_entries': None}
     out['share_le_64'] = float(bins[:8].sum() / max(1, groups))
+    ent = sum((8 * k + 4.5) * int(v) for k, v in enumerate(bins))
+    out['mean_group_entries'] = ent / max(1, groups)
+    # wave-clock sums per phase of k_sweep_pairs (s_memtime: its reads wait for the wave's LDS ops)
+    ph = c[68:74].astype(np.float64)
+    names = ['window_heads', 'sort', 'segment_setup', 'segment_eval', 'tail', 'long_runs']
+    out['phase_clock_share'] = {k: float(v / max(1.0, ph.sum())) for k, v in zip(names, ph)}
     print(json.dumps(out, indent=1))
     with open(sys.argv[1], 'w') as fh:
         json.dump(out, fh, indent=1)
