@@ -71,8 +71,12 @@ __device__ __forceinline__ int part_of(int B, int npass) {
 #ifndef FSLR_SWEEP_DB
 #define FSLR_SWEEP_DB 0
 #endif
+#ifndef FSLR_SWEEP_PF
+#define FSLR_SWEEP_PF 1
+#endif
 constexpr int kRing = FSLR_SWEEP_RING;     // positions per wave in the LDS ring (a power of two >= 64)
 static_assert(kRing >= kWave && (kRing & (kRing - 1)) == 0 && kRing < 1024, "ring size");
+static_assert(!FSLR_SWEEP_PF || kRing >= 2 * kWave, "the next tile's q records are read from the ring");
 constexpr int kRingMask = kRing - 1;
 constexpr int kMapCap = 1024;              // items per map segment (a longer tile takes several)
 constexpr int kTileRun = 8;                // consecutive tiles per work item
@@ -141,15 +145,27 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
   // multi-GPU split), so every wave gets work: the sweep is latency bound
   const int run = max(1, min(kTileRun, nt / nw));
   const int nchunks = (nt + run - 1) / run;
+#if FSLR_SWEEP_PF
+  // the next tile of the chunk, fetched while this one is swept: its 64 positions entering the ring,
+  // its forward counts and its q reads' gate ranges (their records already sit in the ring)
+  int4 pf_rr = make_int4(0, 0, 0, 0), pf_lb = make_int4(0, 0, 0, 0);
+  int2 pf_rg = make_int2(0, 0);
+  int pf_nf = 0;
+#endif
   for (int chunk = wid; chunk < nchunks; chunk += nw)
   for (int tile = chunk * run; tile < min(nt, (chunk + 1) * run); ++tile) {
     const int q0 = tile * kWave;
     const int q = q0 + lane;
     const bool qv = q < g.nq;
     const int qc = qv ? q : q0;
+    const bool first = tile == chunk * run;
+#if FSLR_SWEEP_PF
+    const int nf = first ? (qv ? g.rng_s[qc].x : 0) : pf_nf;
+#else
     const int nf = qv ? g.rng_s[qc].x : 0;
+#endif
     wave_lds_sync();                             // the previous tile's ring and map reads are done
-    if (tile == chunk * run) {
+    if (first) {
       // the chunk's first tile: positions [q0, q0 + kRing)
 #pragma unroll
       for (int k = 0; k < kRing / kWave; ++k) {
@@ -163,13 +179,40 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
       // the ring held [q0 - 64, q0 - 64 + kRing): the 64 positions entering it replace the last tile's
       const int p = q0 + kRing - kWave + lane;
       if (p < g.ni) {
+#if FSLR_SWEEP_PF
+        RR[p & kRingMask] = pf_rr;
+        RG[p & kRingMask] = pf_rg;
+#else
         RR[p & kRingMask] = g.idx4[p];
         RG[p & kRingMask] = g.idx_gate[p];
+#endif
       }
     }
     wave_lds_sync();
+#if FSLR_SWEEP_PF
+    int4 lbq;
+    if (first) {
+      const int4 rq = RR[qc & kRingMask];
+      lbq = g.lb[rq.w >> 6];                     // the gate of q's read as integer ranges
+    } else {
+      lbq = pf_lb;
+    }
+    if (tile + 1 < min(nt, (chunk + 1) * run)) {
+      const int pn = q0 + kRing + lane;          // enters the ring at the next tile
+      if (pn < g.ni) {
+        pf_rr = g.idx4[pn];
+        pf_rg = g.idx_gate[pn];
+      }
+      const int qn = q0 + kWave + lane;
+      const bool qnv = qn < g.nq;
+      pf_nf = qnv ? g.rng_s[qn].x : 0;
+      const int4 rqn = RR[(qnv ? qn : q0 + kWave) & kRingMask];
+      pf_lb = g.lb[rqn.w >> 6];
+    }
+#else
     const int4 rq = RR[qc & kRingMask];
     const int4 lbq = g.lb[rq.w >> 6];            // the gate of q's read as integer ranges
+#endif
     const bool any_zero = __ballot(qv && (lbq.x < 0 || lbq.z < 0)) != 0ull;   // v == 0 (ZeroDivision)
     const int pre = wave_incl_scan(nf);
     const int ex = pre - nf;
