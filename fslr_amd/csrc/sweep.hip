@@ -6,18 +6,21 @@
 // one forward sweep over the sorted positions meets each of them exactly once, in position order —
 // consecutive positions share their windows, so the index streams through L1/L2 once instead of
 // once per query read.  The rest of the reference's per-pair work is then:
-//   1. k_sweep: per overlapping interval pair of two different reads X != Y (A = min, B = max rank):
-//      the pair gate different_lengths_or_alignments (:178-183, the integer ranges of ratio_range),
-//      and calculate_overlap >= overlap (:133-136, folded thresholds: o >= max(thr)).  A pair that
-//      passes both is a match entry A << 39 | B << 14 | i << 7 | j (i, j: the intervals' indices in
-//      their reads' lists, cluster.py:189-191).  Two passes over 64-position tiles: the first counts
-//      each tile's entries, a scan places the tiles, the second writes them — no global atomics
-//      (one contended counter saturates near 90 returning atomics per microsecond).
-//   2. the entries are grouped by A (a two-level counting sort, group_by_a).
-//   3. k_sweep_pairs: per run of one read A, an LDS hash over its partners B collects each pair's
-//      match matrix as row / column masks; first-fit greedy (overall_jaccard_similarity, :152-161)
-//      is the entry count unless two entries share a row or a column, where the rows are walked in
-//      the reference's order (i ascending, lowest unused j).  Edge iff U <= umax[I - 1] (:216-219).
+//   1. k_sweep<2>: per overlapping interval pair of two different reads X != Y (A = min, B = max
+//      rank): the pair gate different_lengths_or_alignments (:178-183, the integer ranges of
+//      ratio_range), and calculate_overlap >= overlap (:133-136, folded thresholds: o >= max(thr)).
+//      A pair that passes both is a match entry A << 39 | B << 14 | i << 7 | j (i, j: the intervals'
+//      indices in their reads' lists, cluster.py:189-191), written at its 64-position tile's
+//      upper-bound slot (the scan of the tiles' pair tests) — one pass, no global atomics — and
+//      counted per coarse A bucket in the block's LDS histogram.
+//   2. the entries are grouped by A: one scan of the sweep's [bucket][block] counts, k_sweep_scatter
+//      (the sweep's tiles walked again in its own chunk order, LDS cursors), k_msd_pass2r (each
+//      bucket by A's low bits, the bucket held in registers between its histogram and its scatter).
+//   3. k_sweep_pairs: whole runs of one read A, up to 128 entries at a time, sorted by (run, B, i, j)
+//      with a wave bitonic network; one lane per read pair: first-fit greedy (overall_jaccard_
+//      similarity, :152-161) is the entry count unless two entries share a row or a column, where the
+//      rows are walked in the reference's order (i ascending, lowest unused j).  Edge iff
+//      U <= umax[I - 1] (:216-219).  A longer run goes through an LDS hash over its partners.
 // A pair with overlapping intervals but no match entry is evaluated too — its I is 0 — so the
 // edge set is the walk engine's E*, bit for bit.  The sweep does not count evaluated pairs (the
 // reference's seen-set size): that is the walk engine's job (query.hip), which the parity tests
@@ -57,24 +60,19 @@ __device__ __forceinline__ int part_of(int B, int npass) {
 // One wavefront per tile of 64 consecutive sorted positions (lane l holds q = q0 + l), tiles dealt in
 // chunks of consecutive tiles, grid-stride over a resident grid.  The tile's forward ranges are
 // flattened into an LDS map (item r -> its lane and p - q0), then walked 64 interval pairs per step,
-// one per lane, the next step's operands read while the current step is tested.
+// one per lane.
 // The index records and gate words of positions [q0, q0 + kRing) sit in a per-wave LDS ring (slot
 // p mod kRing): a tile's pairs have p in q0 + 1 .. q + n_fwd(q), so the p side of almost every pair
 // test — and the q side — is an LDS read instead of a dependent gather through L1 / L2.  Moving to the
 // next tile of a chunk loads only the 64 positions entering the ring (one coalesced record and gate
 // load per lane: every position's 24 B cross HBM once per chunk); a pair beyond the ring (a tile whose
-// forward window is longer) reads the index in global memory.
+// forward window is longer) reads the index in global memory.  The next tile's entering positions,
+// forward counts and q-side gate ranges are loaded while the current tile is swept (FSLR_SWEEP_PF).
 // kEmit = false counts the tile's entries (and the statistics); kEmit = true writes them.
-#ifndef FSLR_SWEEP_RING
-#define FSLR_SWEEP_RING 128
-#endif
-#ifndef FSLR_SWEEP_DB
-#define FSLR_SWEEP_DB 0
-#endif
 #ifndef FSLR_SWEEP_PF
 #define FSLR_SWEEP_PF 1
 #endif
-constexpr int kRing = FSLR_SWEEP_RING;     // positions per wave in the LDS ring (a power of two >= 64)
+constexpr int kRing = 128;                 // positions per wave in the LDS ring (64: +2 %, 256: +7 % step, profiles/r05/r5c)
 static_assert(kRing >= kWave && (kRing & (kRing - 1)) == 0 && kRing < 1024, "ring size");
 static_assert(!FSLR_SWEEP_PF || kRing >= 2 * kWave, "the next tile's q records are read from the ring");
 constexpr int kRingMask = kRing - 1;
@@ -322,26 +320,12 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
         }
       };
       auto run_steps = [&](auto zero_tag) __attribute__((always_inline)) {
-#if FSLR_SWEEP_DB
-        // double buffer unrolled by two: the operands of the next step are in flight while one is tested
-        Step s0, s1;
-        step_load(seg, s0);
-        for (int base = seg; base < se; base += 2 * kWave) {
-          const bool two = base + kWave < se;
-          if (two) step_load(base + kWave, s1);
-          step(zero_tag, base, s0);
-          if (!two) break;
-          if (base + 2 * kWave < se) step_load(base + 2 * kWave, s0);
-          step(zero_tag, base + kWave, s1);
-        }
-#else
         // LDS operands: other waves cover their latency
         for (int base = seg; base < se; base += kWave) {
           Step s0;
           step_load(base, s0);
           step(zero_tag, base, s0);
         }
-#endif
       };
       if (any_zero) run_steps(std::true_type{});
       else run_steps(std::false_type{});
@@ -845,11 +829,7 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
       unsigned long long k1 = v1 ? group_key(e1, r1) : ~0ull;
       // the group's network: the smallest of 32 / 64 / 128 elements that holds it (a group of <= 64
       // entries sits in k0; its upper half moves to lanes [0, 32) as the second slot)
-#ifdef FSLR_SORT128
-      if (true) {
-#else
       if (gend > kWave) {
-#endif
         bitonic_il<128>(k0, k1, lane);
       } else if (gend > kWave / 2) {
         k1 = __shfl(k0, (lane + kWave / 2) & (kWave - 1));
@@ -995,6 +975,10 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
 }
 
 // ---- 2. grouping by A: a two-level counting sort ---------------------------------------------------
+// One GPU (mode 2): the sweep already counted its entries per coarse bucket (sweep_coarse_hist), so
+// the grouping is one scan, k_sweep_scatter and k_msd_pass2r (group_by_a's first branch).  The
+// passes below serve the rest: the two-pass fallback (mode 0), the caller's entries of
+// fslr_sweep_evaluate (mode 3) and the multi-GPU partition (kMod).
 // Pass 1 scatters the entries into H = 2^hb buckets of A's high bits with per-block LDS histograms,
 // one scan over the [bucket][block] counts and LDS cursors; pass 2 groups each bucket by A's low bits
 // in one workgroup (LDS histogram and cursors; the bucket, a few thousand entries, stays in L2
@@ -1448,10 +1432,6 @@ hipError_t launch_sweep_dense(const SweepArgs& a, int mode, hipStream_t s) {
 int grp_ints() { return kGrpInts; }
 
 void sweep_coarse_hist(SweepArgs& a) {
-#ifdef FSLR_GROUP_COUNTED
-  a.hist_mat = nullptr;
-  return;
-#endif
   // at most kHistMax buckets; the rest of A's bits (<= 14 for 2^24 reads) are pass 2's LDS bins
   const int nbits = bits_for(std::max(1, a.n_reads - 1));
   const int hb = std::min(nbits, 10);

@@ -42,14 +42,24 @@ def main():
     ap.add_argument('--reps', type=int, default=5)
     ap.add_argument('--xgmi-gbs', type=float, default=300.0)
     ap.add_argument('--coll-us', type=float, default=30.0)
+    ap.add_argument('--split', default='chrom', choices=['chrom', 'position'],
+                    help='chrom: whole chromosomes per rank (chrom_owner); position: cost-balanced ranges of sorted '
+                         'positions (position_plan), as SweepShard(split=...)')
+    ap.add_argument('--chrom0-weight', type=float, default=0.0,
+                    help='> 0: chromosome 0 gets this many times the number of chromosomes as its locus weight '
+                         '(1.2: ~55 %% of the intervals on one chromosome, tests/test_dist.py skewed_case)')
     args = ap.parse_args()
     import torch
     from fslr_amd import _lib, synth
-    from fslr_amd.dist import chrom_counts_of, chrom_owner
+    from fslr_amd.dist import chrom_counts_of, chrom_owner, position_plan
     from fslr_amd.prep import fold_overlap_threshold, pass_table
 
     t = time.perf_counter()
-    s = synth.generate(args.reads, args.lmax, args.seed, dist=args.dist)
+    w = None
+    if args.chrom0_weight > 0:
+        w = np.ones(len(synth.CHROMS))
+        w[0] = len(synth.CHROMS) * args.chrom0_weight
+    s = synth.generate(args.reads, args.lmax, args.seed, dist=args.dist, chrom_weights=w)
     csr = s.interval_data().csr()
     del s
     log(f'data: {csr.n_reads} reads, {csr.n_intervals} intervals in {time.perf_counter() - t:.0f}s')
@@ -92,17 +102,27 @@ def main():
     ce = _lib.Context(0, stream=stream.cuda_stream)
     ce.load_csr(csr, thr)
     ce.reserve_edges(12 * n)
-    out = {'workload': f'{n} reads x 1-{args.lmax} ({args.dist}), seed {args.seed}', 'n_reads': n,
+    counts = chrom_counts_of(csr)
+    out = {'workload': f'{n} reads x 1-{args.lmax} ({args.dist}), seed {args.seed}'
+                       + (f', chromosome 0 weight {args.chrom0_weight} x {len(counts)}' if w is not None else ''),
+           'split': args.split, 'largest_chrom_share': float(counts.max() / counts.sum()), 'n_reads': n,
            'n_intervals': int(csr.n_intervals), 'single_step_ms': t1, 'match_entries': int(st1['match_entries']),
            'edges': int(st1['n_edges']), 'xgmi_gbs_assumed': args.xgmi_gbs, 'collective_latency_us': args.coll_us,
            'worlds': []}
-    counts = chrom_counts_of(csr)
+    if args.split == 'position':
+        cp.set_chrom_filter(None)
+        cp.build_index()
+        tile_tests, tile_reach = cp.position_costs()
     for W in [int(x) for x in args.worlds.split(',')]:
         owner = chrom_owner(counts, W)
+        plan = position_plan(tile_tests, tile_reach, int(csr.n_intervals), W) if args.split == 'position' else None
         part, part_rep, segs, sent = [], [], [[] for _ in range(W)], []
         buf = torch.empty(max(1 << 16, int(1.2 * st1['match_entries'] / W) + 4096), dtype=torch.int64, device=dev)
         for r in range(W):
-            cp.set_chrom_filter(owner == r if W > 1 else None)
+            if plan is not None and W > 1:
+                cp.set_position_filter(*plan[r])
+            else:
+                cp.set_chrom_filter(owner == r if W > 1 else None)
             res = {}
 
             def p():
@@ -168,6 +188,9 @@ def main():
         # model, none for the reduce), the partition without its readback
         step_rep = (max(part_rep) + a2a_ms - args.coll_us / 1000 + max(evl) + gather_ms + merge) if W > 1 else step
         row = {'W': W, 'part_ms': part, 'part_repeat_ms': part_rep, 'eval_ms': evl, 'merge_ms': merge,
+               'part_max_over_mean': float(max(part) / np.mean(part)),
+               'part_repeat_max_over_mean': float(max(part_rep) / np.mean(part_rep)) if part_rep else 1.0,
+               'eval_max_over_mean': float(max(evl) / np.mean(evl)), 'plan': plan,
                'a2a_ms_model': a2a_ms, 'projected_step_repeat_ms': step_rep, 'projected_speedup_repeat': t1 / step_rep,
                'gather_ms_model': gather_ms, 'entries_sent_per_rank': sent.sum(axis=1).tolist(),
                'entries_recv_per_rank': recv.tolist(), 'edges_per_rank': nedges, 'forest_pairs_per_rank': npairs,
