@@ -49,6 +49,16 @@ if has hist; then
       > $O/hist.log 2>&1 || { echo "hist failed"; tail -20 $O/hist.log; exit 1; }
   tail -30 $O/hist.log
 fi
+if has shard; then
+  # the per-rank model at 1M reads: both splits, uniform and one chromosome holding ~55 %
+  for cfg in "chrom 0" "position 0" "chrom 1.2" "position 1.2"; do
+    set -- $cfg
+    timeout -k 10 600 python3 -u tools/shard_timing.py --reads 1000000 --lmax 16 --seed 1 --worlds 1,2,4,8 --reps 5 \
+        --split $1 --chrom0-weight $2 > $O/shard_$1_$2.jsonl 2> $O/shard_$1_$2.log \
+        || { echo "shard $1 $2 failed"; tail -20 $O/shard_$1_$2.log; exit 1; }
+    grep "W=8" $O/shard_$1_$2.log || true
+  done
+fi
 if has pmc; then
   OUT=gpurun_out/$TAG/pmc timeout -k 10 900 bash tools/pmc.sh > $O/pmc.log 2>&1 || { echo "pmc failed"; tail -20 $O/pmc.log; exit 1; }
   tail -5 $O/pmc.log
