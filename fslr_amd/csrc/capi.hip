@@ -191,12 +191,15 @@ int fslr_set_profiling(fslr_ctx* c, int enable) {
   if (!c) return FSLR_ERR_INVALID;
   HIP_TRY(c, hipSetDevice(c->device));
   if (enable && !c->ev_ok) {
-    for (auto& e : c->ev) HIP_TRY(c, hipEventCreate(&e));
+    // timing-only events: no system-scope fence at record (its cache writeback and invalidation
+    // would cost every profiled step a bubble and start the next kernel on cold caches)
+    const unsigned fl = hipEventDisableSystemFence;
+    for (auto& e : c->ev) HIP_TRY(c, hipEventCreateWithFlags(&e, fl));
     c->kev.assign(2 * fslr_ctx::kKernRing, nullptr);
-    for (auto& e : c->kev) HIP_TRY(c, hipEventCreate(&e));
+    for (auto& e : c->kev) HIP_TRY(c, hipEventCreateWithFlags(&e, fl));
     c->kev2.assign(2 * fslr_ctx::kKernRing, nullptr);
-    for (auto& e : c->kev2) HIP_TRY(c, hipEventCreate(&e));
-    for (auto& e : c->sw_ev) HIP_TRY(c, hipEventCreate(&e));
+    for (auto& e : c->kev2) HIP_TRY(c, hipEventCreateWithFlags(&e, fl));
+    for (auto& e : c->sw_ev) HIP_TRY(c, hipEventCreateWithFlags(&e, fl));
     c->ev_ok = true;
   }
   c->profiling = enable != 0;

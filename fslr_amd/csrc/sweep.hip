@@ -107,7 +107,7 @@ constexpr int kHistMax = 1024;             // coarse A buckets the one-pass swee
 // (two-pass fallback), 2: one pass — write them at the tile's upper-bound slot (its forward-range
 // total, the pair tests) and count them; k_compact then packs the tiles.
 template <int kMode>
-__global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
+__global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(5))) void k_sweep(SweepArgs g) {
   constexpr bool kEmit = kMode != 0;
   constexpr bool kCount = kMode != 1;
   __shared__ int4 rr_all[kSwWaves][kRing];     // ring: index records {start, end, thr, read << 6 | j}
@@ -214,6 +214,11 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
     const bool any_zero = __ballot(qv && (lbq.x < 0 || lbq.z < 0)) != 0ull;   // v == 0 (ZeroDivision)
     const int pre = wave_incl_scan(nf);
     const int ex = pre - nf;
+#ifdef FSLR_SWEEP_NOFITS
+    const bool fits = false;
+#else
+    const bool fits = __ballot(qv && lane + nf >= kRing) == 0ull;   // every p of the tile in the ring
+#endif
     const int T = rdl(pre, kWave - 1);
     // lower bounds with v == 0 (lo < 0: partner 0 raises, [1, hi] passes) folded to 1
     QB[lane] = make_int4(lbq.x < 0 ? 1 : lbq.x, lbq.y, lbq.z < 0 ? 1 : lbq.z, lbq.w);
@@ -255,14 +260,18 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
         int4 b4, a4, rp;
         int2 gp;
       };
-      auto step_load = [&](int base, Step& t) {
+      // kFits: every pair of the tile has its p in the ring (the usual case), so the step reads LDS
+      // only; otherwise a lane beyond the ring reads the index in global memory (a per-lane choice
+      // of address: one flat load for the whole step)
+      auto step_load = [&](auto fits_tag, int base, Step& t) __attribute__((always_inline)) {
+        constexpr bool kFits = decltype(fits_tag)::value;
         const int r = base + lane;
         const unsigned md = r < se ? MAP[r - seg] : 0u;
         t.mi = static_cast<int>(md & 63u);
         const int d = static_cast<int>(md >> 6);
         t.b4 = QB[t.mi];
         t.a4 = RR[(q0 + t.mi) & kRingMask];
-        if (d < kRing) {
+        if (kFits || d < kRing) {
           t.rp = RR[(q0 + d) & kRingMask];
           t.gp = RG[(q0 + d) & kRingMask];
         } else {
@@ -319,16 +328,21 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep(SweepArgs g) {
           sn += ne;
         }
       };
-      auto run_steps = [&](auto zero_tag) __attribute__((always_inline)) {
+      auto run_steps = [&](auto zero_tag, auto fits_tag) __attribute__((always_inline)) {
         // LDS operands: other waves cover their latency
         for (int base = seg; base < se; base += kWave) {
           Step s0;
-          step_load(base, s0);
+          step_load(fits_tag, base, s0);
           step(zero_tag, base, s0);
         }
       };
-      if (any_zero) run_steps(std::true_type{});
-      else run_steps(std::false_type{});
+      if (fits) {
+        if (any_zero) run_steps(std::true_type{}, std::true_type{});
+        else run_steps(std::false_type{}, std::true_type{});
+      } else {
+        if (any_zero) run_steps(std::true_type{}, std::false_type{});
+        else run_steps(std::false_type{}, std::false_type{});
+      }
     }
     if constexpr (kEmit) {
       if (sn > 0) flush();

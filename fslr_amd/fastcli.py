@@ -215,7 +215,9 @@ def _run(args, basename, tsv, ints, strs, t, pool, ctx_f, state):
     cl_k, nr_k = q_cid[keys], q_size[keys]
     if k:
         cl_k, nr_k = cl_k.astype(np.float64), nr_k.astype(np.float64)
+    t['write.assign'] = time.perf_counter() - t3
     _write(tsv, f'{basename}.mappings.cluster.bed', rows, key_of_code[qc], ['cluster', 'n_reads'], [cl_k, nr_k])
+    t['write.cluster'] = time.perf_counter() - t3 - t['write.assign']
     # cluster.py:237-254 choose_alignment: per cluster the qname with the highest mean score, the
     # first in file order on ties; its rows
     cid_k = q_cid[keys]
@@ -227,8 +229,11 @@ def _run(args, basename, tsv, ints, strs, t, pool, ctx_f, state):
     chosen = np.zeros(n_q, bool)
     chosen[qc[win[win < rows.size]]] = True
     rsel = chosen[qc]
+    t4 = time.perf_counter()
+    t['write.choose'] = t4 - t3 - t['write.assign'] - t['write.cluster']
     _write(tsv, f'{basename}.mappings.representative.bed', rows[rsel], key_of_code[qc[rsel]],
            ['cluster', 'n_reads', 'avg_alignment_score'], [cl_k, nr_k, avg[keys]])
+    t['write.representative'] = time.perf_counter() - t4
     t['write'] = time.perf_counter() - t3
     if args.get('timings'):
         st = g.stats

@@ -130,6 +130,7 @@ def run_clustering(args, basename):
         multi.pool(args['gpus'], first_device=args.get('device') or 0)
     path = f'{basename}.mappings.bed'
     tsv = _open_tsv(path) if args.get('native_io', True) else None
+    t['read.open'] = time.perf_counter() - t0
     try:
         if tsv is not None and not args['filter_high_coverage']:
             # the columnar path (fastcli): codes and int columns, no frame of rows; the scan checks
