@@ -143,14 +143,15 @@ def test_cli_matches_reference_outputs(name, io_flag):
 
 @pytest.mark.parametrize('name', ['cfg1_1k_x3', 'capbind_1500', 'zerodiv', 'noclusters', 'longreads_400', 'params_a',
                                   'edge_cases_p0', 'zipf_800_l64', 'chroms_115', 'longcap_240', 'zdcap_skip',
-                                  'zdcap_raise', 'zdcap_skip_long', 'zdcap_raise_long'])
+                                  'zdcap_raise', 'zdcap_skip_long', 'zdcap_raise_long', 'longreads_p0',
+                                  'longzero_60'])
 def test_cli_multi_gpu_matches_reference_outputs(name):
     """``fslr --gpus 2``: two rank processes (sharing this box's one GPU over gloo) run the
-    chromosome-split sweep (fslr_amd.multi); outputs byte-identical to the reference's.  Covers the
-    cap replay on rank 0 (capbind_1500), a ZeroDivisionError raised on every rank (zerodiv), the
-    empty graph and the one-GPU fallback for overlap <= 0 (edge_cases_p0), 115 chromosomes (more than
-    the device chromosome filter's 64-bit mask held before round 3), long reads with the cap binding
-    (longcap_240, one GPU)."""
+    chromosome-split sweep, or the query-shard split where the sweep does not apply (fslr_amd.multi);
+    outputs byte-identical to the reference's.  Covers the cap replay (capbind_1500), a
+    ZeroDivisionError raised on every rank (zerodiv), the empty graph, overlap <= 0 (edge_cases_p0,
+    longreads_p0), 115 chromosomes, long reads with and without the cap binding (longreads_400,
+    longcap_240) and ZeroDivisionError pairs under a binding cap (zdcap_*)."""
     from fslr_amd import multi
     meta = fx.meta(name)
     multi.last_path = None
@@ -159,7 +160,8 @@ def test_cli_multi_gpu_matches_reference_outputs(name):
         # every input takes a two-rank split (no one-GPU fallback): the sweep split, or the query-shard
         # split for overlap <= 0 (edge_cases_p0), aln_size == 0 (zerodiv) and long reads
         want_path = {'edge_cases_p0': 'walk', 'zerodiv': 'walk', 'longreads_400': 'long', 'longcap_240': 'long',
-                     'zdcap_skip_long': 'long', 'zdcap_raise_long': 'long'}.get(name, 'sweep-chrom')
+                     'zdcap_skip_long': 'long', 'zdcap_raise_long': 'long', 'longreads_p0': 'long',
+                     'longzero_60': 'long'}.get(name, 'sweep-chrom')
         assert multi.last_path == want_path, (name, multi.last_path)
         if meta['exception']:
             assert isinstance(res.exception, ZeroDivisionError), (res.output, res.exception)

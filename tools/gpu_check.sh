@@ -40,6 +40,7 @@ PY
 fi
 if has cli10m; then
   export TMPDIR=${TMPDIR:-/tmp}
+  { df -T $TMPDIR | tail -1; python3 -c "import os; print('affinity', len(os.sched_getaffinity(0)))"; } > $O/cli_env.txt 2>&1 || true
   timeout -k 10 600 python3 -u tools/cli_io_timing.py 10000000 64 13 $O/cli_10m.json zipf --native-io > $O/cli_10m.log 2>&1 \
       || { echo "cli10m failed"; tail -20 $O/cli_10m.log; exit 1; }
   tail -3 $O/cli_10m.log
