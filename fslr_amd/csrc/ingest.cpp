@@ -14,6 +14,7 @@
 #include <charconv>
 #include <cmath>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -590,6 +591,7 @@ int fslr_tsv_scan_all(FslrTsv *t, int n_int, const int32_t *int_cols, int64_t *c
     // non-empty NA field and at least one text field (empty fields come back as '' either way).
     // Requested int columns are parsed, requested string columns factorized, in the same pass.
     std::atomic<int> bad{0};
+    const auto t_start = std::chrono::steady_clock::now();
     const int T = (int)std::min<int64_t>(t->n_threads, std::max<int64_t>(1, rows / 4096));
     std::vector<std::vector<unsigned char>> st((size_t)T, std::vector<unsigned char>((size_t)ncol * 3, 0));
     std::vector<std::vector<ChunkDict>> D((size_t)n_str, std::vector<ChunkDict>((size_t)T));
@@ -601,51 +603,71 @@ int fslr_tsv_scan_all(FslrTsv *t, int n_int, const int32_t *int_cols, int64_t *c
         // out): columns such as strand or version repeat one value, which is classified once
         std::vector<std::string_view> prev((size_t)ncol);
         std::vector<unsigned char> pcls((size_t)ncol, 0);
-        std::vector<int64_t> pval((size_t)ncol, 0);
         std::vector<const char *> fs((size_t)ncol + 2);
+        // per column: the requested int output, the requested string codes and dictionary (raw
+        // pointers held in locals: the byte stores below may alias anything held in memory)
+        std::vector<int64_t *> iout((size_t)ncol, nullptr);
+        std::vector<int32_t *> sout((size_t)ncol, nullptr);
+        std::vector<ChunkDict *> dict((size_t)ncol, nullptr);
+        for (int c = 0; c < ncol; ++c) {
+            if (slot[(size_t)c] >= 0) iout[(size_t)c] = outs[slot[(size_t)c]];
+            if (sslot[(size_t)c] >= 0) {
+                sout[(size_t)c] = str_codes[sslot[(size_t)c]];
+                dict[(size_t)c] = &D[(size_t)sslot[(size_t)c]][(size_t)w];
+            }
+        }
+        unsigned char *const AI = ai.data(), *const TK = tk.data(), *const AT = at.data(), *const PC = pcls.data();
+        std::string_view *const PV = prev.data();
+        const char **const FS = fs.data();
+        int64_t *const *const IO = iout.data();
+        int32_t *const *const SO = sout.data();
+        ChunkDict *const *const DI = dict.data();
+        const int64_t *const L0 = t->line.data(), *const L1 = L0 + rows + 1;
         for (int64_t i = a; i < e && !bad.load(std::memory_order_relaxed); ++i) {
-            const char *s = b + t->line[i];
-            const char *le = b + t->line[rows + 1 + i];
+            const char *s = b + L0[i];
+            const char *le = b + L1[i];
             if (le > s && le[-1] == '\n') --le;
             if (le > s && le[-1] == '\r') --le;
-            if (split_fields(s, le, fs.data(), ncol) != ncol) { bad = 1; break; }   // ragged row
+            if (split_fields(s, le, FS, ncol) != ncol) { bad = 1; break; }   // ragged row
             for (int c = 0; c < ncol; ++c) {
-                const std::string_view f(fs[(size_t)c], (size_t)(fs[(size_t)c + 1] - 1 - fs[(size_t)c]));
+                const std::string_view f(FS[c], (size_t)(FS[c + 1] - 1 - FS[c]));
+                if (int64_t *const io = IO[c]) {
+                    // a requested int column: every field a canonical int (its class stays int)
+                    int64_t v;
+                    if (!canon_int(f, &v)) { bad = 1; break; }
+                    io[i] = v;
+                    continue;
+                }
                 unsigned char cls;
-                // (int fields are parsed afresh: canon_int costs about what the compare does)
-                if (i > a && !(pcls[(size_t)c] & 1) && f == prev[(size_t)c]) {
-                    cls = pcls[(size_t)c];
+                if (i > a && !(PC[c] & 1) && f == PV[c]) {
+                    cls = PC[c];
                 } else {
                     int64_t v = 0;
                     cls = canon_int(f, &v) ? 1 : 0;
                     if (!cls && !f.empty() && (is_na(f) || boolish(f) || numeric(f))) cls |= 2;
-                    prev[(size_t)c] = f;
-                    pcls[(size_t)c] = cls;
-                    pval[(size_t)c] = v;
+                    PV[c] = f;
+                    PC[c] = cls;
                 }
-                if (slot[(size_t)c] >= 0) {
-                    if (!(cls & 1)) { bad = 1; break; }                  // a requested int column is not one
-                    outs[slot[(size_t)c]][i] = pval[(size_t)c];
-                } else if (sslot[(size_t)c] >= 0) {
-                    ChunkDict &d = D[(size_t)sslot[(size_t)c]][(size_t)w];
-                    str_codes[sslot[(size_t)c]][i] = d.add(f);
-                    if (d.na) { bad = 1; break; }
+                if (ChunkDict *const d = DI[c]) {
+                    SO[c][i] = d->add(f);
+                    if (d->na) { bad = 1; break; }
                 }
-                if (ai[(size_t)c] && !(cls & 1)) {
-                    ai[(size_t)c] = 0;
-                    if (i > a) tk[(size_t)c] = 0;          // the earlier fields were canonical ints: numeric text
+                if (AI[c] && !(cls & 1)) {
+                    AI[c] = 0;
+                    if (i > a) TK[c] = 0;          // the earlier fields were canonical ints: numeric text
                 }
-                if (!ai[(size_t)c] && !f.empty() && tk[(size_t)c]) {
-                    if (cls & 2) tk[(size_t)c] = 0;
-                    else at[(size_t)c] = 1;
+                if (!AI[c] && !f.empty() && TK[c]) {
+                    if (cls & 2) TK[c] = 0;
+                    else AT[c] = 1;
                 }
-                if (!ai[(size_t)c] && !tk[(size_t)c]) { bad = 1; break; }    // neither int nor text: decline
+                if (!AI[c] && !TK[c]) { bad = 1; break; }    // neither int nor text: decline
             }
         }
         auto &o = st[(size_t)w];
         for (int c = 0; c < ncol; ++c) { o[(size_t)c] = ai[(size_t)c]; o[(size_t)(ncol + c)] = tk[(size_t)c]; o[(size_t)(2 * ncol + c)] = at[(size_t)c]; }
     });
     if (bad) return FSLR_INGEST_DECLINE;
+    const auto t_scan = std::chrono::steady_clock::now();
     for (int c = 0; c < ncol; ++c) {
         bool all_int = true, text_ok = true, any_text = false;
         for (int w = 0; w < T; ++w) {
@@ -661,6 +683,10 @@ int fslr_tsv_scan_all(FslrTsv *t, int n_int, const int32_t *int_cols, int64_t *c
     }
     for (int k = 0; k < n_str; ++k)
         merge_dicts(t, str_cols[k], D[(size_t)k], rows, str_codes[k], &str_counts[2 * k], &str_counts[2 * k + 1]);
+    if (std::getenv("FSLR_INGEST_TIMING"))
+        std::fprintf(stderr, "fslr_tsv_scan_all: rows %lld threads %d scan %.3f s merge %.3f s\n", (long long)rows, T,
+                     std::chrono::duration<double>(t_scan - t_start).count(),
+                     std::chrono::duration<double>(std::chrono::steady_clock::now() - t_scan).count());
     return FSLR_INGEST_OK;
 }
 

@@ -214,11 +214,7 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(5))) v
     const bool any_zero = __ballot(qv && (lbq.x < 0 || lbq.z < 0)) != 0ull;   // v == 0 (ZeroDivision)
     const int pre = wave_incl_scan(nf);
     const int ex = pre - nf;
-#ifdef FSLR_SWEEP_NOFITS
-    const bool fits = false;
-#else
     const bool fits = __ballot(qv && lane + nf >= kRing) == 0ull;   // every p of the tile in the ring
-#endif
     const int T = rdl(pre, kWave - 1);
     // lower bounds with v == 0 (lo < 0: partner 0 raises, [1, hi] passes) folded to 1
     QB[lane] = make_int4(lbq.x < 0 ? 1 : lbq.x, lbq.y, lbq.z < 0 ? 1 : lbq.z, lbq.w);

@@ -216,24 +216,31 @@ def _run(args, basename, tsv, ints, strs, t, pool, ctx_f, state):
     if k:
         cl_k, nr_k = cl_k.astype(np.float64), nr_k.astype(np.float64)
     t['write.assign'] = time.perf_counter() - t3
-    _write(tsv, f'{basename}.mappings.cluster.bed', rows, key_of_code[qc], ['cluster', 'n_reads'], [cl_k, nr_k])
-    t['write.cluster'] = time.perf_counter() - t3 - t['write.assign']
-    # cluster.py:237-254 choose_alignment: per cluster the qname with the highest mean score, the
-    # first in file order on ties; its rows
-    cid_k = q_cid[keys]
-    best = np.full(int(cid_k.max()) + 1, -np.inf)
-    np.maximum.at(best, cid_k, avg[keys])
-    cand = keys[avg[keys] == best[cid_k]]
-    win = np.full(best.size, rows.size, np.int64)
-    np.minimum.at(win, q_cid[cand], first_row[cand])
-    chosen = np.zeros(n_q, bool)
-    chosen[qc[win[win < rows.size]]] = True
-    rsel = chosen[qc]
-    t4 = time.perf_counter()
-    t['write.choose'] = t4 - t3 - t['write.assign'] - t['write.cluster']
-    _write(tsv, f'{basename}.mappings.representative.bed', rows[rsel], key_of_code[qc[rsel]],
-           ['cluster', 'n_reads', 'avg_alignment_score'], [cl_k, nr_k, avg[keys]])
-    t['write.representative'] = time.perf_counter() - t4
+    # the two files are written at once (each by its own native writer threads; ctypes releases the
+    # GIL): the representative rows are chosen while the cluster file is being written
+    wpool = ThreadPoolExecutor(2)
+    try:
+        fut_c = wpool.submit(_write, tsv, f'{basename}.mappings.cluster.bed', rows, key_of_code[qc],
+                             ['cluster', 'n_reads'], [cl_k, nr_k])
+        # cluster.py:237-254 choose_alignment: per cluster the qname with the highest mean score, the
+        # first in file order on ties; its rows
+        cid_k = q_cid[keys]
+        best = np.full(int(cid_k.max()) + 1, -np.inf)
+        np.maximum.at(best, cid_k, avg[keys])
+        cand = keys[avg[keys] == best[cid_k]]
+        win = np.full(best.size, rows.size, np.int64)
+        np.minimum.at(win, q_cid[cand], first_row[cand])
+        chosen = np.zeros(n_q, bool)
+        chosen[qc[win[win < rows.size]]] = True
+        rsel = chosen[qc]
+        t['write.choose'] = time.perf_counter() - t3 - t['write.assign']
+        fut_r = wpool.submit(_write, tsv, f'{basename}.mappings.representative.bed', rows[rsel], key_of_code[qc[rsel]],
+                             ['cluster', 'n_reads', 'avg_alignment_score'], [cl_k, nr_k, avg[keys]])
+        fut_c.result()
+        t['write.cluster'] = time.perf_counter() - t3 - t['write.assign']
+        fut_r.result()
+    finally:
+        wpool.shutdown(wait=True)
     t['write'] = time.perf_counter() - t3
     if args.get('timings'):
         st = g.stats
