@@ -60,6 +60,14 @@ if has shard; then
     grep "W=8" $O/shard_$1_$2.log || true
   done
 fi
+if has shardprof; then
+  # kernel trace of the W = 8 per-rank model (chromosome split): where a rank's repeat step goes
+  ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/shardprof -o run --output-format csv \
+      -- python3 $R/tools/shard_timing.py --reads 1000000 --lmax 16 --seed 1 --worlds 8 --reps 3 > $O/shardprof.log 2>&1 ) \
+      || { echo "shardprof failed"; tail -5 $O/shardprof.log; exit 1; }
+  f=$(find $O/shardprof -name 'run_kernel_stats.csv' | head -1); cp $f $O/shardprof_kernel_stats.csv
+  f=$(find $O/shardprof -name 'run_kernel_trace.csv' | head -1); cp $f $O/shardprof_kernel_trace.csv
+fi
 if has pmc; then
   OUT=gpurun_out/$TAG/pmc timeout -k 10 900 bash tools/pmc.sh > $O/pmc.log 2>&1 || { echo "pmc failed"; tail -20 $O/pmc.log; exit 1; }
   tail -5 $O/pmc.log
