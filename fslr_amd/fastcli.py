@@ -242,6 +242,12 @@ def _run(args, basename, tsv, ints, strs, t, pool, ctx_f, state):
     finally:
         wpool.shutdown(wait=True)
     t['write'] = time.perf_counter() - t3
+    # the device buffers go now (the caller's process would free them at exit anyway)
+    t5 = time.perf_counter()
+    ctx = getattr(trees, 'ctx', None)
+    if ctx is not None and hasattr(ctx, 'close'):
+        ctx.close()
+    t['close'] = time.perf_counter() - t5
     if args.get('timings'):
         st = g.stats
         import sys
