@@ -117,6 +117,7 @@ def main():
         owner = chrom_owner(counts, W)
         plan = position_plan(tile_tests, tile_reach, int(csr.n_intervals), W) if args.split == 'position' else None
         part, part_rep, segs, sent = [], [], [[] for _ in range(W)], []
+        index_ms, rank_tests, rank_pos = [], [], []
         buf = torch.empty(max(1 << 16, int(1.2 * st1['match_entries'] / W) + 4096), dtype=torch.int64, device=dev)
         for r in range(W):
             if plan is not None and W > 1:
@@ -134,6 +135,11 @@ def main():
                     ok, cnt = cp.sweep_partition(qc, nc, pt, W, 6, buf)
                 res['cnt'] = cnt
             part.append(timed(p, args.reps))
+            index_ms.append(timed(cp.build_index, args.reps))
+            if plan is not None and W > 1:
+                lo, hi, end = plan[r]
+                rank_tests.append(int(tile_tests[lo // 64:(hi + 63) // 64].sum()))
+                rank_pos.append(int(hi - lo))
             cnt = res['cnt']
             if W > 1:
                 # the repeat step's partition (SweepShard.step(repeat=True)): no readback inside
@@ -190,7 +196,8 @@ def main():
         row = {'W': W, 'part_ms': part, 'part_repeat_ms': part_rep, 'eval_ms': evl, 'merge_ms': merge,
                'part_max_over_mean': float(max(part) / np.mean(part)),
                'part_repeat_max_over_mean': float(max(part_rep) / np.mean(part_rep)) if part_rep else 1.0,
-               'eval_max_over_mean': float(max(evl) / np.mean(evl)), 'plan': plan,
+               'eval_max_over_mean': float(max(evl) / np.mean(evl)), 'plan': plan, 'index_ms': index_ms,
+               'rank_tests': rank_tests, 'rank_positions': rank_pos,
                'a2a_ms_model': a2a_ms, 'projected_step_repeat_ms': step_rep, 'projected_speedup_repeat': t1 / step_rep,
                'gather_ms_model': gather_ms, 'entries_sent_per_rank': sent.sum(axis=1).tolist(),
                'entries_recv_per_rank': recv.tolist(), 'edges_per_rank': nedges, 'forest_pairs_per_rank': npairs,
