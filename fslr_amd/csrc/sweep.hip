@@ -66,15 +66,10 @@ __device__ __forceinline__ int part_of(int B, int npass) {
 // test — and the q side — is an LDS read instead of a dependent gather through L1 / L2.  Moving to the
 // next tile of a chunk loads only the 64 positions entering the ring (one coalesced record and gate
 // load per lane: every position's 24 B cross HBM once per chunk); a pair beyond the ring (a tile whose
-// forward window is longer) reads the index in global memory.  The next tile's entering positions,
-// forward counts and q-side gate ranges are loaded while the current tile is swept (FSLR_SWEEP_PF).
+// forward window is longer) reads the index in global memory.
 // kEmit = false counts the tile's entries (and the statistics); kEmit = true writes them.
-#ifndef FSLR_SWEEP_PF
-#define FSLR_SWEEP_PF 1
-#endif
 constexpr int kRing = 128;                 // positions per wave in the LDS ring (64: +2 %, 256: +7 % step, profiles/r05/r5c)
 static_assert(kRing >= kWave && (kRing & (kRing - 1)) == 0 && kRing < 1024, "ring size");
-static_assert(!FSLR_SWEEP_PF || kRing >= 2 * kWave, "the next tile's q records are read from the ring");
 constexpr int kRingMask = kRing - 1;
 constexpr int kMapCap = 1024;              // items per map segment (a longer tile takes several)
 constexpr int kTileRun = 8;                // consecutive tiles per work item
@@ -143,13 +138,6 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(5))) v
   // multi-GPU split), so every wave gets work: the sweep is latency bound
   const int run = max(1, min(kTileRun, nt / nw));
   const int nchunks = (nt + run - 1) / run;
-#if FSLR_SWEEP_PF
-  // the next tile of the chunk, fetched while this one is swept: its 64 positions entering the ring,
-  // its forward counts and its q reads' gate ranges (their records already sit in the ring)
-  int4 pf_rr = make_int4(0, 0, 0, 0), pf_lb = make_int4(0, 0, 0, 0);
-  int2 pf_rg = make_int2(0, 0);
-  int pf_nf = 0;
-#endif
   for (int chunk = wid; chunk < nchunks; chunk += nw)
   for (int tile = chunk * run; tile < min(nt, (chunk + 1) * run); ++tile) {
     const int q0 = tile * kWave;
@@ -157,11 +145,7 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(5))) v
     const bool qv = q < g.nq;
     const int qc = qv ? q : q0;
     const bool first = tile == chunk * run;
-#if FSLR_SWEEP_PF
-    const int nf = first ? (qv ? g.rng_s[qc].x : 0) : pf_nf;
-#else
     const int nf = qv ? g.rng_s[qc].x : 0;
-#endif
     wave_lds_sync();                             // the previous tile's ring and map reads are done
     if (first) {
       // the chunk's first tile: positions [q0, q0 + kRing)
@@ -177,40 +161,13 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(5))) v
       // the ring held [q0 - 64, q0 - 64 + kRing): the 64 positions entering it replace the last tile's
       const int p = q0 + kRing - kWave + lane;
       if (p < g.ni) {
-#if FSLR_SWEEP_PF
-        RR[p & kRingMask] = pf_rr;
-        RG[p & kRingMask] = pf_rg;
-#else
         RR[p & kRingMask] = g.idx4[p];
         RG[p & kRingMask] = g.idx_gate[p];
-#endif
       }
     }
     wave_lds_sync();
-#if FSLR_SWEEP_PF
-    int4 lbq;
-    if (first) {
-      const int4 rq = RR[qc & kRingMask];
-      lbq = g.lb[rq.w >> 6];                     // the gate of q's read as integer ranges
-    } else {
-      lbq = pf_lb;
-    }
-    if (tile + 1 < min(nt, (chunk + 1) * run)) {
-      const int pn = q0 + kRing + lane;          // enters the ring at the next tile
-      if (pn < g.ni) {
-        pf_rr = g.idx4[pn];
-        pf_rg = g.idx_gate[pn];
-      }
-      const int qn = q0 + kWave + lane;
-      const bool qnv = qn < g.nq;
-      pf_nf = qnv ? g.rng_s[qn].x : 0;
-      const int4 rqn = RR[(qnv ? qn : q0 + kWave) & kRingMask];
-      pf_lb = g.lb[rqn.w >> 6];
-    }
-#else
     const int4 rq = RR[qc & kRingMask];
     const int4 lbq = g.lb[rq.w >> 6];            // the gate of q's read as integer ranges
-#endif
     const bool any_zero = __ballot(qv && (lbq.x < 0 || lbq.z < 0)) != 0ull;   // v == 0 (ZeroDivision)
     const int pre = wave_incl_scan(nf);
     const int ex = pre - nf;
