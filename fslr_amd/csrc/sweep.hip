@@ -71,7 +71,13 @@ __device__ __forceinline__ int part_of(int B, int npass) {
 constexpr int kRing = 128;                 // positions per wave in the LDS ring (64: +2 %, 256: +7 % step, profiles/r05/r5c)
 static_assert(kRing >= kWave && (kRing & (kRing - 1)) == 0 && kRing < 1024, "ring size");
 constexpr int kRingMask = kRing - 1;
+#ifdef FSLR_SWEEP_W6
+constexpr int kMapCap = 256;
+#define FSLR_SWEEP_WAVES 6
+#else
 constexpr int kMapCap = 1024;              // items per map segment (a longer tile takes several)
+#define FSLR_SWEEP_WAVES 5
+#endif
 constexpr int kTileRun = 8;                // consecutive tiles per work item
 
 // One wave-instruction of keys (lanes with `act`, a contiguous prefix): equal keys on adjacent lanes
@@ -102,7 +108,7 @@ constexpr int kHistMax = 1024;             // coarse A buckets the one-pass swee
 // (two-pass fallback), 2: one pass — write them at the tile's upper-bound slot (its forward-range
 // total, the pair tests) and count them; k_compact then packs the tiles.
 template <int kMode>
-__global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(5))) void k_sweep(SweepArgs g) {
+__global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(FSLR_SWEEP_WAVES))) void k_sweep(SweepArgs g) {
   constexpr bool kEmit = kMode != 0;
   constexpr bool kCount = kMode != 1;
   __shared__ int4 rr_all[kSwWaves][kRing];     // ring: index records {start, end, thr, read << 6 | j}
@@ -455,6 +461,9 @@ constexpr int kChunk2 = 512;               // a wave's work item: whole runs sta
 constexpr int kStageE = 128;
 constexpr int kHash2 = 128;
 constexpr unsigned kEmpty = 0xFFFFFFFFu;
+#ifdef FSLR_PAIRS_W6
+#define FSLR_PAIR_EDGE_STAGE 128
+#endif
 #ifndef FSLR_PAIR_EDGE_STAGE
 #define FSLR_PAIR_EDGE_STAGE 256
 #endif
@@ -541,10 +550,13 @@ __device__ __forceinline__ unsigned long long group_key(unsigned long long e, in
   return (static_cast<unsigned long long>(r) << 39) | (e & ((1ull << 39) - 1));
 }
 
+#ifdef FSLR_PAIRS_W6
+__global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(6))) void k_sweep_pairs(SweepArgs g) {
+#else
 __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
+#endif
   __shared__ __attribute__((aligned(16))) unsigned long long scr_all[kSwWaves][kScrWords];
-  __shared__ int runa_all[kSwWaves][kStageE];                 // per run of the group: A, L_A, edges formed
-  __shared__ int runl_all[kSwWaves][kStageE];
+  __shared__ int runa_all[kSwWaves][kStageE];                 // per run of the group: A | L_A << 25, edges formed
   __shared__ int runf_all[kSwWaves][kStageE];
   __shared__ uint2 rr_all[kSwWaves][kWave];                   // long runs' ordered path: row masks of one partner
   __shared__ unsigned long long es_all[kSwWaves][kPairEdgeStage];
@@ -563,7 +575,6 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
   unsigned long long* PJ = PK + kStageE;                      // per segment: OR of column bits
   int* PH = reinterpret_cast<int*>(PJ + kStageE);             // per segment: first position | row dup << 30
   int* RUNA = runa_all[wv];
-  int* RUNL = runl_all[wv];
   int* RUNF = runf_all[wv];
   uint2* RR = rr_all[wv];
   EdgeStageN<kPairEdgeStage> es{es_all[wv], 0};
@@ -843,13 +854,11 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
       const int g1 = ns0 + __popcll(S1 & upto(lane)) - 1;
       wave_lds_sync();                                             // the previous group's reads are done
       if (hv0) {
-        RUNA[r0] = entry_a(e0);
-        RUNL[r0] = la0;
+        RUNA[r0] = static_cast<int>(static_cast<unsigned>(entry_a(e0)) | static_cast<unsigned>(la0) << 25);
         RUNF[r0] = 0;
       }
       if (hv1) {
-        RUNA[r1] = entry_a(e1);
-        RUNL[r1] = la1;
+        RUNA[r1] = static_cast<int>(static_cast<unsigned>(entry_a(e1)) | static_cast<unsigned>(la1) << 25);
         RUNF[r1] = 0;
       }
       if (s0) {
@@ -902,8 +911,9 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
             I = Ic;
           }
         }
-        const int A = act ? RUNA[r] : 0;
-        const int U = (act ? RUNL[r] : 0) + LB - I;
+        const int ra = act ? RUNA[r] : 0;
+        const int A = static_cast<int>(static_cast<unsigned>(ra) & kRankMask);
+        const int U = static_cast<int>(static_cast<unsigned>(ra) >> 25) + LB - I;
         const int um = __shfl(umax_v, max(I, 1) - 1);     // every lane reads (no && in front)
         const bool edge = act && I > 0 && U <= um;
         es.put(eo, edge, A, B, I, U, lane);
