@@ -13,7 +13,7 @@ import numpy as np
 
 LIB_PATH = os.environ.get('FSLR_LIB') or os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libfslr_hip.so')
 
-ABI_VERSION = 19         # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
+ABI_VERSION = 20         # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
 FSLR_OK, FSLR_ERR_ZERO_DIVISION, FSLR_ERR_INVALID, FSLR_ERR_HIP, FSLR_ERR_NOMEM, FSLR_ERR_STATE = range(6)
 FSLR_MAX_L = 64
 FSLR_MAX_READS = 1 << 25
@@ -42,7 +42,7 @@ EXPORTED = ['fslr_abi_version', 'fslr_last_error', 'fslr_ctx_create', 'fslr_ctx_
             'fslr_local_forest', 'fslr_copy_forest_pairs', 'fslr_sort_edges', 'fslr_cap_bwd_counts',
             'fslr_cap_restrict', 'fslr_cap_copy_restricted', 'fslr_cap_install_restricted', 'fslr_rows_upload',
             'fslr_set_reads_rows', 'fslr_get_read_codes', 'fslr_get_csr', 'fslr_fold_thresholds',
-            'fslr_position_costs', 'fslr_set_position_filter', 'fslr_use_position_filter', 'fslr_long_pairs_shard',
+            'fslr_position_costs', 'fslr_position_entries', 'fslr_set_position_filter', 'fslr_use_position_filter', 'fslr_long_pairs_shard',
             'fslr_edge_cap_deferred', 'fslr_edge_cap_deferred_read']
 
 
@@ -197,6 +197,7 @@ def load(path: str = LIB_PATH):
         'fslr_get_csr': (ctypes.c_int, [vp] + [vp] * 10),
         'fslr_fold_thresholds': (ctypes.c_int, [vp, ctypes.c_double]),
         'fslr_position_costs': (ctypes.c_int, [vp, vp, vp, i64]),
+        'fslr_position_entries': (ctypes.c_int, [vp, vp, vp, i64]),
         'fslr_set_position_filter': (ctypes.c_int, [vp, i64, i64, i64]),
         'fslr_use_position_filter': (ctypes.c_int, [vp]),
         'fslr_long_pairs_shard': (ctypes.c_int, [vp, ctypes.POINTER(Params), i32, i32, ctypes.POINTER(ctypes.c_int64)]),
@@ -439,6 +440,15 @@ class Context:
         tests, reach = np.zeros(nt, np.int64), np.zeros(nt, np.int64)
         self._check(self._L.fslr_position_costs(self._h, _ptr(tests), _ptr(reach), nt))
         return tests, reach
+
+    def position_entries(self, qlen_cut, nal_cut, pass_table, edge_threshold=10):
+        """Match entries per 64-position tile of the full index under these parameters
+        (fslr_position_entries: a counting sweep)."""
+        nt = (self.n_intervals + 63) // 64
+        ent = np.zeros(nt, np.int64)
+        p = self._params(qlen_cut, nal_cut, pass_table, edge_threshold)
+        self._check(self._L.fslr_position_entries(self._h, ctypes.byref(p), _ptr(ent), nt))
+        return ent
 
     def set_position_filter(self, lo, hi, end):
         self._check(self._L.fslr_set_position_filter(self._h, int(lo), int(hi), int(end)))

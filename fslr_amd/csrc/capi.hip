@@ -883,7 +883,8 @@ int fslr_query_shard(fslr_ctx* c, const fslr_params* p, int32_t shard, int32_t n
 // input); an upper bound beyond the budget (half the free HBM, at least 8 GB) takes the two-pass
 // fallback (count, then emit: the sweep runs twice).
 static int sweep_front(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_t a_end, hipEvent_t e0,
-                       hipEvent_t e1, SweepArgs& s, int& mode, bool defer = false, bool coarse = false) {
+                       hipEvent_t e1, SweepArgs& s, int& mode, bool defer = false, bool coarse = false,
+                       bool count_only = false) {
   // upper-bound slots (8 B each) the one-pass sweep may use: half the free HBM, at least 2^30; asked
   // only when the slot buffer has to grow (hipMemGetInfo is a driver round trip, kept off repeat queries)
   auto ub_budget = []() {
@@ -957,7 +958,7 @@ static int sweep_front(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64
     c->lb_q = p->qlen_cut;
     c->lb_n = p->nal_cut;
   }
-  mode = 2;
+  mode = count_only ? 0 : 2;                         // count_only: per-tile entry counts, no slots
   for (int attempt = 0; attempt < 3; ++attempt) {
     s.ent = c->ent;
     s.ent_sorted = c->ent_sorted;
@@ -1230,6 +1231,23 @@ int fslr_position_costs(fslr_ctx* c, int64_t* tests, int64_t* reach, int64_t n_t
     HIP_TRY(c, hipMemcpyAsync(reach, c->pf_cost + nt, nt * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
   }
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FSLR_OK;
+}
+
+int fslr_position_entries(fslr_ctx* c, const fslr_params* p, int64_t* entries, int64_t n_tiles) {
+  if (!c || !p || !p->pass_table || !entries) return FSLR_ERR_INVALID;
+  if (!c->index_built || c->filter_active) return fail(c, FSLR_ERR_STATE, "fslr_build_index over every chromosome first");
+  const int64_t nt = (c->ni + 63) / 64;
+  if (n_tiles != nt) return fail(c, FSLR_ERR_INVALID, "n_tiles must be ceil(n_intervals / 64)");
+  if (c->thr_mode != 0 || c->any_zero_aln)
+    return fail(c, FSLR_ERR_INVALID, "the sweep engine needs overlap thresholds >= 1 and no aln_size == 0 interval");
+  if (int rc = prepare_query(c, p)) return rc;
+  SweepArgs s{};
+  int mode = 0;
+  if (int rc = sweep_front(c, p, 0, c->n, nullptr, nullptr, s, mode, false, false, true)) return rc;
+  if (nt) HIP_TRY(c, hipMemcpyAsync(entries, s.tile_cnt, nt * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->last_full = false;                               // no graph from this sweep
   return FSLR_OK;
 }
 

@@ -125,21 +125,27 @@ def chrom_owner(chrom_counts, world: int) -> np.ndarray:
 
 
 POSITION_COST = 4       # per sorted position, in pair tests: the sweep's per-position work beside its tests
+ENTRY_COST = 16         # per match entry, in pair tests: its write, partition, exchange and evaluation
 
 
-def position_plan(tile_tests, tile_reach, n_intervals: int, world: int, per_position: int = POSITION_COST):
+def position_plan(tile_tests, tile_reach, n_intervals: int, world: int, per_position: int = POSITION_COST,
+                  tile_entries=None, per_entry: int = ENTRY_COST):
     """Contiguous ranges of the (chrom, start)-sorted positions, one per rank: cut at 64-position tile
     boundaries where the running cost (the tile's pair tests, the sweep's work, plus ``per_position``
-    per position) reaches r / world of the total, whatever the chromosomes.  Returns (lo, hi, end) per
-    rank: the rank sweeps the pairs whose lower position lies in [lo, hi) and indexes [lo, end), end
-    covering the forward windows of its tiles (fslr_position_costs).  Deterministic: every rank makes the
-    same plan from its own full index."""
+    per position and, given the tiles' match entries (fslr_position_entries), ``per_entry`` per entry)
+    reaches r / world of the total, whatever the chromosomes.  Returns (lo, hi, end) per rank: the rank
+    sweeps the pairs whose lower position lies in [lo, hi) and indexes [lo, end), end covering the
+    forward windows of its tiles (fslr_position_costs).  Deterministic: every rank makes the same plan
+    from its own full index."""
     tests = np.asarray(tile_tests, np.int64)
     reach = np.asarray(tile_reach, np.int64)
     nt = tests.size
     ni = int(n_intervals)
     width = np.minimum(64, ni - 64 * np.arange(nt, dtype=np.int64))
-    cum = np.cumsum(tests + per_position * width)
+    cost = tests + per_position * width
+    if tile_entries is not None:
+        cost = cost + per_entry * np.asarray(tile_entries, np.int64)
+    cum = np.cumsum(cost)
     total = int(cum[-1]) if nt else 0
     cuts = [0]
     for r in range(1, world):
@@ -339,13 +345,15 @@ class SweepShard:
         if split == 'chrom':
             ctx.set_chrom_filter(self.owned if world > 1 else None)
 
-    def _plan_positions(self):
-        """The position split's range of this rank (every rank makes the same plan from its full index)."""
+    def _plan_positions(self, qlen_cut, nal_cut, pass_table, edge_threshold):
+        """The position split's range of this rank (every rank makes the same plan from its full index):
+        cost = pair tests + per-position work + per-entry work, the entries from one counting sweep."""
         ctx = self.ctx
         ctx.set_chrom_filter(None)
         ctx.build_index()
         tests, reach = ctx.position_costs()
-        self.plan = position_plan(tests, reach, self.n_intervals, self.world)
+        ent = ctx.position_entries(qlen_cut, nal_cut, pass_table, edge_threshold)
+        self.plan = position_plan(tests, reach, self.n_intervals, self.world, tile_entries=ent)
         self.pos = self.plan[self.rank]
         ctx.set_position_filter(*self.pos)
 
@@ -382,7 +390,7 @@ class SweepShard:
         err = None
         try:
             if self.split == 'position' and self.pos is None:
-                self._plan_positions()
+                self._plan_positions(qlen_cut, nal_cut, pass_table, edge_threshold)
             ctx.build_index()
             ok, counts = ctx.sweep_partition(qlen_cut, nal_cut, pass_table, W, self.block_shift, self.send,
                                              edge_threshold)

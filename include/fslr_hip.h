@@ -75,7 +75,7 @@
 extern "C" {
 #endif
 
-#define FSLR_ABI_VERSION 19
+#define FSLR_ABI_VERSION 20
 #define FSLR_MAX_L 64                /* max intervals per read (bitmask width) */
 #define FSLR_MAX_READS (1 << 25)     /* read rank packs into bits 6..30 of the index record */
 #define FSLR_THR_ZERO_ALN INT32_MIN
@@ -319,9 +319,14 @@ int  fslr_set_chrom_filter(fslr_ctx *ctx, const uint8_t *owned);
  *   fslr_sweep_partition sweeps the pairs whose lower position lies in [lo, hi); end must cover the
  *   forward windows of [lo, hi) (fslr_position_costs).  Every pair of overlapping intervals is met by
  *   the rank holding its lower position.  Needs iv_data_pos and <= 64 chromosomes.  Syncs.
+ * fslr_position_entries: after fslr_build_index over every chromosome, the match entries of each
+ *   tile under the query parameters p (the one-pass sweep over the full index, as fslr_query's):
+ *   the per-entry work (partition, exchange, evaluation) is most of a rank's cost where pair tests
+ *   rarely match.  Syncs.
  * fslr_use_position_filter: make the last position filter of these reads active again (after
  *   fslr_set_chrom_filter, which the edge cap's sharded replay lists its hits with). */
 int  fslr_position_costs(fslr_ctx *ctx, int64_t *tile_tests, int64_t *tile_reach, int64_t n_tiles);
+int  fslr_position_entries(fslr_ctx *ctx, const fslr_params *p, int64_t *tile_entries, int64_t n_tiles);
 int  fslr_set_position_filter(fslr_ctx *ctx, int64_t lo, int64_t hi, int64_t end);
 int  fslr_use_position_filter(fslr_ctx *ctx);
 /* Multi-GPU edge cap (cluster.py:197-224).  The replayed loops need every E* edge

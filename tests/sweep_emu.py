@@ -105,7 +105,7 @@ class EmuSweepContext:
             return False, True
         return mn / mx >= ncut, False
 
-    def _entries(self, qcut, ncut):
+    def _entries(self, qcut, ncut, tiles=None):
         c = self.csr
         chrom = np.asarray(c.iv_chrom)
         start, end = np.asarray(c.iv_start, np.int64), np.asarray(c.iv_end, np.int64)
@@ -131,7 +131,21 @@ class EmuSweepContext:
                     self._zd.add((a, b))            # listed, not raised (the edge cap decides)
                 elif passes and m:
                     out.append((a << 39) | (b << 14) | (int(self.slot[p]) << 7) | int(self.slot[q]))
+                    if tiles is not None:
+                        tiles[min(int(self.pos[p]), int(self.pos[q])) // 64] += 1
         return np.array(out, dtype=np.int64)
+
+    def position_entries(self, qlen_cut, nal_cut, pass_table, edge_threshold=10):
+        """fslr_position_entries: match entries per 64-position tile of the full index."""
+        tiles = np.zeros((self.pos.size + 63) // 64, np.int64)
+        owned, prange, zd = self.owned, self.prange, getattr(self, '_zd', set())
+        self.owned = self.prange = None
+        try:
+            self._zd = set()
+            self._entries(qlen_cut, nal_cut, tiles)
+        finally:
+            self.owned, self.prange, self._zd = owned, prange, zd
+        return tiles
 
     def sweep_partition(self, qlen_cut, nal_cut, pass_table, n_dest, block_shift, dst, edge_threshold=10):
         self._zd = set()

@@ -45,6 +45,8 @@ def main():
     ap.add_argument('--split', default='chrom', choices=['chrom', 'position'],
                     help='chrom: whole chromosomes per rank (chrom_owner); position: cost-balanced ranges of sorted '
                          'positions (position_plan), as SweepShard(split=...)')
+    ap.add_argument('--plan-tests-only', action='store_true',
+                    help='position split planned from pair tests and positions only (round-5 first version)')
     ap.add_argument('--chrom0-weight', type=float, default=0.0,
                     help='> 0: chromosome 0 gets this many times the number of chromosomes as its locus weight '
                          '(1.2: ~55 %% of the intervals on one chromosome, tests/test_dist.py skewed_case)')
@@ -113,11 +115,14 @@ def main():
         cp.set_chrom_filter(None)
         cp.build_index()
         tile_tests, tile_reach = cp.position_costs()
+        tile_entries = cp.position_entries(qc, nc, pt, 10)
     for W in [int(x) for x in args.worlds.split(',')]:
         owner = chrom_owner(counts, W)
-        plan = position_plan(tile_tests, tile_reach, int(csr.n_intervals), W) if args.split == 'position' else None
+        plan = (position_plan(tile_tests, tile_reach, int(csr.n_intervals), W,
+                              tile_entries=None if args.plan_tests_only else tile_entries)
+                if args.split == 'position' else None)
         part, part_rep, segs, sent = [], [], [[] for _ in range(W)], []
-        index_ms, rank_tests, rank_pos = [], [], []
+        index_ms, rank_tests, rank_pos, rank_entries = [], [], [], []
         buf = torch.empty(max(1 << 16, int(1.2 * st1['match_entries'] / W) + 4096), dtype=torch.int64, device=dev)
         for r in range(W):
             if plan is not None and W > 1:
@@ -139,6 +144,7 @@ def main():
             if plan is not None and W > 1:
                 lo, hi, end = plan[r]
                 rank_tests.append(int(tile_tests[lo // 64:(hi + 63) // 64].sum()))
+                rank_entries.append(int(tile_entries[lo // 64:(hi + 63) // 64].sum()))
                 rank_pos.append(int(hi - lo))
             cnt = res['cnt']
             if W > 1:
@@ -197,7 +203,7 @@ def main():
                'part_max_over_mean': float(max(part) / np.mean(part)),
                'part_repeat_max_over_mean': float(max(part_rep) / np.mean(part_rep)) if part_rep else 1.0,
                'eval_max_over_mean': float(max(evl) / np.mean(evl)), 'plan': plan, 'index_ms': index_ms,
-               'rank_tests': rank_tests, 'rank_positions': rank_pos,
+               'rank_tests': rank_tests, 'rank_positions': rank_pos, 'rank_entries_planned': rank_entries,
                'a2a_ms_model': a2a_ms, 'projected_step_repeat_ms': step_rep, 'projected_speedup_repeat': t1 / step_rep,
                'gather_ms_model': gather_ms, 'entries_sent_per_rank': sent.sum(axis=1).tolist(),
                'entries_recv_per_rank': recv.tolist(), 'edges_per_rank': nedges, 'forest_pairs_per_rank': npairs,
