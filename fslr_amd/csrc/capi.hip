@@ -168,7 +168,7 @@ void fslr_ctx_destroy(fslr_ctx* c) {
                   c->temp,   c->umax,   c->edges,   c->edge_iu, c->fwd,     c->parent,  c->counters, c->forest, c->forest_cnt, c->forest_blk,
                   c->upl,    c->upl64,
                   c->errw,   c->thr_tmp, c->defer,   c->dchrom,  c->drec,    c->lbounds, c->diag, c->wstat,
-                  c->dgate,  c->chist,  c->heavy, c->ent, c->ent_sorted, c->sweep_temp, c->sw_tile, c->sw_wstat, c->ent_ub,
+                  c->dgate,  c->chist,  c->heavy, c->ent, c->ent_sorted, c->sweep_temp, c->sw_tile, c->sw_wstat, c->sw_wlo, c->ent_ub,
                   c->fdchrom, c->fdrec, c->fdgate, c->crange_f, c->part_cnt, c->grp, c->fmap,
                   c->rows_col, c->rows_ord, c->rows_keep, c->rows_int, c->rows_l, c->rows_temp,
                   c->pf_sel, c->pf_lmap, c->pf_cost};
@@ -909,6 +909,7 @@ static int sweep_front(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64
   if (!c->sw_wstat) {
     const int w = sweep_max_waves();
     if ((rc = dalloc(c, &c->sw_wstat, static_cast<size_t>(w) * 4))) return rc;
+    if ((rc = dalloc(c, &c->sw_wlo, static_cast<size_t>(w) + 1))) return rc;
     c->sw_wstat_waves = w;
   }
   if (c->ent_cap == 0 && (rc = reserve_entries(c, std::max<int64_t>(1 << 20, nix)))) return rc;
@@ -944,6 +945,7 @@ static int sweep_front(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64
   s.err = c->errw;
   s.wstat = c->sw_wstat;
   s.wstat_waves = c->sw_wstat_waves;
+  s.wlo = c->sw_wlo;
   s.n_ent = 0;
   s.n_dev = nullptr;
   s.ent_cap = c->ent_cap;
@@ -1446,6 +1448,7 @@ int fslr_sweep_evaluate(fslr_ctx* c, const fslr_params* p, const void* entries, 
   if (!c->sw_wstat) {
     const int w = sweep_max_waves();
     if (int rc = dalloc(c, &c->sw_wstat, static_cast<size_t>(w) * 4)) return rc;
+    if (int rc = dalloc(c, &c->sw_wlo, static_cast<size_t>(w) + 1)) return rc;
     c->sw_wstat_waves = w;
   }
   c->last_full = false;

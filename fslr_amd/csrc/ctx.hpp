@@ -132,6 +132,7 @@ struct fslr_ctx {
   int64_t ent_ub_cap = 0;
   int64_t sw_tiles = 0;
   unsigned long long* sw_wstat = nullptr;   // per-wave statistics slots of the sweep kernels
+  int* sw_wlo = nullptr;                    // [waves + 1] the one-pass sweep's first tile per wave
   int sw_wstat_waves = 0;
   hipEvent_t sw_ev[5] = {};                 // (profiling) count | scan | emit | sort | pairs
   bool sw_ev_rec = false;

@@ -209,6 +209,8 @@ struct SweepArgs {
   int* err;
   unsigned long long* wstat;          // per-wave statistics slots [waves x 4] (no contended atomics)
   int wstat_waves;
+  int* wlo;                           // (one-pass sweep) [waves + 1]: wave w sweeps tiles [wlo[w], wlo[w + 1])
+
   hipEvent_t ev[5];                   // (profiling) count | scan | emit | sort | pairs boundaries, or null
   hipEvent_t k0, k1;                  // (profiling) around the sweep kernel launch alone, or null
   hipEvent_t p0, p1;                  // (profiling) around the pair-stage kernel (k_sweep_pairs) alone, or null

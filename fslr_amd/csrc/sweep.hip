@@ -71,14 +71,9 @@ __device__ __forceinline__ int part_of(int B, int npass) {
 constexpr int kRing = 128;                 // positions per wave in the LDS ring (64: +2 %, 256: +7 % step, profiles/r05/r5c)
 static_assert(kRing >= kWave && (kRing & (kRing - 1)) == 0 && kRing < 1024, "ring size");
 constexpr int kRingMask = kRing - 1;
-#ifdef FSLR_SWEEP_W6
-constexpr int kMapCap = 256;
-#define FSLR_SWEEP_WAVES 6
-#else
 constexpr int kMapCap = 1024;              // items per map segment (a longer tile takes several)
-#define FSLR_SWEEP_WAVES 5
-#endif
-constexpr int kTileRun = 8;                // consecutive tiles per work item
+constexpr int kTileRun = 8;                // consecutive tiles per work item (two-pass fallback)
+constexpr long long kTileCost = 256;       // a tile's fixed cost in pair tests (its ring load, header, map)
 
 // One wave-instruction of keys (lanes with `act`, a contiguous prefix): equal keys on adjacent lanes
 // form runs; the run's first lane adds its length to bin[key] (returning the base when `ret`), every
@@ -108,7 +103,7 @@ constexpr int kHistMax = 1024;             // coarse A buckets the one-pass swee
 // (two-pass fallback), 2: one pass — write them at the tile's upper-bound slot (its forward-range
 // total, the pair tests) and count them; k_compact then packs the tiles.
 template <int kMode>
-__global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(FSLR_SWEEP_WAVES))) void k_sweep(SweepArgs g) {
+__global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(5))) void k_sweep(SweepArgs g) {
   constexpr bool kEmit = kMode != 0;
   constexpr bool kCount = kMode != 1;
   __shared__ int4 rr_all[kSwWaves][kRing];     // ring: index records {start, end, thr, read << 6 | j}
@@ -142,15 +137,21 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(FSLR_S
   // into the next tile, whose records the ring already holds), chunks dealt grid-stride; shorter
   // chunks when there are fewer than kTileRun tiles per wave of the grid (a rank's share of the
   // multi-GPU split), so every wave gets work: the sweep is latency bound
+  // The one-pass sweep (kMode 2) instead gives each wave one contiguous range of tiles of equal cost
+  // (pair tests + kTileCost per tile, k_wave_bounds): a tile's cost varies by orders of magnitude
+  // with the local depth (a dense locus, one chromosome carrying most intervals), and chunks of equal
+  // tile counts left the waves that drew dense chunks running long after the rest
   const int run = max(1, min(kTileRun, nt / nw));
-  const int nchunks = (nt + run - 1) / run;
-  for (int chunk = wid; chunk < nchunks; chunk += nw)
-  for (int tile = chunk * run; tile < min(nt, (chunk + 1) * run); ++tile) {
+  const int nchunks = kMode == 2 ? 1 : (nt + run - 1) / run;
+  for (int chunk = kMode == 2 ? 0 : wid; chunk < nchunks; chunk += kMode == 2 ? 1 : nw) {
+  const int tb = kMode == 2 ? g.wlo[wid] : chunk * run;
+  const int te = kMode == 2 ? g.wlo[wid + 1] : min(nt, (chunk + 1) * run);
+  for (int tile = tb; tile < te; ++tile) {
     const int q0 = tile * kWave;
     const int q = q0 + lane;
     const bool qv = q < g.nq;
     const int qc = qv ? q : q0;
-    const bool first = tile == chunk * run;
+    const bool first = tile == tb;
     const int nf = qv ? g.rng_s[qc].x : 0;
     wave_lds_sync();                             // the previous tile's ring and map reads are done
     if (first) {
@@ -311,6 +312,7 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(FSLR_S
       w_ent += static_cast<unsigned long long>(cnt);
     }
   }
+  }
   if constexpr (kCount) {
     // statistics: plain stores into this wave's slots, summed by k_sweep_total / k_sum_slots
     const unsigned long long f = lane == 0 ? w_tests : lane == 1 ? w_hits : w_ent;
@@ -424,6 +426,24 @@ __global__ __launch_bounds__(1024) void k_sweep_total(const unsigned long long* 
 }
 
 // pair tests of each tile: the sum of its positions' forward counts (an upper bound of its entries)
+// wlo[w] = the first tile whose cost start (tile_ub[t] + t kTileCost, the exclusive cumulative cost)
+// maps to wave w or later, cost scaled to nw waves: each tile writes the boundaries it crosses
+__global__ __launch_bounds__(256) void k_wave_bounds(const long long* __restrict__ ub, const long long* __restrict__ tests,
+                                                     int nt, int nw, int* __restrict__ wlo) {
+  const long long total = ub[nt - 1] + tests[nt - 1] + static_cast<long long>(nt) * kTileCost;
+  auto wave_of = [&](int t) -> int {
+    const long long c = ub[t] + static_cast<long long>(t) * kTileCost;
+    return total > 0 ? static_cast<int>(min(static_cast<long long>(nw - 1), c * nw / total)) : 0;
+  };
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += gridDim.x * blockDim.x) {
+    const int w = t == 0 ? 0 : wave_of(t);
+    const int wp = t == 0 ? -1 : wave_of(t - 1);
+    for (int x = wp + 1; x <= w; ++x) wlo[x] = t;
+    if (t == nt - 1)
+      for (int x = w + 1; x <= nw; ++x) wlo[x] = nt;
+  }
+}
+
 __global__ __launch_bounds__(256) void k_tile_tests(const int2* __restrict__ rng_s, int ni, long long* __restrict__ tests) {
   const int nt = (ni + kWave - 1) / kWave;
   const int lane = lane_id();
@@ -461,9 +481,6 @@ constexpr int kChunk2 = 512;               // a wave's work item: whole runs sta
 constexpr int kStageE = 128;
 constexpr int kHash2 = 128;
 constexpr unsigned kEmpty = 0xFFFFFFFFu;
-#ifdef FSLR_PAIRS_W6
-#define FSLR_PAIR_EDGE_STAGE 128
-#endif
 #ifndef FSLR_PAIR_EDGE_STAGE
 #define FSLR_PAIR_EDGE_STAGE 256
 #endif
@@ -550,11 +567,7 @@ __device__ __forceinline__ unsigned long long group_key(unsigned long long e, in
   return (static_cast<unsigned long long>(r) << 39) | (e & ((1ull << 39) - 1));
 }
 
-#ifdef FSLR_PAIRS_W6
-__global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(6))) void k_sweep_pairs(SweepArgs g) {
-#else
 __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
-#endif
   __shared__ __attribute__((aligned(16))) unsigned long long scr_all[kSwWaves][kScrWords];
   __shared__ int runa_all[kSwWaves][kStageE];                 // per run of the group: A | L_A << 25, edges formed
   __shared__ int runf_all[kSwWaves][kStageE];
@@ -1255,7 +1268,7 @@ __global__ __launch_bounds__(kP2Threads) void k_msd_pass2r(const unsigned long l
 
 // The one-pass sweep's tile slots into their coarse A buckets (k_sweep<2> counted them per block in
 // hist_mat; off = the scan of those counts): block b walks the tiles its k_sweep<2> block swept (same
-// grid, same chunk -> wave deal), so its LDS cursors start at off[bucket][b].  A wave's chunk of <= 8
+// grid, same wave ranges wlo), so its LDS cursors start at off[bucket][b].  Each group of <= 8
 // consecutive tiles is one dense range: lane l holds tile l's count and slot, each loaded entry finds
 // its tile among those lanes; 4 wave-loads are in flight before their cursor atomics.
 __global__ __launch_bounds__(kSwBlock) void k_sweep_scatter(SweepArgs g, const int* __restrict__ off,
@@ -1264,15 +1277,13 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_scatter(SweepArgs g, const i
   for (int i = threadIdx.x; i < g.hist_h; i += kSwBlock) cur[i] = off[static_cast<long long>(i) * gridDim.x + blockIdx.x];
   __syncthreads();
   const int lane = lane_id();
-  const int nt = (g.nq + kWave - 1) / kWave;
-  const int nw = gridDim.x * kSwWaves;
   const int wid = blockIdx.x * kSwWaves + (threadIdx.x >> 6);
-  const int run = max(1, min(kTileRun, nt / nw));   // as k_sweep
-  const int nchunks = (nt + run - 1) / run;
+  const int tb = g.wlo[wid], te = g.wlo[wid + 1];   // the tiles this wave swept (k_sweep<2>)
   constexpr int kU = 4;
-  for (int chunk = wid; chunk < nchunks; chunk += nw) {
-    const int t = chunk * run + lane;
-    const bool tv = lane < run && t < nt;
+  for (int t0 = tb; t0 < te; t0 += kTileRun) {
+    const int run = min(kTileRun, te - t0);
+    const int t = t0 + lane;
+    const bool tv = lane < run;
     const int c = tv ? g.tile_cnt[t] : 0;
     const long long u0 = tv ? g.tile_ub[t] : 0;
     const int inc = wave_incl_scan(c);
@@ -1330,6 +1341,8 @@ int blocks_mode(int m) {
   return m == 0 ? b0 : m == 1 ? b1 : b2;
 }
 int blocks_pairs() { static const int b = resident_blocks(k_sweep_pairs); return b; }
+// the one-pass sweep's grid for nt tiles (k_wave_bounds, k_sweep<2> and k_sweep_scatter share it)
+int sweep_blocks(int nt) { return std::max(1, std::min(blocks_mode(2), (nt + kSwWaves - 1) / kSwWaves)); }
 int tiles_of(const SweepArgs& a) { return static_cast<int>((static_cast<long long>(a.nq) + kWave - 1) / kWave); }
 
 }  // namespace
@@ -1356,7 +1369,12 @@ hipError_t launch_sweep_plan(const SweepArgs& a, hipStream_t s) {
   if (nt == 0) return hipSuccess;
   k_tile_tests<<<grid_for(static_cast<long long>(nt) * kWave, 256, 4096), 256, 0, s>>>(a.rng_s, a.nq, a.tile_tests);
   size_t tb = a.temp_bytes;
-  return hipcub::DeviceScan::ExclusiveSum(a.temp, tb, a.tile_tests, a.tile_ub, nt, s);
+  hipError_t e = hipcub::DeviceScan::ExclusiveSum(a.temp, tb, a.tile_tests, a.tile_ub, nt, s);
+  if (e != hipSuccess) return e;
+  const int nw = sweep_blocks(nt) * kSwWaves;
+  if (!a.wlo || nw > a.wstat_waves) return hipErrorInvalidValue;
+  k_wave_bounds<<<grid_for(nt, 256, 1024), 256, 0, s>>>(a.tile_ub, a.tile_tests, nt, nw, a.wlo);
+  return hipGetLastError();
 }
 
 hipError_t launch_sweep_count(const SweepArgs& a0, int mode, long long* total_dev, hipStream_t s, long long* n_dev,
@@ -1364,7 +1382,7 @@ hipError_t launch_sweep_count(const SweepArgs& a0, int mode, long long* total_de
   const SweepArgs& a = a0;
   const int nt = tiles_of(a);
   if (nt == 0) return hipMemsetAsync(total_dev, 0, 3 * sizeof(long long), s);
-  const int blocks = std::min(blocks_mode(mode), (nt + kSwWaves - 1) / kSwWaves);
+  const int blocks = mode == 2 ? sweep_blocks(nt) : std::min(blocks_mode(mode), (nt + kSwWaves - 1) / kSwWaves);
   if (blocks * kSwWaves > a.wstat_waves) return hipErrorInvalidValue;
   if (a.k0) (void)hipEventRecord(a.k0, s);
   if (mode == 2)
@@ -1413,7 +1431,7 @@ void sweep_coarse_hist(SweepArgs& a) {
   const int nbits = bits_for(std::max(1, a.n_reads - 1));
   const int hb = std::min(nbits, 10);
   const int nt = tiles_of(a);
-  const long long P = std::min(blocks_mode(2), (nt + kSwWaves - 1) / kSwWaves);
+  const long long P = sweep_blocks(nt);
   if (!a.grp || nbits - hb > 14 || (static_cast<long long>(1) << hb) * P > kGrpInts / 2) {
     a.hist_mat = nullptr;
     return;
@@ -1430,7 +1448,7 @@ static hipError_t group_by_a(const SweepArgs& a, int mode, const unsigned long l
   const int nt = tiles_of(a);
   if (mode == 2 && a.hist_mat) {
     // the sweep counted its entries per coarse bucket: scan, scatter, then each bucket by its low bits
-    const int P = std::min(blocks_mode(2), (nt + kSwWaves - 1) / kSwWaves);   // the sweep's grid
+    const int P = sweep_blocks(nt);                                   // the sweep's grid
     const int H = a.hist_h, lo = a.hist_lo;
     int* off = a.grp + kGrpInts / 2;
     size_t tb = a.temp_bytes;
