@@ -174,7 +174,7 @@ def main():
     if world > 1:
         # chromosome-split sweep: this rank indexes and sweeps its chromosomes, routes
         # the match entries to the first read's owner (RCCL all_to_all), evaluates, merges labels
-        shard = SweepShard(ctx, csr.n_reads, chrom_counts_of(csr), world, rank, dev)
+        shard = SweepShard(ctx, csr.n_reads, chrom_counts_of(csr), world, rank, dev, split='auto')
 
     def step(collect=False, repeat=False):
         if shard is not None:
@@ -404,9 +404,11 @@ def main():
                                                         'its contiguous read range, summed'),
                 'edge_cap_bound': capped,
                 'dense_equivalent_pairs_per_s': (n * (n - 1) / 2) / (elapsed / args.steps),
-                'parallelism': f'chromosome-split sweep x{world}: each rank indexes and sweeps its chromosomes, '
-                               'RCCL all_to_all of match entries to the first read\'s owner (64-rank blocks '
-                               'round robin), evaluation there, RCCL label all_gather + union'
+                'parallelism': (f'{shard.split}-split sweep x{world}: each rank indexes and sweeps '
+                                + ('a cost-balanced range of the sorted positions (tests, positions, entries)'
+                                   if shard.split == 'position' else 'its chromosomes')
+                                + ', RCCL all_to_all of match entries to the first read\'s owner (64-rank blocks '
+                                  'round robin), evaluation there, RCCL all_gather of local forests + union')
                 if world > 1 else 'single GPU',
                 'transfer': transfer,
                 'cold_step_ms': cold_ms,

@@ -310,6 +310,7 @@ class Context:
         r = Reads(len(arrs[1]), len(arrs[3]), int(n_chroms), *(_ptr(a) for a in arrs),
                   _ptr(dp) if dp is not None else None)
         self._check(self._L.fslr_set_reads(self._h, ctypes.byref(r)))
+        self._data_order = dp is not None
         if arrs[2].size and (arrs[2].min() < 0 or arrs[2].max() >= (1 << 24)):
             raise ValueError('n_alignments must lie in [0, 2**24) for the device path')
         self.n_reads = len(arrs[1])
@@ -326,6 +327,7 @@ class Context:
         r = Reads(len(arrs[1]), len(arrs[3]), int(csr.n_chroms), *(_ptr(a) for a in arrs),
                   _ptr(dp) if dp is not None else None)
         self._check(self._L.fslr_set_reads_any(self._h, ctypes.byref(r)))
+        self._data_order = dp is not None
         L = np.diff(arrs[0].astype(np.int64))
         self.n_reads = int(len(arrs[1]) + np.maximum((L + FSLR_MAX_L - 1) // FSLR_MAX_L - 1, 0).sum())
         self.n_intervals = len(arrs[3])
@@ -358,7 +360,13 @@ class Context:
                 raise
         self.n_reads = d['n_reads']
         self.n_intervals = d['n_intervals']
+        self._data_order = True
         return d
+
+    def has_data_order(self) -> bool:
+        """The reads came with prepare_data's start-sorted data order (the data-order index build, which
+        the chromosome filter and the position split need)."""
+        return bool(getattr(self, '_data_order', False))
 
     def read_codes(self) -> np.ndarray:
         out = np.empty(self.n_reads, np.int64)

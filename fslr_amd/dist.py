@@ -317,12 +317,17 @@ class SweepShard:
                  owner=None, comm=None, split: str = 'chrom'):
         """``split``: 'chrom' — each rank indexes and sweeps whole chromosomes (largest first onto the
         least-loaded rank); 'position' — each rank sweeps a contiguous range of sorted positions cut where
-        the pair tests balance (position_plan: one chromosome may span ranks), planned from one full
-        index build on the first step.  The edge cap's sharded replay lists its hits on whole
-        chromosomes in both (chrom_owner)."""
+        the work balances (position_plan: pair tests, positions and match entries; one chromosome may
+        span ranks), planned from one full index build and one counting sweep on the first step;
+        'auto' — the position split when it applies (more than one rank, at most 64 chromosomes, the
+        data-order index build), else the chromosome split.  The edge cap's sharded replay lists its
+        hits on whole chromosomes in both (chrom_owner)."""
         import torch
-        if split not in ('chrom', 'position'):
-            raise ValueError(f'split must be chrom or position, not {split!r}')
+        if split not in ('chrom', 'position', 'auto'):
+            raise ValueError(f'split must be chrom, position or auto, not {split!r}')
+        self._auto = split == 'auto'
+        if self._auto:
+            split = 'position' if int(world) > 1 and len(np.asarray(chrom_counts)) <= 64 else 'chrom'
         self.split = split
         self.pos = None                         # (lo, hi, end) of this rank once planned
         self.n_intervals = int(np.asarray(chrom_counts, np.int64).sum())
@@ -351,6 +356,11 @@ class SweepShard:
         ctx = self.ctx
         ctx.set_chrom_filter(None)
         ctx.build_index()
+        if self._auto and not ctx.has_data_order():
+            # no data-order index build (fslr_set_reads_sorted inputs): the chromosome split, on every rank alike
+            self.split = 'chrom'
+            ctx.set_chrom_filter(self.owned if self.world > 1 else None)
+            return
         tests, reach = ctx.position_costs()
         ent = ctx.position_entries(qlen_cut, nal_cut, pass_table, edge_threshold)
         self.plan = position_plan(tests, reach, self.n_intervals, self.world, tile_entries=ent)

@@ -136,7 +136,7 @@ class _Rank:
                     self.ctx.load_csr(csr, thr)
                     self.ctx.reserve_edges(max(1 << 16, 12 * csr.n_reads // self.world))
                     shard = SweepShard(self.ctx, csr.n_reads, chrom_counts_of(csr), self.world, self.rank, self.dev,
-                                       split=meta.get('split', 'chrom'))
+                                       split=meta.get('split', 'auto'))
                 else:
                     # the query-shard split (dist.PairShard): every rank the full index
                     if long_reads:
@@ -314,7 +314,7 @@ class RankPool:
                                            else f'multi-GPU rank {r} answered {line!r} instead of DONE')
                     del pending[r]
 
-    def query(self, csr, iv_thr, qlen_cut, nal_cut, pass_table, edge_threshold, cutoffs=None, split='chrom') -> dict:
+    def query(self, csr, iv_thr, qlen_cut, nal_cut, pass_table, edge_threshold, cutoffs=None, split='auto') -> dict:
         """One chromosome-split query; returns rank 0's view (labels, edges, fwd, capped, max_fwd, cap,
         backend)."""
         d = os.path.join(self.dir, f'q{self.n_queries}')
@@ -424,7 +424,7 @@ def close_pools():
 
 
 def query(csr, iv_thr, qlen_cut, nal_cut, pass_table, edge_threshold, n_gpus, first_device=0,
-          force_gloo=False, cutoffs=None, split='chrom') -> dict:
+          force_gloo=False, cutoffs=None, split='auto') -> dict:
     """Run the chromosome-split query on ``n_gpus`` ranks of this process's pool; returns rank 0's view:
     ``labels`` (global min-rank labels), ``edges`` (a, b, I, U over all ranks), ``fwd`` (forward
     degrees), ``capped``, ``max_fwd``, ``backend``.  The pool's children start on the first call (or
@@ -432,9 +432,14 @@ def query(csr, iv_thr, qlen_cut, nal_cut, pass_table, edge_threshold, n_gpus, fi
     global last_path
     rlen = np.diff(np.asarray(csr.read_off, np.int64))
     long_reads = bool(rlen.size and rlen.max() > 64)
+    if split == 'auto':                       # SweepShard's resolution of 'auto'
+        split = ('position' if int(n_gpus) > 1 and int(csr.n_chroms) <= 64 and getattr(csr, 'start_sorted', True)
+                 else 'chrom')
     last_path = 'sweep-' + split if sweep_applies(csr, iv_thr) and not long_reads else ('long' if long_reads else 'walk')
-    return pool(n_gpus, first_device, force_gloo).query(csr, iv_thr, qlen_cut, nal_cut, pass_table, edge_threshold,
-                                                        cutoffs=cutoffs, split=split)
+    res = pool(n_gpus, first_device, force_gloo).query(csr, iv_thr, qlen_cut, nal_cut, pass_table, edge_threshold,
+                                                       cutoffs=cutoffs, split=split)
+    last_path = res.get('path') or last_path
+    return res
 
 
 last_path = None           # the split the last multi-GPU query took (tests: no one-GPU fallback)

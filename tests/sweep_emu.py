@@ -63,6 +63,9 @@ class EmuSweepContext:
             nf[k] = np.searchsorted(st[k], en[k], side='right') - np.arange(k.size) - 1
         return nf
 
+    def has_data_order(self):
+        return True
+
     def position_costs(self):
         nf = self._n_fwd()
         nt = (nf.size + 63) // 64

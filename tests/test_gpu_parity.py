@@ -157,11 +157,12 @@ def test_cli_multi_gpu_matches_reference_outputs(name):
     multi.last_path = None
     with tempfile.TemporaryDirectory() as tmp:
         res = run_product_cli(name, tmp, '--gpus=2')
-        # every input takes a two-rank split (no one-GPU fallback): the sweep split, or the query-shard
-        # split for overlap <= 0 (edge_cases_p0), aln_size == 0 (zerodiv) and long reads
+        # every input takes a two-rank split (no one-GPU fallback): the position split of the sweep (the
+        # chromosome split beyond 64 chromosomes), or the query-shard split for overlap <= 0
+        # (edge_cases_p0), aln_size == 0 (zerodiv) and long reads
         want_path = {'edge_cases_p0': 'walk', 'zerodiv': 'walk', 'longreads_400': 'long', 'longcap_240': 'long',
                      'zdcap_skip_long': 'long', 'zdcap_raise_long': 'long', 'longreads_p0': 'long',
-                     'longzero_60': 'long'}.get(name, 'sweep-chrom')
+                     'longzero_60': 'long', 'chroms_115': 'sweep-chrom'}.get(name, 'sweep-position')
         assert multi.last_path == want_path, (name, multi.last_path)
         if meta['exception']:
             assert isinstance(res.exception, ZeroDivisionError), (res.output, res.exception)

@@ -60,6 +60,14 @@ if has shard; then
     grep "W=8" $O/shard_$1_$2.log || true
   done
 fi
+if has rehearse; then
+  # the N-rank bench on this one GPU (gloo between ranks, label check)
+  for n in 2 4; do
+    bash tools/rehearse_multi.sh $n > $O/rehearse_$n.out 2>&1 || { echo "rehearse $n failed"; tail -20 $O/rehearse_$n.out; exit 1; }
+    cp gpurun_out/rehearse_$n.json gpurun_out/rehearse_$n.log $O/ 2>/dev/null || true
+    tail -1 $O/rehearse_$n.out
+  done
+fi
 if has shardprof; then
   # kernel trace of the W = 8 per-rank model (chromosome split): where a rank's repeat step goes
   ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/shardprof -o run --output-format csv \
