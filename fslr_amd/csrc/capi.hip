@@ -883,7 +883,7 @@ int fslr_query_shard(fslr_ctx* c, const fslr_params* p, int32_t shard, int32_t n
 // fallback (count, then emit: the sweep runs twice).
 static int sweep_front(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_t a_end, hipEvent_t e0,
                        hipEvent_t e1, SweepArgs& s, int& mode, bool defer = false, bool coarse = false,
-                       bool count_only = false) {
+                       bool count_only = false, int dest_n = 0, int dest_shift = 0) {
   // upper-bound slots (8 B each) the one-pass sweep may use: half the free HBM, at least 2^30; asked
   // only when the slot buffer has to grow (hipMemGetInfo is a driver round trip, kept off repeat queries)
   auto ub_budget = []() {
@@ -951,7 +951,9 @@ static int sweep_front(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64
   for (int k = 0; k < 5; ++k) s.ev[k] = c->prof_phases ? c->sw_ev[k] : nullptr;
   s.ev[0] = nullptr;                                // recorded here, around the sweep pass
   s.hist_mat = nullptr;
+  s.hist_mod = 0;
   if (coarse) sweep_coarse_hist(s);                  // the sweep counts the grouping's coarse buckets
+  if (dest_n > 0) sweep_dest_hist(s, dest_n, dest_shift);   // ... or a partition's destinations
   // the gate ranges depend on the reads and the two cuts only: a repeat query keeps them
   if (c->lb_gen != c->input_gen || c->lb_q != p->qlen_cut || c->lb_n != p->nal_cut) {
     HIP_TRY(c, launch_len_bounds(c->rmeta, 0, static_cast<int>(c->n), p->qlen_cut, p->nal_cut, c->lbounds, c->stream));
@@ -1365,14 +1367,14 @@ int fslr_sweep_partition(fslr_ctx* c, const fslr_params* p, int32_t n_dest, int3
   }
   SweepArgs s{};
   int mode = 2;
-  if (int rc = sweep_front(c, p, 0, c->n, k0, k1, s, mode, true)) return rc;
+  if (int rc = sweep_front(c, p, 0, c->n, k0, k1, s, mode, true, false, false, n_dest, block_shift)) return rc;
   HIP_TRY(c, launch_sweep_partition(s, 2, block_shift, n_dest, out, dst_cap, totals, c->stream));
   if (int rc = read_back()) return rc;
   const volatile long long* st = c->sw_total;
   if (st[2] & 8) {
     if (int rc = prepare_query(c, p)) return rc;
     mode = 2;
-    if (int rc = sweep_front(c, p, 0, c->n, k0, k1, s, mode)) return rc;
+    if (int rc = sweep_front(c, p, 0, c->n, k0, k1, s, mode, false, false, false, n_dest, block_shift)) return rc;
     if (mode == 0) HIP_TRY(c, launch_sweep_dense(s, 0, c->stream));     // dense entries in `ent`
     HIP_TRY(c, launch_sweep_partition(s, mode, block_shift, n_dest, out, dst_cap, totals, c->stream));
     if (int rc = read_back()) return rc;
@@ -1427,7 +1429,7 @@ int fslr_sweep_partition_repeat(fslr_ctx* c, const fslr_params* p, int32_t n_des
   }
   SweepArgs s{};
   int mode = 2;
-  if (int rc = sweep_front(c, p, 0, c->n, k0, k1, s, mode, true)) return rc;
+  if (int rc = sweep_front(c, p, 0, c->n, k0, k1, s, mode, true, false, false, n_dest, block_shift)) return rc;
   HIP_TRY(c, launch_sweep_partition(s, 2, block_shift, n_dest, static_cast<unsigned long long*>(dst), dst_cap,
                                     c->part_cnt, c->stream));
   PartExpect ex{};

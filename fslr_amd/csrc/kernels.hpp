@@ -196,6 +196,7 @@ struct SweepArgs {
   int* hist_mat;                      // (mode 2, one GPU) k_sweep<2> writes [bucket][block] counts of the
                                       // coarse A buckets A >> hist_lo here (null: the grouping counts them)
   int hist_lo, hist_h;                // coarse bucket shift and count (<= sweep_hist_max())
+  int hist_mod;                       // 1: bucket = (A >> hist_lo) % hist_h (a partition's destinations)
   long long n_ent;                    // (emit / pairs) entries of the count pass (host; with n_dev: an estimate)
   const long long* n_dev;             // null, or the device word holding the count (sync-free repeat query)
   long long ent_cap;                  // capacity of ent / ent_sorted (grouping-sort scatter bound)
@@ -233,6 +234,8 @@ int grp_ints();
 // the one-GPU sweep counts its entries per coarse A bucket while it writes them (no grouping count
 // pass): sets a.hist_mat / hist_lo / hist_h for the input's read count
 void sweep_coarse_hist(SweepArgs& a);
+// the partition's variant: the sweep counts its entries per destination (A >> shift) % n_dest
+void sweep_dest_hist(SweepArgs& a, int n_dest, int shift);
 // multi-GPU: the sweep's entries (mode 2: in the tile slots; 0: dense in a.ent) grouped by destination
 // (A >> shift) % n_dest into dst (entries beyond dst_cap dropped); totals[k] (device) per destination
 hipError_t launch_sweep_partition(const SweepArgs& a, int mode, int shift, int n_dest, unsigned long long* dst,

@@ -204,7 +204,10 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(5))) v
       const bool act = lane < sn;
       const unsigned long long v = act ? ST[lane] : 0ull;
       if (act) dst[out + lane] = v;
-      if (do_hist) run_add<false>(hist_s, static_cast<int>(static_cast<unsigned>(v >> 39) >> g.hist_lo), act, lane);
+      if (do_hist) {
+        const unsigned b = static_cast<unsigned>(v >> 39) >> g.hist_lo;
+        run_add<false>(hist_s, static_cast<int>(g.hist_mod ? b % static_cast<unsigned>(g.hist_h) : b), act, lane);
+      }
     };
     if constexpr (kCount) w_tests += static_cast<unsigned long long>(T);
     for (int seg = 0; seg < T; seg += kMapCap) {
@@ -1308,7 +1311,9 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_scatter(SweepArgs g, const i
       for (int q = 0; q < kU; ++q) {
         if (k0 + q * kWave >= T) break;               // wave-uniform
         const bool act = k0 + q * kWave + lane < T;
-        const int p = run_add<true>(cur, static_cast<int>(static_cast<unsigned>(v[q] >> 39) >> g.hist_lo), act, lane);
+        const unsigned bk = static_cast<unsigned>(v[q] >> 39) >> g.hist_lo;
+        const int p = run_add<true>(cur, static_cast<int>(g.hist_mod ? bk % static_cast<unsigned>(g.hist_h) : bk), act,
+                                    lane);
         if (act && p < cap) dst[p] = v[q];
       }
     }
@@ -1429,6 +1434,19 @@ hipError_t launch_sweep_dense(const SweepArgs& a, int mode, hipStream_t s) {
 
 int grp_ints() { return kGrpInts; }
 
+void sweep_dest_hist(SweepArgs& a, int n_dest, int shift) {
+  const int nt = tiles_of(a);
+  const long long P = sweep_blocks(nt);
+  if (!a.grp || n_dest < 1 || n_dest > kHistMax || static_cast<long long>(n_dest) * P > kGrpInts / 2) {
+    a.hist_mat = nullptr;
+    return;
+  }
+  a.hist_mat = a.grp;
+  a.hist_h = n_dest;
+  a.hist_lo = shift;
+  a.hist_mod = 1;
+}
+
 void sweep_coarse_hist(SweepArgs& a) {
   // at most kHistMax buckets; the rest of A's bits (<= 14 for 2^24 reads) are pass 2's LDS bins
   const int nbits = bits_for(std::max(1, a.n_reads - 1));
@@ -1442,6 +1460,7 @@ void sweep_coarse_hist(SweepArgs& a) {
   a.hist_mat = a.grp;
   a.hist_h = 1 << hb;
   a.hist_lo = nbits - hb;
+  a.hist_mod = 0;
 }
 
 // group the entries by A: from the tile slots (mode 2) or dense `src` into `mid`, then into `out`
@@ -1507,10 +1526,20 @@ __global__ void k_dest_totals(const int* __restrict__ mat, const int* __restrict
 hipError_t launch_sweep_partition(const SweepArgs& a, int mode, int shift, int n_dest, unsigned long long* dst,
                                   long long dst_cap, long long* totals, hipStream_t s) {
   if (n_dest < 1 || n_dest > kMsdMaxH) return hipErrorInvalidValue;
-  const int P = kMsdMaxBlocks;
   int* mat = a.grp;
   int* off = a.grp + kGrpInts / 2;
   const int nt = tiles_of(a);
+  if (mode == 2 && a.hist_mat && a.hist_mod && a.hist_h == n_dest && a.hist_lo == shift) {
+    // the sweep counted its entries per destination: scan, totals, one scatter over its wave ranges
+    const int P = sweep_blocks(nt);
+    size_t tb = a.temp_bytes;
+    hipError_t e = hipcub::DeviceScan::ExclusiveSum(a.temp, tb, mat, off, n_dest * P, s);
+    if (e != hipSuccess) return e;
+    k_dest_totals<<<1, 64, 0, s>>>(mat, off, n_dest, P, totals);
+    k_sweep_scatter<<<P, kSwBlock, 0, s>>>(a, off, dst, dst_cap);
+    return hipGetLastError();
+  }
+  const int P = kMsdMaxBlocks;
   const long long n = a.n_ent;
   if (mode == 2)
     k_msd_pass1<true, false, true><<<P, kMsdThreads, 0, s>>>(a.ent_ub, a.ub_cap, a.tile_ub, a.tile_cnt, nt, shift, n_dest,
