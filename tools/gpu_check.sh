@@ -60,6 +60,19 @@ if has shard; then
     grep "W=8" $O/shard_$1_$2.log || true
   done
 fi
+if has cfg5; then
+  # cfg5 on one GPU under rocprof: the sweep query + the cap replay, checked against the oracle's digests
+  ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/cfg5prof -o run --output-format csv \
+      -- python3 $R/tools/cfg5_cap.py --reps 3 > $O/cfg5_cap.json 2> $O/cfg5_cap.log ) || { echo "cfg5 failed"; tail -20 $O/cfg5_cap.log; exit 1; }
+  f=$(find $O/cfg5prof -name 'run_kernel_stats.csv' | head -1); cp $f $O/cfg5_kernel_stats.csv
+  tail -3 $O/cfg5_cap.log
+  python3 - $O/cfg5_kernel_stats.csv <<'PY'
+import csv, re, sys
+for r in list(csv.DictReader(open(sys.argv[1])))[:12]:
+    n = re.sub(r'^void ', '', r['Name'].replace('(anonymous namespace)::', '')); i = n.find('('); n = n[:i] if i > 0 else n
+    print(f"   {float(r['AverageNs'])/1000:9.1f} us  x{r['Calls']:>4}  {n[:80]}")
+PY
+fi
 if has rehearse; then
   # the N-rank bench on this one GPU (gloo between ranks, label check)
   for n in 2 4; do
