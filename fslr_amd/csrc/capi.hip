@@ -59,6 +59,7 @@ int ensure_capacity(fslr_ctx* c, int64_t n, int64_t ni, int n_chroms) {
     if ((rc = dalloc(c, &c->counters, kNumCounters))) return rc;
     if ((rc = alloc_errw(c, kZdListInit))) return rc;
     if ((rc = dalloc(c, &c->forest_cnt, 1))) return rc;
+    if ((rc = dalloc(c, &c->forest_blk, 1024))) return rc;
     // no query yet: no edges, no errors (fslr_components before any query gives singleton labels)
     HIP_TRY(c, hipMemsetAsync(c->counters, 0, kNumCounters * sizeof(unsigned long long), c->stream));
   }
@@ -164,7 +165,7 @@ void fslr_ctx_destroy(fslr_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void* bufs[] = {c->rmeta,  c->rlen8, c->iv,     c->qpos,    c->rng_s,  c->idx4,    c->idx_gate, c->data_pos, c->s_start,
                   c->crange, c->keys,   c->keys2,   c->vals,    c->vals2,   c->endkey,  c->pmaxkey,
-                  c->temp,   c->umax,   c->edges,   c->edge_iu, c->fwd,     c->parent,  c->counters, c->forest, c->forest_cnt,
+                  c->temp,   c->umax,   c->edges,   c->edge_iu, c->fwd,     c->parent,  c->counters, c->forest, c->forest_cnt, c->forest_blk,
                   c->upl,    c->upl64,
                   c->errw,   c->thr_tmp, c->defer,   c->dchrom,  c->drec,    c->lbounds, c->diag, c->wstat,
                   c->dgate,  c->chist,  c->heavy, c->ent, c->ent_sorted, c->sweep_temp, c->sw_tile, c->sw_wstat, c->sw_wlo, c->ent_ub,
@@ -1754,7 +1755,7 @@ int fslr_local_forest(fslr_ctx* c, int64_t* n_pairs) {
   const int nr = static_cast<int>(c->n);
   HIP_TRY(c, launch_uf_init(c->parent, nr, s));
   if (c->edge_cap) HIP_TRY(c, launch_uf_edges(c->parent, c->edges, c->counters, c->edge_cap, c->errw, s));
-  HIP_TRY(c, launch_forest_fused(c->parent, nr, c->forest, c->forest_cnt, s));
+  HIP_TRY(c, launch_forest_pairs(c->parent, nr, c->forest, c->forest_cnt, c->forest_blk, s));   // finalizes too
   if (n_pairs) {
     unsigned long long k = 0;
     HIP_TRY(c, hipMemcpyAsync(&k, c->forest_cnt, sizeof(k), hipMemcpyDeviceToHost, s));

@@ -101,7 +101,6 @@ __global__ void k_copy_edges(const int2* __restrict__ edges, const unsigned long
     out[k] = k < ne ? edges[k] : make_int2(-1, -1);
 }
 
-
 // find without path halving: the finalize pass's only store is each node's own root.  (With
 // halving here, another thread's late halving store into p[x] — an ancestor that is not the root —
 // could land after x's own root store and leave x labelled with a non-root.)
@@ -113,31 +112,72 @@ __device__ int uf_root(int* p, int x) {
   }
 }
 
+// A finalized forest's (read, root) pairs of the reads that are not their own root, in read order (the
+// multi-GPU merge exchanges these instead of the raw edges: unions of the same partition).  A stream
+// compaction without contended atomics: each block counts its contiguous range, one block scans the
+// counts, each block writes its range at its offset.
+constexpr int kForestBlocks = 1024;
+
+// (finalize fused: each read's root is found and stored here, so k_forest_write reads final parents)
+__global__ __launch_bounds__(256) void k_forest_count(int* __restrict__ p, int n, int chunk, int* __restrict__ bcnt) {
+  __shared__ int ws[4];
+  const int b0 = blockIdx.x * chunk, b1 = min(n, b0 + chunk);
+  int c = 0;
+  for (int x = b0 + static_cast<int>(threadIdx.x); x < b1; x += blockDim.x) {
+    const int r = uf_root(p, x);
+    st_rlx(p + x, r);
+    c += r != x;
+  }
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) bcnt[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+// exclusive scan of the block counts in place (nb <= kForestBlocks), the total into *cnt
+__global__ __launch_bounds__(kForestBlocks) void k_forest_scan(int* __restrict__ bcnt, int nb,
+                                                               unsigned long long* __restrict__ cnt) {
+  __shared__ int v[kForestBlocks];
+  const int t = threadIdx.x;
+  v[t] = t < nb ? bcnt[t] : 0;
+  __syncthreads();
+  for (int o = 1; o < kForestBlocks; o <<= 1) {
+    const int add = t >= o ? v[t - o] : 0;
+    __syncthreads();
+    v[t] += add;
+    __syncthreads();
+  }
+  if (t < nb) bcnt[t] = t ? v[t - 1] : 0;
+  if (t == kForestBlocks - 1) *cnt = static_cast<unsigned long long>(v[t]);
+}
+
+__global__ __launch_bounds__(256) void k_forest_write(const int* __restrict__ p, int n, int chunk,
+                                                      const int* __restrict__ bcnt, int2* __restrict__ out) {
+  __shared__ int ws[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int b0 = blockIdx.x * chunk, b1 = min(n, b0 + chunk);
+  int base = bcnt[blockIdx.x];
+  for (int x0 = b0; x0 < b1; x0 += blockDim.x) {
+    const int x = x0 + static_cast<int>(threadIdx.x);
+    const int r = x < b1 ? p[x] : x;
+    const bool t = r != x;
+    const unsigned long long m = __ballot(t);
+    if (lane == 0) ws[w] = __popcll(m);
+    __syncthreads();
+    int before = 0, total = 0;
+    for (int k = 0; k < 4; ++k) {
+      before += k < w ? ws[k] : 0;
+      total += ws[k];
+    }
+    if (t) out[base + before + __popcll(m & ((1ull << lane) - 1ull))] = make_int2(x, r);
+    base += total;
+    __syncthreads();
+  }
+}
+
 __global__ void k_uf_finalize(int* p, int n) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
     st_rlx(p + i, uf_root(p, i));
-}
-
-// finalize + the local forest in one pass (the multi-GPU merge takes the pairs as a set): every read
-// gets its root; the (read, root) pairs of the reads that are not their own root are appended through
-// one atomic per wave
-__global__ __launch_bounds__(256) void k_forest_fused(int* p, int n, int2* __restrict__ out,
-                                                      unsigned long long* __restrict__ cnt) {
-  const int lane = threadIdx.x & 63;
-  const int stride = gridDim.x * blockDim.x;
-  for (int x0 = blockIdx.x * blockDim.x; x0 < n; x0 += stride) {
-    const int x = x0 + static_cast<int>(threadIdx.x);
-    const bool v = x < n;
-    const int r = v ? uf_root(p, x) : 0;
-    if (v) st_rlx(p + x, r);
-    const bool t = v && r != x;
-    const unsigned long long m = __ballot(t);
-    if (!m) continue;
-    unsigned long long base = 0;
-    if (lane == 0) base = atomicAdd(cnt, static_cast<unsigned long long>(__popcll(m)));
-    base = __shfl(base, 0);
-    if (t) out[base + __popcll(m & ((1ull << lane) - 1))] = make_int2(x, r);
-  }
 }
 
 }  // namespace
@@ -189,13 +229,14 @@ hipError_t launch_copy_edges(const int2* edges, const unsigned long long* count,
   return hipGetLastError();
 }
 
-hipError_t launch_forest_fused(int* parent, int n, int2* out, unsigned long long* cnt, hipStream_t s) {
-  hipError_t e = hipMemsetAsync(cnt, 0, sizeof(unsigned long long), s);
-  if (e != hipSuccess) return e;
-  if (n > 0) k_forest_fused<<<grid_for(n), 256, 0, s>>>(parent, n, out, cnt);
+hipError_t launch_forest_pairs(int* parent, int n, int2* out, unsigned long long* cnt, int* bcnt, hipStream_t s) {
+  const int chunk = std::max(256, (n + kForestBlocks - 1) / kForestBlocks);
+  const int nb = std::max(1, (n + chunk - 1) / chunk);
+  k_forest_count<<<nb, 256, 0, s>>>(parent, n, chunk, bcnt);
+  k_forest_scan<<<1, kForestBlocks, 0, s>>>(bcnt, nb, cnt);
+  k_forest_write<<<nb, 256, 0, s>>>(parent, n, chunk, bcnt, out);
   return hipGetLastError();
 }
-
 
 hipError_t launch_uf_finalize(int* parent, int n, hipStream_t s) {
   if (n > 0) k_uf_finalize<<<grid_for(n), 256, 0, s>>>(parent, n);

@@ -101,6 +101,7 @@ struct fslr_ctx {
   int64_t upl64_cap = 0;
   int2* forest = nullptr;                    // [n] the local forest's (read, root) pairs (fslr_local_forest)
   unsigned long long* forest_cnt = nullptr;  // [1] their count (device)
+  int* forest_blk = nullptr;                 // [1024] compaction scratch
   unsigned long long* counters = nullptr;
   unsigned long long* wstat = nullptr;       // [wstat_waves x kWStride] per-wave statistics of the pair kernel
   int wstat_waves = 0;

@@ -211,7 +211,6 @@ struct SweepArgs {
   unsigned long long* wstat;          // per-wave statistics slots [waves x 4] (no contended atomics)
   int wstat_waves;
   int* wlo;                           // (one-pass sweep) [waves + 1]: wave w sweeps tiles [wlo[w], wlo[w + 1])
-  int chunk2;                         // (pair stage) entries per work item, set by launch_sweep_pairs
 
   hipEvent_t ev[5];                   // (profiling) count | scan | emit | sort | pairs boundaries, or null
   hipEvent_t k0, k1;                  // (profiling) around the sweep kernel launch alone, or null
@@ -326,8 +325,8 @@ hipError_t launch_uf_finalize(int* parent, int n, hipStream_t s);
 hipError_t launch_uf_pair_list(int* parent, const int2* pairs, long long n, hipStream_t s);
 // (x, parent[x]) for every x of a finalized forest with parent[x] != x, in x order; *cnt = their count;
 // bcnt: [1024] scratch
-// finalize + the forest pairs in one launch, in no particular order (cnt zeroed first)
-hipError_t launch_forest_fused(int* parent, int n, int2* out, unsigned long long* cnt, hipStream_t s);
+// the finalized forest's (read, root) pairs in read order (finalizes parent on the way); *cnt = their count
+hipError_t launch_forest_pairs(int* parent, int n, int2* out, unsigned long long* cnt, int* bcnt, hipStream_t s);
 // union of k and vals[w * stride + k] for k < n, w < blocks
 hipError_t launch_uf_strided(int* parent, const int* vals, long long blocks, int n, long long stride, hipStream_t s);
 hipError_t launch_copy_edges(const int2* edges, const unsigned long long* count, long long cap, int2* out,

@@ -471,8 +471,8 @@ __global__ __launch_bounds__(256) void k_compact(const unsigned long long* __res
 }
 
 // ---- 3. pairs from the entries grouped by A ------------------------------------------------------
-// Work item: a chunk of g.chunk2 sorted entries (kChunk2, fewer when the grid would otherwise get less
-// than ~4 chunks per wave: a rank's share of the multi-GPU split); the runs (reads A) that start in it.  Whole runs are
+// Work item: a chunk of kChunk2 sorted entries; the runs (reads A) that start in it.  (Smaller chunks
+// for a rank's small share measured slower: 112 vs 103 us mean, profiles/r05/r5l.)  Whole runs are
 // taken a group of at most kStageE entries at a time (two per lane, in registers) and sorted by
 // (run, B, i, j) with a wave-wide bitonic network: each read pair's entries become one segment, in
 // the reference's row order.  Per segment (one lane each): I = its entry count unless two entries
@@ -481,8 +481,7 @@ __global__ __launch_bounds__(256) void k_compact(const unsigned long long* __res
 // lowest unused column, cluster.py:152-161).  A run longer than the stage is evaluated alone,
 // streamed from HBM, through an LDS hash over its partners in partner partitions (pass k takes the
 // partners with part(B) == k).
-constexpr int kChunk2 = 512;               // a wave's work item: whole runs starting in it (at most)
-constexpr int kChunk2Min = 128;
+constexpr int kChunk2 = 512;               // a wave's work item: whole runs starting in it
 constexpr int kStageE = 128;
 constexpr int kHash2 = 128;
 constexpr unsigned kEmpty = 0xFFFFFFFFu;
@@ -601,8 +600,7 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
   const long long n = g.n_dev ? *g.n_dev : g.n_ent;
   const unsigned long long* E = g.ent_sorted;
   const unsigned char* RL = g.rlen8;
-  const int chunk2 = g.chunk2;
-  const long long nchunks = (n + chunk2 - 1) / chunk2;
+  const long long nchunks = (n + kChunk2 - 1) / kChunk2;
   const long long nw = static_cast<long long>(gridDim.x) * kSwWaves;
   const int wid = blockIdx.x * kSwWaves + wv;
   int w_maxfwd = 0;
@@ -766,7 +764,7 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
 #define FSLR_PCK(k) do { } while (0)
 #endif
   for (long long c = wid; c < nchunks; c += nw) {
-    const long long c0 = c * chunk2, c1 = min(c0 + chunk2, n);
+    const long long c0 = c * kChunk2, c1 = min(c0 + kChunk2, n);
     long long s = c0;
     if (s > 0) s = next_run(s, c1, a_at(s - 1));       // the run in progress belongs to the previous chunk
     unsigned long long e0 = ~0ull, e1 = ~0ull, en = ~0ull;
@@ -1590,11 +1588,7 @@ hipError_t launch_sweep_pairs(const SweepArgs& a0, int mode, hipStream_t s) {
     if (e != hipSuccess) return e;
   }
   if (a.ev[4]) (void)hipEventRecord(a.ev[4], s);
-  // ~4 chunks per wave of the resident grid at least (a small entry set in chunks of 512 leaves each
-  // wave one chunk, and the slowest chunk is the kernel)
-  const long long per = a.n_ent / (static_cast<long long>(blocks_pairs()) * kSwWaves * 4);
-  a.chunk2 = static_cast<int>(std::max<long long>(kChunk2Min, std::min<long long>(kChunk2, per)));
-  const long long chunks = (a.n_ent + a.chunk2 - 1) / a.chunk2;
+  const long long chunks = (a.n_ent + kChunk2 - 1) / kChunk2;
   const int blocks = static_cast<int>(std::max(1ll, std::min<long long>(blocks_pairs(), (chunks + kSwWaves - 1) / kSwWaves)));
   if (blocks * kSwWaves > a.wstat_waves) return hipErrorInvalidValue;
   if (a.p0) (void)hipEventRecord(a.p0, s);
