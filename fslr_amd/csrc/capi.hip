@@ -955,6 +955,7 @@ static int sweep_front(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64
   s.hist_mod = 0;
   if (coarse) sweep_coarse_hist(s);                  // the sweep counts the grouping's coarse buckets
   if (dest_n > 0) sweep_dest_hist(s, dest_n, dest_shift);   // ... or a partition's destinations
+  s.dest_totals = dest_n > 0 ? c->part_cnt : nullptr;
   // the gate ranges depend on the reads and the two cuts only: a repeat query keeps them
   if (c->lb_gen != c->input_gen || c->lb_q != p->qlen_cut || c->lb_n != p->nal_cut) {
     HIP_TRY(c, launch_len_bounds(c->rmeta, 0, static_cast<int>(c->n), p->qlen_cut, p->nal_cut, c->lbounds, c->stream));

@@ -63,6 +63,21 @@ __global__ void k_uf_edges(int* p, const int2* __restrict__ edges, const unsigne
   }
 }
 
+#ifdef FSLR_UF_MIN
+// from the identity: every read points to its smallest neighbour below it (one atomicMin per edge, no
+// finds), a forest of the same components' partial unions; the unions over every edge follow
+__global__ void k_uf_hook_min(int* p, const int2* __restrict__ edges, const unsigned long long* __restrict__ count,
+                              long long cap) {
+  const long long ne = min(static_cast<long long>(*count), cap);
+  for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < ne;
+       k += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const int2 e = edges[k];
+    const int lo = min(e.x, e.y), hi = max(e.x, e.y);
+    if (lo != hi) atomicMin(p + hi, lo);
+  }
+}
+#endif
+
 __global__ void k_uf_pairs(int* p, const int* __restrict__ src, const int* __restrict__ dst, long long n,
                            int period) {
   for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < n;
@@ -204,6 +219,9 @@ hipError_t launch_uf_init(int* parent, int n, hipStream_t s) {
 
 hipError_t launch_uf_edges(int* parent, const int2* edges, const unsigned long long* count, long long cap, int* err,
                            hipStream_t s) {
+#ifdef FSLR_UF_MIN
+  if (cap > 0) k_uf_hook_min<<<grid_for(cap), 256, 0, s>>>(parent, edges, count, cap);
+#endif
   if (cap > 0) k_uf_edges<<<grid_for(cap), 256, 0, s>>>(parent, edges, count, cap, err);
   return hipGetLastError();
 }

@@ -197,6 +197,7 @@ struct SweepArgs {
                                       // coarse A buckets A >> hist_lo here (null: the grouping counts them)
   int hist_lo, hist_h;                // coarse bucket shift and count (<= sweep_hist_max())
   int hist_mod;                       // 1: bucket = (A >> hist_lo) % hist_h (a partition's destinations)
+  long long* dest_totals;             // (partition) per destination entry totals, filled by k_sweep_total when small
   long long n_ent;                    // (emit / pairs) entries of the count pass (host; with n_dev: an estimate)
   const long long* n_dev;             // null, or the device word holding the count (sync-free repeat query)
   long long ent_cap;                  // capacity of ent / ent_sorted (grouping-sort scatter bound)

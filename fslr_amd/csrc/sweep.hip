@@ -388,8 +388,10 @@ __global__ __launch_bounds__(1024) void k_sweep_total(const unsigned long long* 
                                                       const long long* __restrict__ ub,
                                                       const long long* __restrict__ tests, int nt,
                                                       unsigned long long* counters, int* err, long long* total,
-                                                      long long* n_dev, long long cap) {
+                                                      long long* n_dev, long long cap, const int* __restrict__ mat,
+                                                      int* __restrict__ off, int H, int P, long long* __restrict__ dtot) {
   __shared__ unsigned long long part[16][3];
+  __shared__ int wsum[16];
   unsigned long long a0 = 0, a1 = 0, a2 = 0;
   for (int w = threadIdx.x; w < nwaves; w += 1024) {
     a0 += ws[static_cast<long long>(w) * kWsFields];
@@ -425,6 +427,29 @@ __global__ __launch_bounds__(1024) void k_sweep_total(const unsigned long long* 
       if (t > cap) atomicOr(&err[kErrOverflow], 16);
     }
     total[2] = err[kErrOverflow];
+  }
+  if (mat) {
+    // a small partition's [destination][block] counts: their exclusive scan and each destination's
+    // total here (instead of a two-kernel device scan and a totals kernel)
+    const int N = H * P;
+    const int per = (N + 1023) / 1024;
+    const int first = static_cast<int>(threadIdx.x) * per;
+    int loc = 0;
+    for (int i = 0; i < per && first + i < N; ++i) loc += mat[first + i];
+    const int inc = wave_incl_scan(loc);
+    if (lane == kWave - 1) wsum[w] = inc;
+    __syncthreads();
+    int base = inc - loc;
+    for (int x = 0; x < w; ++x) base += wsum[x];
+    for (int i = 0; i < per && first + i < N; ++i) {
+      off[first + i] = base;
+      base += mat[first + i];
+    }
+    __syncthreads();
+    if (static_cast<int>(threadIdx.x) < H) {
+      const long long k0 = static_cast<long long>(threadIdx.x) * P, k1 = k0 + P - 1;
+      dtot[threadIdx.x] = static_cast<long long>(off[k1]) + mat[k1] - off[k0];
+    }
   }
 }
 
@@ -1350,6 +1375,11 @@ int blocks_pairs() { static const int b = resident_blocks(k_sweep_pairs); return
 // the one-pass sweep's grid for nt tiles (k_wave_bounds, k_sweep<2> and k_sweep_scatter share it)
 int sweep_blocks(int nt) { return std::max(1, std::min(blocks_mode(2), (nt + kSwWaves - 1) / kSwWaves)); }
 int tiles_of(const SweepArgs& a) { return static_cast<int>((static_cast<long long>(a.nq) + kWave - 1) / kWave); }
+// a partition's destination counts are scanned inside k_sweep_total when they are few (<= 64K)
+bool dest_scan_fused(const SweepArgs& a, int blocks) {
+  return a.hist_mat && a.hist_mod && a.dest_totals && static_cast<long long>(a.hist_h) * blocks <= 65536 &&
+         a.hist_h <= 1024;
+}
 
 }  // namespace
 
@@ -1397,8 +1427,10 @@ hipError_t launch_sweep_count(const SweepArgs& a0, int mode, long long* total_de
     k_sweep<0><<<blocks, kSwBlock, 0, s>>>(a);
   if (a.k1) (void)hipEventRecord(a.k1, s);
   if (mode == 2) {
+    const bool fuse = dest_scan_fused(a, blocks);
     k_sweep_total<<<1, 1024, 0, s>>>(a.wstat, blocks * kSwWaves, a.tile_ub, a.tile_tests, nt, a.counters, a.err,
-                                     total_dev, n_dev, cap);
+                                     total_dev, n_dev, cap, fuse ? a.hist_mat : nullptr, a.grp + kGrpInts / 2,
+                                     a.hist_h, blocks, a.dest_totals);
     if (a.ev[1]) (void)hipEventRecord(a.ev[1], s);
     return hipGetLastError();
   }
@@ -1530,10 +1562,12 @@ hipError_t launch_sweep_partition(const SweepArgs& a, int mode, int shift, int n
   if (mode == 2 && a.hist_mat && a.hist_mod && a.hist_h == n_dest && a.hist_lo == shift) {
     // the sweep counted its entries per destination: scan, totals, one scatter over its wave ranges
     const int P = sweep_blocks(nt);
-    size_t tb = a.temp_bytes;
-    hipError_t e = hipcub::DeviceScan::ExclusiveSum(a.temp, tb, mat, off, n_dest * P, s);
-    if (e != hipSuccess) return e;
-    k_dest_totals<<<1, 64, 0, s>>>(mat, off, n_dest, P, totals);
+    if (!(dest_scan_fused(a, P) && a.dest_totals == totals)) {   // else k_sweep_total scanned them
+      size_t tb = a.temp_bytes;
+      hipError_t e = hipcub::DeviceScan::ExclusiveSum(a.temp, tb, mat, off, n_dest * P, s);
+      if (e != hipSuccess) return e;
+      k_dest_totals<<<1, 64, 0, s>>>(mat, off, n_dest, P, totals);
+    }
     k_sweep_scatter<<<P, kSwBlock, 0, s>>>(a, off, dst, dst_cap);
     return hipGetLastError();
   }
