@@ -141,6 +141,15 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(5))) v
   // (pair tests + kTileCost per tile, k_wave_bounds): a tile's cost varies by orders of magnitude
   // with the local depth (a dense locus, one chromosome carrying most intervals), and chunks of equal
   // tile counts left the waves that drew dense chunks running long after the rest
+#ifdef FSLR_SWEEP_CLOCK
+  // measurement build: wave-clock sums (kMode 2) of the tile header, the item maps, the steps and the
+  // tail into counters 68..71
+  unsigned long long sck[4] = {0, 0, 0, 0};
+  long long stk = clock64();
+#define FSLR_SCK(k) do { if (kMode == 2) { const long long t_ = clock64(); sck[k] += t_ - stk; stk = t_; } } while (0)
+#else
+#define FSLR_SCK(k) do { } while (0)
+#endif
   const int run = max(1, min(kTileRun, nt / nw));
   const int nchunks = kMode == 2 ? 1 : (nt + run - 1) / run;
   for (int chunk = kMode == 2 ? 0 : wid; chunk < nchunks; chunk += kMode == 2 ? 1 : nw) {
@@ -210,12 +219,14 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(5))) v
       }
     };
     if constexpr (kCount) w_tests += static_cast<unsigned long long>(T);
+    FSLR_SCK(3);
     for (int seg = 0; seg < T; seg += kMapCap) {
       const int se = min(T, seg + kMapCap);
       wave_lds_sync();
       for (int r = max(ex, seg); r < min(pre, se); ++r)
         MAP[r - seg] = static_cast<unsigned short>(lane | min(r - ex + lane + 1, kRing) << 6);
       wave_lds_sync();
+      FSLR_SCK(1);
       // step operands: the mapped lane's gate ranges, q's record (ring), p's record and gate word
       // (ring; global beyond it)
       struct Step {
@@ -306,6 +317,7 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(5))) v
         if (any_zero) run_steps(std::true_type{}, std::false_type{});
         else run_steps(std::false_type{}, std::false_type{});
       }
+      FSLR_SCK(2);
     }
     if constexpr (kEmit) {
       if (sn > 0) flush();
@@ -314,8 +326,14 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(5))) v
       if (lane == 0) g.tile_cnt[tile] = cnt;
       w_ent += static_cast<unsigned long long>(cnt);
     }
+    FSLR_SCK(0);                                 // (the tail, counted with the next tile's header)
   }
   }
+#ifdef FSLR_SWEEP_CLOCK
+  if (kMode == 2 && lane == 0)
+    for (int k = 0; k < 4; ++k) atomicAdd(&g.counters[68 + k], sck[k]);
+#endif
+#undef FSLR_SCK
   if constexpr (kCount) {
     // statistics: plain stores into this wave's slots, summed by k_sweep_total / k_sum_slots
     const unsigned long long f = lane == 0 ? w_tests : lane == 1 ? w_hits : w_ent;
