@@ -234,9 +234,8 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(5))) v
         int4 b4, a4, rp;
         int2 gp;
       };
-      // kFits: every pair of the tile has its p in the ring (the usual case), so the step reads LDS
-      // only; otherwise a lane beyond the ring reads the index in global memory (a per-lane choice
-      // of address: one flat load for the whole step)
+      // kFits: every pair of the tile has its p in the ring (the usual case at cfg3), so the step
+      // reads LDS only; otherwise (a deep locus: cfg5's ~50x coverage) it reads global memory only
       auto step_load = [&](auto fits_tag, int base, Step& t) __attribute__((always_inline)) {
         constexpr bool kFits = decltype(fits_tag)::value;
         const int r = base + lane;
@@ -245,10 +244,12 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(5))) v
         const int d = static_cast<int>(md >> 6);
         t.b4 = QB[t.mi];
         t.a4 = RR[(q0 + t.mi) & kRingMask];
-        if (kFits || d < kRing) {
+        if (kFits) {
           t.rp = RR[(q0 + d) & kRingMask];
           t.gp = RG[(q0 + d) & kRingMask];
         } else {
+          // a deep tile (windows beyond the ring: every p from the index in global memory, as a
+          // per-lane choice of address would make every load of the step a flat load)
           const int p = r + OFF[t.mi];
           t.rp = g.idx4[p];
           t.gp = g.idx_gate[p];
@@ -1496,12 +1497,14 @@ void sweep_dest_hist(SweepArgs& a, int n_dest, int shift) {
 }
 
 void sweep_coarse_hist(SweepArgs& a) {
-  // at most kHistMax buckets; the rest of A's bits (<= 14 for 2^24 reads) are pass 2's LDS bins
+  // at most kHistMax buckets; the rest of A's bits (<= 12) are pass 2's LDS bins.  Beyond 2^22 reads the
+  // counted grouping runs instead: 16384-bin LDS histograms held pass 2 at two blocks per CU (cfg5:
+  // 2.49 ms against 1.40 ms for the counted pass 2, profiles/r05/r5n)
   const int nbits = bits_for(std::max(1, a.n_reads - 1));
   const int hb = std::min(nbits, 10);
   const int nt = tiles_of(a);
   const long long P = sweep_blocks(nt);
-  if (!a.grp || nbits - hb > 14 || (static_cast<long long>(1) << hb) * P > kGrpInts / 2) {
+  if (!a.grp || nbits - hb > 12 || (static_cast<long long>(1) << hb) * P > kGrpInts / 2) {
     a.hist_mat = nullptr;
     return;
   }
@@ -1525,10 +1528,7 @@ static hipError_t group_by_a(const SweepArgs& a, int mode, const unsigned long l
     hipError_t e = hipcub::DeviceScan::ExclusiveSum(a.temp, tb, a.hist_mat, off, H * P, s);
     if (e != hipSuccess) return e;
     k_sweep_scatter<<<P, kSwBlock, 0, s>>>(a, off, mid, a.n_dev ? a.ent_cap : 0x7FFFFFFFFFFFFFFFll);
-    if (lo <= 12)
-      k_msd_pass2r<kMsdMaxLo, 16><<<H, kP2Threads, 0, s>>>(mid, n, a.n_dev, off, P, H, lo, out);
-    else
-      k_msd_pass2r<4 * kMsdMaxLo, 16><<<H, kP2Threads, 0, s>>>(mid, n, a.n_dev, off, P, H, lo, out);
+    k_msd_pass2r<kMsdMaxLo, 16><<<H, kP2Threads, 0, s>>>(mid, n, a.n_dev, off, P, H, lo, out);
     return hipGetLastError();
   }
   const int nbits = bits_for(std::max(1, a.n_reads - 1));

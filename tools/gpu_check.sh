@@ -89,6 +89,11 @@ if has shardprof; then
   f=$(find $O/shardprof -name 'run_kernel_stats.csv' | head -1); cp $f $O/shardprof_kernel_stats.csv
   f=$(find $O/shardprof -name 'run_kernel_trace.csv' | head -1); cp $f $O/shardprof_kernel_trace.csv
 fi
+if has sclock; then
+  FSLR_LIB=$R/fslr_amd/libfslr_hip_sclock.so FSLR_ALLOW_STALE=1 timeout -k 10 300 python3 tools/sweep_clock.py $O/sweep_clock.json \
+      > $O/sclock.log 2>&1 || { echo "sclock failed"; tail -20 $O/sclock.log; exit 1; }
+  tail -12 $O/sclock.log
+fi
 if has pmc; then
   OUT=gpurun_out/$TAG/pmc timeout -k 10 900 bash tools/pmc.sh > $O/pmc.log 2>&1 || { echo "pmc failed"; tail -20 $O/pmc.log; exit 1; }
   tail -5 $O/pmc.log
