@@ -32,7 +32,7 @@ int ensure_capacity(fslr_ctx* c, int64_t n, int64_t ni, int n_chroms) {
     c->cap_n = n;
   }
   if (ni > c->cap_ni) {
-    if ((rc = dalloc(c, &c->iv, ni)) || (rc = dalloc(c, &c->qpos, ni)) || (rc = dalloc(c, &c->rng_s, ni)) || (rc = dalloc(c, &c->idx4, ni)) ||
+    if ((rc = dalloc(c, &c->iv, ni)) || (rc = dalloc(c, &c->qpos, ni)) || (rc = dalloc(c, &c->rng_s, ni)) || (rc = dalloc(c, &c->swin, ni)) || (rc = dalloc(c, &c->idx4, ni)) ||
         (rc = dalloc(c, &c->idx_gate, ni)) || (rc = dalloc(c, &c->data_pos, ni)) ||
         (rc = dalloc(c, &c->dchrom, ni)) || (rc = dalloc(c, &c->drec, ni)) || (rc = dalloc(c, &c->dgate, ni)) ||
         (rc = dalloc(c, &c->chist, (ni / 1024 + 1) * 64)) || (rc = dalloc(c, &c->s_start, ni)) ||
@@ -163,7 +163,7 @@ void fslr_ctx_destroy(fslr_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* bufs[] = {c->rmeta,  c->rlen8, c->iv,     c->qpos,    c->rng_s,  c->idx4,    c->idx_gate, c->data_pos, c->s_start,
+  void* bufs[] = {c->rmeta,  c->rlen8, c->iv,     c->qpos,    c->rng_s,  c->swin, c->idx4,    c->idx_gate, c->data_pos, c->s_start,
                   c->crange, c->keys,   c->keys2,   c->vals,    c->vals2,   c->endkey,  c->pmaxkey,
                   c->temp,   c->umax,   c->edges,   c->edge_iu, c->fwd,     c->parent,  c->counters, c->forest, c->forest_cnt, c->forest_blk,
                   c->upl,    c->upl64,
@@ -352,6 +352,8 @@ int fslr_set_reads(fslr_ctx* c, const fslr_reads* r) {
   return FSLR_OK;
 }
 
+static IndexBufs index_bufs(fslr_ctx* c);
+
 int fslr_set_thresholds(fslr_ctx* c, const int32_t* thr_in) {
   if (!c || (!thr_in && c->ni)) return FSLR_ERR_INVALID;
   if (!c->reads_set) return fail(c, FSLR_ERR_STATE, "fslr_set_reads first");
@@ -376,6 +378,10 @@ int fslr_set_thresholds(fslr_ctx* c, const int32_t* thr_in) {
     if (rc) return rc;
     HIP_TRY(c, launch_set_thr(c->thr_tmp, c->iv, c->qpos, c->index_built ? c->idx4 : nullptr, c->data_pos,
                               c->have_data_pos ? c->drec : nullptr, static_cast<int>(c->ni), c->stream));
+    if (c->index_built) {                                                    // the sweep windows follow
+      const IndexBufs b = index_bufs(c);
+      HIP_TRY(c, launch_index_swin(b, static_cast<int>(c->ni_idx), c->stream));
+    }
     if (c->filter_active && c->pf_on)                                        // refresh the filtered records
       HIP_TRY(c, launch_pos_gather(c->pf_sel, static_cast<int>(c->pf_end - c->pf_lo), c->dchrom, c->drec, c->dgate,
                                    c->pf_lmap, c->fdchrom, c->fdrec, c->fdgate, c->stream));
@@ -770,6 +776,7 @@ static IndexBufs index_bufs(fslr_ctx* c) {
   b.crange = c->filter_active ? c->crange_f : c->crange;
   b.qpos = c->qpos;
   b.rng_s = c->rng_s;
+  b.swin = c->swin;
   b.idx4 = c->idx4;
   b.idx_gate = c->idx_gate;
   return b;
@@ -924,6 +931,7 @@ static int sweep_front(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64
   s.idx4 = c->idx4;
   s.idx_gate = c->idx_gate;
   s.rng_s = c->rng_s;
+  s.swin = c->swin;
   s.umax = c->umax;
   s.ni = static_cast<int>(nix);
   s.nq = c->filter_active && c->pf_on ? static_cast<int>(c->pf_hi - c->pf_lo) : static_cast<int>(nix);
@@ -1230,7 +1238,7 @@ int fslr_position_costs(fslr_ctx* c, int64_t* tests, int64_t* reach, int64_t n_t
     if (int rc = dalloc(c, &c->pf_cost, 2 * std::max<int64_t>(nt, 1))) return rc;
     c->pf_cost_cap = 2 * std::max<int64_t>(nt, 1);
   }
-  HIP_TRY(c, launch_tile_costs(c->rng_s, static_cast<int>(c->ni), c->pf_cost, c->pf_cost + nt, c->stream));
+  HIP_TRY(c, launch_tile_costs(c->swin, static_cast<int>(c->ni), c->pf_cost, c->pf_cost + nt, c->stream));
   if (nt) {
     HIP_TRY(c, hipMemcpyAsync(tests, c->pf_cost, nt * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipMemcpyAsync(reach, c->pf_cost + nt, nt * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));

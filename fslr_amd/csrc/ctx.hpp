@@ -66,6 +66,7 @@ struct fslr_ctx {
   int4* iv = nullptr;
   int* qpos = nullptr;       // [NI] CSR interval -> its position in the sorted index
   int2* rng_s = nullptr;     // [NI] sorted position -> {n_fwd, bwd_begin}
+  int* swin = nullptr;       // [NI] sorted position -> the sweep's forward window (<= n_fwd)
   int4* idx4 = nullptr;
   int2* idx_gate = nullptr;
   unsigned long long* defer = nullptr;

@@ -373,7 +373,8 @@ __global__ __launch_bounds__(kRangeBlock) void k_ranges(const int4* __restrict__
                                                         const unsigned long long* __restrict__ endkey,
                                                         TilePrefix tile_incl,
                                                         const int2* __restrict__ crange, int ni,
-                                                        int2* __restrict__ rng_s, int n_chroms = 0) {
+                                                        int2* __restrict__ rng_s, int* __restrict__ swin,
+                                                        const int2* __restrict__ gate, int n_chroms = 0) {
   __shared__ int w_st[kRangeSpan + 2 * kWin];    // starts of [w0, w1)
   __shared__ int w_pm[kBwd ? kRangeSpan + kWin : 1];   // pmax (end part) of [w0, q0 + kRangeSpan)
   __shared__ unsigned long long t_part[kBwd ? kRangeBlock : 1];
@@ -449,6 +450,30 @@ __global__ __launch_bounds__(kRangeBlock) void k_ranges(const int4* __restrict__
       }
     }
     const int n_fwd = lo - q - 1;
+    // the sweep's window (swin): p with start_p <= end_q - thr_q only, the pairs calculate_overlap can
+    // pass from q's side (cluster.py:133-136: min(end) - start_p >= thr_q); the whole forward range
+    // when q's read has qlen2 or n_alignments 0 (a ZeroDivisionError pair is any hit, cluster.py:178-183)
+    if (swin) {
+      const int2 gq = gate[q];
+      int m = n_fwd;
+      if (gq.x != 0 && (gq.y & 0xFFFFFF) != 0) {
+        const int key = e - idx4[q].z;
+        int a = q + 1, z = lo;                   // first p in (q, lo) with start_p > key
+        if (z <= w1) {
+          while (a < z) {
+            const int mid = (a + z) >> 1;
+            if (w_st[mid - w0] <= key) a = mid + 1; else z = mid;
+          }
+        } else {
+          while (a < z) {
+            const int mid = (a + z) >> 1;
+            if (s_start[mid] <= key) a = mid + 1; else z = mid;
+          }
+        }
+        m = a - q - 1;
+      }
+      swin[q] = m;
+    }
     if constexpr (!kBwd) {
       rng_s[q] = make_int2(n_fwd, -1);
       continue;
@@ -536,7 +561,7 @@ static hipError_t launch_walk_parts(const IndexBufs& b, int n, int ni, hipStream
   k_group_scan<<<1, kGroup, 0, s>>>(grp, ng);
   k_ranges<true><<<(ni + kRangeSpan - 1) / kRangeSpan, kRangeBlock, 0, s>>>(b.idx4, b.shard, b.n_shards, b.s_start,
                                                                             b.endkey, TilePrefix{tloc, grp}, b.crange,
-                                                                            ni, b.rng_s);
+                                                                            ni, b.rng_s, b.swin, b.idx_gate);
   return hipGetLastError();
 }
 
@@ -566,7 +591,7 @@ hipError_t launch_build_index(const IndexBufs& b, int n, int ni, int n_chroms, b
                                                           b.idx_gate, b.s_start, b.endkey, b.vals);
       k_ranges<false><<<(ni + kRangeSpan - 1) / kRangeSpan, kRangeBlock, 0, s>>>(
           b.idx4, b.shard, b.n_shards, b.s_start, reinterpret_cast<const unsigned long long*>(b.vals),
-          TilePrefix{nullptr, nullptr}, b.crange, ni, b.rng_s, n_chroms);
+          TilePrefix{nullptr, nullptr}, b.crange, ni, b.rng_s, b.swin, b.idx_gate, n_chroms);
       return hipGetLastError();
     }
     k_chrom_scatter<true><<<ntl, kTileThreads, 0, s>>>(b.dchrom, b.drec, b.dgate, b.chist, ni, ntl, rounds, b.idx4, b.idx_gate,
@@ -590,6 +615,29 @@ hipError_t launch_build_index(const IndexBufs& b, int n, int ni, int n_chroms, b
   return launch_walk_parts(b, n, ni, s, false);
 }
 
+// the sweep windows again after the thresholds changed in place (fslr_set_thresholds): the same search
+// as k_ranges', over the start column in global memory
+__global__ __launch_bounds__(256) void k_swin(const int4* __restrict__ idx4, const int2* __restrict__ gate,
+                                              const int2* __restrict__ rng_s, const int* __restrict__ s_start, int ni,
+                                              int* __restrict__ swin) {
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < ni; q += gridDim.x * blockDim.x) {
+    const int n_fwd = rng_s[q].x;
+    const int2 gq = gate[q];
+    int m = n_fwd;
+    if (gq.x != 0 && (gq.y & 0xFFFFFF) != 0) {
+      const int4 r = idx4[q];
+      const int key = r.y - r.z;
+      int a = q + 1, z = q + 1 + n_fwd;
+      while (a < z) {
+        const int mid = (a + z) >> 1;
+        if (s_start[mid] <= key) a = mid + 1; else z = mid;
+      }
+      m = a - q - 1;
+    }
+    swin[q] = m;
+  }
+}
+
 // a lean index's (chrom, end) keys from its end column (the backward ranges need them, not the map)
 __global__ __launch_bounds__(256) void k_endkey(const int* __restrict__ s_end, const int2* __restrict__ crange,
                                                 int n_chroms, int ni, unsigned long long* __restrict__ endkey) {
@@ -603,6 +651,12 @@ __global__ __launch_bounds__(256) void k_endkey(const int* __restrict__ s_end, c
       if (c + b < 64 && c_beg[c + b] <= q) c += b;
     endkey[q] = (static_cast<unsigned long long>(c) << 32) | static_cast<unsigned>(s_end[q]);
   }
+}
+
+hipError_t launch_index_swin(const IndexBufs& b, int ni, hipStream_t s) {
+  if (ni <= 0 || !b.swin) return hipSuccess;
+  k_swin<<<grid_for(ni), 256, 0, s>>>(b.idx4, b.idx_gate, b.rng_s, b.s_start, ni, b.swin);
+  return hipGetLastError();
 }
 
 hipError_t launch_index_endkeys(const IndexBufs& b, int ni, int n_chroms, hipStream_t s) {

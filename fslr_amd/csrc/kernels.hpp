@@ -110,6 +110,7 @@ struct IndexBufs {
   const int2* crange;                 // [n_chroms] {begin, end} in sorted order (host counts)
   int* qpos;                          // out [NI] CSR order
   int2* rng_s;                        // out [NI] sorted order
+  int* swin;                          // out [NI] the sweep's forward window (k_ranges: swin)
   int4* idx4;                         // out [NI]
   int2* idx_gate;                     // out [NI]
 };
@@ -122,6 +123,8 @@ hipError_t launch_build_index(const IndexBufs& b, int n_reads, int ni, int n_chr
 // walk parts and the backward ranges read (same records, same order)
 hipError_t launch_index_rescatter(const IndexBufs& b, int ni, int n_chroms, hipStream_t s);
 // a lean index's (chrom, end) keys alone (its end column stays in b.vals): what the backward ranges read
+// the sweep windows again from the index's thresholds (after fslr_set_thresholds patched them)
+hipError_t launch_index_swin(const IndexBufs& b, int ni, hipStream_t s);
 hipError_t launch_index_endkeys(const IndexBufs& b, int ni, int n_chroms, hipStream_t s);
 // the walk engine's parts of a sweep-only index (qpos, tile prefix, backward ranges)
 hipError_t launch_index_walk_parts(const IndexBufs& b, int n_reads, int ni, hipStream_t s);
@@ -177,6 +180,7 @@ struct SweepArgs {
   const int4* idx4;
   const int2* idx_gate;
   const int2* rng_s;
+  const int* swin;                    // [NI] the sweep's forward window of each position (k_ranges)
   const int* umax;
   int ni, n_reads;
   int nq;                             // query positions [0, nq) of the index (the rest: a forward halo)
@@ -247,7 +251,7 @@ constexpr int kMaxDest = 64;          // destination ranks of one partition
 // data order (stable), their chromosome renumbered lmap[c]
 // the position split (shard.hip): per 64-position tile its pair tests and forward-window end; the
 // data positions of a sorted-position range and their records in data order
-hipError_t launch_tile_costs(const int2* rng_s, int ni, long long* tests, long long* reach, hipStream_t s);
+hipError_t launch_tile_costs(const int* swin, int ni, long long* tests, long long* reach, hipStream_t s);
 hipError_t launch_pos_select(const int* qd, int ni, int lo, int end, int* flags, int* offs, int* sel,
                              void* temp, size_t temp_bytes, hipStream_t s);
 hipError_t launch_pos_gather(const int* sel, int m, const unsigned* dchrom, const int4* drec, const int2* dgate,

@@ -47,13 +47,13 @@ __global__ void k_own_scatter(const unsigned* __restrict__ dchrom, const int4* _
 // ---- the position split: a rank's contiguous range of sorted positions --------------------------
 // per tile of 64 sorted positions: its pair tests (the sum of the forward counts, the sweep's cost)
 // and the end of its forward window (max q + n_fwd(q) + 1: the records a rank sweeping the tile needs)
-__global__ void k_tile_costs(const int2* __restrict__ rng_s, int ni, long long* __restrict__ tests,
+__global__ void k_tile_costs(const int* __restrict__ swin, int ni, long long* __restrict__ tests,
                              long long* __restrict__ reach) {
   const int nt = (ni + kWave - 1) / kWave;
   const int lane = threadIdx.x & (kWave - 1);
   for (int t = (blockIdx.x * kBlk + threadIdx.x) >> 6; t < nt; t += (gridDim.x * kBlk) >> 6) {
     const int q = t * kWave + lane;
-    const int nf = q < ni ? rng_s[q].x : 0;
+    const int nf = q < ni ? swin[q] : 0;
     long long sum = nf;
     int r = q < ni ? q + nf + 1 : 0;
     for (int o = 32; o > 0; o >>= 1) {
@@ -92,10 +92,10 @@ __global__ void k_pos_gather(const int* __restrict__ sel, int m, const unsigned*
 
 }  // namespace
 
-hipError_t launch_tile_costs(const int2* rng_s, int ni, long long* tests, long long* reach, hipStream_t s) {
+hipError_t launch_tile_costs(const int* swin, int ni, long long* tests, long long* reach, hipStream_t s) {
   if (ni <= 0) return hipSuccess;
   const long long nt = (ni + kWave - 1) / kWave;
-  k_tile_costs<<<static_cast<int>(std::min<long long>(4096, (nt * kWave + kBlk - 1) / kBlk)), kBlk, 0, s>>>(rng_s, ni, tests,
+  k_tile_costs<<<static_cast<int>(std::min<long long>(4096, (nt * kWave + kBlk - 1) / kBlk)), kBlk, 0, s>>>(swin, ni, tests,
                                                                                                         reach);
   return hipGetLastError();
 }

@@ -161,7 +161,7 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(5))) v
     const bool qv = q < g.nq;
     const int qc = qv ? q : q0;
     const bool first = tile == tb;
-    const int nf = qv ? g.rng_s[qc].x : 0;
+    const int nf = qv ? g.swin[qc] : 0;
     wave_lds_sync();                             // the previous tile's ring and map reads are done
     if (first) {
       // the chunk's first tile: positions [q0, q0 + kRing)
@@ -491,12 +491,12 @@ __global__ __launch_bounds__(256) void k_wave_bounds(const long long* __restrict
   }
 }
 
-__global__ __launch_bounds__(256) void k_tile_tests(const int2* __restrict__ rng_s, int ni, long long* __restrict__ tests) {
+__global__ __launch_bounds__(256) void k_tile_tests(const int* __restrict__ swin, int ni, long long* __restrict__ tests) {
   const int nt = (ni + kWave - 1) / kWave;
   const int lane = lane_id();
   for (int t = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; t < nt; t += (gridDim.x * blockDim.x) >> 6) {
     const int q = t * kWave + lane;
-    int v = q < ni ? rng_s[q].x : 0;
+    int v = q < ni ? swin[q] : 0;
     v = wave_incl_scan(v);
     if (lane == kWave - 1) tests[t] = v;
   }
@@ -1422,7 +1422,7 @@ size_t sweep_temp_bytes(long long ent_cap, long long ni, hipStream_t s) {
 hipError_t launch_sweep_plan(const SweepArgs& a, hipStream_t s) {
   const int nt = tiles_of(a);
   if (nt == 0) return hipSuccess;
-  k_tile_tests<<<grid_for(static_cast<long long>(nt) * kWave, 256, 4096), 256, 0, s>>>(a.rng_s, a.nq, a.tile_tests);
+  k_tile_tests<<<grid_for(static_cast<long long>(nt) * kWave, 256, 4096), 256, 0, s>>>(a.swin, a.nq, a.tile_tests);
   size_t tb = a.temp_bytes;
   hipError_t e = hipcub::DeviceScan::ExclusiveSum(a.temp, tb, a.tile_tests, a.tile_ub, nt, s);
   if (e != hipSuccess) return e;
