@@ -250,7 +250,7 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(5))) v
         } else {
           // a deep tile (windows beyond the ring: every p from the index in global memory, as a
           // per-lane choice of address would make every load of the step a flat load)
-          const int p = r + OFF[t.mi];
+          const int p = r < se ? r + OFF[t.mi] : q0;   // lanes past the segment read a valid position
           t.rp = g.idx4[p];
           t.gp = g.idx_gate[p];
         }
