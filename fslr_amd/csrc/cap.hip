@@ -184,6 +184,65 @@ __global__ void k_cap_frontier(const int* __restrict__ aoff, const int* __restri
   }
 }
 
+// The same fixed point in one launch: T's list tl is a work queue (the seeds first, each read appended
+// when it joins; unwritten entries are -1).  A wave claims 64 entries at a time, walks the forward
+// edges of those already written, and waits for the rest; it ends when every appended entry has been
+// walked (walked == appended: only an entry being walked can append another) or when its claim lies
+// past n (each read joins once).  q: [0] appended (= fcnt[32]), [1] claimed, [2] walked, [3] a wave
+// gave up waiting (the spin bound; reported as an error, never expected).
+template <bool kRows>
+__global__ void __launch_bounds__(256) k_cap_closure_q(const int* __restrict__ a0, const int* __restrict__ a1,
+                                                       const int2* __restrict__ rows, const int* __restrict__ adj,
+                                                       const int* __restrict__ fwd, int thr, int n,
+                                                       int* __restrict__ state, int* __restrict__ back, int* tl,
+                                                       unsigned* q) {
+  const int lane = threadIdx.x & 63;
+  unsigned base = 0;
+  bool pending = false;
+  unsigned spins = 0;
+  for (;;) {
+    if (!__ballot(pending)) {
+      unsigned b = 0;
+      if (lane == 0) b = atomicAdd(q + 1, 64u);
+      base = static_cast<unsigned>(__shfl(static_cast<int>(b), 0));
+      if (base >= static_cast<unsigned>(n)) break;                // no read can fill these entries
+      pending = base + lane < static_cast<unsigned>(n);
+    }
+    int x = -1;
+    if (pending) x = __hip_atomic_load(tl + base + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool work = pending && x >= 0;
+    if (work) {
+      pending = false;
+      const int k0 = a0[x], k1 = kRows ? a1[x] : a0[x + 1];
+      for (int k = k0; k < k1; ++k) {
+        const int y = kRows ? rows[k].y : adj[k];
+        const int b = atomicAdd(back + y, 1) + 1;
+        if (fwd[y] + b >= thr && atomicCAS(state + y, 0, 1) == 0) {
+          const unsigned p = atomicAdd(q, 1u);
+          __hip_atomic_store(tl + p, y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+    const unsigned long long wm = __ballot(work);
+    if (wm) {
+      if (lane == 0)
+        __hip_atomic_fetch_add(q + 2, static_cast<unsigned>(__popcll(wm)), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      spins = 0;
+      continue;
+    }
+    // nothing written yet in this wave's claim: done when every appended entry has been walked (read
+    // walked first: appended is then at least the value it had at that instant)
+    const unsigned d = __hip_atomic_load(q + 2, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned t = __hip_atomic_load(q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    if (d == t) break;
+    if (++spins > (1u << 22)) {
+      if (lane == 0) atomicOr(q + 3, 1u);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(4);
+  }
+}
+
 __global__ void k_cap_fcnt_roll(unsigned* fcnt) {
   if (threadIdx.x == 0) {
     const unsigned v = fcnt[16];
@@ -1947,6 +2006,17 @@ int cap_slot_sort() {
 
 // workgroups of a frontier round (grid-stride over the frontier): FSLR_CAP_FGRID, default 1024 (256 and
 // 128 measured the same on the cfg5 replay, profiles/r04/r4r/)
+// the frontier closure in one work-queue launch (default), or FSLR_CAP_CLOSURE_ROUNDS builds: rounds of
+// k_cap_frontier(_rows) in batches of 16 with a host sync per batch
+bool cap_closure_queue() {
+#ifdef FSLR_CAP_CLOSURE_ROUNDS
+  return false;
+#else
+  return true;
+#endif
+}
+constexpr int kClosureGrid = 256;
+
 int cap_frontier_grid() {
   static const int v = [] {
     const char* e = std::getenv("FSLR_CAP_FGRID");
@@ -2055,7 +2125,24 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, const int2* E, const int* F, int
     if (ne > 0) k_cap_adj_fill<<<grid_for(ne), 256, 0, s>>>(E, ne, w->aoff, w->acur, w->adj);
   }
   unsigned ntl = 0;                    // the frontier closure: |T|
-  if (frontier) {
+  if (frontier && cap_closure_queue()) {
+    // one launch: the T list as a work queue (k_cap_closure_q)
+    HIP_TRY(c, hipMemsetAsync(w->tl, 0xff, static_cast<size_t>(n) * sizeof(int), s));
+    k_cap_seed<<<grid_for(n), 256, 0, s>>>(F, static_cast<int>(n), thr, w->state, w->back, w->fl0, w->fcnt, w->tl,
+                                           w->fcnt + 32);
+    if (rstart)
+      k_cap_closure_q<true><<<kClosureGrid, 256, 0, s>>>(rstart, rend, E, nullptr, F, thr, static_cast<int>(n), w->state,
+                                                          w->back, w->tl, w->fcnt + 32);
+    else
+      k_cap_closure_q<false><<<kClosureGrid, 256, 0, s>>>(w->aoff, nullptr, nullptr, w->adj, F, thr, static_cast<int>(n),
+                                                           w->state, w->back, w->tl, w->fcnt + 32);
+    HIP_TRY(c, hipGetLastError());
+    unsigned qv[4] = {0, 0, 0, 0};
+    HIP_TRY(c, hipMemcpyAsync(qv, w->fcnt + 32, sizeof(qv), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    if (qv[3] || qv[2] != qv[0]) return fail(c, FSLR_ERR_STATE, "edge cap closure: the work queue did not drain");
+    ntl = qv[0];
+  } else if (frontier) {
     k_cap_seed<<<grid_for(n), 256, 0, s>>>(F, static_cast<int>(n), thr, w->state, w->back, w->fl0, w->fcnt, w->tl,
                                            w->fcnt + 32);
     HIP_TRY(c, hipGetLastError());

@@ -89,6 +89,18 @@ if has shardprof; then
   f=$(find $O/shardprof -name 'run_kernel_stats.csv' | head -1); cp $f $O/shardprof_kernel_stats.csv
   f=$(find $O/shardprof -name 'run_kernel_trace.csv' | head -1); cp $f $O/shardprof_kernel_trace.csv
 fi
+if has capshard; then
+  # the sharded cap at cfg5, W = 8 ranks on this GPU: per-stage host times (FSLR_DEBUG_CAP), then a kernel trace
+  FSLR_DEBUG_CAP=1 timeout -k 10 600 python3 -u tools/shard_cap_timing.py --worlds 8 --reps 1 > $O/capshard_dbg.jsonl 2> $O/capshard_dbg.log \
+      || { echo "capshard dbg failed"; tail -20 $O/capshard_dbg.log; exit 1; }
+  ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/capprof -o run --output-format csv \
+      -- python3 $R/tools/shard_cap_timing.py --worlds 8 --reps 2 > $O/capshard.jsonl 2> $O/capshard.log ) \
+      || { echo "capshard prof failed"; tail -5 $O/capshard.log; exit 1; }
+  f=$(find $O/capprof -name 'run_kernel_stats.csv' | head -1); cp $f $O/capshard_kernel_stats.csv
+  f=$(find $O/capprof -name 'run_kernel_trace.csv' | head -1); cp $f $O/capshard_kernel_trace.csv
+  rm -rf $O/capprof
+  tail -3 $O/capshard.log
+fi
 if has sclock; then
   FSLR_LIB=$R/fslr_amd/libfslr_hip_sclock.so FSLR_ALLOW_STALE=1 timeout -k 10 300 python3 tools/sweep_clock.py $O/sweep_clock.json \
       > $O/sclock.log 2>&1 || { echo "sclock failed"; tail -20 $O/sclock.log; exit 1; }
