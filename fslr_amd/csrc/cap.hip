@@ -188,8 +188,10 @@ __global__ void k_cap_frontier(const int* __restrict__ aoff, const int* __restri
 // when it joins; unwritten entries are -1).  A wave claims 64 entries at a time, walks the forward
 // edges of those already written, and waits for the rest; it ends when every appended entry has been
 // walked (walked == appended: only an entry being walked can append another) or when its claim lies
-// past n (each read joins once).  q: [0] appended (= fcnt[32]), [1] claimed, [2] walked, [3] a wave
-// gave up waiting (the spin bound; reported as an error, never expected).
+// past n (each read joins once).  The counters sit on separate 128-B lines (waiting waves poll them):
+// q[0] appended (= fcnt[32]), q[32] claimed, q[64] walked, q[65] a wave gave up waiting (the spin
+// bound; reported as an error, never expected).
+constexpr int kQClaim = 32, kQWalked = 64, kQStuck = 65;
 template <bool kRows>
 __global__ void __launch_bounds__(256) k_cap_closure_q(const int* __restrict__ a0, const int* __restrict__ a1,
                                                        const int2* __restrict__ rows, const int* __restrict__ adj,
@@ -203,7 +205,7 @@ __global__ void __launch_bounds__(256) k_cap_closure_q(const int* __restrict__ a
   for (;;) {
     if (!__ballot(pending)) {
       unsigned b = 0;
-      if (lane == 0) b = atomicAdd(q + 1, 64u);
+      if (lane == 0) b = atomicAdd(q + kQClaim, 64u);
       base = static_cast<unsigned>(__shfl(static_cast<int>(b), 0));
       if (base >= static_cast<unsigned>(n)) break;                // no read can fill these entries
       pending = base + lane < static_cast<unsigned>(n);
@@ -211,35 +213,67 @@ __global__ void __launch_bounds__(256) k_cap_closure_q(const int* __restrict__ a
     int x = -1;
     if (pending) x = __hip_atomic_load(tl + base + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const bool work = pending && x >= 0;
+    // the forward rows of the wave's written entries, one row per lane (a read's rows spread over
+    // lanes; two independent atomics in flight per lane): each returning atomic is a round trip to
+    // memory, which a read walking its own rows would pay once per row
+    int k0 = 0, len = 0;
     if (work) {
       pending = false;
-      const int k0 = a0[x], k1 = kRows ? a1[x] : a0[x + 1];
-      for (int k = k0; k < k1; ++k) {
-        const int y = kRows ? rows[k].y : adj[k];
-        const int b = atomicAdd(back + y, 1) + 1;
-        if (fwd[y] + b >= thr && atomicCAS(state + y, 0, 1) == 0) {
-          const unsigned p = atomicAdd(q, 1u);
-          __hip_atomic_store(tl + p, y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      k0 = a0[x];
+      len = (kRows ? a1[x] : a0[x + 1]) - k0;
+    }
+    const int incl = wave_incl_scan(len);
+    const int total = rdl(incl, 63);
+    for (int r0 = 0; r0 < total; r0 += 128) {
+      int y[2];
+      bool on[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int r = r0 + u * 64 + lane;
+        on[u] = r < total;
+        // the lane holding row r: the first lane whose inclusive count exceeds r
+        int o = 0;
+#pragma unroll
+        for (int st = 32; st > 0; st >>= 1)
+          if (__shfl(incl, o + st - 1) <= r) o += st;
+        const int k = __shfl(k0, o) + r - (__shfl(incl, o) - __shfl(len, o));
+        y[u] = on[u] ? (kRows ? rows[k].y : adj[k]) : 0;
+      }
+      int bk[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) bk[u] = on[u] ? atomicAdd(back + y[u], 1) + 1 : 0;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const bool join = on[u] && fwd[y[u]] + bk[u] >= thr && atomicCAS(state + y[u], 0, 1) == 0;
+        const unsigned long long jm = __ballot(join);
+        if (jm) {
+          unsigned p0 = 0;
+          if (lane == 0) p0 = atomicAdd(q, static_cast<unsigned>(__popcll(jm)));
+          p0 = static_cast<unsigned>(__shfl(static_cast<int>(p0), 0));
+          if (join) __hip_atomic_store(tl + p0 + mbcnt(jm), y[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
     }
     const unsigned long long wm = __ballot(work);
     if (wm) {
       if (lane == 0)
-        __hip_atomic_fetch_add(q + 2, static_cast<unsigned>(__popcll(wm)), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(q + kQWalked, static_cast<unsigned>(__popcll(wm)), __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_AGENT);
       spins = 0;
       continue;
     }
-    // nothing written yet in this wave's claim: done when every appended entry has been walked (read
-    // walked first: appended is then at least the value it had at that instant)
-    const unsigned d = __hip_atomic_load(q + 2, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned t = __hip_atomic_load(q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-    if (d == t) break;
-    if (++spins > (1u << 22)) {
-      if (lane == 0) atomicOr(q + 3, 1u);
-      break;
+    // nothing written yet in this wave's claim: every 4th time, done when every appended entry has been
+    // walked (walked read first: appended is then at least the value it had at that instant)
+    if ((++spins & 3u) == 0) {
+      const unsigned d = __hip_atomic_load(q + kQWalked, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned t = __hip_atomic_load(q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+      if (d == t) break;
+      if (spins > (1u << 22)) {
+        if (lane == 0) atomicOr(q + kQStuck, 1u);
+        break;
+      }
     }
-    __builtin_amdgcn_s_sleep(4);
+    __builtin_amdgcn_s_sleep(8);
   }
 }
 
@@ -2015,7 +2049,10 @@ bool cap_closure_queue() {
   return true;
 #endif
 }
-constexpr int kClosureGrid = 256;
+#ifndef FSLR_CLOSURE_GRID
+#define FSLR_CLOSURE_GRID 64
+#endif
+constexpr int kClosureGrid = FSLR_CLOSURE_GRID;
 
 int cap_frontier_grid() {
   static const int v = [] {
@@ -2096,7 +2133,7 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, const int2* E, const int* F, int
     cv.add(&w->fl0, n);
     cv.add(&w->fl1, n);
     cv.add(&w->tl, n);
-    cv.add(&w->fcnt, 64);
+    cv.add(&w->fcnt, 128);
     if (int rc = cv.commit(c, w->ar[0])) return rc;
   }
   HIP_TRY(c, hipMemsetAsync(w->err, 0, 4 * sizeof(int), s));
@@ -2108,7 +2145,7 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, const int2* E, const int* F, int
   else if (!frontier) k_cap_init<<<grid_for(n), 256, 0, s>>>(F, static_cast<int>(n), thr, w->state, w->back);
   HIP_TRY(c, hipGetLastError());
   if (frontier) {
-    HIP_TRY(c, hipMemsetAsync(w->fcnt, 0, 64 * sizeof(unsigned), s));
+    HIP_TRY(c, hipMemsetAsync(w->fcnt, 0, 128 * sizeof(unsigned), s));
   }
   if (frontier && !rstart) {
     // the adjacency of E grouped by its lower read (rows sorted by lower read come with their runs)
@@ -2137,10 +2174,10 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, const int2* E, const int* F, int
       k_cap_closure_q<false><<<kClosureGrid, 256, 0, s>>>(w->aoff, nullptr, nullptr, w->adj, F, thr, static_cast<int>(n),
                                                            w->state, w->back, w->tl, w->fcnt + 32);
     HIP_TRY(c, hipGetLastError());
-    unsigned qv[4] = {0, 0, 0, 0};
+    unsigned qv[2 + kQStuck] = {};
     HIP_TRY(c, hipMemcpyAsync(qv, w->fcnt + 32, sizeof(qv), hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
-    if (qv[3] || qv[2] != qv[0]) return fail(c, FSLR_ERR_STATE, "edge cap closure: the work queue did not drain");
+    if (qv[kQStuck] || qv[kQWalked] != qv[0]) return fail(c, FSLR_ERR_STATE, "edge cap closure: the work queue did not drain");
     ntl = qv[0];
   } else if (frontier) {
     k_cap_seed<<<grid_for(n), 256, 0, s>>>(F, static_cast<int>(n), thr, w->state, w->back, w->fl0, w->fcnt, w->tl,
