@@ -1482,26 +1482,50 @@ __global__ void k_cap_tcost(const int* __restrict__ gath, int world, int nt, int
 }
 
 // per component (its root = smallest t): its cost (the hits of its reads, plus one per read), and the
-// list of roots with their costs (the host orders them and assigns ranks)
+// roots order them and the ranks are assigned on the device (k_cap_assign_head / _tail)
 __global__ void k_cap_ccost(const int* __restrict__ comp, const int* __restrict__ cost, int nt,
                             unsigned long long* __restrict__ ccost) {
   for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += gridDim.x * blockDim.x)
     atomicAdd(ccost + comp[t], static_cast<unsigned long long>(cost[t]) + 1ull);
 }
 
-// the components' roots as sort keys: cost descending, then root ascending
-__global__ void k_cap_roots(const int* __restrict__ comp, const unsigned long long* __restrict__ ccost, int nt,
-                            unsigned long long* __restrict__ roots, unsigned* __restrict__ nroots) {
-  const int lane = threadIdx.x & 63;
-  for (int t0 = (blockIdx.x * blockDim.x + threadIdx.x) & ~63; t0 < nt; t0 += gridDim.x * blockDim.x) {
-    const int t = t0 + lane;
-    const bool r = t < nt && comp[t] == t;
-    const unsigned long long m = __ballot(r);
-    if (!m) continue;
-    unsigned base = 0;
-    if (lane == 0) base = atomicAdd(nroots, static_cast<unsigned>(__popcll(m)));
-    base = static_cast<unsigned>(__shfl(static_cast<int>(base), 0));
-    if (r) roots[base + mbcnt(m)] = ((0x7fffffffull - min(ccost[t], 0x7fffffffull)) << 32) | static_cast<unsigned>(t);
+// every T slot as a sort key: a root's (cost descending, then root ascending), ~0 for the others (sorted last)
+__global__ void k_cap_rootkeys(const int* __restrict__ comp, const unsigned long long* __restrict__ ccost, int nt,
+                               unsigned long long* __restrict__ keys) {
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += gridDim.x * blockDim.x)
+    keys[t] = comp[t] == t ? ((0x7fffffffull - min(ccost[t], 0x7fffffffull)) << 32) | static_cast<unsigned>(t) : ~0ull;
+}
+
+// the components onto ranks, the same on every rank: the kCapHead largest one by one onto the
+// least-loaded rank (ties: the lower rank), by one lane; the rest (sorted by cost, descending) dealt
+// in snake order, rank 0 .. W-1 then W-1 .. 0, whose sums differ by at most the largest of them
+constexpr int kCapHead = 256;
+__global__ void k_cap_assign_head(const unsigned long long* __restrict__ sorted, int nt, int world,
+                                  int* __restrict__ dmap) {
+  __shared__ unsigned long long hk[kCapHead];
+  const int nh = min(nt, kCapHead);
+  for (int k = threadIdx.x; k < nh; k += blockDim.x) hk[k] = sorted[k];
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  long long load[kMaxDest] = {};
+  for (int k = 0; k < nh; ++k) {
+    const unsigned long long key = hk[k];
+    if (key == ~0ull) break;
+    int d = 0;
+    for (int q = 1; q < world; ++q)
+      if (load[q] < load[d]) d = q;
+    load[d] += static_cast<long long>(0x7fffffffull - (key >> 32));
+    dmap[static_cast<int>(key & 0xffffffffull)] = d;
+  }
+}
+
+__global__ void k_cap_assign_tail(const unsigned long long* __restrict__ sorted, int nt, int world,
+                                  int* __restrict__ dmap) {
+  for (int k = kCapHead + blockIdx.x * blockDim.x + threadIdx.x; k < nt; k += gridDim.x * blockDim.x) {
+    const unsigned long long key = sorted[k];
+    if (key == ~0ull) continue;
+    const int j = k - kCapHead, r = j % world;
+    dmap[static_cast<int>(key & 0xffffffffull)] = (j / world) & 1 ? world - 1 - r : r;
   }
 }
 
@@ -1510,9 +1534,6 @@ __global__ void k_cap_tdest(const int* __restrict__ comp, const int* __restrict_
   for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += gridDim.x * blockDim.x) tdest[t] = dmap[comp[t]];
 }
 
-__global__ void k_cap_dmap(const int2* __restrict__ rd, int nr, int* __restrict__ dmap) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nr; i += gridDim.x * blockDim.x) dmap[rd[i].x] = rd[i].y;
-}
 
 // per T-interval: the rank replaying its read's component (sort key), and its index
 __global__ void k_cap_tikey(const int* __restrict__ tread, const int* __restrict__ tdest, int nti,
@@ -1888,15 +1909,12 @@ struct CapWork {
   unsigned long long* ccost = nullptr;
   int2* roots = nullptr;
   int* dmap = nullptr;
-  unsigned* nroots = nullptr;
   int64_t nmine = 0, mine_off = 0, planned = 0;
   int2* tdeps = nullptr;
   int *roff = nullptr, *chgl = nullptr;
   unsigned* nchg = nullptr;
   int64_t n_chg = 0;
   bool replayed = false;              // fslr_cap_replay_shard ran (changes ready)
-  int* hpin = nullptr;                // pinned host scratch (the plan's per-T arrays)
-  size_t hpin_cap = 0;
   bool runs1 = false;                 // one GPU: the edge list is grouped by lower read (gstart / gend)
   // the restricted gather (fslr_cap_bwd_counts, fslr_cap_restrict, fslr_cap_install_restricted):
   // local forward counts, the local backward counts (before the sum over ranks), kept flags and
@@ -1915,7 +1933,6 @@ void fslr_cap_free(fslr_ctx* c) {
     if (a.base) (void)hipFree(a.base);
   if (w->temp) (void)hipFree(w->temp);
   if (w->host) (void)hipHostFree(w->host);
-  if (w->hpin) (void)hipHostFree(w->hpin);
   delete w;
   c->capw = nullptr;
 }
@@ -3157,13 +3174,11 @@ extern "C" int fslr_cap_shard_plan(fslr_ctx* c, const int32_t* gathered, int32_t
     cv.add(&w->ccost, nt);
     cv.add(&w->roots, nt);
     cv.add(&w->dmap, nt);
-    cv.add(&w->nroots, 4);
     if (int rc = cv.commit(c, w->ar[6])) return rc;
   }
   CapTimer tm(s);
   // the components of the T-T hit graph: the union of the ranks' local forests; each component's cost
   // and the list of roots, on the device
-  unsigned nr = 0;
   unsigned long long* rkeys = reinterpret_cast<unsigned long long*>(w->roots);   // then sorted into ccost
   if (nt > 0) {
     HIP_TRY(c, launch_uf_init(w->comp, nt, s));
@@ -3171,60 +3186,20 @@ extern "C" int fslr_cap_shard_plan(fslr_ctx* c, const int32_t* gathered, int32_t
     HIP_TRY(c, launch_uf_finalize(w->comp, nt, s));
     k_cap_tcost<<<grid_for(nt), 256, 0, s>>>(gathered, world, nt, w->tcost);
     HIP_TRY(c, hipMemsetAsync(w->ccost, 0, static_cast<size_t>(nt) * sizeof(unsigned long long), s));
-    HIP_TRY(c, hipMemsetAsync(w->nroots, 0, sizeof(unsigned), s));
     k_cap_ccost<<<grid_for(nt), 256, 0, s>>>(w->comp, w->tcost, nt, w->ccost);
-    k_cap_roots<<<grid_for(nt), 256, 0, s>>>(w->comp, w->ccost, nt, rkeys, w->nroots);
-    HIP_TRY(c, hipGetLastError());
-    HIP_TRY(c, hipMemcpyAsync(&nr, w->nroots, sizeof(nr), hipMemcpyDeviceToHost, s));
-    HIP_TRY(c, hipStreamSynchronize(s));
-    if (nr > 1) {                      // largest first (ties: the smaller root), on the device
-      size_t tb = 0;
-      HIP_TRY(c, hipcub::DeviceRadixSort::SortKeys(nullptr, tb, rkeys, w->ccost, static_cast<int>(nr), 0, 63, s));
-      if (int rc = ensure_temp(c, w, tb)) return rc;
-      tb = w->temp_bytes;
-      HIP_TRY(c, hipcub::DeviceRadixSort::SortKeys(w->temp, tb, rkeys, w->ccost, static_cast<int>(nr), 0, 63, s));
-    } else if (nr == 1) {
-      HIP_TRY(c, hipMemcpyAsync(w->ccost, rkeys, sizeof(unsigned long long), hipMemcpyDeviceToDevice, s));
-    }
-  }
-  tm.lap("plan: unions");
-  // pinned host copy of the roots (pageable copies go through the driver's staging)
-  if (static_cast<size_t>(2 * nr + 2) > w->hpin_cap) {
-    if (w->hpin) (void)hipHostFree(w->hpin);
-    w->hpin = nullptr;
-    w->hpin_cap = 0;
-    const size_t want = static_cast<size_t>(2 * nr + 2) + nr / 4 + 1024;
-    HIP_TRY(c, hipHostMalloc(reinterpret_cast<void**>(&w->hpin), want * sizeof(int), hipHostMallocDefault));
-    w->hpin_cap = want;
-  }
-  int2* rh = reinterpret_cast<int2*>(w->hpin);
-  const unsigned long long* rk = reinterpret_cast<const unsigned long long*>(w->hpin);
-  if (nr) {
-    HIP_TRY(c, hipMemcpyAsync(w->hpin, w->ccost, static_cast<size_t>(nr) * sizeof(unsigned long long),
-                              hipMemcpyDeviceToHost, s));
-    HIP_TRY(c, hipStreamSynchronize(s));
-  }
-  tm.lap("plan: d2h");
-  // components largest first (ties: the smaller root) onto the least-loaded rank (ties: the lower
-  // rank) — the same assignment on every rank
-  int64_t load[kMaxDest] = {};
-  for (unsigned k = 0; k < nr; ++k) {
-    const unsigned long long key = rk[k];
-    const int root = static_cast<int>(key & 0xffffffffull);
-    const int64_t cost = static_cast<int64_t>(0x7fffffffull - (key >> 32));
-    int d = 0;
-    for (int q = 1; q < world; ++q)
-      if (load[q] < load[d]) d = q;
-    load[d] += cost;
-    rh[k] = make_int2(root, d);        // (in place: the key just read)
-  }
-  tm.lap("plan: assign");
-  if (nr) {
-    HIP_TRY(c, hipMemcpyAsync(w->roots, rh, static_cast<size_t>(nr) * sizeof(int2), hipMemcpyHostToDevice, s));
-    k_cap_dmap<<<grid_for(nr), 256, 0, s>>>(w->roots, static_cast<int>(nr), w->dmap);
+    k_cap_rootkeys<<<grid_for(nt), 256, 0, s>>>(w->comp, w->ccost, nt, rkeys);
+    // largest first (ties: the smaller root), the other slots last; then the ranks, on the device
+    size_t tb = 0;
+    HIP_TRY(c, hipcub::DeviceRadixSort::SortKeys(nullptr, tb, rkeys, w->ccost, nt, 0, 64, s));
+    if (int rc = ensure_temp(c, w, tb)) return rc;
+    tb = w->temp_bytes;
+    HIP_TRY(c, hipcub::DeviceRadixSort::SortKeys(w->temp, tb, rkeys, w->ccost, nt, 0, 64, s));
+    k_cap_assign_head<<<1, 256, 0, s>>>(w->ccost, nt, world, w->dmap);
+    if (nt > kCapHead) k_cap_assign_tail<<<grid_for(nt - kCapHead), 256, 0, s>>>(w->ccost, nt, world, w->dmap);
     k_cap_tdest<<<grid_for(nt), 256, 0, s>>>(w->comp, w->dmap, nt, w->tdest);
     HIP_TRY(c, hipGetLastError());
   }
+  tm.lap("plan: unions + assign");
   // the T-intervals grouped by destination (stable: T order inside a group), their counts and hits
   HIP_TRY(c, hipMemsetAsync(w->totals, 0, 2 * kMaxDest * sizeof(long long), s));
   HIP_TRY(c, hipMemsetAsync(w->scnt + nti, 0, sizeof(int), s));

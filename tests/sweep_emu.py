@@ -465,10 +465,14 @@ class EmuSweepContext:
         roots = sorted(set(comp.tolist()), key=lambda r: (-ccost[r], r))
         load = np.zeros(world, np.int64)
         droot = {}
-        for r in roots:
-            d = int(np.argmin(load))
+        for k, r in enumerate(roots):
+            if k < 256:                  # the largest onto the least-loaded rank (k_cap_assign_head)
+                d = int(np.argmin(load))
+                load[d] += ccost[r]
+            else:                        # the rest dealt in snake order (k_cap_assign_tail)
+                j = k - 256
+                d = world - 1 - j % world if (j // world) & 1 else j % world
             droot[r] = d
-            load[d] += ccost[r]
         self._comp = comp
         self._tdest = np.array([droot[c] for c in comp.tolist()], np.int64)
         tread = self._ti_read()
