@@ -196,8 +196,7 @@ template <bool kRows>
 __global__ void __launch_bounds__(256) k_cap_closure_q(const int* __restrict__ a0, const int* __restrict__ a1,
                                                        const int2* __restrict__ rows, const int* __restrict__ adj,
                                                        const int* __restrict__ fwd, int thr, int n,
-                                                       int* __restrict__ state, int* __restrict__ back, int* tl,
-                                                       unsigned* q) {
+                                                       int* __restrict__ back, int* tl, unsigned* q) {
   const int lane = threadIdx.x & 63;
   unsigned base = 0;
   bool pending = false;
@@ -239,12 +238,16 @@ __global__ void __launch_bounds__(256) k_cap_closure_q(const int* __restrict__ a
         const int k = __shfl(k0, o) + r - (__shfl(incl, o) - __shfl(len, o));
         y[u] = on[u] ? (kRows ? rows[k].y : adj[k]) : 0;
       }
-      int bk[2];
+      // y joins on the one count that brings fwd(y) + back(y) to the cap (back grows by one per
+      // walked edge; a seed has fwd(y) >= thr already), so no flag word is needed
+      int bk[2], fy[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) fy[u] = on[u] ? fwd[y[u]] : 0;
 #pragma unroll
       for (int u = 0; u < 2; ++u) bk[u] = on[u] ? atomicAdd(back + y[u], 1) + 1 : 0;
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        const bool join = on[u] && fwd[y[u]] + bk[u] >= thr && atomicCAS(state + y[u], 0, 1) == 0;
+        const bool join = on[u] && fy[u] + bk[u] == thr;
         const unsigned long long jm = __ballot(join);
         if (jm) {
           unsigned p0 = 0;
@@ -2185,11 +2188,11 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, const int2* E, const int* F, int
     k_cap_seed<<<grid_for(n), 256, 0, s>>>(F, static_cast<int>(n), thr, w->state, w->back, w->fl0, w->fcnt, w->tl,
                                            w->fcnt + 32);
     if (rstart)
-      k_cap_closure_q<true><<<kClosureGrid, 256, 0, s>>>(rstart, rend, E, nullptr, F, thr, static_cast<int>(n), w->state,
-                                                          w->back, w->tl, w->fcnt + 32);
+      k_cap_closure_q<true><<<kClosureGrid, 256, 0, s>>>(rstart, rend, E, nullptr, F, thr, static_cast<int>(n), w->back,
+                                                          w->tl, w->fcnt + 32);
     else
       k_cap_closure_q<false><<<kClosureGrid, 256, 0, s>>>(w->aoff, nullptr, nullptr, w->adj, F, thr, static_cast<int>(n),
-                                                           w->state, w->back, w->tl, w->fcnt + 32);
+                                                           w->back, w->tl, w->fcnt + 32);
     HIP_TRY(c, hipGetLastError());
     unsigned qv[2 + kQStuck] = {};
     HIP_TRY(c, hipMemcpyAsync(qv, w->fcnt + 32, sizeof(qv), hipMemcpyDeviceToHost, s));

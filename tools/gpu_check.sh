@@ -89,6 +89,12 @@ if has shardprof; then
   f=$(find $O/shardprof -name 'run_kernel_stats.csv' | head -1); cp $f $O/shardprof_kernel_stats.csv
   f=$(find $O/shardprof -name 'run_kernel_trace.csv' | head -1); cp $f $O/shardprof_kernel_trace.csv
 fi
+if has capmodel; then
+  # the sharded cap at cfg5: the per-rank model at W = 8
+  timeout -k 10 600 python3 -u tools/shard_cap_timing.py --worlds 8 --reps 3 > $O/capmodel.jsonl 2> $O/capmodel.log \
+      || { echo "capmodel failed"; tail -20 $O/capmodel.log; exit 1; }
+  tail -3 $O/capmodel.log
+fi
 if has capshard; then
   # the sharded cap at cfg5, W = 8 ranks on this GPU: per-stage host times (FSLR_DEBUG_CAP), then a kernel trace
   FSLR_DEBUG_CAP=1 timeout -k 10 600 python3 -u tools/shard_cap_timing.py --worlds 8 --reps 1 > $O/capshard_dbg.jsonl 2> $O/capshard_dbg.log \
