@@ -184,102 +184,6 @@ __global__ void k_cap_frontier(const int* __restrict__ aoff, const int* __restri
   }
 }
 
-// The same fixed point in one launch: T's list tl is a work queue (the seeds first, each read appended
-// when it joins; unwritten entries are -1).  A wave claims 64 entries at a time, walks the forward
-// edges of those already written, and waits for the rest; it ends when every appended entry has been
-// walked (walked == appended: only an entry being walked can append another) or when its claim lies
-// past n (each read joins once).  The counters sit on separate 128-B lines (waiting waves poll them):
-// q[0] appended (= fcnt[32]), q[32] claimed, q[64] walked, q[65] a wave gave up waiting (the spin
-// bound; reported as an error, never expected).
-constexpr int kQClaim = 32, kQWalked = 64, kQStuck = 65;
-template <bool kRows>
-__global__ void __launch_bounds__(256) k_cap_closure_q(const int* __restrict__ a0, const int* __restrict__ a1,
-                                                       const int2* __restrict__ rows, const int* __restrict__ adj,
-                                                       const int* __restrict__ fwd, int thr, int n,
-                                                       int* __restrict__ back, int* tl, unsigned* q) {
-  const int lane = threadIdx.x & 63;
-  unsigned base = 0;
-  bool pending = false;
-  unsigned spins = 0;
-  for (;;) {
-    if (!__ballot(pending)) {
-      unsigned b = 0;
-      if (lane == 0) b = atomicAdd(q + kQClaim, 64u);
-      base = static_cast<unsigned>(__shfl(static_cast<int>(b), 0));
-      if (base >= static_cast<unsigned>(n)) break;                // no read can fill these entries
-      pending = base + lane < static_cast<unsigned>(n);
-    }
-    int x = -1;
-    if (pending) x = __hip_atomic_load(tl + base + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const bool work = pending && x >= 0;
-    // the forward rows of the wave's written entries, one row per lane (a read's rows spread over
-    // lanes; two independent atomics in flight per lane): each returning atomic is a round trip to
-    // memory, which a read walking its own rows would pay once per row
-    int k0 = 0, len = 0;
-    if (work) {
-      pending = false;
-      k0 = a0[x];
-      len = (kRows ? a1[x] : a0[x + 1]) - k0;
-    }
-    const int incl = wave_incl_scan(len);
-    const int total = rdl(incl, 63);
-    for (int r0 = 0; r0 < total; r0 += 128) {
-      int y[2];
-      bool on[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int r = r0 + u * 64 + lane;
-        on[u] = r < total;
-        // the lane holding row r: the first lane whose inclusive count exceeds r
-        int o = 0;
-#pragma unroll
-        for (int st = 32; st > 0; st >>= 1)
-          if (__shfl(incl, o + st - 1) <= r) o += st;
-        const int k = __shfl(k0, o) + r - (__shfl(incl, o) - __shfl(len, o));
-        y[u] = on[u] ? (kRows ? rows[k].y : adj[k]) : 0;
-      }
-      // y joins on the one count that brings fwd(y) + back(y) to the cap (back grows by one per
-      // walked edge; a seed has fwd(y) >= thr already), so no flag word is needed
-      int bk[2], fy[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) fy[u] = on[u] ? fwd[y[u]] : 0;
-#pragma unroll
-      for (int u = 0; u < 2; ++u) bk[u] = on[u] ? atomicAdd(back + y[u], 1) + 1 : 0;
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const bool join = on[u] && fy[u] + bk[u] == thr;
-        const unsigned long long jm = __ballot(join);
-        if (jm) {
-          unsigned p0 = 0;
-          if (lane == 0) p0 = atomicAdd(q, static_cast<unsigned>(__popcll(jm)));
-          p0 = static_cast<unsigned>(__shfl(static_cast<int>(p0), 0));
-          if (join) __hip_atomic_store(tl + p0 + mbcnt(jm), y[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-    }
-    const unsigned long long wm = __ballot(work);
-    if (wm) {
-      if (lane == 0)
-        __hip_atomic_fetch_add(q + kQWalked, static_cast<unsigned>(__popcll(wm)), __ATOMIC_RELEASE,
-                               __HIP_MEMORY_SCOPE_AGENT);
-      spins = 0;
-      continue;
-    }
-    // nothing written yet in this wave's claim: every 4th time, done when every appended entry has been
-    // walked (walked read first: appended is then at least the value it had at that instant)
-    if ((++spins & 3u) == 0) {
-      const unsigned d = __hip_atomic_load(q + kQWalked, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned t = __hip_atomic_load(q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-      if (d == t) break;
-      if (spins > (1u << 22)) {
-        if (lane == 0) atomicOr(q + kQStuck, 1u);
-        break;
-      }
-    }
-    __builtin_amdgcn_s_sleep(8);
-  }
-}
-
 __global__ void k_cap_fcnt_roll(unsigned* fcnt) {
   if (threadIdx.x == 0) {
     const unsigned v = fcnt[16];
@@ -2060,20 +1964,6 @@ int cap_slot_sort() {
 
 // workgroups of a frontier round (grid-stride over the frontier): FSLR_CAP_FGRID, default 1024 (256 and
 // 128 measured the same on the cfg5 replay, profiles/r04/r4r/)
-// the frontier closure in one work-queue launch (default), or FSLR_CAP_CLOSURE_ROUNDS builds: rounds of
-// k_cap_frontier(_rows) in batches of 16 with a host sync per batch
-bool cap_closure_queue() {
-#ifdef FSLR_CAP_CLOSURE_ROUNDS
-  return false;
-#else
-  return true;
-#endif
-}
-#ifndef FSLR_CLOSURE_GRID
-#define FSLR_CLOSURE_GRID 64
-#endif
-constexpr int kClosureGrid = FSLR_CLOSURE_GRID;
-
 int cap_frontier_grid() {
   static const int v = [] {
     const char* e = std::getenv("FSLR_CAP_FGRID");
@@ -2153,7 +2043,7 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, const int2* E, const int* F, int
     cv.add(&w->fl0, n);
     cv.add(&w->fl1, n);
     cv.add(&w->tl, n);
-    cv.add(&w->fcnt, 128);
+    cv.add(&w->fcnt, 64);
     if (int rc = cv.commit(c, w->ar[0])) return rc;
   }
   HIP_TRY(c, hipMemsetAsync(w->err, 0, 4 * sizeof(int), s));
@@ -2165,7 +2055,7 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, const int2* E, const int* F, int
   else if (!frontier) k_cap_init<<<grid_for(n), 256, 0, s>>>(F, static_cast<int>(n), thr, w->state, w->back);
   HIP_TRY(c, hipGetLastError());
   if (frontier) {
-    HIP_TRY(c, hipMemsetAsync(w->fcnt, 0, 128 * sizeof(unsigned), s));
+    HIP_TRY(c, hipMemsetAsync(w->fcnt, 0, 64 * sizeof(unsigned), s));
   }
   if (frontier && !rstart) {
     // the adjacency of E grouped by its lower read (rows sorted by lower read come with their runs)
@@ -2182,24 +2072,7 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, const int2* E, const int* F, int
     if (ne > 0) k_cap_adj_fill<<<grid_for(ne), 256, 0, s>>>(E, ne, w->aoff, w->acur, w->adj);
   }
   unsigned ntl = 0;                    // the frontier closure: |T|
-  if (frontier && cap_closure_queue()) {
-    // one launch: the T list as a work queue (k_cap_closure_q)
-    HIP_TRY(c, hipMemsetAsync(w->tl, 0xff, static_cast<size_t>(n) * sizeof(int), s));
-    k_cap_seed<<<grid_for(n), 256, 0, s>>>(F, static_cast<int>(n), thr, w->state, w->back, w->fl0, w->fcnt, w->tl,
-                                           w->fcnt + 32);
-    if (rstart)
-      k_cap_closure_q<true><<<kClosureGrid, 256, 0, s>>>(rstart, rend, E, nullptr, F, thr, static_cast<int>(n), w->back,
-                                                          w->tl, w->fcnt + 32);
-    else
-      k_cap_closure_q<false><<<kClosureGrid, 256, 0, s>>>(w->aoff, nullptr, nullptr, w->adj, F, thr, static_cast<int>(n),
-                                                           w->back, w->tl, w->fcnt + 32);
-    HIP_TRY(c, hipGetLastError());
-    unsigned qv[2 + kQStuck] = {};
-    HIP_TRY(c, hipMemcpyAsync(qv, w->fcnt + 32, sizeof(qv), hipMemcpyDeviceToHost, s));
-    HIP_TRY(c, hipStreamSynchronize(s));
-    if (qv[kQStuck] || qv[kQWalked] != qv[0]) return fail(c, FSLR_ERR_STATE, "edge cap closure: the work queue did not drain");
-    ntl = qv[0];
-  } else if (frontier) {
+  if (frontier) {
     k_cap_seed<<<grid_for(n), 256, 0, s>>>(F, static_cast<int>(n), thr, w->state, w->back, w->fl0, w->fcnt, w->tl,
                                            w->fcnt + 32);
     HIP_TRY(c, hipGetLastError());
