@@ -198,7 +198,7 @@ __global__ __launch_bounds__(kTileThreads) void k_chrom_scatter(const unsigned* 
                                                               int rounds, int4* __restrict__ idx4, int2* __restrict__ idx_gate,
                                                               int* __restrict__ s_start,
                                                               unsigned long long* __restrict__ endkey,
-                                                              int* __restrict__ qd, int* __restrict__ swkey) {
+                                                              int* __restrict__ qd) {
   __shared__ int wc[kTileWaves][64];      // this round: count of chromosome l in wave w
   __shared__ int wp[kTileWaves][64];      // this round: count of chromosome l in waves < w
   __shared__ int runs[2][64];             // next sorted position of chromosome l (double buffered)
@@ -257,9 +257,6 @@ __global__ __launch_bounds__(kTileThreads) void k_chrom_scatter(const unsigned* 
         qd[e] = q;
       } else {
         qd[q] = rec.y;                           // lean: the end column in the map's buffer
-        // and k_ranges' key for the sweep window: end - thr, or the whole forward range (INT_MAX) when
-        // the read has qlen2 or n_alignments 0 (k_ranges replaces it with the window's length)
-        if (swkey) swkey[q] = gate.x != 0 && (gate.y & 0xFFFFFF) != 0 ? rec.y - rec.z : 0x7FFFFFFF;
       }
     }
   }
@@ -416,10 +413,7 @@ __global__ __launch_bounds__(kRangeBlock) void k_ranges(const int4* __restrict__
   }
   __syncthreads();
   for (int q = q0 + threadIdx.x; q < wp1; q += kRangeBlock) {
-    if (n_shards > 1 && !shard_owns(idx4[q].w >> 6, shard, n_shards)) {   // another shard's A side
-      if (swin) swin[q] = 0;
-      continue;
-    }
+    if (n_shards > 1 && !shard_owns(idx4[q].w >> 6, shard, n_shards)) continue;   // another shard's A side
     int c, e;
     if constexpr (kBwd) {
       const unsigned long long ek = endkey[q];
@@ -460,18 +454,10 @@ __global__ __launch_bounds__(kRangeBlock) void k_ranges(const int4* __restrict__
     // pass from q's side (cluster.py:133-136: min(end) - start_p >= thr_q); the whole forward range
     // when q's read has qlen2 or n_alignments 0 (a ZeroDivisionError pair is any hit, cluster.py:178-183)
     if (swin) {
+      const int2 gq = gate[q];
       int m = n_fwd;
-      bool narrow;
-      int key;
-      if (!kBwd && gate == nullptr) {            // the lean build: the key written by k_chrom_scatter
-        key = swin[q];
-        narrow = key != 0x7FFFFFFF;
-      } else {
-        const int2 gq = gate[q];
-        narrow = gq.x != 0 && (gq.y & 0xFFFFFF) != 0;
-        key = narrow ? e - idx4[q].z : 0;
-      }
-      if (narrow) {
+      if (gq.x != 0 && (gq.y & 0xFFFFFF) != 0) {
+        const int key = e - idx4[q].z;
         int a = q + 1, z = lo;                   // first p in (q, lo) with start_p > key
         if (z <= w1) {
           while (a < z) {
@@ -602,15 +588,14 @@ hipError_t launch_build_index(const IndexBufs& b, int n, int ni, int n_chroms, b
     if (!full) {
       // the sweep engine's lean index: records, gate words, starts and ends, forward counts
       k_chrom_scatter<false><<<ntl, kTileThreads, 0, s>>>(b.dchrom, b.drec, b.dgate, b.chist, ni, ntl, rounds, b.idx4,
-                                                          b.idx_gate, b.s_start, b.endkey, b.vals, b.swin);
-      // (gate null: the window keys come from the scatter, in swin)
+                                                          b.idx_gate, b.s_start, b.endkey, b.vals);
       k_ranges<false><<<(ni + kRangeSpan - 1) / kRangeSpan, kRangeBlock, 0, s>>>(
           b.idx4, b.shard, b.n_shards, b.s_start, reinterpret_cast<const unsigned long long*>(b.vals),
-          TilePrefix{nullptr, nullptr}, b.crange, ni, b.rng_s, b.swin, nullptr, n_chroms);
+          TilePrefix{nullptr, nullptr}, b.crange, ni, b.rng_s, b.swin, b.idx_gate, n_chroms);
       return hipGetLastError();
     }
     k_chrom_scatter<true><<<ntl, kTileThreads, 0, s>>>(b.dchrom, b.drec, b.dgate, b.chist, ni, ntl, rounds, b.idx4, b.idx_gate,
-                                                       b.s_start, b.endkey, b.vals, nullptr);
+                                                       b.s_start, b.endkey, b.vals);
     return launch_walk_parts(b, n, ni, s, true);
   } else if (b.dchrom) {
     unsigned* k32 = reinterpret_cast<unsigned*>(b.keys2);
@@ -689,7 +674,7 @@ hipError_t launch_index_rescatter(const IndexBufs& b, int ni, int n_chroms, hipS
   k_chrom_count<<<ntl, kTileThreads, 0, s>>>(b.dchrom, ni, ntl, rounds, b.chist);
   k_chrom_scan<<<n_chroms, 1024, 0, s>>>(b.chist, ntl, b.crange);
   k_chrom_scatter<true><<<ntl, kTileThreads, 0, s>>>(b.dchrom, b.drec, b.dgate, b.chist, ni, ntl, rounds, b.idx4, b.idx_gate,
-                                                     b.s_start, b.endkey, b.vals, nullptr);
+                                                     b.s_start, b.endkey, b.vals);
   return hipGetLastError();
 }
 
