@@ -63,9 +63,9 @@ __global__ void k_uf_edges(int* p, const int2* __restrict__ edges, const unsigne
   }
 }
 
-#ifdef FSLR_UF_MIN
 // from the identity: every read points to its smallest neighbour below it (one atomicMin per edge, no
-// finds), a forest of the same components' partial unions; the unions over every edge follow
+// finds; pointers only go down, so it is a forest of partial unions of the same components); the unions
+// over every edge then find short paths: 0.049 vs 0.070 ms for the components at cfg3 (profiles/r05/r5u/)
 __global__ void k_uf_hook_min(int* p, const int2* __restrict__ edges, const unsigned long long* __restrict__ count,
                               long long cap) {
   const long long ne = min(static_cast<long long>(*count), cap);
@@ -76,7 +76,6 @@ __global__ void k_uf_hook_min(int* p, const int2* __restrict__ edges, const unsi
     if (lo != hi) atomicMin(p + hi, lo);
   }
 }
-#endif
 
 __global__ void k_uf_pairs(int* p, const int* __restrict__ src, const int* __restrict__ dst, long long n,
                            int period) {
@@ -217,11 +216,10 @@ hipError_t launch_uf_init(int* parent, int n, hipStream_t s) {
   return hipGetLastError();
 }
 
+// parent: the identity (launch_uf_init) — the min pre-hook overwrites links, which every edge's union then restores
 hipError_t launch_uf_edges(int* parent, const int2* edges, const unsigned long long* count, long long cap, int* err,
                            hipStream_t s) {
-#ifdef FSLR_UF_MIN
   if (cap > 0) k_uf_hook_min<<<grid_for(cap), 256, 0, s>>>(parent, edges, count, cap);
-#endif
   if (cap > 0) k_uf_edges<<<grid_for(cap), 256, 0, s>>>(parent, edges, count, cap, err);
   return hipGetLastError();
 }
