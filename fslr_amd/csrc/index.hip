@@ -189,7 +189,7 @@ __global__ __launch_bounds__(1024) void k_chrom_scan(int* __restrict__ chist, in
 // most lines were shared by waves on different XCDs and the stores cost 155 of 215 us.
 // qd[e] = q is written in data order for the CSR -> sorted position gather.
 // kFull = false (the sweep engine's lean index): the (chrom, end) key and the data -> sorted map are
-// not written, only each position's end (in the map's buffer `qd`): 56 instead of 68 B / interval
+// not written (k_ranges reads each position's end from its record): 52 instead of 68 B / interval
 template <bool kFull>
 __global__ __launch_bounds__(kTileThreads) void k_chrom_scatter(const unsigned* __restrict__ dchrom,
                                                               const int4* __restrict__ drec,
@@ -255,9 +255,7 @@ __global__ __launch_bounds__(kTileThreads) void k_chrom_scatter(const unsigned* 
       if constexpr (kFull) {
         endkey[q] = (static_cast<unsigned long long>(c) << 32) | static_cast<unsigned>(rec.y);
         qd[e] = q;
-      } else {
-        qd[q] = rec.y;                           // lean: the end column in the map's buffer
-      }
+      }                                          // (lean: the end column is idx4's .y)
     }
   }
 }
@@ -365,7 +363,7 @@ struct TilePrefix {
 };
 
 // kBwd = false (the sweep engine, lean index): forward counts only, no pmax window (rng_s[q].y = -1);
-// ends from the lean scatter's end column (passed as endkey), the chromosome from its begin in crange
+// ends from the records (idx4 .y; endkey unused), the chromosome from its begin in crange
 // (n_chroms <= 64)
 template <bool kBwd>
 __global__ __launch_bounds__(kRangeBlock) void k_ranges(const int4* __restrict__ idx4, int shard, int n_shards,
@@ -420,7 +418,7 @@ __global__ __launch_bounds__(kRangeBlock) void k_ranges(const int4* __restrict__
       c = static_cast<int>(ek >> 32);
       e = static_cast<int>(static_cast<unsigned>(ek));
     } else {
-      e = reinterpret_cast<const int*>(endkey)[q];
+      e = idx4[q].y;                             // (its .z, the threshold, is the window's below)
       c = 0;                                     // the last chromosome beginning at or before q
 #pragma unroll
       for (int b = 32; b > 0; b >>= 1)
@@ -590,7 +588,7 @@ hipError_t launch_build_index(const IndexBufs& b, int n, int ni, int n_chroms, b
       k_chrom_scatter<false><<<ntl, kTileThreads, 0, s>>>(b.dchrom, b.drec, b.dgate, b.chist, ni, ntl, rounds, b.idx4,
                                                           b.idx_gate, b.s_start, b.endkey, b.vals);
       k_ranges<false><<<(ni + kRangeSpan - 1) / kRangeSpan, kRangeBlock, 0, s>>>(
-          b.idx4, b.shard, b.n_shards, b.s_start, reinterpret_cast<const unsigned long long*>(b.vals),
+          b.idx4, b.shard, b.n_shards, b.s_start, nullptr,
           TilePrefix{nullptr, nullptr}, b.crange, ni, b.rng_s, b.swin, b.idx_gate, n_chroms);
       return hipGetLastError();
     }
@@ -638,8 +636,8 @@ __global__ __launch_bounds__(256) void k_swin(const int4* __restrict__ idx4, con
   }
 }
 
-// a lean index's (chrom, end) keys from its end column (the backward ranges need them, not the map)
-__global__ __launch_bounds__(256) void k_endkey(const int* __restrict__ s_end, const int2* __restrict__ crange,
+// a lean index's (chrom, end) keys from its records' ends (the backward ranges need them, not the map)
+__global__ __launch_bounds__(256) void k_endkey(const int4* __restrict__ idx4, const int2* __restrict__ crange,
                                                 int n_chroms, int ni, unsigned long long* __restrict__ endkey) {
   __shared__ int c_beg[64];
   if (threadIdx.x < 64) c_beg[threadIdx.x] = threadIdx.x < n_chroms ? crange[threadIdx.x].x : 0x7FFFFFFF;
@@ -649,7 +647,7 @@ __global__ __launch_bounds__(256) void k_endkey(const int* __restrict__ s_end, c
 #pragma unroll
     for (int b = 32; b > 0; b >>= 1)
       if (c + b < 64 && c_beg[c + b] <= q) c += b;
-    endkey[q] = (static_cast<unsigned long long>(c) << 32) | static_cast<unsigned>(s_end[q]);
+    endkey[q] = (static_cast<unsigned long long>(c) << 32) | static_cast<unsigned>(idx4[q].y);
   }
 }
 
@@ -662,7 +660,7 @@ hipError_t launch_index_swin(const IndexBufs& b, int ni, hipStream_t s) {
 hipError_t launch_index_endkeys(const IndexBufs& b, int ni, int n_chroms, hipStream_t s) {
   if (ni <= 0) return hipSuccess;
   if (n_chroms > kMaxFusedChroms) return hipErrorInvalidValue;
-  k_endkey<<<grid_for(ni), 256, 0, s>>>(b.vals, b.crange, n_chroms, ni, b.endkey);
+  k_endkey<<<grid_for(ni), 256, 0, s>>>(b.idx4, b.crange, n_chroms, ni, b.endkey);
   return hipGetLastError();
 }
 
