@@ -166,6 +166,7 @@ __global__ void k_cap_seed(const int* __restrict__ fwd, int n, int thr, int* __r
 
 // one round: every forward edge (x, y) of a read x that joined last round counts for y; y joins (and
 // enters the next frontier) when its forward degree plus those counts reaches the cap
+#ifdef FSLR_CAP_FRONTIER_THREAD
 __global__ void k_cap_frontier(const int* __restrict__ aoff, const int* __restrict__ adj, const int* __restrict__ fwd,
                                int thr, int* __restrict__ state, int* __restrict__ back, const int* __restrict__ fin,
                                const unsigned* __restrict__ fin_n, int* __restrict__ fout, unsigned* __restrict__ fout_n,
@@ -179,6 +180,73 @@ __global__ void k_cap_frontier(const int* __restrict__ aoff, const int* __restri
       if (fwd[y] + b >= thr && atomicCAS(state + y, 0, 1) == 0) {
         fout[atomicAdd(fout_n, 1u)] = y;
         tl[atomicAdd(tn, 1u)] = y;
+      }
+    }
+  }
+}
+#endif
+
+// one round, a wave's 64 frontier reads at a time with their forward rows spread over its lanes (two
+// returning atomics in flight per lane; a read walking its own rows pays one memory round trip per
+// row).  y joins on the one count that brings fwd(y) + back(y) to the cap: back grows by one per
+// walked edge and a seed has fwd(y) >= thr already, so no flag word is needed.  kRows: the runs
+// [a0[x], a1[x]) of the rows (gathered, sorted by lower read); else the adjacency a0 / adj
+template <bool kRows>
+__global__ void __launch_bounds__(256) k_cap_frontier_w(const int* __restrict__ a0, const int* __restrict__ a1,
+                                                        const int2* __restrict__ rows, const int* __restrict__ adj,
+                                                        const int* __restrict__ fwd, int thr, int* __restrict__ back,
+                                                        const int* __restrict__ fin, const unsigned* __restrict__ fin_n,
+                                                        int* __restrict__ fout, unsigned* __restrict__ fout_n,
+                                                        int* __restrict__ tl, unsigned* __restrict__ tn) {
+  const int nin = static_cast<int>(*fin_n);
+  const int lane = threadIdx.x & 63;
+  const int wave = static_cast<int>((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  const int nwaves = static_cast<int>((gridDim.x * blockDim.x) >> 6);
+  for (int base = wave * 64; base < nin; base += nwaves * 64) {
+    const int i = base + lane;
+    int k0 = 0, len = 0;
+    if (i < nin) {
+      const int x = fin[i];
+      k0 = a0[x];
+      len = (kRows ? a1[x] : a0[x + 1]) - k0;
+    }
+    const int incl = wave_incl_scan(len);
+    const int total = rdl(incl, 63);
+    for (int r0 = 0; r0 < total; r0 += 128) {
+      int y[2], fy[2], bk[2];
+      bool on[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int r = r0 + u * 64 + lane;
+        on[u] = r < total;
+        int o = 0;                               // the lane holding row r: the first whose count exceeds r
+#pragma unroll
+        for (int st = 32; st > 0; st >>= 1)
+          if (__shfl(incl, o + st - 1) <= r) o += st;
+        const int k = __shfl(k0, o) + r - (__shfl(incl, o) - __shfl(len, o));
+        y[u] = on[u] ? (kRows ? rows[k].y : adj[k]) : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) fy[u] = on[u] ? fwd[y[u]] : 0;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) bk[u] = on[u] ? atomicAdd(back + y[u], 1) + 1 : 0;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const bool join = on[u] && fy[u] + bk[u] == thr;
+        const unsigned long long jm = __ballot(join);
+        if (jm) {
+          unsigned p0 = 0, p1 = 0;
+          if (lane == 0) {
+            p0 = atomicAdd(fout_n, static_cast<unsigned>(__popcll(jm)));
+            p1 = atomicAdd(tn, static_cast<unsigned>(__popcll(jm)));
+          }
+          p0 = static_cast<unsigned>(__shfl(static_cast<int>(p0), 0));
+          p1 = static_cast<unsigned>(__shfl(static_cast<int>(p1), 0));
+          if (join) {
+            fout[p0 + mbcnt(jm)] = y[u];
+            tl[p1 + mbcnt(jm)] = y[u];
+          }
+        }
       }
     }
   }
@@ -1321,6 +1389,7 @@ __global__ void k_cap_runfwd(const int* __restrict__ gstart, const int* __restri
 }
 
 // one closure round over the runs: every forward edge (x, y) of a read x that joined last round
+#ifdef FSLR_CAP_FRONTIER_THREAD
 __global__ void k_cap_frontier_rows(const int* __restrict__ gstart, const int* __restrict__ gend,
                                     const int2* __restrict__ rows, const int* __restrict__ fwd, int thr,
                                     int* __restrict__ state, int* __restrict__ back, const int* __restrict__ fin,
@@ -1339,6 +1408,7 @@ __global__ void k_cap_frontier_rows(const int* __restrict__ gstart, const int* _
     }
   }
 }
+#endif
 
 // this context's edges by lower read (stable): keys and their positions, then the permutation
 __global__ void k_edge_keys(const int2* __restrict__ e, long long n, unsigned* __restrict__ key,
@@ -2081,12 +2151,21 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, const int2* E, const int* F, int
       // rounds r = 0 .. 15 of the batch: frontier fl[r & 1] (count fcnt[r]) -> fl[(r + 1) & 1] (fcnt[r + 1])
       const int fg = cap_frontier_grid();
       for (int r = 0; r < 16; ++r) {
+#ifdef FSLR_CAP_FRONTIER_THREAD
         if (rstart)
           k_cap_frontier_rows<<<fg, 256, 0, s>>>(rstart, rend, E, F, thr, w->state, w->back, fl[r & 1], w->fcnt + r,
                                                    fl[(r + 1) & 1], w->fcnt + r + 1, w->tl, w->fcnt + 32);
         else
           k_cap_frontier<<<fg, 256, 0, s>>>(w->aoff, w->adj, F, thr, w->state, w->back, fl[r & 1], w->fcnt + r,
                                               fl[(r + 1) & 1], w->fcnt + r + 1, w->tl, w->fcnt + 32);
+#else
+        if (rstart)
+          k_cap_frontier_w<true><<<fg, 256, 0, s>>>(rstart, rend, E, nullptr, F, thr, w->back, fl[r & 1], w->fcnt + r,
+                                                     fl[(r + 1) & 1], w->fcnt + r + 1, w->tl, w->fcnt + 32);
+        else
+          k_cap_frontier_w<false><<<fg, 256, 0, s>>>(w->aoff, nullptr, nullptr, w->adj, F, thr, w->back, fl[r & 1],
+                                                      w->fcnt + r, fl[(r + 1) & 1], w->fcnt + r + 1, w->tl, w->fcnt + 32);
+#endif
       }
       HIP_TRY(c, hipGetLastError());
       unsigned last = 0;
