@@ -164,27 +164,6 @@ __global__ void k_cap_seed(const int* __restrict__ fwd, int n, int thr, int* __r
   }
 }
 
-// one round: every forward edge (x, y) of a read x that joined last round counts for y; y joins (and
-// enters the next frontier) when its forward degree plus those counts reaches the cap
-#ifdef FSLR_CAP_FRONTIER_THREAD
-__global__ void k_cap_frontier(const int* __restrict__ aoff, const int* __restrict__ adj, const int* __restrict__ fwd,
-                               int thr, int* __restrict__ state, int* __restrict__ back, const int* __restrict__ fin,
-                               const unsigned* __restrict__ fin_n, int* __restrict__ fout, unsigned* __restrict__ fout_n,
-                               int* __restrict__ tl, unsigned* __restrict__ tn) {
-  const int nin = static_cast<int>(*fin_n);
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nin; i += gridDim.x * blockDim.x) {
-    const int x = fin[i];
-    for (int k = aoff[x]; k < aoff[x + 1]; ++k) {
-      const int y = adj[k];
-      const int b = atomicAdd(back + y, 1) + 1;
-      if (fwd[y] + b >= thr && atomicCAS(state + y, 0, 1) == 0) {
-        fout[atomicAdd(fout_n, 1u)] = y;
-        tl[atomicAdd(tn, 1u)] = y;
-      }
-    }
-  }
-}
-#endif
 
 // one round, a wave's 64 frontier reads at a time with their forward rows spread over its lanes (two
 // returning atomics in flight per lane; a read walking its own rows pays one memory round trip per
@@ -1388,28 +1367,6 @@ __global__ void k_cap_runfwd(const int* __restrict__ gstart, const int* __restri
   if (threadIdx.x == 0 && s) atomicAdd(tot, s);
 }
 
-// one closure round over the runs: every forward edge (x, y) of a read x that joined last round
-#ifdef FSLR_CAP_FRONTIER_THREAD
-__global__ void k_cap_frontier_rows(const int* __restrict__ gstart, const int* __restrict__ gend,
-                                    const int2* __restrict__ rows, const int* __restrict__ fwd, int thr,
-                                    int* __restrict__ state, int* __restrict__ back, const int* __restrict__ fin,
-                                    const unsigned* __restrict__ fin_n, int* __restrict__ fout,
-                                    unsigned* __restrict__ fout_n, int* __restrict__ tl, unsigned* __restrict__ tn) {
-  const int nin = static_cast<int>(*fin_n);
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nin; i += gridDim.x * blockDim.x) {
-    const int x = fin[i];
-    for (int k = gstart[x]; k < gend[x]; ++k) {
-      const int y = rows[k].y;
-      const int b = atomicAdd(back + y, 1) + 1;
-      if (fwd[y] + b >= thr && atomicCAS(state + y, 0, 1) == 0) {
-        fout[atomicAdd(fout_n, 1u)] = y;
-        tl[atomicAdd(tn, 1u)] = y;
-      }
-    }
-  }
-}
-#endif
-
 // this context's edges by lower read (stable): keys and their positions, then the permutation
 __global__ void k_edge_keys(const int2* __restrict__ e, long long n, unsigned* __restrict__ key,
                             int* __restrict__ val) {
@@ -2151,21 +2108,12 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, const int2* E, const int* F, int
       // rounds r = 0 .. 15 of the batch: frontier fl[r & 1] (count fcnt[r]) -> fl[(r + 1) & 1] (fcnt[r + 1])
       const int fg = cap_frontier_grid();
       for (int r = 0; r < 16; ++r) {
-#ifdef FSLR_CAP_FRONTIER_THREAD
-        if (rstart)
-          k_cap_frontier_rows<<<fg, 256, 0, s>>>(rstart, rend, E, F, thr, w->state, w->back, fl[r & 1], w->fcnt + r,
-                                                   fl[(r + 1) & 1], w->fcnt + r + 1, w->tl, w->fcnt + 32);
-        else
-          k_cap_frontier<<<fg, 256, 0, s>>>(w->aoff, w->adj, F, thr, w->state, w->back, fl[r & 1], w->fcnt + r,
-                                              fl[(r + 1) & 1], w->fcnt + r + 1, w->tl, w->fcnt + 32);
-#else
         if (rstart)
           k_cap_frontier_w<true><<<fg, 256, 0, s>>>(rstart, rend, E, nullptr, F, thr, w->back, fl[r & 1], w->fcnt + r,
                                                      fl[(r + 1) & 1], w->fcnt + r + 1, w->tl, w->fcnt + 32);
         else
           k_cap_frontier_w<false><<<fg, 256, 0, s>>>(w->aoff, nullptr, nullptr, w->adj, F, thr, w->back, fl[r & 1],
                                                       w->fcnt + r, fl[(r + 1) & 1], w->fcnt + r + 1, w->tl, w->fcnt + 32);
-#endif
       }
       HIP_TRY(c, hipGetLastError());
       unsigned last = 0;
