@@ -410,15 +410,32 @@ __global__ __launch_bounds__(kRangeBlock) void k_ranges(const int4* __restrict__
     }
   }
   __syncthreads();
-  for (int q = q0 + threadIdx.x; q < wp1; q += kRangeBlock) {
-    if (n_shards > 1 && !shard_owns(idx4[q].w >> 6, shard, n_shards)) continue;   // another shard's A side
+  // the lean build: this thread's records and gate words loaded up front (4 positions, all loads in
+  // flight together instead of one position's behind the previous one's searches)
+  constexpr int kPerQ = kRangeSpan / kRangeBlock;
+  int4 pre4[kPerQ];
+  int2 preg[kPerQ];
+  if constexpr (!kBwd) {
+#pragma unroll
+    for (int u = 0; u < kPerQ; ++u) {
+      const int q = q0 + threadIdx.x + u * kRangeBlock;
+      pre4[u] = q < wp1 ? idx4[q] : make_int4(0, 0, 0, 0);
+      preg[u] = q < wp1 && swin && gate ? gate[q] : make_int2(0, 0);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kPerQ; ++u) {
+    const int q = q0 + threadIdx.x + u * kRangeBlock;
+    if (q >= wp1) break;
+    const int4 rq = kBwd ? make_int4(0, 0, 0, 0) : pre4[u];
+    if (n_shards > 1 && !shard_owns((kBwd ? idx4[q].w : rq.w) >> 6, shard, n_shards)) continue;   // another shard's A side
     int c, e;
     if constexpr (kBwd) {
       const unsigned long long ek = endkey[q];
       c = static_cast<int>(ek >> 32);
       e = static_cast<int>(static_cast<unsigned>(ek));
     } else {
-      e = idx4[q].y;                             // (its .z, the threshold, is the window's below)
+      e = rq.y;                                  // (its .z, the threshold, is the window's below)
       c = 0;                                     // the last chromosome beginning at or before q
 #pragma unroll
       for (int b = 32; b > 0; b >>= 1)
@@ -452,10 +469,10 @@ __global__ __launch_bounds__(kRangeBlock) void k_ranges(const int4* __restrict__
     // pass from q's side (cluster.py:133-136: min(end) - start_p >= thr_q); the whole forward range
     // when q's read has qlen2 or n_alignments 0 (a ZeroDivisionError pair is any hit, cluster.py:178-183)
     if (swin) {
-      const int2 gq = gate[q];
+      const int2 gq = kBwd ? gate[q] : preg[u];
       int m = n_fwd;
       if (gq.x != 0 && (gq.y & 0xFFFFFF) != 0) {
-        const int key = e - idx4[q].z;
+        const int key = e - (kBwd ? idx4[q].z : rq.z);
         int a = q + 1, z = lo;                   // first p in (q, lo) with start_p > key
         if (z <= w1) {
           while (a < z) {
