@@ -86,6 +86,17 @@ __global__ void k_uf_pairs(int* p, const int* __restrict__ src, const int* __res
   }
 }
 
+// the same pre-hook over a pair list ((a, b), a < 0 or b < 0 = padding)
+__global__ void k_uf_hook_min_pairs(int* p, const int2* __restrict__ pairs, long long n) {
+  for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < n;
+       k += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const int2 e = pairs[k];
+    if (e.x < 0 || e.y < 0) continue;
+    const int lo = min(e.x, e.y), hi = max(e.x, e.y);
+    if (lo != hi) atomicMin(p + hi, lo);
+  }
+}
+
 // a gathered edge list (the multi-GPU merge): (a, b) pairs, a < 0 = padding
 __global__ void k_uf_pair_list(int* p, const int2* __restrict__ pairs, long long n) {
   for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < n;
@@ -229,7 +240,9 @@ hipError_t launch_uf_pairs(int* parent, const int* src, const int* dst, long lon
   return hipGetLastError();
 }
 
+// parent: the identity (launch_uf_init), as for launch_uf_edges
 hipError_t launch_uf_pair_list(int* parent, const int2* pairs, long long n, hipStream_t s) {
+  if (n > 0) k_uf_hook_min_pairs<<<grid_for(n), 256, 0, s>>>(parent, pairs, n);
   if (n > 0) k_uf_pair_list<<<grid_for(n), 256, 0, s>>>(parent, pairs, n);
   return hipGetLastError();
 }
