@@ -106,6 +106,18 @@ __global__ void k_uf_pair_list(int* p, const int2* __restrict__ pairs, long long
   }
 }
 
+// the same pre-hook over W label blocks (k_uf_strided's pairs (k, vals[w * stride + k]))
+__global__ void k_uf_hook_min_strided(int* p, const int* __restrict__ vals, long long blocks, int n, long long stride) {
+  for (long long k = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; k < blocks * n;
+       k += static_cast<long long>(gridDim.x) * blockDim.x) {
+    const long long w = k / n;
+    const int i = static_cast<int>(k - w * n);
+    const int v = vals[w * stride + i];
+    const int lo = min(i, v), hi = max(i, v);
+    if (lo != hi) atomicMin(p + hi, lo);
+  }
+}
+
 // W label blocks of n values at vals + w * stride (the multi-GPU cap's gathered forests): union of
 // k and vals[w * stride + k] for every block w
 __global__ void k_uf_strided(int* p, const int* __restrict__ vals, long long blocks, int n, long long stride) {
@@ -247,7 +259,9 @@ hipError_t launch_uf_pair_list(int* parent, const int2* pairs, long long n, hipS
   return hipGetLastError();
 }
 
+// parent: the identity (launch_uf_init), as for launch_uf_edges
 hipError_t launch_uf_strided(int* parent, const int* vals, long long blocks, int n, long long stride, hipStream_t s) {
+  if (blocks > 0 && n > 0) k_uf_hook_min_strided<<<grid_for(blocks * n), 256, 0, s>>>(parent, vals, blocks, n, stride);
   if (blocks > 0 && n > 0) k_uf_strided<<<grid_for(blocks * n), 256, 0, s>>>(parent, vals, blocks, n, stride);
   return hipGetLastError();
 }
