@@ -386,6 +386,7 @@ class Context:
         return out
 
     def fold_thresholds(self, overlap):
+        self.thr_gen = getattr(self, 'thr_gen', 0) + 1
         self._check(self._L.fslr_fold_thresholds(self._h, float(overlap)))
 
     def set_long_cutoffs(self, umax):
@@ -401,6 +402,7 @@ class Context:
 
     def set_thresholds(self, iv_thr):
         t = np.ascontiguousarray(iv_thr, dtype=np.int32)
+        self.thr_gen = getattr(self, 'thr_gen', 0) + 1     # a position plan is cut for the old windows
         self._check(self._L.fslr_set_thresholds(self._h, _ptr(t)))
 
     def reserve_edges(self, cap):

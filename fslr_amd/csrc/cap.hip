@@ -2175,6 +2175,8 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, const int2* E, const int* F, int
     k_cap_tlist<<<grid_for(n), 256, 0, s>>>(w->state, w->tv, w->tvs, static_cast<int>(n), w->T, w->toff, w->t_of,
                                             w->host_dev);
   }
+  if (!all_reads && c->zd_lost)
+    return fail(c, FSLR_ERR_STATE, "the ZeroDivisionError pair list overflowed (grown since); rerun the query");
   if (!all_reads) k_cap_zd_outside<<<1, 256, 0, s>>>(c->errw, w->t_of, w->host_dev + kHZd);
   HIP_TRY(c, hipGetLastError());
   HIP_TRY(c, hipStreamSynchronize(s));
@@ -2761,6 +2763,7 @@ extern "C" int fslr_long_pairs_shard(fslr_ctx* c, const fslr_params* p, int32_t 
   HIP_TRY(c, hipMemsetAsync(c->errw, 0, kErrSticky * sizeof(int), s));   // ZeroDivisionError pairs included
   c->q_thr = p->edge_threshold;
   c->zd_host = true;
+  c->zd_lost = false;
   if (ns > 0)
     k_cap_pairs_out<<<grid_for(ns), 256, 0, s>>>(w->ukey, ns, w->T, w->flags, c->lg_edges, c->lg_edge_cap, c->edges,
                                                   c->edge_iu, c->edge_cap, c->lg_cnt, c->fwd, c->errw);

@@ -354,6 +354,26 @@ int fslr_set_reads(fslr_ctx* c, const fslr_reads* r) {
 
 static IndexBufs index_bufs(fslr_ctx* c);
 
+// thr_tmp (the new folded thresholds, CSR order) into every copy of them: iv, the data-order records, the
+// sorted index, the sweep windows (start_p <= end_q - thr_q decides swin) and the filtered records of a
+// chromosome or position filter. ensure_walk_index(c) first: idx4 is updated through qpos.
+static int install_thresholds(fslr_ctx* c) {
+  HIP_TRY(c, launch_set_thr(c->thr_tmp, c->iv, c->qpos, c->index_built ? c->idx4 : nullptr, c->data_pos,
+                            c->have_data_pos ? c->drec : nullptr, static_cast<int>(c->ni), c->stream));
+  if (c->index_built) {
+    const IndexBufs b = index_bufs(c);
+    HIP_TRY(c, launch_index_swin(b, static_cast<int>(c->ni_idx), c->stream));
+  }
+  if (c->filter_active && c->pf_on)
+    HIP_TRY(c, launch_pos_gather(c->pf_sel, static_cast<int>(c->pf_end - c->pf_lo), c->dchrom, c->drec, c->dgate,
+                                 c->pf_lmap, c->fdchrom, c->fdrec, c->fdgate, c->stream));
+  else if (c->filter_active)
+    HIP_TRY(c, launch_chrom_filter(c->dchrom, c->drec, c->dgate, c->fmap, static_cast<int>(c->ni), c->fdchrom,
+                                   c->fdrec, c->fdgate, c->vals2, c->vals, c->temp, c->temp_bytes, c->stream));
+  ++c->thr_gen;                  // a position plan's halo was cut for the windows of the old thresholds
+  return FSLR_OK;
+}
+
 int fslr_set_thresholds(fslr_ctx* c, const int32_t* thr_in) {
   if (!c || (!thr_in && c->ni)) return FSLR_ERR_INVALID;
   if (!c->reads_set) return fail(c, FSLR_ERR_STATE, "fslr_set_reads first");
@@ -376,18 +396,7 @@ int fslr_set_thresholds(fslr_ctx* c, const int32_t* thr_in) {
       c->index_built = false;                                               // qpos is partial: rebuild
     int rc = ensure_walk_index(c);                                           // idx4 is updated through qpos
     if (rc) return rc;
-    HIP_TRY(c, launch_set_thr(c->thr_tmp, c->iv, c->qpos, c->index_built ? c->idx4 : nullptr, c->data_pos,
-                              c->have_data_pos ? c->drec : nullptr, static_cast<int>(c->ni), c->stream));
-    if (c->index_built) {                                                    // the sweep windows follow
-      const IndexBufs b = index_bufs(c);
-      HIP_TRY(c, launch_index_swin(b, static_cast<int>(c->ni_idx), c->stream));
-    }
-    if (c->filter_active && c->pf_on)                                        // refresh the filtered records
-      HIP_TRY(c, launch_pos_gather(c->pf_sel, static_cast<int>(c->pf_end - c->pf_lo), c->dchrom, c->drec, c->dgate,
-                                   c->pf_lmap, c->fdchrom, c->fdrec, c->fdgate, c->stream));
-    else if (c->filter_active)
-      HIP_TRY(c, launch_chrom_filter(c->dchrom, c->drec, c->dgate, c->fmap, static_cast<int>(c->ni), c->fdchrom,
-                                     c->fdrec, c->fdgate, c->vals2, c->vals, c->temp, c->temp_bytes, c->stream));
+    if (int rc = install_thresholds(c)) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
   }
   c->thr_mode = thr_mode_of(thr, c->ni);
@@ -404,6 +413,14 @@ int fslr_rows_upload(fslr_ctx* c, const fslr_rows* r) {
   HIP_TRY(c, hipSetDevice(c->device));
   const int64_t n = r->n_rows;
   c->rows_n = 0;
+  // the device-made CSR's views (fslr_get_csr, fslr_get_read_codes, fslr_fold_thresholds) are laid out
+  // over rows_cap and the old code / chromosome counts: they end here, and with them the reads they made
+  if (c->rows_set) {
+    c->rows_set = false;
+    c->reads_set = false;
+    c->index_built = false;
+    ++c->input_gen;
+  }
   if (n > c->rows_cap) {
     int rc;
     if ((rc = dalloc(c, &c->rows_col, 7 * static_cast<size_t>(n))) || (rc = dalloc(c, &c->rows_ord, n)) ||
@@ -505,6 +522,13 @@ int fslr_set_reads_rows(fslr_ctx* c, const int64_t* order, const uint8_t* keep, 
   long long mr[2] = {0, 0};
   HIP_TRY(c, rows_rank(w, n, c->rows_codes, c->rows_ord, keep ? c->rows_keep : nullptr, mr, st));
   const int64_t m = mr[0], n_reads = mr[1];
+  {  // an order or qname code out of range ends the build here, before the grouping reads the ranks
+    int err0 = 0;
+    HIP_TRY(c, hipMemcpyAsync(&err0, w.err, sizeof(err0), hipMemcpyDeviceToHost, st));
+    HIP_TRY(c, hipStreamSynchronize(st));
+    if (err0 & kRowsErrOrder) return fail(c, FSLR_ERR_INVALID, "order holds a row out of range");
+    if (err0 & kRowsErrCode) return fail(c, FSLR_ERR_INVALID, "qname code out of range");
+  }
   if (m < 1) return fail(c, FSLR_ERR_INVALID, "no interval is left after the mask");
   if (n_reads >= FSLR_MAX_READS) return fail(c, FSLR_ERR_INVALID, "read count out of range");
   // 2. grouping into the CSR; the read lengths, gate values and the chromosomes present
@@ -675,8 +699,7 @@ int fslr_fold_thresholds(fslr_ctx* c, double overlap) {
                        c->stream));
   if (c->index_built && (c->built_n_shards != 1 || c->filter_active)) c->index_built = false;
   if (int rc = ensure_walk_index(c)) return rc;
-  HIP_TRY(c, launch_set_thr(c->thr_tmp, c->iv, c->qpos, c->index_built ? c->idx4 : nullptr, c->data_pos, c->drec,
-                            static_cast<int>(c->ni), c->stream));
+  if (int rc = install_thresholds(c)) return rc;
   int stat[2] = {0, 0};
   HIP_TRY(c, hipMemcpyAsync(stat, w.stat + 2, sizeof(stat), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -934,6 +957,8 @@ static int sweep_front(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64
   s.swin = c->swin;
   s.umax = c->umax;
   s.ni = static_cast<int>(nix);
+  if (c->filter_active && c->pf_on && c->pf_thr_gen != c->thr_gen)     // the halo ends at the old windows
+    return fail(c, FSLR_ERR_STATE, "the thresholds changed after fslr_set_position_filter: plan the range again");
   s.nq = c->filter_active && c->pf_on ? static_cast<int>(c->pf_hi - c->pf_lo) : static_cast<int>(nix);
   s.n_reads = static_cast<int>(c->n);
   s.a_begin = static_cast<int>(a_begin);
@@ -1095,6 +1120,7 @@ static int prepare_query(fslr_ctx* c, const fslr_params* p, bool keep_sticky = f
                                 static_cast<int>(c->n),
                                 c->stream));
   std::memset(&c->cap_stats, 0, sizeof(c->cap_stats));
+  if (!keep_sticky) c->zd_lost = false;             // a new series lists its pairs from the start
   c->edges_global = false;
   c->cap_gmode = false;
   c->last_qcut = p->qlen_cut;                       // the cap replay's pair predicate
@@ -1335,6 +1361,7 @@ int fslr_set_position_filter(fslr_ctx* c, int64_t lo, int64_t hi, int64_t end) {
   c->pf_cr.swap(cr);
   c->pf_set = true;
   c->pf_gen = c->reads_gen;
+  c->pf_thr_gen = c->thr_gen;
   return pos_activate(c);
 }
 
@@ -1599,7 +1626,20 @@ int fslr_read_stats(fslr_ctx* c, fslr_query_stats* out) {
       out->overflow_flags |= 64;
       return fail(c, FSLR_ERR_STATE, "ZeroDivisionError pair list overflowed; rerun the query");
     }
+    if (c->zd_host && ew[kErrZdCount] > c->zd_cap) {
+      // a partition / query shard: the caller decides, and needs the list only when the cap binds (a
+      // rerun then fills the longer list; the replay refuses the incomplete one). The error words stay.
+      int hdr[kErrZdList];
+      HIP_TRY(c, hipMemcpyAsync(hdr, c->errw, sizeof(hdr), hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(c, hipStreamSynchronize(c->stream));
+      if (int rc = alloc_errw(c, std::max(2 * c->zd_cap, ew[kErrZdCount] + (ew[kErrZdCount] >> 2)))) return rc;
+      hdr[kErrZdCap] = c->zd_cap;
+      HIP_TRY(c, hipMemcpyAsync(c->errw, hdr, sizeof(hdr), hipMemcpyHostToDevice, c->stream));
+      HIP_TRY(c, hipStreamSynchronize(c->stream));
+      c->zd_lost = true;
+    }
   }
+  if (c->zd_lost) out->overflow_flags |= 64;
   if (out->deferred > c->defer_cap) return fail(c, FSLR_ERR_STATE, "deferred list overflowed; reserve and rerun");
   if (out->n_edges > c->edge_cap) return fail(c, FSLR_ERR_STATE, "edge buffer overflowed; reserve and rerun");
   if (ew[kErrOverflow] & 4)

@@ -41,6 +41,8 @@ struct fslr_ctx {
   bool pf_set = false, pf_on = false;
   int64_t pf_lo = 0, pf_hi = 0, pf_end = 0;
   uint64_t pf_gen = 0;                      // reads_gen of the selection
+  uint64_t pf_thr_gen = 0;                  // thr_gen of the plan (its halo covers those thresholds' windows)
+  uint64_t thr_gen = 0;                     // bumped whenever the thresholds change in place
   int* pf_sel = nullptr;                    // [pf_end - pf_lo] their data positions, ascending
   int64_t pf_sel_cap = 0;
   int* pf_lmap = nullptr;                   // [n_chroms] chromosome -> the range's own numbering, -1
@@ -122,6 +124,7 @@ struct fslr_ctx {
   std::vector<int> rows_dmap;       // chromosome number -> dense id, and its inverse
   std::vector<int64_t> rows_cid;
   int zd_cap = 0;          // capacity of that list (pairs)
+  bool zd_lost = false;    // this series' ZeroDivisionError list overflowed (a zd_host query; grown since)
   bool zd_host = false;    // the last query's ZeroDivisionError pairs are decided by the caller (a partition,
                            // an evaluation or a long-read query: the edge cap's binding is known there)
   int q_thr = 0;           // the last query's edge_threshold (fslr_read_stats: does the cap bind?)

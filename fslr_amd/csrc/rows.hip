@@ -43,26 +43,30 @@ __global__ void k_rows_first(const int* __restrict__ sel, int m, const long long
   }
 }
 
+// a code out of range (flagged by k_rows_first) is read nowhere: it counts as no first appearance
 __global__ void k_rows_isfirst(const int* __restrict__ sel, int m, const long long* __restrict__ qcode,
-                               const int* __restrict__ first, int* __restrict__ f) {
+                               long long n_codes, const int* __restrict__ first, int* __restrict__ f) {
   for (int d = blockIdx.x * blockDim.x + threadIdx.x; d < m; d += gridDim.x * blockDim.x) {
     const long long q = qcode[sel[d]];
-    f[d] = q >= 0 && first[q] == d ? 1 : 0;
+    f[d] = q >= 0 && q < n_codes && first[q] == d ? 1 : 0;
   }
 }
 
 // read rank of every data position (the scan of first appearances at its qname's first position), the
 // qname code of every rank, and d as the value of the grouping sort
-__global__ void k_rows_rank(const int* __restrict__ sel, int m, const long long* __restrict__ qcode,
+// (an out-of-range code, flagged before, takes rank 0: every write stays inside its array and the host
+// reports kRowsErrCode after the build)
+__global__ void k_rows_rank(const int* __restrict__ sel, int m, const long long* __restrict__ qcode, long long n_codes,
                             const int* __restrict__ first, const int* __restrict__ fscan, int* __restrict__ key,
                             int* __restrict__ val, long long* __restrict__ code_of_rank) {
   for (int d = blockIdx.x * blockDim.x + threadIdx.x; d < m; d += gridDim.x * blockDim.x) {
     const long long q = qcode[sel[d]];
-    const int f = q >= 0 ? first[q] : d;
-    const int r = fscan[f];
+    const bool ok = q >= 0 && q < n_codes;
+    const int f = ok ? first[q] : d;
+    const int r = ok ? fscan[f] : 0;
     key[d] = r;
     val[d] = d;
-    if (f == d) code_of_rank[r] = q;
+    if (ok && f == d) code_of_rank[r] = q;
   }
 }
 
@@ -217,7 +221,7 @@ hipError_t rows_rank(const RowsWork& w, long long n_rows, long long n_codes, con
   if (m == 0) return hipSuccess;
   k_rows_fill<<<grid_for(n_codes), 256, 0, s>>>(w.first, n_codes, 0x7FFFFFFF);
   k_rows_first<<<grid_for(m), 256, 0, s>>>(w.sel, m, w.qcode, n_codes, w.first, w.err);
-  k_rows_isfirst<<<grid_for(m), 256, 0, s>>>(w.sel, m, w.qcode, w.first, w.f);
+  k_rows_isfirst<<<grid_for(m), 256, 0, s>>>(w.sel, m, w.qcode, n_codes, w.first, w.f);
   tb = w.temp_bytes;
   if ((e = hipcub::DeviceScan::ExclusiveSum(w.temp, tb, w.f, w.fscan, m, s)) != hipSuccess) return e;
   int last[2] = {0, 0};
@@ -225,7 +229,7 @@ hipError_t rows_rank(const RowsWork& w, long long n_rows, long long n_codes, con
   if ((e = hipMemcpyAsync(&last[1], w.f + m - 1, sizeof(int), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
   out[1] = last[0] + last[1];
-  k_rows_rank<<<grid_for(m), 256, 0, s>>>(w.sel, m, w.qcode, w.first, w.fscan, w.key, w.val, w.code_of_rank);
+  k_rows_rank<<<grid_for(m), 256, 0, s>>>(w.sel, m, w.qcode, n_codes, w.first, w.fscan, w.key, w.val, w.code_of_rank);
   return hipGetLastError();
 }
 

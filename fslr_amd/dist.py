@@ -365,6 +365,7 @@ class SweepShard:
         ent = ctx.position_entries(qlen_cut, nal_cut, pass_table, edge_threshold)
         self.plan = position_plan(tests, reach, self.n_intervals, self.world, tile_entries=ent)
         self.pos = self.plan[self.rank]
+        self._plan_thr_gen = getattr(ctx, 'thr_gen', 0)
         ctx.set_position_filter(*self.pos)
 
     # -- collectives (self.comm: RCCL, gloo staged through host memory, or in-process) --------------
@@ -382,7 +383,8 @@ class SweepShard:
 
     # -- one step -----------------------------------------------------------------------------
     def _key(self, qlen_cut, nal_cut, pass_table, edge_threshold):
-        return (float(qlen_cut), float(nal_cut), np.asarray(pass_table, dtype=np.uint8).tobytes(), int(edge_threshold))
+        return (float(qlen_cut), float(nal_cut), np.asarray(pass_table, dtype=np.uint8).tobytes(), int(edge_threshold),
+                getattr(self.ctx, 'thr_gen', 0))
 
     def step(self, qlen_cut, nal_cut, pass_table, edge_threshold=10, collect=False, repeat=False) -> dict:
         """One step.  ``collect``: also read the sweep's counters after the partition (one more
@@ -399,13 +401,20 @@ class SweepShard:
         self._rep = None
         err = None
         try:
-            if self.split == 'position' and self.pos is None:
+            # plan again when the thresholds changed since: the halo covers the old sweep windows only
+            if self.split == 'position' and (self.pos is None or
+                                             self._plan_thr_gen != getattr(ctx, 'thr_gen', 0)):
                 self._plan_positions(qlen_cut, nal_cut, pass_table, edge_threshold)
             ctx.build_index()
             ok, counts = ctx.sweep_partition(qlen_cut, nal_cut, pass_table, W, self.block_shift, self.send,
                                              edge_threshold)
             if not ok:
                 self.send = self._grow(self.send, int(counts.sum()))
+                ok, counts = ctx.sweep_partition(qlen_cut, nal_cut, pass_table, W, self.block_shift, self.send,
+                                                 edge_threshold)
+                assert ok
+            if ctx.stats(check=False).get('overflow_flags', 0) & 64:
+                # the ZeroDivisionError pair list overflowed (and grew): the cap replay needs all of them
                 ok, counts = ctx.sweep_partition(qlen_cut, nal_cut, pass_table, W, self.block_shift, self.send,
                                                  edge_threshold)
                 assert ok
@@ -786,6 +795,9 @@ class PairShard(SweepShard):
             if self.long:
                 n_long = ctx.long_pairs_shard(qlen_cut, nal_cut, pass_table, r, W, thr)
                 st = ctx.stats(check=False)
+                if st.get('overflow_flags', 0) & 64:   # the ZeroDivisionError list grew: list them all
+                    n_long = ctx.long_pairs_shard(qlen_cut, nal_cut, pass_table, r, W, thr)
+                    st = ctx.stats(check=False)
                 part = ctx.long_edges(n_long)
                 ne = int(n_long)
                 mf = int(np.bincount(part[0], minlength=1).max()) if ne else 0
@@ -799,6 +811,8 @@ class PairShard(SweepShard):
                         grow = True
                     if st['deferred'] > st['deferred_capacity']:
                         ctx.reserve_deferred(int(st['deferred'] * 1.25) + 4096)
+                        grow = True
+                    if st.get('overflow_flags', 0) & 64:  # the ZeroDivisionError list grew: list them all
                         grow = True
                     if not grow:
                         break

@@ -527,6 +527,53 @@ def test_sweep_split_capped_one_gpu_equals_oracle(W, thr, gather, monkeypatch):
             c.close()
 
 
+def _zd_overflow_csr(n_dense=60, n_zd=400, seed=5):
+    """A dense locus where the cap binds (n_dense reads) beside a locus of n_zd reads with qlen2 == 0,
+    whose pairs all raise ZeroDivisionError (cluster.py:178-183): n_zd (n_zd - 1) / 2 listed pairs, more
+    than the list's first capacity (65,536)."""
+    from fslr_amd.prep import IntervalData
+    rng = np.random.default_rng(seed)
+    n = n_dense + n_zd
+    start = np.concatenate([100_000 + rng.integers(0, 40, n_dense), 900_000 + rng.integers(0, 40, n_zd)])
+    size = np.full(n, 1000)
+    qlen2 = np.concatenate([np.full(n_dense, 3000), np.zeros(n_zd, np.int64)])
+    o = np.argsort(start, kind='quicksort')
+    col = lambda x: np.asarray(x, np.int64)[o]
+    d = IntervalData(chrom=np.ones(n, np.int64)[o], start=col(start), end=col(start + size), aln_size=col(size),
+                     qcode=col(np.arange(n)), qnames=np.array([f'r{k}' for k in range(n)], dtype=object),
+                     n_alignments=np.full(n, 2, np.int64), qlen2=col(qlen2), middle=np.zeros(n, np.int64),
+                     index=np.arange(n))
+    return d.csr()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('W', [1, 2])
+def test_sweep_split_zero_division_list_overflow_follows_oracle(W):
+    """More ZeroDivisionError pairs than the device list holds, with the cap binding: the partition
+    (a zd_host query) grows the list and runs again, so the sharded replay decides on every pair and the
+    step raises like the oracle's reference loop — not 'rerun the query' forever."""
+    from fslr_amd.prep import fold_overlap_threshold, pass_table
+    csr = _zd_overflow_csr()
+    pt = pass_table([1, 1, 0.66, 0.66, 0.66, 0.5])
+    try:
+        o = O.run_core(_oracle_csr(csr), edge_threshold=10, use_cap=True)
+    except O.OracleZeroDivision:
+        o = None
+    thr_iv = fold_overlap_threshold(csr.iv_aln, 0.8)
+    if o is None:
+        with pytest.raises(ZeroDivisionError):
+            _sweep_shards_threads(csr, thr_iv, pt, W, 10)
+        return
+    ctxs, infos = _sweep_shards_threads(csr, thr_iv, pt, W, 10)
+    try:
+        a, b, I, U, fwd = _union_view(ctxs)
+        want = sorted(zip(o['edge_a'].tolist(), o['edge_b'].tolist(), o['edge_I'].tolist(), o['edge_U'].tolist()))
+        assert sorted(zip(a.tolist(), b.tolist(), I.tolist(), U.tolist())) == want
+    finally:
+        for c in ctxs:
+            c.close()
+
+
 def _sweep_gpu_worker(rank, world, port, out_dir):
     import torch
     import torch.distributed as dist

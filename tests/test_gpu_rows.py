@@ -133,3 +133,79 @@ def test_rows_long_read_declined():
         assert e.value.info['max_len'] == n
     finally:
         ctx.close()
+
+
+def _jittered_rows(n_reads, seed):
+    """Rows of reads with 1-4 intervals of ~1 kb whose starts are jittered by up to 700 bp around shared
+    loci, so the reciprocal overlaps spread over 0.3-1.0 (overlap 0.5 and 0.8 give different graphs)."""
+    rng = np.random.default_rng(seed)
+    L = rng.integers(1, 5, n_reads)
+    q = np.repeat(np.arange(n_reads, dtype=np.int64), L)
+    m = q.size
+    locus = rng.integers(0, 400, m) * 5000
+    start = locus + rng.integers(0, 700, m)
+    size = rng.integers(900, 1100, m)
+    rows = dict(chrom=rng.integers(1, 3, m).astype(np.int64), start=start.astype(np.int64),
+                end=(start + size).astype(np.int64), aln=size.astype(np.int64), qcode=q,
+                nal=np.repeat(L, L).astype(np.int64), qlen2=np.full(m, 5000, np.int64))
+    return rows, n_reads
+
+
+def _edge_set(ctx, st):
+    a, b, I, U = ctx.edges(st['n_edges'])
+    return sorted(zip(a.tolist(), b.tolist(), I.tolist(), U.tolist()))
+
+
+@pytest.mark.parametrize('engine', ['sweep', 'walk'])
+def test_rows_index_refolded_overlap_queries_new_windows(engine):
+    """A RowsIndex built (and its sweep windows cut) at overlap 0.8, then queried at 0.5 through
+    fslr_fold_thresholds: the windows follow the new thresholds (start_p <= end_q - thr_q), so the
+    edges equal a host-CSR context queried at 0.5 from the start (the fold left the
+    windows at 0.8's and the sweep dropped pairs silently)."""
+    from fslr_amd.prep import pass_table
+    rows, n = _jittered_rows(3000, 21)
+    order = np.argsort(rows['start'], kind='stable').astype(np.int64)
+    pt = pass_table([0.3] * 8)
+    r = _lib.Context(0)
+    h = _lib.Context(0)
+    try:
+        r.rows_upload(rows, n, 3)
+        info = r.set_reads_rows(order, None, 0.8)
+        r.reserve_edges(1 << 18)
+        r.build_index()
+        st8 = r.run_query(0.0, 0.0, pt, engine=engine)
+        e8 = _edge_set(r, st8)
+        r.fold_thresholds(0.5)
+        st5 = r.run_query(0.0, 0.0, pt, engine=engine)
+        e5 = _edge_set(r, st5)
+        d = r.device_csr(info['n_intervals'], info['n_chroms'])
+        h.set_reads(d['read_off'], d['read_qlen2'], d['read_nal'], d['iv_chrom'], d['iv_start'], d['iv_end'],
+                    fold_overlap_threshold(d['iv_aln'], 0.5), info['n_chroms'], iv_data_pos=d['data_pos'])
+        h.reserve_edges(1 << 18)
+        h.build_index()
+        sth = h.run_query(0.0, 0.0, pt, engine=engine)
+        assert len(e5) > len(e8) > 0
+        assert e5 == _edge_set(h, sth)
+    finally:
+        r.close()
+        h.close()
+
+
+def test_rows_code_out_of_range_is_invalid_not_a_fault():
+    """A qname code outside [0, n_codes) is reported as FSLR_ERR_INVALID before the grouping reads the
+    ranks (k_rows_isfirst / k_rows_rank read first[q] out of bounds); the context then takes
+    a valid upload."""
+    rows, n = _jittered_rows(200, 3)
+    order = np.argsort(rows['start'], kind='stable').astype(np.int64)
+    ctx = _lib.Context(0)
+    try:
+        for bad in (n, n + 1000, -5):
+            r2 = dict(rows, qcode=rows['qcode'].copy())
+            r2['qcode'][7] = bad
+            ctx.rows_upload(r2, n, 3)
+            with pytest.raises(_lib.FslrError, match='qname code out of range'):
+                ctx.set_reads_rows(order, None, 0.8)
+        ctx.rows_upload(rows, n, 3)
+        assert ctx.set_reads_rows(order, None, 0.8)['n_reads'] == n
+    finally:
+        ctx.close()

@@ -46,6 +46,8 @@ if has cli10m; then
   tail -3 $O/cli_10m.log
 fi
 if has hist; then
+  # the measurement build is made here on demand (it does not travel with the tree: .gpurunignore)
+  timeout -k 10 600 bash tools/build_variant.sh hist -DFSLR_PAIRS_HIST > $O/build_hist.log 2>&1 || { tail -20 $O/build_hist.log; exit 1; }
   FSLR_LIB=$R/fslr_amd/libfslr_hip_hist.so FSLR_ALLOW_STALE=1 timeout -k 10 300 python3 tools/pairs_hist.py $O/pairs_group_hist.json \
       > $O/hist.log 2>&1 || { echo "hist failed"; tail -20 $O/hist.log; exit 1; }
   tail -30 $O/hist.log
@@ -108,6 +110,7 @@ if has capshard; then
   tail -3 $O/capshard.log
 fi
 if has sclock; then
+  timeout -k 10 600 bash tools/build_variant.sh sclock -DFSLR_SWEEP_CLOCK > $O/build_sclock.log 2>&1 || { tail -20 $O/build_sclock.log; exit 1; }
   FSLR_LIB=$R/fslr_amd/libfslr_hip_sclock.so FSLR_ALLOW_STALE=1 timeout -k 10 300 python3 tools/sweep_clock.py $O/sweep_clock.json \
       > $O/sclock.log 2>&1 || { echo "sclock failed"; tail -20 $O/sclock.log; exit 1; }
   tail -12 $O/sclock.log
