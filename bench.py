@@ -212,35 +212,43 @@ def main():
             raise SystemExit(f'{engine} engine differs from the walk engine on this input')
         log(f'[rank 0] {engine} engine: edges and forward degrees identical to the walk engine')
 
-    # timed region: only the pair kernel's own events stay on the stream (profiling level 2); the
-    # per-phase events are recorded in one extra untimed step afterwards
+    # timed regions: only the pair kernels' own events stay on the stream (profiling level 2); the
+    # per-phase events are recorded in one extra untimed step afterwards.
+    # 1. repeat steps (secondary): a query on unchanged input keeps its length-gate ranges and its entry
+    #    count on the device (no mid-step readback), the edge cap checked on the device.
+    # 2. full-work steps (`value`): every query recomputes the gate ranges (k_len_bounds) and, on one GPU,
+    #    reads its entry count back and checks the cap with a host read, as a single query on new input
+    #    does; with N ranks each step still skips the host round trips (the partition's counts are checked
+    #    on the device against the synchronous step's), every kernel runs.
     ctx.set_profiling(2)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    for _ in range(args.steps):
-        step(repeat=True)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t_start
+
+    def timed(repeat, reuse):
+        ctx.set_query_reuse(reuse)
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0_ = time.perf_counter()
+        for _ in range(args.steps):
+            step(repeat=repeat)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        return time.perf_counter() - t0_
+
+    elapsed_rep = timed(True, True)
     if shard is None and not args.sync_cap and ctx.edge_cap_deferred_read():
         # a timed step's cap check fired: those steps needed the replay; time them synchronously
         log('[rank 0] the edge cap bound in a timed step: timing synchronous steps instead')
         args.sync_cap = True
-        torch.cuda.synchronize()
-        t_start = time.perf_counter()
-        for _ in range(args.steps):
-            step(repeat=True)
-        torch.cuda.synchronize()
-        elapsed = time.perf_counter() - t_start
+        elapsed_rep = timed(True, True)
+    elapsed = timed(shard is not None, False)        # one GPU: full synchronous steps
+    ctx.set_query_reuse(True)
     if shard is not None:
         # the timed steps repeated the last warmup step without host syncs (SweepShard.step repeat):
         # every rank's device checks and edge counts must agree with it
         shard.verify_repeat()
     st = ctx.stats()
-    kern = ctx.pair_kernel_times(args.steps)       # the timed steps' main pair-kernel launches
+    kern = ctx.pair_kernel_times(args.steps)       # the full-work steps' main pair-kernel launches
     kern2 = ctx.stage_kernel_times(1, args.steps) if st['engine'] == 'sweep' else np.zeros(0)   # pair stage
     lib_t = None
     cold_ms = None
@@ -249,8 +257,7 @@ def main():
         step()
         torch.cuda.synchronize()
         lib_t = ctx.timings()                         # hipEvents of one untimed step (library side)
-        # one cold step: a new input generation, so the query reads its entry count back mid-step
-        # (what the CLI's single query does; the timed steps repeat a query on unchanged input)
+        # one cold step: a new input generation (fslr_set_thresholds), as the CLI's single query
         ctx.set_profiling(0)
         ctx.set_thresholds(thr)
         torch.cuda.synchronize()
@@ -279,20 +286,19 @@ def main():
                       'query intervals + {B_EDGE} B x edges + {B_DEFER} B x deferred entries')
     cs = counted                                      # the walk engine's counts of this rank's read range
     tot = torch.tensor([elapsed, float(cs['evaluated_pairs']), float(cs['jaccard_evals']), float(st['n_edges']),
-                        float(st['max_fwd'])], dtype=torch.float64, device=dev if backend == 'nccl' else 'cpu')
+                        float(st['max_fwd']), elapsed_rep, float(st['matched_pairs'])], dtype=torch.float64,
+                       device=dev if backend == 'nccl' else 'cpu')
     capped = bool(info['capped']) if info is not None else False
     if dist:
-        t_max = tot[:1].clone()
+        t_max = tot[[0, 4, 5]].clone()
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-        sums = tot[1:4].clone()
+        sums = tot[[1, 2, 3, 6]].clone()
         dist.all_reduce(sums)
-        mf = tot[4:5].clone()
-        dist.all_reduce(mf, op=dist.ReduceOp.MAX)
-        elapsed = float(t_max.item())
-        pairs, jacc, n_edges = (float(x) for x in sums.tolist())
-        max_fwd = int(mf.item())
+        elapsed, max_fwd, elapsed_rep = (float(x) for x in t_max.tolist())
+        max_fwd = int(max_fwd)
+        pairs, jacc, n_edges, matched = (float(x) for x in sums.tolist())
     else:
-        pairs, jacc, n_edges = (float(x) for x in tot[1:4].tolist())
+        pairs, jacc, n_edges, matched = (float(x) for x in tot[[1, 2, 3, 6]].tolist())
         max_fwd = int(st['max_fwd'])
     ms_per_step = 1000.0 * elapsed / args.steps
     value = jacc / (elapsed / args.steps)
@@ -388,6 +394,19 @@ def main():
                             'overlap 0.8, cutoffs 1,1,.66,.66,.66,.5, qlen-diff .04, n-aln-diff .25',
                 'n_reads': n, 'n_intervals': csr.n_intervals,
                 'jaccard_evals_per_step': int(jacc),
+                'step': ('full work: index build, every pair kernel with the length-gate ranges recomputed, '
+                         + ('the entry count read back mid-query, components and the edge-cap check by a host '
+                            'read' if world == 1 else
+                            'both RCCL exchanges, the forest merge; the partition counts checked on the device')),
+                'kernel_evaluated_pairs_per_step': int(matched),
+                'kernel_evaluated_pairs_per_s': matched / (elapsed / args.steps),
+                'kernel_evaluated_note': 'read pairs the sweep actually evaluates (>= 1 match entry: first-fit, '
+                                         'U, the cut); the other Jaccard-evaluated pairs have I = 0 and are '
+                                         'decided without a kernel touching them (DESIGN.md §3.6)',
+                'repeat_step_ms': 1000.0 * elapsed_rep / args.steps,
+                'repeat_value': jacc / (elapsed_rep / args.steps),
+                'repeat_note': 'the same step repeated on unchanged input: the length-gate ranges and the entry '
+                               'count stay on the device, the edge cap is checked on the device',
                 'candidate_pairs_per_step': int(pairs),
                 'candidate_pairs_per_s': pairs / (elapsed / args.steps),
                 'edges': int(n_edges), 'max_fwd_degree': max_fwd,
@@ -412,9 +431,8 @@ def main():
                 if world > 1 else 'single GPU',
                 'transfer': transfer,
                 'cold_step_ms': cold_ms,
-                'cold_step_note': 'one step after a new input generation (fslr_set_thresholds): the query reads '
-                                  'its entry count back mid-step, as the CLI\'s single query does; ms_per_step '
-                                  'repeats the query on unchanged input (the count stays on the device)',
+                'cold_step_note': 'one step after a new input generation (fslr_set_thresholds), timed alone: '
+                                  'the same work as a timed full step',
             },
             'roofline': head_roof,
             'roofline_other_kernels': roofs[1:],

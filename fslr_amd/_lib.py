@@ -13,7 +13,7 @@ import numpy as np
 
 LIB_PATH = os.environ.get('FSLR_LIB') or os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libfslr_hip.so')
 
-ABI_VERSION = 20         # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
+ABI_VERSION = 21         # include/fslr_hip.h FSLR_ABI_VERSION this binding is written against
 FSLR_OK, FSLR_ERR_ZERO_DIVISION, FSLR_ERR_INVALID, FSLR_ERR_HIP, FSLR_ERR_NOMEM, FSLR_ERR_STATE = range(6)
 FSLR_MAX_L = 64
 FSLR_MAX_READS = 1 << 25
@@ -43,7 +43,7 @@ EXPORTED = ['fslr_abi_version', 'fslr_last_error', 'fslr_ctx_create', 'fslr_ctx_
             'fslr_cap_restrict', 'fslr_cap_copy_restricted', 'fslr_cap_install_restricted', 'fslr_rows_upload',
             'fslr_set_reads_rows', 'fslr_get_read_codes', 'fslr_get_csr', 'fslr_fold_thresholds',
             'fslr_position_costs', 'fslr_position_entries', 'fslr_set_position_filter', 'fslr_use_position_filter', 'fslr_long_pairs_shard',
-            'fslr_edge_cap_deferred', 'fslr_edge_cap_deferred_read']
+            'fslr_edge_cap_deferred', 'fslr_edge_cap_deferred_read', 'fslr_set_query_reuse']
 
 
 class HipUnavailable(RuntimeError):
@@ -132,6 +132,7 @@ def load(path: str = LIB_PATH):
         'fslr_ctx_create': (ctypes.c_int, [ctypes.c_int, vp, ctypes.POINTER(vp)]),
         'fslr_ctx_destroy': (None, [vp]),
         'fslr_set_profiling': (ctypes.c_int, [vp, ctypes.c_int]),
+        'fslr_set_query_reuse': (ctypes.c_int, [vp, ctypes.c_int]),
         'fslr_set_reads': (ctypes.c_int, [vp, ctypes.POINTER(Reads)]),
         'fslr_set_thresholds': (ctypes.c_int, [vp, vp]),
         'fslr_reserve_edges': (ctypes.c_int, [vp, i64]),
@@ -277,6 +278,11 @@ class Context:
         self._keep = ()
         if profiling:
             self._check(self._L.fslr_set_profiling(self._h, 1))
+
+    def set_query_reuse(self, enable: bool):
+        """False: every query does the full work (length-gate ranges, entry-count readback), as a single
+        query on new input does; True (default): a repeat on unchanged input keeps them."""
+        self._check(self._L.fslr_set_query_reuse(self._h, 1 if enable else 0))
 
     def set_profiling(self, level: int):
         """1: per-phase events and the pair-kernel events; 2: the pair-kernel events only; 0: off."""

@@ -187,6 +187,12 @@ void fslr_ctx_destroy(fslr_ctx* c) {
   delete c;
 }
 
+int fslr_set_query_reuse(fslr_ctx* c, int enable) {
+  if (!c) return FSLR_ERR_INVALID;
+  c->reuse = enable != 0;
+  return FSLR_OK;
+}
+
 int fslr_set_profiling(fslr_ctx* c, int enable) {
   if (!c) return FSLR_ERR_INVALID;
   HIP_TRY(c, hipSetDevice(c->device));
@@ -990,7 +996,7 @@ static int sweep_front(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64
   if (dest_n > 0) sweep_dest_hist(s, dest_n, dest_shift);   // ... or a partition's destinations
   s.dest_totals = dest_n > 0 ? c->part_cnt : nullptr;
   // the gate ranges depend on the reads and the two cuts only: a repeat query keeps them
-  if (c->lb_gen != c->input_gen || c->lb_q != p->qlen_cut || c->lb_n != p->nal_cut) {
+  if (!c->reuse || c->lb_gen != c->input_gen || c->lb_q != p->qlen_cut || c->lb_n != p->nal_cut) {
     HIP_TRY(c, launch_len_bounds(c->rmeta, 0, static_cast<int>(c->n), p->qlen_cut, p->nal_cut, c->lbounds, c->stream));
     c->lb_gen = c->input_gen;
     c->lb_q = p->qlen_cut;
@@ -1010,7 +1016,7 @@ static int sweep_front(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64
     s.p0 = s.p1 = nullptr;
     if (c->prof_phases) HIP_TRY(c, hipEventRecord(c->sw_ev[0], c->stream));
     // a repeat of the last synchronous query on unchanged input: same entry count, no readback
-    const bool fast = !defer && mode == 2 && attempt == 0 && c->sw_prev_gen == c->input_gen &&
+    const bool fast = c->reuse && !defer && mode == 2 && attempt == 0 && c->sw_prev_gen == c->input_gen &&
                       c->sw_prev_a0 == a_begin && c->sw_prev_a1 == a_end && c->sw_prev_q == p->qlen_cut &&
                       c->sw_prev_nc == p->nal_cut && c->sw_prev_umax == c->umax_host && c->sw_prev_n > 0 &&
                       c->sw_prev_n <= c->ent_cap && c->sw_prev_n < (int64_t(1) << 31) && !c->filter_active;

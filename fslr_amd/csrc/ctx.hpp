@@ -148,6 +148,7 @@ struct fslr_ctx {
   bool any_zero_aln = false;                // an aln_size == 0 interval: the walk engine replays it
   // sync-free repeat query: a full one-pass sweep query on unchanged input (same reads, thresholds,
   // filter, parameters) has the previous query's entry count, so the host need not read it back
+  bool reuse = true;                        // fslr_set_query_reuse: repeat queries keep what they can
   uint64_t input_gen = 1;                   // bumped by set_reads / set_thresholds / set_chrom_filter / set_shard
   uint64_t sw_prev_gen = 0;                 // input_gen of the last synchronous sweep query (0: none)
   double sw_prev_q = 0, sw_prev_nc = 0;

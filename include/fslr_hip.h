@@ -75,7 +75,7 @@
 extern "C" {
 #endif
 
-#define FSLR_ABI_VERSION 20
+#define FSLR_ABI_VERSION 21
 #define FSLR_MAX_L 64                /* max intervals per read (bitmask width) */
 #define FSLR_MAX_READS (1 << 25)     /* read rank packs into bits 6..30 of the index record */
 #define FSLR_THR_ZERO_ALN INT32_MIN
@@ -203,6 +203,10 @@ void fslr_ctx_destroy(fslr_ctx *ctx);
 int  fslr_set_profiling(fslr_ctx *ctx, int enable);     /* 1: hipEvents per phase + around the pair kernel;
                                                            2: around the pair kernel only (fewer stream
                                                            markers in a timed loop); 0: off */
+/* enable (the default) = a sweep query on unchanged input (reads, thresholds, filter, range, cuts) repeats
+ * the last synchronous one: it keeps the length-gate ranges and its entry count stays on the device (no
+ * mid-query readback).  0 = every query does the full work, as a single query on new input does. */
+int  fslr_set_query_reuse(fslr_ctx *ctx, int enable);
 
 /* Copy the CSR (host pointers) into context-owned HBM buffers (H2D). */
 int  fslr_set_reads(fslr_ctx *ctx, const fslr_reads *reads);

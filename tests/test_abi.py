@@ -35,7 +35,7 @@ def test_library_exports_all_symbols(lib):
 
 
 def test_abi_version(lib):
-    assert lib.fslr_abi_version() == _lib.ABI_VERSION == 20
+    assert lib.fslr_abi_version() == _lib.ABI_VERSION == 21
 
 
 def test_gfx950_code_object_present(tmp_path):
