@@ -176,8 +176,10 @@ __global__ void __launch_bounds__(256) k_cap_frontier_w(const int* __restrict__ 
                                                         const int* __restrict__ fwd, int thr, int* __restrict__ back,
                                                         const int* __restrict__ fin, const unsigned* __restrict__ fin_n,
                                                         int* __restrict__ fout, unsigned* __restrict__ fout_n,
-                                                        int* __restrict__ tl, unsigned* __restrict__ tn) {
+                                                        int* __restrict__ tl, unsigned* __restrict__ tn, int n_reads,
+                                                        long long n_rows) {
   const int nin = static_cast<int>(*fin_n);
+  FSLR_BOUND(nin - 1, n_reads + 1);
   const int lane = threadIdx.x & 63;
   const int wave = static_cast<int>((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
   const int nwaves = static_cast<int>((gridDim.x * blockDim.x) >> 6);
@@ -186,8 +188,11 @@ __global__ void __launch_bounds__(256) k_cap_frontier_w(const int* __restrict__ 
     int k0 = 0, len = 0;
     if (i < nin) {
       const int x = fin[i];
+      FSLR_BOUND(x, n_reads);
       k0 = a0[x];
       len = (kRows ? a1[x] : a0[x + 1]) - k0;
+      FSLR_BOUND(k0, n_rows + 1);
+      FSLR_BOUND(k0 + len, n_rows + 1);
     }
     const int incl = wave_incl_scan(len);
     const int total = rdl(incl, 63);
@@ -203,7 +208,9 @@ __global__ void __launch_bounds__(256) k_cap_frontier_w(const int* __restrict__ 
         for (int st = 32; st > 0; st >>= 1)
           if (__shfl(incl, o + st - 1) <= r) o += st;
         const int k = __shfl(k0, o) + r - (__shfl(incl, o) - __shfl(len, o));
+        if (on[u]) FSLR_BOUND(k, n_rows);
         y[u] = on[u] ? (kRows ? rows[k].y : adj[k]) : 0;
+        if (on[u]) FSLR_BOUND(y[u], n_reads);
       }
 #pragma unroll
       for (int u = 0; u < 2; ++u) fy[u] = on[u] ? fwd[y[u]] : 0;
@@ -2110,10 +2117,12 @@ int cap_local(fslr_ctx* c, int thr, CapWork* w, const int2* E, const int* F, int
       for (int r = 0; r < 16; ++r) {
         if (rstart)
           k_cap_frontier_w<true><<<fg, 256, 0, s>>>(rstart, rend, E, nullptr, F, thr, w->back, fl[r & 1], w->fcnt + r,
-                                                     fl[(r + 1) & 1], w->fcnt + r + 1, w->tl, w->fcnt + 32);
+                                                     fl[(r + 1) & 1], w->fcnt + r + 1, w->tl, w->fcnt + 32,
+                                                     static_cast<int>(n), ne);
         else
           k_cap_frontier_w<false><<<fg, 256, 0, s>>>(w->aoff, nullptr, nullptr, w->adj, F, thr, w->back, fl[r & 1],
-                                                      w->fcnt + r, fl[(r + 1) & 1], w->fcnt + r + 1, w->tl, w->fcnt + 32);
+                                                      w->fcnt + r, fl[(r + 1) & 1], w->fcnt + r + 1, w->tl, w->fcnt + 32,
+                                                      static_cast<int>(n), ne);
       }
       HIP_TRY(c, hipGetLastError());
       unsigned last = 0;

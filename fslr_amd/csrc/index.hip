@@ -362,8 +362,8 @@ struct TilePrefix {
   __device__ __forceinline__ unsigned long long incl(int t) const { return max_u64(group_excl[t / kGroup], loc[t]); }
 };
 
-// kBwd = false (the sweep engine, lean index): forward counts only, no pmax window (rng_s[q].y = -1);
-// ends from the records (idx4 .y; endkey unused), the chromosome from its begin in crange
+// kBwd = false (the sweep engine, lean index): the sweep windows (swin) only, no pmax window and no
+// rng_s; ends from the records (idx4 .y; endkey unused), the chromosome from its begin in crange
 // (n_chroms <= 64)
 template <bool kBwd>
 __global__ __launch_bounds__(kRangeBlock) void k_ranges(const int4* __restrict__ idx4, int shard, int n_shards,
@@ -420,7 +420,7 @@ __global__ __launch_bounds__(kRangeBlock) void k_ranges(const int4* __restrict__
     for (int u = 0; u < kPerQ; ++u) {
       const int q = q0 + threadIdx.x + u * kRangeBlock;
       pre4[u] = q < wp1 ? idx4[q] : make_int4(0, 0, 0, 0);
-      preg[u] = q < wp1 && swin && gate ? gate[q] : make_int2(0, 0);
+      preg[u] = q < wp1 ? gate[q] : make_int2(0, 0);
     }
   }
 #pragma unroll
@@ -443,6 +443,36 @@ __global__ __launch_bounds__(kRangeBlock) void k_ranges(const int4* __restrict__
     }
     const int2 cr = crange[c];
     const int s = w_st[q - w0];
+    if constexpr (!kBwd) {
+      // the lean build writes the sweep windows only (the walk engine, the cap replay and k_swin read
+      // n_fwd from k_ranges<true>'s rng_s, ensure_bwd_ranges / ensure_walk_index): one search per
+      // position, for the window's bound start_p <= end_q - thr_q (cluster.py:133-136), or the whole
+      // forward range start_p <= end_q when q's read has qlen2 or n_alignments 0 (cluster.py:178-183)
+      const int2 gq = preg[u];
+      const int key = gq.x != 0 && (gq.y & 0xFFFFFF) != 0 ? min(e, e - rq.z) : e;
+      const int hi_lim = min(cr.y, w1);
+      int lo = q + 1, hi = hi_lim;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (w_st[mid - w0] <= key) lo = mid + 1; else hi = mid;
+      }
+      if (lo == hi_lim && hi_lim < cr.y) {     // the window leaves the LDS span: gallop in global memory
+        int step = 1;
+        hi = lo;
+        while (hi < cr.y && s_start[hi] <= key) {
+          lo = hi + 1;
+          hi = lo + step;
+          step <<= 1;
+        }
+        if (hi > cr.y) hi = cr.y;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (s_start[mid] <= key) lo = mid + 1; else hi = mid;
+        }
+      }
+      swin[q] = lo - q - 1;
+      continue;
+    }
     // forward: first p in (q, cr.y) with start_p > e
     const int hi_lim = min(cr.y, w1);
     int lo = q + 1, hi = hi_lim;
@@ -488,10 +518,6 @@ __global__ __launch_bounds__(kRangeBlock) void k_ranges(const int4* __restrict__
         m = a - q - 1;
       }
       swin[q] = m;
-    }
-    if constexpr (!kBwd) {
-      rng_s[q] = make_int2(n_fwd, -1);
-      continue;
     }
     // backward: first p in [cr.x, q) with pmax_p >= s (pmax non-decreasing inside a chromosome)
     const int lo_lim = max(cr.x, w0);

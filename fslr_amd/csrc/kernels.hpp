@@ -13,8 +13,19 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cassert>
 #include <cstddef>
 #include <cstdint>
+
+// The bounds-checked build (make -C fslr_amd/csrc bounds -> libfslr_hip_bounds.so): a device assert on
+// the global indices of the paths only dense inputs reach (k_sweep<2>'s deep tiles, k_sweep_pairs' long
+// runs and windows, the cap replay's frontier).  A failing index aborts the launch with its file:line
+// instead of reading another allocation.  Compiled out of the product build.
+#ifdef FSLR_DEBUG_BOUNDS
+#define FSLR_BOUND(i, n) assert(static_cast<long long>(i) >= 0 && static_cast<long long>(i) < static_cast<long long>(n))
+#else
+#define FSLR_BOUND(i, n) ((void)0)
+#endif
 
 namespace fslr {
 
