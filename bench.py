@@ -329,6 +329,7 @@ def main():
                 # launch's cycles on 1024 SIMDs (PMC), and where the wave-cycles went
                 'valu_issue_frac': valu, 'wave_cycle_split': split,
                 'traffic_source': os.path.relpath(args.traffic_json, REPO) if traffic else None,
+                'traffic_basis': e.get('correction') if traffic else None,
                 'waste_ratio': (traffic / algo) if traffic else None, 'kernel_ms': kms,
                 'kernel_launches_timed': int(times.size), 'algo_bytes_per_launch': int(algo),
                 'algo_bytes_model': model}

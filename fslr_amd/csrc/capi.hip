@@ -370,6 +370,7 @@ static int install_thresholds(fslr_ctx* c) {
     const IndexBufs b = index_bufs(c);
     HIP_TRY(c, launch_index_swin(b, static_cast<int>(c->ni_idx), c->stream));
   }
+  c->idx_tt_valid = false;                        // the windows changed: the plan sums them again
   if (c->filter_active && c->pf_on)
     HIP_TRY(c, launch_pos_gather(c->pf_sel, static_cast<int>(c->pf_end - c->pf_lo), c->dchrom, c->drec, c->dgate,
                                  c->pf_lmap, c->fdchrom, c->fdrec, c->fdgate, c->stream));
@@ -806,6 +807,7 @@ static IndexBufs index_bufs(fslr_ctx* c) {
   b.qpos = c->qpos;
   b.rng_s = c->rng_s;
   b.swin = c->swin;
+  b.tile_tests = nullptr;
   b.idx4 = c->idx4;
   b.idx_gate = c->idx_gate;
   return b;
@@ -879,8 +881,20 @@ int fslr_build_index(fslr_ctx* c) {
   // where the data-order path applies and one context covers every query read
   const bool full = !c->filter_active && !(c->have_data_pos && c->n_chroms <= 64 && c->n_shards == 1);
   const int nch = c->filter_active ? c->n_chroms_f : c->n_chroms;
-  HIP_TRY(c, launch_build_index(index_bufs(c), static_cast<int>(c->n), static_cast<int>(c->ni_idx), nch, full,
-                                c->stream));
+  IndexBufs ib = index_bufs(c);
+  // the lean build also sums each 64-position tile's windows (the sweep plan's pair tests)
+  const bool tt = !full && ib.dchrom && nch <= 64 && c->n_shards == 1;
+  c->idx_tt_valid = false;
+  if (tt) {
+    const int64_t tiles = (c->ni_idx + 63) / 64 + 1;
+    if (tiles > c->idx_tt_cap) {
+      if (int rc = dalloc(c, &c->idx_tt, tiles)) return rc;
+      c->idx_tt_cap = tiles;
+    }
+    ib.tile_tests = c->idx_tt;
+  }
+  HIP_TRY(c, launch_build_index(ib, static_cast<int>(c->n), static_cast<int>(c->ni_idx), nch, full, c->stream));
+  c->idx_tt_valid = tt;
   c->index_lean = !full && index_bufs(c).dchrom && nch <= 64;
   c->lean_keys = false;
   c->built_n_chroms = nch;
@@ -974,7 +988,10 @@ static int sweep_front(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64
   s.lb = c->lbounds;
   s.tile_cnt = c->sw_tile;
   s.tile_off = c->sw_tile + c->sw_tiles;
-  s.tile_tests = c->sw_tile + 2 * c->sw_tiles;
+  // the lean index build summed the tiles' windows already, unless a position filter's query range ends
+  // inside the index (its last query tile then holds fewer positions than the index tile)
+  s.tests_ready = c->idx_tt_valid && s.nq == static_cast<int>(nix);
+  s.tile_tests = s.tests_ready ? c->idx_tt : c->sw_tile + 2 * c->sw_tiles;
   s.tile_ub = c->sw_tile + 3 * c->sw_tiles;
   s.edges = c->edges;
   s.edge_iu = c->edge_iu;

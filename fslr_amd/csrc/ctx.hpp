@@ -148,6 +148,9 @@ struct fslr_ctx {
   bool any_zero_aln = false;                // an aln_size == 0 interval: the walk engine replays it
   // sync-free repeat query: a full one-pass sweep query on unchanged input (same reads, thresholds,
   // filter, parameters) has the previous query's entry count, so the host need not read it back
+  long long* idx_tt = nullptr;              // the lean index build's per-tile window sums (SweepArgs::tile_tests)
+  int64_t idx_tt_cap = 0;
+  bool idx_tt_valid = false;
   bool reuse = true;                        // fslr_set_query_reuse: repeat queries keep what they can
   uint64_t input_gen = 1;                   // bumped by set_reads / set_thresholds / set_chrom_filter / set_shard
   uint64_t sw_prev_gen = 0;                 // input_gen of the last synchronous sweep query (0: none)

@@ -21,6 +21,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "kernels.hpp"
+#include "wave.hpp"
 
 namespace fslr {
 namespace {
@@ -372,7 +373,8 @@ __global__ __launch_bounds__(kRangeBlock) void k_ranges(const int4* __restrict__
                                                         TilePrefix tile_incl,
                                                         const int2* __restrict__ crange, int ni,
                                                         int2* __restrict__ rng_s, int* __restrict__ swin,
-                                                        const int2* __restrict__ gate, int n_chroms = 0) {
+                                                        const int2* __restrict__ gate, int n_chroms = 0,
+                                                        long long* __restrict__ tile_tests = nullptr) {
   __shared__ int w_st[kRangeSpan + 2 * kWin];    // starts of [w0, w1)
   __shared__ int w_pm[kBwd ? kRangeSpan + kWin : 1];   // pmax (end part) of [w0, q0 + kRangeSpan)
   __shared__ unsigned long long t_part[kBwd ? kRangeBlock : 1];
@@ -422,6 +424,56 @@ __global__ __launch_bounds__(kRangeBlock) void k_ranges(const int4* __restrict__
       pre4[u] = q < wp1 ? idx4[q] : make_int4(0, 0, 0, 0);
       preg[u] = q < wp1 ? gate[q] : make_int2(0, 0);
     }
+    // The lean build writes the sweep windows only (the walk engine, the cap replay and k_swin read
+    // n_fwd from k_ranges<true>'s rng_s: ensure_bwd_ranges / ensure_walk_index): one search per
+    // position, for the window's bound start_p <= end_q - thr_q (cluster.py:133-136), or the whole
+    // forward range start_p <= end_q when q's read has qlen2 or n_alignments 0 (cluster.py:178-183).
+    // With `tile_tests`, each wave's 64 positions are one 64-position tile of the sweep: the wave sums
+    // their windows (the tile's pair tests, which the sweep's plan scans for its upper-bound slots).
+#pragma unroll
+    for (int u = 0; u < kPerQ; ++u) {
+      const int q = q0 + threadIdx.x + u * kRangeBlock;
+      const int4 rq = pre4[u];
+      int m = 0;
+      if (q < wp1 && (n_shards == 1 || shard_owns(rq.w >> 6, shard, n_shards))) {
+        const int e = rq.y;
+        int c = 0;                                   // the last chromosome beginning at or before q
+#pragma unroll
+        for (int b = 32; b > 0; b >>= 1)
+          if (c + b < 64 && c_beg[c + b] <= q) c += b;
+        const int2 cr = crange[c];
+        const int2 gq = preg[u];
+        const int key = gq.x != 0 && (gq.y & 0xFFFFFF) != 0 ? min(e, e - rq.z) : e;
+        const int hi_lim = min(cr.y, w1);
+        int lo = q + 1, hi = hi_lim;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (w_st[mid - w0] <= key) lo = mid + 1; else hi = mid;
+        }
+        if (lo == hi_lim && hi_lim < cr.y) {       // the window leaves the LDS span: gallop in global memory
+          int step = 1;
+          hi = lo;
+          while (hi < cr.y && s_start[hi] <= key) {
+            lo = hi + 1;
+            hi = lo + step;
+            step <<= 1;
+          }
+          if (hi > cr.y) hi = cr.y;
+          while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (s_start[mid] <= key) lo = mid + 1; else hi = mid;
+          }
+        }
+        m = lo - q - 1;
+        swin[q] = m;
+      }
+      if (tile_tests) {
+        const int tot = rdl(wave_incl_scan(m), kWave - 1);
+        const int tq = q0 + (threadIdx.x & ~(kWave - 1)) + u * kRangeBlock;   // the wave's tile
+        if ((threadIdx.x & (kWave - 1)) == 0 && tq < wp1) tile_tests[tq / kWave] = tot;
+      }
+    }
+    return;
   }
 #pragma unroll
   for (int u = 0; u < kPerQ; ++u) {
@@ -443,36 +495,6 @@ __global__ __launch_bounds__(kRangeBlock) void k_ranges(const int4* __restrict__
     }
     const int2 cr = crange[c];
     const int s = w_st[q - w0];
-    if constexpr (!kBwd) {
-      // the lean build writes the sweep windows only (the walk engine, the cap replay and k_swin read
-      // n_fwd from k_ranges<true>'s rng_s, ensure_bwd_ranges / ensure_walk_index): one search per
-      // position, for the window's bound start_p <= end_q - thr_q (cluster.py:133-136), or the whole
-      // forward range start_p <= end_q when q's read has qlen2 or n_alignments 0 (cluster.py:178-183)
-      const int2 gq = preg[u];
-      const int key = gq.x != 0 && (gq.y & 0xFFFFFF) != 0 ? min(e, e - rq.z) : e;
-      const int hi_lim = min(cr.y, w1);
-      int lo = q + 1, hi = hi_lim;
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (w_st[mid - w0] <= key) lo = mid + 1; else hi = mid;
-      }
-      if (lo == hi_lim && hi_lim < cr.y) {     // the window leaves the LDS span: gallop in global memory
-        int step = 1;
-        hi = lo;
-        while (hi < cr.y && s_start[hi] <= key) {
-          lo = hi + 1;
-          hi = lo + step;
-          step <<= 1;
-        }
-        if (hi > cr.y) hi = cr.y;
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          if (s_start[mid] <= key) lo = mid + 1; else hi = mid;
-        }
-      }
-      swin[q] = lo - q - 1;
-      continue;
-    }
     // forward: first p in (q, cr.y) with start_p > e
     const int hi_lim = min(cr.y, w1);
     int lo = q + 1, hi = hi_lim;
@@ -632,7 +654,7 @@ hipError_t launch_build_index(const IndexBufs& b, int n, int ni, int n_chroms, b
                                                           b.idx_gate, b.s_start, b.endkey, b.vals);
       k_ranges<false><<<(ni + kRangeSpan - 1) / kRangeSpan, kRangeBlock, 0, s>>>(
           b.idx4, b.shard, b.n_shards, b.s_start, nullptr,
-          TilePrefix{nullptr, nullptr}, b.crange, ni, b.rng_s, b.swin, b.idx_gate, n_chroms);
+          TilePrefix{nullptr, nullptr}, b.crange, ni, b.rng_s, b.swin, b.idx_gate, n_chroms, b.tile_tests);
       return hipGetLastError();
     }
     k_chrom_scatter<true><<<ntl, kTileThreads, 0, s>>>(b.dchrom, b.drec, b.dgate, b.chist, ni, ntl, rounds, b.idx4, b.idx_gate,

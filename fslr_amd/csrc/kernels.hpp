@@ -122,6 +122,8 @@ struct IndexBufs {
   int* qpos;                          // out [NI] CSR order
   int2* rng_s;                        // out [NI] sorted order
   int* swin;                          // out [NI] the sweep's forward window (k_ranges: swin)
+  long long* tile_tests;              // out [NI / 64 + 1] or nullptr: per 64-position tile, the sum of swin
+                                      // (the lean build; the sweep's plan then skips k_tile_tests)
   int4* idx4;                         // out [NI]
   int2* idx_gate;                     // out [NI]
 };
@@ -201,6 +203,7 @@ struct SweepArgs {
   long long* tile_cnt;                // [ceil(ni / 64)] match entries of each 64-position tile
   long long* tile_off;                // its exclusive scan: the tile's place in `ent`
   long long* tile_tests;              // [tiles] pair tests of the tile (its forward-range total)
+  bool tests_ready;                   // tile_tests already hold the sums (the lean index build's)
   long long* tile_ub;                 // their exclusive scan: the tile's upper-bound slot in ent_ub
   unsigned long long* ent_ub;         // (one pass) entries at their tiles' upper-bound slots
   long long ub_cap;

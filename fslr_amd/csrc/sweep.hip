@@ -99,7 +99,6 @@ __device__ __forceinline__ int run_add(int* bin, int key, bool act, int lane) {
 
 constexpr int kHistMax = 1024;             // coarse A buckets the one-pass sweep counts (LDS)
 
-
 // kMode 0: count the tile's entries (two-pass fallback), 1: write them at the tile's scanned offset
 // (two-pass fallback), 2: one pass — write them at the tile's upper-bound slot (its forward-range
 // total, the pair tests) and count them; k_compact then packs the tiles.
@@ -613,51 +612,12 @@ __device__ __forceinline__ void bitonic_il(unsigned long long& a, unsigned long 
   if constexpr (N >= 128) bitonic_il_steps<128, 64>(a, b, lane);
 }
 
-// 64-bit DPP move (two dword moves with the same control)
-template <int kCtrl, int kRowMask, bool kBound>
-__device__ __forceinline__ unsigned long long dpp64(unsigned long long v) {
-  const unsigned lo = static_cast<unsigned>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), kCtrl, kRowMask, 0xF, kBound));
-  const unsigned hi = static_cast<unsigned>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v >> 32), kCtrl, kRowMask, 0xF, kBound));
-  return (static_cast<unsigned long long>(hi) << 32) | lo;
+// group sort key: run (7 bits) << 39 | B << 14 | i << 7 | j; the segment key (run, B) is key >> 14
+__device__ __forceinline__ unsigned long long group_key(unsigned long long e, int r) {
+  return (static_cast<unsigned long long>(r) << 39) | (e & ((1ull << 39) - 1));
 }
 
-// inclusive OR scan over the wave's 64 lanes restarted at each segment: lane l's result is the OR of
-// lanes [h, l] (h: the lane starting l's segment, h <= l).  The DPP pattern of wave_incl_scan (row_shr
-// 1/2/4/8, row_bcast 15/31), each step taken only from lanes of the same segment.
-__device__ __forceinline__ unsigned long long seg_or_scan(unsigned long long v, int lane, int h) {
-  unsigned long long w;
-  w = dpp64<0x111, 0xF, true>(v);
-  if (lane - 1 >= h) v |= w;
-  w = dpp64<0x112, 0xF, true>(v);
-  if (lane - 2 >= h) v |= w;
-  w = dpp64<0x114, 0xF, true>(v);
-  if (lane - 4 >= h) v |= w;
-  w = dpp64<0x118, 0xF, true>(v);
-  if (lane - 8 >= h) v |= w;
-  w = dpp64<0x142, 0xA, false>(v);                  // rows 1, 3 <- lanes 15, 47
-  if ((lane & 16) && (lane & ~15) - 1 >= h) v |= w;
-  w = dpp64<0x143, 0xC, false>(v);                  // rows 2, 3 <- lane 31
-  if ((lane & 32) && 31 >= h) v |= w;
-  return v;
-}
-
-// group sort key: run (7 bits) << 46 | B << 21 | i << 14 | j << 7 | o, o = the entry's place in the
-// window (keys are distinct without it: it only carries the entry to its sorted place, so its L_B,
-// gathered before the sort, can be fetched from the lane that loaded it). The segment key (run, B) is
-// key >> 21, the row key (run, B, i) key >> 14, the column j (key >> 7) & 63.
-__device__ __forceinline__ unsigned long long group_key(unsigned long long e, int r, int o) {
-  return (static_cast<unsigned long long>(r) << 46) | ((e & ((1ull << 39) - 1)) << 7) | static_cast<unsigned>(o);
-}
-
-#ifndef FSLR_PAIRS_EARLY
-#define FSLR_PAIRS_EARLY 0
-#endif
-#ifdef FSLR_PAIRS_WPE
-#define FSLR_PAIRS_ATTR __attribute__((amdgpu_waves_per_eu(FSLR_PAIRS_WPE)))
-#else
-#define FSLR_PAIRS_ATTR
-#endif
-__global__ __launch_bounds__(kSwBlock) FSLR_PAIRS_ATTR void k_sweep_pairs(SweepArgs g) {
+__global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
   __shared__ __attribute__((aligned(16))) unsigned long long scr_all[kSwWaves][kScrWords];
   __shared__ int runa_all[kSwWaves][kStageE];                 // per run of the group: A | L_A << 25, edges formed
   __shared__ int runf_all[kSwWaves][kStageE];
@@ -907,23 +867,13 @@ __global__ __launch_bounds__(kSwBlock) FSLR_PAIRS_ATTR void k_sweep_pairs(SweepA
       const int r1 = __popcll(H0) + __popcll(H1 & upto(lane)) - 1;
       const bool v0 = lane < gend, v1 = lane + kWave < gend;
       const bool hv0 = h0 && v0, hv1 = h1 && v1;
-      if (v0) FSLR_BOUND(entry_a(e0), g.n_reads), FSLR_BOUND((e0 >> 14) & kRankMask, g.n_reads);
-      if (v1) FSLR_BOUND(entry_a(e1), g.n_reads), FSLR_BOUND((e1 >> 14) & kRankMask, g.n_reads);
-      int la0 = 0, la1 = 0;                                        // in flight during the sort
-      if (hv0) la0 = RL[entry_a(e0)];
+      int la0 = 0, la1 = 0;
+      if (hv0) FSLR_BOUND(entry_a(e0), g.n_reads);
+      if (hv1) FSLR_BOUND(entry_a(e1), g.n_reads);
+      if (hv0) la0 = RL[entry_a(e0)];                              // in flight during the sort
       if (hv1) la1 = RL[entry_a(e1)];
-      const long long sn = s + gend;
-      unsigned long long n0 = ~0ull, n1 = ~0ull, nn = ~0ull;
-#if FSLR_PAIRS_EARLY
-      // every entry's L_B, then the next window, before the sort: loads complete in order, so the
-      // segment setup's wait for L_B leaves the window in flight (measured slower at cfg3: 260 vs 252 us)
-      int lbe0 = 0, lbe1 = 0;
-      if (v0) lbe0 = RL[(e0 >> 14) & kRankMask];
-      if (v1) lbe1 = RL[(e1 >> 14) & kRankMask];
-      if (sn < c1) load_window(sn, n0, n1, nn);
-#endif
-      unsigned long long k0 = v0 ? group_key(e0, r0, lane) : ~0ull;
-      unsigned long long k1 = v1 ? group_key(e1, r1, lane + kWave) : ~0ull;
+      unsigned long long k0 = v0 ? group_key(e0, r0) : ~0ull;
+      unsigned long long k1 = v1 ? group_key(e1, r1) : ~0ull;
       // the group's network: the smallest of 32 / 64 / 128 elements that holds it (a group of <= 64
       // entries sits in k0; its upper half moves to lanes [0, 32) as the second slot)
       if (gend > kWave) {
@@ -949,112 +899,19 @@ __global__ __launch_bounds__(kSwBlock) FSLR_PAIRS_ATTR void k_sweep_pairs(SweepA
       const unsigned long long w1 = __shfl_up(k1, 1);
       const unsigned long long q1 = lane > 0 ? w1 : k0_63;
       // segments = read pairs (run, B); a row repeated inside a segment sits next to itself
-      const bool s0 = v0 && (lane == 0 || (k0 >> 21) != (q0 >> 21));
-      const bool s1 = v1 && (k1 >> 21) != (q1 >> 21);
-      const bool d0 = v0 && !s0 && (k0 >> 14) == (q0 >> 14);
-      const bool d1 = v1 && !s1 && (k1 >> 14) == (q1 >> 14);
-#if FSLR_PAIRS_EARLY
-      // L_B of each segment: fetched from the lane that loaded the entry (window place o)
-      const int lbsrc = lbe0 | lbe1 << 16;
-      const int o0 = static_cast<int>(k0 & 127u), o1 = static_cast<int>(k1 & 127u);
-      const int lv0 = __shfl(lbsrc, o0 & (kWave - 1)), lv1 = __shfl(lbsrc, o1 & (kWave - 1));
-      const int lb0 = (o0 >= kWave ? lv0 >> 16 : lv0) & 0xFFFF;
-      const int lb1 = (o1 >= kWave ? lv1 >> 16 : lv1) & 0xFFFF;
-#endif
-#ifdef FSLR_PAIRS_V2
-      // Register-resident segments: each read pair's last entry (its segment's tail) evaluates it.
-      // The head and row-repeat flags are ballots (the 128 positions are lanes 0-63 of k0, then of k1),
-      // a segment's entry count is the distance to its head, its column bits a segmented OR scan on DPP;
-      // no per-segment LDS tables.
-      const unsigned long long S0 = __ballot(s0), S1 = __ballot(s1);
-      const unsigned long long D0 = __ballot(d0), D1 = __ballot(d1);
-      const int nseg = __popcll(S0) + __popcll(S1);
-#ifdef FSLR_PAIRS_HIST
-      if (lane == 0) {
-        atomicAdd(&g.counters[43], static_cast<unsigned long long>(nseg));
-        atomicAdd(&g.counters[44], static_cast<unsigned long long>(__popcll(H0 & (gend >= kWave ? ~0ull : (1ull << gend) - 1)) +
-                                                                  __popcll(H1 & (gend <= kWave ? 0ull : gend >= 2 * kWave ? ~0ull : (1ull << (gend - kWave)) - 1))));
-      }
-#endif
-      wave_lds_sync();                                             // the previous group's reads are done
-      if (hv0) {
-        RUNA[r0] = static_cast<int>(static_cast<unsigned>(entry_a(e0)) | static_cast<unsigned>(la0) << 25);
-        RUNF[r0] = 0;
-      }
-      if (hv1) {
-        RUNA[r1] = static_cast<int>(static_cast<unsigned>(entry_a(e1)) | static_cast<unsigned>(la1) << 25);
-        RUNF[r1] = 0;
-      }
-      // tails: the next position starts a segment, or ends the group
-      const bool t0 = v0 && (lane + 1 == gend || (lane < kWave - 1 ? ((S0 >> (lane + 1)) & 1ull) != 0 : (S1 & 1ull) != 0));
-      const bool t1 = v1 && (lane + kWave + 1 == gend || (lane < kWave - 1 && ((S1 >> (lane + 1)) & 1ull) != 0));
-      // each position's segment head: in row 0 (S0 holds lane 0), in row 1 or carried over from row 0 (-1)
-      const int hd0 = 63 - __builtin_clzll(S0 & upto(lane));
-      const unsigned long long m1 = S1 & upto(lane);
-      const int hd1 = m1 ? 63 - __builtin_clzll(m1) : -1;
-      const int last0 = 63 - __builtin_clzll(S0);                  // the head of position 63's segment
-#if !FSLR_PAIRS_EARLY
-      int lb0 = 0, lb1 = 0;                                        // L_B, gathered by each segment's tail
-      if (t0) lb0 = RL[(k0 >> 21) & kRankMask];
-      if (t1) lb1 = RL[(k1 >> 21) & kRankMask];
-      if (sn < c1) load_window(sn, n0, n1, nn);                    // the next window, in flight meanwhile
-#endif
-      unsigned long long c0 = v0 ? 1ull << ((k0 >> 7) & 63u) : 0ull;
-      unsigned long long c1 = v1 ? 1ull << ((k1 >> 7) & 63u) : 0ull;
-      c0 = seg_or_scan(c0, lane, hd0);
-      c1 = seg_or_scan(c1, lane, hd1 < 0 ? 0 : hd1);
-      const unsigned long long c63 = (static_cast<unsigned long long>(static_cast<unsigned>(rdl(static_cast<int>(c0 >> 32), 63))) << 32) |
-                                     static_cast<unsigned>(rdl(static_cast<int>(c0), 63));
-      if (hd1 < 0) c1 |= c63;
-      wave_lds_sync();                                             // the run table is written
-      FSLR_PCK(2);
-      if (es.n + nseg > kPairEdgeStage) es.flush(eo, lane);
-#pragma unroll
-      for (int row = 0; row < 2; ++row) {
-        const bool t = row ? t1 : t0;
-        const unsigned long long k = row ? k1 : k0;
-        const int e = row ? lane + kWave : lane;
-        const int h = row ? (hd1 < 0 ? last0 : hd1 + kWave) : hd0;
-        int I = e - h + 1;
-        // a row repeated inside (h, e], or fewer distinct columns than entries: first-fit in order
-        const bool dup = row == 0 ? (D0 & upto(lane) & above(h)) != 0ull
-                         : h >= kWave ? (D1 & upto(lane) & above(h - kWave)) != 0ull
-                                      : ((D0 & above(h)) | (D1 & upto(lane))) != 0ull;
-        const unsigned long long cm = row ? c1 : c0;
-        if (t && (dup || __popcll(cm) < I)) {
-          unsigned long long used = 0ull;
-          int rw = -1, Ic = 0;
-          for (int q = h; q <= e; ++q) {
-            const unsigned long long key = SK[q];
-            const int i = static_cast<int>((key >> 14) & 127u), j = static_cast<int>((key >> 7) & 63u);
-            if (i == rw) continue;                                 // this row already matched
-            if (!((used >> j) & 1ull)) {
-              used |= 1ull << j;
-              ++Ic;
-              rw = i;
-            }
-          }
-          I = Ic;
-        }
-        const int r = static_cast<int>((k >> 46) & 127u);
-        const int B = static_cast<int>((k >> 21) & kRankMask);
-        const int LB = row ? lb1 : lb0;
-        const int ra = t ? RUNA[r] : 0;
-        const int A = static_cast<int>(static_cast<unsigned>(ra) & kRankMask);
-        const int U = static_cast<int>(static_cast<unsigned>(ra) >> 25) + LB - I;
-        const int um = __shfl(umax_v, max(I, 1) - 1);     // every lane reads (no && in front)
-        const bool edge = t && I > 0 && U <= um;
-        es.put(eo, edge, A, B, I, U, lane);
-        if (edge) atomicAdd(&RUNF[r], 1);
-        w_pairs += __popcll(__ballot(t));
-      }
-#else
-#if !FSLR_PAIRS_EARLY
+      const bool s0 = v0 && (lane == 0 || (k0 >> 14) != (q0 >> 14));
+      const bool s1 = v1 && (k1 >> 14) != (q1 >> 14);
+      const bool d0 = v0 && !s0 && (k0 >> 7) == (q0 >> 7);
+      const bool d1 = v1 && !s1 && (k1 >> 7) == (q1 >> 7);
       int lb0 = 0, lb1 = 0;                                        // L_B of each segment, gathered by its head
-      if (s0) lb0 = RL[(k0 >> 21) & kRankMask];
-      if (s1) lb1 = RL[(k1 >> 21) & kRankMask];
-      if (sn < c1) load_window(sn, n0, n1, nn);                    // the next window, in flight meanwhile
-#endif
+      if (s0) FSLR_BOUND((k0 >> 14) & kRankMask, g.n_reads);
+      if (s1) FSLR_BOUND((k1 >> 14) & kRankMask, g.n_reads);
+      if (s0) lb0 = RL[(k0 >> 14) & kRankMask];
+      if (s1) lb1 = RL[(k1 >> 14) & kRankMask];
+      // the next window, in flight while this group is evaluated
+      const long long sn = s + gend;
+      unsigned long long n0 = ~0ull, n1 = ~0ull, nn = ~0ull;
+      if (sn < c1) load_window(sn, n0, n1, nn);
       const unsigned long long S0 = __ballot(s0), S1 = __ballot(s1);
       const int ns0 = __popcll(S0), nseg = ns0 + __popcll(S1);
 #ifdef FSLR_PAIRS_HIST
@@ -1076,19 +933,19 @@ __global__ __launch_bounds__(kSwBlock) FSLR_PAIRS_ATTR void k_sweep_pairs(SweepA
         RUNF[r1] = 0;
       }
       if (s0) {
-        PK[g0] = (k0 >> 21) | (static_cast<unsigned long long>(lb0) << 32);
+        PK[g0] = (k0 >> 14) | (static_cast<unsigned long long>(lb0) << 32);
         PJ[g0] = 0ull;
         PH[g0] = lane;
       }
       if (s1) {
-        PK[g1] = (k1 >> 21) | (static_cast<unsigned long long>(lb1) << 32);
+        PK[g1] = (k1 >> 14) | (static_cast<unsigned long long>(lb1) << 32);
         PJ[g1] = 0ull;
         PH[g1] = lane + kWave;
       }
       if (lane == 0) PH[nseg] = gend;
       wave_lds_sync();
-      if (v0) atomicOr(&PJ[g0], 1ull << ((k0 >> 7) & 63u));
-      if (v1) atomicOr(&PJ[g1], 1ull << ((k1 >> 7) & 63u));
+      if (v0) atomicOr(&PJ[g0], 1ull << (k0 & 63u));
+      if (v1) atomicOr(&PJ[g1], 1ull << (k1 & 63u));
       if (d0) atomicOr(&PH[g0], 1 << 30);
       if (d1) atomicOr(&PH[g1], 1 << 30);
       wave_lds_sync();
@@ -1114,7 +971,7 @@ __global__ __launch_bounds__(kSwBlock) FSLR_PAIRS_ATTR void k_sweep_pairs(SweepA
             int row = -1, Ic = 0;
             for (int k = h; k < he; ++k) {
               const unsigned long long key = SK[k];
-              const int i = static_cast<int>((key >> 14) & 127u), j = static_cast<int>((key >> 7) & 63u);
+              const int i = static_cast<int>((key >> 7) & 127u), j = static_cast<int>(key & 63u);
               if (i == row) continue;                              // this row already matched
               if (!((used >> j) & 1ull)) {
                 used |= 1ull << j;
@@ -1134,7 +991,6 @@ __global__ __launch_bounds__(kSwBlock) FSLR_PAIRS_ATTR void k_sweep_pairs(SweepA
         if (edge) atomicAdd(&RUNF[r], 1);
         w_pairs += __popcll(__ballot(act));
       }
-#endif
       FSLR_PCK(3);
       wave_lds_sync();
       if (hv0) {
@@ -1576,7 +1432,8 @@ size_t sweep_temp_bytes(long long ent_cap, long long ni, hipStream_t s) {
 hipError_t launch_sweep_plan(const SweepArgs& a, hipStream_t s) {
   const int nt = tiles_of(a);
   if (nt == 0) return hipSuccess;
-  k_tile_tests<<<grid_for(static_cast<long long>(nt) * kWave, 256, 4096), 256, 0, s>>>(a.swin, a.nq, a.tile_tests);
+  if (!a.tests_ready)
+    k_tile_tests<<<grid_for(static_cast<long long>(nt) * kWave, 256, 4096), 256, 0, s>>>(a.swin, a.nq, a.tile_tests);
   size_t tb = a.temp_bytes;
   hipError_t e = hipcub::DeviceScan::ExclusiveSum(a.temp, tb, a.tile_tests, a.tile_ub, nt, s);
   if (e != hipSuccess) return e;

@@ -7,9 +7,10 @@ Reads every */pmc_counter_collection.csv under the directory, keeps the dispatch
 named kernel, and averages each counter per dispatch.  HBM bytes per launch follow
 /opt/skills/guides/MI355X_MICROARCH.md (HBM / rocprofv3 section):
   FETCH_SIZE, WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports 1/2 of the bytes of wide
-  (16 B/lane) streaming reads, so the corrected read bytes are 2 x FETCH_SIZE.  The pair
-  kernel's loads are 16-B-per-lane records (idx4) and 8-B gate words, so the x2 correction is
-  applied to all of FETCH_SIZE; the uncorrected figure is kept beside it.
+  (16 B/lane) streaming reads.  Other widths are calibrated on known byte counts
+  (tools/fetchcal.sh -> profiles/r06/fetch_calibration.json: 16-, 8- and 4-B/lane loads all read as
+  0.500 of their bytes), and the kernel's correction is the calibrated one of its load widths; the
+  uncorrected figure is kept beside it.
 """
 from __future__ import annotations
 
@@ -19,6 +20,14 @@ import glob
 import json
 import os
 from collections import defaultdict
+
+
+CALIBRATION = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'profiles', 'r06',
+                           'fetch_calibration.json')
+# the global-load widths per lane of each kernel (all must be calibrated to apply the calibration):
+# k_sweep<2>: 16-B records and gate ranges, 8-B gate words and slots, 4-B windows; k_sweep_pairs: 8-B
+# entries (its 1-B read lengths are gathers that stay in L2)
+LOAD_WIDTHS = {'k_sweep<2>': [16, 8, 4], 'k_sweep_pairs': [8], 'query_kernel<0, false>': [16, 8, 4]}
 
 
 def collect(root, kernel):
@@ -43,21 +52,39 @@ def main():
     ap.add_argument('--source-hash', default=None, help='hash of the kernel sources the counters were taken on')
     ap.add_argument('--merge-into', default=None,
                     help='a JSON object keyed by kernel name (bench.py --traffic-json): set this kernel\'s entry')
+    ap.add_argument('--calibration', default=CALIBRATION,
+                    help='tools/fetch_calibration.py output: FETCH_SIZE / WRITE_SIZE per known byte, per width')
     args = ap.parse_args()
     c, dur = collect(args.root, args.kernel)
     if 'FETCH_SIZE' not in c:
         raise SystemExit(f'no FETCH_SIZE rows for {args.kernel} under {args.root}')
     fetch = c['FETCH_SIZE'] * 1024.0
     write = c.get('WRITE_SIZE', 0.0) * 1024.0
+    # the read correction from the calibration of this kernel's load widths (every width it loads must
+    # be calibrated, and they must agree: FETCH_SIZE cannot be split by width)
+    widths = LOAD_WIDTHS.get(args.kernel)
+    cal = json.load(open(args.calibration)) if args.calibration and os.path.exists(args.calibration) else None
+    factor, basis = None, None
+    if cal and widths:
+        ratios = [cal['ratio_by_width']['read'].get(str(w)) for w in widths]
+        if all(r for r in ratios) and max(ratios) - min(ratios) < 0.01 * max(ratios):
+            factor = 1.0 / (sum(ratios) / len(ratios))
+            basis = (f'{os.path.relpath(args.calibration)}: FETCH_SIZE = {sum(ratios) / len(ratios):.4f} x the bytes '
+                     f'of {"/".join(str(w) for w in widths)}-B/lane streaming loads (a 1 GiB buffer each)')
+    if factor is None:
+        factor = 2.0
+        basis = 'MI355X_MICROARCH.md: FETCH_SIZE x2 on gfx950 for 16-B/lane reads (uncalibrated for other widths)'
     out = {
         'kernel': args.kernel,
-        'hbm_bytes_per_launch': 2.0 * fetch + write,
+        'hbm_bytes_per_launch': factor * fetch + write,
         'fetch_bytes_raw': fetch,
-        'fetch_bytes_corrected_x2': 2.0 * fetch,
+        'fetch_correction_factor': factor,
+        'fetch_bytes_corrected': factor * fetch,
         'write_bytes': write,
+        'load_widths_bytes': widths,
         'pmc_pass_launch_s_mean': (sum(dur) / len(dur)) if dur else None,
         'counters_mean_per_dispatch': c,
-        'correction': 'MI355X_MICROARCH.md: FETCH_SIZE x2 on gfx950 for 16-B/lane reads; WRITE_SIZE as is',
+        'correction': basis + '; WRITE_SIZE as is (calibrated 1.00 for 8- and 16-B streaming stores)',
         'source_hash': args.source_hash,
     }
     if 'TCC_HIT_sum' in c and 'TCC_MISS_sum' in c:
