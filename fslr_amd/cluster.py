@@ -27,7 +27,7 @@ import sys
 import warnings
 
 import numpy as np
-import pandas as pd
+from ._lazy import pandas as pd
 
 from . import bam_header, ingest, multi
 from ._lib import FSLR_MAX_L, FSLR_THR_ZERO_ALN, Context

@@ -179,7 +179,7 @@ __global__ void __launch_bounds__(256) k_cap_frontier_w(const int* __restrict__ 
                                                         int* __restrict__ tl, unsigned* __restrict__ tn, int n_reads,
                                                         long long n_rows) {
   const int nin = static_cast<int>(*fin_n);
-  FSLR_BOUND(nin - 1, n_reads + 1);
+  FSLR_BOUND(nin, n_reads + 1);                  // (an empty frontier is nin = 0)
   const int lane = threadIdx.x & 63;
   const int wave = static_cast<int>((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
   const int nwaves = static_cast<int>((gridDim.x * blockDim.x) >> 6);

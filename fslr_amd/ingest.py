@@ -14,7 +14,7 @@ import ctypes
 import os
 
 import numpy as np
-import pandas as pd
+from ._lazy import pandas as pd
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libfslr_ingest.so')
 OK, ERROR, DECLINE = 0, 1, 2

@@ -19,7 +19,7 @@ import warnings
 
 import click
 import numpy as np
-import pandas as pd
+from ._lazy import pandas as pd
 
 from . import __version__, cluster, fastcli, ingest
 
@@ -98,8 +98,10 @@ def assign_clusters(bed_file: pd.DataFrame, G: cluster.ClusterGraph):
                    '(fslr_ingest.h); inputs it cannot type exactly like pandas fall back to pandas')
 @click.version_option(__version__)
 def pipeline(**args):
-    for cat in (pd.errors.SettingWithCopyWarning, FutureWarning):    # the reference ignores all warnings (main.py:13)
-        warnings.filterwarnings('ignore', category=cat)
+    # the reference ignores all warnings (main.py:13): FutureWarning, and pandas' SettingWithCopyWarning by
+    # its message (its class would import pandas, which the columnar path never needs)
+    warnings.filterwarnings('ignore', category=FutureWarning)
+    warnings.filterwarnings('ignore', message=r'\s*A value is trying to be set on a copy')
     basename = f'{args["out"]}/{args["name"]}'
     print('Basename: ', basename, file=sys.stderr)
     primers = args['primers'].split(',')

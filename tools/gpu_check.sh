@@ -118,9 +118,14 @@ fi
 if has bounds; then
   # the whole GPU suite on the bounds-checked build (FSLR_DEBUG_BOUNDS device asserts, kernels.hpp)
   make -s -C fslr_amd/csrc -j16 bounds > $O/build_bounds.log 2>&1 || { tail -20 $O/build_bounds.log; exit 1; }
-  FSLR_LIB=$R/fslr_amd/libfslr_hip_bounds.so timeout -k 10 1000 python -u -m pytest tests/ --maxfail=5 -q --timeout 300 \
+  FSLR_LIB=$R/fslr_amd/libfslr_hip_bounds.so timeout -k 10 1000 python -u -m pytest tests/ --maxfail=1 -q --timeout 300 \
       --timeout-method thread -m gpu > $O/pytest_bounds.log 2>&1 || { echo "bounds tests failed"; tail -40 $O/pytest_bounds.log; exit 1; }
   tail -2 $O/pytest_bounds.log
+fi
+if has rccl; then
+  # the product's multi-GPU step over RCCL, two ranks sharing this GPU (tools/rccl_one_gpu.py)
+  timeout -k 10 300 python3 -u tools/rccl_one_gpu.py $O/rccl_one_gpu.json > $O/rccl.log 2>&1 || { echo "rccl run failed"; tail -20 $O/rccl.log; }
+  tail -2 $O/rccl.log
 fi
 if has pmc; then
   OUT=gpurun_out/$TAG/pmc timeout -k 10 900 bash tools/pmc.sh > $O/pmc.log 2>&1 || { echo "pmc failed"; tail -20 $O/pmc.log; exit 1; }
