@@ -721,6 +721,15 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
     const int LA = RL[A];
     const long long len = re - rs;
     const int npass = len <= kPairLimit ? 1 : static_cast<int>((len + kPerPass - 1) / kPerPass);
+#ifdef FSLR_PAIRS_HIST
+    // measurement build: long runs' entries (45), their wave-steps over all partner passes (46), the
+    // longest run (47)
+    if (lane == 0) {
+      atomicAdd(&g.counters[45], static_cast<unsigned long long>(len));
+      atomicAdd(&g.counters[46], static_cast<unsigned long long>(npass) * ((len + kWave - 1) / kWave));
+      atomicMax(&g.counters[47], static_cast<unsigned long long>(len));
+    }
+#endif
     int fwdA = 0;
     if (es.n > 0) es.flush(eo, lane);               // A's edges from an empty stage: one run (<= the stage)
     for (int pass = 0; pass < npass; ++pass) {

@@ -51,6 +51,9 @@ if has hist; then
   FSLR_LIB=$R/fslr_amd/libfslr_hip_hist.so FSLR_ALLOW_STALE=1 timeout -k 10 300 python3 tools/pairs_hist.py $O/pairs_group_hist.json \
       > $O/hist.log 2>&1 || { echo "hist failed"; tail -20 $O/hist.log; exit 1; }
   tail -30 $O/hist.log
+  FSLR_LIB=$R/fslr_amd/libfslr_hip_hist.so FSLR_ALLOW_STALE=1 timeout -k 10 500 python3 tools/pairs_hist.py $O/pairs_group_hist_cfg5.json \
+      --cfg5 > $O/hist5.log 2>&1 || { echo "hist cfg5 failed"; tail -20 $O/hist5.log; exit 1; }
+  tail -30 $O/hist5.log
 fi
 if has shard; then
   # the per-rank model at 1M reads: both splits, uniform and one chromosome holding ~55 %
