@@ -210,6 +210,8 @@ struct SweepArgs {
   unsigned long long* ent;            // [n_ent] match entries A << 39 | B << 14 | i << 7 | j, tile order
   unsigned long long* ent_sorted;     // [n_ent] grouped by A
   unsigned long long* ent_mid;        // (mode 3) [n_ent] grouping scratch
+  unsigned long long* pair_scr;       // [n_ent] free during k_sweep_pairs (the grouping's other buffer):
+                                      // long runs are bucketed there at their own positions
   int* grp;                           // [grp_ints()] grouping-sort bucket counts / offsets (null: radix sort)
   int* hist_mat;                      // (mode 2, one GPU) k_sweep<2> writes [bucket][block] counts of the
                                       // coarse A buckets A >> hist_lo here (null: the grouping counts them)

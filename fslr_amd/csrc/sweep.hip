@@ -617,7 +617,7 @@ __device__ __forceinline__ unsigned long long group_key(unsigned long long e, in
   return (static_cast<unsigned long long>(r) << 39) | (e & ((1ull << 39) - 1));
 }
 
-__global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
+__global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(5))) void k_sweep_pairs(SweepArgs g) {
   __shared__ __attribute__((aligned(16))) unsigned long long scr_all[kSwWaves][kScrWords];
   __shared__ int runa_all[kSwWaves][kStageE];                 // per run of the group: A | L_A << 25, edges formed
   __shared__ int runf_all[kSwWaves][kStageE];
@@ -805,6 +805,158 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
     w_maxfwd = max(w_maxfwd, fwdA);
   };
 
+  // ---- a run longer than the stage, bucketed (round 6): its partners hashed into P = ceil(len / 96)
+  // buckets of at most kStageE entries — counted in LDS, scattered into the grouping's free buffer at the
+  // run's own positions — and each bucket sorted by (B, i, j) and evaluated like a group (one run): two
+  // streams over the run and P network sorts instead of one stream per 40-entry partner partition.
+  // Returns false, having written nothing, when the run has more than 64 buckets or one bucket more than
+  // kStageE entries (a pair of reads with that many matches): then the partition path above runs.
+  auto long_run_buckets = [&](long long rs, long long re) -> bool {
+    unsigned long long* S = g.pair_scr;
+    const long long len = re - rs;
+    const int P = static_cast<int>((len + 95) / 96);
+    if (!S || P > kWave) return false;
+    const int A = a_at(rs);
+    FSLR_BOUND(A, g.n_reads);
+    FSLR_BOUND(re - 1, n);
+    auto bucket_of = [&](unsigned long long e) -> int {
+      return static_cast<int>(((static_cast<unsigned>((e >> 14) & kRankMask) * 0x9E3779B1u) >> 8) % static_cast<unsigned>(P));
+    };
+    int* BC = RUNA;                                 // per bucket: entry count, then the scatter cursor
+    int* BO = RUNF;
+    wave_lds_sync();
+    if (lane < P) BC[lane] = 0;
+    wave_lds_sync();
+    for (long long b = rs; b < re; b += kWave) {
+      const long long t = b + lane;
+      if (t < re) atomicAdd(&BC[bucket_of(E[t])], 1);
+    }
+    wave_lds_sync();
+    const int cnt = lane < P ? BC[lane] : 0;
+    int cmax = cnt;
+    for (int o = 32; o > 0; o >>= 1) cmax = max(cmax, __shfl_xor(cmax, o));
+    if (cmax > kStageE) return false;
+    const int off = wave_incl_scan(cnt) - cnt;
+    if (lane < P) BO[lane] = off;
+    wave_lds_sync();
+    for (long long b = rs; b < re; b += kWave) {
+      const long long t = b + lane;
+      if (t < re) {
+        const unsigned long long e = E[t];
+        const int p = atomicAdd(&BO[bucket_of(e)], 1);
+        S[rs + p] = e;
+      }
+    }
+    // the wave reads its own scattered entries back: its stores complete (no other CU touches these
+    // positions, so no L1 on another CU can hold them and the workgroup scope is enough)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const int LA = RL[A];
+#ifdef FSLR_PAIRS_HIST
+    if (lane == 0) {                                // measurement build: bucketed runs (40), their entries (41)
+      atomicAdd(&g.counters[40], 1ull);
+      atomicAdd(&g.counters[41], static_cast<unsigned long long>(len));
+    }
+#endif
+    int fwdA = 0;
+    if (es.n > 0) es.flush(eo, lane);               // A's edges from an empty stage: one run (<= the stage)
+    for (int kb = 0; kb < P; ++kb) {
+      const int bo = rdl(off, kb), bc = rdl(cnt, kb);
+      if (bc == 0) continue;
+      const unsigned long long* Sb = S + rs + bo;
+      const bool v0 = lane < bc, v1 = lane + kWave < bc;
+      unsigned long long k0 = v0 ? (Sb[lane] & ((1ull << 39) - 1)) << 7 : ~0ull;
+      unsigned long long k1 = v1 ? (Sb[kWave + lane] & ((1ull << 39) - 1)) << 7 : ~0ull;
+      if (bc > kWave) {
+        bitonic_il<128>(k0, k1, lane);
+      } else if (bc > kWave / 2) {
+        k1 = __shfl(k0, (lane + kWave / 2) & (kWave - 1));
+        bitonic_il<64>(k0, k1, lane);
+        if (lane >= kWave / 2) k0 = k1 = ~0ull;
+      } else {
+        k1 = __shfl(k0, (lane + kWave / 4) & (kWave - 1));
+        bitonic_il<32>(k0, k1, lane);
+        if (lane >= kWave / 4) k0 = k1 = ~0ull;
+      }
+      wave_lds_sync();                              // the previous bucket's reads are done
+      reinterpret_cast<ulonglong2*>(SK)[lane] = make_ulonglong2(k0, k1);
+      wave_lds_sync();
+      k0 = SK[lane];
+      k1 = SK[lane + kWave];
+      const unsigned long long q0 = __shfl_up(k0, 1);
+      const unsigned long long k0_63 = __shfl(k0, kWave - 1);
+      const unsigned long long w1 = __shfl_up(k1, 1);
+      const unsigned long long q1 = lane > 0 ? w1 : k0_63;
+      // segments = partners B (key >> 21); a row repeated inside a segment sits next to itself
+      const bool s0 = v0 && (lane == 0 || (k0 >> 21) != (q0 >> 21));
+      const bool s1 = v1 && (k1 >> 21) != (q1 >> 21);
+      const bool d0 = v0 && !s0 && (k0 >> 14) == (q0 >> 14);
+      const bool d1 = v1 && !s1 && (k1 >> 14) == (q1 >> 14);
+      int lb0 = 0, lb1 = 0;
+      if (s0) lb0 = RL[(k0 >> 21) & kRankMask];
+      if (s1) lb1 = RL[(k1 >> 21) & kRankMask];
+      const unsigned long long S0 = __ballot(s0), S1 = __ballot(s1);
+      const int ns0 = __popcll(S0), nseg = ns0 + __popcll(S1);
+      const int g0 = __popcll(S0 & upto(lane)) - 1;
+      const int g1 = ns0 + __popcll(S1 & upto(lane)) - 1;
+      wave_lds_sync();
+      if (s0) {
+        PK[g0] = (k0 >> 21) | (static_cast<unsigned long long>(lb0) << 32);
+        PJ[g0] = 0ull;
+        PH[g0] = lane;
+      }
+      if (s1) {
+        PK[g1] = (k1 >> 21) | (static_cast<unsigned long long>(lb1) << 32);
+        PJ[g1] = 0ull;
+        PH[g1] = lane + kWave;
+      }
+      if (lane == 0) PH[nseg] = bc;
+      wave_lds_sync();
+      if (v0) atomicOr(&PJ[g0], 1ull << ((k0 >> 7) & 63u));
+      if (v1) atomicOr(&PJ[g1], 1ull << ((k1 >> 7) & 63u));
+      if (d0) atomicOr(&PH[g0], 1 << 30);
+      if (d1) atomicOr(&PH[g1], 1 << 30);
+      wave_lds_sync();
+      for (int k0s = 0; k0s < nseg; k0s += kWave) {
+        const int p = k0s + lane;
+        const bool act = p < nseg;
+        int I = 0, B = 0, LB = 0;
+        if (act) {
+          const int hp = PH[p];
+          const int h = hp & 0x3FFFFFFF, he = PH[p + 1] & 0x3FFFFFFF;
+          const unsigned long long pk = PK[p];
+          B = static_cast<int>(pk & kRankMask);
+          LB = static_cast<int>(pk >> 32);
+          I = he - h;
+          if ((hp >> 30) || __popcll(PJ[p]) < I) {
+            // a shared row or column: first-fit over the segment, rows ascending, lowest free column
+            unsigned long long used = 0ull;
+            int row = -1, Ic = 0;
+            for (int q = h; q < he; ++q) {
+              const unsigned long long key = SK[q];
+              const int i = static_cast<int>((key >> 14) & 127u), j = static_cast<int>((key >> 7) & 63u);
+              if (i == row) continue;
+              if (!((used >> j) & 1ull)) {
+                used |= 1ull << j;
+                ++Ic;
+                row = i;
+              }
+            }
+            I = Ic;
+          }
+        }
+        const int U = LA + LB - I;
+        const int um = __shfl(umax_v, max(I, 1) - 1);   // every lane reads (no && in front)
+        const bool edge = act && I > 0 && U <= um;
+        fwdA += es.put(eo, edge, A, B, I, U, lane);
+        w_pairs += __popcll(__ballot(act));
+      }
+    }
+    if (lane == 0) g.fwd[A] = fwdA;
+    w_maxfwd = max(w_maxfwd, fwdA);
+    return true;
+  };
+
   // the window of (up to) kStageE entries at s, and (lane 0) the entry after it (~0: none).  Vector
   // loads only: a scalar load in flight would hold every LDS wait (lgkmcnt) of the group behind it
   auto load_window = [&](long long s, unsigned long long& w0, unsigned long long& w1, unsigned long long& wn) {
@@ -865,7 +1017,10 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_pairs(SweepArgs g) {
       if (gend == 0) {
         // the run at s does not fit the stage: alone
         const long long re = next_run(s + lim, n, entry_a(__shfl(e0, 0)));
-        long_run(s, re);
+#ifndef FSLR_PAIRS_NO_BUCKETS
+        if (!long_run_buckets(s, re))
+#endif
+          long_run(s, re);
         FSLR_PCK(5);
         s = re;
         if (s < c1) load_window(s, e0, e1, en);
@@ -1639,6 +1794,8 @@ hipError_t launch_sweep_pairs(const SweepArgs& a0, int mode, hipStream_t s) {
     if (e != hipSuccess) return e;
   }
   if (a.ev[3]) (void)hipEventRecord(a.ev[3], s);
+  unsigned long long* const ent0 = a.ent;
+  unsigned long long* const sorted0 = a.ent_sorted;
   if (msd) {
     // mode 2: tile slots -> ent -> ent_sorted; mode 0: ent -> ent_sorted -> ent (the pair kernel
     // then reads ent); mode 3: the caller's entries -> ent_mid -> ent_sorted
@@ -1660,6 +1817,9 @@ hipError_t launch_sweep_pairs(const SweepArgs& a0, int mode, hipStream_t s) {
     if (e != hipSuccess) return e;
   }
   if (a.ev[4]) (void)hipEventRecord(a.ev[4], s);
+  // the grouping's buffer the pair kernel does not read: its long runs are bucketed there (mode 2 and the
+  // radix fallback: ent; mode 0: the original ent_sorted; mode 3: ent_mid, the caller's ent being input)
+  a.pair_scr = mode == 3 ? (msd ? a.ent_mid : nullptr) : (a.ent_sorted == ent0 ? sorted0 : ent0);
   const long long chunks = (a.n_ent + kChunk2 - 1) / kChunk2;
   const int blocks = static_cast<int>(std::max(1ll, std::min<long long>(blocks_pairs(), (chunks + kSwWaves - 1) / kSwWaves)));
   if (blocks * kSwWaves > a.wstat_waves) return hipErrorInvalidValue;

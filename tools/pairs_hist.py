@@ -29,7 +29,7 @@ def main():
            'match_entries': int(st['match_entries']),
            'groups': groups, 'long_runs': int(c[42]), 'read_pairs_in_groups': int(c[43]),
            'runs_in_groups': int(c[44]), 'long_run_entries': int(c[45]), 'long_run_pass_steps': int(c[46]),
-           'longest_run': int(c[47]),
+           'longest_run': int(c[47]), 'bucketed_runs': int(c[40]), 'bucketed_run_entries': int(c[41]),
            'group_size_hist': {f'{8 * k + 1}-{8 * k + 8}': int(v) for k, v in enumerate(bins)},
            'mean_group_entries': None}
     out['share_le_64'] = float(bins[:8].sum() / max(1, groups))
