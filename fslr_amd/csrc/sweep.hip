@@ -844,6 +844,7 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(5))) v
       if (t < re) {
         const unsigned long long e = E[t];
         const int p = atomicAdd(&BO[bucket_of(e)], 1);
+        FSLR_BOUND(p, len);
         S[rs + p] = e;
       }
     }
@@ -1501,6 +1502,8 @@ __global__ __launch_bounds__(kSwBlock) void k_sweep_scatter(SweepArgs g, const i
   const int lane = lane_id();
   const int wid = blockIdx.x * kSwWaves + (threadIdx.x >> 6);
   const int tb = g.wlo[wid], te = g.wlo[wid + 1];   // the tiles this wave swept (k_sweep<2>)
+  FSLR_BOUND(tb, te + 1);
+  FSLR_BOUND(te, (g.nq + kWave - 1) / kWave + 1);
   constexpr int kU = 4;
   for (int t0 = tb; t0 < te; t0 += kTileRun) {
     const int run = min(kTileRun, te - t0);
@@ -1752,6 +1755,9 @@ hipError_t launch_sweep_partition(const SweepArgs& a, int mode, int shift, int n
   int* mat = a.grp;
   int* off = a.grp + kGrpInts / 2;
   const int nt = tiles_of(a);
+  // a rank whose index range is empty (more ranks than chromosomes, an empty position range): no sweep
+  // ran, so the wave ranges, histograms and totals the scatter would read are last query's — no entries
+  if (nt == 0) return hipMemsetAsync(totals, 0, static_cast<size_t>(n_dest) * sizeof(long long), s);
   if (mode == 2 && a.hist_mat && a.hist_mod && a.hist_h == n_dest && a.hist_lo == shift) {
     // the sweep counted its entries per destination: scan, totals, one scatter over its wave ranges
     const int P = sweep_blocks(nt);
