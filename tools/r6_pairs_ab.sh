@@ -11,7 +11,7 @@ cd $R
 ( while sleep 50; do echo "tick $(date +%T)"; done ) &
 TICK=$!
 trap "kill $TICK" EXIT
-timeout -k 10 900 python -u -m pytest tests/ --maxfail=3 -q --timeout 300 --timeout-method thread -m gpu > $O/pytest_gpu.log 2>&1 \
+timeout -k 10 900 python -u -m pytest tests/ --maxfail=1 -q --timeout 300 --timeout-method thread -m gpu > $O/pytest_gpu.log 2>&1 \
     || { echo "gpu tests failed"; tail -40 $O/pytest_gpu.log; exit 1; }
 tail -1 $O/pytest_gpu.log
 for v in main oldlr; do
