@@ -1430,18 +1430,21 @@ __global__ void k_cap_ccost(const int* __restrict__ comp, const int* __restrict_
     atomicAdd(ccost + comp[t], static_cast<unsigned long long>(cost[t]) + 1ull);
 }
 
-// every T slot as a sort key: a root's (cost descending, then root ascending), ~0 for the others (sorted last)
+// every T slot as a sort key of 31 + tb bits (tb = bits of nt, so the sort skips the empty high digits): a
+// root's (cost descending, then root ascending), all ones for the others (sorted last)
+__device__ __forceinline__ unsigned long long cap_key_none(int tb) { return (1ull << (31 + tb)) - 1; }
 __global__ void k_cap_rootkeys(const int* __restrict__ comp, const unsigned long long* __restrict__ ccost, int nt,
-                               unsigned long long* __restrict__ keys) {
+                               int tb, unsigned long long* __restrict__ keys) {
   for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += gridDim.x * blockDim.x)
-    keys[t] = comp[t] == t ? ((0x7fffffffull - min(ccost[t], 0x7fffffffull)) << 32) | static_cast<unsigned>(t) : ~0ull;
+    keys[t] = comp[t] == t ? ((0x7fffffffull - min(ccost[t], 0x7fffffffull)) << tb) | static_cast<unsigned>(t)
+                           : cap_key_none(tb);
 }
 
 // the components onto ranks, the same on every rank: the kCapHead largest one by one onto the
 // least-loaded rank (ties: the lower rank), by one lane; the rest (sorted by cost, descending) dealt
 // in snake order, rank 0 .. W-1 then W-1 .. 0, whose sums differ by at most the largest of them
 constexpr int kCapHead = 256;
-__global__ void k_cap_assign_head(const unsigned long long* __restrict__ sorted, int nt, int world,
+__global__ void k_cap_assign_head(const unsigned long long* __restrict__ sorted, int nt, int world, int tb,
                                   int* __restrict__ dmap) {
   __shared__ unsigned long long hk[kCapHead];
   const int nh = min(nt, kCapHead);
@@ -1451,22 +1454,22 @@ __global__ void k_cap_assign_head(const unsigned long long* __restrict__ sorted,
   long long load[kMaxDest] = {};
   for (int k = 0; k < nh; ++k) {
     const unsigned long long key = hk[k];
-    if (key == ~0ull) break;
+    if (key == cap_key_none(tb)) break;
     int d = 0;
     for (int q = 1; q < world; ++q)
       if (load[q] < load[d]) d = q;
-    load[d] += static_cast<long long>(0x7fffffffull - (key >> 32));
-    dmap[static_cast<int>(key & 0xffffffffull)] = d;
+    load[d] += static_cast<long long>(0x7fffffffull - (key >> tb));
+    dmap[static_cast<int>(key & ((1ull << tb) - 1))] = d;
   }
 }
 
-__global__ void k_cap_assign_tail(const unsigned long long* __restrict__ sorted, int nt, int world,
+__global__ void k_cap_assign_tail(const unsigned long long* __restrict__ sorted, int nt, int world, int tb,
                                   int* __restrict__ dmap) {
   for (int k = kCapHead + blockIdx.x * blockDim.x + threadIdx.x; k < nt; k += gridDim.x * blockDim.x) {
     const unsigned long long key = sorted[k];
-    if (key == ~0ull) continue;
+    if (key == cap_key_none(tb)) continue;
     const int j = k - kCapHead, r = j % world;
-    dmap[static_cast<int>(key & 0xffffffffull)] = (j / world) & 1 ? world - 1 - r : r;
+    dmap[static_cast<int>(key & ((1ull << tb) - 1))] = (j / world) & 1 ? world - 1 - r : r;
   }
 }
 
@@ -3102,15 +3105,17 @@ extern "C" int fslr_cap_shard_plan(fslr_ctx* c, const int32_t* gathered, int32_t
     k_cap_tcost<<<grid_for(nt), 256, 0, s>>>(gathered, world, nt, w->tcost);
     HIP_TRY(c, hipMemsetAsync(w->ccost, 0, static_cast<size_t>(nt) * sizeof(unsigned long long), s));
     k_cap_ccost<<<grid_for(nt), 256, 0, s>>>(w->comp, w->tcost, nt, w->ccost);
-    k_cap_rootkeys<<<grid_for(nt), 256, 0, s>>>(w->comp, w->ccost, nt, rkeys);
+    const int kbits = bits_for(nt);
+    k_cap_rootkeys<<<grid_for(nt), 256, 0, s>>>(w->comp, w->ccost, nt, kbits, rkeys);
     // largest first (ties: the smaller root), the other slots last; then the ranks, on the device
     size_t tb = 0;
-    HIP_TRY(c, hipcub::DeviceRadixSort::SortKeys(nullptr, tb, rkeys, w->ccost, nt, 0, 64, s));
+    HIP_TRY(c, hipcub::DeviceRadixSort::SortKeys(nullptr, tb, rkeys, w->ccost, nt, 0, 31 + kbits, s));
     if (int rc = ensure_temp(c, w, tb)) return rc;
     tb = w->temp_bytes;
-    HIP_TRY(c, hipcub::DeviceRadixSort::SortKeys(w->temp, tb, rkeys, w->ccost, nt, 0, 64, s));
-    k_cap_assign_head<<<1, 256, 0, s>>>(w->ccost, nt, world, w->dmap);
-    if (nt > kCapHead) k_cap_assign_tail<<<grid_for(nt - kCapHead), 256, 0, s>>>(w->ccost, nt, world, w->dmap);
+    HIP_TRY(c, hipcub::DeviceRadixSort::SortKeys(w->temp, tb, rkeys, w->ccost, nt, 0, 31 + kbits, s));
+    k_cap_assign_head<<<1, 256, 0, s>>>(w->ccost, nt, world, kbits, w->dmap);
+    if (nt > kCapHead)
+      k_cap_assign_tail<<<grid_for(nt - kCapHead), 256, 0, s>>>(w->ccost, nt, world, kbits, w->dmap);
     k_cap_tdest<<<grid_for(nt), 256, 0, s>>>(w->comp, w->dmap, nt, w->tdest);
     HIP_TRY(c, hipGetLastError());
   }
