@@ -527,10 +527,7 @@ __global__ __launch_bounds__(256) void k_compact(const unsigned long long* __res
 // lowest unused column, cluster.py:152-161).  A run longer than the stage is evaluated alone,
 // streamed from HBM, through an LDS hash over its partners in partner partitions (pass k takes the
 // partners with part(B) == k).
-#ifndef FSLR_PAIRS_CHUNK
-#define FSLR_PAIRS_CHUNK 512
-#endif
-constexpr int kChunk2 = FSLR_PAIRS_CHUNK;   // a wave's work item: whole runs starting in it
+constexpr int kChunk2 = 512;               // a wave's work item: whole runs starting in it
 constexpr int kStageE = 128;
 constexpr int kHash2 = 128;
 constexpr unsigned kEmpty = 0xFFFFFFFFu;
