@@ -21,7 +21,8 @@ others in ``roofline_other_kernels``.  Sweep engine (default): the position swee
 k_sweep<2> — every sorted position's index record, gate word and forward
 count and its read's gate ranges read once (48 B), plus each match entry written (8 B) —
 and the pair stage k_sweep_pairs — each grouped match entry read once (8 B), each edge written
-(10 B), each read's forward degree written (4 B) (the same bytes for the fused variant
+(10 B) and its union-find pre-hook (an atomicMin on the upper read's parent: 4 B read + 4 B
+written), each read's forward degree written (4 B) (the same bytes for the fused variant
 k_bucket_pairs, FSLR_PAIR_STAGE=fused, which reads the entries from the grouping's pass-1 buckets).  Walk engine: query_kernel, every
 walked index record (16-B record + 8-B gate word) read once, each query read's header,
 gate bounds and forward degree, each of its intervals' sorted position, row and scan
@@ -337,11 +338,14 @@ def main():
     roofs = [roofline(KERNEL_NAME[st['engine']], kern, algo_bytes, algo_model)]
     if kern2.size:
         # the pair stage: every grouped match entry read once (8 B), each edge written (a, b + I | U:
-        # 10 B), each read's forward degree written (4 B); the 1-byte read lengths it looks up stay in L2
-        pb = B_ENT * sw['match_entries'] + 10 * st['n_edges'] + 4 * csr.n_reads
+        # 10 B) and hooked into the union-find (atomicMin on parent[b]: 4 B read + 4 B written, the work
+        # k_uf_hook_min did before round 6), each read's forward degree written (4 B); the 1-byte read
+        # lengths it looks up stay in L2
+        pb = B_ENT * sw['match_entries'] + (10 + 8) * st['n_edges'] + 4 * csr.n_reads
         roofs.append(roofline(PAIR_STAGE, kern2, pb,
                               f'{B_ENT} B x grouped match entries read ({sw["match_entries"]}) '
-                              f'+ 10 B x edges written ({st["n_edges"]}) + 4 B x forward degrees ({csr.n_reads})'))
+                              f'+ 10 B x edges written ({st["n_edges"]}) + 8 B x their union-find pre-hook '
+                              f'(atomicMin on parent[b]) + 4 B x forward degrees ({csr.n_reads})'))
     # the headline roofline is the longest kernel's (HIP events over the timed steps)
     roofs.sort(key=lambda r: -r['kernel_ms'] if r['kernel_ms'] == r['kernel_ms'] else 0.0)
     head_roof = dict(roofs[0], phase_ms_last_step=lib_t,

@@ -1928,6 +1928,7 @@ int ensure_temp(fslr_ctx* c, CapWork* w, size_t need) {
 }
 
 int cap_work(fslr_ctx* c, CapWork** out) {
+  c->hooked = false;                 // every cap path may rewrite the edges
   if (!c->capw) {
     c->capw = new CapWork();
     HIP_TRY(c, hipHostMalloc(reinterpret_cast<void**>(&c->capw->host), kHWords * sizeof(long long), hipHostMallocMapped));
@@ -3366,6 +3367,7 @@ extern "C" int fslr_cap_apply_changes(fslr_ctx* c, const int32_t* changes, int64
 
 extern "C" int fslr_sort_edges(fslr_ctx* c) {
   if (!c) return FSLR_ERR_INVALID;
+  c->hooked = false;
   if (!c->reads_set) return fail(c, FSLR_ERR_STATE, "fslr_set_reads first");
   HIP_TRY(c, hipSetDevice(c->device));
   if (!c->counters || !c->edge_cap) return FSLR_OK;

@@ -215,6 +215,7 @@ int fslr_set_profiling(fslr_ctx* c, int enable) {
 
 int fslr_set_reads(fslr_ctx* c, const fslr_reads* r) {
   if (!c || !r) return FSLR_ERR_INVALID;
+  c->hooked = false;
   HIP_TRY(c, hipSetDevice(c->device));
   const int64_t n = r->n_reads, ni = r->n_intervals;
   if (n < 0 || ni < 0 || n >= FSLR_MAX_READS || ni >= (int64_t(1) << 31) - 1)
@@ -415,6 +416,7 @@ int fslr_rows_upload(fslr_ctx* c, const fslr_rows* r) {
   if (!c || !r || r->n_rows < 1 || r->n_rows >= (int64_t(1) << 31) - 1 || r->n_codes < 1 ||
       r->n_codes >= (int64_t(1) << 31) || r->n_chrom_ids < 1 || r->n_chrom_ids >= (1 << 24))
     return FSLR_ERR_INVALID;
+  c->hooked = false;
   if (!r->chrom || !r->start || !r->end || !r->aln || !r->qcode || !r->nal || !r->qlen2)
     return fail(c, FSLR_ERR_INVALID, "null array");
   HIP_TRY(c, hipSetDevice(c->device));
@@ -501,6 +503,7 @@ int64_t rows_int_need(int64_t n, int64_t codes, int64_t cids) {
 int fslr_set_reads_rows(fslr_ctx* c, const int64_t* order, const uint8_t* keep, double overlap,
                         fslr_rows_info* info) {
   if (!c || !order || !info) return FSLR_ERR_INVALID;
+  c->hooked = false;
   std::memset(info, 0, sizeof(*info));
   const int64_t n = c->rows_n;
   if (n < 1) return fail(c, FSLR_ERR_STATE, "fslr_rows_upload first");
@@ -752,6 +755,7 @@ int fslr_edge_cap_deferred_read(fslr_ctx* c, int32_t* flags) {
 
 int fslr_reserve_edges(fslr_ctx* c, int64_t capacity) {
   if (!c || capacity < 0) return FSLR_ERR_INVALID;
+  c->hooked = false;
   HIP_TRY(c, hipSetDevice(c->device));
   if (capacity <= c->edge_cap) return FSLR_OK;
   HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -1097,7 +1101,9 @@ static int sweep_impl(fslr_ctx* c, const fslr_params* p, int64_t a_begin, int64_
     s.p0 = c->kev2[2 * slot];
     s.p1 = c->kev2[2 * slot + 1];
   }
+  s.parent = c->parent;                              // the edges hook the union-find as they are formed
   HIP_TRY(c, launch_sweep_pairs(s, mode, c->stream));
+  c->hooked = true;
   c->sw_ev_rec = c->prof_phases;
   return FSLR_OK;
 }
@@ -1140,8 +1146,8 @@ static int prepare_query(fslr_ctx* c, const fslr_params* p, bool keep_sticky = f
     c->wstat_waves = w;
   }
   HIP_TRY(c, launch_query_reset(c->counters, kNumCounters, c->errw, keep_sticky ? kErrKeep : kErrWords, c->fwd,
-                                static_cast<int>(c->n),
-                                c->stream));
+                                c->parent, static_cast<int>(c->n), c->stream));
+  c->hooked = false;
   std::memset(&c->cap_stats, 0, sizeof(c->cap_stats));
   if (!keep_sticky) c->zd_lost = false;             // a new series lists its pairs from the start
   c->edges_global = false;
@@ -1540,7 +1546,9 @@ int fslr_sweep_evaluate(fslr_ctx* c, const fslr_params* p, const void* entries, 
   s.err = c->errw;
   s.wstat = c->sw_wstat;
   s.wstat_waves = c->sw_wstat_waves;
+  s.parent = c->parent;
   HIP_TRY(c, launch_sweep_pairs(s, 3, c->stream));
+  c->hooked = true;
   return FSLR_OK;
 }
 
@@ -1550,8 +1558,12 @@ int fslr_components(fslr_ctx* c) {
   HIP_TRY(c, hipSetDevice(c->device));
   if (c->prof_phases) HIP_TRY(c, hipEventRecord(c->ev[4], c->stream));
   const int n = static_cast<int>(c->n);
-  HIP_TRY(c, launch_uf_init(c->parent, n, c->stream));
-  if (c->edge_cap) HIP_TRY(c, launch_uf_edges(c->parent, c->edges, c->counters, c->edge_cap, c->errw, c->stream));
+  const bool hooked = c->hooked;                    // the sweep's pair kernel initialised and pre-hooked parent
+  c->hooked = false;
+  if (!hooked) HIP_TRY(c, launch_uf_init(c->parent, n, c->stream));
+  if (c->edge_cap)
+    HIP_TRY(c, (hooked ? launch_uf_unions : launch_uf_edges)(c->parent, c->edges, c->counters, c->edge_cap, c->errw,
+                                                             c->stream));
   HIP_TRY(c, launch_uf_finalize(c->parent, n, c->stream));
   if (c->prof_phases) HIP_TRY(c, hipEventRecord(c->ev[5], c->stream));
   c->t_comp_rec = c->prof_phases;
@@ -1785,6 +1797,7 @@ int fslr_copy_fwd_device(fslr_ctx* c, int32_t* dst) {
 
 int fslr_union_pairs(fslr_ctx* c, const int32_t* src, const int32_t* dst, int64_t n, int on_device) {
   if (!c || !dst || n < 0) return FSLR_ERR_INVALID;
+  c->hooked = false;
   HIP_TRY(c, hipSetDevice(c->device));
   if (n == 0) return FSLR_OK;
   const int* ds = src;
@@ -1825,8 +1838,11 @@ int fslr_local_forest(fslr_ctx* c, int64_t* n_pairs) {
   HIP_TRY(c, hipSetDevice(c->device));
   hipStream_t s = c->stream;
   const int nr = static_cast<int>(c->n);
-  HIP_TRY(c, launch_uf_init(c->parent, nr, s));
-  if (c->edge_cap) HIP_TRY(c, launch_uf_edges(c->parent, c->edges, c->counters, c->edge_cap, c->errw, s));
+  const bool hooked = c->hooked;                    // as in fslr_components
+  c->hooked = false;
+  if (!hooked) HIP_TRY(c, launch_uf_init(c->parent, nr, s));
+  if (c->edge_cap)
+    HIP_TRY(c, (hooked ? launch_uf_unions : launch_uf_edges)(c->parent, c->edges, c->counters, c->edge_cap, c->errw, s));
   HIP_TRY(c, launch_forest_pairs(c->parent, nr, c->forest, c->forest_cnt, c->forest_blk, s));   // finalizes too
   if (n_pairs) {
     unsigned long long k = 0;
@@ -1848,6 +1864,7 @@ int fslr_copy_forest_pairs(fslr_ctx* c, int32_t* dst, int64_t n_pad) {
 
 int fslr_components_from_pairs(fslr_ctx* c, const int32_t* pairs, int64_t n) {
   if (!c || (!pairs && n) || n < 0) return FSLR_ERR_INVALID;
+  c->hooked = false;
   if (!c->reads_set) return fail(c, FSLR_ERR_STATE, "fslr_set_reads first");
   HIP_TRY(c, hipSetDevice(c->device));
   const int nr = static_cast<int>(c->n);
@@ -1859,6 +1876,7 @@ int fslr_components_from_pairs(fslr_ctx* c, const int32_t* pairs, int64_t n) {
 
 int fslr_finalize_labels(fslr_ctx* c) {
   if (!c) return FSLR_ERR_INVALID;
+  c->hooked = false;
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, launch_uf_finalize(c->parent, static_cast<int>(c->n), c->stream));
   return FSLR_OK;

@@ -219,18 +219,24 @@ __global__ void k_uf_finalize(int* p, int n) {
 
 }  // namespace
 
-// one launch instead of three fills per query: counters, error words and forward degrees to 0
+// one launch instead of four fills per query: counters, error words and forward degrees to 0, and the
+// union-find parents to the identity (the sweep's pair kernel hooks them as it forms edges, so the
+// components after it skip k_uf_init and k_uf_hook_min)
 __global__ void k_query_reset(unsigned long long* __restrict__ counters, int nc, int* __restrict__ err, int ne,
-                              int* __restrict__ fwd, int n) {
+                              int* __restrict__ fwd, int* __restrict__ parent, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < nc) counters[i] = 0ull;
   if (i < ne) err[i] = 0;
-  for (int k = i; k < n; k += gridDim.x * blockDim.x) fwd[k] = 0;
+  for (int k = i; k < n; k += gridDim.x * blockDim.x) {
+    fwd[k] = 0;
+    if (parent) parent[k] = k;
+  }
 }
 
-hipError_t launch_query_reset(unsigned long long* counters, int nc, int* err, int ne, int* fwd, int n, hipStream_t s) {
+hipError_t launch_query_reset(unsigned long long* counters, int nc, int* err, int ne, int* fwd, int* parent, int n,
+                              hipStream_t s) {
   const long long work = std::max<long long>(std::max(nc, ne), n);
-  k_query_reset<<<grid_for(work), 256, 0, s>>>(counters, nc, err, ne, fwd, n);
+  k_query_reset<<<grid_for(work), 256, 0, s>>>(counters, nc, err, ne, fwd, parent, n);
   return hipGetLastError();
 }
 
@@ -243,6 +249,13 @@ hipError_t launch_uf_init(int* parent, int n, hipStream_t s) {
 hipError_t launch_uf_edges(int* parent, const int2* edges, const unsigned long long* count, long long cap, int* err,
                            hipStream_t s) {
   if (cap > 0) k_uf_hook_min<<<grid_for(cap), 256, 0, s>>>(parent, edges, count, cap);
+  if (cap > 0) k_uf_edges<<<grid_for(cap), 256, 0, s>>>(parent, edges, count, cap, err);
+  return hipGetLastError();
+}
+
+// parent already hooked by the edges' atomicMin (the sweep's pair kernel, SweepArgs::parent): the unions only
+hipError_t launch_uf_unions(int* parent, const int2* edges, const unsigned long long* count, long long cap, int* err,
+                            hipStream_t s) {
   if (cap > 0) k_uf_edges<<<grid_for(cap), 256, 0, s>>>(parent, edges, count, cap, err);
   return hipGetLastError();
 }

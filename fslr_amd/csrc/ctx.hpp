@@ -17,6 +17,10 @@ struct fslr_ctx {
   int n_chroms = 0;
   int thr_mode = 0;
   bool reads_set = false, index_built = false, have_data_pos = false;
+  // parent is the identity taken down by the last sweep query's edges (SweepArgs::parent): the next
+  // fslr_components / fslr_local_forest runs only the unions; anything else that writes the edges or the
+  // parents clears it
+  bool hooked = false;
   bool index_full = false;                 // the walk engine's index parts exist (qpos, backward ranges)
   bool bwd_ranges = false;                 // backward scan ranges exist (the cap replay's hits; no qpos)
   bool index_lean = false;                 // lean scatter (no data -> sorted map; `vals` holds the ends)

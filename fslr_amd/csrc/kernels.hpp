@@ -227,6 +227,8 @@ struct SweepArgs {
   unsigned short* edge_iu;
   long long edge_cap;
   int* fwd;
+  int* parent;                        // non-null: each edge (A, B) also takes parent[B] down to A (the union-find's
+                                      // min pre-hook, components.hip); the query reset made it the identity
   unsigned long long* counters;
   int* err;
   unsigned long long* wstat;          // per-wave statistics slots [waves x 4] (no contended atomics)
@@ -336,10 +338,13 @@ hipError_t rows_zero_flags(const int* thr, int ni, unsigned char* z, hipStream_t
 // ---- components (components.hip) ---------------------------------------------------------
 hipError_t launch_uf_init(int* parent, int n, hipStream_t s);
 // counters[0, nc), err[0, ne) and fwd[0, n) to zero in one launch (start of a query)
-hipError_t launch_query_reset(unsigned long long* counters, int nc, int* err, int ne, int* fwd, int n, hipStream_t s);
+hipError_t launch_query_reset(unsigned long long* counters, int nc, int* err, int ne, int* fwd, int* parent, int n,
+                              hipStream_t s);
 // count > cap (edges were lost) sets err[kErrOverflow]
 hipError_t launch_uf_edges(int* parent, const int2* edges, const unsigned long long* count, long long cap, int* err,
                            hipStream_t s);
+hipError_t launch_uf_unions(int* parent, const int2* edges, const unsigned long long* count, long long cap, int* err,
+                            hipStream_t s);
 // src == nullptr: src[k] = k mod period
 hipError_t launch_uf_pairs(int* parent, const int* src, const int* dst, long long n, int period, hipStream_t s);
 hipError_t launch_uf_finalize(int* parent, int n, hipStream_t s);

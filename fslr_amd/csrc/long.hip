@@ -181,6 +181,7 @@ void fslr_long_free(fslr_ctx* c) {
 // calculate_overlap, :133-136, see only those and the two intervals).  Uploaded with
 // fslr_set_reads, the maps with fslr_set_long_reads (umax later: fslr_set_long_cutoffs).
 extern "C" int fslr_set_reads_any(fslr_ctx* c, const fslr_reads* r) {
+  if (c) c->hooked = false;
   if (!c || !r || r->n_reads < 0 || r->n_intervals < 0 || !r->read_off) return FSLR_ERR_INVALID;
   const int64_t n = r->n_reads, ni = r->n_intervals;
   if (r->read_off[0] != 0 || r->read_off[n] != ni) return fail(c, FSLR_ERR_INVALID, "read_off does not span intervals");
@@ -269,6 +270,7 @@ extern "C" int fslr_set_long_cutoffs(fslr_ctx* c, const int32_t* umax, int32_t n
 
 extern "C" int fslr_set_long_reads(fslr_ctx* c, int64_t n_real, const int32_t* vreal, const int32_t* vbase,
                                    const int32_t* rlen, const int32_t* umax, int32_t n_umax) {
+  if (c) c->hooked = false;
   if (!c || n_real < 0 || !vreal || !vbase || (!rlen && n_real) || (!umax && n_umax) || n_umax < 0)
     return FSLR_ERR_INVALID;
   if (!c->reads_set) return fail(c, FSLR_ERR_STATE, "fslr_set_reads first (the virtual CSR)");

@@ -798,6 +798,7 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(5))) v
         const int um = __shfl(umax_v, max(I, 1) - 1);     // every lane reads (no && in front)
         const bool edge = act && I > 0 && U <= um;
         fwdA += es.put(eo, edge, A, B, I, U, lane);
+        if (edge && g.parent) atomicMin(g.parent + B, A);   // the union-find's pre-hook (A < B)
         w_pairs += __popcll(__ballot(act));
       }
     }
@@ -950,6 +951,7 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(5))) v
         const int um = __shfl(umax_v, max(I, 1) - 1);   // every lane reads (no && in front)
         const bool edge = act && I > 0 && U <= um;
         fwdA += es.put(eo, edge, A, B, I, U, lane);
+        if (edge && g.parent) atomicMin(g.parent + B, A);   // the union-find's pre-hook (A < B)
         w_pairs += __popcll(__ballot(act));
       }
     }
@@ -1154,6 +1156,7 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(5))) v
         const bool edge = act && I > 0 && U <= um;
         es.put(eo, edge, A, B, I, U, lane);
         if (edge) atomicAdd(&RUNF[r], 1);
+        if (edge && g.parent) atomicMin(g.parent + B, A);   // the union-find's pre-hook (A < B)
         w_pairs += __popcll(__ballot(act));
       }
       FSLR_PCK(3);
