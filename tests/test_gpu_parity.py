@@ -358,6 +358,53 @@ def test_union_find_labels_stable_over_repeats(ctx):
         np.testing.assert_array_equal(ctx.labels(), want)
 
 
+def test_components_after_the_sweeps_pre_hook(ctx):
+    """The sweep's pair kernel pre-hooks the union-find as it forms edges, so the next
+    fslr_components runs only the unions: its labels must equal a host union-find over the stored edges,
+    and so must every sequence that invalidates the hook first (a second components call, an edge sort,
+    a walk query, a binding cap's rewritten edges, the local forest's pairs)."""
+    from fslr_amd.dist import union_find_labels
+    s = synth.generate(30_000, 16, 5)
+    csr = s.interval_data().csr()
+    n = csr.n_reads
+    qc, nc, pt = 1 - 0.04, 1 - 0.25, pass_table([1, 1, 0.66, 0.66, 0.66, 0.5])
+    ctx.load_csr(csr, fold_overlap_threshold(csr.iv_aln, 0.8))
+    ctx.reserve_edges(12 * n)
+
+    def host_labels():
+        a, b, _, _ = ctx.edges(ctx.stats()['n_edges'])
+        return union_find_labels(n, a, b)
+
+    for seq in ('direct', 'twice', 'sorted', 'walk_after', 'forest'):
+        ctx.build_index()
+        ctx.query(qc, nc, pt, 10, engine='sweep')
+        if seq == 'walk_after':
+            ctx.query(qc, nc, pt, 10, engine='walk')
+        if seq == 'sorted':
+            ctx.sort_edges()
+        if seq == 'forest':
+            ctx.local_forest()
+            want = host_labels()
+            got = ctx.labels()
+            np.testing.assert_array_equal(got, want, err_msg=seq)     # the forest finalizes the parents
+            continue
+        ctx.components()
+        if seq == 'twice':
+            ctx.components()
+        np.testing.assert_array_equal(ctx.labels(), host_labels(), err_msg=seq)
+    # a binding cap rewrites the edges: the components after it are those of the capped list
+    data, _, _ = host_prepare('capbind_1500')
+    c2 = data.csr()
+    ctx.load_csr(c2, fold_overlap_threshold(c2.iv_aln, 0.8))
+    ctx.reserve_edges(max(1 << 16, 12 * c2.n_reads))
+    ctx.build_index()
+    ctx.query(qc, nc, pt, 10, engine='sweep')
+    assert ctx.apply_edge_cap(10)['applied']
+    ctx.components()
+    a, b, _, _ = ctx.edges(ctx.stats()['n_edges'])
+    np.testing.assert_array_equal(ctx.labels(), union_find_labels(c2.n_reads, a, b))
+
+
 @pytest.mark.parametrize('engine', ['walk', 'auto'])
 def test_zero_division_raises(ctx, engine):
     data, _, _ = host_prepare('zerodiv')
