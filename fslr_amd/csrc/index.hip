@@ -138,16 +138,28 @@ __global__ __launch_bounds__(kTileThreads) void k_chrom_count(const unsigned* __
   const int tl = blockIdx.x;
   const int e0 = tl * rounds * kTileThreads;
   int cnt = 0;
-  for (int r = 0; r < rounds; ++r) {
-    const int e = e0 + r * kTileThreads + threadIdx.x;
-    const unsigned c = e < ni ? dchrom[e] : 0u;
-    unsigned long long m = __ballot(e < ni);
+  // kU rounds' loads in flight before their ballots (one load's latency per kU rounds, not per round)
+  constexpr int kU = 8;
+  for (int r0 = 0; r0 < rounds; r0 += kU) {
+    unsigned cc[kU];
 #pragma unroll
-    for (int b = 0; b < kChromBits; ++b) {
-      const unsigned long long bb = __ballot((c >> b) & 1u);
-      m &= ((lane >> b) & 1) ? bb : ~bb;
+    for (int u = 0; u < kU; ++u) {
+      const int e = e0 + (r0 + u) * kTileThreads + threadIdx.x;
+      cc[u] = r0 + u < rounds && e < ni ? dchrom[e] : 0u;
     }
-    cnt += __popcll(m);
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      if (r0 + u >= rounds) break;                 // block-uniform
+      const int e = e0 + (r0 + u) * kTileThreads + threadIdx.x;
+      const unsigned c = cc[u];
+      unsigned long long m = __ballot(e < ni);
+#pragma unroll
+      for (int b = 0; b < kChromBits; ++b) {
+        const unsigned long long bb = __ballot((c >> b) & 1u);
+        m &= ((lane >> b) & 1) ? bb : ~bb;
+      }
+      cnt += __popcll(m);
+    }
   }
   wc[w][lane] = cnt;
   __syncthreads();
