@@ -291,7 +291,13 @@ int  fslr_apply_edge_cap(fslr_ctx *ctx, int32_t edge_threshold, fslr_cap_stats *
  * fslr_apply_edge_cap (or raised): its results are to be recomputed synchronously. */
 int  fslr_edge_cap_deferred(fslr_ctx *ctx, int32_t edge_threshold);
 int  fslr_edge_cap_deferred_read(fslr_ctx *ctx, int32_t *flags);
-/* cluster.py:230-234 — union-find over the edges: label = min rank in component.  Async. */
+/* cluster.py:230-234 — union-find over the edges: label = min rank in component.  Async.  Every query
+ * resets the parents to the identity; a sweep-engine query (fslr_query, fslr_sweep_evaluate) also
+ * pre-hooks them as its pair kernel forms the edges, and the next fslr_components / fslr_local_forest
+ * then runs only the unions (any call that rewrites the edges or the parents in between — the edge cap,
+ * fslr_sort_edges, fslr_reserve_edges, an upload, fslr_union_pairs — makes it start from the identity
+ * again).  Labels (fslr_get_labels) are those of the last fslr_components / fslr_local_forest /
+ * fslr_components_from_pairs until the next query. */
 int  fslr_components(fslr_ctx *ctx);
 /* Multi-GPU sweep.  A rank indexes only the chromosomes it owns, sweeps them and
  * routes the match entries to the rank owning each pair's first read, which evaluates the pairs.
