@@ -414,6 +414,7 @@ __global__ __launch_bounds__(1024) void k_sweep_total(const unsigned long long* 
   __shared__ unsigned long long part[16][3];
   __shared__ int wsum[16];
   unsigned long long a0 = 0, a1 = 0, a2 = 0;
+#pragma unroll 4
   for (int w = threadIdx.x; w < nwaves; w += 1024) {
     a0 += ws[static_cast<long long>(w) * kWsFields];
     a1 += ws[static_cast<long long>(w) * kWsFields + 1];
@@ -455,16 +456,35 @@ __global__ __launch_bounds__(1024) void k_sweep_total(const unsigned long long* 
     const int N = H * P;
     const int per = (N + 1023) / 1024;
     const int first = static_cast<int>(threadIdx.x) * per;
+    // (up to kPerReg counts per thread — a W <= 8 partition — held in registers: their loads in flight
+    // together and read once, not one dependent load per element and a second pass)
+    constexpr int kPerReg = 16;
+    int v[kPerReg];
     int loc = 0;
-    for (int i = 0; i < per && first + i < N; ++i) loc += mat[first + i];
+    if (per <= kPerReg) {
+#pragma unroll
+      for (int i = 0; i < kPerReg; ++i) v[i] = i < per && first + i < N ? mat[first + i] : 0;
+#pragma unroll
+      for (int i = 0; i < kPerReg; ++i) loc += v[i];
+    } else {
+      for (int i = 0; i < per && first + i < N; ++i) loc += mat[first + i];
+    }
     const int inc = wave_incl_scan(loc);
     if (lane == kWave - 1) wsum[w] = inc;
     __syncthreads();
     int base = inc - loc;
     for (int x = 0; x < w; ++x) base += wsum[x];
-    for (int i = 0; i < per && first + i < N; ++i) {
-      off[first + i] = base;
-      base += mat[first + i];
+    if (per <= kPerReg) {
+#pragma unroll
+      for (int i = 0; i < kPerReg; ++i) {
+        if (i < per && first + i < N) off[first + i] = base;
+        base += v[i];
+      }
+    } else {
+      for (int i = 0; i < per && first + i < N; ++i) {
+        off[first + i] = base;
+        base += mat[first + i];
+      }
     }
     __syncthreads();
     if (static_cast<int>(threadIdx.x) < H) {
