@@ -1446,27 +1446,70 @@ __global__ void k_cap_rootkeys(const int* __restrict__ comp, const unsigned long
 constexpr int kCapHead = 256;
 __global__ void k_cap_assign_head(const unsigned long long* __restrict__ sorted, int nt, int world, int tb,
                                   int* __restrict__ dmap) {
-  // one wavefront: lane q holds rank q's load (world <= kMaxDest = 64), each component's rank is the
-  // wave-wide minimum of (load, rank); the keys wait in LDS (a per-thread array of loads indexed by the
-  // rank lived in scratch memory: 184 us for 256 components at W = 8, profiles/r06/r6i)
-  __shared__ unsigned long long hk[kCapHead];
-  const int lane = threadIdx.x;
+  // One wavefront walks the components (the greedy is sequential) with every value wave-uniform, so
+  // the loop runs on the scalar unit: the keys arrive by scalar loads, up to 8 ranks' loads stay in
+  // scalar registers (every index static after unrolling); more ranks keep them in LDS.  (One thread
+  // with a per-thread array indexed by the rank — scratch memory — took 183 us for 256 components at
+  // W = 8, profiles/r06/r6i; a wave-wide min-reduction per component 105 us, r6v; one lane's vector
+  // loop 78 us, r6w.)
+  __shared__ long long lds_load[kMaxDest];
+  const int lane = threadIdx.x & 63;
   const int nh = min(nt, kCapHead);
-  for (int k = lane; k < nh; k += kWave) hk[k] = sorted[k];
-  __syncthreads();
-  unsigned long long load = 0ull;
-  for (int k = 0; k < nh; ++k) {
-    const unsigned long long key = hk[k];
-    if (key == cap_key_none(tb)) break;
-    unsigned long long v = lane < world ? (load << 6) | static_cast<unsigned long long>(lane) : ~0ull;
+  const unsigned long long none = cap_key_none(tb), tmask = (1ull << tb) - 1;
+  if (world <= 8) {
+    // loads as 32-bit (load << 3 | rank) words: the least-loaded rank (ties: the lower) is a tree of
+    // seven scalar mins.  Costs are scaled down when 256 of the largest could overflow 29 bits.
+    const unsigned long long c0 = nh > 0 && sorted[0] != none ? 0x7fffffffull - (sorted[0] >> tb) : 0ull;
+    int shift = 0;
+    while ((c0 >> shift) > (1ull << 21)) ++shift;   // 256 x 2^21 = 2^29
+    unsigned L[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    for (int k0 = 0; k0 < nh; k0 += 8) {
+      unsigned long long kk[8];                    // uniform addresses: 8 scalar loads, one wait
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const unsigned long long u = __shfl_xor(v, o);
-      v = u < v ? u : v;
+      for (int u = 0; u < 8; ++u) kk[u] = k0 + u < nh ? sorted[k0 + u] : none;
+      bool done = false;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const unsigned long long key = kk[u];
+        if (key == none) {
+          done = true;
+          break;
+        }
+        unsigned w8[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) w8[q] = q < world ? (L[q] << 3) | static_cast<unsigned>(q) : 0xFFFFFFFFu;
+        const unsigned m01 = min(w8[0], w8[1]), m23 = min(w8[2], w8[3]), m45 = min(w8[4], w8[5]),
+                       m67 = min(w8[6], w8[7]);
+        const int d = static_cast<int>(min(min(m01, m23), min(m45, m67)) & 7u);
+        const unsigned cost = static_cast<unsigned>((0x7fffffffull - (key >> tb)) >> shift);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) L[q] += q == d ? cost : 0u;
+        if (lane == 0) dmap[static_cast<int>(key & tmask)] = d;
+      }
+      if (done) break;
     }
-    const int d = static_cast<int>(v & 63ull);
-    if (lane == d) load += 0x7fffffffull - (key >> tb);
-    if (lane == 0) dmap[static_cast<int>(key & ((1ull << tb) - 1))] = d;
+    return;
+  }
+  for (int q = lane; q < kMaxDest; q += kWave) lds_load[q] = 0;
+  __syncthreads();
+  for (int k = 0; k < nh; ++k) {
+    const unsigned long long key = sorted[k];
+    if (key == none) break;
+    int d = 0;
+    long long best = lds_load[0];
+    for (int q = 1; q < world; ++q) {
+      const long long v = lds_load[q];
+      if (v < best) {
+        best = v;
+        d = q;
+      }
+    }
+    __syncthreads();
+    if (lane == 0) {
+      lds_load[d] = best + static_cast<long long>(0x7fffffffull - (key >> tb));
+      dmap[static_cast<int>(key & tmask)] = d;
+    }
+    __syncthreads();
   }
 }
 
