@@ -661,7 +661,7 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(5))) v
   int* RUNF = runf_all[wv];
   uint2* RR = rr_all[wv];
   EdgeStageN<kPairEdgeStage> es{es_all[wv], 0};
-  const EdgeOut eo{g.edges, g.edge_iu, g.edge_cap, &g.counters[kEdgeCount]};
+  const EdgeOut eo{g.edges, g.edge_iu, g.edge_cap, &g.counters[kEdgeCount], g.parent};
   const int umax_v = g.umax[lane];
   const long long n = g.n_dev ? *g.n_dev : g.n_ent;
   const unsigned long long* E = g.ent_sorted;
@@ -818,7 +818,6 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(5))) v
         const int um = __shfl(umax_v, max(I, 1) - 1);     // every lane reads (no && in front)
         const bool edge = act && I > 0 && U <= um;
         fwdA += es.put(eo, edge, A, B, I, U, lane);
-        if (edge && g.parent) atomicMin(g.parent + B, A);   // the union-find's pre-hook (A < B)
         w_pairs += __popcll(__ballot(act));
       }
     }
@@ -971,7 +970,6 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(5))) v
         const int um = __shfl(umax_v, max(I, 1) - 1);   // every lane reads (no && in front)
         const bool edge = act && I > 0 && U <= um;
         fwdA += es.put(eo, edge, A, B, I, U, lane);
-        if (edge && g.parent) atomicMin(g.parent + B, A);   // the union-find's pre-hook (A < B)
         w_pairs += __popcll(__ballot(act));
       }
     }
@@ -1176,7 +1174,6 @@ __global__ __launch_bounds__(kSwBlock) __attribute__((amdgpu_waves_per_eu(5))) v
         const bool edge = act && I > 0 && U <= um;
         es.put(eo, edge, A, B, I, U, lane);
         if (edge) atomicAdd(&RUNF[r], 1);
-        if (edge && g.parent) atomicMin(g.parent + B, A);   // the union-find's pre-hook (A < B)
         w_pairs += __popcll(__ballot(act));
       }
       FSLR_PCK(3);

@@ -93,6 +93,8 @@ struct EdgeOut {
   unsigned short* edge_iu;
   long long cap;
   unsigned long long* count;          // the global edge counter (own cache line)
+  int* parent = nullptr;              // EdgeStageN: each flushed edge (a, b) also takes parent[b] down to a
+                                      // (the union-find's pre-hook, SweepArgs::parent)
 };
 
 struct EdgeStage {
@@ -149,6 +151,9 @@ struct EdgeStageN {
         o.edges[k] = make_int2(static_cast<int>(e >> 39), static_cast<int>((e >> 14) & kRankMask));
         o.edge_iu[k] = static_cast<unsigned short>(((e >> 7) & 127u) | ((e & 127u) << 8));
       }
+      // the pre-hook here, batched with the flush's stores, rather than one atomic per edge as it is formed
+      // (every later load of the wave waits behind its atomics: once per flush instead of once per group)
+      if (o.parent) atomicMin(o.parent + ((e >> 14) & kRankMask), static_cast<int>(e >> 39));
     }
     wave_lds_sync();
     n = 0;
